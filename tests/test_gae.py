@@ -1,0 +1,170 @@
+"""GAE: oracle pinned by closed forms + golden vectors (CPU); HIP kernels vs oracle (GPU).
+
+Reference: GGL::GAE::Compute, GigaLearnCPP/src/private/GigaLearnCPP/PPO/GAE.cpp:7-208.
+Tolerances: the [T,N] rollout kernel is bit-exact (same operation order, no FMA
+contraction); the flat kernel reassociates the recursion as an affine scan, so it is
+checked at rtol 1e-5 (north-star float tolerance) with an absolute floor scaled by the
+magnitude of the terms.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT
+
+GOLDEN = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "gae_flat_*.npz")))
+
+
+def closed_form(rews, vals, gamma, lam):
+    """Single episode ending NORMAL: A_t = sum_k (g*l)^k delta_{t+k}."""
+    n = len(rews)
+    nxt = np.append(vals[1:], 0.0)
+    delta = rews + gamma * nxt - vals
+    adv = np.array([sum((gamma * lam) ** k * delta[t + k] for k in range(n - t)) for t in range(n)])
+    ret = np.array([sum(gamma ** k * rews[t + k] for k in range(n - t)) for t in range(n)])
+    return adv, ret
+
+
+def test_oracle_closed_form_single_episode():
+    rng = np.random.default_rng(0)
+    r = rng.standard_normal(40).astype(np.float32)
+    v = rng.standard_normal(40).astype(np.float32)
+    t = np.zeros(40, np.int8)
+    t[-1] = 1
+    adv, tgt, ret, cp, st = oracle.gae_flat(r, t, v, None, 0.99, 0.95, 1.0, 0.0)
+    ea, er = closed_form(r.astype(np.float64), v.astype(np.float64), 0.99, 0.95)
+    np.testing.assert_allclose(adv, ea, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret, er, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(tgt, v + adv)
+    assert st == 0 and cp == 0.0
+
+
+def test_oracle_truncation_bootstrap_and_normalisation():
+    # two episodes: [0..2] truncated (bootstrap 5.0), [3..4] normal
+    r = np.array([1, 2, 3, 4, 5], np.float32)
+    v = np.array([0.5, 0.25, 0.0, 1.0, 2.0], np.float32)
+    t = np.array([0, 0, 2, 0, 1], np.int8)
+    g, l, std, clip = 0.9, 0.5, 2.0, 1.2
+    adv, tgt, ret, cp, st = oracle.gae_flat(r, t, v, np.array([5.0], np.float32), g, l, std, clip)
+    n = np.clip(r / std, -clip, clip)
+    d2 = n[2] + g * 5.0 - v[2]
+    d1 = n[1] + g * v[2] - v[1]
+    d0 = n[0] + g * v[1] - v[0]
+    d4 = n[4] - v[4]
+    d3 = n[3] + g * v[4] - v[3]
+    exp_adv = [d0 + g * l * (d1 + g * l * d2), d1 + g * l * d2, d2, d3 + g * l * d4, d4]
+    np.testing.assert_allclose(adv, exp_adv, rtol=1e-6)
+    # returns use RAW rewards (GAE.cpp:183-185) and stop at either terminal type
+    np.testing.assert_allclose(ret, [1 + g * (2 + g * 3), 2 + g * 3, 3, 4 + g * 5, 5], rtol=1e-6)
+    raw = np.abs(r / std).sum()
+    assert cp == pytest.approx((raw - np.abs(n).sum()) / raw, rel=1e-6)
+    assert st == 0
+
+
+def test_oracle_truncation_count_mismatch_is_error():
+    r = np.ones(4, np.float32)
+    t = np.array([2, 0, 2, 1], np.int8)
+    *_, st = oracle.gae_flat(r, t, r, np.ones(1, np.float32), 0.99, 0.95, 1.0, 0.0)
+    assert st == -1
+
+
+def test_oracle_empty():
+    e = np.zeros(0, np.float32)
+    adv, tgt, ret, cp, st = oracle.gae_flat(e, np.zeros(0, np.int8), e, None, 0.99, 0.95, 1.0, 0.0)
+    assert adv.size == 0 and cp == 0.0 and st == 0
+
+
+@pytest.mark.parametrize("path", GOLDEN)
+def test_oracle_matches_golden(path):
+    z = np.load(path)
+    g, l, std, clip = [float(x) for x in z["params"]]
+    adv, tgt, ret, cp, st = oracle.gae_flat(z["rews"], z["terms"], z["vals"], z["trunc_vals"], g, l, std, clip)
+    np.testing.assert_array_equal(adv, z["adv"])
+    np.testing.assert_array_equal(ret, z["ret"])
+    np.testing.assert_array_equal(tgt, z["target"])
+    assert np.float32(cp) == z["clip_portion"]
+
+
+def test_oracle_rollout_equals_flat_per_column():
+    rng = np.random.default_rng(3)
+    T, N = 33, 7
+    r = rng.standard_normal((T, N)).astype(np.float32)
+    v = rng.standard_normal((T, N)).astype(np.float32)
+    t = (rng.random((T, N)) < 0.08).astype(np.int8)
+    a, tg, rt = oracle.gae_rollout(r, t, v, None, None, 0.99, 0.95, 3.0, 2.0)
+    for n in range(N):
+        fa, ft, fr, _, _ = oracle.gae_flat(r[:, n], t[:, n], v[:, n], None, 0.99, 0.95, 3.0, 2.0)
+        np.testing.assert_array_equal(a[:, n], fa)
+        np.testing.assert_array_equal(rt[:, n], fr)
+
+
+# ---------------------------------------------------------------- GPU parity (C ABI)
+
+def _flat_case(m, seed):
+    from tests_util import synth_gae
+    return synth_gae(m, seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", GOLDEN)
+def test_gpu_flat_matches_golden(gpu, path):
+    import torch
+    from rlgpu import GAE
+    z = np.load(path)
+    g, l, std, clip = [float(x) for x in z["params"]]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    adv, tgt, ret, cp = GAE.compute(d(z["rews"]), d(z["terms"]), d(z["vals"]), d(z["trunc_vals"]), g, l, std, clip)
+    scale = np.abs(z["adv"]).max() + 1
+    np.testing.assert_allclose(adv.cpu().numpy(), z["adv"], rtol=1e-5, atol=1e-5 * scale)
+    np.testing.assert_allclose(ret.cpu().numpy(), z["ret"], rtol=1e-5, atol=1e-5 * (np.abs(z["ret"]).max() + 1))
+    np.testing.assert_allclose(tgt.cpu().numpy(), z["target"], rtol=1e-5, atol=1e-5 * scale)
+    assert cp == pytest.approx(float(z["clip_portion"]), rel=1e-4, abs=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [1, 7, 2048, 2049, 1 << 21])
+def test_gpu_flat_sizes_and_edges(gpu, m):
+    import torch
+    from rlgpu import GAE
+    from tests_util import synth_gae
+    r, t, v, tv = synth_gae(m, 11 + m)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    adv, tgt, ret, cp = GAE.compute(d(r), d(t), d(v), d(tv) if tv.size else None, 0.99, 0.95, 1.7, 5.0)
+    ea, et, er, ecp, st = oracle.gae_flat(r, t, v, tv, 0.99, 0.95, 1.7, 5.0)
+    assert st == 0
+    np.testing.assert_allclose(adv.cpu().numpy(), ea, rtol=1e-5, atol=1e-5 * (np.abs(ea).max() + 1))
+    np.testing.assert_allclose(ret.cpu().numpy(), er, rtol=1e-5, atol=1e-5 * (np.abs(er).max() + 1))
+    assert cp == pytest.approx(ecp, rel=1e-4, abs=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_flat_trunc_mismatch_raises(gpu):
+    import torch
+    from rlgpu import GAE, RLGPUError
+    r = torch.ones(4, device=gpu)
+    t = torch.tensor([2, 0, 2, 1], dtype=torch.int8, device=gpu)
+    with pytest.raises(RLGPUError, match="truncation count mismatch"):
+        GAE.compute(r, t, r, torch.ones(1, device=gpu), 0.99, 0.95, 1.0, 0.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,N", [(128, 16384), (1, 5), (37, 1000)])
+def test_gpu_rollout_bit_exact(gpu, T, N):
+    import torch
+    from rlgpu import GAE
+    rng = np.random.default_rng(T * 7 + N)
+    r = rng.standard_normal((T, N)).astype(np.float32)
+    v = rng.standard_normal((T, N)).astype(np.float32)
+    u = rng.random((T, N))
+    t = np.where(u < 1 / 128, 1, np.where(u < 1 / 128 + 1 / 512, 2, 0)).astype(np.int8)
+    tv = rng.standard_normal((T, N)).astype(np.float32)
+    bv = rng.standard_normal(N).astype(np.float32)
+    d = lambda a: torch.from_numpy(a).to(gpu)
+    adv, tgt, ret = GAE.compute_rollout(d(r), d(t), d(v), d(tv), d(bv), 0.99, 0.95, 2.0, 10.0)
+    ea, et, er = oracle.gae_rollout(r, t, v, tv, bv, 0.99, 0.95, 2.0, 10.0)
+    np.testing.assert_array_equal(adv.cpu().numpy(), ea)
+    np.testing.assert_array_equal(tgt.cpu().numpy(), et)
+    np.testing.assert_array_equal(ret.cpu().numpy(), er)
