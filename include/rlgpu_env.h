@@ -1,0 +1,184 @@
+/*
+ * rlgpu_env.h -- C ABI of the vectorised RLGymCPP/RocketSim arena set on MI355X.
+ *
+ * Replaces the env side of the reference's hot path:
+ *   RLGC::EnvSet            GigaLearnCPP/RLGymCPP/src/RLGymCPP/EnvSet/EnvSet.h:14-110
+ *     EnvSet(const EnvSetConfig&)          EnvSet.cpp:46-111   -> rlgpu_envset_create
+ *     StepFirstHalf(bool async)            EnvSet.cpp:113-130  -> rlgpu_envset_step_first_half
+ *     StepSecondHalf(actions, bool async)  EnvSet.cpp:132-273  -> rlgpu_envset_step_second_half
+ *     Sync()                               EnvSet.h:107        -> rlgpu_envset_sync
+ *     ResetArena(int) / Reset()            EnvSet.cpp:275-354  -> rlgpu_envset_reset_arena / _reset
+ *     state.{obs,actionMasks,rewards,terminals,arenaPlayerStartIdx}
+ *                                          EnvSet.h:35-65      -> rlgpu_envset_buffers
+ * with the plugin set of src/ExampleMain.cpp:128-226 built in: AdvancedObs, DefaultAction,
+ * KickoffState, the 13 weighted rewards and NoTouchCondition(8) + ScoreLimitCondition(3).
+ *
+ * Arena state lives on the device as struct-of-arrays; one env step is ONE kernel launch
+ * (7 ticks with the previous controls, action parse, 1 tick, builders, reset-if-terminal)
+ * when rlgpu_envset_step() is used, or two launches through the two-half API.
+ *
+ * All "d_" pointers are device pointers; "h_" pointers are host memory owned by the caller.
+ */
+#ifndef RLGPU_ENV_H
+#define RLGPU_ENV_H
+
+#include <stdint.h>
+#include "rlgpu_core.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RLGPU_CARS 4          /* 2v2 (src/ExampleMain.cpp:200-208) */
+#define RLGPU_PADS 34         /* RLConst::BoostPads 6 big + 28 small (RLConst.h:212-214) */
+#define RLGPU_MANIFOLDS 16    /* persistent-manifold slots per arena */
+#define RLGPU_OBS 167         /* AdvancedObs 9+8+34+29*4 (AdvancedObs.cpp:193-270) */
+#define RLGPU_ACTIONS 90      /* DefaultAction table (DefaultAction.cpp:3-89) */
+#define RLGPU_REWARDS 13      /* ExampleMain reward list (src/ExampleMain.cpp:132-177) */
+
+/* One persistent contact point (btManifoldPoint subset, bullet units). */
+typedef struct {
+    float localA[3], localB[3]; /* in body-A / body-B frames */
+    float normalB[3];           /* normal on B, world space, pointing towards A */
+    float dist;                 /* signed distance (negative = penetration) */
+    float applied;              /* m_appliedImpulse (warm start) */
+    float friction, restitution;
+    int32_t special;            /* m_isSpecial: ball-world contact (Arena.cpp:265-273) */
+} rlgpu_contact;
+
+/* Persistent manifold for one body pair.  key: dynamic-static = body*8 + static
+ * (body 0 = ball, 1..4 = cars; static 0..3 = floor/ceiling/-x wall/+x wall planes, 4 = mesh);
+ * dynamic-dynamic = 64 + a*8 + b (a<b).  count == 0 marks a free slot. */
+typedef struct {
+    int32_t key;
+    int32_t count;
+    rlgpu_contact pts[4];
+} rlgpu_manifold;
+
+/* Rigid body, bullet units (1 = 50 uu); rot is btMatrix3x3 row-major, columns = forward,right,up. */
+typedef struct {
+    float pos[3];
+    float rot[9];
+    float vel[3];
+    float angvel[3];
+} rlgpu_body;
+
+/* Car (RocketSim CarState, Car.h:17-100, plus the btVehicleRL wheel values that persist
+ * across ticks, btVehicleRL.h:9-30, and CarControls). */
+typedef struct {
+    rlgpu_body body;
+    float controls[8];      /* throttle, steer, pitch, yaw, roll, jump, boost, handbrake */
+    float last_controls[8];
+    float boost, jump_time, flip_time, air_time, air_time_since_jump, time_spent_boosting;
+    float supersonic_time, handbrake_val, auto_flip_timer, auto_flip_torque_scale;
+    float demo_respawn_timer, car_contact_cooldown;
+    float flip_rel_torque[3];
+    float world_contact_normal[3];
+    float vel_impulse_cache[3];
+    float ball_hit_rel_pos[3], ball_hit_ball_pos[3], ball_hit_extra_vel[3];
+    int64_t ball_hit_tick;        /* -1 == never (~0ULL in the reference) */
+    int64_t ball_hit_extra_tick;  /* -1 == never */
+    uint32_t car_contact_other_id;
+    uint8_t is_on_ground, has_jumped, has_double_jumped, has_flipped;
+    uint8_t is_flipping, is_jumping, is_supersonic, is_auto_flipping;
+    uint8_t world_contact, is_demoed, ball_hit_valid, pad0;
+    uint8_t wheel_contact[4];
+    /* btWheelInfoRL values read one tick after they are written */
+    float wheel_steer[4], wheel_engine_force[4], wheel_brake[4];
+    float wheel_lat_friction[4], wheel_long_friction[4], wheel_extra_pushback[4];
+} rlgpu_car;
+
+typedef struct {
+    float cooldown;
+    uint8_t is_active;
+    uint8_t pad[3];
+    uint32_t prev_locked_car_id;
+} rlgpu_pad;
+
+/* Per-arena env bookkeeping (GameState + plugin state). */
+typedef struct {
+    int64_t tick_count;          /* Arena::tickCount */
+    int64_t last_tick_count;     /* GameState::lastTickCount */
+    float prev_ball_vel[3];      /* GameState::prev->ball.vel (uu/s) */
+    float prev_boost[RLGPU_CARS];
+    uint8_t prev_is_flipping[RLGPU_CARS];
+    uint8_t prev_on_ground[RLGPU_CARS];
+    uint8_t has_prev;            /* prevGameStates[i] non-empty */
+    uint8_t terminal;            /* last terminal type (0/1/2) */
+    uint8_t pad[2];
+    float prev_action[RLGPU_CARS][8];
+    float no_touch_time;         /* NoTouchCondition::timeSinceTouch */
+    int32_t score_blue, score_orange;     /* ScoreLimitCondition */
+    int32_t penalty_blue, penalty_orange; /* LosingPenaltyReward */
+    uint8_t ev_bump[RLGPU_CARS], ev_bumped[RLGPU_CARS], ev_demo[RLGPU_CARS], ev_demoed[RLGPU_CARS];
+    uint32_t rng_counter;        /* Philox counter for this arena's draws */
+    uint32_t manifold_overflow;  /* contacts dropped because all slots were busy */
+} rlgpu_env_extra;
+
+/* Complete serialised arena (the wire format of rlgpu_envset_get/set_arenas). */
+typedef struct {
+    rlgpu_body ball;
+    float ball_vel_impulse_cache[3];
+    int32_t ball_sleeping;
+    rlgpu_car cars[RLGPU_CARS];
+    rlgpu_pad pads[RLGPU_PADS];
+    rlgpu_manifold manifolds[RLGPU_MANIFOLDS];
+    rlgpu_env_extra env;
+} rlgpu_arena_state;
+
+typedef struct {
+    int32_t num_arenas;
+    int32_t tick_skip;       /* LearnerConfig::tickSkip (ExampleMain.cpp:356) */
+    int32_t action_delay;    /* LearnerConfig::actionDelay = tickSkip-1 (ExampleMain.cpp:358) */
+    uint64_t seed;           /* Philox key: kickoff shuffles and demo respawns */
+    int32_t save_rewards;    /* keep per-reward values of player 0 (EnvSetConfig::saveRewards) */
+} rlgpu_envset_config;
+
+typedef struct rlgpu_envset rlgpu_envset;
+
+/* Device views of EnvState (EnvSet.h:35-65).  Valid until rlgpu_envset_destroy. */
+typedef struct {
+    float* obs;              /* [num_players][RLGPU_OBS] */
+    uint8_t* action_masks;   /* [num_players][RLGPU_ACTIONS] */
+    float* rewards;          /* [num_players] */
+    uint8_t* terminals;      /* [num_arenas]: 0, 1 NORMAL, 2 TRUNCATED */
+    float* last_rewards;     /* [num_arenas][RLGPU_REWARDS] (if save_rewards) */
+    float* trunc_obs;        /* [num_players][RLGPU_OBS] pre-reset obs of truncated arenas */
+    int32_t num_players;
+    int32_t num_arenas;
+} rlgpu_envset_buffers;
+
+/* Creates the set, resets every arena to a random kickoff (EnvSet.cpp:105-110). */
+int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset** out);
+int rlgpu_envset_destroy(rlgpu_envset* env);
+int rlgpu_envset_buffers_get(rlgpu_envset* env, rlgpu_envset_buffers* out);
+
+/* EnvSet::Reset(): reset arenas whose terminal flag is set, rebuild their obs/masks. */
+int rlgpu_envset_reset(rlgpu_envset* env, void* stream);
+/* EnvSet::ResetArena(i) for every i with d_mask[i] != 0 (d_mask == NULL: all arenas). */
+int rlgpu_envset_reset_arenas(rlgpu_envset* env, const uint8_t* d_mask, void* stream);
+
+/* Two-half step with the reference's action delay. */
+int rlgpu_envset_step_first_half(rlgpu_envset* env, void* stream);
+int rlgpu_envset_step_second_half(rlgpu_envset* env, const int32_t* d_actions, void* stream);
+/* Fused: first half + second half + (optional) reset of terminated arenas in one launch.
+ * If d_obs_out != NULL the post-reset obs rows are also written there (experience append:
+ * the row for step t+1 of the rollout buffer); pre-reset obs of TRUNCATED arenas go to
+ * buffers.trunc_obs. */
+int rlgpu_envset_step(rlgpu_envset* env, const int32_t* d_actions, int32_t reset_terminated,
+                      float* d_obs_out, void* stream);
+int rlgpu_envset_sync(rlgpu_envset* env, void* stream);
+
+/* Wire-format state transfer (host <-> device), for GameState snapshots, tests and replay. */
+int rlgpu_envset_get_arenas(rlgpu_envset* env, int32_t first, int32_t count, rlgpu_arena_state* h_out);
+int rlgpu_envset_set_arenas(rlgpu_envset* env, int32_t first, int32_t count, const rlgpu_arena_state* h_in);
+/* Rebuild obs/masks of all arenas from the current state (no physics). */
+int rlgpu_envset_build_obs(rlgpu_envset* env, void* stream);
+
+/* Static sizes for binding checks. */
+int rlgpu_arena_state_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

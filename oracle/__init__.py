@@ -65,3 +65,98 @@ def gae_rollout(rews, terms, vals, trunc_vals, boot_vals, gamma, lam, return_std
     f(_p(rews), _p(terms), _p(vals), _p(tv), _p(bv), T, N, gamma, lam, return_std, clip_range,
       _p(adv), _p(tgt), _p(ret))
     return adv, tgt, ret
+
+
+# ------------------------------------------------------------------ env (rsim_ref.cpp + env_ref.cpp)
+OBS, ACTIONS, REWARDS, PADS = 167, 90, 13, 34
+
+
+def arena_state_size():
+    return lib().oracle_arena_state_size()
+
+
+class EnvSet:
+    """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
+
+    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1):
+        L = lib()
+        L.oracle_env_create.restype = ctypes.c_void_p
+        L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        for n in ("oracle_env_destroy", "oracle_env_step_first_half", "oracle_env_reset", "oracle_env_build_obs"):
+            getattr(L, n).argtypes = [ctypes.c_void_p]
+        L.oracle_env_step_second_half.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_env_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_env_reset_arenas.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_env_get_arenas.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_env_set_arenas.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_env_read.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
+        self.L = L
+        self.n = num_arenas
+        self.h = L.oracle_env_create(num_arenas, seed, tick_skip, action_delay, threads)
+        P = 4 * num_arenas
+        self.obs = np.zeros((P, OBS), np.float32)
+        self.masks = np.zeros((P, ACTIONS), np.uint8)
+        self.rewards = np.zeros(P, np.float32)
+        self.terminals = np.zeros(num_arenas, np.uint8)
+        self.trunc_obs = np.zeros((P, OBS), np.float32)
+        self.last_rewards = np.zeros((num_arenas, REWARDS), np.float32)
+        self.read()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oracle_env_destroy(self.h)
+            self.h = None
+
+    def read(self):
+        self.L.oracle_env_read(self.h, _p(self.obs), _p(self.masks), _p(self.rewards), _p(self.terminals),
+                               _p(self.trunc_obs), _p(self.last_rewards))
+
+    def step_first_half(self):
+        self.L.oracle_env_step_first_half(self.h)
+
+    def step_second_half(self, actions):
+        a = np.ascontiguousarray(actions, np.int32)
+        self.L.oracle_env_step_second_half(self.h, _p(a))
+        self.read()
+
+    def step(self, actions, reset_terminated=True):
+        a = np.ascontiguousarray(actions, np.int32)
+        self.L.oracle_env_step(self.h, _p(a), int(reset_terminated))
+        self.read()
+
+    def reset(self):
+        self.L.oracle_env_reset(self.h)
+        self.read()
+
+    def reset_arenas(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self.L.oracle_env_reset_arenas(self.h, _p(m))
+        self.read()
+
+    def build_obs(self):
+        self.L.oracle_env_build_obs(self.h)
+        self.read()
+
+    def get_arenas(self, first=0, count=None):
+        count = self.n - first if count is None else count
+        buf = np.zeros(count * arena_state_size(), np.uint8)
+        self.L.oracle_env_get_arenas(self.h, first, count, _p(buf))
+        return buf
+
+    def set_arenas(self, buf, first=0):
+        buf = np.ascontiguousarray(buf, np.uint8)
+        count = buf.size // arena_state_size()
+        self.L.oracle_env_set_arenas(self.h, first, count, _p(buf))
+
+
+def action_table():
+    t = np.zeros((ACTIONS, 8), np.float32)
+    m = np.zeros((4, ACTIONS), np.uint8)
+    lib().oracle_action_table(_p(t), _p(m))
+    return t, m
+
+
+def pad_map():
+    m = np.zeros(PADS, np.int32)
+    lib().oracle_pad_map(_p(m))
+    return m

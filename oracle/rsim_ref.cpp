@@ -1,0 +1,2188 @@
+// rsim_ref.cpp -- ORACLE (test infrastructure only; never linked into the product).
+//
+// Scalar, one-arena-at-a-time C++ restatement of the reference hot path:
+//   RocketSim arena step   GigaLearnCPP/RLGymCPP/RocketSim/src/Sim/Arena/Arena.cpp:716-812
+//   car logic              .../Sim/Car/Car.cpp:58-833
+//   vehicle                .../Sim/btVehicleRL/btVehicleRL.cpp:64-421
+//   ball / pads            .../Sim/Ball/Ball.cpp:112-138, .../Sim/BoostPad/BoostPad.cpp:51-105,
+//                          .../Sim/BoostPad/BoostPadGrid/BoostPadGrid.cpp:5-25
+//   contact callbacks      Arena.cpp:218-427
+//   Bullet subset          btDiscreteDynamicsWorld.cpp:325-437, btRigidBody.cpp:95-420,
+//                          btSequentialImpulseConstraintSolver.cpp:440-1900 (scalar path),
+//                          btPersistentManifold.cpp:100-330, btManifoldResult.cpp:110-200,
+//                          SphereTriangleDetector.cpp:88-240, btSphereBoxCollisionAlgorithm.cpp,
+//                          btConvexPlaneCollisionAlgorithm.cpp:53-90, btContactConstraint.cpp:60-150
+//   env                    GigaLearnCPP/RLGymCPP/src/RLGymCPP/EnvSet/EnvSet.cpp:113-354 + the plugin set
+//                          of src/ExampleMain.cpp:46-226 (see env_ref.cpp)
+//
+// Parity status: UNPINNED by the reference (no tests, no runnable binary -- SURVEY.md 8c);
+// pinned by known-answer tests of constants/tables/spawn poses (tests/test_env_oracle.py).
+// Documented deviations from the reference (also in DESIGN.md):
+//   * synthetic arena mesh (include/rlgpu_arena_mesh.h) instead of the absent .cmf meshes;
+//   * box-triangle and box-box contacts use SAT (1 point) instead of GJK/EPA / btBoxBoxDetector;
+//   * internal-edge normal adjustment is not applied (no shared edges with differing normals
+//     inside a quad of the synthetic mesh);
+//   * time-based deactivation (btRigidBody.h:531-545) is not modelled -- only the zero-velocity
+//     ball sleep of Arena.cpp:722-727;
+//   * manifolds are cleared on kickoff reset / SetState; wheels resting on another dynamic body
+//     read that body's tick-start velocity (the reference's order is unordered_set iteration order);
+//   * transcendentals use include/rlgpu_detmath.h (shared with the kernels) instead of libm.
+#include "rsim_ref.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "../include/rlgpu_arena_mesh.h"
+#include "../include/rlgpu_detmath.h"
+
+namespace orc {
+
+// ------------------------------------------------------------------ constants (RLConst.h)
+const float UU_TO_BT = 1.f / 50.f;  // BulletLink.h:15
+const float BT_TO_UU = 50.f;        // BulletLink.h:12
+const float TICK_TIME = 1.f / 120.f;
+const float CAR_MASS = 180.f;
+const float BALL_MASS = CAR_MASS / 6.f;
+const float BALL_RADIUS_UU = 91.25f;
+const float GRAVITY_Z_UU = -650.f;
+
+// ---------------------------------------------------------------- LinearPieceCurve (Math.cpp:5-34)
+struct Curve {
+    int n;
+    float k[6], v[6];
+    float out(float input, float def = 1.f) const {
+        if (n == 0) return def;
+        if (input <= k[0]) return v[0];
+        for (int i = 1; i < n; i++) {
+            if (k[i] > input) {
+                float range = k[i] - k[i - 1];
+                float diff = v[i] - v[i - 1];
+                float f = (input - k[i - 1]) / range;
+                return v[i - 1] + diff * f;
+            }
+        }
+        return v[n - 1];
+    }
+};
+// RLConst.h:342-437
+const Curve STEER_ANGLE_FROM_SPEED = {6, {0, 500, 1000, 1500, 1750, 3000}, {0.53356f, 0.31930f, 0.18203f, 0.10570f, 0.08507f, 0.03454f}};
+const Curve POWERSLIDE_STEER_ANGLE = {2, {0, 2500}, {0.39235f, 0.12610f}};
+const Curve DRIVE_SPEED_TORQUE_FACTOR = {3, {0, 1400, 1410}, {1.0f, 0.1f, 0.0f}};
+const Curve NON_STICKY_FRICTION_FACTOR = {3, {0, 0.7075f, 1}, {0.1f, 0.5f, 1.0f}};
+const Curve LAT_FRICTION = {2, {0, 1}, {1.0f, 0.2f}};
+const Curve LONG_FRICTION = {0, {}, {}};
+const Curve HANDBRAKE_LAT_FRICTION_FACTOR = {1, {0}, {0.1f}};
+const Curve HANDBRAKE_LONG_FRICTION_FACTOR = {2, {0, 1}, {0.5f, 0.9f}};
+const Curve BALL_CAR_EXTRA_IMPULSE_FACTOR = {4, {0, 500, 2300, 4600}, {0.65f, 0.65f, 0.55f, 0.30f}};
+const Curve BUMP_VEL_AMOUNT_GROUND = {3, {0, 1400, 2200}, {5.f / 6.f, 1100.f, 1530.f}};
+const Curve BUMP_VEL_AMOUNT_AIR = {3, {0, 1400, 2200}, {5.f / 6.f, 1390.f, 1945.f}};
+const Curve BUMP_UPWARD_VEL_AMOUNT = {3, {0, 1400, 2200}, {2.f / 6.f, 278.f, 417.f}};
+
+// -------------------------------------------------------------------- static world
+World::World() {
+    ball_radius = BALL_RADIUS_UU * UU_TO_BT;
+    // btSphereShape::calculateLocalInertia (btSphereShape.cpp:61-65)
+    float elem = 0.4f * BALL_MASS * ball_radius * ball_radius;
+    ball_inv_inertia = V(1.f / elem, 1.f / elem, 1.f / elem);
+    ball_inv_mass = 1.f / BALL_MASS;
+    // Octane (CarConfig.cpp:20-70): box half extents through btBoxShape margin handling
+    V hs = V(120.507f, 86.6994f, 38.6591f) * UU_TO_BT;
+    V h(hs.x / 2.f, hs.y / 2.f, hs.z / 2.f);
+    const float margin = 0.04f;
+    car_half = V((h.x - margin) + margin, (h.y - margin) + margin, (h.z - margin) + margin);
+    car_offset = V(13.87566f, 0.f, 20.755f) * UU_TO_BT;
+    float lx = 2.f * car_half.x, ly = 2.f * car_half.y, lz = 2.f * car_half.z;  // btBoxShape.cpp
+    V inertia = V(ly * ly + lz * lz, lx * lx + lz * lz, lx * lx + ly * ly) * (CAR_MASS / 12.f);
+    car_inv_inertia = V(1.f / inertia.x, 1.f / inertia.y, 1.f / inertia.z);
+    car_inv_mass = 1.f / CAR_MASS;
+    // wheels (Car.cpp:231-277)
+    for (int i = 0; i < 4; i++) {
+        bool front = i < 2, left = i % 2;
+        float radius = front ? 12.50f : 15.00f;
+        V off = front ? V(51.25f, 25.90f, 20.755f) : V(-33.75f, 29.50f, 20.755f);
+        if (left) off.y *= -1;
+        float rest = (front ? 38.755f : 37.055f) - 12.f;  // minus MAX_SUSPENSION_TRAVEL
+        wheel_conn[i] = off * UU_TO_BT;
+        wheel_rest[i] = rest * UU_TO_BT;
+        wheel_radius[i] = radius * UU_TO_BT;
+        wheel_force_scale[i] = front ? (36.f - (1.f / 4.f)) : (54.f + (1.f / 4.f) + (1.5f / 100.f));
+    }
+    susp_travel = ((12.f * UU_TO_BT) * 100.f) / 100.f;  // m_maxSuspensionTravelCm / 100
+    // contact breaking thresholds (btCollisionShape.cpp:128-158, btCollisionDispatcher.cpp:76-80)
+    ball_cbt = (float)((double)ball_radius + 0.08) * 0.02f;
+    {
+        V mn = car_offset - car_half, mx = car_offset + car_half;
+        V c = (mn + mx) * 0.5f;
+        float r = len(mx - mn) * 0.5f;
+        car_cbt = (r + len(c)) * 0.02f;
+    }
+    gravity = V(0, 0, GRAVITY_Z_UU) * UU_TO_BT;
+    // btPow(1 - 0.03, 1/120): constant per tick (btRigidBody.cpp:153-163); host libm, double
+    ball_damp = (float)std::pow((double)(1.f - 0.03f), (double)TICK_TIME);
+    // planes (Arena.cpp:1052-1100): normal, point
+    plane_n[0] = V(0, 0, 1);
+    plane_p[0] = V(0, 0, 0);
+    plane_n[1] = V(0, 0, -1);
+    plane_p[1] = V(0, 0, 2048) * UU_TO_BT;
+    plane_n[2] = V(1, 0, 0);
+    plane_p[2] = V(-4096, 0, 2048 / 2) * UU_TO_BT;
+    plane_n[3] = V(-1, 0, 0);
+    plane_p[3] = V(4096, 0, 2048 / 2) * UU_TO_BT;
+    ntris = RLGPU_MESH_TRIS;
+    for (int t = 0; t < ntris; t++) {
+        for (int k = 0; k < 3; k++)
+            tri[t][k] = V(RLGPU_MESH_UU[t][3 * k], RLGPU_MESH_UU[t][3 * k + 1], RLGPU_MESH_UU[t][3 * k + 2]) * UU_TO_BT;
+        V mn = tri[t][0], mx = tri[t][0];
+        for (int k = 1; k < 3; k++)
+            for (int a = 0; a < 3; a++) {
+                mn[a] = std::min(mn[a], tri[t][k][a]);
+                mx[a] = std::max(mx[a], tri[t][k][a]);
+            }
+        tri_min[t] = mn;
+        tri_max[t] = mx;
+    }
+    // spawn / respawn rotations precomputed on the host (RLConst.h:297-338, Arena.cpp:183-186)
+    const float spawn_x[5] = {-2048, 2048, -256, 256, 0}, spawn_y[5] = {-2560, -2560, -3840, -3840, -4608};
+    const float spawn_yaw[5] = {(float)(M_PI_4 * 1), (float)(M_PI_4 * 3), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2),
+                                (float)(M_PI_4 * 2)};
+    for (int i = 0; i < 5; i++) {
+        kick_x[i] = spawn_x[i];
+        kick_y[i] = spawn_y[i];
+        kick_rot[0][i] = euler_ypr(spawn_yaw[i], -0.f, -0.f);
+        kick_rot[1][i] = euler_ypr(spawn_yaw[i] + (float)M_PI, -0.f, -0.f);
+    }
+    const float rs_x[4] = {-2304, -2688, 2304, 2688};
+    for (int i = 0; i < 4; i++) {
+        respawn_x[i] = rs_x[i];
+        respawn_y[i] = -4608;
+        respawn_rot[0][i] = euler_ypr((float)(M_PI / 2) + 0.f, 0.f, 0.f);
+        respawn_rot[1][i] = euler_ypr((float)(M_PI / 2) + (float)M_PI, 0.f, 0.f);
+    }
+    // pads: big 6 then small 28 (Arena.cpp:532-556)
+    const float big[6][3] = {{-3584, 0, 73}, {3584, 0, 73}, {-3072, 4096, 73}, {3072, 4096, 73}, {-3072, -4096, 73}, {3072, -4096, 73}};
+    const float small[28][3] = {{0, -4240, 70},    {-1792, -4184, 70}, {1792, -4184, 70}, {-940, -3308, 70},  {940, -3308, 70},
+                                {0, -2816, 70},    {-3584, -2484, 70}, {3584, -2484, 70}, {-1788, -2300, 70}, {1788, -2300, 70},
+                                {-2048, -1036, 70}, {0, -1024, 70},    {2048, -1036, 70}, {-1024, 0, 70},     {1024, 0, 70},
+                                {-2048, 1036, 70}, {0, 1024, 70},      {2048, 1036, 70},  {-1788, 2300, 70},  {1788, 2300, 70},
+                                {-3584, 2484, 70}, {3584, 2484, 70},   {0, 2816, 70},     {-940, 3308, 70},   {940, 3308, 70},
+                                {-1792, 4184, 70}, {1792, 4184, 70},   {0, 4240, 70}};
+    for (int i = 0; i < RLGPU_PADS; i++) {
+        const float* p = i < 6 ? big[i] : small[i - 6];
+        pad_pos_uu[i] = V(p[0], p[1], p[2]);
+        pad_big[i] = i < 6;
+        pad_pos_bt[i] = pad_pos_uu[i] * UU_TO_BT;
+        float box_rad = (pad_big[i] ? 160.f : 120.f) * UU_TO_BT;  // BoostPad.cpp:44-48
+        pad_box_min[i] = pad_pos_bt[i] - V(box_rad, box_rad, 0);
+        pad_box_max[i] = pad_pos_bt[i] + V(box_rad, box_rad, 64.f * UU_TO_BT);
+        pad_cell_x[i] = (int)(pad_pos_uu[i].x / 1024 + 4);  // BoostPadGrid.cpp:30-31
+        pad_cell_y[i] = (int)(pad_pos_uu[i].y / 1024 + 5);
+    }
+}
+
+const World& world() {
+    static World w;
+    return w;
+}
+
+// ------------------------------------------------------------------ Philox 4x32-10
+void philox(uint64_t key, uint32_t c0, uint32_t c1, uint32_t out[4]) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    uint32_t x0 = c0, x1 = c1, x2 = 0x9E3779B9u, x3 = 0x85EBCA6Bu;
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+        uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0, y1 = (uint32_t)p1, y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1,
+                 y3 = (uint32_t)p0;
+        x0 = y0;
+        x1 = y1;
+        x2 = y2;
+        x3 = y3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = x0;
+    out[1] = x1;
+    out[2] = x2;
+    out[3] = x3;
+}
+
+uint32_t rng_next(uint64_t seed, int arena, rlgpu_env_extra& env) {
+    uint32_t o[4];
+    philox(seed, (uint32_t)arena, env.rng_counter++, o);
+    return o[0];
+}
+
+// Working copy of a rigid body during a tick (btRigidBody subset).
+struct Body {
+    V pos, vel, ang, force, torque;
+    M rot, inv_inertia_world;
+    V inv_inertia_local;
+    float inv_mass;
+    bool no_rot, active, present;
+    V pred_pos;  // interpolation transform (predictUnconstraintMotion) -> broadphase AABB
+    M pred_rot;
+    void update_inertia() { inv_inertia_world = scaled(rot, inv_inertia_local) * transpose(rot); }
+    V vel_at(V rel) const { return vel + cross(ang, rel); }  // getVelocityInLocalPoint
+    void apply_central_impulse(V imp) { vel += imp * inv_mass; }
+    void apply_torque_impulse(V t) { ang += inv_inertia_world * t; }
+    void apply_impulse(V imp, V rel) {
+        if (inv_mass != 0.f) {
+            apply_central_impulse(imp);
+            apply_torque_impulse(cross(rel, imp));
+        }
+    }
+    float impulse_denominator(V pos_w, V n) const {  // btRigidBody::computeImpulseDenominator
+        V r0 = pos_w - pos;
+        V c0 = cross(r0, n);
+        V vec = cross(vmul(c0, inv_inertia_world), r0);
+        return inv_mass + dot(n, vec);
+    }
+};
+
+// ---------------------------------------------------------------- arena working set
+struct Sim {
+    const World& w;
+    rlgpu_arena_state& s;
+    uint64_t seed;
+    int arena_index;
+    Body b[5];  // 0 ball, 1..4 cars
+    // per-tick transient vehicle data
+    struct WheelTick {
+        V hard_point, wheel_dir, axle, contact_point, contact_normal, wt_col1;
+        float susp_len, susp_rel_vel, clipped_inv, susp_force;
+        bool in_contact, contact_world;
+        int ground;  // -1 none, 0 ball, 1..4 cars, 10 static
+        V impulse;
+    } wt[4][4];
+    Body snap[5];  // tick-start snapshot for wheel-on-dynamic-body friction
+    // event sink for the env layer
+    bool ev_bump[4], ev_demo[4];
+
+    Sim(const World& w_, rlgpu_arena_state& s_, uint64_t seed_, int idx) : w(w_), s(s_), seed(seed_), arena_index(idx) {}
+
+    rlgpu_car& car(int i) { return s.cars[i]; }  // i = 0..3
+    static bool car_team_orange(int i) { return i & 1; }  // creation order B,O,B,O (ExampleMain.cpp:204-208)
+    static uint32_t car_id(int i) { return (uint32_t)(i + 1); }
+
+    void load_bodies() {
+        const World& W = w;
+        Body& ball = b[0];
+        ball.pos = ld3(s.ball.pos);
+        ball.rot = ldm(s.ball.rot);
+        ball.vel = ld3(s.ball.vel);
+        ball.ang = ld3(s.ball.angvel);
+        ball.inv_mass = W.ball_inv_mass;
+        ball.inv_inertia_local = W.ball_inv_inertia;
+        ball.no_rot = true;
+        ball.present = true;
+        ball.force = ball.torque = V();
+        ball.update_inertia();
+        for (int i = 0; i < 4; i++) {
+            Body& c = b[i + 1];
+            rlgpu_car& cs = car(i);
+            c.pos = ld3(cs.body.pos);
+            c.rot = ldm(cs.body.rot);
+            c.vel = ld3(cs.body.vel);
+            c.ang = ld3(cs.body.angvel);
+            c.inv_mass = W.car_inv_mass;
+            c.inv_inertia_local = W.car_inv_inertia;
+            c.no_rot = false;
+            c.present = true;
+            c.force = c.torque = V();
+            c.update_inertia();
+        }
+    }
+    void store_bodies() {
+        st3(s.ball.pos, b[0].pos);
+        stm(s.ball.rot, b[0].rot);
+        st3(s.ball.vel, b[0].vel);
+        st3(s.ball.angvel, b[0].ang);
+        for (int i = 0; i < 4; i++) {
+            rlgpu_car& cs = car(i);
+            st3(cs.body.pos, b[i + 1].pos);
+            stm(cs.body.rot, b[i + 1].rot);
+            st3(cs.body.vel, b[i + 1].vel);
+            st3(cs.body.angvel, b[i + 1].ang);
+        }
+    }
+
+    // -------------------------------------------------------------- shapes / AABBs
+    V car_box_center(int bi) const { return b[bi].pos + b[bi].rot * w.car_offset; }
+    void body_aabb(int bi, V pos, const M& rot, V& mn, V& mx) const {
+        if (bi == 0) {
+            float m = w.ball_radius + 0.08f;  // btSphereShape.cpp:55 (RocketSim change)
+            mn = pos - V(m, m, m);
+            mx = pos + V(m, m, m);
+        } else {  // btCompoundShape::getAabb
+            V center = pos + rot * w.car_offset;
+            V e;
+            for (int r = 0; r < 3; r++)
+                e[r] = std::fabs(rot.r[r].x) * w.car_half.x + std::fabs(rot.r[r].y) * w.car_half.y +
+                       std::fabs(rot.r[r].z) * w.car_half.z;
+            mn = center - e;
+            mx = center + e;
+        }
+    }
+    // broadphase AABB: current + predicted transform, expanded by gContactBreakingThreshold
+    void broad_aabb(int bi, V& mn, V& mx) const {
+        V a0, a1, p0, p1;
+        body_aabb(bi, b[bi].pos, b[bi].rot, a0, a1);
+        body_aabb(bi, b[bi].pred_pos, b[bi].pred_rot, p0, p1);
+        for (int k = 0; k < 3; k++) {
+            mn[k] = std::min(a0[k], p0[k]) - 0.02f;
+            mx[k] = std::max(a1[k], p1[k]) + 0.02f;
+        }
+    }
+
+    // ---------------------------------------------------------------- ray tests
+    // Closest hit of segment [from,to] against the world (btCollisionWorld::rayTest +
+    // ClosestRayResultCallback), ignoring body `self`.  Returns hit object id:
+    // -1 none, 0 ball, 1..4 car, 10 static.  (btDefaultVehicleRaycaster.cpp:32-52)
+    int ray_cast(V from, V to, int self, V& hit_point, V& hit_normal, float& frac) {
+        float best = 1.0f;
+        int obj = -1;
+        V nrm;
+        V d = to - from;
+        // static planes (btStaticPlaneShape as triangles -> plane intersection)
+        for (int p = 0; p < 4; p++) {
+            float da = dot(w.plane_n[p], from - w.plane_p[p]);
+            float db = dot(w.plane_n[p], to - w.plane_p[p]);
+            if (da * db >= 0.f) continue;
+            float f = da / (da - db);
+            if (f < best) {
+                best = f;
+                obj = 10;
+                nrm = da > 0.f ? w.plane_n[p] : -w.plane_n[p];
+            }
+        }
+        // mesh triangles (btTriangleRaycastCallback::processTriangle)
+        for (int t = 0; t < w.ntris; t++) {
+            const V& v0 = w.tri[t][0];
+            const V& v1 = w.tri[t][1];
+            const V& v2 = w.tri[t][2];
+            V tn = cross(v1 - v0, v2 - v0);
+            float dist = dot(v0, tn);
+            float da = dot(tn, from) - dist;
+            float db = dot(tn, to) - dist;
+            if (da * db >= 0.f) continue;
+            float f = da / (da - db);
+            if (f < best) {
+                float tol = len2(tn) * -0.0001f;
+                V pt = from + d * f;
+                V v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
+                if (dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol) {
+                    best = f;
+                    obj = 10;
+                    V n = normalized(tn);
+                    nrm = da <= 0.f ? -n : n;
+                }
+            }
+        }
+        // ball sphere (analytic; hits only from outside)
+        {
+            V oc = from - b[0].pos;
+            float a = dot(d, d), bb = dot(oc, d), c = dot(oc, oc) - w.ball_radius * w.ball_radius;
+            if (c > 0.f) {
+                float disc = bb * bb - a * c;
+                if (disc >= 0.f && bb < 0.f) {
+                    float f = (-bb - std::sqrt(disc)) / a;
+                    if (f >= 0.f && f < best) {
+                        best = f;
+                        obj = 0;
+                        nrm = normalized((from + d * f) - b[0].pos);
+                    }
+                }
+            }
+        }
+        // other cars (OBB slab test, from outside); demoed cars still block (no response -> miss)
+        for (int ci = 1; ci <= 4; ci++) {
+            if (ci == self) continue;
+            V c = car_box_center(ci);
+            const M& R = b[ci].rot;
+            V lo = vmul(from - c, R), ld = vmul(d, R);  // into box frame (R^T * v)
+            float tmin = 0.f, tmax = best;
+            int axis = -1;
+            float sgn = 0.f;
+            bool ok = true;
+            for (int k = 0; k < 3 && ok; k++) {
+                float h = w.car_half[k];
+                if (std::fabs(ld[k]) < 1e-12f) {
+                    if (lo[k] < -h || lo[k] > h) ok = false;
+                    continue;
+                }
+                float inv = 1.f / ld[k];
+                float t1 = (-h - lo[k]) * inv, t2 = (h - lo[k]) * inv;
+                float s1 = -1.f;
+                if (t1 > t2) {
+                    std::swap(t1, t2);
+                    s1 = 1.f;
+                }
+                if (t1 > tmin) {
+                    tmin = t1;
+                    axis = k;
+                    sgn = s1;
+                }
+                if (t2 < tmax) tmax = t2;
+                if (tmin > tmax) ok = false;
+            }
+            if (ok && axis >= 0 && tmin < best) {
+                best = tmin;
+                obj = ci;
+                V ln;
+                ln[axis] = sgn;
+                nrm = R * ln;
+            }
+        }
+        if (obj < 0) return -1;
+        frac = best;
+        hit_point = from + d * best;  // setInterpolate3
+        hit_normal = normalized(nrm);
+        if (obj >= 1 && obj <= 4 && !b[obj].active) return -1;  // CF_NO_CONTACT_RESPONSE
+        return obj;
+    }
+
+    // ------------------------------------------------------------------ vehicle
+    // btVehicleRL::updateWheelTransform / updateWheelTransformsWS (btVehicleRL.cpp:64-113)
+    void wheel_transforms(int ci) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        for (int i = 0; i < 4; i++) {
+            WheelTick& W = wt[ci][i];
+            W.hard_point = c.rot * w.wheel_conn[i] + c.pos;
+            W.wheel_dir = c.rot * V(0, 0, -1);
+            W.axle = c.rot * V(0, -1, 0);
+            V up = -W.wheel_dir;
+            V right = W.axle;
+            Q q = quat_axis_angle(up, cs.wheel_steer[i]);
+            M steer = mat_from_quat(q);
+            // basis2 column 1 (right axis) = -right; column 1 of steer*basis2 = steer * (-right)
+            W.wt_col1 = steer * (-right);
+        }
+    }
+
+    // btVehicleRL::rayCast (btVehicleRL.cpp:118-207)
+    void wheel_ray(int ci, int i) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        WheelTick& W = wt[ci][i];
+        W.in_contact = false;
+        W.contact_world = false;
+        float rest = w.wheel_rest[i], radius = w.wheel_radius[i], travel = w.susp_travel;
+        float ray_len = rest + travel + radius - 0.05f;
+        V source = W.hard_point;
+        V target = source + W.wheel_dir * ray_len;
+        W.contact_point = target;
+        W.ground = -1;
+        V hp, hn;
+        float frac = 1.f;
+        int obj = ray_cast(source, target, ci + 1, hp, hn, frac);
+        V upv = c.rot.col(2);
+        if (obj >= 0) {
+            W.contact_point = hp;
+            W.contact_normal = hn;
+            W.in_contact = true;
+            W.contact_world = (obj == 10);
+            W.ground = obj;
+            float trace = dot(W.hard_point - W.contact_point, upv);
+            W.susp_len = trace - radius;
+            W.susp_len = std::clamp(W.susp_len, rest - travel, rest + travel);
+            float denom = dot(W.contact_normal, upv);
+            V relpos = W.contact_point - c.pos;
+            V vel_at = c.vel_at(relpos);
+            float proj = dot(W.contact_normal, vel_at);
+            if (denom > 0.1f) {
+                float inv = 1.f / denom;
+                W.susp_rel_vel = proj * inv;
+                W.clipped_inv = inv;
+            } else {
+                W.susp_rel_vel = 0.f;
+                W.clipped_inv = 10.f;
+            }
+            if (obj == 10) {  // static: extra pushback (resolveSingleCollision, btContactConstraint.cpp:60-105)
+                float thresh = (rest + radius) - 0.05f;
+                if (trace < thresh) {
+                    float dist = trace - thresh;
+                    V rel1 = hp - c.pos;
+                    V v1 = c.vel_at(rel1);
+                    float rel_vel = dot(hn, v1);
+                    float pos_err = 0.2f * -dist / TICK_TIME;
+                    float vel_err = -(1.0f + 0.f) * rel_vel;
+                    float denom0 = c.impulse_denominator(hp, hn);
+                    float jinv = 1.f / (denom0 + 0.f);
+                    float imp = pos_err * jinv + vel_err * jinv;
+                    imp = 0.f > imp ? 0.f : imp;
+                    cs.wheel_extra_pushback[i] = imp / 4;
+                }
+            }
+        } else {
+            W.susp_len = rest + travel;
+            W.susp_rel_vel = 0.f;
+            W.contact_normal = -W.wheel_dir;
+            W.clipped_inv = 1.f;
+            cs.wheel_extra_pushback[i] = 0.f;
+        }
+    }
+
+    // ground body data for friction: velocity / mass / inertia (static -> zero)
+    void ground_info(int g, V rel, V& vel, float& inv_mass, V& inv_iner, M& rot, V& com) {
+        if (g >= 0 && g <= 4) {
+            const Body& o = snap[g];
+            vel = o.vel_at(rel);
+            inv_mass = o.inv_mass;
+            inv_iner = o.inv_inertia_local;
+            rot = o.rot;
+            com = o.pos;
+        } else {
+            vel = V();
+            inv_mass = 0.f;
+            inv_iner = V();
+            rot = M::ident();
+            com = V();
+        }
+    }
+
+    // btVehicleRL::calcFrictionImpulses (btVehicleRL.cpp:308-369)
+    void calc_friction(int ci) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        const float friction_scale = CAR_MASS / 3;
+        for (int i = 0; i < 4; i++) {
+            WheelTick& W = wt[ci][i];
+            if (W.ground < 0) {
+                W.impulse = V();
+                continue;
+            }
+            V axle = W.wt_col1;
+            V n = W.contact_normal;
+            float proj = dot(axle, n);
+            axle -= n * proj;
+            axle = safe_normalized(axle);
+            V fwd = safe_normalized(cross(n, axle));
+            // resolveSingleBilateral (btContactConstraint.cpp:108-150)
+            float side;
+            {
+                V cp = W.contact_point;
+                V rel1 = cp - c.pos;
+                V gvel;
+                float g_inv_mass;
+                V g_iner, g_com;
+                M g_rot;
+                ground_info(W.ground, V(), gvel, g_inv_mass, g_iner, g_rot, g_com);
+                V rel2 = cp - g_com;
+                V v1 = c.vel_at(rel1);
+                V v2 = (W.ground >= 0 && W.ground <= 4) ? snap[W.ground].vel_at(rel2) : V();
+                V vel = v1 - v2;
+                V aJ = transpose(c.rot) * cross(rel1, axle);
+                V bJ = transpose(g_rot) * cross(rel2, -axle);
+                V m0 = c.inv_inertia_local * aJ;
+                V m1 = g_iner * bJ;
+                float adiag = c.inv_mass + dot(m0, aJ) + g_inv_mass + dot(m1, bJ);
+                float jinv = 1.f / adiag;
+                float rel_vel = dot(axle, vel);
+                side = -0.2f * rel_vel * jinv;
+            }
+            float rolling;
+            if (cs.wheel_engine_force[i] == 0.f) {
+                if (cs.wheel_brake[i] != 0.f) {
+                    V cp = W.contact_point;
+                    V car_rel = cp - c.pos;
+                    V v1 = c.vel_at(car_rel);
+                    V v2 = (W.ground >= 0 && W.ground <= 4) ? snap[W.ground].vel_at(car_rel) : V();
+                    float rel_vel = dot(v1 - v2, fwd);
+                    const float MAGIC = 113.73963f;
+                    rolling = std::clamp(-rel_vel * MAGIC, -cs.wheel_brake[i], cs.wheel_brake[i]);
+                } else {
+                    rolling = 0.f;
+                }
+            } else {
+                rolling = -cs.wheel_engine_force[i] / friction_scale;
+            }
+            V total = (fwd * rolling * cs.wheel_long_friction[i]) + (axle * side * cs.wheel_lat_friction[i]);
+            W.impulse = total * friction_scale;
+        }
+    }
+
+    V upwards_dir_from_wheels(int ci) {
+        V sum;
+        for (int i = 0; i < 4; i++)
+            if (wt[ci][i].in_contact) sum += wt[ci][i].contact_normal;
+        if (sum.x == 0 && sum.y == 0 && sum.z == 0) return b[ci + 1].rot.col(2);
+        return safe_normalized(sum);
+    }
+
+    // Car::_PreTickUpdate demo block (Car.cpp:66-84), hoisted in front of all cars' pre-ticks so
+    // the vehicle phase can run car-parallel; RNG draws stay in car order.
+    void demo_timers() {
+        for (int ci = 0; ci < 4; ci++) {
+            rlgpu_car& cs = car(ci);
+            if (cs.is_demoed) {
+                cs.demo_respawn_timer = std::max(cs.demo_respawn_timer - TICK_TIME, 0.f);
+                if (cs.demo_respawn_timer == 0.f) respawn(ci);
+            }
+        }
+    }
+
+    // ---------------------------------------------------------------- Car::_PreTickUpdate
+    void car_pre_tick(int ci) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        float* ctl = cs.controls;
+        for (int k = 0; k < 5; k++) ctl[k] = std::clamp(ctl[k], -1.f, 1.f);  // ClampFix
+        // c.active (DISABLE_SIMULATION / CF_NO_CONTACT_RESPONSE) was decided at tick start and the
+        // demo timer / respawn ran for every car before any pre-tick (see demo_timers()).
+        if (cs.is_demoed) return;
+
+        wheel_transforms(ci);
+        for (int i = 0; i < 4; i++) wheel_ray(ci, i);
+        calc_friction(ci);
+
+        bool jump_pressed = ctl[5] != 0.f && cs.last_controls[5] == 0.f;
+        int nwc = 0;
+        for (int i = 0; i < 4; i++) {
+            cs.wheel_contact[i] = wt[ci][i].in_contact;
+            nwc += wt[ci][i].in_contact;
+        }
+        cs.is_on_ground = nwc >= 3;
+        float fwd_speed = dot(c.vel, c.rot.col(0)) * BT_TO_UU;
+        update_wheels(ci, nwc, fwd_speed);
+        if (nwc < 3)
+            update_air_torque(ci, nwc == 0);
+        else
+            cs.is_flipping = false;
+        update_jump(ci, jump_pressed);
+        update_auto_flip(ci, jump_pressed);
+        update_double_jump_or_flip(ci, jump_pressed, fwd_speed);
+        if (ctl[0] != 0.f && ((nwc > 0 && nwc < 4) || cs.world_contact)) update_auto_roll(ci, nwc);
+        cs.world_contact = 0;
+        // updateVehicleSecond: updateSuspension + applyFrictionImpulses (btVehicleRL.cpp:237-306,372-389)
+        for (int i = 0; i < 4; i++) {
+            WheelTick& W = wt[ci][i];
+            if (W.in_contact) {
+                float force = (w.wheel_rest[i] - W.susp_len) * 500.f * W.clipped_inv;
+                float damp = (W.susp_rel_vel < 0) ? 25.f : 40.f;
+                W.susp_force = force - (damp * W.susp_rel_vel);
+                W.susp_force *= w.wheel_force_scale[i];
+                if (W.susp_force < 0) W.susp_force = 0;
+            } else {
+                W.susp_force = 0;
+            }
+        }
+        for (int i = 0; i < 4; i++) {
+            WheelTick& W = wt[ci][i];
+            if (W.susp_force != 0) {
+                V off = W.contact_point - c.pos;
+                float base = (W.susp_force * TICK_TIME) + cs.wheel_extra_pushback[i];
+                c.apply_impulse(W.contact_normal * base, off);
+            }
+        }
+        {
+            V up = c.rot.col(2);
+            for (int i = 0; i < 4; i++) {
+                WheelTick& W = wt[ci][i];
+                if (!is_zero(W.impulse)) {
+                    V off = W.contact_point - c.pos;
+                    float d = dot(up, off);
+                    V rel = off - up * d;
+                    c.apply_impulse(W.impulse * TICK_TIME, rel);
+                }
+            }
+        }
+        update_boost(ci);
+    }
+
+    // Car::_UpdateWheels (Car.cpp:330-475)
+    void update_wheels(int ci, int nwc, float fwd_speed) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        const float* ctl = cs.controls;
+        float abs_fwd = std::fabs(fwd_speed);
+        bool world_contact = false;
+        for (int i = 0; i < 4; i++) world_contact |= wt[ci][i].contact_world;
+        if (ctl[7] != 0.f)
+            cs.handbrake_val += 5.f * TICK_TIME;
+        else
+            cs.handbrake_val -= 2.f * TICK_TIME;
+        cs.handbrake_val = std::clamp(cs.handbrake_val, 0.f, 1.f);
+        float real_throttle = ctl[0];
+        float real_brake = 0;
+        if (ctl[6] != 0.f && cs.boost > 0) real_throttle = 1;
+        {
+            float drive_scale = DRIVE_SPEED_TORQUE_FACTOR.out(abs_fwd);
+            float engine_throttle = real_throttle;
+            if (ctl[7] != 0.f) {
+            } else {
+                float abs_throttle = std::fabs(real_throttle);
+                if (abs_throttle >= 0.001f) {
+                    auto sgn = [](float x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); };  // RS_SGN
+                    if (abs_fwd > 25.f && sgn(real_throttle) != sgn(fwd_speed)) {
+                        real_brake = 1;
+                        if (abs_fwd > 0.01f) engine_throttle = 0;
+                    }
+                } else {
+                    engine_throttle = 0;
+                    bool full_stop = abs_fwd < 25.f;
+                    real_brake = full_stop ? 1 : 0.15f;
+                }
+            }
+            if (nwc < 3) drive_scale /= 4;
+            float engine = engine_throttle * (CAR_MASS * 400.f * UU_TO_BT) * drive_scale;
+            float brake = real_brake * (CAR_MASS * (14.25f + (1.f / 3.f)) * UU_TO_BT);
+            for (int i = 0; i < 4; i++) {
+                cs.wheel_engine_force[i] = engine;
+                cs.wheel_brake[i] = brake;
+            }
+        }
+        {
+            float steer = STEER_ANGLE_FROM_SPEED.out(abs_fwd);
+            if (cs.handbrake_val != 0.f) steer += (POWERSLIDE_STEER_ANGLE.out(abs_fwd) - steer) * cs.handbrake_val;
+            steer *= ctl[1];
+            cs.wheel_steer[0] = steer;
+            cs.wheel_steer[1] = steer;
+        }
+        for (int i = 0; i < 4; i++) {
+            WheelTick& W = wt[ci][i];
+            if (W.ground >= 0) {
+                V lat_dir = W.wt_col1;
+                V long_dir = cross(lat_dir, W.contact_normal);
+                float fin = 0;
+                V delta = W.hard_point - c.pos;
+                V cv = (cross(c.ang, delta) + c.vel) * BT_TO_UU;
+                float base = std::fabs(dot(cv, lat_dir));
+                if (base > 5) fin = base / (std::fabs(dot(cv, long_dir)) + base);
+                float lat = LAT_FRICTION.out(fin);
+                float lon = LONG_FRICTION.out(fin);
+                if (cs.handbrake_val != 0.f) {
+                    float hb = cs.handbrake_val;
+                    lat *= (HANDBRAKE_LAT_FRICTION_FACTOR.out(fin) - 1) * hb + 1;
+                    lon *= (HANDBRAKE_LONG_FRICTION_FACTOR.out(fin) - 1) * hb + 1;
+                } else {
+                    lon = 1;
+                }
+                bool sticky = real_throttle != 0;
+                if (!sticky) {
+                    float ns = NON_STICKY_FRICTION_FACTOR.out(W.contact_normal.z);
+                    lat *= ns;
+                    lon *= ns;
+                }
+                cs.wheel_lat_friction[i] = lat;
+                cs.wheel_long_friction[i] = lon;
+            }
+        }
+        if (world_contact) {
+            V up = upwards_dir_from_wheels(ci);
+            bool full = (real_throttle != 0) || (abs_fwd > 25.f);
+            float scale = 0.5f;
+            if (full) scale += 1 - std::fabs(up.z);
+            c.force += up * scale * (GRAVITY_Z_UU * UU_TO_BT) * CAR_MASS;
+        }
+    }
+
+    // Car::_UpdateBoost (Car.cpp:477-505)
+    void update_boost(int ci) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        bool boosting = cs.controls[6] != 0.f;
+        if (cs.time_spent_boosting > 0) {
+            if (!boosting && cs.time_spent_boosting >= 0.1f)
+                cs.time_spent_boosting = 0;
+            else
+                cs.time_spent_boosting += TICK_TIME;
+        } else {
+            if (boosting) cs.time_spent_boosting = TICK_TIME;
+        }
+        if (cs.boost > 0 && cs.time_spent_boosting > 0) {
+            cs.boost = std::max(cs.boost - (100.f / 3) * TICK_TIME, 0.f);
+            float accel = cs.is_on_ground ? (2975 / 3.f) : (3175 / 3.f);
+            c.force += accel * UU_TO_BT * c.rot.col(0) * CAR_MASS;
+        }
+        cs.boost = std::min(cs.boost, 100.f);
+    }
+
+    // Car::_UpdateJump (Car.cpp:507-554)
+    void update_jump(int ci, bool jump_pressed) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        const float JUMP_MIN = 0.025f, JUMP_MAX = 0.2f, PAD = 1 / 40.f;
+        if (cs.is_on_ground && !cs.is_jumping) {
+            if (cs.has_jumped && cs.jump_time < JUMP_MIN + PAD) {
+            } else {
+                cs.has_jumped = 0;
+                cs.jump_time = 0;
+            }
+        }
+        if (cs.is_jumping) {
+            cs.is_jumping = (cs.jump_time < JUMP_MIN || (cs.controls[5] != 0.f && cs.jump_time < JUMP_MAX));
+        } else if (cs.is_on_ground && jump_pressed) {
+            cs.is_jumping = 1;
+            cs.jump_time = 0;
+            V f = c.rot.col(2) * (875.f / 3.f) * UU_TO_BT * CAR_MASS;
+            c.apply_central_impulse(f);
+        }
+        if (cs.is_jumping) {
+            cs.has_jumped = 1;
+            V total = c.rot.col(2) * (4375.f / 3.f);
+            if (cs.jump_time < JUMP_MIN) total *= 0.62f;
+            c.force += total * UU_TO_BT * CAR_MASS;
+        }
+        if (cs.is_jumping || cs.has_jumped) cs.jump_time += TICK_TIME;
+    }
+
+    // Car::_UpdateAirTorque (Car.cpp:556-641)
+    void update_air_torque(int ci, bool update_air_control) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        const float* ctl = cs.controls;
+        V dir_pitch = -c.rot.col(1), dir_yaw = c.rot.col(2), dir_roll = -c.rot.col(0);
+        bool do_air = false;
+        if (cs.is_flipping) cs.is_flipping = cs.has_flipped && cs.flip_time < 0.65f;
+        if (cs.is_flipping) {
+            V rel = ld3(cs.flip_rel_torque);
+            if (!(rel.x == 0 && rel.y == 0 && rel.z == 0)) {
+                float pitch_scale = 1;
+                if (rel.y != 0 && ctl[2] != 0) {
+                    auto sgn = [](float x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); };
+                    if (sgn(rel.y) == sgn(ctl[2])) {
+                        pitch_scale = 1 - std::min(std::fabs(ctl[2]), 1.f);
+                        do_air = true;
+                    }
+                }
+                rel.y *= pitch_scale;
+                V dodge = rel * V(260.f, 224.f, 0);
+                c.torque += (inverse(c.inv_inertia_world) * c.rot) * dodge;
+            } else {
+                do_air = true;
+            }
+        } else {
+            do_air = true;
+        }
+        do_air &= !cs.is_auto_flipping;
+        do_air &= update_air_control;
+        if (do_air) {
+            float pitch_scale = 1;
+            V torque;
+            if (ctl[2] != 0 || ctl[3] != 0 || ctl[4] != 0) {
+                if (cs.is_flipping)
+                    pitch_scale = 0;
+                else if (cs.has_flipped && cs.flip_time < 0.65f + 0.3f)
+                    pitch_scale = 0;
+                torque = (ctl[2] * dir_pitch * pitch_scale * 130.f) + (ctl[3] * dir_yaw * 95.f) + (ctl[4] * dir_roll * 400.f);
+            }
+            V av = c.ang;
+            float damp_pitch = dot(dir_pitch, av) * 30.f * (1 - std::fabs(do_air ? (ctl[2] * pitch_scale) : 0));
+            float damp_yaw = dot(dir_yaw, av) * 20.f * (1 - std::fabs(do_air ? ctl[3] : 0));
+            float damp_roll = dot(dir_roll, av) * 50.f;
+            V damping = (dir_yaw * damp_yaw) + (dir_pitch * damp_pitch) + (dir_roll * damp_roll);
+            const float TORQUE_SCALE = (float)(2 * M_PI / (1 << 16) * 1000);
+            c.torque += inverse(c.inv_inertia_world) * (torque - damping) * TORQUE_SCALE;
+        }
+        if (ctl[0] != 0) c.force += c.rot.col(0) * ctl[0] * (200 / 3.f) * UU_TO_BT * CAR_MASS;
+    }
+
+    // Car::_UpdateDoubleJumpOrFlip (Car.cpp:643-761)
+    void update_double_jump_or_flip(int ci, bool jump_pressed, float fwd_speed) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        const float* ctl = cs.controls;
+        if (cs.is_on_ground) {
+            cs.has_double_jumped = 0;
+            cs.has_flipped = 0;
+            cs.air_time = 0;
+            cs.air_time_since_jump = 0;
+            cs.flip_time = 0;
+        } else {
+            cs.air_time += TICK_TIME;
+            if (cs.has_jumped && !cs.is_jumping)
+                cs.air_time_since_jump += TICK_TIME;
+            else
+                cs.air_time_since_jump = 0;
+            if (jump_pressed && cs.air_time_since_jump < 1.25f) {
+                float mag = std::fabs(ctl[3]) + std::fabs(ctl[2]) + std::fabs(ctl[4]);
+                bool flip_input = mag >= 0.5f;  // CarConfig::dodgeDeadzone
+                bool can_use = !cs.has_double_jumped && !cs.has_flipped;
+                if (cs.is_auto_flipping) can_use = false;
+                if (can_use) {
+                    if (flip_input) {
+                        cs.flip_time = 0;
+                        cs.has_flipped = 1;
+                        cs.is_flipping = 1;
+                        float ratio = std::fabs(fwd_speed) / 2300.f;
+                        V dodge(-ctl[2], ctl[3] + ctl[4], 0);
+                        if (std::fabs(ctl[3] + ctl[4]) < 0.1f && std::fabs(ctl[2]) < 0.1f)
+                            dodge = V();
+                        else
+                            dodge = safe_normalized(dodge);
+                        st3(cs.flip_rel_torque, V(-dodge.y, dodge.x, 0));
+                        if (std::fabs(dodge.x) < 0.1f) dodge.x = 0;
+                        if (std::fabs(dodge.y) < 0.1f) dodge.y = 0;
+                        if (!fuzzy_zero(dodge)) {
+                            bool back;
+                            if (std::fabs(fwd_speed) < 100.0f)
+                                back = dodge.x < 0.0f;
+                            else
+                                back = (dodge.x >= 0.0f) != (fwd_speed >= 0.0f);
+                            V init = dodge * 500.f;
+                            float max_x = back ? 2.5f : 1.f;
+                            init.x *= ((max_x - 1) * ratio) + 1.f;
+                            init.y *= ((1.9f - 1) * ratio) + 1.f;
+                            if (back) init.x *= 16.f / 15.f;
+                            V fdir = c.rot.col(0);
+                            float ang = rs_atan2f(fdir.y, fdir.x);
+                            float sa, ca;
+                            rs_sincosf(ang, &sa, &ca);
+                            V xdir(ca, -sa, 0.f), ydir(sa, ca, 0.f);
+                            V dv(dot(init, xdir), dot(init, ydir), 0.f);
+                            c.apply_central_impulse(dv * UU_TO_BT * CAR_MASS);
+                        }
+                    } else {
+                        V f = c.rot.col(2) * (875.f / 3.f) * UU_TO_BT * CAR_MASS;
+                        c.apply_central_impulse(f);
+                        cs.has_double_jumped = 1;
+                    }
+                }
+            }
+        }
+        if (cs.is_flipping) {
+            cs.flip_time += TICK_TIME;
+            if (cs.flip_time <= 0.65f) {
+                if (cs.flip_time >= 0.15f && (c.vel.z < 0 || cs.flip_time < 0.21f)) {
+                    // powf(1 - 0.35, tickTime / (1/120)) == 0.65^1 at 120 tps
+                    c.vel.z *= (1 - 0.35f);
+                }
+            }
+        } else if (cs.has_flipped) {
+            cs.flip_time += TICK_TIME;
+        }
+    }
+
+    // Car::_UpdateAutoFlip (Car.cpp:763-797)
+    void update_auto_flip(int ci, bool jump_pressed) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        if (jump_pressed && cs.world_contact && cs.world_contact_normal[2] > (float)M_SQRT1_2) {
+            // Angle::FromRotMat -> btMatrix3x3::getEulerYPR roll, negated (MathTypes.cpp:62-71)
+            const M& m = c.rot;
+            float r0 = rs_atan2f(m.r[2].y, m.r[2].z);
+            float pitch_raw;
+            {
+                float x = -m.r[2].x;
+                float sq = std::sqrt(std::max(0.f, 1.f - x * x));
+                pitch_raw = rs_asinf(x, sq);
+            }
+            if (std::fabs(pitch_raw) == SIMD_HALF_PI) r0 = r0 > 0 ? r0 - SIMD_PI : r0 + SIMD_PI;
+            float roll = -r0;
+            float abs_roll = std::fabs(roll);
+            if (abs_roll > 2.8f) {
+                cs.auto_flip_timer = 0.4f * (abs_roll / (float)M_PI);
+                cs.auto_flip_torque_scale = (roll > 0) ? 1 : -1;
+                cs.is_auto_flipping = 1;
+                c.apply_central_impulse(-c.rot.col(2) * 200.f * UU_TO_BT * CAR_MASS);
+            }
+        }
+        if (cs.is_auto_flipping) {
+            if (cs.auto_flip_timer <= 0) {
+                cs.is_auto_flipping = 0;
+                cs.auto_flip_timer = 0;
+            } else {
+                c.ang += c.rot.col(0) * 50.f * cs.auto_flip_torque_scale * TICK_TIME;
+                cs.auto_flip_timer -= TICK_TIME;
+            }
+        }
+    }
+
+    // Car::_UpdateAutoRoll (Car.cpp:799-831)
+    void update_auto_roll(int ci, int nwc) {
+        Body& c = b[ci + 1];
+        rlgpu_car& cs = car(ci);
+        V gup = nwc > 0 ? upwards_dir_from_wheels(ci) : ld3(cs.world_contact_normal);
+        V gdown = -gup;
+        V fwd = c.rot.col(0), right = c.rot.col(1);
+        V cross_right = cross(gup, fwd);
+        V cross_fwd = cross(gdown, cross_right);
+        float rtf = 1 - std::clamp(dot(right, cross_right), 0.f, 1.f);
+        float ftf = 1 - std::clamp(dot(fwd, cross_fwd), 0.f, 1.f);
+        V tdr = fwd * (dot(right, gup) >= 0 ? -1.f : 1.f);
+        V tdf = right * (dot(fwd, gup) >= 0 ? 1.f : -1.f);
+        V tr = tdr * rtf, tf = tdf * ftf;
+        c.force += gdown * 100.f * UU_TO_BT * CAR_MASS;
+        c.torque += inverse(c.inv_inertia_world) * (tf + tr) * 80.f;
+    }
+
+    // Car::Respawn (Car.cpp:43-56)
+    void respawn(int ci) {
+        rlgpu_car& cs = car(ci);
+        int idx = (int)(rng_next(seed, arena_index, s.env) % 4u);
+        bool orange = car_team_orange(ci);
+        V pos(w.respawn_x[idx], w.respawn_y[idx] * (orange ? -1.f : 1.f), 36.f);
+        set_car_state(ci, pos, w.respawn_rot[orange][idx], 100.f / 3.f, false);
+    }
+
+    // Car::SetState with a default CarState (Car.h defaults) at pos/rot.
+    void set_car_state(int ci, V pos_uu, const M& rot, float boost, bool on_ground) {
+        rlgpu_car& cs = car(ci);
+        float steer[4], eng[4], brk[4], lat[4], lon[4], push[4];
+        float ctl[8];
+        std::memcpy(steer, cs.wheel_steer, sizeof steer);
+        std::memcpy(eng, cs.wheel_engine_force, sizeof eng);
+        std::memcpy(brk, cs.wheel_brake, sizeof brk);
+        std::memcpy(lat, cs.wheel_lat_friction, sizeof lat);
+        std::memcpy(lon, cs.wheel_long_friction, sizeof lon);
+        std::memcpy(push, cs.wheel_extra_pushback, sizeof push);
+        std::memcpy(ctl, cs.controls, sizeof ctl);  // controls are not part of CarState
+        default_car(cs);
+        std::memcpy(cs.wheel_steer, steer, sizeof steer);
+        std::memcpy(cs.wheel_engine_force, eng, sizeof eng);
+        std::memcpy(cs.wheel_brake, brk, sizeof brk);
+        std::memcpy(cs.wheel_lat_friction, lat, sizeof lat);
+        std::memcpy(cs.wheel_long_friction, lon, sizeof lon);
+        std::memcpy(cs.wheel_extra_pushback, push, sizeof push);
+        std::memcpy(cs.controls, ctl, sizeof ctl);
+        cs.boost = boost;
+        cs.is_on_ground = on_ground;
+        Body& c = b[ci + 1];
+        c.pos = pos_uu * UU_TO_BT;
+        c.rot = rot;
+        c.vel = V();
+        c.ang = V();
+        c.update_inertia();
+        clear_manifolds_of(ci + 1);
+    }
+
+    // ------------------------------------------------------------------ manifolds
+    rlgpu_manifold* find_manifold(int key) {
+        for (int m = 0; m < RLGPU_MANIFOLDS; m++)
+            if (s.manifolds[m].count > 0 && s.manifolds[m].key == key) return &s.manifolds[m];
+        return nullptr;
+    }
+    rlgpu_manifold* get_or_new_manifold(int key) {
+        rlgpu_manifold* m = find_manifold(key);
+        if (m) return m;
+        for (int k = 0; k < RLGPU_MANIFOLDS; k++)
+            if (s.manifolds[k].count == 0) {
+                s.manifolds[k].key = key;
+                return &s.manifolds[k];
+            }
+        return nullptr;
+    }
+    void clear_manifolds_of(int body) {
+        for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
+            rlgpu_manifold& mf = s.manifolds[m];
+            if (mf.count == 0) continue;
+            int a, bb;
+            key_bodies(mf.key, a, bb);
+            if (a == body || bb == body) mf.count = 0;
+        }
+    }
+    static void key_bodies(int key, int& a, int& bb) {  // bb: body index, or 10+static
+        if (key >= 64) {
+            a = (key - 64) / 8;
+            bb = (key - 64) % 8;
+        } else {
+            a = key / 8;
+            bb = 10 + key % 8;
+        }
+    }
+    // body transform of a manifold side
+    void side_transform(int id, V& p, M& r) const {
+        if (id >= 10) {
+            p = V();
+            r = M::ident();
+        } else {
+            p = b[id].pos;
+            r = b[id].rot;
+        }
+    }
+    float pair_cbt(int a, int bb) const {
+        float ta = a == 0 ? w.ball_cbt : w.car_cbt;
+        if (bb >= 10) return ta;
+        float tb = bb == 0 ? w.ball_cbt : w.car_cbt;
+        return std::min(ta, tb);
+    }
+
+    // btPersistentManifold::sortCachedPoints (btPersistentManifold.cpp:110-198), area3 variant
+    static int sort_cached(const rlgpu_manifold& m, const rlgpu_contact& pt) {
+        int max_idx = -1;
+        float max_pen = pt.dist;
+        for (int i = 0; i < 4; i++)
+            if (m.pts[i].dist < max_pen) {
+                max_idx = i;
+                max_pen = m.pts[i].dist;
+            }
+        float res[4] = {0, 0, 0, 0};
+        auto la = [&](int i) { return ld3(m.pts[i].localA); };
+        V p = ld3(pt.localA);
+        if (max_idx != 0) res[0] = len2(cross(p - la(1), la(3) - la(2)));
+        if (max_idx != 1) res[1] = len2(cross(p - la(0), la(3) - la(2)));
+        if (max_idx != 2) res[2] = len2(cross(p - la(0), la(3) - la(1)));
+        if (max_idx != 3) res[3] = len2(cross(p - la(0), la(2) - la(1)));
+        // btVector4::closestAxis4 -> absolute().maxAxis4()
+        int best = -1;
+        float mx = -1e30f;
+        for (int i = 0; i < 4; i++) {
+            float v = std::fabs(res[i]);
+            if (v > mx) {
+                best = i;
+                mx = v;
+            }
+        }
+        return best;
+    }
+
+    // btManifoldResult::addContactPoint + contact-added callback (Arena.cpp:218-281)
+    void add_contact(int key, V normal_b, V point_b, float depth) {
+        int a, bb;
+        key_bodies(key, a, bb);
+        float cbt = pair_cbt(a, bb);
+        if (depth > cbt) return;
+        rlgpu_manifold* m = get_or_new_manifold(key);
+        if (!m) {
+            s.env.manifold_overflow++;
+            return;
+        }
+        V pa = point_b + normal_b * depth;
+        V ta_p, tb_p;
+        M ta_r, tb_r;
+        side_transform(a, ta_p, ta_r);
+        side_transform(bb, tb_p, tb_r);
+        rlgpu_contact c;
+        std::memset(&c, 0, sizeof c);
+        st3(c.localA, vmul(pa - ta_p, ta_r));  // invXform
+        st3(c.localB, vmul(point_b - tb_p, tb_r));
+        st3(c.normalB, normal_b);
+        c.dist = depth;
+        c.applied = 0.f;
+        // combined friction / restitution (btManifoldResult.cpp:59-82, RocketSim variant)
+        bool stat = bb >= 10;
+        float fa = a == 0 ? 0.35f : 0.3f, ra = a == 0 ? 0.6f : 0.1f;
+        float fb = stat ? 0.6f : (bb == 0 ? 0.35f : 0.3f), rb = stat ? 0.3f : (bb == 0 ? 0.6f : 0.1f);
+        c.friction = stat ? std::min(fa, fb) : fa * fb;
+        c.restitution = stat ? std::max(ra, rb) : ra * rb;
+        int idx;
+        if (m->count == 4) {
+            idx = sort_cached(*m, c);
+        } else {
+            idx = m->count;
+            m->count++;
+        }
+        if (idx < 0) idx = 0;
+        m->pts[idx] = c;
+        contact_callback(a, bb, m->pts[idx]);
+    }
+
+    void contact_callback(int a, int bb, rlgpu_contact& cp) {
+        if (a >= 1 && a <= 4) {
+            int ci = a - 1;
+            if (bb == 0) {
+                car_ball_hit(ci, cp);
+            } else if (bb >= 1 && bb <= 4) {
+                car_car_hit(ci, bb - 1, cp);
+            } else {  // car-world (Arena.cpp:417-427)
+                rlgpu_car& cs = car(ci);
+                cs.world_contact = 1;
+                std::memcpy(cs.world_contact_normal, cp.normalB, sizeof(float) * 3);
+                cp.friction = 0.3f;
+                cp.restitution = 0.3f;
+            }
+        } else if (a == 0 && bb >= 10) {
+            cp.special = 1;  // ball-world (Arena.cpp:265-273)
+        }
+    }
+
+    // Arena::_BtCallback_OnCarBallCollision (Arena.cpp:283-333)
+    void car_ball_hit(int ci, rlgpu_contact& cp) {
+        rlgpu_car& cs = car(ci);
+        const Body& c = b[ci + 1];
+        const Body& ball = b[0];
+        cp.friction = 2.0f;
+        cp.restitution = 0.0f;
+        V ball_pos = ball.pos * BT_TO_UU, car_pos = c.pos * BT_TO_UU;
+        V ball_vel = ball.vel * BT_TO_UU, car_vel = c.vel * BT_TO_UU;
+        cs.ball_hit_valid = 1;
+        st3(cs.ball_hit_rel_pos, ld3(cp.localB) * BT_TO_UU);
+        cs.ball_hit_tick = s.env.tick_count;
+        st3(cs.ball_hit_ball_pos, ball_pos);
+        st3(cs.ball_hit_extra_vel, V());
+        int64_t tick = s.env.tick_count;
+        int64_t ex = cs.ball_hit_extra_tick;
+        // unsigned comparison of the reference (~0ULL == never)
+        uint64_t uex = (uint64_t)ex, ut = (uint64_t)tick;
+        if ((ut > uex + 1) || (uex > ut)) {
+            cs.ball_hit_extra_tick = tick;
+        } else {
+            return;
+        }
+        V fwd = c.rot.col(0);
+        V rel_pos = ball_pos - car_pos;
+        V rel_vel = ball_vel - car_vel;
+        float rel_speed = std::min(len(rel_vel), 4600.f);
+        if (rel_speed > 0) {
+            V hit_dir = safe_normalized(rel_pos * V(1, 1, 0.35f));
+            V adj = fwd * dot(hit_dir, fwd) * (1 - 0.65f);
+            hit_dir = safe_normalized(hit_dir - adj);
+            V added = (hit_dir * rel_speed) * BALL_CAR_EXTRA_IMPULSE_FACTOR.out(rel_speed) * 1.f;
+            st3(cs.ball_hit_extra_vel, added);
+            V cache = ld3(s.ball_vel_impulse_cache);
+            cache += added * UU_TO_BT;
+            st3(s.ball_vel_impulse_cache, cache);
+        }
+    }
+
+    // Arena::_BtCallback_OnCarCarCollision (Arena.cpp:335-415)
+    void car_car_hit(int c1, int c2, rlgpu_contact& cp) {
+        cp.friction = 0.09f;
+        cp.restitution = 0.1f;
+        for (int i = 0; i < 2; i++) {
+            bool swapped = i == 1;
+            int a = swapped ? c2 : c1, o = swapped ? c1 : c2;
+            rlgpu_car& sa = car(a);
+            rlgpu_car& so = car(o);
+            if (sa.is_demoed || so.is_demoed) return;
+            if (sa.car_contact_other_id == car_id(o) && sa.car_contact_cooldown > 0) continue;
+            V pa = b[a + 1].pos * BT_TO_UU, po = b[o + 1].pos * BT_TO_UU;
+            V va = b[a + 1].vel * BT_TO_UU, vo = b[o + 1].vel * BT_TO_UU;
+            V delta = po - pa;
+            if (dot(va, delta) > 0) {
+                V vel_dir = rs_norm(va);  // RocketSim Vec::Normalized
+                V dir_to = rs_norm(delta);
+                float speed_towards = dot(va, dir_to);
+                float other_away = dot(vo, vel_dir);
+                if (speed_towards > other_away) {
+                    V lp = swapped ? ld3(cp.localB) : ld3(cp.localA);
+                    bool bumper = (lp.x * BT_TO_UU) > 64.5f;
+                    if (bumper) {
+                        bool demo = sa.is_supersonic;
+                        if (demo) demo = car_team_orange(a) != car_team_orange(o);  // enableTeamDemos=false
+                        if (demo) {
+                            so.is_demoed = 1;
+                            so.demo_respawn_timer = 3.f;
+                        } else {
+                            bool ground = so.is_on_ground;
+                            float base = (ground ? BUMP_VEL_AMOUNT_GROUND : BUMP_VEL_AMOUNT_AIR).out(speed_towards);
+                            V up = so.is_on_ground ? b[o + 1].rot.col(2) : V(0, 0, 1);
+                            V imp = vel_dir * base + up * BUMP_UPWARD_VEL_AMOUNT.out(speed_towards) * 1.f;
+                            V cache = ld3(so.vel_impulse_cache);
+                            cache += imp * UU_TO_BT;
+                            st3(so.vel_impulse_cache, cache);
+                        }
+                        sa.car_contact_other_id = car_id(o);
+                        sa.car_contact_cooldown = 0.25f;
+                        // EnvSet _BumpCallback (EnvSet.cpp:31-42): only across teams
+                        if (car_team_orange(a) != car_team_orange(o)) {
+                            s.env.ev_bump[a] = 1;
+                            s.env.ev_bumped[o] = 1;
+                            if (demo) {
+                                s.env.ev_demo[a] = 1;
+                                s.env.ev_demoed[o] = 1;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    // btPersistentManifold::refreshContactPoints (btPersistentManifold.cpp:265-330)
+    void refresh(int key) {
+        rlgpu_manifold* m = find_manifold(key);
+        if (!m) return;
+        int a, bb;
+        key_bodies(key, a, bb);
+        float cbt = pair_cbt(a, bb);
+        V pa_, pb_;
+        M ra, rb;
+        side_transform(a, pa_, ra);
+        side_transform(bb, pb_, rb);
+        V wa[4], wb[4];
+        for (int i = m->count - 1; i >= 0; i--) {
+            rlgpu_contact& p = m->pts[i];
+            wa[i] = ra * ld3(p.localA) + pa_;
+            wb[i] = rb * ld3(p.localB) + pb_;
+            p.dist = dot(wa[i] - wb[i], ld3(p.normalB));
+        }
+        for (int i = m->count - 1; i >= 0; i--) {
+            rlgpu_contact& p = m->pts[i];
+            bool remove;
+            if (!(p.dist <= cbt)) {
+                remove = true;
+            } else {
+                V proj = wa[i] - ld3(p.normalB) * p.dist;
+                V diff = wb[i] - proj;
+                remove = dot(diff, diff) > cbt * cbt;
+            }
+            if (remove) {  // removeContactPoint: move last into i
+                int last = m->count - 1;
+                if (i != last) {
+                    m->pts[i] = m->pts[last];
+                    wa[i] = wa[last];
+                    wb[i] = wb[last];
+                }
+                m->count--;
+            }
+        }
+    }
+
+    // --------------------------------------------------------------- narrowphase
+    void collide_sphere_plane(int key, int p) {
+        V n = w.plane_n[p];
+        V c = b[0].pos;
+        V vtx = c + (-n) * w.ball_radius;  // support vertex (btSphereShape margin = radius)
+        float dist = dot(n, vtx - w.plane_p[p]);
+        V on_plane = vtx - n * dist;
+        float cbt = pair_cbt(0, 10);
+        if (dist < cbt) add_contact(key, n, on_plane, dist);
+    }
+    void collide_sphere_mesh(int key) {
+        V c = b[0].pos;
+        float r = w.ball_radius;
+        float ext = r + 0.08f;
+        float cbt = pair_cbt(0, 10);
+        for (int t = 0; t < w.ntris; t++) {
+            if (!aabb_overlap(c - V(ext, ext, ext), c + V(ext, ext, ext), w.tri_min[t], w.tri_max[t])) continue;
+            V pt, nrm;
+            float depth;
+            if (sphere_triangle(c, r, t, cbt, pt, nrm, depth)) add_contact(key, nrm, pt, depth);
+        }
+    }
+    static bool aabb_overlap(V a0, V a1, V b0, V b1) {
+        return !(a0.x > b1.x || a1.x < b0.x || a0.y > b1.y || a1.y < b0.y || a0.z > b1.z || a1.z < b0.z);
+    }
+    // SphereTriangleDetector::collide (SphereTriangleDetector.cpp:139-240)
+    bool sphere_triangle(V center, float radius, int t, float cbt, V& point, V& normal_out, float& depth) const {
+        const V* v = w.tri[t];
+        float rwt = radius + cbt;
+        V normal = cross(v[1] - v[0], v[2] - v[0]);
+        float l2 = len2(normal);
+        bool has = false;
+        V cp;
+        if (l2 >= SIMD_EPSILON * SIMD_EPSILON) {
+            normal = normal / std::sqrt(l2);
+            V p1c = center - v[0];
+            float dfp = dot(p1c, normal);
+            if (dfp < 0.f) {
+                dfp *= -1.f;
+                normal = normal * -1.f;
+            }
+            if (dfp < rwt) {
+                if (point_in_triangle(v, normal, center)) {
+                    has = true;
+                    cp = center - normal * dfp;
+                } else {
+                    V near = closest_point_triangle(center, v[0], v[1], v[2]);
+                    float d2 = len2(near - center);
+                    if (d2 < rwt * rwt) {
+                        has = true;
+                        cp = near;
+                    }
+                }
+            }
+        }
+        if (!has) return false;
+        V c2c = center - cp;
+        float d2 = len2(c2c);
+        if (!(d2 < rwt * rwt)) return false;
+        if (d2 > SIMD_EPSILON) {
+            float d = std::sqrt(d2);
+            normal_out = normalized(c2c);
+            point = cp;
+            depth = -(radius - d);
+        } else {
+            normal_out = normal;
+            point = cp;
+            depth = -radius;
+        }
+        return true;
+    }
+    // SphereTriangleDetector::pointInTriangle (edge-plane test)
+    static bool point_in_triangle(const V* v, V normal, V p) {
+        V e1 = v[1] - v[0], e2 = v[2] - v[1], e3 = v[0] - v[2];
+        V n1 = cross(e1, normal), n2 = cross(e2, normal), n3 = cross(e3, normal);
+        float r1 = dot(p, n1) - dot(v[0], n1);
+        float r2 = dot(p, n2) - dot(v[1], n2);
+        float r3 = dot(p, n3) - dot(v[2], n3);
+        if (r1 > 0 && r2 > 0 && r3 > 0) return true;
+        if (r1 <= 0 && r2 <= 0 && r3 <= 0) return true;
+        return false;
+    }
+    // closestPointTriangle (SphereTriangleDetector.cpp:88-137)
+    static V closest_point_triangle(V p, V a, V b_, V c) {
+        V ab = b_ - a, ac = c - a, ap = p - a;
+        float d1 = dot(ab, ap), d2 = dot(ac, ap);
+        if (d1 <= 0.f && d2 <= 0.f) return a;
+        V bp = p - b_;
+        float d3 = dot(ab, bp), d4 = dot(ac, bp);
+        if (d3 >= 0.f && d4 <= d3) return b_;
+        V cp = p - c;
+        float d5 = dot(ab, cp), d6 = dot(ac, cp);
+        if (d6 >= 0.f && d5 <= d6) return c;
+        float vc = d1 * d4 - d3 * d2;
+        if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+            float vv = d1 / (d1 - d3);
+            return a + ab * vv;
+        }
+        float vb = d5 * d2 - d1 * d6;
+        if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+            float vv = d2 / (d2 - d6);
+            return a + ac * vv;
+        }
+        float va = d3 * d6 - d5 * d4;
+        if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+            float vv = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+            return b_ + (c - b_) * vv;
+        }
+        float denom = 1.f / (va + vb + vc);
+        float vv = vb * denom, ww = vc * denom;
+        return a + ab * vv + ac * ww;
+    }
+    // box (car hitbox) vs plane: support vertex (btConvexPlaneCollisionAlgorithm.cpp:53-90)
+    void collide_box_plane(int key, int bi, int p) {
+        V n = w.plane_n[p];
+        const M& R = b[bi].rot;
+        V c = car_box_center(bi);
+        V dl = vmul(-n, R);  // direction in box frame
+        V lv(dl.x >= 0 ? w.car_half.x : -w.car_half.x, dl.y >= 0 ? w.car_half.y : -w.car_half.y,
+             dl.z >= 0 ? w.car_half.z : -w.car_half.z);
+        V vtx = R * lv + c;
+        float dist = dot(n, vtx - w.plane_p[p]);
+        V on_plane = vtx - n * dist;
+        if (dist < pair_cbt(bi, 10)) add_contact(key, n, on_plane, dist);
+    }
+    // SAT separation of an OBB and a triangle; returns false if separated beyond cbt.
+    bool box_triangle(int bi, int t, float cbt, V& nrm, V& point_b, float& depth) const {
+        const M& R = b[bi].rot;
+        V c = car_box_center(bi);
+        V ax[3] = {R.col(0), R.col(1), R.col(2)};
+        const V* v = w.tri[t];
+        V e[3] = {v[1] - v[0], v[2] - v[1], v[0] - v[2]};
+        V tn = cross(e[0], v[2] - v[0]);
+        V axes[13];
+        int na = 0;
+        axes[na++] = tn;
+        for (int i = 0; i < 3; i++) axes[na++] = ax[i];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) axes[na++] = cross(ax[i], e[j]);
+        float best = 1e30f;
+        V best_n;
+        for (int k = 0; k < na; k++) {
+            float l2 = len2(axes[k]);
+            if (l2 < 1e-10f) continue;
+            V L = axes[k] / std::sqrt(l2);
+            float r = w.car_half.x * std::fabs(dot(ax[0], L)) + w.car_half.y * std::fabs(dot(ax[1], L)) +
+                      w.car_half.z * std::fabs(dot(ax[2], L));
+            float p0 = dot(v[0], L), p1 = dot(v[1], L), p2 = dot(v[2], L);
+            float tmin = std::min(p0, std::min(p1, p2)), tmax = std::max(p0, std::max(p1, p2));
+            float cl = dot(c, L);
+            float pen_pos = tmax - (cl - r);  // push box along +L
+            float pen_neg = (cl + r) - tmin;  // push box along -L
+            float pen;
+            V n;
+            if (pen_pos < pen_neg) {
+                pen = pen_pos;
+                n = L;
+            } else {
+                pen = pen_neg;
+                n = -L;
+            }
+            if (-pen > cbt) return false;  // separated on this axis
+            if (pen < best) {
+                best = pen;
+                best_n = n;
+            }
+        }
+        nrm = best_n;  // normal on B (triangle) pointing to A (box)
+        depth = -best;
+        // deepest box vertex along -n, then the point on B
+        V dl = vmul(-nrm, R);
+        V lv(dl.x >= 0 ? w.car_half.x : -w.car_half.x, dl.y >= 0 ? w.car_half.y : -w.car_half.y,
+             dl.z >= 0 ? w.car_half.z : -w.car_half.z);
+        V pa = R * lv + c;
+        point_b = pa - nrm * depth;
+        return true;
+    }
+    void collide_box_mesh(int key, int bi) {
+        V mn, mx;
+        body_aabb(bi, b[bi].pos, b[bi].rot, mn, mx);
+        float cbt = pair_cbt(bi, 10);
+        for (int t = 0; t < w.ntris; t++) {
+            if (!aabb_overlap(mn, mx, w.tri_min[t], w.tri_max[t])) continue;
+            V n, pb;
+            float d;
+            if (box_triangle(bi, t, cbt, n, pb, d)) add_contact(key, n, pb, d);
+        }
+    }
+    // btSphereBoxCollisionAlgorithm::getSphereDistance, A = car, B = ball
+    void collide_car_ball(int key, int bi) {
+        const M& R = b[bi].rot;
+        V c = car_box_center(bi);
+        const float margin = 0.04f;
+        V he((w.car_half.x - margin), (w.car_half.y - margin), (w.car_half.z - margin));
+        V rel = vmul(b[0].pos - c, R);
+        V cp(std::max(-he.x, std::min(he.x, rel.x)), std::max(-he.y, std::min(he.y, rel.y)),
+             std::max(-he.z, std::min(he.z, rel.z)));
+        float r = w.ball_radius;
+        float inter = r + margin;
+        float cbt = pair_cbt(bi, 0);
+        float contact_dist = inter + cbt;
+        V normal = rel - cp;
+        float d2 = len2(normal);
+        if (d2 > contact_dist * contact_dist) return;
+        float distance;
+        if (d2 <= SIMD_EPSILON) {
+            // getSpherePenetration: deepest face
+            float fd[6] = {he.x - rel.x, he.x + rel.x, he.y - rel.y, he.y + rel.y, he.z - rel.z, he.z + rel.z};
+            int bf = 0;
+            for (int k = 1; k < 6; k++)
+                if (fd[k] < fd[bf]) bf = k;
+            V nn;
+            cp = rel;
+            int axis = bf / 2;
+            float sg = (bf % 2 == 0) ? 1.f : -1.f;
+            cp[axis] = sg * he[axis];
+            nn[axis] = sg;
+            normal = nn;
+            distance = -fd[bf];
+        } else {
+            distance = len(normal);
+            normal = normal / distance;
+        }
+        V point_on_box = R * (cp + normal * margin) + c;
+        float pen = distance - inter;
+        V nw = R * normal;  // from box towards sphere
+        // manifold A = car, B = ball: normal on B points from ball to car
+        V nB = -nw;
+        V point_b = point_on_box - nB * pen;
+        add_contact(key, nB, point_b, pen);
+    }
+    // OBB vs OBB SAT (1 point), A = car a, B = car b
+    void collide_car_car(int key, int ba, int bb) {
+        const M& Ra = b[ba].rot;
+        const M& Rb = b[bb].rot;
+        V ca = car_box_center(ba), cb = car_box_center(bb);
+        V A[3] = {Ra.col(0), Ra.col(1), Ra.col(2)}, B[3] = {Rb.col(0), Rb.col(1), Rb.col(2)};
+        V h = w.car_half;
+        float cbt = pair_cbt(ba, bb);
+        V axes[15];
+        int na = 0;
+        for (int i = 0; i < 3; i++) axes[na++] = A[i];
+        for (int i = 0; i < 3; i++) axes[na++] = B[i];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) axes[na++] = cross(A[i], B[j]);
+        float best = 1e30f;
+        V best_n;
+        int best_k = -1;
+        for (int k = 0; k < na; k++) {
+            float l2 = len2(axes[k]);
+            if (l2 < 1e-10f) continue;
+            V L = axes[k] / std::sqrt(l2);
+            float ra = h.x * std::fabs(dot(A[0], L)) + h.y * std::fabs(dot(A[1], L)) + h.z * std::fabs(dot(A[2], L));
+            float rb = h.x * std::fabs(dot(B[0], L)) + h.y * std::fabs(dot(B[1], L)) + h.z * std::fabs(dot(B[2], L));
+            float d = dot(ca - cb, L);
+            float pen = ra + rb - std::fabs(d);
+            if (-pen > cbt) return;
+            if (pen < best) {
+                best = pen;
+                best_n = d >= 0 ? L : -L;  // from B towards A
+                best_k = k;
+            }
+        }
+        float depth = -best;
+        V n = best_n;
+        V point_b;
+        if (best_k >= 3 && best_k < 6) {
+            // face of B: deepest vertex of A along -n
+            V dl = vmul(-n, Ra);
+            V lv(dl.x >= 0 ? h.x : -h.x, dl.y >= 0 ? h.y : -h.y, dl.z >= 0 ? h.z : -h.z);
+            V pa = Ra * lv + ca;
+            point_b = pa - n * depth;
+        } else {
+            // face of A or edge-edge: deepest vertex of B along +n
+            V dl = vmul(n, Rb);
+            V lv(dl.x >= 0 ? h.x : -h.x, dl.y >= 0 ? h.y : -h.y, dl.z >= 0 ? h.z : -h.z);
+            point_b = Rb * lv + cb;
+        }
+        add_contact(key, n, point_b, depth);
+    }
+
+    void collision_detection(bool ball_awake) {
+        // dynamic-static pairs (body x {4 planes, mesh}); skipped when both sides inactive
+        for (int bi = 0; bi < 5; bi++) {
+            bool active = bi == 0 ? ball_awake : b[bi].active;
+            for (int st = 0; st < 5; st++) {
+                int key = bi * 8 + st;
+                if (!active) continue;  // needsCollision(inactive, static) == false
+                if (bi == 0) {
+                    if (st < 4) collide_sphere_plane(key, st);
+                    else collide_sphere_mesh(key);
+                } else {
+                    if (st < 4) collide_box_plane(key, bi, st);
+                    else collide_box_mesh(key, bi);
+                }
+                refresh(key);
+            }
+        }
+        // dynamic-dynamic pairs: ball-car then car-car, only while broadphase AABBs overlap
+        for (int a = 0; a < 5; a++)
+            for (int c2 = a + 1; c2 < 5; c2++) {
+                int ka = a == 0 ? c2 : a, kb = a == 0 ? 0 : c2;  // ball pairs keyed (car, ball)
+                int key = 64 + std::min(ka, kb) * 8 + std::max(ka, kb);
+                bool dem = (ka >= 1 && !b[ka].active) || (kb >= 1 && !b[kb].active);
+                V m0, m1, n0, n1;
+                broad_aabb(ka, m0, m1);
+                broad_aabb(kb, n0, n1);
+                bool overlap = !dem && aabb_overlap(m0, m1, n0, n1);
+                if (!overlap) {
+                    rlgpu_manifold* m = find_manifold(key);
+                    if (m) m->count = 0;  // pair removed from the cache -> manifold destroyed
+                    continue;
+                }
+                bool act_a = ka == 0 ? ball_awake : b[ka].active;
+                bool act_b = kb == 0 ? ball_awake : b[kb].active;
+                if (!act_a && !act_b) continue;
+                if (kb == 0)
+                    collide_car_ball(key, ka);
+                else
+                    collide_car_car(key, ka, kb);
+                refresh(key);
+            }
+    }
+
+    // -------------------------------------------------------------------- solver
+    struct SBody {
+        V dlin, dang, push, turn, lin, ang, ext_f, ext_t, inv_mass;
+        bool real;
+        int idx;
+    };
+    struct Row {
+        int a, bb;  // solver body ids
+        V n1, n2, rc1, rc2, angA, angB;
+        float jinv, rhs, rhs_pen, cfm, lower, upper, applied, applied_push, friction;
+        int friction_index;
+        bool special;
+        rlgpu_contact* orig;
+    };
+
+    void solve(bool ball_awake) {
+        // solver bodies: 0..4 as bodies (if active), 5 = fixed
+        SBody sb[6];
+        bool in_solver[5];
+        for (int i = 0; i < 5; i++) {
+            bool act = i == 0 ? ball_awake : b[i].active;
+            in_solver[i] = act;
+            SBody& x = sb[i];
+            x.dlin = x.dang = x.push = x.turn = V();
+            x.real = act;
+            x.idx = i;
+            if (act) {
+                x.inv_mass = V(b[i].inv_mass, b[i].inv_mass, b[i].inv_mass);
+                x.lin = b[i].vel;
+                x.ang = b[i].ang;
+                x.ext_f = b[i].force * b[i].inv_mass * TICK_TIME;
+                x.ext_t = vmul(b[i].torque, b[i].inv_inertia_world) * TICK_TIME;
+            } else {
+                x.inv_mass = V();
+                x.lin = x.ang = x.ext_f = x.ext_t = V();
+            }
+        }
+        SBody& fixed = sb[5];
+        fixed.dlin = fixed.dang = fixed.push = fixed.turn = fixed.lin = fixed.ang = fixed.ext_f = fixed.ext_t = fixed.inv_mass = V();
+        fixed.real = false;
+        fixed.idx = -1;
+
+        std::vector<Row> rows, frows;
+        struct Special {
+            int num = 0;
+            float friction = 0, restitution = 0;
+            V total_n;
+            float total_d = 0;
+        } spec[5];
+
+        auto setup_contact = [&](Row& row, int ia, int ib, const rlgpu_contact& cp, V rel1, V rel2, float dist) {
+            SBody& A = sb[ia];
+            SBody& B = sb[ib];
+            const Body* rb0 = A.real ? &b[A.idx] : nullptr;
+            const Body* rb1 = B.real ? &b[B.idx] : nullptr;
+            V n = ld3(cp.normalB);
+            V t0 = cross(rel1, n);
+            row.angA = rb0 ? rb0->inv_inertia_world * t0 : V();
+            V t1 = cross(rel2, n);
+            row.angB = rb1 ? rb1->inv_inertia_world * -t1 : V();
+            float d0 = 0, d1 = 0;
+            if (rb0) d0 = rb0->inv_mass + dot(n, cross(row.angA, rel1));
+            if (rb1) d1 = rb1->inv_mass + dot(n, cross(-row.angB, rel2));
+            row.jinv = 1.f / (d0 + d1 + 0.f);
+            row.n1 = rb0 ? n : V();
+            row.rc1 = rb0 ? t0 : V();
+            row.n2 = rb1 ? -n : V();
+            row.rc2 = rb1 ? -t1 : V();
+            float penetration = dist + 0.f;
+            V v1 = rb0 ? rb0->vel_at(rel1) : V();
+            V v2 = rb1 ? rb1->vel_at(rel2) : V();
+            float rel_vel = dot(n, v1 - v2);
+            row.friction = cp.friction;
+            float restitution = std::fabs(rel_vel) < 0.2f ? 0.f : cp.restitution * -rel_vel;
+            if (restitution <= 0.f) restitution = 0.f;
+            row.applied = cp.applied * 0.85f;  // warm start
+            if (rb0) {
+                A.dlin += row.n1 * A.inv_mass * row.applied;
+                A.dang += row.angA * row.applied;
+            }
+            if (rb1) {
+                B.dlin += (-row.n2 * B.inv_mass) * -row.applied;
+                B.dang += -row.angB * -row.applied;
+            }
+            row.applied_push = 0;
+            float v1n = dot(row.n1, A.lin + (A.real ? A.ext_f : V())) + dot(row.rc1, A.ang + (A.real ? A.ext_t : V()));
+            float v2n = dot(row.n2, B.lin + (B.real ? B.ext_f : V())) + dot(row.rc2, B.ang + (B.real ? B.ext_t : V()));
+            float rv = v1n + v2n;
+            float pos_err = 0, vel_err = restitution - rv;
+            if (penetration > 0) {
+                pos_err = 0;
+            } else {
+                pos_err = -penetration * 0.8f * (1.f / TICK_TIME);
+            }
+            float pen_imp = pos_err * row.jinv, vel_imp = vel_err * row.jinv;
+            row.rhs = vel_imp;  // split impulse always (threshold 1e30, Arena.cpp:486)
+            row.rhs_pen = pen_imp;
+            row.cfm = 0.f * row.jinv;
+            row.lower = 0;
+            row.upper = 1e10f;
+        };
+        auto add_friction = [&](int ia, int ib, const rlgpu_contact& cp, V rel1, V rel2, int contact_index, float friction) {
+            SBody& A = sb[ia];
+            SBody& B = sb[ib];
+            const Body* rb0 = A.real ? &b[A.idx] : nullptr;
+            const Body* rb1 = B.real ? &b[B.idx] : nullptr;
+            V n = ld3(cp.normalB);
+            V va = A.real ? A.lin + A.ext_f + cross(A.ang + A.ext_t, rel1) : V();
+            V vb = B.real ? B.lin + B.ext_f + cross(B.ang + B.ext_t, rel2) : V();
+            V vel = va - vb;
+            float rel_vel = dot(n, vel);
+            V dir = vel - n * rel_vel;
+            float lat = len2(dir);
+            if (lat > SIMD_EPSILON) {
+                dir = dir * (1.f / std::sqrt(lat));
+            } else {  // btPlaneSpace1
+                V p, q;
+                if (std::fabs(n.z) > 0.7071067811865475244008443621048490f) {
+                    float a = n.y * n.y + n.z * n.z;
+                    float k = 1.f / std::sqrt(a);
+                    p = V(0, -n.z * k, n.y * k);
+                } else {
+                    float a = n.x * n.x + n.y * n.y;
+                    float k = 1.f / std::sqrt(a);
+                    p = V(-n.y * k, n.x * k, 0);
+                }
+                dir = p;
+            }
+            Row f;
+            f.a = ia;
+            f.bb = ib;
+            f.friction = friction;
+            f.orig = nullptr;
+            f.special = false;
+            f.applied = 0;
+            f.applied_push = 0;
+            f.friction_index = contact_index;
+            if (rb0) {
+                f.n1 = dir;
+                V ta = cross(rel1, dir);
+                f.rc1 = ta;
+                f.angA = rb0->inv_inertia_world * ta;
+            } else {
+                f.n1 = f.rc1 = f.angA = V();
+            }
+            if (rb1) {
+                f.n2 = -dir;
+                V tb = cross(rel2, f.n2);
+                f.rc2 = tb;
+                f.angB = rb1->inv_inertia_world * tb;
+            } else {
+                f.n2 = f.rc2 = f.angB = V();
+            }
+            float d0 = 0, d1 = 0;
+            if (rb0) d0 = rb0->inv_mass + dot(dir, cross(f.angA, rel1));
+            if (rb1) d1 = rb1->inv_mass + dot(dir, cross(-f.angB, rel2));
+            f.jinv = 1.f / (d0 + d1);
+            float v1n = dot(f.n1, rb0 ? A.lin + A.ext_f : V()) + dot(f.rc1, rb0 ? A.ang : V());
+            float v2n = dot(f.n2, rb1 ? B.lin + B.ext_f : V()) + dot(f.rc2, rb1 ? B.ang : V());
+            f.rhs = (0.f - (v1n + v2n)) * f.jinv;
+            f.rhs_pen = 0;
+            f.cfm = 0;
+            f.lower = -friction;
+            f.upper = friction;
+            frows.push_back(f);
+        };
+
+        // convert manifolds in canonical key order
+        int order[RLGPU_MANIFOLDS], nm = 0;
+        for (int m = 0; m < RLGPU_MANIFOLDS; m++)
+            if (s.manifolds[m].count > 0) order[nm++] = m;
+        std::sort(order, order + nm, [&](int x, int y) { return s.manifolds[x].key < s.manifolds[y].key; });
+        for (int oi = 0; oi < nm; oi++) {
+            rlgpu_manifold& mf = s.manifolds[order[oi]];
+            int a, bb;
+            key_bodies(mf.key, a, bb);
+            bool aact = a < 10 && in_solver[a];
+            bool bact = bb < 10 && in_solver[bb];
+            if (!aact && !bact) continue;  // sleeping island / both static
+            int ia = aact ? a : 5, ib = bact ? bb : 5;
+            V pa_, pb_;
+            M ra, rb;
+            side_transform(a, pa_, ra);
+            side_transform(bb, pb_, rb);
+            for (int j = 0; j < mf.count; j++) {
+                rlgpu_contact& cp = mf.pts[j];
+                V wa = ra * ld3(cp.localA) + pa_;  // positions from the last refresh
+                V wb = rb * ld3(cp.localB) + pb_;
+                V rel1 = wa - pa_;
+                V rel2 = wb - (bb >= 10 ? V() : pb_);
+                Row row;
+                row.a = ia;
+                row.bb = ib;
+                row.orig = &cp;
+                row.special = cp.special != 0;
+                setup_contact(row, ia, ib, cp, rel1, rel2, cp.dist);
+                int cidx = (int)rows.size();
+                row.friction_index = (int)frows.size();
+                if (cp.special) {
+                    for (int side = 0; side < 2; side++) {
+                        int bid = side ? bb : a;
+                        if (bid < 10) {
+                            Special& sp = spec[bid];
+                            sp.num++;
+                            sp.friction = cp.friction;
+                            sp.restitution = cp.restitution;
+                            sp.total_n += ld3(cp.normalB);
+                            sp.total_d += len(side ? rel2 : rel1);
+                        }
+                    }
+                }
+                rows.push_back(row);
+                add_friction(ia, ib, cp, rel1, rel2, cidx, cp.friction);
+            }
+        }
+        // RocketSim special contacts: one averaged row per body vs the fixed body
+        for (int i = 0; i < 5; i++) {
+            if (spec[i].num <= 0 || !in_solver[i]) continue;
+            float distance = spec[i].total_d / spec[i].num;
+            V normal = spec[i].total_n / (float)spec[i].num;
+            rlgpu_contact tmp;
+            std::memset(&tmp, 0, sizeof tmp);
+            tmp.dist = distance;
+            st3(tmp.normalB, normal);
+            tmp.friction = spec[i].friction;
+            tmp.restitution = spec[i].restitution;
+            V rel1 = normal * -distance, rel2 = V();
+            Row row;
+            row.a = i;
+            row.bb = 5;
+            row.orig = nullptr;
+            row.special = false;
+            setup_contact(row, i, 5, tmp, rel1, rel2, distance);
+            int cidx = (int)rows.size();
+            row.friction_index = (int)frows.size();
+            rows.push_back(row);
+            add_friction(i, 5, tmp, rel1, rel2, cidx, tmp.friction);
+        }
+
+        auto resolve_lower = [&](Row& c, bool generic) {
+            SBody& A = sb[c.a];
+            SBody& B = sb[c.bb];
+            float di = c.rhs - c.applied * c.cfm;
+            float dv1 = dot(c.n1, A.dlin) + dot(c.rc1, A.dang);
+            float dv2 = dot(c.n2, B.dlin) + dot(c.rc2, B.dang);
+            di -= dv1 * c.jinv;
+            di -= dv2 * c.jinv;
+            float sum = c.applied + di;
+            if (sum < c.lower) {
+                di = c.lower - c.applied;
+                c.applied = c.lower;
+            } else if (generic && sum > c.upper) {
+                di = c.upper - c.applied;
+                c.applied = c.upper;
+            } else {
+                c.applied = sum;
+            }
+            if (A.real) {
+                A.dlin += c.n1 * A.inv_mass * di;
+                A.dang += c.angA * di;
+            }
+            if (B.real) {
+                B.dlin += c.n2 * B.inv_mass * di;
+                B.dang += c.angB * di;
+            }
+            return di * (1.f / c.jinv);
+        };
+        auto resolve_split = [&](Row& c) {
+            float di = 0.f;
+            if (c.rhs_pen != 0.f) {
+                SBody& A = sb[c.a];
+                SBody& B = sb[c.bb];
+                di = c.rhs_pen - c.applied_push * c.cfm;
+                float dv1 = dot(c.n1, A.push) + dot(c.rc1, A.turn);
+                float dv2 = dot(c.n2, B.push) + dot(c.rc2, B.turn);
+                di -= dv1 * c.jinv;
+                di -= dv2 * c.jinv;
+                float sum = c.applied_push + di;
+                if (sum < c.lower) {
+                    di = c.lower - c.applied_push;
+                    c.applied_push = c.lower;
+                } else {
+                    c.applied_push = sum;
+                }
+                if (A.real) {
+                    A.push += c.n1 * A.inv_mass * di;
+                    A.turn += c.angA * di;
+                }
+                if (B.real) {
+                    B.push += c.n2 * B.inv_mass * di;
+                    B.turn += c.angB * di;
+                }
+            }
+            return di * (1.f / c.jinv);
+        };
+        // split-impulse iterations (btSequentialImpulseConstraintSolver.cpp:1762-1795)
+        for (int it = 0; it < 10; it++) {
+            float lsr = 0.f;
+            for (auto& r : rows) {
+                float res = resolve_split(r);
+                lsr = std::max(lsr, res * res);
+            }
+            if (lsr <= 0.f || it >= 9) break;
+        }
+        // main iterations (:1640-1760, non-interleaved path, special rows skipped)
+        for (int it = 0; it < 10; it++) {
+            for (auto& r : rows) {
+                if (r.special) continue;
+                resolve_lower(r, false);
+            }
+            for (auto& f : frows) {
+                float total = rows[f.friction_index].applied;
+                if (total > 0.f) {
+                    f.lower = -(f.friction * total);
+                    f.upper = f.friction * total;
+                    resolve_lower(f, true);
+                }
+            }
+        }
+        // write back contacts and bodies (:1830-1900)
+        for (auto& r : rows)
+            if (r.orig) r.orig->applied = r.applied;
+        for (int i = 0; i < 5; i++) {
+            if (!in_solver[i]) continue;
+            SBody& x = sb[i];
+            Body& bd = b[i];
+            x.lin += x.dlin;
+            x.ang += x.dang;
+            if (!(x.push.x == 0 && x.push.y == 0 && x.push.z == 0 && x.turn.x == 0 && x.turn.y == 0 && x.turn.z == 0)) {
+                if (bd.no_rot) {
+                    bd.pos = bd.pos + x.push * TICK_TIME;
+                } else {
+                    V np;
+                    M nr;
+                    integrate_transform(bd.pos, bd.rot, x.push, x.turn * 0.1f, TICK_TIME, np, nr);
+                    bd.pos = np;
+                    bd.rot = nr;
+                }
+            }
+            bd.vel = x.lin + x.ext_f;
+            bd.ang = x.ang + x.ext_t;
+        }
+    }
+
+    // ------------------------------------------------------------ Arena::Step (1 tick)
+    void tick() {
+        const World& W = w;
+        // ball zero-vel sleeping (Arena.cpp:722-727)
+        bool ball_sleep = len2(b[0].vel) == 0 && len2(b[0].ang) == 0;
+        s.ball_sleeping = ball_sleep;
+        b[0].active = true;
+        for (int ci = 0; ci < 4; ci++) b[ci + 1].active = !car(ci).is_demoed;  // Car.cpp:66-81
+        for (int i = 0; i < 5; i++) snap[i] = b[i];
+        demo_timers();
+        for (int ci = 0; ci < 4; ci++) car_pre_tick(ci);
+        for (int i = 0; i < RLGPU_PADS; i++) {  // BoostPad::_PreTickUpdate
+            rlgpu_pad& p = s.pads[i];
+            if (p.cooldown > 0) p.cooldown = std::max(p.cooldown - TICK_TIME, 0.f);
+            p.is_active = p.cooldown == 0;
+        }
+        int locked[RLGPU_PADS];
+        for (int i = 0; i < RLGPU_PADS; i++) locked[i] = -1;
+        // stepSimulation: applyGravity
+        b[0].force += W.gravity * BALL_MASS;
+        for (int ci = 0; ci < 4; ci++) b[ci + 1].force += W.gravity * CAR_MASS;
+        // predictUnconstraintMotion: damping + predicted transform
+        b[0].vel *= W.ball_damp;
+        b[0].ang *= 1.f;  // angular damping 0 -> pow(1, dt) == 1
+        for (int i = 0; i < 5; i++) {
+            if (i == 0 && b[0].no_rot) {
+                b[0].pred_pos = b[0].pos + b[0].vel * TICK_TIME;
+                b[0].pred_rot = b[0].rot;
+            } else {
+                integrate_transform(b[i].pos, b[i].rot, b[i].vel, b[i].ang, TICK_TIME, b[i].pred_pos, b[i].pred_rot);
+            }
+        }
+        // ball island activity: awake if moving, or sharing an island (overlapping broadphase pair)
+        bool ball_awake = !ball_sleep;
+        if (ball_sleep) {
+            V m0, m1;
+            broad_aabb(0, m0, m1);
+            for (int ci = 1; ci <= 4; ci++) {
+                if (!b[ci].active) continue;
+                V n0, n1;
+                broad_aabb(ci, n0, n1);
+                if (aabb_overlap(m0, m1, n0, n1)) ball_awake = true;
+            }
+        }
+        collision_detection(ball_awake);
+        solve(ball_awake);
+        // integrateTransforms (btDiscreteDynamicsWorld.cpp:889-985), active bodies only
+        for (int i = 0; i < 5; i++) {
+            bool act = i == 0 ? ball_awake : b[i].active;
+            if (!act) continue;
+            if (b[i].no_rot) {
+                b[i].pos = b[i].pos + b[i].vel * TICK_TIME;
+            } else {
+                V np;
+                M nr;
+                integrate_transform(b[i].pos, b[i].rot, b[i].vel, b[i].ang, TICK_TIME, np, nr);
+                b[i].pos = np;
+                b[i].rot = nr;
+            }
+            b[i].update_inertia();
+        }
+        for (int i = 0; i < 5; i++) b[i].force = b[i].torque = V();
+        // cars: post tick, finish, pad collide (Arena.cpp:785-800)
+        for (int ci = 0; ci < 4; ci++) {
+            rlgpu_car& cs = car(ci);
+            Body& c = b[ci + 1];
+            if (!cs.is_demoed) {
+                // _PostTickUpdate (Car.cpp:133-163)
+                float sp2 = len2(c.vel * BT_TO_UU);
+                if (cs.is_supersonic && cs.supersonic_time < 1.f)
+                    cs.is_supersonic = sp2 >= 2100.f * 2100.f;
+                else
+                    cs.is_supersonic = sp2 >= 2200.f * 2200.f;
+                if (cs.is_supersonic)
+                    cs.supersonic_time += TICK_TIME;
+                else
+                    cs.supersonic_time = 0;
+                if (cs.car_contact_cooldown > 0) cs.car_contact_cooldown = std::max(cs.car_contact_cooldown - TICK_TIME, 0.f);
+                std::memcpy(cs.last_controls, cs.controls, sizeof cs.controls);
+                // _FinishPhysicsTick (Car.cpp:165-193)
+                V cache = ld3(cs.vel_impulse_cache);
+                if (!is_zero(cache)) {
+                    c.vel += cache;
+                    st3(cs.vel_impulse_cache, V());
+                }
+                const float maxv = 2300.f * UU_TO_BT;
+                if (len2(c.vel) > maxv * maxv) c.vel = normalized(c.vel) * maxv;
+                if (len2(c.ang) > 5.5f * 5.5f) c.ang = normalized(c.ang) * 5.5f;
+            }
+            // BoostPadGrid::CheckCollision (BoostPadGrid.cpp:5-25)
+            if (cs.is_demoed || cs.boost >= 100) continue;
+            V pos_uu = c.pos * BT_TO_UU;
+            if (pos_uu.z > 95.f + 250.f) continue;
+            int ix = (int)(pos_uu.x / 1024 + 4), iy = (int)(pos_uu.y / 1024 + 5);
+            for (int p = 0; p < RLGPU_PADS; p++) {
+                int px = W.pad_cell_x[p], py = W.pad_cell_y[p];
+                if (px < std::max(ix - 1, 0) || px > std::min(ix + 1, 7) || py < std::max(iy - 1, 0) || py > std::min(iy + 1, 9))
+                    continue;
+                rlgpu_pad& pd = s.pads[p];
+                bool col = false;
+                if (pd.prev_locked_car_id == car_id(ci)) {
+                    V mn, mx;
+                    body_aabb(ci + 1, c.pos, c.rot, mn, mx);
+                    col = (W.pad_box_max[p].x > mn.x && W.pad_box_max[p].y > mn.y && W.pad_box_max[p].z > mn.z) &&
+                          (W.pad_box_min[p].x < mx.x && W.pad_box_min[p].y < mx.y && W.pad_box_min[p].z < mx.z);
+                } else {
+                    float rad = (W.pad_big[p] ? 208.f : 144.f) * UU_TO_BT;
+                    float dx = c.pos.x - W.pad_pos_bt[p].x, dy = c.pos.y - W.pad_pos_bt[p].y;
+                    if (dx * dx + dy * dy < rad * rad) col = std::fabs(c.pos.z - W.pad_pos_bt[p].z) < (95.f * UU_TO_BT);
+                }
+                if (col) locked[p] = ci;
+            }
+        }
+        // BoostPad::_PostTickUpdate (BoostPad.cpp:88-105)
+        for (int p = 0; p < RLGPU_PADS; p++) {
+            rlgpu_pad& pd = s.pads[p];
+            uint32_t lid = 0;
+            if (locked[p] >= 0) {
+                lid = car_id(locked[p]);
+                if (pd.is_active) {
+                    rlgpu_car& cs = car(locked[p]);
+                    cs.boost = std::min(cs.boost + (W.pad_big[p] ? 100.f : 12.f), 100.f);
+                    pd.is_active = 0;
+                    pd.cooldown = W.pad_big[p] ? 10.f : 4.f;
+                }
+            }
+            pd.prev_locked_car_id = lid;
+        }
+        // Ball::_FinishPhysicsTick (Ball.cpp:112-138)
+        {
+            Body& ball = b[0];
+            V cache = ld3(s.ball_vel_impulse_cache);
+            if (!is_zero(cache)) {
+                ball.vel += cache;
+                st3(s.ball_vel_impulse_cache, V());
+            }
+            const float maxv = 6000.f * UU_TO_BT;
+            if (len2(ball.vel) > maxv * maxv) ball.vel = normalized(ball.vel) * maxv;
+            if (len2(ball.ang) > 6.f * 6.f) ball.ang = normalized(ball.ang) * 6.f;
+        }
+        s.env.tick_count++;
+    }
+
+    void step(int ticks) {
+        load_bodies();
+        for (int t = 0; t < ticks; t++) tick();
+        store_bodies();
+    }
+};
+
+void default_car(rlgpu_car& cs) {
+    // CarState defaults (Car.h:17-100)
+    std::memset(&cs, 0, sizeof cs);
+    stm(cs.body.rot, M::ident());
+    cs.is_on_ground = 1;
+    cs.boost = 100.f / 3.f;  // BOOST_SPAWN_AMOUNT
+    cs.ball_hit_tick = -1;
+    cs.ball_hit_extra_tick = -1;
+}
+
+// Arena::ResetToRandomKickoff (Arena.cpp:112-216) with Philox draws for std::shuffle.
+void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index) {
+    const World& W = world();
+    int order[5] = {0, 1, 2, 3, 4};
+    for (int i = 4; i > 0; i--) {  // Fisher-Yates
+        int j = (int)(rng_next(seed, arena_index, s.env) % (uint32_t)(i + 1));
+        std::swap(order[i], order[j]);
+    }
+    Sim sim(W, s, seed, arena_index);
+    sim.load_bodies();
+    for (int i = 0; i < 2; i++) {  // two cars per team: blue = cars 0,2; orange = cars 1,3
+        int k = order[i];
+        for (int team = 0; team < 2; team++) {
+            int ci = 2 * i + team;
+            V pos(W.kick_x[k], W.kick_y[k], 17.f);
+            if (team == 1) pos = pos * V(-1, -1, 1);
+            sim.set_car_state(ci, pos, W.kick_rot[team][k], 100.f / 3.f, true);
+        }
+    }
+    // ball: BallState() at rest (pos 0,0,BALL_REST_Z)
+    sim.b[0].pos = V(0, 0, 93.15f) * UU_TO_BT;
+    sim.b[0].rot = M::ident();
+    sim.b[0].vel = sim.b[0].ang = V();
+    sim.store_bodies();
+    for (int i = 0; i < 3; i++) s.ball_vel_impulse_cache[i] = 0;
+    for (int p = 0; p < RLGPU_PADS; p++) {
+        s.pads[p].is_active = 1;
+        s.pads[p].cooldown = 0;
+        s.pads[p].prev_locked_car_id = 0;
+    }
+    for (int m = 0; m < RLGPU_MANIFOLDS; m++) s.manifolds[m].count = 0;
+}
+
+void arena_step(rlgpu_arena_state& s, uint64_t seed, int arena_index, int ticks) {
+    Sim sim(world(), s, seed, arena_index);
+    sim.step(ticks);
+}
+
+}  // namespace orc
