@@ -162,11 +162,12 @@ int rlgpu_envset_reset_arenas(rlgpu_envset* env, const uint8_t* d_mask, void* st
 int rlgpu_envset_step_first_half(rlgpu_envset* env, void* stream);
 int rlgpu_envset_step_second_half(rlgpu_envset* env, const int32_t* d_actions, void* stream);
 /* Fused: first half + second half + (optional) reset of terminated arenas in one launch.
- * If d_obs_out != NULL the post-reset obs rows are also written there (experience append:
- * the row for step t+1 of the rollout buffer); pre-reset obs of TRUNCATED arenas go to
- * buffers.trunc_obs. */
+ * Experience append (GigaLearnCPP Learner.cpp:180-260 collection loop): if non-NULL,
+ * d_obs_out receives the post-reset obs rows [players x OBS] (the rollout buffer row for
+ * step t+1), d_rew_out the rewards [players], d_term_out the terminal codes [arenas].
+ * Pre-reset obs of TRUNCATED arenas go to buffers.trunc_obs. Requires action_delay > 0. */
 int rlgpu_envset_step(rlgpu_envset* env, const int32_t* d_actions, int32_t reset_terminated,
-                      float* d_obs_out, void* stream);
+                      float* d_obs_out, float* d_rew_out, uint8_t* d_term_out, void* stream);
 int rlgpu_envset_sync(rlgpu_envset* env, void* stream);
 
 /* Wire-format state transfer (host <-> device), for GameState snapshots, tests and replay. */

@@ -1,0 +1,827 @@
+// env.hip -- the MI355X arena-set kernel and its C ABI (include/rlgpu_env.h).
+//
+// One launch = one (half) env step for every arena: LDS-resident arena records, quarter-wave
+// teams per arena (env_kernel.hpp), phases of Arena::Step separated by workgroup barriers.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/rlgpu_arena_mesh.h"
+#include "common.hpp"
+#include "env_builders.hpp"
+
+namespace rl {
+
+__constant__ EnvConst C;
+
+
+struct StepArgs {
+    char* arenas;
+    int n;
+    int ticks_first;        // StepFirstHalf ticks (actionDelay), 0 = skip
+    const int32_t* actions; // StepSecondHalf actions (null = skip second half)
+    int ticks_second;       // tickSkip - actionDelay
+    int build;              // run GameState / terminal / reward / obs builders
+    int reset_mode;         // 0 none, 1 reset terminated (fused), 2 EnvSet::Reset, 3 mask, 4 all, 5 obs only
+    const uint8_t* reset_mask;
+    float* obs;
+    uint8_t* masks;
+    float* rewards;
+    uint8_t* terminals;
+    float* last_rewards;
+    float* trunc_obs;
+    float* obs_out;
+    float* rew_out;
+    uint8_t* term_out;
+    uint64_t seed;
+};
+
+DEV void sync() { __syncthreads(); }
+
+// ------------------------------------------------------------------ one tick (Arena::Step body)
+DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
+    if (valid && l == 0) {
+        rlgpu_arena_state& s = A->s;
+        bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
+        s.ball_sleeping = sleep;
+        A->a.ball_sleep = sleep;
+        A->a.active[0] = 1;
+        for (int c = 0; c < 4; c++) {
+            A->a.active[c + 1] = !s.cars[c].is_demoed;
+            float* ctl = s.cars[c].controls;  // CarControls::ClampFix
+            for (int k = 0; k < 5; k++) ctl[k] = stdclamp(ctl[k], -1.f, 1.f);
+        }
+        for (int i = 0; i < 5; i++) {
+            A->a.snap_vel[i] = bvel(A, i);
+            A->a.snap_ang[i] = bang(A, i);
+        }
+        // demo timer / respawn (Car.cpp:66-84), RNG draws in car order
+        for (int c = 0; c < 4; c++) {
+            rlgpu_car& cs = s.cars[c];
+            if (cs.is_demoed) {
+                cs.demo_respawn_timer = stdmax(cs.demo_respawn_timer - kTick, 0.f);
+                if (cs.demo_respawn_timer == 0.f) {
+                    int idx = (int)(rng_next(A, seed, arena) % 4u);
+                    bool orange = c & 1;
+                    v3 pos = v3{C.respawn_x[idx], C.respawn_y[idx] * (orange ? -1.f : 1.f), 36.f};
+                    set_car_state(A, c, pos, C.respawn_rot[orange][idx], 100.f / 3.f, false);
+                }
+            }
+        }
+    }
+    sync();
+    if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase(A, l >> 2, l & 3);
+    sync();
+    if (valid) {
+        if (l < 4) {
+            car_phase(A, l);
+        } else {
+            for (int p = l - 4; p < RLGPU_PADS; p += 12) {  // BoostPad::_PreTickUpdate
+                rlgpu_pad& pd = A->s.pads[p];
+                if (pd.cooldown > 0) pd.cooldown = stdmax(pd.cooldown - kTick, 0.f);
+                pd.is_active = pd.cooldown == 0;
+            }
+        }
+    }
+    sync();
+    if (valid && l < 5) {  // applyGravity + predictUnconstraintMotion
+        add_force(A, l, C.gravity * (l == 0 ? kBallMass : kCarMass));
+        if (l == 0) {
+            rlgpu_body* b = body(A, 0);
+            st3(b->vel, ld3(b->vel) * C.ball_damp);
+            st3(b->angvel, ld3(b->angvel) * 1.f);
+            A->a.pred_pos[0] = bpos(A, 0) + bvel(A, 0) * kTick;
+            A->a.pred_rot[0] = brot(A, 0);
+        } else {
+            integrate_transform(bpos(A, l), brot(A, l), bvel(A, l), bang(A, l), kTick, A->a.pred_pos[l], A->a.pred_rot[l]);
+        }
+    }
+    sync();
+    if (valid && l == 0) {
+        bool awake = !A->a.ball_sleep;
+        if (!awake) {
+            v3 m0, m1;
+            broad_aabb(A, 0, m0, m1);
+            for (int ci = 1; ci <= 4; ci++) {
+                if (!A->a.active[ci]) continue;
+                v3 n0, n1;
+                broad_aabb(A, ci, n0, n1);
+                if (aabb_overlap(m0, m1, n0, n1)) awake = true;
+            }
+        }
+        A->a.ball_awake = awake;
+        A->a.ncand = 0;
+    }
+    sync();
+    if (valid)
+        for (int rank = l; rank < kPairs; rank += kTeam) A->a.pair_mode[rank] = narrow_pair(A, rank);
+    sync();
+    if (valid && l == 0) {
+        commit_contacts(A);
+        solve(A);
+    }
+    sync();
+    if (valid && l < 5) {  // integrateTransforms (btDiscreteDynamicsWorld.cpp:889-985)
+        bool act = l == 0 ? A->a.ball_awake != 0 : A->a.active[l] != 0;
+        if (act) {
+            rlgpu_body* b = body(A, l);
+            if (l == 0) {
+                st3(b->pos, ld3(b->pos) + ld3(b->vel) * kTick);
+            } else {
+                v3 np;
+                m3 nr;
+                integrate_transform(ld3(b->pos), ldm(b->rot), ld3(b->vel), ld3(b->angvel), kTick, np, nr);
+                st3(b->pos, np);
+                stm(b->rot, nr);
+            }
+            update_inertia(A, l);
+        }
+        A->a.force[l] = zero3();
+        A->a.torque[l] = zero3();
+    }
+    sync();
+    if (valid && l < 4) {  // Car::_PostTickUpdate + _FinishPhysicsTick (Car.cpp:133-193)
+        rlgpu_car& cs = A->s.cars[l];
+        if (!cs.is_demoed) {
+            rlgpu_body* b = &cs.body;
+            float sp2 = len2(ld3(b->vel) * kBT2UU);
+            if (cs.is_supersonic && cs.supersonic_time < 1.f)
+                cs.is_supersonic = sp2 >= 2100.f * 2100.f;
+            else
+                cs.is_supersonic = sp2 >= 2200.f * 2200.f;
+            if (cs.is_supersonic)
+                cs.supersonic_time += kTick;
+            else
+                cs.supersonic_time = 0;
+            if (cs.car_contact_cooldown > 0) cs.car_contact_cooldown = stdmax(cs.car_contact_cooldown - kTick, 0.f);
+            for (int k = 0; k < 8; k++) cs.last_controls[k] = cs.controls[k];
+            v3 cache = ld3(cs.vel_impulse_cache);
+            v3 v = ld3(b->vel), w = ld3(b->angvel);
+            if (!is_zero(cache)) {
+                v += cache;
+                st3(cs.vel_impulse_cache, zero3());
+            }
+            const float maxv = 2300.f * kUU2BT;
+            if (len2(v) > maxv * maxv) v = normalized(v) * maxv;
+            if (len2(w) > 5.5f * 5.5f) w = normalized(w) * 5.5f;
+            st3(b->vel, v);
+            st3(b->angvel, w);
+        }
+    }
+    sync();
+    if (valid) {  // BoostPadGrid::CheckCollision per pad (BoostPadGrid.cpp:5-25, BoostPad.cpp:61-86)
+        for (int p = l; p < RLGPU_PADS; p += kTeam) {
+            int locked = -1;
+            rlgpu_pad& pd = A->s.pads[p];
+            for (int ci = 0; ci < 4; ci++) {
+                const rlgpu_car& cs = A->s.cars[ci];
+                if (cs.is_demoed || cs.boost >= 100) continue;
+                v3 cpos = ld3(cs.body.pos);
+                v3 pos_uu = cpos * kBT2UU;
+                if (pos_uu.z > 95.f + 250.f) continue;
+                int ix = (int)(pos_uu.x / 1024 + 4), iy = (int)(pos_uu.y / 1024 + 5);
+                int px = C.pad_cell_x[p], py = C.pad_cell_y[p];
+                int x0 = ix - 1 > 0 ? ix - 1 : 0, x1 = ix + 1 < 7 ? ix + 1 : 7;
+                int y0 = iy - 1 > 0 ? iy - 1 : 0, y1 = iy + 1 < 9 ? iy + 1 : 9;
+                if (px < x0 || px > x1 || py < y0 || py > y1) continue;
+                bool col = false;
+                if (pd.prev_locked_car_id == (uint32_t)(ci + 1)) {
+                    v3 mn, mx;
+                    body_aabb(ci + 1, cpos, ldm(cs.body.rot), mn, mx);
+                    col = (C.pad_box_max[p].x > mn.x && C.pad_box_max[p].y > mn.y && C.pad_box_max[p].z > mn.z) &&
+                          (C.pad_box_min[p].x < mx.x && C.pad_box_min[p].y < mx.y && C.pad_box_min[p].z < mx.z);
+                } else {
+                    float rad = (C.pad_big[p] ? 208.f : 144.f) * kUU2BT;
+                    float dx = cpos.x - C.pad_pos_bt[p].x, dy = cpos.y - C.pad_pos_bt[p].y;
+                    if (dx * dx + dy * dy < rad * rad) col = fabsf(cpos.z - C.pad_pos_bt[p].z) < (95.f * kUU2BT);
+                }
+                if (col) locked = ci;
+            }
+            A->a.locked[p] = locked;
+        }
+    }
+    sync();
+    if (valid && l == 0) {
+        for (int p = 0; p < RLGPU_PADS; p++) {  // BoostPad::_PostTickUpdate (BoostPad.cpp:88-105)
+            rlgpu_pad& pd = A->s.pads[p];
+            uint32_t lid = 0;
+            int lk = A->a.locked[p];
+            if (lk >= 0) {
+                lid = (uint32_t)(lk + 1);
+                if (pd.is_active) {
+                    rlgpu_car& cs = A->s.cars[lk];
+                    cs.boost = stdmin(cs.boost + (C.pad_big[p] ? 100.f : 12.f), 100.f);
+                    pd.is_active = 0;
+                    pd.cooldown = C.pad_big[p] ? 10.f : 4.f;
+                }
+            }
+            pd.prev_locked_car_id = lid;
+        }
+        rlgpu_body* b = &A->s.ball;  // Ball::_FinishPhysicsTick (Ball.cpp:112-138)
+        v3 v = ld3(b->vel), w = ld3(b->angvel);
+        v3 cache = ld3(A->s.ball_vel_impulse_cache);
+        if (!is_zero(cache)) {
+            v += cache;
+            st3(A->s.ball_vel_impulse_cache, zero3());
+        }
+        const float maxv = 6000.f * kUU2BT;
+        if (len2(v) > maxv * maxv) v = normalized(v) * maxv;
+        if (len2(w) > 6.f * 6.f) w = normalized(w) * 6.f;
+        st3(b->vel, v);
+        st3(b->angvel, w);
+        A->s.env.tick_count++;
+    }
+    sync();
+}
+
+// obs / mask rows of all 4 players into LDS, then coalesced copy to the output rows
+DEV void build_and_copy_obs(ArenaLDS* A, int l, bool valid, int arena, const StepArgs& g, float* obs_dst2) {
+    if (valid && l < 4) build_obs_row(A, l);
+    sync();
+    if (valid) {
+        const float* src = &A->u.out.obs[0][0];
+        float* dst = g.obs + (size_t)arena * 4 * RLGPU_OBS;
+        for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
+        if (obs_dst2) {
+            float* d2 = obs_dst2 + (size_t)arena * 4 * RLGPU_OBS;
+            for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) d2[k] = src[k];
+        }
+        const uint8_t* msrc = &A->u.out.masks[0][0];
+        uint8_t* mdst = g.masks + (size_t)arena * 4 * RLGPU_ACTIONS;
+        for (int k = l; k < 4 * RLGPU_ACTIONS; k += kTeam) mdst[k] = msrc[k];
+    }
+    sync();
+}
+
+__global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
+    __shared__ ArenaLDS lds[kArenas];
+    const int team = threadIdx.x >> 4, l = threadIdx.x & 15;
+    const int arena = blockIdx.x * kArenas + team;
+    const bool valid = arena < g.n;
+    ArenaLDS* A = &lds[team];
+    // ---- stage the 4 arena records into LDS (contiguous 16-byte loads)
+    {
+        int first = blockIdx.x * kArenas;
+        int cnt = g.n - first < kArenas ? g.n - first : kArenas;
+        const int chunks = kRec / 16;
+        for (int k = threadIdx.x; k < cnt * chunks; k += 64) {
+            int a = k / chunks, c = k % chunks;
+            const uint4* src = (const uint4*)(g.arenas + (size_t)(first + a) * kRec) + c;
+            uint4* dst = (uint4*)&lds[a] + c;
+            *dst = *src;
+        }
+    }
+    sync();
+    if (valid && l < 5) {
+        A->a.force[l] = zero3();
+        A->a.torque[l] = zero3();
+        update_inertia(A, l);
+    }
+    sync();
+    // ---- StepFirstHalf (EnvSet.cpp:113-130)
+    if (g.ticks_first > 0) {
+        if (valid && l == 0) {
+            rlgpu_env_extra& e = A->s.env;
+            for (int i = 0; i < 3; i++) e.prev_ball_vel[i] = A->s.ball.vel[i] * kBT2UU;
+            for (int i = 0; i < 4; i++) {
+                e.prev_boost[i] = A->s.cars[i].boost;
+                e.prev_is_flipping[i] = A->s.cars[i].is_flipping;
+                e.prev_on_ground[i] = A->s.cars[i].is_on_ground;
+                e.ev_bump[i] = e.ev_bumped[i] = e.ev_demo[i] = e.ev_demoed[i] = 0;
+            }
+            e.has_prev = 1;
+        }
+        sync();
+        for (int t = 0; t < g.ticks_first; t++) tick(A, l, valid, g.seed, arena);
+    }
+    // ---- StepSecondHalf (EnvSet.cpp:132-273)
+    if (g.actions) {
+        if (valid && l < 4) {
+            int a = g.actions[arena * 4 + l];
+            a = a < 0 ? 0 : (a > RLGPU_ACTIONS - 1 ? RLGPU_ACTIONS - 1 : a);
+            const float* x = C.action[a];
+            float* c = A->s.cars[l].controls;
+            for (int k = 0; k < 5; k++) c[k] = x[k];
+            c[5] = x[5] == 1 ? 1.f : 0.f;
+            c[6] = x[6] == 1 ? 1.f : 0.f;
+            c[7] = x[7] == 1 ? 1.f : 0.f;
+            for (int k = 0; k < 8; k++) A->s.env.prev_action[l][k] = x[k];
+        }
+        sync();
+        for (int t = 0; t < g.ticks_second; t++) tick(A, l, valid, g.seed, arena);
+    }
+    // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks
+    uint8_t term = 0;
+    if (g.build) {
+        if (valid && l == 0) {
+            rlgpu_env_extra& e = A->s.env;
+            int64_t cur = e.tick_count;
+            int64_t tick_skip = cur - e.last_tick_count > 0 ? cur - e.last_tick_count : 0;
+            float delta_time = (int)tick_skip * (1.0f / 120.0f);
+            bool any = false;
+            for (int i = 0; i < 4; i++) {
+                const rlgpu_car& c = A->s.cars[i];
+                bool t = c.ball_hit_valid && (uint64_t)c.ball_hit_tick >= (uint64_t)(cur - tick_skip);
+                A->a.touched[i] = t;
+                any |= t;
+            }
+            float by = A->s.ball.pos[1] * kBT2UU;
+            bool goal = fabsf(by) > (5124.25f + 91.25f);
+            A->a.goal = goal;
+            bool t_notouch;
+            if (any) {
+                e.no_touch_time = 0;
+                t_notouch = false;
+            } else {
+                e.no_touch_time += delta_time;
+                t_notouch = e.no_touch_time >= 8.f;
+            }
+            if (goal) {
+                if (by > 0) e.score_blue++;
+                else e.score_orange++;
+            }
+            bool t_score = (e.score_blue >= 3) || (e.score_orange >= 3);
+            uint8_t tt = 0;
+            if (t_notouch) tt = 2;
+            if (t_score) tt = 1;
+            e.terminal = tt;
+            if (goal) {
+                if (by > 0) e.penalty_blue++;
+                else e.penalty_orange++;
+            }
+        }
+        sync();
+        if (valid && l < 4) {
+            PView P[4];
+            for (int i = 0; i < 4; i++) P[i] = view_player(A, i);
+            v3 bp = ld3(A->s.ball.pos) * kBT2UU, bv = ld3(A->s.ball.vel) * kBT2UU, pbv = ld3(A->s.env.prev_ball_vel);
+            float all = 0.f;
+            for (int r = 0; r < RLGPU_REWARDS; r++) {
+                float o = reward_value(A, r, l, P, bp, bv, pbv, A->a.goal != 0);
+                all += o * C.reward_w[r];
+                if (l == 0 && g.last_rewards) g.last_rewards[(size_t)arena * RLGPU_REWARDS + r] = o;
+            }
+            A->a.all_rewards[l] = all;
+        }
+        sync();
+        if (valid && l == 0) {
+            term = A->s.env.terminal;
+            for (int i = 0; i < 4; i++) {
+                g.rewards[arena * 4 + i] = A->a.all_rewards[i];
+                if (g.rew_out) g.rew_out[arena * 4 + i] = A->a.all_rewards[i];
+            }
+            g.terminals[arena] = term;
+            if (g.term_out) g.term_out[arena] = term;
+            A->s.env.last_tick_count = A->s.env.tick_count;
+        }
+        sync();
+        if (valid) term = A->s.env.terminal;
+        bool fused_reset = g.reset_mode == 1 && valid && term != 0;
+        build_and_copy_obs(A, l, valid, arena, g, fused_reset ? nullptr : g.obs_out);
+        if (g.reset_mode == 1) {
+            if (fused_reset && term == 2 && g.trunc_obs) {
+                const float* src = g.obs + (size_t)arena * 4 * RLGPU_OBS;
+                float* dst = g.trunc_obs + (size_t)arena * 4 * RLGPU_OBS;
+                for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
+            }
+            sync();
+            if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena);
+            sync();
+            if (fused_reset && l < 4) build_obs_row(A, l);
+            sync();
+            if (fused_reset) {
+                const float* src = &A->u.out.obs[0][0];
+                float* dst = g.obs + (size_t)arena * 4 * RLGPU_OBS;
+                for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
+                if (g.obs_out) {
+                    float* d2 = g.obs_out + (size_t)arena * 4 * RLGPU_OBS;
+                    for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) d2[k] = src[k];
+                }
+                const uint8_t* msrc = &A->u.out.masks[0][0];
+                uint8_t* mdst = g.masks + (size_t)arena * 4 * RLGPU_ACTIONS;
+                for (int k = l; k < 4 * RLGPU_ACTIONS; k += kTeam) mdst[k] = msrc[k];
+            }
+            sync();
+        }
+    }
+    // ---- EnvSet::Reset / ResetArena / obs rebuild
+    if (g.reset_mode >= 2) {
+        bool do_reset = false;
+        if (valid) {
+            if (g.reset_mode == 2) do_reset = g.terminals[arena] != 0;
+            else if (g.reset_mode == 3) do_reset = g.reset_mask ? g.reset_mask[arena] != 0 : true;
+            else if (g.reset_mode == 4) do_reset = true;
+        }
+        sync();
+        if (do_reset && l == 0) {
+            kickoff_reset(A, g.seed, arena);
+            if (g.reset_mode == 2) g.terminals[arena] = 0;
+        }
+        sync();
+        bool rebuild = do_reset || (valid && g.reset_mode == 5);
+        if (rebuild && l < 4) build_obs_row(A, l);
+        sync();
+        if (rebuild) {
+            const float* src = &A->u.out.obs[0][0];
+            float* dst = g.obs + (size_t)arena * 4 * RLGPU_OBS;
+            for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
+            if (g.obs_out) {
+                float* d2 = g.obs_out + (size_t)arena * 4 * RLGPU_OBS;
+                for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) d2[k] = src[k];
+            }
+            const uint8_t* msrc = &A->u.out.masks[0][0];
+            uint8_t* mdst = g.masks + (size_t)arena * 4 * RLGPU_ACTIONS;
+            for (int k = l; k < 4 * RLGPU_ACTIONS; k += kTeam) mdst[k] = msrc[k];
+        }
+        sync();
+    }
+    // ---- write the records back
+    {
+        int first = blockIdx.x * kArenas;
+        int cnt = g.n - first < kArenas ? g.n - first : kArenas;
+        const int chunks = kRec / 16;
+        for (int k = threadIdx.x; k < cnt * chunks; k += 64) {
+            int a = k / chunks, c = k % chunks;
+            uint4* dst = (uint4*)(g.arenas + (size_t)(first + a) * kRec) + c;
+            const uint4* src = (const uint4*)&lds[a] + c;
+            *dst = *src;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host: constants
+static m3 host_euler_ypr(float yaw, float pitch, float roll) {  // btMatrix3x3::setEulerYPR
+    float ci = std::cos(roll), cj = std::cos(pitch), ch = std::cos(yaw);
+    float si = std::sin(roll), sj = std::sin(pitch), sh = std::sin(yaw);
+    float cc = ci * ch, cs = ci * sh, sc = si * ch, ss = si * sh;
+    return m3{v3{cj * ch, sj * sc - cs, sj * cc + ss}, v3{cj * sh, sj * ss + cc, sj * cs - sc}, v3{-sj, cj * si, cj * ci}};
+}
+
+static EnvConst make_env_const() {
+    EnvConst k;
+    std::memset(&k, 0, sizeof k);
+    const float UU = 1.f / 50.f;
+    k.ball_radius = 91.25f * UU;
+    float elem = 0.4f * kBallMass * k.ball_radius * k.ball_radius;  // btSphereShape::calculateLocalInertia
+    k.ball_inv_inertia = v3{1.f / elem, 1.f / elem, 1.f / elem};
+    k.ball_inv_mass = 1.f / kBallMass;
+    v3 hs = v3{120.507f, 86.6994f, 38.6591f} * UU;  // Octane hitbox (CarConfig.cpp:20-70)
+    v3 h = v3{hs.x / 2.f, hs.y / 2.f, hs.z / 2.f};
+    const float margin = 0.04f;
+    k.car_half = v3{(h.x - margin) + margin, (h.y - margin) + margin, (h.z - margin) + margin};
+    k.car_offset = v3{13.87566f, 0.f, 20.755f} * UU;
+    float lx = 2.f * k.car_half.x, ly = 2.f * k.car_half.y, lz = 2.f * k.car_half.z;
+    v3 inertia = v3{ly * ly + lz * lz, lx * lx + lz * lz, lx * lx + ly * ly} * (kCarMass / 12.f);
+    k.car_inv_inertia = v3{1.f / inertia.x, 1.f / inertia.y, 1.f / inertia.z};
+    k.car_inv_mass = 1.f / kCarMass;
+    for (int i = 0; i < 4; i++) {  // Car.cpp:231-277
+        bool front = i < 2, left = i % 2;
+        float radius = front ? 12.50f : 15.00f;
+        v3 off = front ? v3{51.25f, 25.90f, 20.755f} : v3{-33.75f, 29.50f, 20.755f};
+        if (left) off.y *= -1;
+        float rest = (front ? 38.755f : 37.055f) - 12.f;
+        k.wheel_conn[i] = off * UU;
+        k.wheel_rest[i] = rest * UU;
+        k.wheel_radius[i] = radius * UU;
+        k.wheel_force_scale[i] = front ? (36.f - (1.f / 4.f)) : (54.f + (1.f / 4.f) + (1.5f / 100.f));
+    }
+    k.susp_travel = ((12.f * UU) * 100.f) / 100.f;
+    k.ball_cbt = (float)((double)k.ball_radius + 0.08) * 0.02f;
+    {
+        v3 mn = k.car_offset - k.car_half, mx = k.car_offset + k.car_half;
+        v3 c = (mn + mx) * 0.5f;
+        float r = len(mx - mn) * 0.5f;
+        k.car_cbt = (r + len(c)) * 0.02f;
+    }
+    k.gravity = v3{0, 0, -650.f} * UU;
+    k.ball_damp = (float)std::pow((double)(1.f - 0.03f), (double)(1.f / 120.f));
+    k.plane_n[0] = v3{0, 0, 1};
+    k.plane_p[0] = v3{0, 0, 0};
+    k.plane_n[1] = v3{0, 0, -1};
+    k.plane_p[1] = v3{0, 0, 2048} * UU;
+    k.plane_n[2] = v3{1, 0, 0};
+    k.plane_p[2] = v3{-4096, 0, 2048 / 2} * UU;
+    k.plane_n[3] = v3{-1, 0, 0};
+    k.plane_p[3] = v3{4096, 0, 2048 / 2} * UU;
+    k.ntris = RLGPU_MESH_TRIS;
+    for (int t = 0; t < k.ntris; t++) {
+        for (int j = 0; j < 3; j++)
+            k.tri[t][j] = v3{RLGPU_MESH_UU[t][3 * j], RLGPU_MESH_UU[t][3 * j + 1], RLGPU_MESH_UU[t][3 * j + 2]} * UU;
+        v3 mn = k.tri[t][0], mx = k.tri[t][0];
+        for (int j = 1; j < 3; j++) {
+            mn = v3{std::min(mn.x, k.tri[t][j].x), std::min(mn.y, k.tri[t][j].y), std::min(mn.z, k.tri[t][j].z)};
+            mx = v3{std::max(mx.x, k.tri[t][j].x), std::max(mx.y, k.tri[t][j].y), std::max(mx.z, k.tri[t][j].z)};
+        }
+        k.tri_min[t] = mn;
+        k.tri_max[t] = mx;
+    }
+    const float sx[5] = {-2048, 2048, -256, 256, 0}, sy[5] = {-2560, -2560, -3840, -3840, -4608};
+    const float syaw[5] = {(float)(M_PI_4 * 1), (float)(M_PI_4 * 3), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2)};
+    for (int i = 0; i < 5; i++) {  // RLConst.h:297-303, orange mirrored (Arena.cpp:183-186)
+        k.kick_x[i] = sx[i];
+        k.kick_y[i] = sy[i];
+        k.kick_rot[0][i] = host_euler_ypr(syaw[i], -0.f, -0.f);
+        k.kick_rot[1][i] = host_euler_ypr(syaw[i] + (float)M_PI, -0.f, -0.f);
+    }
+    const float rx[4] = {-2304, -2688, 2304, 2688};
+    for (int i = 0; i < 4; i++) {  // RLConst.h:326-332
+        k.respawn_x[i] = rx[i];
+        k.respawn_y[i] = -4608;
+        k.respawn_rot[0][i] = host_euler_ypr((float)(M_PI / 2) + 0.f, 0.f, 0.f);
+        k.respawn_rot[1][i] = host_euler_ypr((float)(M_PI / 2) + (float)M_PI, 0.f, 0.f);
+    }
+    const float big[6][3] = {{-3584, 0, 73}, {3584, 0, 73}, {-3072, 4096, 73}, {3072, 4096, 73}, {-3072, -4096, 73}, {3072, -4096, 73}};
+    const float small[28][3] = {{0, -4240, 70},     {-1792, -4184, 70}, {1792, -4184, 70}, {-940, -3308, 70},  {940, -3308, 70},
+                                {0, -2816, 70},     {-3584, -2484, 70}, {3584, -2484, 70}, {-1788, -2300, 70}, {1788, -2300, 70},
+                                {-2048, -1036, 70}, {0, -1024, 70},     {2048, -1036, 70}, {-1024, 0, 70},     {1024, 0, 70},
+                                {-2048, 1036, 70},  {0, 1024, 70},      {2048, 1036, 70},  {-1788, 2300, 70},  {1788, 2300, 70},
+                                {-3584, 2484, 70},  {3584, 2484, 70},   {0, 2816, 70},     {-940, 3308, 70},   {940, 3308, 70},
+                                {-1792, 4184, 70},  {1792, 4184, 70},   {0, 4240, 70}};
+    for (int i = 0; i < RLGPU_PADS; i++) {  // RLConst.h:212-264 (big first, Arena.cpp:532-556)
+        const float* p = i < 6 ? big[i] : small[i - 6];
+        k.pad_pos_uu[i] = v3{p[0], p[1], p[2]};
+        k.pad_big[i] = i < 6;
+        k.pad_pos_bt[i] = k.pad_pos_uu[i] * UU;
+        float box_rad = (k.pad_big[i] ? 160.f : 120.f) * UU;
+        k.pad_box_min[i] = k.pad_pos_bt[i] - v3{box_rad, box_rad, 0};
+        k.pad_box_max[i] = k.pad_pos_bt[i] + v3{box_rad, box_rad, 64.f * UU};
+        k.pad_cell_x[i] = (int)(k.pad_pos_uu[i].x / 1024 + 4);
+        k.pad_cell_y[i] = (int)(k.pad_pos_uu[i].y / 1024 + 5);
+    }
+    const float loc[RLGPU_PADS][3] = {  // CommonValues::BOOST_LOCATIONS (CommonValues.h:47-82)
+        {0.f, -4240.0, 70.0},    {-1792.0, -4184.0, 70.0}, {1792.0, -4184.0, 70.0},  {-3072.0, -4096.0, 73.0}, {3072.0, -4096.0, 73.0},
+        {-940.0, -3308.0, 70.0}, {940.0, -3308.0, 70.0},   {0.0, -2816.0, 70.0},     {-3584.0, -2484.0, 70.0}, {3584.0, -2484.0, 70.0},
+        {-1788.0, -2300.0, 70.0}, {1788.0, -2300.0, 70.0}, {-2048.0, -1036.0, 70.0}, {0.0, -1024.0, 70.0},     {2048.0, -1036.0, 70.0},
+        {-3584.0, 0.0, 73.0},    {-1024.0, 0.0, 70.0},     {1024.0, 0.0, 70.0},      {3584.0, 0.0, 73.0},      {-2048.0, 1036.0, 70.0},
+        {0.0, 1024.0, 70.0},     {2048.0, 1036.0, 70.0},   {-1788.0, 2300.0, 70.0},  {1788.0, 2300.0, 70.0},   {-3584.0, 2484.0, 70.0},
+        {3584.0, 2484.0, 70.0},  {0.0, 2816.0, 70.0},      {-940.0, 3310.0, 70.0},   {940.0, 3308.0, 70.0},    {-3072.0, 4096.0, 73.0},
+        {3072.0, 4096.0, 73.0},  {-1792.0, 4184.0, 70.0},  {1792.0, 4184.0, 70.0},   {0.0, 4240.0, 70.0}};
+    for (int i = 0; i < RLGPU_PADS; i++) {
+        k.boost_loc[i] = v3{loc[i][0], loc[i][1], loc[i][2]};
+        k.pad_map[i] = -1;
+        for (int j = 0; j < RLGPU_PADS; j++) {
+            float dx = k.pad_pos_uu[j].x - loc[i][0], dy = k.pad_pos_uu[j].y - loc[i][1];
+            if (dx * dx + dy * dy < 10) {
+                k.pad_map[i] = j;
+                break;
+            }
+        }
+    }
+    {  // DefaultAction (DefaultAction.cpp:3-89)
+        const float RB[2] = {0, 1}, RF[3] = {-1, 0, 1};
+        int n = 0;
+        for (float th : RF)
+            for (float st : RF)
+                for (float bo : RB)
+                    for (float hb : RB) {
+                        if (bo == 1 && th != 1) continue;
+                        float v[8] = {th, st, 0, st, 0, 0, bo, hb};
+                        std::memcpy(k.action[n++], v, sizeof v);
+                    }
+        int ng = n;
+        for (float pi : RF)
+            for (float ya : RF)
+                for (float ro : RF)
+                    for (float ju : RB)
+                        for (float bo : RB) {
+                            if (ju == 1 && ya != 0) continue;
+                            if (pi == ro && ro == ju && ju == 0) continue;
+                            float hb = (ju == 1) && (pi != 0 || ya != 0 || ro != 0);
+                            float v[8] = {bo, ya, pi, ya, ro, ju, bo, hb};
+                            std::memcpy(k.action[n++], v, sizeof v);
+                        }
+        for (int i = 0; i < n; i++) {
+            const float* x = k.action[i];
+            k.mask_jump[i] = x[5] != 0;
+            k.mask_boost[i] = x[6] != 0;
+            k.mask_ground[i] = i < ng;
+            k.mask_air[i] = (i > ng && x[5] == 0);
+            if (i < ng && x[0] == x[6] && ((x[3] != 0) == (x[7] != 0))) k.mask_air[i] = 1;
+        }
+    }
+    const float W[RLGPU_REWARDS] = {0.25f, 0.12f, 5.f, 4.f, 60, 6.f, 8.0f, 0.1f, 0.010f, 20, 80, 150, 1.0f};
+    std::memcpy(k.reward_w, W, sizeof W);
+    return k;
+}
+
+}  // namespace rl
+
+// ------------------------------------------------------------------ C ABI
+struct rlgpu_envset {
+    rlgpu_envset_config cfg;
+    int num_players;
+    char* d_arenas = nullptr;
+    float *d_obs = nullptr, *d_rewards = nullptr, *d_last_rewards = nullptr, *d_trunc_obs = nullptr;
+    uint8_t *d_masks = nullptr, *d_terminals = nullptr;
+};
+
+namespace {
+bool g_const_ready = false;
+
+void ensure_const() {
+    if (g_const_ready) return;
+    rl::EnvConst k = rl::make_env_const();
+    RLGPU_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rl::C), &k, sizeof k));
+    g_const_ready = true;
+}
+
+void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
+    g.arenas = e->d_arenas;
+    g.n = e->cfg.num_arenas;
+    g.obs = e->d_obs;
+    g.masks = e->d_masks;
+    g.rewards = e->d_rewards;
+    g.terminals = e->d_terminals;
+    g.last_rewards = e->cfg.save_rewards ? e->d_last_rewards : nullptr;
+    g.trunc_obs = e->d_trunc_obs;
+    g.seed = e->cfg.seed;
+    unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
+    hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(64), 0, s, g);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+rl::StepArgs blank() {
+    rl::StepArgs g;
+    std::memset(&g, 0, sizeof g);
+    return g;
+}
+}  // namespace
+
+extern "C" int rlgpu_arena_state_size(void) { return (int)sizeof(rlgpu_arena_state); }
+
+extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset** out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(cfg && out, "rlgpu_envset_create: null argument");
+        RLGPU_REQUIRE(cfg->num_arenas > 0, "rlgpu_envset_create: num_arenas must be > 0");
+        RLGPU_REQUIRE(cfg->tick_skip > 0, "tickSkip must be > 0 (EnvSet.cpp:48)");
+        RLGPU_REQUIRE(cfg->action_delay >= 0 && cfg->action_delay <= cfg->tick_skip,
+                      "actionDelay must be in [0, tickSkip] (EnvSet.cpp:49)");
+        ensure_const();
+        auto* e = new rlgpu_envset();
+        e->cfg = *cfg;
+        int n = cfg->num_arenas;
+        e->num_players = 4 * n;
+        size_t P = (size_t)e->num_players;
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_arenas, (size_t)n * rl::kRec));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_obs, P * RLGPU_OBS * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_trunc_obs, P * RLGPU_OBS * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_rewards, P * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_last_rewards, (size_t)n * RLGPU_REWARDS * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_masks, P * RLGPU_ACTIONS));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_terminals, (size_t)n));
+        RLGPU_CHECK_HIP(hipMemset(e->d_terminals, 0, (size_t)n));
+        RLGPU_CHECK_HIP(hipMemset(e->d_rewards, 0, P * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMemset(e->d_trunc_obs, 0, P * RLGPU_OBS * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMemset(e->d_last_rewards, 0, (size_t)n * RLGPU_REWARDS * sizeof(float)));
+        // initial records: Arena ctor + AddCar defaults (Arena.cpp:429-562, Car.cpp:195-277)
+        std::vector<char> host((size_t)n * rl::kRec, 0);
+        rl::EnvConst k = rl::make_env_const();
+        for (int i = 0; i < n; i++) {
+            auto* s = (rlgpu_arena_state*)&host[(size_t)i * rl::kRec];
+            s->ball.rot[0] = s->ball.rot[4] = s->ball.rot[8] = 1.f;
+            s->ball.pos[2] = k.ball_radius;
+            for (int c = 0; c < 4; c++) {
+                rlgpu_car& cs = s->cars[c];
+                cs.body.rot[0] = cs.body.rot[4] = cs.body.rot[8] = 1.f;
+                cs.is_on_ground = 1;
+                cs.boost = 100.f / 3.f;
+                cs.ball_hit_tick = -1;
+                cs.ball_hit_extra_tick = -1;
+            }
+            for (int p = 0; p < RLGPU_PADS; p++) s->pads[p].is_active = 1;
+        }
+        RLGPU_CHECK_HIP(hipMemcpy(e->d_arenas, host.data(), host.size(), hipMemcpyHostToDevice));
+        *out = e;
+        // EnvSet ctor: reset every arena (EnvSet.cpp:105-110)
+        rl::StepArgs g = blank();
+        g.reset_mode = 4;
+        launch(e, g, nullptr);
+        RLGPU_CHECK_HIP(hipDeviceSynchronize());
+    });
+}
+
+extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
+    return rlgpu::guarded([&] {
+        if (!e) return;
+        (void)hipFree(e->d_arenas);
+        (void)hipFree(e->d_obs);
+        (void)hipFree(e->d_trunc_obs);
+        (void)hipFree(e->d_rewards);
+        (void)hipFree(e->d_last_rewards);
+        (void)hipFree(e->d_masks);
+        (void)hipFree(e->d_terminals);
+        delete e;
+    });
+}
+
+extern "C" int rlgpu_envset_buffers_get(rlgpu_envset* e, rlgpu_envset_buffers* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && out, "rlgpu_envset_buffers_get: null argument");
+        out->obs = e->d_obs;
+        out->action_masks = e->d_masks;
+        out->rewards = e->d_rewards;
+        out->terminals = e->d_terminals;
+        out->last_rewards = e->d_last_rewards;
+        out->trunc_obs = e->d_trunc_obs;
+        out->num_players = e->num_players;
+        out->num_arenas = e->cfg.num_arenas;
+    });
+}
+
+extern "C" int rlgpu_envset_reset(rlgpu_envset* e, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        rl::StepArgs g = blank();
+        g.reset_mode = 2;
+        launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_reset_arenas(rlgpu_envset* e, const uint8_t* d_mask, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        rl::StepArgs g = blank();
+        g.reset_mode = 3;
+        g.reset_mask = d_mask;
+        launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_step_first_half(rlgpu_envset* e, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        rl::StepArgs g = blank();
+        g.ticks_first = e->cfg.action_delay;
+        if (g.ticks_first == 0) {  // still snapshot prev state / clear events
+            g.ticks_first = 0;
+        }
+        launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_step_second_half(rlgpu_envset* e, const int32_t* d_actions, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && d_actions, "rlgpu_envset_step_second_half: null argument");
+        rl::StepArgs g = blank();
+        g.actions = d_actions;
+        g.ticks_second = e->cfg.tick_skip - e->cfg.action_delay;
+        g.build = 1;
+        launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_step(rlgpu_envset* e, const int32_t* d_actions, int32_t reset_terminated, float* d_obs_out,
+                                 float* d_rew_out, uint8_t* d_term_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && d_actions, "rlgpu_envset_step: null argument");
+        RLGPU_REQUIRE(e->cfg.action_delay > 0, "fused step needs actionDelay > 0");
+        rl::StepArgs g = blank();
+        g.ticks_first = e->cfg.action_delay;
+        g.actions = d_actions;
+        g.ticks_second = e->cfg.tick_skip - e->cfg.action_delay;
+        g.build = 1;
+        g.reset_mode = reset_terminated ? 1 : 0;
+        g.obs_out = d_obs_out;
+        g.rew_out = d_rew_out;
+        g.term_out = d_term_out;
+        launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_sync(rlgpu_envset* e, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        RLGPU_CHECK_HIP(hipStreamSynchronize(rlgpu::as_stream(stream)));
+    });
+}
+
+extern "C" int rlgpu_envset_build_obs(rlgpu_envset* e, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        rl::StepArgs g = blank();
+        g.reset_mode = 5;
+        launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_get_arenas(rlgpu_envset* e, int32_t first, int32_t count, rlgpu_arena_state* h_out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && h_out, "null argument");
+        RLGPU_REQUIRE(first >= 0 && count >= 0 && first + count <= e->cfg.num_arenas, "arena range out of bounds");
+        if (count == 0) return;
+        RLGPU_CHECK_HIP(hipDeviceSynchronize());
+        RLGPU_CHECK_HIP(hipMemcpy2D(h_out, sizeof(rlgpu_arena_state), e->d_arenas + (size_t)first * rl::kRec, rl::kRec,
+                                    sizeof(rlgpu_arena_state), count, hipMemcpyDeviceToHost));
+    });
+}
+
+extern "C" int rlgpu_envset_set_arenas(rlgpu_envset* e, int32_t first, int32_t count, const rlgpu_arena_state* h_in) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && h_in, "null argument");
+        RLGPU_REQUIRE(first >= 0 && count >= 0 && first + count <= e->cfg.num_arenas, "arena range out of bounds");
+        if (count == 0) return;
+        RLGPU_CHECK_HIP(hipDeviceSynchronize());
+        RLGPU_CHECK_HIP(hipMemcpy2D(e->d_arenas + (size_t)first * rl::kRec, rl::kRec, h_in, sizeof(rlgpu_arena_state),
+                                    sizeof(rlgpu_arena_state), count, hipMemcpyHostToDevice));
+    });
+}

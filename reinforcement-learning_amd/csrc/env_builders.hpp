@@ -1,0 +1,346 @@
+// env_builders.hpp -- the RLGymCPP layer of the env kernel: GameState snapshot, terminal
+// conditions, the ExampleMain reward list, AdvancedObs and DefaultAction masks, kickoff reset.
+#pragma once
+#include "env_contacts.hpp"
+
+namespace rl {
+
+struct PView {
+    v3 pos, vel, ang, fwd, right, up;
+    float boost;
+    bool on_ground, hfj, demoed, has_jumped, is_flipping, orange, world_contact;
+    float wc_z;
+};
+
+DEV PView view_player(ArenaLDS* A, int i) {
+    const rlgpu_car& c = A->s.cars[i];
+    PView p;
+    p.pos = ld3(c.body.pos) * kBT2UU;
+    p.vel = ld3(c.body.vel) * kBT2UU;
+    p.ang = ld3(c.body.angvel);
+    const float* r = c.body.rot;
+    p.fwd = v3{r[0], r[3], r[6]};
+    p.right = v3{r[1], r[4], r[7]};
+    p.up = v3{r[2], r[5], r[8]};
+    p.boost = c.boost;
+    p.on_ground = c.is_on_ground;
+    p.hfj = c.is_on_ground || (!c.has_flipped && !c.has_double_jumped && c.air_time_since_jump < 1.25f);  // Car.cpp:279-283
+    p.demoed = c.is_demoed;
+    p.has_jumped = c.has_jumped;
+    p.is_flipping = c.is_flipping;
+    p.orange = i & 1;
+    p.world_contact = c.world_contact;
+    p.wc_z = c.world_contact_normal[2];
+    return p;
+}
+
+DEV v3 inv_if(v3 v, bool inv) { return inv ? v3{-v.x, -v.y, v.z} : v; }
+
+// AdvancedObs::AddPlayerToObsFast (AdvancedObs.cpp:108-172)
+DEV void add_player_obs(float* o, const PView& pl, bool inv, v3 bp, v3 bv) {
+    const float POS = 1.0f / 2300.0f, VEL = 1.0f / 2300.0f, ANG = 1.0f / 5.5f, BOOST = 0.01f;
+    v3 pos = inv_if(pl.pos, inv), vel = inv_if(pl.vel, inv), ang = inv_if(pl.ang, inv);
+    v3 f = inv_if(pl.fwd, inv), r = inv_if(pl.right, inv), u = inv_if(pl.up, inv);
+    o[0] = pos.x * POS; o[1] = pos.y * POS; o[2] = pos.z * POS;
+    o[3] = f.x; o[4] = f.y; o[5] = f.z;
+    o[6] = u.x; o[7] = u.y; o[8] = u.z;
+    o[9] = vel.x * VEL; o[10] = vel.y * VEL; o[11] = vel.z * VEL;
+    o[12] = ang.x * ANG; o[13] = ang.y * ANG; o[14] = ang.z * ANG;
+    o[15] = (f.x * ang.x + f.y * ang.y + f.z * ang.z) * ANG;
+    o[16] = (r.x * ang.x + r.y * ang.y + r.z * ang.z) * ANG;
+    o[17] = (u.x * ang.x + u.y * ang.y + u.z * ang.z) * ANG;
+    float rx = bp.x - pos.x, ry = bp.y - pos.y, rz = bp.z - pos.z;
+    o[18] = (f.x * rx + f.y * ry + f.z * rz) * POS;
+    o[19] = (r.x * rx + r.y * ry + r.z * rz) * POS;
+    o[20] = (u.x * rx + u.y * ry + u.z * rz) * POS;
+    float vx = bv.x - vel.x, vy = bv.y - vel.y, vz = bv.z - vel.z;
+    o[21] = (f.x * vx + f.y * vy + f.z * vz) * VEL;
+    o[22] = (r.x * vx + r.y * vy + r.z * vz) * VEL;
+    o[23] = (u.x * vx + u.y * vy + u.z * vz) * VEL;
+    o[24] = pl.boost * BOOST;
+    o[25] = pl.on_ground ? 1.0f : 0.0f;
+    o[26] = pl.hfj ? 1.0f : 0.0f;
+    o[27] = pl.demoed ? 1.0f : 0.0f;
+    o[28] = pl.has_jumped ? 1.0f : 0.0f;
+}
+
+// AdvancedObs::BuildObs + DefaultAction::GetActionMask for player pi, into LDS rows
+DEV void build_obs_row(ArenaLDS* A, int pi) {
+    PView P[4];
+    for (int i = 0; i < 4; i++) P[i] = view_player(A, i);
+    float* o = A->u.out.obs[pi];
+    bool inv = P[pi].orange;
+    v3 bp = inv_if(ld3(A->s.ball.pos) * kBT2UU, inv), bv = inv_if(ld3(A->s.ball.vel) * kBT2UU, inv),
+       ba = inv_if(ld3(A->s.ball.angvel), inv);
+    const float BPOS = 1 / 5000.f, BVEL = 1 / 2300.f, BANG = 1 / 3.f;  // AdvancedObs.h:10-13
+    o[0] = bp.x * BPOS; o[1] = bp.y * BPOS; o[2] = bp.z * BPOS;
+    o[3] = bv.x * BVEL; o[4] = bv.y * BVEL; o[5] = bv.z * BVEL;
+    o[6] = ba.x * BANG; o[7] = ba.y * BANG; o[8] = ba.z * BANG;
+    for (int k = 0; k < 8; k++) o[9 + k] = A->s.env.prev_action[pi][k];
+    for (int k = 0; k < RLGPU_PADS; k++) {
+        int act_idx = inv ? C.pad_map[RLGPU_PADS - k - 1] : C.pad_map[k];
+        int tim_idx = inv ? C.pad_map[k] : C.pad_map[RLGPU_PADS - k - 1];  // GameState.h:60 quirk
+        bool active = A->s.pads[act_idx].is_active;
+        float timer = A->s.pads[tim_idx].cooldown;
+        o[17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
+    }
+    float* q = o + 51;
+    add_player_obs(q, P[pi], inv, bp, bv);
+    q += 29;
+    for (int j = 0; j < 4; j++)
+        if (j != pi && P[j].orange == P[pi].orange) {
+            add_player_obs(q, P[j], inv, bp, bv);
+            q += 29;
+        }
+    for (int j = 0; j < 4; j++)
+        if (P[j].orange != P[pi].orange) {
+            add_player_obs(q, P[j], inv, bp, bv);
+            q += 29;
+        }
+    uint8_t* m = A->u.out.masks[pi];
+    bool turtled = P[pi].world_contact && P[pi].wc_z > 0.9f;
+    for (int k = 0; k < RLGPU_ACTIONS; k++) {
+        uint8_t r = P[pi].on_ground ? C.mask_ground[k] : C.mask_air[k];
+        if (P[pi].boost == 0) r &= (uint8_t)~C.mask_boost[k];
+        if (P[pi].hfj || turtled) r |= C.mask_jump[k];
+        m[k] = r & 1;
+    }
+}
+
+// KickoffProximityReward2v2Enhanced (KickoffProximityReward2v2Enhanced.h:14-366)
+DEV float kickoff_reward(int pi, const PView* P, v3 bpos, v3 bvel) {
+    float bspeed = rs_len(bvel);
+    v3 b2 = v3{bpos.x, bpos.y, 0.f};
+    if (!(bspeed < 2.f && bpos.z < 150.f && rs_len(b2) < 50.f)) return 0.f;
+    const PView& pl = P[pi];
+    bool has_tm = false;
+    int tm_i = -1;
+    float tm_dist = 0, closest = 3.402823466e+38f, second = 3.402823466e+38f;
+    v3 opp_com = zero3();
+    int nopp = 0;
+    float tot_speed = 0;
+    for (int j = 0; j < 4; j++) {
+        const PView& p = P[j];
+        if (p.orange == pl.orange && j != pi) {
+            tm_i = j;
+            has_tm = true;
+            tm_dist = rs_len(p.pos - bpos);
+        } else if (p.orange != pl.orange) {
+            float d = rs_len(p.pos - bpos);
+            tot_speed += rs_len(p.vel);
+            nopp++;
+            if (d < closest) {
+                second = closest;
+                closest = d;
+            } else if (d < second) {
+                second = d;
+            }
+            opp_com = opp_com + p.pos;
+        }
+    }
+    if (nopp > 0) opp_com = rs_div(opp_com, (float)nopp);
+    if (!has_tm) return 0.f;
+    const PView& tm = P[tm_i];
+    float pdist = rs_len(pl.pos - bpos);
+    float dscore = (pdist < tm_dist) ? 0.4f : 0.f;
+    v3 p2b = rs_norm(bpos - pl.pos), t2b = rs_norm(bpos - tm.pos);
+    float pvb = dot(pl.vel, p2b), tvb = dot(tm.vel, t2b);
+    float sscore = (pvb > tvb) ? 0.3f : 0.f;
+    float bscore = (pl.boost > tm.boost + 10.f) ? 0.2f : 0.f;
+    float pa = rs_atan2f(pl.pos.y - bpos.y, pl.pos.x - bpos.x);
+    float ta = rs_atan2f(tm.pos.y - bpos.y, tm.pos.x - bpos.x);
+    float adiff = fabsf(pa - ta);
+    float spawn = (adiff > (3.14159f / 3.f)) ? 1.f : 0.f;
+    float total = dscore + sscore + bscore + spawn * 0.1f;
+    if (total >= 0.5f) {
+        float base = (pdist < closest) ? 1.2f : -1.2f * 0.5f;
+        v3 to_b = rs_norm(bpos - pl.pos);
+        float pvel = dot(pl.vel, to_b);
+        float speed_bonus = clampf(pvel / 2300.f, -0.3f, 0.3f);
+        float eff = 0.f;
+        if (pl.boost > 50.f && pdist > 1000.f) eff = 0.1f;
+        else if (pl.boost < 20.f && pdist > 800.f) eff = -0.15f;
+        v3 vn = rs_norm(pl.vel);
+        float approach = dot(to_b, vn);
+        float angle_bonus = stdmax(0.f, approach) * 0.2f;
+        return clampf(base + speed_bonus + eff + angle_bonus, -1.5f, 1.5f);
+    }
+    v3 own = !pl.orange ? v3{0, -6000, 642.775f / 2} : v3{0, 6000, 642.775f / 2};
+    v3 center = v3{0.f, 0.f, 100.f};
+    v3 cm = v3{center.x * 1.3f, center.y * 1.3f, center.z * 1.3f};
+    v3 base_ideal = (own + cm) * 0.5f;
+    v3 threat = rs_norm(opp_com - own);
+    threat = v3{threat.x * 200.f, threat.y * 200.f, threat.z * 200.f};
+    v3 tm_off = zero3();
+    {
+        float tdc = rs_len(tm.pos - center);
+        if (tdc > 1500.f) {
+            v3 dir = rs_norm(tm.pos - base_ideal);
+            tm_off = v3{dir.x * 300.f, dir.y * 300.f, dir.z * 300.f};
+        }
+    }
+    v3 thr_adj = v3{threat.x * 0.3f, threat.y * 0.3f, threat.z * 0.3f};
+    v3 tm_adj = v3{tm_off.x * 0.2f, tm_off.y * 0.2f, tm_off.z * 0.2f};
+    v3 ideal = base_ideal + thr_adj + tm_adj;
+    ideal.x = clampf(ideal.x, -3000.f, 3000.f);
+    ideal.y = clampf(ideal.y, -4000.f, 4000.f);
+    ideal.z = stdmax(ideal.z, 17.f);
+    float dti = rs_len(pl.pos - ideal);
+    float posr;
+    if (dti <= 600.f) posr = 0.5f * (1.f - (dti / 600.f));
+    else if (dti <= 1200.f) posr = 0.5f * (1.f - (dti - 600.f) / (1200.f - 600.f)) * 0.7f;
+    else if (dti <= 2000.f) posr = -0.1f * ((dti - 1200.f) / (2000.f - 1200.f));
+    else posr = -0.3f;
+    float best = 0.f;
+    for (int i = 0; i < RLGPU_PADS; i++) {
+        v3 bl = C.boost_loc[i];
+        if (bl.z > 72.0f) {
+            float dtb = rs_len(pl.pos - bl);
+            float acc = 1.f - clampf(dtb / 1500.f, 0.f, 1.f);
+            float d2b = rs_len(bl - bpos);
+            bool corner = (fabsf(bl.x) > 2500.f && fabsf(bl.y) > 3500.f);
+            float bvv = corner ? 0.8f : 0.6f;
+            float prox = 1.f - clampf(d2b / 3000.f, 0.f, 1.f);
+            float strat = bvv * (0.3f + prox * 0.7f);
+            float od = rs_len(opp_com - bl);
+            float deny = clampf(1.f - (od / 2000.f), 0.f, 0.3f);
+            float tv = acc * (strat + deny);
+            best = stdmax(best, tv);
+        }
+    }
+    float blf = 1.f;
+    if (pl.boost < 30.f) blf = 1.5f;
+    else if (pl.boost > 80.f) blf = 0.5f;
+    float boostr = best * blf * 0.25f;
+    float rot;
+    {
+        v3 t2g = rs_norm(own - tm.pos);
+        v3 perp = rs_norm(v3{-t2g.y, t2g.x, 0.f});
+        v3 goff = v3{t2g.x * 800.f, t2g.y * 800.f, t2g.z * 800.f};
+        v3 poff = v3{perp.x * 600.f, perp.y * 600.f, perp.z * 600.f};
+        v3 sup = tm.pos + goff + poff;
+        float dts = rs_len(pl.pos - sup);
+        float ready = 1.f - clampf(dts / 1000.f, 0.f, 1.f);
+        v3 tos = rs_norm(sup - pl.pos);
+        float align = stdmax(0.f, dot(rs_norm(pl.vel), tos));
+        rot = (ready * 0.7f + align * 0.3f) * 0.2f;
+    }
+    float aware;
+    {
+        v3 toc = rs_norm(opp_com - pl.pos);
+        v3 tob = rs_norm(bpos - pl.pos);
+        float aa = dot(toc, tob);
+        aware = clampf(aa * 0.5f + 0.5f, 0.f, 1.f) * 0.1f;
+    }
+    float camp;
+    {
+        float dtg = rs_len(pl.pos - own);
+        float mind = 800.f;
+        float bdg = rs_len(bpos - own);
+        if (bdg < 2000.f) mind *= 0.7f;
+        camp = 0.f;
+        if (dtg < mind) camp = -0.4f * (1.f - (dtg / mind));
+        camp *= 0.05f;
+    }
+    float tot = posr + boostr + rot + aware + camp;
+    return clampf(tot, -0.8f, 0.8f);
+}
+
+// one reward of the ExampleMain list for player i (src/ExampleMain.cpp:132-177)
+DEV float reward_value(ArenaLDS* A, int r, int i, const PView* P, v3 bpos, v3 bvel, v3 prev_bvel, bool goal) {
+    const PView& pl = P[i];
+    const rlgpu_env_extra& e = A->s.env;
+    const float KPH = 250.f / 9.f;
+    bool touched = A->a.touched[i] != 0;
+    switch (r) {
+        case 0: return !pl.on_ground;
+        case 1: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1.f : 0.f;
+        case 2: return kickoff_reward(i, P, bpos, bvel);
+        case 3: {
+            v3 dir = rs_norm(bpos - pl.pos);
+            v3 nv = rs_div(pl.vel, 2300.f);
+            return dot(dir, nv);
+        }
+        case 4: {
+            float minv = 20 * KPH, maxv = 120 * KPH;
+            if (!touched) return 0.f;
+            float hit = rs_len(bvel - prev_bvel);
+            return hit < minv ? 0.f : stdmin(1.f, hit / maxv);
+        }
+        case 5: {
+            const float MAXS = 110 * KPH;
+            if (!touched) return 0.f;
+            float pf = stdmin(1.f, rs_len(prev_bvel) / MAXS);
+            float cf = stdmin(1.f, rs_len(bvel) / MAXS);
+            return cf > pf ? (cf - pf) : 0.f;
+        }
+        case 6: {
+            v3 tgt = !pl.orange ? v3{0, 6000, 642.775f / 2} : v3{0, -6000, 642.775f / 2};
+            v3 d = rs_norm(tgt - bpos);
+            return dot(d, rs_div(bvel, 6000.f));
+        }
+        case 7: return pl.boost > e.prev_boost[i] ? sqrtf(pl.boost / 100.f) - sqrtf(e.prev_boost[i] / 100.f) : 0.f;
+        case 8: {
+            float x = sqrtf(pl.boost / 100);
+            return stdmin(stdmax(x, 0.f), 1.f);
+        }
+        case 9: return e.ev_bump[i];
+        case 10: return e.ev_demo[i];
+        case 11: {
+            if (!goal) return 0.f;
+            bool team_from_y_orange = !(bpos.y < 0);
+            return (pl.orange != team_from_y_orange) ? 1.f : -1.f;
+        }
+        case 12: {
+            int own = pl.orange ? e.penalty_orange : e.penalty_blue;
+            int opp = pl.orange ? e.penalty_blue : e.penalty_orange;
+            int deficit = opp - own;
+            return deficit > 0 ? -0.02f * (float)deficit : 0.f;
+        }
+    }
+    return 0.f;
+}
+
+// Arena::ResetToRandomKickoff (Arena.cpp:112-216) + EnvSet::ResetArena state (EnvSet.cpp:275-304), one lane
+DEV void kickoff_reset(ArenaLDS* A, uint64_t seed, int arena) {
+    int order[5] = {0, 1, 2, 3, 4};
+    for (int i = 4; i > 0; i--) {
+        int j = (int)(rng_next(A, seed, arena) % (uint32_t)(i + 1));
+        int t = order[i];
+        order[i] = order[j];
+        order[j] = t;
+    }
+    for (int i = 0; i < 2; i++) {
+        int k = order[i];
+        for (int team = 0; team < 2; team++) {
+            int ci = 2 * i + team;
+            v3 pos = v3{C.kick_x[k], C.kick_y[k], 17.f};
+            if (team == 1) pos = pos * v3{-1, -1, 1};
+            set_car_state(A, ci, pos, C.kick_rot[team][k], 100.f / 3.f, true);
+        }
+    }
+    st3(A->s.ball.pos, v3{0, 0, 93.15f} * kUU2BT);
+    stm(A->s.ball.rot, ident3());
+    st3(A->s.ball.vel, zero3());
+    st3(A->s.ball.angvel, zero3());
+    st3(A->s.ball_vel_impulse_cache, zero3());
+    for (int p = 0; p < RLGPU_PADS; p++) {
+        A->s.pads[p].is_active = 1;
+        A->s.pads[p].cooldown = 0;
+        A->s.pads[p].prev_locked_car_id = 0;
+    }
+    for (int m = 0; m < RLGPU_MANIFOLDS; m++) A->s.manifolds[m].count = 0;
+    rlgpu_env_extra& e = A->s.env;
+    e.last_tick_count = e.tick_count;
+    e.no_touch_time = 0;
+    e.score_blue = e.score_orange = 0;
+    e.penalty_blue = e.penalty_orange = 0;
+    e.has_prev = 0;
+    e.terminal = 0;
+    for (int p = 0; p < 4; p++) {
+        for (int k = 0; k < 8; k++) e.prev_action[p][k] = 0.f;
+        e.ev_bump[p] = e.ev_bumped[p] = e.ev_demo[p] = e.ev_demoed[p] = 0;
+    }
+}
+
+}  // namespace rl

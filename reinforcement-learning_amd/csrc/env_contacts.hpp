@@ -1,0 +1,936 @@
+// env_contacts.hpp -- persistent manifolds, narrowphase, contact callbacks and the
+// sequential-impulse solver of the env kernel.  Reference map in env_kernel.hpp; each
+// function cites the Bullet / RocketSim code it restates.
+#pragma once
+#include "env_device.hpp"
+
+namespace rl {
+
+// canonical pair order: rank 0..24 = body*5 + static, rank 25..34 = dynamic pairs
+DEV int pair_key(int rank) {
+    if (rank < 25) return (rank / 5) * 8 + (rank % 5);
+    const int keys[10] = {65, 66, 67, 68, 74, 75, 76, 83, 84, 92};
+    return keys[rank - 25];
+}
+DEV void key_bodies(int key, int& a, int& b) {
+    if (key >= 64) {
+        a = (key - 64) / 8;
+        b = (key - 64) % 8;
+    } else {
+        a = key / 8;
+        b = 10 + key % 8;
+    }
+}
+DEV void side_transform(ArenaLDS* A, int id, v3& p, m3& r) {
+    if (id >= 10) {
+        p = zero3();
+        r = ident3();
+    } else {
+        p = bpos(A, id);
+        r = brot(A, id);
+    }
+}
+DEV float pair_cbt(int a, int b) {
+    float ta = a == 0 ? C.ball_cbt : C.car_cbt;
+    if (b >= 10) return ta;
+    float tb = b == 0 ? C.ball_cbt : C.car_cbt;
+    return stdmin(ta, tb);
+}
+
+DEV rlgpu_manifold* find_manifold(ArenaLDS* A, int key) {
+    for (int m = 0; m < RLGPU_MANIFOLDS; m++)
+        if (A->s.manifolds[m].count > 0 && A->s.manifolds[m].key == key) return &A->s.manifolds[m];
+    return nullptr;
+}
+DEV rlgpu_manifold* get_or_new_manifold(ArenaLDS* A, int key) {
+    rlgpu_manifold* m = find_manifold(A, key);
+    if (m) return m;
+    for (int k = 0; k < RLGPU_MANIFOLDS; k++)
+        if (A->s.manifolds[k].count == 0) {
+            A->s.manifolds[k].key = key;
+            return &A->s.manifolds[k];
+        }
+    return nullptr;
+}
+DEV void clear_manifolds_of(ArenaLDS* A, int bodyi) {
+    for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
+        rlgpu_manifold& mf = A->s.manifolds[m];
+        if (mf.count == 0) continue;
+        int a, b;
+        key_bodies(mf.key, a, b);
+        if (a == bodyi || b == bodyi) mf.count = 0;
+    }
+}
+
+// btPersistentManifold::sortCachedPoints (btPersistentManifold.cpp:110-198)
+DEV int sort_cached(const rlgpu_manifold& m, const rlgpu_contact& pt) {
+    int max_idx = -1;
+    float max_pen = pt.dist;
+    for (int i = 0; i < 4; i++)
+        if (m.pts[i].dist < max_pen) {
+            max_idx = i;
+            max_pen = m.pts[i].dist;
+        }
+    float res[4] = {0, 0, 0, 0};
+    v3 p = ld3(pt.localA);
+    v3 l0 = ld3(m.pts[0].localA), l1 = ld3(m.pts[1].localA), l2 = ld3(m.pts[2].localA), l3 = ld3(m.pts[3].localA);
+    if (max_idx != 0) res[0] = len2(cross(p - l1, l3 - l2));
+    if (max_idx != 1) res[1] = len2(cross(p - l0, l3 - l2));
+    if (max_idx != 2) res[2] = len2(cross(p - l0, l3 - l1));
+    if (max_idx != 3) res[3] = len2(cross(p - l0, l2 - l1));
+    int best = -1;
+    float mx = -1e30f;
+    for (int i = 0; i < 4; i++) {
+        float v = fabsf(res[i]);
+        if (v > mx) {
+            best = i;
+            mx = v;
+        }
+    }
+    return best;
+}
+
+// Arena::_BtCallback_OnCarBallCollision (Arena.cpp:283-333)
+DEV void car_ball_hit(ArenaLDS* A, int ci, rlgpu_contact& cp) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    cp.friction = 2.0f;
+    cp.restitution = 0.0f;
+    v3 ball_pos = bpos(A, 0) * kBT2UU, car_pos = bpos(A, bi) * kBT2UU;
+    v3 ball_vel = bvel(A, 0) * kBT2UU, car_vel = bvel(A, bi) * kBT2UU;
+    cs.ball_hit_valid = 1;
+    st3(cs.ball_hit_rel_pos, ld3(cp.localB) * kBT2UU);
+    cs.ball_hit_tick = A->s.env.tick_count;
+    st3(cs.ball_hit_ball_pos, ball_pos);
+    st3(cs.ball_hit_extra_vel, zero3());
+    int64_t tick = A->s.env.tick_count;
+    uint64_t uex = (uint64_t)cs.ball_hit_extra_tick, ut = (uint64_t)tick;
+    if ((ut > uex + 1) || (uex > ut)) {
+        cs.ball_hit_extra_tick = tick;
+    } else {
+        return;
+    }
+    v3 fwd = col(brot(A, bi), 0);
+    v3 rel_pos = ball_pos - car_pos;
+    v3 rel_vel = ball_vel - car_vel;
+    float rel_speed = stdmin(len(rel_vel), 4600.f);
+    if (rel_speed > 0) {
+        v3 hit_dir = safe_normalized(rel_pos * v3{1, 1, 0.35f});
+        v3 adj = fwd * dot(hit_dir, fwd) * (1 - 0.65f);
+        hit_dir = safe_normalized(hit_dir - adj);
+        v3 added = (hit_dir * rel_speed) * curve_out(kBallCarExtra, rel_speed) * 1.f;
+        st3(cs.ball_hit_extra_vel, added);
+        st3(A->s.ball_vel_impulse_cache, ld3(A->s.ball_vel_impulse_cache) + added * kUU2BT);
+    }
+}
+
+// Arena::_BtCallback_OnCarCarCollision (Arena.cpp:335-415) + EnvSet _BumpCallback (EnvSet.cpp:31-42)
+DEV void car_car_hit(ArenaLDS* A, int c1, int c2, rlgpu_contact& cp) {
+    cp.friction = 0.09f;
+    cp.restitution = 0.1f;
+    for (int i = 0; i < 2; i++) {
+        bool swapped = i == 1;
+        int a = swapped ? c2 : c1, o = swapped ? c1 : c2;
+        rlgpu_car& sa = A->s.cars[a];
+        rlgpu_car& so = A->s.cars[o];
+        if (sa.is_demoed || so.is_demoed) return;
+        if (sa.car_contact_other_id == (uint32_t)(o + 1) && sa.car_contact_cooldown > 0) continue;
+        v3 pa = bpos(A, a + 1) * kBT2UU, po = bpos(A, o + 1) * kBT2UU;
+        v3 va = bvel(A, a + 1) * kBT2UU, vo = bvel(A, o + 1) * kBT2UU;
+        v3 delta = po - pa;
+        if (dot(va, delta) > 0) {
+            v3 vel_dir = rs_norm(va);
+            v3 dir_to = rs_norm(delta);
+            float speed_towards = dot(va, dir_to);
+            float other_away = dot(vo, vel_dir);
+            if (speed_towards > other_away) {
+                v3 lp = swapped ? ld3(cp.localB) : ld3(cp.localA);
+                bool bumper = (lp.x * kBT2UU) > 64.5f;
+                if (bumper) {
+                    bool demo = sa.is_supersonic;
+                    if (demo) demo = (a & 1) != (o & 1);
+                    if (demo) {
+                        so.is_demoed = 1;
+                        so.demo_respawn_timer = 3.f;
+                    } else {
+                        bool ground = so.is_on_ground;
+                        float base = curve_out(ground ? kBumpGround : kBumpAir, speed_towards);
+                        v3 up = so.is_on_ground ? col(brot(A, o + 1), 2) : v3{0, 0, 1};
+                        v3 imp = vel_dir * base + up * curve_out(kBumpUp, speed_towards) * 1.f;
+                        st3(so.vel_impulse_cache, ld3(so.vel_impulse_cache) + imp * kUU2BT);
+                    }
+                    sa.car_contact_other_id = (uint32_t)(o + 1);
+                    sa.car_contact_cooldown = 0.25f;
+                    if ((a & 1) != (o & 1)) {
+                        A->s.env.ev_bump[a] = 1;
+                        A->s.env.ev_bumped[o] = 1;
+                        if (demo) {
+                            A->s.env.ev_demo[a] = 1;
+                            A->s.env.ev_demoed[o] = 1;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+DEV void contact_callback(ArenaLDS* A, int a, int b, rlgpu_contact& cp) {
+    if (a >= 1 && a <= 4) {
+        int ci = a - 1;
+        if (b == 0) {
+            car_ball_hit(A, ci, cp);
+        } else if (b >= 1 && b <= 4) {
+            car_car_hit(A, ci, b - 1, cp);
+        } else {  // car-world (Arena.cpp:417-427)
+            rlgpu_car& cs = A->s.cars[ci];
+            cs.world_contact = 1;
+            cs.world_contact_normal[0] = cp.normalB[0];
+            cs.world_contact_normal[1] = cp.normalB[1];
+            cs.world_contact_normal[2] = cp.normalB[2];
+            cp.friction = 0.3f;
+            cp.restitution = 0.3f;
+        }
+    } else if (a == 0 && b >= 10) {
+        cp.special = 1;  // Arena.cpp:265-273
+    }
+}
+
+// btManifoldResult::addContactPoint (btManifoldResult.cpp:110-200)
+DEV void add_contact(ArenaLDS* A, int key, v3 normal_b, v3 point_b, float depth) {
+    int a, b;
+    key_bodies(key, a, b);
+    float cbt = pair_cbt(a, b);
+    if (depth > cbt) return;
+    rlgpu_manifold* m = get_or_new_manifold(A, key);
+    if (!m) {
+        A->s.env.manifold_overflow++;
+        return;
+    }
+    v3 pa = point_b + normal_b * depth;
+    v3 ta_p, tb_p;
+    m3 ta_r, tb_r;
+    side_transform(A, a, ta_p, ta_r);
+    side_transform(A, b, tb_p, tb_r);
+    rlgpu_contact c;
+    st3(c.localA, vmul(pa - ta_p, ta_r));
+    st3(c.localB, vmul(point_b - tb_p, tb_r));
+    st3(c.normalB, normal_b);
+    c.dist = depth;
+    c.applied = 0.f;
+    bool stat = b >= 10;
+    float fa = a == 0 ? 0.35f : 0.3f, ra = a == 0 ? 0.6f : 0.1f;
+    float fb = stat ? 0.6f : (b == 0 ? 0.35f : 0.3f), rb = stat ? 0.3f : (b == 0 ? 0.6f : 0.1f);
+    c.friction = stat ? stdmin(fa, fb) : fa * fb;
+    c.restitution = stat ? stdmax(ra, rb) : ra * rb;
+    c.special = 0;
+    int idx;
+    if (m->count == 4) {
+        idx = sort_cached(*m, c);
+    } else {
+        idx = m->count;
+        m->count++;
+    }
+    if (idx < 0) idx = 0;
+    m->pts[idx] = c;
+    contact_callback(A, a, b, m->pts[idx]);
+}
+
+// btPersistentManifold::refreshContactPoints (btPersistentManifold.cpp:265-330)
+DEV void refresh(ArenaLDS* A, int key) {
+    rlgpu_manifold* m = find_manifold(A, key);
+    if (!m) return;
+    int a, b;
+    key_bodies(key, a, b);
+    float cbt = pair_cbt(a, b);
+    v3 pa_, pb_;
+    m3 ra, rb;
+    side_transform(A, a, pa_, ra);
+    side_transform(A, b, pb_, rb);
+    v3 wa[4], wb[4];
+    for (int i = m->count - 1; i >= 0; i--) {
+        rlgpu_contact& p = m->pts[i];
+        wa[i] = ra * ld3(p.localA) + pa_;
+        wb[i] = rb * ld3(p.localB) + pb_;
+        p.dist = dot(wa[i] - wb[i], ld3(p.normalB));
+    }
+    for (int i = m->count - 1; i >= 0; i--) {
+        rlgpu_contact& p = m->pts[i];
+        bool remove;
+        if (!(p.dist <= cbt)) {
+            remove = true;
+        } else {
+            v3 proj = wa[i] - ld3(p.normalB) * p.dist;
+            v3 diff = wb[i] - proj;
+            remove = dot(diff, diff) > cbt * cbt;
+        }
+        if (remove) {
+            int last = m->count - 1;
+            if (i != last) {
+                m->pts[i] = m->pts[last];
+                wa[i] = wa[last];
+                wb[i] = wb[last];
+            }
+            m->count--;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ narrowphase (candidates)
+DEV void emit(ArenaLDS* A, int rank, int tri, v3 n, v3 p, float depth) {
+    int slot = atomicAdd(&A->a.ncand, 1);
+    if (slot >= kMaxCand) return;  // counted by the committing lane
+    Cand& c = A->u.cand[slot];
+    c.n[0] = n.x; c.n[1] = n.y; c.n[2] = n.z;
+    c.p[0] = p.x; c.p[1] = p.y; c.p[2] = p.z;
+    c.depth = depth;
+    c.order = rank * 64 + tri;
+}
+
+// SphereTriangleDetector::pointInTriangle / closestPointTriangle / collide (SphereTriangleDetector.cpp:88-240)
+DEV bool point_in_triangle(v3 v0, v3 v1, v3 v2, v3 normal, v3 p) {
+    v3 e1 = v1 - v0, e2 = v2 - v1, e3 = v0 - v2;
+    v3 n1 = cross(e1, normal), n2 = cross(e2, normal), n3 = cross(e3, normal);
+    float r1 = dot(p, n1) - dot(v0, n1);
+    float r2 = dot(p, n2) - dot(v1, n2);
+    float r3 = dot(p, n3) - dot(v2, n3);
+    if (r1 > 0 && r2 > 0 && r3 > 0) return true;
+    if (r1 <= 0 && r2 <= 0 && r3 <= 0) return true;
+    return false;
+}
+DEV v3 closest_point_triangle(v3 p, v3 a, v3 b, v3 c) {
+    v3 ab = b - a, ac = c - a, ap = p - a;
+    float d1 = dot(ab, ap), d2 = dot(ac, ap);
+    if (d1 <= 0.f && d2 <= 0.f) return a;
+    v3 bp = p - b;
+    float d3 = dot(ab, bp), d4 = dot(ac, bp);
+    if (d3 >= 0.f && d4 <= d3) return b;
+    v3 cp = p - c;
+    float d5 = dot(ab, cp), d6 = dot(ac, cp);
+    if (d6 >= 0.f && d5 <= d6) return c;
+    float vc = d1 * d4 - d3 * d2;
+    if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+        float vv = d1 / (d1 - d3);
+        return a + ab * vv;
+    }
+    float vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+        float vv = d2 / (d2 - d6);
+        return a + ac * vv;
+    }
+    float va = d3 * d6 - d5 * d4;
+    if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+        float vv = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        return b + (c - b) * vv;
+    }
+    float denom = 1.f / (va + vb + vc);
+    float vv = vb * denom, ww = vc * denom;
+    return a + ab * vv + ac * ww;
+}
+DEV bool sphere_triangle(v3 center, float radius, int t, float cbt, v3& point, v3& normal_out, float& depth) {
+    v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
+    float rwt = radius + cbt;
+    v3 normal = cross(v1 - v0, v2 - v0);
+    float l2 = len2(normal);
+    bool has = false;
+    v3 cp = zero3();
+    if (l2 >= kEps * kEps) {
+        normal = normal / sqrtf(l2);
+        v3 p1c = center - v0;
+        float dfp = dot(p1c, normal);
+        if (dfp < 0.f) {
+            dfp *= -1.f;
+            normal = normal * -1.f;
+        }
+        if (dfp < rwt) {
+            if (point_in_triangle(v0, v1, v2, normal, center)) {
+                has = true;
+                cp = center - normal * dfp;
+            } else {
+                v3 nr = closest_point_triangle(center, v0, v1, v2);
+                float d2 = len2(nr - center);
+                if (d2 < rwt * rwt) {
+                    has = true;
+                    cp = nr;
+                }
+            }
+        }
+    }
+    if (!has) return false;
+    v3 c2c = center - cp;
+    float d2 = len2(c2c);
+    if (!(d2 < rwt * rwt)) return false;
+    if (d2 > kEps) {
+        float d = sqrtf(d2);
+        normal_out = normalized(c2c);
+        point = cp;
+        depth = -(radius - d);
+    } else {
+        normal_out = normal;
+        point = cp;
+        depth = -radius;
+    }
+    return true;
+}
+DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
+    v3 dl = vmul(dir_world, R);
+    v3 lv = v3{dl.x >= 0 ? C.car_half.x : -C.car_half.x, dl.y >= 0 ? C.car_half.y : -C.car_half.y,
+               dl.z >= 0 ? C.car_half.z : -C.car_half.z};
+    return R * lv + c;
+}
+// box (car) vs triangle: SAT (stand-in for GJK/EPA)
+DEV bool box_triangle(ArenaLDS* A, int bi, int t, float cbt, v3& nrm, v3& point_b, float& depth) {
+    m3 R = brot(A, bi);
+    v3 c = car_box_center(A, bi);
+    v3 ax[3] = {col(R, 0), col(R, 1), col(R, 2)};
+    v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
+    v3 e[3] = {v1 - v0, v2 - v1, v0 - v2};
+    float best = 1e30f;
+    v3 best_n = zero3();
+    for (int k = 0; k < 13; k++) {
+        v3 axis;
+        if (k == 0) axis = cross(e[0], v2 - v0);
+        else if (k < 4) axis = ax[k - 1];
+        else axis = cross(ax[(k - 4) / 3], e[(k - 4) % 3]);
+        float l2 = len2(axis);
+        if (l2 < 1e-10f) continue;
+        v3 L = axis / sqrtf(l2);
+        float r = C.car_half.x * fabsf(dot(ax[0], L)) + C.car_half.y * fabsf(dot(ax[1], L)) +
+                  C.car_half.z * fabsf(dot(ax[2], L));
+        float p0 = dot(v0, L), p1 = dot(v1, L), p2 = dot(v2, L);
+        float tmin = stdmin(p0, stdmin(p1, p2)), tmax = stdmax(p0, stdmax(p1, p2));
+        float cl = dot(c, L);
+        float pen_pos = tmax - (cl - r);
+        float pen_neg = (cl + r) - tmin;
+        float pen;
+        v3 n;
+        if (pen_pos < pen_neg) {
+            pen = pen_pos;
+            n = L;
+        } else {
+            pen = pen_neg;
+            n = -L;
+        }
+        if (-pen > cbt) return false;
+        if (pen < best) {
+            best = pen;
+            best_n = n;
+        }
+    }
+    nrm = best_n;
+    depth = -best;
+    v3 pa = box_support(R, c, -nrm);
+    point_b = pa - nrm * depth;
+    return true;
+}
+
+// runs the narrowphase of one canonical pair rank and emits candidates; returns pair mode
+DEV int narrow_pair(ArenaLDS* A, int rank) {
+    if (rank < 25) {
+        int bi = rank / 5, st = rank % 5;
+        bool active = bi == 0 ? A->a.ball_awake != 0 : A->a.active[bi] != 0;
+        if (!active) return 0;
+        if (bi == 0) {
+            v3 c = bpos(A, 0);
+            if (st < 4) {  // sphere vs plane (btConvexPlaneCollisionAlgorithm.cpp:53-90)
+                v3 n = C.plane_n[st];
+                v3 vtx = c + (-n) * C.ball_radius;
+                float dist = dot(n, vtx - C.plane_p[st]);
+                v3 on_plane = vtx - n * dist;
+                if (dist < pair_cbt(0, 10)) emit(A, rank, 0, n, on_plane, dist);
+            } else {
+                float r = C.ball_radius, ext = r + 0.08f, cbt = pair_cbt(0, 10);
+                v3 mn = c - v3{ext, ext, ext}, mx = c + v3{ext, ext, ext};
+                for (int t = 0; t < C.ntris; t++) {
+                    if (!aabb_overlap(mn, mx, C.tri_min[t], C.tri_max[t])) continue;
+                    v3 pt, nrm;
+                    float depth;
+                    if (sphere_triangle(c, r, t, cbt, pt, nrm, depth)) emit(A, rank, t, nrm, pt, depth);
+                }
+            }
+        } else {
+            m3 R = brot(A, bi);
+            if (st < 4) {  // box vs plane
+                v3 n = C.plane_n[st];
+                v3 vtx = box_support(R, car_box_center(A, bi), -n);
+                float dist = dot(n, vtx - C.plane_p[st]);
+                v3 on_plane = vtx - n * dist;
+                if (dist < pair_cbt(bi, 10)) emit(A, rank, 0, n, on_plane, dist);
+            } else {
+                v3 mn, mx;
+                body_aabb(bi, bpos(A, bi), R, mn, mx);
+                float cbt = pair_cbt(bi, 10);
+                for (int t = 0; t < C.ntris; t++) {
+                    if (!aabb_overlap(mn, mx, C.tri_min[t], C.tri_max[t])) continue;
+                    v3 n, pb;
+                    float d;
+                    if (box_triangle(A, bi, t, cbt, n, pb, d)) emit(A, rank, t, n, pb, d);
+                }
+            }
+        }
+        return 1;
+    }
+    int key = pair_key(rank);
+    int ka = (key - 64) / 8, kb = (key - 64) % 8;  // ka < kb; ball pairs keyed (ball=0, car)
+    // ball pairs are processed as A = car, B = ball
+    int A_ = ka == 0 ? kb : ka, B_ = ka == 0 ? 0 : kb;
+    bool dem = (A_ >= 1 && !A->a.active[A_]) || (B_ >= 1 && !A->a.active[B_]);
+    v3 m0, m1, n0, n1;
+    broad_aabb(A, A_, m0, m1);
+    broad_aabb(A, B_, n0, n1);
+    if (dem || !aabb_overlap(m0, m1, n0, n1)) return 2;
+    bool act_a = A_ == 0 ? A->a.ball_awake != 0 : A->a.active[A_] != 0;
+    bool act_b = B_ == 0 ? A->a.ball_awake != 0 : A->a.active[B_] != 0;
+    if (!act_a && !act_b) return 0;
+    if (B_ == 0) {  // btSphereBoxCollisionAlgorithm::getSphereDistance, A = car, B = ball
+        m3 R = brot(A, A_);
+        v3 c = car_box_center(A, A_);
+        const float margin = 0.04f;
+        v3 he = v3{(C.car_half.x - margin), (C.car_half.y - margin), (C.car_half.z - margin)};
+        v3 rel = vmul(bpos(A, 0) - c, R);
+        v3 cp = v3{stdmax(-he.x, stdmin(he.x, rel.x)), stdmax(-he.y, stdmin(he.y, rel.y)), stdmax(-he.z, stdmin(he.z, rel.z))};
+        float r = C.ball_radius;
+        float inter = r + margin;
+        float cbt = pair_cbt(A_, 0);
+        float contact_dist = inter + cbt;
+        v3 normal = rel - cp;
+        float d2 = len2(normal);
+        if (d2 > contact_dist * contact_dist) return 1;
+        float distance;
+        if (d2 <= kEps) {
+            float fd[6] = {he.x - rel.x, he.x + rel.x, he.y - rel.y, he.y + rel.y, he.z - rel.z, he.z + rel.z};
+            int bf = 0;
+            for (int k = 1; k < 6; k++)
+                if (fd[k] < fd[bf]) bf = k;
+            cp = rel;
+            int axis = bf / 2;
+            float sg = (bf % 2 == 0) ? 1.f : -1.f;
+            set_comp(cp, axis, sg * comp(he, axis));
+            v3 nn = zero3();
+            set_comp(nn, axis, sg);
+            normal = nn;
+            distance = -fd[bf];
+        } else {
+            distance = len(normal);
+            normal = normal / distance;
+        }
+        v3 point_on_box = R * (cp + normal * margin) + c;
+        float pen = distance - inter;
+        v3 nw = R * normal;
+        v3 nB = -nw;
+        v3 point_b = point_on_box - nB * pen;
+        emit(A, rank, 0, nB, point_b, pen);
+        return 1;
+    }
+    // OBB vs OBB SAT (stand-in for btBoxBoxDetector), A = car ka, B = car kb
+    {
+        m3 Ra = brot(A, A_), Rb = brot(A, B_);
+        v3 ca = car_box_center(A, A_), cb = car_box_center(A, B_);
+        v3 Ax[3] = {col(Ra, 0), col(Ra, 1), col(Ra, 2)}, Bx[3] = {col(Rb, 0), col(Rb, 1), col(Rb, 2)};
+        v3 h = C.car_half;
+        float cbt = pair_cbt(A_, B_);
+        float best = 1e30f;
+        v3 best_n = zero3();
+        int best_k = -1;
+        for (int k = 0; k < 15; k++) {
+            v3 axis;
+            if (k < 3) axis = Ax[k];
+            else if (k < 6) axis = Bx[k - 3];
+            else axis = cross(Ax[(k - 6) / 3], Bx[(k - 6) % 3]);
+            float l2 = len2(axis);
+            if (l2 < 1e-10f) continue;
+            v3 L = axis / sqrtf(l2);
+            float ra = h.x * fabsf(dot(Ax[0], L)) + h.y * fabsf(dot(Ax[1], L)) + h.z * fabsf(dot(Ax[2], L));
+            float rb = h.x * fabsf(dot(Bx[0], L)) + h.y * fabsf(dot(Bx[1], L)) + h.z * fabsf(dot(Bx[2], L));
+            float d = dot(ca - cb, L);
+            float pen = ra + rb - fabsf(d);
+            if (-pen > cbt) return 1;
+            if (pen < best) {
+                best = pen;
+                best_n = d >= 0 ? L : -L;
+                best_k = k;
+            }
+        }
+        float depth = -best;
+        v3 n = best_n;
+        v3 point_b;
+        if (best_k >= 3 && best_k < 6) {
+            v3 pa = box_support(Ra, ca, -n);
+            point_b = pa - n * depth;
+        } else {
+            point_b = box_support(Rb, cb, n);
+        }
+        emit(A, rank, 0, n, point_b, depth);
+    }
+    return 1;
+}
+
+// single lane: commit candidates in canonical order, with callbacks, then refresh each pair
+DEV void commit_contacts(ArenaLDS* A) {
+    int n = A->a.ncand;
+    if (n > kMaxCand) {
+        A->s.env.manifold_overflow += (uint32_t)(n - kMaxCand);
+        n = kMaxCand;
+    }
+    // insertion sort by commit order (few elements)
+    for (int i = 1; i < n; i++) {
+        Cand x = A->u.cand[i];
+        int j = i - 1;
+        while (j >= 0 && A->u.cand[j].order > x.order) {
+            A->u.cand[j + 1] = A->u.cand[j];
+            j--;
+        }
+        A->u.cand[j + 1] = x;
+    }
+    int ci = 0;
+    for (int rank = 0; rank < kPairs; rank++) {
+        int mode = A->a.pair_mode[rank];
+        int key = pair_key(rank);
+        if (mode == 2) {
+            rlgpu_manifold* m = find_manifold(A, key);
+            if (m) m->count = 0;
+            continue;
+        }
+        if (mode == 0) continue;
+        while (ci < n && (A->u.cand[ci].order >> 6) == rank) {
+            const Cand& c = A->u.cand[ci];
+            add_contact(A, key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth);
+            ci++;
+        }
+        refresh(A, key);
+    }
+}
+
+// ------------------------------------------------------------------ sequential impulse solver
+DEV void setup_contact(ArenaLDS* A, Solver& S, CRow& row, int ia, int ib, const rlgpu_contact& cp, v3 rel1, v3 rel2,
+                       float dist) {
+    SB& Sa = S.sb[ia];
+    SB& Sb = S.sb[ib];
+    bool r0 = Sa.real != 0, r1 = Sb.real != 0;
+    v3 n = ld3(cp.normalB);
+    v3 t0 = cross(rel1, n);
+    row.angA = r0 ? A->a.iiw[ia] * t0 : zero3();
+    v3 t1 = cross(rel2, n);
+    row.angB = r1 ? A->a.iiw[ib] * -t1 : zero3();
+    float d0 = 0, d1 = 0;
+    if (r0) d0 = binv_mass(ia) + dot(n, cross(row.angA, rel1));
+    if (r1) d1 = binv_mass(ib) + dot(n, cross(-row.angB, rel2));
+    row.jinv = 1.f / (d0 + d1 + 0.f);
+    row.n1 = r0 ? n : zero3();
+    row.rc1 = r0 ? t0 : zero3();
+    row.n2 = r1 ? -n : zero3();
+    row.rc2 = r1 ? -t1 : zero3();
+    float penetration = dist + 0.f;
+    v3 v1 = r0 ? vel_at(A, ia, rel1) : zero3();
+    v3 v2 = r1 ? vel_at(A, ib, rel2) : zero3();
+    float rel_vel = dot(n, v1 - v2);
+    row.friction = cp.friction;
+    float restitution = fabsf(rel_vel) < 0.2f ? 0.f : cp.restitution * -rel_vel;
+    if (restitution <= 0.f) restitution = 0.f;
+    row.applied = cp.applied * 0.85f;
+    if (r0) {
+        Sa.dlin += row.n1 * v3{Sa.inv_mass, Sa.inv_mass, Sa.inv_mass} * row.applied;
+        Sa.dang += row.angA * row.applied;
+    }
+    if (r1) {
+        Sb.dlin += (-row.n2 * v3{Sb.inv_mass, Sb.inv_mass, Sb.inv_mass}) * -row.applied;
+        Sb.dang += -row.angB * -row.applied;
+    }
+    row.applied_push = 0;
+    float v1n = dot(row.n1, Sa.lin + (r0 ? Sa.ext_f : zero3())) + dot(row.rc1, Sa.ang + (r0 ? Sa.ext_t : zero3()));
+    float v2n = dot(row.n2, Sb.lin + (r1 ? Sb.ext_f : zero3())) + dot(row.rc2, Sb.ang + (r1 ? Sb.ext_t : zero3()));
+    float rv = v1n + v2n;
+    float pos_err = 0, vel_err = restitution - rv;
+    if (penetration > 0) {
+        pos_err = 0;
+    } else {
+        pos_err = -penetration * 0.8f * (1.f / kTick);
+    }
+    row.rhs = vel_err * row.jinv;
+    row.rhs_pen = pos_err * row.jinv;
+}
+
+DEV void add_friction(ArenaLDS* A, Solver& S, int ia, int ib, const rlgpu_contact& cp, v3 rel1, v3 rel2, int cidx,
+                      float friction) {
+    SB& Sa = S.sb[ia];
+    SB& Sb = S.sb[ib];
+    bool r0 = Sa.real != 0, r1 = Sb.real != 0;
+    v3 n = ld3(cp.normalB);
+    v3 va = r0 ? Sa.lin + Sa.ext_f + cross(Sa.ang + Sa.ext_t, rel1) : zero3();
+    v3 vb = r1 ? Sb.lin + Sb.ext_f + cross(Sb.ang + Sb.ext_t, rel2) : zero3();
+    v3 vel = va - vb;
+    float rel_vel = dot(n, vel);
+    v3 dir = vel - n * rel_vel;
+    float lat = len2(dir);
+    if (lat > kEps) {
+        dir = dir * (1.f / sqrtf(lat));
+    } else {  // btPlaneSpace1
+        if (fabsf(n.z) > 0.7071067811865475244008443621048490f) {
+            float a = n.y * n.y + n.z * n.z;
+            float k = 1.f / sqrtf(a);
+            dir = v3{0, -n.z * k, n.y * k};
+        } else {
+            float a = n.x * n.x + n.y * n.y;
+            float k = 1.f / sqrtf(a);
+            dir = v3{-n.y * k, n.x * k, 0};
+        }
+    }
+    FRow& f = S.frows[cidx];
+    f.a = ia;
+    f.b = ib;
+    f.friction = friction;
+    f.applied = 0;
+    f.cidx = cidx;
+    if (r0) {
+        f.n1 = dir;
+        v3 ta = cross(rel1, dir);
+        f.rc1 = ta;
+        f.angA = A->a.iiw[ia] * ta;
+    } else {
+        f.n1 = f.rc1 = f.angA = zero3();
+    }
+    if (r1) {
+        f.n2 = -dir;
+        v3 tb = cross(rel2, f.n2);
+        f.rc2 = tb;
+        f.angB = A->a.iiw[ib] * tb;
+    } else {
+        f.n2 = f.rc2 = f.angB = zero3();
+    }
+    float d0 = 0, d1 = 0;
+    if (r0) d0 = binv_mass(ia) + dot(dir, cross(f.angA, rel1));
+    if (r1) d1 = binv_mass(ib) + dot(dir, cross(-f.angB, rel2));
+    f.jinv = 1.f / (d0 + d1);
+    float v1n = dot(f.n1, r0 ? Sa.lin + Sa.ext_f : zero3()) + dot(f.rc1, r0 ? Sa.ang : zero3());
+    float v2n = dot(f.n2, r1 ? Sb.lin + Sb.ext_f : zero3()) + dot(f.rc2, r1 ? Sb.ang : zero3());
+    f.rhs = (0.f - (v1n + v2n)) * f.jinv;
+    f.lower = -friction;
+    f.upper = friction;
+}
+
+template <class Row>
+DEV float resolve_row(Solver& S, Row& c, float lower, float upper, bool generic) {
+    SB& A = S.sb[c.a];
+    SB& B = S.sb[c.b];
+    float di = c.rhs - c.applied * 0.f;
+    float dv1 = dot(c.n1, A.dlin) + dot(c.rc1, A.dang);
+    float dv2 = dot(c.n2, B.dlin) + dot(c.rc2, B.dang);
+    di -= dv1 * c.jinv;
+    di -= dv2 * c.jinv;
+    float sum = c.applied + di;
+    if (sum < lower) {
+        di = lower - c.applied;
+        c.applied = lower;
+    } else if (generic && sum > upper) {
+        di = upper - c.applied;
+        c.applied = upper;
+    } else {
+        c.applied = sum;
+    }
+    if (A.real) {
+        A.dlin += c.n1 * v3{A.inv_mass, A.inv_mass, A.inv_mass} * di;
+        A.dang += c.angA * di;
+    }
+    if (B.real) {
+        B.dlin += c.n2 * v3{B.inv_mass, B.inv_mass, B.inv_mass} * di;
+        B.dang += c.angB * di;
+    }
+    return di * (1.f / c.jinv);
+}
+DEV float resolve_split(Solver& S, CRow& c) {
+    float di = 0.f;
+    if (c.rhs_pen != 0.f) {
+        SB& A = S.sb[c.a];
+        SB& B = S.sb[c.b];
+        di = c.rhs_pen - c.applied_push * 0.f;
+        float dv1 = dot(c.n1, A.push) + dot(c.rc1, A.turn);
+        float dv2 = dot(c.n2, B.push) + dot(c.rc2, B.turn);
+        di -= dv1 * c.jinv;
+        di -= dv2 * c.jinv;
+        float sum = c.applied_push + di;
+        if (sum < 0.f) {
+            di = 0.f - c.applied_push;
+            c.applied_push = 0.f;
+        } else {
+            c.applied_push = sum;
+        }
+        if (A.real) {
+            A.push += c.n1 * v3{A.inv_mass, A.inv_mass, A.inv_mass} * di;
+            A.turn += c.angA * di;
+        }
+        if (B.real) {
+            B.push += c.n2 * v3{B.inv_mass, B.inv_mass, B.inv_mass} * di;
+            B.turn += c.angB * di;
+        }
+    }
+    return di * (1.f / c.jinv);
+}
+
+// btSequentialImpulseConstraintSolver::solveGroup (single lane per arena)
+DEV void solve(ArenaLDS* A) {
+    Solver& S = A->u.sv;
+    bool in_solver[5];
+    for (int i = 0; i < 5; i++) {
+        bool act = i == 0 ? A->a.ball_awake != 0 : A->a.active[i] != 0;
+        in_solver[i] = act;
+        SB& x = S.sb[i];
+        x.dlin = x.dang = x.push = x.turn = zero3();
+        x.real = act;
+        if (act) {
+            float im = binv_mass(i);
+            x.inv_mass = im;
+            x.lin = bvel(A, i);
+            x.ang = bang(A, i);
+            x.ext_f = A->a.force[i] * im * kTick;
+            x.ext_t = vmul(A->a.torque[i], A->a.iiw[i]) * kTick;
+        } else {
+            x.inv_mass = 0.f;
+            x.lin = x.ang = x.ext_f = x.ext_t = zero3();
+        }
+        S.spec_num[i] = 0;
+        S.spec_fric[i] = 0;
+        S.spec_rest[i] = 0;
+        S.spec_d[i] = 0;
+        S.spec_n[i] = zero3();
+    }
+    {
+        SB& f = S.sb[5];
+        f.dlin = f.dang = f.push = f.turn = f.lin = f.ang = f.ext_f = f.ext_t = zero3();
+        f.inv_mass = 0.f;
+        f.real = 0;
+    }
+    int nrows = 0;
+    // manifolds in ascending key order
+    int last_key = -1;
+    for (;;) {
+        int best = -1, bkey = 1 << 30;
+        for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
+            const rlgpu_manifold& mf = A->s.manifolds[m];
+            if (mf.count > 0 && mf.key > last_key && mf.key < bkey) {
+                bkey = mf.key;
+                best = m;
+            }
+        }
+        if (best < 0) break;
+        last_key = bkey;
+        rlgpu_manifold& mf = A->s.manifolds[best];
+        int a, b;
+        key_bodies(mf.key, a, b);
+        bool aact = a < 10 && in_solver[a];
+        bool bact = b < 10 && in_solver[b];
+        if (!aact && !bact) continue;
+        int ia = aact ? a : 5, ib = bact ? b : 5;
+        v3 pa_, pb_;
+        m3 ra, rb;
+        side_transform(A, a, pa_, ra);
+        side_transform(A, b, pb_, rb);
+        for (int j = 0; j < mf.count; j++) {
+            if (nrows >= kMaxRows) {
+                A->s.env.manifold_overflow++;
+                continue;
+            }
+            rlgpu_contact& cp = mf.pts[j];
+            v3 wa = ra * ld3(cp.localA) + pa_;
+            v3 wb = rb * ld3(cp.localB) + pb_;
+            v3 rel1 = wa - pa_;
+            v3 rel2 = wb - (b >= 10 ? zero3() : pb_);
+            CRow& row = S.rows[nrows];
+            row.a = ia;
+            row.b = ib;
+            row.orig = best * 4 + j;
+            row.special = cp.special != 0;
+            setup_contact(A, S, row, ia, ib, cp, rel1, rel2, cp.dist);
+            if (cp.special) {
+                for (int side = 0; side < 2; side++) {
+                    int bid = side ? b : a;
+                    if (bid < 10) {
+                        S.spec_num[bid]++;
+                        S.spec_fric[bid] = cp.friction;
+                        S.spec_rest[bid] = cp.restitution;
+                        S.spec_n[bid] += ld3(cp.normalB);
+                        S.spec_d[bid] += len(side ? rel2 : rel1);
+                    }
+                }
+            }
+            add_friction(A, S, ia, ib, cp, rel1, rel2, nrows, cp.friction);
+            nrows++;
+        }
+    }
+    for (int i = 0; i < 5; i++) {
+        if (S.spec_num[i] <= 0 || !in_solver[i]) continue;
+        if (nrows >= kMaxRows) {
+            A->s.env.manifold_overflow++;
+            continue;
+        }
+        float distance = S.spec_d[i] / S.spec_num[i];
+        v3 normal = S.spec_n[i] / (float)S.spec_num[i];
+        rlgpu_contact tmp;
+        st3(tmp.localA, zero3());
+        st3(tmp.localB, zero3());
+        st3(tmp.normalB, normal);
+        tmp.dist = distance;
+        tmp.applied = 0.f;
+        tmp.friction = S.spec_fric[i];
+        tmp.restitution = S.spec_rest[i];
+        tmp.special = 0;
+        v3 rel1 = normal * -distance, rel2 = zero3();
+        CRow& row = S.rows[nrows];
+        row.a = i;
+        row.b = 5;
+        row.orig = -1;
+        row.special = 0;
+        setup_contact(A, S, row, i, 5, tmp, rel1, rel2, distance);
+        add_friction(A, S, i, 5, tmp, rel1, rel2, nrows, tmp.friction);
+        nrows++;
+    }
+    for (int it = 0; it < 10; it++) {
+        float lsr = 0.f;
+        for (int r = 0; r < nrows; r++) {
+            float res = resolve_split(S, S.rows[r]);
+            lsr = stdmax(lsr, res * res);
+        }
+        if (lsr <= 0.f || it >= 9) break;
+    }
+    for (int it = 0; it < 10; it++) {
+        for (int r = 0; r < nrows; r++) {
+            CRow& row = S.rows[r];
+            if (row.special) continue;
+            resolve_row(S, row, 0.f, 1e10f, false);
+        }
+        for (int r = 0; r < nrows; r++) {
+            FRow& f = S.frows[r];
+            float total = S.rows[f.cidx].applied;
+            if (total > 0.f) {
+                f.lower = -(f.friction * total);
+                f.upper = f.friction * total;
+                resolve_row(S, f, f.lower, f.upper, true);
+            }
+        }
+    }
+    for (int r = 0; r < nrows; r++) {
+        const CRow& row = S.rows[r];
+        if (row.orig >= 0) A->s.manifolds[row.orig >> 2].pts[row.orig & 3].applied = row.applied;
+    }
+    for (int i = 0; i < 5; i++) {
+        if (!in_solver[i]) continue;
+        SB& x = S.sb[i];
+        rlgpu_body* bd = body(A, i);
+        x.lin += x.dlin;
+        x.ang += x.dang;
+        if (!(x.push.x == 0 && x.push.y == 0 && x.push.z == 0 && x.turn.x == 0 && x.turn.y == 0 && x.turn.z == 0)) {
+            if (i == 0) {
+                st3(bd->pos, ld3(bd->pos) + x.push * kTick);
+            } else {
+                v3 np;
+                m3 nr;
+                integrate_transform(ld3(bd->pos), ldm(bd->rot), x.push, x.turn * 0.1f, kTick, np, nr);
+                st3(bd->pos, np);
+                stm(bd->rot, nr);
+            }
+        }
+        st3(bd->vel, x.lin + x.ext_f);
+        st3(bd->angvel, x.ang + x.ext_t);
+    }
+}
+
+}  // namespace rl

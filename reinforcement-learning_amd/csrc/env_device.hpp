@@ -1,0 +1,797 @@
+// env_device.hpp -- per-arena device functions of the env kernel (see env_kernel.hpp).
+// Every function cites the reference code it restates; the operation order matches the
+// CPU oracle so strict-FP builds agree bit for bit.
+#pragma once
+#include "env_kernel.hpp"
+
+namespace rl {
+
+extern __constant__ EnvConst C;
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------------ state accessors
+DEV v3 ld3(const float* p) { return v3{p[0], p[1], p[2]}; }
+DEV void st3(float* p, v3 v) {
+    p[0] = v.x;
+    p[1] = v.y;
+    p[2] = v.z;
+}
+DEV m3 ldm(const float* p) { return m3{v3{p[0], p[1], p[2]}, v3{p[3], p[4], p[5]}, v3{p[6], p[7], p[8]}}; }
+DEV void stm(float* p, const m3& m) {
+    p[0] = m.r0.x; p[1] = m.r0.y; p[2] = m.r0.z;
+    p[3] = m.r1.x; p[4] = m.r1.y; p[5] = m.r1.z;
+    p[6] = m.r2.x; p[7] = m.r2.y; p[8] = m.r2.z;
+}
+DEV rlgpu_body* body(ArenaLDS* A, int i) { return i == 0 ? &A->s.ball : &A->s.cars[i - 1].body; }
+DEV v3 bpos(ArenaLDS* A, int i) { return ld3(body(A, i)->pos); }
+DEV v3 bvel(ArenaLDS* A, int i) { return ld3(body(A, i)->vel); }
+DEV v3 bang(ArenaLDS* A, int i) { return ld3(body(A, i)->angvel); }
+DEV m3 brot(ArenaLDS* A, int i) { return ldm(body(A, i)->rot); }
+DEV float binv_mass(int i) { return i == 0 ? C.ball_inv_mass : C.car_inv_mass; }
+DEV v3 binv_iner(int i) { return i == 0 ? C.ball_inv_inertia : C.car_inv_inertia; }
+DEV v3 vel_at(ArenaLDS* A, int i, v3 rel) { return bvel(A, i) + cross(bang(A, i), rel); }
+DEV void update_inertia(ArenaLDS* A, int i) {
+    m3 r = brot(A, i);
+    A->a.iiw[i] = scaled(r, binv_iner(i)) * transpose(r);
+}
+DEV void apply_central_impulse(ArenaLDS* A, int i, v3 imp) {
+    rlgpu_body* b = body(A, i);
+    st3(b->vel, ld3(b->vel) + imp * binv_mass(i));
+}
+DEV void apply_impulse(ArenaLDS* A, int i, v3 imp, v3 rel) {
+    if (binv_mass(i) != 0.f) {
+        apply_central_impulse(A, i, imp);
+        rlgpu_body* b = body(A, i);
+        st3(b->angvel, ld3(b->angvel) + A->a.iiw[i] * cross(rel, imp));
+    }
+}
+DEV float impulse_denominator(ArenaLDS* A, int i, v3 pos_w, v3 n) {
+    v3 r0 = pos_w - bpos(A, i);
+    v3 c0 = cross(r0, n);
+    v3 vec = cross(vmul(c0, A->a.iiw[i]), r0);
+    return binv_mass(i) + dot(n, vec);
+}
+DEV void add_force(ArenaLDS* A, int i, v3 f) { A->a.force[i] = A->a.force[i] + f; }
+DEV void add_torque(ArenaLDS* A, int i, v3 t) { A->a.torque[i] = A->a.torque[i] + t; }
+DEV float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+DEV float stdclamp(float v, float lo, float hi) { return v < lo ? lo : (hi < v ? hi : v); }  // std::clamp
+DEV float stdmax(float a, float b) { return a < b ? b : a; }                                  // std::max
+DEV float stdmin(float a, float b) { return b < a ? b : a; }                                  // std::min
+DEV int sgn(float x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); }                                  // RS_SGN
+
+// ------------------------------------------------------------------ LinearPieceCurve (Math.cpp:5-34)
+struct Curve {
+    int n;
+    float k[6], v[6];
+};
+DEV float curve_out(const Curve& c, float input, float def = 1.f) {
+    if (c.n == 0) return def;
+    if (input <= c.k[0]) return c.v[0];
+    for (int i = 1; i < c.n; i++) {
+        if (c.k[i] > input) {
+            float range = c.k[i] - c.k[i - 1];
+            float diff = c.v[i] - c.v[i - 1];
+            float f = (input - c.k[i - 1]) / range;
+            return c.v[i - 1] + diff * f;
+        }
+    }
+    return c.v[c.n - 1];
+}
+// RLConst.h:342-437
+__device__ const Curve kSteerAngle = {6, {0, 500, 1000, 1500, 1750, 3000}, {0.53356f, 0.31930f, 0.18203f, 0.10570f, 0.08507f, 0.03454f}};
+__device__ const Curve kPowerslideSteer = {2, {0, 2500}, {0.39235f, 0.12610f}};
+__device__ const Curve kDriveTorque = {3, {0, 1400, 1410}, {1.0f, 0.1f, 0.0f}};
+__device__ const Curve kNonSticky = {3, {0, 0.7075f, 1}, {0.1f, 0.5f, 1.0f}};
+__device__ const Curve kLatFriction = {2, {0, 1}, {1.0f, 0.2f}};
+__device__ const Curve kLongFriction = {0, {}, {}};
+__device__ const Curve kHbLat = {1, {0}, {0.1f}};
+__device__ const Curve kHbLong = {2, {0, 1}, {0.5f, 0.9f}};
+__device__ const Curve kBallCarExtra = {4, {0, 500, 2300, 4600}, {0.65f, 0.65f, 0.55f, 0.30f}};
+__device__ const Curve kBumpGround = {3, {0, 1400, 2200}, {5.f / 6.f, 1100.f, 1530.f}};
+__device__ const Curve kBumpAir = {3, {0, 1400, 2200}, {5.f / 6.f, 1390.f, 1945.f}};
+__device__ const Curve kBumpUp = {3, {0, 1400, 2200}, {2.f / 6.f, 278.f, 417.f}};
+
+// ------------------------------------------------------------------ Philox 4x32-10 (same as oracle)
+DEV uint32_t philox0(uint64_t key, uint32_t c0, uint32_t c1) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    uint32_t x0 = c0, x1 = c1, x2 = 0x9E3779B9u, x3 = 0x85EBCA6Bu;
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+        uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0, y1 = (uint32_t)p1, y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1,
+                 y3 = (uint32_t)p0;
+        x0 = y0;
+        x1 = y1;
+        x2 = y2;
+        x3 = y3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return x0;
+}
+DEV uint32_t rng_next(ArenaLDS* A, uint64_t seed, int arena) { return philox0(seed, (uint32_t)arena, A->s.env.rng_counter++); }
+
+// ------------------------------------------------------------------ shapes / AABBs
+DEV v3 car_box_center(ArenaLDS* A, int bi) { return bpos(A, bi) + brot(A, bi) * C.car_offset; }
+DEV void body_aabb(int bi, v3 pos, const m3& rot, v3& mn, v3& mx) {
+    if (bi == 0) {
+        float m = C.ball_radius + 0.08f;
+        mn = pos - v3{m, m, m};
+        mx = pos + v3{m, m, m};
+    } else {
+        v3 center = pos + rot * C.car_offset;
+        v3 e;
+        e.x = fabsf(rot.r0.x) * C.car_half.x + fabsf(rot.r0.y) * C.car_half.y + fabsf(rot.r0.z) * C.car_half.z;
+        e.y = fabsf(rot.r1.x) * C.car_half.x + fabsf(rot.r1.y) * C.car_half.y + fabsf(rot.r1.z) * C.car_half.z;
+        e.z = fabsf(rot.r2.x) * C.car_half.x + fabsf(rot.r2.y) * C.car_half.y + fabsf(rot.r2.z) * C.car_half.z;
+        mn = center - e;
+        mx = center + e;
+    }
+}
+DEV void broad_aabb(ArenaLDS* A, int bi, v3& mn, v3& mx) {
+    v3 a0, a1, p0, p1;
+    body_aabb(bi, bpos(A, bi), brot(A, bi), a0, a1);
+    body_aabb(bi, A->a.pred_pos[bi], A->a.pred_rot[bi], p0, p1);
+    mn = v3{stdmin(a0.x, p0.x) - 0.02f, stdmin(a0.y, p0.y) - 0.02f, stdmin(a0.z, p0.z) - 0.02f};
+    mx = v3{stdmax(a1.x, p1.x) + 0.02f, stdmax(a1.y, p1.y) + 0.02f, stdmax(a1.z, p1.z) + 0.02f};
+}
+DEV bool aabb_overlap(v3 a0, v3 a1, v3 b0, v3 b1) {
+    return !(a0.x > b1.x || a1.x < b0.x || a0.y > b1.y || a1.y < b0.y || a0.z > b1.z || a1.z < b0.z);
+}
+
+// ------------------------------------------------------------------ ray cast (btCollisionWorld::rayTest)
+DEV int ray_cast(ArenaLDS* A, v3 from, v3 to, int self, v3& hit_point, v3& hit_normal) {
+    float best = 1.0f;
+    int obj = -1;
+    v3 nrm = zero3();
+    v3 d = to - from;
+    for (int p = 0; p < 4; p++) {
+        float da = dot(C.plane_n[p], from - C.plane_p[p]);
+        float db = dot(C.plane_n[p], to - C.plane_p[p]);
+        if (da * db >= 0.f) continue;
+        float f = da / (da - db);
+        if (f < best) {
+            best = f;
+            obj = 10;
+            nrm = da > 0.f ? C.plane_n[p] : -C.plane_n[p];
+        }
+    }
+    for (int t = 0; t < C.ntris; t++) {
+        v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
+        v3 tn = cross(v1 - v0, v2 - v0);
+        float dist = dot(v0, tn);
+        float da = dot(tn, from) - dist;
+        float db = dot(tn, to) - dist;
+        if (da * db >= 0.f) continue;
+        float f = da / (da - db);
+        if (f < best) {
+            float tol = len2(tn) * -0.0001f;
+            v3 pt = from + d * f;
+            v3 v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
+            if (dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol) {
+                best = f;
+                obj = 10;
+                v3 n = normalized(tn);
+                nrm = da <= 0.f ? -n : n;
+            }
+        }
+    }
+    {
+        v3 bp = bpos(A, 0);
+        v3 oc = from - bp;
+        float a = dot(d, d), bb = dot(oc, d), c = dot(oc, oc) - C.ball_radius * C.ball_radius;
+        if (c > 0.f) {
+            float disc = bb * bb - a * c;
+            if (disc >= 0.f && bb < 0.f) {
+                float f = (-bb - sqrtf(disc)) / a;
+                if (f >= 0.f && f < best) {
+                    best = f;
+                    obj = 0;
+                    nrm = normalized((from + d * f) - bp);
+                }
+            }
+        }
+    }
+    for (int ci = 1; ci <= 4; ci++) {
+        if (ci == self) continue;
+        v3 c = car_box_center(A, ci);
+        m3 R = brot(A, ci);
+        v3 lo = vmul(from - c, R), ldir = vmul(d, R);
+        float tmin = 0.f, tmax = best;
+        int axis = -1;
+        float sg = 0.f;
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; k++) {
+            float h = comp(C.car_half, k);
+            float lk = comp(ldir, k), ok_ = comp(lo, k);
+            if (fabsf(lk) < 1e-12f) {
+                if (ok_ < -h || ok_ > h) ok = false;
+                continue;
+            }
+            float inv = 1.f / lk;
+            float t1 = (-h - ok_) * inv, t2 = (h - ok_) * inv;
+            float s1 = -1.f;
+            if (t1 > t2) {
+                float tt = t1;
+                t1 = t2;
+                t2 = tt;
+                s1 = 1.f;
+            }
+            if (t1 > tmin) {
+                tmin = t1;
+                axis = k;
+                sg = s1;
+            }
+            if (t2 < tmax) tmax = t2;
+            if (tmin > tmax) ok = false;
+        }
+        if (ok && axis >= 0 && tmin < best) {
+            best = tmin;
+            obj = ci;
+            v3 ln = zero3();
+            set_comp(ln, axis, sg);
+            nrm = R * ln;
+        }
+    }
+    if (obj < 0) return -1;
+    hit_point = from + d * best;
+    hit_normal = normalized(nrm);
+    if (obj >= 1 && obj <= 4 && !A->a.active[obj]) return -1;
+    return obj;
+}
+
+// ------------------------------------------------------------------ vehicle, one wheel per lane
+// btVehicleRL::updateWheelTransform + rayCast (btVehicleRL.cpp:64-207)
+DEV void wheel_phase(ArenaLDS* A, int ci, int i) {
+    rlgpu_car& cs = A->s.cars[ci];
+    WheelT& W = A->u.wt[ci * 4 + i];
+    int bi = ci + 1;
+    m3 R = brot(A, bi);
+    v3 P = bpos(A, bi);
+    W.hard_point = R * C.wheel_conn[i] + P;
+    W.wheel_dir = R * v3{0, 0, -1};
+    v3 axle = R * v3{0, -1, 0};
+    v3 up = -W.wheel_dir;
+    quat q = quat_axis_angle(up, cs.wheel_steer[i]);
+    m3 steer = mat_from_quat(q);
+    W.wt_col1 = steer * (-axle);
+    // rayCast
+    W.in_contact = 0;
+    W.contact_world = 0;
+    float rest = C.wheel_rest[i], radius = C.wheel_radius[i], travel = C.susp_travel;
+    float ray_len = rest + travel + radius - 0.05f;
+    v3 source = W.hard_point;
+    v3 target = source + W.wheel_dir * ray_len;
+    W.contact_point = target;
+    W.ground = -1;
+    v3 hp, hn;
+    int obj = ray_cast(A, source, target, bi, hp, hn);
+    v3 upv = col(R, 2);
+    if (obj >= 0) {
+        W.contact_point = hp;
+        W.contact_normal = hn;
+        W.in_contact = 1;
+        W.contact_world = (obj == 10);
+        W.ground = obj;
+        float trace = dot(W.hard_point - W.contact_point, upv);
+        W.susp_len = trace - radius;
+        W.susp_len = stdclamp(W.susp_len, rest - travel, rest + travel);
+        float denom = dot(W.contact_normal, upv);
+        v3 relpos = W.contact_point - P;
+        v3 va = vel_at(A, bi, relpos);
+        float proj = dot(W.contact_normal, va);
+        if (denom > 0.1f) {
+            float inv = 1.f / denom;
+            W.susp_rel_vel = proj * inv;
+            W.clipped_inv = inv;
+        } else {
+            W.susp_rel_vel = 0.f;
+            W.clipped_inv = 10.f;
+        }
+        if (obj == 10) {
+            float thresh = (rest + radius) - 0.05f;
+            if (trace < thresh) {
+                float dist = trace - thresh;
+                v3 rel1 = hp - P;
+                v3 v1 = vel_at(A, bi, rel1);
+                float rel_vel = dot(hn, v1);
+                float pos_err = 0.2f * -dist / kTick;
+                float vel_err = -(1.0f + 0.f) * rel_vel;
+                float denom0 = impulse_denominator(A, bi, hp, hn);
+                float jinv = 1.f / (denom0 + 0.f);
+                float imp = pos_err * jinv + vel_err * jinv;
+                imp = 0.f > imp ? 0.f : imp;
+                cs.wheel_extra_pushback[i] = imp / 4;
+            }
+        }
+    } else {
+        W.susp_len = rest + travel;
+        W.susp_rel_vel = 0.f;
+        W.contact_normal = -W.wheel_dir;
+        W.clipped_inv = 1.f;
+        cs.wheel_extra_pushback[i] = 0.f;
+    }
+    // calcFrictionImpulses (btVehicleRL.cpp:308-369), tick-start velocities of a dynamic ground
+    if (W.ground < 0) {
+        W.impulse = zero3();
+        return;
+    }
+    const float friction_scale = kCarMass / 3;
+    v3 ax = W.wt_col1;
+    v3 n = W.contact_normal;
+    float pj = dot(ax, n);
+    ax -= n * pj;
+    ax = safe_normalized(ax);
+    v3 fwd = safe_normalized(cross(n, ax));
+    bool dyn = W.ground >= 0 && W.ground <= 4;
+    int g = W.ground;
+    float side;
+    {
+        v3 cp = W.contact_point;
+        v3 rel1 = cp - P;
+        v3 gcom = dyn ? bpos(A, g) : zero3();
+        m3 grot = dyn ? brot(A, g) : ident3();
+        float g_inv_mass = dyn ? binv_mass(g) : 0.f;
+        v3 g_iner = dyn ? binv_iner(g) : zero3();
+        v3 rel2 = cp - gcom;
+        v3 v1 = vel_at(A, bi, rel1);
+        v3 v2 = dyn ? (A->a.snap_vel[g] + cross(A->a.snap_ang[g], rel2)) : zero3();
+        v3 vel = v1 - v2;
+        v3 aJ = transpose(R) * cross(rel1, ax);
+        v3 bJ = transpose(grot) * cross(rel2, -ax);
+        v3 m0 = C.car_inv_inertia * aJ;
+        v3 m1 = g_iner * bJ;
+        float adiag = C.car_inv_mass + dot(m0, aJ) + g_inv_mass + dot(m1, bJ);
+        float jinv = 1.f / adiag;
+        float rel_vel = dot(ax, vel);
+        side = -0.2f * rel_vel * jinv;
+    }
+    float rolling;
+    if (cs.wheel_engine_force[i] == 0.f) {
+        if (cs.wheel_brake[i] != 0.f) {
+            v3 car_rel = W.contact_point - P;
+            v3 v1 = vel_at(A, bi, car_rel);
+            v3 v2 = dyn ? (A->a.snap_vel[g] + cross(A->a.snap_ang[g], car_rel)) : zero3();
+            float rel_vel = dot(v1 - v2, fwd);
+            const float MAGIC = 113.73963f;
+            rolling = stdclamp(-rel_vel * MAGIC, -cs.wheel_brake[i], cs.wheel_brake[i]);
+        } else {
+            rolling = 0.f;
+        }
+    } else {
+        rolling = -cs.wheel_engine_force[i] / friction_scale;
+    }
+    v3 total = (fwd * rolling * cs.wheel_long_friction[i]) + (ax * side * cs.wheel_lat_friction[i]);
+    W.impulse = total * friction_scale;
+}
+
+DEV v3 upwards_dir_from_wheels(ArenaLDS* A, int ci) {
+    v3 sum = zero3();
+    for (int i = 0; i < 4; i++)
+        if (A->u.wt[ci * 4 + i].in_contact) sum += A->u.wt[ci * 4 + i].contact_normal;
+    if (sum.x == 0 && sum.y == 0 && sum.z == 0) return col(brot(A, ci + 1), 2);
+    return safe_normalized(sum);
+}
+
+// Car::_UpdateWheels (Car.cpp:330-475)
+DEV void update_wheels(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    const float* ctl = cs.controls;
+    float abs_fwd = fabsf(fwd_speed);
+    bool world_contact = false;
+    for (int i = 0; i < 4; i++) world_contact |= A->u.wt[ci * 4 + i].contact_world != 0;
+    if (ctl[7] != 0.f)
+        cs.handbrake_val += 5.f * kTick;
+    else
+        cs.handbrake_val -= 2.f * kTick;
+    cs.handbrake_val = stdclamp(cs.handbrake_val, 0.f, 1.f);
+    float real_throttle = ctl[0];
+    float real_brake = 0;
+    if (ctl[6] != 0.f && cs.boost > 0) real_throttle = 1;
+    {
+        float drive_scale = curve_out(kDriveTorque, abs_fwd);
+        float engine_throttle = real_throttle;
+        if (ctl[7] != 0.f) {
+        } else {
+            float abs_throttle = fabsf(real_throttle);
+            if (abs_throttle >= 0.001f) {
+                if (abs_fwd > 25.f && sgn(real_throttle) != sgn(fwd_speed)) {
+                    real_brake = 1;
+                    if (abs_fwd > 0.01f) engine_throttle = 0;
+                }
+            } else {
+                engine_throttle = 0;
+                bool full_stop = abs_fwd < 25.f;
+                real_brake = full_stop ? 1 : 0.15f;
+            }
+        }
+        if (nwc < 3) drive_scale /= 4;
+        float engine = engine_throttle * (kCarMass * 400.f * kUU2BT) * drive_scale;
+        float brake = real_brake * (kCarMass * (14.25f + (1.f / 3.f)) * kUU2BT);
+        for (int i = 0; i < 4; i++) {
+            cs.wheel_engine_force[i] = engine;
+            cs.wheel_brake[i] = brake;
+        }
+    }
+    {
+        float steer = curve_out(kSteerAngle, abs_fwd);
+        if (cs.handbrake_val != 0.f) steer += (curve_out(kPowerslideSteer, abs_fwd) - steer) * cs.handbrake_val;
+        steer *= ctl[1];
+        cs.wheel_steer[0] = steer;
+        cs.wheel_steer[1] = steer;
+    }
+    v3 P = bpos(A, bi), Vv = bvel(A, bi), Av = bang(A, bi);
+    for (int i = 0; i < 4; i++) {
+        WheelT& W = A->u.wt[ci * 4 + i];
+        if (W.ground >= 0) {
+            v3 lat_dir = W.wt_col1;
+            v3 long_dir = cross(lat_dir, W.contact_normal);
+            float fin = 0;
+            v3 delta = W.hard_point - P;
+            v3 cv = (cross(Av, delta) + Vv) * kBT2UU;
+            float base = fabsf(dot(cv, lat_dir));
+            if (base > 5) fin = base / (fabsf(dot(cv, long_dir)) + base);
+            float lat = curve_out(kLatFriction, fin);
+            float lon = curve_out(kLongFriction, fin);
+            if (cs.handbrake_val != 0.f) {
+                float hb = cs.handbrake_val;
+                lat *= (curve_out(kHbLat, fin) - 1) * hb + 1;
+                lon *= (curve_out(kHbLong, fin) - 1) * hb + 1;
+            } else {
+                lon = 1;
+            }
+            bool sticky = real_throttle != 0;
+            if (!sticky) {
+                float ns = curve_out(kNonSticky, W.contact_normal.z);
+                lat *= ns;
+                lon *= ns;
+            }
+            cs.wheel_lat_friction[i] = lat;
+            cs.wheel_long_friction[i] = lon;
+        }
+    }
+    if (world_contact) {
+        v3 up = upwards_dir_from_wheels(A, ci);
+        bool full = (real_throttle != 0) || (abs_fwd > 25.f);
+        float scale = 0.5f;
+        if (full) scale += 1 - fabsf(up.z);
+        add_force(A, bi, up * scale * (-650.f * kUU2BT) * kCarMass);
+    }
+}
+
+// Car::_UpdateBoost (Car.cpp:477-505)
+DEV void update_boost(ArenaLDS* A, int ci) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    bool boosting = cs.controls[6] != 0.f;
+    if (cs.time_spent_boosting > 0) {
+        if (!boosting && cs.time_spent_boosting >= 0.1f)
+            cs.time_spent_boosting = 0;
+        else
+            cs.time_spent_boosting += kTick;
+    } else {
+        if (boosting) cs.time_spent_boosting = kTick;
+    }
+    if (cs.boost > 0 && cs.time_spent_boosting > 0) {
+        cs.boost = stdmax(cs.boost - (100.f / 3) * kTick, 0.f);
+        float accel = cs.is_on_ground ? (2975 / 3.f) : (3175 / 3.f);
+        add_force(A, bi, accel * kUU2BT * col(brot(A, bi), 0) * kCarMass);
+    }
+    cs.boost = stdmin(cs.boost, 100.f);
+}
+
+// Car::_UpdateJump (Car.cpp:507-554)
+DEV void update_jump(ArenaLDS* A, int ci, bool jump_pressed) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    const float JUMP_MIN = 0.025f, JUMP_MAX = 0.2f, PAD = 1 / 40.f;
+    if (cs.is_on_ground && !cs.is_jumping) {
+        if (cs.has_jumped && cs.jump_time < JUMP_MIN + PAD) {
+        } else {
+            cs.has_jumped = 0;
+            cs.jump_time = 0;
+        }
+    }
+    if (cs.is_jumping) {
+        cs.is_jumping = (cs.jump_time < JUMP_MIN || (cs.controls[5] != 0.f && cs.jump_time < JUMP_MAX));
+    } else if (cs.is_on_ground && jump_pressed) {
+        cs.is_jumping = 1;
+        cs.jump_time = 0;
+        v3 f = col(brot(A, bi), 2) * (875.f / 3.f) * kUU2BT * kCarMass;
+        apply_central_impulse(A, bi, f);
+    }
+    if (cs.is_jumping) {
+        cs.has_jumped = 1;
+        v3 total = col(brot(A, bi), 2) * (4375.f / 3.f);
+        if (cs.jump_time < JUMP_MIN) total *= 0.62f;
+        add_force(A, bi, total * kUU2BT * kCarMass);
+    }
+    if (cs.is_jumping || cs.has_jumped) cs.jump_time += kTick;
+}
+
+// Car::_UpdateAirTorque (Car.cpp:556-641)
+DEV void update_air_torque(ArenaLDS* A, int ci, bool update_air_control) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    const float* ctl = cs.controls;
+    m3 R = brot(A, bi);
+    v3 dir_pitch = -col(R, 1), dir_yaw = col(R, 2), dir_roll = -col(R, 0);
+    bool do_air = false;
+    if (cs.is_flipping) cs.is_flipping = cs.has_flipped && cs.flip_time < 0.65f;
+    if (cs.is_flipping) {
+        v3 rel = ld3(cs.flip_rel_torque);
+        if (!(rel.x == 0 && rel.y == 0 && rel.z == 0)) {
+            float pitch_scale = 1;
+            if (rel.y != 0 && ctl[2] != 0) {
+                if (sgn(rel.y) == sgn(ctl[2])) {
+                    pitch_scale = 1 - stdmin(fabsf(ctl[2]), 1.f);
+                    do_air = true;
+                }
+            }
+            rel.y *= pitch_scale;
+            v3 dodge = rel * v3{260.f, 224.f, 0};
+            add_torque(A, bi, (inverse(A->a.iiw[bi]) * R) * dodge);
+        } else {
+            do_air = true;
+        }
+    } else {
+        do_air = true;
+    }
+    do_air &= !cs.is_auto_flipping;
+    do_air &= update_air_control;
+    if (do_air) {
+        float pitch_scale = 1;
+        v3 torque = zero3();
+        if (ctl[2] != 0 || ctl[3] != 0 || ctl[4] != 0) {
+            if (cs.is_flipping)
+                pitch_scale = 0;
+            else if (cs.has_flipped && cs.flip_time < 0.65f + 0.3f)
+                pitch_scale = 0;
+            torque = (ctl[2] * dir_pitch * pitch_scale * 130.f) + (ctl[3] * dir_yaw * 95.f) + (ctl[4] * dir_roll * 400.f);
+        }
+        v3 av = bang(A, bi);
+        float damp_pitch = dot(dir_pitch, av) * 30.f * (1 - fabsf(do_air ? (ctl[2] * pitch_scale) : 0));
+        float damp_yaw = dot(dir_yaw, av) * 20.f * (1 - fabsf(do_air ? ctl[3] : 0));
+        float damp_roll = dot(dir_roll, av) * 50.f;
+        v3 damping = (dir_yaw * damp_yaw) + (dir_pitch * damp_pitch) + (dir_roll * damp_roll);
+        const float TORQUE_SCALE = (float)(2 * 3.14159265358979323846 / (1 << 16) * 1000);
+        add_torque(A, bi, inverse(A->a.iiw[bi]) * (torque - damping) * TORQUE_SCALE);
+    }
+    if (ctl[0] != 0) add_force(A, bi, col(R, 0) * ctl[0] * (200 / 3.f) * kUU2BT * kCarMass);
+}
+
+// Car::_UpdateDoubleJumpOrFlip (Car.cpp:643-761)
+DEV void update_double_jump_or_flip(ArenaLDS* A, int ci, bool jump_pressed, float fwd_speed) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    const float* ctl = cs.controls;
+    if (cs.is_on_ground) {
+        cs.has_double_jumped = 0;
+        cs.has_flipped = 0;
+        cs.air_time = 0;
+        cs.air_time_since_jump = 0;
+        cs.flip_time = 0;
+    } else {
+        cs.air_time += kTick;
+        if (cs.has_jumped && !cs.is_jumping)
+            cs.air_time_since_jump += kTick;
+        else
+            cs.air_time_since_jump = 0;
+        if (jump_pressed && cs.air_time_since_jump < 1.25f) {
+            float mag = fabsf(ctl[3]) + fabsf(ctl[2]) + fabsf(ctl[4]);
+            bool flip_input = mag >= 0.5f;
+            bool can_use = !cs.has_double_jumped && !cs.has_flipped;
+            if (cs.is_auto_flipping) can_use = false;
+            if (can_use) {
+                if (flip_input) {
+                    cs.flip_time = 0;
+                    cs.has_flipped = 1;
+                    cs.is_flipping = 1;
+                    float ratio = fabsf(fwd_speed) / 2300.f;
+                    v3 dodge = v3{-ctl[2], ctl[3] + ctl[4], 0};
+                    if (fabsf(ctl[3] + ctl[4]) < 0.1f && fabsf(ctl[2]) < 0.1f)
+                        dodge = zero3();
+                    else
+                        dodge = safe_normalized(dodge);
+                    st3(cs.flip_rel_torque, v3{-dodge.y, dodge.x, 0});
+                    if (fabsf(dodge.x) < 0.1f) dodge.x = 0;
+                    if (fabsf(dodge.y) < 0.1f) dodge.y = 0;
+                    if (!fuzzy_zero(dodge)) {
+                        bool back;
+                        if (fabsf(fwd_speed) < 100.0f)
+                            back = dodge.x < 0.0f;
+                        else
+                            back = (dodge.x >= 0.0f) != (fwd_speed >= 0.0f);
+                        v3 init = dodge * 500.f;
+                        float max_x = back ? 2.5f : 1.f;
+                        init.x *= ((max_x - 1) * ratio) + 1.f;
+                        init.y *= ((1.9f - 1) * ratio) + 1.f;
+                        if (back) init.x *= 16.f / 15.f;
+                        v3 fdir = col(brot(A, bi), 0);
+                        float ang = rs_atan2f(fdir.y, fdir.x);
+                        float sa, ca;
+                        rs_sincosf(ang, &sa, &ca);
+                        v3 xdir = v3{ca, -sa, 0.f}, ydir = v3{sa, ca, 0.f};
+                        v3 dv = v3{dot(init, xdir), dot(init, ydir), 0.f};
+                        apply_central_impulse(A, bi, dv * kUU2BT * kCarMass);
+                    }
+                } else {
+                    v3 f = col(brot(A, bi), 2) * (875.f / 3.f) * kUU2BT * kCarMass;
+                    apply_central_impulse(A, bi, f);
+                    cs.has_double_jumped = 1;
+                }
+            }
+        }
+    }
+    if (cs.is_flipping) {
+        cs.flip_time += kTick;
+        if (cs.flip_time <= 0.65f) {
+            rlgpu_body* b = body(A, bi);
+            if (cs.flip_time >= 0.15f && (b->vel[2] < 0 || cs.flip_time < 0.21f)) b->vel[2] *= (1 - 0.35f);
+        }
+    } else if (cs.has_flipped) {
+        cs.flip_time += kTick;
+    }
+}
+
+// Car::_UpdateAutoFlip (Car.cpp:763-797)
+DEV void update_auto_flip(ArenaLDS* A, int ci, bool jump_pressed) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    m3 m = brot(A, bi);
+    if (jump_pressed && cs.world_contact && cs.world_contact_normal[2] > 0.70710678118654752440f) {
+        float r0 = rs_atan2f(m.r2.y, m.r2.z);
+        float pitch_raw;
+        {
+            float x = -m.r2.x;
+            float sq = sqrtf(stdmax(0.f, 1.f - x * x));
+            pitch_raw = rs_asinf(x, sq);
+        }
+        if (fabsf(pitch_raw) == kHalfPi) r0 = r0 > 0 ? r0 - kPi : r0 + kPi;
+        float roll = -r0;
+        float abs_roll = fabsf(roll);
+        if (abs_roll > 2.8f) {
+            cs.auto_flip_timer = 0.4f * (abs_roll / (float)3.14159265358979323846);
+            cs.auto_flip_torque_scale = (roll > 0) ? 1 : -1;
+            cs.is_auto_flipping = 1;
+            apply_central_impulse(A, bi, -col(m, 2) * 200.f * kUU2BT * kCarMass);
+        }
+    }
+    if (cs.is_auto_flipping) {
+        if (cs.auto_flip_timer <= 0) {
+            cs.is_auto_flipping = 0;
+            cs.auto_flip_timer = 0;
+        } else {
+            rlgpu_body* b = body(A, bi);
+            st3(b->angvel, ld3(b->angvel) + col(m, 0) * 50.f * cs.auto_flip_torque_scale * kTick);
+            cs.auto_flip_timer -= kTick;
+        }
+    }
+}
+
+// Car::_UpdateAutoRoll (Car.cpp:799-831)
+DEV void update_auto_roll(ArenaLDS* A, int ci, int nwc) {
+    rlgpu_car& cs = A->s.cars[ci];
+    int bi = ci + 1;
+    v3 gup = nwc > 0 ? upwards_dir_from_wheels(A, ci) : ld3(cs.world_contact_normal);
+    v3 gdown = -gup;
+    m3 R = brot(A, bi);
+    v3 fwd = col(R, 0), right = col(R, 1);
+    v3 cross_right = cross(gup, fwd);
+    v3 cross_fwd = cross(gdown, cross_right);
+    float rtf = 1 - stdclamp(dot(right, cross_right), 0.f, 1.f);
+    float ftf = 1 - stdclamp(dot(fwd, cross_fwd), 0.f, 1.f);
+    v3 tdr = fwd * (dot(right, gup) >= 0 ? -1.f : 1.f);
+    v3 tdf = right * (dot(fwd, gup) >= 0 ? 1.f : -1.f);
+    v3 tr = tdr * rtf, tf = tdf * ftf;
+    add_force(A, bi, gdown * 100.f * kUU2BT * kCarMass);
+    add_torque(A, bi, inverse(A->a.iiw[bi]) * (tf + tr) * 80.f);
+}
+
+// Car::_PreTickUpdate after the wheel phase (Car.cpp:86-131 + btVehicleRL::updateVehicleSecond)
+DEV void car_phase(ArenaLDS* A, int ci) {
+    rlgpu_car& cs = A->s.cars[ci];
+    if (cs.is_demoed) return;
+    int bi = ci + 1;
+    float* ctl = cs.controls;
+    bool jump_pressed = ctl[5] != 0.f && cs.last_controls[5] == 0.f;
+    int nwc = 0;
+    for (int i = 0; i < 4; i++) {
+        cs.wheel_contact[i] = (uint8_t)A->u.wt[ci * 4 + i].in_contact;
+        nwc += A->u.wt[ci * 4 + i].in_contact;
+    }
+    cs.is_on_ground = nwc >= 3;
+    float fwd_speed = dot(bvel(A, bi), col(brot(A, bi), 0)) * kBT2UU;
+    update_wheels(A, ci, nwc, fwd_speed);
+    if (nwc < 3)
+        update_air_torque(A, ci, nwc == 0);
+    else
+        cs.is_flipping = 0;
+    update_jump(A, ci, jump_pressed);
+    update_auto_flip(A, ci, jump_pressed);
+    update_double_jump_or_flip(A, ci, jump_pressed, fwd_speed);
+    if (ctl[0] != 0.f && ((nwc > 0 && nwc < 4) || cs.world_contact)) update_auto_roll(A, ci, nwc);
+    cs.world_contact = 0;
+    for (int i = 0; i < 4; i++) {
+        WheelT& W = A->u.wt[ci * 4 + i];
+        if (W.in_contact) {
+            float force = (C.wheel_rest[i] - W.susp_len) * 500.f * W.clipped_inv;
+            float damp = (W.susp_rel_vel < 0) ? 25.f : 40.f;
+            float sf = force - (damp * W.susp_rel_vel);
+            sf *= C.wheel_force_scale[i];
+            if (sf < 0) sf = 0;
+            W.susp_rel_vel = sf;  // reuse: suspension force
+        } else {
+            W.susp_rel_vel = 0;
+        }
+    }
+    for (int i = 0; i < 4; i++) {
+        WheelT& W = A->u.wt[ci * 4 + i];
+        if (W.susp_rel_vel != 0) {
+            v3 off = W.contact_point - bpos(A, bi);
+            float base = (W.susp_rel_vel * kTick) + cs.wheel_extra_pushback[i];
+            apply_impulse(A, bi, W.contact_normal * base, off);
+        }
+    }
+    {
+        v3 up = col(brot(A, bi), 2);
+        for (int i = 0; i < 4; i++) {
+            WheelT& W = A->u.wt[ci * 4 + i];
+            if (!is_zero(W.impulse)) {
+                v3 off = W.contact_point - bpos(A, bi);
+                float d = dot(up, off);
+                v3 rel = off - up * d;
+                apply_impulse(A, bi, W.impulse * kTick, rel);
+            }
+        }
+    }
+    update_boost(A, ci);
+}
+
+// ------------------------------------------------------------------ car state reset helpers
+DEV void default_car(rlgpu_car& cs) {
+    // CarState defaults (Car.h:17-100); wheel values and controls survive SetState
+    float keep[24 + 8];
+    for (int i = 0; i < 4; i++) {
+        keep[i] = cs.wheel_steer[i];
+        keep[4 + i] = cs.wheel_engine_force[i];
+        keep[8 + i] = cs.wheel_brake[i];
+        keep[12 + i] = cs.wheel_lat_friction[i];
+        keep[16 + i] = cs.wheel_long_friction[i];
+        keep[20 + i] = cs.wheel_extra_pushback[i];
+    }
+    for (int k = 0; k < 8; k++) keep[24 + k] = cs.controls[k];
+    __builtin_memset(&cs, 0, sizeof(rlgpu_car));  // (no type-punned stores: they may be reordered)
+    for (int i = 0; i < 4; i++) {
+        cs.wheel_steer[i] = keep[i];
+        cs.wheel_engine_force[i] = keep[4 + i];
+        cs.wheel_brake[i] = keep[8 + i];
+        cs.wheel_lat_friction[i] = keep[12 + i];
+        cs.wheel_long_friction[i] = keep[16 + i];
+        cs.wheel_extra_pushback[i] = keep[20 + i];
+    }
+    for (int k = 0; k < 8; k++) cs.controls[k] = keep[24 + k];
+    cs.is_on_ground = 1;
+    cs.boost = 100.f / 3.f;
+    cs.ball_hit_tick = -1;
+    cs.ball_hit_extra_tick = -1;
+}
+
+DEV void clear_manifolds_of(ArenaLDS* A, int bodyi);
+
+DEV void set_car_state(ArenaLDS* A, int ci, v3 pos_uu, const m3& rot, float boost, bool on_ground) {
+    rlgpu_car& cs = A->s.cars[ci];
+    default_car(cs);
+    cs.boost = boost;
+    cs.is_on_ground = on_ground;
+    rlgpu_body* b = &cs.body;
+    st3(b->pos, pos_uu * kUU2BT);
+    stm(b->rot, rot);
+    st3(b->vel, zero3());
+    st3(b->angvel, zero3());
+    update_inertia(A, ci + 1);
+    clear_manifolds_of(A, ci + 1);
+}
+
+}  // namespace rl

@@ -1,0 +1,137 @@
+// env_kernel.hpp -- device-side arena simulation for MI355X (gfx950).
+//
+// Layout: each arena is one rlgpu_arena_state record (include/rlgpu_env.h) in HBM.  A
+// 64-thread workgroup (one wavefront) owns kArenas = 4 arenas; the 16 lanes of a quarter-wave
+// ("team") own one arena.  At launch the record is copied whole into LDS with coalesced
+// 16-byte loads, all ticks of the env step run against LDS, and the record is written back
+// once -- HBM traffic is ~2 x 6 KB per arena per env step plus the obs/mask/reward rows.
+//
+// Inside a tick the team runs the phases of Arena::Step
+// (GigaLearnCPP/RLGymCPP/RocketSim/src/Sim/Arena/Arena.cpp:716-812) with lane-level parallelism
+// where the reference has independent work:
+//   * 16 lanes = 4 cars x 4 wheels for the btVehicleRL wheel transforms / suspension rays /
+//     friction impulses (btVehicleRL.cpp:64-369);
+//   * 4 lanes = cars for Car::_PreTickUpdate (Car.cpp:58-131) while 12 lanes tick boost pads;
+//   * 16 lanes over the 35 canonical body pairs for the narrowphase, whose contact candidates
+//     are then committed to the persistent manifolds in canonical order by one lane (contact
+//     callbacks mutate shared state and Bullet processes pairs serially);
+//   * one lane per arena for the order-dependent sequential-impulse solver
+//     (btSequentialImpulseConstraintSolver.cpp:1540-1900), rows staged in LDS;
+//   * 5 lanes = bodies for integration, 34 pads over 16 lanes for pickups.
+// The arithmetic is the CPU oracle's (oracle/rsim_ref.cpp) operation for operation: the
+// product and the oracle are independent implementations of the same reference algorithm,
+// so a strict-FP build makes them agree bit for bit on every tick.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rlgpu_env.h"
+#include "dmath.hpp"
+
+namespace rl {
+
+constexpr int kTeam = 16;           // lanes per arena
+constexpr int kArenas = 4;          // arenas per 64-thread workgroup
+constexpr int kMaxCand = 32;        // narrowphase candidates per tick per arena
+constexpr int kMaxRows = 24;        // solver contact rows per arena (+ as many friction rows)
+constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic
+constexpr float kTick = 1.f / 120.f;
+constexpr float kUU2BT = 1.f / 50.f;
+constexpr float kBT2UU = 50.f;
+constexpr float kCarMass = 180.f;
+constexpr float kBallMass = kCarMass / 6.f;
+
+// Static arena / car constants computed once on the host (env.hip: make_env_const).
+struct EnvConst {
+    float ball_radius, ball_inv_mass, car_inv_mass, ball_cbt, car_cbt, ball_damp, susp_travel;
+    v3 ball_inv_inertia, car_half, car_offset, car_inv_inertia, gravity;
+    v3 wheel_conn[4];
+    float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
+    v3 plane_n[4], plane_p[4];
+    int ntris;
+    v3 tri[40][3];
+    v3 tri_min[40], tri_max[40];
+    float kick_x[5], kick_y[5];
+    m3 kick_rot[2][5];
+    float respawn_x[4], respawn_y[4];
+    m3 respawn_rot[2][4];
+    v3 pad_pos_uu[RLGPU_PADS], pad_pos_bt[RLGPU_PADS], pad_box_min[RLGPU_PADS], pad_box_max[RLGPU_PADS];
+    int pad_big[RLGPU_PADS], pad_cell_x[RLGPU_PADS], pad_cell_y[RLGPU_PADS];
+    int pad_map[RLGPU_PADS];           // CommonValues::BOOST_LOCATIONS -> arena pad (GameState.cpp:11-51)
+    v3 boost_loc[RLGPU_PADS];          // CommonValues::BOOST_LOCATIONS (uu)
+    float action[RLGPU_ACTIONS][8];    // DefaultAction table
+    uint8_t mask_ground[RLGPU_ACTIONS], mask_air[RLGPU_ACTIONS], mask_jump[RLGPU_ACTIONS], mask_boost[RLGPU_ACTIONS];
+    float reward_w[RLGPU_REWARDS];
+};
+
+struct WheelT {
+    v3 hard_point, wheel_dir, contact_point, contact_normal, wt_col1, impulse;
+    float susp_len, susp_rel_vel, clipped_inv;
+    int ground, in_contact, contact_world;
+};
+
+struct Cand {
+    float n[3], p[3], depth;
+    int order;  // pair_rank * 64 + triangle (commit order)
+};
+
+struct SB {  // btSolverBody subset
+    v3 dlin, dang, push, turn, lin, ang, ext_f, ext_t;
+    float inv_mass;
+    int real;
+};
+struct CRow {  // contact row (btSolverConstraint subset)
+    v3 n1, n2, rc1, rc2, angA, angB;
+    float jinv, rhs, rhs_pen, applied, applied_push, friction;
+    int a, b, special, orig;  // orig = manifold slot * 4 + point, or -1
+};
+struct FRow {  // friction row
+    v3 n1, n2, rc1, rc2, angA, angB;
+    float jinv, rhs, applied, friction, lower, upper;
+    int a, b, cidx;
+};
+struct Solver {
+    SB sb[6];
+    CRow rows[kMaxRows];
+    FRow frows[kMaxRows];
+    int nrows;
+    int spec_num[5];
+    float spec_fric[5], spec_rest[5], spec_d[5];
+    v3 spec_n[5];
+};
+
+struct Aux {
+    v3 force[5], torque[5];
+    m3 iiw[5];
+    v3 pred_pos[5];
+    m3 pred_rot[5];
+    v3 snap_vel[5], snap_ang[5];
+    int active[5];
+    int ball_awake, ball_sleep, ncand;
+    int pair_mode[kPairs];  // 0 skip, 1 narrowphase ran, 2 destroy manifold
+    int locked[RLGPU_PADS];
+    int touched[4];
+    int goal;
+    float all_rewards[4];
+};
+
+union Scratch {
+    WheelT wt[16];
+    Cand cand[kMaxCand];
+    Solver sv;
+    struct {
+        float obs[4][RLGPU_OBS];
+        uint8_t masks[4][RLGPU_ACTIONS];
+    } out;
+};
+
+constexpr int kRec = (int)((sizeof(rlgpu_arena_state) + 15) / 16 * 16);  // HBM record stride
+
+struct alignas(16) ArenaLDS {
+    rlgpu_arena_state s;
+    char pad_[kRec - sizeof(rlgpu_arena_state)];
+    Aux a;
+    Scratch u;
+};
+
+}  // namespace rl

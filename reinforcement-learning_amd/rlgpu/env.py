@@ -1,0 +1,171 @@
+"""EnvSet -- Python mirror of RLGC::EnvSet (GigaLearnCPP/RLGymCPP/src/RLGymCPP/EnvSet/EnvSet.h:67-124)
+over the C ABI of include/rlgpu_env.h.  Every arena lives in HBM; the state buffers
+(obs, action masks, rewards, terminals) are exposed as torch tensors that alias the
+library's device memory, so the policy reads observations without a copy.
+
+Method map (reference -> here):
+    EnvSet(config)          EnvSet.cpp:46-111    -> EnvSet(num_arenas, seed, tick_skip, action_delay)
+    StepFirstHalf(async)    EnvSet.cpp:113-130   -> step_first_half()
+    StepSecondHalf(a, async)EnvSet.cpp:132-273   -> step_second_half(actions)
+    Sync()                  EnvSet.h:107         -> sync()
+    Reset()                 EnvSet.cpp:331-354   -> reset()
+    ResetArena(i)           EnvSet.cpp:275-329   -> reset_arenas(mask)
+    state.obs / actionMasks / rewards / terminals EnvSet.h:35-65 -> .obs / .action_masks / ...
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .state import ARENA
+
+OBS, ACTIONS, REWARDS, PADS, CARS = 167, 90, 13, 34, 4
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("num_arenas", ctypes.c_int32), ("tick_skip", ctypes.c_int32), ("action_delay", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("save_rewards", ctypes.c_int32)]
+
+
+class _Buffers(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("action_masks", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("terminals", ctypes.c_void_p), ("last_rewards", ctypes.c_void_p), ("trunc_obs", ctypes.c_void_p),
+                ("num_players", ctypes.c_int32), ("num_arenas", ctypes.c_int32)]
+
+
+_bound = False
+
+
+def _bind():
+    global _bound
+    if _bound:
+        return _lib.lib()
+    L = _lib.lib()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    L.rlgpu_envset_create.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(vp)]
+    L.rlgpu_envset_destroy.argtypes = [vp]
+    L.rlgpu_envset_buffers_get.argtypes = [vp, ctypes.POINTER(_Buffers)]
+    L.rlgpu_envset_reset.argtypes = [vp, vp]
+    L.rlgpu_envset_reset_arenas.argtypes = [vp, vp, vp]
+    L.rlgpu_envset_step_first_half.argtypes = [vp, vp]
+    L.rlgpu_envset_step_second_half.argtypes = [vp, vp, vp]
+    L.rlgpu_envset_step.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    L.rlgpu_envset_sync.argtypes = [vp, vp]
+    L.rlgpu_envset_build_obs.argtypes = [vp, vp]
+    L.rlgpu_envset_get_arenas.argtypes = [vp, i32, i32, vp]
+    L.rlgpu_envset_set_arenas.argtypes = [vp, i32, i32, vp]
+    _bound = True
+    return L
+
+
+def arena_state_size():
+    return _lib.lib().rlgpu_arena_state_size()
+
+
+def _alias(ptr, shape, dtype, device):
+    """torch tensor aliasing library-owned device memory (no copy, no ownership)."""
+    import torch
+    n = int(np.prod(shape))
+    elt = torch.empty((), dtype=dtype).element_size()
+
+    class _Holder:
+        __cuda_array_interface__ = {
+            "shape": (n,), "typestr": {torch.float32: "<f4", torch.uint8: "|u1"}[dtype],
+            "data": (ptr, False), "version": 2, "strides": (elt,)}
+
+    t = torch.as_tensor(_Holder(), device=device)
+    return t.view(*shape)
+
+
+class EnvSet:
+    """Vectorised 2v2 arena set resident in HBM (ExampleMain plugin set: AdvancedObs,
+    DefaultAction, 13 rewards, NoTouch(8 s) + GoalScore(3) terminals, KickoffState)."""
+
+    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, save_rewards=True, device="cuda:0"):
+        import torch
+        if not torch.cuda.is_available():
+            raise _lib.RLGPUError("EnvSet needs an MI355X: the product path has no CPU fallback")
+        L = _bind()
+        self.device = torch.device(device)
+        torch.cuda.set_device(self.device)
+        cfg = _Config(num_arenas, tick_skip, action_delay, seed, int(save_rewards))
+        h = ctypes.c_void_p()
+        _lib.check(L.rlgpu_envset_create(ctypes.byref(cfg), ctypes.byref(h)), "rlgpu_envset_create")
+        self._h = h
+        self.num_arenas = num_arenas
+        self.num_players = 4 * num_arenas
+        self.tick_skip, self.action_delay = tick_skip, action_delay
+        b = _Buffers()
+        _lib.check(L.rlgpu_envset_buffers_get(h, ctypes.byref(b)), "rlgpu_envset_buffers_get")
+        P, dev = self.num_players, self.device
+        self.obs = _alias(b.obs, (P, OBS), torch.float32, dev)
+        self.action_masks = _alias(b.action_masks, (P, ACTIONS), torch.uint8, dev)
+        self.rewards = _alias(b.rewards, (P,), torch.float32, dev)
+        self.terminals = _alias(b.terminals, (num_arenas,), torch.uint8, dev)
+        self.last_rewards = _alias(b.last_rewards, (num_arenas, REWARDS), torch.float32, dev)
+        self.trunc_obs = _alias(b.trunc_obs, (P, OBS), torch.float32, dev)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.check(_lib.lib().rlgpu_envset_destroy(self._h), "rlgpu_envset_destroy")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _actions(actions):
+        import torch
+        _lib.require_gpu_tensor(actions, "actions")
+        if actions.dtype != torch.int32 or not actions.is_contiguous():
+            raise _lib.RLGPUError("actions must be a contiguous int32 device tensor [num_players]")
+        return _lib.ptr(actions)
+
+    def step_first_half(self, stream=None):
+        _lib.check(_lib.lib().rlgpu_envset_step_first_half(self._h, _lib.stream_ptr(stream)), "step_first_half")
+
+    def step_second_half(self, actions, stream=None):
+        _lib.check(_lib.lib().rlgpu_envset_step_second_half(self._h, self._actions(actions), _lib.stream_ptr(stream)),
+                   "step_second_half")
+
+    def step(self, actions, reset_terminated=True, obs_out=None, rew_out=None, term_out=None, stream=None):
+        for t, n in ((obs_out, "obs_out"), (rew_out, "rew_out"), (term_out, "term_out")):
+            _lib.require_gpu_tensor(t, n)
+        _lib.check(_lib.lib().rlgpu_envset_step(self._h, self._actions(actions), int(reset_terminated),
+                                                _lib.ptr(obs_out), _lib.ptr(rew_out), _lib.ptr(term_out),
+                                                _lib.stream_ptr(stream)), "rlgpu_envset_step")
+
+    def sync(self, stream=None):
+        _lib.check(_lib.lib().rlgpu_envset_sync(self._h, _lib.stream_ptr(stream)), "sync")
+
+    def reset(self, stream=None):
+        _lib.check(_lib.lib().rlgpu_envset_reset(self._h, _lib.stream_ptr(stream)), "reset")
+
+    def reset_arenas(self, mask=None, stream=None):
+        _lib.require_gpu_tensor(mask, "mask")
+        _lib.check(_lib.lib().rlgpu_envset_reset_arenas(self._h, _lib.ptr(mask), _lib.stream_ptr(stream)),
+                   "reset_arenas")
+
+    def build_obs(self, stream=None):
+        _lib.check(_lib.lib().rlgpu_envset_build_obs(self._h, _lib.stream_ptr(stream)), "build_obs")
+
+    def get_arenas(self, first=0, count=None):
+        """Wire-format snapshot (uint8 [count * arena_state_size()]) of arenas [first, first+count)."""
+        import torch
+        torch.cuda.synchronize(self.device)
+        count = self.num_arenas - first if count is None else count
+        buf = np.zeros(count * ARENA.itemsize, np.uint8)
+        _lib.check(_lib.lib().rlgpu_envset_get_arenas(self._h, first, count, buf.ctypes.data_as(ctypes.c_void_p)),
+                   "get_arenas")
+        return buf
+
+    def set_arenas(self, buf, first=0):
+        import torch
+        torch.cuda.synchronize(self.device)
+        buf = np.ascontiguousarray(buf, np.uint8)
+        count = buf.size // ARENA.itemsize
+        _lib.check(_lib.lib().rlgpu_envset_set_arenas(self._h, first, count, buf.ctypes.data_as(ctypes.c_void_p)),
+                   "set_arenas")
