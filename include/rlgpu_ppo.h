@@ -1,0 +1,120 @@
+/*
+ * rlgpu_ppo.h -- C ABI for the PPO actor/critic of the MI355X rollout engine.
+ *
+ * Replaces (GigaLearnCPP, libtorch-based):
+ *   GGL::Model  [Linear -> LayerNorm -> LeakyReLU] x k -> Linear
+ *                                   src/private/GigaLearnCPP/Util/Models.cpp:7-69, Models.h:21-163
+ *   PPOLearner::InferActionsFromModels / InferPolicyProbsFromModels
+ *                                   src/private/GigaLearnCPP/PPO/PPOLearner.cpp:78-184
+ *   PPOLearner::InferCritic / InferCriticBatched     PPOLearner.cpp:186-251
+ *   PPOLearner::Learn (minibatch loss + backward, clip_grad_norm_, optimizer step)
+ *                                   PPOLearner.cpp:278-581
+ *   AdamW (libtorch defaults)        Models.h:40-56, torch/csrc/api/src/optim/adamw.cpp
+ *
+ * One handle owns, in HBM: the flat fp32 parameters of every model (torch parameters()
+ * order: per layer Linear.weight [out,in], Linear.bias, LayerNorm.weight, LayerNorm.bias;
+ * then the output Linear), their gradients, AdamW moments, the bf16 inference copy
+ * ("seqHalf", refreshed after every optimizer step) and the activation workspace for
+ * up to cfg.max_rows rows.  Models: 0 = policy (actor), 1 = critic.
+ *
+ * Arithmetic: training forward/backward in fp32 on f32-input MFMA (v_mfma_f32_32x32x2_f32),
+ * inference in bf16 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- the reference's
+ * precision split (Model::Forward: halfPrec only without grad).
+ *
+ * All d_ pointers are device pointers; every call is enqueued on `stream` (NULL = default)
+ * without a host sync unless stated.  Return 0 or a negative rlgpu_status (rlgpu_core.h).
+ */
+#ifndef RLGPU_PPO_H
+#define RLGPU_PPO_H
+
+#include <stdint.h>
+#include "rlgpu_core.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RLGPU_MAX_LAYERS 8
+
+typedef struct {
+    int32_t obs_size;                         /* 167 (AdvancedObs) */
+    int32_t num_actions;                      /* 90 (DefaultAction) */
+    int32_t policy_layers[RLGPU_MAX_LAYERS];  /* hidden sizes, e.g. {512, 512} */
+    int32_t n_policy_layers;
+    int32_t critic_layers[RLGPU_MAX_LAYERS];
+    int32_t n_critic_layers;
+    int32_t layer_norm;                       /* ModelConfig::addLayerNorm (eps 1e-5, affine) */
+    float leaky_slope;                        /* torch::nn::LeakyReLU default 0.01 */
+    float policy_lr, critic_lr;               /* PPOLearnerConfig::policyLR / criticLR */
+    float beta1, beta2, eps, weight_decay;    /* AdamW: 0.9, 0.999, 1e-8, 1e-2 */
+    float clip_range;                         /* 0.2 */
+    float entropy_scale;                      /* 0.035 (ExampleMain) */
+    float max_grad_norm;                      /* 0.5 (PPOLearner.cpp:521-526) */
+    int32_t max_rows;                         /* workspace rows: max(minibatch, inference chunk) */
+    uint64_t seed;                            /* parameter init + action sampling (Philox) */
+} rlgpu_ppo_config;
+
+typedef struct rlgpu_ppo rlgpu_ppo;
+
+/* Metrics accumulated by rlgpu_ppo_minibatch (PPOLearner.cpp:283-296,399-475), one float each,
+ * summed over minibatches; divide by the count (the reference's numAccumulated). */
+enum {
+    RLGPU_M_ENTROPY = 0, RLGPU_M_KL, RLGPU_M_POLICY_LOSS, RLGPU_M_CRITIC_LOSS, RLGPU_M_RATIO,
+    RLGPU_M_CLIP_FRACTION, RLGPU_M_COUNT, RLGPU_M_GRAD_NORM_POLICY, RLGPU_M_GRAD_NORM_CRITIC,
+    RLGPU_NUM_METRICS = 16
+};
+
+int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out);
+int rlgpu_ppo_destroy(rlgpu_ppo* h);
+
+/* Flat fp32 buffers of all models, contiguous (policy first, then critic). */
+int rlgpu_ppo_buffers(rlgpu_ppo* h, float** d_params, float** d_grads, int64_t* num_params);
+/* Offset / count of one model inside the flat buffers. */
+int rlgpu_ppo_model_range(rlgpu_ppo* h, int32_t model, int64_t* offset, int64_t* count);
+/* torch-default init (Linear: U(+-1/sqrt(fan_in)) weight and bias; LayerNorm 1 / 0), Philox. */
+int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream);
+/* Refresh the bf16 inference copy from the fp32 parameters (Model::Forward seqHalf). */
+int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream);
+
+/* Plain forward of one model on n rows (n <= max_rows): precision 0 = fp32 (training path,
+ * no activations kept), 1 = bf16 inference path.  d_out [n, out_size] fp32. */
+int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision, const float* d_in, int32_t n,
+                      float* d_out, void* stream);
+
+/* InferActions: bf16 policy forward, logits + (-1e10)*!mask, softmax, clamp [1e-11, 1],
+ * then argmax (deterministic) or a multinomial draw by inverse CDF on a Philox uniform
+ * (key = cfg.seed, counter = (row, rng_step)).  d_actions int32 [n], d_logp [n] (may be NULL). */
+int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n,
+                            int32_t deterministic, uint64_t rng_step, int32_t* d_actions, float* d_logp,
+                            void* stream);
+/* InferCriticBatched: bf16 critic forward over n rows (any n; chunked by max_rows). */
+int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t n, float* d_values, void* stream);
+
+/* Mean and unbiased std of d_x[n] into d_out[2] (batch advantage normalisation,
+ * PPOLearner.cpp:360-371). */
+int rlgpu_mean_std(const float* d_x, int64_t n, float* d_out, void* stream);
+
+/* One Learn minibatch: rows idx[start..start+n) of the batch (d_index may be NULL = identity)
+ * gathered from d_obs [*, obs_size], d_masks [*, A], d_actions int32, d_old_logp, d_adv,
+ * d_target.  Advantages are normalised with d_adv_stats = (mean, std) as (a - mean)/(std+1e-8).
+ * loss = (policyLoss - entropy*entropy_scale)*n/batch_size + MSE(V, target)*n/batch_size;
+ * gradients are ACCUMULATED into the grad buffer; metrics summed into d_metrics. */
+int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, const int32_t* d_actions,
+                        const float* d_old_logp, const float* d_adv, const float* d_target,
+                        const int32_t* d_index, int64_t start, int32_t n, int64_t batch_size,
+                        const float* d_adv_stats, float* d_metrics, void* stream);
+
+/* clip_grad_norm_(model, max_grad_norm) per model, AdamW step (libtorch semantics), zero
+ * grads, refresh the bf16 copy.  Grad norms written to d_metrics (optional). */
+int rlgpu_ppo_optimizer_step(rlgpu_ppo* h, float* d_metrics, void* stream);
+int rlgpu_ppo_zero_grad(rlgpu_ppo* h, void* stream);
+/* Optimizer state (step count + moments) for checkpointing; moments are device pointers. */
+int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_exp_avg, float** d_exp_avg_sq);
+
+/* Random permutation of [0, n) (Philox keys + device radix sort): ExperienceBuffer shuffle. */
+int rlgpu_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,544 @@
+// ppo.hip -- C ABI of include/rlgpu_ppo.h: actor/critic MLPs, action sampling, PPO minibatch
+// loss + backward, clip_grad_norm_ + AdamW, on hand-written MFMA / wave kernels.
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/rlgpu_ppo.h"
+#include "common.hpp"
+#include "mlp_kernels.hpp"
+#include "ppo_kernels.hpp"
+
+namespace {
+
+using rlgpu::ceil_div;
+
+struct Layer {
+    int in, out;
+    int64_t w, b, g, be;  // offsets into the flat buffers (g/be = -1 without LayerNorm)
+};
+
+struct Model {
+    std::vector<Layer> L;  // hidden layers then the output layer (last)
+    int in, out;
+    int64_t off, count;
+    float lr;
+    // fp32 training workspace
+    std::vector<float*> xhat, act, rstd;
+};
+
+constexpr int kMaxSplits = 64;
+
+}  // namespace
+
+struct rlgpu_ppo {
+    rlgpu_ppo_config cfg;
+    Model M[2];
+    int64_t nparams = 0;
+    float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr;
+    uint16_t* half = nullptr;
+    int64_t step = 0;
+    int hmax = 0;
+    // shared workspace
+    float *out = nullptr, *dout = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr;
+    float *scratch = nullptr;  // clip partials + coefficients
+    uint16_t *zh = nullptr, *ah[2] = {nullptr, nullptr}, *logits_h = nullptr;
+    std::vector<void*> allocs;
+
+    template <class T>
+    T* alloc(size_t count) {
+        void* p = nullptr;
+        RLGPU_CHECK_HIP(hipMalloc(&p, count * sizeof(T) + 16));
+        allocs.push_back(p);
+        return (T*)p;
+    }
+};
+
+namespace {
+
+void gemm_f32(int la, int lb, const float* A, int64_t lda, const int32_t* a_idx, int64_t a_off, const float* B, int64_t ldb,
+              const int32_t* b_idx, int64_t b_off, float* C, int64_t ldc, const float* bias, int I, int J, int K, int splits,
+              hipStream_t s) {
+    mlp::GemmArgs g;
+    g.A = A;
+    g.B = B;
+    g.C = C;
+    g.bias = bias;
+    g.a_idx = a_idx;
+    g.b_idx = b_idx;
+    g.a_off = a_off;
+    g.b_off = b_off;
+    g.lda = lda;
+    g.ldb = ldb;
+    g.ldc = ldc;
+    g.I = I;
+    g.J = J;
+    g.K = K;
+    int chunk = (int)ceil_div(K, splits);
+    g.kchunk = (int)ceil_div(chunk, mlp::BK) * mlp::BK;
+    int z = (int)ceil_div(K, g.kchunk);
+    g.c_split = (int64_t)I * ldc;
+    dim3 grid(ceil_div(J, mlp::BN), ceil_div(I, mlp::BM), z);
+    if (la == mlp::A_IK && lb == mlp::B_JK)
+        hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_IK, mlp::B_JK>), grid, dim3(256), 0, s, g);
+    else if (la == mlp::A_IK && lb == mlp::B_KJ)
+        hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_IK, mlp::B_KJ>), grid, dim3(256), 0, s, g);
+    else if (la == mlp::A_KI && lb == mlp::B_KJ)
+        hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_KI, mlp::B_KJ>), grid, dim3(256), 0, s, g);
+    else
+        throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "gemm layout");
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+int splits_for(int rows) {
+    int s = (int)ceil_div(rows, 1024);
+    return s < 1 ? 1 : (s > kMaxSplits ? kMaxSplits : s);
+}
+
+// dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
+void weight_grad(rlgpu_ppo* h, const float* dZ, int out, const float* X, int64_t ldx, const int32_t* x_idx, int64_t x_off,
+                 int in, int n, float* gW, hipStream_t s) {
+    int splits = splits_for(n);
+    int chunk = (int)ceil_div(ceil_div(n, splits), mlp::BK) * mlp::BK;
+    int z = (int)ceil_div(n, chunk);
+    gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, nullptr, 0, X, ldx, x_idx, x_off, h->wpart, in, nullptr, out, in, n, splits, s);
+    int64_t e = (int64_t)out * in;
+    hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->wpart, z, e, e, gW, 1);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+void colsum_into(rlgpu_ppo* h, const float* X, int n, int C, float* g, hipStream_t s) {
+    int nb = (int)ceil_div(n, mlp::CS_ROWS);
+    hipLaunchKernelGGL(mlp::colsum_partial, dim3(nb), dim3(256), 0, s, X, n, C, h->cpart);
+    hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(C, 256)), dim3(256), 0, s, h->cpart, nb, (int64_t)C, (int64_t)0, C, g);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+// fp32 training forward; keeps activations; writes the output layer to `out`.
+void forward_train(rlgpu_ppo* h, int mi, const float* X, const int32_t* idx, int64_t start, int n, float* out, hipStream_t s) {
+    Model& m = h->M[mi];
+    const float* P = h->params;
+    int nh = (int)m.L.size() - 1;
+    const float* in = X;
+    const int32_t* in_idx = idx;
+    int64_t in_off = start, ld = m.in;
+    for (int l = 0; l < nh; l++) {
+        const Layer& L = m.L[l];
+        gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, in_idx, in_off, P + L.w, L.in, nullptr, 0, m.xhat[l], L.out, P + L.b, n, L.out,
+                 L.in, 1, s);
+        const float* gg = L.g >= 0 ? P + L.g : nullptr;
+        const float* bb = L.be >= 0 ? P + L.be : nullptr;
+        hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, 4)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
+                           h->cfg.leaky_slope, h->cfg.layer_norm, m.xhat[l], m.act[l], m.rstd[l]);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        in = m.act[l];
+        in_idx = nullptr;
+        in_off = 0;
+        ld = L.out;
+    }
+    const Layer& O = m.L[nh];
+    gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, nullptr, 0, P + O.w, O.in, nullptr, 0, out, O.out, P + O.b, n, O.out, O.in, 1, s);
+}
+
+// backward from dout [n, out] into the grad buffer (accumulating)
+void backward(rlgpu_ppo* h, int mi, const float* X, const int32_t* idx, int64_t start, int n, const float* dout, hipStream_t s) {
+    Model& m = h->M[mi];
+    const float* P = h->params;
+    float* G = h->grads;
+    int nh = (int)m.L.size() - 1;
+    const Layer& O = m.L[nh];
+    weight_grad(h, dout, O.out, m.act[nh - 1], O.in, nullptr, 0, O.in, n, G + O.w, s);
+    colsum_into(h, dout, n, O.out, G + O.b, s);
+    // dA = dout . W_out
+    gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, nullptr, 0, P + O.w, O.in, nullptr, 0, h->dA, O.in, nullptr, n, O.in, O.out, 1,
+             s);
+    for (int l = nh - 1; l >= 0; l--) {
+        const Layer& L = m.L[l];
+        int nb = (int)ceil_div(n, mlp::LNB_ROWS);
+        const float* gg = L.g >= 0 ? P + L.g : nullptr;
+        const float* bb = L.be >= 0 ? P + L.be : nullptr;
+        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, h->dA, m.xhat[l], m.rstd[l], gg, bb, n, L.out,
+                           h->cfg.leaky_slope, h->cfg.layer_norm, h->dZ, h->cpart);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        int64_t st = 3 * (int64_t)L.out;
+        dim3 rg(ceil_div(L.out, 256));
+        if (h->cfg.layer_norm) {
+            hipLaunchKernelGGL(mlp::reduce_cols, rg, dim3(256), 0, s, h->cpart, nb, st, (int64_t)0, L.out, G + L.g);
+            hipLaunchKernelGGL(mlp::reduce_cols, rg, dim3(256), 0, s, h->cpart, nb, st, (int64_t)L.out, L.out, G + L.be);
+        }
+        hipLaunchKernelGGL(mlp::reduce_cols, rg, dim3(256), 0, s, h->cpart, nb, st, 2 * (int64_t)L.out, L.out, G + L.b);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        if (l == 0)
+            weight_grad(h, h->dZ, L.out, X, m.in, idx, start, L.in, n, G + L.w, s);
+        else
+            weight_grad(h, h->dZ, L.out, m.act[l - 1], L.in, nullptr, 0, L.in, n, G + L.w, s);
+        if (l > 0)
+            gemm_f32(mlp::A_IK, mlp::B_KJ, h->dZ, L.out, nullptr, 0, P + L.w, L.in, nullptr, 0, h->dA, L.in, nullptr, n, L.in,
+                     L.out, 1, s);
+    }
+}
+
+// bf16 inference forward of n rows; result in h->logits_h [n, out] (bf16)
+void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s) {
+    Model& m = h->M[mi];
+    const uint16_t* P = h->half;
+    int nh = (int)m.L.size() - 1;
+    const void* in = X;
+    bool in_f32 = true;
+    int64_t ld = m.in;
+    int cur = 0;
+    for (int l = 0; l <= nh; l++) {
+        const Layer& L = m.L[l];
+        mlp::HGemmArgs g;
+        g.A = in;
+        g.B = P + L.w;
+        g.bias = P + L.b;
+        g.C = l < nh ? h->zh : h->logits_h;
+        g.lda = ld;
+        g.ldb = L.in;
+        g.ldc = L.out;
+        g.I = n;
+        g.J = L.out;
+        g.K = L.in;
+        dim3 grid(ceil_div(L.out, mlp::BN), ceil_div(n, mlp::BM));
+        if (in_f32)
+            hipLaunchKernelGGL(mlp::gemm_bf16<true>, grid, dim3(256), 0, s, g);
+        else
+            hipLaunchKernelGGL(mlp::gemm_bf16<false>, grid, dim3(256), 0, s, g);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        if (l == nh) break;
+        const uint16_t* gg = L.g >= 0 ? P + L.g : nullptr;
+        const uint16_t* bb = L.be >= 0 ? P + L.be : nullptr;
+        hipLaunchKernelGGL(mlp::ln_act_fwd_bf16_any(L.out), dim3(ceil_div(n, 4)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
+                           h->cfg.leaky_slope, h->cfg.layer_norm, h->ah[cur]);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        in = h->ah[cur];
+        in_f32 = false;
+        ld = L.out;
+        cur ^= 1;
+    }
+}
+
+void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, int out, float lr) {
+    m.in = in;
+    m.out = out;
+    m.lr = lr;
+    m.off = h->nparams;
+    int prev = in;
+    for (int l = 0; l <= nl; l++) {
+        Layer L;
+        L.in = prev;
+        L.out = l < nl ? layers[l] : out;
+        L.w = h->nparams;
+        h->nparams += (int64_t)L.in * L.out;
+        L.b = h->nparams;
+        h->nparams += L.out;
+        L.g = L.be = -1;
+        if (l < nl && h->cfg.layer_norm) {
+            L.g = h->nparams;
+            h->nparams += L.out;
+            L.be = h->nparams;
+            h->nparams += L.out;
+        }
+        if (L.out > h->hmax) h->hmax = L.out;
+        if (L.in > h->hmax && l > 0) h->hmax = L.in;
+        m.L.push_back(L);
+        prev = L.out;
+    }
+    m.count = h->nparams - m.off;
+}
+
+void sumsq_coef(rlgpu_ppo* h, const float* x, int64_t n, float max_norm, float* coef, float* norm_out, hipStream_t s) {
+    const int nb = 512;
+    hipLaunchKernelGGL(ppo::sumsq_partial, dim3(nb), dim3(256), 0, s, x, n, h->scratch);
+    hipLaunchKernelGGL(ppo::clip_coef, dim3(1), dim3(64), 0, s, h->scratch, nb, max_norm, coef, norm_out);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+void refresh_half(rlgpu_ppo* h, hipStream_t s) {
+    hipLaunchKernelGGL(ppo::to_half, dim3(ceil_div(h->nparams, 256)), dim3(256), 0, s, h->params, h->half, h->nparams);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(cfg && out, "rlgpu_ppo_create: null argument");
+        RLGPU_REQUIRE(cfg->obs_size > 0 && cfg->num_actions > 0 && cfg->num_actions <= ppo::kMaxA,
+                      "num_actions must be in [1, 128]");
+        RLGPU_REQUIRE(cfg->n_policy_layers >= 1 && cfg->n_policy_layers <= RLGPU_MAX_LAYERS && cfg->n_critic_layers >= 1 &&
+                          cfg->n_critic_layers <= RLGPU_MAX_LAYERS,
+                      "1..8 hidden layers per model");
+        RLGPU_REQUIRE(cfg->max_rows > 0, "max_rows must be > 0");
+        for (int i = 0; i < cfg->n_policy_layers; i++)
+            RLGPU_REQUIRE(cfg->policy_layers[i] > 0 && cfg->policy_layers[i] <= 1024, "hidden sizes must be in [1, 1024]");
+        for (int i = 0; i < cfg->n_critic_layers; i++)
+            RLGPU_REQUIRE(cfg->critic_layers[i] > 0 && cfg->critic_layers[i] <= 1024, "hidden sizes must be in [1, 1024]");
+        auto* h = new rlgpu_ppo();
+        try {
+            h->cfg = *cfg;
+            build_model(h, h->M[0], cfg->obs_size, cfg->policy_layers, cfg->n_policy_layers, cfg->num_actions, cfg->policy_lr);
+            build_model(h, h->M[1], cfg->obs_size, cfg->critic_layers, cfg->n_critic_layers, 1, cfg->critic_lr);
+            int64_t P = h->nparams, R = cfg->max_rows;
+            h->params = h->alloc<float>(P);
+            h->grads = h->alloc<float>(P);
+            h->exp_avg = h->alloc<float>(P);
+            h->exp_avg_sq = h->alloc<float>(P);
+            h->half = h->alloc<uint16_t>(P);
+            RLGPU_CHECK_HIP(hipMemset(h->params, 0, P * 4));
+            RLGPU_CHECK_HIP(hipMemset(h->grads, 0, P * 4));
+            RLGPU_CHECK_HIP(hipMemset(h->exp_avg, 0, P * 4));
+            RLGPU_CHECK_HIP(hipMemset(h->exp_avg_sq, 0, P * 4));
+            for (auto& m : h->M) {
+                int nh = (int)m.L.size() - 1;
+                for (int l = 0; l < nh; l++) {
+                    m.xhat.push_back(h->alloc<float>(R * m.L[l].out));
+                    m.act.push_back(h->alloc<float>(R * m.L[l].out));
+                    m.rstd.push_back(h->alloc<float>(R));
+                }
+            }
+            int H = h->hmax;
+            int omax = cfg->num_actions > 1 ? cfg->num_actions : 1;
+            h->out = h->alloc<float>(R * omax);
+            h->dout = h->alloc<float>(R * omax);
+            h->dA = h->alloc<float>(R * H);
+            h->dZ = h->alloc<float>(R * H);
+            int64_t wmax = 0;
+            for (auto& m : h->M)
+                for (auto& L : m.L) wmax = std::max<int64_t>(wmax, (int64_t)L.in * L.out);
+            h->wpart = h->alloc<float>(kMaxSplits * wmax);
+            int64_t nb = ceil_div(R, std::min(mlp::LNB_ROWS, mlp::CS_ROWS));
+            h->cpart = h->alloc<float>(nb * 3 * std::max(H, omax));
+            h->scratch = h->alloc<float>(1024);
+            h->zh = h->alloc<uint16_t>(R * H);
+            h->ah[0] = h->alloc<uint16_t>(R * H);
+            h->ah[1] = h->alloc<uint16_t>(R * H);
+            h->logits_h = h->alloc<uint16_t>(R * omax);
+            *out = h;
+        } catch (...) {
+            for (void* p : h->allocs) (void)hipFree(p);
+            delete h;
+            throw;
+        }
+    });
+}
+
+extern "C" int rlgpu_ppo_destroy(rlgpu_ppo* h) {
+    return rlgpu::guarded([&] {
+        if (!h) return;
+        for (void* p : h->allocs) (void)hipFree(p);
+        delete h;
+    });
+}
+
+extern "C" int rlgpu_ppo_buffers(rlgpu_ppo* h, float** d_params, float** d_grads, int64_t* num_params) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h, "null handle");
+        if (d_params) *d_params = h->params;
+        if (d_grads) *d_grads = h->grads;
+        if (num_params) *num_params = h->nparams;
+    });
+}
+
+extern "C" int rlgpu_ppo_model_range(rlgpu_ppo* h, int32_t model, int64_t* offset, int64_t* count) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && (model == 0 || model == 1), "model must be 0 (policy) or 1 (critic)");
+        if (offset) *offset = h->M[model].off;
+        if (count) *count = h->M[model].count;
+    });
+}
+
+extern "C" int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h, "null handle");
+        hipStream_t s = rlgpu::as_stream(stream);
+        uint32_t sid = 0;
+        for (auto& m : h->M)
+            for (auto& L : m.L) {
+                float bound = 1.f / std::sqrt((float)L.in);
+                int64_t nw = (int64_t)L.in * L.out;
+                hipLaunchKernelGGL(ppo::init_uniform, dim3(ceil_div(nw, 256)), dim3(256), 0, s, h->params + L.w, nw, bound, seed,
+                                   sid++);
+                hipLaunchKernelGGL(ppo::init_uniform, dim3(ceil_div(L.out, 256)), dim3(256), 0, s, h->params + L.b,
+                                   (int64_t)L.out, bound, seed, sid++);
+                if (L.g >= 0) {
+                    hipLaunchKernelGGL(ppo::fill, dim3(ceil_div(L.out, 256)), dim3(256), 0, s, h->params + L.g, (int64_t)L.out,
+                                       1.f);
+                    hipLaunchKernelGGL(ppo::fill, dim3(ceil_div(L.out, 256)), dim3(256), 0, s, h->params + L.be, (int64_t)L.out,
+                                       0.f);
+                }
+            }
+        RLGPU_CHECK_HIP(hipGetLastError());
+        refresh_half(h, s);
+    });
+}
+
+extern "C" int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h, "null handle");
+        refresh_half(h, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision, const float* d_in, int32_t n, float* d_out,
+                                 void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_in && d_out, "null argument");
+        RLGPU_REQUIRE(model == 0 || model == 1, "model must be 0 or 1");
+        RLGPU_REQUIRE(n >= 0 && n <= h->cfg.max_rows, "n must be in [0, max_rows]");
+        if (n == 0) return;
+        hipStream_t s = rlgpu::as_stream(stream);
+        if (precision == 0) {
+            forward_train(h, model, d_in, nullptr, 0, n, d_out, s);
+        } else {
+            forward_half(h, model, d_in, n, s);
+            int64_t e = (int64_t)n * h->M[model].out;
+            hipLaunchKernelGGL(ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->logits_h, d_out, e);
+            RLGPU_CHECK_HIP(hipGetLastError());
+        }
+    });
+}
+
+extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n,
+                                       int32_t deterministic, uint64_t rng_step, int32_t* d_actions, float* d_logp,
+                                       void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_obs && d_masks && d_actions, "null argument");
+        RLGPU_REQUIRE(n >= 0, "n must be >= 0");
+        hipStream_t s = rlgpu::as_stream(stream);
+        int R = h->cfg.max_rows;
+        for (int64_t b = 0; b < n; b += R) {
+            int m = (int)std::min<int64_t>(R, n - b);
+            forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s);
+            hipLaunchKernelGGL(ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
+                               d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
+                               rng_step, d_actions + b, d_logp ? d_logp + b : nullptr);
+            RLGPU_CHECK_HIP(hipGetLastError());
+        }
+    });
+}
+
+extern "C" int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t n, float* d_values, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_obs && d_values, "null argument");
+        hipStream_t s = rlgpu::as_stream(stream);
+        int R = h->cfg.max_rows;
+        for (int64_t b = 0; b < n; b += R) {
+            int m = (int)std::min<int64_t>(R, n - b);
+            forward_half(h, 1, d_obs + b * h->cfg.obs_size, m, s);
+            hipLaunchKernelGGL(ppo::bf16_to_f32, dim3(ceil_div(m, 256)), dim3(256), 0, s, h->logits_h, d_values + b,
+                               (int64_t)m);
+            RLGPU_CHECK_HIP(hipGetLastError());
+        }
+    });
+}
+
+extern "C" int rlgpu_mean_std(const float* d_x, int64_t n, float* d_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(d_x && d_out && n > 0, "rlgpu_mean_std: bad argument");
+        hipStream_t s = rlgpu::as_stream(stream);
+        const int nb = 256;
+        double* part = nullptr;
+        RLGPU_CHECK_HIP(hipMallocAsync((void**)&part, nb * 2 * sizeof(double), s));
+        hipLaunchKernelGGL(ppo::moments_partial, dim3(nb), dim3(256), 0, s, d_x, n, part);
+        hipLaunchKernelGGL(ppo::moments_final, dim3(1), dim3(64), 0, s, part, nb, n, d_out);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        RLGPU_CHECK_HIP(hipFreeAsync(part, s));
+    });
+}
+
+extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, const int32_t* d_actions,
+                                   const float* d_old_logp, const float* d_adv, const float* d_target, const int32_t* d_index,
+                                   int64_t start, int32_t n, int64_t batch_size, const float* d_adv_stats, float* d_metrics,
+                                   void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_obs && d_masks && d_actions && d_old_logp && d_adv && d_target && d_adv_stats,
+                      "rlgpu_ppo_minibatch: null argument");
+        RLGPU_REQUIRE(n > 0 && n <= h->cfg.max_rows, "minibatch rows must be in [1, max_rows]");
+        RLGPU_REQUIRE(batch_size > 0, "batch_size must be > 0");
+        hipStream_t s = rlgpu::as_stream(stream);
+        float bsr = (float)n / (float)batch_size;  // PPOLearner.cpp:374
+        int A = h->cfg.num_actions;
+        // policy
+        forward_train(h, 0, d_obs, d_index, start, n, h->out, s);
+        hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, 4)), dim3(256), 0, s, h->out, d_masks, d_actions, d_old_logp,
+                           d_adv, d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
+                           1.f / std::log((float)A), h->dout, d_metrics);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        backward(h, 0, d_obs, d_index, start, n, h->dout, s);
+        // critic
+        forward_train(h, 1, d_obs, d_index, start, n, h->out, s);
+        hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, s, h->out, d_target, d_index, start, n, bsr,
+                           h->dout, d_metrics);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        backward(h, 1, d_obs, d_index, start, n, h->dout, s);
+    });
+}
+
+extern "C" int rlgpu_ppo_optimizer_step(rlgpu_ppo* h, float* d_metrics, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h, "null handle");
+        hipStream_t s = rlgpu::as_stream(stream);
+        h->step++;
+        const auto& c = h->cfg;
+        double bc1 = 1.0 - std::pow((double)c.beta1, (double)h->step);
+        double bc2 = 1.0 - std::pow((double)c.beta2, (double)h->step);
+        for (int mi = 0; mi < 2; mi++) {
+            Model& m = h->M[mi];
+            float* coef = h->scratch + 600 + mi;
+            float* norm_out = d_metrics ? d_metrics + (mi == 0 ? RLGPU_M_GRAD_NORM_POLICY : RLGPU_M_GRAD_NORM_CRITIC) : nullptr;
+            sumsq_coef(h, h->grads + m.off, m.count, c.max_grad_norm, coef, norm_out, s);
+            double lr = m.lr;
+            float decay_mul = (float)(1.0 - lr * (double)c.weight_decay);
+            float step_size = (float)(lr / bc1);
+            float bc2_sqrt = (float)std::sqrt(bc2);
+            hipLaunchKernelGGL(ppo::adamw, dim3(ceil_div(m.count, 256)), dim3(256), 0, s, h->params + m.off, h->grads + m.off,
+                               h->exp_avg + m.off, h->exp_avg_sq + m.off, h->half + m.off, m.count, coef, decay_mul, c.beta1,
+                               c.beta2, 1.f - c.beta1, 1.f - c.beta2, step_size, bc2_sqrt, c.eps);
+            RLGPU_CHECK_HIP(hipGetLastError());
+        }
+    });
+}
+
+extern "C" int rlgpu_ppo_zero_grad(rlgpu_ppo* h, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h, "null handle");
+        RLGPU_CHECK_HIP(hipMemsetAsync(h->grads, 0, h->nparams * sizeof(float), rlgpu::as_stream(stream)));
+    });
+}
+
+extern "C" int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_exp_avg, float** d_exp_avg_sq) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h, "null handle");
+        if (step) *step = h->step;
+        if (d_exp_avg) *d_exp_avg = h->exp_avg;
+        if (d_exp_avg_sq) *d_exp_avg_sq = h->exp_avg_sq;
+    });
+}
+
+extern "C" int rlgpu_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t* d_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(d_out && n >= 0 && n < (1ll << 31), "rlgpu_permutation: bad argument");
+        if (n == 0) return;
+        hipStream_t s = rlgpu::as_stream(stream);
+        uint32_t *k0 = nullptr, *k1 = nullptr;
+        int32_t* v0 = nullptr;
+        RLGPU_CHECK_HIP(hipMallocAsync((void**)&k0, n * 4, s));
+        RLGPU_CHECK_HIP(hipMallocAsync((void**)&k1, n * 4, s));
+        RLGPU_CHECK_HIP(hipMallocAsync((void**)&v0, n * 4, s));
+        hipLaunchKernelGGL(ppo::perm_keys, dim3(ceil_div(n, 256)), dim3(256), 0, s, k0, v0, n, seed, (uint32_t)counter);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        size_t tmp_bytes = 0;
+        RLGPU_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, v0, d_out, (int)n, 0, 32, s));
+        void* tmp = nullptr;
+        RLGPU_CHECK_HIP(hipMallocAsync(&tmp, tmp_bytes + 16, s));
+        RLGPU_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, v0, d_out, (int)n, 0, 32, s));
+        RLGPU_CHECK_HIP(hipFreeAsync(tmp, s));
+        RLGPU_CHECK_HIP(hipFreeAsync(k0, s));
+        RLGPU_CHECK_HIP(hipFreeAsync(k1, s));
+        RLGPU_CHECK_HIP(hipFreeAsync(v0, s));
+    });
+}

@@ -1,0 +1,292 @@
+// ppo_kernels.hpp -- policy head, PPO losses and optimizer kernels (gfx950, one wave per row).
+// Semantics follow GigaLearnCPP PPOLearner.cpp (InferPolicyProbsFromModels :78-112,
+// InferActionsFromModels :114-184, Learn :278-581) with the libtorch op semantics spelled out
+// where they matter (clamp / min tie gradients, softmax backward, AdamW, clip_grad_norm_).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mlp_kernels.hpp"
+
+namespace ppo {
+
+using mlp::bf2f;
+using mlp::wave_max;
+using mlp::wave_sum;
+
+constexpr float kMinProb = 1e-11f;        // ACTION_MIN_PROB
+constexpr float kDisabledLogit = -1e10f;  // ACTION_DISABLED_LOGIT
+constexpr int kMaxA = 128;                // actions per row: 2 per lane
+
+__device__ __forceinline__ uint32_t philox(uint64_t key, uint32_t c0, uint32_t c1) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    uint32_t x0 = c0, x1 = c1, x2 = 0x2545F491u, x3 = 0x4F6CDD1Du;
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+        uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0, y1 = (uint32_t)p1, y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1,
+                 y3 = (uint32_t)p0;
+        x0 = y0;
+        x1 = y1;
+        x2 = y2;
+        x3 = y3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return x0;
+}
+
+// masked softmax of one row held 2 per lane (actions 2l, 2l+1); returns probs (unclamped)
+__device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool v1, float& p0, float& p1) {
+    float m = wave_max(fmaxf(v0 ? z0 : -INFINITY, v1 ? z1 : -INFINITY));
+    float e0 = v0 ? __expf(z0 - m) : 0.f, e1 = v1 ? __expf(z1 - m) : 0.f;
+    float s = wave_sum(e0 + e1);
+    p0 = e0 / s;
+    p1 = e1 / s;
+}
+
+// InferActions: logits bf16 [n, A] -> action (int32), log prob.  Inverse-CDF multinomial on the
+// clamped probs (torch.multinomial normalises by their sum); argmax when deterministic.
+__global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
+                                                     int deterministic, uint64_t seed, uint64_t step, int32_t* act,
+                                                     float* logp) {
+    int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= n) return;
+    int a0 = 2 * lane, a1 = 2 * lane + 1;
+    const uint16_t* lg = logits + (int64_t)row * A;
+    const uint8_t* mk = masks + (int64_t)row * A;
+    bool in0 = a0 < A, in1 = a1 < A;
+    float z0 = in0 ? bf2f(lg[a0]) + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
+    float z1 = in1 ? bf2f(lg[a1]) + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
+    // softmax over all A columns (masked ones carry -1e10, exactly as the reference)
+    float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
+    float e0 = in0 ? __expf(z0 - m) : 0.f, e1 = in1 ? __expf(z1 - m) : 0.f;
+    float s = wave_sum(e0 + e1);
+    float p0 = in0 ? fminf(fmaxf(e0 / s, kMinProb), 1.f) : 0.f;
+    float p1 = in1 ? fminf(fmaxf(e1 / s, kMinProb), 1.f) : 0.f;
+    int pick;
+    if (deterministic) {
+        float best = fmaxf(p0, p1);
+        int bi = p0 >= p1 ? a0 : a1;
+        for (int o = 32; o > 0; o >>= 1) {
+            float ob = __shfl_xor(best, o, 64);
+            int oi = __shfl_xor(bi, o, 64);
+            if (ob > best || (ob == best && oi < bi)) {
+                best = ob;
+                bi = oi;
+            }
+        }
+        pick = bi;
+    } else {
+        float pair = p0 + p1, inc = pair;
+        for (int o = 1; o < 64; o <<= 1) {
+            float up = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += up;
+        }
+        float total = __shfl(inc, 63, 64);
+        float u = (float)(philox(seed, (uint32_t)row, (uint32_t)step) >> 8) * (1.f / 16777216.f) * total;
+        float excl = inc - pair;
+        bool hit = (u < inc) && (u >= excl) && pair > 0.f;
+        unsigned long long bal = __ballot(hit);
+        int lsel = bal ? __ffsll((long long)bal) - 1 : 0;
+        if (!bal) {  // u landed past the last positive pair by rounding: take the last valid action
+            unsigned long long nz = __ballot(pair > 0.f);
+            lsel = 63 - __clzll((long long)nz);
+        }
+        int c = 2 * lsel;
+        float e = __shfl(excl, lsel, 64), q0 = __shfl(p0, lsel, 64), q1 = __shfl(p1, lsel, 64);
+        pick = (u < e + q0 || q1 == 0.f) ? c : c + 1;
+    }
+    float pp0 = __shfl(p0, pick >> 1, 64), pp1 = __shfl(p1, pick >> 1, 64);
+    if (lane == 0) {
+        act[row] = pick;
+        if (logp) logp[row] = __logf((pick & 1) ? pp1 : pp0);
+    }
+}
+
+// PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.
+// Rows are minibatch-ordered; sample s = idx ? idx[start + r] : start + r addresses the
+// batch buffers.  scale_pl = bsr / n (d loss / d min(surr1,surr2) = -scale_pl).
+__global__ void __launch_bounds__(256) policy_loss(const float* logits, const uint8_t* masks, const int32_t* actions,
+                                                  const float* old_logp, const float* adv, const int32_t* idx, int64_t start,
+                                                  int n, int A, const float* adv_stats, float bsr, float clip_range,
+                                                  float ent_scale, float inv_log_a, float* dlogits, float* metrics) {
+    int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= n) return;
+    int64_t s = idx ? (int64_t)idx[start + row] : start + row;
+    int a0 = 2 * lane, a1 = 2 * lane + 1;
+    bool in0 = a0 < A, in1 = a1 < A;
+    const float* lg = logits + (int64_t)row * A;
+    const uint8_t* mk = masks + s * A;
+    float z0 = in0 ? lg[a0] + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
+    float z1 = in1 ? lg[a1] + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
+    float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
+    float e0 = in0 ? expf(z0 - m) : 0.f, e1 = in1 ? expf(z1 - m) : 0.f;
+    float sum = wave_sum(e0 + e1);
+    float p0 = e0 / sum, p1 = e1 / sum;
+    float c0 = fminf(fmaxf(p0, kMinProb), 1.f), c1 = fminf(fmaxf(p1, kMinProb), 1.f);
+    float l0 = in0 ? logf(c0) : 0.f, l1 = in1 ? logf(c1) : 0.f;
+    float ent = -wave_sum((in0 ? l0 * c0 : 0.f) + (in1 ? l1 * c1 : 0.f));
+    int a = actions[s];
+    a = a < 0 ? 0 : (a > A - 1 ? A - 1 : a);
+    float pa = __shfl((a & 1) ? c1 : c0, a >> 1, 64);
+    float lp = logf(pa);
+    float old = old_logp[s];
+    float ratio = expf(lp - old);
+    float advn = (adv[s] - adv_stats[0]) / (adv_stats[1] + 1e-8f);
+    float clipped = fminf(fmaxf(ratio, 1.f - clip_range), 1.f + clip_range);
+    float s1 = ratio * advn, s2 = clipped * advn;
+    float pl = fminf(s1, s2);
+    // ---- backward
+    float g_pl = -bsr / (float)n;
+    float g_s1 = s1 < s2 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
+    float g_s2 = s2 < s1 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
+    float in_rng = (ratio >= 1.f - clip_range && ratio <= 1.f + clip_range) ? 1.f : 0.f;
+    float g_ratio = g_s1 * advn + g_s2 * advn * in_rng;
+    float g_lp = g_ratio * ratio;
+    float g_ent = -ent_scale * bsr * inv_log_a / (float)n;  // d loss / d H_i (H_i unnormalised)
+    // d/dc_j: entropy term -g_ent*(log c_j + 1) ; log-prob term g_lp / c_a at j == a
+    float d0 = in0 ? -g_ent * (l0 + 1.f) : 0.f, d1 = in1 ? -g_ent * (l1 + 1.f) : 0.f;
+    if (a == a0) d0 += g_lp / c0;
+    if (a == a1) d1 += g_lp / c1;
+    // clamp backward (pass where min <= p <= max)
+    d0 = (p0 >= kMinProb && p0 <= 1.f) ? d0 : 0.f;
+    d1 = (p1 >= kMinProb && p1 <= 1.f) ? d1 : 0.f;
+    float dot = wave_sum((in0 ? d0 * p0 : 0.f) + (in1 ? d1 * p1 : 0.f));
+    float* dl = dlogits + (int64_t)row * A;
+    if (in0) dl[a0] = p0 * (d0 - dot);
+    if (in1) dl[a1] = p1 * (d1 - dot);
+    if (lane == 0 && metrics) {
+        float lr = lp - old;
+        float inv_n = 1.f / (float)n;
+        atomicAdd(&metrics[0], ent * inv_log_a * inv_n);                      // entropy
+        atomicAdd(&metrics[1], (expf(lr) - 1.f - lr) * inv_n);                // KL
+        atomicAdd(&metrics[2], -pl * inv_n);                                  // policy loss
+        atomicAdd(&metrics[4], ratio * inv_n);                                // ratio
+        atomicAdd(&metrics[5], (fabsf(ratio - 1.f) > clip_range ? 1.f : 0.f) * inv_n);  // clip fraction
+    }
+}
+
+// Critic MSE: loss = mean((v - t)^2) * bsr ; dv = 2 (v - t) / n * bsr.
+__global__ void critic_loss(const float* vals, const float* target, const int32_t* idx, int64_t start, int n, float bsr,
+                            float* dvals, float* metrics) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    float contrib = 0.f;
+    if (r < n) {
+        int64_t s = idx ? (int64_t)idx[start + r] : start + r;
+        float d = vals[r] - target[s];
+        dvals[r] = 2.f * d / (float)n * bsr;
+        contrib = d * d / (float)n * bsr;
+    }
+    contrib = wave_sum(contrib);
+    if ((threadIdx.x & 63) == 0 && metrics) atomicAdd(&metrics[3], contrib);
+}
+
+// sum of squares partials (fixed grid -> deterministic)
+__global__ void __launch_bounds__(256) sumsq_partial(const float* x, int64_t n, float* part) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) s += x[e] * x[e];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// clip_grad_norm_: coef = min(max_norm / (||g|| + 1e-6), 1) (torch/csrc/api/src/nn/utils/clip_grad.h)
+__global__ void clip_coef(const float* part, int nblk, float max_norm, float* coef, float* norm_out) {
+    if (threadIdx.x != 0) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; b++) s += part[b];
+    float norm = sqrtf(s);
+    float c = max_norm / (norm + 1e-6f);
+    *coef = c < 1.f ? c : 1.f;
+    if (norm_out) *norm_out = norm;
+}
+
+// AdamW step, libtorch semantics (torch/csrc/api/src/optim/adamw.cpp): grads pre-scaled by the
+// clip coefficient; grads zeroed after use; bf16 copy refreshed.
+__global__ void adamw(float* p, float* g, float* m, float* v, uint16_t* half, int64_t n, const float* coef, float decay_mul,
+                      float beta1, float beta2, float one_m_b1, float one_m_b2, float step_size, float bc2_sqrt, float eps) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    float gr = g[e] * *coef;
+    float pv = p[e] * decay_mul;
+    float mv = m[e] * beta1 + gr * one_m_b1;
+    float vv = v[e] * beta2 + one_m_b2 * gr * gr;
+    float denom = sqrtf(vv) / bc2_sqrt + eps;
+    pv = pv + (-step_size) * (mv / denom);
+    p[e] = pv;
+    m[e] = mv;
+    v[e] = vv;
+    g[e] = 0.f;
+    half[e] = mlp::f2bf(pv);
+}
+
+__global__ void to_half(const float* p, uint16_t* h, int64_t n) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) h[e] = mlp::f2bf(p[e]);
+}
+
+__global__ void bf16_to_f32(const uint16_t* h, float* f, int64_t n) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) f[e] = bf2f(h[e]);
+}
+
+// torch-default Linear init U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (kaiming_uniform a=sqrt(5) for
+// weights, the same bound for biases); LayerNorm weight 1, bias 0.
+__global__ void init_uniform(float* p, int64_t n, float bound, uint64_t seed, uint32_t stream_id) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    float u = (float)(philox(seed, (uint32_t)e, stream_id) >> 8) * (1.f / 16777216.f);
+    p[e] = (2.f * u - 1.f) * bound;
+}
+__global__ void fill(float* p, int64_t n, float v) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) p[e] = v;
+}
+
+// mean / unbiased std (fp64 accumulation): part[blk] = (sum, sumsq)
+__global__ void __launch_bounds__(256) moments_partial(const float* x, int64_t n, double* part) {
+    __shared__ double red[2][256];
+    double s = 0, s2 = 0;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        double v = x[e];
+        s += v;
+        s2 += v * v;
+    }
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = red[0][0];
+        part[2 * blockIdx.x + 1] = red[1][0];
+    }
+}
+__global__ void moments_final(const double* part, int nblk, int64_t n, float* out) {
+    if (threadIdx.x != 0) return;
+    double s = 0, s2 = 0;
+    for (int b = 0; b < nblk; b++) {
+        s += part[2 * b];
+        s2 += part[2 * b + 1];
+    }
+    double mean = s / (double)n;
+    double var = n > 1 ? (s2 - s * mean) / (double)(n - 1) : 0.0;
+    out[0] = (float)mean;
+    out[1] = (float)sqrt(var > 0 ? var : 0.0);
+}
+
+__global__ void perm_keys(uint32_t* keys, int32_t* vals, int64_t n, uint64_t seed, uint32_t counter) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    keys[e] = philox(seed, (uint32_t)e, counter);
+    vals[e] = (int32_t)e;
+}
+
+}  // namespace ppo

@@ -7,6 +7,8 @@ and is never imported from here.)
 import ctypes
 import os
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librlgpu.so")
 _lib = None
@@ -50,3 +52,18 @@ def stream_ptr(stream=None):
 def require_gpu_tensor(t, name):
     if t is not None and not t.is_cuda:
         raise RLGPUError(f"{name} must be a device (HBM) tensor; the product path has no CPU fallback")
+
+
+def alias(ptr, shape, dtype, device):
+    """torch tensor aliasing library-owned device memory (no copy, no ownership)."""
+    import torch
+    n = int(np.prod(shape))
+    elt = torch.empty((), dtype=dtype).element_size()
+
+    class _Holder:
+        __cuda_array_interface__ = {
+            "shape": (n,), "typestr": {torch.float32: "<f4", torch.uint8: "|u1", torch.int32: "<i4"}[dtype],
+            "data": (ptr, False), "version": 2, "strides": (elt,)}
+
+    t = torch.as_tensor(_Holder(), device=device)
+    return t.view(*shape)

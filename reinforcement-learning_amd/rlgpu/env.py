@@ -17,6 +17,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
+from ._lib import alias as _alias
 from .state import ARENA
 
 OBS, ACTIONS, REWARDS, PADS, CARS = 167, 90, 13, 34, 4
@@ -60,21 +61,6 @@ def _bind():
 
 def arena_state_size():
     return _lib.lib().rlgpu_arena_state_size()
-
-
-def _alias(ptr, shape, dtype, device):
-    """torch tensor aliasing library-owned device memory (no copy, no ownership)."""
-    import torch
-    n = int(np.prod(shape))
-    elt = torch.empty((), dtype=dtype).element_size()
-
-    class _Holder:
-        __cuda_array_interface__ = {
-            "shape": (n,), "typestr": {torch.float32: "<f4", torch.uint8: "|u1"}[dtype],
-            "data": (ptr, False), "version": 2, "strides": (elt,)}
-
-    t = torch.as_tensor(_Holder(), device=device)
-    return t.view(*shape)
 
 
 class EnvSet:

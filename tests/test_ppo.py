@@ -1,0 +1,223 @@
+"""PPO actor/critic (include/rlgpu_ppo.h) against a plain PyTorch fp32 restatement of the
+reference's libtorch code (GigaLearnCPP PPOLearner.cpp:78-184 and :341-529, Models.cpp:7-69).
+
+libtorch itself is not vendored and unpinned -> this CPU torch restatement is the
+checker; tolerances are written per test: fp32 training path rtol 1e-4 (summation order of the
+MFMA GEMMs differs from torch's), bf16 inference path 2e-2 of the output scale.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from rlgpu.ppo import param_count
+
+
+# ------------------------------------------------------------------ CPU: known answers
+def test_param_count_known_answers():
+    """run_out.log:36-39: shared head [384,384] / policy [384]x3 / critic [384]x3."""
+    assert param_count(167, 0, [384, 384], out=0) == 213_888
+    assert param_count(384, 90, [384, 384, 384]) == 480_474
+    assert param_count(384, 1, [384, 384, 384], out=1) == 446_209
+
+
+def test_param_count_c2():
+    a = param_count(167, 90, [512, 512])
+    c = param_count(167, 1, [512, 512], out=1)
+    assert (a, c, a + c) == (396_890, 351_233, 748_123)
+
+
+# ------------------------------------------------------------------ torch reference
+def torch_models(ppo):
+    return ppo.torch_module(0), ppo.torch_module(1)
+
+
+def ref_minibatch(pol, crit, obs, masks, acts, old_logp, adv, target, batch_size, clip=0.2, ent_scale=0.035):
+    """PPOLearner::Learn minibatch body (PPOLearner.cpp:341-475), fp32 torch."""
+    import torch
+    n = obs.shape[0]
+    bsr = n / float(batch_size)
+    logits = pol(obs)
+    logits = logits + -1e10 * masks.bool().logical_not()
+    probs = torch.softmax(logits, -1).clamp(1e-11, 1.0)
+    logp = probs.gather(-1, acts.long().unsqueeze(-1)).squeeze(-1).log()
+    ent = -(probs.log() * probs).sum(-1) / math.log(probs.shape[1])
+    ent = ent.mean()
+    ratio = (logp - old_logp).exp()
+    clipped = ratio.clamp(1 - clip, 1 + clip)
+    pl = -torch.min(ratio * adv, clipped * adv).mean()
+    ppo_loss = (pl - ent * ent_scale) * bsr
+    vals = crit(obs).flatten()
+    closs = torch.nn.functional.mse_loss(vals, target) * bsr
+    (ppo_loss + closs).backward()
+    return {"entropy": ent.item(), "policy_loss": pl.item(), "critic_loss": closs.item(),
+            "ratio": ratio.mean().item()}
+
+
+def flat_grads(*mods):
+    import torch
+    return torch.cat([p.grad.reshape(-1) for m in mods for p in m.parameters()])
+
+
+def make_batch(rng, n, obs_size=167, A=90):
+    obs = rng.standard_normal((n, obs_size)).astype(np.float32)
+    masks = (rng.random((n, A)) < 0.6).astype(np.uint8)
+    masks[:, 0] = 1
+    acts = np.array([rng.choice(np.nonzero(m)[0]) for m in masks], np.int32)
+    old = (np.log(1 / 40.0) + 0.3 * rng.standard_normal(n)).astype(np.float32)
+    adv = rng.standard_normal(n).astype(np.float32)
+    tgt = rng.standard_normal(n).astype(np.float32)
+    return obs, masks, acts, old, adv, tgt
+
+
+@pytest.mark.gpu
+def test_forward_fp32_matches_torch(gpu):
+    import torch
+    from rlgpu.ppo import PPO
+    p = PPO(max_rows=2048, seed=3)
+    pol, crit = torch_models(p)
+    x = torch.randn(1000, 167)
+    for m, ref in ((0, pol), (1, crit)):
+        got = p.forward(m, x.to(gpu)).cpu()
+        want = ref(x).detach()
+        np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_forward_bf16_close_to_fp32(gpu):
+    import torch
+    from rlgpu.ppo import PPO
+    p = PPO(max_rows=4096, seed=5)
+    pol, crit = torch_models(p)
+    x = torch.randn(3000, 167)
+    for m, ref in ((0, pol), (1, crit)):
+        got = p.forward(m, x.to(gpu), half=True).cpu().numpy()
+        want = ref(x).detach().numpy()
+        scale = np.abs(want).max()
+        assert np.abs(got - want).max() <= 2e-2 * scale + 1e-3, (m, np.abs(got - want).max(), scale)
+        want_h = ref.to(torch.bfloat16)(x.to(torch.bfloat16)).float().detach().numpy()
+        assert np.abs(got - want_h).max() <= 2e-2 * scale + 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,batch", [(300, 600), (1029, 1029)])
+def test_minibatch_grads_match_torch(gpu, n, batch):
+    import torch
+    from rlgpu.ppo import PPO
+    rng = np.random.default_rng(n)
+    p = PPO(max_rows=2048, seed=7)
+    pol, crit = torch_models(p)
+    obs, masks, acts, old, adv, tgt = make_batch(rng, n)
+    T = lambda a: torch.from_numpy(a)  # noqa: E731
+    advn = (adv - adv.mean()) / (adv.std(ddof=1) + 1e-8)
+    ref = ref_minibatch(pol, crit, T(obs), T(masks), T(acts), T(old), T(advn.astype(np.float32)), T(tgt), batch)
+    d = {k: T(v).to(gpu) for k, v in dict(obs=obs, masks=masks, acts=acts, old=old, adv=adv, tgt=tgt).items()}
+    p.adv_normalizer(d["adv"])
+    p.zero_grad()
+    p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], None, 0, n, batch)
+    got = p.grads.cpu()
+    want = flat_grads(pol, crit)
+    scale = want.abs().max().item()
+    err = (got - want).abs()
+    assert (err <= 1e-3 * want.abs() + 1e-4 * scale).all(), f"max err {err.max().item()} scale {scale}"
+    rep = p.read_metrics()
+    assert abs(rep["Policy Entropy"] - ref["entropy"]) < 1e-4
+    assert abs(rep["Policy Loss"] - ref["policy_loss"]) < 1e-4 * max(1, abs(ref["policy_loss"]))
+    assert abs(rep["Critic Loss"] - ref["critic_loss"]) < 1e-4 * max(1, abs(ref["critic_loss"]))
+
+
+@pytest.mark.gpu
+def test_minibatch_gather_and_accumulation(gpu):
+    """Two minibatches through a permutation index accumulate the same gradient as one."""
+    import torch
+    from rlgpu.ppo import PPO, permutation
+    rng = np.random.default_rng(11)
+    n = 512
+    obs, masks, acts, old, adv, tgt = make_batch(rng, n)
+    d = {k: torch.from_numpy(v).to(gpu) for k, v in dict(obs=obs, masks=masks, acts=acts, old=old, adv=adv,
+                                                              tgt=tgt).items()}
+    p = PPO(max_rows=1024, seed=9)
+    p.adv_normalizer(d["adv"])
+    idx = permutation(n, 5, 0)
+    assert torch.equal(torch.sort(idx.long()).values.cpu(), torch.arange(n))
+    p.zero_grad()
+    p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], idx, 0, 256, n)
+    p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], idx, 256, 256, n)
+    g2 = p.grads.clone()
+    p.zero_grad()
+    p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], None, 0, n, n)
+    g1 = p.grads.clone()
+    scale = g1.abs().max().item()
+    assert ((g1 - g2).abs() <= 1e-3 * g1.abs() + 1e-4 * scale).all()
+
+
+@pytest.mark.gpu
+def test_optimizer_step_matches_torch_adamw(gpu):
+    import torch
+    from rlgpu.ppo import PPO
+    rng = np.random.default_rng(13)
+    p = PPO(max_rows=1024, seed=15, policy_lr=1e-3, critic_lr=5e-4)
+    pol, crit = torch_models(p)
+    opts = [torch.optim.AdamW(pol.parameters(), lr=1e-3), torch.optim.AdamW(crit.parameters(), lr=5e-4)]
+    for it in range(3):
+        obs, masks, acts, old, adv, tgt = make_batch(rng, 400)
+        T = lambda a: torch.from_numpy(a)  # noqa: E731
+        advn = (adv - adv.mean()) / (adv.std(ddof=1) + 1e-8)
+        for o in opts:
+            o.zero_grad(set_to_none=True)
+        ref_minibatch(pol, crit, T(obs), T(masks), T(acts), T(old), T(advn.astype(np.float32)), T(tgt), 400)
+        torch.nn.utils.clip_grad_norm_(pol.parameters(), 0.5)
+        torch.nn.utils.clip_grad_norm_(crit.parameters(), 0.5)
+        for o in opts:
+            o.step()
+        d = [torch.from_numpy(v).to(gpu) for v in (obs, masks, acts, old, adv, tgt)]
+        p.adv_normalizer(d[4])
+        p.minibatch(*d, None, 0, 400, 400)
+        p.optimizer_step()
+    want = torch.cat([q.detach().reshape(-1) for m in (pol, crit) for q in m.parameters()])
+    got = p.params.cpu()
+    # Adam divides by sqrt(v): coordinates whose gradient is ~0 get an update of O(lr) whose sign
+    # follows rounding noise, so a handful may differ by a fraction of lr; all others agree tightly.
+    diff = np.abs(got.numpy() - want.numpy())
+    tight = diff <= 1e-4 * np.abs(want.numpy()) + 2e-6
+    assert tight.mean() > 0.9999, tight.mean()
+    assert diff.max() < 0.1 * 1e-3, diff.max()
+    assert float(p.grads.abs().max()) == 0.0  # zero_grad after the step
+
+
+@pytest.mark.gpu
+def test_infer_actions_respect_masks_and_distribution(gpu):
+    import torch
+    from rlgpu.ppo import PPO
+    p = PPO(max_rows=8192, seed=17)
+    rng = np.random.default_rng(3)
+    obs, masks, *_ = make_batch(rng, 4096)
+    o, m = torch.from_numpy(obs).to(gpu), torch.from_numpy(masks).to(gpu)
+    a, lp = p.infer_actions(o, m, step=1)
+    a = a.cpu().numpy()
+    assert (masks[np.arange(4096), a] == 1).all()
+    logits = p.forward(0, o, half=True).cpu()
+    probs = torch.softmax(logits + -1e10 * torch.from_numpy(masks == 0), -1).clamp(1e-11, 1).numpy()
+    np.testing.assert_allclose(lp.cpu().numpy(), np.log(probs[np.arange(4096), a]), rtol=1e-3, atol=1e-4)
+    ad, _ = p.infer_actions(o, m, deterministic=True)
+    np.testing.assert_array_equal(ad.cpu().numpy(), probs.argmax(1))
+    # one row sampled many times: empirical frequencies ~ probs
+    row = np.repeat(obs[:1], 8192, 0)
+    rm = np.repeat(masks[:1], 8192, 0)
+    counts = np.zeros(90)
+    for s in range(4):
+        aa, _ = p.infer_actions(torch.from_numpy(row).to(gpu), torch.from_numpy(rm).to(gpu), step=100 + s)
+        counts += np.bincount(aa.cpu().numpy(), minlength=90)
+    freq = counts / counts.sum()
+    pr = probs[0] / probs[0].sum()
+    assert np.abs(freq - pr).max() < 0.02
+
+
+@pytest.mark.gpu
+def test_mean_std(gpu):
+    import torch
+    from rlgpu.ppo import PPO
+    p = PPO(max_rows=64, seed=1)
+    x = torch.randn(100_003) * 3 + 1
+    st = p.adv_normalizer(x.to(gpu)).cpu().numpy()
+    np.testing.assert_allclose(st, [x.mean().item(), x.std().item()], rtol=1e-5)
