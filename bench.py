@@ -1,13 +1,16 @@
-"""bench.py -- BASELINE.json metric on MI355X: env-steps/s (whole job) for the C2 workload
-(4096 arenas per GPU, 2v2, tickSkip 8 / actionDelay 7, ExampleMain plugin set).
+"""bench.py -- BASELINE.json metric on MI355X: env-steps/s (whole job) and PPO wall-clock per
+1M agent-steps for the C2 workload: 4096 arenas per GPU (2v2, tickSkip 8 / actionDelay 7,
+ExampleMain plugin set), rollout T = 128, actor/critic MLP [512, 512] (bf16 inference, fp32
+training), PPO epochs 2, minibatch 50k, AdamW.
 
 Contract (driver): python bench.py --gpus N --steps K --warmup W ; for N > 1 launched by
-torch.distributed.run, one rank per GPU.  Rank 0 prints ONE JSON line.
+torch.distributed.run, one rank per GPU over RCCL.  Rank 0 prints ONE JSON line.
 
-A "step" here is one env step of every arena on every rank: the fused HIP env kernel
-(7 + 1 physics ticks, rewards, terminals, obs, masks, reset-if-terminal) with the actions of
-that step already resident in HBM.  Arenas shard across ranks with no data-path collective
-(weak scaling); the barrier + max-over-ranks timing follows the contract.
+A "step" is one PPO iteration of every rank: T = 128 env steps of all arenas (bf16 policy
+inference + fused env kernel with experience append), critic over the rollout, GAE, then
+Learn (2 epochs of shuffled 50k minibatches, fp32 forward/backward, RCCL gradient all-reduce
+for N > 1, clip_grad_norm_, AdamW).  value = env-steps/s summed over ranks (weak scaling:
+4096 arenas per GPU).  Synthetic inputs: random-init weights (seed 123), Philox kickoffs.
 """
 import argparse
 import json
@@ -23,14 +26,19 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 ARENAS_PER_GPU = 4096   # BASELINE configs[1] (C2)
 
 
-def env_bytes_per_step(arena_state_size):
-    """B_env = 2*S_arena + 16 (actions) + 2672 (obs) + 360 (masks) + 16 (rewards) + 1 (terminal)."""
-    return 2 * arena_state_size + 16 + 4 * 167 * 4 + 4 * 90 + 16 + 1
+def env_bytes_per_step(arena_state_size, append=True):
+    """B_env = 2*S_arena + 16 (actions) + 2672 (obs) + 360 (masks) + 16 (rewards) + 1
+    (terminal); the fused step's experience append writes the obs / mask / reward / terminal rows a
+    second time into the rollout buffer (+2672 + 360 + 16 + 4)."""
+    b = 2 * arena_state_size + 16 + 4 * 167 * 4 + 4 * 90 + 16 + 1
+    if append:
+        b += 4 * 167 * 4 + 4 * 90 + 16 + 4
+    return b
 
 
 def cpu_baseline(seconds=12.0, arenas=256):
     """The CPU restatement (oracle/, reference threading model: contiguous arena chunks over a
-    pool) timed on this box's host cores on a bounded sample of the same workload."""
+    pool) timed on this box's host cores on a bounded sample of the same env workload."""
     import numpy as np
     import oracle
     cores = min(16, os.cpu_count() or 1)  # the box's CPU share is 16 (gpurun)
@@ -47,16 +55,17 @@ def cpu_baseline(seconds=12.0, arenas=256):
         if el >= seconds:
             break
     return {"value": arenas * steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{arenas} arenas x {steps} env steps (oracle/ CPU restatement, {cores} threads, "
-                      f"random valid actions)"}
+            "sample": f"env only: {arenas} arenas x {steps} env steps of the oracle/ CPU restatement "
+                      f"({cores} threads, uniform valid actions); no policy / PPO on CPU"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=3, help="timed PPO iterations")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed PPO iterations")
     ap.add_argument("--arenas", type=int, default=ARENAS_PER_GPU)
+    ap.add_argument("--rollout", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -65,40 +74,42 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
     if world > 1:
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from rlgpu.env import EnvSet, arena_state_size
-    n = args.arenas
-    env = EnvSet(n, seed=1234 + 1000003 * rank, device=dev)
-    gen = torch.Generator(device=dev).manual_seed(7 + rank)
-    P = 4 * n
-    # actions for every step drawn up front (uniform over valid actions is mask-dependent, so
-    # draw per-step uniforms now and pick inside the loop with one fused torch op)
-    total = args.warmup + args.steps
-    uni = torch.rand((min(total, 32), P, 90), device=dev, generator=gen)
-    acts = torch.empty(P, dtype=torch.int32, device=dev)
+    from rlgpu.env import arena_state_size
+    from rlgpu.learner import Learner, LearnerConfig
+    cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout)
+    L = Learner(cfg, device=dev, rank=rank, world=world)
 
-    def one_step(i, e0=None, e1=None):
-        acts.copy_(torch.argmax(uni[i % uni.shape[0]] * env.action_masks, dim=1))
-        if e0 is not None:
-            e0.record()
-        env.step(acts, True)
-        if e1 is not None:
-            e1.record()
-
-    for i in range(args.warmup):
-        one_step(i)
+    for _ in range(args.warmup):
+        L.iterate()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    L.env_events = []
+    phase = {"collect": 0.0, "consume": 0.0, "learn": 0.0}
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(args.warmup + i, *evs[i])
+    for _ in range(args.steps):
+        a = time.perf_counter()
+        L.collect()
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        L.consume()
+        torch.cuda.synchronize()
+        c = time.perf_counter()
+        L.learn()
+        L.obs[0].copy_(L.obs[L.T])
+        L.masks[0].copy_(L.masks[L.T])
+        L.iteration += 1
+        torch.cuda.synchronize()
+        d = time.perf_counter()
+        phase["collect"] += b - a
+        phase["consume"] += c - b
+        phase["learn"] += d - c
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -108,22 +119,29 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    value = world * n * args.steps / el
+    env_steps = world * args.arenas * cfg.rollout_len * args.steps
+    agent_steps = 4 * env_steps
+    value = env_steps / el
+    kern_ms = sum(x.elapsed_time(y) for x, y in L.env_events) / len(L.env_events)
     b_env = env_bytes_per_step(arena_state_size())
-    achieved = b_env * n / (kern_ms * 1e-3) / 1e9
+    achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
     out = {
         "metric": "env-steps/sec (whole node) at 32768 arenas; PPO wall-clock per 1M steps",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "C2 env collection: 4096 arenas/GPU 2v2, tickSkip 8 / actionDelay 7, "
-                               "AdvancedObs+DefaultAction+13 rewards, uniform valid actions",
-                   "arenas_per_gpu": n, "agents_per_gpu": P, "parallelism": f"arena-sharded x{world}"},
-        "agent_steps_per_s": 4 * value,
+        "config": {"workload": "C2: 4096 arenas/GPU 2v2 RocketSim-equivalent physics, tickSkip 8 / actionDelay 7, "
+                               "AdvancedObs + DefaultAction(90) + 13 ExampleMain rewards; PPO actor/critic [512,512] "
+                               "LayerNorm+LeakyReLU, bf16 inference / fp32 training, T=128, 2 epochs, minibatch 50k",
+                   "arenas_per_gpu": args.arenas, "agents_per_gpu": 4 * args.arenas, "rollout_len": cfg.rollout_len,
+                   "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32"},
+        "agent_steps_per_s": agent_steps / el,
+        "ppo_s_per_1M_agent_steps": el / agent_steps * 1e6,
+        "phase_s_per_iteration": {k: v / args.steps for k, v in phase.items()},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "rl::env_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": b_env},
+                     "kernel": "rl::env_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": b_env,
+                     "units_per_launch": args.arenas},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()

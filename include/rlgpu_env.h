@@ -113,6 +113,8 @@ typedef struct {
     uint8_t ev_bump[RLGPU_CARS], ev_bumped[RLGPU_CARS], ev_demo[RLGPU_CARS], ev_demoed[RLGPU_CARS];
     uint32_t rng_counter;        /* Philox counter for this arena's draws */
     uint32_t manifold_overflow;  /* contacts dropped because all slots were busy */
+    int32_t episode_steps;       /* steps in the current trajectory (Learner maxEpisodeLength) */
+    int32_t reserved0;
 } rlgpu_env_extra;
 
 /* Complete serialised arena (the wire format of rlgpu_envset_get/set_arenas). */
@@ -132,7 +134,18 @@ typedef struct {
     int32_t action_delay;    /* LearnerConfig::actionDelay = tickSkip-1 (ExampleMain.cpp:358) */
     uint64_t seed;           /* Philox key: kickoff shuffles and demo respawns */
     int32_t save_rewards;    /* keep per-reward values of player 0 (EnvSetConfig::saveRewards) */
+    int32_t max_episode_steps; /* trajectory truncation (Learner.cpp:550,848): 0 = off; ExampleMain
+                                  maxEpisodeDuration 300 s -> 300*120/tickSkip = 4500 */
 } rlgpu_envset_config;
+
+/* Experience-append destinations of the fused step (Learner.cpp:823-861); any may be NULL. */
+typedef struct {
+    float* obs;          /* [players][OBS] obs after the step (post-reset): rollout row t+1 */
+    uint8_t* masks;      /* [players][ACTIONS] masks after the step (post-reset) */
+    float* rewards;      /* [players] */
+    int8_t* terminals;   /* [players] trajectory codes 0 / 1 NORMAL / 2 TRUNCATED (incl. max length) */
+    float* trunc_obs;    /* [players][OBS] obs before the reset, written where the code is 2 */
+} rlgpu_step_outputs;
 
 typedef struct rlgpu_envset rlgpu_envset;
 
@@ -161,13 +174,11 @@ int rlgpu_envset_reset_arenas(rlgpu_envset* env, const uint8_t* d_mask, void* st
 /* Two-half step with the reference's action delay. */
 int rlgpu_envset_step_first_half(rlgpu_envset* env, void* stream);
 int rlgpu_envset_step_second_half(rlgpu_envset* env, const int32_t* d_actions, void* stream);
-/* Fused: first half + second half + (optional) reset of terminated arenas in one launch.
- * Experience append (GigaLearnCPP Learner.cpp:180-260 collection loop): if non-NULL,
- * d_obs_out receives the post-reset obs rows [players x OBS] (the rollout buffer row for
- * step t+1), d_rew_out the rewards [players], d_term_out the terminal codes [arenas].
- * Pre-reset obs of TRUNCATED arenas go to buffers.trunc_obs. Requires action_delay > 0. */
+/* Fused: first half + second half + (optional) reset of terminated arenas in one launch, plus
+ * the experience append into `out` (may be NULL).  buffers.trunc_obs also receives the
+ * pre-reset rows of trajectories ending TRUNCATED.  Requires action_delay > 0. */
 int rlgpu_envset_step(rlgpu_envset* env, const int32_t* d_actions, int32_t reset_terminated,
-                      float* d_obs_out, float* d_rew_out, uint8_t* d_term_out, void* stream);
+                      const rlgpu_step_outputs* out, void* stream);
 int rlgpu_envset_sync(rlgpu_envset* env, void* stream);
 
 /* Wire-format state transfer (host <-> device), for GameState snapshots, tests and replay. */

@@ -78,7 +78,7 @@ def arena_state_size():
 class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
-    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1):
+    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0):
         L = lib()
         L.oracle_env_create.restype = ctypes.c_void_p
         L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -93,6 +93,10 @@ class EnvSet:
         self.L = L
         self.n = num_arenas
         self.h = L.oracle_env_create(num_arenas, seed, tick_skip, action_delay, threads)
+        L.oracle_env_set_max_episode_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_env_read_traj_terms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_env_set_max_episode_steps(self.h, max_episode_steps)
+        self.traj_terms = np.zeros(4 * num_arenas, np.int8)
         P = 4 * num_arenas
         self.obs = np.zeros((P, OBS), np.float32)
         self.masks = np.zeros((P, ACTIONS), np.uint8)
@@ -108,6 +112,8 @@ class EnvSet:
             self.h = None
 
     def read(self):
+        if hasattr(self, "traj_terms"):
+            self.L.oracle_env_read_traj_terms(self.h, _p(self.traj_terms))
         self.L.oracle_env_read(self.h, _p(self.obs), _p(self.masks), _p(self.rewards), _p(self.terminals),
                                _p(self.trunc_obs), _p(self.last_rewards))
 

@@ -374,6 +374,8 @@ struct StepOut {
     float* rewards;
     uint8_t* terminal;
     float* last_rewards;  // [RLGPU_REWARDS] of player 0 (may be null)
+    int8_t* traj_term;    // [4] trajectory codes (Learner.cpp:829-861), may be null
+    int max_episode_steps;
 };
 
 // GameState::UpdateFromArena + terminals + rewards + obs/masks (EnvSet.cpp:157-270)
@@ -413,6 +415,13 @@ void second_half_builders(rlgpu_arena_state& s, const StepOut& out, int tick_ski
         if (t_score) term = 1;  // NORMAL dominates (EnvSet.cpp:167-180)
     }
     e.terminal = term;
+    // trajectory-level code: maxEpisodeLength truncates without an arena reset (Learner.cpp:848-850)
+    e.episode_steps++;
+    int8_t tj = (int8_t)term;
+    if (!tj && out.max_episode_steps > 0 && e.episode_steps >= out.max_episode_steps) tj = 2;
+    if (tj) e.episode_steps = 0;
+    if (out.traj_term)
+        for (int i = 0; i < 4; i++) out.traj_term[i] = tj;
     // PreStep: LosingPenaltyReward
     if (goal) {
         if (bpos.y > 0) e.penalty_blue++;
@@ -540,6 +549,7 @@ void reset_arena(rlgpu_arena_state& s, uint64_t seed, int idx, float* obs, uint8
     e.penalty_blue = e.penalty_orange = 0;
     e.has_prev = 0;
     e.terminal = 0;
+    e.episode_steps = 0;
     std::memset(e.prev_action, 0, sizeof e.prev_action);
     for (int i = 0; i < 4; i++) e.ev_bump[i] = e.ev_bumped[i] = e.ev_demo[i] = e.ev_demoed[i] = 0;
     bool touched[4] = {false, false, false, false};  // fresh CarState: ballHitInfo invalid
@@ -604,6 +614,8 @@ struct EnvSet {
     std::vector<rlgpu_arena_state> arenas;
     std::vector<float> obs, trunc_obs, rewards, last_rewards;
     std::vector<uint8_t> masks, terminals;
+    std::vector<int8_t> traj_terms;
+    int max_episode_steps = 0;
     Pool* pool = nullptr;
     ~EnvSet() { delete pool; }
     void par(std::function<void(int)> f) {
@@ -617,7 +629,7 @@ struct EnvSet {
     }
     StepOut out(int i) {
         return {&obs[(size_t)i * 4 * RLGPU_OBS], &masks[(size_t)i * 4 * RLGPU_ACTIONS], &rewards[(size_t)i * 4], &terminals[i],
-                &last_rewards[(size_t)i * RLGPU_REWARDS]};
+                &last_rewards[(size_t)i * RLGPU_REWARDS], &traj_terms[(size_t)i * 4], max_episode_steps};
     }
 };
 
@@ -641,6 +653,7 @@ void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action
     e->rewards.assign((size_t)num_arenas * 4, 0.f);
     e->last_rewards.assign((size_t)num_arenas * RLGPU_REWARDS, 0.f);
     e->terminals.assign(num_arenas, 0);
+    e->traj_terms.assign((size_t)num_arenas * 4, 0);
     if (threads > 1) e->pool = new Pool(threads);
     for (int i = 0; i < num_arenas; i++) {
         rlgpu_arena_state& s = e->arenas[i];
@@ -707,10 +720,8 @@ void oracle_env_step(void* h, const int32_t* actions, int reset_terminated) {
         first_half(s, e->seed, i, e->action_delay);
         StepOut o = e->out(i);
         second_half(s, e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, o);
-        if (reset_terminated && *o.terminal) {
-            if (*o.terminal == 2) std::memcpy(&e->trunc_obs[(size_t)i * 4 * RLGPU_OBS], o.obs, sizeof(float) * 4 * RLGPU_OBS);
-            reset_arena(s, e->seed, i, o.obs, o.masks);
-        }
+        if (o.traj_term[0] == 2) std::memcpy(&e->trunc_obs[(size_t)i * 4 * RLGPU_OBS], o.obs, sizeof(float) * 4 * RLGPU_OBS);
+        if (reset_terminated && *o.terminal) reset_arena(s, e->seed, i, o.obs, o.masks);
     });
 }
 
@@ -731,6 +742,13 @@ void oracle_env_read(void* h, float* obs, uint8_t* masks, float* rewards, uint8_
     if (terminals) std::memcpy(terminals, e->terminals.data(), e->terminals.size());
     if (trunc_obs) std::memcpy(trunc_obs, e->trunc_obs.data(), e->trunc_obs.size() * sizeof(float));
     if (last_rewards) std::memcpy(last_rewards, e->last_rewards.data(), e->last_rewards.size() * sizeof(float));
+}
+
+void oracle_env_set_max_episode_steps(void* h, int n) { ((EnvSet*)h)->max_episode_steps = n; }
+
+void oracle_env_read_traj_terms(void* h, int8_t* out) {
+    EnvSet* e = (EnvSet*)h;
+    std::memcpy(out, e->traj_terms.data(), e->traj_terms.size());
 }
 
 // Known-answer helpers for tests.

@@ -30,9 +30,12 @@ struct StepArgs {
     uint8_t* terminals;
     float* last_rewards;
     float* trunc_obs;
-    float* obs_out;
-    float* rew_out;
-    uint8_t* term_out;
+    float* out_obs;        // experience append (rlgpu_step_outputs), each may be null
+    uint8_t* out_masks;
+    float* out_rew;
+    int8_t* out_term;
+    float* out_trunc;
+    int max_episode_steps;
     uint64_t seed;
 };
 
@@ -234,23 +237,18 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
     sync();
 }
 
-// obs / mask rows of all 4 players into LDS, then coalesced copy to the output rows
-DEV void build_and_copy_obs(ArenaLDS* A, int l, bool valid, int arena, const StepArgs& g, float* obs_dst2) {
-    if (valid && l < 4) build_obs_row(A, l);
-    sync();
-    if (valid) {
+// copy the 4 obs rows (and mask rows) of this arena from LDS to [players x OBS] outputs
+DEV void copy_rows(ArenaLDS* A, int l, int arena, float* obs, uint8_t* masks) {
+    if (obs) {
         const float* src = &A->u.out.obs[0][0];
-        float* dst = g.obs + (size_t)arena * 4 * RLGPU_OBS;
+        float* dst = obs + (size_t)arena * 4 * RLGPU_OBS;
         for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
-        if (obs_dst2) {
-            float* d2 = obs_dst2 + (size_t)arena * 4 * RLGPU_OBS;
-            for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) d2[k] = src[k];
-        }
+    }
+    if (masks) {
         const uint8_t* msrc = &A->u.out.masks[0][0];
-        uint8_t* mdst = g.masks + (size_t)arena * 4 * RLGPU_ACTIONS;
+        uint8_t* mdst = masks + (size_t)arena * 4 * RLGPU_ACTIONS;
         for (int k = l; k < 4 * RLGPU_ACTIONS; k += kTeam) mdst[k] = msrc[k];
     }
-    sync();
 }
 
 __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
@@ -349,6 +347,13 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
                 if (by > 0) e.penalty_blue++;
                 else e.penalty_orange++;
             }
+            // trajectory-level code (Learner.cpp:829-861): max episode length truncates the
+            // trajectory without resetting the arena
+            e.episode_steps++;
+            uint8_t tj = tt;
+            if (!tj && g.max_episode_steps > 0 && e.episode_steps >= g.max_episode_steps) tj = 2;
+            if (tj) e.episode_steps = 0;
+            A->a.traj_term = tj;
         }
         sync();
         if (valid && l < 4) {
@@ -364,42 +369,42 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             A->a.all_rewards[l] = all;
         }
         sync();
-        if (valid && l == 0) {
+        if (valid && l < 4) {
+            float r = A->a.all_rewards[l];
+            g.rewards[arena * 4 + l] = r;
+            if (g.out_rew) g.out_rew[arena * 4 + l] = r;
+            if (g.out_term) g.out_term[arena * 4 + l] = (int8_t)A->a.traj_term;
+        }
+        uint8_t tj = 0;
+        if (valid) {
             term = A->s.env.terminal;
-            for (int i = 0; i < 4; i++) {
-                g.rewards[arena * 4 + i] = A->a.all_rewards[i];
-                if (g.rew_out) g.rew_out[arena * 4 + i] = A->a.all_rewards[i];
-            }
-            g.terminals[arena] = term;
-            if (g.term_out) g.term_out[arena] = term;
-            A->s.env.last_tick_count = A->s.env.tick_count;
+            tj = (uint8_t)A->a.traj_term;
         }
         sync();
-        if (valid) term = A->s.env.terminal;
-        bool fused_reset = g.reset_mode == 1 && valid && term != 0;
-        build_and_copy_obs(A, l, valid, arena, g, fused_reset ? nullptr : g.obs_out);
-        if (g.reset_mode == 1) {
-            if (fused_reset && term == 2 && g.trunc_obs) {
-                const float* src = g.obs + (size_t)arena * 4 * RLGPU_OBS;
-                float* dst = g.trunc_obs + (size_t)arena * 4 * RLGPU_OBS;
-                for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
+        if (valid && l == 0) {
+            g.terminals[arena] = term;
+            A->s.env.last_tick_count = A->s.env.tick_count;
+        }
+        const bool fused_reset = g.reset_mode == 1 && valid && term != 0;
+        if (valid && l < 4) build_obs_row(A, l);
+        sync();
+        if (valid) {
+            copy_rows(A, l, arena, g.obs, g.masks);
+            if (!fused_reset) copy_rows(A, l, arena, g.out_obs, g.out_masks);
+            if (tj == 2) {
+                copy_rows(A, l, arena, g.trunc_obs, nullptr);
+                copy_rows(A, l, arena, g.out_trunc, nullptr);
             }
-            sync();
+        }
+        sync();
+        if (g.reset_mode == 1) {
             if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena);
             sync();
             if (fused_reset && l < 4) build_obs_row(A, l);
             sync();
             if (fused_reset) {
-                const float* src = &A->u.out.obs[0][0];
-                float* dst = g.obs + (size_t)arena * 4 * RLGPU_OBS;
-                for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
-                if (g.obs_out) {
-                    float* d2 = g.obs_out + (size_t)arena * 4 * RLGPU_OBS;
-                    for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) d2[k] = src[k];
-                }
-                const uint8_t* msrc = &A->u.out.masks[0][0];
-                uint8_t* mdst = g.masks + (size_t)arena * 4 * RLGPU_ACTIONS;
-                for (int k = l; k < 4 * RLGPU_ACTIONS; k += kTeam) mdst[k] = msrc[k];
+                copy_rows(A, l, arena, g.obs, g.masks);
+                copy_rows(A, l, arena, g.out_obs, g.out_masks);
             }
             sync();
         }
@@ -421,18 +426,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
         bool rebuild = do_reset || (valid && g.reset_mode == 5);
         if (rebuild && l < 4) build_obs_row(A, l);
         sync();
-        if (rebuild) {
-            const float* src = &A->u.out.obs[0][0];
-            float* dst = g.obs + (size_t)arena * 4 * RLGPU_OBS;
-            for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) dst[k] = src[k];
-            if (g.obs_out) {
-                float* d2 = g.obs_out + (size_t)arena * 4 * RLGPU_OBS;
-                for (int k = l; k < 4 * RLGPU_OBS; k += kTeam) d2[k] = src[k];
-            }
-            const uint8_t* msrc = &A->u.out.masks[0][0];
-            uint8_t* mdst = g.masks + (size_t)arena * 4 * RLGPU_ACTIONS;
-            for (int k = l; k < 4 * RLGPU_ACTIONS; k += kTeam) mdst[k] = msrc[k];
-        }
+        if (rebuild) copy_rows(A, l, arena, g.obs, g.masks);
         sync();
     }
     // ---- write the records back
@@ -635,6 +629,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.last_rewards = e->cfg.save_rewards ? e->d_last_rewards : nullptr;
     g.trunc_obs = e->d_trunc_obs;
     g.seed = e->cfg.seed;
+    g.max_episode_steps = e->cfg.max_episode_steps;
     unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
     hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(64), 0, s, g);
     RLGPU_CHECK_HIP(hipGetLastError());
@@ -770,8 +765,8 @@ extern "C" int rlgpu_envset_step_second_half(rlgpu_envset* e, const int32_t* d_a
     });
 }
 
-extern "C" int rlgpu_envset_step(rlgpu_envset* e, const int32_t* d_actions, int32_t reset_terminated, float* d_obs_out,
-                                 float* d_rew_out, uint8_t* d_term_out, void* stream) {
+extern "C" int rlgpu_envset_step(rlgpu_envset* e, const int32_t* d_actions, int32_t reset_terminated,
+                                 const rlgpu_step_outputs* out, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(e && d_actions, "rlgpu_envset_step: null argument");
         RLGPU_REQUIRE(e->cfg.action_delay > 0, "fused step needs actionDelay > 0");
@@ -781,9 +776,13 @@ extern "C" int rlgpu_envset_step(rlgpu_envset* e, const int32_t* d_actions, int3
         g.ticks_second = e->cfg.tick_skip - e->cfg.action_delay;
         g.build = 1;
         g.reset_mode = reset_terminated ? 1 : 0;
-        g.obs_out = d_obs_out;
-        g.rew_out = d_rew_out;
-        g.term_out = d_term_out;
+        if (out) {
+            g.out_obs = out->obs;
+            g.out_masks = out->masks;
+            g.out_rew = out->rewards;
+            g.out_term = out->terminals;
+            g.out_trunc = out->trunc_obs;
+        }
         launch(e, g, rlgpu::as_stream(stream));
     });
 }

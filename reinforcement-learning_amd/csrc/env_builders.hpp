@@ -337,6 +337,7 @@ DEV void kickoff_reset(ArenaLDS* A, uint64_t seed, int arena) {
     e.penalty_blue = e.penalty_orange = 0;
     e.has_prev = 0;
     e.terminal = 0;
+    e.episode_steps = 0;
     for (int p = 0; p < 4; p++) {
         for (int k = 0; k < 8; k++) e.prev_action[p][k] = 0.f;
         e.ev_bump[p] = e.ev_bumped[p] = e.ev_demo[p] = e.ev_demoed[p] = 0;

@@ -112,6 +112,7 @@ struct Aux {
     int locked[RLGPU_PADS];
     int touched[4];
     int goal;
+    int traj_term;
     float all_rewards[4];
 };
 

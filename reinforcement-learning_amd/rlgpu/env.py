@@ -25,7 +25,21 @@ OBS, ACTIONS, REWARDS, PADS, CARS = 167, 90, 13, 34, 4
 
 class _Config(ctypes.Structure):
     _fields_ = [("num_arenas", ctypes.c_int32), ("tick_skip", ctypes.c_int32), ("action_delay", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("save_rewards", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("save_rewards", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32)]
+
+
+class StepOutputs(ctypes.Structure):
+    """rlgpu_step_outputs: experience-append destinations of the fused step (device pointers)."""
+    _fields_ = [("obs", ctypes.c_void_p), ("masks", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("terminals", ctypes.c_void_p), ("trunc_obs", ctypes.c_void_p)]
+
+    @classmethod
+    def of(cls, obs=None, masks=None, rewards=None, terminals=None, trunc_obs=None):
+        for t, n in ((obs, "obs"), (masks, "masks"), (rewards, "rewards"), (terminals, "terminals"),
+                     (trunc_obs, "trunc_obs")):
+            _lib.require_gpu_tensor(t, n)
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        return cls(p(obs), p(masks), p(rewards), p(terminals), p(trunc_obs))
 
 
 class _Buffers(ctypes.Structure):
@@ -50,7 +64,7 @@ def _bind():
     L.rlgpu_envset_reset_arenas.argtypes = [vp, vp, vp]
     L.rlgpu_envset_step_first_half.argtypes = [vp, vp]
     L.rlgpu_envset_step_second_half.argtypes = [vp, vp, vp]
-    L.rlgpu_envset_step.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    L.rlgpu_envset_step.argtypes = [vp, vp, i32, ctypes.POINTER(StepOutputs), vp]
     L.rlgpu_envset_sync.argtypes = [vp, vp]
     L.rlgpu_envset_build_obs.argtypes = [vp, vp]
     L.rlgpu_envset_get_arenas.argtypes = [vp, i32, i32, vp]
@@ -67,14 +81,15 @@ class EnvSet:
     """Vectorised 2v2 arena set resident in HBM (ExampleMain plugin set: AdvancedObs,
     DefaultAction, 13 rewards, NoTouch(8 s) + GoalScore(3) terminals, KickoffState)."""
 
-    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, save_rewards=True, device="cuda:0"):
+    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, save_rewards=True, device="cuda:0",
+                 max_episode_steps=0):
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("EnvSet needs an MI355X: the product path has no CPU fallback")
         L = _bind()
         self.device = torch.device(device)
         torch.cuda.set_device(self.device)
-        cfg = _Config(num_arenas, tick_skip, action_delay, seed, int(save_rewards))
+        cfg = _Config(num_arenas, tick_skip, action_delay, seed, int(save_rewards), max_episode_steps)
         h = ctypes.c_void_p()
         _lib.check(L.rlgpu_envset_create(ctypes.byref(cfg), ctypes.byref(h)), "rlgpu_envset_create")
         self._h = h
@@ -117,11 +132,11 @@ class EnvSet:
         _lib.check(_lib.lib().rlgpu_envset_step_second_half(self._h, self._actions(actions), _lib.stream_ptr(stream)),
                    "step_second_half")
 
-    def step(self, actions, reset_terminated=True, obs_out=None, rew_out=None, term_out=None, stream=None):
-        for t, n in ((obs_out, "obs_out"), (rew_out, "rew_out"), (term_out, "term_out")):
-            _lib.require_gpu_tensor(t, n)
-        _lib.check(_lib.lib().rlgpu_envset_step(self._h, self._actions(actions), int(reset_terminated),
-                                                _lib.ptr(obs_out), _lib.ptr(rew_out), _lib.ptr(term_out),
+    def step(self, actions, reset_terminated=True, out=None, stream=None):
+        """Fused StepFirstHalf + StepSecondHalf (+ Reset of terminated arenas); `out` is a
+        StepOutputs (experience append into rollout rows) or None."""
+        o = ctypes.byref(out) if out is not None else None
+        _lib.check(_lib.lib().rlgpu_envset_step(self._h, self._actions(actions), int(reset_terminated), o,
                                                 _lib.stream_ptr(stream)), "rlgpu_envset_step")
 
     def sync(self, stream=None):

@@ -53,15 +53,15 @@ class GAE:
 
     @staticmethod
     def compute_rollout(rews, terminals, val_preds, trunc_vals, boot_vals, gamma, lam, return_std,
-                        clip_range, clip_partials=None):
-        """[T, N] rollout-layout GAE (the engine's own experience buffer)."""
+                        clip_range, clip_partials=None, adv=None, target=None, ret=None):
+        """[T, N] rollout-layout GAE (the engine's own experience buffer); optional outputs."""
         for n_, t in (("rews", rews), ("terminals", terminals), ("val_preds", val_preds),
                       ("trunc_vals", trunc_vals), ("boot_vals", boot_vals)):
             require_gpu_tensor(t, n_)
         T, N = rews.shape
-        adv = torch.empty((T, N), dtype=torch.float32, device=rews.device)
-        tgt = torch.empty_like(adv)
-        ret = torch.empty_like(adv)
+        adv = torch.empty((T, N), dtype=torch.float32, device=rews.device) if adv is None else adv
+        tgt = torch.empty_like(adv) if target is None else target
+        ret = torch.empty_like(adv) if ret is None else ret
         _, g = _sig()
         check(g(ptr(rews), ptr(terminals), ptr(val_preds), ptr(trunc_vals), ptr(boot_vals), T, N,
                 gamma, lam, return_std, clip_range, ptr(adv), ptr(tgt), ptr(ret), ptr(clip_partials),

@@ -1,0 +1,203 @@
+"""Learner -- the GigaLearnCPP training loop for one GPU rank, every array resident in HBM.
+
+Mirrors GGL::Learner::Start (GigaLearnCPP/src/public/GigaLearnCPP/Learner.cpp:482-1056):
+  collection   infer actions (bf16 policy) -> fused env step with experience append     :669-861
+  consumption  critic over the rollout (InferCriticBatched), GAE, return-std Welford    :863-990
+  learning     PPOLearner::Learn: epochs x shuffled minibatches, clip_grad_norm_, AdamW :990-1000
+Distributed: one Learner per rank (arenas sharded), PPO gradients all-reduced (sum) over
+RCCL before clip_grad_norm_; advantage moments and return samples reduced too.
+
+Experience layout ([T, P] time-major, P = 4 * arenas): the reference keeps per-player
+trajectory vectors and trains only on finished trajectories (unfinished ones carry over to the
+next iteration); here every collected step is trained in the iteration that collected it, with
+the unfinished tail bootstrapped from V(obs_T) -- see DESIGN.md "Deviations".
+"""
+import math
+import time
+
+import numpy as np
+
+from . import gae as _gae
+from .env import EnvSet, StepOutputs
+from .ppo import PPO, permutation
+
+OBS, ACTIONS = 167, 90
+
+
+class WelfordStat:
+    """GGL::WelfordStat (Util/WelfordStat.h:7-67): fp64 running mean / variance."""
+
+    def __init__(self):
+        self.n, self.mean, self.m2 = 0, 0.0, 0.0
+
+    def add(self, xs):
+        for x in np.asarray(xs, np.float64).ravel():
+            self.n += 1
+            d = x - self.mean
+            self.mean += d / self.n
+            self.m2 += d * (x - self.mean)
+
+    def std(self):
+        if self.n < 2:
+            return 1.0
+        return math.sqrt(self.m2 / (self.n - 1))
+
+
+class LearnerConfig:
+    """The subset of GGL::LearnerConfig / PPOLearnerConfig on the hot path (ExampleMain values)."""
+
+    def __init__(self, **kw):
+        self.num_arenas = 4096
+        self.tick_skip = 8
+        self.action_delay = 7
+        self.seed = 123
+        self.rollout_len = 128
+        self.epochs = 2
+        self.mini_batch_size = 50_000
+        self.batch_size = None            # None = the whole iteration (ExampleMain: batchSize = tsPerItr)
+        self.gamma = 0.99
+        self.gae_lambda = 0.95
+        self.clip_range = 0.2
+        self.entropy_scale = 0.035
+        self.policy_lr = 2.5e-4
+        self.critic_lr = 2.5e-4
+        self.reward_clip_range = 200.0       # PPOLearnerConfig::rewardClipRange
+        self.return_samples = 150         # Learner.cpp:959-967
+        self.policy_layers = (512, 512)
+        self.critic_layers = (512, 512)
+        self.max_episode_duration = 300.0  # seconds (ExampleMain)
+        self.deterministic = False
+        for k, v in kw.items():
+            if not hasattr(self, k):
+                raise AttributeError(f"unknown LearnerConfig field {k}")
+            setattr(self, k, v)
+
+
+class Learner:
+    def __init__(self, cfg, device="cuda:0", rank=0, world=1, group=None):
+        import torch
+        self.cfg, self.rank, self.world, self.group = cfg, rank, world, group
+        self.device = torch.device(device)
+        T, N = cfg.rollout_len, cfg.num_arenas
+        P = 4 * N
+        self.P, self.T = P, T
+        max_ep = int(cfg.max_episode_duration * (120.0 / cfg.tick_skip))
+        self.env = EnvSet(N, seed=cfg.seed * 1000003 + rank, tick_skip=cfg.tick_skip, action_delay=cfg.action_delay,
+                          device=device, max_episode_steps=max_ep)
+        mb = min(cfg.mini_batch_size, T * P)
+        self.ppo = PPO(OBS, ACTIONS, cfg.policy_layers, cfg.critic_layers, policy_lr=cfg.policy_lr,
+                       critic_lr=cfg.critic_lr, clip_range=cfg.clip_range, entropy_scale=cfg.entropy_scale,
+                       max_rows=max(mb, min(P, 65536)), seed=cfg.seed, device=device)
+        if world > 1:  # identical initial weights on every rank
+            torch.distributed.broadcast(self.ppo.params, 0, group=group)
+            self.ppo.refresh_half()
+        d = self.device
+        # experience buffer (HBM)
+        self.obs = torch.empty((T + 1, P, OBS), device=d)
+        self.masks = torch.empty((T + 1, P, ACTIONS), dtype=torch.uint8, device=d)
+        self.actions = torch.empty((T, P), dtype=torch.int32, device=d)
+        self.logp = torch.empty((T, P), device=d)
+        self.rewards = torch.empty((T, P), device=d)
+        self.terms = torch.empty((T, P), dtype=torch.int8, device=d)
+        self.trunc_obs = torch.zeros((T, P, OBS), device=d)
+        self.values = torch.empty((T + 1, P), device=d)
+        self.trunc_vals = torch.empty((T, P), device=d)
+        self.adv = torch.empty((T, P), device=d)
+        self.target = torch.empty((T, P), device=d)
+        self.ret = torch.empty((T, P), device=d)
+        self.obs[0].copy_(self.env.obs)
+        self.masks[0].copy_(self.env.action_masks)
+        self.return_stat = WelfordStat()
+        self.total_steps = 0
+        self.iteration = 0
+        self._rng_step = 0
+        self.rng = np.random.default_rng(cfg.seed + 7919 * rank)
+        self.env_events = None  # optional list collecting (start, end) events around env steps
+
+    # ---------------------------------------------------------------- collection
+    def collect(self):
+        """T env steps: bf16 policy inference, fused env step + experience append."""
+        import torch
+        ppo, env = self.ppo, self.env
+        for t in range(self.T):
+            ppo.infer_actions(self.obs[t], self.masks[t], step=self._rng_step, deterministic=self.cfg.deterministic,
+                              actions=self.actions[t], logp=self.logp[t])
+            self._rng_step += 1
+            if self.env_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            env.step(self.actions[t], True,
+                     StepOutputs.of(obs=self.obs[t + 1], masks=self.masks[t + 1], rewards=self.rewards[t],
+                                    terminals=self.terms[t], trunc_obs=self.trunc_obs[t]))
+            if self.env_events is not None:
+                e1.record()
+                self.env_events.append((e0, e1))
+
+    # ---------------------------------------------------------------- consumption
+    def consume(self):
+        """InferCriticBatched over obs[0..T] and the truncation rows, GAE, return statistics."""
+        import torch
+        T, P = self.T, self.P
+        self.ppo.infer_critic(self.obs.view(-1, OBS), out=self.values.view(-1))
+        self.ppo.infer_critic(self.trunc_obs.view(-1, OBS), out=self.trunc_vals.view(-1))
+        std = self.return_stat.std()
+        _gae.GAE.compute_rollout(self.rewards, self.terms, self.values[:T], self.trunc_vals, self.values[T],
+                                 self.cfg.gamma, self.cfg.gae_lambda, std, self.cfg.reward_clip_range,
+                                 adv=self.adv, target=self.target, ret=self.ret)
+        # return-std Welford over randomly sampled returns (Learner.cpp:959-967)
+        k = self.cfg.return_samples
+        idx = torch.from_numpy(self.rng.integers(0, T * P, size=k)).to(self.device)
+        samples = self.ret.view(-1)[idx]
+        if self.world > 1:
+            allv = [torch.empty_like(samples) for _ in range(self.world)]
+            torch.distributed.all_gather(allv, samples, group=self.group)
+            samples = torch.cat(allv)
+        self.return_stat.add(samples.cpu().numpy())
+
+    # ---------------------------------------------------------------- learning
+    def learn(self):
+        import torch
+        import torch.distributed as dist
+        cfg, ppo = self.cfg, self.ppo
+        M = self.T * self.P
+        global_m = M * self.world
+        batch = global_m if cfg.batch_size is None else cfg.batch_size
+        obs = self.obs[:self.T].reshape(-1, OBS)
+        masks = self.masks[:self.T].reshape(-1, ACTIONS)
+        acts, logp = self.actions.view(-1), self.logp.view(-1)
+        adv, tgt = self.adv.view(-1), self.target.view(-1)
+        for epoch in range(cfg.epochs):
+            perm = permutation(M, cfg.seed + self.rank, self.iteration * cfg.epochs + epoch, device=self.device)
+            # batch advantage normalisation (PPOLearner.cpp:360-371), global over ranks
+            if self.world > 1:
+                s = torch.stack([adv.double().sum(), (adv.double() ** 2).sum()])
+                dist.all_reduce(s, group=self.group)
+                mean = s[0] / global_m
+                std = torch.sqrt((s[1] - s[0] * mean) / (global_m - 1))
+                ppo.adv_stats.copy_(torch.stack([mean, std]).float())
+            else:
+                ppo.adv_normalizer(adv)
+            local_batch = M if cfg.batch_size is None else min(M, cfg.batch_size // self.world)
+            for b0 in range(0, M, local_batch):
+                b1 = min(M, b0 + local_batch)
+                for s0 in range(b0, b1, cfg.mini_batch_size):
+                    n = min(cfg.mini_batch_size, b1 - s0)
+                    ppo.minibatch(obs, masks, acts, logp, adv, tgt, perm, s0, n, batch)
+                if self.world > 1:
+                    dist.all_reduce(ppo.grads, group=self.group)
+                ppo.optimizer_step()
+
+    def iterate(self):
+        """One PPO iteration (collect T steps, consume, learn); returns a report dict."""
+        import torch
+        t0 = time.perf_counter()
+        self.collect()
+        self.consume()
+        self.learn()
+        # next rollout starts from the last obs
+        self.obs[0].copy_(self.obs[self.T])
+        self.masks[0].copy_(self.masks[self.T])
+        self.iteration += 1
+        self.total_steps += self.T * self.P * self.world
+        torch.cuda.synchronize(self.device)
+        return {"iteration_s": time.perf_counter() - t0}

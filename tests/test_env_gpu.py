@@ -130,15 +130,43 @@ def test_env_reset_arenas_mask(gpu):
 def test_env_step_outputs_append(gpu):
     """rlgpu_envset_step's experience-append outputs equal the state buffers."""
     import torch
+    from rlgpu.env import StepOutputs
     n = 8
     g, o = _mk(n, 4, gpu)
     obs_out = torch.empty((4 * n, 167), device=gpu)
+    mask_out = torch.empty((4 * n, 90), dtype=torch.uint8, device=gpu)
     rew_out = torch.empty(4 * n, device=gpu)
-    term_out = torch.empty(n, dtype=torch.uint8, device=gpu)
+    term_out = torch.empty(4 * n, dtype=torch.int8, device=gpu)
     a = torch.zeros(4 * n, dtype=torch.int32, device=gpu)
-    g.step(a, True, obs_out, rew_out, term_out)
+    g.step(a, True, StepOutputs.of(obs_out, mask_out, rew_out, term_out))
     torch.cuda.synchronize()
-    assert torch.equal(obs_out, g.obs) and torch.equal(rew_out, g.rewards) and torch.equal(term_out, g.terminals)
+    assert torch.equal(obs_out, g.obs) and torch.equal(rew_out, g.rewards) and torch.equal(mask_out, g.action_masks)
+    assert torch.equal(term_out.view(n, 4)[:, 0].to(torch.uint8), g.terminals)
+
+
+def test_env_max_episode_truncation_parity(gpu):
+    """Learner maxEpisodeLength (Learner.cpp:848-850): trajectories cut TRUNCATED without an arena
+    reset; codes and trunc obs rows bit-exact vs the oracle."""
+    import torch
+    from rlgpu.env import EnvSet, StepOutputs
+    n, L = 24, 37
+    g = EnvSet(n, seed=8, device=gpu, max_episode_steps=L)
+    o = oracle.EnvSet(n, seed=8, max_episode_steps=L)
+    rng = np.random.default_rng(5)
+    term_out = torch.empty(4 * n, dtype=torch.int8, device=gpu)
+    trunc = torch.zeros((4 * n, 167), device=gpu)
+    saw = 0
+    for t in range(130):
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True, StepOutputs.of(terminals=term_out, trunc_obs=trunc))
+        _check_step(g, o, f"step {t}")
+        np.testing.assert_array_equal(term_out.cpu().numpy(), o.traj_terms, err_msg=f"traj terms step {t}")
+        saw += int((o.traj_terms == 2).sum())
+        sel = o.traj_terms == 2
+        if sel.any():
+            np.testing.assert_array_equal(trunc.cpu().numpy()[sel], o.trunc_obs[sel])
+    assert saw > 0
 
 
 def test_env_full_size_invariants(gpu):
