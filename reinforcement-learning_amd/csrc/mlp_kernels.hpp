@@ -26,7 +26,9 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 enum { A_IK = 0, A_KI = 1 };
 enum { B_JK = 0, B_KJ = 1 };
 
-constexpr int BM = 128, BN = 128, BK = 16, PAD = 4;
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int KP = 4;  // pad of k-contiguous LDS rows ([m][BK + KP]: 144 B = 9 x 16 B, odd)
+constexpr int MP = 4;  // pad of m-contiguous LDS rows ([k][BM + MP])
 
 struct GemmArgs {
     const float* A;
@@ -40,6 +42,7 @@ struct GemmArgs {
     int I, J, K;
     int kchunk;            // K range per split (multiple of BK)
     int64_t c_split;       // element stride between split partials
+    int a_vec, b_vec;      // 16-byte aligned rows (ld % 4 == 0, base aligned): float4 loads
 };
 
 DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays NaN)
@@ -48,75 +51,104 @@ DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays Na
 }
 DEV float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
 
+// 4 consecutive elements p[c..c+3] of a row, zero outside [.., lim)
+DEV float4 load4(const float* p, int c, int lim, bool vec) {
+    if (!p) return make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec && c + 3 < lim) return *reinterpret_cast<const float4*>(p + c);
+    float4 v;
+    v.x = c < lim ? p[c] : 0.f;
+    v.y = c + 1 < lim ? p[c + 1] : 0.f;
+    v.z = c + 2 < lim ? p[c + 2] : 0.f;
+    v.w = c + 3 < lim ? p[c + 3] : 0.f;
+    return v;
+}
+
+// One 128 x 32 tile of an operand, 4 float4 per thread.
+//  KMAJ (global row = output index, k contiguous) -> LDS [row][BK + KP]
+//  !KMAJ (global row = k, output index contiguous) -> LDS [k][BM + MP]
+template <bool KMAJ>
+DEV void tile_load(float4 (&r)[4], const float* base, int64_t ld, const int32_t* idx, int64_t off, int o0, int on, int k0,
+                   int ke, bool vec) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int e = t + 256 * q;
+        if (KMAJ) {
+            int row = e >> 3, c = (e & 7) * 4;
+            int go = o0 + row;
+            const float* p = nullptr;
+            if (go < on) p = base + (idx ? (int64_t)idx[off + go] : (int64_t)go) * ld;
+            r[q] = load4(p, k0 + c, ke, vec);
+        } else {
+            int kr = e >> 5, c = (e & 31) * 4;
+            int k = k0 + kr;
+            const float* p = nullptr;
+            if (k < ke) p = base + (idx ? (int64_t)idx[off + k] : (int64_t)k) * ld;
+            r[q] = load4(p, o0 + c, on, vec);
+        }
+    }
+}
+
+template <bool KMAJ>
+DEV void tile_store(float* lds, const float4 (&r)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int e = t + 256 * q;
+        if (KMAJ) {
+            int row = e >> 3, c = (e & 7) * 4;
+            *reinterpret_cast<float4*>(lds + row * (BK + KP) + c) = r[q];
+        } else {
+            int kr = e >> 5, c = (e & 31) * 4;
+            *reinterpret_cast<float4*>(lds + kr * (BM + MP) + c) = r[q];
+        }
+    }
+}
+
+// element (output index o, k) of an LDS tile
+template <bool KMAJ>
+DEV float tile_at(const float* lds, int o, int k) {
+    return KMAJ ? lds[o * (BK + KP) + k] : lds[k * (BM + MP) + o];
+}
+
+// fp32 GEMM on v_mfma_f32_32x32x2_f32: each MFMA j of a BK step takes k = j (lanes 0-31) and
+// k = 16 + j (lanes 32-63) so that k-contiguous tiles are read as 16-byte vectors.
 template <int LA, int LB>
-__global__ void __launch_bounds__(256) gemm_f32(GemmArgs g) {
-    __shared__ float As[BK][BM + PAD];
-    __shared__ float Bs[BK][BN + PAD];
+__global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
+    constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
+    constexpr int ASZ = AK ? BM * (BK + KP) : BK * (BM + MP);
+    constexpr int BSZ = BKM ? BN * (BK + KP) : BK * (BN + MP);
+    __shared__ float As[ASZ];
+    __shared__ float Bs[BSZ];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
     const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
     const int kb = blockIdx.z * g.kchunk;
     const int ke = min(g.K, kb + g.kchunk);
+    const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[2][2];
     for (int a = 0; a < 2; a++)
         for (int b = 0; b < 2; b++)
             for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
-
+    float4 ra[4], rb[4];
+    if (kb < ke) {
+        tile_load<AK>(ra, g.A, g.lda, g.a_idx, g.a_off, i0, g.I, kb, ke, g.a_vec);
+        tile_load<BKM>(rb, g.B, g.ldb, g.b_idx, g.b_off, j0, g.J, kb, ke, g.b_vec);
+    }
     for (int k0 = kb; k0 < ke; k0 += BK) {
-        // ---- stage A
-        if (LA == A_IK) {
-            int r = t >> 1, kh = (t & 1) * 8;
-            int gi = i0 + r;
-            const float* p = nullptr;
-            if (gi < g.I) {
-                int64_t row = g.a_idx ? (int64_t)g.a_idx[g.a_off + gi] : (int64_t)gi;
-                p = g.A + row * g.lda;
-            }
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) {
-                int k = k0 + kh + kk;
-                As[kh + kk][r] = (p && k < ke) ? p[k] : 0.f;
-            }
-        } else {
-            int kr = t >> 4, c = (t & 15) * 8;
-            int k = k0 + kr;
-            const float* p = k < ke ? g.A + (int64_t)k * g.lda : nullptr;
-#pragma unroll
-            for (int cc = 0; cc < 8; cc++) {
-                int i = i0 + c + cc;
-                As[kr][c + cc] = (p && i < g.I) ? p[i] : 0.f;
-            }
-        }
-        // ---- stage B
-        if (LB == B_JK) {
-            int r = t >> 1, kh = (t & 1) * 8;
-            int gj = j0 + r;
-            const float* p = gj < g.J ? g.B + (int64_t)gj * g.ldb : nullptr;
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) {
-                int k = k0 + kh + kk;
-                Bs[kh + kk][r] = (p && k < ke) ? p[k] : 0.f;
-            }
-        } else {
-            int kr = t >> 4, c = (t & 15) * 8;
-            int k = k0 + kr;
-            const float* p = nullptr;
-            if (k < ke) {
-                int64_t row = g.b_idx ? (int64_t)g.b_idx[g.b_off + k] : (int64_t)k;
-                p = g.B + row * g.ldb;
-            }
-#pragma unroll
-            for (int cc = 0; cc < 8; cc++) {
-                int j = j0 + c + cc;
-                Bs[kr][c + cc] = (p && j < g.J) ? p[j] : 0.f;
-            }
-        }
+        tile_store<AK>(As, ra);
+        tile_store<BKM>(Bs, rb);
         __syncthreads();
+        if (k0 + BK < ke) {  // prefetch the next stage into registers while the MFMAs run
+            tile_load<AK>(ra, g.A, g.lda, g.a_idx, g.a_off, i0, g.I, k0 + BK, ke, g.a_vec);
+            tile_load<BKM>(rb, g.B, g.ldb, g.b_idx, g.b_off, j0, g.J, k0 + BK, ke, g.b_vec);
+        }
+        const int ma = wm * 64 + l32, nb = wn * 64 + l32;
 #pragma unroll
-        for (int k2 = 0; k2 < BK / 2; k2++) {
-            int kk = 2 * k2 + (lane >> 5);
-            float a0 = As[kk][wm * 64 + (lane & 31)], a1 = As[kk][wm * 64 + 32 + (lane & 31)];
-            float b0 = Bs[kk][wn * 64 + (lane & 31)], b1 = Bs[kk][wn * 64 + 32 + (lane & 31)];
+        for (int j = 0; j < BK / 2; j++) {
+            int kk = 16 * h + j;
+            float a0 = tile_at<AK>(As, ma, kk), a1 = tile_at<AK>(As, ma + 32, kk);
+            float b0 = tile_at<BKM>(Bs, nb, kk), b1 = tile_at<BKM>(Bs, nb + 32, kk);
             acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
@@ -129,12 +161,12 @@ __global__ void __launch_bounds__(256) gemm_f32(GemmArgs g) {
     for (int ti = 0; ti < 2; ti++)
 #pragma unroll
         for (int tj = 0; tj < 2; tj++) {
-            int j = j0 + wn * 64 + tj * 32 + (lane & 31);
+            int j = j0 + wn * 64 + tj * 32 + l32;
             if (j >= g.J) continue;
             float bj = g.bias ? g.bias[j] : 0.f;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (i < g.I) C[(int64_t)i * g.ldc + j] = acc[ti][tj][r] + bj;
             }
         }
@@ -324,8 +356,9 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 }
 
 // Backward of LeakyReLU(LN(Z)): dZ from dA; per-block column partials of
-// dgamma = sum dH*xhat, dbeta = sum dH, dbias = sum dZ  -> part[blk][3][H].
-constexpr int LNB_ROWS = 64;
+// dbias = sum dZ, dgamma = sum dH*xhat, dbeta = sum dH -> part[blk][3][H] (the flat parameter
+// order Linear.bias, LayerNorm.weight, LayerNorm.bias, so one reduction serves all three).
+constexpr int LNB_ROWS = 128;
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* xhat, const float* rstd, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
@@ -385,9 +418,9 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
     for (int q = 0; q < nper; q++) {
         int c = lane + 64 * q;
         if (c < H) {
-            red[w][0][c] = pg[q];
-            red[w][1][c] = pb[q];
-            red[w][2][c] = pz[q];
+            red[w][0][c] = pz[q];
+            red[w][1][c] = pg[q];
+            red[w][2][c] = pb[q];
         }
     }
     __syncthreads();
@@ -421,13 +454,23 @@ __global__ void __launch_bounds__(256) colsum_partial(const float* X, int R, int
     }
 }
 
-// grad[c] += sum_b part[b*stride + k*H + c]  (fixed order)
-__global__ void reduce_cols(const float* part, int nblk, int64_t stride, int64_t off, int n, float* grad) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
+// grad[c] += sum_b part[b*stride + off + c] for c < n: 16 row groups x 64 columns per
+// 1024-thread block, combined in LDS in a fixed order (deterministic).
+__global__ void __launch_bounds__(1024) reduce_cols(const float* part, int nblk, int64_t stride, int64_t off, int n,
+                                                   float* grad) {
+    __shared__ float red[16][64];
+    int cl = threadIdx.x & 63, gi = threadIdx.x >> 6;
+    int c = blockIdx.x * 64 + cl;
     float s = 0.f;
-    for (int b = 0; b < nblk; b++) s += part[(int64_t)b * stride + off + c];
-    grad[c] += s;
+    if (c < n)
+        for (int b = gi; b < nblk; b += 16) s += part[(int64_t)b * stride + off + c];
+    red[gi][cl] = s;
+    __syncthreads();
+    if (gi == 0 && c < n) {
+        float tot = 0.f;
+        for (int k = 0; k < 16; k++) tot += red[k][cl];
+        grad[c] += tot;
+    }
 }
 
 }  // namespace mlp

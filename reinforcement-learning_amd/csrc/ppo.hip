@@ -80,6 +80,8 @@ void gemm_f32(int la, int lb, const float* A, int64_t lda, const int32_t* a_idx,
     g.kchunk = (int)ceil_div(chunk, mlp::BK) * mlp::BK;
     int z = (int)ceil_div(K, g.kchunk);
     g.c_split = (int64_t)I * ldc;
+    g.a_vec = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
+    g.b_vec = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
     dim3 grid(ceil_div(J, mlp::BN), ceil_div(I, mlp::BM), z);
     if (la == mlp::A_IK && lb == mlp::B_JK)
         hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_IK, mlp::B_JK>), grid, dim3(256), 0, s, g);
@@ -112,7 +114,7 @@ void weight_grad(rlgpu_ppo* h, const float* dZ, int out, const float* X, int64_t
 void colsum_into(rlgpu_ppo* h, const float* X, int n, int C, float* g, hipStream_t s) {
     int nb = (int)ceil_div(n, mlp::CS_ROWS);
     hipLaunchKernelGGL(mlp::colsum_partial, dim3(nb), dim3(256), 0, s, X, n, C, h->cpart);
-    hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(C, 256)), dim3(256), 0, s, h->cpart, nb, (int64_t)C, (int64_t)0, C, g);
+    hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(C, 64)), dim3(1024), 0, s, h->cpart, nb, (int64_t)C, (int64_t)0, C, g);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -162,13 +164,10 @@ void backward(rlgpu_ppo* h, int mi, const float* X, const int32_t* idx, int64_t 
         hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, h->dA, m.xhat[l], m.rstd[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, h->dZ, h->cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
-        int64_t st = 3 * (int64_t)L.out;
-        dim3 rg(ceil_div(L.out, 256));
-        if (h->cfg.layer_norm) {
-            hipLaunchKernelGGL(mlp::reduce_cols, rg, dim3(256), 0, s, h->cpart, nb, st, (int64_t)0, L.out, G + L.g);
-            hipLaunchKernelGGL(mlp::reduce_cols, rg, dim3(256), 0, s, h->cpart, nb, st, (int64_t)L.out, L.out, G + L.be);
-        }
-        hipLaunchKernelGGL(mlp::reduce_cols, rg, dim3(256), 0, s, h->cpart, nb, st, 2 * (int64_t)L.out, L.out, G + L.b);
+        // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
+        int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
+        hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(ncol, 64)), dim3(1024), 0, s, h->cpart, nb, 3 * (int64_t)L.out,
+                           (int64_t)0, ncol, G + L.b);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (l == 0)
             weight_grad(h, h->dZ, L.out, X, m.in, idx, start, L.in, n, G + L.w, s);
@@ -464,7 +463,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         int A = h->cfg.num_actions;
         // policy
         forward_train(h, 0, d_obs, d_index, start, n, h->out, s);
-        hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, 4)), dim3(256), 0, s, h->out, d_masks, d_actions, d_old_logp,
+        hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, ppo::PL_ROWS)), dim3(256), 0, s, h->out, d_masks, d_actions, d_old_logp,
                            d_adv, d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
                            1.f / std::log((float)A), h->dout, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());

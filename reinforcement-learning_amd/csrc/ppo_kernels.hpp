@@ -105,64 +105,79 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.
 // Rows are minibatch-ordered; sample s = idx ? idx[start + r] : start + r addresses the
-// batch buffers.  scale_pl = bsr / n (d loss / d min(surr1,surr2) = -scale_pl).
+// batch buffers.  Each wave handles 16 rows; metrics are reduced per block (one atomic each).
+constexpr int PL_ROWS = 64;
 __global__ void __launch_bounds__(256) policy_loss(const float* logits, const uint8_t* masks, const int32_t* actions,
                                                   const float* old_logp, const float* adv, const int32_t* idx, int64_t start,
                                                   int n, int A, const float* adv_stats, float bsr, float clip_range,
                                                   float ent_scale, float inv_log_a, float* dlogits, float* metrics) {
-    int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (row >= n) return;
-    int64_t s = idx ? (int64_t)idx[start + row] : start + row;
-    int a0 = 2 * lane, a1 = 2 * lane + 1;
-    bool in0 = a0 < A, in1 = a1 < A;
-    const float* lg = logits + (int64_t)row * A;
-    const uint8_t* mk = masks + s * A;
-    float z0 = in0 ? lg[a0] + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
-    float z1 = in1 ? lg[a1] + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
-    float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
-    float e0 = in0 ? expf(z0 - m) : 0.f, e1 = in1 ? expf(z1 - m) : 0.f;
-    float sum = wave_sum(e0 + e1);
-    float p0 = e0 / sum, p1 = e1 / sum;
-    float c0 = fminf(fmaxf(p0, kMinProb), 1.f), c1 = fminf(fmaxf(p1, kMinProb), 1.f);
-    float l0 = in0 ? logf(c0) : 0.f, l1 = in1 ? logf(c1) : 0.f;
-    float ent = -wave_sum((in0 ? l0 * c0 : 0.f) + (in1 ? l1 * c1 : 0.f));
-    int a = actions[s];
-    a = a < 0 ? 0 : (a > A - 1 ? A - 1 : a);
-    float pa = __shfl((a & 1) ? c1 : c0, a >> 1, 64);
-    float lp = logf(pa);
-    float old = old_logp[s];
-    float ratio = expf(lp - old);
-    float advn = (adv[s] - adv_stats[0]) / (adv_stats[1] + 1e-8f);
-    float clipped = fminf(fmaxf(ratio, 1.f - clip_range), 1.f + clip_range);
-    float s1 = ratio * advn, s2 = clipped * advn;
-    float pl = fminf(s1, s2);
-    // ---- backward
-    float g_pl = -bsr / (float)n;
-    float g_s1 = s1 < s2 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
-    float g_s2 = s2 < s1 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
-    float in_rng = (ratio >= 1.f - clip_range && ratio <= 1.f + clip_range) ? 1.f : 0.f;
-    float g_ratio = g_s1 * advn + g_s2 * advn * in_rng;
-    float g_lp = g_ratio * ratio;
-    float g_ent = -ent_scale * bsr * inv_log_a / (float)n;  // d loss / d H_i (H_i unnormalised)
-    // d/dc_j: entropy term -g_ent*(log c_j + 1) ; log-prob term g_lp / c_a at j == a
-    float d0 = in0 ? -g_ent * (l0 + 1.f) : 0.f, d1 = in1 ? -g_ent * (l1 + 1.f) : 0.f;
-    if (a == a0) d0 += g_lp / c0;
-    if (a == a1) d1 += g_lp / c1;
-    // clamp backward (pass where min <= p <= max)
-    d0 = (p0 >= kMinProb && p0 <= 1.f) ? d0 : 0.f;
-    d1 = (p1 >= kMinProb && p1 <= 1.f) ? d1 : 0.f;
-    float dot = wave_sum((in0 ? d0 * p0 : 0.f) + (in1 ? d1 * p1 : 0.f));
-    float* dl = dlogits + (int64_t)row * A;
-    if (in0) dl[a0] = p0 * (d0 - dot);
-    if (in1) dl[a1] = p1 * (d1 - dot);
-    if (lane == 0 && metrics) {
+    __shared__ float red[4][5];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int a0 = 2 * lane, a1 = 2 * lane + 1;
+    const bool in0 = a0 < A, in1 = a1 < A;
+    const float mean = adv_stats[0], sd = adv_stats[1];
+    float m_ent = 0.f, m_kl = 0.f, m_pl = 0.f, m_ratio = 0.f, m_clip = 0.f;
+    for (int i = 0; i < PL_ROWS / 4; i++) {
+        int row = blockIdx.x * PL_ROWS + i * 4 + w;
+        if (row >= n) break;
+        int64_t s = idx ? (int64_t)idx[start + row] : start + row;
+        const float* lg = logits + (int64_t)row * A;
+        const uint8_t* mk = masks + s * A;
+        float z0 = in0 ? lg[a0] + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
+        float z1 = in1 ? lg[a1] + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
+        float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
+        float e0 = in0 ? expf(z0 - m) : 0.f, e1 = in1 ? expf(z1 - m) : 0.f;
+        float sum = wave_sum(e0 + e1);
+        float p0 = e0 / sum, p1 = e1 / sum;
+        float c0 = fminf(fmaxf(p0, kMinProb), 1.f), c1 = fminf(fmaxf(p1, kMinProb), 1.f);
+        float l0 = in0 ? logf(c0) : 0.f, l1 = in1 ? logf(c1) : 0.f;
+        float ent = -wave_sum((in0 ? l0 * c0 : 0.f) + (in1 ? l1 * c1 : 0.f));
+        int a = actions[s];
+        a = a < 0 ? 0 : (a > A - 1 ? A - 1 : a);
+        float pa = __shfl((a & 1) ? c1 : c0, a >> 1, 64);
+        float lp = logf(pa);
+        float old = old_logp[s];
+        float ratio = expf(lp - old);
+        float advn = (adv[s] - mean) / (sd + 1e-8f);
+        float clipped = fminf(fmaxf(ratio, 1.f - clip_range), 1.f + clip_range);
+        float s1 = ratio * advn, s2 = clipped * advn;
+        float pl = fminf(s1, s2);
+        // ---- backward (torch semantics: min() ties split the gradient, clamp passes inside [lo, hi])
+        float g_pl = -bsr / (float)n;
+        float g_s1 = s1 < s2 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
+        float g_s2 = s2 < s1 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
+        float in_rng = (ratio >= 1.f - clip_range && ratio <= 1.f + clip_range) ? 1.f : 0.f;
+        float g_ratio = g_s1 * advn + g_s2 * advn * in_rng;
+        float g_lp = g_ratio * ratio;
+        float g_ent = -ent_scale * bsr * inv_log_a / (float)n;  // d loss / d H_i (H_i unnormalised)
+        float d0 = in0 ? -g_ent * (l0 + 1.f) : 0.f, d1 = in1 ? -g_ent * (l1 + 1.f) : 0.f;
+        if (a == a0) d0 += g_lp / c0;
+        if (a == a1) d1 += g_lp / c1;
+        d0 = (p0 >= kMinProb && p0 <= 1.f) ? d0 : 0.f;
+        d1 = (p1 >= kMinProb && p1 <= 1.f) ? d1 : 0.f;
+        float dot = wave_sum((in0 ? d0 * p0 : 0.f) + (in1 ? d1 * p1 : 0.f));
+        float* dl = dlogits + (int64_t)row * A;
+        if (in0) dl[a0] = p0 * (d0 - dot);
+        if (in1) dl[a1] = p1 * (d1 - dot);
         float lr = lp - old;
-        float inv_n = 1.f / (float)n;
-        atomicAdd(&metrics[0], ent * inv_log_a * inv_n);                      // entropy
-        atomicAdd(&metrics[1], (expf(lr) - 1.f - lr) * inv_n);                // KL
-        atomicAdd(&metrics[2], -pl * inv_n);                                  // policy loss
-        atomicAdd(&metrics[4], ratio * inv_n);                                // ratio
-        atomicAdd(&metrics[5], (fabsf(ratio - 1.f) > clip_range ? 1.f : 0.f) * inv_n);  // clip fraction
+        m_ent += ent * inv_log_a;
+        m_kl += expf(lr) - 1.f - lr;
+        m_pl += -pl;
+        m_ratio += ratio;
+        m_clip += fabsf(ratio - 1.f) > clip_range ? 1.f : 0.f;
+    }
+    if (lane == 0) {
+        red[w][0] = m_ent;
+        red[w][1] = m_kl;
+        red[w][2] = m_pl;
+        red[w][3] = m_ratio;
+        red[w][4] = m_clip;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5 && metrics) {
+        const int slot[5] = {0, 1, 2, 4, 5};  // entropy, KL, policy loss, ratio, clip fraction
+        float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        atomicAdd(&metrics[slot[threadIdx.x]], v / (float)n);
     }
 }
 

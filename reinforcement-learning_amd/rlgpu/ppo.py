@@ -79,7 +79,7 @@ class PPO:
     def __init__(self, obs_size=167, num_actions=90, policy_layers=(512, 512), critic_layers=(512, 512),
                  layer_norm=True, policy_lr=2.5e-4, critic_lr=2.5e-4, clip_range=0.2, entropy_scale=0.035,
                  max_grad_norm=0.5, max_rows=50_000, seed=42, init=True, device="cuda:0",
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, leaky_slope=0.01):
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("PPO needs an MI355X: the product path has no CPU fallback")
@@ -93,7 +93,8 @@ class PPO:
             c.policy_layers[i] = v
         for i, v in enumerate(critic_layers):
             c.critic_layers[i] = v
-        c.layer_norm, c.leaky_slope = int(layer_norm), 0.01
+        c.layer_norm, c.leaky_slope = int(layer_norm), leaky_slope
+        self.leaky_slope = leaky_slope
         c.policy_lr, c.critic_lr = policy_lr, critic_lr
         c.beta1, c.beta2, c.eps, c.weight_decay = betas[0], betas[1], eps, weight_decay
         c.clip_range, c.entropy_scale, c.max_grad_norm = clip_range, entropy_scale, max_grad_norm
@@ -153,7 +154,7 @@ class PPO:
             mods.append(torch.nn.Linear(prev, hdim))
             if self.layer_norm:
                 mods.append(torch.nn.LayerNorm(hdim))
-            mods.append(torch.nn.LeakyReLU())
+            mods.append(torch.nn.LeakyReLU(self.leaky_slope))
             prev = hdim
         mods.append(torch.nn.Linear(prev, out))
         seq = torch.nn.Sequential(*mods)
