@@ -31,7 +31,8 @@ extern "C" {
 
 #define RLGPU_CARS 4          /* 2v2 (src/ExampleMain.cpp:200-208) */
 #define RLGPU_PADS 34         /* RLConst::BoostPads 6 big + 28 small (RLConst.h:212-214) */
-#define RLGPU_MANIFOLDS 16    /* persistent-manifold slots per arena */
+#define RLGPU_MANIFOLDS 12    /* persistent-manifold slots per arena (build limit, overflow counted) */
+#define RLGPU_MAX_SOLVER_ROWS 14 /* contact rows per arena per tick (build limit, overflow counted) */
 #define RLGPU_OBS 167         /* AdvancedObs 9+8+34+29*4 (AdvancedObs.cpp:193-270) */
 #define RLGPU_ACTIONS 90      /* DefaultAction table (DefaultAction.cpp:3-89) */
 #define RLGPU_REWARDS 13      /* ExampleMain reward list (src/ExampleMain.cpp:132-177) */
@@ -186,6 +187,11 @@ int rlgpu_envset_get_arenas(rlgpu_envset* env, int32_t first, int32_t count, rlg
 int rlgpu_envset_set_arenas(rlgpu_envset* env, int32_t first, int32_t count, const rlgpu_arena_state* h_in);
 /* Rebuild obs/masks of all arenas from the current state (no physics). */
 int rlgpu_envset_build_obs(rlgpu_envset* env, void* stream);
+
+/* Diagnostics: when d_counters (32 x uint64, device) is non-NULL, every launch adds the shader
+ * cycles thread 0 of each workgroup spends per phase (0-10 tick phases, 11 load/halves prelude,
+ * 12 builders, 13 obs rows, 14 resets, 15 store).  NULL disables (the default). */
+int rlgpu_envset_set_profile(rlgpu_envset* env, unsigned long long* d_counters);
 
 /* Static sizes for binding checks. */
 int rlgpu_arena_state_size(void);

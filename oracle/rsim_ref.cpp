@@ -1828,6 +1828,10 @@ struct Sim {
             side_transform(a, pa_, ra);
             side_transform(bb, pb_, rb);
             for (int j = 0; j < mf.count; j++) {
+                if ((int)rows.size() >= RLGPU_MAX_SOLVER_ROWS) {  // build limit shared with the kernel
+                    s.env.manifold_overflow++;
+                    continue;
+                }
                 rlgpu_contact& cp = mf.pts[j];
                 V wa = ra * ld3(cp.localA) + pa_;  // positions from the last refresh
                 V wb = rb * ld3(cp.localB) + pb_;
@@ -1861,6 +1865,10 @@ struct Sim {
         // RocketSim special contacts: one averaged row per body vs the fixed body
         for (int i = 0; i < 5; i++) {
             if (spec[i].num <= 0 || !in_solver[i]) continue;
+            if ((int)rows.size() >= RLGPU_MAX_SOLVER_ROWS) {
+                s.env.manifold_overflow++;
+                continue;
+            }
             float distance = spec[i].total_d / spec[i].num;
             V normal = spec[i].total_n / (float)spec[i].num;
             rlgpu_contact tmp;

@@ -37,12 +37,27 @@ struct StepArgs {
     float* out_trunc;
     int max_episode_steps;
     uint64_t seed;
+    unsigned long long* prof;  // [32] phase cycle counters or null
 };
 
 DEV void sync() { __syncthreads(); }
 
+// Optional per-phase cycle accounting (StepArgs::prof != null): thread 0 of every workgroup adds
+// the s_memtime delta since the previous mark to prof[phase].  Used by tools/env_phase_profile.py.
+struct Prof {
+    unsigned long long* p;
+    long long t;
+    DEV void mark(int k) {
+        if (p) {
+            long long now = clock64();
+            if (threadIdx.x == 0) atomicAdd(&p[k], (unsigned long long)(now - t));
+            t = now;
+        }
+    }
+};
+
 // ------------------------------------------------------------------ one tick (Arena::Step body)
-DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
+DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P) {
     if (valid && l == 0) {
         rlgpu_arena_state& s = A->s;
         bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
@@ -73,8 +88,10 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         }
     }
     sync();
+    P.mark(0);
     if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase(A, l >> 2, l & 3);
     sync();
+    P.mark(1);
     if (valid) {
         if (l < 4) {
             car_phase(A, l);
@@ -87,6 +104,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         }
     }
     sync();
+    P.mark(2);
     if (valid && l < 5) {  // applyGravity + predictUnconstraintMotion
         add_force(A, l, C.gravity * (l == 0 ? kBallMass : kCarMass));
         if (l == 0) {
@@ -100,6 +118,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         }
     }
     sync();
+    P.mark(3);
     if (valid && l == 0) {
         bool awake = !A->a.ball_sleep;
         if (!awake) {
@@ -116,14 +135,18 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         A->a.ncand = 0;
     }
     sync();
+    P.mark(4);
     if (valid)
         for (int rank = l; rank < kPairs; rank += kTeam) A->a.pair_mode[rank] = narrow_pair(A, rank);
     sync();
+    P.mark(5);
     if (valid && l == 0) {
         commit_contacts(A);
+        if (threadIdx.x == 0) P.mark(16);
         solve(A);
     }
     sync();
+    P.mark(6);
     if (valid && l < 5) {  // integrateTransforms (btDiscreteDynamicsWorld.cpp:889-985)
         bool act = l == 0 ? A->a.ball_awake != 0 : A->a.active[l] != 0;
         if (act) {
@@ -143,6 +166,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         A->a.torque[l] = zero3();
     }
     sync();
+    P.mark(7);
     if (valid && l < 4) {  // Car::_PostTickUpdate + _FinishPhysicsTick (Car.cpp:133-193)
         rlgpu_car& cs = A->s.cars[l];
         if (!cs.is_demoed) {
@@ -172,6 +196,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         }
     }
     sync();
+    P.mark(8);
     if (valid) {  // BoostPadGrid::CheckCollision per pad (BoostPadGrid.cpp:5-25, BoostPad.cpp:61-86)
         for (int p = l; p < RLGPU_PADS; p += kTeam) {
             int locked = -1;
@@ -204,6 +229,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         }
     }
     sync();
+    P.mark(9);
     if (valid && l == 0) {
         for (int p = 0; p < RLGPU_PADS; p++) {  // BoostPad::_PostTickUpdate (BoostPad.cpp:88-105)
             rlgpu_pad& pd = A->s.pads[p];
@@ -235,6 +261,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena) {
         A->s.env.tick_count++;
     }
     sync();
+    P.mark(10);
 }
 
 // copy the 4 obs rows (and mask rows) of this arena from LDS to [players x OBS] outputs
@@ -257,6 +284,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
     const int arena = blockIdx.x * kArenas + team;
     const bool valid = arena < g.n;
     ArenaLDS* A = &lds[team];
+    Prof P{g.prof, g.prof ? (long long)clock64() : 0};
     // ---- stage the 4 arena records into LDS (contiguous 16-byte loads)
     {
         int first = blockIdx.x * kArenas;
@@ -269,13 +297,14 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             *dst = *src;
         }
     }
-    sync();
+    sync(); P.mark(11);
     if (valid && l < 5) {
         A->a.force[l] = zero3();
         A->a.torque[l] = zero3();
         update_inertia(A, l);
     }
-    sync();
+    if (valid && l == 5) build_slot_map(A);
+    sync(); P.mark(11);
     // ---- StepFirstHalf (EnvSet.cpp:113-130)
     if (g.ticks_first > 0) {
         if (valid && l == 0) {
@@ -289,8 +318,8 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             }
             e.has_prev = 1;
         }
-        sync();
-        for (int t = 0; t < g.ticks_first; t++) tick(A, l, valid, g.seed, arena);
+        sync(); P.mark(11);
+        for (int t = 0; t < g.ticks_first; t++) tick(A, l, valid, g.seed, arena, P);
     }
     // ---- StepSecondHalf (EnvSet.cpp:132-273)
     if (g.actions) {
@@ -305,8 +334,8 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             c[7] = x[7] == 1 ? 1.f : 0.f;
             for (int k = 0; k < 8; k++) A->s.env.prev_action[l][k] = x[k];
         }
-        sync();
-        for (int t = 0; t < g.ticks_second; t++) tick(A, l, valid, g.seed, arena);
+        sync(); P.mark(11);
+        for (int t = 0; t < g.ticks_second; t++) tick(A, l, valid, g.seed, arena, P);
     }
     // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks
     uint8_t term = 0;
@@ -355,7 +384,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             if (tj) e.episode_steps = 0;
             A->a.traj_term = tj;
         }
-        sync();
+        sync(); P.mark(12);
         if (valid && l < 4) {
             PView P[4];
             for (int i = 0; i < 4; i++) P[i] = view_player(A, i);
@@ -368,7 +397,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             }
             A->a.all_rewards[l] = all;
         }
-        sync();
+        sync(); P.mark(12);
         if (valid && l < 4) {
             float r = A->a.all_rewards[l];
             g.rewards[arena * 4 + l] = r;
@@ -380,14 +409,14 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             term = A->s.env.terminal;
             tj = (uint8_t)A->a.traj_term;
         }
-        sync();
+        sync(); P.mark(12);
         if (valid && l == 0) {
             g.terminals[arena] = term;
             A->s.env.last_tick_count = A->s.env.tick_count;
         }
         const bool fused_reset = g.reset_mode == 1 && valid && term != 0;
         if (valid && l < 4) build_obs_row(A, l);
-        sync();
+        sync(); P.mark(13);
         if (valid) {
             copy_rows(A, l, arena, g.obs, g.masks);
             if (!fused_reset) copy_rows(A, l, arena, g.out_obs, g.out_masks);
@@ -396,17 +425,17 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
                 copy_rows(A, l, arena, g.out_trunc, nullptr);
             }
         }
-        sync();
+        sync(); P.mark(13);
         if (g.reset_mode == 1) {
             if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena);
-            sync();
+            sync(); P.mark(14);
             if (fused_reset && l < 4) build_obs_row(A, l);
-            sync();
+            sync(); P.mark(14);
             if (fused_reset) {
                 copy_rows(A, l, arena, g.obs, g.masks);
                 copy_rows(A, l, arena, g.out_obs, g.out_masks);
             }
-            sync();
+            sync(); P.mark(14);
         }
     }
     // ---- EnvSet::Reset / ResetArena / obs rebuild
@@ -417,17 +446,17 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             else if (g.reset_mode == 3) do_reset = g.reset_mask ? g.reset_mask[arena] != 0 : true;
             else if (g.reset_mode == 4) do_reset = true;
         }
-        sync();
+        sync(); P.mark(14);
         if (do_reset && l == 0) {
             kickoff_reset(A, g.seed, arena);
             if (g.reset_mode == 2) g.terminals[arena] = 0;
         }
-        sync();
+        sync(); P.mark(14);
         bool rebuild = do_reset || (valid && g.reset_mode == 5);
         if (rebuild && l < 4) build_obs_row(A, l);
-        sync();
+        sync(); P.mark(14);
         if (rebuild) copy_rows(A, l, arena, g.obs, g.masks);
-        sync();
+        sync(); P.mark(14);
     }
     // ---- write the records back
     {
@@ -441,6 +470,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             *dst = *src;
         }
     }
+    P.mark(15);
 }
 
 // ------------------------------------------------------------------ host: constants
@@ -607,6 +637,7 @@ struct rlgpu_envset {
     char* d_arenas = nullptr;
     float *d_obs = nullptr, *d_rewards = nullptr, *d_last_rewards = nullptr, *d_trunc_obs = nullptr;
     uint8_t *d_masks = nullptr, *d_terminals = nullptr;
+    unsigned long long* d_prof = nullptr;
 };
 
 namespace {
@@ -630,6 +661,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.trunc_obs = e->d_trunc_obs;
     g.seed = e->cfg.seed;
     g.max_episode_steps = e->cfg.max_episode_steps;
+    g.prof = e->d_prof;
     unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
     hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(64), 0, s, g);
     RLGPU_CHECK_HIP(hipGetLastError());
@@ -692,6 +724,13 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         g.reset_mode = 4;
         launch(e, g, nullptr);
         RLGPU_CHECK_HIP(hipDeviceSynchronize());
+    });
+}
+
+extern "C" int rlgpu_envset_set_profile(rlgpu_envset* e, unsigned long long* d_counters) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        e->d_prof = d_counters;
     });
 }
 

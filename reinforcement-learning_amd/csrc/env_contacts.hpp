@@ -9,8 +9,11 @@ namespace rl {
 // canonical pair order: rank 0..24 = body*5 + static, rank 25..34 = dynamic pairs
 DEV int pair_key(int rank) {
     if (rank < 25) return (rank / 5) * 8 + (rank % 5);
-    const int keys[10] = {65, 66, 67, 68, 74, 75, 76, 83, 84, 92};
-    return keys[rank - 25];
+    int r = rank - 25;  // (a,b), a < b: (0,1..4) (1,2..4) (2,3..4) (3,4)
+    int a = r < 4 ? 0 : (r < 7 ? 1 : (r < 9 ? 2 : 3));
+    int first = a == 0 ? 0 : (a == 1 ? 4 : (a == 2 ? 7 : 9));
+    int b = a + 1 + (r - first);
+    return 64 + a * 8 + b;
 }
 DEV void key_bodies(int key, int& a, int& b) {
     if (key >= 64) {
@@ -37,10 +40,21 @@ DEV float pair_cbt(int a, int b) {
     return stdmin(ta, tb);
 }
 
+// key -> slot map (Aux::slot_of_key, rebuilt from the record at every launch): the manifold
+// of a key, if live, is the one the map points to (a live manifold only appears through
+// get_or_new_manifold, which records it), so lookups match a scan of the 16 slots.
+DEV void build_slot_map(ArenaLDS* A) {
+    for (int k = 0; k < kKeys; k++) A->a.slot_of_key[k] = -1;
+    for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
+        const rlgpu_manifold& mf = A->s.manifolds[m];
+        if (mf.count > 0 && mf.key >= 0 && mf.key < kKeys && A->a.slot_of_key[mf.key] < 0) A->a.slot_of_key[mf.key] = m;
+    }
+}
 DEV rlgpu_manifold* find_manifold(ArenaLDS* A, int key) {
-    for (int m = 0; m < RLGPU_MANIFOLDS; m++)
-        if (A->s.manifolds[m].count > 0 && A->s.manifolds[m].key == key) return &A->s.manifolds[m];
-    return nullptr;
+    int m = A->a.slot_of_key[key];
+    if (m < 0) return nullptr;
+    rlgpu_manifold* mf = &A->s.manifolds[m];
+    return (mf->count > 0 && mf->key == key) ? mf : nullptr;
 }
 DEV rlgpu_manifold* get_or_new_manifold(ArenaLDS* A, int key) {
     rlgpu_manifold* m = find_manifold(A, key);
@@ -48,6 +62,7 @@ DEV rlgpu_manifold* get_or_new_manifold(ArenaLDS* A, int key) {
     for (int k = 0; k < RLGPU_MANIFOLDS; k++)
         if (A->s.manifolds[k].count == 0) {
             A->s.manifolds[k].key = key;
+            A->a.slot_of_key[key] = (int8_t)k;
             return &A->s.manifolds[k];
         }
     return nullptr;
@@ -247,30 +262,29 @@ DEV void refresh(ArenaLDS* A, int key) {
     m3 ra, rb;
     side_transform(A, a, pa_, ra);
     side_transform(A, b, pb_, rb);
-    v3 wa[4], wb[4];
     for (int i = m->count - 1; i >= 0; i--) {
         rlgpu_contact& p = m->pts[i];
-        wa[i] = ra * ld3(p.localA) + pa_;
-        wb[i] = rb * ld3(p.localB) + pb_;
-        p.dist = dot(wa[i] - wb[i], ld3(p.normalB));
+        v3 wa = ra * ld3(p.localA) + pa_;
+        v3 wb = rb * ld3(p.localB) + pb_;
+        p.dist = dot(wa - wb, ld3(p.normalB));
     }
+    // (world points recomputed from the local ones: same operations, so the same values as
+    // the cached world positions of the reference)
     for (int i = m->count - 1; i >= 0; i--) {
         rlgpu_contact& p = m->pts[i];
         bool remove;
         if (!(p.dist <= cbt)) {
             remove = true;
         } else {
-            v3 proj = wa[i] - ld3(p.normalB) * p.dist;
-            v3 diff = wb[i] - proj;
+            v3 wa = ra * ld3(p.localA) + pa_;
+            v3 wb = rb * ld3(p.localB) + pb_;
+            v3 proj = wa - ld3(p.normalB) * p.dist;
+            v3 diff = wb - proj;
             remove = dot(diff, diff) > cbt * cbt;
         }
         if (remove) {
             int last = m->count - 1;
-            if (i != last) {
-                m->pts[i] = m->pts[last];
-                wa[i] = wa[last];
-                wb[i] = wb[last];
-            }
+            if (i != last) m->pts[i] = m->pts[last];
             m->count--;
         }
     }
@@ -769,10 +783,10 @@ DEV float resolve_split(Solver& S, CRow& c) {
 // btSequentialImpulseConstraintSolver::solveGroup (single lane per arena)
 DEV void solve(ArenaLDS* A) {
     Solver& S = A->u.sv;
-    bool in_solver[5];
+    unsigned in_solver = 0;  // bit i: body i takes part (bitmask: no private-memory array)
     for (int i = 0; i < 5; i++) {
         bool act = i == 0 ? A->a.ball_awake != 0 : A->a.active[i] != 0;
-        in_solver[i] = act;
+        if (act) in_solver |= 1u << i;
         SB& x = S.sb[i];
         x.dlin = x.dang = x.push = x.turn = zero3();
         x.real = act;
@@ -800,24 +814,16 @@ DEV void solve(ArenaLDS* A) {
         f.real = 0;
     }
     int nrows = 0;
-    // manifolds in ascending key order
-    int last_key = -1;
-    for (;;) {
-        int best = -1, bkey = 1 << 30;
-        for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
-            const rlgpu_manifold& mf = A->s.manifolds[m];
-            if (mf.count > 0 && mf.key > last_key && mf.key < bkey) {
-                bkey = mf.key;
-                best = m;
-            }
-        }
-        if (best < 0) break;
-        last_key = bkey;
-        rlgpu_manifold& mf = A->s.manifolds[best];
+    // manifolds in ascending key order = canonical rank order (pair_key is increasing)
+    for (int rank = 0; rank < kPairs; rank++) {
+        rlgpu_manifold* mfp = find_manifold(A, pair_key(rank));
+        if (!mfp) continue;
+        rlgpu_manifold& mf = *mfp;
+        const int best = (int)(mfp - A->s.manifolds);
         int a, b;
         key_bodies(mf.key, a, b);
-        bool aact = a < 10 && in_solver[a];
-        bool bact = b < 10 && in_solver[b];
+        bool aact = a < 10 && ((in_solver >> a) & 1u);
+        bool bact = b < 10 && ((in_solver >> b) & 1u);
         if (!aact && !bact) continue;
         int ia = aact ? a : 5, ib = bact ? b : 5;
         v3 pa_, pb_;
@@ -857,7 +863,7 @@ DEV void solve(ArenaLDS* A) {
         }
     }
     for (int i = 0; i < 5; i++) {
-        if (S.spec_num[i] <= 0 || !in_solver[i]) continue;
+        if (S.spec_num[i] <= 0 || !((in_solver >> i) & 1u)) continue;
         if (nrows >= kMaxRows) {
             A->s.env.manifold_overflow++;
             continue;
@@ -912,7 +918,7 @@ DEV void solve(ArenaLDS* A) {
         if (row.orig >= 0) A->s.manifolds[row.orig >> 2].pts[row.orig & 3].applied = row.applied;
     }
     for (int i = 0; i < 5; i++) {
-        if (!in_solver[i]) continue;
+        if (!((in_solver >> i) & 1u)) continue;
         SB& x = S.sb[i];
         rlgpu_body* bd = body(A, i);
         x.lin += x.dlin;

@@ -33,8 +33,9 @@ namespace rl {
 constexpr int kTeam = 16;           // lanes per arena
 constexpr int kArenas = 4;          // arenas per 64-thread workgroup
 constexpr int kMaxCand = 32;        // narrowphase candidates per tick per arena
-constexpr int kMaxRows = 24;        // solver contact rows per arena (+ as many friction rows)
+constexpr int kMaxRows = RLGPU_MAX_SOLVER_ROWS;  // solver contact rows per arena (+ as many friction rows)
 constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic
+constexpr int kKeys = 93;           // manifold keys 0..92 (env.h key encoding)
 constexpr float kTick = 1.f / 120.f;
 constexpr float kUU2BT = 1.f / 50.f;
 constexpr float kBT2UU = 50.f;
@@ -113,6 +114,7 @@ struct Aux {
     int touched[4];
     int goal;
     int traj_term;
+    int8_t slot_of_key[kKeys];  // manifold key -> slot (-1 none)
     float all_rewards[4];
 };
 

@@ -38,7 +38,7 @@ ENV = np.dtype([
     ("rng_counter", "<u4"), ("manifold_overflow", "<u4"), ("episode_steps", "<i4"), ("reserved0", "<i4"),
 ], align=True)
 ARENA = np.dtype([("ball", BODY), ("ball_vel_impulse_cache", "<f4", 3), ("ball_sleeping", "<i4"),
-                  ("cars", CAR, 4), ("pads", PAD, 34), ("manifolds", MANIFOLD, 16), ("env", ENV)], align=True)
+                  ("cars", CAR, 4), ("pads", PAD, 34), ("manifolds", MANIFOLD, 12), ("env", ENV)], align=True)
 
 
 def view(buf):

@@ -50,3 +50,11 @@ def test_error_channel_without_gpu():
                              None, None, None, None, None)
     assert st == -1
     assert b"negative" in L.rlgpu_last_error()
+
+
+def test_arena_wire_format_sizes_agree():
+    """numpy ARENA dtype == C sizeof(rlgpu_arena_state) in the product library and the oracle."""
+    import oracle
+    from rlgpu._lib import lib
+    from rlgpu.state import ARENA
+    assert lib().rlgpu_arena_state_size() == ARENA.itemsize == oracle.arena_state_size()

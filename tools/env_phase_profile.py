@@ -1,0 +1,44 @@
+"""Per-phase cycle breakdown of the env kernel (rlgpu_envset_set_profile) at the C2 size."""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "reinforcement-learning_amd")]
+from rlgpu import _lib  # noqa: E402
+from rlgpu.env import EnvSet  # noqa: E402
+
+NAMES = ["T0 sleep/demo/snapshot", "T1 wheels (16 lanes)", "T2 car logic + pads pre", "T3 gravity/predict",
+         "T4 ball awake", "T5 narrowphase", "T6 commit + solve (lane 0)", "T7 integrate", "T8 car post/finish",
+         "T9 pad collide", "T10 pad post + ball finish", "prelude / halves", "builders", "obs rows", "resets", "store", "T6a commit (part of T6 above)"]
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+dev = torch.device("cuda:0")
+env = EnvSet(n, seed=1234, device=dev)
+gen = torch.Generator(device=dev).manual_seed(7)
+acts = torch.empty(4 * n, dtype=torch.int32, device=dev)
+for i in range(8):
+    acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
+    env.step(acts, True)
+prof = torch.zeros(32, dtype=torch.int64, device=dev)
+L = _lib.lib()
+L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+_lib.check(L.rlgpu_envset_set_profile(env._h, ctypes.c_void_p(prof.data_ptr())), "set_profile")
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+tot_ms = 0.0
+for i in range(steps):
+    acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
+    e0.record()
+    env.step(acts, True)
+    e1.record()
+    torch.cuda.synchronize()
+    tot_ms += e0.elapsed_time(e1)
+c = prof.cpu().tolist()
+wg = (n + 3) // 4
+total = sum(c[:16])
+c[6] += c[16]  # T6 = commit + solve
+print(f"{n} arenas, {steps} steps, {tot_ms / steps:.3f} ms/step (profiled build)")
+for k in range(17):
+    print(f"  {NAMES[k]:28s} {c[k] / total * 100:6.2f} %   {c[k] / wg / steps:12.0f} cycles/WG/step")
