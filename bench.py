@@ -115,10 +115,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    from rlgpu.dist import max_over_ranks
+    el = max_over_ranks(el, device=dev)
     env_steps = world * args.arenas * cfg.rollout_len * args.steps
     agent_steps = 4 * env_steps
     value = env_steps / el

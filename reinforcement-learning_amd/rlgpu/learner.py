@@ -17,6 +17,7 @@ import time
 
 import numpy as np
 
+from . import dist as _dist
 from . import gae as _gae
 from .env import EnvSet, StepOutputs
 from .ppo import PPO, permutation
@@ -147,17 +148,11 @@ class Learner:
         # return-std Welford over randomly sampled returns (Learner.cpp:959-967)
         k = self.cfg.return_samples
         idx = torch.from_numpy(self.rng.integers(0, T * P, size=k)).to(self.device)
-        samples = self.ret.view(-1)[idx]
-        if self.world > 1:
-            allv = [torch.empty_like(samples) for _ in range(self.world)]
-            torch.distributed.all_gather(allv, samples, group=self.group)
-            samples = torch.cat(allv)
+        samples = _dist.gather_samples(self.ret.view(-1)[idx], self.group)
         self.return_stat.add(samples.cpu().numpy())
 
     # ---------------------------------------------------------------- learning
     def learn(self):
-        import torch
-        import torch.distributed as dist
         cfg, ppo = self.cfg, self.ppo
         M = self.T * self.P
         global_m = M * self.world
@@ -170,11 +165,7 @@ class Learner:
             perm = permutation(M, cfg.seed + self.rank, self.iteration * cfg.epochs + epoch, device=self.device)
             # batch advantage normalisation (PPOLearner.cpp:360-371), global over ranks
             if self.world > 1:
-                s = torch.stack([adv.double().sum(), (adv.double() ** 2).sum()])
-                dist.all_reduce(s, group=self.group)
-                mean = s[0] / global_m
-                std = torch.sqrt((s[1] - s[0] * mean) / (global_m - 1))
-                ppo.adv_stats.copy_(torch.stack([mean, std]).float())
+                ppo.adv_stats.copy_(_dist.global_mean_std(adv, self.group))
             else:
                 ppo.adv_normalizer(adv)
             local_batch = M if cfg.batch_size is None else min(M, cfg.batch_size // self.world)
@@ -183,8 +174,7 @@ class Learner:
                 for s0 in range(b0, b1, cfg.mini_batch_size):
                     n = min(cfg.mini_batch_size, b1 - s0)
                     ppo.minibatch(obs, masks, acts, logp, adv, tgt, perm, s0, n, batch)
-                if self.world > 1:
-                    dist.all_reduce(ppo.grads, group=self.group)
+                _dist.allreduce_grads(ppo.grads, self.group)  # RCCL over xGMI, before clip_grad_norm_
                 ppo.optimizer_step()
 
     def iterate(self):

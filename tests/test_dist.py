@@ -1,0 +1,96 @@
+"""Multi-rank logic of the Learner (rlgpu/dist.py) on CPU with gloo, world size 2.
+
+The GPU path uses the same functions over RCCL; here torch CPU tensors stand in for the HBM
+buffers.  Checks: gradient all-reduce with global-batch loss scaling equals the single-device
+gradient of the whole batch; global advantage moments equal the single-device ones; return samples
+gathered identically on every rank; max-over-ranks timing; arena sharding is a partition.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.LayerNorm(16), torch.nn.LeakyReLU(),
+                               torch.nn.Linear(16, 3))
+
+
+def _loss(m, x, y, global_batch):
+    # the reference scales each minibatch loss by mb / batchSize (PPOLearner.cpp:374)
+    return torch.nn.functional.mse_loss(m(x), y) * (x.shape[0] / global_batch)
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd"))
+    from rlgpu import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(1)
+        X, Y = torch.randn(64, 6, generator=g), torch.randn(64, 3, generator=g)
+        lo, hi = D.arena_range(rank, 32)
+        m = _model()
+        # each rank: two minibatches of its shard, accumulate, then all-reduce
+        for a in range(lo, hi, 16):
+            _loss(m, X[a:a + 16], Y[a:a + 16], 64).backward()
+        flat = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+        D.allreduce_grads(flat)
+        adv = torch.randn(1000, generator=torch.Generator().manual_seed(10 + rank))
+        st = D.global_mean_std(adv)
+        smp = D.gather_samples(torch.full((3,), float(rank)))
+        t = D.max_over_ranks(0.5 + rank)
+        q.put((rank, flat.numpy(), st.numpy(), smp.numpy(), t))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_gloo_reductions():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    # single-device reference over the whole batch
+    g = torch.Generator().manual_seed(1)
+    X, Y = torch.randn(64, 6, generator=g), torch.randn(64, 3, generator=g)
+    m = _model()
+    _loss(m, X, Y, 64).backward()
+    want = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).numpy()
+    for r in res:
+        np.testing.assert_allclose(r[1], want, rtol=1e-5, atol=1e-7)
+    advs = torch.cat([torch.randn(1000, generator=torch.Generator().manual_seed(10 + r)) for r in range(world)])
+    np.testing.assert_allclose(res[0][2], [advs.mean().item(), advs.std().item()], rtol=1e-5)
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+    np.testing.assert_array_equal(res[0][3], [0, 0, 0, 1, 1, 1])
+    np.testing.assert_array_equal(res[1][3], res[0][3])
+    assert res[0][4] == res[1][4] == 1.5
+
+
+def test_arena_sharding_is_a_partition():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd"))
+    from rlgpu.dist import arena_range
+    seen = []
+    for r in range(8):
+        lo, hi = arena_range(r, 4096)
+        seen.extend(range(lo, hi))
+    assert seen == list(range(32768))
