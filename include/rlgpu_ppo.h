@@ -111,6 +111,14 @@ int rlgpu_ppo_zero_grad(rlgpu_ppo* h, void* stream);
 /* Optimizer state (step count + moments) for checkpointing; moments are device pointers. */
 int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_exp_avg, float** d_exp_avg_sq);
 
+/* Building block, exported for tests and microbenchmarks: C[I,J] = sum_k A(i,k) B(k,j) (+ bias[j])
+ * on f32-input MFMA.  a_layout 0: A stored [I][lda] (k contiguous), 1: [K][lda] (i contiguous);
+ * b_layout 0: B stored [J][ldb] (k contiguous), 1: [K][ldb] (j contiguous).  splits > 1 writes
+ * per-split partials to C + s*I*ldc (caller reduces).  Supported pairs: (0,0), (0,1), (1,1). */
+int rlgpu_gemm_f32(int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B, int64_t ldb,
+                   float* d_C, int64_t ldc, const float* d_bias, int32_t I, int32_t J, int32_t K, int32_t splits,
+                   void* stream);
+
 /* Random permutation of [0, n) (Philox keys + device radix sort): ExperienceBuffer shuffle. */
 int rlgpu_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t* d_out, void* stream);
 

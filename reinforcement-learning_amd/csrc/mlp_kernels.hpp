@@ -35,14 +35,11 @@ struct GemmArgs {
     const float* B;
     float* C;
     const float* bias;     // [J] or null
-    const int32_t* a_idx;  // row gather for A_IK (indexed by i + a_off)
-    const int32_t* b_idx;  // row gather for B_KJ (indexed by k + b_off)
-    int64_t a_off, b_off;
     int64_t lda, ldb, ldc;
     int I, J, K;
     int kchunk;            // K range per split (multiple of BK)
     int64_t c_split;       // element stride between split partials
-    int a_vec, b_vec;      // 16-byte aligned rows (ld % 4 == 0, base aligned): float4 loads
+    int gx, gy, gz;        // logical tile grid (J tiles, I tiles, K splits); launched as 1-D
 };
 
 DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays NaN)
@@ -51,40 +48,63 @@ DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays Na
 }
 DEV float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
 
-// 4 consecutive elements p[c..c+3] of a row, zero outside [.., lim)
-DEV float4 load4(const float* p, int c, int lim, bool vec) {
-    if (!p) return make_float4(0.f, 0.f, 0.f, 0.f);
-    if (vec && c + 3 < lim) return *reinterpret_cast<const float4*>(p + c);
-    float4 v;
-    v.x = c < lim ? p[c] : 0.f;
-    v.y = c + 1 < lim ? p[c + 1] : 0.f;
-    v.z = c + 2 < lim ? p[c + 2] : 0.f;
-    v.w = c + 3 < lim ? p[c + 3] : 0.f;
-    return v;
+// Operand staging.  Every global load is branch-free (divergent bounds branches made the compiler
+// drain vmcnt after each load and serialised the register prefetch): absent rows read a zero row,
+// out-of-range elements are zeroed by a select after an in-bounds load.  VEC (compile time):
+// 16-byte aligned rows whose elements past the bound up to the next multiple of 4 are readable
+// and finite (they meet zeros of the other operand).
+__device__ float4 g_zero_row[4];  // zero-initialised device memory
+
+template <bool VEC>
+DEV float4 load4(const float* p, int c, int lim) {
+    const float* z = reinterpret_cast<const float*>(g_zero_row);
+    if (VEC) {
+        const float* q = (p && c < lim) ? p + c : z;
+        return *reinterpret_cast<const float4*>(q);
+    }
+    const float* base = p ? p : z;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        bool ok = p && (c + k < lim);
+        float t = base[ok ? c + k : 0];
+        v[k] = ok ? t : 0.f;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// One 128 x 32 tile of an operand, 4 float4 per thread.
-//  KMAJ (global row = output index, k contiguous) -> LDS [row][BK + KP]
-//  !KMAJ (global row = k, output index contiguous) -> LDS [k][BM + MP]
+// Per-thread share of one 128 x 32 tile: 4 float4.  KMAJ (global row = output index, k contiguous):
+// the 4 row pointers are fixed for the whole K loop (computed once).  !KMAJ (global row = k):
+// row pointers follow k.
+struct RowPtrs {
+    const float* p[4];
+};
 template <bool KMAJ>
-DEV void tile_load(float4 (&r)[4], const float* base, int64_t ld, const int32_t* idx, int64_t off, int o0, int on, int k0,
-                   int ke, bool vec) {
-    const int t = threadIdx.x;
+DEV RowPtrs kmaj_rows(const float* base, int64_t ld, int o0, int on) {
+    RowPtrs r;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        int e = t + 256 * q;
+        if (!KMAJ) {
+            r.p[q] = nullptr;
+            continue;
+        }
+        int e = threadIdx.x + 256 * q;
+        int go = o0 + (e >> 3);
+        r.p[q] = go < on ? base + (int64_t)go * ld : nullptr;
+    }
+    return r;
+}
+template <bool KMAJ, bool VEC>
+DEV void tile_load(float4 (&r)[4], const RowPtrs& rows, const float* base, int64_t ld, int o0, int on, int k0, int ke) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int e = threadIdx.x + 256 * q;
         if (KMAJ) {
-            int row = e >> 3, c = (e & 7) * 4;
-            int go = o0 + row;
-            const float* p = nullptr;
-            if (go < on) p = base + (idx ? (int64_t)idx[off + go] : (int64_t)go) * ld;
-            r[q] = load4(p, k0 + c, ke, vec);
+            r[q] = load4<VEC>(rows.p[q], k0 + (e & 7) * 4, ke);
         } else {
-            int kr = e >> 5, c = (e & 31) * 4;
-            int k = k0 + kr;
-            const float* p = nullptr;
-            if (k < ke) p = base + (idx ? (int64_t)idx[off + k] : (int64_t)k) * ld;
-            r[q] = load4(p, o0 + c, on, vec);
+            int k = k0 + (e >> 5);
+            const float* p = k < ke ? base + (int64_t)k * ld : nullptr;
+            r[q] = load4<VEC>(p, o0 + (e & 31) * 4, on);
         }
     }
 }
@@ -111,9 +131,27 @@ DEV float tile_at(const float* lds, int o, int k) {
     return KMAJ ? lds[o * (BK + KP) + k] : lds[k * (BM + MP) + o];
 }
 
+// XCD-aware tile order.  Workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// L2), so consecutive block ids land on different L2s.  Launch a 1-D grid and map block p to the
+// logical tile t so that consecutive logical tiles -- the J tiles sharing one A panel, or the
+// (I, J) tiles of one split-K chunk -- run on the same XCD and share its L2.
+struct Tile {
+    int x, y, z;
+};
+DEV Tile xcd_tile(int gx, int gy, int gz) {
+    const int n = gx * gy * gz, p = blockIdx.x;
+    const int q = n >> 3, r = n & 7, xcd = p & 7, slot = p >> 3;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+    Tile o;
+    o.x = t % gx;
+    o.y = (t / gx) % gy;
+    o.z = t / (gx * gy);
+    return o;
+}
+
 // fp32 GEMM on v_mfma_f32_32x32x2_f32: each MFMA j of a BK step takes k = j (lanes 0-31) and
 // k = 16 + j (lanes 32-63) so that k-contiguous tiles are read as 16-byte vectors.
-template <int LA, int LB>
+template <int LA, int LB, bool AV, bool BV>
 __global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
     constexpr int ASZ = AK ? BM * (BK + KP) : BK * (BM + MP);
@@ -122,8 +160,9 @@ __global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
     __shared__ float Bs[BSZ];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
-    const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
-    const int kb = blockIdx.z * g.kchunk;
+    const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
+    const int i0 = tl.y * BM, j0 = tl.x * BN;
+    const int kb = tl.z * g.kchunk;
     const int ke = min(g.K, kb + g.kchunk);
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[2][2];
@@ -131,17 +170,19 @@ __global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
         for (int b = 0; b < 2; b++)
             for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
     float4 ra[4], rb[4];
+    const RowPtrs arow = kmaj_rows<AK>(g.A, g.lda, i0, g.I);
+    const RowPtrs brow = kmaj_rows<BKM>(g.B, g.ldb, j0, g.J);
     if (kb < ke) {
-        tile_load<AK>(ra, g.A, g.lda, g.a_idx, g.a_off, i0, g.I, kb, ke, g.a_vec);
-        tile_load<BKM>(rb, g.B, g.ldb, g.b_idx, g.b_off, j0, g.J, kb, ke, g.b_vec);
+        tile_load<AK, AV>(ra, arow, g.A, g.lda, i0, g.I, kb, ke);
+        tile_load<BKM, BV>(rb, brow, g.B, g.ldb, j0, g.J, kb, ke);
     }
     for (int k0 = kb; k0 < ke; k0 += BK) {
         tile_store<AK>(As, ra);
         tile_store<BKM>(Bs, rb);
         __syncthreads();
         if (k0 + BK < ke) {  // prefetch the next stage into registers while the MFMAs run
-            tile_load<AK>(ra, g.A, g.lda, g.a_idx, g.a_off, i0, g.I, k0 + BK, ke, g.a_vec);
-            tile_load<BKM>(rb, g.B, g.ldb, g.b_idx, g.b_off, j0, g.J, k0 + BK, ke, g.b_vec);
+            tile_load<AK, AV>(ra, arow, g.A, g.lda, i0, g.I, k0 + BK, ke);
+            tile_load<BKM, BV>(rb, brow, g.B, g.ldb, j0, g.J, k0 + BK, ke);
         }
         const int ma = wm * 64 + l32, nb = wn * 64 + l32;
 #pragma unroll
@@ -156,7 +197,7 @@ __global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
         }
         __syncthreads();
     }
-    float* C = g.C + (int64_t)blockIdx.z * g.c_split;
+    float* C = g.C + (int64_t)tl.z * g.c_split;
 #pragma unroll
     for (int ti = 0; ti < 2; ti++)
 #pragma unroll
@@ -182,6 +223,7 @@ struct HGemmArgs {
     uint16_t* C;            // [I][ldc] bf16
     int64_t lda, ldb, ldc;
     int I, J, K;
+    int gx, gy;             // logical tile grid; launched as 1-D (xcd_tile)
 };
 
 template <bool A_F32>
@@ -190,7 +232,8 @@ __global__ void __launch_bounds__(256) gemm_bf16(HGemmArgs g) {
     __shared__ uint16_t Bs[BN][HBK + HPAD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
-    const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
+    const Tile tl = xcd_tile(g.gx, g.gy, 1);
+    const int i0 = tl.y * BM, j0 = tl.x * BN;
     f32x16 acc[2][2];
     for (int a = 0; a < 2; a++)
         for (int b = 0; b < 2; b++)
@@ -249,6 +292,16 @@ __global__ void __launch_bounds__(256) gemm_bf16(HGemmArgs g) {
 }
 
 // out[e] (+)= sum_s part[s*stride + e], fixed order (deterministic split-K reduction)
+// Minibatch gather (ExperienceBuffer::_GetSamples index_select, ExperienceBuffer.cpp:140-163):
+// X[r, 0..C) = src[idx[start + r], 0..C), rows padded to ldx (16-byte aligned) with zeros.
+__global__ void gather_rows(const float* src, int C, const int32_t* idx, int64_t start, int n, float* X, int ldx) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)n * ldx) return;
+    int r = (int)(e / ldx), c = (int)(e % ldx);
+    int64_t s = idx ? (int64_t)idx[start + r] : start + r;
+    X[e] = c < C ? src[s * C + c] : 0.f;
+}
+
 __global__ void reduce_splits(const float* part, int splits, int64_t stride, int64_t n, float* out, int accumulate) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
@@ -358,76 +411,96 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 // Backward of LeakyReLU(LN(Z)): dZ from dA; per-block column partials of
 // dbias = sum dZ, dgamma = sum dH*xhat, dbeta = sum dH -> part[blk][3][H] (the flat parameter
 // order Linear.bias, LayerNorm.weight, LayerNorm.bias, so one reduction serves all three).
-constexpr int LNB_ROWS = 128;
+// Lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (float4 loads); gamma / beta stay
+// in registers; each of the 4 waves walks LNB_ROWS/4 rows.
+constexpr int LNB_ROWS = 32;
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* xhat, const float* rstd, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
                                                  float* part) {
-    __shared__ float red[4][3][1024];
-    int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int nper = MAXH;
-    float pg[MAXH], pb[MAXH], pz[MAXH];
-    for (int q = 0; q < nper; q++) pg[q] = pb[q] = pz[q] = 0.f;
-    int r0 = blockIdx.x * LNB_ROWS;
+    __shared__ float red[4][3][64 * MAXH];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c0 = lane * MAXH;
+    const bool vec = (H % 4 == 0) && (c0 + MAXH <= H);
+    float g[MAXH], b[MAXH], pg[MAXH], pb[MAXH], pz[MAXH];
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) {
+        int c = c0 + q;
+        g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
+        b[q] = (use_ln && c < H) ? beta[c] : 0.f;
+        pg[q] = pb[q] = pz[q] = 0.f;
+    }
+    const int r0 = blockIdx.x * LNB_ROWS;
     for (int rr = w; rr < LNB_ROWS; rr += 4) {
-        int row = r0 + rr;
+        const int row = r0 + rr;
         if (row >= R) break;
-        const float* da = dA + (int64_t)row * H;
-        const float* xh = xhat + (int64_t)row * H;
-        float dh[MAXH], x[MAXH];
-        float s1 = 0.f, s2 = 0.f;
-        for (int q = 0; q < nper; q++) {
-            int c = lane + 64 * q;
-            dh[q] = 0.f;
-            x[q] = 0.f;
-            if (c < H) {
-                x[q] = xh[c];
-                float h = use_ln ? x[q] * gamma[c] + beta[c] : x[q];
-                dh[q] = h > 0.f ? da[c] : da[c] * slope;
-                if (use_ln) {
-                    float gg = dh[q] * gamma[c];
-                    s1 += gg;
-                    s2 += gg * x[q];
-                }
+        const float* da = dA + (int64_t)row * H + c0;
+        const float* xh = xhat + (int64_t)row * H + c0;
+        float dh[MAXH], x[MAXH], av[MAXH];
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 4) {
+                float4 t = *reinterpret_cast<const float4*>(xh + q);
+                float4 u = *reinterpret_cast<const float4*>(da + q);
+                x[q] = t.x; x[q + 1] = t.y; x[q + 2] = t.z; x[q + 3] = t.w;
+                av[q] = u.x; av[q + 1] = u.y; av[q + 2] = u.z; av[q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) {
+                bool in = c0 + q < H;
+                x[q] = in ? xh[q] : 0.f;
+                av[q] = in ? da[q] : 0.f;
             }
         }
-        float* dz = dZ + (int64_t)row * H;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) {
+            float h = x[q] * g[q] + b[q];
+            dh[q] = h > 0.f ? av[q] : av[q] * slope;
+            float gg = dh[q] * g[q];
+            s1 += gg;
+            s2 += gg * x[q];
+        }
+        float* dz = dZ + (int64_t)row * H + c0;
+        float d[MAXH];
         if (use_ln) {
             float m1 = wave_sum(s1) / (float)H, m2 = wave_sum(s2) / (float)H;
             float rs = rstd[row];
-            for (int q = 0; q < nper; q++) {
-                int c = lane + 64 * q;
-                if (c < H) {
-                    float d = rs * (dh[q] * gamma[c] - m1 - x[q] * m2);
-                    dz[c] = d;
-                    pg[q] += dh[q] * x[q];
-                    pb[q] += dh[q];
-                    pz[q] += d;
-                }
-            }
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) d[q] = rs * (dh[q] * g[q] - m1 - x[q] * m2);
         } else {
-            for (int q = 0; q < nper; q++) {
-                int c = lane + 64 * q;
-                if (c < H) {
-                    dz[c] = dh[q];
-                    pz[q] += dh[q];
-                }
-            }
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) d[q] = dh[q];
+        }
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 4)
+                *reinterpret_cast<float4*>(dz + q) = make_float4(d[q], d[q + 1], d[q + 2], d[q + 3]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++)
+                if (c0 + q < H) dz[q] = d[q];
+        }
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) {
+            bool in = c0 + q < H;
+            pz[q] += in ? d[q] : 0.f;
+            pg[q] += in ? dh[q] * x[q] : 0.f;
+            pb[q] += in ? dh[q] : 0.f;
         }
     }
-    for (int q = 0; q < nper; q++) {
-        int c = lane + 64 * q;
-        if (c < H) {
-            red[w][0][c] = pz[q];
-            red[w][1][c] = pg[q];
-            red[w][2][c] = pb[q];
-        }
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) {
+        red[w][0][c0 + q] = pz[q];
+        red[w][1][c0 + q] = pg[q];
+        red[w][2][c0 + q] = pb[q];
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 3 * H; e += 256) {
-        int k = e / H, c = e % H;
-        part[(int64_t)blockIdx.x * 3 * H + e] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
-    }
+    float* out = part + (int64_t)blockIdx.x * 3 * H;
+    for (int k = 0; k < 3; k++)
+        for (int c = threadIdx.x; c < H; c += 256)
+            out[k * H + c] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
 }
 
 // NPER (columns per lane) dispatch: H <= 64 * NPER
@@ -443,6 +516,67 @@ RLGPU_NPER_DISPATCH(ln_act_fwd_f32)
 RLGPU_NPER_DISPATCH(ln_act_fwd_bf16)
 RLGPU_NPER_DISPATCH(ln_act_bwd)
 
+// Rank-1 output layer (the critic's Linear(H, 1)): GEMM tiles would be 1/128 occupied, so the
+// head runs as wave-per-row dot products.  Lane l owns columns [MAXH*l, MAXH*l + MAXH).
+template <int MAXH>
+__global__ void __launch_bounds__(256) head1_fwd(const float* X, const float* w, const float* b, int R, int H, float* out) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= R) return;
+    const int c0 = lane * MAXH;
+    const float* x = X + (int64_t)row * H;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) {
+        int c = c0 + q;
+        if (c < H) s += x[c] * w[c];
+    }
+    s = wave_sum(s);
+    if (lane == 0) out[row] = s + b[0];
+}
+
+// Backward of the rank-1 head: dA[i, :] = dv[i] * w; partials part[blk][0..H) = sum dv*X[i, :],
+// part[blk][H] = sum dv (bias) over the block's rows.
+template <int MAXH>
+__global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w, const float* dv, int R, int H, float* dA,
+                                                float* part) {
+    __shared__ float red[4][64 * MAXH + 1];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c0 = lane * MAXH;
+    float wr[MAXH], acc[MAXH];
+    float accb = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) {
+        wr[q] = c0 + q < H ? w[c0 + q] : 0.f;
+        acc[q] = 0.f;
+    }
+    const int r0 = blockIdx.x * LNB_ROWS;
+    for (int rr = wv; rr < LNB_ROWS; rr += 4) {
+        const int row = r0 + rr;
+        if (row >= R) break;
+        const float d = dv[row];
+        const float* x = X + (int64_t)row * H;
+        float* da = dA + (int64_t)row * H;
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) {
+            int c = c0 + q;
+            if (c < H) {
+                da[c] = d * wr[q];
+                acc[q] += d * x[c];
+            }
+        }
+        accb += d;
+    }
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) red[wv][c0 + q] = acc[q];
+    if (lane == 0) red[wv][64 * MAXH] = accb;
+    __syncthreads();
+    float* out = part + (int64_t)blockIdx.x * (H + 1);
+    for (int c = threadIdx.x; c < H; c += 256) out[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    if (threadIdx.x == 0) out[H] = red[0][64 * MAXH] + red[1][64 * MAXH] + red[2][64 * MAXH] + red[3][64 * MAXH];
+}
+RLGPU_NPER_DISPATCH(head1_fwd)
+RLGPU_NPER_DISPATCH(head1_bwd)
+
 // Per-block column partial sums of X [R, Cn] (Cn <= 1024): part[blk][Cn].
 constexpr int CS_ROWS = 256;
 __global__ void __launch_bounds__(256) colsum_partial(const float* X, int R, int Cn, float* part) {
@@ -454,22 +588,26 @@ __global__ void __launch_bounds__(256) colsum_partial(const float* X, int R, int
     }
 }
 
-// grad[c] += sum_b part[b*stride + off + c] for c < n: 16 row groups x 64 columns per
-// 1024-thread block, combined in LDS in a fixed order (deterministic).
+// Column reduction of per-block partials, deterministic, two levels:
+//   stage 1 (grid ceil(n/64) x G): block (x, y) sums partial rows b = y, y+G, ... of 64 columns
+//            (16 row groups of 64 threads, combined in LDS in a fixed order) -> out2[y][c]
+//   stage 2 (the same kernel with G = 1 on out2, accumulate = 1): grad[c] += sum_y out2[y][c]
 __global__ void __launch_bounds__(1024) reduce_cols(const float* part, int nblk, int64_t stride, int64_t off, int n,
-                                                   float* grad) {
+                                                   float* out, int64_t out_stride, int accumulate) {
     __shared__ float red[16][64];
-    int cl = threadIdx.x & 63, gi = threadIdx.x >> 6;
-    int c = blockIdx.x * 64 + cl;
+    const int cl = threadIdx.x & 63, gi = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const int G = gridDim.y, y = blockIdx.y;
     float s = 0.f;
     if (c < n)
-        for (int b = gi; b < nblk; b += 16) s += part[(int64_t)b * stride + off + c];
+        for (int b = y + G * gi; b < nblk; b += 16 * G) s += part[(int64_t)b * stride + off + c];
     red[gi][cl] = s;
     __syncthreads();
     if (gi == 0 && c < n) {
         float tot = 0.f;
         for (int k = 0; k < 16; k++) tot += red[k][cl];
-        grad[c] += tot;
+        float* o = out + (int64_t)y * out_stride + c;
+        *o = accumulate ? *o + tot : tot;
     }
 }
 

@@ -44,6 +44,8 @@ struct rlgpu_ppo {
     // shared workspace
     float *out = nullptr, *dout = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr;
     float *scratch = nullptr;  // clip partials + coefficients
+    float* x0 = nullptr;       // gathered minibatch obs, rows padded to x_ld floats
+    int x_ld = 0;
     uint16_t *zh = nullptr, *ah[2] = {nullptr, nullptr}, *logits_h = nullptr;
     std::vector<void*> allocs;
 
@@ -58,18 +60,16 @@ struct rlgpu_ppo {
 
 namespace {
 
-void gemm_f32(int la, int lb, const float* A, int64_t lda, const int32_t* a_idx, int64_t a_off, const float* B, int64_t ldb,
-              const int32_t* b_idx, int64_t b_off, float* C, int64_t ldc, const float* bias, int I, int J, int K, int splits,
-              hipStream_t s) {
+// C[I,J] (+ bias) = A . B with the layouts of mlp::gemm_f32.  *_tail_ok: the operand's rows are
+// zero-padded up to a multiple of 4 past the bound (so float4 loads may straddle it).
+void gemm_f32(int la, int lb, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+              const float* bias, int I, int J, int K, int splits, hipStream_t s, bool a_tail_ok = false,
+              bool b_tail_ok = false) {
     mlp::GemmArgs g;
     g.A = A;
     g.B = B;
     g.C = C;
     g.bias = bias;
-    g.a_idx = a_idx;
-    g.b_idx = b_idx;
-    g.a_off = a_off;
-    g.b_off = b_off;
     g.lda = lda;
     g.ldb = ldb;
     g.ldc = ldc;
@@ -80,18 +80,29 @@ void gemm_f32(int la, int lb, const float* A, int64_t lda, const int32_t* a_idx,
     g.kchunk = (int)ceil_div(chunk, mlp::BK) * mlp::BK;
     int z = (int)ceil_div(K, g.kchunk);
     g.c_split = (int64_t)I * ldc;
-    g.a_vec = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
-    g.b_vec = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
-    dim3 grid(ceil_div(J, mlp::BN), ceil_div(I, mlp::BM), z);
-    if (la == mlp::A_IK && lb == mlp::B_JK)
-        hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_IK, mlp::B_JK>), grid, dim3(256), 0, s, g);
-    else if (la == mlp::A_IK && lb == mlp::B_KJ)
-        hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_IK, mlp::B_KJ>), grid, dim3(256), 0, s, g);
-    else if (la == mlp::A_KI && lb == mlp::B_KJ)
-        hipLaunchKernelGGL((mlp::gemm_f32<mlp::A_KI, mlp::B_KJ>), grid, dim3(256), 0, s, g);
-    else
-        throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "gemm layout");
-    RLGPU_CHECK_HIP(hipGetLastError());
+    // float4 path: 16-byte aligned rows and a bound (K for k-contiguous, I / J otherwise) that is a
+    // multiple of 4 or zero-padded past it (split-K chunk ends are multiples of BK)
+    const int a_lim = la == mlp::A_IK ? K : I, b_lim = lb == mlp::B_JK ? K : J;
+    const bool av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && (a_lim % 4 == 0 || a_tail_ok);
+    const bool bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0) && (b_lim % 4 == 0 || b_tail_ok);
+    g.gx = (int)ceil_div(J, mlp::BN);
+    g.gy = (int)ceil_div(I, mlp::BM);
+    g.gz = z;
+    dim3 grid(g.gx * g.gy * g.gz), blk(256);
+#define RLGPU_GEMM_CASE(LA, LB)                                                                                  \
+    if (la == LA && lb == LB) {                                                                                  \
+        if (av && bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, true>), grid, blk, 0, s, g);               \
+        else if (av) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, false>), grid, blk, 0, s, g);              \
+        else if (bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, false, true>), grid, blk, 0, s, g);              \
+        else hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, false, false>), grid, blk, 0, s, g);                     \
+        RLGPU_CHECK_HIP(hipGetLastError());                                                                      \
+        return;                                                                                                  \
+    }
+    RLGPU_GEMM_CASE(mlp::A_IK, mlp::B_JK)
+    RLGPU_GEMM_CASE(mlp::A_IK, mlp::B_KJ)
+    RLGPU_GEMM_CASE(mlp::A_KI, mlp::B_KJ)
+#undef RLGPU_GEMM_CASE
+    throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "gemm layout");
 }
 
 int splits_for(int rows) {
@@ -100,62 +111,89 @@ int splits_for(int rows) {
 }
 
 // dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
-void weight_grad(rlgpu_ppo* h, const float* dZ, int out, const float* X, int64_t ldx, const int32_t* x_idx, int64_t x_off,
-                 int in, int n, float* gW, hipStream_t s) {
+void weight_grad(rlgpu_ppo* h, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
+                 bool x_tail_ok = false) {
     int splits = splits_for(n);
     int chunk = (int)ceil_div(ceil_div(n, splits), mlp::BK) * mlp::BK;
     int z = (int)ceil_div(n, chunk);
-    gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, nullptr, 0, X, ldx, x_idx, x_off, h->wpart, in, nullptr, out, in, n, splits, s);
+    gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, h->wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
     int64_t e = (int64_t)out * in;
     hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->wpart, z, e, e, gW, 1);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+// grad[0..n) += column sums of nblk partial rows (stride apart) -- two fixed-order levels
+void reduce_partials(rlgpu_ppo* h, const float* part, int nblk, int64_t stride, int n, float* grad, hipStream_t s) {
+    const int G = nblk >= 256 ? 16 : 1;
+    float* mid = h->scratch + 2048;  // [16][<= 3 * 1024]
+    if (G > 1) {
+        hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(n, 64), G), dim3(1024), 0, s, part, nblk, stride, (int64_t)0, n,
+                           mid, (int64_t)n, 0);
+        hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(n, 64), 1), dim3(1024), 0, s, mid, G, (int64_t)n, (int64_t)0, n,
+                           grad, (int64_t)0, 1);
+    } else {
+        hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(n, 64), 1), dim3(1024), 0, s, part, nblk, stride, (int64_t)0, n,
+                           grad, (int64_t)0, 1);
+    }
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
 void colsum_into(rlgpu_ppo* h, const float* X, int n, int C, float* g, hipStream_t s) {
     int nb = (int)ceil_div(n, mlp::CS_ROWS);
     hipLaunchKernelGGL(mlp::colsum_partial, dim3(nb), dim3(256), 0, s, X, n, C, h->cpart);
-    hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(C, 64)), dim3(1024), 0, s, h->cpart, nb, (int64_t)C, (int64_t)0, C, g);
     RLGPU_CHECK_HIP(hipGetLastError());
+    reduce_partials(h, h->cpart, nb, C, C, g, s);
 }
 
-// fp32 training forward; keeps activations; writes the output layer to `out`.
-void forward_train(rlgpu_ppo* h, int mi, const float* X, const int32_t* idx, int64_t start, int n, float* out, hipStream_t s) {
+// fp32 training forward; keeps activations; writes the output layer to `out`.  X is the
+// gathered, zero-padded minibatch copy (row stride h->x_ld).
+void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipStream_t s) {
     Model& m = h->M[mi];
     const float* P = h->params;
     int nh = (int)m.L.size() - 1;
     const float* in = X;
-    const int32_t* in_idx = idx;
-    int64_t in_off = start, ld = m.in;
+    int64_t ld = h->x_ld;
+    bool tail_ok = true;
     for (int l = 0; l < nh; l++) {
         const Layer& L = m.L[l];
-        gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, in_idx, in_off, P + L.w, L.in, nullptr, 0, m.xhat[l], L.out, P + L.b, n, L.out,
-                 L.in, 1, s);
+        gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s, tail_ok);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, 4)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.xhat[l], m.act[l], m.rstd[l]);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = m.act[l];
-        in_idx = nullptr;
-        in_off = 0;
         ld = L.out;
+        tail_ok = false;
     }
     const Layer& O = m.L[nh];
-    gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, nullptr, 0, P + O.w, O.in, nullptr, 0, out, O.out, P + O.b, n, O.out, O.in, 1, s);
+    if (O.out == 1) {  // rank-1 head (critic value): wave-per-row dot products
+        hipLaunchKernelGGL(mlp::head1_fwd_any(O.in), dim3(ceil_div(n, 4)), dim3(256), 0, s, in, P + O.w, P + O.b, n, O.in, out);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        return;
+    }
+    gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, P + O.w, O.in, out, O.out, P + O.b, n, O.out, O.in, 1, s);
 }
 
 // backward from dout [n, out] into the grad buffer (accumulating)
-void backward(rlgpu_ppo* h, int mi, const float* X, const int32_t* idx, int64_t start, int n, const float* dout, hipStream_t s) {
+void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hipStream_t s) {
     Model& m = h->M[mi];
     const float* P = h->params;
     float* G = h->grads;
     int nh = (int)m.L.size() - 1;
     const Layer& O = m.L[nh];
-    weight_grad(h, dout, O.out, m.act[nh - 1], O.in, nullptr, 0, O.in, n, G + O.w, s);
-    colsum_into(h, dout, n, O.out, G + O.b, s);
-    // dA = dout . W_out
-    gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, nullptr, 0, P + O.w, O.in, nullptr, 0, h->dA, O.in, nullptr, n, O.in, O.out, 1,
-             s);
+    if (O.out == 1) {  // rank-1 head: dA = dv w^T, dw / db partials in one pass
+        int nb = (int)ceil_div(n, mlp::LNB_ROWS);
+        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, m.act[nh - 1], P + O.w, dout, n, O.in, h->dA,
+                           h->cpart);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        reduce_partials(h, h->cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
+    } else {
+        weight_grad(h, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s);
+        colsum_into(h, dout, n, O.out, G + O.b, s);
+        // dA = dout . W_out
+        gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, h->dA, O.in, nullptr, n, O.in, O.out, 1, s);
+    }
     for (int l = nh - 1; l >= 0; l--) {
         const Layer& L = m.L[l];
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
@@ -166,17 +204,22 @@ void backward(rlgpu_ppo* h, int mi, const float* X, const int32_t* idx, int64_t 
         RLGPU_CHECK_HIP(hipGetLastError());
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
-        hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(ncol, 64)), dim3(1024), 0, s, h->cpart, nb, 3 * (int64_t)L.out,
-                           (int64_t)0, ncol, G + L.b);
+        reduce_partials(h, h->cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (l == 0)
-            weight_grad(h, h->dZ, L.out, X, m.in, idx, start, L.in, n, G + L.w, s);
+            weight_grad(h, h->dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true);
         else
-            weight_grad(h, h->dZ, L.out, m.act[l - 1], L.in, nullptr, 0, L.in, n, G + L.w, s);
+            weight_grad(h, h->dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s);
         if (l > 0)
-            gemm_f32(mlp::A_IK, mlp::B_KJ, h->dZ, L.out, nullptr, 0, P + L.w, L.in, nullptr, 0, h->dA, L.in, nullptr, n, L.in,
-                     L.out, 1, s);
+            gemm_f32(mlp::A_IK, mlp::B_KJ, h->dZ, L.out, P + L.w, L.in, h->dA, L.in, nullptr, n, L.in, L.out, 1, s);
     }
+}
+
+void gather_obs(rlgpu_ppo* h, const float* obs, const int32_t* idx, int64_t start, int n, hipStream_t s) {
+    int64_t e = (int64_t)n * h->x_ld;
+    hipLaunchKernelGGL(mlp::gather_rows, dim3(ceil_div(e, 256)), dim3(256), 0, s, obs, h->cfg.obs_size, idx, start, n, h->x0,
+                       h->x_ld);
+    RLGPU_CHECK_HIP(hipGetLastError());
 }
 
 // bf16 inference forward of n rows; result in h->logits_h [n, out] (bf16)
@@ -201,7 +244,9 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s) {
         g.I = n;
         g.J = L.out;
         g.K = L.in;
-        dim3 grid(ceil_div(L.out, mlp::BN), ceil_div(n, mlp::BM));
+        g.gx = (int)ceil_div(L.out, mlp::BN);
+        g.gy = (int)ceil_div(n, mlp::BM);
+        dim3 grid(g.gx * g.gy);
         if (in_f32)
             hipLaunchKernelGGL(mlp::gemm_bf16<true>, grid, dim3(256), 0, s, g);
         else
@@ -311,7 +356,9 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             h->wpart = h->alloc<float>(kMaxSplits * wmax);
             int64_t nb = ceil_div(R, std::min(mlp::LNB_ROWS, mlp::CS_ROWS));
             h->cpart = h->alloc<float>(nb * 3 * std::max(H, omax));
-            h->scratch = h->alloc<float>(1024);
+            h->scratch = h->alloc<float>(2048 + 16 * 3 * 1024);
+            h->x_ld = (cfg->obs_size + 3) / 4 * 4;
+            h->x0 = h->alloc<float>(R * h->x_ld);
             h->zh = h->alloc<uint16_t>(R * H);
             h->ah[0] = h->alloc<uint16_t>(R * H);
             h->ah[1] = h->alloc<uint16_t>(R * H);
@@ -391,7 +438,8 @@ extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision,
         if (n == 0) return;
         hipStream_t s = rlgpu::as_stream(stream);
         if (precision == 0) {
-            forward_train(h, model, d_in, nullptr, 0, n, d_out, s);
+            gather_obs(h, d_in, nullptr, 0, n, s);
+            forward_train(h, model, h->x0, n, d_out, s);
         } else {
             forward_half(h, model, d_in, n, s);
             int64_t e = (int64_t)n * h->M[model].out;
@@ -461,19 +509,20 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         hipStream_t s = rlgpu::as_stream(stream);
         float bsr = (float)n / (float)batch_size;  // PPOLearner.cpp:374
         int A = h->cfg.num_actions;
+        gather_obs(h, d_obs, d_index, start, n, s);  // one gathered, padded copy serves both models
         // policy
-        forward_train(h, 0, d_obs, d_index, start, n, h->out, s);
+        forward_train(h, 0, h->x0, n, h->out, s);
         hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, ppo::PL_ROWS)), dim3(256), 0, s, h->out, d_masks, d_actions, d_old_logp,
                            d_adv, d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
                            1.f / std::log((float)A), h->dout, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 0, d_obs, d_index, start, n, h->dout, s);
+        backward(h, 0, h->x0, n, h->dout, s);
         // critic
-        forward_train(h, 1, d_obs, d_index, start, n, h->out, s);
+        forward_train(h, 1, h->x0, n, h->out, s);
         hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, s, h->out, d_target, d_index, start, n, bsr,
                            h->dout, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 1, d_obs, d_index, start, n, h->dout, s);
+        backward(h, 1, h->x0, n, h->dout, s);
     });
 }
 
@@ -539,5 +588,17 @@ extern "C" int rlgpu_permutation(int64_t n, uint64_t seed, uint64_t counter, int
         RLGPU_CHECK_HIP(hipFreeAsync(k0, s));
         RLGPU_CHECK_HIP(hipFreeAsync(k1, s));
         RLGPU_CHECK_HIP(hipFreeAsync(v0, s));
+    });
+}
+
+extern "C" int rlgpu_gemm_f32(int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B, int64_t ldb,
+                              float* d_C, int64_t ldc, const float* d_bias, int32_t I, int32_t J, int32_t K, int32_t splits,
+                              void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(d_A && d_B && d_C, "rlgpu_gemm_f32: null argument");
+        RLGPU_REQUIRE(I > 0 && J > 0 && K > 0 && splits >= 1, "rlgpu_gemm_f32: bad sizes");
+        RLGPU_REQUIRE((a_layout == 0 && (b_layout == 0 || b_layout == 1)) || (a_layout == 1 && b_layout == 1),
+                      "rlgpu_gemm_f32: unsupported layout pair");
+        gemm_f32(a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, rlgpu::as_stream(stream));
     });
 }
