@@ -213,55 +213,71 @@ __global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
         }
 }
 
-// ---- bf16 inference GEMM: C[i,j] = bf16( sum_k A[i,k] W[j,k] + bias[j] ), A fp32 or bf16.
+// ---- bf16 inference GEMM: C[i,j] = bf16( sum_k A[i,k] W[j,k] + bias[j] ) on
+// v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  A [I][lda] and W [J][ldb] bf16, k contiguous,
+// 16-byte aligned rows, K a multiple of 8 with zero padding (the padded inference copy of the
+// weights and the converted obs), so every staging load is one uint4 of 8 bf16 per thread.
 constexpr int HBK = 32, HPAD = 8;
 
 struct HGemmArgs {
-    const void* A;          // float* (a_f32) or uint16_t* (bf16)
+    const uint16_t* A;      // [I][lda] bf16
     const uint16_t* B;      // [J][ldb] bf16
     const uint16_t* bias;   // [J] bf16 or null
     uint16_t* C;            // [I][ldc] bf16
     int64_t lda, ldb, ldc;
-    int I, J, K;
+    int I, J, K;            // K multiple of 8
     int gx, gy;             // logical tile grid; launched as 1-D (xcd_tile)
 };
 
-template <bool A_F32>
-__global__ void __launch_bounds__(256) gemm_bf16(HGemmArgs g) {
+__device__ uint4 g_zero_u4[4];
+
+// 2 uint4 per thread: rows (t + 256q) >> 2, 8-element column chunk ((t + 256q) & 3) * 8
+DEV void htile_load(uint4 (&r)[2], const uint16_t* const (&rows)[2], int k0, int K) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        int c = k0 + ((threadIdx.x + 256 * q) & 3) * 8;
+        const uint16_t* p = (rows[q] && c < K) ? rows[q] + c : reinterpret_cast<const uint16_t*>(g_zero_u4);
+        r[q] = *reinterpret_cast<const uint4*>(p);
+    }
+}
+DEV void htile_store(uint16_t (*lds)[HBK + HPAD], const uint4 (&r)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        int e = threadIdx.x + 256 * q;
+        *reinterpret_cast<uint4*>(&lds[e >> 2][(e & 3) * 8]) = r[q];
+    }
+}
+
+__global__ void __launch_bounds__(256, 2) gemm_bf16(HGemmArgs g) {
     __shared__ uint16_t As[BM][HBK + HPAD];
     __shared__ uint16_t Bs[BN][HBK + HPAD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
     const Tile tl = xcd_tile(g.gx, g.gy, 1);
     const int i0 = tl.y * BM, j0 = tl.x * BN;
+    const uint16_t* arow[2];
+    const uint16_t* brow[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        int rr = (t + 256 * q) >> 2;
+        arow[q] = i0 + rr < g.I ? g.A + (int64_t)(i0 + rr) * g.lda : nullptr;
+        brow[q] = j0 + rr < g.J ? g.B + (int64_t)(j0 + rr) * g.ldb : nullptr;
+    }
     f32x16 acc[2][2];
     for (int a = 0; a < 2; a++)
         for (int b = 0; b < 2; b++)
             for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
+    uint4 ra[2], rb[2];
+    htile_load(ra, arow, 0, g.K);
+    htile_load(rb, brow, 0, g.K);
     for (int k0 = 0; k0 < g.K; k0 += HBK) {
-        {
-            int r = t >> 1, kh = (t & 1) * 16;
-            int gi = i0 + r;
-#pragma unroll
-            for (int kk = 0; kk < 16; kk++) {
-                int k = k0 + kh + kk;
-                uint16_t v = 0;
-                if (gi < g.I && k < g.K) {
-                    if (A_F32)
-                        v = f2bf(((const float*)g.A)[(int64_t)gi * g.lda + k]);
-                    else
-                        v = ((const uint16_t*)g.A)[(int64_t)gi * g.lda + k];
-                }
-                As[r][kh + kk] = v;
-            }
-            int gj = j0 + r;
-#pragma unroll
-            for (int kk = 0; kk < 16; kk++) {
-                int k = k0 + kh + kk;
-                Bs[r][kh + kk] = (gj < g.J && k < g.K) ? g.B[(int64_t)gj * g.ldb + k] : (uint16_t)0;
-            }
-        }
+        htile_store(As, ra);
+        htile_store(Bs, rb);
         __syncthreads();
+        if (k0 + HBK < g.K) {
+            htile_load(ra, arow, k0 + HBK, g.K);
+            htile_load(rb, brow, k0 + HBK, g.K);
+        }
 #pragma unroll
         for (int ks = 0; ks < HBK / 16; ks++) {
             int kof = ks * 16 + 8 * (lane >> 5);
@@ -289,6 +305,22 @@ __global__ void __launch_bounds__(256) gemm_bf16(HGemmArgs g) {
                 if (i < g.I) g.C[(int64_t)i * g.ldc + j] = f2bf(acc[ti][tj][r] + bj);
             }
         }
+}
+
+// f32 rows [n][C] -> bf16 rows [n][ldx] (zero padded): the inference input of the first layer
+__global__ void rows_to_bf16(const float* src, int C, int n, uint16_t* X, int ldx) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)n * ldx) return;
+    int r = (int)(e / ldx), c = (int)(e % ldx);
+    X[e] = c < C ? f2bf(src[(int64_t)r * C + c]) : (uint16_t)0;
+}
+
+// fp32 Linear.weight [out][in] -> padded bf16 [out][ldp] (zeros past in)
+__global__ void weight_to_bf16(const float* w, int out, int in, uint16_t* h, int ldp) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)out * ldp) return;
+    int o = (int)(e / ldp), k = (int)(e % ldp);
+    h[e] = k < in ? f2bf(w[(int64_t)o * in + k]) : (uint16_t)0;
 }
 
 // out[e] (+)= sum_s part[s*stride + e], fixed order (deterministic split-K reduction)

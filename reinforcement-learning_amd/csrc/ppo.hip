@@ -17,7 +17,9 @@ using rlgpu::ceil_div;
 
 struct Layer {
     int in, out;
-    int64_t w, b, g, be;  // offsets into the flat buffers (g/be = -1 without LayerNorm)
+    int64_t w, b, g, be;      // offsets into the flat fp32 buffers (g/be = -1 without LayerNorm)
+    int in_pad;               // bf16 copy: weight rows padded to a multiple of 8 (16 bytes)
+    int64_t hw, hb, hg, hbe;  // offsets into the padded bf16 inference copy
 };
 
 struct Model {
@@ -36,7 +38,7 @@ constexpr int kMaxSplits = 64;
 struct rlgpu_ppo {
     rlgpu_ppo_config cfg;
     Model M[2];
-    int64_t nparams = 0;
+    int64_t nparams = 0, nhalf = 0;
     float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr;
     uint16_t* half = nullptr;
     int64_t step = 0;
@@ -46,6 +48,8 @@ struct rlgpu_ppo {
     float *scratch = nullptr;  // clip partials + coefficients
     float* x0 = nullptr;       // gathered minibatch obs, rows padded to x_ld floats
     int x_ld = 0;
+    uint16_t* xh = nullptr;    // bf16 obs for inference, rows padded to xh_ld
+    int xh_ld = 0;
     uint16_t *zh = nullptr, *ah[2] = {nullptr, nullptr}, *logits_h = nullptr;
     std::vector<void*> allocs;
 
@@ -222,44 +226,44 @@ void gather_obs(rlgpu_ppo* h, const float* obs, const int32_t* idx, int64_t star
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
-// bf16 inference forward of n rows; result in h->logits_h [n, out] (bf16)
+// bf16 inference forward of n rows; result in h->logits_h [n, out] (bf16).  Model::Forward with
+// halfPrec (Models.cpp:42-68): every module runs on the bf16 copy, activations rounded to bf16.
 void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s) {
     Model& m = h->M[mi];
     const uint16_t* P = h->half;
     int nh = (int)m.L.size() - 1;
-    const void* in = X;
-    bool in_f32 = true;
-    int64_t ld = m.in;
+    {
+        int64_t e = (int64_t)n * h->xh_ld;
+        hipLaunchKernelGGL(mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, m.in, n, h->xh, h->xh_ld);
+        RLGPU_CHECK_HIP(hipGetLastError());
+    }
+    const uint16_t* in = h->xh;
+    int64_t ld = h->xh_ld;
     int cur = 0;
     for (int l = 0; l <= nh; l++) {
         const Layer& L = m.L[l];
         mlp::HGemmArgs g;
         g.A = in;
-        g.B = P + L.w;
-        g.bias = P + L.b;
+        g.B = P + L.hw;
+        g.bias = P + L.hb;
         g.C = l < nh ? h->zh : h->logits_h;
         g.lda = ld;
-        g.ldb = L.in;
+        g.ldb = L.in_pad;
         g.ldc = L.out;
         g.I = n;
         g.J = L.out;
-        g.K = L.in;
+        g.K = L.in_pad;
         g.gx = (int)ceil_div(L.out, mlp::BN);
         g.gy = (int)ceil_div(n, mlp::BM);
-        dim3 grid(g.gx * g.gy);
-        if (in_f32)
-            hipLaunchKernelGGL(mlp::gemm_bf16<true>, grid, dim3(256), 0, s, g);
-        else
-            hipLaunchKernelGGL(mlp::gemm_bf16<false>, grid, dim3(256), 0, s, g);
+        hipLaunchKernelGGL(mlp::gemm_bf16, dim3(g.gx * g.gy), dim3(256), 0, s, g);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (l == nh) break;
-        const uint16_t* gg = L.g >= 0 ? P + L.g : nullptr;
-        const uint16_t* bb = L.be >= 0 ? P + L.be : nullptr;
+        const uint16_t* gg = L.hg >= 0 ? P + L.hg : nullptr;
+        const uint16_t* bb = L.hbe >= 0 ? P + L.hbe : nullptr;
         hipLaunchKernelGGL(mlp::ln_act_fwd_bf16_any(L.out), dim3(ceil_div(n, 4)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, h->ah[cur]);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = h->ah[cur];
-        in_f32 = false;
         ld = L.out;
         cur ^= 1;
     }
@@ -286,6 +290,19 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
             L.be = h->nparams;
             h->nparams += L.out;
         }
+        L.in_pad = (L.in + 7) / 8 * 8;
+        h->nhalf = (h->nhalf + 7) / 8 * 8;
+        L.hw = h->nhalf;
+        h->nhalf += (int64_t)L.out * L.in_pad;
+        L.hb = h->nhalf;
+        h->nhalf += L.out;
+        L.hg = L.hbe = -1;
+        if (L.g >= 0) {
+            L.hg = h->nhalf;
+            h->nhalf += L.out;
+            L.hbe = h->nhalf;
+            h->nhalf += L.out;
+        }
         if (L.out > h->hmax) h->hmax = L.out;
         if (L.in > h->hmax && l > 0) h->hmax = L.in;
         m.L.push_back(L);
@@ -302,7 +319,15 @@ void sumsq_coef(rlgpu_ppo* h, const float* x, int64_t n, float max_norm, float* 
 }
 
 void refresh_half(rlgpu_ppo* h, hipStream_t s) {
-    hipLaunchKernelGGL(ppo::to_half, dim3(ceil_div(h->nparams, 256)), dim3(256), 0, s, h->params, h->half, h->nparams);
+    for (auto& m : h->M)
+        for (auto& L : m.L) {
+            int64_t e = (int64_t)L.out * L.in_pad;
+            hipLaunchKernelGGL(mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->params + L.w, L.out, L.in,
+                               h->half + L.hw, L.in_pad);
+            int nv = L.g >= 0 ? 3 * L.out : L.out;  // bias | LN weight | LN bias, contiguous in both layouts
+            hipLaunchKernelGGL(ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, h->params + L.b, h->half + L.hb,
+                               (int64_t)nv);
+        }
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -331,7 +356,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             h->grads = h->alloc<float>(P);
             h->exp_avg = h->alloc<float>(P);
             h->exp_avg_sq = h->alloc<float>(P);
-            h->half = h->alloc<uint16_t>(P);
+            h->half = h->alloc<uint16_t>(h->nhalf + 8);
             RLGPU_CHECK_HIP(hipMemset(h->params, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->grads, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->exp_avg, 0, P * 4));
@@ -359,6 +384,8 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             h->scratch = h->alloc<float>(2048 + 16 * 3 * 1024);
             h->x_ld = (cfg->obs_size + 3) / 4 * 4;
             h->x0 = h->alloc<float>(R * h->x_ld);
+            h->xh_ld = (cfg->obs_size + 7) / 8 * 8;
+            h->xh = h->alloc<uint16_t>(R * h->xh_ld);
             h->zh = h->alloc<uint16_t>(R * H);
             h->ah[0] = h->alloc<uint16_t>(R * H);
             h->ah[1] = h->alloc<uint16_t>(R * H);
@@ -544,10 +571,11 @@ extern "C" int rlgpu_ppo_optimizer_step(rlgpu_ppo* h, float* d_metrics, void* st
             float step_size = (float)(lr / bc1);
             float bc2_sqrt = (float)std::sqrt(bc2);
             hipLaunchKernelGGL(ppo::adamw, dim3(ceil_div(m.count, 256)), dim3(256), 0, s, h->params + m.off, h->grads + m.off,
-                               h->exp_avg + m.off, h->exp_avg_sq + m.off, h->half + m.off, m.count, coef, decay_mul, c.beta1,
+                               h->exp_avg + m.off, h->exp_avg_sq + m.off, m.count, coef, decay_mul, c.beta1,
                                c.beta2, 1.f - c.beta1, 1.f - c.beta2, step_size, bc2_sqrt, c.eps);
             RLGPU_CHECK_HIP(hipGetLastError());
         }
+        refresh_half(h, s);  // Model::Forward's lazily refreshed seqHalf (Models.cpp:46-66)
     });
 }
 

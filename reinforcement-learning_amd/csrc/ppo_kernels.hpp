@@ -219,8 +219,8 @@ __global__ void clip_coef(const float* part, int nblk, float max_norm, float* co
 }
 
 // AdamW step, libtorch semantics (torch/csrc/api/src/optim/adamw.cpp): grads pre-scaled by the
-// clip coefficient; grads zeroed after use; bf16 copy refreshed.
-__global__ void adamw(float* p, float* g, float* m, float* v, uint16_t* half, int64_t n, const float* coef, float decay_mul,
+// clip coefficient; grads zeroed after use (the bf16 copy is refreshed afterwards).
+__global__ void adamw(float* p, float* g, float* m, float* v, int64_t n, const float* coef, float decay_mul,
                       float beta1, float beta2, float one_m_b1, float one_m_b2, float step_size, float bc2_sqrt, float eps) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
@@ -234,7 +234,6 @@ __global__ void adamw(float* p, float* g, float* m, float* v, uint16_t* half, in
     m[e] = mv;
     v[e] = vv;
     g[e] = 0.f;
-    half[e] = mlp::f2bf(pv);
 }
 
 __global__ void to_half(const float* p, uint16_t* h, int64_t n) {
