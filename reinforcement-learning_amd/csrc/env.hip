@@ -198,30 +198,41 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P)
     sync();
     P.mark(8);
     if (valid) {  // BoostPadGrid::CheckCollision per pad (BoostPadGrid.cpp:5-25, BoostPad.cpp:61-86)
+        // per-car eligibility and 3x3 grid-cell window, computed once (not per pad)
+        int cx0[4], cx1[4], cy0[4], cy1[4];
+        v3 cp[4];
+#pragma unroll
+        for (int ci = 0; ci < 4; ci++) {
+            const rlgpu_car& cs = A->s.cars[ci];
+            v3 cpos = ld3(cs.body.pos);
+            v3 pos_uu = cpos * kBT2UU;
+            cp[ci] = cpos;
+            bool ok = !(cs.is_demoed || cs.boost >= 100) && !(pos_uu.z > 95.f + 250.f);
+            int ix = (int)(pos_uu.x / 1024 + 4), iy = (int)(pos_uu.y / 1024 + 5);
+            cx0[ci] = ok ? (ix - 1 > 0 ? ix - 1 : 0) : 1 << 20;  // empty window when not eligible
+            cx1[ci] = ix + 1 < 7 ? ix + 1 : 7;
+            cy0[ci] = iy - 1 > 0 ? iy - 1 : 0;
+            cy1[ci] = iy + 1 < 9 ? iy + 1 : 9;
+        }
         for (int p = l; p < RLGPU_PADS; p += kTeam) {
+            const int px = C.pad_cell_x[p], py = C.pad_cell_y[p];
+            const v3 ppos = C.pad_pos_bt[p];
+            const float rad = (C.pad_big[p] ? 208.f : 144.f) * kUU2BT;
+            const uint32_t prev_locked = A->s.pads[p].prev_locked_car_id;
             int locked = -1;
-            rlgpu_pad& pd = A->s.pads[p];
+#pragma unroll
             for (int ci = 0; ci < 4; ci++) {
-                const rlgpu_car& cs = A->s.cars[ci];
-                if (cs.is_demoed || cs.boost >= 100) continue;
-                v3 cpos = ld3(cs.body.pos);
-                v3 pos_uu = cpos * kBT2UU;
-                if (pos_uu.z > 95.f + 250.f) continue;
-                int ix = (int)(pos_uu.x / 1024 + 4), iy = (int)(pos_uu.y / 1024 + 5);
-                int px = C.pad_cell_x[p], py = C.pad_cell_y[p];
-                int x0 = ix - 1 > 0 ? ix - 1 : 0, x1 = ix + 1 < 7 ? ix + 1 : 7;
-                int y0 = iy - 1 > 0 ? iy - 1 : 0, y1 = iy + 1 < 9 ? iy + 1 : 9;
-                if (px < x0 || px > x1 || py < y0 || py > y1) continue;
+                if (px < cx0[ci] || px > cx1[ci] || py < cy0[ci] || py > cy1[ci]) continue;
+                v3 cpos = cp[ci];
                 bool col = false;
-                if (pd.prev_locked_car_id == (uint32_t)(ci + 1)) {
+                if (prev_locked == (uint32_t)(ci + 1)) {
                     v3 mn, mx;
-                    body_aabb(ci + 1, cpos, ldm(cs.body.rot), mn, mx);
-                    col = (C.pad_box_max[p].x > mn.x && C.pad_box_max[p].y > mn.y && C.pad_box_max[p].z > mn.z) &&
-                          (C.pad_box_min[p].x < mx.x && C.pad_box_min[p].y < mx.y && C.pad_box_min[p].z < mx.z);
+                    body_aabb(ci + 1, cpos, ldm(A->s.cars[ci].body.rot), mn, mx);
+                    const v3 bmin = C.pad_box_min[p], bmax = C.pad_box_max[p];
+                    col = (bmax.x > mn.x && bmax.y > mn.y && bmax.z > mn.z) && (bmin.x < mx.x && bmin.y < mx.y && bmin.z < mx.z);
                 } else {
-                    float rad = (C.pad_big[p] ? 208.f : 144.f) * kUU2BT;
-                    float dx = cpos.x - C.pad_pos_bt[p].x, dy = cpos.y - C.pad_pos_bt[p].y;
-                    if (dx * dx + dy * dy < rad * rad) col = fabsf(cpos.z - C.pad_pos_bt[p].z) < (95.f * kUU2BT);
+                    float dx = cpos.x - ppos.x, dy = cpos.y - ppos.y;
+                    if (dx * dx + dy * dy < rad * rad) col = fabsf(cpos.z - ppos.z) < (95.f * kUU2BT);
                 }
                 if (col) locked = ci;
             }
