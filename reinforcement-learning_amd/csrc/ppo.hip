@@ -27,8 +27,9 @@ struct Model {
     int in, out;
     int64_t off, count;
     float lr;
-    // fp32 training workspace
+    // fp32 training workspace (per model, so the two models' passes can overlap on two streams)
     std::vector<float*> xhat, act, rstd;
+    float *y = nullptr, *dy = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr, *mid = nullptr;  // y: model output
 };
 
 constexpr int kMaxSplits = 64;
@@ -43,9 +44,9 @@ struct rlgpu_ppo {
     uint16_t* half = nullptr;
     int64_t step = 0;
     int hmax = 0;
-    // shared workspace
-    float *out = nullptr, *dout = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr;
     float *scratch = nullptr;  // clip partials + coefficients
+    hipStream_t aux = nullptr;  // second stream: the critic's minibatch pass overlaps the policy's
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     float* x0 = nullptr;       // gathered minibatch obs, rows padded to x_ld floats
     int x_ld = 0;
     uint16_t* xh = nullptr;    // bf16 obs for inference, rows padded to xh_ld
@@ -115,21 +116,21 @@ int splits_for(int rows) {
 }
 
 // dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
-void weight_grad(rlgpu_ppo* h, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
+void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
                  bool x_tail_ok = false) {
     int splits = splits_for(n);
     int chunk = (int)ceil_div(ceil_div(n, splits), mlp::BK) * mlp::BK;
     int z = (int)ceil_div(n, chunk);
-    gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, h->wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
+    gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
     int64_t e = (int64_t)out * in;
-    hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->wpart, z, e, e, gW, 1);
+    hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
 // grad[0..n) += column sums of nblk partial rows (stride apart) -- two fixed-order levels
-void reduce_partials(rlgpu_ppo* h, const float* part, int nblk, int64_t stride, int n, float* grad, hipStream_t s) {
+void reduce_partials(Model& m, const float* part, int nblk, int64_t stride, int n, float* grad, hipStream_t s) {
     const int G = nblk >= 256 ? 16 : 1;
-    float* mid = h->scratch + 2048;  // [16][<= 3 * 1024]
+    float* mid = m.mid;  // [16][<= 3 * 1024]
     if (G > 1) {
         hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(n, 64), G), dim3(1024), 0, s, part, nblk, stride, (int64_t)0, n,
                            mid, (int64_t)n, 0);
@@ -142,11 +143,11 @@ void reduce_partials(rlgpu_ppo* h, const float* part, int nblk, int64_t stride, 
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
-void colsum_into(rlgpu_ppo* h, const float* X, int n, int C, float* g, hipStream_t s) {
+void colsum_into(Model& m, const float* X, int n, int C, float* g, hipStream_t s) {
     int nb = (int)ceil_div(n, mlp::CS_ROWS);
-    hipLaunchKernelGGL(mlp::colsum_partial, dim3(nb), dim3(256), 0, s, X, n, C, h->cpart);
+    hipLaunchKernelGGL(mlp::colsum_partial, dim3(nb), dim3(256), 0, s, X, n, C, m.cpart);
     RLGPU_CHECK_HIP(hipGetLastError());
-    reduce_partials(h, h->cpart, nb, C, C, g, s);
+    reduce_partials(m, m.cpart, nb, C, C, g, s);
 }
 
 // fp32 training forward; keeps activations; writes the output layer to `out`.  X is the
@@ -188,34 +189,34 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
     const Layer& O = m.L[nh];
     if (O.out == 1) {  // rank-1 head: dA = dv w^T, dw / db partials in one pass
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
-        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, m.act[nh - 1], P + O.w, dout, n, O.in, h->dA,
-                           h->cpart);
+        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, m.act[nh - 1], P + O.w, dout, n, O.in, m.dA,
+                           m.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
-        reduce_partials(h, h->cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
+        reduce_partials(m, m.cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
     } else {
-        weight_grad(h, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s);
-        colsum_into(h, dout, n, O.out, G + O.b, s);
+        weight_grad(m, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s);
+        colsum_into(m, dout, n, O.out, G + O.b, s);
         // dA = dout . W_out
-        gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, h->dA, O.in, nullptr, n, O.in, O.out, 1, s);
+        gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s);
     }
     for (int l = nh - 1; l >= 0; l--) {
         const Layer& L = m.L[l];
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
-        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, h->dA, m.xhat[l], m.rstd[l], gg, bb, n, L.out,
-                           h->cfg.leaky_slope, h->cfg.layer_norm, h->dZ, h->cpart);
+        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, m.dA, m.xhat[l], m.rstd[l], gg, bb, n, L.out,
+                           h->cfg.leaky_slope, h->cfg.layer_norm, m.dZ, m.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
-        reduce_partials(h, h->cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
+        reduce_partials(m, m.cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (l == 0)
-            weight_grad(h, h->dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true);
+            weight_grad(m, m.dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true);
         else
-            weight_grad(h, h->dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s);
+            weight_grad(m, m.dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s);
         if (l > 0)
-            gemm_f32(mlp::A_IK, mlp::B_KJ, h->dZ, L.out, P + L.w, L.in, h->dA, L.in, nullptr, n, L.in, L.out, 1, s);
+            gemm_f32(mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, m.dA, L.in, nullptr, n, L.in, L.out, 1, s);
     }
 }
 
@@ -350,6 +351,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
         try {
             h->cfg = *cfg;
             build_model(h, h->M[0], cfg->obs_size, cfg->policy_layers, cfg->n_policy_layers, cfg->num_actions, cfg->policy_lr);
+            h->nparams = (h->nparams + 63) / 64 * 64;  // 256-byte aligned model start: float4 weight rows
             build_model(h, h->M[1], cfg->obs_size, cfg->critic_layers, cfg->n_critic_layers, 1, cfg->critic_lr);
             int64_t P = h->nparams, R = cfg->max_rows;
             h->params = h->alloc<float>(P);
@@ -371,16 +373,22 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             }
             int H = h->hmax;
             int omax = cfg->num_actions > 1 ? cfg->num_actions : 1;
-            h->out = h->alloc<float>(R * omax);
-            h->dout = h->alloc<float>(R * omax);
-            h->dA = h->alloc<float>(R * H);
-            h->dZ = h->alloc<float>(R * H);
             int64_t wmax = 0;
             for (auto& m : h->M)
                 for (auto& L : m.L) wmax = std::max<int64_t>(wmax, (int64_t)L.in * L.out);
-            h->wpart = h->alloc<float>(kMaxSplits * wmax);
             int64_t nb = ceil_div(R, std::min(mlp::LNB_ROWS, mlp::CS_ROWS));
-            h->cpart = h->alloc<float>(nb * 3 * std::max(H, omax));
+            for (auto& m : h->M) {
+                m.y = h->alloc<float>(R * omax);
+                m.dy = h->alloc<float>(R * omax);
+                m.dA = h->alloc<float>(R * H);
+                m.dZ = h->alloc<float>(R * H);
+                m.wpart = h->alloc<float>(kMaxSplits * wmax);
+                m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
+                m.mid = h->alloc<float>(16 * 3 * 1024);
+            }
+            RLGPU_CHECK_HIP(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
+            RLGPU_CHECK_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+            RLGPU_CHECK_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
             h->scratch = h->alloc<float>(2048 + 16 * 3 * 1024);
             h->x_ld = (cfg->obs_size + 3) / 4 * 4;
             h->x0 = h->alloc<float>(R * h->x_ld);
@@ -402,6 +410,10 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
 extern "C" int rlgpu_ppo_destroy(rlgpu_ppo* h) {
     return rlgpu::guarded([&] {
         if (!h) return;
+        if (h->aux) (void)hipStreamSynchronize(h->aux);
+        if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+        if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+        if (h->aux) (void)hipStreamDestroy(h->aux);
         for (void* p : h->allocs) (void)hipFree(p);
         delete h;
     });
@@ -537,19 +549,26 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         float bsr = (float)n / (float)batch_size;  // PPOLearner.cpp:374
         int A = h->cfg.num_actions;
         gather_obs(h, d_obs, d_index, start, n, s);  // one gathered, padded copy serves both models
-        // policy
-        forward_train(h, 0, h->x0, n, h->out, s);
-        hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, ppo::PL_ROWS)), dim3(256), 0, s, h->out, d_masks, d_actions, d_old_logp,
-                           d_adv, d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
-                           1.f / std::log((float)A), h->dout, d_metrics);
+        // the critic's pass runs on the auxiliary stream (disjoint parameters, gradients, workspace
+        // and metric slots), overlapping the policy's; the caller's stream waits for both
+        RLGPU_CHECK_HIP(hipEventRecord(h->ev_fork, s));
+        RLGPU_CHECK_HIP(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+        Model& pm = h->M[0];
+        Model& cm = h->M[1];
+        forward_train(h, 1, h->x0, n, cm.y, h->aux);
+        hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, h->aux, cm.y, d_target, d_index, start, n,
+                           bsr, cm.dy, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 0, h->x0, n, h->dout, s);
-        // critic
-        forward_train(h, 1, h->x0, n, h->out, s);
-        hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, s, h->out, d_target, d_index, start, n, bsr,
-                           h->dout, d_metrics);
+        backward(h, 1, h->x0, n, cm.dy, h->aux);
+        RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
+        // policy on the caller's stream
+        forward_train(h, 0, h->x0, n, pm.y, s);
+        hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, ppo::PL_ROWS)), dim3(256), 0, s, pm.y, d_masks, d_actions,
+                           d_old_logp, d_adv, d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
+                           1.f / std::log((float)A), pm.dy, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 1, h->x0, n, h->dout, s);
+        backward(h, 0, h->x0, n, pm.dy, s);
+        RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
     });
 }
 

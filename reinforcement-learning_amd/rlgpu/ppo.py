@@ -137,6 +137,12 @@ class PPO:
         off, cnt = self.model_range(model)
         return (self.grads if grads else self.params)[off:off + cnt]
 
+    def flat(self, grads=False):
+        """Concatenation of the models' parameters (or gradients) in torch parameters() order,
+        without the alignment gap between models."""
+        import torch
+        return torch.cat([self.model_slice(0, grads), self.model_slice(1, grads)])
+
     def init_params(self, seed):
         _lib.check(_lib.lib().rlgpu_ppo_init_params(self._h, seed, _lib.stream_ptr()), "init_params")
 

@@ -132,7 +132,7 @@ def test_minibatch_grads_match_torch(gpu, n, batch, slope):
     p.adv_normalizer(d["adv"])
     p.zero_grad()
     p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], None, 0, n, batch)
-    got = p.grads.cpu()
+    got = p.flat(grads=True).cpu()
     if slope == 1.0:
         assert_grads_close(got, pol, crit, rel_tol=1e-4, frac=1.0)
     else:
@@ -192,7 +192,7 @@ def test_optimizer_step_matches_torch_adamw(gpu):
         p.minibatch(*d, None, 0, 400, 400)
         p.optimizer_step()
     want = torch.cat([q.detach().reshape(-1) for m in (pol, crit) for q in m.parameters()])
-    got = p.params.cpu()
+    got = p.flat().cpu()
     # Adam divides by sqrt(v): coordinates whose gradient is ~0 get an update of O(lr) whose sign
     # follows rounding noise, so a handful may differ by a fraction of lr; all others agree tightly.
     diff = np.abs(got.numpy() - want.numpy())

@@ -23,7 +23,7 @@ d = [T(v).to(gpu) for v in (obs, masks, acts, old, adv, tgt)]
 p.adv_normalizer(d[4])
 p.zero_grad()
 p.minibatch(*d, None, 0, n, batch)
-got = p.grads.cpu()
+got = p.flat(grads=True).cpu()
 o = 0
 for name, m in (("pol", pol), ("crit", crit)):
     for pn, prm in m.named_parameters():
