@@ -151,8 +151,11 @@ DEV Tile xcd_tile(int gx, int gy, int gz) {
 
 // fp32 GEMM on v_mfma_f32_32x32x2_f32: each MFMA j of a BK step takes k = j (lanes 0-31) and
 // k = 16 + j (lanes 32-63) so that k-contiguous tiles are read as 16-byte vectors.
+#ifndef RLGPU_GEMM_OCC
+#define RLGPU_GEMM_OCC 3
+#endif
 template <int LA, int LB, bool AV, bool BV>
-__global__ void __launch_bounds__(256, 2) gemm_f32(GemmArgs g) {
+__global__ void __launch_bounds__(256, RLGPU_GEMM_OCC) gemm_f32(GemmArgs g) {
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
     constexpr int ASZ = AK ? BM * (BK + KP) : BK * (BM + MP);
     constexpr int BSZ = BKM ? BN * (BK + KP) : BK * (BN + MP);
