@@ -36,6 +36,19 @@ def env_bytes_per_step(arena_state_size, append=True):
     return b
 
 
+def pmc_traffic(kernel_ms):
+    """HBM traffic of the env kernel from the committed rocprofv3 PMC passes (profiles/*_env_pmc.json,
+    made by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE runs of this bench), as GB/s
+    over the average launch duration measured here; None when no summary is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    b = d["hbm_bytes_per_launch"]
+    return b / (kernel_ms * 1e-3) / 1e9, {"bytes_per_launch": b, "source": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(seconds=12.0, arenas=256):
     """The CPU restatement (oracle/, reference threading model: contiguous arena chunks over a
     pool) timed on this box's host cores on a bounded sample of the same env workload."""
@@ -123,6 +136,7 @@ def main():
     kern_ms = sum(x.elapsed_time(y) for x, y in L.env_events) / len(L.env_events)
     b_env = env_bytes_per_step(arena_state_size())
     achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(kern_ms)
     out = {
         "metric": "env-steps/sec (whole node) at 32768 arenas; PPO wall-clock per 1M steps",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -137,9 +151,10 @@ def main():
         "ppo_s_per_1M_agent_steps": el / agent_steps * 1e6,
         "phase_s_per_iteration": {k: v / args.steps for k, v in phase.items()},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_pmc": traffic_src,
                      "kernel": "rl::env_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": b_env,
-                     "units_per_launch": args.arenas},
+                     "units_per_launch": args.arenas,
+                     "algorithmic_bytes_per_launch": b_env * args.arenas},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()

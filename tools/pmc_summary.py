@@ -1,0 +1,34 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (run separately, as
+MI355X_MICROARCH.md prescribes) into per-launch HBM bytes for one kernel.
+
+usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel substring> <min grid threads> <out.json>
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
+coalesced streaming reads -> doubled; WRITE_SIZE is taken as is.  Both counters are in KB.
+"""
+import csv
+import json
+import sys
+
+
+def per_launch(path, kernel, min_grid):
+    rows = list(csv.DictReader(open(path)))
+    v = [float(r["Counter_Value"]) for r in rows if kernel in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid]
+    return len(v), sum(v) / max(len(v), 1)
+
+
+def main():
+    fdir, wdir, kernel, min_grid, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    nf, fetch_kb = per_launch(f"{fdir}/run_counter_collection.csv", kernel, min_grid)
+    nw, write_kb = per_launch(f"{wdir}/run_counter_collection.csv", kernel, min_grid)
+    res = {"kernel": kernel, "launches": [nf, nw], "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+           "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1; KB = 1024 B",
+           "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --output-format csv -- python3 bench.py --steps 1 "
+                      "--warmup 0 --no-cpu-baseline (two separate passes)"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
