@@ -42,20 +42,6 @@ struct StepArgs {
 
 DEV void sync() { __syncthreads(); }
 
-// Optional per-phase cycle accounting (StepArgs::prof != null): thread 0 of every workgroup adds
-// the s_memtime delta since the previous mark to prof[phase].  Used by tools/env_phase_profile.py.
-struct Prof {
-    unsigned long long* p;
-    long long t;
-    DEV void mark(int k) {
-        if (p) {
-            long long now = clock64();
-            if (threadIdx.x == 0) atomicAdd(&p[k], (unsigned long long)(now - t));
-            t = now;
-        }
-    }
-};
-
 // ------------------------------------------------------------------ one tick (Arena::Step body)
 DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P) {
     if (valid && l == 0) {
@@ -141,9 +127,9 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P)
     sync();
     P.mark(5);
     if (valid && l == 0) {
-        commit_contacts(A);
+        commit_contacts(A, &P);
         if (threadIdx.x == 0) P.mark(16);
-        solve(A);
+        solve(A, &P);
     }
     sync();
     P.mark(6);
@@ -316,7 +302,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
     }
     if (valid && l == 5) build_slot_map(A);
     sync(); P.mark(11);
-    // ---- StepFirstHalf (EnvSet.cpp:113-130)
+    // ---- StepFirstHalf (EnvSet.cpp:113-130) prelude
     if (g.ticks_first > 0) {
         if (valid && l == 0) {
             rlgpu_env_extra& e = A->s.env;
@@ -330,23 +316,30 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             e.has_prev = 1;
         }
         sync(); P.mark(11);
-        for (int t = 0; t < g.ticks_first; t++) tick(A, l, valid, g.seed, arena, P);
     }
-    // ---- StepSecondHalf (EnvSet.cpp:132-273)
-    if (g.actions) {
-        if (valid && l < 4) {
-            int a = g.actions[arena * 4 + l];
-            a = a < 0 ? 0 : (a > RLGPU_ACTIONS - 1 ? RLGPU_ACTIONS - 1 : a);
-            const float* x = C.action[a];
-            float* c = A->s.cars[l].controls;
-            for (int k = 0; k < 5; k++) c[k] = x[k];
-            c[5] = x[5] == 1 ? 1.f : 0.f;
-            c[6] = x[6] == 1 ? 1.f : 0.f;
-            c[7] = x[7] == 1 ? 1.f : 0.f;
-            for (int k = 0; k < 8; k++) A->s.env.prev_action[l][k] = x[k];
+    // ---- the ticks of both halves in ONE loop (a single inlined copy of the tick body keeps the
+    // kernel's hot code small enough for the instruction cache); StepSecondHalf's action parse
+    // (EnvSet.cpp:132-156) runs when the first half's actionDelay ticks are done
+    {
+        const int t1 = g.ticks_first, t2 = g.actions ? g.ticks_second : 0;
+        for (int t = 0;; t++) {
+            if (g.actions && t == t1) {
+                if (valid && l < 4) {
+                    int a = g.actions[arena * 4 + l];
+                    a = a < 0 ? 0 : (a > RLGPU_ACTIONS - 1 ? RLGPU_ACTIONS - 1 : a);
+                    const float* x = C.action[a];
+                    float* c = A->s.cars[l].controls;
+                    for (int k = 0; k < 5; k++) c[k] = x[k];
+                    c[5] = x[5] == 1 ? 1.f : 0.f;
+                    c[6] = x[6] == 1 ? 1.f : 0.f;
+                    c[7] = x[7] == 1 ? 1.f : 0.f;
+                    for (int k = 0; k < 8; k++) A->s.env.prev_action[l][k] = x[k];
+                }
+                sync(); P.mark(11);
+            }
+            if (t >= t1 + t2) break;
+            tick(A, l, valid, g.seed, arena, P);
         }
-        sync(); P.mark(11);
-        for (int t = 0; t < g.ticks_second; t++) tick(A, l, valid, g.seed, arena, P);
     }
     // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks
     uint8_t term = 0;

@@ -43,12 +43,23 @@ DEV float pair_cbt(int a, int b) {
 // key -> slot map (Aux::slot_of_key, rebuilt from the record at every launch): the manifold
 // of a key, if live, is the one the map points to (a live manifold only appears through
 // get_or_new_manifold, which records it), so lookups match a scan of the 16 slots.
+DEV int rank_of_key(int key) {
+    if (key < 64) return (key / 8) * 5 + key % 8;
+    int a = (key - 64) / 8, b = (key - 64) % 8;
+    int first = a == 0 ? 0 : (a == 1 ? 4 : (a == 2 ? 7 : 9));
+    return 25 + first + (b - a - 1);
+}
 DEV void build_slot_map(ArenaLDS* A) {
     for (int k = 0; k < kKeys; k++) A->a.slot_of_key[k] = -1;
+    uint64_t have = 0;
     for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
         const rlgpu_manifold& mf = A->s.manifolds[m];
-        if (mf.count > 0 && mf.key >= 0 && mf.key < kKeys && A->a.slot_of_key[mf.key] < 0) A->a.slot_of_key[mf.key] = m;
+        if (mf.count > 0 && mf.key >= 0 && mf.key < kKeys && A->a.slot_of_key[mf.key] < 0) {
+            A->a.slot_of_key[mf.key] = m;
+            have |= 1ull << rank_of_key(mf.key);
+        }
     }
+    A->a.have_ranks = have;  // superset of the ranks with a live manifold (see commit_contacts)
 }
 DEV rlgpu_manifold* find_manifold(ArenaLDS* A, int key) {
     int m = A->a.slot_of_key[key];
@@ -252,9 +263,9 @@ DEV void add_contact(ArenaLDS* A, int key, v3 normal_b, v3 point_b, float depth)
 }
 
 // btPersistentManifold::refreshContactPoints (btPersistentManifold.cpp:265-330)
-DEV void refresh(ArenaLDS* A, int key) {
+DEV bool refresh(ArenaLDS* A, int key) {
     rlgpu_manifold* m = find_manifold(A, key);
-    if (!m) return;
+    if (!m) return false;
     int a, b;
     key_bodies(key, a, b);
     float cbt = pair_cbt(a, b);
@@ -288,6 +299,7 @@ DEV void refresh(ArenaLDS* A, int key) {
             m->count--;
         }
     }
+    return m->count > 0;
 }
 
 // ------------------------------------------------------------------ narrowphase (candidates)
@@ -580,7 +592,7 @@ DEV int narrow_pair(ArenaLDS* A, int rank) {
 }
 
 // single lane: commit candidates in canonical order, with callbacks, then refresh each pair
-DEV void commit_contacts(ArenaLDS* A) {
+DEV void commit_contacts(ArenaLDS* A, Prof* P = nullptr) {
     int n = A->a.ncand;
     if (n > kMaxCand) {
         A->s.env.manifold_overflow += (uint32_t)(n - kMaxCand);
@@ -596,23 +608,51 @@ DEV void commit_contacts(ArenaLDS* A) {
         }
         A->u.cand[j + 1] = x;
     }
+    pmark(P, 17);
+    // rank masks from the narrowphase verdicts (independent LDS reads, no per-rank branching)
+    uint64_t m1 = 0, m2 = 0;
+#pragma unroll
+    for (int r = 0; r < kPairs; r++) {
+        int md = A->a.pair_mode[r];
+        m1 |= (uint64_t)(md == 1) << r;
+        m2 |= (uint64_t)(md == 2) << r;
+    }
+    const uint64_t have = A->a.have_ranks;
+    if (P && P->p && threadIdx.x == 0) {  // diagnostics: candidates / refreshed ranks / live ranks
+        atomicAdd(&P->p[24], (unsigned long long)n);
+        atomicAdd(&P->p[25], (unsigned long long)__popcll(m1 & (have | 0)));
+        atomicAdd(&P->p[27], (unsigned long long)__popcll(m1));
+    }
+    uint64_t todo = m1 | m2, live = 0;
     int ci = 0;
-    for (int rank = 0; rank < kPairs; rank++) {
-        int mode = A->a.pair_mode[rank];
-        int key = pair_key(rank);
-        if (mode == 2) {
-            rlgpu_manifold* m = find_manifold(A, key);
-            if (m) m->count = 0;
+    while (todo) {  // ascending canonical rank = Bullet's pair order
+        const int rank = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const int key = pair_key(rank);
+        const bool has = (have >> rank) & 1;
+        if ((m2 >> rank) & 1) {
+            if (has) {
+                rlgpu_manifold* m = find_manifold(A, key);
+                if (m) m->count = 0;
+            }
             continue;
         }
-        if (mode == 0) continue;
+        // no manifold and no new point: nothing to add or refresh
+        if (!has && !(ci < n && (A->u.cand[ci].order >> 6) == rank)) continue;
         while (ci < n && (A->u.cand[ci].order >> 6) == rank) {
             const Cand& c = A->u.cand[ci];
             add_contact(A, key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth);
             ci++;
         }
-        refresh(A, key);
+        if (refresh(A, key)) live |= 1ull << rank;
     }
+    // manifolds the solver must visit: narrowphase ran (bodies active) and points remain.  Live
+    // manifolds of mode-0 ranks belong to inactive bodies only, which the solver skips anyway.
+    A->a.live_ranks = live;
+    if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[26], (unsigned long long)__popcll(live));
+    // next tick's superset: refreshed ranks as found live, untouched (inactive) ranks as before.
+    // (Manifolds are only created here, so a rank outside the set has none.)
+    A->a.have_ranks = live | (have & ~(m1 | m2));
 }
 
 // ------------------------------------------------------------------ sequential impulse solver
@@ -781,7 +821,7 @@ DEV float resolve_split(Solver& S, CRow& c) {
 }
 
 // btSequentialImpulseConstraintSolver::solveGroup (single lane per arena)
-DEV void solve(ArenaLDS* A) {
+DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
     Solver& S = A->u.sv;
     unsigned in_solver = 0;  // bit i: body i takes part (bitmask: no private-memory array)
     for (int i = 0; i < 5; i++) {
@@ -813,9 +853,12 @@ DEV void solve(ArenaLDS* A) {
         f.inv_mass = 0.f;
         f.real = 0;
     }
+    pmark(P, 19);
     int nrows = 0;
-    // manifolds in ascending key order = canonical rank order (pair_key is increasing)
-    for (int rank = 0; rank < kPairs; rank++) {
+    // manifolds in ascending key order = canonical rank order (pair_key is increasing); only the
+    // ranks the commit left live (A->a.live_ranks)
+    for (uint64_t todo = A->a.live_ranks; todo; todo &= todo - 1) {
+        const int rank = __builtin_ctzll(todo);
         rlgpu_manifold* mfp = find_manifold(A, pair_key(rank));
         if (!mfp) continue;
         rlgpu_manifold& mf = *mfp;
@@ -889,6 +932,7 @@ DEV void solve(ArenaLDS* A) {
         add_friction(A, S, i, 5, tmp, rel1, rel2, nrows, tmp.friction);
         nrows++;
     }
+    pmark(P, 20);
     for (int it = 0; it < 10; it++) {
         float lsr = 0.f;
         for (int r = 0; r < nrows; r++) {
@@ -913,6 +957,7 @@ DEV void solve(ArenaLDS* A) {
             }
         }
     }
+    pmark(P, 21);
     for (int r = 0; r < nrows; r++) {
         const CRow& row = S.rows[r];
         if (row.orig >= 0) A->s.manifolds[row.orig >> 2].pts[row.orig & 3].applied = row.applied;

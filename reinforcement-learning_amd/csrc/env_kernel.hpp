@@ -115,6 +115,8 @@ struct Aux {
     int goal;
     int traj_term;
     int8_t slot_of_key[kKeys];  // manifold key -> slot (-1 none)
+    uint64_t live_ranks;        // ranks with a live manifold after the commit (solver visit list)
+    uint64_t have_ranks;        // superset of ranks owning a live manifold (skips empty refreshes)
     float all_rewards[4];
 };
 
@@ -136,5 +138,22 @@ struct alignas(16) ArenaLDS {
     Aux a;
     Scratch u;
 };
+
+// Optional per-phase cycle accounting (StepArgs::prof != null): thread 0 of every workgroup adds
+// the s_memtime delta since the previous mark to prof[phase].  Used by tools/env_phase_profile.py.
+struct Prof {
+    unsigned long long* p;
+    long long t;
+    __device__ __forceinline__ void mark(int k) {
+        if (p) {
+            long long now = clock64();
+            if (threadIdx.x == 0) atomicAdd(&p[k], (unsigned long long)(now - t));
+            t = now;
+        }
+    }
+};
+__device__ __forceinline__ void pmark(Prof* P, int k) {
+    if (P && threadIdx.x == 0) P->mark(k);
+}
 
 }  // namespace rl

@@ -12,7 +12,8 @@ from rlgpu.env import EnvSet  # noqa: E402
 
 NAMES = ["T0 sleep/demo/snapshot", "T1 wheels (16 lanes)", "T2 car logic + pads pre", "T3 gravity/predict",
          "T4 ball awake", "T5 narrowphase", "T6 commit + solve (lane 0)", "T7 integrate", "T8 car post/finish",
-         "T9 pad collide", "T10 pad post + ball finish", "prelude / halves", "builders", "obs rows", "resets", "store", "T6a commit (part of T6 above)"]
+         "T9 pad collide", "T10 pad post + ball finish", "prelude / halves", "builders", "obs rows", "resets", "store", "T6 commit loop", "T6 commit sort",
+         "(unused)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T6 solve writeback"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 dev = torch.device("cuda:0")
@@ -37,8 +38,10 @@ for i in range(steps):
     tot_ms += e0.elapsed_time(e1)
 c = prof.cpu().tolist()
 wg = (n + 3) // 4
-total = sum(c[:16])
-c[6] += c[16]  # T6 = commit + solve
+total = sum(c[:23])
 print(f"{n} arenas, {steps} steps, {tot_ms / steps:.3f} ms/step (profiled build)")
-for k in range(17):
+ticks = steps * 8
+print(f"  per tick (workgroup 0, arena 0): candidates {c[24] / ticks / wg:.2f}, mode-1 ranks {c[27] / ticks / wg:.2f}, "
+      f"refresh-needing ranks {c[25] / ticks / wg:.2f}, live ranks {c[26] / ticks / wg:.2f}")
+for k in range(23):
     print(f"  {NAMES[k]:28s} {c[k] / total * 100:6.2f} %   {c[k] / wg / steps:12.0f} cycles/WG/step")
