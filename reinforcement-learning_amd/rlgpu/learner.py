@@ -44,6 +44,30 @@ class WelfordStat:
         return math.sqrt(self.m2 / (self.n - 1))
 
 
+def batch_ranges(exp_size, batch_size, overbatching=True):
+    """ExperienceBuffer::GetAllBatchesShuffled batch boundaries (ExperienceBuffer.cpp:117-162):
+    consecutive [start, start + batch) slices of the shuffled order; with overbatching the last
+    batch absorbs a remainder that would leave less than one more full batch; without it the
+    remainder is dropped."""
+    out = []
+    if exp_size <= 0:
+        return out
+    start = 0
+    while start < exp_size:
+        end = start + batch_size
+        if end + batch_size > exp_size and overbatching:
+            end = exp_size
+        if end > exp_size:
+            break
+        if end - start <= 0:
+            break
+        out.append((start, end))
+        if end == exp_size:
+            break
+        start += batch_size
+    return out
+
+
 class LearnerConfig:
     """The subset of GGL::LearnerConfig / PPOLearnerConfig on the hot path (ExampleMain values)."""
 
@@ -56,6 +80,7 @@ class LearnerConfig:
         self.epochs = 2
         self.mini_batch_size = 50_000
         self.batch_size = None            # None = the whole iteration (ExampleMain: batchSize = tsPerItr)
+        self.overbatching = True          # PPOLearnerConfig::overbatching
         self.gamma = 0.99
         self.gae_lambda = 0.95
         self.clip_range = 0.2
@@ -161,16 +186,16 @@ class Learner:
         masks = self.masks[:self.T].reshape(-1, ACTIONS)
         acts, logp = self.actions.view(-1), self.logp.view(-1)
         adv, tgt = self.adv.view(-1), self.target.view(-1)
+        local_batch = M if cfg.batch_size is None else max(1, cfg.batch_size // self.world)
         for epoch in range(cfg.epochs):
             perm = permutation(M, cfg.seed + self.rank, self.iteration * cfg.epochs + epoch, device=self.device)
-            # batch advantage normalisation (PPOLearner.cpp:360-371), global over ranks
-            if self.world > 1:
-                ppo.adv_stats.copy_(_dist.global_mean_std(adv, self.group))
-            else:
-                ppo.adv_normalizer(adv)
-            local_batch = M if cfg.batch_size is None else min(M, cfg.batch_size // self.world)
-            for b0 in range(0, M, local_batch):
-                b1 = min(M, b0 + local_batch)
+            for b0, b1 in batch_ranges(M, local_batch, cfg.overbatching):
+                # batch advantage normalisation (PPOLearner.cpp:360-371), global over ranks
+                badv = adv if (b0, b1) == (0, M) else adv.index_select(0, perm[b0:b1].long())
+                if self.world > 1:
+                    ppo.adv_stats.copy_(_dist.global_mean_std(badv, self.group))
+                else:
+                    ppo.adv_normalizer(badv)
                 for s0 in range(b0, b1, cfg.mini_batch_size):
                     n = min(cfg.mini_batch_size, b1 - s0)
                     ppo.minibatch(obs, masks, acts, logp, adv, tgt, perm, s0, n, batch)

@@ -94,3 +94,17 @@ def test_arena_sharding_is_a_partition():
         lo, hi = arena_range(r, 4096)
         seen.extend(range(lo, hi))
     assert seen == list(range(32768))
+
+
+def test_batch_ranges_match_experience_buffer():
+    """ExperienceBuffer::GetAllBatchesShuffled (ExperienceBuffer.cpp:117-162) batch boundaries."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd"))
+    from rlgpu.learner import batch_ranges
+    assert batch_ranges(100_000, 100_000) == [(0, 100_000)]            # ExampleMain: batch = tsPerItr
+    assert batch_ranges(250, 100) == [(0, 100), (100, 250)]            # remainder folded (overbatching)
+    assert batch_ranges(250, 100, False) == [(0, 100), (100, 200)]     # remainder dropped
+    assert batch_ranges(300, 100) == [(0, 100), (100, 200), (200, 300)]
+    assert batch_ranges(50, 100) == [(0, 50)]                          # fewer than one batch
+    assert batch_ranges(50, 100, False) == []
+    assert batch_ranges(0, 100) == []
