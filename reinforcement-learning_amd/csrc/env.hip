@@ -123,7 +123,20 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P)
     sync();
     P.mark(4);
     if (valid)
-        for (int rank = l; rank < kPairs; rank += kTeam) A->a.pair_mode[rank] = narrow_pair(A, rank);
+        // work items: the 5 body-vs-mesh pairs split into kMeshChunks triangle ranges each (the heavy
+        // items, spread over distinct lanes first), then the 30 light pairs
+        for (int item = l; item < 5 * kMeshChunks + 30; item += kTeam) {
+            if (item < 5 * kMeshChunks) {
+                const int rank = (item / kMeshChunks) * 5 + 4, ch = item % kMeshChunks;
+                const int per = (RLGPU_MESH_TRIS + kMeshChunks - 1) / kMeshChunks;
+                const int mode = narrow_pair(A, rank, ch * per, ch * per + per);
+                if (ch == 0) A->a.pair_mode[rank] = mode;
+            } else {
+                int j = item - 5 * kMeshChunks;           // 0..29 -> ranks without the mesh ones
+                int rank = j < 20 ? (j / 4) * 5 + (j % 4) : 25 + (j - 20);
+                A->a.pair_mode[rank] = narrow_pair(A, rank);
+            }
+        }
     sync();
     P.mark(5);
     if (valid && l == 0) {

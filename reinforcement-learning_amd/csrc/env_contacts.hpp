@@ -451,7 +451,9 @@ DEV bool box_triangle(ArenaLDS* A, int bi, int t, float cbt, v3& nrm, v3& point_
 }
 
 // runs the narrowphase of one canonical pair rank and emits candidates; returns pair mode
-DEV int narrow_pair(ArenaLDS* A, int rank) {
+// t0 / t1: triangle sub-range for the body-vs-mesh pairs (split over lanes; candidates carry
+// rank * 64 + triangle, so the commit order does not depend on the split)
+DEV int narrow_pair(ArenaLDS* A, int rank, int t0 = 0, int t1 = 1 << 30) {
     if (rank < 25) {
         int bi = rank / 5, st = rank % 5;
         bool active = bi == 0 ? A->a.ball_awake != 0 : A->a.active[bi] != 0;
@@ -467,7 +469,7 @@ DEV int narrow_pair(ArenaLDS* A, int rank) {
             } else {
                 float r = C.ball_radius, ext = r + 0.08f, cbt = pair_cbt(0, 10);
                 v3 mn = c - v3{ext, ext, ext}, mx = c + v3{ext, ext, ext};
-                for (int t = 0; t < C.ntris; t++) {
+                for (int t = t0; t < C.ntris && t < t1; t++) {
                     if (!aabb_overlap(mn, mx, C.tri_min[t], C.tri_max[t])) continue;
                     v3 pt, nrm;
                     float depth;
@@ -486,7 +488,7 @@ DEV int narrow_pair(ArenaLDS* A, int rank) {
                 v3 mn, mx;
                 body_aabb(bi, bpos(A, bi), R, mn, mx);
                 float cbt = pair_cbt(bi, 10);
-                for (int t = 0; t < C.ntris; t++) {
+                for (int t = t0; t < C.ntris && t < t1; t++) {
                     if (!aabb_overlap(mn, mx, C.tri_min[t], C.tri_max[t])) continue;
                     v3 n, pb;
                     float d;

@@ -35,6 +35,7 @@ constexpr int kArenas = 4;          // arenas per 64-thread workgroup
 constexpr int kMaxCand = 32;        // narrowphase candidates per tick per arena
 constexpr int kMaxRows = RLGPU_MAX_SOLVER_ROWS;  // solver contact rows per arena (+ as many friction rows)
 constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic
+constexpr int kMeshChunks = 3;      // lanes per body-vs-mesh pair in the narrowphase
 constexpr int kKeys = 93;           // manifold keys 0..92 (env.h key encoding)
 constexpr float kTick = 1.f / 120.f;
 constexpr float kUU2BT = 1.f / 50.f;
