@@ -156,7 +156,13 @@ DEV int ray_cast(ArenaLDS* A, v3 from, v3 to, int self, v3& hit_point, v3& hit_n
             nrm = da > 0.f ? C.plane_n[p] : -C.plane_n[p];
         }
     }
+    // segment AABB, grown by a margin well above the edge-test tolerance below: a triangle whose
+    // (grown) AABB misses it cannot be hit, so skipping it changes no result
+    const float kRayCull = 0.1f;
+    const v3 smin = v3{fminf(from.x, to.x) - kRayCull, fminf(from.y, to.y) - kRayCull, fminf(from.z, to.z) - kRayCull};
+    const v3 smax = v3{fmaxf(from.x, to.x) + kRayCull, fmaxf(from.y, to.y) + kRayCull, fmaxf(from.z, to.z) + kRayCull};
     for (int t = 0; t < C.ntris; t++) {
+        if (!aabb_overlap(smin, smax, C.tri_min[t], C.tri_max[t])) continue;
         v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
         v3 tn = cross(v1 - v0, v2 - v0);
         float dist = dot(v0, tn);
