@@ -31,25 +31,30 @@ extern "C" {
 
 #define RLGPU_CARS 4          /* 2v2 (src/ExampleMain.cpp:200-208) */
 #define RLGPU_PADS 34         /* RLConst::BoostPads 6 big + 28 small (RLConst.h:212-214) */
-#define RLGPU_MANIFOLDS 12    /* persistent-manifold slots per arena (build limit, overflow counted) */
+#define RLGPU_MANIFOLDS 12    /* contact-manifold slots per arena per tick (build limit, overflow counted) */
 #define RLGPU_MAX_SOLVER_ROWS 14 /* contact rows per arena per tick (build limit, overflow counted) */
+#define RLGPU_MAX_MESH_OBJECTS 32 /* static collision meshes per arena (SOCCAR loads 16, HOOPS 12) */
 #define RLGPU_OBS 167         /* AdvancedObs 9+8+34+29*4 (AdvancedObs.cpp:193-270) */
 #define RLGPU_ACTIONS 90      /* DefaultAction table (DefaultAction.cpp:3-89) */
 #define RLGPU_REWARDS 13      /* ExampleMain reward list (src/ExampleMain.cpp:132-177) */
 
-/* One persistent contact point (btManifoldPoint subset, bullet units). */
+/* One contact point (btManifoldPoint subset, bullet units). */
 typedef struct {
     float localA[3], localB[3]; /* in body-A / body-B frames */
     float normalB[3];           /* normal on B, world space, pointing towards A */
     float dist;                 /* signed distance (negative = penetration) */
-    float applied;              /* m_appliedImpulse (warm start) */
+    float applied;              /* m_appliedImpulse (warm start; 0 for a fresh point) */
     float friction, restitution;
     int32_t special;            /* m_isSpecial: ball-world contact (Arena.cpp:265-273) */
 } rlgpu_contact;
 
-/* Persistent manifold for one body pair.  key: dynamic-static = body*8 + static
- * (body 0 = ball, 1..4 = cars; static 0..3 = floor/ceiling/-x wall/+x wall planes, 4 = mesh);
- * dynamic-dynamic = 64 + a*8 + b (a<b).  count == 0 marks a free slot. */
+/* Contact manifold of one body pair, rebuilt every tick: RocketSim's broadphase removes every
+ * overlapping pair at the start of each collision pass and re-adds the ones that still overlap
+ * (btRSBroadphase.cpp:392-465), which destroys the pair's algorithm and its manifold
+ * (btOverlappingPairCache.cpp:36-46, btConvexConvexAlgorithm.cpp:198-205,
+ * btConvexConcaveCollisionAlgorithm.cpp:60-64).  So manifolds never outlive a tick and are not
+ * part of the arena record; the kernels keep them in LDS scratch.  Key encoding: see
+ * env_kernel.hpp / rsim_ref.cpp (pair_key). */
 typedef struct {
     int32_t key;
     int32_t count;
@@ -113,7 +118,7 @@ typedef struct {
     int32_t penalty_blue, penalty_orange; /* LosingPenaltyReward */
     uint8_t ev_bump[RLGPU_CARS], ev_bumped[RLGPU_CARS], ev_demo[RLGPU_CARS], ev_demoed[RLGPU_CARS];
     uint32_t rng_counter;        /* Philox counter for this arena's draws */
-    uint32_t manifold_overflow;  /* contacts dropped because all slots were busy */
+    uint32_t manifold_overflow;  /* contacts dropped by a build limit (manifolds, candidates, rows) */
     int32_t episode_steps;       /* steps in the current trajectory (Learner maxEpisodeLength) */
     int32_t reserved0;
 } rlgpu_env_extra;
@@ -125,7 +130,6 @@ typedef struct {
     int32_t ball_sleeping;
     rlgpu_car cars[RLGPU_CARS];
     rlgpu_pad pads[RLGPU_PADS];
-    rlgpu_manifold manifolds[RLGPU_MANIFOLDS];
     rlgpu_env_extra env;
 } rlgpu_arena_state;
 
@@ -137,6 +141,16 @@ typedef struct {
     int32_t save_rewards;    /* keep per-reward values of player 0 (EnvSetConfig::saveRewards) */
     int32_t max_episode_steps; /* trajectory truncation (Learner.cpp:550,848): 0 = off; ExampleMain
                                   maxEpisodeDuration 300 s -> 300*120/tickSkip = 4500 */
+    /* Arena collision meshes (RocketSim::GetArenaCollisionShapes -> Arena::_SetupArenaCollisionShapes,
+     * RocketSim.cpp:100-170, Arena.cpp:1015-1058).  mesh_tris == NULL selects the built-in
+     * synthetic mesh (include/rlgpu_arena_mesh.h).  Otherwise mesh_ntris triangles of 9 floats
+     * (v0, v1, v2 in bullet units, i.e. the .cmf vertices as stored -- see rlgpu_cmf_parse),
+     * grouped by collision object in load order: object k owns the next mesh_object_ntris[k]
+     * triangles (mesh_object_ntris == NULL: one object).  Host memory, copied at create. */
+    const float* mesh_tris;
+    int32_t mesh_ntris;
+    int32_t mesh_objects;
+    const int32_t* mesh_object_ntris;
 } rlgpu_envset_config;
 
 /* Experience-append destinations of the fused step (Learner.cpp:823-861); any may be NULL. */

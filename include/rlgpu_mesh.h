@@ -1,0 +1,44 @@
+/*
+ * rlgpu_mesh.h -- arena collision-mesh ingestion (host side, no GPU needed).
+ *
+ * Replaces:
+ *   RocketSim::CollisionMeshFile::ReadFromStream   RocketSim/src/CollisionMeshFile/CollisionMeshFile.cpp:11-57
+ *   RocketSim::CollisionMeshFile::UpdateHash       CollisionMeshFile.cpp:70-95
+ *   CollisionMeshFile::MakeBulletMesh              CollisionMeshFile.cpp:59-68 (vertices as stored,
+ *                                                  no de-duplication, no scaling: bullet units)
+ *   MeshHashSet (known SOCCAR / HOOPS hashes)      RocketSim/src/RocketSim.cpp:12-44
+ *
+ * The parsed triangles go to rlgpu_envset_config.mesh_tris (rlgpu_env.h), one collision object per
+ * file, where the env builds its device-side triangle table and uniform-grid index.
+ */
+#ifndef RLGPU_MESH_H
+#define RLGPU_MESH_H
+
+#include <stdint.h>
+#include "rlgpu_core.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RLGPU_GAMEMODE_SOCCAR 0   /* GameMode::SOCCAR (Sim/GameMode.h:6-16) */
+#define RLGPU_GAMEMODE_HOOPS 1    /* GameMode::HOOPS */
+#define RLGPU_CMF_MAX_COUNT 1000000 /* MAX_VERT_OR_TRI_COUNT (CollisionMeshFile.cpp:15) */
+
+/* Parse one .cmf image: int32 numTris, int32 numVertices, numTris x int32[3] vertex indices,
+ * numVertices x float[3] (little endian).  Errors as the reference: a count <= 0 or > 1e6, data
+ * shorter than the counts need ("input data overflown"), a vertex index out of range.  Trailing
+ * bytes are ignored.  Outputs (each may be NULL): *out_ntris, *out_nverts, *out_hash (UpdateHash)
+ * and, when out_tris != NULL, the triangles expanded to 9 floats each (v0, v1, v2) -- at most
+ * max_tris of them are written, call first with out_tris == NULL to size the buffer. */
+int rlgpu_cmf_parse(const void* data, int64_t size, float* out_tris, int32_t max_tris, int32_t* out_ntris,
+                    int32_t* out_nverts, uint32_t* out_hash);
+
+/* Position of `hash` in the reference's list of known meshes for the game mode, or -1 (the
+ * reference only warns about unknown or duplicate meshes, RocketSim.cpp:140-155). */
+int rlgpu_mesh_known_hash(int32_t game_mode, uint32_t hash);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

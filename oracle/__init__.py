@@ -78,7 +78,10 @@ def arena_state_size():
 class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
-    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0):
+    def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0,
+                 mesh=None):
+        """mesh: (tris [N, 9] float32 bullet units, object_ntris int32 [K]) or an object with
+        .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh."""
         L = lib()
         L.oracle_env_create.restype = ctypes.c_void_p
         L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -96,6 +99,11 @@ class EnvSet:
         L.oracle_env_set_max_episode_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.oracle_env_read_traj_terms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_env_set_max_episode_steps(self.h, max_episode_steps)
+        if mesh is not None:
+            tris, objs = (mesh.tris, mesh.object_ntris) if hasattr(mesh, "tris") else mesh
+            self._mesh = (np.ascontiguousarray(tris, np.float32).reshape(-1, 9), np.ascontiguousarray(objs, np.int32))
+            L.oracle_env_set_mesh.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+            L.oracle_env_set_mesh(self.h, _p(self._mesh[0]), len(self._mesh[0]), _p(self._mesh[1]), len(self._mesh[1]))
         self.traj_terms = np.zeros(4 * num_arenas, np.int8)
         P = 4 * num_arenas
         self.obs = np.zeros((P, OBS), np.float32)

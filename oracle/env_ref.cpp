@@ -510,7 +510,7 @@ void second_half_builders(rlgpu_arena_state& s, const StepOut& out, int tick_ski
 }
 
 // StepFirstHalf body for one arena (EnvSet.cpp:115-127)
-void first_half(rlgpu_arena_state& s, uint64_t seed, int idx, int action_delay) {
+void first_half(const World& w, rlgpu_arena_state& s, uint64_t seed, int idx, int action_delay) {
     rlgpu_env_extra& e = s.env;
     for (int i = 0; i < 3; i++) e.prev_ball_vel[i] = s.ball.vel[i] * BT_TO_UU;
     for (int i = 0; i < 4; i++) {
@@ -520,10 +520,11 @@ void first_half(rlgpu_arena_state& s, uint64_t seed, int idx, int action_delay) 
         e.ev_bump[i] = e.ev_bumped[i] = e.ev_demo[i] = e.ev_demoed[i] = 0;  // ResetBeforeStep
     }
     e.has_prev = 1;
-    arena_step(s, seed, idx, action_delay);
+    arena_step(w, s, seed, idx, action_delay);
 }
 
-void second_half(rlgpu_arena_state& s, uint64_t seed, int idx, int ticks, const int32_t* acts, const StepOut& out) {
+void second_half(const World& w, rlgpu_arena_state& s, uint64_t seed, int idx, int ticks, const int32_t* acts,
+                 const StepOut& out) {
     const ActionTable& at = actions();
     for (int i = 0; i < 4; i++) {
         int a = std::min(std::max(acts[i], 0), RLGPU_ACTIONS - 1);
@@ -535,7 +536,7 @@ void second_half(rlgpu_arena_state& s, uint64_t seed, int idx, int ticks, const 
         c[7] = x[7] == 1 ? 1.f : 0.f;
         for (int k = 0; k < 8; k++) s.env.prev_action[i][k] = x[k];
     }
-    arena_step(s, seed, idx, ticks);
+    arena_step(w, s, seed, idx, ticks);
     second_half_builders(s, out, ticks);
 }
 
@@ -617,7 +618,12 @@ struct EnvSet {
     std::vector<int8_t> traj_terms;
     int max_episode_steps = 0;
     Pool* pool = nullptr;
-    ~EnvSet() { delete pool; }
+    World* own_world = nullptr;     // set by oracle_env_set_mesh
+    const World* w = &world();
+    ~EnvSet() {
+        delete pool;
+        delete own_world;
+    }
     void par(std::function<void(int)> f) {
         if (!pool) {
             for (int i = 0; i < n; i++) f(i);
@@ -684,13 +690,13 @@ void oracle_env_set_arenas(void* h, int first, int count, const rlgpu_arena_stat
 
 void oracle_env_step_first_half(void* h) {
     EnvSet* e = (EnvSet*)h;
-    e->par([&](int i) { first_half(e->arenas[i], e->seed, i, e->action_delay); });
+    e->par([&](int i) { first_half(*e->w, e->arenas[i], e->seed, i, e->action_delay); });
 }
 
 void oracle_env_step_second_half(void* h, const int32_t* actions) {
     EnvSet* e = (EnvSet*)h;
     e->par([&](int i) {
-        second_half(e->arenas[i], e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, e->out(i));
+        second_half(*e->w, e->arenas[i], e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, e->out(i));
     });
 }
 
@@ -717,9 +723,9 @@ void oracle_env_step(void* h, const int32_t* actions, int reset_terminated) {
     EnvSet* e = (EnvSet*)h;
     e->par([&](int i) {
         rlgpu_arena_state& s = e->arenas[i];
-        first_half(s, e->seed, i, e->action_delay);
+        first_half(*e->w, s, e->seed, i, e->action_delay);
         StepOut o = e->out(i);
-        second_half(s, e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, o);
+        second_half(*e->w, s, e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, o);
         if (o.traj_term[0] == 2) std::memcpy(&e->trunc_obs[(size_t)i * 4 * RLGPU_OBS], o.obs, sizeof(float) * 4 * RLGPU_OBS);
         if (reset_terminated && *o.terminal) reset_arena(s, e->seed, i, o.obs, o.masks);
     });
@@ -745,6 +751,16 @@ void oracle_env_read(void* h, float* obs, uint8_t* masks, float* rewards, uint8_
 }
 
 void oracle_env_set_max_episode_steps(void* h, int n) { ((EnvSet*)h)->max_episode_steps = n; }
+
+// Arena collision meshes for this set (rlgpu_envset_config.mesh_*): ntris x 9 floats (bullet
+// units), object k owns the next obj_ntris[k] triangles (obj_ntris NULL: one object).
+void oracle_env_set_mesh(void* h, const float* tris, int ntris, const int* obj_ntris, int nobj) {
+    EnvSet* e = (EnvSet*)h;
+    delete e->own_world;
+    e->own_world = new World();
+    e->own_world->set_mesh(tris, ntris, obj_ntris, nobj);
+    e->w = e->own_world;
+}
 
 void oracle_env_read_traj_terms(void* h, int8_t* out) {
     EnvSet* e = (EnvSet*)h;

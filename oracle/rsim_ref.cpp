@@ -18,14 +18,15 @@
 // Parity status: UNPINNED by the reference (no tests, no runnable binary -- SURVEY.md 8c);
 // pinned by known-answer tests of constants/tables/spawn poses (tests/test_env_oracle.py).
 // Documented deviations from the reference (also in DESIGN.md):
-//   * synthetic arena mesh (include/rlgpu_arena_mesh.h) instead of the absent .cmf meshes;
+//   * synthetic arena mesh (include/rlgpu_arena_mesh.h) by default; real .cmf meshes can be
+//     loaded (World::set_mesh), one collision object per file;
 //   * box-triangle and box-box contacts use SAT (1 point) instead of GJK/EPA / btBoxBoxDetector;
-//   * internal-edge normal adjustment is not applied (no shared edges with differing normals
-//     inside a quad of the synthetic mesh);
+//   * internal-edge normal adjustment (btAdjustInternalEdgeContacts) is not applied;
 //   * time-based deactivation (btRigidBody.h:531-545) is not modelled -- only the zero-velocity
 //     ball sleep of Arena.cpp:722-727;
-//   * manifolds are cleared on kickoff reset / SetState; wheels resting on another dynamic body
-//     read that body's tick-start velocity (the reference's order is unordered_set iteration order);
+//   * pairs are processed in a canonical order (per body: mesh objects, planes; then the dynamic
+//     pairs) instead of the broadphase cells' insertion order; wheels resting on another dynamic
+//     body read that body's tick-start velocity (the reference's order is unordered_set order);
 //   * transcendentals use include/rlgpu_detmath.h (shared with the kernels) instead of libm.
 #include "rsim_ref.hpp"
 
@@ -128,18 +129,11 @@ World::World() {
     plane_p[2] = V(-4096, 0, 2048 / 2) * UU_TO_BT;
     plane_n[3] = V(-1, 0, 0);
     plane_p[3] = V(4096, 0, 2048 / 2) * UU_TO_BT;
-    ntris = RLGPU_MESH_TRIS;
-    for (int t = 0; t < ntris; t++) {
-        for (int k = 0; k < 3; k++)
-            tri[t][k] = V(RLGPU_MESH_UU[t][3 * k], RLGPU_MESH_UU[t][3 * k + 1], RLGPU_MESH_UU[t][3 * k + 2]) * UU_TO_BT;
-        V mn = tri[t][0], mx = tri[t][0];
-        for (int k = 1; k < 3; k++)
-            for (int a = 0; a < 3; a++) {
-                mn[a] = std::min(mn[a], tri[t][k][a]);
-                mx[a] = std::max(mx[a], tri[t][k][a]);
-            }
-        tri_min[t] = mn;
-        tri_max[t] = mx;
+    {
+        std::vector<float> bt((size_t)RLGPU_MESH_TRIS * 9);
+        for (int t = 0; t < RLGPU_MESH_TRIS; t++)
+            for (int k = 0; k < 9; k++) bt[(size_t)t * 9 + k] = RLGPU_MESH_UU[t][k] * UU_TO_BT;
+        set_mesh(bt.data(), RLGPU_MESH_TRIS, nullptr, 1);
     }
     // spawn / respawn rotations precomputed on the host (RLConst.h:297-338, Arena.cpp:183-186)
     const float spawn_x[5] = {-2048, 2048, -256, 256, 0}, spawn_y[5] = {-2560, -2560, -3840, -3840, -4608};
@@ -176,6 +170,31 @@ World::World() {
         pad_box_max[i] = pad_pos_bt[i] + V(box_rad, box_rad, 64.f * UU_TO_BT);
         pad_cell_x[i] = (int)(pad_pos_uu[i].x / 1024 + 4);  // BoostPadGrid.cpp:30-31
         pad_cell_y[i] = (int)(pad_pos_uu[i].y / 1024 + 5);
+    }
+}
+
+void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) {
+    ntris = n;
+    nobj = obj_ntris ? nobjects : 1;
+    tri.resize((size_t)n * 3);
+    tri_min.resize(n);
+    tri_max.resize(n);
+    tri_obj.assign(n, 0);
+    for (int t = 0; t < n; t++) {
+        for (int k = 0; k < 3; k++) tri[(size_t)t * 3 + k] = V(p[t * 9 + 3 * k], p[t * 9 + 3 * k + 1], p[t * 9 + 3 * k + 2]);
+        V mn = tri[(size_t)t * 3], mx = mn;
+        for (int k = 1; k < 3; k++)
+            for (int a = 0; a < 3; a++) {
+                mn[a] = std::min(mn[a], tri[(size_t)t * 3 + k][a]);
+                mx[a] = std::max(mx[a], tri[(size_t)t * 3 + k][a]);
+            }
+        tri_min[t] = mn;
+        tri_max[t] = mx;
+    }
+    if (obj_ntris) {
+        int t = 0;
+        for (int k = 0; k < nobjects; k++)
+            for (int i = 0; i < obj_ntris[k] && t < n; i++) tri_obj[t++] = k;
     }
 }
 
@@ -356,9 +375,9 @@ struct Sim {
         }
         // mesh triangles (btTriangleRaycastCallback::processTriangle)
         for (int t = 0; t < w.ntris; t++) {
-            const V& v0 = w.tri[t][0];
-            const V& v1 = w.tri[t][1];
-            const V& v2 = w.tri[t][2];
+            const V& v0 = w.tri[(size_t)t * 3];
+            const V& v1 = w.tri[(size_t)t * 3 + 1];
+            const V& v2 = w.tri[(size_t)t * 3 + 2];
             V tn = cross(v1 - v0, v2 - v0);
             float dist = dot(v0, tn);
             float da = dot(tn, from) - dist;
@@ -1043,41 +1062,41 @@ struct Sim {
         c.vel = V();
         c.ang = V();
         c.update_inertia();
-        clear_manifolds_of(ci + 1);
     }
 
     // ------------------------------------------------------------------ manifolds
+    // Manifolds live for one tick: RocketSim's broadphase removes every overlapping pair before the
+    // collision pass and re-adds the overlapping ones (btRSBroadphase.cpp:392-465); removing a pair
+    // destroys its algorithm and manifold (btOverlappingPairCache.cpp:36-46,
+    // btConvexConvexAlgorithm.cpp:198-205, btConvexConcaveCollisionAlgorithm.cpp:60-64).  Pairs are
+    // processed in ascending key order, so a pair's manifold is the last one created.
+    //
+    // Keys: dynamic-static body*KSTAT + s, s = mesh object 0..KOBJ-1 then KOBJ + plane (meshes
+    // are created before the planes, Arena.cpp:1015-1100, and the broadphase cell keeps static
+    // proxies in creation order, btRSBroadphase.cpp:160-176); dynamic-dynamic KDYN + a*8 + b,
+    // a < b (manifold A = the lower body: the ball for ball-car pairs, which Bullet creates as
+    // (sphere, box), btSphereBoxCollisionAlgorithm.cpp:30-37).
+    static constexpr int KOBJ = RLGPU_MAX_MESH_OBJECTS, KSTAT = KOBJ + 4, KDYN = 5 * KSTAT;
+    rlgpu_manifold mf[RLGPU_MANIFOLDS];
+    int nmf = 0;
     rlgpu_manifold* find_manifold(int key) {
-        for (int m = 0; m < RLGPU_MANIFOLDS; m++)
-            if (s.manifolds[m].count > 0 && s.manifolds[m].key == key) return &s.manifolds[m];
-        return nullptr;
+        return (nmf > 0 && mf[nmf - 1].key == key) ? &mf[nmf - 1] : nullptr;
     }
     rlgpu_manifold* get_or_new_manifold(int key) {
         rlgpu_manifold* m = find_manifold(key);
         if (m) return m;
-        for (int k = 0; k < RLGPU_MANIFOLDS; k++)
-            if (s.manifolds[k].count == 0) {
-                s.manifolds[k].key = key;
-                return &s.manifolds[k];
-            }
-        return nullptr;
+        if (nmf >= RLGPU_MANIFOLDS) return nullptr;
+        mf[nmf].key = key;
+        mf[nmf].count = 0;
+        return &mf[nmf++];
     }
-    void clear_manifolds_of(int body) {
-        for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
-            rlgpu_manifold& mf = s.manifolds[m];
-            if (mf.count == 0) continue;
-            int a, bb;
-            key_bodies(mf.key, a, bb);
-            if (a == body || bb == body) mf.count = 0;
-        }
-    }
-    static void key_bodies(int key, int& a, int& bb) {  // bb: body index, or 10+static
-        if (key >= 64) {
-            a = (key - 64) / 8;
-            bb = (key - 64) % 8;
+    static void key_bodies(int key, int& a, int& bb) {  // bb: body index, or 10+static slot
+        if (key >= KDYN) {
+            a = (key - KDYN) / 8;
+            bb = (key - KDYN) % 8;
         } else {
-            a = key / 8;
-            bb = 10 + key % 8;
+            a = key / KSTAT;
+            bb = 10 + key % KSTAT;
         }
     }
     // body transform of a manifold side
@@ -1167,22 +1186,24 @@ struct Sim {
         contact_callback(a, bb, m->pts[idx]);
     }
 
+    // Arena::_BulletContactAddedCallback (Arena.cpp:218-281): bodies ordered car < ball < world
     void contact_callback(int a, int bb, rlgpu_contact& cp) {
         if (a >= 1 && a <= 4) {
             int ci = a - 1;
-            if (bb == 0) {
-                car_ball_hit(ci, cp);
-            } else if (bb >= 1 && bb <= 4) {
+            if (bb >= 1 && bb <= 4) {
                 car_car_hit(ci, bb - 1, cp);
-            } else {  // car-world (Arena.cpp:417-427)
+            } else if (bb >= 10) {  // car-world (Arena.cpp:417-427)
                 rlgpu_car& cs = car(ci);
                 cs.world_contact = 1;
                 std::memcpy(cs.world_contact_normal, cp.normalB, sizeof(float) * 3);
                 cp.friction = 0.3f;
                 cp.restitution = 0.3f;
             }
-        } else if (a == 0 && bb >= 10) {
-            cp.special = 1;  // ball-world (Arena.cpp:265-273)
+        } else if (a == 0) {
+            if (bb >= 1 && bb <= 4)
+                car_ball_hit(bb - 1, cp);  // manifold A = ball: the callback swaps to (car, ball)
+            else if (bb >= 10)
+                cp.special = 1;  // ball-world (Arena.cpp:265-273)
         }
     }
 
@@ -1196,7 +1217,7 @@ struct Sim {
         V ball_pos = ball.pos * BT_TO_UU, car_pos = c.pos * BT_TO_UU;
         V ball_vel = ball.vel * BT_TO_UU, car_vel = c.vel * BT_TO_UU;
         cs.ball_hit_valid = 1;
-        st3(cs.ball_hit_rel_pos, ld3(cp.localB) * BT_TO_UU);
+        st3(cs.ball_hit_rel_pos, ld3(cp.localA) * BT_TO_UU);  // ballIsBodyA (Arena.cpp:297)
         cs.ball_hit_tick = s.env.tick_count;
         st3(cs.ball_hit_ball_pos, ball_pos);
         st3(cs.ball_hit_extra_vel, V());
@@ -1329,12 +1350,13 @@ struct Sim {
         float cbt = pair_cbt(0, 10);
         if (dist < cbt) add_contact(key, n, on_plane, dist);
     }
-    void collide_sphere_mesh(int key) {
+    // triangles [t0, t1) of one mesh object, in index order (btConvexTriangleCallback)
+    void collide_sphere_mesh(int key, int t0, int t1) {
         V c = b[0].pos;
         float r = w.ball_radius;
         float ext = r + 0.08f;
         float cbt = pair_cbt(0, 10);
-        for (int t = 0; t < w.ntris; t++) {
+        for (int t = t0; t < t1; t++) {
             if (!aabb_overlap(c - V(ext, ext, ext), c + V(ext, ext, ext), w.tri_min[t], w.tri_max[t])) continue;
             V pt, nrm;
             float depth;
@@ -1346,7 +1368,7 @@ struct Sim {
     }
     // SphereTriangleDetector::collide (SphereTriangleDetector.cpp:139-240)
     bool sphere_triangle(V center, float radius, int t, float cbt, V& point, V& normal_out, float& depth) const {
-        const V* v = w.tri[t];
+        const V* v = &w.tri[(size_t)t * 3];
         float rwt = radius + cbt;
         V normal = cross(v[1] - v[0], v[2] - v[0]);
         float l2 = len2(normal);
@@ -1449,7 +1471,7 @@ struct Sim {
         const M& R = b[bi].rot;
         V c = car_box_center(bi);
         V ax[3] = {R.col(0), R.col(1), R.col(2)};
-        const V* v = w.tri[t];
+        const V* v = &w.tri[(size_t)t * 3];
         V e[3] = {v[1] - v[0], v[2] - v[1], v[0] - v[2]};
         V tn = cross(e[0], v[2] - v[0]);
         V axes[13];
@@ -1496,18 +1518,18 @@ struct Sim {
         point_b = pa - nrm * depth;
         return true;
     }
-    void collide_box_mesh(int key, int bi) {
+    void collide_box_mesh(int key, int bi, int t0, int t1) {
         V mn, mx;
         body_aabb(bi, b[bi].pos, b[bi].rot, mn, mx);
         float cbt = pair_cbt(bi, 10);
-        for (int t = 0; t < w.ntris; t++) {
+        for (int t = t0; t < t1; t++) {
             if (!aabb_overlap(mn, mx, w.tri_min[t], w.tri_max[t])) continue;
             V n, pb;
             float d;
             if (box_triangle(bi, t, cbt, n, pb, d)) add_contact(key, n, pb, d);
         }
     }
-    // btSphereBoxCollisionAlgorithm::getSphereDistance, A = car, B = ball
+    // btSphereBoxCollisionAlgorithm::getSphereDistance (box = the car), manifold A = ball, B = car
     void collide_car_ball(int key, int bi) {
         const M& R = b[bi].rot;
         V c = car_box_center(bi);
@@ -1545,10 +1567,9 @@ struct Sim {
         V point_on_box = R * (cp + normal * margin) + c;
         float pen = distance - inter;
         V nw = R * normal;  // from box towards sphere
-        // manifold A = car, B = ball: normal on B points from ball to car
-        V nB = -nw;
-        V point_b = point_on_box - nB * pen;
-        add_contact(key, nB, point_b, pen);
+        // addContactPoint(normalOnSurfaceB, pOnBox, depth) into the (sphere, box) manifold, unswapped
+        // (btSphereBoxCollisionAlgorithm.cpp:30-37,66-75, btManifoldResult.cpp:118-135)
+        add_contact(key, nw, point_on_box, pen);
     }
     // OBB vs OBB SAT (1 point), A = car a, B = car b
     void collide_car_car(int key, int ba, int bb) {
@@ -1601,37 +1622,42 @@ struct Sim {
     }
 
     void collision_detection(bool ball_awake) {
-        // dynamic-static pairs (body x {4 planes, mesh}); skipped when both sides inactive
+        nmf = 0;  // last tick's pairs (and manifolds) were removed by the broadphase
+        // dynamic-static pairs: per body, the mesh objects then the 4 planes; skipped when the body
+        // is inactive (needsCollision(inactive, static) == false)
         for (int bi = 0; bi < 5; bi++) {
             bool active = bi == 0 ? ball_awake : b[bi].active;
-            for (int st = 0; st < 5; st++) {
-                int key = bi * 8 + st;
-                if (!active) continue;  // needsCollision(inactive, static) == false
-                if (bi == 0) {
-                    if (st < 4) collide_sphere_plane(key, st);
-                    else collide_sphere_mesh(key);
-                } else {
-                    if (st < 4) collide_box_plane(key, bi, st);
-                    else collide_box_mesh(key, bi);
-                }
+            if (!active) continue;
+            for (int o = 0, t0 = 0; o < w.nobj; o++) {
+                int t1 = t0;
+                while (t1 < w.ntris && w.tri_obj[t1] == o) t1++;
+                int key = bi * KSTAT + o;
+                if (bi == 0)
+                    collide_sphere_mesh(key, t0, t1);
+                else
+                    collide_box_mesh(key, bi, t0, t1);
+                refresh(key);
+                t0 = t1;
+            }
+            for (int p = 0; p < 4; p++) {
+                int key = bi * KSTAT + KOBJ + p;
+                if (bi == 0)
+                    collide_sphere_plane(key, p);
+                else
+                    collide_box_plane(key, bi, p);
                 refresh(key);
             }
         }
         // dynamic-dynamic pairs: ball-car then car-car, only while broadphase AABBs overlap
         for (int a = 0; a < 5; a++)
             for (int c2 = a + 1; c2 < 5; c2++) {
-                int ka = a == 0 ? c2 : a, kb = a == 0 ? 0 : c2;  // ball pairs keyed (car, ball)
-                int key = 64 + std::min(ka, kb) * 8 + std::max(ka, kb);
+                int ka = a == 0 ? c2 : a, kb = a == 0 ? 0 : c2;  // the car first for ball pairs
+                int key = KDYN + a * 8 + c2;
                 bool dem = (ka >= 1 && !b[ka].active) || (kb >= 1 && !b[kb].active);
                 V m0, m1, n0, n1;
                 broad_aabb(ka, m0, m1);
                 broad_aabb(kb, n0, n1);
-                bool overlap = !dem && aabb_overlap(m0, m1, n0, n1);
-                if (!overlap) {
-                    rlgpu_manifold* m = find_manifold(key);
-                    if (m) m->count = 0;  // pair removed from the cache -> manifold destroyed
-                    continue;
-                }
+                if (dem || !aabb_overlap(m0, m1, n0, n1)) continue;
                 bool act_a = ka == 0 ? ball_awake : b[ka].active;
                 bool act_b = kb == 0 ? ball_awake : b[kb].active;
                 if (!act_a && !act_b) continue;
@@ -1810,13 +1836,10 @@ struct Sim {
             frows.push_back(f);
         };
 
-        // convert manifolds in canonical key order
-        int order[RLGPU_MANIFOLDS], nm = 0;
-        for (int m = 0; m < RLGPU_MANIFOLDS; m++)
-            if (s.manifolds[m].count > 0) order[nm++] = m;
-        std::sort(order, order + nm, [&](int x, int y) { return s.manifolds[x].key < s.manifolds[y].key; });
-        for (int oi = 0; oi < nm; oi++) {
-            rlgpu_manifold& mf = s.manifolds[order[oi]];
+        // manifolds in creation order = ascending key order (the dispatcher's manifold array)
+        for (int oi = 0; oi < nmf; oi++) {
+            rlgpu_manifold& mf = this->mf[oi];
+            if (mf.count == 0) continue;
             int a, bb;
             key_bodies(mf.key, a, bb);
             bool aact = a < 10 && in_solver[a];
@@ -2185,11 +2208,10 @@ void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index) {
         s.pads[p].cooldown = 0;
         s.pads[p].prev_locked_car_id = 0;
     }
-    for (int m = 0; m < RLGPU_MANIFOLDS; m++) s.manifolds[m].count = 0;
 }
 
-void arena_step(rlgpu_arena_state& s, uint64_t seed, int arena_index, int ticks) {
-    Sim sim(world(), s, seed, arena_index);
+void arena_step(const World& w, rlgpu_arena_state& s, uint64_t seed, int arena_index, int ticks) {
+    Sim sim(w, s, seed, arena_index);
     sim.step(ticks);
 }
 

@@ -17,8 +17,12 @@ struct World {
     V wheel_conn[4];
     float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
     V plane_n[4], plane_p[4];
-    int ntris;
-    V tri[64][3], tri_min[64], tri_max[64];
+    // arena collision meshes (Arena::_SetupArenaCollisionShapes): triangles in load order, object
+    // by object (3 vertices each, bullet units), their AABBs and owning object
+    int ntris = 0, nobj = 1;
+    std::vector<V> tri, tri_min, tri_max;
+    std::vector<int> tri_obj;
+    void set_mesh(const float* tris_bt, int n, const int* obj_ntris, int nobjects);
     float kick_x[5], kick_y[5];
     M kick_rot[2][5];
     float respawn_x[4], respawn_y[4];
@@ -54,6 +58,6 @@ void philox(uint64_t key, uint32_t c0, uint32_t c1, uint32_t out[4]);
 uint32_t rng_next(uint64_t seed, int arena, rlgpu_env_extra& env);
 void default_car(rlgpu_car& cs);
 void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index);
-void arena_step(rlgpu_arena_state& s, uint64_t seed, int arena_index, int ticks);
+void arena_step(const World& w, rlgpu_arena_state& s, uint64_t seed, int arena_index, int ticks);
 
 }  // namespace orc

@@ -2,13 +2,14 @@
 //
 // One launch = one (half) env step for every arena: LDS-resident arena records, quarter-wave
 // teams per arena (env_kernel.hpp), phases of Arena::Step separated by workgroup barriers.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
 
-#include "../../include/rlgpu_arena_mesh.h"
 #include "common.hpp"
 #include "env_builders.hpp"
+#include "mesh.hpp"
 
 namespace rl {
 
@@ -38,12 +39,13 @@ struct StepArgs {
     int max_episode_steps;
     uint64_t seed;
     unsigned long long* prof;  // [32] phase cycle counters or null
+    MeshView mesh;
 };
 
 DEV void sync() { __syncthreads(); }
 
 // ------------------------------------------------------------------ one tick (Arena::Step body)
-DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P) {
+DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P) {
     if (valid && l == 0) {
         rlgpu_arena_state& s = A->s;
         bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
@@ -75,7 +77,7 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P)
     }
     sync();
     P.mark(0);
-    if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase(A, l >> 2, l & 3);
+    if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase(A, M, l >> 2, l & 3);
     sync();
     P.mark(1);
     if (valid) {
@@ -123,18 +125,14 @@ DEV void tick(ArenaLDS* A, int l, bool valid, uint64_t seed, int arena, Prof& P)
     sync();
     P.mark(4);
     if (valid)
-        // work items: the 5 body-vs-mesh pairs split into kMeshChunks triangle ranges each (the heavy
-        // items, spread over distinct lanes first), then the 30 light pairs
+        // work items: the 5 body-vs-mesh pairs split into kMeshChunks parts each (the heavy items,
+        // spread over distinct lanes first), then the 30 light pairs
         for (int item = l; item < 5 * kMeshChunks + 30; item += kTeam) {
             if (item < 5 * kMeshChunks) {
-                const int rank = (item / kMeshChunks) * 5 + 4, ch = item % kMeshChunks;
-                const int per = (RLGPU_MESH_TRIS + kMeshChunks - 1) / kMeshChunks;
-                const int mode = narrow_pair(A, rank, ch * per, ch * per + per);
-                if (ch == 0) A->a.pair_mode[rank] = mode;
+                narrow_pair(A, M, (item / kMeshChunks) * 5, item % kMeshChunks, kMeshChunks);
             } else {
-                int j = item - 5 * kMeshChunks;           // 0..29 -> ranks without the mesh ones
-                int rank = j < 20 ? (j / 4) * 5 + (j % 4) : 25 + (j - 20);
-                A->a.pair_mode[rank] = narrow_pair(A, rank);
+                int j = item - 5 * kMeshChunks;  // 0..29 -> the plane and dynamic ranks
+                narrow_pair(A, M, j < 20 ? (j / 4) * 5 + 1 + (j % 4) : 25 + (j - 20));
             }
         }
     sync();
@@ -313,7 +311,6 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
         A->a.torque[l] = zero3();
         update_inertia(A, l);
     }
-    if (valid && l == 5) build_slot_map(A);
     sync(); P.mark(11);
     // ---- StepFirstHalf (EnvSet.cpp:113-130) prelude
     if (g.ticks_first > 0) {
@@ -351,7 +348,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
                 sync(); P.mark(11);
             }
             if (t >= t1 + t2) break;
-            tick(A, l, valid, g.seed, arena, P);
+            tick(A, g.mesh, l, valid, g.seed, arena, P);
         }
     }
     // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks
@@ -544,18 +541,6 @@ static EnvConst make_env_const() {
     k.plane_p[2] = v3{-4096, 0, 2048 / 2} * UU;
     k.plane_n[3] = v3{-1, 0, 0};
     k.plane_p[3] = v3{4096, 0, 2048 / 2} * UU;
-    k.ntris = RLGPU_MESH_TRIS;
-    for (int t = 0; t < k.ntris; t++) {
-        for (int j = 0; j < 3; j++)
-            k.tri[t][j] = v3{RLGPU_MESH_UU[t][3 * j], RLGPU_MESH_UU[t][3 * j + 1], RLGPU_MESH_UU[t][3 * j + 2]} * UU;
-        v3 mn = k.tri[t][0], mx = k.tri[t][0];
-        for (int j = 1; j < 3; j++) {
-            mn = v3{std::min(mn.x, k.tri[t][j].x), std::min(mn.y, k.tri[t][j].y), std::min(mn.z, k.tri[t][j].z)};
-            mx = v3{std::max(mx.x, k.tri[t][j].x), std::max(mx.y, k.tri[t][j].y), std::max(mx.z, k.tri[t][j].z)};
-        }
-        k.tri_min[t] = mn;
-        k.tri_max[t] = mx;
-    }
     const float sx[5] = {-2048, 2048, -256, 256, 0}, sy[5] = {-2560, -2560, -3840, -3840, -4608};
     const float syaw[5] = {(float)(M_PI_4 * 1), (float)(M_PI_4 * 3), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2)};
     for (int i = 0; i < 5; i++) {  // RLConst.h:297-303, orange mirrored (Arena.cpp:183-186)
@@ -655,6 +640,8 @@ struct rlgpu_envset {
     float *d_obs = nullptr, *d_rewards = nullptr, *d_last_rewards = nullptr, *d_trunc_obs = nullptr;
     uint8_t *d_masks = nullptr, *d_terminals = nullptr;
     unsigned long long* d_prof = nullptr;
+    void *d_tri = nullptr, *d_cell_start = nullptr, *d_cell_tris = nullptr;  // arena mesh (MeshView)
+    rl::MeshView mesh{};
 };
 
 namespace {
@@ -679,6 +666,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.seed = e->cfg.seed;
     g.max_episode_steps = e->cfg.max_episode_steps;
     g.prof = e->d_prof;
+    g.mesh = e->mesh;
     unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
     hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(64), 0, s, g);
     RLGPU_CHECK_HIP(hipGetLastError());
@@ -700,9 +688,43 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         RLGPU_REQUIRE(cfg->tick_skip > 0, "tickSkip must be > 0 (EnvSet.cpp:48)");
         RLGPU_REQUIRE(cfg->action_delay >= 0 && cfg->action_delay <= cfg->tick_skip,
                       "actionDelay must be in [0, tickSkip] (EnvSet.cpp:49)");
+        RLGPU_REQUIRE(cfg->mesh_tris == nullptr || cfg->mesh_ntris > 0, "mesh_ntris must be > 0 with mesh_tris");
         ensure_const();
+        // arena meshes (Arena::_SetupArenaCollisionShapes): triangle table + grid index in HBM
+        std::vector<float> builtin;
+        const float* tris = cfg->mesh_tris;
+        int ntris = cfg->mesh_ntris;
+        if (!tris) {
+            builtin = rlgpu::builtin_mesh_bt();
+            tris = builtin.data();
+            ntris = (int)(builtin.size() / 9);
+        }
+        rlgpu::MeshGrid grid = rlgpu::build_mesh_grid(tris, ntris, cfg->mesh_tris ? cfg->mesh_object_ntris : nullptr,
+                                                      cfg->mesh_tris ? cfg->mesh_objects : 1);
         auto* e = new rlgpu_envset();
         e->cfg = *cfg;
+        e->cfg.mesh_tris = nullptr;  // host pointers are not kept
+        e->cfg.mesh_object_ntris = nullptr;
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_tri, grid.tri.size() * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_start, grid.cell_start.size() * sizeof(int)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_tris, std::max<size_t>(grid.cell_tris.size(), 1) * sizeof(int)));
+        RLGPU_CHECK_HIP(hipMemcpy(e->d_tri, grid.tri.data(), grid.tri.size() * sizeof(float), hipMemcpyHostToDevice));
+        RLGPU_CHECK_HIP(hipMemcpy(e->d_cell_start, grid.cell_start.data(), grid.cell_start.size() * sizeof(int),
+                                  hipMemcpyHostToDevice));
+        if (!grid.cell_tris.empty())
+            RLGPU_CHECK_HIP(hipMemcpy(e->d_cell_tris, grid.cell_tris.data(), grid.cell_tris.size() * sizeof(int),
+                                      hipMemcpyHostToDevice));
+        e->mesh.tri = (const float4*)e->d_tri;
+        e->mesh.cell_start = (const int*)e->d_cell_start;
+        e->mesh.cell_tris = (const int*)e->d_cell_tris;
+        e->mesh.ox = grid.ox;
+        e->mesh.oy = grid.oy;
+        e->mesh.oz = grid.oz;
+        e->mesh.inv_cell = grid.inv_cell;
+        e->mesh.nx = grid.nx;
+        e->mesh.ny = grid.ny;
+        e->mesh.nz = grid.nz;
+        e->mesh.ntris = grid.ntris;
         int n = cfg->num_arenas;
         e->num_players = 4 * n;
         size_t P = (size_t)e->num_players;
@@ -761,6 +783,9 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_last_rewards);
         (void)hipFree(e->d_masks);
         (void)hipFree(e->d_terminals);
+        (void)hipFree(e->d_tri);
+        (void)hipFree(e->d_cell_start);
+        (void)hipFree(e->d_cell_tris);
         delete e;
     });
 }

@@ -329,7 +329,6 @@ DEV void kickoff_reset(ArenaLDS* A, uint64_t seed, int arena) {
         A->s.pads[p].cooldown = 0;
         A->s.pads[p].prev_locked_car_id = 0;
     }
-    for (int m = 0; m < RLGPU_MANIFOLDS; m++) A->s.manifolds[m].count = 0;
     rlgpu_env_extra& e = A->s.env;
     e.last_tick_count = e.tick_count;
     e.no_touch_time = 0;

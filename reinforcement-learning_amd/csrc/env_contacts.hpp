@@ -6,22 +6,28 @@
 
 namespace rl {
 
-// canonical pair order: rank 0..24 = body*5 + static, rank 25..34 = dynamic pairs
-DEV int pair_key(int rank) {
-    if (rank < 25) return (rank / 5) * 8 + (rank % 5);
-    int r = rank - 25;  // (a,b), a < b: (0,1..4) (1,2..4) (2,3..4) (3,4)
-    int a = r < 4 ? 0 : (r < 7 ? 1 : (r < 9 ? 2 : 3));
+// Work items ("ranks") of the narrowphase, in Bullet's pair order: rank body*5 + 0 = the body vs
+// every mesh object, body*5 + 1..4 = the body vs plane 0..3; ranks 25..34 = dynamic pairs
+// (a, b), a < b: (0,1..4) (1,2..4) (2,3..4) (3,4).
+DEV void dyn_pair(int rank, int& a, int& b) {
+    int r = rank - 25;
+    a = r < 4 ? 0 : (r < 7 ? 1 : (r < 9 ? 2 : 3));
     int first = a == 0 ? 0 : (a == 1 ? 4 : (a == 2 ? 7 : 9));
-    int b = a + 1 + (r - first);
-    return 64 + a * 8 + b;
+    b = a + 1 + (r - first);
 }
+DEV int mesh_key(int body, int obj) { return body * kStat + obj; }
+DEV int plane_key(int body, int plane) { return body * kStat + kMaxObj + plane; }
+DEV int dyn_key(int a, int b) { return kDynKey + a * 8 + b; }
+// manifold body A / B of a key: a body (0 ball, 1..4 cars) or 10 + static slot.  Dynamic pairs:
+// A = the lower body, so A = ball for ball-car pairs (Bullet creates that manifold as
+// (sphere, box), btSphereBoxCollisionAlgorithm.cpp:30-37).
 DEV void key_bodies(int key, int& a, int& b) {
-    if (key >= 64) {
-        a = (key - 64) / 8;
-        b = (key - 64) % 8;
+    if (key >= kDynKey) {
+        a = (key - kDynKey) / 8;
+        b = (key - kDynKey) % 8;
     } else {
-        a = key / 8;
-        b = 10 + key % 8;
+        a = key / kStat;
+        b = 10 + key % kStat;
     }
 }
 DEV void side_transform(ArenaLDS* A, int id, v3& p, m3& r) {
@@ -40,52 +46,22 @@ DEV float pair_cbt(int a, int b) {
     return stdmin(ta, tb);
 }
 
-// key -> slot map (Aux::slot_of_key, rebuilt from the record at every launch): the manifold
-// of a key, if live, is the one the map points to (a live manifold only appears through
-// get_or_new_manifold, which records it), so lookups match a scan of the 16 slots.
-DEV int rank_of_key(int key) {
-    if (key < 64) return (key / 8) * 5 + key % 8;
-    int a = (key - 64) / 8, b = (key - 64) % 8;
-    int first = a == 0 ? 0 : (a == 1 ? 4 : (a == 2 ? 7 : 9));
-    return 25 + first + (b - a - 1);
-}
-DEV void build_slot_map(ArenaLDS* A) {
-    for (int k = 0; k < kKeys; k++) A->a.slot_of_key[k] = -1;
-    uint64_t have = 0;
-    for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
-        const rlgpu_manifold& mf = A->s.manifolds[m];
-        if (mf.count > 0 && mf.key >= 0 && mf.key < kKeys && A->a.slot_of_key[mf.key] < 0) {
-            A->a.slot_of_key[mf.key] = m;
-            have |= 1ull << rank_of_key(mf.key);
-        }
-    }
-    A->a.have_ranks = have;  // superset of the ranks with a live manifold (see commit_contacts)
-}
+// Manifolds live for one tick (rlgpu_env.h): the commit processes keys in ascending order and
+// creates each pair's manifold on its first point, so the current key's manifold, if any, is the
+// last one created.
 DEV rlgpu_manifold* find_manifold(ArenaLDS* A, int key) {
-    int m = A->a.slot_of_key[key];
-    if (m < 0) return nullptr;
-    rlgpu_manifold* mf = &A->s.manifolds[m];
-    return (mf->count > 0 && mf->key == key) ? mf : nullptr;
+    const int n = A->a.nmf;
+    return (n > 0 && A->mf[n - 1].key == key) ? &A->mf[n - 1] : nullptr;
 }
 DEV rlgpu_manifold* get_or_new_manifold(ArenaLDS* A, int key) {
     rlgpu_manifold* m = find_manifold(A, key);
     if (m) return m;
-    for (int k = 0; k < RLGPU_MANIFOLDS; k++)
-        if (A->s.manifolds[k].count == 0) {
-            A->s.manifolds[k].key = key;
-            A->a.slot_of_key[key] = (int8_t)k;
-            return &A->s.manifolds[k];
-        }
-    return nullptr;
-}
-DEV void clear_manifolds_of(ArenaLDS* A, int bodyi) {
-    for (int m = 0; m < RLGPU_MANIFOLDS; m++) {
-        rlgpu_manifold& mf = A->s.manifolds[m];
-        if (mf.count == 0) continue;
-        int a, b;
-        key_bodies(mf.key, a, b);
-        if (a == bodyi || b == bodyi) mf.count = 0;
-    }
+    const int n = A->a.nmf;
+    if (n >= RLGPU_MANIFOLDS) return nullptr;
+    A->a.nmf = n + 1;
+    A->mf[n].key = key;
+    A->mf[n].count = 0;
+    return &A->mf[n];
 }
 
 // btPersistentManifold::sortCachedPoints (btPersistentManifold.cpp:110-198)
@@ -125,7 +101,7 @@ DEV void car_ball_hit(ArenaLDS* A, int ci, rlgpu_contact& cp) {
     v3 ball_pos = bpos(A, 0) * kBT2UU, car_pos = bpos(A, bi) * kBT2UU;
     v3 ball_vel = bvel(A, 0) * kBT2UU, car_vel = bvel(A, bi) * kBT2UU;
     cs.ball_hit_valid = 1;
-    st3(cs.ball_hit_rel_pos, ld3(cp.localB) * kBT2UU);
+    st3(cs.ball_hit_rel_pos, ld3(cp.localA) * kBT2UU);  // ballIsBodyA (Arena.cpp:297)
     cs.ball_hit_tick = A->s.env.tick_count;
     st3(cs.ball_hit_ball_pos, ball_pos);
     st3(cs.ball_hit_extra_vel, zero3());
@@ -201,14 +177,13 @@ DEV void car_car_hit(ArenaLDS* A, int c1, int c2, rlgpu_contact& cp) {
     }
 }
 
+// Arena::_BulletContactAddedCallback (Arena.cpp:218-281): bodies ordered car < ball < world
 DEV void contact_callback(ArenaLDS* A, int a, int b, rlgpu_contact& cp) {
     if (a >= 1 && a <= 4) {
         int ci = a - 1;
-        if (b == 0) {
-            car_ball_hit(A, ci, cp);
-        } else if (b >= 1 && b <= 4) {
+        if (b >= 1 && b <= 4) {
             car_car_hit(A, ci, b - 1, cp);
-        } else {  // car-world (Arena.cpp:417-427)
+        } else if (b >= 10) {  // car-world (Arena.cpp:417-427)
             rlgpu_car& cs = A->s.cars[ci];
             cs.world_contact = 1;
             cs.world_contact_normal[0] = cp.normalB[0];
@@ -217,8 +192,12 @@ DEV void contact_callback(ArenaLDS* A, int a, int b, rlgpu_contact& cp) {
             cp.friction = 0.3f;
             cp.restitution = 0.3f;
         }
-    } else if (a == 0 && b >= 10) {
-        cp.special = 1;  // Arena.cpp:265-273
+    } else if (a == 0) {
+        if (b >= 1 && b <= 4) {
+            car_ball_hit(A, b - 1, cp);  // manifold A = ball: swapped into (car, ball)
+        } else if (b >= 10) {
+            cp.special = 1;  // Arena.cpp:265-273
+        }
     }
 }
 
@@ -303,14 +282,15 @@ DEV bool refresh(ArenaLDS* A, int key) {
 }
 
 // ------------------------------------------------------------------ narrowphase (candidates)
-DEV void emit(ArenaLDS* A, int rank, int tri, v3 n, v3 p, float depth) {
+DEV void emit(ArenaLDS* A, int rank, int tri, int key, v3 n, v3 p, float depth) {
     int slot = atomicAdd(&A->a.ncand, 1);
     if (slot >= kMaxCand) return;  // counted by the committing lane
     Cand& c = A->u.cand[slot];
     c.n[0] = n.x; c.n[1] = n.y; c.n[2] = n.z;
     c.p[0] = p.x; c.p[1] = p.y; c.p[2] = p.z;
     c.depth = depth;
-    c.order = rank * 64 + tri;
+    c.order = (rank << 20) | tri;
+    c.key = key;
 }
 
 // SphereTriangleDetector::pointInTriangle / closestPointTriangle / collide (SphereTriangleDetector.cpp:88-240)
@@ -353,8 +333,8 @@ DEV v3 closest_point_triangle(v3 p, v3 a, v3 b, v3 c) {
     float vv = vb * denom, ww = vc * denom;
     return a + ab * vv + ac * ww;
 }
-DEV bool sphere_triangle(v3 center, float radius, int t, float cbt, v3& point, v3& normal_out, float& depth) {
-    v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
+DEV bool sphere_triangle(v3 center, float radius, v3 v0, v3 v1, v3 v2, float cbt, v3& point, v3& normal_out,
+                         float& depth) {
     float rwt = radius + cbt;
     v3 normal = cross(v1 - v0, v2 - v0);
     float l2 = len2(normal);
@@ -405,11 +385,10 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
     return R * lv + c;
 }
 // box (car) vs triangle: SAT (stand-in for GJK/EPA)
-DEV bool box_triangle(ArenaLDS* A, int bi, int t, float cbt, v3& nrm, v3& point_b, float& depth) {
+DEV bool box_triangle(ArenaLDS* A, int bi, v3 v0, v3 v1, v3 v2, float cbt, v3& nrm, v3& point_b, float& depth) {
     m3 R = brot(A, bi);
     v3 c = car_box_center(A, bi);
     v3 ax[3] = {col(R, 0), col(R, 1), col(R, 2)};
-    v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
     v3 e[3] = {v1 - v0, v2 - v1, v0 - v2};
     float best = 1e30f;
     v3 best_n = zero3();
@@ -450,63 +429,64 @@ DEV bool box_triangle(ArenaLDS* A, int bi, int t, float cbt, v3& nrm, v3& point_
     return true;
 }
 
-// runs the narrowphase of one canonical pair rank and emits candidates; returns pair mode
-// t0 / t1: triangle sub-range for the body-vs-mesh pairs (split over lanes; candidates carry
-// rank * 64 + triangle, so the commit order does not depend on the split)
-DEV int narrow_pair(ArenaLDS* A, int rank, int t0 = 0, int t1 = 1 << 30) {
+// runs the narrowphase of one canonical pair rank and emits candidates; returns 1 when it ran.
+// Body-vs-mesh ranks are split over `parts` lanes (grid entries dealt round-robin); candidates
+// carry (rank, triangle), so the commit order does not depend on the split.
+DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int parts = 1) {
     if (rank < 25) {
-        int bi = rank / 5, st = rank % 5;
+        const int bi = rank / 5, st = rank % 5;
         bool active = bi == 0 ? A->a.ball_awake != 0 : A->a.active[bi] != 0;
         if (!active) return 0;
+        const int pl = st - 1;
         if (bi == 0) {
             v3 c = bpos(A, 0);
-            if (st < 4) {  // sphere vs plane (btConvexPlaneCollisionAlgorithm.cpp:53-90)
-                v3 n = C.plane_n[st];
+            if (st > 0) {  // sphere vs plane (btConvexPlaneCollisionAlgorithm.cpp:53-90)
+                v3 n = C.plane_n[pl];
                 v3 vtx = c + (-n) * C.ball_radius;
-                float dist = dot(n, vtx - C.plane_p[st]);
+                float dist = dot(n, vtx - C.plane_p[pl]);
                 v3 on_plane = vtx - n * dist;
-                if (dist < pair_cbt(0, 10)) emit(A, rank, 0, n, on_plane, dist);
-            } else {
+                if (dist < pair_cbt(0, 10)) emit(A, rank, 0, plane_key(0, pl), n, on_plane, dist);
+            } else {  // sphere vs mesh triangles (SphereTriangleDetector, RocketSim variant)
                 float r = C.ball_radius, ext = r + 0.08f, cbt = pair_cbt(0, 10);
                 v3 mn = c - v3{ext, ext, ext}, mx = c + v3{ext, ext, ext};
-                for (int t = t0; t < C.ntris && t < t1; t++) {
-                    if (!aabb_overlap(mn, mx, C.tri_min[t], C.tri_max[t])) continue;
+                grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) {
                     v3 pt, nrm;
                     float depth;
-                    if (sphere_triangle(c, r, t, cbt, pt, nrm, depth)) emit(A, rank, t, nrm, pt, depth);
-                }
+                    if (sphere_triangle(c, r, v0, v1, v2, cbt, pt, nrm, depth))
+                        emit(A, rank, t, mesh_key(0, obj), nrm, pt, depth);
+                });
             }
         } else {
             m3 R = brot(A, bi);
-            if (st < 4) {  // box vs plane
-                v3 n = C.plane_n[st];
+            if (st > 0) {  // box vs plane
+                v3 n = C.plane_n[pl];
                 v3 vtx = box_support(R, car_box_center(A, bi), -n);
-                float dist = dot(n, vtx - C.plane_p[st]);
+                float dist = dot(n, vtx - C.plane_p[pl]);
                 v3 on_plane = vtx - n * dist;
-                if (dist < pair_cbt(bi, 10)) emit(A, rank, 0, n, on_plane, dist);
+                if (dist < pair_cbt(bi, 10)) emit(A, rank, 0, plane_key(bi, pl), n, on_plane, dist);
             } else {
                 v3 mn, mx;
                 body_aabb(bi, bpos(A, bi), R, mn, mx);
                 float cbt = pair_cbt(bi, 10);
-                for (int t = t0; t < C.ntris && t < t1; t++) {
-                    if (!aabb_overlap(mn, mx, C.tri_min[t], C.tri_max[t])) continue;
+                grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) {
                     v3 n, pb;
                     float d;
-                    if (box_triangle(A, bi, t, cbt, n, pb, d)) emit(A, rank, t, n, pb, d);
-                }
+                    if (box_triangle(A, bi, v0, v1, v2, cbt, n, pb, d)) emit(A, rank, t, mesh_key(bi, obj), n, pb, d);
+                });
             }
         }
         return 1;
     }
-    int key = pair_key(rank);
-    int ka = (key - 64) / 8, kb = (key - 64) % 8;  // ka < kb; ball pairs keyed (ball=0, car)
-    // ball pairs are processed as A = car, B = ball
+    int ka, kb;
+    dyn_pair(rank, ka, kb);
+    const int key = dyn_key(ka, kb);
+    // ball pairs are computed with the box as the algorithm's body (A_ = car, B_ = ball)
     int A_ = ka == 0 ? kb : ka, B_ = ka == 0 ? 0 : kb;
     bool dem = (A_ >= 1 && !A->a.active[A_]) || (B_ >= 1 && !A->a.active[B_]);
     v3 m0, m1, n0, n1;
     broad_aabb(A, A_, m0, m1);
     broad_aabb(A, B_, n0, n1);
-    if (dem || !aabb_overlap(m0, m1, n0, n1)) return 2;
+    if (dem || !aabb_overlap(m0, m1, n0, n1)) return 0;
     bool act_a = A_ == 0 ? A->a.ball_awake != 0 : A->a.active[A_] != 0;
     bool act_b = B_ == 0 ? A->a.ball_awake != 0 : A->a.active[B_] != 0;
     if (!act_a && !act_b) return 0;
@@ -545,9 +525,9 @@ DEV int narrow_pair(ArenaLDS* A, int rank, int t0 = 0, int t1 = 1 << 30) {
         v3 point_on_box = R * (cp + normal * margin) + c;
         float pen = distance - inter;
         v3 nw = R * normal;
-        v3 nB = -nw;
-        v3 point_b = point_on_box - nB * pen;
-        emit(A, rank, 0, nB, point_b, pen);
+        // manifold (A = ball, B = car): normal on the car towards the ball, point on the car
+        // (btSphereBoxCollisionAlgorithm.cpp:66-75 -> btManifoldResult::addContactPoint unswapped)
+        emit(A, rank, 0, key, nw, point_on_box, pen);
         return 1;
     }
     // OBB vs OBB SAT (stand-in for btBoxBoxDetector), A = car ka, B = car kb
@@ -588,12 +568,14 @@ DEV int narrow_pair(ArenaLDS* A, int rank, int t0 = 0, int t1 = 1 << 30) {
         } else {
             point_b = box_support(Rb, cb, n);
         }
-        emit(A, rank, 0, n, point_b, depth);
+        emit(A, rank, 0, key, n, point_b, depth);
     }
     return 1;
 }
 
-// single lane: commit candidates in canonical order, with callbacks, then refresh each pair
+// single lane: commit this tick's candidates in canonical order -- per pair (key): add its points
+// (contact callbacks fire here), then refresh its manifold, as Bullet's dispatch loop does
+// (btCollisionDispatcher::dispatchAllCollisionPairs, processCollision -> refreshContactPoints)
 DEV void commit_contacts(ArenaLDS* A, Prof* P = nullptr) {
     int n = A->a.ncand;
     if (n > kMaxCand) {
@@ -611,50 +593,19 @@ DEV void commit_contacts(ArenaLDS* A, Prof* P = nullptr) {
         A->u.cand[j + 1] = x;
     }
     pmark(P, 17);
-    // rank masks from the narrowphase verdicts (independent LDS reads, no per-rank branching)
-    uint64_t m1 = 0, m2 = 0;
-#pragma unroll
-    for (int r = 0; r < kPairs; r++) {
-        int md = A->a.pair_mode[r];
-        m1 |= (uint64_t)(md == 1) << r;
-        m2 |= (uint64_t)(md == 2) << r;
-    }
-    const uint64_t have = A->a.have_ranks;
-    if (P && P->p && threadIdx.x == 0) {  // diagnostics: candidates / refreshed ranks / live ranks
-        atomicAdd(&P->p[24], (unsigned long long)n);
-        atomicAdd(&P->p[25], (unsigned long long)__popcll(m1 & (have | 0)));
-        atomicAdd(&P->p[27], (unsigned long long)__popcll(m1));
-    }
-    uint64_t todo = m1 | m2, live = 0;
-    int ci = 0;
-    while (todo) {  // ascending canonical rank = Bullet's pair order
-        const int rank = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        const int key = pair_key(rank);
-        const bool has = (have >> rank) & 1;
-        if ((m2 >> rank) & 1) {
-            if (has) {
-                rlgpu_manifold* m = find_manifold(A, key);
-                if (m) m->count = 0;
-            }
-            continue;
+    if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[24], (unsigned long long)n);
+    A->a.nmf = 0;  // the previous tick's manifolds were destroyed with their pairs
+    int cur = -1;
+    for (int ci = 0; ci < n; ci++) {
+        const Cand& c = A->u.cand[ci];
+        if (c.key != cur) {
+            if (cur >= 0) refresh(A, cur);
+            cur = c.key;
         }
-        // no manifold and no new point: nothing to add or refresh
-        if (!has && !(ci < n && (A->u.cand[ci].order >> 6) == rank)) continue;
-        while (ci < n && (A->u.cand[ci].order >> 6) == rank) {
-            const Cand& c = A->u.cand[ci];
-            add_contact(A, key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth);
-            ci++;
-        }
-        if (refresh(A, key)) live |= 1ull << rank;
+        add_contact(A, c.key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth);
     }
-    // manifolds the solver must visit: narrowphase ran (bodies active) and points remain.  Live
-    // manifolds of mode-0 ranks belong to inactive bodies only, which the solver skips anyway.
-    A->a.live_ranks = live;
-    if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[26], (unsigned long long)__popcll(live));
-    // next tick's superset: refreshed ranks as found live, untouched (inactive) ranks as before.
-    // (Manifolds are only created here, so a rank outside the set has none.)
-    A->a.have_ranks = live | (have & ~(m1 | m2));
+    if (cur >= 0) refresh(A, cur);
+    if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[26], (unsigned long long)A->a.nmf);
 }
 
 // ------------------------------------------------------------------ sequential impulse solver
@@ -857,14 +808,10 @@ DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
     }
     pmark(P, 19);
     int nrows = 0;
-    // manifolds in ascending key order = canonical rank order (pair_key is increasing); only the
-    // ranks the commit left live (A->a.live_ranks)
-    for (uint64_t todo = A->a.live_ranks; todo; todo &= todo - 1) {
-        const int rank = __builtin_ctzll(todo);
-        rlgpu_manifold* mfp = find_manifold(A, pair_key(rank));
-        if (!mfp) continue;
-        rlgpu_manifold& mf = *mfp;
-        const int best = (int)(mfp - A->s.manifolds);
+    // manifolds in creation order = ascending key order (Bullet: dispatcher manifold order)
+    for (int mi = 0; mi < A->a.nmf; mi++) {
+        rlgpu_manifold& mf = A->mf[mi];
+        if (mf.count == 0) continue;
         int a, b;
         key_bodies(mf.key, a, b);
         bool aact = a < 10 && ((in_solver >> a) & 1u);
@@ -888,7 +835,6 @@ DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
             CRow& row = S.rows[nrows];
             row.a = ia;
             row.b = ib;
-            row.orig = best * 4 + j;
             row.special = cp.special != 0;
             setup_contact(A, S, row, ia, ib, cp, rel1, rel2, cp.dist);
             if (cp.special) {
@@ -928,7 +874,6 @@ DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
         CRow& row = S.rows[nrows];
         row.a = i;
         row.b = 5;
-        row.orig = -1;
         row.special = 0;
         setup_contact(A, S, row, i, 5, tmp, rel1, rel2, distance);
         add_friction(A, S, i, 5, tmp, rel1, rel2, nrows, tmp.friction);
@@ -960,10 +905,7 @@ DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
         }
     }
     pmark(P, 21);
-    for (int r = 0; r < nrows; r++) {
-        const CRow& row = S.rows[r];
-        if (row.orig >= 0) A->s.manifolds[row.orig >> 2].pts[row.orig & 3].applied = row.applied;
-    }
+    // (the applied impulses are not written back: the manifolds die with this tick)
     for (int i = 0; i < 5; i++) {
         if (!((in_solver >> i) & 1u)) continue;
         SB& x = S.sb[i];

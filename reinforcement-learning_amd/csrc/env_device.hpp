@@ -139,8 +139,58 @@ DEV bool aabb_overlap(v3 a0, v3 a1, v3 b0, v3 b1) {
     return !(a0.x > b1.x || a1.x < b0.x || a0.y > b1.y || a1.y < b0.y || a0.z > b1.z || a1.z < b0.z);
 }
 
+// ------------------------------------------------------------------ mesh grid queries
+// cell of a coordinate along one axis: IEEE sub / mul / floor / min / max only, so host binning
+// (mesh.hip) and device queries agree exactly; NaN maps to cell 0
+DEV int grid_cell(float x, float o, float inv, int n) {
+    float f = floorf((x - o) * inv);
+    f = fminf(fmaxf(f, 0.f), (float)(n - 1));
+    return (int)f;
+}
+DEV void load_tri(const MeshView& M, int t, v3& v0, v3& v1, v3& v2, int& obj) {
+    const float4 a = M.tri[3 * t], b = M.tri[3 * t + 1], c = M.tri[3 * t + 2];
+    v0 = v3{a.x, a.y, a.z};
+    v1 = v3{b.x, b.y, b.z};
+    v2 = v3{c.x, c.y, c.z};
+    obj = __float_as_int(a.w);
+}
+// Calls f(t, v0, v1, v2, obj) once for every triangle whose AABB overlaps [qmn, qmx] (the exact
+// test of the linear scan it replaces), in no particular order.  A triangle is listed in every
+// cell its AABB touches; it is visited only from the cell max(query lo, triangle lo) per axis,
+// which lies in both cell ranges whenever the boxes overlap (grid_cell is monotone).  Entries
+// are dealt round-robin over `parts` callers.
+template <class F>
+DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& f) {
+    const int x0 = grid_cell(qmn.x, M.ox, M.inv_cell, M.nx), x1 = grid_cell(qmx.x, M.ox, M.inv_cell, M.nx);
+    const int y0 = grid_cell(qmn.y, M.oy, M.inv_cell, M.ny), y1 = grid_cell(qmx.y, M.oy, M.inv_cell, M.ny);
+    const int z0 = grid_cell(qmn.z, M.oz, M.inv_cell, M.nz), z1 = grid_cell(qmx.z, M.oz, M.inv_cell, M.nz);
+    int seen = 0;
+    for (int cz = z0; cz <= z1; cz++)
+        for (int cy = y0; cy <= y1; cy++)
+            for (int cx = x0; cx <= x1; cx++) {
+                const int cell = (cz * M.ny + cy) * M.nx + cx;
+                const int b = M.cell_start[cell], e = M.cell_start[cell + 1];
+                int k = b + ((part - seen % parts) + parts) % parts;
+                seen += e - b;
+                for (; k < e; k += parts) {
+                    const int t = M.cell_tris[k];
+                    v3 v0, v1, v2;
+                    int obj;
+                    load_tri(M, t, v0, v1, v2, obj);
+                    const v3 tmn = v3{fminf(v0.x, fminf(v1.x, v2.x)), fminf(v0.y, fminf(v1.y, v2.y)), fminf(v0.z, fminf(v1.z, v2.z))};
+                    const v3 tmx = v3{fmaxf(v0.x, fmaxf(v1.x, v2.x)), fmaxf(v0.y, fmaxf(v1.y, v2.y)), fmaxf(v0.z, fmaxf(v1.z, v2.z))};
+                    if (!aabb_overlap(qmn, qmx, tmn, tmx)) continue;
+                    if (cx != max(x0, grid_cell(tmn.x, M.ox, M.inv_cell, M.nx)) ||
+                        cy != max(y0, grid_cell(tmn.y, M.oy, M.inv_cell, M.ny)) ||
+                        cz != max(z0, grid_cell(tmn.z, M.oz, M.inv_cell, M.nz)))
+                        continue;
+                    f(t, v0, v1, v2, obj);
+                }
+            }
+}
+
 // ------------------------------------------------------------------ ray cast (btCollisionWorld::rayTest)
-DEV int ray_cast(ArenaLDS* A, v3 from, v3 to, int self, v3& hit_point, v3& hit_normal) {
+DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& hit_point, v3& hit_normal) {
     float best = 1.0f;
     int obj = -1;
     v3 nrm = zero3();
@@ -161,27 +211,29 @@ DEV int ray_cast(ArenaLDS* A, v3 from, v3 to, int self, v3& hit_point, v3& hit_n
     const float kRayCull = 0.1f;
     const v3 smin = v3{fminf(from.x, to.x) - kRayCull, fminf(from.y, to.y) - kRayCull, fminf(from.z, to.z) - kRayCull};
     const v3 smax = v3{fmaxf(from.x, to.x) + kRayCull, fmaxf(from.y, to.y) + kRayCull, fmaxf(from.z, to.z) + kRayCull};
-    for (int t = 0; t < C.ntris; t++) {
-        if (!aabb_overlap(smin, smax, C.tri_min[t], C.tri_max[t])) continue;
-        v3 v0 = C.tri[t][0], v1 = C.tri[t][1], v2 = C.tri[t][2];
+    // closest hit over the mesh = the first minimum of the reference's index-order scan: ties in
+    // f go to the lower triangle index, and a plane hit at the same f is kept (strict <)
+    int best_t = -1;
+    grid_query(M, smin, smax, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int) {
         v3 tn = cross(v1 - v0, v2 - v0);
         float dist = dot(v0, tn);
         float da = dot(tn, from) - dist;
         float db = dot(tn, to) - dist;
-        if (da * db >= 0.f) continue;
+        if (da * db >= 0.f) return;
         float f = da / (da - db);
-        if (f < best) {
+        if (f < best || (f == best && best_t >= 0 && t < best_t)) {
             float tol = len2(tn) * -0.0001f;
             v3 pt = from + d * f;
             v3 v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
             if (dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol) {
                 best = f;
+                best_t = t;
                 obj = 10;
                 v3 n = normalized(tn);
                 nrm = da <= 0.f ? -n : n;
             }
         }
-    }
+    });
     {
         v3 bp = bpos(A, 0);
         v3 oc = from - bp;
@@ -248,7 +300,7 @@ DEV int ray_cast(ArenaLDS* A, v3 from, v3 to, int self, v3& hit_point, v3& hit_n
 
 // ------------------------------------------------------------------ vehicle, one wheel per lane
 // btVehicleRL::updateWheelTransform + rayCast (btVehicleRL.cpp:64-207)
-DEV void wheel_phase(ArenaLDS* A, int ci, int i) {
+DEV void wheel_phase(ArenaLDS* A, const MeshView& M, int ci, int i) {
     rlgpu_car& cs = A->s.cars[ci];
     WheelT& W = A->u.wt[ci * 4 + i];
     int bi = ci + 1;
@@ -271,7 +323,7 @@ DEV void wheel_phase(ArenaLDS* A, int ci, int i) {
     W.contact_point = target;
     W.ground = -1;
     v3 hp, hn;
-    int obj = ray_cast(A, source, target, bi, hp, hn);
+    int obj = ray_cast(A, M, source, target, bi, hp, hn);
     v3 upv = col(R, 2);
     if (obj >= 0) {
         W.contact_point = hp;
@@ -784,8 +836,6 @@ DEV void default_car(rlgpu_car& cs) {
     cs.ball_hit_extra_tick = -1;
 }
 
-DEV void clear_manifolds_of(ArenaLDS* A, int bodyi);
-
 DEV void set_car_state(ArenaLDS* A, int ci, v3 pos_uu, const m3& rot, float boost, bool on_ground) {
     rlgpu_car& cs = A->s.cars[ci];
     default_car(cs);
@@ -797,7 +847,6 @@ DEV void set_car_state(ArenaLDS* A, int ci, v3 pos_uu, const m3& rot, float boos
     st3(b->vel, zero3());
     st3(b->angvel, zero3());
     update_inertia(A, ci + 1);
-    clear_manifolds_of(A, ci + 1);
 }
 
 }  // namespace rl

@@ -4,7 +4,8 @@
 // 64-thread workgroup (one wavefront) owns kArenas = 4 arenas; the 16 lanes of a quarter-wave
 // ("team") own one arena.  At launch the record is copied whole into LDS with coalesced
 // 16-byte loads, all ticks of the env step run against LDS, and the record is written back
-// once -- HBM traffic is ~2 x 6 KB per arena per env step plus the obs/mask/reward rows.
+// once -- HBM traffic is ~2 x 2 KB per arena per env step plus the obs/mask/reward rows and the
+// (L2-resident) arena mesh.
 //
 // Inside a tick the team runs the phases of Arena::Step
 // (GigaLearnCPP/RLGymCPP/RocketSim/src/Sim/Arena/Arena.cpp:716-812) with lane-level parallelism
@@ -12,9 +13,10 @@
 //   * 16 lanes = 4 cars x 4 wheels for the btVehicleRL wheel transforms / suspension rays /
 //     friction impulses (btVehicleRL.cpp:64-369);
 //   * 4 lanes = cars for Car::_PreTickUpdate (Car.cpp:58-131) while 12 lanes tick boost pads;
-//   * 16 lanes over the 35 canonical body pairs for the narrowphase, whose contact candidates
-//     are then committed to the persistent manifolds in canonical order by one lane (contact
-//     callbacks mutate shared state and Bullet processes pairs serially);
+//   * 16 lanes over the 35 canonical body pairs for the narrowphase (body-vs-mesh pairs split
+//     over several lanes, triangles found through the uniform-grid index of MeshView), whose
+//     contact candidates are then committed to this tick's manifolds in canonical order by one
+//     lane (contact callbacks mutate shared state and Bullet processes pairs serially);
 //   * one lane per arena for the order-dependent sequential-impulse solver
 //     (btSequentialImpulseConstraintSolver.cpp:1540-1900), rows staged in LDS;
 //   * 5 lanes = bodies for integration, 34 pads over 16 lanes for pickups.
@@ -32,11 +34,18 @@ namespace rl {
 
 constexpr int kTeam = 16;           // lanes per arena
 constexpr int kArenas = 4;          // arenas per 64-thread workgroup
-constexpr int kMaxCand = 32;        // narrowphase candidates per tick per arena
+constexpr int kMaxCand = 64;        // narrowphase candidates per tick per arena
 constexpr int kMaxRows = RLGPU_MAX_SOLVER_ROWS;  // solver contact rows per arena (+ as many friction rows)
-constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic
+constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic work items ("ranks")
 constexpr int kMeshChunks = 3;      // lanes per body-vs-mesh pair in the narrowphase
-constexpr int kKeys = 93;           // manifold keys 0..92 (env.h key encoding)
+// Manifold keys, ascending in Bullet's pair order (rsim_ref.cpp pair_key restates the same):
+//   dynamic-static  body * kStat + s, s = mesh object 0..kMaxObj-1, then kMaxObj + plane 0..3
+//                   (meshes are created before the planes, Arena.cpp:1015-1100, and a cell's static
+//                   list keeps creation order, btRSBroadphase.cpp:160-176)
+//   dynamic-dynamic kDynKey + a * 8 + b, a < b
+constexpr int kMaxObj = RLGPU_MAX_MESH_OBJECTS;
+constexpr int kStat = kMaxObj + 4;
+constexpr int kDynKey = 5 * kStat;
 constexpr float kTick = 1.f / 120.f;
 constexpr float kUU2BT = 1.f / 50.f;
 constexpr float kBT2UU = 50.f;
@@ -50,9 +59,6 @@ struct EnvConst {
     v3 wheel_conn[4];
     float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
     v3 plane_n[4], plane_p[4];
-    int ntris;
-    v3 tri[40][3];
-    v3 tri_min[40], tri_max[40];
     float kick_x[5], kick_y[5];
     m3 kick_rot[2][5];
     float respawn_x[4], respawn_y[4];
@@ -74,7 +80,22 @@ struct WheelT {
 
 struct Cand {
     float n[3], p[3], depth;
-    int order;  // pair_rank * 64 + triangle (commit order)
+    int order;  // (pair rank << 20) | triangle: commit order
+    int key;    // manifold key
+};
+
+// Arena collision mesh on the device (built by mesh.cpp from the config's triangle list): the
+// triangles in load order (3 float4: v0|object, v1, v2 -- bullet units) and a uniform grid over
+// their bounding box whose cells list, in CSR form, every triangle whose AABB (grown by kGridPad)
+// touches the cell.  Queries are conservative: the exact AABB / edge tests of the reference run
+// on every triangle the grid returns, so results equal a scan of all triangles.
+constexpr int kMaxTris = 1 << 20;   // triangle index fits the low 20 bits of Cand::order
+struct MeshView {
+    const float4* tri;       // [ntris * 3]
+    const int* cell_start;   // [ncell + 1]
+    const int* cell_tris;    // triangle indices, ascending within a cell
+    float ox, oy, oz, inv_cell;
+    int nx, ny, nz, ntris;
 };
 
 struct SB {  // btSolverBody subset
@@ -85,7 +106,7 @@ struct SB {  // btSolverBody subset
 struct CRow {  // contact row (btSolverConstraint subset)
     v3 n1, n2, rc1, rc2, angA, angB;
     float jinv, rhs, rhs_pen, applied, applied_push, friction;
-    int a, b, special, orig;  // orig = manifold slot * 4 + point, or -1
+    int a, b, special;
 };
 struct FRow {  // friction row
     v3 n1, n2, rc1, rc2, angA, angB;
@@ -109,15 +130,11 @@ struct Aux {
     m3 pred_rot[5];
     v3 snap_vel[5], snap_ang[5];
     int active[5];
-    int ball_awake, ball_sleep, ncand;
-    int pair_mode[kPairs];  // 0 skip, 1 narrowphase ran, 2 destroy manifold
+    int ball_awake, ball_sleep, ncand, nmf;
     int locked[RLGPU_PADS];
     int touched[4];
     int goal;
     int traj_term;
-    int8_t slot_of_key[kKeys];  // manifold key -> slot (-1 none)
-    uint64_t live_ranks;        // ranks with a live manifold after the commit (solver visit list)
-    uint64_t have_ranks;        // superset of ranks owning a live manifold (skips empty refreshes)
     float all_rewards[4];
 };
 
@@ -137,6 +154,7 @@ struct alignas(16) ArenaLDS {
     rlgpu_arena_state s;
     char pad_[kRec - sizeof(rlgpu_arena_state)];
     Aux a;
+    rlgpu_manifold mf[RLGPU_MANIFOLDS];  // this tick's manifolds, in creation (= key) order
     Scratch u;
 };
 

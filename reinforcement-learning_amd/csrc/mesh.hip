@@ -1,0 +1,190 @@
+// mesh.hip -- collision-mesh ingestion (include/rlgpu_mesh.h) and the host build of the env
+// kernel's mesh table + uniform-grid index (mesh.hpp).  Host code only.
+#include "mesh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../include/rlgpu_arena_mesh.h"
+#include "../../include/rlgpu_env.h"
+#include "../../include/rlgpu_mesh.h"
+#include "common.hpp"
+
+namespace rlgpu {
+
+namespace {
+
+// The reference converts each vertex component with `uint32_t curVal = float`
+// (CollisionMeshFile.cpp:79).  Out-of-range conversions are undefined in C++; x86-64 compilers
+// emit a truncating float->int64 conversion (cvttss2si) and keep the low 32 bits, which is what
+// this restates (NaN and |x| >= 2^63 give the int64 "indefinite" value, low bits 0).
+uint32_t hash_component(float x) {
+    if (!(std::fabs(x) < 9.2233720368547758e18f)) return 0u;
+    return (uint32_t)(uint64_t)(int64_t)x;
+}
+
+// CollisionMeshFile::UpdateHash (CollisionMeshFile.cpp:70-95)
+uint32_t cmf_hash(const int32_t* idx, int ntris, const float* verts, int nverts) {
+    uint32_t hash = (uint32_t)((uint64_t)nverts + (uint64_t)ntris * (uint64_t)nverts);
+    const uint32_t kMueller = 0x45D9F3B, kShift = 0x9E3779B9;
+    for (int t = 0; t < ntris; t++)
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                uint32_t v = hash_component(verts[3 * idx[3 * t + i] + j]);
+                for (int k = 0; k < 2; k++) v = ((v >> 16) ^ v) * kMueller;
+                v = (v >> 16) ^ v;
+                hash ^= v + kShift + (hash << 6) + (hash >> 2);
+            }
+    return hash;
+}
+
+const uint32_t kSoccarHashes[] = {0xA160BAF9, 0x2811EEE8, 0xB81AC8B9, 0x760358D3, 0x73AE4940, 0x918F4A4E,
+                                  0x1F8EE550, 0x255BA8C1, 0x14B84668, 0xEC759EBF, 0x94FB0D5C, 0xDEA07102,
+                                  0xBD4FBEA8, 0x39A47F63, 0x3D79D25D, 0xD84C7A68};
+const uint32_t kHoopsHashes[] = {0x72F2359E, 0x5ED14A26, 0xFD5A0D07, 0x92AFA5B5, 0x0E4133C7, 0x399E8B5F,
+                                 0xBB9D4FB5, 0x8C87FB93, 0x1CFD0E16, 0xE19E1DF6, 0x9CA179DC, 0x16F3CC19};
+
+}  // namespace
+
+std::vector<float> builtin_mesh_bt() {
+    std::vector<float> out((size_t)RLGPU_MESH_TRIS * 9);
+    const float UU = 1.f / 50.f;
+    for (int t = 0; t < RLGPU_MESH_TRIS; t++)
+        for (int k = 0; k < 9; k++) out[(size_t)t * 9 + k] = RLGPU_MESH_UU[t][k] * UU;
+    return out;
+}
+
+MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntris, int nobjects) {
+    RLGPU_REQUIRE(tris && ntris > 0, "mesh: no triangles");
+    RLGPU_REQUIRE(ntris < (1 << 20), "mesh: more than 2^20 - 1 triangles");
+    if (!object_ntris) nobjects = 1;
+    RLGPU_REQUIRE(nobjects >= 1 && nobjects <= RLGPU_MAX_MESH_OBJECTS,
+                  "mesh: object count must be in [1, RLGPU_MAX_MESH_OBJECTS]");
+    MeshGrid g;
+    g.ntris = ntris;
+    std::vector<int> obj(ntris, 0);
+    if (object_ntris) {
+        int64_t sum = 0;
+        for (int k = 0; k < nobjects; k++) {
+            RLGPU_REQUIRE(object_ntris[k] >= 0, "mesh: negative object triangle count");
+            sum += object_ntris[k];
+        }
+        RLGPU_REQUIRE(sum == ntris, "mesh: object triangle counts do not add up to mesh_ntris");
+        int t = 0;
+        for (int k = 0; k < nobjects; k++)
+            for (int i = 0; i < object_ntris[k]; i++) obj[t++] = k;
+    }
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int t = 0; t < ntris; t++)
+        for (int v = 0; v < 3; v++)
+            for (int a = 0; a < 3; a++) {
+                float x = tris[(size_t)t * 9 + v * 3 + a];
+                RLGPU_REQUIRE(std::isfinite(x), "mesh: non-finite vertex coordinate");
+                mn[a] = std::fmin(mn[a], x);
+                mx[a] = std::fmax(mx[a], x);
+            }
+    // cells of >= 256 uu (5.12 bullet units): a car or ball query touches at most 2 cells per axis
+    float ext = std::fmax(mx[0] - mn[0], std::fmax(mx[1] - mn[1], mx[2] - mn[2]));
+    float cell = std::fmax(5.12f, ext / 96.f);
+    g.inv_cell = 1.f / cell;
+    g.ox = mn[0];
+    g.oy = mn[1];
+    g.oz = mn[2];
+    int* dims[3] = {&g.nx, &g.ny, &g.nz};
+    for (int a = 0; a < 3; a++) {
+        int n = (int)std::floor((mx[a] - mn[a]) * g.inv_cell) + 1;
+        *dims[a] = n < 1 ? 1 : (n > 128 ? 128 : n);
+    }
+    const float o[3] = {g.ox, g.oy, g.oz};
+    const int n3[3] = {g.nx, g.ny, g.nz};
+    auto cell_range = [&](int t, int lo[3], int hi[3]) {
+        const float* p = tris + (size_t)t * 9;
+        for (int a = 0; a < 3; a++) {
+            float tmn = std::fmin(p[a], std::fmin(p[3 + a], p[6 + a]));
+            float tmx = std::fmax(p[a], std::fmax(p[3 + a], p[6 + a]));
+            lo[a] = grid_cell_host(tmn, o[a], g.inv_cell, n3[a]);
+            hi[a] = grid_cell_host(tmx, o[a], g.inv_cell, n3[a]);
+        }
+    };
+    const size_t ncell = (size_t)g.nx * g.ny * g.nz;
+    std::vector<int> count(ncell + 1, 0);
+    for (int t = 0; t < ntris; t++) {
+        int lo[3], hi[3];
+        cell_range(t, lo, hi);
+        for (int z = lo[2]; z <= hi[2]; z++)
+            for (int y = lo[1]; y <= hi[1]; y++)
+                for (int x = lo[0]; x <= hi[0]; x++) count[((size_t)z * g.ny + y) * g.nx + x]++;
+    }
+    g.cell_start.assign(ncell + 1, 0);
+    for (size_t c = 0; c < ncell; c++) g.cell_start[c + 1] = g.cell_start[c] + count[c];
+    g.cell_tris.assign((size_t)g.cell_start[ncell], 0);
+    std::vector<int> fill(g.cell_start.begin(), g.cell_start.end() - 1);
+    for (int t = 0; t < ntris; t++) {  // ascending t within every cell
+        int lo[3], hi[3];
+        cell_range(t, lo, hi);
+        for (int z = lo[2]; z <= hi[2]; z++)
+            for (int y = lo[1]; y <= hi[1]; y++)
+                for (int x = lo[0]; x <= hi[0]; x++) g.cell_tris[fill[((size_t)z * g.ny + y) * g.nx + x]++] = t;
+    }
+    g.tri.assign((size_t)ntris * 12, 0.f);
+    for (int t = 0; t < ntris; t++) {
+        float* d = &g.tri[(size_t)t * 12];
+        const float* p = tris + (size_t)t * 9;
+        for (int v = 0; v < 3; v++)
+            for (int a = 0; a < 3; a++) d[v * 4 + a] = p[v * 3 + a];
+        std::memcpy(&d[3], &obj[t], sizeof(int));
+    }
+    return g;
+}
+
+}  // namespace rlgpu
+
+extern "C" int rlgpu_cmf_parse(const void* data, int64_t size, float* out_tris, int32_t max_tris, int32_t* out_ntris,
+                               int32_t* out_nverts, uint32_t* out_hash) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(data || size == 0, "rlgpu_cmf_parse: null data");
+        RLGPU_REQUIRE(size >= 8, "Invalid collision mesh file (input data overflown)");
+        const unsigned char* b = (const unsigned char*)data;
+        int32_t nt, nv;
+        std::memcpy(&nt, b, 4);
+        std::memcpy(&nv, b + 4, 4);
+        RLGPU_REQUIRE(!(std::min(nt, nv) <= 0 || std::max(nt, nv) > RLGPU_CMF_MAX_COUNT),
+                      "Invalid collision mesh file (bad triangle/vertex count: [" + std::to_string(nt) + ", " +
+                          std::to_string(nv) + "])");
+        const int64_t need = 8 + (int64_t)nt * 12 + (int64_t)nv * 12;
+        RLGPU_REQUIRE(size >= need, "Invalid collision mesh file (input data overflown by " +
+                                        std::to_string(need - size) + " bytes!)");
+        std::vector<int32_t> idx((size_t)nt * 3);
+        std::vector<float> verts((size_t)nv * 3);
+        std::memcpy(idx.data(), b + 8, idx.size() * 4);
+        std::memcpy(verts.data(), b + 8 + (size_t)nt * 12, verts.size() * 4);
+        for (int32_t v : idx)
+            RLGPU_REQUIRE(v >= 0 && v < nv, "Invalid collision mesh file (bad triangle vertex index)");
+        if (out_ntris) *out_ntris = nt;
+        if (out_nverts) *out_nverts = nv;
+        if (out_hash) *out_hash = rlgpu::cmf_hash(idx.data(), nt, verts.data(), nv);
+        if (out_tris) {
+            int32_t n = nt < max_tris ? nt : max_tris;
+            for (int32_t t = 0; t < n; t++)
+                for (int i = 0; i < 3; i++)
+                    for (int j = 0; j < 3; j++) out_tris[(size_t)t * 9 + i * 3 + j] = verts[(size_t)idx[(size_t)t * 3 + i] * 3 + j];
+        }
+    });
+}
+
+extern "C" int rlgpu_mesh_known_hash(int32_t game_mode, uint32_t hash) {
+    const uint32_t* list = nullptr;
+    int n = 0;
+    if (game_mode == RLGPU_GAMEMODE_SOCCAR) {
+        list = rlgpu::kSoccarHashes;
+        n = (int)(sizeof(rlgpu::kSoccarHashes) / sizeof(uint32_t));
+    } else if (game_mode == RLGPU_GAMEMODE_HOOPS) {
+        list = rlgpu::kHoopsHashes;
+        n = (int)(sizeof(rlgpu::kHoopsHashes) / sizeof(uint32_t));
+    }
+    for (int i = 0; i < n; i++)
+        if (list[i] == hash) return i;
+    return -1;
+}

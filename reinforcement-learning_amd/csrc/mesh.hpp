@@ -1,0 +1,30 @@
+// mesh.hpp -- host-side construction of the env kernel's MeshView (env_kernel.hpp): the triangle
+// table in load order and its uniform-grid index.  Implemented in mesh.hip.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace rlgpu {
+
+struct MeshGrid {
+    std::vector<float> tri;  // ntris x 12 floats: v0.xyz | object id bits, v1.xyz | 0, v2.xyz | 0
+    std::vector<int> cell_start, cell_tris;
+    float ox = 0, oy = 0, oz = 0, inv_cell = 1;
+    int nx = 1, ny = 1, nz = 1, ntris = 0;
+};
+
+// tris_bt: ntris x 9 floats (bullet units); object k owns the next object_ntris[k] triangles
+// (object_ntris == nullptr: one object).  Throws rlgpu::Error on invalid input.
+MeshGrid build_mesh_grid(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects);
+
+// The built-in synthetic arena mesh (include/rlgpu_arena_mesh.h) in bullet units (uu / 50).
+std::vector<float> builtin_mesh_bt();
+
+// Axis cell of a coordinate, the same IEEE operations as the device's grid_cell.
+inline int grid_cell_host(float x, float o, float inv, int n) {
+    float f = __builtin_floorf((x - o) * inv);
+    f = __builtin_fminf(__builtin_fmaxf(f, 0.f), (float)(n - 1));
+    return (int)f;
+}
+
+}  // namespace rlgpu

@@ -25,7 +25,9 @@ OBS, ACTIONS, REWARDS, PADS, CARS = 167, 90, 13, 34, 4
 
 class _Config(ctypes.Structure):
     _fields_ = [("num_arenas", ctypes.c_int32), ("tick_skip", ctypes.c_int32), ("action_delay", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("save_rewards", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("save_rewards", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32),
+                ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
+                ("mesh_object_ntris", ctypes.c_void_p)]
 
 
 class StepOutputs(ctypes.Structure):
@@ -82,7 +84,9 @@ class EnvSet:
     DefaultAction, 13 rewards, NoTouch(8 s) + GoalScore(3) terminals, KickoffState)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, save_rewards=True, device="cuda:0",
-                 max_episode_steps=0):
+                 max_episode_steps=0, mesh=None):
+        """mesh: an rlgpu.mesh.ArenaMesh (e.g. ArenaMesh.from_folder("collision_meshes")), or None for
+        the built-in synthetic arena mesh."""
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("EnvSet needs an MI355X: the product path has no CPU fallback")
@@ -90,6 +94,11 @@ class EnvSet:
         self.device = torch.device(device)
         torch.cuda.set_device(self.device)
         cfg = _Config(num_arenas, tick_skip, action_delay, seed, int(save_rewards), max_episode_steps)
+        if mesh is not None:
+            cfg.mesh_tris = mesh.tris.ctypes.data
+            cfg.mesh_ntris = mesh.num_tris
+            cfg.mesh_objects = mesh.num_objects
+            cfg.mesh_object_ntris = mesh.object_ntris.ctypes.data
         h = ctypes.c_void_p()
         _lib.check(L.rlgpu_envset_create(ctypes.byref(cfg), ctypes.byref(h)), "rlgpu_envset_create")
         self._h = h

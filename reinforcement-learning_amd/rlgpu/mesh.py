@@ -1,0 +1,115 @@
+"""Arena collision meshes -- Python mirror of RocketSim's mesh loading over include/rlgpu_mesh.h.
+
+Reference map:
+    CollisionMeshFile::ReadFromStream + UpdateHash   RocketSim/src/CollisionMeshFile/CollisionMeshFile.cpp:11-95
+                                                     -> parse_cmf(data)
+    CollisionMeshFile::MakeBulletMesh                CollisionMeshFile.cpp:59-68 (vertices as stored,
+                                                     bullet units) -> ArenaMesh.tris
+    RocketSim::Init(folder) / InitFromMem            RocketSim.cpp:70-170 -> ArenaMesh.from_folder /
+                                                     ArenaMesh.from_cmf
+    MeshHashSet                                      RocketSim.cpp:12-44 -> known_hash(h, mode)
+
+Each .cmf file becomes one collision object (the reference adds one static btBvhTriangleMeshShape
+per file, Arena.cpp:1015-1058).  The reference iterates the folder in directory order, which the
+standard leaves unspecified; here files are taken in sorted name order so a set is reproducible.
+An ArenaMesh is passed to EnvSet(mesh=...); the library copies it into HBM and indexes it.
+"""
+import ctypes
+import os
+import warnings
+
+import numpy as np
+
+from . import _lib
+
+GAMEMODES = {"soccar": 0, "hoops": 1}
+MAX_OBJECTS = 32  # RLGPU_MAX_MESH_OBJECTS
+
+_bound = False
+
+
+def _bind():
+    global _bound
+    L = _lib.lib()
+    if not _bound:
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.rlgpu_cmf_parse.argtypes = [vp, i64, vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                      ctypes.POINTER(ctypes.c_uint32)]
+        L.rlgpu_mesh_known_hash.argtypes = [i32, ctypes.c_uint32]
+        _bound = True
+    return L
+
+
+def parse_cmf(data):
+    """(tris [N, 9] float32 in bullet units, num_vertices, hash) of one .cmf image; raises
+    RLGPUError on the reference's error conditions."""
+    L = _bind()
+    buf = bytes(data)
+    nt, nv, h = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_uint32()
+    _lib.check(L.rlgpu_cmf_parse(buf, len(buf), None, 0, ctypes.byref(nt), ctypes.byref(nv), ctypes.byref(h)),
+               "rlgpu_cmf_parse")
+    tris = np.empty((nt.value, 9), np.float32)
+    _lib.check(L.rlgpu_cmf_parse(buf, len(buf), tris.ctypes.data, nt.value, None, None, None), "rlgpu_cmf_parse")
+    return tris, nv.value, h.value
+
+
+def known_hash(h, game_mode="soccar"):
+    """Index of `h` in the reference's known-mesh list for the mode, or -1."""
+    return _bind().rlgpu_mesh_known_hash(GAMEMODES[game_mode], h)
+
+
+class ArenaMesh:
+    """Triangles of all collision objects, object by object (bullet units)."""
+
+    def __init__(self, objects, hashes=None):
+        objs = [np.ascontiguousarray(o, np.float32).reshape(-1, 9) for o in objects]
+        if not objs or len(objs) > MAX_OBJECTS:
+            raise _lib.RLGPUError(f"an arena needs 1..{MAX_OBJECTS} collision objects, got {len(objs)}")
+        self.tris = np.ascontiguousarray(np.concatenate(objs), np.float32)
+        self.object_ntris = np.array([len(o) for o in objs], np.int32)
+        self.hashes = list(hashes) if hashes is not None else []
+
+    @property
+    def num_tris(self):
+        return len(self.tris)
+
+    @property
+    def num_objects(self):
+        return len(self.object_ntris)
+
+    @classmethod
+    def from_cmf(cls, images, game_mode="soccar"):
+        """RocketSim::InitFromMem: one object per image; unknown / duplicate hashes warn, as the
+        reference does (RocketSim.cpp:140-155)."""
+        objects, hashes, seen = [], [], set()
+        for i, data in enumerate(images):
+            tris, _, h = parse_cmf(data)
+            if h in seen:
+                warnings.warn(f"collision mesh [{i}] is a duplicate (0x{h:08x})")
+            elif known_hash(h, game_mode) < 0:
+                warnings.warn(f"collision mesh [{i}] does not match any known {game_mode} mesh (0x{h:08x})")
+            seen.add(h)
+            objects.append(tris)
+            hashes.append(h)
+        return cls(objects, hashes)
+
+    @classmethod
+    def from_folder(cls, folder, game_mode="soccar"):
+        """RocketSim::Init(collisionMeshesFolder): <folder>/<mode>/*.cmf, sorted by name."""
+        sub = os.path.join(folder, game_mode)
+        names = sorted(n for n in os.listdir(sub) if n.endswith(".cmf"))
+        if not names:
+            raise _lib.RLGPUError(f"no .cmf meshes in {sub}")
+        images = []
+        for n in names:
+            with open(os.path.join(sub, n), "rb") as f:
+                images.append(f.read())
+        return cls.from_cmf(images, game_mode)
+
+
+def cmf_bytes(vertices, triangles):
+    """Serialise a mesh in the .cmf layout (test fixtures, tools): int32 nTris, int32 nVerts,
+    int32[3] per triangle, float32[3] per vertex, little endian."""
+    v = np.ascontiguousarray(vertices, "<f4").reshape(-1, 3)
+    t = np.ascontiguousarray(triangles, "<i4").reshape(-1, 3)
+    return np.array([len(t), len(v)], "<i4").tobytes() + t.tobytes() + v.tobytes()

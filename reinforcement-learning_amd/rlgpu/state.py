@@ -10,7 +10,7 @@ UU_TO_BT = 1.0 / 50.0
 
 CONTACT = np.dtype([("localA", "<f4", 3), ("localB", "<f4", 3), ("normalB", "<f4", 3), ("dist", "<f4"),
                     ("applied", "<f4"), ("friction", "<f4"), ("restitution", "<f4"), ("special", "<i4")], align=True)
-MANIFOLD = np.dtype([("key", "<i4"), ("count", "<i4"), ("pts", CONTACT, 4)], align=True)
+MANIFOLD = np.dtype([("key", "<i4"), ("count", "<i4"), ("pts", CONTACT, 4)], align=True)  # per-tick scratch only
 BODY = np.dtype([("pos", "<f4", 3), ("rot", "<f4", 9), ("vel", "<f4", 3), ("angvel", "<f4", 3)], align=True)
 CAR = np.dtype([
     ("body", BODY), ("controls", "<f4", 8), ("last_controls", "<f4", 8),
@@ -38,7 +38,7 @@ ENV = np.dtype([
     ("rng_counter", "<u4"), ("manifold_overflow", "<u4"), ("episode_steps", "<i4"), ("reserved0", "<i4"),
 ], align=True)
 ARENA = np.dtype([("ball", BODY), ("ball_vel_impulse_cache", "<f4", 3), ("ball_sleeping", "<i4"),
-                  ("cars", CAR, 4), ("pads", PAD, 34), ("manifolds", MANIFOLD, 12), ("env", ENV)], align=True)
+                  ("cars", CAR, 4), ("pads", PAD, 34), ("env", ENV)], align=True)
 
 
 def view(buf):

@@ -112,6 +112,47 @@ def test_env_perturbed_contacts_parity(gpu):
         _check_step(g, o, f"perturbed step {t}")
 
 
+def test_env_custom_mesh_parity(gpu):
+    """A dense 8-object collision mesh loaded from .cmf images (bumpy heightfield floor, side
+    ramps, back walls; 3.5k triangles): wheel rays, ball and car contacts against the uniform-grid
+    index on the GPU must equal the oracle's scan of every triangle in index order, with one
+    manifold per (body, mesh object) pair."""
+    import warnings
+
+    import torch
+    from rlgpu.env import EnvSet
+    from rlgpu.mesh import ArenaMesh, cmf_bytes
+    from rlgpu.state import ARENA
+    from tests_util import procedural_arena_mesh
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        mesh = ArenaMesh.from_cmf([cmf_bytes(v, t) for v, t in procedural_arena_mesh()])
+    n = 48
+    g, o = EnvSet(n, seed=9, device=gpu, mesh=mesh), oracle.EnvSet(n, seed=9, mesh=mesh, threads=4)
+    _check(g, o, "create")
+    rng = np.random.default_rng(4)
+    for t in range(10):
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True)
+        _check_step(g, o, f"mesh step {t}")
+    st = np.frombuffer(o.get_arenas().tobytes(), ARENA).copy()
+    for i in range(n):  # throw the ball at the ramps / back walls, launch cars
+        d = rng.normal(size=3)
+        d[2] = abs(d[2])
+        st["ball"][i]["vel"] = (d / np.linalg.norm(d) * rng.uniform(40, 110)).astype(np.float32)
+        for k in range(4):
+            st["cars"][i]["body"]["vel"][k] = rng.uniform(-40, 40, 3).astype(np.float32) * [1, 1, 0.3]
+    buf = np.frombuffer(st.tobytes(), np.uint8)
+    o.set_arenas(buf)
+    g.set_arenas(buf)
+    for t in range(50):
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True)
+        _check_step(g, o, f"mesh perturbed step {t}")
+
+
 def test_env_reset_arenas_mask(gpu):
     import torch
     n = 12

@@ -1,0 +1,138 @@
+"""Collision-mesh ingestion (include/rlgpu_mesh.h, rlgpu/mesh.py) and the oracle's mesh path.
+CPU only: the .cmf parser and hash are host code of librlgpu.so.
+
+Parity anchors (the reference ships no .cmf files, so no golden meshes exist):
+  * the hash is restated here independently in Python from CollisionMeshFile.cpp:70-95 and must
+    equal the library's on meshes with positive and negative coordinates (parity unpinned beyond
+    the formula: no reference hash of a mesh we hold is known);
+  * the reference's error conditions (CollisionMeshFile.cpp:21-51) are reproduced;
+  * the known-hash table equals RocketSim.cpp:20-35.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from rlgpu import _lib
+from rlgpu.mesh import ArenaMesh, cmf_bytes, known_hash, parse_cmf
+from rlgpu.state import ARENA, BT_TO_UU, UU_TO_BT
+from tests_util import mesh_from_objects, procedural_arena_mesh
+
+
+def py_cmf_hash(verts, tris):
+    """CollisionMeshFile::UpdateHash restated (uint32 arithmetic; float -> uint32 as x86-64
+    compilers do it: truncate to int64, keep the low 32 bits)."""
+    M = 0xFFFFFFFF
+    h = (len(verts) + len(tris) * len(verts)) & M
+    for t in tris:
+        for i in range(3):
+            for j in range(3):
+                v = int(np.float32(verts[t[i]][j])) & M  # int() truncates toward zero
+                for _ in range(2):
+                    v = (((v >> 16) ^ v) * 0x45D9F3B) & M
+                v = ((v >> 16) ^ v) & M
+                h ^= (v + 0x9E3779B9 + ((h << 6) & M) + (h >> 2)) & M
+    return h
+
+
+def test_parse_roundtrip_and_hash():
+    rng = np.random.default_rng(0)
+    verts = (rng.random((40, 3)) * 2000 - 1000).astype(np.float32)  # negative coordinates too
+    tris = rng.integers(0, 40, (70, 3)).astype(np.int32)
+    data = cmf_bytes(verts, tris)
+    out, nv, h = parse_cmf(data)
+    assert nv == 40 and out.shape == (70, 9)
+    np.testing.assert_array_equal(out, verts[tris].reshape(-1, 9))
+    assert h == py_cmf_hash(verts, tris)
+    # trailing bytes are ignored (the reference only checks for overflow)
+    out2, _, h2 = parse_cmf(data + b"\x00" * 7)
+    assert h2 == h and (out2 == out).all()
+
+
+def test_hash_is_order_sensitive():
+    verts = np.array([[0, 0, 0], [100, 0, 0], [0, 100, 0], [0, 0, 100]], np.float32)
+    a = np.array([[0, 1, 2], [0, 2, 3]], np.int32)
+    assert parse_cmf(cmf_bytes(verts, a))[2] != parse_cmf(cmf_bytes(verts, a[::-1].copy()))[2]
+    assert parse_cmf(cmf_bytes(verts, a))[2] == py_cmf_hash(verts, a)
+
+
+@pytest.mark.parametrize("bad", ["count0", "count_big", "short", "index"])
+def test_parse_errors_match_reference(bad):
+    verts = np.zeros((3, 3), np.float32)
+    tris = np.array([[0, 1, 2]], np.int32)
+    data = cmf_bytes(verts, tris)
+    if bad == "count0":
+        data = np.array([0, 3], "<i4").tobytes() + data[8:]
+        msg = "bad triangle/vertex count"
+    elif bad == "count_big":
+        data = np.array([1, 1000001], "<i4").tobytes() + data[8:]
+        msg = "bad triangle/vertex count"
+    elif bad == "short":
+        data = data[:-1]
+        msg = "overflown"
+    else:
+        data = cmf_bytes(verts, np.array([[0, 1, 3]], np.int32))
+        msg = "bad triangle vertex index"
+    with pytest.raises(_lib.RLGPUError, match=msg):
+        parse_cmf(data)
+
+
+def test_known_hashes():
+    assert known_hash(0xA160BAF9) == 0 and known_hash(0xD84C7A68) == 15
+    assert known_hash(0x16F3CC19, "hoops") == 11 and known_hash(0x16F3CC19) == -1
+    assert known_hash(0x12345678) == -1
+
+
+def test_arena_mesh_from_cmf_objects_and_warnings():
+    objs = procedural_arena_mesh(nx=8, ny=8)
+    with pytest.warns(UserWarning, match="does not match any known soccar"):
+        m = ArenaMesh.from_cmf([cmf_bytes(v, t) for v, t in objs])
+    tris, counts = mesh_from_objects(objs)
+    np.testing.assert_array_equal(m.tris, tris)
+    np.testing.assert_array_equal(m.object_ntris, counts)
+    assert m.num_objects == len(objs) and len(m.hashes) == len(objs)
+    with pytest.raises(_lib.RLGPUError):
+        ArenaMesh([np.zeros((1, 9), np.float32)] * 33)
+
+
+def _state(env):
+    return np.frombuffer(env.get_arenas().tobytes(), ARENA).copy()
+
+
+def test_oracle_ball_rolls_off_mesh_ramp():
+    """A ball dropped onto the +x side-wall ramp (45 degrees, its own collision object) is pushed
+    towards -x; with the built-in mesh (no ramp there) it falls straight onto the floor plane."""
+    objs = procedural_arena_mesh(nx=8, ny=8)
+    outs = []
+    for mesh in (mesh_from_objects(objs), None):
+        env = oracle.EnvSet(1, seed=2, mesh=mesh)
+        st = _state(env)
+        st["ball"][0]["pos"] = np.array([3950, 0, 400], np.float32) * UU_TO_BT
+        st["ball"][0]["vel"] = np.array([0, 0, -1e-3], np.float32)
+        env.set_arenas(np.frombuffer(st.tobytes(), np.uint8))
+        for _ in range(15):
+            env.step(np.full(4, 8, np.int32), False)
+        outs.append(_state(env)["ball"][0]["vel"] * BT_TO_UU)
+    assert outs[0][0] < -200, outs[0]
+    assert abs(outs[1][0]) < 1.0, outs[1]
+
+
+def test_oracle_car_ball_hit_registers():
+    """Car driving into the ball at 1500 uu/s: the ball-car manifold is (A = ball, B = car), so the
+    callback fires (ballHitInfo valid, Arena.cpp:283-333) and the ball leaves faster than the car."""
+    env = oracle.EnvSet(1, seed=3)
+    st = _state(env)
+    st["ball"][0]["vel"] = np.array([0, 0, 1e-3], np.float32)
+    c = st["cars"][0]
+    c["body"]["pos"][0] = np.array([0, -250, 17], np.float32) * UU_TO_BT
+    c["body"]["rot"][0] = np.array([[0, -1, 0], [1, 0, 0], [0, 0, 1]], np.float32).reshape(-1)
+    c["body"]["vel"][0] = np.array([0, 1500, 0], np.float32) * UU_TO_BT
+    env.set_arenas(np.frombuffer(st.tobytes(), np.uint8))
+    for _ in range(2):
+        env.step(np.full(4, 8, np.int32), False)
+    s2 = _state(env)
+    assert s2["cars"][0]["ball_hit_valid"][0] == 1
+    rel = s2["cars"][0]["ball_hit_rel_pos"][0]  # on the ball: |rel| ~ ball radius (uu)
+    assert 80 < np.linalg.norm(rel) < 100, rel
+    vb = s2["ball"][0]["vel"] * BT_TO_UU
+    vc = s2["cars"][0]["body"]["vel"][0] * BT_TO_UU
+    assert vb[1] > vc[1] + 300, (vb, vc)
