@@ -344,6 +344,27 @@ __global__ void reduce_splits(const float* part, int splits, int64_t stride, int
     for (int k = 0; k < splits; k++) s += part[k * stride + e];
     out[e] = accumulate ? out[e] + s : s;
 }
+// the same sums, 4 columns per thread (n, stride multiples of 4, 16-byte aligned pointers); the
+// split loop is unrolled so several partial loads are in flight
+__global__ void reduce_splits4(const float* part, int splits, int64_t stride, int64_t n, float* out, int accumulate) {
+    int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (e >= n) return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int k = 0; k < splits; k++) {
+        float4 v = *reinterpret_cast<const float4*>(part + k * stride + e);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + e);
+    if (accumulate) {
+        float4 v = *o;
+        s = make_float4(v.x + s.x, v.y + s.y, v.z + s.z, v.w + s.w);
+    }
+    *o = s;
+}
 
 // ---------------------------------------------------------------- wave helpers
 DEV float wave_sum(float v) {
@@ -360,51 +381,80 @@ DEV float wave_max(float v) {
 
 // LayerNorm (eps 1e-5, biased variance) + LeakyReLU, training: one wave per row.
 // Keeps xhat [R,H] and act [R,H] for the backward, rstd [R].
+// Lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (float4 loads / stores when H is a
+// multiple of 4); gamma / beta stay in registers and each wave walks LNF_ROWS/4 rows.
+constexpr int LNF_ROWS = 8;
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const float* gamma, const float* beta, int R, int H,
                                                      float slope, int use_ln, float* xhat, float* act, float* rstd_out) {
-    int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (row >= R) return;
-    const float* z = Z + (int64_t)row * H;
-    float v[MAXH];
-    constexpr int nper = MAXH;
-    float s = 0.f;
-    for (int q = 0; q < nper; q++) {
-        int c = lane + 64 * q;
-        v[q] = c < H ? z[c] : 0.f;
-        s += v[q];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c0 = lane * MAXH;
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
+    float g[MAXH], b[MAXH];
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) {
+        const int c = c0 + q;
+        g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
+        b[q] = (use_ln && c < H) ? beta[c] : 0.f;
     }
-    float* xo = xhat + (int64_t)row * H;
-    float* ao = act + (int64_t)row * H;
-    if (!use_ln) {
-        for (int q = 0; q < nper; q++) {
-            int c = lane + 64 * q;
-            if (c < H) {
-                xo[c] = v[q];
-                ao[c] = v[q] > 0.f ? v[q] : v[q] * slope;
+    for (int i = 0; i < LNF_ROWS / 4; i++) {
+        const int row = blockIdx.x * LNF_ROWS + i * 4 + wv;
+        if (row >= R) break;
+        const float* z = Z + (int64_t)row * H + c0;
+        float v[MAXH];
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 4) {
+                float4 t = *reinterpret_cast<const float4*>(z + q);
+                v[q] = t.x; v[q + 1] = t.y; v[q + 2] = t.z; v[q + 3] = t.w;
             }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? z[q] : 0.f;
         }
-        return;
-    }
-    float mean = wave_sum(s) / (float)H;
-    float s2 = 0.f;
-    for (int q = 0; q < nper; q++) {
-        int c = lane + 64 * q;
-        float d = c < H ? v[q] - mean : 0.f;
-        s2 += d * d;
-    }
-    float var = wave_sum(s2) / (float)H;
-    float rs = 1.f / sqrtf(var + 1e-5f);
-    for (int q = 0; q < nper; q++) {
-        int c = lane + 64 * q;
-        if (c < H) {
-            float xh = (v[q] - mean) * rs;
-            float h = xh * gamma[c] + beta[c];
-            xo[c] = xh;
-            ao[c] = h > 0.f ? h : h * slope;
+        float xh[MAXH], a[MAXH];
+        float rs = 1.f;
+        if (use_ln) {
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) s += v[q];
+            const float mean = wave_sum(s) / (float)H;
+            float s2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) {
+                float d = c0 + q < H ? v[q] - mean : 0.f;
+                s2 += d * d;
+            }
+            rs = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) xh[q] = (v[q] - mean) * rs;
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) xh[q] = v[q];
         }
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) {
+            float hv = use_ln ? xh[q] * g[q] + b[q] : xh[q];
+            a[q] = hv > 0.f ? hv : hv * slope;
+        }
+        float* xo = xhat + (int64_t)row * H + c0;
+        float* ao = act + (int64_t)row * H + c0;
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 4) {
+                *reinterpret_cast<float4*>(xo + q) = make_float4(xh[q], xh[q + 1], xh[q + 2], xh[q + 3]);
+                *reinterpret_cast<float4*>(ao + q) = make_float4(a[q], a[q + 1], a[q + 2], a[q + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++)
+                if (c0 + q < H) {
+                    xo[q] = xh[q];
+                    ao[q] = a[q];
+                }
+        }
+        if (use_ln && lane == 0) rstd_out[row] = rs;
     }
-    if (lane == 0) rstd_out[row] = rs;
 }
 
 // bf16 inference variant: Z bf16 in, bf16(LeakyReLU(bf16(LN(Z)))) out (torch bf16 module chain).
@@ -552,31 +602,49 @@ RLGPU_NPER_DISPATCH(ln_act_fwd_bf16)
 RLGPU_NPER_DISPATCH(ln_act_bwd)
 
 // Rank-1 output layer (the critic's Linear(H, 1)): GEMM tiles would be 1/128 occupied, so the
-// head runs as wave-per-row dot products.  Lane l owns columns [MAXH*l, MAXH*l + MAXH).
+// head runs as wave-per-row dot products.  Lane l owns the contiguous columns
+// [MAXH*l, MAXH*l + MAXH) (float4 loads when H is a multiple of 4); w stays in registers and each
+// wave walks H1_ROWS/4 rows.
+constexpr int H1_ROWS = 16;
 template <int MAXH>
 __global__ void __launch_bounds__(256) head1_fwd(const float* X, const float* w, const float* b, int R, int H, float* out) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (row >= R) return;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c0 = lane * MAXH;
-    const float* x = X + (int64_t)row * H;
-    float s = 0.f;
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
+    float wr[MAXH];
 #pragma unroll
-    for (int q = 0; q < MAXH; q++) {
-        int c = c0 + q;
-        if (c < H) s += x[c] * w[c];
+    for (int q = 0; q < MAXH; q++) wr[q] = c0 + q < H ? w[c0 + q] : 0.f;
+    const float bias = b[0];
+    for (int i = 0; i < H1_ROWS / 4; i++) {
+        const int row = blockIdx.x * H1_ROWS + i * 4 + wv;
+        if (row >= R) break;
+        const float* x = X + (int64_t)row * H + c0;
+        float s = 0.f;
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 4) {
+                float4 t = *reinterpret_cast<const float4*>(x + q);
+                s += t.x * wr[q] + t.y * wr[q + 1] + t.z * wr[q + 2] + t.w * wr[q + 3];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++)
+                if (c0 + q < H) s += x[q] * wr[q];
+        }
+        s = wave_sum(s);
+        if (lane == 0) out[row] = s + bias;
     }
-    s = wave_sum(s);
-    if (lane == 0) out[row] = s + b[0];
 }
 
 // Backward of the rank-1 head: dA[i, :] = dv[i] * w; partials part[blk][0..H) = sum dv*X[i, :],
-// part[blk][H] = sum dv (bias) over the block's rows.
+// part[blk][H] = sum dv (bias) over the block's rows.  Same lane layout as head1_fwd.
 template <int MAXH>
 __global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w, const float* dv, int R, int H, float* dA,
                                                 float* part) {
     __shared__ float red[4][64 * MAXH + 1];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c0 = lane * MAXH;
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
     float wr[MAXH], acc[MAXH];
     float accb = 0.f;
 #pragma unroll
@@ -589,14 +657,25 @@ __global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w,
         const int row = r0 + rr;
         if (row >= R) break;
         const float d = dv[row];
-        const float* x = X + (int64_t)row * H;
-        float* da = dA + (int64_t)row * H;
+        const float* x = X + (int64_t)row * H + c0;
+        float* da = dA + (int64_t)row * H + c0;
+        if (vec) {
 #pragma unroll
-        for (int q = 0; q < MAXH; q++) {
-            int c = c0 + q;
-            if (c < H) {
-                da[c] = d * wr[q];
-                acc[q] += d * x[c];
+            for (int q = 0; q < MAXH; q += 4) {
+                float4 t = *reinterpret_cast<const float4*>(x + q);
+                *reinterpret_cast<float4*>(da + q) = make_float4(d * wr[q], d * wr[q + 1], d * wr[q + 2], d * wr[q + 3]);
+                acc[q] += d * t.x;
+                acc[q + 1] += d * t.y;
+                acc[q + 2] += d * t.z;
+                acc[q + 3] += d * t.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) {
+                if (c0 + q < H) {
+                    da[q] = d * wr[q];
+                    acc[q] += d * x[q];
+                }
             }
         }
         accb += d;

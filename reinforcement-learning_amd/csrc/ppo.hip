@@ -123,7 +123,10 @@ void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx
     int z = (int)ceil_div(n, chunk);
     gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
     int64_t e = (int64_t)out * in;
-    hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
+    if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)m.wpart & 15) == 0)
+        hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
+    else
+        hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -164,7 +167,7 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
         gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s, tail_ok);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
-        hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, 4)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
+        hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.xhat[l], m.act[l], m.rstd[l]);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = m.act[l];
@@ -173,15 +176,19 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
     }
     const Layer& O = m.L[nh];
     if (O.out == 1) {  // rank-1 head (critic value): wave-per-row dot products
-        hipLaunchKernelGGL(mlp::head1_fwd_any(O.in), dim3(ceil_div(n, 4)), dim3(256), 0, s, in, P + O.w, P + O.b, n, O.in, out);
+        hipLaunchKernelGGL(mlp::head1_fwd_any(O.in), dim3(ceil_div(n, mlp::H1_ROWS)), dim3(256), 0, s, in, P + O.w, P + O.b, n,
+                           O.in, out);
         RLGPU_CHECK_HIP(hipGetLastError());
         return;
     }
     gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, P + O.w, O.in, out, O.out, P + O.b, n, O.out, O.in, 1, s);
 }
 
-// backward from dout [n, out] into the grad buffer (accumulating)
-void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hipStream_t s) {
+// backward from dout [n, out] into the grad buffer (accumulating).  dout_part: optional per-block
+// column partials of dout (dout_nblk rows of `out` floats, written by the loss kernel) for the
+// output bias, instead of a separate column-sum pass.
+void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hipStream_t s,
+              const float* dout_part = nullptr, int dout_nblk = 0) {
     Model& m = h->M[mi];
     const float* P = h->params;
     float* G = h->grads;
@@ -195,7 +202,10 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         reduce_partials(m, m.cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
     } else {
         weight_grad(m, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s);
-        colsum_into(m, dout, n, O.out, G + O.b, s);
+        if (dout_part)
+            reduce_partials(m, dout_part, dout_nblk, O.out, O.out, G + O.b, s);
+        else
+            colsum_into(m, dout, n, O.out, G + O.b, s);
         // dA = dout . W_out
         gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s);
     }
@@ -563,11 +573,12 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
         // policy on the caller's stream
         forward_train(h, 0, h->x0, n, pm.y, s);
-        hipLaunchKernelGGL(ppo::policy_loss, dim3(ceil_div(n, ppo::PL_ROWS)), dim3(256), 0, s, pm.y, d_masks, d_actions,
-                           d_old_logp, d_adv, d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
-                           1.f / std::log((float)A), pm.dy, d_metrics);
+        const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
+        hipLaunchKernelGGL(ppo::policy_loss, dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
+                           d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
+                           1.f / std::log((float)A), pm.dy, d_metrics, pm.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 0, h->x0, n, pm.dy, s);
+        backward(h, 0, h->x0, n, pm.dy, s, pm.cpart, pl_blocks);
         RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
     });
 }

@@ -110,13 +110,16 @@ constexpr int PL_ROWS = 64;
 __global__ void __launch_bounds__(256) policy_loss(const float* logits, const uint8_t* masks, const int32_t* actions,
                                                   const float* old_logp, const float* adv, const int32_t* idx, int64_t start,
                                                   int n, int A, const float* adv_stats, float bsr, float clip_range,
-                                                  float ent_scale, float inv_log_a, float* dlogits, float* metrics) {
+                                                  float ent_scale, float inv_log_a, float* dlogits, float* metrics,
+                                                  float* bias_part) {
     __shared__ float red[4][5];
+    __shared__ float colred[4][128];  // per-wave column sums of dlogits (A <= 128)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int a0 = 2 * lane, a1 = 2 * lane + 1;
     const bool in0 = a0 < A, in1 = a1 < A;
     const float mean = adv_stats[0], sd = adv_stats[1];
     float m_ent = 0.f, m_kl = 0.f, m_pl = 0.f, m_ratio = 0.f, m_clip = 0.f;
+    float col0 = 0.f, col1 = 0.f;
     for (int i = 0; i < PL_ROWS / 4; i++) {
         int row = blockIdx.x * PL_ROWS + i * 4 + w;
         if (row >= n) break;
@@ -157,8 +160,11 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         d1 = (p1 >= kMinProb && p1 <= 1.f) ? d1 : 0.f;
         float dot = wave_sum((in0 ? d0 * p0 : 0.f) + (in1 ? d1 * p1 : 0.f));
         float* dl = dlogits + (int64_t)row * A;
-        if (in0) dl[a0] = p0 * (d0 - dot);
-        if (in1) dl[a1] = p1 * (d1 - dot);
+        const float g0 = p0 * (d0 - dot), g1 = p1 * (d1 - dot);
+        if (in0) dl[a0] = g0;
+        if (in1) dl[a1] = g1;
+        col0 += in0 ? g0 : 0.f;
+        col1 += in1 ? g1 : 0.f;
         float lr = lp - old;
         m_ent += ent * inv_log_a;
         m_kl += expf(lr) - 1.f - lr;
@@ -166,6 +172,8 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         m_ratio += ratio;
         m_clip += fabsf(ratio - 1.f) > clip_range ? 1.f : 0.f;
     }
+    colred[w][a0] = col0;
+    colred[w][a1] = col1;
     if (lane == 0) {
         red[w][0] = m_ent;
         red[w][1] = m_kl;
@@ -174,6 +182,9 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         red[w][4] = m_clip;
     }
     __syncthreads();
+    if (bias_part)  // output-bias gradient partials of this block's rows: part[blk][A]
+        for (int c = threadIdx.x; c < A; c += 256)
+            bias_part[(int64_t)blockIdx.x * A + c] = colred[0][c] + colred[1][c] + colred[2][c] + colred[3][c];
     if (threadIdx.x < 5 && metrics) {
         const int slot[5] = {0, 1, 2, 4, 5};  // entropy, KL, policy loss, ratio, clip fraction
         float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
