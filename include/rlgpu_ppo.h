@@ -110,6 +110,9 @@ int rlgpu_ppo_optimizer_step(rlgpu_ppo* h, float* d_metrics, void* stream);
 int rlgpu_ppo_zero_grad(rlgpu_ppo* h, void* stream);
 /* Optimizer state (step count + moments) for checkpointing; moments are device pointers. */
 int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_exp_avg, float** d_exp_avg_sq);
+/* Restore the AdamW step count (checkpoint resume; the moments are written through the pointers
+ * rlgpu_ppo_optimizer_state returns). */
+int rlgpu_ppo_set_optimizer_step(rlgpu_ppo* h, int64_t step);
 
 /* Building block, exported for tests and microbenchmarks: C[I,J] = sum_k A(i,k) B(k,j) (+ bias[j])
  * on f32-input MFMA.  a_layout 0: A stored [I][lda] (k contiguous), 1: [K][lda] (i contiguous);

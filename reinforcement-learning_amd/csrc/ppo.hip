@@ -625,6 +625,13 @@ extern "C" int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_
     });
 }
 
+extern "C" int rlgpu_ppo_set_optimizer_step(rlgpu_ppo* h, int64_t step) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && step >= 0, "rlgpu_ppo_set_optimizer_step: bad argument");
+        h->step = step;
+    });
+}
+
 extern "C" int rlgpu_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t* d_out, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(d_out && n >= 0 && n < (1ll << 31), "rlgpu_permutation: bad argument");

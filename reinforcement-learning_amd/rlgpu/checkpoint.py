@@ -1,0 +1,145 @@
+"""Checkpoints in the reference's on-disk format.
+
+Reference map:
+    Learner::Save / Load                 GigaLearnCPP/src/public/GigaLearnCPP/Learner.cpp:224-279
+      <checkpointFolder>/<totalTimesteps>/ numbered directories, the highest one is loaded,
+      checkpointsToKeep (default 8, -1 = keep all) oldest-first pruning      :236-252
+    Learner::SaveStats / LoadStats       Learner.cpp:166-221  -> RUNNING_STATS.json
+      {"total_timesteps", "total_iterations", "return_stat": WelfordStat::ToJSON}
+    Model::Save / Load                   src/private/GigaLearnCPP/Util/Models.cpp:116-195
+      <NAME>.lt = torch::save(nn::Sequential): a TorchScript archive whose submodules "0", "1", ...
+      hold the Linear / LayerNorm parameters ("weight", "bias"); Load refuses a checkpoint whose
+      per-parameter sizes differ (GetSeqSizes, Models.cpp:79-87, 147-166)
+    Utils::FindNumberedDirs              src/public/GigaLearnCPP/Util/Utils.cpp:3-27
+
+The model files written here are TorchScript-scripted torch.nn.Sequential modules with the same
+layer order as GGL::Model (Linear [, LayerNorm], LeakyReLU per hidden layer, then the output
+Linear), which libtorch's torch::load(seq, stream) reads into the reference's Sequential
+(verified by tools/lt_load_check.cpp, tests/test_checkpoint.py), so a GPU-trained policy loads in
+the reference's InferUnit / RLBotClient; reference-written POLICY.lt / CRITIC.lt load here.
+
+Optimizer state: the reference writes <NAME>_OPTIM.lt with torch::optim::AdamW::save, keyed by
+tensor addresses; it tolerates the file being absent (warns and resets the optimizer,
+Models.cpp:168-186).  This module keeps the exact AdamW state (step, exp_avg, exp_avg_sq in the
+flat torch parameter order) in RLGPU_OPTIM.safetensors next to the model files, which the
+reference ignores; loading a checkpoint without it resets the optimizer, as the reference does.
+"""
+import json
+import os
+import shutil
+import warnings
+
+STATS_FILE = "RUNNING_STATS.json"          # Learner.cpp:221
+MODEL_NAMES = ("policy", "critic")         # PPOLearner model names (PPOLearner.cpp:13-74)
+OPTIM_FILE = "RLGPU_OPTIM.safetensors"
+
+
+def model_path(folder, name, suffix=""):
+    """Model::GetSuffixedSavePath (Models.h:114-128): upper-cased name + suffix + ".lt"."""
+    return os.path.join(folder, (name + suffix).upper() + ".lt")
+
+
+def numbered_dirs(base):
+    """Utils::FindNumberedDirs: integer-named subdirectories of base."""
+    if not os.path.isdir(base):
+        return set()
+    return {int(n) for n in os.listdir(base) if n.isdigit() and os.path.isdir(os.path.join(base, n))}
+
+
+def write_model(seq, path):
+    """torch::save(seq) equivalent: a scripted nn.Sequential (CPU tensors)."""
+    import torch
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", DeprecationWarning)  # TorchScript is the format libtorch reads
+        torch.jit.script(seq.cpu()).save(path)
+
+
+def read_model_state(path):
+    """Parameters of a <NAME>.lt in torch parameters() order (reference- or rlgpu-written)."""
+    import torch
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", DeprecationWarning)
+        m = torch.jit.load(path, map_location="cpu")
+    return [p.detach().float() for p in m.parameters()]
+
+
+def save(learner, folder, keep=8):
+    """Learner::Save: <folder>/<total_timesteps>/{RUNNING_STATS.json, POLICY.lt, CRITIC.lt,
+    RLGPU_OPTIM.safetensors}, then prune to `keep` checkpoints (-1 keeps all).  Returns the path."""
+    import torch
+    from safetensors.torch import save_file
+    path = os.path.join(folder, str(int(learner.total_steps)))
+    os.makedirs(path, exist_ok=True)
+    stats = {"total_timesteps": int(learner.total_steps), "total_iterations": int(learner.iteration),
+             "return_stat": learner.return_stat.to_json()}
+    with open(os.path.join(path, STATS_FILE), "w") as f:
+        json.dump(stats, f, indent=4)
+    ppo = learner.ppo
+    for mi, name in enumerate(MODEL_NAMES):
+        write_model(ppo.torch_module(mi), model_path(path, name))
+    step, m, v = ppo.optimizer_state()
+    t = {"step": torch.tensor([step], dtype=torch.int64)}
+    for mi, name in enumerate(MODEL_NAMES):
+        o, c = ppo.model_range(mi)
+        t[name + ".exp_avg"] = m[o:o + c].detach().cpu().contiguous()
+        t[name + ".exp_avg_sq"] = v[o:o + c].detach().cpu().contiguous()
+    save_file(t, os.path.join(path, OPTIM_FILE))
+    if keep != -1:
+        dirs = numbered_dirs(folder)
+        while len(dirs) > keep:
+            low = min(dirs)
+            shutil.rmtree(os.path.join(folder, str(low)))
+            dirs.discard(low)
+    return path
+
+
+def load(learner, folder, allow_missing_models=True):
+    """Learner::Load: the highest numbered checkpoint under `folder` (none: start fresh, returns
+    None).  Model sizes must match the current architecture (Models.cpp:147-166)."""
+    import torch
+    dirs = numbered_dirs(folder)
+    if not dirs:
+        return None
+    path = os.path.join(folder, str(max(dirs)))
+    with open(os.path.join(path, STATS_FILE)) as f:
+        j = json.load(f)
+    learner.total_steps = int(j["total_timesteps"])
+    learner.iteration = int(j["total_iterations"])
+    if "return_stat" in j:
+        learner.return_stat.read_json(j["return_stat"])
+    ppo = learner.ppo
+    for mi, name in enumerate(MODEL_NAMES):
+        p = model_path(path, name)
+        if not os.path.exists(p):
+            if allow_missing_models:
+                warnings.warn(f'model "{name}" does not exist in {path} and will be reset')
+                continue
+            raise FileNotFoundError(f'model "{name}" does not exist in {path}')
+        tensors = read_model_state(p)
+        want = ppo.model_sizes(mi)
+        got = [t.numel() for t in tensors]
+        if got != want:
+            raise ValueError(f"Saved model has different size than current model, cannot load model from {p}:\n"
+                             f" > Current model: {want},\n > Saved model:   {got}")
+        o, c = ppo.model_range(mi)
+        ppo.params[o:o + c].copy_(torch.cat([t.reshape(-1) for t in tensors]).to(ppo.params.device))
+    ppo.refresh_half()
+    op = os.path.join(path, OPTIM_FILE)
+    if os.path.exists(op):
+        from safetensors.torch import load_file
+        t = load_file(op)
+        step, m, v = ppo.optimizer_state()
+        for mi, name in enumerate(MODEL_NAMES):
+            o, c = ppo.model_range(mi)
+            if t[name + ".exp_avg"].numel() != c:
+                raise ValueError(f"optimizer state in {op} does not match the model sizes")
+            m[o:o + c].copy_(t[name + ".exp_avg"].to(m.device))
+            v[o:o + c].copy_(t[name + ".exp_avg_sq"].to(v.device))
+        ppo.set_optimizer_step(int(t["step"][0]))
+    else:
+        warnings.warn(f"no optimizer state found in {path}, optimizer will be reset")
+        step, m, v = ppo.optimizer_state()
+        m.zero_()
+        v.zero_()
+        ppo.set_optimizer_step(0)
+    return path

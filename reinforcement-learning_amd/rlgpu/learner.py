@@ -26,22 +26,36 @@ OBS, ACTIONS = 167, 90
 
 
 class WelfordStat:
-    """GGL::WelfordStat (Util/WelfordStat.h:7-67): fp64 running mean / variance."""
+    """GGL::WelfordStat (Util/WelfordStat.h:7-67): fp64 running mean / variance, the reference's
+    update order (delta, delta / (count + 1), variance += delta * deltaN * count)."""
 
     def __init__(self):
         self.n, self.mean, self.m2 = 0, 0.0, 0.0
 
     def add(self, xs):
-        for x in np.asarray(xs, np.float64).ravel():
+        for x in np.asarray(xs, np.float32).ravel():
+            delta = float(x) - self.mean
+            delta_n = delta / (self.n + 1)
+            self.mean += delta_n
+            self.m2 += delta * delta_n * self.n
             self.n += 1
-            d = x - self.mean
-            self.mean += d / self.n
-            self.m2 += d * (x - self.mean)
+
+    def get_mean(self):
+        return 0.0 if self.n < 2 else self.mean
 
     def std(self):
         if self.n < 2:
             return 1.0
-        return math.sqrt(self.m2 / (self.n - 1))
+        var = self.m2 / (self.n - 1)
+        if var <= 0:
+            var = 1.0
+        return math.sqrt(var)
+
+    def to_json(self):  # WelfordStat::ToJSON
+        return {"mean": self.mean, "var": self.m2, "count": self.n}
+
+    def read_json(self, j):  # WelfordStat::ReadFromJSON
+        self.mean, self.m2, self.n = float(j["mean"]), float(j["var"]), int(j["count"])
 
 
 def batch_ranges(exp_size, batch_size, overbatching=True):
@@ -93,6 +107,10 @@ class LearnerConfig:
         self.critic_layers = (512, 512)
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
+        # checkpoints (LearnerConfig.h:31-38): None = no save / load
+        self.checkpoint_folder = None
+        self.ts_per_save = 10_000_000     # 0 = every iteration (Learner.cpp:44-45)
+        self.checkpoints_to_keep = 8      # -1 keeps all
         for k, v in kw.items():
             if not hasattr(self, k):
                 raise AttributeError(f"unknown LearnerConfig field {k}")
@@ -139,6 +157,19 @@ class Learner:
         self._rng_step = 0
         self.rng = np.random.default_rng(cfg.seed + 7919 * rank)
         self.env_events = None  # optional list collecting (start, end) events around env steps
+        self.last_checkpoint = None
+        if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-146)
+            from . import checkpoint as _ckpt
+            self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
+
+    def save(self):
+        """Learner::Save (rank 0 writes; every rank holds the same weights)."""
+        from . import checkpoint as _ckpt
+        if not self.cfg.checkpoint_folder:
+            raise ValueError("Learner.save: cfg.checkpoint_folder is not set")
+        if self.rank == 0:
+            self.last_checkpoint = _ckpt.save(self, self.cfg.checkpoint_folder, self.cfg.checkpoints_to_keep)
+        return self.last_checkpoint
 
     # ---------------------------------------------------------------- collection
     def collect(self):
@@ -213,6 +244,12 @@ class Learner:
         self.obs[0].copy_(self.obs[self.T])
         self.masks[0].copy_(self.masks[self.T])
         self.iteration += 1
+        prev = self.total_steps
         self.total_steps += self.T * self.P * self.world
         torch.cuda.synchronize(self.device)
-        return {"iteration_s": time.perf_counter() - t0}
+        rep = {"iteration_s": time.perf_counter() - t0}
+        if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)
+            per = self.cfg.ts_per_save or self.T * self.P * self.world
+            if self.total_steps // per > prev // per:
+                rep["checkpoint"] = self.save()
+        return rep

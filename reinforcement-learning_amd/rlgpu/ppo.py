@@ -57,6 +57,7 @@ def _bind():
     L.rlgpu_ppo_optimizer_step.argtypes = [vp, vp, vp]
     L.rlgpu_ppo_zero_grad.argtypes = [vp, vp]
     L.rlgpu_ppo_optimizer_state.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.rlgpu_ppo_set_optimizer_step.argtypes = [vp, i64]
     L.rlgpu_permutation.argtypes = [i64, u64, u64, vp, vp]
     _ = f32
     _bound = True
@@ -155,15 +156,7 @@ class PPO:
         import torch
         layers = self.policy_layers if model == 0 else self.critic_layers
         out = self.num_actions if model == 0 else 1
-        mods, prev = [], self.obs_size
-        for hdim in layers:
-            mods.append(torch.nn.Linear(prev, hdim))
-            if self.layer_norm:
-                mods.append(torch.nn.LayerNorm(hdim))
-            mods.append(torch.nn.LeakyReLU(self.leaky_slope))
-            prev = hdim
-        mods.append(torch.nn.Linear(prev, out))
-        seq = torch.nn.Sequential(*mods)
+        seq = make_sequential(self.obs_size, out, layers, self.layer_norm, self.leaky_slope)
         flat = self.model_slice(model).detach().cpu()
         o = 0
         with torch.no_grad():
@@ -249,6 +242,28 @@ class PPO:
                    "optimizer_state")
         return (step.value, alias(m.value, (self.num_params,), torch.float32, self.device),
                 alias(v.value, (self.num_params,), torch.float32, self.device))
+
+    def set_optimizer_step(self, step):
+        _lib.check(_lib.lib().rlgpu_ppo_set_optimizer_step(self._h, int(step)), "set_optimizer_step")
+
+    def model_sizes(self, model):
+        """Per-parameter element counts in torch order (GetSeqSizes, Models.cpp:79-87)."""
+        return [p.numel() for p in self.torch_module(model).parameters()]
+
+
+def make_sequential(obs_size, out, layers, layer_norm=True, leaky_slope=0.01):
+    """GGL::Model's module list (Models.cpp:7-33): per hidden layer Linear [, LayerNorm],
+    LeakyReLU; then the output Linear.  CPU, torch default init."""
+    import torch
+    mods, prev = [], obs_size
+    for hdim in layers:
+        mods.append(torch.nn.Linear(prev, hdim))
+        if layer_norm:
+            mods.append(torch.nn.LayerNorm(hdim))
+        mods.append(torch.nn.LeakyReLU(leaky_slope))
+        prev = hdim
+    mods.append(torch.nn.Linear(prev, out))
+    return torch.nn.Sequential(*mods)
 
 
 def permutation(n, seed, counter, out=None, device="cuda:0"):

@@ -1,0 +1,112 @@
+"""Checkpoint format compatibility (rlgpu/checkpoint.py).  CPU only.
+
+Anchor: libtorch itself.  tools/lt_load_check.cpp restates GGL::Model's Sequential and loads our
+<NAME>.lt with torch::load(seq, stream) exactly as Model::Load does (Models.cpp:130-166); it also
+writes a module with torch::save(seq, stream) (Model::Save, Models.cpp:116-120) for the reverse
+direction.  The harness is compiled here against the installed libtorch (skipped if that fails).
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from rlgpu import checkpoint as ckpt
+from rlgpu.learner import WelfordStat
+from rlgpu.ppo import make_sequential
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    import torch.utils.cpp_extension as ext
+    out = tmp_path_factory.mktemp("lt") / "lt_load_check"
+    inc = sum([["-I", p] for p in ext.include_paths()], [])
+    libs = ext.library_paths()
+    cmd = ["g++", "-std=c++17", "-O1", os.path.join(ROOT, "tools", "lt_load_check.cpp"), *inc,
+           "-L" + libs[0], "-ltorch", "-ltorch_cpu", "-lc10", "-Wl,-rpath," + libs[0], "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        pytest.skip("cannot build the libtorch harness: " + r.stderr[-400:])
+    return str(out)
+
+
+ARCH = dict(obs=167, out=90, ln=1, layers=(64, 48))
+
+
+def _args():
+    return [str(ARCH["obs"]), str(ARCH["out"]), str(ARCH["ln"])] + [str(h) for h in ARCH["layers"]]
+
+
+def test_model_file_loads_in_libtorch(harness, tmp_path):
+    import torch
+    torch.manual_seed(3)
+    seq = make_sequential(ARCH["obs"], ARCH["out"], ARCH["layers"], True)
+    with torch.no_grad():  # non-trivial LayerNorm affine parameters
+        for m in seq:
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    p = str(tmp_path / "POLICY.lt")
+    ckpt.write_model(seq, p)
+    x = np.random.default_rng(0).standard_normal((7, ARCH["obs"])).astype(np.float32)
+    x.tofile(tmp_path / "x.f32")
+    r = subprocess.run([harness, "load", p, str(tmp_path / "x.f32"), "7", str(tmp_path / "y.f32"), *_args()],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    y = np.fromfile(tmp_path / "y.f32", np.float32).reshape(7, ARCH["out"])
+    with torch.no_grad():
+        want = seq(torch.from_numpy(x)).numpy()
+    np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6)
+
+
+def test_libtorch_written_model_loads_here(harness, tmp_path):
+    import torch
+    n = sum(p.numel() for p in make_sequential(ARCH["obs"], ARCH["out"], ARCH["layers"], True).parameters())
+    flat = np.random.default_rng(1).standard_normal(n).astype(np.float32)
+    flat.tofile(tmp_path / "p.f32")
+    p = str(tmp_path / "CRITIC.lt")
+    r = subprocess.run([harness, "save", str(tmp_path / "p.f32"), p, *_args()], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    got = torch.cat([t.reshape(-1) for t in ckpt.read_model_state(p)]).numpy()
+    np.testing.assert_array_equal(got, flat)
+
+
+def test_size_mismatch_is_refused(harness, tmp_path):
+    seq = make_sequential(ARCH["obs"], ARCH["out"], (32, 48), True)
+    p = str(tmp_path / "POLICY.lt")
+    ckpt.write_model(seq, p)
+    np.zeros((1, ARCH["obs"]), np.float32).tofile(tmp_path / "x.f32")
+    r = subprocess.run([harness, "load", p, str(tmp_path / "x.f32"), "1", str(tmp_path / "y.f32"), *_args()],
+                       capture_output=True, text=True)
+    assert r.returncode != 0
+
+
+def test_numbered_dirs_and_paths(tmp_path):
+    for n in ("100", "2000", "abc", "12x"):
+        (tmp_path / n).mkdir()
+    (tmp_path / "300").write_text("file, not a dir")
+    assert ckpt.numbered_dirs(str(tmp_path)) == {100, 2000}
+    assert ckpt.numbered_dirs(str(tmp_path / "missing")) == set()
+    assert ckpt.model_path("d", "policy") == os.path.join("d", "POLICY.lt")
+    assert ckpt.model_path("d", "critic", "_optim") == os.path.join("d", "CRITIC_OPTIM.lt")
+
+
+def test_welford_stat_reference_rules():
+    w = WelfordStat()
+    assert w.std() == 1.0 and w.get_mean() == 0.0
+    w.add([3.0])
+    assert w.std() == 1.0  # count < 2
+    w.add([3.0])
+    assert w.std() == 1.0  # variance 0 -> 1 (WelfordStat.h:43-47)
+    xs = np.random.default_rng(0).standard_normal(500).astype(np.float32)
+    v = WelfordStat()
+    v.add(xs)
+    assert abs(v.std() - np.std(xs.astype(np.float64), ddof=1)) < 1e-9
+    j = json.loads(json.dumps(v.to_json()))
+    assert set(j) == {"mean", "var", "count"}
+    u = WelfordStat()
+    u.read_json(j)
+    assert (u.n, u.mean, u.m2) == (v.n, v.mean, v.m2)

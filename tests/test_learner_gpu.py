@@ -79,3 +79,40 @@ def test_learn_updates_parameters(gpu):
     # a second iteration starts from the last obs of the first
     L.iterate()
     assert torch.isfinite(L.ppo.flat()).all()
+
+
+def test_checkpoint_save_load_roundtrip(gpu, tmp_path):
+    """Learner::Save / Load (Learner.cpp:224-279) in the reference layout: numbered directories,
+    RUNNING_STATS.json, POLICY.lt / CRITIC.lt, pruning to checkpointsToKeep; a new Learner resumes
+    with identical parameters, AdamW moments and step, and return statistics."""
+    import json
+    import os
+
+    import torch
+    folder = str(tmp_path / "ckpt")
+    L = _learner(gpu, checkpoint_folder=folder, ts_per_save=0, checkpoints_to_keep=2)
+    assert L.last_checkpoint is None  # nothing to load yet
+    for _ in range(3):
+        rep = L.iterate()
+        assert "checkpoint" in rep
+    dirs = sorted(int(d) for d in os.listdir(folder))
+    per = L.T * L.P
+    assert dirs == [2 * per, 3 * per]  # the oldest one was pruned
+    with open(os.path.join(folder, str(3 * per), "RUNNING_STATS.json")) as f:
+        j = json.load(f)
+    assert j["total_timesteps"] == 3 * per and j["total_iterations"] == 3
+    assert set(j["return_stat"]) == {"mean", "var", "count"}
+    assert os.path.exists(os.path.join(folder, str(3 * per), "POLICY.lt"))
+    L2 = _learner(gpu, checkpoint_folder=folder, ts_per_save=0)
+    assert L2.total_steps == L.total_steps and L2.iteration == 3
+    assert (L2.return_stat.n, L2.return_stat.mean, L2.return_stat.m2) == (L.return_stat.n, L.return_stat.mean,
+                                                                          L.return_stat.m2)
+    assert torch.equal(L2.ppo.flat(), L.ppo.flat())
+    s1, m1, v1 = L.ppo.optimizer_state()
+    s2, m2, v2 = L2.ppo.optimizer_state()
+    assert s1 == s2 and s1 > 0
+    for mi in range(2):
+        o, c = L.ppo.model_range(mi)
+        assert torch.equal(m1[o:o + c], m2[o:o + c]) and torch.equal(v1[o:o + c], v2[o:o + c])
+    x = L.obs[0][:64].contiguous()
+    assert torch.equal(L.ppo.forward(0, x), L2.ppo.forward(0, x))
