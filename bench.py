@@ -100,7 +100,9 @@ def main():
 
     from rlgpu.env import arena_state_size
     from rlgpu.learner import Learner, LearnerConfig
-    cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout)
+    # self-play iterations (15 % chance, LearnerConfig.h:67-68) are off so every timed iteration has
+    # the same work; the mixed-policy path is covered by tests/test_learner_gpu.py
+    cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False)
     L = Learner(cfg, device=dev, rank=rank, world=world)
 
     for _ in range(args.warmup):

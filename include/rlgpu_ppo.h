@@ -87,6 +87,16 @@ int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision, const floa
 int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n,
                             int32_t deterministic, uint64_t rng_step, int32_t* d_actions, float* d_logp,
                             void* stream);
+/* Self-play against an old policy version (LearnerConfig trainAgainstOldVersions,
+ * Learner.cpp:587-627,733-767; versions kept by PolicyVersionManager, PolicyVersionManager.cpp:38-62).
+ * set_version: bf16 inference copy of a policy given as its flat fp32 parameters (torch order,
+ * the policy's rlgpu_ppo_model_range count).  infer_actions_mixed: rows with d_old_rows[i] != 0
+ * act with that version (no log-prob written), the others with the current policy (as
+ * rlgpu_ppo_infer_actions). */
+int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stream);
+int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n,
+                                  int32_t deterministic, uint64_t rng_step, const uint8_t* d_old_rows,
+                                  int32_t* d_actions, float* d_logp, void* stream);
 /* InferCriticBatched: bf16 critic forward over n rows (any n; chunked by max_rows). */
 int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t n, float* d_values, void* stream);
 

@@ -42,6 +42,8 @@ struct rlgpu_ppo {
     int64_t nparams = 0, nhalf = 0;
     float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr;
     uint16_t* half = nullptr;
+    uint16_t* half_ver = nullptr;  // bf16 policy copy of an old version (self-play), same layout as half
+    bool has_ver = false;
     int64_t step = 0;
     int hmax = 0;
     float *scratch = nullptr;  // clip partials + coefficients
@@ -239,9 +241,9 @@ void gather_obs(rlgpu_ppo* h, const float* obs, const int32_t* idx, int64_t star
 
 // bf16 inference forward of n rows; result in h->logits_h [n, out] (bf16).  Model::Forward with
 // halfPrec (Models.cpp:42-68): every module runs on the bf16 copy, activations rounded to bf16.
-void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s) {
+void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, const uint16_t* weights = nullptr) {
     Model& m = h->M[mi];
-    const uint16_t* P = h->half;
+    const uint16_t* P = weights ? weights : h->half;
     int nh = (int)m.L.size() - 1;
     {
         int64_t e = (int64_t)n * h->xh_ld;
@@ -329,17 +331,23 @@ void sumsq_coef(rlgpu_ppo* h, const float* x, int64_t n, float max_norm, float* 
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
-void refresh_half(rlgpu_ppo* h, hipStream_t s) {
-    for (auto& m : h->M)
-        for (auto& L : m.L) {
-            int64_t e = (int64_t)L.out * L.in_pad;
-            hipLaunchKernelGGL(mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->params + L.w, L.out, L.in,
-                               h->half + L.hw, L.in_pad);
-            int nv = L.g >= 0 ? 3 * L.out : L.out;  // bias | LN weight | LN bias, contiguous in both layouts
-            hipLaunchKernelGGL(ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, h->params + L.b, h->half + L.hb,
-                               (int64_t)nv);
-        }
+// bf16 inference copy of model mi from `src` (the model's flat fp32 parameters, torch order) into
+// the padded layout at `dst` (h->half or h->half_ver)
+void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, hipStream_t s) {
+    const Model& m = h->M[mi];
+    for (auto& L : m.L) {
+        int64_t e = (int64_t)L.out * L.in_pad;
+        hipLaunchKernelGGL(mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, src + (L.w - m.off), L.out, L.in,
+                           dst + L.hw, L.in_pad);
+        int nv = L.g >= 0 ? 3 * L.out : L.out;  // bias | LN weight | LN bias, contiguous in both layouts
+        hipLaunchKernelGGL(ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, src + (L.b - m.off), dst + L.hb,
+                           (int64_t)nv);
+    }
     RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+void refresh_half(rlgpu_ppo* h, hipStream_t s) {
+    for (int mi = 0; mi < 2; mi++) half_from(h, mi, h->params + h->M[mi].off, h->half, s);
 }
 
 }  // namespace
@@ -369,6 +377,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             h->exp_avg = h->alloc<float>(P);
             h->exp_avg_sq = h->alloc<float>(P);
             h->half = h->alloc<uint16_t>(h->nhalf + 8);
+            h->half_ver = h->alloc<uint16_t>(h->nhalf + 8);
             RLGPU_CHECK_HIP(hipMemset(h->params, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->grads, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->exp_avg, 0, P * 4));
@@ -513,6 +522,36 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
                                d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
                                rng_step, d_actions + b, d_logp ? d_logp + b : nullptr);
             RLGPU_CHECK_HIP(hipGetLastError());
+        }
+    });
+}
+
+extern "C" int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_policy_params, "rlgpu_ppo_set_version: null argument");
+        half_from(h, 0, d_policy_params, h->half_ver, rlgpu::as_stream(stream));
+        h->has_ver = true;
+    });
+}
+
+extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n,
+                                             int32_t deterministic, uint64_t rng_step, const uint8_t* d_old_rows,
+                                             int32_t* d_actions, float* d_logp, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_obs && d_masks && d_actions && d_old_rows, "null argument");
+        RLGPU_REQUIRE(h->has_ver, "rlgpu_ppo_infer_actions_mixed: no version set (rlgpu_ppo_set_version)");
+        RLGPU_REQUIRE(n >= 0, "n must be >= 0");
+        hipStream_t s = rlgpu::as_stream(stream);
+        int R = h->cfg.max_rows;
+        for (int64_t b = 0; b < n; b += R) {
+            int m = (int)std::min<int64_t>(R, n - b);
+            for (int old = 0; old < 2; old++) {  // current policy rows, then the old version's rows
+                forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s, old ? h->half_ver : h->half);
+                hipLaunchKernelGGL(ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
+                                   d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
+                                   rng_step, d_actions + b, (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
+                RLGPU_CHECK_HIP(hipGetLastError());
+            }
         }
     });
 }

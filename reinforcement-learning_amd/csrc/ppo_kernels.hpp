@@ -46,11 +46,13 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 
 // InferActions: logits bf16 [n, A] -> action (int32), log prob.  Inverse-CDF multinomial on the
 // clamped probs (torch.multinomial normalises by their sum); argmax when deterministic.
+// row_sel (optional): only rows with (row_sel[row] != 0) == sel are written (mixed-policy inference).
 __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
                                                      int deterministic, uint64_t seed, uint64_t step, int32_t* act,
-                                                     float* logp) {
+                                                     float* logp, const uint8_t* row_sel = nullptr, int sel = 0) {
     int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= n) return;
+    if (row_sel && ((row_sel[row] != 0) != (sel != 0))) return;
     int a0 = 2 * lane, a1 = 2 * lane + 1;
     const uint16_t* lg = logits + (int64_t)row * A;
     const uint8_t* mk = masks + (int64_t)row * A;

@@ -111,6 +111,11 @@ class LearnerConfig:
         self.checkpoint_folder = None
         self.ts_per_save = 10_000_000     # 0 = every iteration (Learner.cpp:44-45)
         self.checkpoints_to_keep = 8      # -1 keeps all
+        # self-play against old policy versions (LearnerConfig.h:62-68)
+        self.train_against_old_versions = True
+        self.train_against_old_chance = 0.15
+        self.ts_per_version = 25_000_000
+        self.max_old_versions = 32
         for k, v in kw.items():
             if not hasattr(self, k):
                 raise AttributeError(f"unknown LearnerConfig field {k}")
@@ -157,10 +162,25 @@ class Learner:
         self._rng_step = 0
         self.rng = np.random.default_rng(cfg.seed + 7919 * rank)
         self.env_events = None  # optional list collecting (start, end) events around env steps
+        # self-play: the manager of old versions, this iteration's version and team (None = all
+        # players use the current policy); the draw is rank-independent so every rank agrees
+        self.versions = None
+        self.old_version, self.old_team = None, 0
+        self._vrng = np.random.default_rng(cfg.seed + 104729)
+        if cfg.train_against_old_versions:
+            from .versions import PolicyVersionManager
+            import os
+            vf = os.path.join(cfg.checkpoint_folder, "policy_versions") if cfg.checkpoint_folder else None
+            self.versions = PolicyVersionManager(self.ppo, vf, cfg.max_old_versions, cfg.ts_per_version)
+        # old-version player rows: team of player p is p % 2 (cars 0, 2 blue; 1, 3 orange)
+        team = torch.arange(P, device=d) % 2
+        self._old_rows = [(team == k).to(torch.uint8) for k in range(2)]
         self.last_checkpoint = None
-        if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-146)
+        if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-153)
             from . import checkpoint as _ckpt
             self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
+            if self.versions is not None:
+                self.versions.load_versions(self.total_steps)
 
     def save(self):
         """Learner::Save (rank 0 writes; every rank holds the same weights)."""
@@ -169,6 +189,8 @@ class Learner:
             raise ValueError("Learner.save: cfg.checkpoint_folder is not set")
         if self.rank == 0:
             self.last_checkpoint = _ckpt.save(self, self.cfg.checkpoint_folder, self.cfg.checkpoints_to_keep)
+            if self.versions is not None:
+                self.versions.save_versions()
         return self.last_checkpoint
 
     # ---------------------------------------------------------------- collection
@@ -177,8 +199,13 @@ class Learner:
         import torch
         ppo, env = self.ppo, self.env
         for t in range(self.T):
-            ppo.infer_actions(self.obs[t], self.masks[t], step=self._rng_step, deterministic=self.cfg.deterministic,
-                              actions=self.actions[t], logp=self.logp[t])
+            if self.old_version is None:
+                ppo.infer_actions(self.obs[t], self.masks[t], step=self._rng_step, deterministic=self.cfg.deterministic,
+                                  actions=self.actions[t], logp=self.logp[t])
+            else:  # one team plays the old version (Learner.cpp:733-767)
+                ppo.infer_actions_mixed(self.obs[t], self.masks[t], self._old_rows[self.old_team], step=self._rng_step,
+                                        deterministic=self.cfg.deterministic, actions=self.actions[t],
+                                        logp=self.logp[t])
             self._rng_step += 1
             if self.env_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -203,14 +230,26 @@ class Learner:
                                  adv=self.adv, target=self.target, ret=self.ret)
         # return-std Welford over randomly sampled returns (Learner.cpp:959-967)
         k = self.cfg.return_samples
-        idx = torch.from_numpy(self.rng.integers(0, T * P, size=k)).to(self.device)
+        if self.old_version is None:
+            idx = torch.from_numpy(self.rng.integers(0, T * P, size=k)).to(self.device)
+        else:  # only the current policy's players have trajectories
+            idx = self._train_rows()[torch.from_numpy(self.rng.integers(0, T * P // 2, size=k)).to(self.device)]
         samples = _dist.gather_samples(self.ret.view(-1)[idx], self.group)
         self.return_stat.add(samples.cpu().numpy())
+
+    def _train_rows(self):
+        """Sample indices (t * P + p) of the players on the current policy in an old-version iteration."""
+        import torch
+        new_team = 1 - self.old_team
+        p = torch.arange(new_team, self.P, 2, device=self.device)
+        t = torch.arange(self.T, device=self.device)
+        return (t[:, None] * self.P + p[None, :]).reshape(-1).to(torch.int32)
 
     # ---------------------------------------------------------------- learning
     def learn(self):
         cfg, ppo = self.cfg, self.ppo
-        M = self.T * self.P
+        rows = None if self.old_version is None else self._train_rows()
+        M = self.T * self.P if rows is None else rows.numel()
         global_m = M * self.world
         batch = global_m if cfg.batch_size is None else cfg.batch_size
         obs = self.obs[:self.T].reshape(-1, OBS)
@@ -220,9 +259,12 @@ class Learner:
         local_batch = M if cfg.batch_size is None else max(1, cfg.batch_size // self.world)
         for epoch in range(cfg.epochs):
             perm = permutation(M, cfg.seed + self.rank, self.iteration * cfg.epochs + epoch, device=self.device)
+            if rows is not None:
+                perm = rows[perm.long()]
             for b0, b1 in batch_ranges(M, local_batch, cfg.overbatching):
                 # batch advantage normalisation (PPOLearner.cpp:360-371), global over ranks
-                badv = adv if (b0, b1) == (0, M) else adv.index_select(0, perm[b0:b1].long())
+                whole = rows is None and (b0, b1) == (0, M)
+                badv = adv if whole else adv.index_select(0, perm[b0:b1].long())
                 if self.world > 1:
                     ppo.adv_stats.copy_(_dist.global_mean_std(badv, self.group))
                 else:
@@ -237,6 +279,12 @@ class Learner:
         """One PPO iteration (collect T steps, consume, learn); returns a report dict."""
         import torch
         t0 = time.perf_counter()
+        self.old_version = None
+        if self.versions is not None and self.versions.versions:  # Learner.cpp:587-627
+            if self._vrng.random() < self.cfg.train_against_old_chance:
+                self.old_version = self.versions.versions[int(self._vrng.integers(0, len(self.versions.versions)))]
+                self.old_team = int(self._vrng.integers(0, 2))
+                self.ppo.set_version(self.old_version.params)
         self.collect()
         self.consume()
         self.learn()
@@ -245,9 +293,13 @@ class Learner:
         self.masks[0].copy_(self.masks[self.T])
         self.iteration += 1
         prev = self.total_steps
-        self.total_steps += self.T * self.P * self.world
+        real_players = self.P if self.old_version is None else self.P // 2  # numRealPlayers (Learner.cpp:629)
+        self.total_steps += self.T * real_players * self.world
+        if self.versions is not None:
+            self.versions.on_iteration(self.total_steps, prev)
         torch.cuda.synchronize(self.device)
-        rep = {"iteration_s": time.perf_counter() - t0}
+        rep = {"iteration_s": time.perf_counter() - t0, "old_version": None if self.old_version is None
+               else (self.old_version.timesteps, self.old_team)}
         if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)
             per = self.cfg.ts_per_save or self.T * self.P * self.world
             if self.total_steps // per > prev // per:

@@ -58,6 +58,8 @@ def _bind():
     L.rlgpu_ppo_zero_grad.argtypes = [vp, vp]
     L.rlgpu_ppo_optimizer_state.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(vp), ctypes.POINTER(vp)]
     L.rlgpu_ppo_set_optimizer_step.argtypes = [vp, i64]
+    L.rlgpu_ppo_set_version.argtypes = [vp, vp, vp]
+    L.rlgpu_ppo_infer_actions_mixed.argtypes = [vp, vp, vp, i32, i32, u64, vp, vp, vp, vp]
     L.rlgpu_permutation.argtypes = [i64, u64, u64, vp, vp]
     _ = f32
     _bound = True
@@ -191,6 +193,25 @@ class PPO:
         _lib.check(_lib.lib().rlgpu_ppo_infer_actions(self._h, _lib.ptr(obs), _lib.ptr(masks), n, int(deterministic),
                                                       step, _lib.ptr(actions), _lib.ptr(logp), _lib.stream_ptr()),
                    "rlgpu_ppo_infer_actions")
+        return actions, logp
+
+    def set_version(self, policy_params):
+        """bf16 inference copy of an old policy version (flat fp32 policy parameters on the device)."""
+        _, cnt = self.model_range(0)
+        if policy_params.numel() != cnt:
+            raise _lib.RLGPUError("policy version has the wrong parameter count")
+        _lib.check(_lib.lib().rlgpu_ppo_set_version(self._h, _lib.ptr(policy_params.contiguous()), _lib.stream_ptr()),
+                   "rlgpu_ppo_set_version")
+
+    def infer_actions_mixed(self, obs, masks, old_rows, step=0, deterministic=False, actions=None, logp=None):
+        """Rows with old_rows != 0 act with the version of set_version (their logp is not written)."""
+        import torch
+        n = obs.shape[0]
+        actions = torch.empty(n, dtype=torch.int32, device=self.device) if actions is None else actions
+        logp = torch.empty(n, device=self.device) if logp is None else logp
+        _lib.check(_lib.lib().rlgpu_ppo_infer_actions_mixed(self._h, _lib.ptr(obs), _lib.ptr(masks), n, int(deterministic),
+                                                            step, _lib.ptr(old_rows), _lib.ptr(actions), _lib.ptr(logp),
+                                                            _lib.stream_ptr()), "rlgpu_ppo_infer_actions_mixed")
         return actions, logp
 
     def infer_critic(self, obs, out=None):

@@ -1,0 +1,102 @@
+"""Old policy versions for self-play -- Python mirror of GGL::PolicyVersionManager.
+
+Reference map:
+    PolicyVersionManager::AddVersion      PolicyVersionManager.cpp:38-62 (clone, sort by timesteps,
+                                          drop the oldest beyond maxVersions)
+    PolicyVersionManager::OnIteration     PolicyVersionManager.cpp:302-315 (a version every
+                                          tsPerVersion timesteps, and after the first iteration)
+    PolicyVersionManager::SaveVersions    PolicyVersionManager.cpp:64-104 (<checkpoint>/policy_versions/
+                                          <timesteps>/POLICY.lt + STATS.json, stale dirs removed)
+    PolicyVersionManager::LoadVersions    PolicyVersionManager.cpp:106-144 (refuses versions newer than
+                                          the current model)
+    LearnerConfig                         LearnerConfig.h:62-68 (tsPerVersion 25M, maxOldVersions 32,
+                                          trainAgainstOldVersions, trainAgainstOldChance 0.15)
+
+Versions are the policy's flat fp32 parameters kept in HBM (1.6 MB each at [512, 512]); the active
+one is converted once per iteration into the PPO handle's second bf16 inference copy
+(rlgpu_ppo_set_version) and used by the mixed-policy inference of the Learner.  The skill/ELO
+tracker is not part of this tier (SURVEY.md 8f-3 lists it as optional); STATS.json carries an
+empty "skill_ratings" object so the reference's loader accepts the directories.
+"""
+import json
+import os
+import shutil
+
+from . import checkpoint as _ckpt
+
+
+class PolicyVersion:
+    def __init__(self, timesteps, params, ratings=None):
+        self.timesteps = int(timesteps)
+        self.params = params            # device tensor, flat fp32 policy parameters
+        self.ratings = dict(ratings or {})
+
+
+class PolicyVersionManager:
+    def __init__(self, ppo, save_folder=None, max_versions=32, ts_per_version=25_000_000):
+        self.ppo = ppo
+        self.save_folder = save_folder
+        self.max_versions = max_versions
+        self.ts_per_version = ts_per_version
+        self.versions = []
+        if save_folder:
+            os.makedirs(save_folder, exist_ok=True)
+
+    def add_version(self, timesteps, params=None):
+        """AddVersion: a copy of the current policy (or of `params`)."""
+        src = self.ppo.model_slice(0) if params is None else params
+        v = PolicyVersion(timesteps, src.detach().clone())
+        self.versions.append(v)
+        self.versions.sort(key=lambda x: x.timesteps)
+        while len(self.versions) > self.max_versions:
+            self.versions.pop(0)
+        return v
+
+    def on_iteration(self, total_timesteps, prev_timesteps):
+        if total_timesteps // self.ts_per_version > prev_timesteps // self.ts_per_version or prev_timesteps == 0:
+            self.add_version(total_timesteps)
+
+    def save_versions(self):
+        if not self.save_folder:
+            return
+        keep = {v.timesteps for v in self.versions}
+        saved = _ckpt.numbered_dirs(self.save_folder)
+        for ts in saved - keep:
+            shutil.rmtree(os.path.join(self.save_folder, str(ts)))
+        for v in self.versions:
+            if v.timesteps in saved:
+                continue
+            d = os.path.join(self.save_folder, str(v.timesteps))
+            os.makedirs(d, exist_ok=True)
+            seq = self.ppo.torch_module(0)
+            o = 0
+            import torch
+            flat = v.params.detach().cpu()
+            with torch.no_grad():
+                for p in seq.parameters():
+                    p.copy_(flat[o:o + p.numel()].view_as(p))
+                    o += p.numel()
+            _ckpt.write_model(seq, _ckpt.model_path(d, "policy"))
+            with open(os.path.join(d, "STATS.json"), "w") as f:
+                json.dump({"skill_ratings": v.ratings}, f, indent=4)
+
+    def load_versions(self, cur_timesteps):
+        import torch
+        self.versions = []
+        if not self.save_folder:
+            return
+        want = self.ppo.model_sizes(0)
+        for ts in sorted(_ckpt.numbered_dirs(self.save_folder)):
+            if ts > cur_timesteps:
+                raise ValueError(f"Tried to load saved policy version that is newer than our current model "
+                                 f"({ts} > {cur_timesteps})")
+            d = os.path.join(self.save_folder, str(ts))
+            tensors = _ckpt.read_model_state(_ckpt.model_path(d, "policy"))
+            if [t.numel() for t in tensors] != want:
+                raise ValueError(f"saved policy version in {d} has a different size than the current model")
+            flat = torch.cat([t.reshape(-1) for t in tensors]).to(self.ppo.params.device)
+            v = self.add_version(ts, flat)
+            p = os.path.join(d, "STATS.json")
+            if os.path.exists(p):
+                with open(p) as f:
+                    v.ratings = json.load(f).get("skill_ratings", {})

@@ -90,12 +90,12 @@ def test_checkpoint_save_load_roundtrip(gpu, tmp_path):
 
     import torch
     folder = str(tmp_path / "ckpt")
-    L = _learner(gpu, checkpoint_folder=folder, ts_per_save=0, checkpoints_to_keep=2)
+    L = _learner(gpu, checkpoint_folder=folder, ts_per_save=0, checkpoints_to_keep=2, train_against_old_versions=False)
     assert L.last_checkpoint is None  # nothing to load yet
     for _ in range(3):
         rep = L.iterate()
         assert "checkpoint" in rep
-    dirs = sorted(int(d) for d in os.listdir(folder))
+    dirs = sorted(int(d) for d in os.listdir(folder) if d.isdigit())
     per = L.T * L.P
     assert dirs == [2 * per, 3 * per]  # the oldest one was pruned
     with open(os.path.join(folder, str(3 * per), "RUNNING_STATS.json")) as f:
@@ -103,7 +103,7 @@ def test_checkpoint_save_load_roundtrip(gpu, tmp_path):
     assert j["total_timesteps"] == 3 * per and j["total_iterations"] == 3
     assert set(j["return_stat"]) == {"mean", "var", "count"}
     assert os.path.exists(os.path.join(folder, str(3 * per), "POLICY.lt"))
-    L2 = _learner(gpu, checkpoint_folder=folder, ts_per_save=0)
+    L2 = _learner(gpu, checkpoint_folder=folder, ts_per_save=0, train_against_old_versions=False)
     assert L2.total_steps == L.total_steps and L2.iteration == 3
     assert (L2.return_stat.n, L2.return_stat.mean, L2.return_stat.m2) == (L.return_stat.n, L.return_stat.mean,
                                                                           L.return_stat.m2)
@@ -116,3 +116,53 @@ def test_checkpoint_save_load_roundtrip(gpu, tmp_path):
         assert torch.equal(m1[o:o + c], m2[o:o + c]) and torch.equal(v1[o:o + c], v2[o:o + c])
     x = L.obs[0][:64].contiguous()
     assert torch.equal(L.ppo.forward(0, x), L2.ppo.forward(0, x))
+
+
+def test_self_play_old_version(gpu, tmp_path):
+    """trainAgainstOldVersions (Learner.cpp:587-627,733-767): one team acts with an old policy
+    version, only the other team's experience is trained and counted; versions are kept every
+    tsPerVersion and after the first iteration (PolicyVersionManager.cpp:302-306), saved under
+    policy_versions/<timesteps>/POLICY.lt and reloaded."""
+    import os
+
+    import torch
+    folder = str(tmp_path / "ck")
+    L = _learner(gpu, train_against_old_chance=1.0, checkpoint_folder=folder, ts_per_save=0)
+    rep = L.iterate()
+    assert rep["old_version"] is None and len(L.versions.versions) == 1  # added after the first iteration
+    v = L.versions.versions[0]
+    assert torch.equal(v.params, L.ppo.model_slice(0))
+    obs, masks = L.obs[0], L.masks[0]
+    # mixed inference with a version equal to the current policy == plain inference
+    L.ppo.set_version(v.params)
+    old_rows = L._old_rows[1]
+    a_mix, lp_mix = L.ppo.infer_actions_mixed(obs, masks, old_rows, step=77)
+    a_pl, lp_pl = L.ppo.infer_actions(obs, masks, step=77)
+    assert torch.equal(a_mix, a_pl)
+    new = old_rows == 0
+    assert torch.equal(lp_mix[new], lp_pl[new])
+    # a different version: old rows follow it, new rows the current policy
+    cur = L.ppo.model_slice(0).clone()
+    pert = cur + 0.05 * torch.randn_like(cur)
+    L.ppo.model_slice(0).copy_(pert)
+    L.ppo.refresh_half()
+    a_pert, _ = L.ppo.infer_actions(obs, masks, step=78)
+    L.ppo.model_slice(0).copy_(cur)
+    L.ppo.refresh_half()
+    a_cur, _ = L.ppo.infer_actions(obs, masks, step=78)
+    L.ppo.set_version(pert)
+    a_mix, _ = L.ppo.infer_actions_mixed(obs, masks, old_rows, step=78)
+    old = old_rows == 1
+    assert torch.equal(a_mix[old], a_pert[old]) and torch.equal(a_mix[new], a_cur[new])
+    assert not torch.equal(a_pert, a_cur)
+    # a full old-version iteration: half the players count
+    before = L.total_steps
+    rep = L.iterate()
+    assert rep["old_version"] is not None
+    assert L.total_steps - before == L.T * L.P // 2
+    assert torch.isfinite(L.ppo.flat()).all()
+    vdirs = os.listdir(os.path.join(folder, "policy_versions"))
+    assert len(vdirs) >= 1 and os.path.exists(os.path.join(folder, "policy_versions", vdirs[0], "POLICY.lt"))
+    L2 = _learner(gpu, checkpoint_folder=folder, ts_per_save=0)
+    assert [x.timesteps for x in L2.versions.versions] == [x.timesteps for x in L.versions.versions]
+    assert torch.equal(L2.versions.versions[0].params, L.versions.versions[0].params)
