@@ -201,6 +201,19 @@ __global__ void __launch_bounds__(256, RLGPU_GEMM_OCC) gemm_f32(GemmArgs g) {
         __syncthreads();
     }
     float* C = g.C + (int64_t)tl.z * g.c_split;
+    if (i0 + BM <= g.I && j0 + BN <= g.J) {  // interior tile: no bounds checks, one base pointer
+        float* cb = C + (int64_t)(i0 + wm * 64 + 4 * h) * g.ldc + j0 + wn * 64 + l32;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                const float bj = g.bias ? g.bias[j0 + wn * 64 + tj * 32 + l32] : 0.f;
+                float* ct = cb + (int64_t)(ti * 32) * g.ldc + tj * 32;
+#pragma unroll
+                for (int r = 0; r < 16; r++) ct[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = acc[ti][tj][r] + bj;
+            }
+        return;
+    }
 #pragma unroll
     for (int ti = 0; ti < 2; ti++)
 #pragma unroll
@@ -220,7 +233,9 @@ __global__ void __launch_bounds__(256, RLGPU_GEMM_OCC) gemm_f32(GemmArgs g) {
 // v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  A [I][lda] and W [J][ldb] bf16, k contiguous,
 // 16-byte aligned rows, K a multiple of 8 with zero padding (the padded inference copy of the
 // weights and the converted obs), so every staging load is one uint4 of 8 bf16 per thread.
-constexpr int HBK = 32, HPAD = 8;
+constexpr int HBK = 64, HPAD = 8;             // K per LDS stage: 16 MFMAs per wave between barriers
+constexpr int HCH = HBK / 8;                   // 16-byte chunks per tile row
+constexpr int HQ = BM * HCH / 256;             // uint4 per thread per operand tile
 
 struct HGemmArgs {
     const uint16_t* A;      // [I][lda] bf16
@@ -234,20 +249,21 @@ struct HGemmArgs {
 
 __device__ uint4 g_zero_u4[4];
 
-// 2 uint4 per thread: rows (t + 256q) >> 2, 8-element column chunk ((t + 256q) & 3) * 8
-DEV void htile_load(uint4 (&r)[2], const uint16_t* const (&rows)[2], int k0, int K) {
+// HQ 16-byte vectors per thread: row (t + 256q) / HCH, 8-element column chunk ((t + 256q) % HCH) * 8
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs
+DEV void htile_load(u32x4 (&r)[HQ], const uint16_t* const (&rows)[HQ], int k0, int K) {
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        int c = k0 + ((threadIdx.x + 256 * q) & 3) * 8;
+    for (int q = 0; q < HQ; q++) {
+        int c = k0 + ((threadIdx.x + 256 * q) % HCH) * 8;
         const uint16_t* p = (rows[q] && c < K) ? rows[q] + c : reinterpret_cast<const uint16_t*>(g_zero_u4);
-        r[q] = *reinterpret_cast<const uint4*>(p);
+        r[q] = *reinterpret_cast<const u32x4*>(p);
     }
 }
-DEV void htile_store(uint16_t (*lds)[HBK + HPAD], const uint4 (&r)[2]) {
+DEV void htile_store(uint16_t (*lds)[HBK + HPAD], const u32x4 (&r)[HQ]) {
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < HQ; q++) {
         int e = threadIdx.x + 256 * q;
-        *reinterpret_cast<uint4*>(&lds[e >> 2][(e & 3) * 8]) = r[q];
+        *reinterpret_cast<u32x4*>(&lds[e / HCH][(e % HCH) * 8]) = r[q];
     }
 }
 
@@ -258,11 +274,11 @@ __global__ void __launch_bounds__(256, 2) gemm_bf16(HGemmArgs g) {
     const int wm = w >> 1, wn = w & 1;
     const Tile tl = xcd_tile(g.gx, g.gy, 1);
     const int i0 = tl.y * BM, j0 = tl.x * BN;
-    const uint16_t* arow[2];
-    const uint16_t* brow[2];
+    const uint16_t* arow[HQ];
+    const uint16_t* brow[HQ];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        int rr = (t + 256 * q) >> 2;
+    for (int q = 0; q < HQ; q++) {
+        int rr = (t + 256 * q) / HCH;
         arow[q] = i0 + rr < g.I ? g.A + (int64_t)(i0 + rr) * g.lda : nullptr;
         brow[q] = j0 + rr < g.J ? g.B + (int64_t)(j0 + rr) * g.ldb : nullptr;
     }
@@ -270,7 +286,7 @@ __global__ void __launch_bounds__(256, 2) gemm_bf16(HGemmArgs g) {
     for (int a = 0; a < 2; a++)
         for (int b = 0; b < 2; b++)
             for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
-    uint4 ra[2], rb[2];
+    u32x4 ra[HQ], rb[HQ];
     htile_load(ra, arow, 0, g.K);
     htile_load(rb, brow, 0, g.K);
     for (int k0 = 0; k0 < g.K; k0 += HBK) {
@@ -461,34 +477,70 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const uint16_t* gamma, const uint16_t* beta, int R,
                                                       int H, float slope, int use_ln, uint16_t* out) {
-    int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (row >= R) return;
-    const uint16_t* z = Z + (int64_t)row * H;
-    float v[MAXH];
-    constexpr int nper = MAXH;
-    float s = 0.f;
-    for (int q = 0; q < nper; q++) {
-        int c = lane + 64 * q;
-        v[q] = c < H ? bf2f(z[c]) : 0.f;
-        s += v[q];
+    // lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (16-byte loads / stores of 8 bf16
+    // when H is a multiple of 8); gamma / beta in registers; each wave walks LNF_ROWS/4 rows
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c0 = lane * MAXH;
+    const bool vec = (H % 8 == 0) && (MAXH % 8 == 0) && (c0 + MAXH <= H);
+    float g[MAXH], b[MAXH];
+#pragma unroll
+    for (int q = 0; q < MAXH; q++) {
+        const int c = c0 + q;
+        g[q] = (use_ln && c < H) ? bf2f(gamma[c]) : 1.f;
+        b[q] = (use_ln && c < H) ? bf2f(beta[c]) : 0.f;
     }
-    uint16_t* o = out + (int64_t)row * H;
-    float mean = 0.f, rs = 1.f;
-    if (use_ln) {
-        mean = wave_sum(s) / (float)H;
-        float s2 = 0.f;
-        for (int q = 0; q < nper; q++) {
-            int c = lane + 64 * q;
-            float d = c < H ? v[q] - mean : 0.f;
-            s2 += d * d;
+    for (int i = 0; i < LNF_ROWS / 4; i++) {
+        const int row = blockIdx.x * LNF_ROWS + i * 4 + wv;
+        if (row >= R) break;
+        const uint16_t* z = Z + (int64_t)row * H + c0;
+        float v[MAXH];
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 8) {
+                u32x4 t = *reinterpret_cast<const u32x4*>(z + q);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    v[q + 2 * k] = __uint_as_float(t[k] << 16);
+                    v[q + 2 * k + 1] = __uint_as_float(t[k] & 0xffff0000u);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? bf2f(z[q]) : 0.f;
         }
-        rs = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
-    }
-    for (int q = 0; q < nper; q++) {
-        int c = lane + 64 * q;
-        if (c < H) {
-            float h = use_ln ? bf2f(f2bf((v[q] - mean) * rs * bf2f(gamma[c]) + bf2f(beta[c]))) : v[q];
-            o[c] = f2bf(h > 0.f ? h : h * slope);
+        float mean = 0.f, rs = 1.f;
+        if (use_ln) {
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) s += v[q];
+            mean = wave_sum(s) / (float)H;
+            float s2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) {
+                float d = c0 + q < H ? v[q] - mean : 0.f;
+                s2 += d * d;
+            }
+            rs = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
+        }
+        uint16_t o[MAXH];
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) {
+            float hv = use_ln ? bf2f(f2bf((v[q] - mean) * rs * g[q] + b[q])) : v[q];
+            o[q] = f2bf(hv > 0.f ? hv : hv * slope);
+        }
+        uint16_t* op = out + (int64_t)row * H + c0;
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q += 8) {
+                u32x4 t;
+#pragma unroll
+                for (int k = 0; k < 4; k++) t[k] = (uint32_t)o[q + 2 * k] | ((uint32_t)o[q + 2 * k + 1] << 16);
+                *reinterpret_cast<u32x4*>(op + q) = t;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++)
+                if (c0 + q < H) op[q] = o[q];
         }
     }
 }

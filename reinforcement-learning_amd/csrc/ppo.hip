@@ -32,7 +32,10 @@ struct Model {
     float *y = nullptr, *dy = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr, *mid = nullptr;  // y: model output
 };
 
-constexpr int kMaxSplits = 64;
+constexpr int kMaxSplits = 256;
+// concurrent gemm_f32 workgroups on the device (CUs x RLGPU_GEMM_OCC), set at create: the split-K
+// weight gradients are sized to fill whole rounds of workgroups
+int g_gemm_slots = 256 * RLGPU_GEMM_OCC;
 
 }  // namespace
 
@@ -112,15 +115,21 @@ void gemm_f32(int la, int lb, const float* A, int64_t lda, const float* B, int64
     throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "gemm layout");
 }
 
-int splits_for(int rows) {
-    int s = (int)ceil_div(rows, 1024);
-    return s < 1 ? 1 : (s > kMaxSplits ? kMaxSplits : s);
+// split-K count of a weight gradient [out, in] over `rows`: one full round of workgroups
+// (tiles x splits ~ g_gemm_slots), each split at least 4 K steps
+int splits_for(int rows, int out, int in) {
+    const int tiles = (int)(ceil_div(out, mlp::BM) * ceil_div(in, mlp::BN));
+    int s = g_gemm_slots / tiles;
+    const int maxs = rows / (4 * mlp::BK);
+    if (s > maxs) s = maxs;
+    if (s > kMaxSplits) s = kMaxSplits;
+    return s < 1 ? 1 : s;
 }
 
 // dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
 void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
                  bool x_tail_ok = false) {
-    int splits = splits_for(n);
+    int splits = splits_for(n, out, in);
     int chunk = (int)ceil_div(ceil_div(n, splits), mlp::BK) * mlp::BK;
     int z = (int)ceil_div(n, chunk);
     gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
@@ -273,7 +282,7 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, co
         if (l == nh) break;
         const uint16_t* gg = L.hg >= 0 ? P + L.hg : nullptr;
         const uint16_t* bb = L.hbe >= 0 ? P + L.hbe : nullptr;
-        hipLaunchKernelGGL(mlp::ln_act_fwd_bf16_any(L.out), dim3(ceil_div(n, 4)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
+        hipLaunchKernelGGL(mlp::ln_act_fwd_bf16_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, h->ah[cur]);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = h->ah[cur];
@@ -392,16 +401,29 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             }
             int H = h->hmax;
             int omax = cfg->num_actions > 1 ? cfg->num_actions : 1;
-            int64_t wmax = 0;
+            int64_t wmax = 0, wpart_max = 0;
+            {
+                int dev = 0, cus = 256;
+                if (hipGetDevice(&dev) == hipSuccess) {
+                    hipDeviceProp_t prop;
+                    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+                        cus = prop.multiProcessorCount;
+                }
+                g_gemm_slots = cus * RLGPU_GEMM_OCC;
+            }
             for (auto& m : h->M)
-                for (auto& L : m.L) wmax = std::max<int64_t>(wmax, (int64_t)L.in * L.out);
+                for (auto& L : m.L) {
+                    wmax = std::max<int64_t>(wmax, (int64_t)L.in * L.out);
+                    // splits_for is non-decreasing in the row count, and z = ceil(n / chunk) <= splits
+                    wpart_max = std::max<int64_t>(wpart_max, (int64_t)splits_for((int)R, L.out, L.in) * L.in * L.out);
+                }
             int64_t nb = ceil_div(R, std::min(mlp::LNB_ROWS, mlp::CS_ROWS));
             for (auto& m : h->M) {
                 m.y = h->alloc<float>(R * omax);
                 m.dy = h->alloc<float>(R * omax);
                 m.dA = h->alloc<float>(R * H);
                 m.dZ = h->alloc<float>(R * H);
-                m.wpart = h->alloc<float>(kMaxSplits * wmax);
+                m.wpart = h->alloc<float>(wpart_max);
                 m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
                 m.mid = h->alloc<float>(16 * 3 * 1024);
             }
@@ -600,16 +622,20 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         gather_obs(h, d_obs, d_index, start, n, s);  // one gathered, padded copy serves both models
         // the critic's pass runs on the auxiliary stream (disjoint parameters, gradients, workspace
         // and metric slots), overlapping the policy's; the caller's stream waits for both
-        RLGPU_CHECK_HIP(hipEventRecord(h->ev_fork, s));
-        RLGPU_CHECK_HIP(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+        static const bool serial = getenv("RLGPU_SERIAL_MINIBATCH") != nullptr;  // experiment switch
+        hipStream_t cs = serial ? s : h->aux;
+        if (!serial) {
+            RLGPU_CHECK_HIP(hipEventRecord(h->ev_fork, s));
+            RLGPU_CHECK_HIP(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+        }
         Model& pm = h->M[0];
         Model& cm = h->M[1];
-        forward_train(h, 1, h->x0, n, cm.y, h->aux);
-        hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, h->aux, cm.y, d_target, d_index, start, n,
+        forward_train(h, 1, h->x0, n, cm.y, cs);
+        hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, cs, cm.y, d_target, d_index, start, n,
                            bsr, cm.dy, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 1, h->x0, n, cm.dy, h->aux);
-        RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
+        backward(h, 1, h->x0, n, cm.dy, cs);
+        if (!serial) RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
         // policy on the caller's stream
         forward_train(h, 0, h->x0, n, pm.y, s);
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
@@ -618,7 +644,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
                            1.f / std::log((float)A), pm.dy, d_metrics, pm.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
         backward(h, 0, h->x0, n, pm.dy, s, pm.cpart, pl_blocks);
-        RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
+        if (!serial) RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
     });
 }
 

@@ -150,7 +150,7 @@ class Learner:
         self.terms = torch.empty((T, P), dtype=torch.int8, device=d)
         self.trunc_obs = torch.zeros((T, P, OBS), device=d)
         self.values = torch.empty((T + 1, P), device=d)
-        self.trunc_vals = torch.empty((T, P), device=d)
+        self.trunc_vals = torch.zeros((T, P), device=d)
         self.adv = torch.empty((T, P), device=d)
         self.target = torch.empty((T, P), device=d)
         self.ret = torch.empty((T, P), device=d)
@@ -223,7 +223,12 @@ class Learner:
         import torch
         T, P = self.T, self.P
         self.ppo.infer_critic(self.obs.view(-1, OBS), out=self.values.view(-1))
-        self.ppo.infer_critic(self.trunc_obs.view(-1, OBS), out=self.trunc_vals.view(-1))
+        # truncation values only where a trajectory was truncated (code 2): InferCritic on the
+        # truncated next-states (Learner.cpp:944); the other rows of trunc_vals are never read
+        rows = torch.nonzero(self.terms.view(-1) == 2).squeeze(1)
+        if rows.numel():
+            tv = self.ppo.infer_critic(self.trunc_obs.view(-1, OBS).index_select(0, rows))
+            self.trunc_vals.view(-1).index_copy_(0, rows, tv)
         std = self.return_stat.std()
         _gae.GAE.compute_rollout(self.rewards, self.terms, self.values[:T], self.trunc_vals, self.values[T],
                                  self.cfg.gamma, self.cfg.gae_lambda, std, self.cfg.reward_clip_range,
