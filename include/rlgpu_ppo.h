@@ -17,8 +17,8 @@
  * ("seqHalf", refreshed after every optimizer step) and the activation workspace for
  * up to cfg.max_rows rows.  Models: 0 = policy (actor), 1 = critic.
  *
- * Arithmetic: training forward/backward in fp32 on f32-input MFMA (v_mfma_f32_32x32x2_f32),
- * inference in bf16 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- the reference's
+ * Arithmetic: training forward/backward in fp32 (cfg.train_gemm: the three-way bf16 split on
+ * bf16 MFMA by default, or f32-input MFMA v_mfma_f32_32x32x2_f32), inference in bf16 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- the reference's
  * precision split (Model::Forward: halfPrec only without grad).
  *
  * All d_ pointers are device pointers; every call is enqueued on `stream` (NULL = default)
@@ -52,7 +52,18 @@ typedef struct {
     float max_grad_norm;                      /* 0.5 (PPOLearner.cpp:521-526) */
     int32_t max_rows;                         /* workspace rows: max(minibatch, inference chunk) */
     uint64_t seed;                            /* parameter init + action sampling (Philox) */
+    int32_t train_gemm;                       /* training GEMM arithmetic: RLGPU_GEMM_F32X6 (0, default)
+                                                 or RLGPU_GEMM_F32 (1) -- see rlgpu_gemm */
 } rlgpu_ppo_config;
+
+/* fp32 GEMM arithmetic of the training path (libtorch fp32 Linear forward / backward in the
+ * reference, Models.cpp:42-68):
+ *   RLGPU_GEMM_F32X6  every f32 operand split exactly into three bf16 terms (h + m + l), the six
+ *                     products above 2^-24 relative on v_mfma_f32_32x32x16_bf16, leading and
+ *                     correction terms in separate f32 accumulators: f32-class accuracy at 8/3 x
+ *                     the f32-MFMA rate (gfx950's f32-input MFMA runs at 1/16 of bf16);
+ *   RLGPU_GEMM_F32    v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate). */
+enum { RLGPU_GEMM_F32X6 = 0, RLGPU_GEMM_F32 = 1 };
 
 typedef struct rlgpu_ppo rlgpu_ppo;
 
@@ -125,9 +136,13 @@ int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_exp_avg, fl
 int rlgpu_ppo_set_optimizer_step(rlgpu_ppo* h, int64_t step);
 
 /* Building block, exported for tests and microbenchmarks: C[I,J] = sum_k A(i,k) B(k,j) (+ bias[j])
- * on f32-input MFMA.  a_layout 0: A stored [I][lda] (k contiguous), 1: [K][lda] (i contiguous);
+ * in the fp32 arithmetic `mode` (RLGPU_GEMM_F32X6 / RLGPU_GEMM_F32).  a_layout 0: A stored [I][lda] (k contiguous), 1: [K][lda] (i contiguous);
  * b_layout 0: B stored [J][ldb] (k contiguous), 1: [K][ldb] (j contiguous).  splits > 1 writes
  * per-split partials to C + s*I*ldc (caller reduces).  Supported pairs: (0,0), (0,1), (1,1). */
+int rlgpu_gemm(int32_t mode, int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B,
+               int64_t ldb, float* d_C, int64_t ldc, const float* d_bias, int32_t I, int32_t J, int32_t K, int32_t splits,
+               void* stream);
+/* rlgpu_gemm with mode RLGPU_GEMM_F32. */
 int rlgpu_gemm_f32(int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B, int64_t ldb,
                    float* d_C, int64_t ldc, const float* d_bias, int32_t I, int32_t J, int32_t K, int32_t splits,
                    void* stream);

@@ -40,6 +40,7 @@ struct GemmArgs {
     int kchunk;            // K range per split (multiple of BK)
     int64_t c_split;       // element stride between split partials
     int gx, gy, gz;        // logical tile grid (J tiles, I tiles, K splits); launched as 1-D
+    int64_t bplane;        // gemm_x6 with a pre-split B: element stride between the bf16 planes
 };
 
 DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays NaN)
@@ -225,6 +226,257 @@ __global__ void __launch_bounds__(256, RLGPU_GEMM_OCC) gemm_f32(GemmArgs g) {
             for (int r = 0; r < 16; r++) {
                 int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (i < g.I) C[(int64_t)i * g.ldc + j] = acc[ti][tj][r] + bj;
+            }
+        }
+}
+
+// ---- fp32 GEMM on bf16 MFMA by a three-way split (training path, default).
+// gfx950 runs f32-input MFMA at 1/16 of the bf16 rate.  Every f32 operand x is split exactly into
+// three bf16 terms, x = h + m + l (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m); each
+// subtraction is exact by Sterbenz, and 3 x 8 significant bits cover f32's 24), and
+//   a.b ~= h_a h_b + [h_a m_b + m_a h_b + h_a l_b + l_a h_b + m_a m_b]
+// on v_mfma_f32_32x32x16_bf16 (bf16 products are exact in f32).  The dropped terms (m l, l m, l l)
+// are below 2^-24 relative, so each product carries f32-class error; the leading term and the
+// bracketed correction terms accumulate in separate f32 accumulators (summed once at the end) so
+// the rounding of the large running sum is the same count as an f32 FMA chain's.  Six bf16 MFMAs
+// (6 x 32 cycles per K = 16) replace eight f32 ones (8 x 64 cycles).  Same tiles, layouts, split-K
+// and epilogue as gemm_f32; operands are split once per LDS stage into three k-contiguous bf16
+// planes, so the MFMA loop reads b128 vectors whatever the global layout.
+constexpr int XBK = 32;            // K per LDS stage (two 32x32x16 k-steps)
+constexpr int XPAD = 8;            // bf16 pad per LDS row (row = 80 B)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+DEV uint32_t pack_bf16x2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+// split 8 floats (two native 4-vectors) into three bf16x8 planes
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+DEV void split3(const f32x4_t (&v)[2], u32x4_t& h, u32x4_t& m, u32x4_t& l) {
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const float x0 = v[p >> 1][(2 * p) & 3], x1 = v[p >> 1][(2 * p + 1) & 3];
+        const uint32_t hh = pack_bf16x2(x0, x1);
+        const float r0 = x0 - __uint_as_float(hh << 16), r1 = x1 - __uint_as_float(hh & 0xffff0000u);
+        const uint32_t mm = pack_bf16x2(r0, r1);
+        const float s0 = r0 - __uint_as_float(mm << 16), s1 = r1 - __uint_as_float(mm & 0xffff0000u);
+        const uint32_t ll = pack_bf16x2(s0, s1);
+        h[p] = hh;
+        m[p] = mm;
+        l[p] = ll;
+    }
+}
+
+// Per-thread share of one 128 x XBK operand stage: two groups of 8 consecutive k of one row, held
+// in native 4-vectors (loop-carried prefetch registers stay where the loads land, so the wait for
+// them sits at the next stage's store, after this stage's MFMAs).
+//   KMAJ (k contiguous in memory): group e = t + 256 q -> row e >> 2, k group e & 3 (2 float4 loads)
+//   !KMAJ (row index contiguous):  group e -> row e & 127, k group e >> 7 (8 scalar loads, each a
+//                                  256-byte contiguous wave access)
+template <bool KMAJ>
+DEV int xs_row(int q) {
+    const int e = threadIdx.x + 256 * q;
+    return KMAJ ? e >> 2 : e & 127;
+}
+template <bool KMAJ>
+DEV int xs_kg(int q) {
+    const int e = threadIdx.x + 256 * q;
+    return KMAJ ? e & 3 : e >> 7;
+}
+template <bool KMAJ>
+DEV RowPtrs xs_rows(const float* base, int64_t ld, int o0, int on) {
+    RowPtrs r;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int go = o0 + xs_row<KMAJ>(q);
+        r.p[q] = (KMAJ && go < on) ? base + (int64_t)go * ld : nullptr;
+    }
+    r.p[2] = r.p[3] = nullptr;
+    return r;
+}
+template <bool VEC>
+DEV f32x4_t load4v(const float* p, int c, int lim) {
+    const float* z = reinterpret_cast<const float*>(g_zero_row);
+    if (VEC) return *reinterpret_cast<const f32x4_t*>((p && c < lim) ? p + c : z);
+    const float* base = p ? p : z;
+    f32x4_t v;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const bool ok = p && (c + k < lim);
+        v[k] = *(ok ? base + c + k : z);
+    }
+    return v;
+}
+template <bool KMAJ, bool VEC>
+DEV void xs_load(f32x4_t (&v)[2][2], const RowPtrs& rows, const float* base, int64_t ld, int o0, int on, int k0, int ke) {
+    const float* z = reinterpret_cast<const float*>(g_zero_row);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int kk = k0 + xs_kg<KMAJ>(q) * 8;
+        if (KMAJ) {
+            v[q][0] = load4v<VEC>(rows.p[q], kk, ke);
+            v[q][1] = load4v<VEC>(rows.p[q], kk + 4, ke);
+        } else {
+            const int o = o0 + xs_row<KMAJ>(q);
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const bool ok = (kk + c < ke) && (o < on);
+                v[q][c >> 2][c & 3] = *(ok ? base + (int64_t)(kk + c) * ld + o : z);  // absent: the zero row
+            }
+        }
+    }
+}
+template <bool KMAJ>
+DEV void xs_store(uint16_t (*lds)[BM][XBK + XPAD], const f32x4_t (&v)[2][2]) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        u32x4_t h, m, l;
+        split3(v[q], h, m, l);
+        const int row = xs_row<KMAJ>(q), c = xs_kg<KMAJ>(q) * 8;
+        *reinterpret_cast<u32x4_t*>(&lds[0][row][c]) = h;
+        *reinterpret_cast<u32x4_t*>(&lds[1][row][c]) = m;
+        *reinterpret_cast<u32x4_t*>(&lds[2][row][c]) = l;
+    }
+}
+
+// B operand given pre-split (BPRE): three bf16 planes [3][rows][ldbp] (k contiguous; rows padded to a
+// multiple of 128 and ldbp a multiple of XBK, zero filled), plane stride g.bplane elements.  A
+// weight matrix is reused by every row tile of a minibatch, so it is split once per minibatch
+// (split_weight) instead of once per tile and stage.  Per thread and stage: two 16-byte chunks
+// per plane (row e >> 2, chunk e & 3 of 8 bf16).
+DEV void xp_load(u32x4_t (&v)[3][2], const uint16_t* B, int64_t ldb, int64_t plane, int j0, int k0, int ke) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int e = threadIdx.x + 256 * q;
+        const int64_t off = (int64_t)(j0 + (e >> 2)) * ldb + k0 + (e & 3) * 8;
+        const bool ok = k0 + (e & 3) * 8 < ke;
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+            v[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? B + p * plane + off : reinterpret_cast<const uint16_t*>(g_zero_row));
+    }
+}
+DEV void xp_store(uint16_t (*lds)[BM][XBK + XPAD], const u32x4_t (&v)[3][2]) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int e = threadIdx.x + 256 * q;
+#pragma unroll
+        for (int p = 0; p < 3; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e >> 2][(e & 3) * 8]) = v[p][q];
+    }
+}
+
+// W [out][in] f32 -> three bf16 planes of W (trans = 0: [out_pad][in_pad]) or W^T (trans = 1:
+// [in_pad][out_pad]), zero padded; one thread per padded element.
+__global__ void split_weight(const float* W, int out, int in, int trans, int rows_pad, int ld_pad, uint16_t* planes) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t plane = (int64_t)rows_pad * ld_pad;
+    if (e >= plane) return;
+    const int r = (int)(e / ld_pad), c = (int)(e % ld_pad);
+    const int o = trans ? c : r, i = trans ? r : c;
+    const float x = (o < out && i < in) ? W[(int64_t)o * in + i] : 0.f;
+    const uint16_t h = f2bf(x);
+    const float r1 = x - bf2f(h);
+    const uint16_t m = f2bf(r1);
+    planes[e] = h;
+    planes[plane + e] = m;
+    planes[2 * plane + e] = f2bf(r1 - bf2f(m));
+}
+
+template <int LA, int LB, bool AV, bool BV, bool BPRE = false>
+__global__ void __launch_bounds__(256, 2) gemm_x6(GemmArgs g) {
+    constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
+    __shared__ uint16_t As[3][BM][XBK + XPAD];
+    __shared__ uint16_t Bs[3][BN][XBK + XPAD];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
+    const int i0 = tl.y * BM, j0 = tl.x * BN;
+    const int kb = tl.z * g.kchunk;
+    const int ke = min(g.K, kb + g.kchunk);
+    f32x16 acc[2][2], cor[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = cor[a][b][r] = 0.f;
+    f32x4_t va[2][2], vb[2][2];
+    u32x4_t vp[3][2];
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+    const RowPtrs arow = xs_rows<AK>(g.A, g.lda, i0, g.I);
+    const RowPtrs brow = xs_rows<BKM>(g.B, g.ldb, j0, g.J);
+    xs_load<AK, AV>(va, arow, g.A, g.lda, i0, g.I, kb, ke);
+    if (BPRE)
+        xp_load(vp, Bp, g.ldb, g.bplane, j0, kb, ke);
+    else
+        xs_load<BKM, BV>(vb, brow, g.B, g.ldb, j0, g.J, kb, ke);
+    const int ra = wm * 64 + (lane & 31), rb = wn * 64 + (lane & 31);
+    for (int k0 = kb; k0 < ke; k0 += XBK) {
+        xs_store<AK>(As, va);
+        if (BPRE)
+            xp_store(Bs, vp);
+        else
+            xs_store<BKM>(Bs, vb);
+        __syncthreads();
+        // prefetch the next stage into registers while the MFMAs run; unconditional (past ke it
+        // reads the zero row) so the loop-carried registers are the load destinations
+        xs_load<AK, AV>(va, arow, g.A, g.lda, i0, g.I, k0 + XBK, ke);
+        if (BPRE)
+            xp_load(vp, Bp, g.ldb, g.bplane, j0, k0 + XBK, ke);
+        else
+            xs_load<BKM, BV>(vb, brow, g.B, g.ldb, j0, g.J, k0 + XBK, ke);
+        __builtin_amdgcn_sched_barrier(0);  // keep the split of the prefetched stage after the MFMAs
+#pragma unroll
+        for (int ks = 0; ks < XBK / 16; ks++) {
+            const int kof = ks * 16 + 8 * (lane >> 5);
+            bf16x8 a[3][2], b[3][2];
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    a[p][u] = *(const bf16x8*)&As[p][ra + 32 * u][kof];
+                    b[p][u] = *(const bf16x8*)&Bs[p][rb + 32 * u][kof];
+                }
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++) {
+                    f32x16 c = cor[ti][tj];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ti], b[1][tj], c, 0, 0, 0);  // m m
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][ti], b[0][tj], c, 0, 0, 0);  // l h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[2][tj], c, 0, 0, 0);  // h l
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ti], b[0][tj], c, 0, 0, 0);  // m h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h m
+                    cor[ti][tj] = c;
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[0][tj], acc[ti][tj], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+    float* C = g.C + (int64_t)tl.z * g.c_split;
+    const int h = lane >> 5, l32 = lane & 31;
+    if (i0 + BM <= g.I && j0 + BN <= g.J) {  // interior tile: no bounds checks, one base pointer
+        float* cb = C + (int64_t)(i0 + wm * 64 + 4 * h) * g.ldc + j0 + wn * 64 + l32;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                const float bj = g.bias ? g.bias[j0 + wn * 64 + tj * 32 + l32] : 0.f;
+                float* ct = cb + (int64_t)(ti * 32) * g.ldc + tj * 32;
+#pragma unroll
+                for (int r = 0; r < 16; r++)
+                    ct[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = (acc[ti][tj][r] + cor[ti][tj][r]) + bj;
+            }
+        return;
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+        for (int tj = 0; tj < 2; tj++) {
+            int j = j0 + wn * 64 + tj * 32 + l32;
+            if (j >= g.J) continue;
+            float bj = g.bias ? g.bias[j] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (i < g.I) C[(int64_t)i * g.ldc + j] = (acc[ti][tj][r] + cor[ti][tj][r]) + bj;
             }
         }
 }

@@ -20,6 +20,10 @@ struct Layer {
     int64_t w, b, g, be;      // offsets into the flat fp32 buffers (g/be = -1 without LayerNorm)
     int in_pad;               // bf16 copy: weight rows padded to a multiple of 8 (16 bytes)
     int64_t hw, hb, hg, hbe;  // offsets into the padded bf16 inference copy
+    // three-way bf16 split of the weight for the x6 training GEMMs (offsets into Model::wsplit):
+    // forward B = W [out_pad128][in_pad32], backward dA B = W^T [in_pad128][out_pad32]; -1 = none
+    int64_t sf = -1, sb = -1;
+    int sf_rows = 0, sf_ld = 0, sb_rows = 0, sb_ld = 0;
 };
 
 struct Model {
@@ -27,15 +31,19 @@ struct Model {
     int in, out;
     int64_t off, count;
     float lr;
+    int mode = 0;  // training GEMM arithmetic (rlgpu_ppo_config.train_gemm)
     // fp32 training workspace (per model, so the two models' passes can overlap on two streams)
     std::vector<float*> xhat, act, rstd;
     float *y = nullptr, *dy = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr, *mid = nullptr;  // y: model output
+    uint16_t* wsplit = nullptr;  // split weight planes (x6 mode)
+    int64_t nsplit = 0;
 };
 
 constexpr int kMaxSplits = 256;
 // concurrent gemm_f32 workgroups on the device (CUs x RLGPU_GEMM_OCC), set at create: the split-K
 // weight gradients are sized to fill whole rounds of workgroups
-int g_gemm_slots = 256 * RLGPU_GEMM_OCC;
+int g_cus = 256;  // compute units of the device, set at create
+inline int gemm_slots(int mode) { return g_cus * (mode == RLGPU_GEMM_F32X6 ? 2 : RLGPU_GEMM_OCC); }
 
 }  // namespace
 
@@ -72,7 +80,7 @@ namespace {
 
 // C[I,J] (+ bias) = A . B with the layouts of mlp::gemm_f32.  *_tail_ok: the operand's rows are
 // zero-padded up to a multiple of 4 past the bound (so float4 loads may straddle it).
-void gemm_f32(int la, int lb, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
               const float* bias, int I, int J, int K, int splits, hipStream_t s, bool a_tail_ok = false,
               bool b_tail_ok = false) {
     mlp::GemmArgs g;
@@ -101,10 +109,17 @@ void gemm_f32(int la, int lb, const float* A, int64_t lda, const float* B, int64
     dim3 grid(g.gx * g.gy * g.gz), blk(256);
 #define RLGPU_GEMM_CASE(LA, LB)                                                                                  \
     if (la == LA && lb == LB) {                                                                                  \
-        if (av && bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, true>), grid, blk, 0, s, g);               \
-        else if (av) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, false>), grid, blk, 0, s, g);              \
-        else if (bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, false, true>), grid, blk, 0, s, g);              \
-        else hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, false, false>), grid, blk, 0, s, g);                     \
+        if (mode == RLGPU_GEMM_F32X6) {                                                                          \
+            if (av && bv) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, true, true>), grid, blk, 0, s, g);            \
+            else if (av) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, true, false>), grid, blk, 0, s, g);           \
+            else if (bv) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, false, true>), grid, blk, 0, s, g);           \
+            else hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, false, false>), grid, blk, 0, s, g);                  \
+        } else {                                                                                                 \
+            if (av && bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, true>), grid, blk, 0, s, g);           \
+            else if (av) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, false>), grid, blk, 0, s, g);          \
+            else if (bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, false, true>), grid, blk, 0, s, g);          \
+            else hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, false, false>), grid, blk, 0, s, g);                 \
+        }                                                                                                        \
         RLGPU_CHECK_HIP(hipGetLastError());                                                                      \
         return;                                                                                                  \
     }
@@ -115,11 +130,59 @@ void gemm_f32(int la, int lb, const float* A, int64_t lda, const float* B, int64
     throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "gemm layout");
 }
 
+// C[I,J] (+ bias) = A . B on the x6 GEMM with B given as pre-split planes (Layer::sf / sb layout)
+void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int64_t bplane, float* C, int64_t ldc,
+                 const float* bias, int I, int J, int K, hipStream_t s, bool a_tail_ok = false) {
+    mlp::GemmArgs g;
+    g.A = A;
+    g.B = reinterpret_cast<const float*>(Bp);
+    g.C = C;
+    g.bias = bias;
+    g.lda = lda;
+    g.ldb = ldbp;
+    g.ldc = ldc;
+    g.I = I;
+    g.J = J;
+    g.K = K;
+    g.kchunk = (int)ceil_div(K, mlp::BK) * mlp::BK;
+    g.c_split = 0;
+    g.bplane = bplane;
+    g.gx = (int)ceil_div(J, mlp::BN);
+    g.gy = (int)ceil_div(I, mlp::BM);
+    g.gz = 1;
+    const bool av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && (K % 4 == 0 || a_tail_ok);
+    dim3 grid(g.gx * g.gy), blk(256);
+    if (av)
+        hipLaunchKernelGGL((mlp::gemm_x6<mlp::A_IK, mlp::B_JK, true, true, true>), grid, blk, 0, s, g);
+    else
+        hipLaunchKernelGGL((mlp::gemm_x6<mlp::A_IK, mlp::B_JK, false, true, true>), grid, blk, 0, s, g);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+// refresh the split weight planes of model m from the current parameters (once per minibatch /
+// training forward: the weights change only at the optimizer step, but may be written directly)
+void split_weights(const float* P, Model& m, hipStream_t s) {
+    if (m.mode != RLGPU_GEMM_F32X6) return;
+    for (auto& L : m.L) {
+        if (L.sf >= 0) {
+            int64_t e = (int64_t)L.sf_rows * L.sf_ld;
+            hipLaunchKernelGGL(mlp::split_weight, dim3(ceil_div(e, 256)), dim3(256), 0, s, P + L.w, L.out, L.in, 0, L.sf_rows,
+                               L.sf_ld, m.wsplit + L.sf);
+        }
+        if (L.sb >= 0) {
+            int64_t e = (int64_t)L.sb_rows * L.sb_ld;
+            hipLaunchKernelGGL(mlp::split_weight, dim3(ceil_div(e, 256)), dim3(256), 0, s, P + L.w, L.out, L.in, 1, L.sb_rows,
+                               L.sb_ld, m.wsplit + L.sb);
+        }
+    }
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
 // split-K count of a weight gradient [out, in] over `rows`: one full round of workgroups
-// (tiles x splits ~ g_gemm_slots), each split at least 4 K steps
-int splits_for(int rows, int out, int in) {
+// (tiles x splits ~ gemm_slots), each split at least 4 K steps
+int splits_for(int mode, int rows, int out, int in) {
     const int tiles = (int)(ceil_div(out, mlp::BM) * ceil_div(in, mlp::BN));
-    int s = g_gemm_slots / tiles;
+    int s = gemm_slots(mode) / tiles;
     const int maxs = rows / (4 * mlp::BK);
     if (s > maxs) s = maxs;
     if (s > kMaxSplits) s = kMaxSplits;
@@ -129,10 +192,10 @@ int splits_for(int rows, int out, int in) {
 // dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
 void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
                  bool x_tail_ok = false) {
-    int splits = splits_for(n, out, in);
+    int splits = splits_for(m.mode, n, out, in);
     int chunk = (int)ceil_div(ceil_div(n, splits), mlp::BK) * mlp::BK;
     int z = (int)ceil_div(n, chunk);
-    gemm_f32(mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
+    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
     int64_t e = (int64_t)out * in;
     if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)m.wpart & 15) == 0)
         hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
@@ -169,13 +232,19 @@ void colsum_into(Model& m, const float* X, int n, int C, float* g, hipStream_t s
 void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipStream_t s) {
     Model& m = h->M[mi];
     const float* P = h->params;
+    split_weights(P, m, s);
     int nh = (int)m.L.size() - 1;
     const float* in = X;
     int64_t ld = h->x_ld;
     bool tail_ok = true;
     for (int l = 0; l < nh; l++) {
         const Layer& L = m.L[l];
-        gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s, tail_ok);
+        if (L.sf >= 0)
+            gemm_x6_pre(in, ld, m.wsplit + L.sf, L.sf_ld, (int64_t)L.sf_rows * L.sf_ld, m.xhat[l], L.out, P + L.b, n, L.out,
+                        L.in, s, tail_ok);
+        else
+            gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s,
+                     tail_ok);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
@@ -192,7 +261,10 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
         RLGPU_CHECK_HIP(hipGetLastError());
         return;
     }
-    gemm_f32(mlp::A_IK, mlp::B_JK, in, ld, P + O.w, O.in, out, O.out, P + O.b, n, O.out, O.in, 1, s);
+    if (O.sf >= 0)
+        gemm_x6_pre(in, ld, m.wsplit + O.sf, O.sf_ld, (int64_t)O.sf_rows * O.sf_ld, out, O.out, P + O.b, n, O.out, O.in, s);
+    else
+        gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + O.w, O.in, out, O.out, P + O.b, n, O.out, O.in, 1, s);
 }
 
 // backward from dout [n, out] into the grad buffer (accumulating).  dout_part: optional per-block
@@ -218,7 +290,11 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         else
             colsum_into(m, dout, n, O.out, G + O.b, s);
         // dA = dout . W_out
-        gemm_f32(mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s);
+        if (O.sb >= 0)
+            gemm_x6_pre(dout, O.out, m.wsplit + O.sb, O.sb_ld, (int64_t)O.sb_rows * O.sb_ld, m.dA, O.in, nullptr, n, O.in,
+                        O.out, s);
+        else
+            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s);
     }
     for (int l = nh - 1; l >= 0; l--) {
         const Layer& L = m.L[l];
@@ -236,8 +312,11 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
             weight_grad(m, m.dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true);
         else
             weight_grad(m, m.dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s);
-        if (l > 0)
-            gemm_f32(mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, m.dA, L.in, nullptr, n, L.in, L.out, 1, s);
+        if (l > 0 && L.sb >= 0)
+            gemm_x6_pre(m.dZ, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, m.dA, L.in, nullptr, n, L.in,
+                        L.out, s);
+        else if (l > 0)
+            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, m.dA, L.in, nullptr, n, L.in, L.out, 1, s);
     }
 }
 
@@ -295,6 +374,7 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
     m.in = in;
     m.out = out;
     m.lr = lr;
+    m.mode = h->cfg.train_gemm;
     m.off = h->nparams;
     int prev = in;
     for (int l = 0; l <= nl; l++) {
@@ -327,6 +407,18 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
         }
         if (L.out > h->hmax) h->hmax = L.out;
         if (L.in > h->hmax && l > 0) h->hmax = L.in;
+        if (m.mode == RLGPU_GEMM_F32X6 && L.out > 1) {  // the rank-1 critic head has no GEMM
+            L.sf_rows = (int)ceil_div(L.out, mlp::BN) * mlp::BN;
+            L.sf_ld = (int)ceil_div(L.in, mlp::BK) * mlp::BK;
+            L.sf = m.nsplit;
+            m.nsplit += 3 * (int64_t)L.sf_rows * L.sf_ld;
+            if (l > 0) {  // dA of the first layer is never needed
+                L.sb_rows = (int)ceil_div(L.in, mlp::BN) * mlp::BN;
+                L.sb_ld = (int)ceil_div(L.out, mlp::BK) * mlp::BK;
+                L.sb = m.nsplit;
+                m.nsplit += 3 * (int64_t)L.sb_rows * L.sb_ld;
+            }
+        }
         m.L.push_back(L);
         prev = L.out;
     }
@@ -409,13 +501,13 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
                         cus = prop.multiProcessorCount;
                 }
-                g_gemm_slots = cus * RLGPU_GEMM_OCC;
+                g_cus = cus;
             }
             for (auto& m : h->M)
                 for (auto& L : m.L) {
                     wmax = std::max<int64_t>(wmax, (int64_t)L.in * L.out);
                     // splits_for is non-decreasing in the row count, and z = ceil(n / chunk) <= splits
-                    wpart_max = std::max<int64_t>(wpart_max, (int64_t)splits_for((int)R, L.out, L.in) * L.in * L.out);
+                    wpart_max = std::max<int64_t>(wpart_max, (int64_t)splits_for(m.mode, (int)R, L.out, L.in) * L.in * L.out);
                 }
             int64_t nb = ceil_div(R, std::min(mlp::LNB_ROWS, mlp::CS_ROWS));
             for (auto& m : h->M) {
@@ -426,6 +518,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 m.wpart = h->alloc<float>(wpart_max);
                 m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
                 m.mid = h->alloc<float>(16 * 3 * 1024);
+                if (m.nsplit) m.wsplit = h->alloc<uint16_t>(m.nsplit);
             }
             RLGPU_CHECK_HIP(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
             RLGPU_CHECK_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -721,6 +814,19 @@ extern "C" int rlgpu_permutation(int64_t n, uint64_t seed, uint64_t counter, int
     });
 }
 
+extern "C" int rlgpu_gemm(int32_t mode, int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B,
+                          int64_t ldb, float* d_C, int64_t ldc, const float* d_bias, int32_t I, int32_t J, int32_t K,
+                          int32_t splits, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(d_A && d_B && d_C, "rlgpu_gemm: null argument");
+        RLGPU_REQUIRE(mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F32, "rlgpu_gemm: unknown mode");
+        RLGPU_REQUIRE(I > 0 && J > 0 && K > 0 && splits >= 1, "rlgpu_gemm: bad sizes");
+        RLGPU_REQUIRE((a_layout == 0 && (b_layout == 0 || b_layout == 1)) || (a_layout == 1 && b_layout == 1),
+                      "rlgpu_gemm: unsupported layout pair");
+        gemm_f32(mode, a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, rlgpu::as_stream(stream));
+    });
+}
+
 extern "C" int rlgpu_gemm_f32(int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B, int64_t ldb,
                               float* d_C, int64_t ldc, const float* d_bias, int32_t I, int32_t J, int32_t K, int32_t splits,
                               void* stream) {
@@ -729,6 +835,6 @@ extern "C" int rlgpu_gemm_f32(int32_t a_layout, int32_t b_layout, const float* d
         RLGPU_REQUIRE(I > 0 && J > 0 && K > 0 && splits >= 1, "rlgpu_gemm_f32: bad sizes");
         RLGPU_REQUIRE((a_layout == 0 && (b_layout == 0 || b_layout == 1)) || (a_layout == 1 && b_layout == 1),
                       "rlgpu_gemm_f32: unsupported layout pair");
-        gemm_f32(a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, rlgpu::as_stream(stream));
+        gemm_f32(RLGPU_GEMM_F32, a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, rlgpu::as_stream(stream));
     });
 }

@@ -117,12 +117,13 @@ def test_forward_bf16_close_to_fp32(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["x6", "f32"])
 @pytest.mark.parametrize("n,batch,slope", [(300, 600, 0.01), (1029, 1029, 0.01), (777, 1000, 1.0)])
-def test_minibatch_grads_match_torch(gpu, n, batch, slope):
+def test_minibatch_grads_match_torch(gpu, n, batch, slope, mode):
     import torch
     from rlgpu.ppo import PPO
     rng = np.random.default_rng(n)
-    p = PPO(max_rows=2048, seed=7, leaky_slope=slope)
+    p = PPO(max_rows=2048, seed=7, leaky_slope=slope, train_gemm=mode)
     pol, crit = torch_models(p)
     obs, masks, acts, old, adv, tgt = make_batch(rng, n)
     T = lambda a: torch.from_numpy(a)  # noqa: E731
@@ -238,3 +239,42 @@ def test_mean_std(gpu):
     x = torch.randn(100_003) * 3 + 1
     st = p.adv_normalizer(x.to(gpu)).cpu().numpy()
     np.testing.assert_allclose(st, [x.mean().item(), x.std().item()], rtol=1e-5)
+
+
+# ------------------------------------------------------------------ GEMM arithmetic
+GEMM_SHAPES = [  # (a_layout, b_layout, I, J, K, splits): the PPO shapes' layouts, ragged edges
+    (0, 0, 1029, 512, 167, 1), (0, 0, 777, 90, 512, 1), (0, 0, 300, 130, 33, 1),
+    (0, 1, 1029, 167, 512, 1), (0, 1, 513, 512, 90, 1),
+    (1, 1, 512, 167, 3001, 7), (1, 1, 90, 512, 2048, 4), (1, 1, 130, 200, 97, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("la,lb,I,J,K,splits", GEMM_SHAPES)
+def test_gemm_modes_fp32_class_accuracy(gpu, la, lb, I, J, K, splits):
+    """rlgpu_gemm in both training arithmetics against an fp64 product: the three-way bf16 split
+    (RLGPU_GEMM_F32X6) must carry f32-class error -- within 4x of torch's own fp32 matmul error
+    on the same operands (the reference's libtorch fp32 Linear) -- and so must the f32 MFMA."""
+    import ctypes
+    import torch
+    from rlgpu import _lib
+    from rlgpu.ppo import _bind
+    L = _bind()
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.rlgpu_gemm.argtypes = [i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i32, i32, i32, i32, vp]
+    g = torch.Generator().manual_seed(I * 7 + J * 3 + K)
+    A = torch.randn((I, K) if la == 0 else (K, I), generator=g)
+    B = torch.randn((J, K) if lb == 0 else (K, J), generator=g)
+    bias = torch.randn(J, generator=g) if splits == 1 else None
+    tA, tB = (A if la == 0 else A.t()), (B.t() if lb == 0 else B)
+    ref = tA.double() @ tB.double() + (bias.double() if bias is not None else 0)
+    scale = ref.abs().max().item()
+    terr = ((tA @ tB + (bias if bias is not None else 0)).double() - ref).abs().max().item() / scale
+    dA, dB = A.to(gpu), B.to(gpu)
+    db = bias.to(gpu) if bias is not None else None
+    for mode in (0, 1):
+        C = torch.full((splits, I, J), float("nan"), device=gpu)
+        _lib.check(L.rlgpu_gemm(mode, la, lb, _lib.ptr(dA), A.shape[1], _lib.ptr(dB), B.shape[1], _lib.ptr(C), J,
+                                _lib.ptr(db), I, J, K, splits, _lib.stream_ptr()), "rlgpu_gemm")
+        got = C.sum(0).double().cpu()
+        err = (got - ref).abs().max().item() / scale
+        assert err <= 4 * terr + 1e-7, f"mode {mode}: rel err {err:.2e} vs torch fp32 {terr:.2e}"
