@@ -6,7 +6,8 @@ training), PPO epochs 2, minibatch 50k, AdamW.
 Contract (driver): python bench.py --gpus N --steps K --warmup W ; for N > 1 launched by
 torch.distributed.run, one rank per GPU over RCCL.  Rank 0 prints ONE JSON line.
 
-A "step" is one PPO iteration of every rank: T = 128 env steps of all arenas (bf16 policy
+The loop is the C++ host Learner (reinforcement-learning_amd/host/learner.cpp, GGL::Learner over
+the C ABI), driven through rlgpu.learner.  A "step" is one PPO iteration of every rank: T = 128 env steps of all arenas (bf16 policy
 inference + fused env kernel with experience append), critic over the rollout, GAE, then
 Learn (2 epochs of shuffled 50k minibatches, fp32 forward/backward, RCCL gradient all-reduce
 for N > 1, clip_grad_norm_, AdamW).  value = env-steps/s summed over ranks (weak scaling:
@@ -103,7 +104,8 @@ def main():
     # self-play iterations (15 % chance, LearnerConfig.h:67-68) are off so every timed iteration has
     # the same work; the mixed-policy path is covered by tests/test_learner_gpu.py
     cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False)
-    L = Learner(cfg, device=dev, rank=rank, world=world)
+    L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
+    L.set_env_timing(True)  # HIP events around every fused env step, on the learner's stream
 
     for _ in range(args.warmup):
         L.iterate()
@@ -111,26 +113,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    L.env_events = []
     phase = {"collect": 0.0, "consume": 0.0, "learn": 0.0}
+    kern = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        a = time.perf_counter()
-        L.collect()
-        torch.cuda.synchronize()
-        b = time.perf_counter()
-        L.consume()
-        torch.cuda.synchronize()
-        c = time.perf_counter()
-        L.learn()
-        L.obs[0].copy_(L.obs[L.T])
-        L.masks[0].copy_(L.masks[L.T])
-        L.iteration += 1
-        torch.cuda.synchronize()
-        d = time.perf_counter()
-        phase["collect"] += b - a
-        phase["consume"] += c - b
-        phase["learn"] += d - c
+        rep = L.iterate()
+        phase["collect"] += rep["collect_s"]
+        phase["consume"] += rep["consume_s"]
+        phase["learn"] += rep["learn_s"]
+        kern.append(rep["env_kernel_ms"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -141,7 +132,7 @@ def main():
     env_steps = world * args.arenas * cfg.rollout_len * args.steps
     agent_steps = 4 * env_steps
     value = env_steps / el
-    kern_ms = sum(x.elapsed_time(y) for x, y in L.env_events) / len(L.env_events)
+    kern_ms = sum(kern) / len(kern)
     b_env = env_bytes_per_step(arena_state_size())
     achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(kern_ms)

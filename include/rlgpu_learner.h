@@ -1,0 +1,171 @@
+/*
+ * rlgpu_learner.h -- C ABI of the C++ host Learner (reinforcement-learning_amd/host/): the
+ * GigaLearnCPP training loop for one GPU rank, every array resident in HBM.
+ *
+ * Replaces (GigaLearnCPP):
+ *   GGL::Learner(EnvCreateFn, LearnerConfig, StepCallbackFn) / Start()
+ *                                   src/public/GigaLearnCPP/Learner.h:11-45, Learner.cpp:482-1056
+ *     collection   InferActions -> EnvSet step -> trajectory append        Learner.cpp:669-861
+ *     consumption  InferCriticBatched, truncation values, GAE::Compute,
+ *                  return-std WelfordStat over sampled returns             Learner.cpp:863-990
+ *     learning     PPOLearner::Learn (epochs x shuffled batches x minibatches,
+ *                  batch advantage normalisation, clip_grad_norm_, AdamW)   PPOLearner.cpp:278-581
+ *   GGL::ExperienceBuffer           src/private/GigaLearnCPP/PPO/ExperienceBuffer.{h,cpp}
+ *   GGL::WelfordStat                src/private/GigaLearnCPP/Util/WelfordStat.h:7-67
+ *   GGL::LearnerConfig / PPOLearnerConfig (hot-path subset, ExampleMain values as defaults)
+ *                                   src/public/GigaLearnCPP/LearnerConfig.h, PPO/PPOLearnerConfig.h,
+ *                                   src/ExampleMain.cpp:340-430
+ *
+ * The C++ API (namespaces GGL / RLGC, host/learner.hpp) is the product host code; this C ABI
+ * exposes it to other languages (the Python mirror rlgpu/learner.py, bench.py).
+ *
+ * Multi-GPU: one Learner per rank, arenas sharded (rank r owns its own num_arenas).  The
+ * exchanges go through the caller-supplied rlgpu_collective (bench.py binds it to
+ * torch.distributed, i.e. RCCL over xGMI on MI355X): the flat fp32 gradient all-reduce (sum)
+ * before clip_grad_norm_ (PPOLearner.cpp:521-526), the fp64 batch-advantage moments
+ * (PPOLearner.cpp:360-371) and the return samples of the WelfordStat (Learner.cpp:959-967).
+ *
+ * Return 0 or a negative rlgpu_status (rlgpu_core.h); rlgpu_last_error() has the message.
+ */
+#ifndef RLGPU_LEARNER_H
+#define RLGPU_LEARNER_H
+
+#include <stdint.h>
+#include "rlgpu_core.h"
+#include "rlgpu_env.h"
+#include "rlgpu_ppo.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    /* env (EnvSetConfig + LearnerConfig::tickSkip / actionDelay, ExampleMain.cpp:356-358) */
+    int32_t num_arenas;            /* arenas of THIS rank */
+    int32_t tick_skip;             /* 8 */
+    int32_t action_delay;          /* 7 */
+    uint64_t seed;                 /* LearnerConfig::randomSeed (123) */
+    float max_episode_duration;    /* seconds (300, ExampleMain) -> 300 * 120 / tickSkip steps */
+    /* experience / PPO (PPOLearnerConfig, ExampleMain.cpp:404-430) */
+    int32_t rollout_len;           /* T env steps per iteration and rank (tsPerItr = T * 4 * arenas) */
+    int32_t epochs;                /* 2 */
+    int32_t mini_batch_size;       /* 50000 (per rank) */
+    int64_t batch_size;            /* global batch; 0 = the whole iteration (batchSize = tsPerItr) */
+    int32_t overbatching;          /* 1 */
+    float gamma, gae_lambda;       /* 0.99, 0.95 */
+    float clip_range;              /* 0.2 */
+    float entropy_scale;           /* 0.035 */
+    float policy_lr, critic_lr;    /* 2.5e-4 */
+    float reward_clip_range;       /* 200 */
+    int32_t return_samples;        /* 150 (Learner.cpp:959-967) */
+    int32_t policy_layers[RLGPU_MAX_LAYERS];
+    int32_t n_policy_layers;
+    int32_t critic_layers[RLGPU_MAX_LAYERS];
+    int32_t n_critic_layers;
+    int32_t deterministic;         /* LearnerConfig::deterministic */
+    int32_t train_gemm;            /* rlgpu_ppo_config.train_gemm */
+    /* sharding */
+    int32_t rank, world;
+    /* arena meshes (rlgpu_envset_config.mesh_*; NULL = built-in synthetic arena) */
+    const float* mesh_tris;
+    int32_t mesh_ntris;
+    int32_t mesh_objects;
+    const int32_t* mesh_object_ntris;
+} rlgpu_learner_config;
+
+/* Fills ExampleMain's values (src/ExampleMain.cpp:340-430) for a C2 rank: 4096 arenas, T = 128,
+ * [512, 512] actor / critic, world 1. */
+int rlgpu_learner_default_config(rlgpu_learner_config* cfg);
+
+/* Collectives for world > 1, called synchronously from the learner's host thread (the learner's
+ * stream is synchronised before each call).  Return 0 on success. */
+typedef struct {
+    void* user;
+    int (*allreduce_sum_f32)(void* user, float* d_buf, int64_t n);           /* device buffer, in place */
+    int (*allreduce_sum_f64)(void* user, double* h_buf, int64_t n);          /* host buffer, in place */
+    int (*allgather_f32)(void* user, const float* h_in, int64_t n, float* h_out); /* host, out [world * n] */
+} rlgpu_collective;
+
+/* Device views of the rollout (ExperienceBuffer) in HBM, [T, P] time-major, P = 4 * num_arenas. */
+typedef struct {
+    float* obs;          /* [T + 1][P][RLGPU_OBS] */
+    uint8_t* masks;      /* [T + 1][P][RLGPU_ACTIONS] */
+    int32_t* actions;    /* [T][P] */
+    float* logp;         /* [T][P] */
+    float* rewards;      /* [T][P] */
+    int8_t* terms;       /* [T][P] trajectory codes 0 / 1 NORMAL / 2 TRUNCATED */
+    float* trunc_obs;    /* [T][P][RLGPU_OBS] */
+    float* values;       /* [T + 1][P] */
+    float* trunc_vals;   /* [T][P] (rows with code 2) */
+    float* adv;          /* [T][P] */
+    float* target;       /* [T][P] */
+    float* ret;          /* [T][P] */
+    int32_t T, P;
+} rlgpu_rollout_view;
+
+/* Host-side statistics (checkpoint RUNNING_STATS.json, Learner.cpp:224-279). */
+typedef struct {
+    int64_t total_steps;        /* timesteps of the current policy's players, all ranks */
+    int64_t iteration;
+    int64_t return_n;           /* WelfordStat of sampled returns */
+    double return_mean, return_m2;
+    int64_t rng_step;           /* action-sampling counter */
+} rlgpu_learner_stats;
+
+typedef struct {
+    double collect_s, consume_s, learn_s;   /* host wall time of the phases (stream-synchronised) */
+    double env_kernel_ms;                   /* mean fused env-step time (HIP events), if timing is on */
+    int64_t env_steps;                      /* env steps of this rank this iteration */
+} rlgpu_learner_report;
+
+typedef struct rlgpu_learner rlgpu_learner;
+
+int rlgpu_learner_create(const rlgpu_learner_config* cfg, const rlgpu_collective* coll, void* stream,
+                         rlgpu_learner** out);
+int rlgpu_learner_destroy(rlgpu_learner* h);
+/* The owned env set and PPO handles (valid until destroy). */
+int rlgpu_learner_handles(rlgpu_learner* h, rlgpu_envset** env, rlgpu_ppo** ppo);
+int rlgpu_learner_rollout(rlgpu_learner* h, rlgpu_rollout_view* out);
+
+/* One iteration = collect + consume + learn + finish (Learner::Start loop body). */
+int rlgpu_learner_iterate(rlgpu_learner* h, rlgpu_learner_report* rep);
+/* The phases separately (enqueued on the learner's stream; consume and learn synchronise where
+ * the host needs device results). */
+int rlgpu_learner_collect(rlgpu_learner* h);
+int rlgpu_learner_consume(rlgpu_learner* h);
+int rlgpu_learner_learn(rlgpu_learner* h);
+/* Next rollout starts from the last obs; counters (total steps of the current policy's players). */
+int rlgpu_learner_finish_iteration(rlgpu_learner* h);
+
+/* Self-play (Learner.cpp:587-627,733-767): team 0 / 1 acts with the old version set through
+ * rlgpu_ppo_set_version (its rows are simulated but not trained or counted); -1 = off. */
+int rlgpu_learner_set_old_team(rlgpu_learner* h, int32_t team);
+
+int rlgpu_learner_get_stats(rlgpu_learner* h, rlgpu_learner_stats* out);
+int rlgpu_learner_set_stats(rlgpu_learner* h, const rlgpu_learner_stats* in);
+/* PPO report metrics accumulated since the last reset (PPOLearner.cpp:537-566): h_out receives
+ * RLGPU_NUM_METRICS sums (rlgpu_ppo.h RLGPU_M_*), *count the number of minibatches summed. */
+int rlgpu_learner_metrics(rlgpu_learner* h, float* h_out, int64_t* count, int32_t reset);
+/* Record HIP events around every fused env step (rlgpu_learner_report.env_kernel_ms). */
+int rlgpu_learner_set_env_timing(rlgpu_learner* h, int32_t enable);
+
+/* Host building blocks, exported for tests (no GPU needed). */
+/* ExperienceBuffer::GetAllBatchesShuffled batch boundaries (ExperienceBuffer.cpp:117-162): writes up
+ * to max_ranges [start, end) pairs into out (2 * max_ranges int64), returns the count (>= 0). */
+int64_t rlgpu_batch_ranges(int64_t exp_size, int64_t batch_size, int32_t overbatching, int64_t* out,
+                           int64_t max_ranges);
+/* WelfordStat::Increment over n floats (fp64 state in/out: count, mean, m2). */
+int rlgpu_welford_add(int64_t* count, double* mean, double* m2, const float* xs, int64_t n);
+/* WelfordStat::GetSTD (1 when count < 2 or variance <= 0). */
+double rlgpu_welford_std(int64_t count, double m2);
+/* Global batch-advantage (mean, unbiased std) from all-reduced fp64 moments (sum, sum of squares,
+ * count) -- the multi-rank form of PPOLearner.cpp:360-371. */
+int rlgpu_moments_mean_std(const double* moments3, float* out2);
+/* The return-sample indices of one iteration: n draws in [0, range) from a counter-based
+ * generator keyed by (seed, rank, iteration) -- every language binding reproduces the same draws. */
+int rlgpu_sample_indices(uint64_t seed, int32_t rank, int64_t iteration, int64_t range, int32_t n, int64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,144 @@
+// learner_kernels.hip -- small device helpers of the C++ host Learner (host/learner.cpp):
+// truncated-row compaction, index gathers / scatters, self-play row lists, fp64 moments.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+#include "learner_kernels.hpp"
+
+namespace lk {
+namespace {
+
+using rlgpu::ceil_div;
+
+__global__ void k_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+__global__ void k_scatter_f32(const float* src, const int32_t* idx, int64_t n, float* dst) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[idx[i]] = src[i];
+}
+
+__global__ void k_gather_rows(const float* src, int C, const int32_t* idx, int64_t n, float* dst) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * C) return;
+    int64_t r = e / C;
+    int c = (int)(e % C);
+    dst[e] = src[(int64_t)idx[r] * C + c];
+}
+
+__global__ void k_compose(const int32_t* rows, const int32_t* perm, int64_t n, int32_t* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = rows[perm[i]];
+}
+
+__global__ void k_train_rows(int T, int P, int team, int32_t* out) {
+    const int half = P / 2;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)T * half) return;
+    int t = (int)(i / half), q = (int)(i % half);
+    out[i] = t * P + 2 * q + team;  // team of player p is p % 2 (cars 0, 2 blue; 1, 3 orange)
+}
+
+__global__ void k_gather_samples(const float* src, const int64_t* idx, int n, float* dst) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+// fp64 (sum, sum of squares) partials over a grid-stride range, then a fixed-order final sum:
+// deterministic run to run
+constexpr int kMomBlocks = 256;
+__global__ void __launch_bounds__(256) k_moments_partial(const float* x, const int32_t* idx, int64_t n, double* part) {
+    __shared__ double s1[256], s2[256];
+    double a = 0, b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        double v = idx ? x[idx[i]] : x[i];
+        a += v;
+        b += v * v;
+    }
+    s1[threadIdx.x] = a;
+    s2[threadIdx.x] = b;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            s1[threadIdx.x] += s1[threadIdx.x + o];
+            s2[threadIdx.x] += s2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s1[0];
+        part[2 * blockIdx.x + 1] = s2[0];
+    }
+}
+__global__ void k_moments_final(const double* part, int nb, int64_t n, double* out) {
+    if (threadIdx.x != 0) return;
+    double a = 0, b = 0;
+    for (int k = 0; k < nb; k++) {
+        a += part[2 * k];
+        b += part[2 * k + 1];
+    }
+    out[0] = a;
+    out[1] = b;
+    out[2] = (double)n;
+}
+
+struct IsTrunc {
+    const int8_t* t;
+    __device__ bool operator()(const int32_t& i) const { return t[i] == 2; }
+};
+
+}  // namespace
+
+void gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gather_f32, dim3(ceil_div(n, 256)), dim3(256), 0, s, src, idx, n, dst);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void scatter_f32(const float* src, const int32_t* idx, int64_t n, float* dst, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_scatter_f32, dim3(ceil_div(n, 256)), dim3(256), 0, s, src, idx, n, dst);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void gather_rows(const float* src, int C, const int32_t* idx, int64_t n, float* dst, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gather_rows, dim3(ceil_div(n * C, 256)), dim3(256), 0, s, src, C, idx, n, dst);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void compose(const int32_t* rows, const int32_t* perm, int64_t n, int32_t* out, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_compose, dim3(ceil_div(n, 256)), dim3(256), 0, s, rows, perm, n, out);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void train_rows(int T, int P, int team, int32_t* out, hipStream_t s) {
+    int64_t n = (int64_t)T * (P / 2);
+    hipLaunchKernelGGL(k_train_rows, dim3(ceil_div(n, 256)), dim3(256), 0, s, T, P, team, out);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void gather_samples(const float* src, const int64_t* idx, int n, float* dst, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gather_samples, dim3(ceil_div(n, 256)), dim3(256), 0, s, src, idx, n, dst);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+size_t moments_scratch_bytes() { return 2 * kMomBlocks * sizeof(double); }
+void moments_f64(const float* x, const int32_t* idx, int64_t n, double* scratch, double* out3, hipStream_t s) {
+    hipLaunchKernelGGL(k_moments_partial, dim3(kMomBlocks), dim3(256), 0, s, x, idx, n, scratch);
+    hipLaunchKernelGGL(k_moments_final, dim3(1), dim3(64), 0, s, scratch, kMomBlocks, n, out3);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+size_t select_trunc_scratch_bytes(int64_t n) {
+    size_t bytes = 0;
+    hipcub::CountingInputIterator<int32_t> it(0);
+    RLGPU_CHECK_HIP(hipcub::DeviceSelect::If(nullptr, bytes, it, (int32_t*)nullptr, (int32_t*)nullptr, (int)n,
+                                             IsTrunc{nullptr}, (hipStream_t)0));
+    return bytes;
+}
+void select_trunc(const int8_t* terms, int64_t n, void* scratch, size_t scratch_bytes, int32_t* rows, int32_t* count,
+                  hipStream_t s) {
+    hipcub::CountingInputIterator<int32_t> it(0);
+    RLGPU_CHECK_HIP(hipcub::DeviceSelect::If(scratch, scratch_bytes, it, rows, count, (int)n, IsTrunc{terms}, s));
+}
+
+}  // namespace lk

@@ -1,0 +1,50 @@
+// example_main.cpp -- the reference's src/ExampleMain.cpp on the MI355X engine (one GPU rank).
+//
+// ExampleMain builds the 2v2 EnvSet (AdvancedObs, DefaultAction, the 13 weighted rewards,
+// NoTouch(8) + ScoreLimit(3), KickoffState; ExampleMain.cpp:128-226), sets the LearnerConfig /
+// PPOLearnerConfig of ExampleMain.cpp:340-430 and calls Learner::Start.  Here the plugin set is
+// the one built into the env kernel and the config is rlgpu_learner_default_config; the loop is
+// GGL::Learner::Start over a fixed number of iterations, printing the reference's report keys.
+//
+//   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--f32-gemm]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+
+#include "learner.hpp"
+
+int main(int argc, char** argv) {
+    rlgpu_learner_config cfg;
+    rlgpu_learner_default_config(&cfg);
+    long iterations = 3;
+    for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "--iterations") && i + 1 < argc) iterations = std::atol(argv[++i]);
+        else if (!std::strcmp(argv[i], "--arenas") && i + 1 < argc) cfg.num_arenas = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--rollout") && i + 1 < argc) cfg.rollout_len = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--f32-gemm")) cfg.train_gemm = RLGPU_GEMM_F32;
+        else {
+            std::fprintf(stderr, "usage: %s [--iterations N] [--arenas A] [--rollout T] [--f32-gemm]\n", argv[0]);
+            return 2;
+        }
+    }
+    try {
+        hipStream_t s = nullptr;
+        if (hipStreamCreate(&s) != hipSuccess) throw std::runtime_error("hipStreamCreate failed");
+        GGL::Learner learner(cfg, nullptr, s);
+        for (long it = 0; it < iterations; it++) {
+            rlgpu_learner_report r = learner.Iterate();
+            const double total = r.collect_s + r.consume_s + r.learn_s;
+            const double agentSteps = 4.0 * (double)r.env_steps;
+            std::printf("iteration %ld: Steps/Second %.0f (agent), env-steps/s %.0f, Collection Time %.3f s, "
+                        "Consumption Time %.3f s, PPO Learn Time %.3f s, Total Timesteps %lld\n",
+                        it + 1, agentSteps / total, (double)r.env_steps / total, r.collect_s, r.consume_s, r.learn_s,
+                        (long long)learner.stats.total_steps);
+        }
+        (void)hipStreamDestroy(s);
+    } catch (const std::exception& e) {  // ExampleMain.cpp:603-612
+        std::fprintf(stderr, "Exception thrown: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

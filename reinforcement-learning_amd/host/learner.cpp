@@ -1,0 +1,664 @@
+// learner.cpp -- the C++ host Learner (host/learner.hpp) and its C ABI (include/rlgpu_learner.h).
+//
+// One rank's GigaLearnCPP training loop (Learner::Start, GL/public/GigaLearnCPP/Learner.cpp:482-1056)
+// driving the HIP path through the rlgpu C ABI: bf16 policy inference + the fused env kernel with
+// the experience append (collection), critic + GAE + return statistics (consumption), and
+// PPOLearner::Learn (learning).  Nothing leaves HBM during an iteration except the handful of
+// scalars the host needs (truncation count, 150 return samples, distributed moments).
+#include "learner.hpp"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../csrc/common.hpp"
+#include "../csrc/learner_kernels.hpp"
+
+namespace {
+constexpr int OBS = RLGPU_OBS, ACT = RLGPU_ACTIONS;
+using clk = std::chrono::steady_clock;
+double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+inline void hipCheck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw rlgpu::Error(RLGPU_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// splitmix64 (Steele et al.): the counter-based generator of rlgpu_sample_indices
+inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+}  // namespace
+
+// ------------------------------------------------------------------ RLGC::EnvSetGPU
+namespace RLGC {
+
+EnvSetGPU::EnvSetGPU(const rlgpu_envset_config& cfg, hipStream_t stream) : stream_(stream) {
+    RlgpuCheck(rlgpu_envset_create(&cfg, &h_), "EnvSet");
+    RlgpuCheck(rlgpu_envset_buffers_get(h_, &state_), "EnvSet buffers");
+}
+EnvSetGPU::~EnvSetGPU() {
+    if (h_) rlgpu_envset_destroy(h_);
+}
+void EnvSetGPU::StepFirstHalf(bool) { RlgpuCheck(rlgpu_envset_step_first_half(h_, stream_), "StepFirstHalf"); }
+void EnvSetGPU::StepSecondHalf(const int32_t* d_actions, bool async) {
+    RlgpuCheck(rlgpu_envset_step_second_half(h_, d_actions, stream_), "StepSecondHalf");
+    if (!async) Sync();
+}
+void EnvSetGPU::Step(const int32_t* d_actions, const rlgpu_step_outputs* out) {
+    RlgpuCheck(rlgpu_envset_step(h_, d_actions, 1, out, stream_), "EnvSet step");
+}
+void EnvSetGPU::Sync() { RlgpuCheck(rlgpu_envset_sync(h_, stream_), "Sync"); }
+void EnvSetGPU::Reset() { RlgpuCheck(rlgpu_envset_reset(h_, stream_), "Reset"); }
+void EnvSetGPU::ResetArenas(const uint8_t* d_mask) {
+    RlgpuCheck(rlgpu_envset_reset_arenas(h_, d_mask, stream_), "ResetArena");
+}
+
+}  // namespace RLGC
+
+// ------------------------------------------------------------------ GGL
+namespace GGL {
+
+void WelfordStat::Increment(const float* xs, int64_t n) {
+    for (int64_t i = 0; i < n; i++) {  // WelfordStat.h:25-35
+        double delta = (double)xs[i] - mean;
+        double deltaN = delta / (double)(count + 1);
+        mean += deltaN;
+        m2 += delta * deltaN * (double)count;
+        count++;
+    }
+}
+double WelfordStat::GetSTD() const {  // WelfordStat.h:41-50
+    if (count < 2) return 1.0;
+    double var = m2 / (double)(count - 1);
+    if (var <= 0) var = 1.0;
+    return std::sqrt(var);
+}
+
+void MomentsMeanStd(const double* m, float* out) {
+    const double mean = m[0] / m[2];
+    double var = (m[1] - m[0] * mean) / (m[2] - 1);
+    if (!(var > 0)) var = 0;
+    out[0] = (float)mean;
+    out[1] = (float)std::sqrt(var);
+}
+
+std::vector<std::pair<int64_t, int64_t>> BatchRanges(int64_t expSize, int64_t batchSize, bool overbatching) {
+    std::vector<std::pair<int64_t, int64_t>> out;
+    if (expSize <= 0 || batchSize <= 0) return out;
+    for (int64_t start = 0; start < expSize; start += batchSize) {  // ExperienceBuffer.cpp:117-162
+        int64_t end = start + batchSize;
+        if (end + batchSize > expSize && overbatching) end = expSize;
+        if (end > expSize || end - start <= 0) break;
+        out.emplace_back(start, end);
+        if (end == expSize) break;
+    }
+    return out;
+}
+
+void ExperienceBuffer::Allocate(int T_, int P_) {
+    T = T_;
+    P = P_;
+    auto A = [&](size_t bytes) {
+        void* p = nullptr;
+        hipCheck(hipMalloc(&p, bytes + 16), "ExperienceBuffer alloc");
+        hipCheck(hipMemset(p, 0, bytes + 16), "ExperienceBuffer memset");
+        allocs.push_back(p);
+        return p;
+    };
+    const size_t TP = (size_t)T * P, T1P = (size_t)(T + 1) * P;
+    v.obs = (float*)A(T1P * OBS * 4);
+    v.masks = (uint8_t*)A(T1P * ACT);
+    v.actions = (int32_t*)A(TP * 4);
+    v.logp = (float*)A(TP * 4);
+    v.rewards = (float*)A(TP * 4);
+    v.terms = (int8_t*)A(TP);
+    v.trunc_obs = (float*)A(TP * OBS * 4);
+    v.values = (float*)A(T1P * 4);
+    v.trunc_vals = (float*)A(TP * 4);
+    v.adv = (float*)A(TP * 4);
+    v.target = (float*)A(TP * 4);
+    v.ret = (float*)A(TP * 4);
+    v.T = T;
+    v.P = P;
+}
+void ExperienceBuffer::Free() {
+    for (void* p : allocs) (void)hipFree(p);
+    allocs.clear();
+}
+
+PPOLearnerGPU::PPOLearnerGPU(const rlgpu_ppo_config& cfg, hipStream_t stream) : stream_(stream) {
+    RlgpuCheck(rlgpu_ppo_create(&cfg, &h_), "PPOLearner");
+    float* params = nullptr;
+    RlgpuCheck(rlgpu_ppo_buffers(h_, &params, &grads_, &nparams_), "PPOLearner buffers");
+    hipCheck(hipMalloc((void**)&adv_stats_, 2 * sizeof(float)), "adv stats");
+    hipCheck(hipMalloc((void**)&metrics_, RLGPU_NUM_METRICS * sizeof(float)), "metrics");
+    hipCheck(hipMemset(metrics_, 0, RLGPU_NUM_METRICS * sizeof(float)), "metrics");
+    RlgpuCheck(rlgpu_ppo_init_params(h_, cfg.seed, stream_), "init params");
+}
+PPOLearnerGPU::~PPOLearnerGPU() {
+    if (adv_stats_) (void)hipFree(adv_stats_);
+    if (metrics_) (void)hipFree(metrics_);
+    if (h_) rlgpu_ppo_destroy(h_);
+}
+void PPOLearnerGPU::InferActions(const float* d_obs, const uint8_t* d_masks, int n, bool det, uint64_t step,
+                                 int32_t* d_actions, float* d_logp, const uint8_t* d_old_rows) {
+    if (d_old_rows)
+        RlgpuCheck(rlgpu_ppo_infer_actions_mixed(h_, d_obs, d_masks, n, det, step, d_old_rows, d_actions, d_logp, stream_),
+                   "InferActions (old version)");
+    else
+        RlgpuCheck(rlgpu_ppo_infer_actions(h_, d_obs, d_masks, n, det, step, d_actions, d_logp, stream_), "InferActions");
+}
+void PPOLearnerGPU::InferCritic(const float* d_obs, int64_t n, float* d_values) {
+    RlgpuCheck(rlgpu_ppo_infer_critic(h_, d_obs, n, d_values, stream_), "InferCritic");
+}
+void PPOLearnerGPU::AdvantageStats(const float* d_adv, int64_t n) {
+    RlgpuCheck(rlgpu_mean_std(d_adv, n, adv_stats_, stream_), "advantage stats");
+}
+void PPOLearnerGPU::Minibatch(const float* d_obs, const uint8_t* d_masks, const int32_t* d_actions, const float* d_logp,
+                              const float* d_adv, const float* d_target, const int32_t* d_index, int64_t start, int n,
+                              int64_t batch) {
+    RlgpuCheck(rlgpu_ppo_minibatch(h_, d_obs, d_masks, d_actions, d_logp, d_adv, d_target, d_index, start, n, batch,
+                                   adv_stats_, metrics_, stream_),
+               "Learn minibatch");
+    minibatches++;
+}
+void PPOLearnerGPU::OptimizerStep() { RlgpuCheck(rlgpu_ppo_optimizer_step(h_, metrics_, stream_), "optimizer step"); }
+
+template <class T>
+T* Learner::Alloc(size_t count) {
+    void* p = nullptr;
+    hipCheck(hipMalloc(&p, count * sizeof(T) + 16), "Learner alloc");
+    allocs_.push_back(p);
+    return (T*)p;
+}
+
+Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, hipStream_t stream)
+    : s_(stream), cfg_(cfg) {
+    RLGPU_REQUIRE(cfg.num_arenas > 0 && cfg.rollout_len > 0 && cfg.epochs > 0 && cfg.mini_batch_size > 0,
+                  "Learner: num_arenas, rollout_len, epochs and mini_batch_size must be > 0");
+    RLGPU_REQUIRE(cfg.world >= 1 && cfg.rank >= 0 && cfg.rank < cfg.world, "Learner: bad rank / world");
+    RLGPU_REQUIRE(cfg.world == 1 || (coll && coll->allreduce_sum_f32 && coll->allreduce_sum_f64 && coll->allgather_f32),
+                  "Learner: world > 1 needs a complete rlgpu_collective");
+    RLGPU_REQUIRE(cfg.return_samples >= 0, "Learner: return_samples must be >= 0");
+    if (coll) {
+        coll_ = *coll;
+        hasColl_ = cfg.world > 1;
+    }
+    std::memset(&stats, 0, sizeof(stats));
+    const int T = cfg.rollout_len, N = cfg.num_arenas, P = 4 * N;
+    rlgpu_envset_config ec{};
+    ec.num_arenas = N;
+    ec.tick_skip = cfg.tick_skip;
+    ec.action_delay = cfg.action_delay;
+    ec.seed = cfg.seed * 1000003ull + (uint64_t)cfg.rank;
+    ec.save_rewards = 1;
+    ec.max_episode_steps = (int32_t)(cfg.max_episode_duration * (120.0f / (float)cfg.tick_skip));
+    ec.mesh_tris = cfg.mesh_tris;
+    ec.mesh_ntris = cfg.mesh_ntris;
+    ec.mesh_objects = cfg.mesh_objects;
+    ec.mesh_object_ntris = cfg.mesh_object_ntris;
+    env_ = new RLGC::EnvSetGPU(ec, s_);
+    rlgpu_ppo_config pc{};
+    pc.obs_size = OBS;
+    pc.num_actions = ACT;
+    std::memcpy(pc.policy_layers, cfg.policy_layers, sizeof(pc.policy_layers));
+    pc.n_policy_layers = cfg.n_policy_layers;
+    std::memcpy(pc.critic_layers, cfg.critic_layers, sizeof(pc.critic_layers));
+    pc.n_critic_layers = cfg.n_critic_layers;
+    pc.layer_norm = 1;
+    pc.leaky_slope = 0.01f;
+    pc.policy_lr = cfg.policy_lr;
+    pc.critic_lr = cfg.critic_lr;
+    pc.beta1 = 0.9f;
+    pc.beta2 = 0.999f;
+    pc.eps = 1e-8f;
+    pc.weight_decay = 1e-2f;
+    pc.clip_range = cfg.clip_range;
+    pc.entropy_scale = cfg.entropy_scale;
+    pc.max_grad_norm = 0.5f;
+    const int64_t TP = (int64_t)T * P;
+    pc.max_rows = (int32_t)std::max<int64_t>(std::min<int64_t>(cfg.mini_batch_size, TP), std::min<int64_t>(P, 65536));
+    pc.seed = cfg.seed;
+    pc.train_gemm = cfg.train_gemm;
+    ppo_ = new PPOLearnerGPU(pc, s_);
+    if (hasColl_) {  // identical initial weights on every rank: rank 0's (sum of zeros elsewhere)
+        float* params = nullptr;
+        float* g = nullptr;
+        int64_t n = 0;
+        RlgpuCheck(rlgpu_ppo_buffers(ppo_->handle(), &params, &g, &n), "buffers");
+        if (cfg.rank != 0) hipCheck(hipMemsetAsync(params, 0, n * sizeof(float), s_), "broadcast");
+        hipCheck(hipStreamSynchronize(s_), "sync");
+        if (coll_.allreduce_sum_f32(coll_.user, params, n) != 0)
+            throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: parameter broadcast failed");
+        RlgpuCheck(rlgpu_ppo_refresh_half(ppo_->handle(), s_), "refresh half");
+    }
+    exp_.Allocate(T, P);
+    // rollout row 0 = the env's initial obs / masks
+    const rlgpu_envset_buffers& st = env_->state();
+    hipCheck(hipMemcpyAsync(exp_.v.obs, st.obs, (size_t)P * OBS * 4, hipMemcpyDeviceToDevice, s_), "obs0");
+    hipCheck(hipMemcpyAsync(exp_.v.masks, st.action_masks, (size_t)P * ACT, hipMemcpyDeviceToDevice, s_), "masks0");
+    // self-play team masks (team of player p is p % 2)
+    std::vector<uint8_t> team(P);
+    for (int k = 0; k < 2; k++) {
+        oldRows_[k] = Alloc<uint8_t>(P);
+        for (int p = 0; p < P; p++) team[p] = (uint8_t)(p % 2 == k);
+        hipCheck(hipMemcpy(oldRows_[k], team.data(), P, hipMemcpyHostToDevice), "old rows");
+    }
+    trainRows_ = Alloc<int32_t>((size_t)TP / 2 + 1);
+    perm_ = Alloc<int32_t>(TP);
+    permRows_ = Alloc<int32_t>(TP);
+    badv_ = Alloc<float>(TP);
+    truncRows_ = Alloc<int32_t>(TP);
+    truncCount_ = Alloc<int32_t>(1);
+    selBytes_ = lk::select_trunc_scratch_bytes(TP);
+    selScratch_ = Alloc<char>(selBytes_);
+    sampleIdx_ = Alloc<int64_t>((size_t)std::max(1, cfg.return_samples));
+    samples_ = Alloc<float>((size_t)std::max(1, cfg.return_samples));
+    mom_ = (double*)Alloc<char>(4 * sizeof(double) + lk::moments_scratch_bytes());
+    hipCheck(hipStreamSynchronize(s_), "Learner init");
+}
+
+Learner::~Learner() {
+    if (s_) (void)hipStreamSynchronize(s_);
+    for (auto e : ev_) (void)hipEventDestroy(e);
+    for (void* p : allocs_) (void)hipFree(p);
+    if (truncObsC_) (void)hipFree(truncObsC_);
+    if (truncValC_) (void)hipFree(truncValC_);
+    exp_.Free();
+    delete ppo_;
+    delete env_;
+}
+
+void Learner::Collect() {
+    const int T = exp_.T, P = exp_.P;
+    const rlgpu_rollout_view& v = exp_.v;
+    const uint8_t* old = oldTeam_ >= 0 ? oldRows_[oldTeam_] : nullptr;
+    if (envTiming_ && ev_.size() < (size_t)2 * T) {
+        for (auto e : ev_) (void)hipEventDestroy(e);
+        ev_.assign(2 * T, nullptr);
+        for (auto& e : ev_) hipCheck(hipEventCreate(&e), "event");
+    }
+    for (int t = 0; t < T; t++) {
+        const size_t r = (size_t)t * P;
+        ppo_->InferActions(v.obs + r * OBS, v.masks + r * ACT, P, cfg_.deterministic != 0, (uint64_t)stats.rng_step,
+                           v.actions + r, v.logp + r, old);
+        stats.rng_step++;
+        rlgpu_step_outputs o{v.obs + (r + P) * OBS, v.masks + (r + P) * ACT, v.rewards + r, v.terms + r,
+                             v.trunc_obs + r * OBS};
+        if (envTiming_) hipCheck(hipEventRecord(ev_[2 * t], s_), "event");
+        env_->Step(v.actions + r, &o);
+        if (envTiming_) hipCheck(hipEventRecord(ev_[2 * t + 1], s_), "event");
+    }
+}
+
+void Learner::Consume() {
+    const int T = exp_.T, P = exp_.P;
+    const int64_t TP = (int64_t)T * P;
+    const rlgpu_rollout_view& v = exp_.v;
+    ppo_->InferCritic(v.obs, TP + P, v.values);  // InferCriticBatched over obs[0..T]
+    // truncation values only where a trajectory was truncated (code 2): Learner.cpp:944
+    lk::select_trunc(v.terms, TP, selScratch_, selBytes_, truncRows_, truncCount_, s_);
+    int32_t ntr = 0;
+    hipCheck(hipMemcpyAsync(&ntr, truncCount_, sizeof(int32_t), hipMemcpyDeviceToHost, s_), "trunc count");
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    if (ntr > 0) {
+        if (ntr > truncCap_) {
+            if (truncObsC_) (void)hipFree(truncObsC_);
+            if (truncValC_) (void)hipFree(truncValC_);
+            truncCap_ = std::max<int64_t>(ntr, 2 * truncCap_);
+            hipCheck(hipMalloc((void**)&truncObsC_, (size_t)truncCap_ * OBS * 4), "trunc obs");
+            hipCheck(hipMalloc((void**)&truncValC_, (size_t)truncCap_ * 4), "trunc vals");
+        }
+        lk::gather_rows(v.trunc_obs, OBS, truncRows_, ntr, truncObsC_, s_);
+        ppo_->InferCritic(truncObsC_, ntr, truncValC_);
+        lk::scatter_f32(truncValC_, truncRows_, ntr, v.trunc_vals, s_);
+    }
+    const float std_ = (float)returnStat.GetSTD();
+    RlgpuCheck(rlgpu_gae_rollout(v.rewards, v.terms, v.values, v.trunc_vals, v.values + TP, T, P, cfg_.gamma,
+                                 cfg_.gae_lambda, std_, cfg_.reward_clip_range, v.adv, v.target, v.ret, nullptr, s_),
+               "GAE");
+    // return-std Welford over randomly sampled returns (Learner.cpp:959-967); in an old-version
+    // iteration only the current policy's players have trajectories
+    const int k = cfg_.return_samples;
+    if (k <= 0) return;
+    std::vector<int64_t> idx(k);
+    const int64_t range = oldTeam_ < 0 ? TP : TP / 2;
+    rlgpu_sample_indices(cfg_.seed, cfg_.rank, stats.iteration, range, k, idx.data());
+    if (oldTeam_ >= 0) {
+        const int half = P / 2, team = 1 - oldTeam_;
+        for (auto& j : idx) j = (j / half) * P + 2 * (j % half) + team;
+    }
+    hipCheck(hipMemcpyAsync(sampleIdx_, idx.data(), k * sizeof(int64_t), hipMemcpyHostToDevice, s_), "sample idx");
+    lk::gather_samples(v.ret, sampleIdx_, k, samples_, s_);
+    std::vector<float> hs(k);
+    hipCheck(hipMemcpyAsync(hs.data(), samples_, k * sizeof(float), hipMemcpyDeviceToHost, s_), "samples");
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    if (hasColl_) {
+        std::vector<float> all((size_t)k * cfg_.world);
+        if (coll_.allgather_f32(coll_.user, hs.data(), k, all.data()) != 0)
+            throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: return-sample all-gather failed");
+        returnStat.Increment(all.data(), (int64_t)all.size());
+    } else {
+        returnStat.Increment(hs.data(), k);
+    }
+}
+
+void Learner::AllReduceGrads() {
+    if (!hasColl_) return;
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    if (coll_.allreduce_sum_f32(coll_.user, ppo_->grads(), ppo_->num_params()) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: gradient all-reduce failed");
+}
+
+// batch advantage normalisation (PPOLearner.cpp:360-371): (mean, unbiased std) of the batch's
+// advantages, global over ranks in fp64
+void Learner::BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int64_t n) {
+    if (!hasColl_) {
+        if (d_idx) {
+            lk::gather_f32(d_adv, d_idx, n, badv_, s_);
+            ppo_->AdvantageStats(badv_, n);
+        } else {
+            ppo_->AdvantageStats(d_adv, n);
+        }
+        return;
+    }
+    lk::moments_f64(d_adv, d_idx, n, mom_ + 4, mom_, s_);
+    double m[3];
+    hipCheck(hipMemcpyAsync(m, mom_, sizeof(m), hipMemcpyDeviceToHost, s_), "moments");
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    if (coll_.allreduce_sum_f64(coll_.user, m, 3) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: advantage-moment all-reduce failed");
+    float st[2];
+    MomentsMeanStd(m, st);
+    hipCheck(hipMemcpyAsync(ppo_->adv_stats(), st, sizeof(st), hipMemcpyHostToDevice, s_), "adv stats");
+    hipCheck(hipStreamSynchronize(s_), "sync");
+}
+
+void Learner::Learn() {
+    const int T = exp_.T, P = exp_.P;
+    const rlgpu_rollout_view& v = exp_.v;
+    const bool rows = oldTeam_ >= 0;
+    const int64_t M = rows ? (int64_t)T * (P / 2) : (int64_t)T * P;
+    const int64_t globalM = M * cfg_.world;
+    const int64_t batch = cfg_.batch_size > 0 ? cfg_.batch_size : globalM;
+    const int64_t localBatch = cfg_.batch_size > 0 ? std::max<int64_t>(1, cfg_.batch_size / cfg_.world) : M;
+    if (rows) lk::train_rows(T, P, 1 - oldTeam_, trainRows_, s_);
+    for (int epoch = 0; epoch < cfg_.epochs; epoch++) {
+        RlgpuCheck(rlgpu_permutation(M, cfg_.seed + (uint64_t)cfg_.rank, (uint64_t)(stats.iteration * cfg_.epochs + epoch),
+                                     perm_, s_),
+                   "shuffle");
+        const int32_t* order = perm_;
+        if (rows) {
+            lk::compose(trainRows_, perm_, M, permRows_, s_);
+            order = permRows_;
+        }
+        for (auto [b0, b1] : BatchRanges(M, localBatch, cfg_.overbatching != 0)) {
+            const bool whole = !rows && b0 == 0 && b1 == M;
+            BatchAdvantageStats(v.adv, whole ? nullptr : order + b0, b1 - b0);
+            for (int64_t s0 = b0; s0 < b1; s0 += cfg_.mini_batch_size) {
+                const int n = (int)std::min<int64_t>(cfg_.mini_batch_size, b1 - s0);
+                ppo_->Minibatch(v.obs, v.masks, v.actions, v.logp, v.adv, v.target, order, s0, n, batch);
+            }
+            AllReduceGrads();  // RCCL over xGMI (via the collective), before clip_grad_norm_
+            ppo_->OptimizerStep();
+        }
+    }
+}
+
+void Learner::FinishIteration() {
+    const int T = exp_.T, P = exp_.P;
+    const rlgpu_rollout_view& v = exp_.v;
+    hipCheck(hipMemcpyAsync(v.obs, v.obs + (size_t)T * P * OBS, (size_t)P * OBS * 4, hipMemcpyDeviceToDevice, s_), "obs");
+    hipCheck(hipMemcpyAsync(v.masks, v.masks + (size_t)T * P * ACT, (size_t)P * ACT, hipMemcpyDeviceToDevice, s_), "masks");
+    stats.iteration++;
+    const int64_t realPlayers = oldTeam_ < 0 ? P : P / 2;  // numRealPlayers (Learner.cpp:629)
+    stats.total_steps += (int64_t)T * realPlayers * cfg_.world;
+}
+
+rlgpu_learner_report Learner::Iterate() {
+    rlgpu_learner_report r{};
+    auto t0 = clk::now();
+    Collect();
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    auto t1 = clk::now();
+    Consume();
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    auto t2 = clk::now();
+    Learn();
+    FinishIteration();
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    auto t3 = clk::now();
+    r.collect_s = secs(t0, t1);
+    r.consume_s = secs(t1, t2);
+    r.learn_s = secs(t2, t3);
+    r.env_steps = (int64_t)exp_.T * cfg_.num_arenas;
+    if (envTiming_ && !ev_.empty()) {
+        double ms = 0;
+        for (int t = 0; t < exp_.T; t++) {
+            float x = 0;
+            hipCheck(hipEventElapsedTime(&x, ev_[2 * t], ev_[2 * t + 1]), "elapsed");
+            ms += x;
+        }
+        r.env_kernel_ms = ms / exp_.T;
+    }
+    return r;
+}
+
+void Learner::Start(int64_t iterations) {
+    for (int64_t i = 0; i < iterations; i++) Iterate();
+}
+
+}  // namespace GGL
+
+// ------------------------------------------------------------------ C ABI
+struct rlgpu_learner {
+    GGL::Learner* L = nullptr;
+};
+
+extern "C" int rlgpu_learner_default_config(rlgpu_learner_config* c) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(c, "null config");
+        std::memset(c, 0, sizeof(*c));
+        c->num_arenas = 4096;  // C2 (BASELINE.json configs[1])
+        c->tick_skip = 8;      // ExampleMain.cpp:356-358
+        c->action_delay = 7;
+        c->seed = 123;
+        c->max_episode_duration = 300.f;
+        c->rollout_len = 128;
+        c->epochs = 2;  // ExampleMain.cpp:404-430
+        c->mini_batch_size = 50000;
+        c->batch_size = 0;
+        c->overbatching = 1;
+        c->gamma = 0.99f;
+        c->gae_lambda = 0.95f;
+        c->clip_range = 0.2f;
+        c->entropy_scale = 0.035f;
+        c->policy_lr = 2.5e-4f;
+        c->critic_lr = 2.5e-4f;
+        c->reward_clip_range = 200.f;
+        c->return_samples = 150;
+        c->policy_layers[0] = c->policy_layers[1] = 512;
+        c->n_policy_layers = 2;
+        c->critic_layers[0] = c->critic_layers[1] = 512;
+        c->n_critic_layers = 2;
+        c->train_gemm = RLGPU_GEMM_F32X6;
+        c->rank = 0;
+        c->world = 1;
+    });
+}
+
+extern "C" int rlgpu_learner_create(const rlgpu_learner_config* cfg, const rlgpu_collective* coll, void* stream,
+                                    rlgpu_learner** out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(cfg && out, "rlgpu_learner_create: null argument");
+        auto* h = new rlgpu_learner();
+        try {
+            h->L = new GGL::Learner(*cfg, coll, rlgpu::as_stream(stream));
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+extern "C" int rlgpu_learner_destroy(rlgpu_learner* h) {
+    return rlgpu::guarded([&] {
+        if (!h) return;
+        delete h->L;
+        delete h;
+    });
+}
+
+#define RLGPU_LEARNER(h) RLGPU_REQUIRE((h) && (h)->L, "null learner handle")
+
+extern "C" int rlgpu_learner_handles(rlgpu_learner* h, rlgpu_envset** env, rlgpu_ppo** ppo) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        if (env) *env = h->L->env().handle();
+        if (ppo) *ppo = h->L->ppo().handle();
+    });
+}
+extern "C" int rlgpu_learner_rollout(rlgpu_learner* h, rlgpu_rollout_view* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        RLGPU_REQUIRE(out, "null output");
+        *out = h->L->exp().v;
+    });
+}
+extern "C" int rlgpu_learner_iterate(rlgpu_learner* h, rlgpu_learner_report* rep) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        rlgpu_learner_report r = h->L->Iterate();
+        if (rep) *rep = r;
+    });
+}
+extern "C" int rlgpu_learner_collect(rlgpu_learner* h) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->Collect();
+    });
+}
+extern "C" int rlgpu_learner_consume(rlgpu_learner* h) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->Consume();
+    });
+}
+extern "C" int rlgpu_learner_learn(rlgpu_learner* h) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->Learn();
+    });
+}
+extern "C" int rlgpu_learner_finish_iteration(rlgpu_learner* h) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->FinishIteration();
+    });
+}
+extern "C" int rlgpu_learner_set_old_team(rlgpu_learner* h, int32_t team) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        RLGPU_REQUIRE(team >= -1 && team <= 1, "team must be -1, 0 or 1");
+        h->L->SetOldTeam(team);
+    });
+}
+extern "C" int rlgpu_learner_get_stats(rlgpu_learner* h, rlgpu_learner_stats* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        RLGPU_REQUIRE(out, "null output");
+        *out = h->L->stats;
+        out->return_n = h->L->returnStat.count;
+        out->return_mean = h->L->returnStat.mean;
+        out->return_m2 = h->L->returnStat.m2;
+    });
+}
+extern "C" int rlgpu_learner_set_stats(rlgpu_learner* h, const rlgpu_learner_stats* in) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        RLGPU_REQUIRE(in && in->return_n >= 0 && in->iteration >= 0, "bad stats");
+        h->L->stats = *in;
+        h->L->returnStat.count = in->return_n;
+        h->L->returnStat.mean = in->return_mean;
+        h->L->returnStat.m2 = in->return_m2;
+    });
+}
+extern "C" int rlgpu_learner_metrics(rlgpu_learner* h, float* h_out, int64_t* count, int32_t reset) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        GGL::PPOLearnerGPU& p = h->L->ppo();
+        hipStream_t s = nullptr;
+        if (h_out) {
+            RLGPU_CHECK_HIP(hipDeviceSynchronize());
+            RLGPU_CHECK_HIP(hipMemcpy(h_out, p.metrics(), RLGPU_NUM_METRICS * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        if (count) *count = p.minibatches;
+        if (reset) {
+            RLGPU_CHECK_HIP(hipMemsetAsync(p.metrics(), 0, RLGPU_NUM_METRICS * sizeof(float), s));
+            RLGPU_CHECK_HIP(hipDeviceSynchronize());
+            p.minibatches = 0;
+        }
+    });
+}
+
+extern "C" int rlgpu_moments_mean_std(const double* m3, float* out2) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(m3 && out2 && m3[2] > 1, "rlgpu_moments_mean_std: bad argument");
+        GGL::MomentsMeanStd(m3, out2);
+    });
+}
+
+extern "C" int rlgpu_learner_set_env_timing(rlgpu_learner* h, int32_t enable) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->SetEnvTiming(enable != 0);
+    });
+}
+
+extern "C" int64_t rlgpu_batch_ranges(int64_t exp_size, int64_t batch_size, int32_t overbatching, int64_t* out,
+                                      int64_t max_ranges) {
+    auto r = GGL::BatchRanges(exp_size, batch_size, overbatching != 0);
+    for (int64_t i = 0; i < (int64_t)r.size() && i < max_ranges; i++) {
+        out[2 * i] = r[i].first;
+        out[2 * i + 1] = r[i].second;
+    }
+    return (int64_t)r.size();
+}
+
+extern "C" int rlgpu_welford_add(int64_t* count, double* mean, double* m2, const float* xs, int64_t n) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(count && mean && m2 && (xs || n == 0) && n >= 0, "rlgpu_welford_add: bad argument");
+        GGL::WelfordStat w;
+        w.count = *count;
+        w.mean = *mean;
+        w.m2 = *m2;
+        w.Increment(xs, n);
+        *count = w.count;
+        *mean = w.mean;
+        *m2 = w.m2;
+    });
+}
+
+extern "C" double rlgpu_welford_std(int64_t count, double m2) {
+    GGL::WelfordStat w;
+    w.count = count;
+    w.m2 = m2;
+    return w.GetSTD();
+}
+
+extern "C" int rlgpu_sample_indices(uint64_t seed, int32_t rank, int64_t iteration, int64_t range, int32_t n,
+                                    int64_t* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(out && n >= 0 && range > 0, "rlgpu_sample_indices: bad argument");
+        const uint64_t key = splitmix64(seed ^ splitmix64(((uint64_t)(uint32_t)rank << 40) ^ (uint64_t)iteration));
+        for (int32_t i = 0; i < n; i++) {
+            const uint64_t x = splitmix64(key + (uint64_t)i);
+            out[i] = (int64_t)(((unsigned __int128)x * (unsigned __int128)(uint64_t)range) >> 64);
+        }
+    });
+}

@@ -1,0 +1,182 @@
+// learner.hpp -- C++ host API of the MI355X rollout engine: the GigaLearnCPP Learner /
+// ExperienceBuffer / WelfordStat and the RLGymCPP EnvSet surface over the rlgpu C ABI.
+//
+// This is the host code the reference's src/ExampleMain.cpp drops onto (host/example_main.cpp
+// mirrors it).  Every C-ABI status is turned back into std::runtime_error, so the reference's
+// try/catch (Learner.cpp:466-474, ExampleMain.cpp:603-612) keeps its behaviour.
+//
+// Reference map (GigaLearnCPP/RLGymCPP, paths as SURVEY.md):
+//   RLGC::EnvSetGPU      RG/EnvSet/EnvSet.h:67-124        (EnvSet: StepFirstHalf / StepSecondHalf /
+//                                                           Sync / Reset / ResetArena / state)
+//   GGL::WelfordStat     GL/private/GigaLearnCPP/Util/WelfordStat.h:7-67
+//   GGL::ExperienceBuffer GL/private/GigaLearnCPP/PPO/ExperienceBuffer.{h,cpp} ([T, P] in HBM)
+//   GGL::PPOLearnerGPU   GL/private/GigaLearnCPP/PPO/PPOLearner.{h,cpp}
+//   GGL::Learner         GL/public/GigaLearnCPP/Learner.{h,cpp}
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/rlgpu_env.h"
+#include "../../include/rlgpu_gae.h"
+#include "../../include/rlgpu_learner.h"
+#include "../../include/rlgpu_ppo.h"
+
+namespace RLGC {
+
+inline void RlgpuCheck(int st, const char* what) {
+    if (st != RLGPU_OK) throw std::runtime_error(std::string(what) + ": " + rlgpu_last_error());
+}
+
+// RLGC::EnvSet on the device (EnvSet.h:67-124): the ExampleMain plugin set built in.
+class EnvSetGPU {
+public:
+    EnvSetGPU(const rlgpu_envset_config& cfg, hipStream_t stream);
+    ~EnvSetGPU();
+    EnvSetGPU(const EnvSetGPU&) = delete;
+    EnvSetGPU& operator=(const EnvSetGPU&) = delete;
+
+    void StepFirstHalf(bool async = true);                        // EnvSet.cpp:113-130
+    void StepSecondHalf(const int32_t* d_actions, bool async);    // EnvSet.cpp:132-273
+    void Step(const int32_t* d_actions, const rlgpu_step_outputs* out);  // fused + reset + append
+    void Sync();                                                  // EnvSet.h:107
+    void Reset();                                                 // EnvSet.cpp:331-354
+    void ResetArenas(const uint8_t* d_mask);                      // EnvSet.cpp:275-329
+
+    rlgpu_envset* handle() const { return h_; }
+    const rlgpu_envset_buffers& state() const { return state_; }  // EnvSet::state (device views)
+
+private:
+    rlgpu_envset* h_ = nullptr;
+    rlgpu_envset_buffers state_{};
+    hipStream_t stream_;
+};
+
+}  // namespace RLGC
+
+namespace GGL {
+
+using RLGC::RlgpuCheck;
+
+// WelfordStat.h:7-67: fp64 running mean / variance in the reference's update order.
+struct WelfordStat {
+    int64_t count = 0;
+    double mean = 0, m2 = 0;
+    void Increment(const float* xs, int64_t n);
+    double GetMean() const { return count < 2 ? 0.0 : mean; }
+    double GetSTD() const;
+};
+
+// (mean, unbiased std) from fp64 (sum, sum of squares, count): PPOLearner.cpp:360-371 over ranks
+void MomentsMeanStd(const double* m3, float* out2);
+
+// ExperienceBuffer::GetAllBatchesShuffled boundaries (ExperienceBuffer.cpp:117-162).
+std::vector<std::pair<int64_t, int64_t>> BatchRanges(int64_t expSize, int64_t batchSize, bool overbatching);
+
+// The rollout ([T, P] time-major) in HBM; every collected step is trained in the iteration that
+// collected it (the unfinished tail bootstrapped from V(obs_T), DESIGN.md Deviations 5).
+struct ExperienceBuffer {
+    int T = 0, P = 0;
+    rlgpu_rollout_view v{};
+    std::vector<void*> allocs;
+    void Allocate(int T, int P);
+    void Free();
+};
+
+// PPOLearner (PPOLearner.h:41-59) over rlgpu_ppo.
+class PPOLearnerGPU {
+public:
+    PPOLearnerGPU(const rlgpu_ppo_config& cfg, hipStream_t stream);
+    ~PPOLearnerGPU();
+    PPOLearnerGPU(const PPOLearnerGPU&) = delete;
+    PPOLearnerGPU& operator=(const PPOLearnerGPU&) = delete;
+
+    void InferActions(const float* d_obs, const uint8_t* d_masks, int n, bool deterministic, uint64_t step,
+                      int32_t* d_actions, float* d_logp, const uint8_t* d_old_rows = nullptr);
+    void InferCritic(const float* d_obs, int64_t n, float* d_values);
+    void AdvantageStats(const float* d_adv, int64_t n);  // (mean, unbiased std) -> adv_stats
+    void Minibatch(const float* d_obs, const uint8_t* d_masks, const int32_t* d_actions, const float* d_logp,
+                   const float* d_adv, const float* d_target, const int32_t* d_index, int64_t start, int n,
+                   int64_t batch);
+    void OptimizerStep();
+    int64_t minibatches = 0;  // summed into metrics() since the last reset
+
+    rlgpu_ppo* handle() const { return h_; }
+    float* grads() const { return grads_; }
+    int64_t num_params() const { return nparams_; }
+    float* adv_stats() const { return adv_stats_; }
+    float* metrics() const { return metrics_; }
+
+private:
+    rlgpu_ppo* h_ = nullptr;
+    hipStream_t stream_;
+    float* grads_ = nullptr;
+    int64_t nparams_ = 0;
+    float* adv_stats_ = nullptr;  // device [2]
+    float* metrics_ = nullptr;    // device [RLGPU_NUM_METRICS]
+};
+
+// GGL::Learner (Learner.h:11-45): one rank's training loop.
+class Learner {
+public:
+    Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, hipStream_t stream);
+    ~Learner();
+    Learner(const Learner&) = delete;
+    Learner& operator=(const Learner&) = delete;
+
+    void Collect();           // Learner.cpp:669-861
+    void Consume();           // Learner.cpp:863-990
+    void Learn();             // PPOLearner::Learn, PPOLearner.cpp:278-581
+    void FinishIteration();   // obs[0] <- obs[T], step counters
+    rlgpu_learner_report Iterate();
+    void Start(int64_t iterations);  // Learner::Start loop (Learner.cpp:482-1056), a fixed count
+
+    void SetOldTeam(int team) { oldTeam_ = team; }
+    void SetEnvTiming(bool on) { envTiming_ = on; }
+
+    const rlgpu_learner_config& config() const { return cfg_; }
+    RLGC::EnvSetGPU& env() { return *env_; }
+    PPOLearnerGPU& ppo() { return *ppo_; }
+    ExperienceBuffer& exp() { return exp_; }
+    rlgpu_learner_stats stats;
+    WelfordStat returnStat;
+
+private:
+    void AllReduceGrads();
+    void BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int64_t n);
+    hipStream_t s_;
+    rlgpu_learner_config cfg_;
+    rlgpu_collective coll_{};
+    bool hasColl_ = false;
+    RLGC::EnvSetGPU* env_ = nullptr;
+    PPOLearnerGPU* ppo_ = nullptr;
+    ExperienceBuffer exp_;
+    int oldTeam_ = -1;
+    bool envTiming_ = false;
+    std::vector<hipEvent_t> ev_;
+    // device scratch
+    uint8_t* oldRows_[2] = {nullptr, nullptr};
+    int32_t* trainRows_ = nullptr;
+    int32_t* perm_ = nullptr;
+    int32_t* permRows_ = nullptr;
+    float* badv_ = nullptr;
+    int32_t* truncRows_ = nullptr;
+    int32_t* truncCount_ = nullptr;
+    void* selScratch_ = nullptr;
+    size_t selBytes_ = 0;
+    float* truncObsC_ = nullptr;
+    float* truncValC_ = nullptr;
+    int64_t truncCap_ = 0;
+    int64_t* sampleIdx_ = nullptr;
+    float* samples_ = nullptr;
+    double* mom_ = nullptr;   // [3] + scratch
+    std::vector<void*> allocs_;
+    template <class T>
+    T* Alloc(size_t count);
+};
+
+}  // namespace GGL

@@ -62,7 +62,8 @@ def alias(ptr, shape, dtype, device):
 
     class _Holder:
         __cuda_array_interface__ = {
-            "shape": (n,), "typestr": {torch.float32: "<f4", torch.uint8: "|u1", torch.int32: "<i4"}[dtype],
+            "shape": (n,), "typestr": {torch.float32: "<f4", torch.uint8: "|u1", torch.int32: "<i4",
+                                       torch.int8: "|i1", torch.float64: "<f8", torch.int64: "<i8"}[dtype],
             "data": (ptr, False), "version": 2, "strides": (elt,)}
 
     t = torch.as_tensor(_Holder(), device=device)

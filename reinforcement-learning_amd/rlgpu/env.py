@@ -102,22 +102,40 @@ class EnvSet:
         h = ctypes.c_void_p()
         _lib.check(L.rlgpu_envset_create(ctypes.byref(cfg), ctypes.byref(h)), "rlgpu_envset_create")
         self._h = h
-        self.num_arenas = num_arenas
-        self.num_players = 4 * num_arenas
         self.tick_skip, self.action_delay = tick_skip, action_delay
+        self._alias_buffers(L)
+
+    @classmethod
+    def wrap(cls, handle, device, tick_skip=8, action_delay=7, owner=None):
+        """An EnvSet view of a handle owned elsewhere (the C++ Learner's RLGC::EnvSetGPU)."""
+        import torch
+        L = _bind()
+        self = cls.__new__(cls)
+        self._h, self._owned, self._owner = ctypes.c_void_p(handle), False, owner
+        self.device = torch.device(device)
+        self.tick_skip, self.action_delay = tick_skip, action_delay
+        self._alias_buffers(L)
+        return self
+
+    _owned = True
+
+    def _alias_buffers(self, L):
+        import torch
         b = _Buffers()
-        _lib.check(L.rlgpu_envset_buffers_get(h, ctypes.byref(b)), "rlgpu_envset_buffers_get")
-        P, dev = self.num_players, self.device
+        _lib.check(L.rlgpu_envset_buffers_get(self._h, ctypes.byref(b)), "rlgpu_envset_buffers_get")
+        self.num_arenas, self.num_players = b.num_arenas, b.num_players
+        P, N, dev = b.num_players, b.num_arenas, self.device
         self.obs = _alias(b.obs, (P, OBS), torch.float32, dev)
         self.action_masks = _alias(b.action_masks, (P, ACTIONS), torch.uint8, dev)
         self.rewards = _alias(b.rewards, (P,), torch.float32, dev)
-        self.terminals = _alias(b.terminals, (num_arenas,), torch.uint8, dev)
-        self.last_rewards = _alias(b.last_rewards, (num_arenas, REWARDS), torch.float32, dev)
+        self.terminals = _alias(b.terminals, (N,), torch.uint8, dev)
+        self.last_rewards = _alias(b.last_rewards, (N, REWARDS), torch.float32, dev)
         self.trunc_obs = _alias(b.trunc_obs, (P, OBS), torch.float32, dev)
 
     def close(self):
         if getattr(self, "_h", None):
-            _lib.check(_lib.lib().rlgpu_envset_destroy(self._h), "rlgpu_envset_destroy")
+            if self._owned:
+                _lib.check(_lib.lib().rlgpu_envset_destroy(self._h), "rlgpu_envset_destroy")
             self._h = None
 
     def __del__(self):

@@ -1,87 +1,92 @@
-"""Learner -- the GigaLearnCPP training loop for one GPU rank, every array resident in HBM.
+"""Learner -- Python binding of the C++ host Learner (reinforcement-learning_amd/host/learner.cpp,
+include/rlgpu_learner.h): the GigaLearnCPP training loop for one GPU rank, every array resident
+in HBM.
 
-Mirrors GGL::Learner::Start (GigaLearnCPP/src/public/GigaLearnCPP/Learner.cpp:482-1056):
+The loop itself (GGL::Learner::Start, GigaLearnCPP/src/public/GigaLearnCPP/Learner.cpp:482-1056)
+is C++:
   collection   infer actions (bf16 policy) -> fused env step with experience append     :669-861
   consumption  critic over the rollout (InferCriticBatched), GAE, return-std Welford    :863-990
   learning     PPOLearner::Learn: epochs x shuffled minibatches, clip_grad_norm_, AdamW :990-1000
-Distributed: one Learner per rank (arenas sharded), PPO gradients all-reduced (sum) over
-RCCL before clip_grad_norm_; advantage moments and return samples reduced too.
+This module adds what sits around it in the reference: the config object, torch views of the
+rollout buffers, checkpoints (rlgpu/checkpoint.py) and the old-version manager for self-play
+(rlgpu/versions.py).  Distributed: the C++ Learner's exchanges go through rlgpu/dist.py's
+TorchCollective (RCCL over xGMI on MI355X).
 
 Experience layout ([T, P] time-major, P = 4 * arenas): the reference keeps per-player
 trajectory vectors and trains only on finished trajectories (unfinished ones carry over to the
 next iteration); here every collected step is trained in the iteration that collected it, with
 the unfinished tail bootstrapped from V(obs_T) -- see DESIGN.md "Deviations".
 """
-import math
+import ctypes
 import time
 
 import numpy as np
 
-from . import dist as _dist
-from . import gae as _gae
-from .env import EnvSet, StepOutputs
-from .ppo import PPO, permutation
+from . import _lib
+from .ppo import MAX_LAYERS, NUM_METRICS
 
 OBS, ACTIONS = 167, 90
 
 
+# ------------------------------------------------------------------ host building blocks (C++)
+def _host_lib():
+    L = _lib.lib()
+    i64p, f64p = ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
+    L.rlgpu_batch_ranges.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
+    L.rlgpu_batch_ranges.restype = ctypes.c_int64
+    L.rlgpu_welford_add.argtypes = [i64p, f64p, f64p, ctypes.c_void_p, ctypes.c_int64]
+    L.rlgpu_welford_std.argtypes = [ctypes.c_int64, ctypes.c_double]
+    L.rlgpu_welford_std.restype = ctypes.c_double
+    L.rlgpu_sample_indices.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.c_void_p]
+    return L
+
+
 class WelfordStat:
-    """GGL::WelfordStat (Util/WelfordStat.h:7-67): fp64 running mean / variance, the reference's
-    update order (delta, delta / (count + 1), variance += delta * deltaN * count)."""
+    """GGL::WelfordStat (Util/WelfordStat.h:7-67) -- the C++ implementation (host/learner.cpp),
+    fp64 state in the reference's update order."""
 
     def __init__(self):
         self.n, self.mean, self.m2 = 0, 0.0, 0.0
 
     def add(self, xs):
-        for x in np.asarray(xs, np.float32).ravel():
-            delta = float(x) - self.mean
-            delta_n = delta / (self.n + 1)
-            self.mean += delta_n
-            self.m2 += delta * delta_n * self.n
-            self.n += 1
+        x = np.ascontiguousarray(np.asarray(xs, np.float32).ravel())
+        c, m, s = ctypes.c_int64(self.n), ctypes.c_double(self.mean), ctypes.c_double(self.m2)
+        _lib.check(_host_lib().rlgpu_welford_add(ctypes.byref(c), ctypes.byref(m), ctypes.byref(s), x.ctypes.data, x.size),
+                   "rlgpu_welford_add")
+        self.n, self.mean, self.m2 = c.value, m.value, s.value
 
     def get_mean(self):
         return 0.0 if self.n < 2 else self.mean
 
     def std(self):
-        if self.n < 2:
-            return 1.0
-        var = self.m2 / (self.n - 1)
-        if var <= 0:
-            var = 1.0
-        return math.sqrt(var)
+        return _host_lib().rlgpu_welford_std(self.n, self.m2)
 
     def to_json(self):  # WelfordStat::ToJSON
         return {"mean": self.mean, "var": self.m2, "count": self.n}
 
     def read_json(self, j):  # WelfordStat::ReadFromJSON
-        self.mean, self.m2, self.n = float(j["mean"]), float(j["var"]), int(j["count"])
+        self.n, self.mean, self.m2 = int(j["count"]), float(j["mean"]), float(j["var"])
 
 
 def batch_ranges(exp_size, batch_size, overbatching=True):
-    """ExperienceBuffer::GetAllBatchesShuffled batch boundaries (ExperienceBuffer.cpp:117-162):
-    consecutive [start, start + batch) slices of the shuffled order; with overbatching the last
-    batch absorbs a remainder that would leave less than one more full batch; without it the
-    remainder is dropped."""
-    out = []
-    if exp_size <= 0:
-        return out
-    start = 0
-    while start < exp_size:
-        end = start + batch_size
-        if end + batch_size > exp_size and overbatching:
-            end = exp_size
-        if end > exp_size:
-            break
-        if end - start <= 0:
-            break
-        out.append((start, end))
-        if end == exp_size:
-            break
-        start += batch_size
-    return out
+    """ExperienceBuffer::GetAllBatchesShuffled batch boundaries (ExperienceBuffer.cpp:117-162),
+    from the C++ ExperienceBuffer (GGL::BatchRanges)."""
+    L = _host_lib()
+    n = L.rlgpu_batch_ranges(exp_size, batch_size, int(overbatching), None, 0)
+    out = np.zeros(2 * max(n, 1), np.int64)
+    L.rlgpu_batch_ranges(exp_size, batch_size, int(overbatching), out.ctypes.data, n)
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
 
 
+def sample_indices(seed, rank, iteration, rng, n):
+    """rlgpu_sample_indices: the return-sample draws of one iteration."""
+    out = np.zeros(max(n, 1), np.int64)
+    _lib.check(_host_lib().rlgpu_sample_indices(seed, rank, iteration, rng, n, out.ctypes.data), "rlgpu_sample_indices")
+    return out[:n]
+
+
+# ------------------------------------------------------------------ config
 class LearnerConfig:
     """The subset of GGL::LearnerConfig / PPOLearnerConfig on the hot path (ExampleMain values)."""
 
@@ -107,6 +112,7 @@ class LearnerConfig:
         self.critic_layers = (512, 512)
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
+        self.train_gemm = 0               # rlgpu_ppo_config.train_gemm: 0 = f32 via bf16x3 split, 1 = f32 MFMA
         # checkpoints (LearnerConfig.h:31-38): None = no save / load
         self.checkpoint_folder = None
         self.ts_per_save = 10_000_000     # 0 = every iteration (Learner.cpp:44-45)
@@ -122,65 +128,204 @@ class LearnerConfig:
             setattr(self, k, v)
 
 
+class _CConfig(ctypes.Structure):
+    """rlgpu_learner_config (include/rlgpu_learner.h)."""
+    _fields_ = [("num_arenas", ctypes.c_int32), ("tick_skip", ctypes.c_int32), ("action_delay", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("max_episode_duration", ctypes.c_float),
+                ("rollout_len", ctypes.c_int32), ("epochs", ctypes.c_int32), ("mini_batch_size", ctypes.c_int32),
+                ("batch_size", ctypes.c_int64), ("overbatching", ctypes.c_int32),
+                ("gamma", ctypes.c_float), ("gae_lambda", ctypes.c_float), ("clip_range", ctypes.c_float),
+                ("entropy_scale", ctypes.c_float), ("policy_lr", ctypes.c_float), ("critic_lr", ctypes.c_float),
+                ("reward_clip_range", ctypes.c_float), ("return_samples", ctypes.c_int32),
+                ("policy_layers", ctypes.c_int32 * MAX_LAYERS), ("n_policy_layers", ctypes.c_int32),
+                ("critic_layers", ctypes.c_int32 * MAX_LAYERS), ("n_critic_layers", ctypes.c_int32),
+                ("deterministic", ctypes.c_int32), ("train_gemm", ctypes.c_int32),
+                ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
+                ("mesh_object_ntris", ctypes.c_void_p)]
+
+
+class _CRollout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("obs", "masks", "actions", "logp", "rewards", "terms", "trunc_obs",
+                                               "values", "trunc_vals", "adv", "target", "ret")] + \
+               [("T", ctypes.c_int32), ("P", ctypes.c_int32)]
+
+
+class _CStats(ctypes.Structure):
+    _fields_ = [("total_steps", ctypes.c_int64), ("iteration", ctypes.c_int64), ("return_n", ctypes.c_int64),
+                ("return_mean", ctypes.c_double), ("return_m2", ctypes.c_double), ("rng_step", ctypes.c_int64)]
+
+
+class _CReport(ctypes.Structure):
+    _fields_ = [("collect_s", ctypes.c_double), ("consume_s", ctypes.c_double), ("learn_s", ctypes.c_double),
+                ("env_kernel_ms", ctypes.c_double), ("env_steps", ctypes.c_int64)]
+
+
+def _bind():
+    L = _lib.lib()
+    vp = ctypes.c_void_p
+    L.rlgpu_learner_create.argtypes = [ctypes.POINTER(_CConfig), vp, vp, ctypes.POINTER(vp)]
+    L.rlgpu_learner_destroy.argtypes = [vp]
+    L.rlgpu_learner_handles.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.rlgpu_learner_rollout.argtypes = [vp, ctypes.POINTER(_CRollout)]
+    L.rlgpu_learner_iterate.argtypes = [vp, ctypes.POINTER(_CReport)]
+    for f in ("collect", "consume", "learn", "finish_iteration"):
+        getattr(L, "rlgpu_learner_" + f).argtypes = [vp]
+    L.rlgpu_learner_set_old_team.argtypes = [vp, ctypes.c_int32]
+    L.rlgpu_learner_get_stats.argtypes = [vp, ctypes.POINTER(_CStats)]
+    L.rlgpu_learner_set_stats.argtypes = [vp, ctypes.POINTER(_CStats)]
+    L.rlgpu_learner_metrics.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
+    L.rlgpu_learner_set_env_timing.argtypes = [vp, ctypes.c_int32]
+    return L
+
+
+class _ReturnStat:
+    """The C++ Learner's return-std WelfordStat, seen through get/set_stats (checkpoint JSON)."""
+
+    def __init__(self, learner):
+        self._L = learner
+
+    n = property(lambda self: self._L._stats().return_n)
+    mean = property(lambda self: self._L._stats().return_mean)
+    m2 = property(lambda self: self._L._stats().return_m2)
+
+    def std(self):
+        return _host_lib().rlgpu_welford_std(self.n, self.m2)
+
+    def to_json(self):
+        return {"mean": self.mean, "var": self.m2, "count": self.n}
+
+    def read_json(self, j):
+        st = self._L._stats()
+        st.return_n, st.return_mean, st.return_m2 = int(j["count"]), float(j["mean"]), float(j["var"])
+        self._L._set_stats(st)
+
+
 class Learner:
+    """GGL::Learner for one rank (the C++ host Learner) with torch views of its HBM rollout."""
+
     def __init__(self, cfg, device="cuda:0", rank=0, world=1, group=None):
         import torch
+        from .env import EnvSet
+        from .ppo import PPO
+        if not torch.cuda.is_available():
+            raise _lib.RLGPUError("Learner needs an MI355X: the product path has no CPU fallback")
         self.cfg, self.rank, self.world, self.group = cfg, rank, world, group
         self.device = torch.device(device)
-        T, N = cfg.rollout_len, cfg.num_arenas
-        P = 4 * N
-        self.P, self.T = P, T
-        max_ep = int(cfg.max_episode_duration * (120.0 / cfg.tick_skip))
-        self.env = EnvSet(N, seed=cfg.seed * 1000003 + rank, tick_skip=cfg.tick_skip, action_delay=cfg.action_delay,
-                          device=device, max_episode_steps=max_ep)
-        mb = min(cfg.mini_batch_size, T * P)
-        self.ppo = PPO(OBS, ACTIONS, cfg.policy_layers, cfg.critic_layers, policy_lr=cfg.policy_lr,
-                       critic_lr=cfg.critic_lr, clip_range=cfg.clip_range, entropy_scale=cfg.entropy_scale,
-                       max_rows=max(mb, min(P, 65536)), seed=cfg.seed, device=device)
-        if world > 1:  # identical initial weights on every rank
-            torch.distributed.broadcast(self.ppo.params, 0, group=group)
-            self.ppo.refresh_half()
+        torch.cuda.set_device(self.device)
+        L = _bind()
+        c = _CConfig()
+        c.num_arenas, c.tick_skip, c.action_delay, c.seed = cfg.num_arenas, cfg.tick_skip, cfg.action_delay, cfg.seed
+        c.max_episode_duration, c.rollout_len, c.epochs = cfg.max_episode_duration, cfg.rollout_len, cfg.epochs
+        c.mini_batch_size = cfg.mini_batch_size
+        c.batch_size = 0 if cfg.batch_size is None else cfg.batch_size
+        c.overbatching = int(cfg.overbatching)
+        c.gamma, c.gae_lambda, c.clip_range, c.entropy_scale = cfg.gamma, cfg.gae_lambda, cfg.clip_range, cfg.entropy_scale
+        c.policy_lr, c.critic_lr, c.reward_clip_range = cfg.policy_lr, cfg.critic_lr, cfg.reward_clip_range
+        c.return_samples = cfg.return_samples
+        for i, v in enumerate(cfg.policy_layers):
+            c.policy_layers[i] = v
+        for i, v in enumerate(cfg.critic_layers):
+            c.critic_layers[i] = v
+        c.n_policy_layers, c.n_critic_layers = len(cfg.policy_layers), len(cfg.critic_layers)
+        c.deterministic, c.train_gemm = int(cfg.deterministic), cfg.train_gemm
+        c.rank, c.world = rank, world
+        self._coll = None
+        coll = None
+        if world > 1:
+            from .dist import TorchCollective
+            self._coll = TorchCollective(group, self.device)
+            coll = ctypes.byref(self._coll.c_struct())
+        h = ctypes.c_void_p()
+        _lib.check(L.rlgpu_learner_create(ctypes.byref(c), coll, _lib.stream_ptr(), ctypes.byref(h)),
+                   "rlgpu_learner_create")
+        self._h = h
+        eh, ph = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(L.rlgpu_learner_handles(h, ctypes.byref(eh), ctypes.byref(ph)), "rlgpu_learner_handles")
+        self.env = EnvSet.wrap(eh.value, self.device, cfg.tick_skip, cfg.action_delay, owner=self)
+        max_rows = max(min(cfg.mini_batch_size, cfg.rollout_len * 4 * cfg.num_arenas), min(4 * cfg.num_arenas, 65536))
+        self.ppo = PPO.wrap(ph.value, self.device, cfg.policy_layers, cfg.critic_layers, max_rows,
+                            metrics_source=self._metrics, owner=self)
+        r = _CRollout()
+        _lib.check(L.rlgpu_learner_rollout(h, ctypes.byref(r)), "rlgpu_learner_rollout")
+        T, P = r.T, r.P
+        self.T, self.P = T, P
+        a, f32, u8, i32, i8 = _lib.alias, torch.float32, torch.uint8, torch.int32, torch.int8
         d = self.device
-        # experience buffer (HBM)
-        self.obs = torch.empty((T + 1, P, OBS), device=d)
-        self.masks = torch.empty((T + 1, P, ACTIONS), dtype=torch.uint8, device=d)
-        self.actions = torch.empty((T, P), dtype=torch.int32, device=d)
-        self.logp = torch.empty((T, P), device=d)
-        self.rewards = torch.empty((T, P), device=d)
-        self.terms = torch.empty((T, P), dtype=torch.int8, device=d)
-        self.trunc_obs = torch.zeros((T, P, OBS), device=d)
-        self.values = torch.empty((T + 1, P), device=d)
-        self.trunc_vals = torch.zeros((T, P), device=d)
-        self.adv = torch.empty((T, P), device=d)
-        self.target = torch.empty((T, P), device=d)
-        self.ret = torch.empty((T, P), device=d)
-        self.obs[0].copy_(self.env.obs)
-        self.masks[0].copy_(self.env.action_masks)
-        self.return_stat = WelfordStat()
-        self.total_steps = 0
-        self.iteration = 0
-        self._rng_step = 0
-        self.rng = np.random.default_rng(cfg.seed + 7919 * rank)
-        self.env_events = None  # optional list collecting (start, end) events around env steps
+        self.obs = a(r.obs, (T + 1, P, OBS), f32, d)
+        self.masks = a(r.masks, (T + 1, P, ACTIONS), u8, d)
+        self.actions = a(r.actions, (T, P), i32, d)
+        self.logp = a(r.logp, (T, P), f32, d)
+        self.rewards = a(r.rewards, (T, P), f32, d)
+        self.terms = a(r.terms, (T, P), i8, d)
+        self.trunc_obs = a(r.trunc_obs, (T, P, OBS), f32, d)
+        self.values = a(r.values, (T + 1, P), f32, d)
+        self.trunc_vals = a(r.trunc_vals, (T, P), f32, d)
+        self.adv = a(r.adv, (T, P), f32, d)
+        self.target = a(r.target, (T, P), f32, d)
+        self.ret = a(r.ret, (T, P), f32, d)
+        self.return_stat = _ReturnStat(self)
+        # old-version player rows: team of player p is p % 2 (cars 0, 2 blue; 1, 3 orange)
+        team = torch.arange(P, device=d) % 2
+        self._old_rows = [(team == k).to(torch.uint8) for k in range(2)]
         # self-play: the manager of old versions, this iteration's version and team (None = all
         # players use the current policy); the draw is rank-independent so every rank agrees
         self.versions = None
         self.old_version, self.old_team = None, 0
         self._vrng = np.random.default_rng(cfg.seed + 104729)
         if cfg.train_against_old_versions:
-            from .versions import PolicyVersionManager
             import os
+            from .versions import PolicyVersionManager
             vf = os.path.join(cfg.checkpoint_folder, "policy_versions") if cfg.checkpoint_folder else None
             self.versions = PolicyVersionManager(self.ppo, vf, cfg.max_old_versions, cfg.ts_per_version)
-        # old-version player rows: team of player p is p % 2 (cars 0, 2 blue; 1, 3 orange)
-        team = torch.arange(P, device=d) % 2
-        self._old_rows = [(team == k).to(torch.uint8) for k in range(2)]
         self.last_checkpoint = None
         if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-153)
             from . import checkpoint as _ckpt
             self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
             if self.versions is not None:
                 self.versions.load_versions(self.total_steps)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            import torch
+            torch.cuda.synchronize(self.device)
+            self.env.close()
+            self.ppo.close()
+            _lib.check(_lib.lib().rlgpu_learner_destroy(self._h), "rlgpu_learner_destroy")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- state
+    def _stats(self):
+        st = _CStats()
+        _lib.check(_lib.lib().rlgpu_learner_get_stats(self._h, ctypes.byref(st)), "rlgpu_learner_get_stats")
+        return st
+
+    def _set_stats(self, st):
+        _lib.check(_lib.lib().rlgpu_learner_set_stats(self._h, ctypes.byref(st)), "rlgpu_learner_set_stats")
+
+    def _set_stat(self, name, v):
+        st = self._stats()
+        setattr(st, name, int(v))
+        self._set_stats(st)
+
+    total_steps = property(lambda self: self._stats().total_steps, lambda self, v: self._set_stat("total_steps", v))
+    iteration = property(lambda self: self._stats().iteration, lambda self, v: self._set_stat("iteration", v))
+
+    def _metrics(self, reset):
+        out = np.zeros(NUM_METRICS, np.float32)
+        cnt = ctypes.c_int64()
+        _lib.check(_lib.lib().rlgpu_learner_metrics(self._h, out.ctypes.data, ctypes.byref(cnt), int(reset)),
+                   "rlgpu_learner_metrics")
+        return out.tolist(), cnt.value
+
+    def set_env_timing(self, on=True):
+        _lib.check(_lib.lib().rlgpu_learner_set_env_timing(self._h, int(on)), "rlgpu_learner_set_env_timing")
 
     def save(self):
         """Learner::Save (rank 0 writes; every rank holds the same weights)."""
@@ -193,92 +338,20 @@ class Learner:
                 self.versions.save_versions()
         return self.last_checkpoint
 
-    # ---------------------------------------------------------------- collection
+    # ---------------------------------------------------------------- phases (C++)
     def collect(self):
         """T env steps: bf16 policy inference, fused env step + experience append."""
-        import torch
-        ppo, env = self.ppo, self.env
-        for t in range(self.T):
-            if self.old_version is None:
-                ppo.infer_actions(self.obs[t], self.masks[t], step=self._rng_step, deterministic=self.cfg.deterministic,
-                                  actions=self.actions[t], logp=self.logp[t])
-            else:  # one team plays the old version (Learner.cpp:733-767)
-                ppo.infer_actions_mixed(self.obs[t], self.masks[t], self._old_rows[self.old_team], step=self._rng_step,
-                                        deterministic=self.cfg.deterministic, actions=self.actions[t],
-                                        logp=self.logp[t])
-            self._rng_step += 1
-            if self.env_events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            env.step(self.actions[t], True,
-                     StepOutputs.of(obs=self.obs[t + 1], masks=self.masks[t + 1], rewards=self.rewards[t],
-                                    terminals=self.terms[t], trunc_obs=self.trunc_obs[t]))
-            if self.env_events is not None:
-                e1.record()
-                self.env_events.append((e0, e1))
+        _lib.check(_lib.lib().rlgpu_learner_collect(self._h), "rlgpu_learner_collect")
 
-    # ---------------------------------------------------------------- consumption
     def consume(self):
         """InferCriticBatched over obs[0..T] and the truncation rows, GAE, return statistics."""
-        import torch
-        T, P = self.T, self.P
-        self.ppo.infer_critic(self.obs.view(-1, OBS), out=self.values.view(-1))
-        # truncation values only where a trajectory was truncated (code 2): InferCritic on the
-        # truncated next-states (Learner.cpp:944); the other rows of trunc_vals are never read
-        rows = torch.nonzero(self.terms.view(-1) == 2).squeeze(1)
-        if rows.numel():
-            tv = self.ppo.infer_critic(self.trunc_obs.view(-1, OBS).index_select(0, rows))
-            self.trunc_vals.view(-1).index_copy_(0, rows, tv)
-        std = self.return_stat.std()
-        _gae.GAE.compute_rollout(self.rewards, self.terms, self.values[:T], self.trunc_vals, self.values[T],
-                                 self.cfg.gamma, self.cfg.gae_lambda, std, self.cfg.reward_clip_range,
-                                 adv=self.adv, target=self.target, ret=self.ret)
-        # return-std Welford over randomly sampled returns (Learner.cpp:959-967)
-        k = self.cfg.return_samples
-        if self.old_version is None:
-            idx = torch.from_numpy(self.rng.integers(0, T * P, size=k)).to(self.device)
-        else:  # only the current policy's players have trajectories
-            idx = self._train_rows()[torch.from_numpy(self.rng.integers(0, T * P // 2, size=k)).to(self.device)]
-        samples = _dist.gather_samples(self.ret.view(-1)[idx], self.group)
-        self.return_stat.add(samples.cpu().numpy())
+        _lib.check(_lib.lib().rlgpu_learner_consume(self._h), "rlgpu_learner_consume")
 
-    def _train_rows(self):
-        """Sample indices (t * P + p) of the players on the current policy in an old-version iteration."""
-        import torch
-        new_team = 1 - self.old_team
-        p = torch.arange(new_team, self.P, 2, device=self.device)
-        t = torch.arange(self.T, device=self.device)
-        return (t[:, None] * self.P + p[None, :]).reshape(-1).to(torch.int32)
-
-    # ---------------------------------------------------------------- learning
     def learn(self):
-        cfg, ppo = self.cfg, self.ppo
-        rows = None if self.old_version is None else self._train_rows()
-        M = self.T * self.P if rows is None else rows.numel()
-        global_m = M * self.world
-        batch = global_m if cfg.batch_size is None else cfg.batch_size
-        obs = self.obs[:self.T].reshape(-1, OBS)
-        masks = self.masks[:self.T].reshape(-1, ACTIONS)
-        acts, logp = self.actions.view(-1), self.logp.view(-1)
-        adv, tgt = self.adv.view(-1), self.target.view(-1)
-        local_batch = M if cfg.batch_size is None else max(1, cfg.batch_size // self.world)
-        for epoch in range(cfg.epochs):
-            perm = permutation(M, cfg.seed + self.rank, self.iteration * cfg.epochs + epoch, device=self.device)
-            if rows is not None:
-                perm = rows[perm.long()]
-            for b0, b1 in batch_ranges(M, local_batch, cfg.overbatching):
-                # batch advantage normalisation (PPOLearner.cpp:360-371), global over ranks
-                whole = rows is None and (b0, b1) == (0, M)
-                badv = adv if whole else adv.index_select(0, perm[b0:b1].long())
-                if self.world > 1:
-                    ppo.adv_stats.copy_(_dist.global_mean_std(badv, self.group))
-                else:
-                    ppo.adv_normalizer(badv)
-                for s0 in range(b0, b1, cfg.mini_batch_size):
-                    n = min(cfg.mini_batch_size, b1 - s0)
-                    ppo.minibatch(obs, masks, acts, logp, adv, tgt, perm, s0, n, batch)
-                _dist.allreduce_grads(ppo.grads, self.group)  # RCCL over xGMI, before clip_grad_norm_
-                ppo.optimizer_step()
+        _lib.check(_lib.lib().rlgpu_learner_learn(self._h), "rlgpu_learner_learn")
+
+    def finish_iteration(self):
+        _lib.check(_lib.lib().rlgpu_learner_finish_iteration(self._h), "rlgpu_learner_finish_iteration")
 
     def iterate(self):
         """One PPO iteration (collect T steps, consume, learn); returns a report dict."""
@@ -290,23 +363,19 @@ class Learner:
                 self.old_version = self.versions.versions[int(self._vrng.integers(0, len(self.versions.versions)))]
                 self.old_team = int(self._vrng.integers(0, 2))
                 self.ppo.set_version(self.old_version.params)
-        self.collect()
-        self.consume()
-        self.learn()
-        # next rollout starts from the last obs
-        self.obs[0].copy_(self.obs[self.T])
-        self.masks[0].copy_(self.masks[self.T])
-        self.iteration += 1
+        team = -1 if self.old_version is None else self.old_team
+        _lib.check(_lib.lib().rlgpu_learner_set_old_team(self._h, team), "rlgpu_learner_set_old_team")
         prev = self.total_steps
-        real_players = self.P if self.old_version is None else self.P // 2  # numRealPlayers (Learner.cpp:629)
-        self.total_steps += self.T * real_players * self.world
+        rep = _CReport()
+        _lib.check(_lib.lib().rlgpu_learner_iterate(self._h, ctypes.byref(rep)), "rlgpu_learner_iterate")
         if self.versions is not None:
             self.versions.on_iteration(self.total_steps, prev)
         torch.cuda.synchronize(self.device)
-        rep = {"iteration_s": time.perf_counter() - t0, "old_version": None if self.old_version is None
-               else (self.old_version.timesteps, self.old_team)}
+        out = {"iteration_s": time.perf_counter() - t0, "collect_s": rep.collect_s, "consume_s": rep.consume_s,
+               "learn_s": rep.learn_s, "env_kernel_ms": rep.env_kernel_ms,
+               "old_version": None if self.old_version is None else (self.old_version.timesteps, self.old_team)}
         if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)
             per = self.cfg.ts_per_save or self.T * self.P * self.world
             if self.total_steps // per > prev // per:
-                rep["checkpoint"] = self.save()
-        return rep
+                out["checkpoint"] = self.save()
+        return out

@@ -122,9 +122,36 @@ class PPO:
         if init:
             self.init_params(seed)
 
+    @classmethod
+    def wrap(cls, handle, device, policy_layers, critic_layers, max_rows, obs_size=167, num_actions=90,
+             layer_norm=True, leaky_slope=0.01, metrics_source=None, owner=None):
+        """A PPO view of a handle owned elsewhere (the C++ Learner's PPOLearner): not destroyed
+        by this object.  metrics_source(reset) -> (sums, count) replaces the own metric buffer."""
+        import torch
+        L = _bind()
+        self = cls.__new__(cls)
+        self._h, self._owned, self._owner = ctypes.c_void_p(handle), False, owner
+        self.device = torch.device(device)
+        self.obs_size, self.num_actions = obs_size, num_actions
+        self.policy_layers, self.critic_layers, self.layer_norm = tuple(policy_layers), tuple(critic_layers), layer_norm
+        self.leaky_slope, self.max_rows = leaky_slope, max_rows
+        p, g, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        _lib.check(L.rlgpu_ppo_buffers(self._h, ctypes.byref(p), ctypes.byref(g), ctypes.byref(n)), "rlgpu_ppo_buffers")
+        self.num_params = n.value
+        self.params = alias(p.value, (n.value,), torch.float32, self.device)
+        self.grads = alias(g.value, (n.value,), torch.float32, self.device)
+        self.metrics = torch.zeros(NUM_METRICS, device=self.device)
+        self.adv_stats = torch.zeros(2, device=self.device)
+        self._metrics_source = metrics_source
+        return self
+
+    _owned = True
+    _metrics_source = None
+
     def close(self):
         if getattr(self, "_h", None):
-            _lib.check(_lib.lib().rlgpu_ppo_destroy(self._h), "rlgpu_ppo_destroy")
+            if self._owned:
+                _lib.check(_lib.lib().rlgpu_ppo_destroy(self._h), "rlgpu_ppo_destroy")
             self._h = None
 
     def __del__(self):
@@ -249,6 +276,12 @@ class PPO:
 
     def read_metrics(self, reset=True):
         """Report entries of PPOLearner::Learn (:537-566): means over the accumulated minibatches."""
+        if self._metrics_source is not None:
+            m, cnt = self._metrics_source(reset)
+            cnt = max(cnt, 1)
+            return {"Policy Entropy": m[0] / cnt, "Mean KL Divergence": m[1] / cnt, "Policy Loss": m[2] / cnt,
+                    "Critic Loss": m[3] / cnt, "Ratio": m[4] / cnt, "SB3 Clip Fraction": m[5] / cnt,
+                    "Policy Grad Norm": m[7], "Critic Grad Norm": m[8]}
         m = self.metrics.cpu().tolist()
         cnt = max(self._count, 1)
         rep = {"Policy Entropy": m[0] / cnt, "Mean KL Divergence": m[1] / cnt, "Policy Loss": m[2] / cnt,

@@ -1,8 +1,11 @@
-"""Multi-rank logic of the Learner (rlgpu/dist.py) on CPU with gloo, world size 2.
+"""Multi-rank logic of the Learner on CPU with gloo, world size 2.
 
-The GPU path uses the same functions over RCCL; here torch CPU tensors stand in for the HBM
-buffers.  Checks: gradient all-reduce with global-batch loss scaling equals the single-device
-gradient of the whole batch; global advantage moments equal the single-device ones; return samples
+The C++ Learner (host/learner.cpp) issues its exchanges through an rlgpu_collective; on the GPUs
+bench.py / rlgpu.learner bind it to rlgpu.dist.TorchCollective over RCCL.  Here the same
+TorchCollective runs over gloo with host buffers, called exactly as the C++ Learner calls it
+(through its ctypes C callbacks).  Checks: gradient all-reduce with global-batch loss scaling equals
+the single-device gradient of the whole batch; global advantage (mean, std) from all-reduced fp64
+moments (rlgpu_moments_mean_std, the C++ finish) equals the single-device one; return samples
 gathered identically on every rank; max-over-ranks timing; arena sharding is a partition.
 """
 import os
@@ -46,13 +49,19 @@ def _worker(rank, world, port, q):
         # each rank: two minibatches of its shard, accumulate, then all-reduce
         for a in range(lo, hi, 16):
             _loss(m, X[a:a + 16], Y[a:a + 16], 64).backward()
-        flat = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
-        D.allreduce_grads(flat)
-        adv = torch.randn(1000, generator=torch.Generator().manual_seed(10 + rank))
-        st = D.global_mean_std(adv)
-        smp = D.gather_samples(torch.full((3,), float(rank)))
+        flat = np.ascontiguousarray(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).numpy())
+        coll = D.TorchCollective(device="cpu")
+        c = coll.c_struct()  # the C callbacks the C++ Learner receives
+        assert c.allreduce_sum_f32(None, flat.ctypes.data, flat.size) == 0
+        adv = torch.randn(1000, generator=torch.Generator().manual_seed(10 + rank)).double()
+        mom = np.array([adv.sum().item(), (adv * adv).sum().item(), float(adv.numel())])
+        assert c.allreduce_sum_f64(None, mom.ctypes.data, 3) == 0
+        st = D.moments_mean_std(mom)
+        mine = np.full(3, float(rank), np.float32)
+        smp = np.zeros(3 * world, np.float32)
+        assert c.allgather_f32(None, mine.ctypes.data, 3, smp.ctypes.data) == 0
         t = D.max_over_ranks(0.5 + rank)
-        q.put((rank, flat.numpy(), st.numpy(), smp.numpy(), t))
+        q.put((rank, flat, st, smp, t))
     finally:
         dist.destroy_process_group()
 
@@ -78,7 +87,7 @@ def test_two_rank_gloo_reductions():
     for r in res:
         np.testing.assert_allclose(r[1], want, rtol=1e-5, atol=1e-7)
     advs = torch.cat([torch.randn(1000, generator=torch.Generator().manual_seed(10 + r)) for r in range(world)])
-    np.testing.assert_allclose(res[0][2], [advs.mean().item(), advs.std().item()], rtol=1e-5)
+    np.testing.assert_allclose(res[0][2], [advs.mean().item(), advs.double().std().item()], rtol=1e-5, atol=1e-7)
     np.testing.assert_array_equal(res[0][2], res[1][2])
     np.testing.assert_array_equal(res[0][3], [0, 0, 0, 1, 1, 1])
     np.testing.assert_array_equal(res[1][3], res[0][3])

@@ -166,3 +166,33 @@ def test_self_play_old_version(gpu, tmp_path):
     L2 = _learner(gpu, checkpoint_folder=folder, ts_per_save=0)
     assert [x.timesteps for x in L2.versions.versions] == [x.timesteps for x in L.versions.versions]
     assert torch.equal(L2.versions.versions[0].params, L.versions.versions[0].params)
+
+
+def test_example_main_binary(gpu):
+    """host/example_main.cpp (the reference's src/ExampleMain.cpp on this engine): the C++ host
+    Learner runs stand-alone, no Python in the loop."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd",
+                       "rlgpu", "rlgpu_train")
+    r = subprocess.run([exe, "--iterations", "2", "--arenas", "32", "--rollout", "16"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = [x for x in r.stdout.splitlines() if x.startswith("iteration")]
+    assert len(lines) == 2 and "Total Timesteps 4096" in lines[-1], r.stdout
+
+
+def test_sample_indices_and_welford_state(gpu):
+    """The return samples of an iteration come from rlgpu_sample_indices (seed, rank, iteration) and
+    feed the C++ WelfordStat: recompute them from the ret buffer and compare the Welford state."""
+    import torch
+    from rlgpu.learner import WelfordStat, sample_indices
+    L = _learner(gpu, train_against_old_versions=False)
+    L.collect()
+    L.consume()
+    torch.cuda.synchronize()
+    idx = sample_indices(L.cfg.seed, 0, 0, L.T * L.P, L.cfg.return_samples)
+    assert idx.min() >= 0 and idx.max() < L.T * L.P
+    w = WelfordStat()
+    w.add(L.ret.view(-1).cpu().numpy()[idx])
+    assert (w.n, w.mean, w.m2) == (L.return_stat.n, L.return_stat.mean, L.return_stat.m2)
