@@ -33,6 +33,8 @@ HD v3& operator+=(v3& a, v3 b) { a = a + b; return a; }
 HD v3& operator-=(v3& a, v3 b) { a = a - b; return a; }
 HD v3& operator*=(v3& a, float s) { a = a * s; return a; }
 HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// one of three vectors by a runtime index, as selects (keeps small vector tables in registers)
+HD v3 sel3(const v3& a, const v3& b, const v3& c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
 HD v3 cross(v3 a, v3 b) { return v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 HD float len2(v3 a) { return dot(a, a); }
 HD float len(v3 a) { return sqrtf(len2(a)); }

@@ -44,8 +44,30 @@ struct StepArgs {
 
 DEV void sync() { __syncthreads(); }
 
+// The boost-pad constants a lane tests every tick (pads l, l + 16, l + 32), held in registers for
+// the whole launch instead of re-read from the constant buffer with lane-varying addresses in every
+// tick's pad-collision phase.
+constexpr int kPadsPerLane = (RLGPU_PADS + kTeam - 1) / kTeam;
+struct PadRegs {
+    int px[kPadsPerLane], py[kPadsPerLane];
+    v3 pos[kPadsPerLane], bmin[kPadsPerLane], bmax[kPadsPerLane];
+    float rad[kPadsPerLane];
+};
+DEV void load_pad_regs(PadRegs& R, int l) {
+#pragma unroll
+    for (int k = 0; k < kPadsPerLane; k++) {
+        const int p = l + k * kTeam < RLGPU_PADS ? l + k * kTeam : 0;
+        R.px[k] = C.pad_cell_x[p];
+        R.py[k] = C.pad_cell_y[p];
+        R.pos[k] = C.pad_pos_bt[p];
+        R.bmin[k] = C.pad_box_min[p];
+        R.bmax[k] = C.pad_box_max[p];
+        R.rad[k] = (C.pad_big[p] ? 208.f : 144.f) * kUU2BT;
+    }
+}
+
 // ------------------------------------------------------------------ one tick (Arena::Step body)
-DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P) {
+DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R) {
     if (valid && l == 0) {
         rlgpu_arena_state& s = A->s;
         bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
@@ -211,10 +233,13 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
             cy0[ci] = iy - 1 > 0 ? iy - 1 : 0;
             cy1[ci] = iy + 1 < 9 ? iy + 1 : 9;
         }
-        for (int p = l; p < RLGPU_PADS; p += kTeam) {
-            const int px = C.pad_cell_x[p], py = C.pad_cell_y[p];
-            const v3 ppos = C.pad_pos_bt[p];
-            const float rad = (C.pad_big[p] ? 208.f : 144.f) * kUU2BT;
+#pragma unroll
+        for (int k = 0; k < kPadsPerLane; k++) {
+            const int p = l + k * kTeam;
+            if (p >= RLGPU_PADS) break;
+            const int px = R.px[k], py = R.py[k];
+            const v3 ppos = R.pos[k];
+            const float rad = R.rad[k];
             const uint32_t prev_locked = A->s.pads[p].prev_locked_car_id;
             int locked = -1;
 #pragma unroll
@@ -225,7 +250,7 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
                 if (prev_locked == (uint32_t)(ci + 1)) {
                     v3 mn, mx;
                     body_aabb(ci + 1, cpos, ldm(A->s.cars[ci].body.rot), mn, mx);
-                    const v3 bmin = C.pad_box_min[p], bmax = C.pad_box_max[p];
+                    const v3 bmin = R.bmin[k], bmax = R.bmax[k];
                     col = (bmax.x > mn.x && bmax.y > mn.y && bmax.z > mn.z) && (bmin.x < mx.x && bmin.y < mx.y && bmin.z < mx.z);
                 } else {
                     float dx = cpos.x - ppos.x, dy = cpos.y - ppos.y;
@@ -331,6 +356,8 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
     // kernel's hot code small enough for the instruction cache); StepSecondHalf's action parse
     // (EnvSet.cpp:132-156) runs when the first half's actionDelay ticks are done
     {
+        PadRegs pregs;
+        load_pad_regs(pregs, l);
         const int t1 = g.ticks_first, t2 = g.actions ? g.ticks_second : 0;
         for (int t = 0;; t++) {
             if (g.actions && t == t1) {
@@ -348,7 +375,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
                 sync(); P.mark(11);
             }
             if (t >= t1 + t2) break;
-            tick(A, g.mesh, l, valid, g.seed, arena, P);
+            tick(A, g.mesh, l, valid, g.seed, arena, P, pregs);
         }
     }
     // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks

@@ -73,22 +73,19 @@ DEV int sort_cached(const rlgpu_manifold& m, const rlgpu_contact& pt) {
             max_idx = i;
             max_pen = m.pts[i].dist;
         }
-    float res[4] = {0, 0, 0, 0};
     v3 p = ld3(pt.localA);
     v3 l0 = ld3(m.pts[0].localA), l1 = ld3(m.pts[1].localA), l2 = ld3(m.pts[2].localA), l3 = ld3(m.pts[3].localA);
-    if (max_idx != 0) res[0] = len2(cross(p - l1, l3 - l2));
-    if (max_idx != 1) res[1] = len2(cross(p - l0, l3 - l2));
-    if (max_idx != 2) res[2] = len2(cross(p - l0, l3 - l1));
-    if (max_idx != 3) res[3] = len2(cross(p - l0, l2 - l1));
+    // four named values, not an array: a lane-indexed private array lives in scratch memory
+    const float r0 = max_idx != 0 ? len2(cross(p - l1, l3 - l2)) : 0.f;
+    const float r1 = max_idx != 1 ? len2(cross(p - l0, l3 - l2)) : 0.f;
+    const float r2 = max_idx != 2 ? len2(cross(p - l0, l3 - l1)) : 0.f;
+    const float r3 = max_idx != 3 ? len2(cross(p - l0, l2 - l1)) : 0.f;
     int best = -1;
     float mx = -1e30f;
-    for (int i = 0; i < 4; i++) {
-        float v = fabsf(res[i]);
-        if (v > mx) {
-            best = i;
-            mx = v;
-        }
-    }
+    if (fabsf(r0) > mx) best = 0, mx = fabsf(r0);
+    if (fabsf(r1) > mx) best = 1, mx = fabsf(r1);
+    if (fabsf(r2) > mx) best = 2, mx = fabsf(r2);
+    if (fabsf(r3) > mx) best = 3, mx = fabsf(r3);
     return best;
 }
 
@@ -120,7 +117,7 @@ DEV void car_ball_hit(ArenaLDS* A, int ci, rlgpu_contact& cp) {
         v3 hit_dir = safe_normalized(rel_pos * v3{1, 1, 0.35f});
         v3 adj = fwd * dot(hit_dir, fwd) * (1 - 0.65f);
         hit_dir = safe_normalized(hit_dir - adj);
-        v3 added = (hit_dir * rel_speed) * curve_out(kBallCarExtra, rel_speed) * 1.f;
+        v3 added = (hit_dir * rel_speed) * curve_out<kBallCarExtra>(rel_speed) * 1.f;
         st3(cs.ball_hit_extra_vel, added);
         st3(A->s.ball_vel_impulse_cache, ld3(A->s.ball_vel_impulse_cache) + added * kUU2BT);
     }
@@ -156,9 +153,9 @@ DEV void car_car_hit(ArenaLDS* A, int c1, int c2, rlgpu_contact& cp) {
                         so.demo_respawn_timer = 3.f;
                     } else {
                         bool ground = so.is_on_ground;
-                        float base = curve_out(ground ? kBumpGround : kBumpAir, speed_towards);
+                        float base = ground ? curve_out<kBumpGround>(speed_towards) : curve_out<kBumpAir>(speed_towards);
                         v3 up = so.is_on_ground ? col(brot(A, o + 1), 2) : v3{0, 0, 1};
-                        v3 imp = vel_dir * base + up * curve_out(kBumpUp, speed_towards) * 1.f;
+                        v3 imp = vel_dir * base + up * curve_out<kBumpUp>(speed_towards) * 1.f;
                         st3(so.vel_impulse_cache, ld3(so.vel_impulse_cache) + imp * kUU2BT);
                     }
                     sa.car_contact_other_id = (uint32_t)(o + 1);
@@ -388,20 +385,21 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
 DEV bool box_triangle(ArenaLDS* A, int bi, v3 v0, v3 v1, v3 v2, float cbt, v3& nrm, v3& point_b, float& depth) {
     m3 R = brot(A, bi);
     v3 c = car_box_center(A, bi);
-    v3 ax[3] = {col(R, 0), col(R, 1), col(R, 2)};
-    v3 e[3] = {v1 - v0, v2 - v1, v0 - v2};
+    // the axes as named registers picked by selects (a k-indexed private array lives in scratch)
+    const v3 ax0 = col(R, 0), ax1 = col(R, 1), ax2 = col(R, 2);
+    const v3 e0 = v1 - v0, e1 = v2 - v1, e2 = v0 - v2;
     float best = 1e30f;
     v3 best_n = zero3();
     for (int k = 0; k < 13; k++) {
         v3 axis;
-        if (k == 0) axis = cross(e[0], v2 - v0);
-        else if (k < 4) axis = ax[k - 1];
-        else axis = cross(ax[(k - 4) / 3], e[(k - 4) % 3]);
+        if (k == 0) axis = cross(e0, v2 - v0);
+        else if (k < 4) axis = sel3(ax0, ax1, ax2, k - 1);
+        else axis = cross(sel3(ax0, ax1, ax2, (k - 4) / 3), sel3(e0, e1, e2, (k - 4) % 3));
         float l2 = len2(axis);
         if (l2 < 1e-10f) continue;
         v3 L = axis / sqrtf(l2);
-        float r = C.car_half.x * fabsf(dot(ax[0], L)) + C.car_half.y * fabsf(dot(ax[1], L)) +
-                  C.car_half.z * fabsf(dot(ax[2], L));
+        float r = C.car_half.x * fabsf(dot(ax0, L)) + C.car_half.y * fabsf(dot(ax1, L)) +
+                  C.car_half.z * fabsf(dot(ax2, L));
         float p0 = dot(v0, L), p1 = dot(v1, L), p2 = dot(v2, L);
         float tmin = stdmin(p0, stdmin(p1, p2)), tmax = stdmax(p0, stdmax(p1, p2));
         float cl = dot(c, L);
@@ -508,8 +506,10 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
         if (d2 <= kEps) {
             float fd[6] = {he.x - rel.x, he.x + rel.x, he.y - rel.y, he.y + rel.y, he.z - rel.z, he.z + rel.z};
             int bf = 0;
+            float fmin = fd[0];
+#pragma unroll
             for (int k = 1; k < 6; k++)
-                if (fd[k] < fd[bf]) bf = k;
+                if (fd[k] < fmin) bf = k, fmin = fd[k];
             cp = rel;
             int axis = bf / 2;
             float sg = (bf % 2 == 0) ? 1.f : -1.f;
@@ -517,7 +517,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
             v3 nn = zero3();
             set_comp(nn, axis, sg);
             normal = nn;
-            distance = -fd[bf];
+            distance = -fmin;
         } else {
             distance = len(normal);
             normal = normal / distance;
@@ -534,7 +534,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
     {
         m3 Ra = brot(A, A_), Rb = brot(A, B_);
         v3 ca = car_box_center(A, A_), cb = car_box_center(A, B_);
-        v3 Ax[3] = {col(Ra, 0), col(Ra, 1), col(Ra, 2)}, Bx[3] = {col(Rb, 0), col(Rb, 1), col(Rb, 2)};
+        const v3 A0 = col(Ra, 0), A1 = col(Ra, 1), A2 = col(Ra, 2), B0 = col(Rb, 0), B1 = col(Rb, 1), B2 = col(Rb, 2);
         v3 h = C.car_half;
         float cbt = pair_cbt(A_, B_);
         float best = 1e30f;
@@ -542,14 +542,14 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
         int best_k = -1;
         for (int k = 0; k < 15; k++) {
             v3 axis;
-            if (k < 3) axis = Ax[k];
-            else if (k < 6) axis = Bx[k - 3];
-            else axis = cross(Ax[(k - 6) / 3], Bx[(k - 6) % 3]);
+            if (k < 3) axis = sel3(A0, A1, A2, k);
+            else if (k < 6) axis = sel3(B0, B1, B2, k - 3);
+            else axis = cross(sel3(A0, A1, A2, (k - 6) / 3), sel3(B0, B1, B2, (k - 6) % 3));
             float l2 = len2(axis);
             if (l2 < 1e-10f) continue;
             v3 L = axis / sqrtf(l2);
-            float ra = h.x * fabsf(dot(Ax[0], L)) + h.y * fabsf(dot(Ax[1], L)) + h.z * fabsf(dot(Ax[2], L));
-            float rb = h.x * fabsf(dot(Bx[0], L)) + h.y * fabsf(dot(Bx[1], L)) + h.z * fabsf(dot(Bx[2], L));
+            float ra = h.x * fabsf(dot(A0, L)) + h.y * fabsf(dot(A1, L)) + h.z * fabsf(dot(A2, L));
+            float rb = h.x * fabsf(dot(B0, L)) + h.y * fabsf(dot(B1, L)) + h.z * fabsf(dot(B2, L));
             float d = dot(ca - cb, L);
             float pen = ra + rb - fabsf(d);
             if (-pen > cbt) return 1;

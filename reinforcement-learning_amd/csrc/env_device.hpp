@@ -61,36 +61,42 @@ DEV float stdmin(float a, float b) { return b < a ? b : a; }                    
 DEV int sgn(float x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); }                                  // RS_SGN
 
 // ------------------------------------------------------------------ LinearPieceCurve (Math.cpp:5-34)
+// The curves are compile-time constants (template arguments) of a fully unrolled lookup, so every
+// knot is an immediate: no memory loads (the lookup used to walk knots in global memory, a
+// dependent load chain per call, several calls per car per tick).
 struct Curve {
     int n;
     float k[6], v[6];
 };
-DEV float curve_out(const Curve& c, float input, float def = 1.f) {
-    if (c.n == 0) return def;
-    if (input <= c.k[0]) return c.v[0];
-    for (int i = 1; i < c.n; i++) {
-        if (c.k[i] > input) {
-            float range = c.k[i] - c.k[i - 1];
-            float diff = c.v[i] - c.v[i - 1];
-            float f = (input - c.k[i - 1]) / range;
-            return c.v[i - 1] + diff * f;
+// RLConst.h:342-437
+constexpr Curve kSteerAngle = {6, {0, 500, 1000, 1500, 1750, 3000}, {0.53356f, 0.31930f, 0.18203f, 0.10570f, 0.08507f, 0.03454f}};
+constexpr Curve kPowerslideSteer = {2, {0, 2500}, {0.39235f, 0.12610f}};
+constexpr Curve kDriveTorque = {3, {0, 1400, 1410}, {1.0f, 0.1f, 0.0f}};
+constexpr Curve kNonSticky = {3, {0, 0.7075f, 1}, {0.1f, 0.5f, 1.0f}};
+constexpr Curve kLatFriction = {2, {0, 1}, {1.0f, 0.2f}};
+constexpr Curve kLongFriction = {0, {}, {}};
+constexpr Curve kHbLat = {1, {0}, {0.1f}};
+constexpr Curve kHbLong = {2, {0, 1}, {0.5f, 0.9f}};
+constexpr Curve kBallCarExtra = {4, {0, 500, 2300, 4600}, {0.65f, 0.65f, 0.55f, 0.30f}};
+constexpr Curve kBumpGround = {3, {0, 1400, 2200}, {5.f / 6.f, 1100.f, 1530.f}};
+constexpr Curve kBumpAir = {3, {0, 1400, 2200}, {5.f / 6.f, 1390.f, 1945.f}};
+constexpr Curve kBumpUp = {3, {0, 1400, 2200}, {2.f / 6.f, 278.f, 417.f}};
+
+template <const Curve& CV>
+DEV float curve_out(float input, float def = 1.f) {
+    if (CV.n == 0) return def;
+    if (input <= CV.k[0]) return CV.v[0];
+#pragma unroll
+    for (int i = 1; i < 6; i++) {
+        if (i < CV.n && CV.k[i] > input) {
+            float range = CV.k[i] - CV.k[i - 1];
+            float diff = CV.v[i] - CV.v[i - 1];
+            float f = (input - CV.k[i - 1]) / range;
+            return CV.v[i - 1] + diff * f;
         }
     }
-    return c.v[c.n - 1];
+    return CV.v[CV.n > 0 ? CV.n - 1 : 0];
 }
-// RLConst.h:342-437
-__device__ const Curve kSteerAngle = {6, {0, 500, 1000, 1500, 1750, 3000}, {0.53356f, 0.31930f, 0.18203f, 0.10570f, 0.08507f, 0.03454f}};
-__device__ const Curve kPowerslideSteer = {2, {0, 2500}, {0.39235f, 0.12610f}};
-__device__ const Curve kDriveTorque = {3, {0, 1400, 1410}, {1.0f, 0.1f, 0.0f}};
-__device__ const Curve kNonSticky = {3, {0, 0.7075f, 1}, {0.1f, 0.5f, 1.0f}};
-__device__ const Curve kLatFriction = {2, {0, 1}, {1.0f, 0.2f}};
-__device__ const Curve kLongFriction = {0, {}, {}};
-__device__ const Curve kHbLat = {1, {0}, {0.1f}};
-__device__ const Curve kHbLong = {2, {0, 1}, {0.5f, 0.9f}};
-__device__ const Curve kBallCarExtra = {4, {0, 500, 2300, 4600}, {0.65f, 0.65f, 0.55f, 0.30f}};
-__device__ const Curve kBumpGround = {3, {0, 1400, 2200}, {5.f / 6.f, 1100.f, 1530.f}};
-__device__ const Curve kBumpAir = {3, {0, 1400, 2200}, {5.f / 6.f, 1390.f, 1945.f}};
-__device__ const Curve kBumpUp = {3, {0, 1400, 2200}, {2.f / 6.f, 278.f, 417.f}};
 
 // ------------------------------------------------------------------ Philox 4x32-10 (same as oracle)
 DEV uint32_t philox0(uint64_t key, uint32_t c0, uint32_t c1) {
@@ -448,7 +454,7 @@ DEV void update_wheels(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
     float real_brake = 0;
     if (ctl[6] != 0.f && cs.boost > 0) real_throttle = 1;
     {
-        float drive_scale = curve_out(kDriveTorque, abs_fwd);
+        float drive_scale = curve_out<kDriveTorque>(abs_fwd);
         float engine_throttle = real_throttle;
         if (ctl[7] != 0.f) {
         } else {
@@ -473,8 +479,8 @@ DEV void update_wheels(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
         }
     }
     {
-        float steer = curve_out(kSteerAngle, abs_fwd);
-        if (cs.handbrake_val != 0.f) steer += (curve_out(kPowerslideSteer, abs_fwd) - steer) * cs.handbrake_val;
+        float steer = curve_out<kSteerAngle>(abs_fwd);
+        if (cs.handbrake_val != 0.f) steer += (curve_out<kPowerslideSteer>(abs_fwd) - steer) * cs.handbrake_val;
         steer *= ctl[1];
         cs.wheel_steer[0] = steer;
         cs.wheel_steer[1] = steer;
@@ -490,18 +496,18 @@ DEV void update_wheels(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
             v3 cv = (cross(Av, delta) + Vv) * kBT2UU;
             float base = fabsf(dot(cv, lat_dir));
             if (base > 5) fin = base / (fabsf(dot(cv, long_dir)) + base);
-            float lat = curve_out(kLatFriction, fin);
-            float lon = curve_out(kLongFriction, fin);
+            float lat = curve_out<kLatFriction>(fin);
+            float lon = curve_out<kLongFriction>(fin);
             if (cs.handbrake_val != 0.f) {
                 float hb = cs.handbrake_val;
-                lat *= (curve_out(kHbLat, fin) - 1) * hb + 1;
-                lon *= (curve_out(kHbLong, fin) - 1) * hb + 1;
+                lat *= (curve_out<kHbLat>(fin) - 1) * hb + 1;
+                lon *= (curve_out<kHbLong>(fin) - 1) * hb + 1;
             } else {
                 lon = 1;
             }
             bool sticky = real_throttle != 0;
             if (!sticky) {
-                float ns = curve_out(kNonSticky, W.contact_normal.z);
+                float ns = curve_out<kNonSticky>(W.contact_normal.z);
                 lat *= ns;
                 lon *= ns;
             }
