@@ -242,8 +242,9 @@ __global__ void __launch_bounds__(256, RLGPU_GEMM_OCC) gemm_f32(GemmArgs g) {
 // (6 x 32 cycles per K = 16) replace eight f32 ones (8 x 64 cycles).  Same tiles, layouts, split-K
 // and epilogue as gemm_f32; operands are split once per LDS stage into three k-contiguous bf16
 // planes, so the MFMA loop reads b128 vectors whatever the global layout.
-constexpr int XBK = 32;            // K per LDS stage (two 32x32x16 k-steps)
-constexpr int XPAD = 8;            // bf16 pad per LDS row (row = 80 B)
+constexpr int XPAD = 8;            // bf16 pad per LDS row
+constexpr int XKMAX = 64;          // deepest stage of any variant: split-K chunks and weight-plane
+                                   // padding are multiples of it
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 DEV uint32_t pack_bf16x2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
@@ -265,31 +266,32 @@ DEV void split3(const f32x4_t (&v)[2], u32x4_t& h, u32x4_t& m, u32x4_t& l) {
     }
 }
 
-// Per-thread share of one 128 x XBK operand stage: two groups of 8 consecutive k of one row, held
-// in native 4-vectors (loop-carried prefetch registers stay where the loads land, so the wait for
-// them sits at the next stage's store, after this stage's MFMAs).
-//   KMAJ (k contiguous in memory): group e = t + 256 q -> row e >> 2, k group e & 3 (2 float4 loads)
+// Per-thread share of one 128 x XK operand stage (XK = 32 or 64 k): NQ = XK / 16 groups of 8
+// consecutive k of one row, held in native 4-vectors (loop-carried prefetch registers stay where
+// the loads land, so the wait for them sits at the next stage's store, after this stage's MFMAs).
+//   KMAJ (k contiguous in memory): group e = t + 256 q -> row e / KG, k group e % KG (2 float4 loads)
 //   !KMAJ (row index contiguous):  group e -> row e & 127, k group e >> 7 (8 scalar loads, each a
 //                                  256-byte contiguous wave access)
-template <bool KMAJ>
+template <bool KMAJ, int XK>
 DEV int xs_row(int q) {
+    constexpr int KG = XK / 8;
     const int e = threadIdx.x + 256 * q;
-    return KMAJ ? e >> 2 : e & 127;
+    return KMAJ ? e / KG : e & 127;
 }
-template <bool KMAJ>
+template <bool KMAJ, int XK>
 DEV int xs_kg(int q) {
+    constexpr int KG = XK / 8;
     const int e = threadIdx.x + 256 * q;
-    return KMAJ ? e & 3 : e >> 7;
+    return KMAJ ? e % KG : e >> 7;
 }
-template <bool KMAJ>
+template <bool KMAJ, int XK>
 DEV RowPtrs xs_rows(const float* base, int64_t ld, int o0, int on) {
     RowPtrs r;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const int go = o0 + xs_row<KMAJ>(q);
-        r.p[q] = (KMAJ && go < on) ? base + (int64_t)go * ld : nullptr;
+    for (int q = 0; q < 4; q++) {
+        const int go = o0 + xs_row<KMAJ, XK>(q);
+        r.p[q] = (KMAJ && q < XK / 16 && go < on) ? base + (int64_t)go * ld : nullptr;
     }
-    r.p[2] = r.p[3] = nullptr;
     return r;
 }
 template <bool VEC>
@@ -305,17 +307,18 @@ DEV f32x4_t load4v(const float* p, int c, int lim) {
     }
     return v;
 }
-template <bool KMAJ, bool VEC>
-DEV void xs_load(f32x4_t (&v)[2][2], const RowPtrs& rows, const float* base, int64_t ld, int o0, int on, int k0, int ke) {
+template <bool KMAJ, bool VEC, int XK>
+DEV void xs_load(f32x4_t (&v)[XK / 16][2], const RowPtrs& rows, const float* base, int64_t ld, int o0, int on, int k0,
+                 int ke) {
     const float* z = reinterpret_cast<const float*>(g_zero_row);
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const int kk = k0 + xs_kg<KMAJ>(q) * 8;
+    for (int q = 0; q < XK / 16; q++) {
+        const int kk = k0 + xs_kg<KMAJ, XK>(q) * 8;
         if (KMAJ) {
             v[q][0] = load4v<VEC>(rows.p[q], kk, ke);
             v[q][1] = load4v<VEC>(rows.p[q], kk + 4, ke);
         } else {
-            const int o = o0 + xs_row<KMAJ>(q);
+            const int o = o0 + xs_row<KMAJ, XK>(q);
 #pragma unroll
             for (int c = 0; c < 8; c++) {
                 const bool ok = (kk + c < ke) && (o < on);
@@ -324,13 +327,13 @@ DEV void xs_load(f32x4_t (&v)[2][2], const RowPtrs& rows, const float* base, int
         }
     }
 }
-template <bool KMAJ>
-DEV void xs_store(uint16_t (*lds)[BM][XBK + XPAD], const f32x4_t (&v)[2][2]) {
+template <bool KMAJ, int XK>
+DEV void xs_store(uint16_t (*lds)[BM][XK + XPAD], const f32x4_t (&v)[XK / 16][2]) {
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < XK / 16; q++) {
         u32x4_t h, m, l;
         split3(v[q], h, m, l);
-        const int row = xs_row<KMAJ>(q), c = xs_kg<KMAJ>(q) * 8;
+        const int row = xs_row<KMAJ, XK>(q), c = xs_kg<KMAJ, XK>(q) * 8;
         *reinterpret_cast<u32x4_t*>(&lds[0][row][c]) = h;
         *reinterpret_cast<u32x4_t*>(&lds[1][row][c]) = m;
         *reinterpret_cast<u32x4_t*>(&lds[2][row][c]) = l;
@@ -338,27 +341,31 @@ DEV void xs_store(uint16_t (*lds)[BM][XBK + XPAD], const f32x4_t (&v)[2][2]) {
 }
 
 // B operand given pre-split (BPRE): three bf16 planes [3][rows][ldbp] (k contiguous; rows padded to a
-// multiple of 128 and ldbp a multiple of XBK, zero filled), plane stride g.bplane elements.  A
+// multiple of 128 and ldbp a multiple of 64, zero filled), plane stride g.bplane elements.  A
 // weight matrix is reused by every row tile of a minibatch, so it is split once per minibatch
-// (split_weight) instead of once per tile and stage.  Per thread and stage: two 16-byte chunks
-// per plane (row e >> 2, chunk e & 3 of 8 bf16).
-DEV void xp_load(u32x4_t (&v)[3][2], const uint16_t* B, int64_t ldb, int64_t plane, int j0, int k0, int ke) {
+// (split_weight) instead of once per tile and stage.  Per thread and stage: XK / 16 16-byte chunks
+// per plane (row e / KG, chunk e % KG of 8 bf16).
+template <int XK>
+DEV void xp_load(u32x4_t (&v)[3][XK / 16], const uint16_t* B, int64_t ldb, int64_t plane, int j0, int k0, int ke) {
+    constexpr int KG = XK / 8;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < XK / 16; q++) {
         const int e = threadIdx.x + 256 * q;
-        const int64_t off = (int64_t)(j0 + (e >> 2)) * ldb + k0 + (e & 3) * 8;
-        const bool ok = k0 + (e & 3) * 8 < ke;
+        const int64_t off = (int64_t)(j0 + e / KG) * ldb + k0 + (e % KG) * 8;
+        const bool ok = k0 + (e % KG) * 8 < ke;
 #pragma unroll
         for (int p = 0; p < 3; p++)
             v[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? B + p * plane + off : reinterpret_cast<const uint16_t*>(g_zero_row));
     }
 }
-DEV void xp_store(uint16_t (*lds)[BM][XBK + XPAD], const u32x4_t (&v)[3][2]) {
+template <int XK>
+DEV void xp_store(uint16_t (*lds)[BM][XK + XPAD], const u32x4_t (&v)[3][XK / 16]) {
+    constexpr int KG = XK / 8;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < XK / 16; q++) {
         const int e = threadIdx.x + 256 * q;
 #pragma unroll
-        for (int p = 0; p < 3; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e >> 2][(e & 3) * 8]) = v[p][q];
+        for (int p = 0; p < 3; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e / KG][(e % KG) * 8]) = v[p][q];
     }
 }
 
@@ -379,11 +386,52 @@ __global__ void split_weight(const float* W, int out, int in, int trans, int row
     planes[2 * plane + e] = f2bf(r1 - bf2f(m));
 }
 
-template <int LA, int LB, bool AV, bool BV, bool BPRE = false>
-__global__ void __launch_bounds__(256, 2) gemm_x6(GemmArgs g) {
+// Stage variants (the x6 GEMM's pipeline shape):
+//   V = 0: 32-deep stages, one LDS buffer, two workgroups per CU
+//   V = 1: 64-deep stages, one LDS buffer, one workgroup per CU
+//   V = 2: 32-deep stages, two LDS buffers (one barrier per stage: the next stage is split and
+//          stored while this stage's MFMAs run), one workgroup per CU
+template <int V> struct X6Shape;
+template <> struct X6Shape<0> { static constexpr int XK = 32, NB = 1, OCC = 2; };
+template <> struct X6Shape<1> { static constexpr int XK = 64, NB = 1, OCC = 1; };
+template <> struct X6Shape<2> { static constexpr int XK = 32, NB = 2, OCC = 1; };
+
+template <int XK>
+DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
+                       f32x16 (&acc)[2][2], f32x16 (&cor)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < XK / 16; ks++) {
+        const int kof = ks * 16 + 8 * (lane >> 5);
+        bf16x8 a[3][2], b[3][2];
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                a[p][u] = *(const bf16x8*)&As[p][ra + 32 * u][kof];
+                b[p][u] = *(const bf16x8*)&Bs[p][rb + 32 * u][kof];
+            }
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                f32x16 c = cor[ti][tj];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ti], b[1][tj], c, 0, 0, 0);  // m m
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][ti], b[0][tj], c, 0, 0, 0);  // l h
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[2][tj], c, 0, 0, 0);  // h l
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ti], b[0][tj], c, 0, 0, 0);  // m h
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h m
+                cor[ti][tj] = c;
+                acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[0][tj], acc[ti][tj], 0, 0, 0);
+            }
+    }
+}
+
+template <int LA, int LB, bool AV, bool BV, bool BPRE, int V>
+__global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
+    constexpr int XK = X6Shape<V>::XK, NB = X6Shape<V>::NB, NQ = XK / 16;
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
-    __shared__ uint16_t As[3][BM][XBK + XPAD];
-    __shared__ uint16_t Bs[3][BN][XBK + XPAD];
+    __shared__ uint16_t As[NB][3][BM][XK + XPAD];
+    __shared__ uint16_t Bs[NB][3][BN][XK + XPAD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
     const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
@@ -397,58 +445,52 @@ __global__ void __launch_bounds__(256, 2) gemm_x6(GemmArgs g) {
         for (int b = 0; b < 2; b++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[a][b][r] = cor[a][b][r] = 0.f;
-    f32x4_t va[2][2], vb[2][2];
-    u32x4_t vp[3][2];
+    f32x4_t va[NQ][2], vb[NQ][2];
+    u32x4_t vp[3][NQ];
     const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
-    const RowPtrs arow = xs_rows<AK>(g.A, g.lda, i0, g.I);
-    const RowPtrs brow = xs_rows<BKM>(g.B, g.ldb, j0, g.J);
-    xs_load<AK, AV>(va, arow, g.A, g.lda, i0, g.I, kb, ke);
-    if (BPRE)
-        xp_load(vp, Bp, g.ldb, g.bplane, j0, kb, ke);
-    else
-        xs_load<BKM, BV>(vb, brow, g.B, g.ldb, j0, g.J, kb, ke);
+    const RowPtrs arow = xs_rows<AK, XK>(g.A, g.lda, i0, g.I);
+    const RowPtrs brow = xs_rows<BKM, XK>(g.B, g.ldb, j0, g.J);
+    auto load_stage = [&](int k0) {
+        xs_load<AK, AV, XK>(va, arow, g.A, g.lda, i0, g.I, k0, ke);
+        if (BPRE)
+            xp_load<XK>(vp, Bp, g.ldb, g.bplane, j0, k0, ke);
+        else
+            xs_load<BKM, BV, XK>(vb, brow, g.B, g.ldb, j0, g.J, k0, ke);
+    };
+    auto store_stage = [&](int buf) {
+        xs_store<AK, XK>(As[buf], va);
+        if (BPRE)
+            xp_store<XK>(Bs[buf], vp);
+        else
+            xs_store<BKM, XK>(Bs[buf], vb);
+    };
     const int ra = wm * 64 + (lane & 31), rb = wn * 64 + (lane & 31);
-    for (int k0 = kb; k0 < ke; k0 += XBK) {
-        xs_store<AK>(As, va);
-        if (BPRE)
-            xp_store(Bs, vp);
-        else
-            xs_store<BKM>(Bs, vb);
-        __syncthreads();
-        // prefetch the next stage into registers while the MFMAs run; unconditional (past ke it
-        // reads the zero row) so the loop-carried registers are the load destinations
-        xs_load<AK, AV>(va, arow, g.A, g.lda, i0, g.I, k0 + XBK, ke);
-        if (BPRE)
-            xp_load(vp, Bp, g.ldb, g.bplane, j0, k0 + XBK, ke);
-        else
-            xs_load<BKM, BV>(vb, brow, g.B, g.ldb, j0, g.J, k0 + XBK, ke);
-        __builtin_amdgcn_sched_barrier(0);  // keep the split of the prefetched stage after the MFMAs
-#pragma unroll
-        for (int ks = 0; ks < XBK / 16; ks++) {
-            const int kof = ks * 16 + 8 * (lane >> 5);
-            bf16x8 a[3][2], b[3][2];
-#pragma unroll
-            for (int p = 0; p < 3; p++)
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    a[p][u] = *(const bf16x8*)&As[p][ra + 32 * u][kof];
-                    b[p][u] = *(const bf16x8*)&Bs[p][rb + 32 * u][kof];
-                }
-#pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++) {
-                    f32x16 c = cor[ti][tj];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ti], b[1][tj], c, 0, 0, 0);  // m m
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][ti], b[0][tj], c, 0, 0, 0);  // l h
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[2][tj], c, 0, 0, 0);  // h l
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ti], b[0][tj], c, 0, 0, 0);  // m h
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h m
-                    cor[ti][tj] = c;
-                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ti], b[0][tj], acc[ti][tj], 0, 0, 0);
-                }
+    load_stage(kb);
+    if (NB == 1) {
+        for (int k0 = kb; k0 < ke; k0 += XK) {
+            store_stage(0);
+            __syncthreads();
+            // prefetch the next stage into registers while the MFMAs run; unconditional (past ke it
+            // reads the zero row) so the loop-carried registers are the load destinations
+            load_stage(k0 + XK);
+            __builtin_amdgcn_sched_barrier(0);  // keep the split of the prefetched stage after the MFMAs
+            x6_mfma_stage<XK>(As[0], Bs[0], ra, rb, lane, acc, cor);
+            __syncthreads();
         }
+    } else {
+        store_stage(0);
         __syncthreads();
+        load_stage(kb + XK);
+        int buf = 0;
+        for (int k0 = kb; k0 < ke; k0 += XK) {
+            // this stage's MFMAs on buf; the next stage (already in registers) is split into the
+            // other buffer, free since the previous barrier; then the stage after is prefetched
+            x6_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
+            store_stage(buf ^ 1);
+            load_stage(k0 + 2 * XK);
+            __syncthreads();
+            buf ^= 1;
+        }
     }
     float* C = g.C + (int64_t)tl.z * g.c_split;
     const int h = lane >> 5, l32 = lane & 31;
@@ -648,13 +690,15 @@ DEV float wave_max(float v) {
 
 
 // LayerNorm (eps 1e-5, biased variance) + LeakyReLU, training: one wave per row.
-// Keeps xhat [R,H] and act [R,H] for the backward, rstd [R].
+// Keeps act [R,H] and the row statistics stats [R] = (mean, rstd) for the backward, which
+// recomputes xhat = (z - mean) * rstd from the untouched pre-norm input z with the same operations
+// (bit-identical to a stored xhat, one [R,H] write less per layer).
 // Lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (float4 loads / stores when H is a
 // multiple of 4); gamma / beta stay in registers and each wave walks LNF_ROWS/4 rows.
 constexpr int LNF_ROWS = 8;
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const float* gamma, const float* beta, int R, int H,
-                                                     float slope, int use_ln, float* xhat, float* act, float* rstd_out) {
+                                                     float slope, int use_ln, float* act, float2* stats) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c0 = lane * MAXH;
     const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
@@ -681,12 +725,12 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
             for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? z[q] : 0.f;
         }
         float xh[MAXH], a[MAXH];
-        float rs = 1.f;
+        float rs = 1.f, mean = 0.f;
         if (use_ln) {
             float s = 0.f;
 #pragma unroll
             for (int q = 0; q < MAXH; q++) s += v[q];
-            const float mean = wave_sum(s) / (float)H;
+            mean = wave_sum(s) / (float)H;
             float s2 = 0.f;
 #pragma unroll
             for (int q = 0; q < MAXH; q++) {
@@ -705,23 +749,17 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
             float hv = use_ln ? xh[q] * g[q] + b[q] : xh[q];
             a[q] = hv > 0.f ? hv : hv * slope;
         }
-        float* xo = xhat + (int64_t)row * H + c0;
         float* ao = act + (int64_t)row * H + c0;
         if (vec) {
 #pragma unroll
-            for (int q = 0; q < MAXH; q += 4) {
-                *reinterpret_cast<float4*>(xo + q) = make_float4(xh[q], xh[q + 1], xh[q + 2], xh[q + 3]);
+            for (int q = 0; q < MAXH; q += 4)
                 *reinterpret_cast<float4*>(ao + q) = make_float4(a[q], a[q + 1], a[q + 2], a[q + 3]);
-            }
         } else {
 #pragma unroll
             for (int q = 0; q < MAXH; q++)
-                if (c0 + q < H) {
-                    xo[q] = xh[q];
-                    ao[q] = a[q];
-                }
+                if (c0 + q < H) ao[q] = a[q];
         }
-        if (use_ln && lane == 0) rstd_out[row] = rs;
+        if (lane == 0) stats[row] = make_float2(mean, rs);
     }
 }
 
@@ -804,7 +842,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 // in registers; each of the 4 waves walks LNB_ROWS/4 rows.
 constexpr int LNB_ROWS = 32;
 template <int MAXH>
-__global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* xhat, const float* rstd, const float* gamma,
+__global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* Z, const float2* stats, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
                                                  float* part) {
     __shared__ float red[4][3][64 * MAXH];
@@ -824,7 +862,8 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         const int row = r0 + rr;
         if (row >= R) break;
         const float* da = dA + (int64_t)row * H + c0;
-        const float* xh = xhat + (int64_t)row * H + c0;
+        const float* xh = Z + (int64_t)row * H + c0;  // pre-norm z; xhat recomputed below
+        const float2 st = stats[row];
         float dh[MAXH], x[MAXH], av[MAXH];
         if (vec) {
 #pragma unroll
@@ -842,6 +881,10 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
                 av[q] = in ? da[q] : 0.f;
             }
         }
+        if (use_ln) {
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) x[q] = (x[q] - st.x) * st.y;  // the forward's xhat, same ops
+        }
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int q = 0; q < MAXH; q++) {
@@ -855,7 +898,7 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         float d[MAXH];
         if (use_ln) {
             float m1 = wave_sum(s1) / (float)H, m2 = wave_sum(s2) / (float)H;
-            float rs = rstd[row];
+            float rs = st.y;
 #pragma unroll
             for (int q = 0; q < MAXH; q++) d[q] = rs * (dh[q] * g[q] - m1 - x[q] * m2);
         } else {

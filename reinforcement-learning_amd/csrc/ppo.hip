@@ -43,7 +43,19 @@ constexpr int kMaxSplits = 256;
 // concurrent gemm_f32 workgroups on the device (CUs x RLGPU_GEMM_OCC), set at create: the split-K
 // weight gradients are sized to fill whole rounds of workgroups
 int g_cus = 256;  // compute units of the device, set at create
-inline int gemm_slots(int mode) { return g_cus * (mode == RLGPU_GEMM_F32X6 ? 2 : RLGPU_GEMM_OCC); }
+// x6 GEMM pipeline shape (mlp::X6Shape): RLGPU_X6_VARIANT=0/1/2 selects it (experiments), default 0
+inline int x6_variant() {
+    static const int v = [] {
+        const char* e = getenv("RLGPU_X6_VARIANT");
+        int x = e ? atoi(e) : 0;
+        return (x >= 0 && x <= 2) ? x : 0;
+    }();
+    return v;
+}
+inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
+inline int gemm_slots(int mode) { return g_cus * (mode == RLGPU_GEMM_F32X6 ? x6_occ() : RLGPU_GEMM_OCC); }
+// K granularity of a split-K chunk: a whole number of stages of either kernel
+inline int kgran(int mode) { return mode == RLGPU_GEMM_F32X6 ? mlp::XKMAX : mlp::BK; }
 
 }  // namespace
 
@@ -80,6 +92,22 @@ namespace {
 
 // C[I,J] (+ bias) = A . B with the layouts of mlp::gemm_f32.  *_tail_ok: the operand's rows are
 // zero-padded up to a multiple of 4 past the bound (so float4 loads may straddle it).
+template <int LA, int LB, bool AV, bool BV, bool PRE>
+void x6_launch_v(dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
+    switch (x6_variant()) {
+        case 1: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 1>), grid, blk, 0, s, g); break;
+        case 2: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 2>), grid, blk, 0, s, g); break;
+        default: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 0>), grid, blk, 0, s, g); break;
+    }
+}
+template <int LA, int LB>
+void x6_launch(bool av, bool bv, dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
+    if (av && bv) x6_launch_v<LA, LB, true, true, false>(grid, blk, s, g);
+    else if (av) x6_launch_v<LA, LB, true, false, false>(grid, blk, s, g);
+    else if (bv) x6_launch_v<LA, LB, false, true, false>(grid, blk, s, g);
+    else x6_launch_v<LA, LB, false, false, false>(grid, blk, s, g);
+}
+
 void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
               const float* bias, int I, int J, int K, int splits, hipStream_t s, bool a_tail_ok = false,
               bool b_tail_ok = false) {
@@ -95,7 +123,7 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
     g.J = J;
     g.K = K;
     int chunk = (int)ceil_div(K, splits);
-    g.kchunk = (int)ceil_div(chunk, mlp::BK) * mlp::BK;
+    g.kchunk = (int)ceil_div(chunk, kgran(mode)) * kgran(mode);
     int z = (int)ceil_div(K, g.kchunk);
     g.c_split = (int64_t)I * ldc;
     // float4 path: 16-byte aligned rows and a bound (K for k-contiguous, I / J otherwise) that is a
@@ -110,10 +138,7 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
 #define RLGPU_GEMM_CASE(LA, LB)                                                                                  \
     if (la == LA && lb == LB) {                                                                                  \
         if (mode == RLGPU_GEMM_F32X6) {                                                                          \
-            if (av && bv) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, true, true>), grid, blk, 0, s, g);            \
-            else if (av) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, true, false>), grid, blk, 0, s, g);           \
-            else if (bv) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, false, true>), grid, blk, 0, s, g);           \
-            else hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, false, false>), grid, blk, 0, s, g);                  \
+            x6_launch<LA, LB>(av, bv, grid, blk, s, g);                                                          \
         } else {                                                                                                 \
             if (av && bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, true>), grid, blk, 0, s, g);           \
             else if (av) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, false>), grid, blk, 0, s, g);          \
@@ -144,7 +169,7 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
     g.I = I;
     g.J = J;
     g.K = K;
-    g.kchunk = (int)ceil_div(K, mlp::BK) * mlp::BK;
+    g.kchunk = (int)ceil_div(K, mlp::XKMAX) * mlp::XKMAX;
     g.c_split = 0;
     g.bplane = bplane;
     g.gx = (int)ceil_div(J, mlp::BN);
@@ -153,9 +178,9 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
     const bool av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && (K % 4 == 0 || a_tail_ok);
     dim3 grid(g.gx * g.gy), blk(256);
     if (av)
-        hipLaunchKernelGGL((mlp::gemm_x6<mlp::A_IK, mlp::B_JK, true, true, true>), grid, blk, 0, s, g);
+        x6_launch_v<mlp::A_IK, mlp::B_JK, true, true, true>(grid, blk, s, g);
     else
-        hipLaunchKernelGGL((mlp::gemm_x6<mlp::A_IK, mlp::B_JK, false, true, true>), grid, blk, 0, s, g);
+        x6_launch_v<mlp::A_IK, mlp::B_JK, false, true, true>(grid, blk, s, g);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -193,7 +218,7 @@ int splits_for(int mode, int rows, int out, int in) {
 void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
                  bool x_tail_ok = false) {
     int splits = splits_for(m.mode, n, out, in);
-    int chunk = (int)ceil_div(ceil_div(n, splits), mlp::BK) * mlp::BK;
+    int chunk = (int)ceil_div(ceil_div(n, splits), kgran(m.mode)) * kgran(m.mode);
     int z = (int)ceil_div(n, chunk);
     gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
     int64_t e = (int64_t)out * in;
@@ -248,7 +273,7 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
-                           h->cfg.leaky_slope, h->cfg.layer_norm, m.xhat[l], m.act[l], m.rstd[l]);
+                           h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]));
         RLGPU_CHECK_HIP(hipGetLastError());
         in = m.act[l];
         ld = L.out;
@@ -301,7 +326,7 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
-        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, m.dA, m.xhat[l], m.rstd[l], gg, bb, n, L.out,
+        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, m.dA, m.xhat[l], reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.dZ, m.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
@@ -409,12 +434,12 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
         if (L.in > h->hmax && l > 0) h->hmax = L.in;
         if (m.mode == RLGPU_GEMM_F32X6 && L.out > 1) {  // the rank-1 critic head has no GEMM
             L.sf_rows = (int)ceil_div(L.out, mlp::BN) * mlp::BN;
-            L.sf_ld = (int)ceil_div(L.in, mlp::BK) * mlp::BK;
+            L.sf_ld = (int)ceil_div(L.in, mlp::XKMAX) * mlp::XKMAX;
             L.sf = m.nsplit;
             m.nsplit += 3 * (int64_t)L.sf_rows * L.sf_ld;
             if (l > 0) {  // dA of the first layer is never needed
                 L.sb_rows = (int)ceil_div(L.in, mlp::BN) * mlp::BN;
-                L.sb_ld = (int)ceil_div(L.out, mlp::BK) * mlp::BK;
+                L.sb_ld = (int)ceil_div(L.out, mlp::XKMAX) * mlp::XKMAX;
                 L.sb = m.nsplit;
                 m.nsplit += 3 * (int64_t)L.sb_rows * L.sb_ld;
             }
@@ -488,7 +513,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 for (int l = 0; l < nh; l++) {
                     m.xhat.push_back(h->alloc<float>(R * m.L[l].out));
                     m.act.push_back(h->alloc<float>(R * m.L[l].out));
-                    m.rstd.push_back(h->alloc<float>(R));
+                    m.rstd.push_back(h->alloc<float>(2 * R));  // (mean, rstd) per row
                 }
             }
             int H = h->hmax;
@@ -823,7 +848,25 @@ extern "C" int rlgpu_gemm(int32_t mode, int32_t a_layout, int32_t b_layout, cons
         RLGPU_REQUIRE(I > 0 && J > 0 && K > 0 && splits >= 1, "rlgpu_gemm: bad sizes");
         RLGPU_REQUIRE((a_layout == 0 && (b_layout == 0 || b_layout == 1)) || (a_layout == 1 && b_layout == 1),
                       "rlgpu_gemm: unsupported layout pair");
-        gemm_f32(mode, a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, rlgpu::as_stream(stream));
+        hipStream_t s = rlgpu::as_stream(stream);
+        if (mode == RLGPU_GEMM_F32X6 && a_layout == 0 && splits == 1) {
+            // the training path's form: B split once into padded planes, then the pre-split kernel
+            const int rows = (int)ceil_div(J, mlp::BN) * mlp::BN, ld = (int)ceil_div(K, mlp::XKMAX) * mlp::XKMAX;
+            const int64_t plane = (int64_t)rows * ld;
+            uint16_t* planes = nullptr;
+            RLGPU_CHECK_HIP(hipMallocAsync((void**)&planes, 3 * plane * sizeof(uint16_t), s));
+            if (b_layout == 0)
+                hipLaunchKernelGGL(mlp::split_weight, dim3(ceil_div(plane, 256)), dim3(256), 0, s, d_B, J, (int)ldb, 0, rows, ld,
+                                   planes);
+            else
+                hipLaunchKernelGGL(mlp::split_weight, dim3(ceil_div(plane, 256)), dim3(256), 0, s, d_B, K, (int)ldb, 1, rows, ld,
+                                   planes);
+            RLGPU_CHECK_HIP(hipGetLastError());
+            gemm_x6_pre(d_A, lda, planes, ld, plane, d_C, ldc, d_bias, I, J, K, s);
+            RLGPU_CHECK_HIP(hipFreeAsync(planes, s));
+            return;
+        }
+        gemm_f32(mode, a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, s);
     });
 }
 
