@@ -64,6 +64,7 @@ typedef struct {
     int32_t n_critic_layers;
     int32_t deterministic;         /* LearnerConfig::deterministic */
     int32_t train_gemm;            /* rlgpu_ppo_config.train_gemm */
+    int32_t infer_fp16;            /* rlgpu_ppo_config.infer_fp16 (C5: fp16 inference) */
     /* sharding */
     int32_t rank, world;
     /* arena meshes (rlgpu_envset_config.mesh_*; NULL = built-in synthetic arena) */

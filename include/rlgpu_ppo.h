@@ -39,7 +39,7 @@ extern "C" {
 typedef struct {
     int32_t obs_size;                         /* 167 (AdvancedObs) */
     int32_t num_actions;                      /* 90 (DefaultAction) */
-    int32_t policy_layers[RLGPU_MAX_LAYERS];  /* hidden sizes, e.g. {512, 512} */
+    int32_t policy_layers[RLGPU_MAX_LAYERS];  /* hidden sizes (1..2048), e.g. {512, 512} */
     int32_t n_policy_layers;
     int32_t critic_layers[RLGPU_MAX_LAYERS];
     int32_t n_critic_layers;
@@ -54,6 +54,8 @@ typedef struct {
     uint64_t seed;                            /* parameter init + action sampling (Philox) */
     int32_t train_gemm;                       /* training GEMM arithmetic: RLGPU_GEMM_F32X6 (0, default)
                                                  or RLGPU_GEMM_F32 (1) -- see rlgpu_gemm */
+    int32_t infer_fp16;                       /* 16-bit inference copy: 0 = bf16 (the reference's seqHalf),
+                                                 1 = fp16 on v_mfma_f32_32x32x16_f16 (BASELINE config C5) */
 } rlgpu_ppo_config;
 
 /* fp32 GEMM arithmetic of the training path (libtorch fp32 Linear forward / backward in the

@@ -13,6 +13,7 @@
 // order, so every result is deterministic run to run.
 #pragma once
 #include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -48,6 +49,17 @@ DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays Na
     return *reinterpret_cast<uint16_t*>(&b);
 }
 DEV float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+// 16-bit inference storage: bf16 (the reference's seqHalf) or fp16 (F16, BASELINE config C5)
+template <bool F16>
+DEV float h2f(uint16_t u) {
+    if (F16) return __half2float(__ushort_as_half(u));
+    return bf2f(u);
+}
+template <bool F16>
+DEV uint16_t f2h(float f) {
+    if (F16) return __half_as_ushort(__float2half(f));
+    return f2bf(f);
+}
 
 // Operand staging.  Every global load is branch-free (divergent bounds branches made the compiler
 // drain vmcnt after each load and serialised the register prefetch): absent rows read a zero row,
@@ -561,6 +573,15 @@ DEV void htile_store(uint16_t (*lds)[HBK + HPAD], const u32x4 (&r)[HQ]) {
     }
 }
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <bool F16>
+DEV f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool F16>
 __global__ void __launch_bounds__(256, 2) gemm_bf16(HGemmArgs g) {
     __shared__ uint16_t As[BM][HBK + HPAD];
     __shared__ uint16_t Bs[BN][HBK + HPAD];
@@ -598,10 +619,10 @@ __global__ void __launch_bounds__(256, 2) gemm_bf16(HGemmArgs g) {
             bf16x8 a1 = *(const bf16x8*)&As[wm * 64 + 32 + (lane & 31)][kof];
             bf16x8 b0 = *(const bf16x8*)&Bs[wn * 64 + (lane & 31)][kof];
             bf16x8 b1 = *(const bf16x8*)&Bs[wn * 64 + 32 + (lane & 31)][kof];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+            acc[0][0] = mfma16<F16>(a0, b0, acc[0][0]);
+            acc[0][1] = mfma16<F16>(a0, b1, acc[0][1]);
+            acc[1][0] = mfma16<F16>(a1, b0, acc[1][0]);
+            acc[1][1] = mfma16<F16>(a1, b1, acc[1][1]);
         }
         __syncthreads();
     }
@@ -611,29 +632,31 @@ __global__ void __launch_bounds__(256, 2) gemm_bf16(HGemmArgs g) {
         for (int tj = 0; tj < 2; tj++) {
             int j = j0 + wn * 64 + tj * 32 + (lane & 31);
             if (j >= g.J) continue;
-            float bj = g.bias ? bf2f(g.bias[j]) : 0.f;
+            float bj = g.bias ? h2f<F16>(g.bias[j]) : 0.f;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (i < g.I) g.C[(int64_t)i * g.ldc + j] = f2bf(acc[ti][tj][r] + bj);
+                if (i < g.I) g.C[(int64_t)i * g.ldc + j] = f2h<F16>(acc[ti][tj][r] + bj);
             }
         }
 }
 
 // f32 rows [n][C] -> bf16 rows [n][ldx] (zero padded): the inference input of the first layer
+template <bool F16>
 __global__ void rows_to_bf16(const float* src, int C, int n, uint16_t* X, int ldx) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)n * ldx) return;
     int r = (int)(e / ldx), c = (int)(e % ldx);
-    X[e] = c < C ? f2bf(src[(int64_t)r * C + c]) : (uint16_t)0;
+    X[e] = c < C ? f2h<F16>(src[(int64_t)r * C + c]) : (uint16_t)0;
 }
 
 // fp32 Linear.weight [out][in] -> padded bf16 [out][ldp] (zeros past in)
+template <bool F16>
 __global__ void weight_to_bf16(const float* w, int out, int in, uint16_t* h, int ldp) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)out * ldp) return;
     int o = (int)(e / ldp), k = (int)(e % ldp);
-    h[e] = k < in ? f2bf(w[(int64_t)o * in + k]) : (uint16_t)0;
+    h[e] = k < in ? f2h<F16>(w[(int64_t)o * in + k]) : (uint16_t)0;
 }
 
 // out[e] (+)= sum_s part[s*stride + e], fixed order (deterministic split-K reduction)
@@ -764,7 +787,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
 }
 
 // bf16 inference variant: Z bf16 in, bf16(LeakyReLU(bf16(LN(Z)))) out (torch bf16 module chain).
-template <int MAXH>
+template <int MAXH, bool F16>
 __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const uint16_t* gamma, const uint16_t* beta, int R,
                                                       int H, float slope, int use_ln, uint16_t* out) {
     // lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (16-byte loads / stores of 8 bf16
@@ -776,8 +799,8 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
         const int c = c0 + q;
-        g[q] = (use_ln && c < H) ? bf2f(gamma[c]) : 1.f;
-        b[q] = (use_ln && c < H) ? bf2f(beta[c]) : 0.f;
+        g[q] = (use_ln && c < H) ? h2f<F16>(gamma[c]) : 1.f;
+        b[q] = (use_ln && c < H) ? h2f<F16>(beta[c]) : 0.f;
     }
     for (int i = 0; i < LNF_ROWS / 4; i++) {
         const int row = blockIdx.x * LNF_ROWS + i * 4 + wv;
@@ -790,13 +813,13 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
                 u32x4 t = *reinterpret_cast<const u32x4*>(z + q);
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    v[q + 2 * k] = __uint_as_float(t[k] << 16);
-                    v[q + 2 * k + 1] = __uint_as_float(t[k] & 0xffff0000u);
+                    v[q + 2 * k] = h2f<F16>((uint16_t)(t[k] & 0xffffu));
+                    v[q + 2 * k + 1] = h2f<F16>((uint16_t)(t[k] >> 16));
                 }
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? bf2f(z[q]) : 0.f;
+            for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? h2f<F16>(z[q]) : 0.f;
         }
         float mean = 0.f, rs = 1.f;
         if (use_ln) {
@@ -815,8 +838,8 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
         uint16_t o[MAXH];
 #pragma unroll
         for (int q = 0; q < MAXH; q++) {
-            float hv = use_ln ? bf2f(f2bf((v[q] - mean) * rs * g[q] + b[q])) : v[q];
-            o[q] = f2bf(hv > 0.f ? hv : hv * slope);
+            float hv = use_ln ? h2f<F16>(f2h<F16>((v[q] - mean) * rs * g[q] + b[q])) : v[q];
+            o[q] = f2h<F16>(hv > 0.f ? hv : hv * slope);
         }
         uint16_t* op = out + (int64_t)row * H + c0;
         if (vec) {
@@ -942,10 +965,19 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         if (H <= 128) return &NAME<2>;                             \
         if (H <= 256) return &NAME<4>;                             \
         if (H <= 512) return &NAME<8>;                             \
-        return &NAME<16>;                                          \
+        if (H <= 1024) return &NAME<16>;                           \
+        return &NAME<32>;                                          \
     }
 RLGPU_NPER_DISPATCH(ln_act_fwd_f32)
-RLGPU_NPER_DISPATCH(ln_act_fwd_bf16)
+template <bool F16>
+inline decltype(&ln_act_fwd_bf16<16, F16>) ln_act_fwd_bf16_any(int H) {
+    if (H <= 64) return &ln_act_fwd_bf16<1, F16>;
+    if (H <= 128) return &ln_act_fwd_bf16<2, F16>;
+    if (H <= 256) return &ln_act_fwd_bf16<4, F16>;
+    if (H <= 512) return &ln_act_fwd_bf16<8, F16>;
+    if (H <= 1024) return &ln_act_fwd_bf16<16, F16>;
+    return &ln_act_fwd_bf16<32, F16>;
+}
 RLGPU_NPER_DISPATCH(ln_act_bwd)
 
 // Rank-1 output layer (the critic's Linear(H, 1)): GEMM tiles would be 1/128 occupied, so the

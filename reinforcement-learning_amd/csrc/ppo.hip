@@ -15,6 +15,13 @@ namespace {
 
 using rlgpu::ceil_div;
 
+// launch a kernel template instantiated on the 16-bit inference format (bf16 / fp16)
+#define RLGPU_H16_LAUNCH(F16, KERN, ...)                                                     \
+    do {                                                                                     \
+        if (F16) hipLaunchKernelGGL(KERN<true>, __VA_ARGS__);                                \
+        else hipLaunchKernelGGL(KERN<false>, __VA_ARGS__);                                   \
+    } while (0)
+
 struct Layer {
     int in, out;
     int64_t w, b, g, be;      // offsets into the flat fp32 buffers (g/be = -1 without LayerNorm)
@@ -232,7 +239,7 @@ void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx
 // grad[0..n) += column sums of nblk partial rows (stride apart) -- two fixed-order levels
 void reduce_partials(Model& m, const float* part, int nblk, int64_t stride, int n, float* grad, hipStream_t s) {
     const int G = nblk >= 256 ? 16 : 1;
-    float* mid = m.mid;  // [16][<= 3 * 1024]
+    float* mid = m.mid;  // [16][<= 3 * max(H, 1024)]
     if (G > 1) {
         hipLaunchKernelGGL(mlp::reduce_cols, dim3(ceil_div(n, 64), G), dim3(1024), 0, s, part, nblk, stride, (int64_t)0, n,
                            mid, (int64_t)n, 0);
@@ -360,7 +367,7 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, co
     int nh = (int)m.L.size() - 1;
     {
         int64_t e = (int64_t)n * h->xh_ld;
-        hipLaunchKernelGGL(mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, m.in, n, h->xh, h->xh_ld);
+        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, m.in, n, h->xh, h->xh_ld);
         RLGPU_CHECK_HIP(hipGetLastError());
     }
     const uint16_t* in = h->xh;
@@ -381,12 +388,12 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, co
         g.K = L.in_pad;
         g.gx = (int)ceil_div(L.out, mlp::BN);
         g.gy = (int)ceil_div(n, mlp::BM);
-        hipLaunchKernelGGL(mlp::gemm_bf16, dim3(g.gx * g.gy), dim3(256), 0, s, g);
+        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::gemm_bf16, dim3(g.gx * g.gy), dim3(256), 0, s, g);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (l == nh) break;
         const uint16_t* gg = L.hg >= 0 ? P + L.hg : nullptr;
         const uint16_t* bb = L.hbe >= 0 ? P + L.hbe : nullptr;
-        hipLaunchKernelGGL(mlp::ln_act_fwd_bf16_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
+        hipLaunchKernelGGL(h->cfg.infer_fp16 ? mlp::ln_act_fwd_bf16_any<true>(L.out) : mlp::ln_act_fwd_bf16_any<false>(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, h->ah[cur]);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = h->ah[cur];
@@ -463,10 +470,10 @@ void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, hipStream_
     const Model& m = h->M[mi];
     for (auto& L : m.L) {
         int64_t e = (int64_t)L.out * L.in_pad;
-        hipLaunchKernelGGL(mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, src + (L.w - m.off), L.out, L.in,
+        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, src + (L.w - m.off), L.out, L.in,
                            dst + L.hw, L.in_pad);
         int nv = L.g >= 0 ? 3 * L.out : L.out;  // bias | LN weight | LN bias, contiguous in both layouts
-        hipLaunchKernelGGL(ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, src + (L.b - m.off), dst + L.hb,
+        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, src + (L.b - m.off), dst + L.hb,
                            (int64_t)nv);
     }
     RLGPU_CHECK_HIP(hipGetLastError());
@@ -488,9 +495,9 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                       "1..8 hidden layers per model");
         RLGPU_REQUIRE(cfg->max_rows > 0, "max_rows must be > 0");
         for (int i = 0; i < cfg->n_policy_layers; i++)
-            RLGPU_REQUIRE(cfg->policy_layers[i] > 0 && cfg->policy_layers[i] <= 1024, "hidden sizes must be in [1, 1024]");
+            RLGPU_REQUIRE(cfg->policy_layers[i] > 0 && cfg->policy_layers[i] <= 2048, "hidden sizes must be in [1, 2048]");
         for (int i = 0; i < cfg->n_critic_layers; i++)
-            RLGPU_REQUIRE(cfg->critic_layers[i] > 0 && cfg->critic_layers[i] <= 1024, "hidden sizes must be in [1, 1024]");
+            RLGPU_REQUIRE(cfg->critic_layers[i] > 0 && cfg->critic_layers[i] <= 2048, "hidden sizes must be in [1, 2048]");
         auto* h = new rlgpu_ppo();
         try {
             h->cfg = *cfg;
@@ -542,7 +549,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 m.dZ = h->alloc<float>(R * H);
                 m.wpart = h->alloc<float>(wpart_max);
                 m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
-                m.mid = h->alloc<float>(16 * 3 * 1024);
+                m.mid = h->alloc<float>(16 * 3 * (int64_t)std::max(std::max(H, omax) + 1, 1024));
                 if (m.nsplit) m.wsplit = h->alloc<uint16_t>(m.nsplit);
             }
             RLGPU_CHECK_HIP(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
@@ -641,7 +648,7 @@ extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision,
         } else {
             forward_half(h, model, d_in, n, s);
             int64_t e = (int64_t)n * h->M[model].out;
-            hipLaunchKernelGGL(ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->logits_h, d_out, e);
+            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->logits_h, d_out, e);
             RLGPU_CHECK_HIP(hipGetLastError());
         }
     });
@@ -658,7 +665,7 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
             forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s);
-            hipLaunchKernelGGL(ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
+            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
                                rng_step, d_actions + b, d_logp ? d_logp + b : nullptr);
             RLGPU_CHECK_HIP(hipGetLastError());
@@ -687,7 +694,7 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
             int m = (int)std::min<int64_t>(R, n - b);
             for (int old = 0; old < 2; old++) {  // current policy rows, then the old version's rows
                 forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s, old ? h->half_ver : h->half);
-                hipLaunchKernelGGL(ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
+                RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                    d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
                                    rng_step, d_actions + b, (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
                 RLGPU_CHECK_HIP(hipGetLastError());
@@ -704,7 +711,7 @@ extern "C" int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t 
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
             forward_half(h, 1, d_obs + b * h->cfg.obs_size, m, s);
-            hipLaunchKernelGGL(ppo::bf16_to_f32, dim3(ceil_div(m, 256)), dim3(256), 0, s, h->logits_h, d_values + b,
+            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(m, 256)), dim3(256), 0, s, h->logits_h, d_values + b,
                                (int64_t)m);
             RLGPU_CHECK_HIP(hipGetLastError());
         }

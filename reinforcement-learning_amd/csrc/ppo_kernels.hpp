@@ -47,6 +47,7 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 // InferActions: logits bf16 [n, A] -> action (int32), log prob.  Inverse-CDF multinomial on the
 // clamped probs (torch.multinomial normalises by their sum); argmax when deterministic.
 // row_sel (optional): only rows with (row_sel[row] != 0) == sel are written (mixed-policy inference).
+template <bool F16>
 __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
                                                      int deterministic, uint64_t seed, uint64_t step, int32_t* act,
                                                      float* logp, const uint8_t* row_sel = nullptr, int sel = 0) {
@@ -57,8 +58,8 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
     const uint16_t* lg = logits + (int64_t)row * A;
     const uint8_t* mk = masks + (int64_t)row * A;
     bool in0 = a0 < A, in1 = a1 < A;
-    float z0 = in0 ? bf2f(lg[a0]) + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
-    float z1 = in1 ? bf2f(lg[a1]) + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
+    float z0 = in0 ? mlp::h2f<F16>(lg[a0]) + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
+    float z1 = in1 ? mlp::h2f<F16>(lg[a1]) + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
     // softmax over all A columns (masked ones carry -1e10, exactly as the reference)
     float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
     float e0 = in0 ? __expf(z0 - m) : 0.f, e1 = in1 ? __expf(z1 - m) : 0.f;
@@ -249,14 +250,16 @@ __global__ void adamw(float* p, float* g, float* m, float* v, int64_t n, const f
     g[e] = 0.f;
 }
 
+template <bool F16>
 __global__ void to_half(const float* p, uint16_t* h, int64_t n) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) h[e] = mlp::f2bf(p[e]);
+    if (e < n) h[e] = mlp::f2h<F16>(p[e]);
 }
 
+template <bool F16>
 __global__ void bf16_to_f32(const uint16_t* h, float* f, int64_t n) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) f[e] = bf2f(h[e]);
+    if (e < n) f[e] = mlp::h2f<F16>(h[e]);
 }
 
 // torch-default Linear init U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (kaiming_uniform a=sqrt(5) for

@@ -224,6 +224,7 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     pc.max_rows = (int32_t)std::max<int64_t>(std::min<int64_t>(cfg.mini_batch_size, TP), std::min<int64_t>(P, 65536));
     pc.seed = cfg.seed;
     pc.train_gemm = cfg.train_gemm;
+    pc.infer_fp16 = cfg.infer_fp16;
     ppo_ = new PPOLearnerGPU(pc, s_);
     if (hasColl_) {  // identical initial weights on every rank: rank 0's (sum of zeros elsewhere)
         float* params = nullptr;

@@ -113,6 +113,7 @@ class LearnerConfig:
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
         self.train_gemm = 0               # rlgpu_ppo_config.train_gemm: 0 = f32 via bf16x3 split, 1 = f32 MFMA
+        self.infer_fp16 = False           # rlgpu_ppo_config.infer_fp16: fp16 inference copy (C5) instead of bf16
         # checkpoints (LearnerConfig.h:31-38): None = no save / load
         self.checkpoint_folder = None
         self.ts_per_save = 10_000_000     # 0 = every iteration (Learner.cpp:44-45)
@@ -139,7 +140,7 @@ class _CConfig(ctypes.Structure):
                 ("reward_clip_range", ctypes.c_float), ("return_samples", ctypes.c_int32),
                 ("policy_layers", ctypes.c_int32 * MAX_LAYERS), ("n_policy_layers", ctypes.c_int32),
                 ("critic_layers", ctypes.c_int32 * MAX_LAYERS), ("n_critic_layers", ctypes.c_int32),
-                ("deterministic", ctypes.c_int32), ("train_gemm", ctypes.c_int32),
+                ("deterministic", ctypes.c_int32), ("train_gemm", ctypes.c_int32), ("infer_fp16", ctypes.c_int32),
                 ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
                 ("mesh_object_ntris", ctypes.c_void_p)]
@@ -228,7 +229,7 @@ class Learner:
         for i, v in enumerate(cfg.critic_layers):
             c.critic_layers[i] = v
         c.n_policy_layers, c.n_critic_layers = len(cfg.policy_layers), len(cfg.critic_layers)
-        c.deterministic, c.train_gemm = int(cfg.deterministic), cfg.train_gemm
+        c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
         c.rank, c.world = rank, world
         self._coll = None
         coll = None

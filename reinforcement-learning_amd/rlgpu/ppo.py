@@ -31,7 +31,8 @@ class _Cfg(ctypes.Structure):
                 ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
                 ("weight_decay", ctypes.c_float), ("clip_range", ctypes.c_float),
                 ("entropy_scale", ctypes.c_float), ("max_grad_norm", ctypes.c_float),
-                ("max_rows", ctypes.c_int32), ("seed", ctypes.c_uint64), ("train_gemm", ctypes.c_int32)]
+                ("max_rows", ctypes.c_int32), ("seed", ctypes.c_uint64), ("train_gemm", ctypes.c_int32),
+                ("infer_fp16", ctypes.c_int32)]
 
 GEMM_F32X6, GEMM_F32 = 0, 1  # rlgpu_ppo_config.train_gemm (include/rlgpu_ppo.h)
 
@@ -84,7 +85,8 @@ class PPO:
     def __init__(self, obs_size=167, num_actions=90, policy_layers=(512, 512), critic_layers=(512, 512),
                  layer_norm=True, policy_lr=2.5e-4, critic_lr=2.5e-4, clip_range=0.2, entropy_scale=0.035,
                  max_grad_norm=0.5, max_rows=50_000, seed=42, init=True, device="cuda:0",
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, leaky_slope=0.01, train_gemm=GEMM_F32X6):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, leaky_slope=0.01, train_gemm=GEMM_F32X6,
+                 infer_fp16=False):
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("PPO needs an MI355X: the product path has no CPU fallback")
@@ -105,6 +107,7 @@ class PPO:
         c.clip_range, c.entropy_scale, c.max_grad_norm = clip_range, entropy_scale, max_grad_norm
         c.max_rows, c.seed = max_rows, seed
         c.train_gemm = train_gemm
+        c.infer_fp16 = int(infer_fp16)
         h = ctypes.c_void_p()
         _lib.check(L.rlgpu_ppo_create(ctypes.byref(c), ctypes.byref(h)), "rlgpu_ppo_create")
         self._h = h

@@ -196,3 +196,19 @@ def test_sample_indices_and_welford_state(gpu):
     w = WelfordStat()
     w.add(L.ret.view(-1).cpu().numpy()[idx])
     assert (w.n, w.mean, w.m2) == (L.return_stat.n, L.return_stat.mean, L.return_stat.m2)
+
+
+def test_c5_learner_iteration_fp16(gpu):
+    """BASELINE config C5 (actor / critic [2048] x 4, fp16 inference) through the C++ Learner at a small
+    arena count: one iteration collects with the fp16 policy, learns, and moves every model."""
+    import torch
+    L = _learner(gpu, policy_layers=(2048,) * 4, critic_layers=(2048,) * 4, infer_fp16=True,
+                 train_against_old_versions=False)
+    before = L.ppo.flat().clone()
+    L.iterate()
+    after = L.ppo.flat()
+    assert torch.isfinite(after).all() and not torch.equal(before, after)
+    # rows 1..T-1 still pair each step's masks with its actions (row 0 now holds the next rollout's start)
+    acts = L.actions[1:].cpu().numpy()
+    masks = L.masks[1:L.T].cpu().numpy()
+    assert (np.take_along_axis(masks, acts[..., None].astype(np.int64), axis=2) == 1).all()

@@ -278,3 +278,51 @@ def test_gemm_modes_fp32_class_accuracy(gpu, la, lb, I, J, K, splits):
         got = C.sum(0).double().cpu()
         err = (got - ref).abs().max().item() / scale
         assert err <= 4 * terr + 1e-7, f"mode {mode}: rel err {err:.2e} vs torch fp32 {terr:.2e}"
+
+
+# ------------------------------------------------------------------ BASELINE config C5 (4 x 2048, fp16 inference)
+def test_param_count_c5():
+    """actor + critic [2048] x 4 = 26.1 M parameters."""
+    a = param_count(167, 90, [2048] * 4)
+    c = param_count(167, 1, [2048] * 4, out=1)
+    assert (a, c, a + c) == (13_133_914, 12_951_553, 26_085_467)
+
+
+@pytest.mark.gpu
+def test_c5_forward_fp32_and_fp16_inference(gpu):
+    """C5 shapes: fp32 training forward vs torch fp32 (rtol 1e-4), fp16 inference copy (v_mfma_f32_32x32x16_f16)
+    within 1e-2 of the output scale of fp32, and closer than the bf16 copy of the same weights."""
+    import torch
+    from rlgpu.ppo import PPO
+    x = torch.randn(300, 167)
+    p16 = PPO(policy_layers=(2048,) * 4, critic_layers=(2048,) * 4, max_rows=512, seed=5, infer_fp16=True)
+    pbf = PPO(policy_layers=(2048,) * 4, critic_layers=(2048,) * 4, max_rows=512, seed=5)
+    assert torch.equal(p16.params, pbf.params)
+    for m in (0, 1):
+        want = p16.torch_module(m)(x).detach()
+        got = p16.forward(m, x.to(gpu)).cpu()
+        np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+        scale = want.abs().max().item()
+        e16 = (p16.forward(m, x.to(gpu), half=True).cpu() - want).abs().max().item() / scale
+        ebf = (pbf.forward(m, x.to(gpu), half=True).cpu() - want).abs().max().item() / scale
+        assert e16 < 1e-2 and e16 < ebf, (m, e16, ebf)
+
+
+@pytest.mark.gpu
+def test_c5_minibatch_grads_match_torch(gpu):
+    """The full PPO minibatch at C5 shapes (kink-free slope 1.0) against the torch fp32 restatement."""
+    import torch
+    from rlgpu.ppo import PPO
+    rng = np.random.default_rng(55)
+    n = 256
+    p = PPO(policy_layers=(2048,) * 4, critic_layers=(2048,) * 4, max_rows=512, seed=9, leaky_slope=1.0)
+    pol, crit = torch_models(p)
+    obs, masks, acts, old, adv, tgt = make_batch(rng, n)
+    T = lambda a: torch.from_numpy(a)  # noqa: E731
+    advn = (adv - adv.mean()) / (adv.std(ddof=1) + 1e-8)
+    ref_minibatch(pol, crit, T(obs), T(masks), T(acts), T(old), T(advn.astype(np.float32)), T(tgt), n)
+    d = {k: T(v).to(gpu) for k, v in dict(obs=obs, masks=masks, acts=acts, old=old, adv=adv, tgt=tgt).items()}
+    p.adv_normalizer(d["adv"])
+    p.zero_grad()
+    p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], None, 0, n, n)
+    assert_grads_close(p.flat(grads=True).cpu(), pol, crit, rel_tol=1e-4, frac=1.0)
