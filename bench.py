@@ -68,9 +68,18 @@ def cpu_baseline(seconds=12.0, arenas=256):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": arenas * steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"env only: {arenas} arenas x {steps} env steps of the oracle/ CPU restatement "
-                      f"({cores} threads, uniform valid actions); no policy / PPO on CPU"}
+    out = {"value": arenas * steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+           "sample": f"env only: {arenas} arenas x {steps} env steps of the oracle/ CPU restatement "
+                     f"({cores} threads, uniform valid actions)"}
+    # BASELINE config C1 on CPU (PPO wall-clock per 1M agent-steps with the C1 model):
+    # 64 arenas, actor / critic [256, 256], oracle env + torch CPU fp32 MLP / PPO, bounded sample
+    from oracle.ppo_cpu import run_c1
+    c1 = run_c1(seconds=10.0, threads=cores)
+    out["c1_ppo"] = {"ppo_s_per_1M_agent_steps": c1["ppo_s_per_1M_agent_steps"],
+                     "env_steps_per_s": c1["env_steps_per_s"], "cores": cores,
+                     "sample": f"C1: 64 arenas, [256,256] actor/critic, T=64, {c1['iterations']} PPO iterations "
+                               f"({c1['agent_steps']} agent-steps) of oracle env + torch CPU fp32 PPO"}
+    return out
 
 
 def main():

@@ -168,3 +168,11 @@ def test_gpu_rollout_bit_exact(gpu, T, N):
     np.testing.assert_array_equal(adv.cpu().numpy(), ea)
     np.testing.assert_array_equal(tgt.cpu().numpy(), et)
     np.testing.assert_array_equal(ret.cpu().numpy(), er)
+
+
+def test_c1_cpu_loop_runs():
+    """oracle/ppo_cpu.py (the timed C1 CPU baseline leg of bench.py) completes an iteration."""
+    from oracle.ppo_cpu import run_c1
+    r = run_c1(seconds=0.01, arenas=4, rollout=4, threads=2)
+    assert r["iterations"] >= 1 and r["agent_steps"] == 4 * 4 * 4 * r["iterations"]
+    assert r["ppo_s_per_1M_agent_steps"] > 0
