@@ -65,6 +65,9 @@ typedef struct {
     int32_t deterministic;         /* LearnerConfig::deterministic */
     int32_t train_gemm;            /* rlgpu_ppo_config.train_gemm */
     int32_t infer_fp16;            /* rlgpu_ppo_config.infer_fp16 (C5: fp16 inference) */
+    int32_t frame_stack;           /* K >= 2: the policy / critic see the last K AdvancedObs frames
+                                      concatenated (BASELINE config C4; a build extension -- the
+                                      reference has no frame stacking); 0 / 1 = off */
     /* sharding */
     int32_t rank, world;
     /* arena meshes (rlgpu_envset_config.mesh_*; NULL = built-in synthetic arena) */
@@ -87,21 +90,23 @@ typedef struct {
     int (*allgather_f32)(void* user, const float* h_in, int64_t n, float* h_out); /* host, out [world * n] */
 } rlgpu_collective;
 
-/* Device views of the rollout (ExperienceBuffer) in HBM, [T, P] time-major, P = 4 * num_arenas. */
+/* Device views of the rollout (ExperienceBuffer) in HBM, [T, P] time-major, P = 4 * num_arenas.
+ * W = obs_width = RLGPU_OBS * max(1, frame_stack). */
 typedef struct {
-    float* obs;          /* [T + 1][P][RLGPU_OBS] */
+    float* obs;          /* [T + 1][P][W] */
     uint8_t* masks;      /* [T + 1][P][RLGPU_ACTIONS] */
     int32_t* actions;    /* [T][P] */
     float* logp;         /* [T][P] */
     float* rewards;      /* [T][P] */
     int8_t* terms;       /* [T][P] trajectory codes 0 / 1 NORMAL / 2 TRUNCATED */
-    float* trunc_obs;    /* [T][P][RLGPU_OBS] */
+    float* trunc_obs;    /* [T][P][W] */
     float* values;       /* [T + 1][P] */
     float* trunc_vals;   /* [T][P] (rows with code 2) */
     float* adv;          /* [T][P] */
     float* target;       /* [T][P] */
     float* ret;          /* [T][P] */
     int32_t T, P;
+    int32_t obs_width;   /* W */
 } rlgpu_rollout_view;
 
 /* Host-side statistics (checkpoint RUNNING_STATS.json, Learner.cpp:224-279). */

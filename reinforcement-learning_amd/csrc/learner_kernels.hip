@@ -84,6 +84,35 @@ __global__ void k_moments_final(const double* part, int nb, int64_t n, double* o
     out[2] = (double)n;
 }
 
+__global__ void k_stack_frames(const float* cur, const float* trunc, const int8_t* codes, float* hist, int K, int P,
+                               int obs, float* out, float* out_trunc) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)P * obs) return;
+    const int p = (int)(e / obs), c = (int)(e % obs);
+    const float x = cur[e];
+    const int code = codes ? codes[p] : 1;
+    const int64_t W = (int64_t)K * obs, plane = (int64_t)P * obs;
+    float* o = out + p * W + c;
+    if (code == 2 && out_trunc && trunc) {  // the ended trajectory's last stacked row
+        float* ot = out_trunc + p * W + c;
+        ot[0] = trunc[e];
+        for (int k = 1; k < K; k++) ot[(int64_t)k * obs] = hist[(int64_t)(k - 1) * plane + e];
+    }
+    if (code != 0) {
+        for (int k = 0; k < K; k++) o[(int64_t)k * obs] = x;
+        for (int k = 0; k < K - 1; k++) hist[(int64_t)k * plane + e] = x;
+        return;
+    }
+    float prev = x;
+    o[0] = x;
+    for (int k = 0; k < K - 1; k++) {  // read the old frame before overwriting it with the newer one
+        const float h = hist[(int64_t)k * plane + e];
+        o[(int64_t)(k + 1) * obs] = h;
+        hist[(int64_t)k * plane + e] = prev;
+        prev = h;
+    }
+}
+
 struct IsTrunc {
     const int8_t* t;
     __device__ bool operator()(const int32_t& i) const { return t[i] == 2; }
@@ -125,6 +154,14 @@ size_t moments_scratch_bytes() { return 2 * kMomBlocks * sizeof(double); }
 void moments_f64(const float* x, const int32_t* idx, int64_t n, double* scratch, double* out3, hipStream_t s) {
     hipLaunchKernelGGL(k_moments_partial, dim3(kMomBlocks), dim3(256), 0, s, x, idx, n, scratch);
     hipLaunchKernelGGL(k_moments_final, dim3(1), dim3(64), 0, s, scratch, kMomBlocks, n, out3);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+void stack_frames(const float* cur, const float* trunc, const int8_t* codes, float* hist, int K, int P, int obs,
+                  float* out, float* out_trunc, hipStream_t s) {
+    const int64_t n = (int64_t)P * obs;
+    hipLaunchKernelGGL(k_stack_frames, dim3(ceil_div(n, 256)), dim3(256), 0, s, cur, trunc, codes, hist, K, P, obs, out,
+                       out_trunc);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 

@@ -23,4 +23,10 @@ void moments_f64(const float* x, const int32_t* idx, int64_t n, double* scratch,
 size_t select_trunc_scratch_bytes(int64_t n);
 void select_trunc(const int8_t* terms, int64_t n, void* scratch, size_t scratch_bytes, int32_t* rows, int32_t* count,
                   hipStream_t s);
+// Frame stacking (BASELINE config C4): out[p] = [cur, h0, .., h(K-2)] (OBS floats each), then the
+// history shifts (h0 <- cur); a trajectory that ended this step (codes[p] != 0) restarts its stack
+// with the current frame repeated, and its pre-reset row out_trunc[p] = [trunc, h0, .., h(K-2)].
+// hist [K-1][P][OBS].  codes == null: initialise (every stack = the current frame repeated).
+void stack_frames(const float* cur, const float* trunc, const int8_t* codes, float* hist, int K, int P, int obs,
+                  float* out, float* out_trunc, hipStream_t s);
 }  // namespace lk

@@ -99,9 +99,10 @@ std::vector<std::pair<int64_t, int64_t>> BatchRanges(int64_t expSize, int64_t ba
     return out;
 }
 
-void ExperienceBuffer::Allocate(int T_, int P_) {
+void ExperienceBuffer::Allocate(int T_, int P_, int W_) {
     T = T_;
     P = P_;
+    W = W_;
     auto A = [&](size_t bytes) {
         void* p = nullptr;
         hipCheck(hipMalloc(&p, bytes + 16), "ExperienceBuffer alloc");
@@ -110,13 +111,13 @@ void ExperienceBuffer::Allocate(int T_, int P_) {
         return p;
     };
     const size_t TP = (size_t)T * P, T1P = (size_t)(T + 1) * P;
-    v.obs = (float*)A(T1P * OBS * 4);
+    v.obs = (float*)A(T1P * W * 4);
     v.masks = (uint8_t*)A(T1P * ACT);
     v.actions = (int32_t*)A(TP * 4);
     v.logp = (float*)A(TP * 4);
     v.rewards = (float*)A(TP * 4);
     v.terms = (int8_t*)A(TP);
-    v.trunc_obs = (float*)A(TP * OBS * 4);
+    v.trunc_obs = (float*)A(TP * W * 4);
     v.values = (float*)A(T1P * 4);
     v.trunc_vals = (float*)A(TP * 4);
     v.adv = (float*)A(TP * 4);
@@ -124,6 +125,7 @@ void ExperienceBuffer::Allocate(int T_, int P_) {
     v.ret = (float*)A(TP * 4);
     v.T = T;
     v.P = P;
+    v.obs_width = W;
 }
 void ExperienceBuffer::Free() {
     for (void* p : allocs) (void)hipFree(p);
@@ -202,8 +204,11 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     ec.mesh_objects = cfg.mesh_objects;
     ec.mesh_object_ntris = cfg.mesh_object_ntris;
     env_ = new RLGC::EnvSetGPU(ec, s_);
+    K_ = cfg.frame_stack > 1 ? cfg.frame_stack : 1;
+    RLGPU_REQUIRE(K_ <= 16, "Learner: frame_stack must be <= 16");
+    const int W = OBS * K_;
     rlgpu_ppo_config pc{};
-    pc.obs_size = OBS;
+    pc.obs_size = W;
     pc.num_actions = ACT;
     std::memcpy(pc.policy_layers, cfg.policy_layers, sizeof(pc.policy_layers));
     pc.n_policy_layers = cfg.n_policy_layers;
@@ -237,10 +242,15 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
             throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: parameter broadcast failed");
         RlgpuCheck(rlgpu_ppo_refresh_half(ppo_->handle(), s_), "refresh half");
     }
-    exp_.Allocate(T, P);
-    // rollout row 0 = the env's initial obs / masks
+    exp_.Allocate(T, P, W);
+    // rollout row 0 = the env's initial obs (stacked: the first frame repeated) / masks
     const rlgpu_envset_buffers& st = env_->state();
-    hipCheck(hipMemcpyAsync(exp_.v.obs, st.obs, (size_t)P * OBS * 4, hipMemcpyDeviceToDevice, s_), "obs0");
+    if (K_ > 1) {
+        hist_ = Alloc<float>((size_t)(K_ - 1) * P * OBS);
+        lk::stack_frames(st.obs, nullptr, nullptr, hist_, K_, P, OBS, exp_.v.obs, nullptr, s_);
+    } else {
+        hipCheck(hipMemcpyAsync(exp_.v.obs, st.obs, (size_t)P * OBS * 4, hipMemcpyDeviceToDevice, s_), "obs0");
+    }
     hipCheck(hipMemcpyAsync(exp_.v.masks, st.action_masks, (size_t)P * ACT, hipMemcpyDeviceToDevice, s_), "masks0");
     // self-play team masks (team of player p is p % 2)
     std::vector<uint8_t> team(P);
@@ -283,16 +293,23 @@ void Learner::Collect() {
         ev_.assign(2 * T, nullptr);
         for (auto& e : ev_) hipCheck(hipEventCreate(&e), "event");
     }
+    const int W = exp_.W;
+    const rlgpu_envset_buffers& st = env_->state();
     for (int t = 0; t < T; t++) {
         const size_t r = (size_t)t * P;
-        ppo_->InferActions(v.obs + r * OBS, v.masks + r * ACT, P, cfg_.deterministic != 0, (uint64_t)stats.rng_step,
+        ppo_->InferActions(v.obs + r * W, v.masks + r * ACT, P, cfg_.deterministic != 0, (uint64_t)stats.rng_step,
                            v.actions + r, v.logp + r, old);
         stats.rng_step++;
-        rlgpu_step_outputs o{v.obs + (r + P) * OBS, v.masks + (r + P) * ACT, v.rewards + r, v.terms + r,
-                             v.trunc_obs + r * OBS};
+        // the fused step appends straight into the rollout; stacked obs are assembled from the env's
+        // own obs / pre-reset rows after it
+        rlgpu_step_outputs o{K_ > 1 ? nullptr : v.obs + (r + P) * OBS, v.masks + (r + P) * ACT, v.rewards + r,
+                             v.terms + r, K_ > 1 ? nullptr : v.trunc_obs + r * OBS};
         if (envTiming_) hipCheck(hipEventRecord(ev_[2 * t], s_), "event");
         env_->Step(v.actions + r, &o);
         if (envTiming_) hipCheck(hipEventRecord(ev_[2 * t + 1], s_), "event");
+        if (K_ > 1)
+            lk::stack_frames(st.obs, st.trunc_obs, v.terms + r, hist_, K_, P, OBS, v.obs + (r + P) * W, v.trunc_obs + r * W,
+                             s_);
     }
 }
 
@@ -311,10 +328,10 @@ void Learner::Consume() {
             if (truncObsC_) (void)hipFree(truncObsC_);
             if (truncValC_) (void)hipFree(truncValC_);
             truncCap_ = std::max<int64_t>(ntr, 2 * truncCap_);
-            hipCheck(hipMalloc((void**)&truncObsC_, (size_t)truncCap_ * OBS * 4), "trunc obs");
+            hipCheck(hipMalloc((void**)&truncObsC_, (size_t)truncCap_ * exp_.W * 4), "trunc obs");
             hipCheck(hipMalloc((void**)&truncValC_, (size_t)truncCap_ * 4), "trunc vals");
         }
-        lk::gather_rows(v.trunc_obs, OBS, truncRows_, ntr, truncObsC_, s_);
+        lk::gather_rows(v.trunc_obs, exp_.W, truncRows_, ntr, truncObsC_, s_);
         ppo_->InferCritic(truncObsC_, ntr, truncValC_);
         lk::scatter_f32(truncValC_, truncRows_, ntr, v.trunc_vals, s_);
     }
@@ -413,7 +430,8 @@ void Learner::Learn() {
 void Learner::FinishIteration() {
     const int T = exp_.T, P = exp_.P;
     const rlgpu_rollout_view& v = exp_.v;
-    hipCheck(hipMemcpyAsync(v.obs, v.obs + (size_t)T * P * OBS, (size_t)P * OBS * 4, hipMemcpyDeviceToDevice, s_), "obs");
+    const size_t W = (size_t)exp_.W;
+    hipCheck(hipMemcpyAsync(v.obs, v.obs + (size_t)T * P * W, (size_t)P * W * 4, hipMemcpyDeviceToDevice, s_), "obs");
     hipCheck(hipMemcpyAsync(v.masks, v.masks + (size_t)T * P * ACT, (size_t)P * ACT, hipMemcpyDeviceToDevice, s_), "masks");
     stats.iteration++;
     const int64_t realPlayers = oldTeam_ < 0 ? P : P / 2;  // numRealPlayers (Learner.cpp:629)

@@ -80,10 +80,10 @@ std::vector<std::pair<int64_t, int64_t>> BatchRanges(int64_t expSize, int64_t ba
 // The rollout ([T, P] time-major) in HBM; every collected step is trained in the iteration that
 // collected it (the unfinished tail bootstrapped from V(obs_T), DESIGN.md Deviations 5).
 struct ExperienceBuffer {
-    int T = 0, P = 0;
+    int T = 0, P = 0, W = 0;  // W: obs row width (RLGPU_OBS x frames)
     rlgpu_rollout_view v{};
     std::vector<void*> allocs;
-    void Allocate(int T, int P);
+    void Allocate(int T, int P, int W);
     void Free();
 };
 
@@ -157,6 +157,8 @@ private:
     ExperienceBuffer exp_;
     int oldTeam_ = -1;
     bool envTiming_ = false;
+    int K_ = 1;                 // frames stacked (config C4)
+    float* hist_ = nullptr;     // [K-1][P][OBS] frame history
     std::vector<hipEvent_t> ev_;
     // device scratch
     uint8_t* oldRows_[2] = {nullptr, nullptr};

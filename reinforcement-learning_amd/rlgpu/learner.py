@@ -114,6 +114,7 @@ class LearnerConfig:
         self.deterministic = False
         self.train_gemm = 0               # rlgpu_ppo_config.train_gemm: 0 = f32 via bf16x3 split, 1 = f32 MFMA
         self.infer_fp16 = False           # rlgpu_ppo_config.infer_fp16: fp16 inference copy (C5) instead of bf16
+        self.frame_stack = 1              # K >= 2: stacked AdvancedObs frames (C4; no reference counterpart)
         # checkpoints (LearnerConfig.h:31-38): None = no save / load
         self.checkpoint_folder = None
         self.ts_per_save = 10_000_000     # 0 = every iteration (Learner.cpp:44-45)
@@ -141,7 +142,7 @@ class _CConfig(ctypes.Structure):
                 ("policy_layers", ctypes.c_int32 * MAX_LAYERS), ("n_policy_layers", ctypes.c_int32),
                 ("critic_layers", ctypes.c_int32 * MAX_LAYERS), ("n_critic_layers", ctypes.c_int32),
                 ("deterministic", ctypes.c_int32), ("train_gemm", ctypes.c_int32), ("infer_fp16", ctypes.c_int32),
-                ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("frame_stack", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
                 ("mesh_object_ntris", ctypes.c_void_p)]
 
@@ -149,7 +150,7 @@ class _CConfig(ctypes.Structure):
 class _CRollout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("obs", "masks", "actions", "logp", "rewards", "terms", "trunc_obs",
                                                "values", "trunc_vals", "adv", "target", "ret")] + \
-               [("T", ctypes.c_int32), ("P", ctypes.c_int32)]
+               [("T", ctypes.c_int32), ("P", ctypes.c_int32), ("obs_width", ctypes.c_int32)]
 
 
 class _CStats(ctypes.Structure):
@@ -230,6 +231,7 @@ class Learner:
             c.critic_layers[i] = v
         c.n_policy_layers, c.n_critic_layers = len(cfg.policy_layers), len(cfg.critic_layers)
         c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
+        c.frame_stack = cfg.frame_stack
         c.rank, c.world = rank, world
         self._coll = None
         coll = None
@@ -246,20 +248,20 @@ class Learner:
         self.env = EnvSet.wrap(eh.value, self.device, cfg.tick_skip, cfg.action_delay, owner=self)
         max_rows = max(min(cfg.mini_batch_size, cfg.rollout_len * 4 * cfg.num_arenas), min(4 * cfg.num_arenas, 65536))
         self.ppo = PPO.wrap(ph.value, self.device, cfg.policy_layers, cfg.critic_layers, max_rows,
-                            metrics_source=self._metrics, owner=self)
+                            obs_size=OBS * max(1, cfg.frame_stack), metrics_source=self._metrics, owner=self)
         r = _CRollout()
         _lib.check(L.rlgpu_learner_rollout(h, ctypes.byref(r)), "rlgpu_learner_rollout")
-        T, P = r.T, r.P
-        self.T, self.P = T, P
+        T, P, W = r.T, r.P, r.obs_width
+        self.T, self.P, self.W = T, P, W
         a, f32, u8, i32, i8 = _lib.alias, torch.float32, torch.uint8, torch.int32, torch.int8
         d = self.device
-        self.obs = a(r.obs, (T + 1, P, OBS), f32, d)
+        self.obs = a(r.obs, (T + 1, P, W), f32, d)
         self.masks = a(r.masks, (T + 1, P, ACTIONS), u8, d)
         self.actions = a(r.actions, (T, P), i32, d)
         self.logp = a(r.logp, (T, P), f32, d)
         self.rewards = a(r.rewards, (T, P), f32, d)
         self.terms = a(r.terms, (T, P), i8, d)
-        self.trunc_obs = a(r.trunc_obs, (T, P, OBS), f32, d)
+        self.trunc_obs = a(r.trunc_obs, (T, P, W), f32, d)
         self.values = a(r.values, (T + 1, P), f32, d)
         self.trunc_vals = a(r.trunc_vals, (T, P), f32, d)
         self.adv = a(r.adv, (T, P), f32, d)

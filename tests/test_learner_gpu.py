@@ -212,3 +212,40 @@ def test_c5_learner_iteration_fp16(gpu):
     acts = L.actions[1:].cpu().numpy()
     masks = L.masks[1:L.T].cpu().numpy()
     assert (np.take_along_axis(masks, acts[..., None].astype(np.int64), axis=2) == 1).all()
+
+
+def test_c4_frame_stack_rollout(gpu):
+    """BASELINE config C4 (stacked AdvancedObs frames, K = 4; a build extension -- the reference has no
+    frame stacking): frame 0 of every stacked row is the env's obs (bit-exact vs the oracle env fed
+    the same actions); frames 1..3 are the previous row's frames 0..2 unless the trajectory ended,
+    which restarts the stack with the new frame repeated; truncated rows keep [pre-reset obs,
+    history]; one learn iteration on 668-wide obs runs."""
+    import torch
+    K = 4
+    L = _learner(gpu, frame_stack=K, max_episode_duration=1.2, train_against_old_versions=False)
+    assert L.W == 167 * K and L.obs.shape[-1] == 167 * K
+    o = oracle.EnvSet(L.cfg.num_arenas, seed=L.cfg.seed * 1000003, max_episode_steps=18)
+    obs0 = L.obs[0].cpu().numpy()
+    for k in range(K):
+        np.testing.assert_array_equal(obs0[:, 167 * k:167 * (k + 1)].view(np.uint32), o.obs.view(np.uint32))
+    L.collect()
+    torch.cuda.synchronize()
+    obs, terms, trunc, acts = L.obs.cpu().numpy(), L.terms.cpu().numpy(), L.trunc_obs.cpu().numpy(), L.actions.cpu().numpy()
+    F = lambda x, k: x[..., 167 * k:167 * (k + 1)]  # noqa: E731
+    for t in range(L.T):
+        o.step(acts[t], True)
+        np.testing.assert_array_equal(F(obs[t + 1], 0).view(np.uint32), o.obs.view(np.uint32), err_msg=f"t={t}")
+        cont = terms[t] == 0
+        for k in range(1, K):
+            np.testing.assert_array_equal(F(obs[t + 1], k)[cont], F(obs[t], k - 1)[cont])
+            np.testing.assert_array_equal(F(obs[t + 1], k)[~cont], F(obs[t + 1], 0)[~cont])
+        tr = terms[t] == 2
+        if tr.any():
+            np.testing.assert_array_equal(F(trunc[t], 0)[tr], o.trunc_obs[tr])
+            for k in range(1, K):
+                np.testing.assert_array_equal(F(trunc[t], k)[tr], F(obs[t], k - 1)[tr])
+    assert (terms == 2).any() and (terms == 0).any()
+    L.consume()
+    L.learn()
+    torch.cuda.synchronize()
+    assert torch.isfinite(L.ppo.flat()).all()
