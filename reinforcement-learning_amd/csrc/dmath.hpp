@@ -141,13 +141,29 @@ HD quat quat_from_mat(const m3& m) {
         t[2] = (m.r1.x - m.r0.y) * s;
     } else {
         int i = m.r0.x < m.r1.y ? (m.r1.y < m.r2.z ? 2 : 1) : (m.r0.x < m.r2.z ? 2 : 0);
-        int j = (i + 1) % 3, k = (i + 2) % 3;
-        float s = sqrtf(mel(m, i, i) - mel(m, j, j) - mel(m, k, k) + 1.0f);
-        t[i] = s * 0.5f;
-        s = 0.5f / s;
-        t[3] = (mel(m, k, j) - mel(m, j, k)) * s;
-        t[j] = (mel(m, j, i) + mel(m, i, j)) * s;
-        t[k] = (mel(m, k, i) + mel(m, i, k)) * s;
+        // written out per i (j = i+1, k = i+2 mod 3): a runtime index would put m and t in scratch
+        if (i == 0) {
+            float s = sqrtf(m.r0.x - m.r1.y - m.r2.z + 1.0f);
+            t[0] = s * 0.5f;
+            s = 0.5f / s;
+            t[3] = (m.r2.y - m.r1.z) * s;
+            t[1] = (m.r1.x + m.r0.y) * s;
+            t[2] = (m.r2.x + m.r0.z) * s;
+        } else if (i == 1) {
+            float s = sqrtf(m.r1.y - m.r2.z - m.r0.x + 1.0f);
+            t[1] = s * 0.5f;
+            s = 0.5f / s;
+            t[3] = (m.r0.z - m.r2.x) * s;
+            t[2] = (m.r2.y + m.r1.z) * s;
+            t[0] = (m.r0.y + m.r1.x) * s;
+        } else {
+            float s = sqrtf(m.r2.z - m.r0.x - m.r1.y + 1.0f);
+            t[2] = s * 0.5f;
+            s = 0.5f / s;
+            t[3] = (m.r1.x - m.r0.y) * s;
+            t[0] = (m.r0.z + m.r2.x) * s;
+            t[1] = (m.r1.z + m.r2.y) * s;
+        }
     }
     return quat{t[0], t[1], t[2], t[3]};
 }

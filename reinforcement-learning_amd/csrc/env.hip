@@ -427,12 +427,11 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
         }
         sync(); P.mark(12);
         if (valid && l < 4) {
-            PView P[4];
-            for (int i = 0; i < 4; i++) P[i] = view_player(A, i);
+            const PView me = view_player(A, l);  // the other players' views are read where used
             v3 bp = ld3(A->s.ball.pos) * kBT2UU, bv = ld3(A->s.ball.vel) * kBT2UU, pbv = ld3(A->s.env.prev_ball_vel);
             float all = 0.f;
             for (int r = 0; r < RLGPU_REWARDS; r++) {
-                float o = reward_value(A, r, l, P, bp, bv, pbv, A->a.goal != 0);
+                float o = reward_value(A, r, l, me, bp, bv, pbv, A->a.goal != 0);
                 all += o * C.reward_w[r];
                 if (l == 0 && g.last_rewards) g.last_rewards[(size_t)arena * RLGPU_REWARDS + r] = o;
             }

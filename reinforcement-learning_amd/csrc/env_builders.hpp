@@ -66,10 +66,11 @@ DEV void add_player_obs(float* o, const PView& pl, bool inv, v3 bp, v3 bv) {
 
 // AdvancedObs::BuildObs + DefaultAction::GetActionMask for player pi, into LDS rows
 DEV void build_obs_row(ArenaLDS* A, int pi) {
-    PView P[4];
-    for (int i = 0; i < 4; i++) P[i] = view_player(A, i);
+    // player views are read from LDS where used: an array of them indexed by the lane's player
+    // would live in private (scratch) memory
+    const PView me = view_player(A, pi);
     float* o = A->u.out.obs[pi];
-    bool inv = P[pi].orange;
+    bool inv = me.orange;
     v3 bp = inv_if(ld3(A->s.ball.pos) * kBT2UU, inv), bv = inv_if(ld3(A->s.ball.vel) * kBT2UU, inv),
        ba = inv_if(ld3(A->s.ball.angvel), inv);
     const float BPOS = 1 / 5000.f, BVEL = 1 / 2300.f, BANG = 1 / 3.f;  // AdvancedObs.h:10-13
@@ -85,34 +86,33 @@ DEV void build_obs_row(ArenaLDS* A, int pi) {
         o[17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
     }
     float* q = o + 51;
-    add_player_obs(q, P[pi], inv, bp, bv);
+    add_player_obs(q, me, inv, bp, bv);
     q += 29;
     for (int j = 0; j < 4; j++)
-        if (j != pi && P[j].orange == P[pi].orange) {
-            add_player_obs(q, P[j], inv, bp, bv);
+        if (j != pi && (j & 1) == (pi & 1)) {  // teammates (orange = j & 1)
+            add_player_obs(q, view_player(A, j), inv, bp, bv);
             q += 29;
         }
     for (int j = 0; j < 4; j++)
-        if (P[j].orange != P[pi].orange) {
-            add_player_obs(q, P[j], inv, bp, bv);
+        if ((j & 1) != (pi & 1)) {  // opponents
+            add_player_obs(q, view_player(A, j), inv, bp, bv);
             q += 29;
         }
     uint8_t* m = A->u.out.masks[pi];
-    bool turtled = P[pi].world_contact && P[pi].wc_z > 0.9f;
+    bool turtled = me.world_contact && me.wc_z > 0.9f;
     for (int k = 0; k < RLGPU_ACTIONS; k++) {
-        uint8_t r = P[pi].on_ground ? C.mask_ground[k] : C.mask_air[k];
-        if (P[pi].boost == 0) r &= (uint8_t)~C.mask_boost[k];
-        if (P[pi].hfj || turtled) r |= C.mask_jump[k];
+        uint8_t r = me.on_ground ? C.mask_ground[k] : C.mask_air[k];
+        if (me.boost == 0) r &= (uint8_t)~C.mask_boost[k];
+        if (me.hfj || turtled) r |= C.mask_jump[k];
         m[k] = r & 1;
     }
 }
 
 // KickoffProximityReward2v2Enhanced (KickoffProximityReward2v2Enhanced.h:14-366)
-DEV float kickoff_reward(int pi, const PView* P, v3 bpos, v3 bvel) {
+DEV float kickoff_reward(ArenaLDS* A, int pi, const PView& pl, v3 bpos, v3 bvel) {
     float bspeed = rs_len(bvel);
     v3 b2 = v3{bpos.x, bpos.y, 0.f};
     if (!(bspeed < 2.f && bpos.z < 150.f && rs_len(b2) < 50.f)) return 0.f;
-    const PView& pl = P[pi];
     bool has_tm = false;
     int tm_i = -1;
     float tm_dist = 0, closest = 3.402823466e+38f, second = 3.402823466e+38f;
@@ -120,7 +120,7 @@ DEV float kickoff_reward(int pi, const PView* P, v3 bpos, v3 bvel) {
     int nopp = 0;
     float tot_speed = 0;
     for (int j = 0; j < 4; j++) {
-        const PView& p = P[j];
+        const PView p = view_player(A, j);
         if (p.orange == pl.orange && j != pi) {
             tm_i = j;
             has_tm = true;
@@ -140,7 +140,7 @@ DEV float kickoff_reward(int pi, const PView* P, v3 bpos, v3 bvel) {
     }
     if (nopp > 0) opp_com = rs_div(opp_com, (float)nopp);
     if (!has_tm) return 0.f;
-    const PView& tm = P[tm_i];
+    const PView tm = view_player(A, tm_i);
     float pdist = rs_len(pl.pos - bpos);
     float dscore = (pdist < tm_dist) ? 0.4f : 0.f;
     v3 p2b = rs_norm(bpos - pl.pos), t2b = rs_norm(bpos - tm.pos);
@@ -247,15 +247,14 @@ DEV float kickoff_reward(int pi, const PView* P, v3 bpos, v3 bvel) {
 }
 
 // one reward of the ExampleMain list for player i (src/ExampleMain.cpp:132-177)
-DEV float reward_value(ArenaLDS* A, int r, int i, const PView* P, v3 bpos, v3 bvel, v3 prev_bvel, bool goal) {
-    const PView& pl = P[i];
+DEV float reward_value(ArenaLDS* A, int r, int i, const PView& pl, v3 bpos, v3 bvel, v3 prev_bvel, bool goal) {
     const rlgpu_env_extra& e = A->s.env;
     const float KPH = 250.f / 9.f;
     bool touched = A->a.touched[i] != 0;
     switch (r) {
         case 0: return !pl.on_ground;
         case 1: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1.f : 0.f;
-        case 2: return kickoff_reward(i, P, bpos, bvel);
+        case 2: return kickoff_reward(A, i, pl, bpos, bvel);
         case 3: {
             v3 dir = rs_norm(bpos - pl.pos);
             v3 nv = rs_div(pl.vel, 2300.f);

@@ -583,14 +583,27 @@ DEV void commit_contacts(ArenaLDS* A, Prof* P = nullptr) {
         n = kMaxCand;
     }
     // insertion sort by commit order (few elements)
+    // (the element being inserted is held field by field: a Cand temporary is a private-memory copy)
     for (int i = 1; i < n; i++) {
-        Cand x = A->u.cand[i];
+        const Cand& ci = A->u.cand[i];
+        const float xn0 = ci.n[0], xn1 = ci.n[1], xn2 = ci.n[2], xp0 = ci.p[0], xp1 = ci.p[1], xp2 = ci.p[2];
+        const float xd = ci.depth;
+        const int xo = ci.order, xk = ci.key;
         int j = i - 1;
-        while (j >= 0 && A->u.cand[j].order > x.order) {
+        while (j >= 0 && A->u.cand[j].order > xo) {
             A->u.cand[j + 1] = A->u.cand[j];
             j--;
         }
-        A->u.cand[j + 1] = x;
+        Cand& d = A->u.cand[j + 1];
+        d.n[0] = xn0;
+        d.n[1] = xn1;
+        d.n[2] = xn2;
+        d.p[0] = xp0;
+        d.p[1] = xp1;
+        d.p[2] = xp2;
+        d.depth = xd;
+        d.order = xo;
+        d.key = xk;
     }
     pmark(P, 17);
     if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[24], (unsigned long long)n);

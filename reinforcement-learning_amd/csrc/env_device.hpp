@@ -394,7 +394,6 @@ DEV void wheel_phase(ArenaLDS* A, const MeshView& M, int ci, int i) {
         v3 cp = W.contact_point;
         v3 rel1 = cp - P;
         v3 gcom = dyn ? bpos(A, g) : zero3();
-        m3 grot = dyn ? brot(A, g) : ident3();
         float g_inv_mass = dyn ? binv_mass(g) : 0.f;
         v3 g_iner = dyn ? binv_iner(g) : zero3();
         v3 rel2 = cp - gcom;
@@ -402,7 +401,10 @@ DEV void wheel_phase(ArenaLDS* A, const MeshView& M, int ci, int i) {
         v3 v2 = dyn ? (A->a.snap_vel[g] + cross(A->a.snap_ang[g], rel2)) : zero3();
         v3 vel = v1 - v2;
         v3 aJ = transpose(R) * cross(rel1, ax);
-        v3 bJ = transpose(grot) * cross(rel2, -ax);
+        // static ground: identity rotation (bJ = cross(rel2, -ax) exactly); no select of a whole
+        // matrix (a select of two 3x3 aggregates is lowered through a private-memory copy)
+        v3 bJ = cross(rel2, -ax);
+        if (dyn) bJ = transpose(brot(A, g)) * bJ;
         v3 m0 = C.car_inv_inertia * aJ;
         v3 m1 = g_iner * bJ;
         float adiag = C.car_inv_mass + dot(m0, aJ) + g_inv_mass + dot(m1, bJ);
