@@ -197,3 +197,14 @@ class EnvSet:
         count = buf.size // ARENA.itemsize
         _lib.check(_lib.lib().rlgpu_envset_set_arenas(self._h, first, count, buf.ctypes.data_as(ctypes.c_void_p)),
                    "set_arenas")
+
+    def serialize_arena(self, index):
+        """RocketSim Arena::Serialize bytes of arena `index` (rlgpu.arena_wire)."""
+        from . import arena_wire
+        return arena_wire.envset_serialize(self, index)
+
+    def deserialize_arena(self, index, data):
+        """Arena::DeserializeNew of `data` into arena `index`; returns the bytes consumed (build_obs()
+        refreshes the arena's obs / mask rows)."""
+        from . import arena_wire
+        return arena_wire.envset_deserialize(self, index, data)
