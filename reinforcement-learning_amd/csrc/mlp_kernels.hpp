@@ -717,8 +717,15 @@ DEV float wave_max(float v) {
 // recomputes xhat = (z - mean) * rstd from the untouched pre-norm input z with the same operations
 // (bit-identical to a stored xhat, one [R,H] write less per layer).
 // Lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (float4 loads / stores when H is a
-// multiple of 4); gamma / beta stay in registers and each wave walks LNF_ROWS/4 rows.
-constexpr int LNF_ROWS = 8;
+// multiple of 4); gamma / beta stay in registers.  Each wave walks LNF_ROWS/4 rows, lnf_rf<MAXH>()
+// of them at a time: their loads are issued together before the first reduction and their wave
+// reductions interleave, so a wave keeps that many rows of HBM traffic in flight (the per-row
+// arithmetic and its order are unchanged).
+constexpr int LNF_ROWS = 16;
+template <int MAXH>
+constexpr int lnf_rf() {
+    return MAXH <= 8 ? 4 : (MAXH <= 16 ? 2 : 1);
+}
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const float* gamma, const float* beta, int R, int H,
                                                      float slope, int use_ln, float* act, float2* stats) {
@@ -732,57 +739,72 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
         g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
         b[q] = (use_ln && c < H) ? beta[c] : 0.f;
     }
-    for (int i = 0; i < LNF_ROWS / 4; i++) {
-        const int row = blockIdx.x * LNF_ROWS + i * 4 + wv;
-        if (row >= R) break;
-        const float* z = Z + (int64_t)row * H + c0;
-        float v[MAXH];
-        if (vec) {
+    constexpr int RF = lnf_rf<MAXH>();
+    for (int i0 = 0; i0 < LNF_ROWS / 4; i0 += RF) {
+        int row[RF];
+        float v[RF][MAXH];
 #pragma unroll
-            for (int q = 0; q < MAXH; q += 4) {
-                float4 t = *reinterpret_cast<const float4*>(z + q);
-                v[q] = t.x; v[q + 1] = t.y; v[q + 2] = t.z; v[q + 3] = t.w;
+        for (int r = 0; r < RF; r++) {  // all RF rows' loads first (a row past R reloads row R-1)
+            row[r] = blockIdx.x * LNF_ROWS + (i0 + r) * 4 + wv;
+            const float* z = Z + (int64_t)min(row[r], R - 1) * H + c0;
+            if (vec) {
+#pragma unroll
+                for (int q = 0; q < MAXH; q += 4) {
+                    float4 t = *reinterpret_cast<const float4*>(z + q);
+                    v[r][q] = t.x; v[r][q + 1] = t.y; v[r][q + 2] = t.z; v[r][q + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < MAXH; q++) v[r][q] = c0 + q < H ? z[q] : 0.f;
             }
-        } else {
-#pragma unroll
-            for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? z[q] : 0.f;
         }
-        float xh[MAXH], a[MAXH];
-        float rs = 1.f, mean = 0.f;
-        if (use_ln) {
-            float s = 0.f;
+        float mean[RF], rs[RF];
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) s += v[q];
-            mean = wave_sum(s) / (float)H;
-            float s2 = 0.f;
+        for (int r = 0; r < RF; r++) {
+            mean[r] = 0.f;
+            rs[r] = 1.f;
+        }
+        if (use_ln) {
+#pragma unroll
+            for (int r = 0; r < RF; r++) {
+                float s = 0.f;
+#pragma unroll
+                for (int q = 0; q < MAXH; q++) s += v[r][q];
+                mean[r] = wave_sum(s) / (float)H;
+            }
+#pragma unroll
+            for (int r = 0; r < RF; r++) {
+                float s2 = 0.f;
+#pragma unroll
+                for (int q = 0; q < MAXH; q++) {
+                    float d = c0 + q < H ? v[r][q] - mean[r] : 0.f;
+                    s2 += d * d;
+                }
+                rs[r] = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RF; r++) {
+            if (row[r] >= R) continue;
+            float a[MAXH];
 #pragma unroll
             for (int q = 0; q < MAXH; q++) {
-                float d = c0 + q < H ? v[q] - mean : 0.f;
-                s2 += d * d;
+                const float xh = use_ln ? (v[r][q] - mean[r]) * rs[r] : v[r][q];
+                const float hv = use_ln ? xh * g[q] + b[q] : xh;
+                a[q] = hv > 0.f ? hv : hv * slope;
             }
-            rs = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
+            float* ao = act + (int64_t)row[r] * H + c0;
+            if (vec) {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) xh[q] = (v[q] - mean) * rs;
-        } else {
+                for (int q = 0; q < MAXH; q += 4)
+                    *reinterpret_cast<float4*>(ao + q) = make_float4(a[q], a[q + 1], a[q + 2], a[q + 3]);
+            } else {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) xh[q] = v[q];
+                for (int q = 0; q < MAXH; q++)
+                    if (c0 + q < H) ao[q] = a[q];
+            }
+            if (lane == 0) stats[row[r]] = make_float2(mean[r], rs[r]);
         }
-#pragma unroll
-        for (int q = 0; q < MAXH; q++) {
-            float hv = use_ln ? xh[q] * g[q] + b[q] : xh[q];
-            a[q] = hv > 0.f ? hv : hv * slope;
-        }
-        float* ao = act + (int64_t)row * H + c0;
-        if (vec) {
-#pragma unroll
-            for (int q = 0; q < MAXH; q += 4)
-                *reinterpret_cast<float4*>(ao + q) = make_float4(a[q], a[q + 1], a[q + 2], a[q + 3]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < MAXH; q++)
-                if (c0 + q < H) ao[q] = a[q];
-        }
-        if (lane == 0) stats[row] = make_float2(mean, rs);
     }
 }
 
