@@ -170,6 +170,15 @@ int rlgpu_moments_mean_std(const double* moments3, float* out2);
 /* The return-sample indices of one iteration: n draws in [0, range) from a counter-based
  * generator keyed by (seed, rank, iteration) -- every language binding reproduces the same draws. */
 int rlgpu_sample_indices(uint64_t seed, int32_t rank, int64_t iteration, int64_t range, int32_t n, int64_t* out);
+/* The return-sample rows of one iteration, drawn only from steps of FINISHED trajectories -- the
+ * reference samples tReturns of combinedTraj, which holds complete trajectories only
+ * (Learner.cpp:823-861, 959-967).  ends[p] = the last step t of column p whose trajectory code is
+ * nonzero (-1: no trajectory of p ends inside the rollout, or p is not sampled); the eligible rows
+ * are (t, p) with t <= ends[p], whose discounted returns run to their trajectory's end.  Draws
+ * min(n, #eligible) rows uniformly with replacement (torch::randint, Learner.cpp:963) from the
+ * rlgpu_sample_indices sequence; writes row indices t * P + p to out and their count to *n_out. */
+int rlgpu_sample_finished_rows(uint64_t seed, int32_t rank, int64_t iteration, const int32_t* ends, int32_t P,
+                               int32_t n, int64_t* out, int32_t* n_out);
 
 #ifdef __cplusplus
 }

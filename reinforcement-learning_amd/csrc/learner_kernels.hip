@@ -41,6 +41,19 @@ __global__ void k_train_rows(int T, int P, int team, int32_t* out) {
     out[i] = t * P + 2 * q + team;  // team of player p is p % 2 (cars 0, 2 blue; 1, 3 orange)
 }
 
+// one lane per player column: the last step t whose trajectory code is nonzero, -1 if none
+__global__ void k_last_ends(const int8_t* terms, int T, int P, int32_t* out) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    int last = -1;
+    for (int t = T - 1; t >= 0; --t)
+        if (terms[(int64_t)t * P + p] != 0) {
+            last = t;
+            break;
+        }
+    out[p] = last;
+}
+
 __global__ void k_gather_samples(const float* src, const int64_t* idx, int n, float* dst) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[i] = src[idx[i]];
@@ -143,6 +156,11 @@ void compose(const int32_t* rows, const int32_t* perm, int64_t n, int32_t* out, 
 void train_rows(int T, int P, int team, int32_t* out, hipStream_t s) {
     int64_t n = (int64_t)T * (P / 2);
     hipLaunchKernelGGL(k_train_rows, dim3(ceil_div(n, 256)), dim3(256), 0, s, T, P, team, out);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void last_ends(const int8_t* terms, int T, int P, int32_t* out, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_last_ends, dim3(ceil_div(P, 256)), dim3(256), 0, s, terms, T, P, out);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 void gather_samples(const float* src, const int64_t* idx, int n, float* dst, hipStream_t s) {

@@ -15,6 +15,8 @@ void gather_rows(const float* src, int C, const int32_t* idx, int64_t n, float* 
 void compose(const int32_t* rows, const int32_t* perm, int64_t n, int32_t* out, hipStream_t s);
 // sample indices t * P + p of the players of `team` (p % 2 == team), [T][P / 2]
 void train_rows(int T, int P, int team, int32_t* out, hipStream_t s);
+// out[p] = the last t with terms[t * P + p] != 0 (the column's last trajectory end), -1 if none
+void last_ends(const int8_t* terms, int T, int P, int32_t* out, hipStream_t s);
 void gather_samples(const float* src, const int64_t* idx, int n, float* dst, hipStream_t s);
 // (sum, sum of squares, n) in fp64 of x[idx[i]] (idx may be null), deterministic
 size_t moments_scratch_bytes();

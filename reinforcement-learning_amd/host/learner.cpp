@@ -7,6 +7,7 @@
 // scalars the host needs (truncation count, 150 return samples, distributed moments).
 #include "learner.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -269,6 +270,8 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     selScratch_ = Alloc<char>(selBytes_);
     sampleIdx_ = Alloc<int64_t>((size_t)std::max(1, cfg.return_samples));
     samples_ = Alloc<float>((size_t)std::max(1, cfg.return_samples));
+    ends_ = Alloc<int32_t>(P);
+    hostEnds_.assign(P, -1);
     mom_ = (double*)Alloc<char>(4 * sizeof(double) + lk::moments_scratch_bytes());
     hipCheck(hipStreamSynchronize(s_), "Learner init");
 }
@@ -339,29 +342,41 @@ void Learner::Consume() {
     RlgpuCheck(rlgpu_gae_rollout(v.rewards, v.terms, v.values, v.trunc_vals, v.values + TP, T, P, cfg_.gamma,
                                  cfg_.gae_lambda, std_, cfg_.reward_clip_range, v.adv, v.target, v.ret, nullptr, s_),
                "GAE");
-    // return-std Welford over randomly sampled returns (Learner.cpp:959-967); in an old-version
-    // iteration only the current policy's players have trajectories
+    // return-std Welford over randomly sampled returns (Learner.cpp:959-967).  The reference samples
+    // combinedTraj, i.e. steps of finished trajectories only, whose returns run to the trajectory's
+    // end; here only rows (t, p) with t <= the column's last trajectory end qualify (an unfinished
+    // tail's return would be cut at T).  In an old-version iteration only the current policy's
+    // players have trajectories.
     const int k = cfg_.return_samples;
     if (k <= 0) return;
-    std::vector<int64_t> idx(k);
-    const int64_t range = oldTeam_ < 0 ? TP : TP / 2;
-    rlgpu_sample_indices(cfg_.seed, cfg_.rank, stats.iteration, range, k, idx.data());
-    if (oldTeam_ >= 0) {
-        const int half = P / 2, team = 1 - oldTeam_;
-        for (auto& j : idx) j = (j / half) * P + 2 * (j % half) + team;
-    }
-    hipCheck(hipMemcpyAsync(sampleIdx_, idx.data(), k * sizeof(int64_t), hipMemcpyHostToDevice, s_), "sample idx");
-    lk::gather_samples(v.ret, sampleIdx_, k, samples_, s_);
-    std::vector<float> hs(k);
-    hipCheck(hipMemcpyAsync(hs.data(), samples_, k * sizeof(float), hipMemcpyDeviceToHost, s_), "samples");
+    lk::last_ends(v.terms, T, P, ends_, s_);
+    hipCheck(hipMemcpyAsync(hostEnds_.data(), ends_, (size_t)P * sizeof(int32_t), hipMemcpyDeviceToHost, s_), "ends");
     hipCheck(hipStreamSynchronize(s_), "sync");
-    if (hasColl_) {
-        std::vector<float> all((size_t)k * cfg_.world);
-        if (coll_.allgather_f32(coll_.user, hs.data(), k, all.data()) != 0)
+    if (oldTeam_ >= 0)
+        for (int p = oldTeam_; p < P; p += 2) hostEnds_[p] = -1;  // team of player p is p % 2
+    std::vector<int64_t> idx(k);
+    int32_t m = 0;
+    RlgpuCheck(rlgpu_sample_finished_rows(cfg_.seed, cfg_.rank, stats.iteration, hostEnds_.data(), P, k, idx.data(), &m),
+               "return samples");
+    std::vector<float> hs((size_t)std::max(m, 1));
+    if (m > 0) {
+        hipCheck(hipMemcpyAsync(sampleIdx_, idx.data(), m * sizeof(int64_t), hipMemcpyHostToDevice, s_), "sample idx");
+        lk::gather_samples(v.ret, sampleIdx_, m, samples_, s_);
+        hipCheck(hipMemcpyAsync(hs.data(), samples_, m * sizeof(float), hipMemcpyDeviceToHost, s_), "samples");
+        hipCheck(hipStreamSynchronize(s_), "sync");
+    }
+    if (hasColl_) {  // ranks may hold different sample counts: gather (count, k padded samples)
+        std::vector<float> mine((size_t)k + 1, 0.f), all((size_t)(k + 1) * cfg_.world);
+        mine[0] = (float)m;
+        std::copy(hs.begin(), hs.begin() + m, mine.begin() + 1);
+        if (coll_.allgather_f32(coll_.user, mine.data(), k + 1, all.data()) != 0)
             throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: return-sample all-gather failed");
-        returnStat.Increment(all.data(), (int64_t)all.size());
+        for (int r = 0; r < cfg_.world; r++) {
+            const float* blk = all.data() + (size_t)r * (k + 1);
+            returnStat.Increment(blk + 1, (int64_t)blk[0]);
+        }
     } else {
-        returnStat.Increment(hs.data(), k);
+        returnStat.Increment(hs.data(), m);
     }
 }
 
@@ -668,6 +683,27 @@ extern "C" double rlgpu_welford_std(int64_t count, double m2) {
     w.count = count;
     w.m2 = m2;
     return w.GetSTD();
+}
+
+extern "C" int rlgpu_sample_finished_rows(uint64_t seed, int32_t rank, int64_t iteration, const int32_t* ends,
+                                          int32_t P, int32_t n, int64_t* out, int32_t* n_out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(ends && out && n_out && n >= 0 && P > 0, "rlgpu_sample_finished_rows: bad argument");
+        // cumulative eligible-row counts per column, then each draw j in [0, total) -> (column, t)
+        std::vector<int64_t> cum((size_t)P + 1, 0);
+        for (int32_t p = 0; p < P; p++) cum[p + 1] = cum[p] + (ends[p] >= 0 ? (int64_t)ends[p] + 1 : 0);
+        const int64_t total = cum[P];
+        const int32_t m = (int32_t)std::min<int64_t>(n, total);
+        *n_out = m;
+        if (m == 0) return;
+        std::vector<int64_t> draws(m);
+        RLGC::RlgpuCheck(rlgpu_sample_indices(seed, rank, iteration, total, m, draws.data()), "sample indices");
+        for (int32_t i = 0; i < m; i++) {
+            const int64_t j = draws[i];
+            const int32_t p = (int32_t)(std::upper_bound(cum.begin(), cum.end(), j) - cum.begin()) - 1;
+            out[i] = (j - cum[p]) * (int64_t)P + p;
+        }
+    });
 }
 
 extern "C" int rlgpu_sample_indices(uint64_t seed, int32_t rank, int64_t iteration, int64_t range, int32_t n,

@@ -175,6 +175,8 @@ private:
     int64_t truncCap_ = 0;
     int64_t* sampleIdx_ = nullptr;
     float* samples_ = nullptr;
+    int32_t* ends_ = nullptr;          // [P] last trajectory end per column (return sampling)
+    std::vector<int32_t> hostEnds_;
     double* mom_ = nullptr;   // [3] + scratch
     std::vector<void*> allocs_;
     template <class T>

@@ -54,13 +54,76 @@ def write_model(seq, path):
         torch.jit.script(seq.cpu()).save(path)
 
 
+class _ScriptObject:
+    """Stand-in for a pickled TorchScript module object: only its attribute dict is kept."""
+
+
+_STORAGE_DTYPES = {"FloatStorage": "float32", "DoubleStorage": "float64", "HalfStorage": "float16",
+                   "BFloat16Storage": "bfloat16", "LongStorage": "int64", "IntStorage": "int32",
+                   "ShortStorage": "int16", "CharStorage": "int8", "ByteStorage": "uint8", "BoolStorage": "bool"}
+
+
+def _rebuild_tensor(storage, offset, size, stride, *_):
+    return storage.as_strided(tuple(size), tuple(stride), offset).clone()
+
+
 def read_model_state(path):
-    """Parameters of a <NAME>.lt in torch parameters() order (reference- or rlgpu-written)."""
+    """Parameters of a <NAME>.lt in torch parameters() order (reference- or rlgpu-written), read
+    without executing anything from the archive: the TorchScript zip's data.pkl is unpickled by a
+    loader that admits only tensor rebuilds (torch._utils._rebuild_tensor_v2 with typed storages
+    from the archive's data/ records), OrderedDict and inert stand-ins for the __torch__ module
+    classes -- the archive's code/ is never read.  Tensors are collected depth-first, each object's
+    own tensors before its submodules' (Module::parameters() order; Linear / LayerNorm hold only
+    weight and bias)."""
+    import collections
+    import io
+    import pickle
+    import zipfile
+
     import torch
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore", DeprecationWarning)
-        m = torch.jit.load(path, map_location="cpu")
-    return [p.detach().float() for p in m.parameters()]
+
+    with zipfile.ZipFile(path) as z:
+        names = z.namelist()
+        pkl = [n for n in names if n.endswith("/data.pkl") and n.count("/") == 1]
+        if len(pkl) != 1:
+            raise ValueError(f"{path}: not a TorchScript archive (no top-level data.pkl)")
+        prefix = pkl[0][:-len("data.pkl")]
+
+        class _Reader(pickle.Unpickler):
+            def find_class(self, module, name):
+                if module.startswith("__torch__"):
+                    return _ScriptObject
+                if (module, name) == ("torch._utils", "_rebuild_tensor_v2"):
+                    return _rebuild_tensor
+                if (module, name) == ("collections", "OrderedDict"):
+                    return collections.OrderedDict
+                if module == "torch" and name in _STORAGE_DTYPES:
+                    return getattr(torch, _STORAGE_DTYPES[name])
+                raise pickle.UnpicklingError(f"{path}: refusing to load global {module}.{name}")
+
+            def persistent_load(self, pid):
+                if not (isinstance(pid, tuple) and len(pid) == 5 and pid[0] == "storage"):
+                    raise pickle.UnpicklingError(f"{path}: unexpected persistent id {pid!r}")
+                _, dtype, key, _loc, numel = pid
+                raw = bytearray(z.read(prefix + "data/" + str(key)))
+                t = torch.frombuffer(raw, dtype=dtype) if raw else torch.empty(0, dtype=dtype)
+                if t.numel() < numel:
+                    raise pickle.UnpicklingError(f"{path}: storage {key} is truncated")
+                return t
+
+        root = _Reader(io.BytesIO(z.read(pkl[0]))).load()
+
+    out = []
+
+    def walk(obj):
+        attrs = obj.__dict__ if isinstance(obj, _ScriptObject) else {}
+        out.extend(v.detach().float() for v in attrs.values() if isinstance(v, torch.Tensor))
+        for v in attrs.values():
+            if isinstance(v, _ScriptObject):
+                walk(v)
+
+    walk(root)
+    return out
 
 
 def save(learner, folder, keep=8):

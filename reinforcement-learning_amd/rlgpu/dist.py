@@ -11,7 +11,10 @@ another rank.  The exchanges are the PPO ones, issued by the C++ Learner (host/l
     finished by rlgpu_moments_mean_std;
   * return samples for the WelfordStat (Learner.cpp:959-967), all-gathered so every rank holds the
     same return-std state;
-  * max over ranks of the timed region (bench contract).
+  * max over ranks of the timed region (bench contract);
+  * at start-up, rank 0's checkpoint (parameters, AdamW state, counters, return statistics, old
+    policy versions) broadcast to every rank (rlgpu.learner.sync_from_rank0), so ranks without the
+    checkpoint folder cannot start from diverged replicas.
 """
 import ctypes
 
@@ -113,6 +116,19 @@ def moments_mean_std(m3):
     out = np.zeros(2, np.float32)
     _lib.check(L.rlgpu_moments_mean_std(m.ctypes.data, out.ctypes.data), "rlgpu_moments_mean_std")
     return out
+
+
+def broadcast_(t, group=None):
+    """Rank 0's tensor into `t` on every rank, in place (RCCL for device tensors on nccl; through the
+    host for gloo)."""
+    backend = dist.get_backend(group)
+    if t.device.type == "cpu" or backend == "nccl":
+        dist.broadcast(t, 0, group=group)
+    else:
+        c = t.cpu()
+        dist.broadcast(c, 0, group=group)
+        t.copy_(c)
+    return t
 
 
 def max_over_ranks(seconds, device=None, group=None):

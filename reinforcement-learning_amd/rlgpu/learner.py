@@ -39,6 +39,9 @@ def _host_lib():
     L.rlgpu_welford_std.restype = ctypes.c_double
     L.rlgpu_sample_indices.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_void_p]
+    L.rlgpu_sample_finished_rows.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_int32)]
     return L
 
 
@@ -84,6 +87,62 @@ def sample_indices(seed, rank, iteration, rng, n):
     out = np.zeros(max(n, 1), np.int64)
     _lib.check(_host_lib().rlgpu_sample_indices(seed, rank, iteration, rng, n, out.ctypes.data), "rlgpu_sample_indices")
     return out[:n]
+
+
+def last_ends(terms):
+    """Per column of a [T, P] trajectory-code array: the last step with a nonzero code, -1 if none."""
+    t = np.asarray(terms)
+    nz = t != 0
+    T = t.shape[0]
+    last = T - 1 - np.argmax(nz[::-1], axis=0)
+    return np.where(nz.any(axis=0), last, -1).astype(np.int32)
+
+
+def sample_finished_rows(seed, rank, iteration, ends, n):
+    """rlgpu_sample_finished_rows: the return-sample rows t * P + p (t <= ends[p]) of one iteration,
+    drawn from finished trajectories only (Learner.cpp:823-861, 959-967)."""
+    e = np.ascontiguousarray(ends, np.int32)
+    out = np.zeros(max(n, 1), np.int64)
+    m = ctypes.c_int32()
+    _lib.check(_host_lib().rlgpu_sample_finished_rows(seed, rank, iteration, e.ctypes.data, e.size, n, out.ctypes.data,
+                                                      ctypes.byref(m)), "rlgpu_sample_finished_rows")
+    return out[:m.value]
+
+
+def sync_from_rank0(learner, group=None):
+    """Every rank takes rank 0's training state: parameters, AdamW moments and step, step counters,
+    return statistics and the old policy versions.  Only rank 0 reads the checkpoint folder
+    (Learner.cpp:145-153 loads in the single-process reference); the ranks need not share a
+    filesystem, and replicas can never start diverged."""
+    import torch
+    from .dist import broadcast_
+    st = learner._stats()
+    ppo = learner.ppo
+    step, m, v = ppo.optimizer_state()
+    vers = learner.versions.versions if learner.versions is not None else []
+    hdr = torch.tensor([float(learner.last_checkpoint is not None), st.total_steps, st.iteration, st.return_n,
+                        st.return_mean, st.return_m2, step, len(vers)], dtype=torch.float64)
+    broadcast_(hdr, group)
+    loaded, total, it, rn, rmean, rm2, step, nv = hdr.tolist()
+    if not loaded:
+        return
+    for t in (ppo.params, m, v):
+        broadcast_(t, group)
+    st.total_steps, st.iteration, st.return_n = int(total), int(it), int(rn)
+    st.return_mean, st.return_m2 = rmean, rm2
+    learner._set_stats(st)
+    ppo.set_optimizer_step(int(step))
+    ppo.refresh_half()
+    if learner.versions is not None and int(nv) > 0:
+        ts = torch.tensor([float(x.timesteps) for x in vers] if vers else [0.0] * int(nv), dtype=torch.float64)
+        broadcast_(ts, group)
+        like = ppo.model_slice(0)
+        params = [x.params for x in vers] if vers else [torch.empty_like(like) for _ in range(int(nv))]
+        for t in params:
+            broadcast_(t, group)
+        if not vers:
+            for k, t in enumerate(params):
+                learner.versions.add_version(int(ts[k]), t)
 
 
 # ------------------------------------------------------------------ config
@@ -284,9 +343,12 @@ class Learner:
         self.last_checkpoint = None
         if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-153)
             from . import checkpoint as _ckpt
-            self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
-            if self.versions is not None:
-                self.versions.load_versions(self.total_steps)
+            if rank == 0:  # rank 0 reads the folder, every other rank receives its state
+                self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
+                if self.versions is not None:
+                    self.versions.load_versions(self.total_steps)
+            if world > 1:
+                sync_from_rank0(self, group)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -110,3 +110,41 @@ def test_welford_stat_reference_rules():
     u = WelfordStat()
     u.read_json(j)
     assert (u.n, u.mean, u.m2) == (v.n, v.mean, v.m2)
+
+
+def test_model_reader_executes_nothing(tmp_path):
+    """read_model_state admits only tensor rebuilds, OrderedDict and inert module stand-ins: an archive
+    whose data.pkl names any other global is refused before anything runs (user-supplied
+    POLICY.lt / policy_versions archives are untrusted input)."""
+    import pickle
+    import zipfile
+    marker = tmp_path / "ran"
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, (f"touch {marker}",))
+
+    p = str(tmp_path / "POLICY.lt")
+    with zipfile.ZipFile(p, "w") as z:
+        z.writestr("POLICY/data.pkl", pickle.dumps(Evil(), protocol=2))
+    with pytest.raises(pickle.UnpicklingError):
+        ckpt.read_model_state(p)
+    assert not marker.exists()
+    with zipfile.ZipFile(str(tmp_path / "x.lt"), "w") as z:
+        z.writestr("x/other.bin", b"")
+    with pytest.raises(ValueError):
+        ckpt.read_model_state(str(tmp_path / "x.lt"))
+
+
+def test_model_reader_matches_parameters(tmp_path):
+    """The code-free reader returns exactly the module's parameters() in order."""
+    import torch
+    torch.manual_seed(5)
+    seq = make_sequential(ARCH["obs"], ARCH["out"], ARCH["layers"], True)
+    p = str(tmp_path / "POLICY.lt")
+    ckpt.write_model(seq, p)
+    got = ckpt.read_model_state(p)
+    want = list(seq.parameters())
+    assert [t.shape for t in got] == [w.shape for w in want]
+    for g, w in zip(got, want):
+        assert torch.equal(g, w.detach())

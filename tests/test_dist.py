@@ -117,3 +117,123 @@ def test_batch_ranges_match_experience_buffer():
     assert batch_ranges(50, 100) == [(0, 50)]                          # fewer than one batch
     assert batch_ranges(50, 100, False) == []
     assert batch_ranges(0, 100) == []
+
+
+def test_return_samples_come_from_finished_trajectories():
+    """rlgpu_sample_finished_rows: the reference samples returns of combinedTraj, which holds
+    finished trajectories only (Learner.cpp:823-861, 959-967).  Every drawn row (t, p) has t <= the
+    column's last trajectory end; the count is min(n, #eligible); the draws are reproducible and
+    cover the eligible set roughly uniformly; no finished trajectory -> no samples."""
+    import numpy as np
+    from rlgpu.learner import last_ends, sample_finished_rows
+    T, P = 16, 12
+    rng = np.random.default_rng(3)
+    terms = np.zeros((T, P), np.int8)
+    terms[rng.random((T, P)) < 0.08] = 1
+    terms[5, 3], terms[15, 4], terms[0, 6] = 2, 1, 1
+    terms[:, 0] = 0  # column 0: an unfinished trajectory only
+    ends = last_ends(terms)
+    assert ends[0] == -1 and ends[4] == 15 and ends[6] >= 0
+    for p in range(P):
+        nz = np.nonzero(terms[:, p])[0]
+        assert ends[p] == (nz.max() if nz.size else -1)
+    eligible = {t * P + p for p in range(P) for t in range(ends[p] + 1)}
+    rows = sample_finished_rows(123, 0, 7, ends, 150)
+    assert rows.size == min(150, len(eligible))
+    assert set(rows.tolist()) <= eligible
+    assert np.array_equal(rows, sample_finished_rows(123, 0, 7, ends, 150))      # reproducible
+    assert not np.array_equal(rows, sample_finished_rows(123, 0, 8, ends, 150))  # per-iteration draws
+    big = sample_finished_rows(1, 0, 0, ends, 200_000)
+    assert big.size == len(eligible)  # capped at the eligible count (torch::randint over tReturns)
+    many = np.concatenate([sample_finished_rows(1, 0, it, ends, 150) for it in range(400)])
+    cnt = np.bincount(many, minlength=T * P)[sorted(eligible)]
+    assert cnt.min() > 0 and cnt.max() < 3 * cnt.mean()
+    assert sample_finished_rows(1, 0, 0, np.full(P, -1, np.int32), 150).size == 0
+
+
+class _FakeStats:
+    def __init__(self):
+        self.total_steps = self.iteration = self.return_n = 0
+        self.return_mean = self.return_m2 = 0.0
+
+
+class _FakePPO:
+    """The slice of rlgpu.ppo.PPO that sync_from_rank0 touches, on CPU tensors."""
+
+    def __init__(self, n, policy):
+        self.params, self.m, self.v = torch.zeros(n), torch.zeros(n), torch.zeros(n)
+        self.policy, self.step, self.refreshed = policy, 0, False
+
+    def optimizer_state(self):
+        return self.step, self.m, self.v
+
+    def set_optimizer_step(self, s):
+        self.step = s
+
+    def refresh_half(self):
+        self.refreshed = True
+
+    def model_slice(self, model):
+        return self.params[:self.policy]
+
+
+class _FakeLearner:
+    def __init__(self, rank):
+        from rlgpu.versions import PolicyVersionManager
+        self.ppo = _FakePPO(10, 4)
+        self.versions = PolicyVersionManager(self.ppo)
+        self.st = _FakeStats()
+        self.last_checkpoint = None
+        if rank == 0:  # what checkpoint.load + load_versions leave on rank 0
+            self.last_checkpoint = "/ckpt/300"
+            self.ppo.params.copy_(torch.arange(10.0))
+            self.ppo.m.fill_(0.5)
+            self.ppo.v.fill_(0.25)
+            self.ppo.step = 7
+            self.st.total_steps, self.st.iteration, self.st.return_n = 300, 3, 450
+            self.st.return_mean, self.st.return_m2 = 1.25, 9.5
+            self.versions.add_version(100, torch.full((4,), 1.0))
+            self.versions.add_version(200, torch.full((4,), 2.0))
+
+    def _stats(self):
+        return self.st
+
+    def _set_stats(self, st):
+        self.st = st
+
+
+def _sync_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd"))
+    from rlgpu.learner import sync_from_rank0
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = _FakeLearner(rank)
+        sync_from_rank0(L)
+        s = L.st
+        q.put((rank, L.ppo.params.tolist(), L.ppo.m.tolist(), L.ppo.v.tolist(), L.ppo.step, L.ppo.refreshed,
+               (s.total_steps, s.iteration, s.return_n, s.return_mean, s.return_m2),
+               [(x.timesteps, x.params.tolist()) for x in L.versions.versions]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_checkpoint_state_broadcast_from_rank0():
+    """Only rank 0 reads the checkpoint folder; sync_from_rank0 hands its parameters, AdamW state,
+    counters, return statistics and old policy versions to every other rank (world size 2, gloo)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[1][1:] == res[0][1:]
+    assert res[1][1] == list(np.arange(10.0)) and res[1][4] == 7 and res[1][5]
+    assert res[1][6] == (300, 3, 450, 1.25, 9.5)
+    assert res[1][7] == [(100, [1.0] * 4), (200, [2.0] * 4)]

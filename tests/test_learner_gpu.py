@@ -60,7 +60,9 @@ def test_consume_gae_matches_oracle(gpu):
     np.testing.assert_array_equal(L.adv.cpu().numpy(), adv)
     np.testing.assert_array_equal(L.target.cpu().numpy(), tgt)
     np.testing.assert_array_equal(L.ret.cpu().numpy(), ret)
-    assert L.return_stat.n == L.cfg.return_samples
+    from rlgpu.learner import last_ends
+    eligible = int((last_ends(terms) + 1).sum())  # steps of trajectories finished inside the rollout
+    assert L.return_stat.n == min(L.cfg.return_samples, eligible)
 
 
 def test_learn_updates_parameters(gpu):
@@ -182,20 +184,35 @@ def test_example_main_binary(gpu):
     assert len(lines) == 2 and "Total Timesteps 4096" in lines[-1], r.stdout
 
 
-def test_sample_indices_and_welford_state(gpu):
-    """The return samples of an iteration come from rlgpu_sample_indices (seed, rank, iteration) and
-    feed the C++ WelfordStat: recompute them from the ret buffer and compare the Welford state."""
+def test_return_samples_finished_trajectories_and_welford_state(gpu):
+    """The return samples of an iteration (rlgpu_sample_finished_rows over the columns' last trajectory
+    ends) feed the C++ WelfordStat: recompute them from the rollout and compare the Welford state.
+    Each sampled return is a complete one -- equal, bit for bit, to the return the reference's flat
+    path (oracle/gae_ref.c, GAE.cpp:169-193) computes over the finished trajectory segment alone."""
     import torch
-    from rlgpu.learner import WelfordStat, sample_indices
-    L = _learner(gpu, train_against_old_versions=False)
+    from rlgpu.learner import WelfordStat, last_ends, sample_finished_rows
+    L = _learner(gpu, train_against_old_versions=False, max_episode_duration=1.0)
     L.collect()
     L.consume()
     torch.cuda.synchronize()
-    idx = sample_indices(L.cfg.seed, 0, 0, L.T * L.P, L.cfg.return_samples)
-    assert idx.min() >= 0 and idx.max() < L.T * L.P
+    terms = L.terms.cpu().numpy()
+    ends = last_ends(terms)
+    assert (ends >= 0).any() and (ends < L.T - 1).any()
+    rows = sample_finished_rows(L.cfg.seed, 0, 0, ends, L.cfg.return_samples)
+    assert rows.size == L.return_stat.n > 0
+    t_idx, p_idx = rows // L.P, rows % L.P
+    assert (t_idx <= ends[p_idx]).all()
+    ret = L.ret.cpu().numpy()
     w = WelfordStat()
-    w.add(L.ret.view(-1).cpu().numpy()[idx])
+    w.add(ret.reshape(-1)[rows])
     assert (w.n, w.mean, w.m2) == (L.return_stat.n, L.return_stat.mean, L.return_stat.m2)
+    rews = L.rewards.cpu().numpy()
+    vals = L.values.cpu().numpy()
+    for t, p in zip(t_idx[:40], p_idx[:40]):
+        e = ends[p] + 1  # the column's finished prefix, as one flat combined-trajectory segment
+        _, _, fr, _, st = oracle.gae_flat(rews[:e, p], terms[:e, p], vals[:e, p], None, L.cfg.gamma, L.cfg.gae_lambda,
+                                          1.0, 0.0)
+        assert fr[t].view(np.uint32) == ret[t, p].view(np.uint32)
 
 
 def test_c5_learner_iteration_fp16(gpu):
