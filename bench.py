@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--arenas", type=int, default=ARENAS_PER_GPU)
     ap.add_argument("--rollout", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-gemm", choices=("h3", "x6", "f32"), default="h3",
+                    help="fp32 training GEMM arithmetic (include/rlgpu_ppo.h rlgpu_gemm modes)")
     args = ap.parse_args()
 
     import torch
@@ -115,7 +117,10 @@ def main():
     from rlgpu.learner import Learner, LearnerConfig
     # self-play iterations (15 % chance, LearnerConfig.h:67-68) are off so every timed iteration has
     # the same work; the mixed-policy path is covered by tests/test_learner_gpu.py
-    cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False)
+    from rlgpu.ppo import GEMM_F16X3, GEMM_F32, GEMM_F32X6
+    train_gemm = {"h3": GEMM_F16X3, "x6": GEMM_F32X6, "f32": GEMM_F32}[args.train_gemm]
+    cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False,
+                        train_gemm=train_gemm)
     L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
     L.set_env_timing(True)  # HIP events around every fused env step, on the learner's stream
 
@@ -159,7 +164,8 @@ def main():
                                "AdvancedObs + DefaultAction(90) + 13 ExampleMain rewards; PPO actor/critic [512,512] "
                                "LayerNorm+LeakyReLU, bf16 inference / fp32 training, T=128, 2 epochs, minibatch 50k",
                    "arenas_per_gpu": args.arenas, "agents_per_gpu": 4 * args.arenas, "rollout_len": cfg.rollout_len,
-                   "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32"},
+                   "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32",
+                   "train_gemm": args.train_gemm},
         "agent_steps_per_s": agent_steps / el,
         "ppo_s_per_1M_agent_steps": el / agent_steps * 1e6,
         "phase_s_per_iteration": {k: v / args.steps for k, v in phase.items()},

@@ -52,8 +52,8 @@ typedef struct {
     float max_grad_norm;                      /* 0.5 (PPOLearner.cpp:521-526) */
     int32_t max_rows;                         /* workspace rows: max(minibatch, inference chunk) */
     uint64_t seed;                            /* parameter init + action sampling (Philox) */
-    int32_t train_gemm;                       /* training GEMM arithmetic: RLGPU_GEMM_F32X6 (0, default)
-                                                 or RLGPU_GEMM_F32 (1) -- see rlgpu_gemm */
+    int32_t train_gemm;                       /* training GEMM arithmetic: RLGPU_GEMM_F32X6 (0),
+                                                 RLGPU_GEMM_F32 (1) or RLGPU_GEMM_F16X3 (2) -- see rlgpu_gemm */
     int32_t infer_fp16;                       /* 16-bit inference copy: 0 = bf16 (the reference's seqHalf),
                                                  1 = fp16 on v_mfma_f32_32x32x16_f16 (BASELINE config C5) */
 } rlgpu_ppo_config;
@@ -64,8 +64,13 @@ typedef struct {
  *                     products above 2^-24 relative on v_mfma_f32_32x32x16_bf16, leading and
  *                     correction terms in separate f32 accumulators: f32-class accuracy at 8/3 x
  *                     the f32-MFMA rate (gfx950's f32-input MFMA runs at 1/16 of bf16);
- *   RLGPU_GEMM_F32    v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate). */
-enum { RLGPU_GEMM_F32X6 = 0, RLGPU_GEMM_F32 = 1 };
+ *   RLGPU_GEMM_F32    v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate);
+ *   RLGPU_GEMM_F16X3  every operand tensor scaled by a power of two (its max |x| into [2^14, 2^15))
+ *                     and split exactly into two fp16 terms (h + l, 22 significant bits), the
+ *                     three products h h + h l + l h on v_mfma_f32_32x32x16_f16, leading and
+ *                     correction terms in separate f32 accumulators (the 3xTF32 scheme of fp32
+ *                     emulation): half the MFMAs of F32X6, products within 2^-22 relative. */
+enum { RLGPU_GEMM_F32X6 = 0, RLGPU_GEMM_F32 = 1, RLGPU_GEMM_F16X3 = 2 };
 
 typedef struct rlgpu_ppo rlgpu_ppo;
 
@@ -138,7 +143,7 @@ int rlgpu_ppo_optimizer_state(rlgpu_ppo* h, int64_t* step, float** d_exp_avg, fl
 int rlgpu_ppo_set_optimizer_step(rlgpu_ppo* h, int64_t step);
 
 /* Building block, exported for tests and microbenchmarks: C[I,J] = sum_k A(i,k) B(k,j) (+ bias[j])
- * in the fp32 arithmetic `mode` (RLGPU_GEMM_F32X6 / RLGPU_GEMM_F32).  a_layout 0: A stored [I][lda] (k contiguous), 1: [K][lda] (i contiguous);
+ * in the fp32 arithmetic `mode` (RLGPU_GEMM_F32X6 / RLGPU_GEMM_F32 / RLGPU_GEMM_F16X3).  a_layout 0: A stored [I][lda] (k contiguous), 1: [K][lda] (i contiguous);
  * b_layout 0: B stored [J][ldb] (k contiguous), 1: [K][ldb] (j contiguous).  splits > 1 writes
  * per-split partials to C + s*I*ldc (caller reduces).  Supported pairs: (0,0), (0,1), (1,1). */
 int rlgpu_gemm(int32_t mode, int32_t a_layout, int32_t b_layout, const float* d_A, int64_t lda, const float* d_B,

@@ -42,6 +42,11 @@ struct GemmArgs {
     int64_t c_split;       // element stride between split partials
     int gx, gy, gz;        // logical tile grid (J tiles, I tiles, K splits); launched as 1-D
     int64_t bplane;        // gemm_x6 with a pre-split B: element stride between the bf16 planes
+    // fp16x3 arithmetic (H3): 64 shards of max |x| (float bits) of each operand tensor, and for a
+    // pre-split B its per-row inverse scales [rows]
+    const float* amax_a;
+    const float* amax_b;
+    const float* bscale;
 };
 
 DEV uint16_t f2bf(float f) {  // round-to-nearest-even (plain cast: NaN stays NaN)
@@ -278,6 +283,67 @@ DEV void split3(const f32x4_t (&v)[2], u32x4_t& h, u32x4_t& m, u32x4_t& l) {
     }
 }
 
+// ---- fp32 GEMM on fp16 MFMA by a scaled two-way split (H3: RLGPU_GEMM_F16X3).
+// Each operand tensor is scaled by a power of two s (exact) that puts its largest magnitude in
+// [2^14, 2^15), then every element splits exactly into two fp16 terms, x s = h + l (h = fp16(x s),
+// l = fp16(x s - h); the subtraction is exact).  h + l carries 22 significant bits for every
+// element within 2^16 of the tensor's largest (below that, an absolute error under 2^-39 of it),
+// fp16 x fp16 products are exact in f32, and
+//   a.b ~= (h_a h_b + [h_a l_b + l_a h_b]) / (s_a s_b)
+// on v_mfma_f32_32x32x16_f16 drops only l_a l_b (below 2^-22 relative): the 3xTF32 scheme of fp32
+// emulation, with fp16's narrower exponent range covered by the scale.  Three MFMAs per K = 16
+// instead of the x6 path's six, two LDS planes instead of three.  The scales come from 64 shards
+// of max |x| that the operand's producer kernel fills (h3_amax_commit), so no extra pass reads the
+// tensor; pre-split weights carry one scale per row.
+DEV uint32_t shard_max_bits(const float* shards) {  // max over the 64 shards, every lane gets it
+    uint32_t v = __float_as_uint(shards[threadIdx.x & 63]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+// power-of-two p with amax * 2^p in [2^14, 2^15); 0 for a zero, subnormal, infinite or NaN max
+DEV int h3_pow(uint32_t amax_bits) {
+    const int e = (int)((amax_bits >> 23) & 255u);
+    if (amax_bits > 0x7f7fffffu || e == 0) return 0;
+    int p = 14 - (e - 127);
+    return p > 126 ? 126 : p;
+}
+DEV float pow2f(int p) { return __uint_as_float((uint32_t)(p + 127) << 23); }  // p in [-126, 127]
+DEV uint16_t f2hf(float f) { return __half_as_ushort(__float2half(f)); }
+DEV float hf2f(uint16_t u) { return __half2float(__ushort_as_half(u)); }
+DEV uint32_t pack_h2(uint16_t a, uint16_t b) { return (uint32_t)a | ((uint32_t)b << 16); }
+// split 8 floats (two native 4-vectors), scaled by sc, into two fp16x8 planes
+DEV void split2h(const f32x4_t (&v)[2], float sc, u32x4_t& h, u32x4_t& l) {
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const float x0 = v[p >> 1][(2 * p) & 3] * sc, x1 = v[p >> 1][(2 * p + 1) & 3] * sc;
+        const uint16_t h0 = f2hf(x0), h1 = f2hf(x1);
+        h[p] = pack_h2(h0, h1);
+        l[p] = pack_h2(f2hf(x0 - hf2f(h0)), f2hf(x1 - hf2f(h1)));
+    }
+}
+// Producers: this thread's max |x| bits (vmax) -> block max -> atomicMax into shard blockIdx % 64.
+// Must be reached by every thread of the 256-thread block.
+DEV void h3_amax_commit(float* shards, uint32_t vmax) {
+    __shared__ uint32_t red[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)vmax, o, 64);
+        vmax = u > vmax ? u : vmax;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = red[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = red[w] > m ? red[w] : m;
+        atomicMax(reinterpret_cast<unsigned int*>(shards) + (blockIdx.x & 63), m);
+    }
+}
+DEV uint32_t abs_bits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+
 // Per-thread share of one 128 x XK operand stage (XK = 32 or 64 k): NQ = XK / 16 groups of 8
 // consecutive k of one row, held in native 4-vectors (loop-carried prefetch registers stay where
 // the loads land, so the wait for them sits at the next stage's store, after this stage's MFMAs).
@@ -339,16 +405,23 @@ DEV void xs_load(f32x4_t (&v)[XK / 16][2], const RowPtrs& rows, const float* bas
         }
     }
 }
-template <bool KMAJ, int XK>
-DEV void xs_store(uint16_t (*lds)[BM][XK + XPAD], const f32x4_t (&v)[XK / 16][2]) {
+template <bool KMAJ, int XK, bool H3>
+DEV void xs_store(uint16_t (*lds)[BM][XK + XPAD], const f32x4_t (&v)[XK / 16][2], float sc) {
 #pragma unroll
     for (int q = 0; q < XK / 16; q++) {
-        u32x4_t h, m, l;
-        split3(v[q], h, m, l);
         const int row = xs_row<KMAJ, XK>(q), c = xs_kg<KMAJ, XK>(q) * 8;
-        *reinterpret_cast<u32x4_t*>(&lds[0][row][c]) = h;
-        *reinterpret_cast<u32x4_t*>(&lds[1][row][c]) = m;
-        *reinterpret_cast<u32x4_t*>(&lds[2][row][c]) = l;
+        if (H3) {
+            u32x4_t h, l;
+            split2h(v[q], sc, h, l);
+            *reinterpret_cast<u32x4_t*>(&lds[0][row][c]) = h;
+            *reinterpret_cast<u32x4_t*>(&lds[1][row][c]) = l;
+        } else {
+            u32x4_t h, m, l;
+            split3(v[q], h, m, l);
+            *reinterpret_cast<u32x4_t*>(&lds[0][row][c]) = h;
+            *reinterpret_cast<u32x4_t*>(&lds[1][row][c]) = m;
+            *reinterpret_cast<u32x4_t*>(&lds[2][row][c]) = l;
+        }
     }
 }
 
@@ -357,8 +430,8 @@ DEV void xs_store(uint16_t (*lds)[BM][XK + XPAD], const f32x4_t (&v)[XK / 16][2]
 // weight matrix is reused by every row tile of a minibatch, so it is split once per minibatch
 // (split_weight) instead of once per tile and stage.  Per thread and stage: XK / 16 16-byte chunks
 // per plane (row e / KG, chunk e % KG of 8 bf16).
-template <int XK>
-DEV void xp_load(u32x4_t (&v)[3][XK / 16], const uint16_t* B, int64_t ldb, int64_t plane, int j0, int k0, int ke) {
+template <int XK, int NP>
+DEV void xp_load(u32x4_t (&v)[NP][XK / 16], const uint16_t* B, int64_t ldb, int64_t plane, int j0, int k0, int ke) {
     constexpr int KG = XK / 8;
 #pragma unroll
     for (int q = 0; q < XK / 16; q++) {
@@ -366,18 +439,18 @@ DEV void xp_load(u32x4_t (&v)[3][XK / 16], const uint16_t* B, int64_t ldb, int64
         const int64_t off = (int64_t)(j0 + e / KG) * ldb + k0 + (e % KG) * 8;
         const bool ok = k0 + (e % KG) * 8 < ke;
 #pragma unroll
-        for (int p = 0; p < 3; p++)
+        for (int p = 0; p < NP; p++)
             v[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? B + p * plane + off : reinterpret_cast<const uint16_t*>(g_zero_row));
     }
 }
-template <int XK>
-DEV void xp_store(uint16_t (*lds)[BM][XK + XPAD], const u32x4_t (&v)[3][XK / 16]) {
+template <int XK, int NP>
+DEV void xp_store(uint16_t (*lds)[BM][XK + XPAD], const u32x4_t (&v)[NP][XK / 16]) {
     constexpr int KG = XK / 8;
 #pragma unroll
     for (int q = 0; q < XK / 16; q++) {
         const int e = threadIdx.x + 256 * q;
 #pragma unroll
-        for (int p = 0; p < 3; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e / KG][(e % KG) * 8]) = v[p][q];
+        for (int p = 0; p < NP; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e / KG][(e % KG) * 8]) = v[p][q];
     }
 }
 
@@ -398,6 +471,55 @@ __global__ void split_weight(const float* W, int out, int in, int trans, int row
     planes[2 * plane + e] = f2bf(r1 - bf2f(m));
 }
 
+// H3: W [out][in] (row stride ldw) f32 -> two scaled fp16 planes of W (trans = 0: rows = out, k = in) or W^T
+// (trans = 1: rows = in, k = out), zero padded, one scale per plane row: the 256-thread block of
+// row r finds max |W| over the row's k, then writes x * 2^p split into (h, l) and inv[r] = 2^-p.
+__global__ void __launch_bounds__(256) split_weight_h3(const float* W, int out, int in, int64_t ldw, int trans, int ld_pad,
+                                                      uint16_t* planes, int64_t plane, float* inv) {
+    __shared__ uint32_t red[4];
+    const int r = blockIdx.x;
+    const int nk = trans ? out : in, nr = trans ? in : out;
+    auto at = [&](int k) -> float {  // W element (o, i) at W[o * ldw + i]
+        if (r >= nr || k >= nk) return 0.f;
+        return trans ? W[(int64_t)k * ldw + r] : W[(int64_t)r * ldw + k];
+    };
+    uint32_t m = 0;
+    for (int k = threadIdx.x; k < nk; k += 256) {
+        const uint32_t b = abs_bits(at(k));
+        m = b > m ? b : m;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)m, o, 64);
+        m = u > m ? u : m;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = red[0];
+    for (int w = 1; w < 4; w++) m = red[w] > m ? red[w] : m;
+    const int p = h3_pow(m);
+    const float sc = pow2f(p);
+    for (int k = threadIdx.x; k < ld_pad; k += 256) {
+        const float x = at(k) * sc;
+        const uint16_t h = f2hf(x);
+        planes[(int64_t)r * ld_pad + k] = h;
+        planes[plane + (int64_t)r * ld_pad + k] = f2hf(x - hf2f(h));
+    }
+    if (threadIdx.x == 0) inv[r] = pow2f(-p);
+}
+
+// max |x| over a [rows][cols] f32 matrix (row stride ld) into 64 shards: the stand-alone producer
+// for callers of the H3 GEMM whose operand has no producer kernel of ours (rlgpu_gemm, tests)
+__global__ void __launch_bounds__(256) amax_rows(const float* X, int64_t rows, int cols, int64_t ld, float* shards) {
+    uint32_t m = 0;
+    const int64_t n = rows * cols;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        const uint32_t b = abs_bits(X[(e / cols) * ld + e % cols]);
+        m = b > m ? b : m;
+    }
+    h3_amax_commit(shards, m);
+}
+
 // Stage variants (the x6 GEMM's pipeline shape):
 //   V = 0: 32-deep stages, one LDS buffer, two workgroups per CU
 //   V = 1: 64-deep stages, one LDS buffer, one workgroup per CU
@@ -407,6 +529,17 @@ template <int V> struct X6Shape;
 template <> struct X6Shape<0> { static constexpr int XK = 32, NB = 1, OCC = 2; };
 template <> struct X6Shape<1> { static constexpr int XK = 64, NB = 1, OCC = 1; };
 template <> struct X6Shape<2> { static constexpr int XK = 32, NB = 2, OCC = 1; };
+//   V = 3: 64-deep stages, one LDS buffer, two workgroups per CU (H3: two planes fit 2 x 73.7 KB)
+template <> struct X6Shape<3> { static constexpr int XK = 64, NB = 1, OCC = 2; };
+//   V = 4: 32-deep stages, two LDS buffers (one barrier per stage), two workgroups per CU (H3:
+//          2 x 80 KB of LDS)
+template <> struct X6Shape<4> { static constexpr int XK = 32, NB = 2, OCC = 2; };
+//   V = 5: V = 4 with the next stage's split / LDS stores interleaved between this stage's MFMAs
+//          (sched_group_barrier pattern), so one wave keeps the matrix pipe fed while it stages
+template <> struct X6Shape<5> { static constexpr int XK = 32, NB = 2, OCC = 2; };
+//   V = 6: V = 4 with the next stage stored first, then the stage after it loaded, then this
+//          stage's MFMAs (the loads get a whole stage of MFMAs and a barrier to land)
+template <> struct X6Shape<6> { static constexpr int XK = 32, NB = 2, OCC = 2; };
 
 template <int XK>
 DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
@@ -438,12 +571,42 @@ DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)
     }
 }
 
-template <int LA, int LB, bool AV, bool BV, bool BPRE, int V>
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+template <int XK>
+DEV void h3_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
+                       f32x16 (&acc)[2][2], f32x16 (&cor)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < XK / 16; ks++) {
+        const int kof = ks * 16 + 8 * (lane >> 5);
+        h16x8 a[2][2], b[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                a[p][u] = *(const h16x8*)&As[p][ra + 32 * u][kof];
+                b[p][u] = *(const h16x8*)&Bs[p][rb + 32 * u][kof];
+            }
+        // one accumulator: the corrections, then the leading product, enter the running f32 sum (the
+        // rounding count of an f32 FMA chain; a separate correction accumulator would cost 64
+        // registers that the deeper stage uses instead)
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                f32x16 c = acc[ti][tj];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1][ti], b[0][tj], c, 0, 0, 0);  // l h
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h l
+                acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[0][tj], c, 0, 0, 0);  // h h
+            }
+    }
+}
+
+template <int LA, int LB, bool AV, bool BV, bool BPRE, int V, bool H3 = false>
 __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
-    constexpr int XK = X6Shape<V>::XK, NB = X6Shape<V>::NB, NQ = XK / 16;
+    constexpr int XK = X6Shape<V>::XK, NB = X6Shape<V>::NB, NQ = XK / 16, NP = H3 ? 2 : 3;
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
-    __shared__ uint16_t As[NB][3][BM][XK + XPAD];
-    __shared__ uint16_t Bs[NB][3][BN][XK + XPAD];
+    __shared__ uint16_t As[NB][NP][BM][XK + XPAD];
+    __shared__ uint16_t Bs[NB][NP][BN][XK + XPAD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
     const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
@@ -458,25 +621,38 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[a][b][r] = cor[a][b][r] = 0.f;
     f32x4_t va[NQ][2], vb[NQ][2];
-    u32x4_t vp[3][NQ];
+    u32x4_t vp[NP][NQ];
     const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+    // H3 operand scales (per tensor; a pre-split B carries per-row scales instead)
+    int pa = 0, pb = 0;
+    if (H3) {
+        pa = h3_pow(shard_max_bits(g.amax_a));
+        if (!BPRE) pb = h3_pow(shard_max_bits(g.amax_b));
+    }
+    const float sa = pow2f(pa), sb = pow2f(pb);
     const RowPtrs arow = xs_rows<AK, XK>(g.A, g.lda, i0, g.I);
     const RowPtrs brow = xs_rows<BKM, XK>(g.B, g.ldb, j0, g.J);
     auto load_stage = [&](int k0) {
         xs_load<AK, AV, XK>(va, arow, g.A, g.lda, i0, g.I, k0, ke);
         if (BPRE)
-            xp_load<XK>(vp, Bp, g.ldb, g.bplane, j0, k0, ke);
+            xp_load<XK, NP>(vp, Bp, g.ldb, g.bplane, j0, k0, ke);
         else
             xs_load<BKM, BV, XK>(vb, brow, g.B, g.ldb, j0, g.J, k0, ke);
     };
-    auto store_stage = [&](int buf) {
-        xs_store<AK, XK>(As[buf], va);
-        if (BPRE)
-            xp_store<XK>(Bs[buf], vp);
-        else
-            xs_store<BKM, XK>(Bs[buf], vb);
-    };
     const int ra = wm * 64 + (lane & 31), rb = wn * 64 + (lane & 31);
+    auto store_stage = [&](int buf) {
+        xs_store<AK, XK, H3>(As[buf], va, sa);
+        if (BPRE)
+            xp_store<XK, NP>(Bs[buf], vp);
+        else
+            xs_store<BKM, XK, H3>(Bs[buf], vb, sb);
+    };
+    auto mfma_stage = [&](int buf) {
+        if (H3)
+            h3_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
+        else
+            x6_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
+    };
     load_stage(kb);
     if (NB == 1) {
         for (int k0 = kb; k0 < ke; k0 += XK) {
@@ -486,7 +662,7 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
             // reads the zero row) so the loop-carried registers are the load destinations
             load_stage(k0 + XK);
             __builtin_amdgcn_sched_barrier(0);  // keep the split of the prefetched stage after the MFMAs
-            x6_mfma_stage<XK>(As[0], Bs[0], ra, rb, lane, acc, cor);
+            mfma_stage(0);
             __syncthreads();
         }
     } else {
@@ -497,15 +673,46 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
         for (int k0 = kb; k0 < ke; k0 += XK) {
             // this stage's MFMAs on buf; the next stage (already in registers) is split into the
             // other buffer, free since the previous barrier; then the stage after is prefetched
-            x6_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
-            store_stage(buf ^ 1);
-            load_stage(k0 + 2 * XK);
+            if (V == 6) {
+                store_stage(buf ^ 1);
+                load_stage(k0 + 2 * XK);
+                mfma_stage(buf);
+            } else {
+                mfma_stage(buf);
+                store_stage(buf ^ 1);
+                load_stage(k0 + 2 * XK);
+            }
+            if (V == 5 && H3) {
+                // per stage and wave: 16 ds_read (8 per 16-deep k step), 24 MFMA, 8 ds_write and the
+                // split VALU of the next stage, 8 global loads.  Masks: 0x8 MFMA, 0x2 VALU, 0x100
+                // DS read, 0x200 DS write, 0x20 VMEM read.
+                __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                for (int i = 0; i < 12; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 12; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (i < 8) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);
+            }
             __syncthreads();
             buf ^= 1;
         }
     }
     float* C = g.C + (int64_t)tl.z * g.c_split;
     const int h = lane >> 5, l32 = lane & 31;
+    // H3: undo the operand scales (powers of two: exact); the pre-split B's per-row inverse scale
+    // is read for the tile's columns (rows past J carry 1)
+    const int pab = pa + pb;
+    float csc[2];
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++) csc[tj] = (H3 && BPRE) ? g.bscale[j0 + wn * 64 + tj * 32 + l32] : 1.f;
     if (i0 + BM <= g.I && j0 + BN <= g.J) {  // interior tile: no bounds checks, one base pointer
         float* cb = C + (int64_t)(i0 + wm * 64 + 4 * h) * g.ldc + j0 + wn * 64 + l32;
 #pragma unroll
@@ -515,8 +722,10 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
                 const float bj = g.bias ? g.bias[j0 + wn * 64 + tj * 32 + l32] : 0.f;
                 float* ct = cb + (int64_t)(ti * 32) * g.ldc + tj * 32;
 #pragma unroll
-                for (int r = 0; r < 16; r++)
-                    ct[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = (acc[ti][tj][r] + cor[ti][tj][r]) + bj;
+                for (int r = 0; r < 16; r++) {
+                    const float v = acc[ti][tj][r] + cor[ti][tj][r];
+                    ct[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = (H3 ? ldexpf(v * csc[tj], -pab) : v) + bj;
+                }
             }
         return;
     }
@@ -530,7 +739,8 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (i < g.I) C[(int64_t)i * g.ldc + j] = (acc[ti][tj][r] + cor[ti][tj][r]) + bj;
+                const float v = acc[ti][tj][r] + cor[ti][tj][r];
+                if (i < g.I) C[(int64_t)i * g.ldc + j] = (H3 ? ldexpf(v * csc[tj], -pab) : v) + bj;
             }
         }
 }
@@ -662,12 +872,22 @@ __global__ void weight_to_bf16(const float* w, int out, int in, uint16_t* h, int
 // out[e] (+)= sum_s part[s*stride + e], fixed order (deterministic split-K reduction)
 // Minibatch gather (ExperienceBuffer::_GetSamples index_select, ExperienceBuffer.cpp:140-163):
 // X[r, 0..C) = src[idx[start + r], 0..C), rows padded to ldx (16-byte aligned) with zeros.
-__global__ void gather_rows(const float* src, int C, const int32_t* idx, int64_t start, int n, float* X, int ldx) {
-    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= (int64_t)n * ldx) return;
-    int r = (int)(e / ldx), c = (int)(e % ldx);
-    int64_t s = idx ? (int64_t)idx[start + r] : start + r;
-    X[e] = c < C ? src[s * C + c] : 0.f;
+// amax (optional): 64 shards of max |X| for the H3 training GEMMs (h3_amax_commit).
+// Grid-stride (launch at most GATHER_BLOCKS blocks) so that the per-block max commits stay few.
+constexpr int GATHER_BLOCKS = 2048;
+__global__ void __launch_bounds__(256) gather_rows(const float* src, int C, const int32_t* idx, int64_t start, int n, float* X,
+                                                  int ldx, float* amax) {
+    uint32_t m = 0;
+    const int64_t total = (int64_t)n * ldx;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        int r = (int)(e / ldx), c = (int)(e % ldx);
+        int64_t s = idx ? (int64_t)idx[start + r] : start + r;
+        const float v = c < C ? src[s * C + c] : 0.f;
+        X[e] = v;
+        const uint32_t b = abs_bits(v);
+        m = b > m ? b : m;
+    }
+    if (amax) h3_amax_commit(amax, m);
 }
 
 __global__ void reduce_splits(const float* part, int splits, int64_t stride, int64_t n, float* out, int accumulate) {
@@ -712,15 +932,23 @@ DEV float wave_max(float v) {
 }
 
 
+// Column ownership of the wave-per-row kernels: with MAXH >= 4 columns per lane, lane l owns the
+// 4-column groups starting at 4 l + 256 q (q < MAXH / 4), so every 16-byte load / store instruction
+// of a wave covers one contiguous 1 KB span of the row (full 128-byte lines, no half-line writes);
+// MAXH < 4 (H <= 128): the contiguous columns [MAXH l, MAXH l + MAXH).
+template <int MAXH>
+DEV int lcol(int lane, int q) {
+    return MAXH >= 4 ? 4 * lane + 256 * (q >> 2) + (q & 3) : MAXH * lane + q;
+}
+
 // LayerNorm (eps 1e-5, biased variance) + LeakyReLU, training: one wave per row.
 // Keeps act [R,H] and the row statistics stats [R] = (mean, rstd) for the backward, which
 // recomputes xhat = (z - mean) * rstd from the untouched pre-norm input z with the same operations
 // (bit-identical to a stored xhat, one [R,H] write less per layer).
-// Lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (float4 loads / stores when H is a
-// multiple of 4); gamma / beta stay in registers.  Each wave walks LNF_ROWS/4 rows, lnf_rf<MAXH>()
-// of them at a time: their loads are issued together before the first reduction and their wave
-// reductions interleave, so a wave keeps that many rows of HBM traffic in flight (the per-row
-// arithmetic and its order are unchanged).
+// Columns per lane: lcol (float4 loads / stores when H is a multiple of 4); gamma / beta stay in
+// registers.  Each wave walks LNF_ROWS/4 rows, lnf_rf<MAXH>() of them at a time: their loads are
+// issued together before the first reduction and their wave reductions interleave, so a wave keeps
+// that many rows of HBM traffic in flight (the per-row arithmetic and its order are unchanged).
 constexpr int LNF_ROWS = 16;
 template <int MAXH>
 constexpr int lnf_rf() {
@@ -728,14 +956,14 @@ constexpr int lnf_rf() {
 }
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const float* gamma, const float* beta, int R, int H,
-                                                     float slope, int use_ln, float* act, float2* stats) {
+                                                     float slope, int use_ln, float* act, float2* stats, float* amax) {
+    uint32_t vmax = 0;  // max |act| of this thread's outputs (H3 operand scale, when amax is given)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c0 = lane * MAXH;
-    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
     float g[MAXH], b[MAXH];
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
-        const int c = c0 + q;
+        const int c = lcol<MAXH>(lane, q);
         g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
         b[q] = (use_ln && c < H) ? beta[c] : 0.f;
     }
@@ -746,16 +974,20 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
 #pragma unroll
         for (int r = 0; r < RF; r++) {  // all RF rows' loads first (a row past R reloads row R-1)
             row[r] = blockIdx.x * LNF_ROWS + (i0 + r) * 4 + wv;
-            const float* z = Z + (int64_t)min(row[r], R - 1) * H + c0;
+            const float* z = Z + (int64_t)min(row[r], R - 1) * H;
             if (vec) {
 #pragma unroll
                 for (int q = 0; q < MAXH; q += 4) {
-                    float4 t = *reinterpret_cast<const float4*>(z + q);
+                    const int c = lcol<MAXH>(lane, q);
+                    float4 t = c < H ? *reinterpret_cast<const float4*>(z + c) : make_float4(0.f, 0.f, 0.f, 0.f);
                     v[r][q] = t.x; v[r][q + 1] = t.y; v[r][q + 2] = t.z; v[r][q + 3] = t.w;
                 }
             } else {
 #pragma unroll
-                for (int q = 0; q < MAXH; q++) v[r][q] = c0 + q < H ? z[q] : 0.f;
+                for (int q = 0; q < MAXH; q++) {
+                    const int c = lcol<MAXH>(lane, q);
+                    v[r][q] = c < H ? z[c] : 0.f;
+                }
             }
         }
         float mean[RF], rs[RF];
@@ -777,7 +1009,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
                 float s2 = 0.f;
 #pragma unroll
                 for (int q = 0; q < MAXH; q++) {
-                    float d = c0 + q < H ? v[r][q] - mean[r] : 0.f;
+                    float d = lcol<MAXH>(lane, q) < H ? v[r][q] - mean[r] : 0.f;
                     s2 += d * d;
                 }
                 rs[r] = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
@@ -793,46 +1025,62 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
                 const float hv = use_ln ? xh * g[q] + b[q] : xh;
                 a[q] = hv > 0.f ? hv : hv * slope;
             }
-            float* ao = act + (int64_t)row[r] * H + c0;
+            float* ao = act + (int64_t)row[r] * H;
             if (vec) {
 #pragma unroll
-                for (int q = 0; q < MAXH; q += 4)
-                    *reinterpret_cast<float4*>(ao + q) = make_float4(a[q], a[q + 1], a[q + 2], a[q + 3]);
+                for (int q = 0; q < MAXH; q += 4) {
+                    const int c = lcol<MAXH>(lane, q);
+                    if (c < H) *reinterpret_cast<float4*>(ao + c) = make_float4(a[q], a[q + 1], a[q + 2], a[q + 3]);
+                }
             } else {
 #pragma unroll
-                for (int q = 0; q < MAXH; q++)
-                    if (c0 + q < H) ao[q] = a[q];
+                for (int q = 0; q < MAXH; q++) {
+                    const int c = lcol<MAXH>(lane, q);
+                    if (c < H) ao[c] = a[q];
+                }
             }
             if (lane == 0) stats[row[r]] = make_float2(mean[r], rs[r]);
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) {
+                const uint32_t b = lcol<MAXH>(lane, q) < H ? abs_bits(a[q]) : 0u;
+                vmax = b > vmax ? b : vmax;
+            }
         }
     }
+    if (amax) h3_amax_commit(amax, vmax);
 }
 
 // bf16 inference variant: Z bf16 in, bf16(LeakyReLU(bf16(LN(Z)))) out (torch bf16 module chain).
+// With MAXH >= 8 columns per lane, lane l owns the 8-column groups at 8 l + 512 q (each 16-byte
+// load / store instruction of a wave covers one contiguous 1 KB span); gamma / beta in registers;
+// each wave walks LNF_ROWS/4 rows.
+template <int MAXH>
+DEV int hcol(int lane, int q) {
+    return MAXH >= 8 ? 8 * lane + 512 * (q >> 3) + (q & 7) : MAXH * lane + q;
+}
 template <int MAXH, bool F16>
 __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const uint16_t* gamma, const uint16_t* beta, int R,
                                                       int H, float slope, int use_ln, uint16_t* out) {
-    // lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (16-byte loads / stores of 8 bf16
-    // when H is a multiple of 8); gamma / beta in registers; each wave walks LNF_ROWS/4 rows
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c0 = lane * MAXH;
-    const bool vec = (H % 8 == 0) && (MAXH % 8 == 0) && (c0 + MAXH <= H);
+    const bool vec = (H % 8 == 0) && (MAXH % 8 == 0);
     float g[MAXH], b[MAXH];
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
-        const int c = c0 + q;
+        const int c = hcol<MAXH>(lane, q);
         g[q] = (use_ln && c < H) ? h2f<F16>(gamma[c]) : 1.f;
         b[q] = (use_ln && c < H) ? h2f<F16>(beta[c]) : 0.f;
     }
     for (int i = 0; i < LNF_ROWS / 4; i++) {
         const int row = blockIdx.x * LNF_ROWS + i * 4 + wv;
         if (row >= R) break;
-        const uint16_t* z = Z + (int64_t)row * H + c0;
+        const uint16_t* z = Z + (int64_t)row * H;
         float v[MAXH];
         if (vec) {
 #pragma unroll
             for (int q = 0; q < MAXH; q += 8) {
-                u32x4 t = *reinterpret_cast<const u32x4*>(z + q);
+                const int c = hcol<MAXH>(lane, q);
+                u32x4 t = {0u, 0u, 0u, 0u};
+                if (c < H) t = *reinterpret_cast<const u32x4*>(z + c);
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     v[q + 2 * k] = h2f<F16>((uint16_t)(t[k] & 0xffffu));
@@ -841,7 +1089,10 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) v[q] = c0 + q < H ? h2f<F16>(z[q]) : 0.f;
+            for (int q = 0; q < MAXH; q++) {
+                const int c = hcol<MAXH>(lane, q);
+                v[q] = c < H ? h2f<F16>(z[c]) : 0.f;
+            }
         }
         float mean = 0.f, rs = 1.f;
         if (use_ln) {
@@ -852,7 +1103,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
             float s2 = 0.f;
 #pragma unroll
             for (int q = 0; q < MAXH; q++) {
-                float d = c0 + q < H ? v[q] - mean : 0.f;
+                float d = hcol<MAXH>(lane, q) < H ? v[q] - mean : 0.f;
                 s2 += d * d;
             }
             rs = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
@@ -863,19 +1114,22 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
             float hv = use_ln ? h2f<F16>(f2h<F16>((v[q] - mean) * rs * g[q] + b[q])) : v[q];
             o[q] = f2h<F16>(hv > 0.f ? hv : hv * slope);
         }
-        uint16_t* op = out + (int64_t)row * H + c0;
+        uint16_t* op = out + (int64_t)row * H;
         if (vec) {
 #pragma unroll
             for (int q = 0; q < MAXH; q += 8) {
+                const int c = hcol<MAXH>(lane, q);
                 u32x4 t;
 #pragma unroll
                 for (int k = 0; k < 4; k++) t[k] = (uint32_t)o[q + 2 * k] | ((uint32_t)o[q + 2 * k + 1] << 16);
-                *reinterpret_cast<u32x4*>(op + q) = t;
+                if (c < H) *reinterpret_cast<u32x4*>(op + c) = t;
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++)
-                if (c0 + q < H) op[q] = o[q];
+            for (int q = 0; q < MAXH; q++) {
+                const int c = hcol<MAXH>(lane, q);
+                if (c < H) op[c] = o[q];
+            }
         }
     }
 }
@@ -883,21 +1137,21 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 // Backward of LeakyReLU(LN(Z)): dZ from dA; per-block column partials of
 // dbias = sum dZ, dgamma = sum dH*xhat, dbeta = sum dH -> part[blk][3][H] (the flat parameter
 // order Linear.bias, LayerNorm.weight, LayerNorm.bias, so one reduction serves all three).
-// Lane l owns the contiguous columns [MAXH*l, MAXH*l + MAXH) (float4 loads); gamma / beta stay
-// in registers; each of the 4 waves walks LNB_ROWS/4 rows.
+// Columns per lane: lcol (float4 loads / stores); gamma / beta stay in registers; each of the 4
+// waves walks LNB_ROWS/4 rows.
 constexpr int LNB_ROWS = 32;
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* Z, const float2* stats, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
-                                                 float* part) {
+                                                 float* part, float* amax) {
     __shared__ float red[4][3][64 * MAXH];
+    uint32_t vmax = 0;  // max |dZ| of this thread's outputs (H3 operand scale, when amax is given)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c0 = lane * MAXH;
-    const bool vec = (H % 4 == 0) && (c0 + MAXH <= H);
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
     float g[MAXH], b[MAXH], pg[MAXH], pb[MAXH], pz[MAXH];
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
-        int c = c0 + q;
+        int c = lcol<MAXH>(lane, q);
         g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
         b[q] = (use_ln && c < H) ? beta[c] : 0.f;
         pg[q] = pb[q] = pz[q] = 0.f;
@@ -906,24 +1160,27 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
     for (int rr = w; rr < LNB_ROWS; rr += 4) {
         const int row = r0 + rr;
         if (row >= R) break;
-        const float* da = dA + (int64_t)row * H + c0;
-        const float* xh = Z + (int64_t)row * H + c0;  // pre-norm z; xhat recomputed below
+        const float* da = dA + (int64_t)row * H;
+        const float* xh = Z + (int64_t)row * H;  // pre-norm z; xhat recomputed below
         const float2 st = stats[row];
         float dh[MAXH], x[MAXH], av[MAXH];
         if (vec) {
 #pragma unroll
             for (int q = 0; q < MAXH; q += 4) {
-                float4 t = *reinterpret_cast<const float4*>(xh + q);
-                float4 u = *reinterpret_cast<const float4*>(da + q);
+                const int c = lcol<MAXH>(lane, q);
+                const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 t = c < H ? *reinterpret_cast<const float4*>(xh + c) : zero;
+                float4 u = c < H ? *reinterpret_cast<const float4*>(da + c) : zero;
                 x[q] = t.x; x[q + 1] = t.y; x[q + 2] = t.z; x[q + 3] = t.w;
                 av[q] = u.x; av[q + 1] = u.y; av[q + 2] = u.z; av[q + 3] = u.w;
             }
         } else {
 #pragma unroll
             for (int q = 0; q < MAXH; q++) {
-                bool in = c0 + q < H;
-                x[q] = in ? xh[q] : 0.f;
-                av[q] = in ? da[q] : 0.f;
+                const int c = lcol<MAXH>(lane, q);
+                bool in = c < H;
+                x[q] = in ? xh[c] : 0.f;
+                av[q] = in ? da[c] : 0.f;
             }
         }
         if (use_ln) {
@@ -939,7 +1196,7 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
             s1 += gg;
             s2 += gg * x[q];
         }
-        float* dz = dZ + (int64_t)row * H + c0;
+        float* dz = dZ + (int64_t)row * H;
         float d[MAXH];
         if (use_ln) {
             float m1 = wave_sum(s1) / (float)H, m2 = wave_sum(s2) / (float)H;
@@ -952,32 +1209,40 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         }
         if (vec) {
 #pragma unroll
-            for (int q = 0; q < MAXH; q += 4)
-                *reinterpret_cast<float4*>(dz + q) = make_float4(d[q], d[q + 1], d[q + 2], d[q + 3]);
+            for (int q = 0; q < MAXH; q += 4) {
+                const int c = lcol<MAXH>(lane, q);
+                if (c < H) *reinterpret_cast<float4*>(dz + c) = make_float4(d[q], d[q + 1], d[q + 2], d[q + 3]);
+            }
         } else {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++)
-                if (c0 + q < H) dz[q] = d[q];
+            for (int q = 0; q < MAXH; q++) {
+                const int c = lcol<MAXH>(lane, q);
+                if (c < H) dz[c] = d[q];
+            }
         }
 #pragma unroll
         for (int q = 0; q < MAXH; q++) {
-            bool in = c0 + q < H;
+            bool in = lcol<MAXH>(lane, q) < H;
             pz[q] += in ? d[q] : 0.f;
             pg[q] += in ? dh[q] * x[q] : 0.f;
             pb[q] += in ? dh[q] : 0.f;
+            const uint32_t bb = in ? abs_bits(d[q]) : 0u;
+            vmax = bb > vmax ? bb : vmax;
         }
     }
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
-        red[w][0][c0 + q] = pz[q];
-        red[w][1][c0 + q] = pg[q];
-        red[w][2][c0 + q] = pb[q];
+        const int c = lcol<MAXH>(lane, q);
+        red[w][0][c] = pz[q];
+        red[w][1][c] = pg[q];
+        red[w][2][c] = pb[q];
     }
     __syncthreads();
     float* out = part + (int64_t)blockIdx.x * 3 * H;
     for (int k = 0; k < 3; k++)
         for (int c = threadIdx.x; c < H; c += 256)
             out[k * H + c] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    if (amax) h3_amax_commit(amax, vmax);
 }
 
 // NPER (columns per lane) dispatch: H <= 64 * NPER
@@ -1003,34 +1268,40 @@ inline decltype(&ln_act_fwd_bf16<16, F16>) ln_act_fwd_bf16_any(int H) {
 RLGPU_NPER_DISPATCH(ln_act_bwd)
 
 // Rank-1 output layer (the critic's Linear(H, 1)): GEMM tiles would be 1/128 occupied, so the
-// head runs as wave-per-row dot products.  Lane l owns the contiguous columns
-// [MAXH*l, MAXH*l + MAXH) (float4 loads when H is a multiple of 4); w stays in registers and each
-// wave walks H1_ROWS/4 rows.
+// head runs as wave-per-row dot products.  Columns per lane: lcol (float4 loads when H is a
+// multiple of 4); w stays in registers and each wave walks H1_ROWS/4 rows.
 constexpr int H1_ROWS = 16;
 template <int MAXH>
 __global__ void __launch_bounds__(256) head1_fwd(const float* X, const float* w, const float* b, int R, int H, float* out) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c0 = lane * MAXH;
-    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
     float wr[MAXH];
 #pragma unroll
-    for (int q = 0; q < MAXH; q++) wr[q] = c0 + q < H ? w[c0 + q] : 0.f;
+    for (int q = 0; q < MAXH; q++) {
+        const int c = lcol<MAXH>(lane, q);
+        wr[q] = c < H ? w[c] : 0.f;
+    }
     const float bias = b[0];
     for (int i = 0; i < H1_ROWS / 4; i++) {
         const int row = blockIdx.x * H1_ROWS + i * 4 + wv;
         if (row >= R) break;
-        const float* x = X + (int64_t)row * H + c0;
+        const float* x = X + (int64_t)row * H;
         float s = 0.f;
         if (vec) {
 #pragma unroll
             for (int q = 0; q < MAXH; q += 4) {
-                float4 t = *reinterpret_cast<const float4*>(x + q);
-                s += t.x * wr[q] + t.y * wr[q + 1] + t.z * wr[q + 2] + t.w * wr[q + 3];
+                const int c = lcol<MAXH>(lane, q);
+                if (c < H) {
+                    float4 t = *reinterpret_cast<const float4*>(x + c);
+                    s += t.x * wr[q] + t.y * wr[q + 1] + t.z * wr[q + 2] + t.w * wr[q + 3];
+                }
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < MAXH; q++)
-                if (c0 + q < H) s += x[q] * wr[q];
+            for (int q = 0; q < MAXH; q++) {
+                const int c = lcol<MAXH>(lane, q);
+                if (c < H) s += x[c] * wr[q];
+            }
         }
         s = wave_sum(s);
         if (lane == 0) out[row] = s + bias;
@@ -1044,13 +1315,13 @@ __global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w,
                                                 float* part) {
     __shared__ float red[4][64 * MAXH + 1];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c0 = lane * MAXH;
-    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0) && (c0 + MAXH <= H);
+    const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
     float wr[MAXH], acc[MAXH];
     float accb = 0.f;
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
-        wr[q] = c0 + q < H ? w[c0 + q] : 0.f;
+        const int c = lcol<MAXH>(lane, q);
+        wr[q] = c < H ? w[c] : 0.f;
         acc[q] = 0.f;
     }
     const int r0 = blockIdx.x * LNB_ROWS;
@@ -1058,31 +1329,35 @@ __global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w,
         const int row = r0 + rr;
         if (row >= R) break;
         const float d = dv[row];
-        const float* x = X + (int64_t)row * H + c0;
-        float* da = dA + (int64_t)row * H + c0;
+        const float* x = X + (int64_t)row * H;
+        float* da = dA + (int64_t)row * H;
         if (vec) {
 #pragma unroll
             for (int q = 0; q < MAXH; q += 4) {
-                float4 t = *reinterpret_cast<const float4*>(x + q);
-                *reinterpret_cast<float4*>(da + q) = make_float4(d * wr[q], d * wr[q + 1], d * wr[q + 2], d * wr[q + 3]);
-                acc[q] += d * t.x;
-                acc[q + 1] += d * t.y;
-                acc[q + 2] += d * t.z;
-                acc[q + 3] += d * t.w;
+                const int c = lcol<MAXH>(lane, q);
+                if (c < H) {
+                    float4 t = *reinterpret_cast<const float4*>(x + c);
+                    *reinterpret_cast<float4*>(da + c) = make_float4(d * wr[q], d * wr[q + 1], d * wr[q + 2], d * wr[q + 3]);
+                    acc[q] += d * t.x;
+                    acc[q + 1] += d * t.y;
+                    acc[q + 2] += d * t.z;
+                    acc[q + 3] += d * t.w;
+                }
             }
         } else {
 #pragma unroll
             for (int q = 0; q < MAXH; q++) {
-                if (c0 + q < H) {
-                    da[q] = d * wr[q];
-                    acc[q] += d * x[q];
+                const int c = lcol<MAXH>(lane, q);
+                if (c < H) {
+                    da[c] = d * wr[q];
+                    acc[q] += d * x[c];
                 }
             }
         }
         accb += d;
     }
 #pragma unroll
-    for (int q = 0; q < MAXH; q++) red[wv][c0 + q] = acc[q];
+    for (int q = 0; q < MAXH; q++) red[wv][lcol<MAXH>(lane, q)] = acc[q];
     if (lane == 0) red[wv][64 * MAXH] = accb;
     __syncthreads();
     float* out = part + (int64_t)blockIdx.x * (H + 1);

@@ -31,6 +31,7 @@ struct Layer {
     // forward B = W [out_pad128][in_pad32], backward dA B = W^T [in_pad128][out_pad32]; -1 = none
     int64_t sf = -1, sb = -1;
     int sf_rows = 0, sf_ld = 0, sb_rows = 0, sb_ld = 0;
+    int64_t sfs = -1, sbs = -1;  // H3: per-row inverse scales of the planes (offsets into Model::wscale)
 };
 
 struct Model {
@@ -42,9 +43,16 @@ struct Model {
     // fp32 training workspace (per model, so the two models' passes can overlap on two streams)
     std::vector<float*> xhat, act, rstd;
     float *y = nullptr, *dy = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr, *mid = nullptr;  // y: model output
-    uint16_t* wsplit = nullptr;  // split weight planes (x6 mode)
+    uint16_t* wsplit = nullptr;  // split weight planes (x6 / H3 modes)
     int64_t nsplit = 0;
+    float* wscale = nullptr;     // H3: per-row inverse scales of the weight planes
+    int64_t nscale = 0;
+    // H3: 64-shard max |x| slots of the GEMM operand tensors (kAmaxSlots x 64 floats):
+    // act[l] at slot l, dZ of layer l at kAmaxDZ + l, the loss gradient dout at kAmaxOut
+    float* amax = nullptr;
 };
+constexpr int kAmaxDZ = RLGPU_MAX_LAYERS, kAmaxOut = 2 * RLGPU_MAX_LAYERS, kAmaxSlots = 2 * RLGPU_MAX_LAYERS + 1;
+inline bool split_mode(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
 
 constexpr int kMaxSplits = 256;
 // concurrent gemm_f32 workgroups on the device (CUs x RLGPU_GEMM_OCC), set at create: the split-K
@@ -59,10 +67,24 @@ inline int x6_variant() {
     }();
     return v;
 }
+// H3 pipeline shape: RLGPU_H3_VARIANT=0..3 (experiments), default 0 (32-deep stages, 2 WGs / CU:
+// measured 144.6 ms learn per C2 iteration against 153.1 ms for the 64-deep variant 3)
+inline int h3_variant() {
+    static const int v = [] {
+        const char* e = getenv("RLGPU_H3_VARIANT");
+        int x = e ? atoi(e) : 0;
+        return (x >= 0 && x <= 6) ? x : 0;
+    }();
+    return v;
+}
 inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
-inline int gemm_slots(int mode) { return g_cus * (mode == RLGPU_GEMM_F32X6 ? x6_occ() : RLGPU_GEMM_OCC); }
+inline bool split_mode_(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
+inline int gemm_slots(int mode) {
+    if (mode == RLGPU_GEMM_F16X3) return g_cus * ((h3_variant() == 0 || h3_variant() >= 3) ? 2 : 1);
+    return g_cus * (split_mode_(mode) ? x6_occ() : RLGPU_GEMM_OCC);
+}
 // K granularity of a split-K chunk: a whole number of stages of either kernel
-inline int kgran(int mode) { return mode == RLGPU_GEMM_F32X6 ? mlp::XKMAX : mlp::BK; }
+inline int kgran(int mode) { return split_mode_(mode) ? mlp::XKMAX : mlp::BK; }
 
 }  // namespace
 
@@ -81,6 +103,9 @@ struct rlgpu_ppo {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     float* x0 = nullptr;       // gathered minibatch obs, rows padded to x_ld floats
     int x_ld = 0;
+    float* x_amax = nullptr;   // H3: 64-shard max |x0| (with both models' slots: one memset per pass)
+    float* amax_all = nullptr;
+    int64_t amax_count = 0;
     uint16_t* xh = nullptr;    // bf16 obs for inference, rows padded to xh_ld
     int xh_ld = 0;
     uint16_t *zh = nullptr, *ah[2] = {nullptr, nullptr}, *logits_h = nullptr;
@@ -99,26 +124,49 @@ namespace {
 
 // C[I,J] (+ bias) = A . B with the layouts of mlp::gemm_f32.  *_tail_ok: the operand's rows are
 // zero-padded up to a multiple of 4 past the bound (so float4 loads may straddle it).
-template <int LA, int LB, bool AV, bool BV, bool PRE>
+template <int LA, int LB, bool AV, bool BV, bool PRE, bool H3>
 void x6_launch_v(dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
-    switch (x6_variant()) {
-        case 1: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 1>), grid, blk, 0, s, g); break;
-        case 2: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 2>), grid, blk, 0, s, g); break;
-        default: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 0>), grid, blk, 0, s, g); break;
+    switch (H3 ? h3_variant() : x6_variant()) {
+        case 3: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 3, H3>), grid, blk, 0, s, g); break;
+        case 4:
+            if (H3) {  // two-plane LDS only: 2 x 80 KB per CU
+                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 4, true>), grid, blk, 0, s, g);
+                break;
+            }
+            [[fallthrough]];
+        case 5:
+            if (H3) {
+                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 5, true>), grid, blk, 0, s, g);
+                break;
+            }
+            [[fallthrough]];
+        case 6:
+            if (H3) {
+                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 6, true>), grid, blk, 0, s, g);
+                break;
+            }
+            [[fallthrough]];
+        case 1: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 1, H3>), grid, blk, 0, s, g); break;
+        case 2: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 2, H3>), grid, blk, 0, s, g); break;
+        default: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 0, H3>), grid, blk, 0, s, g); break;
     }
 }
-template <int LA, int LB>
+template <int LA, int LB, bool H3>
 void x6_launch(bool av, bool bv, dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
-    if (av && bv) x6_launch_v<LA, LB, true, true, false>(grid, blk, s, g);
-    else if (av) x6_launch_v<LA, LB, true, false, false>(grid, blk, s, g);
-    else if (bv) x6_launch_v<LA, LB, false, true, false>(grid, blk, s, g);
-    else x6_launch_v<LA, LB, false, false, false>(grid, blk, s, g);
+    if (av && bv) x6_launch_v<LA, LB, true, true, false, H3>(grid, blk, s, g);
+    else if (av) x6_launch_v<LA, LB, true, false, false, H3>(grid, blk, s, g);
+    else if (bv) x6_launch_v<LA, LB, false, true, false, H3>(grid, blk, s, g);
+    else x6_launch_v<LA, LB, false, false, false, H3>(grid, blk, s, g);
 }
 
+// amax_a / amax_b: the operands' 64-shard max |x| (RLGPU_GEMM_F16X3 only)
 void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
               const float* bias, int I, int J, int K, int splits, hipStream_t s, bool a_tail_ok = false,
-              bool b_tail_ok = false) {
-    mlp::GemmArgs g;
+              bool b_tail_ok = false, const float* amax_a = nullptr, const float* amax_b = nullptr) {
+    mlp::GemmArgs g{};
+    g.amax_a = amax_a;
+    g.amax_b = amax_b;
+    if (mode == RLGPU_GEMM_F16X3 && !(amax_a && amax_b)) throw rlgpu::Error(RLGPU_ERR_STATE, "H3 GEMM without operand scales");
     g.A = A;
     g.B = B;
     g.C = C;
@@ -145,7 +193,9 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
 #define RLGPU_GEMM_CASE(LA, LB)                                                                                  \
     if (la == LA && lb == LB) {                                                                                  \
         if (mode == RLGPU_GEMM_F32X6) {                                                                          \
-            x6_launch<LA, LB>(av, bv, grid, blk, s, g);                                                          \
+            x6_launch<LA, LB, false>(av, bv, grid, blk, s, g);                                                   \
+        } else if (mode == RLGPU_GEMM_F16X3) {                                                                   \
+            x6_launch<LA, LB, true>(av, bv, grid, blk, s, g);                                                    \
         } else {                                                                                                 \
             if (av && bv) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, true>), grid, blk, 0, s, g);           \
             else if (av) hipLaunchKernelGGL((mlp::gemm_f32<LA, LB, true, false>), grid, blk, 0, s, g);          \
@@ -163,9 +213,15 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
 }
 
 // C[I,J] (+ bias) = A . B on the x6 GEMM with B given as pre-split planes (Layer::sf / sb layout)
+// H3 (bscale given): fp16 planes with per-row inverse scales bscale, A scaled by amax_a's shards
 void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int64_t bplane, float* C, int64_t ldc,
-                 const float* bias, int I, int J, int K, hipStream_t s, bool a_tail_ok = false) {
-    mlp::GemmArgs g;
+                 const float* bias, int I, int J, int K, hipStream_t s, bool a_tail_ok = false,
+                 const float* amax_a = nullptr, const float* bscale = nullptr) {
+    mlp::GemmArgs g{};
+    g.amax_a = amax_a;
+    g.bscale = bscale;
+    const bool h3 = bscale != nullptr;
+    if (h3 && !amax_a) throw rlgpu::Error(RLGPU_ERR_STATE, "H3 GEMM without operand scales");
     g.A = A;
     g.B = reinterpret_cast<const float*>(Bp);
     g.C = C;
@@ -184,17 +240,36 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
     g.gz = 1;
     const bool av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && (K % 4 == 0 || a_tail_ok);
     dim3 grid(g.gx * g.gy), blk(256);
-    if (av)
-        x6_launch_v<mlp::A_IK, mlp::B_JK, true, true, true>(grid, blk, s, g);
-    else
-        x6_launch_v<mlp::A_IK, mlp::B_JK, false, true, true>(grid, blk, s, g);
+    if (h3) {
+        if (av)
+            x6_launch_v<mlp::A_IK, mlp::B_JK, true, true, true, true>(grid, blk, s, g);
+        else
+            x6_launch_v<mlp::A_IK, mlp::B_JK, false, true, true, true>(grid, blk, s, g);
+    } else {
+        if (av)
+            x6_launch_v<mlp::A_IK, mlp::B_JK, true, true, true, false>(grid, blk, s, g);
+        else
+            x6_launch_v<mlp::A_IK, mlp::B_JK, false, true, true, false>(grid, blk, s, g);
+    }
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
 // refresh the split weight planes of model m from the current parameters (once per minibatch /
 // training forward: the weights change only at the optimizer step, but may be written directly)
 void split_weights(const float* P, Model& m, hipStream_t s) {
-    if (m.mode != RLGPU_GEMM_F32X6) return;
+    if (!split_mode(m.mode)) return;
+    if (m.mode == RLGPU_GEMM_F16X3) {
+        for (auto& L : m.L) {
+            if (L.sf >= 0)
+                hipLaunchKernelGGL(mlp::split_weight_h3, dim3(L.sf_rows), dim3(256), 0, s, P + L.w, L.out, L.in, (int64_t)L.in, 0, L.sf_ld,
+                                   m.wsplit + L.sf, (int64_t)L.sf_rows * L.sf_ld, m.wscale + L.sfs);
+            if (L.sb >= 0)
+                hipLaunchKernelGGL(mlp::split_weight_h3, dim3(L.sb_rows), dim3(256), 0, s, P + L.w, L.out, L.in, (int64_t)L.in, 1, L.sb_ld,
+                                   m.wsplit + L.sb, (int64_t)L.sb_rows * L.sb_ld, m.wscale + L.sbs);
+        }
+        RLGPU_CHECK_HIP(hipGetLastError());
+        return;
+    }
     for (auto& L : m.L) {
         if (L.sf >= 0) {
             int64_t e = (int64_t)L.sf_rows * L.sf_ld;
@@ -223,11 +298,12 @@ int splits_for(int mode, int rows, int out, int in) {
 
 // dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
 void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
-                 bool x_tail_ok = false) {
+                 bool x_tail_ok = false, const float* amax_dz = nullptr, const float* amax_x = nullptr) {
     int splits = splits_for(m.mode, n, out, in);
     int chunk = (int)ceil_div(ceil_div(n, splits), kgran(m.mode)) * kgran(m.mode);
     int z = (int)ceil_div(n, chunk);
-    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok);
+    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok,
+             amax_dz, amax_x);
     int64_t e = (int64_t)out * in;
     if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)m.wpart & 15) == 0)
         hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
@@ -259,6 +335,13 @@ void colsum_into(Model& m, const float* X, int n, int C, float* g, hipStream_t s
     reduce_partials(m, m.cpart, nb, C, C, g, s);
 }
 
+// H3 operand scale slots (null in the other modes): slot k of model m, and the gathered obs
+inline float* amax_slot(Model& m, int k) { return m.mode == RLGPU_GEMM_F16X3 ? m.amax + (int64_t)k * 64 : nullptr; }
+inline float* amax_x(rlgpu_ppo* h, const Model& m) { return m.mode == RLGPU_GEMM_F16X3 ? h->x_amax : nullptr; }
+inline const float* wscale_at(const Model& m, int64_t off) {
+    return m.mode == RLGPU_GEMM_F16X3 ? m.wscale + off : nullptr;
+}
+
 // fp32 training forward; keeps activations; writes the output layer to `out`.  X is the
 // gathered, zero-padded minibatch copy (row stride h->x_ld).
 void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipStream_t s) {
@@ -267,22 +350,25 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
     split_weights(P, m, s);
     int nh = (int)m.L.size() - 1;
     const float* in = X;
+    const float* in_amax = amax_x(h, m);
     int64_t ld = h->x_ld;
     bool tail_ok = true;
     for (int l = 0; l < nh; l++) {
         const Layer& L = m.L[l];
         if (L.sf >= 0)
             gemm_x6_pre(in, ld, m.wsplit + L.sf, L.sf_ld, (int64_t)L.sf_rows * L.sf_ld, m.xhat[l], L.out, P + L.b, n, L.out,
-                        L.in, s, tail_ok);
+                        L.in, s, tail_ok, in_amax, wscale_at(m, L.sfs));
         else
             gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s,
                      tail_ok);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
-                           h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]));
+                           h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
+                           amax_slot(m, l));
         RLGPU_CHECK_HIP(hipGetLastError());
         in = m.act[l];
+        in_amax = amax_slot(m, l);
         ld = L.out;
         tail_ok = false;
     }
@@ -294,14 +380,15 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
         return;
     }
     if (O.sf >= 0)
-        gemm_x6_pre(in, ld, m.wsplit + O.sf, O.sf_ld, (int64_t)O.sf_rows * O.sf_ld, out, O.out, P + O.b, n, O.out, O.in, s);
+        gemm_x6_pre(in, ld, m.wsplit + O.sf, O.sf_ld, (int64_t)O.sf_rows * O.sf_ld, out, O.out, P + O.b, n, O.out, O.in, s,
+                    false, in_amax, wscale_at(m, O.sfs));
     else
         gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + O.w, O.in, out, O.out, P + O.b, n, O.out, O.in, 1, s);
 }
 
 // backward from dout [n, out] into the grad buffer (accumulating).  dout_part: optional per-block
 // column partials of dout (dout_nblk rows of `out` floats, written by the loss kernel) for the
-// output bias, instead of a separate column-sum pass.
+// output bias, instead of a separate column-sum pass.  H3: dout's max |x| is in slot kAmaxOut.
 void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hipStream_t s,
               const float* dout_part = nullptr, int dout_nblk = 0) {
     Model& m = h->M[mi];
@@ -316,7 +403,10 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         RLGPU_CHECK_HIP(hipGetLastError());
         reduce_partials(m, m.cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
     } else {
-        weight_grad(m, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s);
+        if (m.mode == RLGPU_GEMM_F16X3 && !dout_part)
+            throw rlgpu::Error(RLGPU_ERR_STATE, "H3 backward: the loss kernel must provide dout's scale");
+        weight_grad(m, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s, false, amax_slot(m, kAmaxOut),
+                    amax_slot(m, nh - 1));
         if (dout_part)
             reduce_partials(m, dout_part, dout_nblk, O.out, O.out, G + O.b, s);
         else
@@ -324,7 +414,7 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         // dA = dout . W_out
         if (O.sb >= 0)
             gemm_x6_pre(dout, O.out, m.wsplit + O.sb, O.sb_ld, (int64_t)O.sb_rows * O.sb_ld, m.dA, O.in, nullptr, n, O.in,
-                        O.out, s);
+                        O.out, s, false, amax_slot(m, kAmaxOut), wscale_at(m, O.sbs));
         else
             gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s);
     }
@@ -334,19 +424,20 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, m.dA, m.xhat[l], reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out,
-                           h->cfg.leaky_slope, h->cfg.layer_norm, m.dZ, m.cpart);
+                           h->cfg.leaky_slope, h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l));
         RLGPU_CHECK_HIP(hipGetLastError());
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
         reduce_partials(m, m.cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (l == 0)
-            weight_grad(m, m.dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true);
+            weight_grad(m, m.dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true, amax_slot(m, kAmaxDZ + l), amax_x(h, m));
         else
-            weight_grad(m, m.dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s);
+            weight_grad(m, m.dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s, false, amax_slot(m, kAmaxDZ + l),
+                        amax_slot(m, l - 1));
         if (l > 0 && L.sb >= 0)
             gemm_x6_pre(m.dZ, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, m.dA, L.in, nullptr, n, L.in,
-                        L.out, s);
+                        L.out, s, false, amax_slot(m, kAmaxDZ + l), wscale_at(m, L.sbs));
         else if (l > 0)
             gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, m.dA, L.in, nullptr, n, L.in, L.out, 1, s);
     }
@@ -354,8 +445,10 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
 
 void gather_obs(rlgpu_ppo* h, const float* obs, const int32_t* idx, int64_t start, int n, hipStream_t s) {
     int64_t e = (int64_t)n * h->x_ld;
-    hipLaunchKernelGGL(mlp::gather_rows, dim3(ceil_div(e, 256)), dim3(256), 0, s, obs, h->cfg.obs_size, idx, start, n, h->x0,
-                       h->x_ld);
+    // H3: clear every operand-scale slot of this pass, then the gather fills the obs slot
+    if (h->amax_all) RLGPU_CHECK_HIP(hipMemsetAsync(h->amax_all, 0, h->amax_count * sizeof(float), s));
+    hipLaunchKernelGGL(mlp::gather_rows, dim3(std::min<int64_t>(ceil_div(e, 256), mlp::GATHER_BLOCKS)), dim3(256), 0, s, obs,
+                       h->cfg.obs_size, idx, start, n, h->x0, h->x_ld, h->x_amax);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -439,16 +532,21 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
         }
         if (L.out > h->hmax) h->hmax = L.out;
         if (L.in > h->hmax && l > 0) h->hmax = L.in;
-        if (m.mode == RLGPU_GEMM_F32X6 && L.out > 1) {  // the rank-1 critic head has no GEMM
+        if (split_mode(m.mode) && L.out > 1) {  // the rank-1 critic head has no GEMM
+            const int np = m.mode == RLGPU_GEMM_F16X3 ? 2 : 3;  // planes per split weight
             L.sf_rows = (int)ceil_div(L.out, mlp::BN) * mlp::BN;
             L.sf_ld = (int)ceil_div(L.in, mlp::XKMAX) * mlp::XKMAX;
             L.sf = m.nsplit;
-            m.nsplit += 3 * (int64_t)L.sf_rows * L.sf_ld;
+            m.nsplit += np * (int64_t)L.sf_rows * L.sf_ld;
+            L.sfs = m.nscale;
+            m.nscale += L.sf_rows;
             if (l > 0) {  // dA of the first layer is never needed
                 L.sb_rows = (int)ceil_div(L.in, mlp::BN) * mlp::BN;
                 L.sb_ld = (int)ceil_div(L.out, mlp::XKMAX) * mlp::XKMAX;
                 L.sb = m.nsplit;
-                m.nsplit += 3 * (int64_t)L.sb_rows * L.sb_ld;
+                m.nsplit += np * (int64_t)L.sb_rows * L.sb_ld;
+                L.sbs = m.nscale;
+                m.nscale += L.sb_rows;
             }
         }
         m.L.push_back(L);
@@ -541,7 +639,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                     // splits_for is non-decreasing in the row count, and z = ceil(n / chunk) <= splits
                     wpart_max = std::max<int64_t>(wpart_max, (int64_t)splits_for(m.mode, (int)R, L.out, L.in) * L.in * L.out);
                 }
-            int64_t nb = ceil_div(R, std::min(mlp::LNB_ROWS, mlp::CS_ROWS));
+            int64_t nb = ceil_div(R, std::min(std::min(mlp::LNB_ROWS, mlp::CS_ROWS), ppo::PL_ROWS));
             for (auto& m : h->M) {
                 m.y = h->alloc<float>(R * omax);
                 m.dy = h->alloc<float>(R * omax);
@@ -551,6 +649,15 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
                 m.mid = h->alloc<float>(16 * 3 * (int64_t)std::max(std::max(H, omax) + 1, 1024));
                 if (m.nsplit) m.wsplit = h->alloc<uint16_t>(m.nsplit);
+                if (m.mode == RLGPU_GEMM_F16X3 && m.nscale) m.wscale = h->alloc<float>(m.nscale);
+            }
+            if (cfg->train_gemm == RLGPU_GEMM_F16X3) {  // operand-scale shards: both models' slots + the obs
+                h->amax_count = (2 * (int64_t)kAmaxSlots + 1) * 64;
+                h->amax_all = h->alloc<float>(h->amax_count);
+                RLGPU_CHECK_HIP(hipMemset(h->amax_all, 0, h->amax_count * sizeof(float)));
+                h->M[0].amax = h->amax_all;
+                h->M[1].amax = h->amax_all + (int64_t)kAmaxSlots * 64;
+                h->x_amax = h->amax_all + 2 * (int64_t)kAmaxSlots * 64;
             }
             RLGPU_CHECK_HIP(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
             RLGPU_CHECK_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -766,7 +873,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
         hipLaunchKernelGGL(ppo::policy_loss, dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
                            d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
-                           1.f / std::log((float)A), pm.dy, d_metrics, pm.cpart);
+                           1.f / std::log((float)A), pm.dy, d_metrics, pm.cpart, amax_slot(pm, kAmaxOut));
         RLGPU_CHECK_HIP(hipGetLastError());
         backward(h, 0, h->x0, n, pm.dy, s, pm.cpart, pl_blocks);
         if (!serial) RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
@@ -851,11 +958,45 @@ extern "C" int rlgpu_gemm(int32_t mode, int32_t a_layout, int32_t b_layout, cons
                           int32_t splits, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(d_A && d_B && d_C, "rlgpu_gemm: null argument");
-        RLGPU_REQUIRE(mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F32, "rlgpu_gemm: unknown mode");
+        RLGPU_REQUIRE(mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F32 || mode == RLGPU_GEMM_F16X3,
+                      "rlgpu_gemm: unknown mode");
         RLGPU_REQUIRE(I > 0 && J > 0 && K > 0 && splits >= 1, "rlgpu_gemm: bad sizes");
         RLGPU_REQUIRE((a_layout == 0 && (b_layout == 0 || b_layout == 1)) || (a_layout == 1 && b_layout == 1),
                       "rlgpu_gemm: unsupported layout pair");
         hipStream_t s = rlgpu::as_stream(stream);
+        if (mode == RLGPU_GEMM_F16X3) {
+            // operand scales from stand-alone max |x| passes (the training path gets them from the
+            // producer kernels); B pre-split into scaled planes when the training path would be
+            float* sh = nullptr;
+            RLGPU_CHECK_HIP(hipMallocAsync((void**)&sh, 128 * sizeof(float), s));
+            RLGPU_CHECK_HIP(hipMemsetAsync(sh, 0, 128 * sizeof(float), s));
+            const int64_t ar = a_layout == 0 ? I : K, ac = a_layout == 0 ? K : I;
+            hipLaunchKernelGGL(mlp::amax_rows, dim3(256), dim3(256), 0, s, d_A, ar, (int)ac, lda, sh);
+            if (a_layout == 0 && splits == 1) {
+                const int rows = (int)ceil_div(J, mlp::BN) * mlp::BN, ld = (int)ceil_div(K, mlp::XKMAX) * mlp::XKMAX;
+                const int64_t plane = (int64_t)rows * ld;
+                uint16_t* planes = nullptr;
+                float* inv = nullptr;
+                RLGPU_CHECK_HIP(hipMallocAsync((void**)&planes, 2 * plane * sizeof(uint16_t), s));
+                RLGPU_CHECK_HIP(hipMallocAsync((void**)&inv, rows * sizeof(float), s));
+                if (b_layout == 0)  // B [J][ldb]: W = B (out = J, in = K)
+                    hipLaunchKernelGGL(mlp::split_weight_h3, dim3(rows), dim3(256), 0, s, d_B, J, K, ldb, 0, ld, planes, plane, inv);
+                else  // B [K][ldb]: W^T (out = K, in = J)
+                    hipLaunchKernelGGL(mlp::split_weight_h3, dim3(rows), dim3(256), 0, s, d_B, K, J, ldb, 1, ld, planes, plane, inv);
+                RLGPU_CHECK_HIP(hipGetLastError());
+                gemm_x6_pre(d_A, lda, planes, ld, plane, d_C, ldc, d_bias, I, J, K, s, false, sh, inv);
+                RLGPU_CHECK_HIP(hipFreeAsync(planes, s));
+                RLGPU_CHECK_HIP(hipFreeAsync(inv, s));
+            } else {
+                const int64_t br = b_layout == 0 ? J : K, bc = b_layout == 0 ? K : J;
+                hipLaunchKernelGGL(mlp::amax_rows, dim3(256), dim3(256), 0, s, d_B, br, (int)bc, ldb, sh + 64);
+                gemm_f32(mode, a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, s, false, false, sh,
+                         sh + 64);
+            }
+            RLGPU_CHECK_HIP(hipGetLastError());
+            RLGPU_CHECK_HIP(hipFreeAsync(sh, s));
+            return;
+        }
         if (mode == RLGPU_GEMM_F32X6 && a_layout == 0 && splits == 1) {
             // the training path's form: B split once into padded planes, then the pre-split kernel
             const int rows = (int)ceil_div(J, mlp::BN) * mlp::BN, ld = (int)ceil_div(K, mlp::XKMAX) * mlp::XKMAX;

@@ -108,13 +108,15 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.
 // Rows are minibatch-ordered; sample s = idx ? idx[start + r] : start + r addresses the
-// batch buffers.  Each wave handles 16 rows; metrics are reduced per block (one atomic each).
-constexpr int PL_ROWS = 64;
+// batch buffers.  Each wave handles PL_RF rows; metrics are reduced per block (one atomic each).
+constexpr int PL_RF = 4;                // rows per wave, all gathered before any is computed
+constexpr int PL_ROWS = 4 * PL_RF;      // rows per 256-thread block
 __global__ void __launch_bounds__(256) policy_loss(const float* logits, const uint8_t* masks, const int32_t* actions,
                                                   const float* old_logp, const float* adv, const int32_t* idx, int64_t start,
                                                   int n, int A, const float* adv_stats, float bsr, float clip_range,
                                                   float ent_scale, float inv_log_a, float* dlogits, float* metrics,
-                                                  float* bias_part) {
+                                                  float* bias_part, float* amax) {
+    uint32_t vmax = 0;  // max |dlogits| (H3 operand scale, when amax is given)
     __shared__ float red[4][5];
     __shared__ float colred[4][128];  // per-wave column sums of dlogits (A <= 128)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -123,14 +125,39 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
     const float mean = adv_stats[0], sd = adv_stats[1];
     float m_ent = 0.f, m_kl = 0.f, m_pl = 0.f, m_ratio = 0.f, m_clip = 0.f;
     float col0 = 0.f, col1 = 0.f;
-    for (int i = 0; i < PL_ROWS / 4; i++) {
-        int row = blockIdx.x * PL_ROWS + i * 4 + w;
-        if (row >= n) break;
-        int64_t s = idx ? (int64_t)idx[start + row] : start + row;
+    // The wave's PL_RF rows are gathered together (the minibatch rows sit at random rollout
+    // positions, so every gather is a dependent round trip): lane r < PL_RF fetches row r's sample
+    // index and scalars, then every lane issues all rows' logit / mask loads, then the rows are
+    // computed one after another from registers.
+    const int row0 = blockIdx.x * PL_ROWS + w * PL_RF;
+    int s_l = 0, a_l = 0;
+    float old_l = 0.f, adv_l = 0.f;
+    if (lane < PL_RF && row0 + lane < n) {
+        const int64_t sr = idx ? (int64_t)idx[start + row0 + lane] : start + row0 + lane;
+        s_l = (int)sr;
+        a_l = actions[sr];
+        old_l = old_logp[sr];
+        adv_l = adv[sr];
+    }
+    float zl0[PL_RF], zl1[PL_RF];
+    uint8_t mk0[PL_RF], mk1[PL_RF];
+#pragma unroll
+    for (int i = 0; i < PL_RF; i++) {
+        const int row = min(row0 + i, n - 1);
+        const int64_t s = __shfl(s_l, i, 64);
         const float* lg = logits + (int64_t)row * A;
         const uint8_t* mk = masks + s * A;
-        float z0 = in0 ? lg[a0] + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
-        float z1 = in1 ? lg[a1] + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
+        zl0[i] = in0 ? lg[a0] : 0.f;
+        zl1[i] = in1 ? lg[a1] : 0.f;
+        mk0[i] = in0 ? mk[a0] : 0;
+        mk1[i] = in1 ? mk[a1] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < PL_RF; i++) {
+        const int row = row0 + i;
+        if (row >= n) break;
+        float z0 = in0 ? zl0[i] + (mk0[i] ? 0.f : kDisabledLogit) : 0.f;
+        float z1 = in1 ? zl1[i] + (mk1[i] ? 0.f : kDisabledLogit) : 0.f;
         float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
         float e0 = in0 ? expf(z0 - m) : 0.f, e1 = in1 ? expf(z1 - m) : 0.f;
         float sum = wave_sum(e0 + e1);
@@ -138,13 +165,13 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         float c0 = fminf(fmaxf(p0, kMinProb), 1.f), c1 = fminf(fmaxf(p1, kMinProb), 1.f);
         float l0 = in0 ? logf(c0) : 0.f, l1 = in1 ? logf(c1) : 0.f;
         float ent = -wave_sum((in0 ? l0 * c0 : 0.f) + (in1 ? l1 * c1 : 0.f));
-        int a = actions[s];
+        int a = __shfl(a_l, i, 64);
         a = a < 0 ? 0 : (a > A - 1 ? A - 1 : a);
         float pa = __shfl((a & 1) ? c1 : c0, a >> 1, 64);
         float lp = logf(pa);
-        float old = old_logp[s];
+        float old = __shfl(old_l, i, 64);
         float ratio = expf(lp - old);
-        float advn = (adv[s] - mean) / (sd + 1e-8f);
+        float advn = (__shfl(adv_l, i, 64) - mean) / (sd + 1e-8f);
         float clipped = fminf(fmaxf(ratio, 1.f - clip_range), 1.f + clip_range);
         float s1 = ratio * advn, s2 = clipped * advn;
         float pl = fminf(s1, s2);
@@ -168,6 +195,9 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         if (in1) dl[a1] = g1;
         col0 += in0 ? g0 : 0.f;
         col1 += in1 ? g1 : 0.f;
+        const uint32_t b0 = in0 ? mlp::abs_bits(g0) : 0u, b1 = in1 ? mlp::abs_bits(g1) : 0u;
+        vmax = b0 > vmax ? b0 : vmax;
+        vmax = b1 > vmax ? b1 : vmax;
         float lr = lp - old;
         m_ent += ent * inv_log_a;
         m_kl += expf(lr) - 1.f - lr;
@@ -193,6 +223,7 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
         atomicAdd(&metrics[slot[threadIdx.x]], v / (float)n);
     }
+    if (amax) mlp::h3_amax_commit(amax, vmax);
 }
 
 // Critic MSE: loss = mean((v - t)^2) * bsr ; dv = 2 (v - t) / n * bsr.

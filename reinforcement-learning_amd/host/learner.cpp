@@ -519,7 +519,7 @@ extern "C" int rlgpu_learner_default_config(rlgpu_learner_config* c) {
         c->n_policy_layers = 2;
         c->critic_layers[0] = c->critic_layers[1] = 512;
         c->n_critic_layers = 2;
-        c->train_gemm = RLGPU_GEMM_F32X6;
+        c->train_gemm = RLGPU_GEMM_F16X3;  // fp32-class training GEMMs at half the MFMAs of F32X6
         c->rank = 0;
         c->world = 1;
     });

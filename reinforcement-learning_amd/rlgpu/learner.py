@@ -171,7 +171,7 @@ class LearnerConfig:
         self.critic_layers = (512, 512)
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
-        self.train_gemm = 0               # rlgpu_ppo_config.train_gemm: 0 = f32 via bf16x3 split, 1 = f32 MFMA
+        self.train_gemm = 2               # rlgpu_ppo_config.train_gemm: 2 = f32 via scaled fp16 split (H3), 0 = bf16 x6 split, 1 = f32 MFMA
         self.infer_fp16 = False           # rlgpu_ppo_config.infer_fp16: fp16 inference copy (C5) instead of bf16
         self.frame_stack = 1              # K >= 2: stacked AdvancedObs frames (C4; no reference counterpart)
         # checkpoints (LearnerConfig.h:31-38): None = no save / load

@@ -34,7 +34,7 @@ class _Cfg(ctypes.Structure):
                 ("max_rows", ctypes.c_int32), ("seed", ctypes.c_uint64), ("train_gemm", ctypes.c_int32),
                 ("infer_fp16", ctypes.c_int32)]
 
-GEMM_F32X6, GEMM_F32 = 0, 1  # rlgpu_ppo_config.train_gemm (include/rlgpu_ppo.h)
+GEMM_F32X6, GEMM_F32, GEMM_F16X3 = 0, 1, 2  # rlgpu_ppo_config.train_gemm (include/rlgpu_ppo.h)
 
 
 _bound = False
@@ -85,7 +85,7 @@ class PPO:
     def __init__(self, obs_size=167, num_actions=90, policy_layers=(512, 512), critic_layers=(512, 512),
                  layer_norm=True, policy_lr=2.5e-4, critic_lr=2.5e-4, clip_range=0.2, entropy_scale=0.035,
                  max_grad_norm=0.5, max_rows=50_000, seed=42, init=True, device="cuda:0",
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, leaky_slope=0.01, train_gemm=GEMM_F32X6,
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, leaky_slope=0.01, train_gemm=GEMM_F16X3,
                  infer_fp16=False):
         import torch
         if not torch.cuda.is_available():

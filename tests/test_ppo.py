@@ -117,7 +117,7 @@ def test_forward_bf16_close_to_fp32(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [0, 1], ids=["x6", "f32"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["x6", "f32", "h3"])
 @pytest.mark.parametrize("n,batch,slope", [(300, 600, 0.01), (1029, 1029, 0.01), (777, 1000, 1.0)])
 def test_minibatch_grads_match_torch(gpu, n, batch, slope, mode):
     import torch
@@ -251,9 +251,10 @@ GEMM_SHAPES = [  # (a_layout, b_layout, I, J, K, splits): the PPO shapes' layout
 @pytest.mark.gpu
 @pytest.mark.parametrize("la,lb,I,J,K,splits", GEMM_SHAPES)
 def test_gemm_modes_fp32_class_accuracy(gpu, la, lb, I, J, K, splits):
-    """rlgpu_gemm in both training arithmetics against an fp64 product: the three-way bf16 split
-    (RLGPU_GEMM_F32X6) must carry f32-class error -- within 4x of torch's own fp32 matmul error
-    on the same operands (the reference's libtorch fp32 Linear) -- and so must the f32 MFMA."""
+    """rlgpu_gemm in every training arithmetic against an fp64 product: the three-way bf16 split
+    (RLGPU_GEMM_F32X6) and the scaled two-way fp16 split (RLGPU_GEMM_F16X3) must carry f32-class
+    error -- within 4x of torch's own fp32 matmul error on the same operands (the reference's
+    libtorch fp32 Linear) -- and so must the f32 MFMA."""
     import ctypes
     import torch
     from rlgpu import _lib
@@ -271,13 +272,83 @@ def test_gemm_modes_fp32_class_accuracy(gpu, la, lb, I, J, K, splits):
     terr = ((tA @ tB + (bias if bias is not None else 0)).double() - ref).abs().max().item() / scale
     dA, dB = A.to(gpu), B.to(gpu)
     db = bias.to(gpu) if bias is not None else None
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         C = torch.full((splits, I, J), float("nan"), device=gpu)
         _lib.check(L.rlgpu_gemm(mode, la, lb, _lib.ptr(dA), A.shape[1], _lib.ptr(dB), B.shape[1], _lib.ptr(C), J,
                                 _lib.ptr(db), I, J, K, splits, _lib.stream_ptr()), "rlgpu_gemm")
         got = C.sum(0).double().cpu()
         err = (got - ref).abs().max().item() / scale
         assert err <= 4 * terr + 1e-7, f"mode {mode}: rel err {err:.2e} vs torch fp32 {terr:.2e}"
+
+
+def _gemm(gpu, mode, la, lb, A, B, I, J, K, splits=1, bias=None):
+    import ctypes
+    import torch
+    from rlgpu import _lib
+    from rlgpu.ppo import _bind
+    L = _bind()
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.rlgpu_gemm.argtypes = [i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i32, i32, i32, i32, vp]
+    dA, dB = A.to(gpu), B.to(gpu)
+    db = bias.to(gpu) if bias is not None else None
+    C = torch.full((splits, I, J), float("nan"), device=gpu)
+    _lib.check(L.rlgpu_gemm(mode, la, lb, _lib.ptr(dA), A.shape[1], _lib.ptr(dB), B.shape[1], _lib.ptr(C), J,
+                            _lib.ptr(db), I, J, K, splits, _lib.stream_ptr()), "rlgpu_gemm")
+    return C.sum(0).double().cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("la,lb,splits", [(0, 0, 1), (0, 1, 1), (1, 1, 3)])
+def test_gemm_h3_scales(gpu, la, lb, splits):
+    """RLGPU_GEMM_F16X3's power-of-two operand scales.  Tensors far outside fp16's range (1e-30,
+    1e25) and rows spread over 2^+-8 (a 2^16 range inside one tensor) keep f32-class error on every
+    element, normwise (|C - C64| / (|A||B|) <= 4 x torch fp32's); with rows spread over 2^+-20 the
+    smallest rows sit 2^40 below the tensor's largest, under fp16's range after the per-tensor scale,
+    and the error stays f32-class relative to the output's scale (max |A||B|), not per element.
+    An all-zero operand gives exactly zero, and a NaN in an operand reaches the output."""
+    import torch
+    I, J, K = 300, 200, 257
+    g = torch.Generator().manual_seed(5)
+    for sa, sb, spread in ((1e-30, 1e25, 0), (1.0, 1.0, 8), (3e5, 2e-7, 8), (1.0, 1.0, 20)):
+        A = torch.randn((I, K) if la == 0 else (K, I), generator=g) * sa
+        B = torch.randn((J, K) if lb == 0 else (K, J), generator=g) * sb
+        if spread:  # rows of A (output rows i) at scales 2^-spread .. 2^spread
+            ei = torch.randint(-spread, spread + 1, (I,), generator=g).double()
+            if la == 0:
+                A = (A.double() * torch.pow(2.0, ei)[:, None]).float()
+            else:
+                A = (A.double() * torch.pow(2.0, ei)[None, :]).float()
+        tA, tB = (A if la == 0 else A.t()), (B.t() if lb == 0 else B)
+        ref = tA.double() @ tB.double()
+        norm = tA.double().abs() @ tB.double().abs()
+        if spread <= 8:
+            nrm = norm
+        else:
+            nrm = norm.max()
+        terr = ((tA @ tB).double() - ref).abs().div(nrm).max().item()
+        got = _gemm(gpu, 2, la, lb, A, B, I, J, K, splits)
+        err = (got - ref).abs().div(nrm).max().item()
+        assert err <= 4 * terr + 1e-7, (sa, sb, spread, err, terr)
+    Z = torch.zeros((I, K) if la == 0 else (K, I))
+    B = torch.randn((J, K) if lb == 0 else (K, J), generator=g)
+    assert (_gemm(gpu, 2, la, lb, Z, B, I, J, K, splits) == 0).all()
+    A = torch.randn((I, K) if la == 0 else (K, I), generator=g)
+    A[3, 5] = float("nan")
+    assert torch.isnan(_gemm(gpu, 2, la, lb, A, B, I, J, K, splits)).any()
+
+
+@pytest.mark.gpu
+def test_forward_fp32_h3_matches_torch(gpu):
+    """The training forward in RLGPU_GEMM_F16X3 against torch fp32 (rtol 1e-4), at C2 and C5 widths."""
+    import torch
+    from rlgpu.ppo import PPO
+    x = torch.randn(700, 167)
+    for layers in ((512, 512), (2048,) * 4):
+        p = PPO(policy_layers=layers, critic_layers=layers, max_rows=1024, seed=3, train_gemm=2)
+        pol, crit = torch_models(p)
+        for m, ref in ((0, pol), (1, crit)):
+            got = p.forward(m, x.to(gpu)).cpu()
+            np.testing.assert_allclose(got.numpy(), ref(x).detach().numpy(), rtol=1e-4, atol=1e-4)
 
 
 # ------------------------------------------------------------------ BASELINE config C5 (4 x 2048, fp16 inference)

@@ -16,11 +16,12 @@ NAMES = ["T0 sleep/demo/snapshot", "T1 wheels (16 lanes)", "T2 car logic + pads 
          "(unused)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T6 solve writeback"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+warm = int(sys.argv[3]) if len(sys.argv) > 3 else 8  # env steps before profiling (late-episode states)
 dev = torch.device("cuda:0")
 env = EnvSet(n, seed=1234, device=dev)
 gen = torch.Generator(device=dev).manual_seed(7)
 acts = torch.empty(4 * n, dtype=torch.int32, device=dev)
-for i in range(8):
+for i in range(warm):
     acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
     env.step(acts, True)
 prof = torch.zeros(32, dtype=torch.int64, device=dev)

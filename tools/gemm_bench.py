@@ -36,13 +36,17 @@ def run(mode, la, lb, I, J, K, splits=1, reps=20):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
     tf = 2.0 * I * J * K / (us * 1e-6) / 1e12
-    print(f"{'x6 ' if mode == 0 else 'f32'} la={la} lb={lb} I={I:6d} J={J:4d} K={K:6d} splits={splits:3d}: {us:8.1f} us "
+    print(f"{('x6 ', 'f32', 'h3 ')[mode]} la={la} lb={lb} I={I:6d} J={J:4d} K={K:6d} splits={splits:3d}: {us:8.1f} us "
           f"{tf:7.1f} TF/s  max rel err vs fp64 {err:.1e} (torch fp32 {terr:.1e})")
 
 
-for shape in [(0, 0, 50000, 512, 512), (0, 0, 50000, 512, 167), (0, 0, 50000, 90, 512),
-              (0, 1, 50000, 512, 512), (0, 1, 50000, 512, 90),
-              (1, 1, 512, 512, 50000, 49), (1, 1, 512, 167, 50000, 49), (1, 1, 90, 512, 50000, 49),
-              (0, 0, 8192, 8192, 8192)]:
-    for mode in (0, 1):
-        run(mode, *shape)
+SHAPES = [(0, 0, 50000, 512, 512), (0, 0, 50000, 512, 167), (0, 0, 50000, 90, 512),
+          (0, 1, 50000, 512, 512), (0, 1, 50000, 512, 90),
+          (1, 1, 512, 512, 50000, 49), (1, 1, 512, 167, 50000, 49), (1, 1, 90, 512, 50000, 49),
+          (0, 0, 8192, 8192, 8192)]
+# argv: modes (e.g. "2" or "0,2") and optionally shape indices ("0,5")
+modes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2]
+picks = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else range(len(SHAPES))
+for i in picks:
+    for mode in modes:
+        run(mode, *SHAPES[i])
