@@ -572,7 +572,62 @@ DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)
 }
 
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
-template <int XK>
+
+// ---- k-major ("T") staging of a row-index-contiguous operand (H3, 32-deep stages): A_KI (dZ^T)
+// and B_KJ (activations) of the weight gradients.  Global rows are k, contiguous in the output
+// index o, so each thread loads float4s along o (coalesced 512-byte rows per half wave, no scalar
+// gathers) and stores each plane k-major: element (k, o) at k * TPITCH + o of the plane (the
+// plane's [BM][XK + XPAD] storage, same size).  The MFMA fragments (8 consecutive k of one o per
+// lane) are read back transposed with ds_read_b64_tr_b16: per 16-lane group a 4 (k) x 16 (o)
+// block, lane 4q+p addressing row q, columns 4p..4p+3; two reads give k .. k+7.  TPITCH = 160
+// halves puts the 4 rows of a 32-lane half at bank offsets 0 / 16 / 32 / 48: conflict-free.
+constexpr int TPITCH = 160;
+static_assert(32 * TPITCH == BM * (32 + XPAD), "k-major plane must fit the row-major plane storage");
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+template <bool VEC>
+DEV void xt_load(f32x4_t (&v)[2][2], const float* base, int64_t ld, int o0, int on, int k0, int ke) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = threadIdx.x + 256 * q;
+        const int k = k0 + (e >> 5), o = o0 + (e & 31) * 4;
+        const float* row = k < ke ? base + (int64_t)k * ld : nullptr;
+        v[q >> 1][q & 1] = load4v<VEC>(row, o, on);
+    }
+}
+DEV void xt_store(uint16_t (*lds)[BM][32 + XPAD], const f32x4_t (&v)[2][2], float sc) {
+    uint16_t* ph = &lds[0][0][0];
+    uint16_t* pl = &lds[1][0][0];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = threadIdx.x + 256 * q;
+        const int off = (e >> 5) * TPITCH + (e & 31) * 4;
+        const f32x4_t x = v[q >> 1][q & 1];
+        uint32_t h2[2], l2[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const float x0 = x[2 * c] * sc, x1 = x[2 * c + 1] * sc;
+            const uint16_t h0 = f2hf(x0), h1 = f2hf(x1);
+            h2[c] = pack_h2(h0, h1);
+            l2[c] = pack_h2(f2hf(x0 - hf2f(h0)), f2hf(x1 - hf2f(h1)));
+        }
+        *reinterpret_cast<uint2*>(ph + off) = make_uint2(h2[0], h2[1]);
+        *reinterpret_cast<uint2*>(pl + off) = make_uint2(l2[0], l2[1]);
+    }
+}
+// the 32x32x16 operand fragment of output rows ob .. ob+31 at k = kof0 + 8 (lane >> 5) + 0..7
+DEV h16x8 tr_frag(const uint16_t* plane, int ob, int kof0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int o = ob + 16 * (g & 1) + 4 * (i & 3);
+    const int k = kof0 + 8 * (g >> 1) + (i >> 2);
+    typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+    const v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + k * TPITCH + o));
+    const v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + (k + 4) * TPITCH + o));
+    typedef short v8i16 __attribute__((ext_vector_type(8)));
+    const v8i16 r = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    return __builtin_bit_cast(h16x8, r);
+}
+
+template <int XK, bool TA = false, bool TB = false>
 DEV void h3_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
                        f32x16 (&acc)[2][2], f32x16 (&cor)[2][2]) {
 #pragma unroll
@@ -583,8 +638,11 @@ DEV void h3_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)
         for (int p = 0; p < 2; p++)
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-                a[p][u] = *(const h16x8*)&As[p][ra + 32 * u][kof];
-                b[p][u] = *(const h16x8*)&Bs[p][rb + 32 * u][kof];
+                // ra / rb: this lane's row; (ra & ~31) the wave's 32-row block base
+                a[p][u] = TA ? tr_frag(&As[p][0][0], (ra & ~31) + 32 * u, ks * 16, lane)
+                             : *(const h16x8*)&As[p][ra + 32 * u][kof];
+                b[p][u] = TB ? tr_frag(&Bs[p][0][0], (rb & ~31) + 32 * u, ks * 16, lane)
+                             : *(const h16x8*)&Bs[p][rb + 32 * u][kof];
             }
         // one accumulator: the corrections, then the leading product, enter the running f32 sum (the
         // rounding count of an f32 FMA chain; a separate correction accumulator would cost 64
@@ -605,6 +663,8 @@ template <int LA, int LB, bool AV, bool BV, bool BPRE, int V, bool H3 = false>
 __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     constexpr int XK = X6Shape<V>::XK, NB = X6Shape<V>::NB, NQ = XK / 16, NP = H3 ? 2 : 3;
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
+    // H3 with 32-deep stages: row-index-contiguous operands staged k-major (xt_load / tr_frag)
+    constexpr bool TA = H3 && !AK && XK == 32, TB = H3 && !BPRE && !BKM && XK == 32;
     __shared__ uint16_t As[NB][NP][BM][XK + XPAD];
     __shared__ uint16_t Bs[NB][NP][BN][XK + XPAD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -633,23 +693,33 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     const RowPtrs arow = xs_rows<AK, XK>(g.A, g.lda, i0, g.I);
     const RowPtrs brow = xs_rows<BKM, XK>(g.B, g.ldb, j0, g.J);
     auto load_stage = [&](int k0) {
-        xs_load<AK, AV, XK>(va, arow, g.A, g.lda, i0, g.I, k0, ke);
+        if constexpr (TA)
+            xt_load<AV>(va, g.A, g.lda, i0, g.I, k0, ke);
+        else
+            xs_load<AK, AV, XK>(va, arow, g.A, g.lda, i0, g.I, k0, ke);
         if (BPRE)
             xp_load<XK, NP>(vp, Bp, g.ldb, g.bplane, j0, k0, ke);
+        else if constexpr (TB)
+            xt_load<BV>(vb, g.B, g.ldb, j0, g.J, k0, ke);
         else
             xs_load<BKM, BV, XK>(vb, brow, g.B, g.ldb, j0, g.J, k0, ke);
     };
     const int ra = wm * 64 + (lane & 31), rb = wn * 64 + (lane & 31);
     auto store_stage = [&](int buf) {
-        xs_store<AK, XK, H3>(As[buf], va, sa);
+        if constexpr (TA)
+            xt_store(As[buf], va, sa);
+        else
+            xs_store<AK, XK, H3>(As[buf], va, sa);
         if (BPRE)
             xp_store<XK, NP>(Bs[buf], vp);
+        else if constexpr (TB)
+            xt_store(Bs[buf], vb, sb);
         else
             xs_store<BKM, XK, H3>(Bs[buf], vb, sb);
     };
     auto mfma_stage = [&](int buf) {
         if (H3)
-            h3_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
+            h3_mfma_stage<XK, TA, TB>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
         else
             x6_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
     };
