@@ -540,6 +540,13 @@ template <> struct X6Shape<5> { static constexpr int XK = 32, NB = 2, OCC = 2; }
 //   V = 6: V = 4 with the next stage stored first, then the stage after it loaded, then this
 //          stage's MFMAs (the loads get a whole stage of MFMAs and a barrier to land)
 template <> struct X6Shape<6> { static constexpr int XK = 32, NB = 2, OCC = 2; };
+//   V = 7 / 8 / 9: ablations of V = 0 for timing only (results are garbage): 7 stores the loaded
+//          bits without the split VALU, 8 issues no global loads after the first stage, 9 runs no MFMA
+template <> struct X6Shape<7> { static constexpr int XK = 32, NB = 1, OCC = 2; };
+template <> struct X6Shape<8> { static constexpr int XK = 32, NB = 1, OCC = 2; };
+template <> struct X6Shape<9> { static constexpr int XK = 32, NB = 1, OCC = 2; };
+template <> struct X6Shape<10> { static constexpr int XK = 32, NB = 1, OCC = 2; };  // 8 + 9
+template <> struct X6Shape<11> { static constexpr int XK = 32, NB = 1, OCC = 2; };  // no epilogue stores
 
 template <int XK>
 DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
@@ -692,7 +699,10 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     const float sa = pow2f(pa), sb = pow2f(pb);
     const RowPtrs arow = xs_rows<AK, XK>(g.A, g.lda, i0, g.I);
     const RowPtrs brow = xs_rows<BKM, XK>(g.B, g.ldb, j0, g.J);
+    bool first_load = true;
     auto load_stage = [&](int k0) {
+        if ((V == 8 || V == 10) && !first_load) return;
+        first_load = false;
         if constexpr (TA)
             xt_load<AV>(va, g.A, g.lda, i0, g.I, k0, ke);
         else
@@ -706,6 +716,16 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     };
     const int ra = wm * 64 + (lane & 31), rb = wn * 64 + (lane & 31);
     auto store_stage = [&](int buf) {
+        if (V == 7 && !TA && !TB) {  // ablation: the loaded bits straight into the planes
+#pragma unroll
+            for (int q = 0; q < NQ; q++) {
+                const int row = xs_row<AK, XK>(q), c = xs_kg<AK, XK>(q) * 8;
+                *reinterpret_cast<f32x4_t*>(&As[buf][0][row][c]) = va[q][0];
+                *reinterpret_cast<f32x4_t*>(&As[buf][1][row][c]) = va[q][1];
+            }
+            if (BPRE) xp_store<XK, NP>(Bs[buf], vp);
+            return;
+        }
         if constexpr (TA)
             xt_store(As[buf], va, sa);
         else
@@ -718,6 +738,7 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
             xs_store<BKM, XK, H3>(Bs[buf], vb, sb);
     };
     auto mfma_stage = [&](int buf) {
+        if (V == 9 || V == 10) return;
         if (H3)
             h3_mfma_stage<XK, TA, TB>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
         else
@@ -777,6 +798,7 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     }
     float* C = g.C + (int64_t)tl.z * g.c_split;
     const int h = lane >> 5, l32 = lane & 31;
+    if (V == 11 && g.ldc != -7) return;  // ablation: no epilogue (the condition keeps the MFMAs alive)
     // H3: undo the operand scales (powers of two: exact); the pre-split B's per-row inverse scale
     // is read for the tile's columns (rows past J carry 1)
     const int pab = pa + pb;

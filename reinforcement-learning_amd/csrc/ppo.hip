@@ -73,7 +73,7 @@ inline int h3_variant() {
     static const int v = [] {
         const char* e = getenv("RLGPU_H3_VARIANT");
         int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 6) ? x : 0;
+        return (x >= 0 && x <= 11) ? x : 0;
     }();
     return v;
 }
@@ -143,6 +143,21 @@ void x6_launch_v(dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
         case 6:
             if (H3) {
                 hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 6, true>), grid, blk, 0, s, g);
+                break;
+            }
+            [[fallthrough]];
+        case 7:
+        case 8:
+        case 9:
+        case 10:
+        case 11:  // timing ablations (garbage results): RLGPU_H3_VARIANT=7/8/9 in microbenchmarks only
+            if (H3 && PRE) {
+                const int v = h3_variant();
+                if (v == 7) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 7, true>), grid, blk, 0, s, g);
+                if (v == 8) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 8, true>), grid, blk, 0, s, g);
+                if (v == 9) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 9, true>), grid, blk, 0, s, g);
+                if (v == 10) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 10, true>), grid, blk, 0, s, g);
+                if (v == 11) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 11, true>), grid, blk, 0, s, g);
                 break;
             }
             [[fallthrough]];
