@@ -547,6 +547,8 @@ template <> struct X6Shape<8> { static constexpr int XK = 32, NB = 1, OCC = 2; }
 template <> struct X6Shape<9> { static constexpr int XK = 32, NB = 1, OCC = 2; };
 template <> struct X6Shape<10> { static constexpr int XK = 32, NB = 1, OCC = 2; };  // 8 + 9
 template <> struct X6Shape<11> { static constexpr int XK = 32, NB = 1, OCC = 2; };  // no epilogue stores
+//   V = 12: V = 0 compiled for four workgroups per CU (<= 128 VGPRs; 4 x 40 KB of LDS)
+template <> struct X6Shape<12> { static constexpr int XK = 32, NB = 1, OCC = 4; };
 
 template <int XK>
 DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
@@ -835,6 +837,186 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
                 if (i < g.I) C[(int64_t)i * g.ldc + j] = (H3 ? ldexpf(v * csc[tj], -pab) : v) + bj;
             }
         }
+}
+
+// ---- H3 GEMM with 128 x 256 tiles (gemm_h3w): each of the 4 waves computes 64 x 128 (2 x 4 MFMA
+// blocks), so per 16-deep k step a wave issues 24 MFMAs for 12 LDS fragment reads (the 128 x 128
+// kernel: 12 for 8) and every A panel is read once per 256 output columns instead of per 128.
+// Operands: A_IK (k-contiguous, split in the loader) or A_KI (k-major staging, tr reads); B the
+// pre-split planes (rows padded to a multiple of 256) or B_KJ (k-major staging).  32-deep stages,
+// one LDS buffer (20 KB A + 40 KB B), two workgroups per CU.  Same arithmetic and epilogue as the
+// H3 path of gemm_x6.
+constexpr int BNW = 2 * BN;
+template <bool VEC, int COLS>
+DEV void xtn_load(f32x4_t* v, const float* base, int64_t ld, int o0, int on, int k0, int ke) {
+    constexpr int PER = COLS / 4;  // float4 per k row
+#pragma unroll
+    for (int q = 0; q < COLS / 32; q++) {
+        const int e = threadIdx.x + 256 * q;
+        const int k = k0 + e / PER, o = o0 + (e % PER) * 4;
+        const float* row = k < ke ? base + (int64_t)k * ld : nullptr;
+        v[q] = load4v<VEC>(row, o, on);
+    }
+}
+template <int COLS>
+DEV void xtn_store(uint16_t* ph, uint16_t* pl, const f32x4_t* v, float sc) {
+    constexpr int PER = COLS / 4, P = COLS + 32;
+#pragma unroll
+    for (int q = 0; q < COLS / 32; q++) {
+        const int e = threadIdx.x + 256 * q;
+        const int off = (e / PER) * P + (e % PER) * 4;
+        const f32x4_t x = v[q];
+        uint32_t h2[2], l2[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const float x0 = x[2 * c] * sc, x1 = x[2 * c + 1] * sc;
+            const uint16_t h0 = f2hf(x0), h1 = f2hf(x1);
+            h2[c] = pack_h2(h0, h1);
+            l2[c] = pack_h2(f2hf(x0 - hf2f(h0)), f2hf(x1 - hf2f(h1)));
+        }
+        *reinterpret_cast<uint2*>(ph + off) = make_uint2(h2[0], h2[1]);
+        *reinterpret_cast<uint2*>(pl + off) = make_uint2(l2[0], l2[1]);
+    }
+}
+// tr_frag over a k-major plane of row pitch P halves (P = COLS + 32: conflict-free, see TPITCH)
+template <int P>
+DEV h16x8 trp_frag(const uint16_t* plane, int ob, int kof0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int o = ob + 16 * (g & 1) + 4 * (i & 3);
+    const int k = kof0 + 8 * (g >> 1) + (i >> 2);
+    typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+    const v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + k * P + o));
+    const v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + (k + 4) * P + o));
+    typedef short v8i16 __attribute__((ext_vector_type(8)));
+    const v8i16 r = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    return __builtin_bit_cast(h16x8, r);
+}
+
+template <int LA, int LB, bool AV, bool BV, bool BPRE>
+__global__ void __launch_bounds__(256, 2) gemm_h3w(GemmArgs g) {
+    constexpr int XK = 32;
+    constexpr bool TA = LA == A_KI, TB = !BPRE;
+    static_assert(BPRE || LB == B_KJ, "gemm_h3w: B is either pre-split or B_KJ");
+    static_assert(32 * (BNW + 32) <= BNW * (XK + XPAD), "k-major B plane must fit");
+    __shared__ uint16_t As[2][BM][XK + XPAD];
+    __shared__ uint16_t Bs[2][BNW][XK + XPAD];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
+    const int i0 = tl.y * BM, j0 = tl.x * BNW;
+    const int kb = tl.z * g.kchunk;
+    const int ke = min(g.K, kb + g.kchunk);
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
+    f32x4_t va[4];           // A stage: 128 x 32 floats
+    f32x4_t vb[8];           // B_KJ stage: 32 x 256 floats
+    u32x4_t vp[2][4];        // pre-split B stage: 2 planes x 256 rows x 32 halves
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+    const int pa = h3_pow(shard_max_bits(g.amax_a));
+    const int pb = BPRE ? 0 : h3_pow(shard_max_bits(g.amax_b));
+    const float sa = pow2f(pa), sb = pow2f(pb);
+    const RowPtrs arow = xs_rows<!TA, XK>(g.A, g.lda, i0, g.I);
+    auto load_stage = [&](int k0) {
+        if constexpr (TA) {
+            xtn_load<AV, BM>(va, g.A, g.lda, i0, g.I, k0, ke);
+        } else {
+            f32x4_t (&v2)[2][2] = *reinterpret_cast<f32x4_t (*)[2][2]>(va);
+            xs_load<true, AV, XK>(v2, arow, g.A, g.lda, i0, g.I, k0, ke);
+        }
+        if constexpr (BPRE) {
+            constexpr int KG = XK / 8;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int e = threadIdx.x + 256 * q;
+                const int64_t off = (int64_t)(j0 + e / KG) * g.ldb + k0 + (e % KG) * 8;
+                const bool ok = k0 + (e % KG) * 8 < ke;
+#pragma unroll
+                for (int p = 0; p < 2; p++)
+                    vp[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? Bp + p * g.bplane + off
+                                                                   : reinterpret_cast<const uint16_t*>(g_zero_row));
+            }
+        } else {
+            xtn_load<BV, BNW>(vb, g.B, g.ldb, j0, g.J, k0, ke);
+        }
+    };
+    auto store_stage = [&]() {
+        if constexpr (TA) {
+            xtn_store<BM>(&As[0][0][0], &As[1][0][0], va, sa);
+        } else {
+            const f32x4_t (&v2)[2][2] = *reinterpret_cast<const f32x4_t (*)[2][2]>(va);
+            xs_store<true, XK, true>(As, v2, sa);
+        }
+        if constexpr (BPRE) {
+            constexpr int KG = XK / 8;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int e = threadIdx.x + 256 * q;
+#pragma unroll
+                for (int p = 0; p < 2; p++) *reinterpret_cast<u32x4_t*>(&Bs[p][e / KG][(e % KG) * 8]) = vp[p][q];
+            }
+        } else {
+            xtn_store<BNW>(&Bs[0][0][0], &Bs[1][0][0], vb, sb);
+        }
+    };
+    const int ra = wm * 64 + (lane & 31), rb = wn * 128 + (lane & 31);
+    auto mfma_stage = [&]() {
+#pragma unroll
+        for (int ks = 0; ks < XK / 16; ks++) {
+            const int kof = ks * 16 + 8 * (lane >> 5);
+            h16x8 a[2][2], b[2][4];
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+#pragma unroll
+                for (int u = 0; u < 2; u++)
+                    a[p][u] = TA ? trp_frag<BM + 32>(&As[p][0][0], wm * 64 + 32 * u, ks * 16, lane)
+                                 : *(const h16x8*)&As[p][ra + 32 * u][kof];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    b[p][u] = TB ? trp_frag<BNW + 32>(&Bs[p][0][0], wn * 128 + 32 * u, ks * 16, lane)
+                                 : *(const h16x8*)&Bs[p][rb + 32 * u][kof];
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 4; tj++) {
+                    f32x16 c = acc[ti][tj];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1][ti], b[0][tj], c, 0, 0, 0);  // l h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h l
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[0][tj], c, 0, 0, 0);  // h h
+                }
+        }
+    };
+    load_stage(kb);
+    for (int k0 = kb; k0 < ke; k0 += XK) {
+        store_stage();
+        __syncthreads();
+        load_stage(k0 + XK);  // unconditional: past ke it reads the zero row
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_stage();
+        __syncthreads();
+    }
+    float* C = g.C + (int64_t)tl.z * g.c_split;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int pab = pa + pb;
+#pragma unroll
+    for (int tj = 0; tj < 4; tj++) {
+        const int j = j0 + wn * 128 + tj * 32 + l32;
+        if (j >= g.J) continue;
+        const float bsc = BPRE ? g.bscale[j] : 1.f;
+        const float bj = g.bias ? g.bias[j] : 0.f;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (i < g.I) C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * bsc, -pab) + bj;
+            }
+    }
 }
 
 // ---- bf16 inference GEMM: C[i,j] = bf16( sum_k A[i,k] W[j,k] + bias[j] ) on

@@ -73,9 +73,19 @@ inline int h3_variant() {
     static const int v = [] {
         const char* e = getenv("RLGPU_H3_VARIANT");
         int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 11) ? x : 0;
+        return (x >= 0 && x <= 12) ? x : 0;
     }();
     return v;
+}
+// H3 GEMMs with more than 128 output columns on the 128 x 256 tile kernel (mlp::gemm_h3w) when
+// RLGPU_H3_WIDE=1 (experiment: 50000 x 512 x 512 took 134 us against 111 us on gemm_x6's 128 x 128
+// tiles at three workgroups per CU)
+inline bool h3_wide(int J) {
+    static const bool on = [] {
+        const char* e = getenv("RLGPU_H3_WIDE");  // measured slower (254 VGPRs, 2 WGs / CU): off by default
+        return e && atoi(e) == 1;
+    }();
+    return on && J > mlp::BN;
 }
 inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
 inline bool split_mode_(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
@@ -146,6 +156,12 @@ void x6_launch_v(dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
                 break;
             }
             [[fallthrough]];
+        case 12:
+            if (H3) {
+                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 12, true>), grid, blk, 0, s, g);
+                break;
+            }
+            [[fallthrough]];
         case 7:
         case 8:
         case 9:
@@ -204,6 +220,16 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
     g.gx = (int)ceil_div(J, mlp::BN);
     g.gy = (int)ceil_div(I, mlp::BM);
     g.gz = z;
+    if (mode == RLGPU_GEMM_F16X3 && la == mlp::A_KI && lb == mlp::B_KJ && h3_wide(J)) {
+        g.gx = (int)ceil_div(J, mlp::BNW);
+        dim3 gridw(g.gx * g.gy * g.gz), blkw(256);
+        if (av && bv) hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, true, true, false>), gridw, blkw, 0, s, g);
+        else if (av) hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, true, false, false>), gridw, blkw, 0, s, g);
+        else if (bv) hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, false, true, false>), gridw, blkw, 0, s, g);
+        else hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, false, false, false>), gridw, blkw, 0, s, g);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        return;
+    }
     dim3 grid(g.gx * g.gy * g.gz), blk(256);
 #define RLGPU_GEMM_CASE(LA, LB)                                                                                  \
     if (la == LA && lb == LB) {                                                                                  \
@@ -254,6 +280,16 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
     g.gy = (int)ceil_div(I, mlp::BM);
     g.gz = 1;
     const bool av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && (K % 4 == 0 || a_tail_ok);
+    if (h3 && h3_wide(J)) {  // planes padded to a multiple of BNW rows (build_model)
+        g.gx = (int)ceil_div(J, mlp::BNW);
+        dim3 gridw(g.gx * g.gy);
+        if (av)
+            hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_IK, mlp::B_JK, true, true, true>), gridw, dim3(256), 0, s, g);
+        else
+            hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_IK, mlp::B_JK, false, true, true>), gridw, dim3(256), 0, s, g);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        return;
+    }
     dim3 grid(g.gx * g.gy), blk(256);
     if (h3) {
         if (av)
@@ -303,7 +339,8 @@ void split_weights(const float* P, Model& m, hipStream_t s) {
 // split-K count of a weight gradient [out, in] over `rows`: one full round of workgroups
 // (tiles x splits ~ gemm_slots), each split at least 4 K steps
 int splits_for(int mode, int rows, int out, int in) {
-    const int tiles = (int)(ceil_div(out, mlp::BM) * ceil_div(in, mlp::BN));
+    const int bn = (mode == RLGPU_GEMM_F16X3 && h3_wide(in)) ? mlp::BNW : mlp::BN;
+    const int tiles = (int)(ceil_div(out, mlp::BM) * ceil_div(in, bn));
     int s = gemm_slots(mode) / tiles;
     const int maxs = rows / (4 * mlp::BK);
     if (s > maxs) s = maxs;
@@ -549,14 +586,15 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
         if (L.in > h->hmax && l > 0) h->hmax = L.in;
         if (split_mode(m.mode) && L.out > 1) {  // the rank-1 critic head has no GEMM
             const int np = m.mode == RLGPU_GEMM_F16X3 ? 2 : 3;  // planes per split weight
-            L.sf_rows = (int)ceil_div(L.out, mlp::BN) * mlp::BN;
+            const int rpad = m.mode == RLGPU_GEMM_F16X3 ? mlp::BNW : mlp::BN;  // rows: whole B tiles
+            L.sf_rows = (int)ceil_div(L.out, rpad) * rpad;
             L.sf_ld = (int)ceil_div(L.in, mlp::XKMAX) * mlp::XKMAX;
             L.sf = m.nsplit;
             m.nsplit += np * (int64_t)L.sf_rows * L.sf_ld;
             L.sfs = m.nscale;
             m.nscale += L.sf_rows;
             if (l > 0) {  // dA of the first layer is never needed
-                L.sb_rows = (int)ceil_div(L.in, mlp::BN) * mlp::BN;
+                L.sb_rows = (int)ceil_div(L.in, rpad) * rpad;
                 L.sb_ld = (int)ceil_div(L.out, mlp::XKMAX) * mlp::XKMAX;
                 L.sb = m.nsplit;
                 m.nsplit += np * (int64_t)L.sb_rows * L.sb_ld;
@@ -988,7 +1026,7 @@ extern "C" int rlgpu_gemm(int32_t mode, int32_t a_layout, int32_t b_layout, cons
             const int64_t ar = a_layout == 0 ? I : K, ac = a_layout == 0 ? K : I;
             hipLaunchKernelGGL(mlp::amax_rows, dim3(256), dim3(256), 0, s, d_A, ar, (int)ac, lda, sh);
             if (a_layout == 0 && splits == 1) {
-                const int rows = (int)ceil_div(J, mlp::BN) * mlp::BN, ld = (int)ceil_div(K, mlp::XKMAX) * mlp::XKMAX;
+                const int rows = (int)ceil_div(J, mlp::BNW) * mlp::BNW, ld = (int)ceil_div(K, mlp::XKMAX) * mlp::XKMAX;
                 const int64_t plane = (int64_t)rows * ld;
                 uint16_t* planes = nullptr;
                 float* inv = nullptr;
