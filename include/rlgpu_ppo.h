@@ -91,7 +91,9 @@ int rlgpu_ppo_buffers(rlgpu_ppo* h, float** d_params, float** d_grads, int64_t* 
 int rlgpu_ppo_model_range(rlgpu_ppo* h, int32_t model, int64_t* offset, int64_t* count);
 /* torch-default init (Linear: U(+-1/sqrt(fan_in)) weight and bias; LayerNorm 1 / 0), Philox. */
 int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream);
-/* Refresh the bf16 inference copy from the fp32 parameters (Model::Forward seqHalf). */
+/* Refresh the bf16 inference copy from the fp32 parameters (Model::Forward seqHalf) and mark the
+ * training GEMMs' split weight planes stale.  Call it after writing d_params directly (checkpoint
+ * load, broadcasts); the optimizer step does it itself. */
 int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream);
 
 /* Plain forward of one model on n rows (n <= max_rows): precision 0 = fp32 (training path,

@@ -106,6 +106,11 @@ struct rlgpu_ppo {
     uint16_t* half = nullptr;
     uint16_t* half_ver = nullptr;  // bf16 policy copy of an old version (self-play), same layout as half
     bool has_ver = false;
+    // the training GEMMs' split weight planes are stale (parameters changed since the last split):
+    // set by init / refresh_half / the optimizer step, cleared when forward_train re-splits.  With
+    // the whole iteration as one batch the planes are rebuilt once per optimizer step, not per
+    // minibatch.
+    bool split_dirty[2] = {true, true};
     int64_t step = 0;
     int hmax = 0;
     float *scratch = nullptr;  // clip partials + coefficients
@@ -399,7 +404,10 @@ inline const float* wscale_at(const Model& m, int64_t off) {
 void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipStream_t s) {
     Model& m = h->M[mi];
     const float* P = h->params;
-    split_weights(P, m, s);
+    if (h->split_dirty[mi]) {
+        split_weights(P, m, s);
+        h->split_dirty[mi] = false;
+    }
     int nh = (int)m.L.size() - 1;
     const float* in = X;
     const float* in_amax = amax_x(h, m);
@@ -632,6 +640,7 @@ void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, hipStream_
 
 void refresh_half(rlgpu_ppo* h, hipStream_t s) {
     for (int mi = 0; mi < 2; mi++) half_from(h, mi, h->params + h->M[mi].off, h->half, s);
+    h->split_dirty[0] = h->split_dirty[1] = true;
 }
 
 }  // namespace
