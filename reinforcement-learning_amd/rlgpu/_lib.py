@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librlgpu.so")
+# RLGPU_LIB: an alternative build of the same library (experiments, e.g. other compiler flags)
+LIB_PATH = os.environ.get("RLGPU_LIB") or os.path.join(_HERE, "librlgpu.so")
 _lib = None
 
 
