@@ -130,7 +130,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    phase = {"collect": 0.0, "consume": 0.0, "learn": 0.0}
+    phase = {"collect": 0.0, "consume": 0.0, "learn": 0.0, "learn_issue": 0.0, "collect_issue": 0.0}
     kern = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -138,6 +138,8 @@ def main():
         phase["collect"] += rep["collect_s"]
         phase["consume"] += rep["consume_s"]
         phase["learn"] += rep["learn_s"]
+        phase["learn_issue"] += rep["learn_issue_s"]
+        phase["collect_issue"] += rep["collect_issue_s"]
         kern.append(rep["env_kernel_ms"])
     torch.cuda.synchronize()
     if world > 1:

@@ -122,6 +122,9 @@ typedef struct {
     double collect_s, consume_s, learn_s;   /* host wall time of the phases (stream-synchronised) */
     double env_kernel_ms;                   /* mean fused env-step time (HIP events), if timing is on */
     int64_t env_steps;                      /* env steps of this rank this iteration */
+    double learn_issue_s;                   /* host time to enqueue the learn phase (before its sync):
+                                               close to learn_s means the phase is launch-bound */
+    double collect_issue_s;                 /* the same for the collection phase */
 } rlgpu_learner_report;
 
 typedef struct rlgpu_learner rlgpu_learner;

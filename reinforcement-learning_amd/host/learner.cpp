@@ -457,15 +457,19 @@ rlgpu_learner_report Learner::Iterate() {
     rlgpu_learner_report r{};
     auto t0 = clk::now();
     Collect();
+    auto t0i = clk::now();
     hipCheck(hipStreamSynchronize(s_), "sync");
     auto t1 = clk::now();
+    r.collect_issue_s = secs(t0, t0i);
     Consume();
     hipCheck(hipStreamSynchronize(s_), "sync");
     auto t2 = clk::now();
     Learn();
     FinishIteration();
+    auto t2i = clk::now();
     hipCheck(hipStreamSynchronize(s_), "sync");
     auto t3 = clk::now();
+    r.learn_issue_s = secs(t2, t2i);
     r.collect_s = secs(t0, t1);
     r.consume_s = secs(t1, t2);
     r.learn_s = secs(t2, t3);

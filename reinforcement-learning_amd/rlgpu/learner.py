@@ -219,7 +219,8 @@ class _CStats(ctypes.Structure):
 
 class _CReport(ctypes.Structure):
     _fields_ = [("collect_s", ctypes.c_double), ("consume_s", ctypes.c_double), ("learn_s", ctypes.c_double),
-                ("env_kernel_ms", ctypes.c_double), ("env_steps", ctypes.c_int64)]
+                ("env_kernel_ms", ctypes.c_double), ("env_steps", ctypes.c_int64), ("learn_issue_s", ctypes.c_double),
+                ("collect_issue_s", ctypes.c_double)]
 
 
 def _bind():
@@ -437,7 +438,7 @@ class Learner:
             self.versions.on_iteration(self.total_steps, prev)
         torch.cuda.synchronize(self.device)
         out = {"iteration_s": time.perf_counter() - t0, "collect_s": rep.collect_s, "consume_s": rep.consume_s,
-               "learn_s": rep.learn_s, "env_kernel_ms": rep.env_kernel_ms,
+               "learn_s": rep.learn_s, "learn_issue_s": rep.learn_issue_s, "collect_issue_s": rep.collect_issue_s, "env_kernel_ms": rep.env_kernel_ms,
                "old_version": None if self.old_version is None else (self.old_version.timesteps, self.old_team)}
         if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)
             per = self.cfg.ts_per_save or self.T * self.P * self.world
