@@ -108,120 +108,147 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.
 // Rows are minibatch-ordered; sample s = idx ? idx[start + r] : start + r addresses the
-// batch buffers.  Each wave handles PL_RF rows; metrics are reduced per block (one atomic each).
-constexpr int PL_RF = 4;                // rows per wave, all gathered before any is computed
-constexpr int PL_ROWS = 4 * PL_RF;      // rows per 256-thread block
+// batch buffers.  Metrics are reduced per block (one atomic each).
+// 16 lanes per row, 4 rows in parallel per wave (lane group q = lane / 16 owns row q of the pass),
+// each lane holding the PL_K actions i, i + 16, .., i + 16 (PL_K - 1) of its row: the row's
+// reductions take 4 shuffle steps and one instruction stream serves 4 rows.
+constexpr int PL_K = (kMaxA + 15) / 16;  // actions per lane (A <= 128)
+constexpr int PL_PASSES = 2;             // passes of 4 rows per wave
+constexpr int PL_ROWS = 4 * 4 * PL_PASSES;  // rows per 256-thread block
+__device__ __forceinline__ float grp_sum(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float grp_max(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+template <int K>
 __global__ void __launch_bounds__(256) policy_loss(const float* logits, const uint8_t* masks, const int32_t* actions,
                                                   const float* old_logp, const float* adv, const int32_t* idx, int64_t start,
                                                   int n, int A, const float* adv_stats, float bsr, float clip_range,
                                                   float ent_scale, float inv_log_a, float* dlogits, float* metrics,
                                                   float* bias_part, float* amax) {
+    __shared__ float red[16][5];
+    __shared__ float colred[16][16 * K];  // per (wave, lane group) column sums of dlogits
     uint32_t vmax = 0;  // max |dlogits| (H3 operand scale, when amax is given)
-    __shared__ float red[4][5];
-    __shared__ float colred[4][128];  // per-wave column sums of dlogits (A <= 128)
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int a0 = 2 * lane, a1 = 2 * lane + 1;
-    const bool in0 = a0 < A, in1 = a1 < A;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, grp = lane >> 4, i = lane & 15;
     const float mean = adv_stats[0], sd = adv_stats[1];
     float m_ent = 0.f, m_kl = 0.f, m_pl = 0.f, m_ratio = 0.f, m_clip = 0.f;
-    float col0 = 0.f, col1 = 0.f;
-    // The wave's PL_RF rows are gathered together (the minibatch rows sit at random rollout
-    // positions, so every gather is a dependent round trip): lane r < PL_RF fetches row r's sample
-    // index and scalars, then every lane issues all rows' logit / mask loads, then the rows are
-    // computed one after another from registers.
-    const int row0 = blockIdx.x * PL_ROWS + w * PL_RF;
-    int s_l = 0, a_l = 0;
-    float old_l = 0.f, adv_l = 0.f;
-    if (lane < PL_RF && row0 + lane < n) {
-        const int64_t sr = idx ? (int64_t)idx[start + row0 + lane] : start + row0 + lane;
-        s_l = (int)sr;
-        a_l = actions[sr];
-        old_l = old_logp[sr];
-        adv_l = adv[sr];
-    }
-    float zl0[PL_RF], zl1[PL_RF];
-    uint8_t mk0[PL_RF], mk1[PL_RF];
+    float col[K];
 #pragma unroll
-    for (int i = 0; i < PL_RF; i++) {
-        const int row = min(row0 + i, n - 1);
-        const int64_t s = __shfl(s_l, i, 64);
-        const float* lg = logits + (int64_t)row * A;
-        const uint8_t* mk = masks + s * A;
-        zl0[i] = in0 ? lg[a0] : 0.f;
-        zl1[i] = in1 ? lg[a1] : 0.f;
-        mk0[i] = in0 ? mk[a0] : 0;
-        mk1[i] = in1 ? mk[a1] : 0;
-    }
+    for (int k = 0; k < K; k++) col[k] = 0.f;
+    const float g_pl = -bsr / (float)n;
+    const float g_ent = -ent_scale * bsr * inv_log_a / (float)n;  // d loss / d H_i (H_i unnormalised)
 #pragma unroll
-    for (int i = 0; i < PL_RF; i++) {
-        const int row = row0 + i;
-        if (row >= n) break;
-        float z0 = in0 ? zl0[i] + (mk0[i] ? 0.f : kDisabledLogit) : 0.f;
-        float z1 = in1 ? zl1[i] + (mk1[i] ? 0.f : kDisabledLogit) : 0.f;
-        float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
-        float e0 = in0 ? expf(z0 - m) : 0.f, e1 = in1 ? expf(z1 - m) : 0.f;
-        float sum = wave_sum(e0 + e1);
-        float p0 = e0 / sum, p1 = e1 / sum;
-        float c0 = fminf(fmaxf(p0, kMinProb), 1.f), c1 = fminf(fmaxf(p1, kMinProb), 1.f);
-        float l0 = in0 ? logf(c0) : 0.f, l1 = in1 ? logf(c1) : 0.f;
-        float ent = -wave_sum((in0 ? l0 * c0 : 0.f) + (in1 ? l1 * c1 : 0.f));
-        int a = __shfl(a_l, i, 64);
-        a = a < 0 ? 0 : (a > A - 1 ? A - 1 : a);
-        float pa = __shfl((a & 1) ? c1 : c0, a >> 1, 64);
-        float lp = logf(pa);
-        float old = __shfl(old_l, i, 64);
-        float ratio = expf(lp - old);
-        float advn = (__shfl(adv_l, i, 64) - mean) / (sd + 1e-8f);
-        float clipped = fminf(fmaxf(ratio, 1.f - clip_range), 1.f + clip_range);
-        float s1 = ratio * advn, s2 = clipped * advn;
-        float pl = fminf(s1, s2);
+    for (int pass = 0; pass < PL_PASSES; pass++) {
+        const int row = blockIdx.x * PL_ROWS + (w * PL_PASSES + pass) * 4 + grp;
+        const bool valid = row < n;
+        const int rowc = valid ? row : n - 1;
+        const int64_t sidx = idx ? (int64_t)idx[start + rowc] : start + rowc;
+        const float* lg = logits + (int64_t)rowc * A;
+        const uint8_t* mk = masks + sidx * A;
+        float z[K];
+        bool in[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int a = i + 16 * k;
+            in[k] = a < A;
+            z[k] = in[k] ? lg[a] + (mk[a] ? 0.f : kDisabledLogit) : -INFINITY;
+        }
+        const int a_raw = actions[sidx];
+        const float old = old_logp[sidx], advr = adv[sidx];
+        float m = z[0];
+#pragma unroll
+        for (int k = 1; k < K; k++) m = fmaxf(m, z[k]);
+        m = grp_max(m);
+        float e[K], esum = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            e[k] = in[k] ? expf(z[k] - m) : 0.f;
+            esum += e[k];
+        }
+        const float sum = grp_sum(esum);
+        float p[K], c[K], lgc[K], ent_l = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            p[k] = e[k] / sum;
+            c[k] = fminf(fmaxf(p[k], kMinProb), 1.f);
+            lgc[k] = in[k] ? logf(c[k]) : 0.f;
+            ent_l += in[k] ? lgc[k] * c[k] : 0.f;
+        }
+        const float ent = -grp_sum(ent_l);
+        const int a = a_raw < 0 ? 0 : (a_raw > A - 1 ? A - 1 : a_raw);
+        // the action's clamped probability: lane a % 16 of the group holds it in slot a / 16
+        float mine = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            if (a == i + 16 * k) mine = c[k];
+        const float pa = __shfl(mine, (lane & ~15) | (a & 15), 64);
+        const float lp = logf(pa);
+        const float ratio = expf(lp - old);
+        const float advn = (advr - mean) / (sd + 1e-8f);
+        const float clipped = fminf(fmaxf(ratio, 1.f - clip_range), 1.f + clip_range);
+        const float s1 = ratio * advn, s2 = clipped * advn;
+        const float pl = fminf(s1, s2);
         // ---- backward (torch semantics: min() ties split the gradient, clamp passes inside [lo, hi])
-        float g_pl = -bsr / (float)n;
-        float g_s1 = s1 < s2 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
-        float g_s2 = s2 < s1 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
-        float in_rng = (ratio >= 1.f - clip_range && ratio <= 1.f + clip_range) ? 1.f : 0.f;
-        float g_ratio = g_s1 * advn + g_s2 * advn * in_rng;
-        float g_lp = g_ratio * ratio;
-        float g_ent = -ent_scale * bsr * inv_log_a / (float)n;  // d loss / d H_i (H_i unnormalised)
-        float d0 = in0 ? -g_ent * (l0 + 1.f) : 0.f, d1 = in1 ? -g_ent * (l1 + 1.f) : 0.f;
-        if (a == a0) d0 += g_lp / c0;
-        if (a == a1) d1 += g_lp / c1;
-        d0 = (p0 >= kMinProb && p0 <= 1.f) ? d0 : 0.f;
-        d1 = (p1 >= kMinProb && p1 <= 1.f) ? d1 : 0.f;
-        float dot = wave_sum((in0 ? d0 * p0 : 0.f) + (in1 ? d1 * p1 : 0.f));
-        float* dl = dlogits + (int64_t)row * A;
-        const float g0 = p0 * (d0 - dot), g1 = p1 * (d1 - dot);
-        if (in0) dl[a0] = g0;
-        if (in1) dl[a1] = g1;
-        col0 += in0 ? g0 : 0.f;
-        col1 += in1 ? g1 : 0.f;
-        const uint32_t b0 = in0 ? mlp::abs_bits(g0) : 0u, b1 = in1 ? mlp::abs_bits(g1) : 0u;
-        vmax = b0 > vmax ? b0 : vmax;
-        vmax = b1 > vmax ? b1 : vmax;
-        float lr = lp - old;
-        m_ent += ent * inv_log_a;
-        m_kl += expf(lr) - 1.f - lr;
-        m_pl += -pl;
-        m_ratio += ratio;
-        m_clip += fabsf(ratio - 1.f) > clip_range ? 1.f : 0.f;
+        const float g_s1 = s1 < s2 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
+        const float g_s2 = s2 < s1 ? g_pl : (s1 == s2 ? g_pl * 0.5f : 0.f);
+        const float in_rng = (ratio >= 1.f - clip_range && ratio <= 1.f + clip_range) ? 1.f : 0.f;
+        const float g_ratio = g_s1 * advn + g_s2 * advn * in_rng;
+        const float g_lp = g_ratio * ratio;
+        float d[K], dot_l = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            d[k] = in[k] ? -g_ent * (lgc[k] + 1.f) : 0.f;
+            if (a == i + 16 * k) d[k] += g_lp / c[k];
+            d[k] = (p[k] >= kMinProb && p[k] <= 1.f) ? d[k] : 0.f;
+            dot_l += in[k] ? d[k] * p[k] : 0.f;
+        }
+        const float dot = grp_sum(dot_l);
+        if (valid) {
+            float* dl = dlogits + (int64_t)row * A;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                if (!in[k]) continue;
+                const float gk = p[k] * (d[k] - dot);
+                dl[i + 16 * k] = gk;
+                col[k] += gk;
+                const uint32_t b = mlp::abs_bits(gk);
+                vmax = b > vmax ? b : vmax;
+            }
+            const float lr = lp - old;
+            m_ent += ent * inv_log_a;
+            m_kl += expf(lr) - 1.f - lr;
+            m_pl += -pl;
+            m_ratio += ratio;
+            m_clip += fabsf(ratio - 1.f) > clip_range ? 1.f : 0.f;
+        }
     }
-    colred[w][a0] = col0;
-    colred[w][a1] = col1;
-    if (lane == 0) {
-        red[w][0] = m_ent;
-        red[w][1] = m_kl;
-        red[w][2] = m_pl;
-        red[w][3] = m_ratio;
-        red[w][4] = m_clip;
+    const int slot = w * 4 + grp;
+#pragma unroll
+    for (int k = 0; k < K; k++) colred[slot][i + 16 * k] = col[k];
+    if (i == 0) {
+        red[slot][0] = m_ent;
+        red[slot][1] = m_kl;
+        red[slot][2] = m_pl;
+        red[slot][3] = m_ratio;
+        red[slot][4] = m_clip;
     }
     __syncthreads();
     if (bias_part)  // output-bias gradient partials of this block's rows: part[blk][A]
-        for (int c = threadIdx.x; c < A; c += 256)
-            bias_part[(int64_t)blockIdx.x * A + c] = colred[0][c] + colred[1][c] + colred[2][c] + colred[3][c];
+        for (int c2 = threadIdx.x; c2 < A; c2 += 256) {
+            float t = 0.f;
+            for (int q = 0; q < 16; q++) t += colred[q][c2];
+            bias_part[(int64_t)blockIdx.x * A + c2] = t;
+        }
     if (threadIdx.x < 5 && metrics) {
-        const int slot[5] = {0, 1, 2, 4, 5};  // entropy, KL, policy loss, ratio, clip fraction
-        float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        atomicAdd(&metrics[slot[threadIdx.x]], v / (float)n);
+        const int mslot[5] = {0, 1, 2, 4, 5};  // entropy, KL, policy loss, ratio, clip fraction
+        float v = 0.f;
+        for (int q = 0; q < 16; q++) v += red[q][threadIdx.x];
+        atomicAdd(&metrics[mslot[threadIdx.x]], v / (float)n);
     }
     if (amax) mlp::h3_amax_commit(amax, vmax);
 }
