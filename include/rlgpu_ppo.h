@@ -96,8 +96,15 @@ int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream);
  * load, broadcasts); the optimizer step does it itself. */
 int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream);
 
+/* Diagnostics: while d_buf != NULL, every fused inference launch writes 16 wall-clock (100 MHz)
+ * phase marks per 64-row workgroup into d_buf (uint64 [workgroups * 16]; tools/infer_trace.py). */
+int rlgpu_debug_infer_trace(void* d_buf);
+
 /* Plain forward of one model on n rows (n <= max_rows): precision 0 = fp32 (training path,
- * no activations kept), 1 = bf16 inference path.  d_out [n, out_size] fp32. */
+ * no activations kept), 1 = bf16 inference path.  d_out [n, out_size] fp32.
+ * The 16-bit inference (this, rlgpu_ppo_infer_actions*, rlgpu_ppo_infer_critic) runs as one fused
+ * kernel per call when every layer fits it (inputs / hidden widths <= 512, outputs <= 128); the
+ * environment variable RLGPU_FUSED_INFER=0 selects the layer-by-layer kernels, same results. */
 int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision, const float* d_in, int32_t n,
                       float* d_out, void* stream);
 

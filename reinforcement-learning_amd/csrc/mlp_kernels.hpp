@@ -1204,6 +1204,42 @@ DEV float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
+// The same butterflies without the LDS crossbar: the xor-32 / xor-16 exchanges by
+// v_permlane32_swap / v_permlane16_swap (both halves of the swap are summed, own + partner in either
+// order), xor 8 / 4 / 2 / 1 by DPP row_ror 8 / 4 / 2 / 1 -- after the wider steps a lane's value
+// depends only on its index modulo twice the distance, where the rotation reaches the xor partner.
+// Every lane combines the same two partial values as in wave_sum / wave_max, so the results are
+// bit-identical.
+DEV float xchg32_sum(float v, bool mx) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float a = __uint_as_float(r[0]), b = __uint_as_float(r[1]);
+    return mx ? fmaxf(a, b) : a + b;
+}
+DEV float xchg16_sum(float v, bool mx) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float a = __uint_as_float(r[0]), b = __uint_as_float(r[1]);
+    return mx ? fmaxf(a, b) : a + b;
+}
+template <int CTRL>
+DEV float dpp_f(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)); }
+DEV float wave_sum_x(float v) {
+    v = xchg32_sum(v, false);
+    v = xchg16_sum(v, false);
+    v += dpp_f<0x128>(v);
+    v += dpp_f<0x124>(v);
+    v += dpp_f<0x122>(v);
+    v += dpp_f<0x121>(v);
+    return v;
+}
+DEV float wave_max_x(float v) {
+    v = xchg32_sum(v, true);
+    v = xchg16_sum(v, true);
+    v = fmaxf(v, dpp_f<0x128>(v));
+    v = fmaxf(v, dpp_f<0x124>(v));
+    v = fmaxf(v, dpp_f<0x122>(v));
+    v = fmaxf(v, dpp_f<0x121>(v));
+    return v;
+}
 
 
 // Column ownership of the wave-per-row kernels: with MAXH >= 4 columns per lane, lane l owns the

@@ -10,6 +10,7 @@
 #include "common.hpp"
 #include "mlp_kernels.hpp"
 #include "ppo_kernels.hpp"
+#include "infer_kernels.hpp"
 
 namespace {
 
@@ -27,6 +28,7 @@ struct Layer {
     int64_t w, b, g, be;      // offsets into the flat fp32 buffers (g/be = -1 without LayerNorm)
     int in_pad;               // bf16 copy: weight rows padded to a multiple of 8 (16 bytes)
     int64_t hw, hb, hg, hbe;  // offsets into the padded bf16 inference copy
+    int64_t fw = -1;          // offset into the fragment-major inference copy (infer::weight_to_frag)
     // three-way bf16 split of the weight for the x6 training GEMMs (offsets into Model::wsplit):
     // forward B = W [out_pad128][in_pad32], backward dA B = W^T [in_pad128][out_pad32]; -1 = none
     int64_t sf = -1, sb = -1;
@@ -105,6 +107,8 @@ struct rlgpu_ppo {
     float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr;
     uint16_t* half = nullptr;
     uint16_t* half_ver = nullptr;  // bf16 policy copy of an old version (self-play), same layout as half
+    uint16_t *frag = nullptr, *frag_ver = nullptr;  // the weights of half / half_ver in MFMA fragment order
+    int64_t nfrag = 0;
     bool has_ver = false;
     // the training GEMMs' split weight planes are stale (parameters changed since the last split):
     // set by init / refresh_half / the optimizer step, cleared when forward_train re-splits.  With
@@ -555,6 +559,61 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, co
     }
 }
 
+// Fused inference (infer::mlp_infer): one launch per forward when every layer fits the kernel's
+// LDS tile (inputs / hidden widths <= 512, outputs <= 128); RLGPU_FUSED_INFER=0 selects the
+// layer-by-layer path (forward_half), which computes the same bits.
+unsigned long long* g_infer_trace = nullptr;  // rlgpu_debug_infer_trace
+bool fused_ok(const rlgpu_ppo* h, int mi) {
+    const char* e = getenv("RLGPU_FUSED_INFER");
+    if (e && atoi(e) == 0) return false;
+    const Model& m = h->M[mi];
+    if ((int)m.L.size() > infer::kMaxLinear) return false;
+    for (size_t l = 0; l < m.L.size(); l++) {
+        if (m.L[l].in > infer::IMAX) return false;
+        if (m.L[l].out > (l + 1 < m.L.size() ? infer::IMAX : infer::IOUT)) return false;
+    }
+    return true;
+}
+
+// one fused forward over n rows of X with the 16-bit copy P: mode 0 writes f32 outputs to out_f,
+// mode 1 samples actions (masks, act, logp; row_sel / sel as ppo::sample_actions)
+void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode, float* out_f,
+                 const uint8_t* masks, int det, uint64_t step, int32_t* act, float* logp, const uint8_t* row_sel, int sel,
+                 hipStream_t s) {
+    const Model& m = h->M[mi];
+    infer::InferArgs a{};
+    a.X = X;
+    a.n = n;
+    a.in = m.in;
+    a.P = ver ? h->half_ver : h->half;
+    a.F = ver ? h->frag_ver : h->frag;
+    a.nl = (int)m.L.size();
+    a.width[0] = m.in;
+    for (int l = 0; l < a.nl; l++) {
+        const Layer& L = m.L[l];
+        a.width[l + 1] = L.out;
+        a.fw[l] = L.fw;
+        a.hb[l] = L.hb;
+        a.hg[l] = L.hg;
+        a.hbe[l] = L.hbe;
+    }
+    a.slope = h->cfg.leaky_slope;
+    a.use_ln = h->cfg.layer_norm;
+    a.mode = mode;
+    a.out_f = out_f;
+    a.masks = masks;
+    a.det = det;
+    a.seed = h->cfg.seed;
+    a.step = step;
+    a.act = act;
+    a.logp = logp;
+    a.row_sel = row_sel;
+    a.sel = sel;
+    a.trace = g_infer_trace;
+    RLGPU_H16_LAUNCH(h->cfg.infer_fp16, infer::mlp_infer, dim3(ceil_div(n, infer::IR)), dim3(infer::IT), 0, s, a);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
 void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, int out, float lr) {
     m.in = in;
     m.out = out;
@@ -584,6 +643,8 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
         L.hb = h->nhalf;
         h->nhalf += L.out;
         L.hg = L.hbe = -1;
+        L.fw = h->nfrag;
+        h->nfrag += infer::frag_size(L.out, L.in);
         if (L.g >= 0) {
             L.hg = h->nhalf;
             h->nhalf += L.out;
@@ -625,9 +686,12 @@ void sumsq_coef(rlgpu_ppo* h, const float* x, int64_t n, float max_norm, float* 
 
 // bf16 inference copy of model mi from `src` (the model's flat fp32 parameters, torch order) into
 // the padded layout at `dst` (h->half or h->half_ver)
-void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, hipStream_t s) {
+void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, uint16_t* fdst, hipStream_t s) {
     const Model& m = h->M[mi];
     for (auto& L : m.L) {
+        const int64_t nf = infer::frag_size(L.out, L.in);
+        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, infer::weight_to_frag, dim3(ceil_div(nf, 256)), dim3(256), 0, s, src + (L.w - m.off),
+                         L.out, L.in, fdst + L.fw);
         int64_t e = (int64_t)L.out * L.in_pad;
         RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, src + (L.w - m.off), L.out, L.in,
                            dst + L.hw, L.in_pad);
@@ -639,7 +703,7 @@ void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, hipStream_
 }
 
 void refresh_half(rlgpu_ppo* h, hipStream_t s) {
-    for (int mi = 0; mi < 2; mi++) half_from(h, mi, h->params + h->M[mi].off, h->half, s);
+    for (int mi = 0; mi < 2; mi++) half_from(h, mi, h->params + h->M[mi].off, h->half, h->frag, s);
     h->split_dirty[0] = h->split_dirty[1] = true;
 }
 
@@ -671,6 +735,8 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             h->exp_avg_sq = h->alloc<float>(P);
             h->half = h->alloc<uint16_t>(h->nhalf + 8);
             h->half_ver = h->alloc<uint16_t>(h->nhalf + 8);
+            h->frag = h->alloc<uint16_t>(h->nfrag);
+            h->frag_ver = h->alloc<uint16_t>(h->nfrag);
             RLGPU_CHECK_HIP(hipMemset(h->params, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->grads, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->exp_avg, 0, P * 4));
@@ -814,6 +880,8 @@ extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision,
         if (precision == 0) {
             gather_obs(h, d_in, nullptr, 0, n, s);
             forward_train(h, model, h->x0, n, d_out, s);
+        } else if (fused_ok(h, model)) {
+            infer_fused(h, model, false, d_in, n, 0, d_out, nullptr, 0, 0, nullptr, nullptr, nullptr, 0, s);
         } else {
             forward_half(h, model, d_in, n, s);
             int64_t e = (int64_t)n * h->M[model].out;
@@ -833,6 +901,11 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
         int R = h->cfg.max_rows;
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
+            if (fused_ok(h, 0)) {
+                infer_fused(h, 0, false, d_obs + b * h->cfg.obs_size, m, 1, nullptr, d_masks + b * h->cfg.num_actions,
+                            deterministic, rng_step, d_actions + b, d_logp ? d_logp + b : nullptr, nullptr, 0, s);
+                continue;
+            }
             forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s);
             RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
@@ -842,10 +915,15 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
     });
 }
 
+extern "C" int rlgpu_debug_infer_trace(void* d_buf) {
+    g_infer_trace = (unsigned long long*)d_buf;
+    return 0;
+}
+
 extern "C" int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h && d_policy_params, "rlgpu_ppo_set_version: null argument");
-        half_from(h, 0, d_policy_params, h->half_ver, rlgpu::as_stream(stream));
+        half_from(h, 0, d_policy_params, h->half_ver, h->frag_ver, rlgpu::as_stream(stream));
         h->has_ver = true;
     });
 }
@@ -862,6 +940,12 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
             for (int old = 0; old < 2; old++) {  // current policy rows, then the old version's rows
+                if (fused_ok(h, 0)) {
+                    infer_fused(h, 0, old != 0, d_obs + b * h->cfg.obs_size, m, 1, nullptr,
+                                d_masks + b * h->cfg.num_actions, deterministic, rng_step, d_actions + b,
+                                (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old, s);
+                    continue;
+                }
                 forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s, old ? h->half_ver : h->half);
                 RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                    d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
@@ -876,9 +960,15 @@ extern "C" int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t 
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h && d_obs && d_values, "null argument");
         hipStream_t s = rlgpu::as_stream(stream);
-        int R = h->cfg.max_rows;
+        // the fused kernel keeps no per-row buffers: one launch over up to 2^30 rows (no max_rows chunks)
+        const int64_t R = fused_ok(h, 1) ? (int64_t)1 << 30 : h->cfg.max_rows;
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
+            if (fused_ok(h, 1)) {
+                infer_fused(h, 1, false, d_obs + b * h->cfg.obs_size, m, 0, d_values + b, nullptr, 0, 0, nullptr, nullptr,
+                            nullptr, 0, s);
+                continue;
+            }
             forward_half(h, 1, d_obs + b * h->cfg.obs_size, m, s);
             RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(m, 256)), dim3(256), 0, s, h->logits_h, d_values + b,
                                (int64_t)m);

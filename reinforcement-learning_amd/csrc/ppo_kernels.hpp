@@ -47,6 +47,101 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 // InferActions: logits bf16 [n, A] -> action (int32), log prob.  Inverse-CDF multinomial on the
 // clamped probs (torch.multinomial normalises by their sum); argmax when deterministic.
 // row_sel (optional): only rows with (row_sel[row] != 0) == sel are written (mixed-policy inference).
+// RG rows, one wave, interleaved (each cross-lane step issues for all RG rows before the next, so
+// one wave hides the shuffle latency of RG independent rows): lg[g] = row g's A logits (global or
+// LDS), mk[g] its masks; writes act[row[g]], logp[row[g]] where ok[g].  sample_actions runs it with
+// RG = 1, the fused inference kernel (infer_kernels.hpp) with RG = 8 -- the per-row arithmetic is the
+// same, so both draw the same actions from the same logits.
+template <int RG, bool F16>
+__device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], const uint8_t* const (&mk)[RG], int A,
+                                            int deterministic, uint64_t seed, uint64_t step, const int (&row)[RG],
+                                            const bool (&ok)[RG], int lane, int32_t* act, float* logp) {
+    const int a0 = 2 * lane, a1 = 2 * lane + 1;
+    const bool in0 = a0 < A, in1 = a1 < A;
+    float z0[RG], z1[RG], m[RG], s[RG], p0[RG], p1[RG];
+    int pick[RG];
+#pragma unroll
+    for (int g = 0; g < RG; g++) {
+        z0[g] = in0 ? mlp::h2f<F16>(lg[g][a0]) + (mk[g][a0] ? 0.f : kDisabledLogit) : 0.f;
+        z1[g] = in1 ? mlp::h2f<F16>(lg[g][a1]) + (mk[g][a1] ? 0.f : kDisabledLogit) : 0.f;
+        // softmax over all A columns (masked ones carry -1e10, exactly as the reference)
+        m[g] = fmaxf(in0 ? z0[g] : -INFINITY, in1 ? z1[g] : -INFINITY);
+    }
+#pragma unroll
+    for (int g = 0; g < RG; g++) m[g] = mlp::wave_max_x(m[g]);
+#pragma unroll
+    for (int g = 0; g < RG; g++) {
+        z0[g] = in0 ? __expf(z0[g] - m[g]) : 0.f;  // e0, e1
+        z1[g] = in1 ? __expf(z1[g] - m[g]) : 0.f;
+        s[g] = z0[g] + z1[g];
+    }
+#pragma unroll
+    for (int g = 0; g < RG; g++) s[g] = mlp::wave_sum_x(s[g]);
+#pragma unroll
+    for (int g = 0; g < RG; g++) {
+        p0[g] = in0 ? fminf(fmaxf(z0[g] / s[g], kMinProb), 1.f) : 0.f;
+        p1[g] = in1 ? fminf(fmaxf(z1[g] / s[g], kMinProb), 1.f) : 0.f;
+    }
+    if (deterministic) {
+        float best[RG];
+        int bi[RG];
+#pragma unroll
+        for (int g = 0; g < RG; g++) {
+            best[g] = fmaxf(p0[g], p1[g]);
+            bi[g] = p0[g] >= p1[g] ? a0 : a1;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int g = 0; g < RG; g++) {
+                float ob = __shfl_xor(best[g], o, 64);
+                int oi = __shfl_xor(bi[g], o, 64);
+                if (ob > best[g] || (ob == best[g] && oi < bi[g])) {
+                    best[g] = ob;
+                    bi[g] = oi;
+                }
+            }
+#pragma unroll
+        for (int g = 0; g < RG; g++) pick[g] = bi[g];
+    } else {
+        float pair[RG], inc[RG];
+#pragma unroll
+        for (int g = 0; g < RG; g++) inc[g] = pair[g] = p0[g] + p1[g];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1)
+#pragma unroll
+            for (int g = 0; g < RG; g++) {
+                float up = __shfl_up(inc[g], o, 64);
+                if (lane >= o) inc[g] += up;
+            }
+        // the rows' uniform draws: lane g computes row g's (one philox per row, not per lane)
+        int myrow = row[0];
+#pragma unroll
+        for (int g = 1; g < RG; g++) myrow = lane == g ? row[g] : myrow;
+        const uint32_t ph = philox(seed, (uint32_t)myrow, (uint32_t)step);
+#pragma unroll
+        for (int g = 0; g < RG; g++) {
+            float total = __shfl(inc[g], 63, 64);
+            float u = (float)((uint32_t)__builtin_amdgcn_readlane((int)ph, g) >> 8) * (1.f / 16777216.f) * total;
+            float excl = inc[g] - pair[g];
+            bool hit = (u < inc[g]) && (u >= excl) && pair[g] > 0.f;
+            const unsigned long long bal = __ballot(hit), nz = __ballot(pair[g] > 0.f);
+            // no hit: u landed past the last positive pair by rounding -- take the last valid action
+            const int lsel = bal ? __ffsll((long long)bal) - 1 : 63 - __clzll((long long)nz);
+            int c = 2 * lsel;
+            float e = __shfl(excl, lsel, 64), q0 = __shfl(p0[g], lsel, 64), q1 = __shfl(p1[g], lsel, 64);
+            pick[g] = (u < e + q0 || q1 == 0.f) ? c : c + 1;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < RG; g++) {
+        float pp0 = __shfl(p0[g], pick[g] >> 1, 64), pp1 = __shfl(p1[g], pick[g] >> 1, 64);
+        if (lane == 0 && ok[g]) {
+            act[row[g]] = pick[g];
+            if (logp) logp[row[g]] = __logf((pick[g] & 1) ? pp1 : pp0);
+        }
+    }
+}
 template <bool F16>
 __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
                                                      int deterministic, uint64_t seed, uint64_t step, int32_t* act,
@@ -54,56 +149,11 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
     int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= n) return;
     if (row_sel && ((row_sel[row] != 0) != (sel != 0))) return;
-    int a0 = 2 * lane, a1 = 2 * lane + 1;
-    const uint16_t* lg = logits + (int64_t)row * A;
-    const uint8_t* mk = masks + (int64_t)row * A;
-    bool in0 = a0 < A, in1 = a1 < A;
-    float z0 = in0 ? mlp::h2f<F16>(lg[a0]) + (mk[a0] ? 0.f : kDisabledLogit) : 0.f;
-    float z1 = in1 ? mlp::h2f<F16>(lg[a1]) + (mk[a1] ? 0.f : kDisabledLogit) : 0.f;
-    // softmax over all A columns (masked ones carry -1e10, exactly as the reference)
-    float m = wave_max(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
-    float e0 = in0 ? __expf(z0 - m) : 0.f, e1 = in1 ? __expf(z1 - m) : 0.f;
-    float s = wave_sum(e0 + e1);
-    float p0 = in0 ? fminf(fmaxf(e0 / s, kMinProb), 1.f) : 0.f;
-    float p1 = in1 ? fminf(fmaxf(e1 / s, kMinProb), 1.f) : 0.f;
-    int pick;
-    if (deterministic) {
-        float best = fmaxf(p0, p1);
-        int bi = p0 >= p1 ? a0 : a1;
-        for (int o = 32; o > 0; o >>= 1) {
-            float ob = __shfl_xor(best, o, 64);
-            int oi = __shfl_xor(bi, o, 64);
-            if (ob > best || (ob == best && oi < bi)) {
-                best = ob;
-                bi = oi;
-            }
-        }
-        pick = bi;
-    } else {
-        float pair = p0 + p1, inc = pair;
-        for (int o = 1; o < 64; o <<= 1) {
-            float up = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += up;
-        }
-        float total = __shfl(inc, 63, 64);
-        float u = (float)(philox(seed, (uint32_t)row, (uint32_t)step) >> 8) * (1.f / 16777216.f) * total;
-        float excl = inc - pair;
-        bool hit = (u < inc) && (u >= excl) && pair > 0.f;
-        unsigned long long bal = __ballot(hit);
-        int lsel = bal ? __ffsll((long long)bal) - 1 : 0;
-        if (!bal) {  // u landed past the last positive pair by rounding: take the last valid action
-            unsigned long long nz = __ballot(pair > 0.f);
-            lsel = 63 - __clzll((long long)nz);
-        }
-        int c = 2 * lsel;
-        float e = __shfl(excl, lsel, 64), q0 = __shfl(p0, lsel, 64), q1 = __shfl(p1, lsel, 64);
-        pick = (u < e + q0 || q1 == 0.f) ? c : c + 1;
-    }
-    float pp0 = __shfl(p0, pick >> 1, 64), pp1 = __shfl(p1, pick >> 1, 64);
-    if (lane == 0) {
-        act[row] = pick;
-        if (logp) logp[row] = __logf((pick & 1) ? pp1 : pp0);
-    }
+    const uint16_t* const lg[1] = {logits + (int64_t)row * A};
+    const uint8_t* const mk[1] = {masks + (int64_t)row * A};
+    const int rw[1] = {row};
+    const bool ok[1] = {true};
+    sample_rows<1, F16>(lg, mk, A, deterministic, seed, step, rw, ok, lane, act, logp);
 }
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.

@@ -232,6 +232,48 @@ def test_infer_actions_respect_masks_and_distribution(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layers,ln,fp16,n,rows", [((512, 512), True, False, 16384 + 37, 16384 + 37),
+                                                   ((512, 512), True, True, 1000, 1000),
+                                                   ((40, 72, 130), True, False, 777, 300),
+                                                   ((256,), False, False, 300, 300),
+                                                   ((96, 200, 512), True, True, 129, 129)])
+def test_fused_inference_matches_layer_path(gpu, monkeypatch, layers, ln, fp16, n, rows):
+    """infer::mlp_infer (one launch per forward) against the layer-by-layer path forward_half ->
+    sample_actions (RLGPU_FUSED_INFER=0): the same MFMA instruction over the same K order, the same
+    roundings and the same sampler, so logits, critic values, actions and log probs are bit-identical
+    -- for odd widths (LDS zero padding), without LayerNorm, in fp16 and bf16, for row counts off the
+    64-row workgroup tile, and for the mixed-version (self-play) inference.  With n > max_rows the
+    layer path works in max_rows chunks and the fused critic in one launch."""
+    import torch
+    from rlgpu.ppo import PPO
+    p = PPO(policy_layers=layers, critic_layers=layers, layer_norm=ln, max_rows=rows, seed=11, infer_fp16=fp16)
+    rng = np.random.default_rng(n)
+    obs, masks, *_ = make_batch(rng, n)
+    o, m = torch.from_numpy(obs).to(gpu), torch.from_numpy(masks).to(gpu)
+    old_rows = torch.from_numpy((rng.random(n) < 0.5).astype(np.uint8)).to(gpu)
+    p.set_version(p.model_slice(0) * 0.5)
+
+    def run():
+        torch.cuda.synchronize()
+        res = [p.forward(0, o[:rows], half=True).cpu(), p.infer_critic(o).cpu()]
+        for det in (False, True):
+            a, lp = p.infer_actions(o, m, step=5, deterministic=det)
+            res += [a.cpu(), lp.cpu()]
+        a, lp = p.infer_actions_mixed(o, m, old_rows, step=9)
+        res += [a.cpu(), lp.cpu()]
+        torch.cuda.synchronize()
+        return res
+
+    fused = run()
+    monkeypatch.setenv("RLGPU_FUSED_INFER", "0")
+    layer = run()
+    names = ["logits", "values", "actions", "logp", "argmax", "logp_det", "mixed_actions", "mixed_logp"]
+    for nm, f, l in zip(names, fused, layer):
+        assert torch.equal(f, l), (nm, (f != l).sum().item())
+    assert (masks[np.arange(n), fused[2].numpy()] == 1).all()
+
+
+@pytest.mark.gpu
 def test_mean_std(gpu):
     import torch
     from rlgpu.ppo import PPO
