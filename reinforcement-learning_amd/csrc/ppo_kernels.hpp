@@ -60,10 +60,13 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
     const bool in0 = a0 < A, in1 = a1 < A;
     float z0[RG], z1[RG], m[RG], s[RG], p0[RG], p1[RG];
     int pick[RG];
+    const int c0 = min(a0, A - 1), c1 = min(a1, A - 1);  // loads stay unconditional (no branches between them)
 #pragma unroll
     for (int g = 0; g < RG; g++) {
-        z0[g] = in0 ? mlp::h2f<F16>(lg[g][a0]) + (mk[g][a0] ? 0.f : kDisabledLogit) : 0.f;
-        z1[g] = in1 ? mlp::h2f<F16>(lg[g][a1]) + (mk[g][a1] ? 0.f : kDisabledLogit) : 0.f;
+        const float l0 = mlp::h2f<F16>(lg[g][c0]), l1 = mlp::h2f<F16>(lg[g][c1]);
+        const uint8_t m0 = mk[g][c0], m1 = mk[g][c1];
+        z0[g] = in0 ? l0 + (m0 ? 0.f : kDisabledLogit) : 0.f;
+        z1[g] = in1 ? l1 + (m1 ? 0.f : kDisabledLogit) : 0.f;
         // softmax over all A columns (masked ones carry -1e10, exactly as the reference)
         m[g] = fmaxf(in0 ? z0[g] : -INFINITY, in1 ? z1[g] : -INFINITY);
     }
@@ -96,10 +99,9 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
             for (int g = 0; g < RG; g++) {
                 float ob = __shfl_xor(best[g], o, 64);
                 int oi = __shfl_xor(bi[g], o, 64);
-                if (ob > best[g] || (ob == best[g] && oi < bi[g])) {
-                    best[g] = ob;
-                    bi[g] = oi;
-                }
+                const bool take = ob > best[g] || (ob == best[g] && oi < bi[g]);
+                best[g] = take ? ob : best[g];
+                bi[g] = take ? oi : bi[g];
             }
 #pragma unroll
         for (int g = 0; g < RG; g++) pick[g] = bi[g];
@@ -114,15 +116,10 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
                 float up = __shfl_up(inc[g], o, 64);
                 if (lane >= o) inc[g] += up;
             }
-        // the rows' uniform draws: lane g computes row g's (one philox per row, not per lane)
-        int myrow = row[0];
-#pragma unroll
-        for (int g = 1; g < RG; g++) myrow = lane == g ? row[g] : myrow;
-        const uint32_t ph = philox(seed, (uint32_t)myrow, (uint32_t)step);
 #pragma unroll
         for (int g = 0; g < RG; g++) {
             float total = __shfl(inc[g], 63, 64);
-            float u = (float)((uint32_t)__builtin_amdgcn_readlane((int)ph, g) >> 8) * (1.f / 16777216.f) * total;
+            float u = (float)(philox(seed, (uint32_t)row[g], (uint32_t)step) >> 8) * (1.f / 16777216.f) * total;
             float excl = inc[g] - pair[g];
             bool hit = (u < inc[g]) && (u >= excl) && pair[g] > 0.f;
             const unsigned long long bal = __ballot(hit), nz = __ballot(pair[g] > 0.f);
