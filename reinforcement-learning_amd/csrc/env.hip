@@ -42,7 +42,6 @@ struct StepArgs {
     MeshView mesh;
 };
 
-DEV void sync() { __syncthreads(); }
 
 // The boost-pad constants a lane tests every tick (pads l, l + 16, l + 32), held in registers for
 // the whole launch instead of re-read from the constant buffer with lane-varying addresses in every
@@ -162,8 +161,9 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
     if (valid && l == 0) {
         commit_contacts(A, &P);
         if (threadIdx.x == 0) P.mark(16);
-        solve(A, &P);
     }
+    sync();
+    solve_lanes(A, l, valid, &P);
     sync();
     P.mark(6);
     if (valid && l < 5) {  // integrateTransforms (btDiscreteDynamicsWorld.cpp:889-985)

@@ -648,11 +648,13 @@ DEV void setup_contact(ArenaLDS* A, Solver& S, CRow& row, int ia, int ib, const 
     float restitution = fabsf(rel_vel) < 0.2f ? 0.f : cp.restitution * -rel_vel;
     if (restitution <= 0.f) restitution = 0.f;
     row.applied = cp.applied * 0.85f;
-    if (r0) {
+    // warm start (a fresh point's applied impulse is 0: adding the zero product leaves the +0 deltas
+    // unchanged, so it is skipped and rows can be set up concurrently)
+    if (r0 && row.applied != 0.f) {
         Sa.dlin += row.n1 * v3{Sa.inv_mass, Sa.inv_mass, Sa.inv_mass} * row.applied;
         Sa.dang += row.angA * row.applied;
     }
-    if (r1) {
+    if (r1 && row.applied != 0.f) {
         Sb.dlin += (-row.n2 * v3{Sb.inv_mass, Sb.inv_mass, Sb.inv_mass}) * -row.applied;
         Sb.dang += -row.angB * -row.applied;
     }
@@ -786,13 +788,28 @@ DEV float resolve_split(Solver& S, CRow& c) {
     return di * (1.f / c.jinv);
 }
 
-// btSequentialImpulseConstraintSolver::solveGroup (single lane per arena)
-DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
+// max over the 16 lanes of an arena (xor partners stay inside the 16-lane group)
+DEV float group16_max(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v = stdmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// btSequentialImpulseConstraintSolver::solveGroup on the 16 lanes of an arena.
+// Bullet sweeps the rows in order (Gauss-Seidel), and a row reads and writes only the velocity
+// deltas of its own two bodies.  Lane 0 gives row r the level 1 + max(level of the last earlier row
+// sharing a dynamic body with it); level L's rows then run concurrently, row r on lane r
+// (kMaxRows <= 16), after level L - 1's.  Every body therefore receives its updates in the
+// sequential order, from the same operands: the same bits as the one-lane sweep, in as many steps
+// as the longest chain of rows on one body instead of one step per row.  Rows are set up
+// concurrently too (independent: a fresh point's warm start is zero), bodies one per lane.
+// Called by all threads of the workgroup (it synchronises); `valid`: this lane's arena exists.
+DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
     Solver& S = A->u.sv;
-    unsigned in_solver = 0;  // bit i: body i takes part (bitmask: no private-memory array)
-    for (int i = 0; i < 5; i++) {
+    static_assert(kMaxRows <= kTeam, "one lane per solver row");
+    if (valid && l < 5) {  // bodies (btSolverBody init), one per lane
+        const int i = l;
         bool act = i == 0 ? A->a.ball_awake != 0 : A->a.active[i] != 0;
-        if (act) in_solver |= 1u << i;
         SB& x = S.sb[i];
         x.dlin = x.dang = x.push = x.turn = zero3();
         x.real = act;
@@ -812,115 +829,180 @@ DEV void solve(ArenaLDS* A, Prof* P = nullptr) {
         S.spec_rest[i] = 0;
         S.spec_d[i] = 0;
         S.spec_n[i] = zero3();
-    }
-    {
+    } else if (valid && l == 5) {
         SB& f = S.sb[5];
         f.dlin = f.dang = f.push = f.turn = f.lin = f.ang = f.ext_f = f.ext_t = zero3();
         f.inv_mass = 0.f;
         f.real = 0;
     }
+    sync();
     pmark(P, 19);
-    int nrows = 0;
-    // manifolds in creation order = ascending key order (Bullet: dispatcher manifold order)
-    for (int mi = 0; mi < A->a.nmf; mi++) {
-        rlgpu_manifold& mf = A->mf[mi];
-        if (mf.count == 0) continue;
+    if (valid && l == 0) {  // the rows' (manifold, point) in creation order; the special-point sums
+        unsigned in_solver = 0;
+        for (int i = 0; i < 5; i++)
+            if (S.sb[i].real) in_solver |= 1u << i;
+        S.in_solver = in_solver;
+        int nrows = 0;
+        for (int mi = 0; mi < A->a.nmf; mi++) {
+            rlgpu_manifold& mf = A->mf[mi];
+            if (mf.count == 0) continue;
+            int a, b;
+            key_bodies(mf.key, a, b);
+            bool aact = a < 10 && ((in_solver >> a) & 1u);
+            bool bact = b < 10 && ((in_solver >> b) & 1u);
+            if (!aact && !bact) continue;
+            for (int j = 0; j < mf.count; j++) {
+                if (nrows >= kMaxRows) {
+                    A->s.env.manifold_overflow++;
+                    continue;
+                }
+                rlgpu_contact& cp = mf.pts[j];
+                if (cp.special) {
+                    v3 pa_, pb_;
+                    m3 ra, rb;
+                    side_transform(A, a, pa_, ra);
+                    side_transform(A, b, pb_, rb);
+                    v3 wa = ra * ld3(cp.localA) + pa_;
+                    v3 wb = rb * ld3(cp.localB) + pb_;
+                    v3 rel1 = wa - pa_;
+                    v3 rel2 = wb - (b >= 10 ? zero3() : pb_);
+                    for (int side = 0; side < 2; side++) {
+                        int bid = side ? b : a;
+                        if (bid < 10) {
+                            S.spec_num[bid]++;
+                            S.spec_fric[bid] = cp.friction;
+                            S.spec_rest[bid] = cp.restitution;
+                            S.spec_n[bid] += ld3(cp.normalB);
+                            S.spec_d[bid] += len(side ? rel2 : rel1);
+                        }
+                    }
+                }
+                S.rmf[nrows] = (int8_t)mi;
+                S.rpt[nrows] = (int8_t)j;
+                nrows++;
+            }
+        }
+        S.nmrows = nrows;
+        for (int i = 0; i < 5; i++) {  // the averaged special rows, after the manifold rows
+            if (S.spec_num[i] <= 0 || !((in_solver >> i) & 1u)) continue;
+            if (nrows >= kMaxRows) {
+                A->s.env.manifold_overflow++;
+                continue;
+            }
+            float distance = S.spec_d[i] / S.spec_num[i];
+            v3 normal = S.spec_n[i] / (float)S.spec_num[i];
+            rlgpu_contact tmp;
+            st3(tmp.localA, zero3());
+            st3(tmp.localB, zero3());
+            st3(tmp.normalB, normal);
+            tmp.dist = distance;
+            tmp.applied = 0.f;
+            tmp.friction = S.spec_fric[i];
+            tmp.restitution = S.spec_rest[i];
+            tmp.special = 0;
+            v3 rel1 = normal * -distance, rel2 = zero3();
+            CRow& row = S.rows[nrows];
+            row.a = i;
+            row.b = 5;
+            row.special = 0;
+            setup_contact(A, S, row, i, 5, tmp, rel1, rel2, distance);
+            add_friction(A, S, i, 5, tmp, rel1, rel2, nrows, tmp.friction);
+            nrows++;
+        }
+        S.nrows = nrows;
+    }
+    sync();
+    if (valid && l < S.nmrows) {  // manifold row l
+        const unsigned in_solver = S.in_solver;
+        rlgpu_manifold& mf = A->mf[S.rmf[l]];
         int a, b;
         key_bodies(mf.key, a, b);
         bool aact = a < 10 && ((in_solver >> a) & 1u);
         bool bact = b < 10 && ((in_solver >> b) & 1u);
-        if (!aact && !bact) continue;
         int ia = aact ? a : 5, ib = bact ? b : 5;
         v3 pa_, pb_;
         m3 ra, rb;
         side_transform(A, a, pa_, ra);
         side_transform(A, b, pb_, rb);
-        for (int j = 0; j < mf.count; j++) {
-            if (nrows >= kMaxRows) {
-                A->s.env.manifold_overflow++;
-                continue;
-            }
-            rlgpu_contact& cp = mf.pts[j];
-            v3 wa = ra * ld3(cp.localA) + pa_;
-            v3 wb = rb * ld3(cp.localB) + pb_;
-            v3 rel1 = wa - pa_;
-            v3 rel2 = wb - (b >= 10 ? zero3() : pb_);
-            CRow& row = S.rows[nrows];
-            row.a = ia;
-            row.b = ib;
-            row.special = cp.special != 0;
-            setup_contact(A, S, row, ia, ib, cp, rel1, rel2, cp.dist);
-            if (cp.special) {
-                for (int side = 0; side < 2; side++) {
-                    int bid = side ? b : a;
-                    if (bid < 10) {
-                        S.spec_num[bid]++;
-                        S.spec_fric[bid] = cp.friction;
-                        S.spec_rest[bid] = cp.restitution;
-                        S.spec_n[bid] += ld3(cp.normalB);
-                        S.spec_d[bid] += len(side ? rel2 : rel1);
-                    }
-                }
-            }
-            add_friction(A, S, ia, ib, cp, rel1, rel2, nrows, cp.friction);
-            nrows++;
-        }
+        rlgpu_contact& cp = mf.pts[S.rpt[l]];
+        v3 wa = ra * ld3(cp.localA) + pa_;
+        v3 wb = rb * ld3(cp.localB) + pb_;
+        v3 rel1 = wa - pa_;
+        v3 rel2 = wb - (b >= 10 ? zero3() : pb_);
+        CRow& row = S.rows[l];
+        row.a = ia;
+        row.b = ib;
+        row.special = cp.special != 0;
+        setup_contact(A, S, row, ia, ib, cp, rel1, rel2, cp.dist);
+        add_friction(A, S, ia, ib, cp, rel1, rel2, l, cp.friction);
     }
-    for (int i = 0; i < 5; i++) {
-        if (S.spec_num[i] <= 0 || !((in_solver >> i) & 1u)) continue;
-        if (nrows >= kMaxRows) {
-            A->s.env.manifold_overflow++;
-            continue;
+    sync();
+    if (valid && l == 0) {  // sweep levels
+        for (int i = 0; i < 6; i++) S.blev[i] = -1;
+        int nlev = 0;
+        for (int r = 0; r < S.nrows; r++) {
+            const int a = S.rows[r].a, b = S.rows[r].b;  // 5 = static / inactive: never written
+            const int lv = stdmax(a < 5 ? S.blev[a] : -1, b < 5 ? S.blev[b] : -1) + 1;
+            S.lvl[r] = (int8_t)lv;
+            if (a < 5) S.blev[a] = lv;
+            if (b < 5) S.blev[b] = lv;
+            nlev = stdmax(nlev, lv + 1);
         }
-        float distance = S.spec_d[i] / S.spec_num[i];
-        v3 normal = S.spec_n[i] / (float)S.spec_num[i];
-        rlgpu_contact tmp;
-        st3(tmp.localA, zero3());
-        st3(tmp.localB, zero3());
-        st3(tmp.normalB, normal);
-        tmp.dist = distance;
-        tmp.applied = 0.f;
-        tmp.friction = S.spec_fric[i];
-        tmp.restitution = S.spec_rest[i];
-        tmp.special = 0;
-        v3 rel1 = normal * -distance, rel2 = zero3();
-        CRow& row = S.rows[nrows];
-        row.a = i;
-        row.b = 5;
-        row.special = 0;
-        setup_contact(A, S, row, i, 5, tmp, rel1, rel2, distance);
-        add_friction(A, S, i, 5, tmp, rel1, rel2, nrows, tmp.friction);
-        nrows++;
+        S.nlev = nlev;
     }
+    sync();
     pmark(P, 20);
+    int nlev = valid ? S.nlev : 0;  // workgroup-uniform: the max over its arenas
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nlev = stdmax(nlev, __shfl_xor(nlev, o, 64));
+    const bool mine = valid && l < S.nrows;
+    const int lv = mine ? S.lvl[l] : -1;
+    // this lane's contact and friction rows stay in registers for the sweeps (only the bodies'
+    // deltas travel through LDS); the impulses they accumulate die with the tick
+    CRow cr;
+    FRow fr;
+    if (mine) {
+        cr = S.rows[l];
+        fr = S.frows[l];
+    }
+    // split-impulse iterations (solveGroupCacheFriendlySplitImpulseIterations): until no row pushes
+    bool done = !valid;
     for (int it = 0; it < 10; it++) {
         float lsr = 0.f;
-        for (int r = 0; r < nrows; r++) {
-            float res = resolve_split(S, S.rows[r]);
-            lsr = stdmax(lsr, res * res);
-        }
-        if (lsr <= 0.f || it >= 9) break;
-    }
-    for (int it = 0; it < 10; it++) {
-        for (int r = 0; r < nrows; r++) {
-            CRow& row = S.rows[r];
-            if (row.special) continue;
-            resolve_row(S, row, 0.f, 1e10f, false);
-        }
-        for (int r = 0; r < nrows; r++) {
-            FRow& f = S.frows[r];
-            float total = S.rows[f.cidx].applied;
-            if (total > 0.f) {
-                f.lower = -(f.friction * total);
-                f.upper = f.friction * total;
-                resolve_row(S, f, f.lower, f.upper, true);
+        for (int L = 0; L < nlev; L++) {
+            if (!done && lv == L) {
+                float res = resolve_split(S, cr);
+                lsr = stdmax(lsr, res * res);
             }
+            sync();
+        }
+        lsr = group16_max(lsr);
+        if (lsr <= 0.f || it >= 9) done = true;
+        if (__all(done)) break;
+    }
+    // velocity iterations: every contact row, then every friction row (bounded by its contact's impulse)
+    const bool special = mine && cr.special;
+    for (int it = 0; it < 10; it++) {
+        for (int L = 0; L < nlev; L++) {
+            if (lv == L && !special) resolve_row(S, cr, 0.f, 1e10f, false);
+            sync();
+        }
+        for (int L = 0; L < nlev; L++) {
+            if (lv == L) {
+                float total = cr.applied;  // frows[l].cidx == l
+                if (total > 0.f) {
+                    fr.lower = -(fr.friction * total);
+                    fr.upper = fr.friction * total;
+                    resolve_row(S, fr, fr.lower, fr.upper, true);
+                }
+            }
+            sync();
         }
     }
     pmark(P, 21);
     // (the applied impulses are not written back: the manifolds die with this tick)
-    for (int i = 0; i < 5; i++) {
-        if (!((in_solver >> i) & 1u)) continue;
+    if (valid && l < 5 && ((S.in_solver >> l) & 1u)) {  // one body per lane
+        const int i = l;
         SB& x = S.sb[i];
         rlgpu_body* bd = body(A, i);
         x.lin += x.dlin;

@@ -118,6 +118,12 @@ struct Solver {
     CRow rows[kMaxRows];
     FRow frows[kMaxRows];
     int nrows;
+    int nmrows;                   // rows from manifold points (the first nmrows)
+    int nlev;                     // sweep levels (solve_lanes)
+    unsigned in_solver;           // bit i: body i takes part
+    int blev[6];                  // level scan: last level that touched each body
+    int8_t rmf[kMaxRows], rpt[kMaxRows];  // row -> (manifold, point)
+    int8_t lvl[kMaxRows];         // row -> sweep level
     int spec_num[5];
     float spec_fric[5], spec_rest[5], spec_d[5];
     v3 spec_n[5];
@@ -159,14 +165,22 @@ struct alignas(16) ArenaLDS {
 };
 
 // Optional per-phase cycle accounting (StepArgs::prof != null): thread 0 of every workgroup adds
-// the s_memtime delta since the previous mark to prof[phase].  Used by tools/env_phase_profile.py.
+// the s_memtime delta since the previous mark to prof[phase] (all workgroups) and to
+// prof[kProfWG + blockIdx.x * kProfPhases + phase] (this workgroup: the kernel ends with its slowest
+// workgroup, so the spread matters as much as the mean).  Used by tools/env_phase_profile.py.
+constexpr int kProfPhases = 24, kProfWG = 64;
+// workgroup barrier (a workgroup is one wave of 4 arenas): LDS writes before it are visible after it
+__device__ __forceinline__ void sync() { __syncthreads(); }
 struct Prof {
     unsigned long long* p;
     long long t;
     __device__ __forceinline__ void mark(int k) {
         if (p) {
             long long now = clock64();
-            if (threadIdx.x == 0) atomicAdd(&p[k], (unsigned long long)(now - t));
+            if (threadIdx.x == 0) {
+                atomicAdd(&p[k], (unsigned long long)(now - t));
+                p[kProfWG + (size_t)blockIdx.x * kProfPhases + k] += (unsigned long long)(now - t);
+            }
             t = now;
         }
     }

@@ -24,7 +24,10 @@ acts = torch.empty(4 * n, dtype=torch.int32, device=dev)
 for i in range(warm):
     acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
     env.step(acts, True)
-prof = torch.zeros(32, dtype=torch.int64, device=dev)
+wg = (n + 3) // 4
+KP, KW = 24, 64  # env_kernel.hpp kProfPhases, kProfWG
+prof = torch.zeros(KW + wg * KP, dtype=torch.int64, device=dev)
+spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
 L = _lib.lib()
 L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 _lib.check(L.rlgpu_envset_set_profile(env._h, ctypes.c_void_p(prof.data_ptr())), "set_profile")
@@ -37,8 +40,12 @@ for i in range(steps):
     e1.record()
     torch.cuda.synchronize()
     tot_ms += e0.elapsed_time(e1)
+    per = prof[KW:].view(wg, KP)[:, :23].double()
+    tots = per.sum(1)
+    k = int(tots.argmax())
+    spread.append((tots.max().item(), tots.mean().item(), per[k].cpu(), per.mean(0).cpu()))
+    prof[KW:].zero_()
 c = prof.cpu().tolist()
-wg = (n + 3) // 4
 total = sum(c[:23])
 print(f"{n} arenas, {steps} steps, {tot_ms / steps:.3f} ms/step (profiled build)")
 ticks = steps * 8
@@ -46,3 +53,14 @@ print(f"  per tick (workgroup 0, arena 0): candidates {c[24] / ticks / wg:.2f}, 
       f"refresh-needing ranks {c[25] / ticks / wg:.2f}, live ranks {c[26] / ticks / wg:.2f}")
 for k in range(23):
     print(f"  {NAMES[k]:28s} {c[k] / total * 100:6.2f} %   {c[k] / wg / steps:12.0f} cycles/WG/step")
+
+# The kernel ends with its slowest workgroup: per step, slowest vs mean workgroup, and where the
+# slowest one spends the difference.
+mx = sum(x[0] for x in spread) / len(spread)
+mn = sum(x[1] for x in spread) / len(spread)
+print(f"  slowest workgroup per step: {mx:.0f} cycles, mean workgroup {mn:.0f} (max / mean {mx / mn:.2f})")
+slow = sum(x[2] for x in spread) / len(spread)
+mean = sum(x[3] for x in spread) / len(spread)
+order = sorted(range(23), key=lambda k: -(slow[k] - mean[k]).item())
+for k in order[:8]:
+    print(f"    {NAMES[k]:28s} slowest {slow[k].item():10.0f}  mean {mean[k].item():10.0f}  excess {slow[k].item() - mean[k].item():10.0f}")
