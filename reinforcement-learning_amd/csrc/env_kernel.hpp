@@ -37,7 +37,7 @@ constexpr int kArenas = 4;          // arenas per 64-thread workgroup
 constexpr int kMaxCand = 64;        // narrowphase candidates per tick per arena
 constexpr int kMaxRows = RLGPU_MAX_SOLVER_ROWS;  // solver contact rows per arena (+ as many friction rows)
 constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic work items ("ranks")
-constexpr int kMeshChunks = 3;      // lanes per body-vs-mesh pair in the narrowphase
+constexpr int kMeshChunks = 6;      // lanes per body-vs-mesh pair in the narrowphase
 // Manifold keys, ascending in Bullet's pair order (rsim_ref.cpp pair_key restates the same):
 //   dynamic-static  body * kStat + s, s = mesh object 0..kMaxObj-1, then kMaxObj + plane 0..3
 //                   (meshes are created before the planes, Arena.cpp:1015-1100, and a cell's static
