@@ -1312,7 +1312,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
                 float s = 0.f;
 #pragma unroll
                 for (int q = 0; q < MAXH; q++) s += v[r][q];
-                mean[r] = wave_sum(s) / (float)H;
+                mean[r] = wave_sum_x(s) / (float)H;
             }
 #pragma unroll
             for (int r = 0; r < RF; r++) {
@@ -1322,7 +1322,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
                     float d = lcol<MAXH>(lane, q) < H ? v[r][q] - mean[r] : 0.f;
                     s2 += d * d;
                 }
-                rs[r] = 1.f / sqrtf(wave_sum(s2) / (float)H + 1e-5f);
+                rs[r] = 1.f / sqrtf(wave_sum_x(s2) / (float)H + 1e-5f);
             }
         }
 #pragma unroll
@@ -1509,7 +1509,7 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         float* dz = dZ + (int64_t)row * H;
         float d[MAXH];
         if (use_ln) {
-            float m1 = wave_sum(s1) / (float)H, m2 = wave_sum(s2) / (float)H;
+            float m1 = wave_sum_x(s1) / (float)H, m2 = wave_sum_x(s2) / (float)H;  // == wave_sum
             float rs = st.y;
 #pragma unroll
             for (int q = 0; q < MAXH; q++) d[q] = rs * (dh[q] * g[q] - m1 - x[q] * m2);
