@@ -1259,6 +1259,29 @@ DEV int lcol(int lane, int q) {
 // registers.  Each wave walks LNF_ROWS/4 rows, lnf_rf<MAXH>() of them at a time: their loads are
 // issued together before the first reduction and their wave reductions interleave, so a wave keeps
 // that many rows of HBM traffic in flight (the per-row arithmetic and its order are unchanged).
+// The rank-1 head (critic value) of one row already in registers, lcol layout: the arithmetic of
+// head1_fwd (same per-lane order, same reduction), so fusing it into the LayerNorm forward that
+// produces the row changes no bit; lane 0 writes *out.
+template <int MAXH>
+DEV void head1_row(const float (&x)[MAXH], const float* w, const float* b, int H, bool vec, int lane, float* out) {
+    float s = 0.f;
+    if (vec) {
+#pragma unroll
+        for (int q = 0; q < MAXH; q += 4) {
+            const int c = lcol<MAXH>(lane, q);
+            if (c < H) s += x[q] * w[c] + x[q + 1] * w[c + 1] + x[q + 2] * w[c + 2] + x[q + 3] * w[c + 3];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) {
+            const int c = lcol<MAXH>(lane, q);
+            if (c < H) s += x[q] * w[c];
+        }
+    }
+    s = wave_sum(s);
+    if (lane == 0) *out = s + b[0];
+}
+
 constexpr int LNF_ROWS = 16;
 template <int MAXH>
 constexpr int lnf_rf() {
@@ -1266,7 +1289,9 @@ constexpr int lnf_rf() {
 }
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const float* gamma, const float* beta, int R, int H,
-                                                     float slope, int use_ln, float* act, float2* stats, float* amax) {
+                                                     float slope, int use_ln, float* act, float2* stats, float* amax,
+                                                     const float* head_w = nullptr, const float* head_b = nullptr,
+                                                     float* head_out = nullptr) {
     uint32_t vmax = 0;  // max |act| of this thread's outputs (H3 operand scale, when amax is given)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
@@ -1355,6 +1380,7 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
                 const uint32_t b = lcol<MAXH>(lane, q) < H ? abs_bits(a[q]) : 0u;
                 vmax = b > vmax ? b : vmax;
             }
+            if (head_w) head1_row<MAXH>(a, head_w, head_b, H, vec, lane, head_out + row[r]);
         }
     }
     if (amax) h3_amax_commit(amax, vmax);
@@ -1453,17 +1479,19 @@ constexpr int LNB_ROWS = 32;
 template <int MAXH>
 __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* Z, const float2* stats, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
-                                                 float* part, float* amax) {
+                                                 float* part, float* amax, const float* head_dv = nullptr,
+                                                 const float* head_w = nullptr) {
     __shared__ float red[4][3][64 * MAXH];
     uint32_t vmax = 0;  // max |dZ| of this thread's outputs (H3 operand scale, when amax is given)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
-    float g[MAXH], b[MAXH], pg[MAXH], pb[MAXH], pz[MAXH];
+    float g[MAXH], b[MAXH], pg[MAXH], pb[MAXH], pz[MAXH], hw[MAXH];
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
         int c = lcol<MAXH>(lane, q);
         g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
         b[q] = (use_ln && c < H) ? beta[c] : 0.f;
+        hw[q] = (!dA && c < H) ? head_w[c] : 0.f;
         pg[q] = pb[q] = pz[q] = 0.f;
     }
     const int r0 = blockIdx.x * LNB_ROWS;
@@ -1480,9 +1508,11 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
                 const int c = lcol<MAXH>(lane, q);
                 const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
                 float4 t = c < H ? *reinterpret_cast<const float4*>(xh + c) : zero;
-                float4 u = c < H ? *reinterpret_cast<const float4*>(da + c) : zero;
                 x[q] = t.x; x[q + 1] = t.y; x[q + 2] = t.z; x[q + 3] = t.w;
-                av[q] = u.x; av[q + 1] = u.y; av[q + 2] = u.z; av[q + 3] = u.w;
+                if (dA) {
+                    float4 u = c < H ? *reinterpret_cast<const float4*>(da + c) : zero;
+                    av[q] = u.x; av[q + 1] = u.y; av[q + 2] = u.z; av[q + 3] = u.w;
+                }
             }
         } else {
 #pragma unroll
@@ -1490,8 +1520,13 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
                 const int c = lcol<MAXH>(lane, q);
                 bool in = c < H;
                 x[q] = in ? xh[c] : 0.f;
-                av[q] = in ? da[c] : 0.f;
+                if (dA) av[q] = in ? da[c] : 0.f;
             }
+        }
+        if (!dA) {  // rank-1 head: dA[row, c] = dv[row] * w[c], the product head1_bwd would have stored
+            const float dv = head_dv[row];
+#pragma unroll
+            for (int q = 0; q < MAXH; q++) av[q] = dv * hw[q];
         }
         if (use_ln) {
 #pragma unroll
@@ -1640,14 +1675,14 @@ __global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w,
         if (row >= R) break;
         const float d = dv[row];
         const float* x = X + (int64_t)row * H;
-        float* da = dA + (int64_t)row * H;
+        float* da = dA ? dA + (int64_t)row * H : nullptr;  // null: the LayerNorm backward recomputes dA
         if (vec) {
 #pragma unroll
             for (int q = 0; q < MAXH; q += 4) {
                 const int c = lcol<MAXH>(lane, q);
                 if (c < H) {
                     float4 t = *reinterpret_cast<const float4*>(x + c);
-                    *reinterpret_cast<float4*>(da + c) = make_float4(d * wr[q], d * wr[q + 1], d * wr[q + 2], d * wr[q + 3]);
+                    if (dA) *reinterpret_cast<float4*>(da + c) = make_float4(d * wr[q], d * wr[q + 1], d * wr[q + 2], d * wr[q + 3]);
                     acc[q] += d * t.x;
                     acc[q + 1] += d * t.y;
                     acc[q + 2] += d * t.z;
@@ -1659,7 +1694,7 @@ __global__ void __launch_bounds__(256) head1_bwd(const float* X, const float* w,
             for (int q = 0; q < MAXH; q++) {
                 const int c = lcol<MAXH>(lane, q);
                 if (c < H) {
-                    da[c] = d * wr[q];
+                    if (dA) da[c] = d * wr[q];
                     acc[q] += d * x[c];
                 }
             }

@@ -417,6 +417,8 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
     const float* in_amax = amax_x(h, m);
     int64_t ld = h->x_ld;
     bool tail_ok = true;
+    const Layer& O = m.L[nh];
+    const bool head1 = O.out == 1 && nh > 0;  // rank-1 head fused into the last LayerNorm forward
     for (int l = 0; l < nh; l++) {
         const Layer& L = m.L[l];
         if (L.sf >= 0)
@@ -427,17 +429,18 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
                      tail_ok);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
+        const bool fuse = head1 && l == nh - 1;
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
-                           amax_slot(m, l));
+                           amax_slot(m, l), fuse ? P + O.w : nullptr, fuse ? P + O.b : nullptr, fuse ? out : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = m.act[l];
         in_amax = amax_slot(m, l);
         ld = L.out;
         tail_ok = false;
     }
-    const Layer& O = m.L[nh];
-    if (O.out == 1) {  // rank-1 head (critic value): wave-per-row dot products
+    if (head1) return;
+    if (O.out == 1) {  // rank-1 head (critic value) of a model without hidden layers: wave-per-row dot products
         hipLaunchKernelGGL(mlp::head1_fwd_any(O.in), dim3(ceil_div(n, mlp::H1_ROWS)), dim3(256), 0, s, in, P + O.w, P + O.b, n,
                            O.in, out);
         RLGPU_CHECK_HIP(hipGetLastError());
@@ -462,8 +465,9 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
     const Layer& O = m.L[nh];
     if (O.out == 1) {  // rank-1 head: dA = dv w^T, dw / db partials in one pass
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
-        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, m.act[nh - 1], P + O.w, dout, n, O.in, m.dA,
-                           m.cpart);
+        // dA = dout w^T is not stored when a LayerNorm backward follows: it recomputes the product
+        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, m.act[nh - 1], P + O.w, dout, n, O.in,
+                           nh > 0 ? nullptr : m.dA, m.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
         reduce_partials(m, m.cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
     } else {
@@ -487,8 +491,11 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
-        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, m.dA, m.xhat[l], reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out,
-                           h->cfg.leaky_slope, h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l));
+        const bool rank1 = O.out == 1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
+        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, rank1 ? nullptr : m.dA, m.xhat[l],
+                           reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
+                           h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), rank1 ? dout : nullptr,
+                           rank1 ? P + O.w : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
