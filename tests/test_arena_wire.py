@@ -33,8 +33,17 @@ def _fill(a, rng):
 
 
 def _data(rec):
-    """the record's field bytes (struct padding normalised: it carries no data)"""
-    return np.array(rec, dtype=ARENA).tobytes()
+    """the record's field bytes (struct padding normalised: it carries no data). Fields are copied
+    one by one into a zeroed record: a whole-record copy would carry the padding bytes along."""
+    def copy(dst, src):
+        for name in dst.dtype.names:
+            if dst[name].dtype.names:
+                copy(dst[name], src[name])
+            else:
+                dst[name] = src[name]
+    out = np.zeros(1, ARENA)
+    copy(out, np.asarray(rec).reshape(1))
+    return out.tobytes()
 
 
 def random_arena(seed):
