@@ -209,6 +209,42 @@ int rlgpu_envset_build_obs(rlgpu_envset* env, void* stream);
  * (the default). */
 int rlgpu_envset_set_profile(rlgpu_envset* env, unsigned long long* d_counters);
 
+/* ExampleMain's StepCallback metrics on the device.  Replaces the StepCallbackFn that
+ * Learner::Start calls after every StepSecondHalf (GL/public/GigaLearnCPP/Learner.h:11,
+ * Learner.cpp:796-797) with the callback src/ExampleMain.cpp:233-283 registers: on every 4th call
+ * (its stepCounter) each player of each GameState adds "Player/In Air Ratio", "Ball Touch Ratio",
+ * "Demoed Ratio", "Speed", "Speed Towards Ball", "Boost" and, when it touched the ball this step,
+ * "Touch Height"; on every call each state that scored adds "Game/Goal Speed" -- Report::AddAvg's
+ * (total, count) in fp64 (Report.h:11-45).  When enabled, every launch that runs the builders (fused
+ * step, second half) is one callback call: the kernel adds the pre-reset GameState's values to
+ * per-arena fp64 slots (RLGPU_STEP_METRIC_SLOTS per arena: metric x 4 + player for the 7 player
+ * metrics, then goal-speed total, goal count, player-pass count). */
+enum {
+    RLGPU_SM_IN_AIR = 0,
+    RLGPU_SM_BALL_TOUCH = 1,
+    RLGPU_SM_DEMOED = 2,
+    RLGPU_SM_SPEED = 3,
+    RLGPU_SM_SPEED_TO_BALL = 4,
+    RLGPU_SM_BOOST = 5,
+    RLGPU_SM_TOUCH_HEIGHT = 6,
+    RLGPU_SM_GOAL_SPEED = 7,
+    RLGPU_NUM_STEP_METRICS = 8,
+    RLGPU_SM_SLOT_GOAL_SPEED = 28, /* per-arena slots after the 7 x 4 player slots */
+    RLGPU_SM_SLOT_GOALS = 29,
+    RLGPU_SM_SLOT_PASSES = 30,
+    RLGPU_STEP_METRIC_SLOTS = 32
+};
+/* Report key of metric i ("Player/In Air Ratio", ...), NULL when out of range. */
+const char* rlgpu_step_metric_name(int32_t i);
+/* enable != 0: allocate and zero the per-arena slots and the call counter; 0: free them. */
+int rlgpu_envset_enable_step_metrics(rlgpu_envset* env, int32_t enable);
+/* Report::Avg totals and counts of the RLGPU_NUM_STEP_METRICS metrics since the last reset: the
+ * per-arena slots summed in fp64 in arena order (host), after synchronising `stream`.  reset != 0
+ * zeroes the slots afterwards (Report cleared at each metrics report).  Either output may be NULL. */
+int rlgpu_envset_step_metrics(rlgpu_envset* env, double* h_total, uint64_t* h_count, int32_t reset, void* stream);
+/* The raw per-arena slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] (tests, custom reductions). */
+int rlgpu_envset_step_metric_slots(rlgpu_envset* env, double* h_out, void* stream);
+
 /* Static sizes for binding checks. */
 int rlgpu_arena_state_size(void);
 

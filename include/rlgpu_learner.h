@@ -155,6 +155,10 @@ int rlgpu_learner_set_stats(rlgpu_learner* h, const rlgpu_learner_stats* in);
 /* PPO report metrics accumulated since the last reset (PPOLearner.cpp:537-566): h_out receives
  * RLGPU_NUM_METRICS sums (rlgpu_ppo.h RLGPU_M_*), *count the number of minibatches summed. */
 int rlgpu_learner_metrics(rlgpu_learner* h, float* h_out, int64_t* count, int32_t reset);
+/* ExampleMain's StepCallback metrics over the collection steps since the last reset (enabled at
+ * create; rlgpu_envset_step_metrics of the owned env set): Report::Avg totals / counts of the
+ * RLGPU_NUM_STEP_METRICS keys (rlgpu_step_metric_name). */
+int rlgpu_learner_step_metrics(rlgpu_learner* h, double* h_total, uint64_t* h_count, int32_t reset);
 /* Record HIP events around every fused env step (rlgpu_learner_report.env_kernel_ms). */
 int rlgpu_learner_set_env_timing(rlgpu_learner* h, int32_t enable);
 

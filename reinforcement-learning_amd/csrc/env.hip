@@ -40,7 +40,39 @@ struct StepArgs {
     uint64_t seed;
     unsigned long long* prof;  // [32] phase cycle counters or null
     MeshView mesh;
+    double* metrics;           // [n][RLGPU_STEP_METRIC_SLOTS] StepCallback sums (build steps) or null
+    int metrics_players;       // this call is one of ExampleMain's every-4th "expensive" calls
 };
+
+// ExampleMain's StepCallback (src/ExampleMain.cpp:233-283) on this arena's GameState as the
+// builders left it (after UpdateFromArena, before any reset), Report::AddAvg's fp64 totals kept per
+// arena and player: slot RLGPU_SM_* x 4 + player.  Lane l = player l; lane 0 adds the per-state
+// goal speed and the arena's count of player passes.  Vec::Length / Normalized / Dot / RS_MAX are
+// restated in float (MathTypes.h:31-93, Framework.h:47); the totals are fp64 as Report::Avg.
+DEV void step_metrics(ArenaLDS* A, int l, double* m, bool players) {
+    if (players) {
+        const rlgpu_car& c = A->s.cars[l];
+        const v3 pos = ld3(c.body.pos) * kBT2UU, vel = ld3(c.body.vel) * kBT2UU;
+        const v3 bp = ld3(A->s.ball.pos) * kBT2UU;
+        const bool touched = A->a.touched[l] != 0;
+        const v3 dir = rs_norm(bp - pos);
+        const float toward = vel.x * dir.x + vel.y * dir.y + vel.z * dir.z;
+        m[RLGPU_SM_IN_AIR * 4 + l] += c.is_on_ground ? 0.0 : 1.0;
+        m[RLGPU_SM_BALL_TOUCH * 4 + l] += touched ? 1.0 : 0.0;
+        m[RLGPU_SM_DEMOED * 4 + l] += c.is_demoed ? 1.0 : 0.0;
+        m[RLGPU_SM_SPEED * 4 + l] += (double)rs_len(vel);
+        m[RLGPU_SM_SPEED_TO_BALL * 4 + l] += (double)(0.f > toward ? 0.f : toward);
+        m[RLGPU_SM_BOOST * 4 + l] += (double)c.boost;
+        if (touched) m[RLGPU_SM_TOUCH_HEIGHT * 4 + l] += (double)bp.z;
+    }
+    if (l == 0) {
+        if (players) m[RLGPU_SM_SLOT_PASSES] += 1.0;
+        if (A->a.goal) {
+            m[RLGPU_SM_SLOT_GOAL_SPEED] += (double)rs_len(ld3(A->s.ball.vel) * kBT2UU);
+            m[RLGPU_SM_SLOT_GOALS] += 1.0;
+        }
+    }
+}
 
 
 // The boost-pad constants a lane tests every tick (pads l, l + 16, l + 32), held in registers for
@@ -444,6 +476,8 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             if (g.out_rew) g.out_rew[arena * 4 + l] = r;
             if (g.out_term) g.out_term[arena * 4 + l] = (int8_t)A->a.traj_term;
         }
+        if (g.metrics && valid && l < 4) step_metrics(A, l, g.metrics + (size_t)arena * RLGPU_STEP_METRIC_SLOTS,
+                                                      g.metrics_players != 0);
         uint8_t tj = 0;
         if (valid) {
             term = A->s.env.terminal;
@@ -666,6 +700,8 @@ struct rlgpu_envset {
     float *d_obs = nullptr, *d_rewards = nullptr, *d_last_rewards = nullptr, *d_trunc_obs = nullptr;
     uint8_t *d_masks = nullptr, *d_terminals = nullptr;
     unsigned long long* d_prof = nullptr;
+    double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
+    uint64_t metric_calls = 0;     // ExampleMain's stepCounter
     void *d_tri = nullptr, *d_cell_start = nullptr, *d_cell_tris = nullptr;  // arena mesh (MeshView)
     rl::MeshView mesh{};
 };
@@ -693,6 +729,10 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.max_episode_steps = e->cfg.max_episode_steps;
     g.prof = e->d_prof;
     g.mesh = e->mesh;
+    if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
+        g.metrics = e->d_metrics;
+        g.metrics_players = (++e->metric_calls % 4) == 0;
+    }
     unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
     hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(64), 0, s, g);
     RLGPU_CHECK_HIP(hipGetLastError());
@@ -799,9 +839,78 @@ extern "C" int rlgpu_envset_set_profile(rlgpu_envset* e, unsigned long long* d_c
     });
 }
 
+namespace {
+const char* const kStepMetricNames[RLGPU_NUM_STEP_METRICS] = {
+    "Player/In Air Ratio", "Player/Ball Touch Ratio", "Player/Demoed Ratio", "Player/Speed",
+    "Player/Speed Towards Ball", "Player/Boost", "Player/Touch Height", "Game/Goal Speed"};
+}
+
+extern "C" const char* rlgpu_step_metric_name(int32_t i) {
+    return i >= 0 && i < RLGPU_NUM_STEP_METRICS ? kStepMetricNames[i] : nullptr;
+}
+
+extern "C" int rlgpu_envset_enable_step_metrics(rlgpu_envset* e, int32_t enable) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        const size_t bytes = (size_t)e->cfg.num_arenas * RLGPU_STEP_METRIC_SLOTS * sizeof(double);
+        if (enable && !e->d_metrics) RLGPU_CHECK_HIP(hipMalloc(&e->d_metrics, bytes));
+        if (!enable && e->d_metrics) {
+            RLGPU_CHECK_HIP(hipDeviceSynchronize());
+            (void)hipFree(e->d_metrics);
+            e->d_metrics = nullptr;
+        }
+        if (enable) RLGPU_CHECK_HIP(hipMemset(e->d_metrics, 0, bytes));
+        e->metric_calls = 0;
+    });
+}
+
+extern "C" int rlgpu_envset_step_metric_slots(rlgpu_envset* e, double* h_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && h_out, "null argument");
+        RLGPU_REQUIRE(e->d_metrics, "step metrics are not enabled (rlgpu_envset_enable_step_metrics)");
+        hipStream_t s = rlgpu::as_stream(stream);
+        RLGPU_CHECK_HIP(hipMemcpyAsync(h_out, e->d_metrics,
+                                       (size_t)e->cfg.num_arenas * RLGPU_STEP_METRIC_SLOTS * sizeof(double),
+                                       hipMemcpyDeviceToHost, s));
+        RLGPU_CHECK_HIP(hipStreamSynchronize(s));
+    });
+}
+
+extern "C" int rlgpu_envset_step_metrics(rlgpu_envset* e, double* h_total, uint64_t* h_count, int32_t reset,
+                                         void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        RLGPU_REQUIRE(e->d_metrics, "step metrics are not enabled (rlgpu_envset_enable_step_metrics)");
+        const int n = e->cfg.num_arenas;
+        std::vector<double> slots((size_t)n * RLGPU_STEP_METRIC_SLOTS);
+        hipStream_t s = rlgpu::as_stream(stream);
+        RLGPU_CHECK_HIP(hipMemcpyAsync(slots.data(), e->d_metrics, slots.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        RLGPU_CHECK_HIP(hipStreamSynchronize(s));
+        double tot[RLGPU_NUM_STEP_METRICS] = {};
+        double passes = 0, goals = 0;
+        for (int a = 0; a < n; a++) {
+            const double* m = &slots[(size_t)a * RLGPU_STEP_METRIC_SLOTS];
+            for (int k = 0; k < RLGPU_SM_GOAL_SPEED; k++)
+                for (int p = 0; p < 4; p++) tot[k] += m[k * 4 + p];
+            tot[RLGPU_SM_GOAL_SPEED] += m[RLGPU_SM_SLOT_GOAL_SPEED];
+            goals += m[RLGPU_SM_SLOT_GOALS];
+            passes += m[RLGPU_SM_SLOT_PASSES];
+        }
+        if (h_total)
+            for (int k = 0; k < RLGPU_NUM_STEP_METRICS; k++) h_total[k] = tot[k];
+        if (h_count) {
+            for (int k = 0; k < RLGPU_SM_TOUCH_HEIGHT; k++) h_count[k] = (uint64_t)(4 * passes);
+            h_count[RLGPU_SM_TOUCH_HEIGHT] = (uint64_t)tot[RLGPU_SM_BALL_TOUCH];  // one AddAvg per touching player
+            h_count[RLGPU_SM_GOAL_SPEED] = (uint64_t)goals;
+        }
+        if (reset) RLGPU_CHECK_HIP(hipMemsetAsync(e->d_metrics, 0, slots.size() * sizeof(double), s));
+    });
+}
+
 extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
     return rlgpu::guarded([&] {
         if (!e) return;
+        if (e->d_metrics) (void)hipFree(e->d_metrics);
         (void)hipFree(e->d_arenas);
         (void)hipFree(e->d_obs);
         (void)hipFree(e->d_trunc_obs);

@@ -40,6 +40,12 @@ int main(int argc, char** argv) {
                         "Consumption Time %.3f s, PPO Learn Time %.3f s, Total Timesteps %lld\n",
                         it + 1, agentSteps / total, (double)r.env_steps / total, r.collect_s, r.consume_s, r.learn_s,
                         (long long)learner.stats.total_steps);
+            // the StepCallback's report (ExampleMain.cpp:233-283), averaged over this iteration
+            double tot[RLGPU_NUM_STEP_METRICS];
+            uint64_t cnt[RLGPU_NUM_STEP_METRICS];
+            RLGC::RlgpuCheck(rlgpu_envset_step_metrics(learner.env().handle(), tot, cnt, 1, s), "step metrics");
+            for (int k = 0; k < RLGPU_NUM_STEP_METRICS; k++)
+                if (cnt[k]) std::printf("  %s: %.4g\n", rlgpu_step_metric_name(k), tot[k] / (double)cnt[k]);
         }
         (void)hipStreamDestroy(s);
     } catch (const std::exception& e) {  // ExampleMain.cpp:603-612

@@ -205,6 +205,8 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     ec.mesh_objects = cfg.mesh_objects;
     ec.mesh_object_ntris = cfg.mesh_object_ntris;
     env_ = new RLGC::EnvSetGPU(ec, s_);
+    // ExampleMain registers its StepCallback (ExampleMain.cpp:233-283, 592): restated on the device
+    RlgpuCheck(rlgpu_envset_enable_step_metrics(env_->handle(), 1), "step metrics");
     K_ = cfg.frame_stack > 1 ? cfg.frame_stack : 1;
     RLGPU_REQUIRE(K_ <= 16, "Learner: frame_stack must be <= 16");
     const int W = OBS * K_;
@@ -626,6 +628,14 @@ extern "C" int rlgpu_learner_set_stats(rlgpu_learner* h, const rlgpu_learner_sta
         h->L->returnStat.m2 = in->return_m2;
     });
 }
+extern "C" int rlgpu_learner_step_metrics(rlgpu_learner* h, double* h_total, uint64_t* h_count, int32_t reset) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        RLGPU_CHECK_HIP(hipDeviceSynchronize());
+        RLGC::RlgpuCheck(rlgpu_envset_step_metrics(h->L->env().handle(), h_total, h_count, reset, nullptr), "step metrics");
+    });
+}
+
 extern "C" int rlgpu_learner_metrics(rlgpu_learner* h, float* h_out, int64_t* count, int32_t reset) {
     return rlgpu::guarded([&] {
         RLGPU_LEARNER(h);

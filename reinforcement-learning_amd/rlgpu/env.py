@@ -71,6 +71,11 @@ def _bind():
     L.rlgpu_envset_build_obs.argtypes = [vp, vp]
     L.rlgpu_envset_get_arenas.argtypes = [vp, i32, i32, vp]
     L.rlgpu_envset_set_arenas.argtypes = [vp, i32, i32, vp]
+    L.rlgpu_step_metric_name.argtypes = [i32]
+    L.rlgpu_step_metric_name.restype = ctypes.c_char_p
+    L.rlgpu_envset_enable_step_metrics.argtypes = [vp, i32]
+    L.rlgpu_envset_step_metrics.argtypes = [vp, vp, vp, i32, vp]
+    L.rlgpu_envset_step_metric_slots.argtypes = [vp, vp, vp]
     _bound = True
     return L
 
@@ -197,6 +202,33 @@ class EnvSet:
         count = buf.size // ARENA.itemsize
         _lib.check(_lib.lib().rlgpu_envset_set_arenas(self._h, first, count, buf.ctypes.data_as(ctypes.c_void_p)),
                    "set_arenas")
+
+    # ---- ExampleMain's StepCallback metrics (include/rlgpu_env.h rlgpu_envset_step_metrics)
+    STEP_METRIC_SLOTS = 32
+
+    @staticmethod
+    def step_metric_names():
+        L = _bind()
+        return [L.rlgpu_step_metric_name(i).decode() for i in range(8)]
+
+    def enable_step_metrics(self, on=True):
+        """Every later builders launch (fused step / second half) is one StepCallback call."""
+        _lib.check(_bind().rlgpu_envset_enable_step_metrics(self._h, int(on)), "enable_step_metrics")
+
+    def step_metrics(self, reset=False, stream=None):
+        """{Report key: (total, count)} since the last reset (Report::Avg, Report.h:11-45)."""
+        tot, cnt = np.zeros(8, np.float64), np.zeros(8, np.uint64)
+        _lib.check(_bind().rlgpu_envset_step_metrics(self._h, tot.ctypes.data_as(ctypes.c_void_p),
+                                                     cnt.ctypes.data_as(ctypes.c_void_p), int(reset),
+                                                     _lib.stream_ptr(stream)), "step_metrics")
+        return {k: (float(t), int(c)) for k, t, c in zip(self.step_metric_names(), tot, cnt)}
+
+    def step_metric_slots(self, stream=None):
+        """The raw per-arena fp64 slots [num_arenas, 32]."""
+        out = np.zeros((self.num_arenas, self.STEP_METRIC_SLOTS), np.float64)
+        _lib.check(_bind().rlgpu_envset_step_metric_slots(self._h, out.ctypes.data_as(ctypes.c_void_p),
+                                                          _lib.stream_ptr(stream)), "step_metric_slots")
+        return out
 
     def serialize_arena(self, index):
         """RocketSim Arena::Serialize bytes of arena `index` (rlgpu.arena_wire)."""

@@ -238,6 +238,7 @@ def _bind():
     L.rlgpu_learner_set_stats.argtypes = [vp, ctypes.POINTER(_CStats)]
     L.rlgpu_learner_metrics.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
     L.rlgpu_learner_set_env_timing.argtypes = [vp, ctypes.c_int32]
+    L.rlgpu_learner_step_metrics.argtypes = [vp, vp, vp, ctypes.c_int32]
     return L
 
 
@@ -389,6 +390,17 @@ class Learner:
         _lib.check(_lib.lib().rlgpu_learner_metrics(self._h, out.ctypes.data, ctypes.byref(cnt), int(reset)),
                    "rlgpu_learner_metrics")
         return out.tolist(), cnt.value
+
+    def step_metrics(self, reset=True):
+        """ExampleMain's StepCallback report (ExampleMain.cpp:233-283): {key: average} over the
+        collection steps since the last reset (keys without samples are left out, as a Report without
+        that AddAvg)."""
+        import numpy as np
+        from .env import EnvSet
+        tot, cnt = np.zeros(8, np.float64), np.zeros(8, np.uint64)
+        _lib.check(_lib.lib().rlgpu_learner_step_metrics(self._h, tot.ctypes.data, cnt.ctypes.data, int(reset)),
+                   "rlgpu_learner_step_metrics")
+        return {k: float(t) / int(c) for k, t, c in zip(EnvSet.step_metric_names(), tot, cnt) if c}
 
     def set_env_timing(self, on=True):
         _lib.check(_lib.lib().rlgpu_learner_set_env_timing(self._h, int(on)), "rlgpu_learner_set_env_timing")

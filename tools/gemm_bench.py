@@ -44,9 +44,13 @@ SHAPES = [(0, 0, 50000, 512, 512), (0, 0, 50000, 512, 167), (0, 0, 50000, 90, 51
           (0, 1, 50000, 512, 512), (0, 1, 50000, 512, 90),
           (1, 1, 512, 512, 50000, 49), (1, 1, 512, 167, 50000, 49), (1, 1, 90, 512, 50000, 49),
           (0, 0, 8192, 8192, 8192)]
-# argv: modes (e.g. "2" or "0,2") and optionally shape indices ("0,5")
+# argv: modes (e.g. "2" or "0,2"), optionally shape indices ("0,5") and row counts replacing the
+# 50000 of the picked shapes ("49152,50000": tile-round quantization)
 modes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2]
 picks = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else range(len(SHAPES))
+rows = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [None]
 for i in picks:
-    for mode in modes:
-        run(mode, *SHAPES[i])
+    for r in rows:
+        shp = tuple(r if (r is not None and v == 50000) else v for v in SHAPES[i])
+        for mode in modes:
+            run(mode, *shp)
