@@ -1495,39 +1495,53 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         pg[q] = pb[q] = pz[q] = 0.f;
     }
     const int r0 = blockIdx.x * LNB_ROWS;
-    for (int rr = w; rr < LNB_ROWS; rr += 4) {
-        const int row = r0 + rr;
-        if (row >= R) break;
-        const float* da = dA + (int64_t)row * H;
-        const float* xh = Z + (int64_t)row * H;  // pre-norm z; xhat recomputed below
-        const float2 st = stats[row];
-        float dh[MAXH], x[MAXH], av[MAXH];
-        if (vec) {
+    // two rows per wave and pass: both rows' loads are issued before either row's reductions
+    for (int rr = w; rr < LNB_ROWS; rr += 8) {
+        float xs[2][MAXH], as[2][MAXH];
+        float2 sts[2];
 #pragma unroll
-            for (int q = 0; q < MAXH; q += 4) {
-                const int c = lcol<MAXH>(lane, q);
-                const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
-                float4 t = c < H ? *reinterpret_cast<const float4*>(xh + c) : zero;
-                x[q] = t.x; x[q + 1] = t.y; x[q + 2] = t.z; x[q + 3] = t.w;
-                if (dA) {
-                    float4 u = c < H ? *reinterpret_cast<const float4*>(da + c) : zero;
-                    av[q] = u.x; av[q + 1] = u.y; av[q + 2] = u.z; av[q + 3] = u.w;
+        for (int j = 0; j < 2; j++) {
+            const int row = r0 + rr + 4 * j;
+            const bool ok = row < R;
+            const int rw = ok ? row : r0 + rr;  // a valid row (its values are not used)
+            const float* da = dA + (int64_t)rw * H;
+            const float* xh = Z + (int64_t)rw * H;  // pre-norm z; xhat recomputed below
+            sts[j] = stats[rw];
+            if (vec) {
+#pragma unroll
+                for (int q = 0; q < MAXH; q += 4) {
+                    const int c = lcol<MAXH>(lane, q);
+                    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+                    float4 t = c < H ? *reinterpret_cast<const float4*>(xh + c) : zero;
+                    xs[j][q] = t.x; xs[j][q + 1] = t.y; xs[j][q + 2] = t.z; xs[j][q + 3] = t.w;
+                    if (dA) {
+                        float4 u = c < H ? *reinterpret_cast<const float4*>(da + c) : zero;
+                        as[j][q] = u.x; as[j][q + 1] = u.y; as[j][q + 2] = u.z; as[j][q + 3] = u.w;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < MAXH; q++) {
+                    const int c = lcol<MAXH>(lane, q);
+                    bool in = c < H;
+                    xs[j][q] = in ? xh[c] : 0.f;
+                    if (dA) as[j][q] = in ? da[c] : 0.f;
                 }
             }
-        } else {
+            if (!dA) {  // rank-1 head: dA[row, c] = dv[row] * w[c], the product head1_bwd would have stored
+                const float dv = head_dv[rw];
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) {
-                const int c = lcol<MAXH>(lane, q);
-                bool in = c < H;
-                x[q] = in ? xh[c] : 0.f;
-                if (dA) av[q] = in ? da[c] : 0.f;
+                for (int q = 0; q < MAXH; q++) as[j][q] = dv * hw[q];
             }
         }
-        if (!dA) {  // rank-1 head: dA[row, c] = dv[row] * w[c], the product head1_bwd would have stored
-            const float dv = head_dv[row];
 #pragma unroll
-            for (int q = 0; q < MAXH; q++) av[q] = dv * hw[q];
-        }
+        for (int j = 0; j < 2; j++) {
+        const int row = r0 + rr + 4 * j;
+        if (row >= R) break;
+        const float2 st = sts[j];
+        float* x = xs[j];
+        const float* av = as[j];
+        float dh[MAXH];
         if (use_ln) {
 #pragma unroll
             for (int q = 0; q < MAXH; q++) x[q] = (x[q] - st.x) * st.y;  // the forward's xhat, same ops
@@ -1573,6 +1587,7 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
             pb[q] += in ? dh[q] : 0.f;
             const uint32_t bb = in ? abs_bits(d[q]) : 0u;
             vmax = bb > vmax ? bb : vmax;
+        }
         }
     }
 #pragma unroll
@@ -1734,8 +1749,22 @@ __global__ void __launch_bounds__(1024) reduce_cols(const float* part, int nblk,
     const int c = blockIdx.x * 64 + cl;
     const int G = gridDim.y, y = blockIdx.y;
     float s = 0.f;
-    if (c < n)
-        for (int b = y + G * gi; b < nblk; b += 16 * G) s += part[(int64_t)b * stride + off + c];
+    if (c < n) {
+        // eight partial rows loaded before they are added (in the same order as a plain loop: the
+        // same bits), so a thread has eight loads in flight instead of one
+        const int step = 16 * G;
+        for (int b = y + G * gi; b < nblk; b += 8 * step) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int bk = b + k * step;
+                v[k] = part[(int64_t)(bk < nblk ? bk : b) * stride + off + c];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (b + k * step < nblk) s += v[k];
+        }
+    }
     red[gi][cl] = s;
     __syncthreads();
     if (gi == 0 && c < n) {
