@@ -359,12 +359,13 @@ int splits_for(int mode, int rows, int out, int in) {
 
 // dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
 void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
-                 bool x_tail_ok = false, const float* amax_dz = nullptr, const float* amax_x = nullptr) {
+                 bool x_tail_ok = false, const float* amax_dz = nullptr, const float* amax_x = nullptr, int64_t ldz = 0) {
     int splits = splits_for(m.mode, n, out, in);
     int chunk = (int)ceil_div(ceil_div(n, splits), kgran(m.mode)) * kgran(m.mode);
     int z = (int)ceil_div(n, chunk);
-    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s, false, x_tail_ok,
-             amax_dz, amax_x);
+    // ldz > out: dZ rows zero-padded to ldz floats (16-byte loads across the row end)
+    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, ldz ? ldz : out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s,
+             ldz > out, x_tail_ok, amax_dz, amax_x);
     int64_t e = (int64_t)out * in;
     if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)m.wpart & 15) == 0)
         hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
@@ -395,6 +396,10 @@ void colsum_into(Model& m, const float* X, int n, int C, float* g, hipStream_t s
     RLGPU_CHECK_HIP(hipGetLastError());
     reduce_partials(m, m.cpart, nb, C, C, g, s);
 }
+
+// row stride of a multi-column loss gradient dout [n, out]: a multiple of 4 floats (the policy loss
+// writes the padding columns as zeros)
+inline int dout_ld(int out) { return out > 1 ? (out + 3) / 4 * 4 : out; }
 
 // H3 operand scale slots (null in the other modes): slot k of model m, and the gathered obs
 inline float* amax_slot(Model& m, int k) { return m.mode == RLGPU_GEMM_F16X3 ? m.amax + (int64_t)k * 64 : nullptr; }
@@ -473,18 +478,23 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
     } else {
         if (m.mode == RLGPU_GEMM_F16X3 && !dout_part)
             throw rlgpu::Error(RLGPU_ERR_STATE, "H3 backward: the loss kernel must provide dout's scale");
+        // dout rows of dld floats (the policy loss pads them with zeros to a multiple of 4)
+        const int dld = dout_ld(O.out);
         weight_grad(m, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s, false, amax_slot(m, kAmaxOut),
-                    amax_slot(m, nh - 1));
+                    amax_slot(m, nh - 1), dld);
         if (dout_part)
             reduce_partials(m, dout_part, dout_nblk, O.out, O.out, G + O.b, s);
-        else
+        else if (dld == O.out)
             colsum_into(m, dout, n, O.out, G + O.b, s);
+        else
+            throw rlgpu::Error(RLGPU_ERR_STATE, "backward: padded dout needs the loss kernel's bias partials");
         // dA = dout . W_out
         if (O.sb >= 0)
-            gemm_x6_pre(dout, O.out, m.wsplit + O.sb, O.sb_ld, (int64_t)O.sb_rows * O.sb_ld, m.dA, O.in, nullptr, n, O.in,
-                        O.out, s, false, amax_slot(m, kAmaxOut), wscale_at(m, O.sbs));
+            gemm_x6_pre(dout, dld, m.wsplit + O.sb, O.sb_ld, (int64_t)O.sb_rows * O.sb_ld, m.dA, O.in, nullptr, n, O.in,
+                        O.out, s, dld > O.out, amax_slot(m, kAmaxOut), wscale_at(m, O.sbs));
         else
-            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dout, O.out, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s);
+            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dout, dld, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s,
+                     dld > O.out);
     }
     for (int l = nh - 1; l >= 0; l--) {
         const Layer& L = m.L[l];
@@ -777,7 +787,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             int64_t nb = ceil_div(R, std::min(std::min(mlp::LNB_ROWS, mlp::CS_ROWS), ppo::PL_ROWS));
             for (auto& m : h->M) {
                 m.y = h->alloc<float>(R * omax);
-                m.dy = h->alloc<float>(R * omax);
+                m.dy = h->alloc<float>(R * ((omax + 3) / 4 * 4));
                 m.dA = h->alloc<float>(R * H);
                 m.dZ = h->alloc<float>(R * H);
                 m.wpart = h->alloc<float>(wpart_max);
@@ -1032,7 +1042,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
         hipLaunchKernelGGL(ppo::policy_loss<ppo::PL_K>, dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
                            d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
-                           1.f / std::log((float)A), pm.dy, d_metrics, pm.cpart, amax_slot(pm, kAmaxOut));
+                           1.f / std::log((float)A), pm.dy, dout_ld(A), d_metrics, pm.cpart, amax_slot(pm, kAmaxOut));
         RLGPU_CHECK_HIP(hipGetLastError());
         backward(h, 0, h->x0, n, pm.dy, s, pm.cpart, pl_blocks);
         if (!serial) RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));

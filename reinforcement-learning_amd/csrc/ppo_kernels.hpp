@@ -176,8 +176,8 @@ template <int K>
 __global__ void __launch_bounds__(256) policy_loss(const float* logits, const uint8_t* masks, const int32_t* actions,
                                                   const float* old_logp, const float* adv, const int32_t* idx, int64_t start,
                                                   int n, int A, const float* adv_stats, float bsr, float clip_range,
-                                                  float ent_scale, float inv_log_a, float* dlogits, float* metrics,
-                                                  float* bias_part, float* amax) {
+                                                  float ent_scale, float inv_log_a, float* dlogits, int ldd,
+                                                  float* metrics, float* bias_part, float* amax) {
     __shared__ float red[16][5];
     __shared__ float colred[16][16 * K];  // per (wave, lane group) column sums of dlogits
     uint32_t vmax = 0;  // max |dlogits| (H3 operand scale, when amax is given)
@@ -256,10 +256,15 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
         }
         const float dot = grp_sum(dot_l);
         if (valid) {
-            float* dl = dlogits + (int64_t)row * A;
+            // dlogits rows of ldd >= A floats: the columns [A, ldd) are written as zeros, so the
+            // output layer's GEMMs read 16-byte vectors across the row end
+            float* dl = dlogits + (int64_t)row * ldd;
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                if (!in[k]) continue;
+                if (!in[k]) {
+                    if (i + 16 * k < ldd) dl[i + 16 * k] = 0.f;
+                    continue;
+                }
                 const float gk = p[k] * (d[k] - dot);
                 dl[i + 16 * k] = gk;
                 col[k] += gk;
