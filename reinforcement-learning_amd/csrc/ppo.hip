@@ -92,7 +92,9 @@ inline bool h3_wide(int J) {
 inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
 inline bool split_mode_(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
 inline int gemm_slots(int mode) {
-    if (mode == RLGPU_GEMM_F16X3) return g_cus * ((h3_variant() == 0 || h3_variant() >= 3) ? 2 : 1);
+    // H3 variant 0: 146 / 156 VGPRs (forward / weight-gradient instances), 40 KB LDS -> three
+    // workgroups per CU (-Rpass-analysis=kernel-resource-usage: occupancy 3 waves / SIMD)
+    if (mode == RLGPU_GEMM_F16X3) return g_cus * (h3_variant() == 0 ? 3 : (h3_variant() >= 3 ? 2 : 1));
     return g_cus * (split_mode_(mode) ? x6_occ() : RLGPU_GEMM_OCC);
 }
 // K granularity of a split-K chunk: a whole number of stages of either kernel
