@@ -1042,7 +1042,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         // policy on the caller's stream
         forward_train(h, 0, h->x0, n, pm.y, s);
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
-        hipLaunchKernelGGL(ppo::policy_loss<ppo::PL_K>, dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
+        hipLaunchKernelGGL(ppo::policy_loss_any(A), dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
                            d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
                            1.f / std::log((float)A), pm.dy, dout_ld(A), d_metrics, pm.cpart, amax_slot(pm, kAmaxOut));
         RLGPU_CHECK_HIP(hipGetLastError());

@@ -305,6 +305,20 @@ __global__ void __launch_bounds__(256) policy_loss(const float* logits, const ui
     if (amax) mlp::h3_amax_commit(amax, vmax);
 }
 
+// the instantiation with ceil(A / 16) actions per lane (A = 90: 6 of the 8 slots PL_K allows)
+inline decltype(&policy_loss<PL_K>) policy_loss_any(int A) {
+    switch ((A + 15) / 16) {
+        case 1: return &policy_loss<1>;
+        case 2: return &policy_loss<2>;
+        case 3: return &policy_loss<3>;
+        case 4: return &policy_loss<4>;
+        case 5: return &policy_loss<5>;
+        case 6: return &policy_loss<6>;
+        case 7: return &policy_loss<7>;
+        default: return &policy_loss<PL_K>;
+    }
+}
+
 // Critic MSE: loss = mean((v - t)^2) * bsr ; dv = 2 (v - t) / n * bsr.
 __global__ void critic_loss(const float* vals, const float* target, const int32_t* idx, int64_t start, int n, float bsr,
                             float* dvals, float* metrics) {
