@@ -37,13 +37,14 @@ def env_bytes_per_step(arena_state_size, append=True):
     return b
 
 
-def pmc_traffic(kernel_ms):
+def pmc_traffic(kernel_ms, arenas):
     """HBM traffic of the env kernel from the committed rocprofv3 PMC passes (profiles/*_env_pmc.json,
-    made by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE runs of this bench), as GB/s
-    over the average launch duration measured here; None when no summary is present."""
+    made by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE runs of this bench at its
+    default ARENAS_PER_GPU arenas), as GB/s over the average launch duration measured here; None when
+    no summary is present or this run steps another arena count (the bytes were counted for that one)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_pmc.json")))
-    if not files:
+    if not files or arenas != ARENAS_PER_GPU:
         return None, None
     d = json.load(open(files[-1]))
     b = d["hbm_bytes_per_launch"]
@@ -154,7 +155,7 @@ def main():
     kern_ms = sum(kern) / len(kern)
     b_env = env_bytes_per_step(arena_state_size())
     achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kern_ms)
+    traffic, traffic_src = pmc_traffic(kern_ms, args.arenas)
     out = {
         "metric": "env-steps/sec (whole node) at 32768 arenas; PPO wall-clock per 1M steps",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
