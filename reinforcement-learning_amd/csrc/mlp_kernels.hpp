@@ -1476,29 +1476,32 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 // Columns per lane: lcol (float4 loads / stores); gamma / beta stay in registers; each of the 4
 // waves walks LNB_ROWS/4 rows.
 constexpr int LNB_ROWS = 32;
-template <int MAXH>
+template <int MAXH, bool HEAD = false>
 __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* Z, const float2* stats, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
                                                  float* part, float* amax, const float* head_dv = nullptr,
-                                                 const float* head_w = nullptr) {
+                                                 const float* head_w = nullptr, float* head_part = nullptr) {
     __shared__ float red[4][3][64 * MAXH];
+    __shared__ float hred[HEAD ? 4 : 1][HEAD ? 64 * MAXH + 1 : 1];  // rank-1 head partials (head_part)
     uint32_t vmax = 0;  // max |dZ| of this thread's outputs (H3 operand scale, when amax is given)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool vec = (H % 4 == 0) && (MAXH % 4 == 0);
-    float g[MAXH], b[MAXH], pg[MAXH], pb[MAXH], pz[MAXH], hw[MAXH];
+    float g[MAXH], b[MAXH], pg[MAXH], pb[MAXH], pz[MAXH], hw[MAXH], ph[MAXH];
+    float phb = 0.f;
 #pragma unroll
     for (int q = 0; q < MAXH; q++) {
         int c = lcol<MAXH>(lane, q);
         g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
         b[q] = (use_ln && c < H) ? beta[c] : 0.f;
         hw[q] = (!dA && c < H) ? head_w[c] : 0.f;
-        pg[q] = pb[q] = pz[q] = 0.f;
+        pg[q] = pb[q] = pz[q] = ph[q] = 0.f;
     }
     const int r0 = blockIdx.x * LNB_ROWS;
     // two rows per wave and pass: both rows' loads are issued before either row's reductions
     for (int rr = w; rr < LNB_ROWS; rr += 8) {
         float xs[2][MAXH], as[2][MAXH];
         float2 sts[2];
+        float dvs[2] = {0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int row = r0 + rr + 4 * j;
@@ -1530,6 +1533,7 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
             }
             if (!dA) {  // rank-1 head: dA[row, c] = dv[row] * w[c], the product head1_bwd would have stored
                 const float dv = head_dv[rw];
+                dvs[j] = dv;
 #pragma unroll
                 for (int q = 0; q < MAXH; q++) as[j][q] = dv * hw[q];
             }
@@ -1554,7 +1558,11 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
             float gg = dh[q] * g[q];
             s1 += gg;
             s2 += gg * x[q];
+            // the rank-1 head's weight gradient dv * act, act recomputed as the forward made it
+            // (head1_bwd's per-lane sums in its row order: the same bits)
+            if (HEAD && lcol<MAXH>(lane, q) < H) ph[q] += dvs[j] * (h > 0.f ? h : h * slope);
         }
+        if (HEAD) phb += dvs[j];
         float* dz = dZ + (int64_t)row * H;
         float d[MAXH];
         if (use_ln) {
@@ -1598,10 +1606,22 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         red[w][2][c] = pb[q];
     }
     __syncthreads();
+    if (HEAD) {
+#pragma unroll
+        for (int q = 0; q < MAXH; q++) hred[w][lcol<MAXH>(lane, q)] = ph[q];
+        if (lane == 0) hred[w][64 * MAXH] = phb;
+    }
+    __syncthreads();
     float* out = part + (int64_t)blockIdx.x * 3 * H;
     for (int k = 0; k < 3; k++)
         for (int c = threadIdx.x; c < H; c += 256)
             out[k * H + c] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    if (HEAD) {  // [blk][w | b], head1_bwd's layout and order
+        float* ho = head_part + (int64_t)blockIdx.x * (H + 1);
+        for (int c = threadIdx.x; c < H; c += 256) ho[c] = hred[0][c] + hred[1][c] + hred[2][c] + hred[3][c];
+        if (threadIdx.x == 0)
+            ho[H] = hred[0][64 * MAXH] + hred[1][64 * MAXH] + hred[2][64 * MAXH] + hred[3][64 * MAXH];
+    }
     if (amax) h3_amax_commit(amax, vmax);
 }
 
@@ -1626,6 +1646,15 @@ inline decltype(&ln_act_fwd_bf16<16, F16>) ln_act_fwd_bf16_any(int H) {
     return &ln_act_fwd_bf16<32, F16>;
 }
 RLGPU_NPER_DISPATCH(ln_act_bwd)
+// the variant that also emits a following rank-1 head's dw / db partials (head_part)
+inline decltype(&ln_act_bwd<16, true>) ln_act_bwd_head_any(int H) {
+    if (H <= 64) return &ln_act_bwd<1, true>;
+    if (H <= 128) return &ln_act_bwd<2, true>;
+    if (H <= 256) return &ln_act_bwd<4, true>;
+    if (H <= 512) return &ln_act_bwd<8, true>;
+    if (H <= 1024) return &ln_act_bwd<16, true>;
+    return &ln_act_bwd<32, true>;
+}
 
 // Rank-1 output layer (the critic's Linear(H, 1)): GEMM tiles would be 1/128 occupied, so the
 // head runs as wave-per-row dot products.  Columns per lane: lcol (float4 loads when H is a

@@ -45,6 +45,7 @@ struct Model {
     // fp32 training workspace (per model, so the two models' passes can overlap on two streams)
     std::vector<float*> xhat, act, rstd;
     float *y = nullptr, *dy = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr, *mid = nullptr;  // y: model output
+    float* hpart = nullptr;  // rank-1 head dw / db partials, written by the last LayerNorm backward
     uint16_t* wsplit = nullptr;  // split weight planes (x6 / H3 modes)
     int64_t nsplit = 0;
     float* wscale = nullptr;     // H3: per-row inverse scales of the weight planes
@@ -448,6 +449,8 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
     }
     if (head1) return;
     if (O.out == 1) {  // rank-1 head (critic value) of a model without hidden layers: wave-per-row dot products
+        if (ld != O.in)
+            throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "a rank-1 model without hidden layers needs obs_size % 4 == 0");
         hipLaunchKernelGGL(mlp::head1_fwd_any(O.in), dim3(ceil_div(n, mlp::H1_ROWS)), dim3(256), 0, s, in, P + O.w, P + O.b, n,
                            O.in, out);
         RLGPU_CHECK_HIP(hipGetLastError());
@@ -470,13 +473,16 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
     float* G = h->grads;
     int nh = (int)m.L.size() - 1;
     const Layer& O = m.L[nh];
-    if (O.out == 1) {  // rank-1 head: dA = dv w^T, dw / db partials in one pass
+    if (O.out == 1 && nh == 0) {  // rank-1 head on the input: dA = dv w^T, dw / db partials in one pass
+        if (h->x_ld != O.in)
+            throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "a rank-1 model without hidden layers needs obs_size % 4 == 0");
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
-        // dA = dout w^T is not stored when a LayerNorm backward follows: it recomputes the product
-        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, m.act[nh - 1], P + O.w, dout, n, O.in,
-                           nh > 0 ? nullptr : m.dA, m.cpart);
+        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, X, P + O.w, dout, n, O.in, m.dA, m.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
         reduce_partials(m, m.cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
+    } else if (O.out == 1) {
+        // rank-1 head after a LayerNorm: its backward recomputes dA = dv w^T and the activation, and
+        // emits the head's dw / db partials (m.hpart) beside its own -- no separate head pass
     } else {
         if (m.mode == RLGPU_GEMM_F16X3 && !dout_part)
             throw rlgpu::Error(RLGPU_ERR_STATE, "H3 backward: the loss kernel must provide dout's scale");
@@ -504,11 +510,12 @@ void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hi
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool rank1 = O.out == 1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
-        hipLaunchKernelGGL(mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, rank1 ? nullptr : m.dA, m.xhat[l],
+        hipLaunchKernelGGL(rank1 ? mlp::ln_act_bwd_head_any(L.out) : mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, rank1 ? nullptr : m.dA, m.xhat[l],
                            reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
                            h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), rank1 ? dout : nullptr,
-                           rank1 ? P + O.w : nullptr);
+                           rank1 ? P + O.w : nullptr, rank1 ? m.hpart : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
+        if (rank1) reduce_partials(m, m.hpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
         reduce_partials(m, m.cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
@@ -794,6 +801,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 m.dZ = h->alloc<float>(R * H);
                 m.wpart = h->alloc<float>(wpart_max);
                 m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
+                m.hpart = h->alloc<float>(nb * ((int64_t)H + 1));
                 m.mid = h->alloc<float>(16 * 3 * (int64_t)std::max(std::max(H, omax) + 1, 1024));
                 if (m.nsplit) m.wsplit = h->alloc<uint16_t>(m.nsplit);
                 if (m.mode == RLGPU_GEMM_F16X3 && m.nscale) m.wscale = h->alloc<float>(m.nscale);
