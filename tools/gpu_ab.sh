@@ -1,0 +1,8 @@
+# A/B of two library builds on one box: bench.py alternately with $RLGPU_LIB_A (A) and the in-tree
+# library (B), a few rounds each, so box-to-box spread does not enter the comparison.
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ab
+for i in 1 2 3; do
+  RLGPU_LIB=$RLGPU_LIB_A timeout -k 10 300 python bench.py --steps 6 --warmup 1 --no-cpu-baseline > gpurun_out/ab/a$i.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py --steps 6 --warmup 1 --no-cpu-baseline > gpurun_out/ab/b$i.log 2>&1 || exit 1
+done
