@@ -75,10 +75,15 @@ typedef struct {
     int32_t mesh_ntris;
     int32_t mesh_objects;
     const int32_t* mesh_object_ntris;
+    /* PPOLearnerConfig::sharedHead (rlgpu_ppo_config.shared_layers); n_shared_layers = 0: none */
+    int32_t shared_layers[RLGPU_MAX_LAYERS];
+    int32_t n_shared_layers;
 } rlgpu_learner_config;
 
 /* Fills ExampleMain's values (src/ExampleMain.cpp:340-430) for a C2 rank: 4096 arenas, T = 128,
- * [512, 512] actor / critic, world 1. */
+ * [512, 512] actor / critic (BASELINE config C2, no shared head), world 1.  ExampleMain's own
+ * topology -- shared head [384, 384], policy / critic [384] x 3 as its log prints it
+ * (run_out.log:25-28) -- is what host/example_main.cpp (rlgpu_train) selects. */
 int rlgpu_learner_default_config(rlgpu_learner_config* cfg);
 
 /* Collectives for world > 1, called synchronously from the learner's host thread (the learner's

@@ -15,7 +15,10 @@
  * order: per layer Linear.weight [out,in], Linear.bias, LayerNorm.weight, LayerNorm.bias;
  * then the output Linear), their gradients, AdamW moments, the bf16 inference copy
  * ("seqHalf", refreshed after every optimizer step) and the activation workspace for
- * up to cfg.max_rows rows.  Models: 0 = policy (actor), 1 = critic.
+ * up to cfg.max_rows rows.  Models: 0 = policy (actor), 1 = critic, 2 = the optional shared head
+ * (cfg.n_shared_layers > 0; it comes last in the flat buffers so the policy / critic offsets do not
+ * depend on it).  With a shared head every policy / critic entry point runs it first, as
+ * PPOLearner::InferPolicyProbsFromModels / InferCritic / Learn do (PPOLearner.cpp:78-112,186-199,396-398).
  *
  * Arithmetic: training forward/backward in fp32 (cfg.train_gemm: the three-way bf16 split on
  * bf16 MFMA by default, or f32-input MFMA v_mfma_f32_32x32x2_f32), inference in bf16 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- the reference's
@@ -56,6 +59,13 @@ typedef struct {
                                                  RLGPU_GEMM_F32 (1) or RLGPU_GEMM_F16X3 (2) -- see rlgpu_gemm */
     int32_t infer_fp16;                       /* 16-bit inference copy: 0 = bf16 (the reference's seqHalf),
                                                  1 = fp16 on v_mfma_f32_32x32x16_f16 (BASELINE config C5) */
+    /* PPOLearnerConfig::sharedHead (PPOLearner.cpp:42-74): [Linear -> LayerNorm -> LeakyReLU] x k with
+     * no output layer, run once on the obs; policy and critic then take its last activation as input
+     * (ExampleMain: {512, 512} x scale, run_out.log:25-28 shows [384, 384]).  n_shared_layers = 0: no
+     * shared head (policy and critic read the obs).  Model index 2; learning rate
+     * min(policy_lr, critic_lr) (PPOLearner::SetLearningRates, PPOLearner.cpp:652-663). */
+    int32_t shared_layers[RLGPU_MAX_LAYERS];
+    int32_t n_shared_layers;
 } rlgpu_ppo_config;
 
 /* fp32 GEMM arithmetic of the training path (libtorch fp32 Linear forward / backward in the
@@ -79,15 +89,16 @@ typedef struct rlgpu_ppo rlgpu_ppo;
 enum {
     RLGPU_M_ENTROPY = 0, RLGPU_M_KL, RLGPU_M_POLICY_LOSS, RLGPU_M_CRITIC_LOSS, RLGPU_M_RATIO,
     RLGPU_M_CLIP_FRACTION, RLGPU_M_COUNT, RLGPU_M_GRAD_NORM_POLICY, RLGPU_M_GRAD_NORM_CRITIC,
-    RLGPU_NUM_METRICS = 16
+    RLGPU_M_GRAD_NORM_SHARED, RLGPU_NUM_METRICS = 16
 };
 
 int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out);
 int rlgpu_ppo_destroy(rlgpu_ppo* h);
 
-/* Flat fp32 buffers of all models, contiguous (policy first, then critic). */
+/* Flat fp32 buffers of all models, contiguous (policy first, then critic, then the shared head). */
 int rlgpu_ppo_buffers(rlgpu_ppo* h, float** d_params, float** d_grads, int64_t* num_params);
-/* Offset / count of one model inside the flat buffers. */
+/* Offset / count of one model (0 policy, 1 critic, 2 shared head) inside the flat buffers; without a
+ * shared head model 2 has count 0 (offset = the end of the buffers). */
 int rlgpu_ppo_model_range(rlgpu_ppo* h, int32_t model, int64_t* offset, int64_t* count);
 /* torch-default init (Linear: U(+-1/sqrt(fan_in)) weight and bias; LayerNorm 1 / 0), Philox. */
 int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream);
@@ -101,7 +112,9 @@ int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream);
 int rlgpu_debug_infer_trace(void* d_buf);
 
 /* Plain forward of one model on n rows (n <= max_rows): precision 0 = fp32 (training path,
- * no activations kept), 1 = bf16 inference path.  d_out [n, out_size] fp32.
+ * no activations kept), 1 = bf16 inference path.  d_out [n, out_size] fp32.  With a shared head,
+ * models 0 / 1 are shared head -> policy / critic (Model::Forward chained as the reference does) and
+ * model 2 is the shared head alone (out_size = its last width).
  * The 16-bit inference (this, rlgpu_ppo_infer_actions*, rlgpu_ppo_infer_critic) runs as one fused
  * kernel per call when every layer fits it (inputs / hidden widths <= 512, outputs <= 128); the
  * environment variable RLGPU_FUSED_INFER=0 selects the layer-by-layer kernels, same results. */
@@ -117,7 +130,8 @@ int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_m
 /* Self-play against an old policy version (LearnerConfig trainAgainstOldVersions,
  * Learner.cpp:587-627,733-767; versions kept by PolicyVersionManager, PolicyVersionManager.cpp:38-62).
  * set_version: bf16 inference copy of a policy given as its flat fp32 parameters (torch order,
- * the policy's rlgpu_ppo_model_range count).  infer_actions_mixed: rows with d_old_rows[i] != 0
+ * the policy's rlgpu_ppo_model_range count), followed by the shared head's when there is one (the
+ * reference versions GetPolicyModels() = every model but the critic, PPOLearner.cpp:665-674).  infer_actions_mixed: rows with d_old_rows[i] != 0
  * act with that version (no log-prob written), the others with the current policy (as
  * rlgpu_ppo_infer_actions). */
 int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stream);
@@ -132,6 +146,8 @@ int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t n, float* d
 int rlgpu_mean_std(const float* d_x, int64_t n, float* d_out, void* stream);
 
 /* One Learn minibatch: rows idx[start..start+n) of the batch (d_index may be NULL = identity)
+ * (with a shared head: its forward once, policy and critic on its output, and its backward from the
+ * sum of their input gradients -- PPOLearner.cpp:396-398,478-498)
  * gathered from d_obs [*, obs_size], d_masks [*, A], d_actions int32, d_old_logp, d_adv,
  * d_target.  Advantages are normalised with d_adv_stats = (mean, std) as (a - mean)/(std+1e-8).
  * loss = (policyLoss - entropy*entropy_scale)*n/batch_size + MSE(V, target)*n/batch_size;
@@ -141,8 +157,9 @@ int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks
                         const int32_t* d_index, int64_t start, int32_t n, int64_t batch_size,
                         const float* d_adv_stats, float* d_metrics, void* stream);
 
-/* clip_grad_norm_(model, max_grad_norm) per model, AdamW step (libtorch semantics), zero
- * grads, refresh the bf16 copy.  Grad norms written to d_metrics (optional). */
+/* clip_grad_norm_(model, max_grad_norm) per model (policy, critic, shared head: PPOLearner.cpp:521-526),
+ * AdamW step (libtorch semantics), zero grads, refresh the bf16 copy.  Grad norms written to
+ * d_metrics (optional). */
 int rlgpu_ppo_optimizer_step(rlgpu_ppo* h, float* d_metrics, void* stream);
 int rlgpu_ppo_zero_grad(rlgpu_ppo* h, void* stream);
 /* Optimizer state (step count + moments) for checkpointing; moments are device pointers. */

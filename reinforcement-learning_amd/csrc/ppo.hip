@@ -37,7 +37,8 @@ struct Layer {
 };
 
 struct Model {
-    std::vector<Layer> L;  // hidden layers then the output layer (last)
+    std::vector<Layer> L;  // hidden layers then the output layer (last; none for the shared head)
+    bool head_only = false;  // the shared head: every layer is [Linear -> LayerNorm -> LeakyReLU]
     int in, out;
     int64_t off, count;
     float lr;
@@ -53,7 +54,10 @@ struct Model {
     // H3: 64-shard max |x| slots of the GEMM operand tensors (kAmaxSlots x 64 floats):
     // act[l] at slot l, dZ of layer l at kAmaxDZ + l, the loss gradient dout at kAmaxOut
     float* amax = nullptr;
+    float* dX = nullptr;  // gradient w.r.t. the model input (policy / critic behind a shared head)
 };
+// hidden [Linear -> LayerNorm -> LeakyReLU] layers of a model (all of the shared head's)
+inline int nhid(const Model& m) { return (int)m.L.size() - (m.head_only ? 0 : 1); }
 constexpr int kAmaxDZ = RLGPU_MAX_LAYERS, kAmaxOut = 2 * RLGPU_MAX_LAYERS, kAmaxSlots = 2 * RLGPU_MAX_LAYERS + 1;
 inline bool split_mode(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
 
@@ -105,7 +109,10 @@ inline int kgran(int mode) { return split_mode_(mode) ? mlp::XKMAX : mlp::BK; }
 
 struct rlgpu_ppo {
     rlgpu_ppo_config cfg;
-    Model M[2];
+    Model M[3];       // policy, critic, shared head (M[2], present when nm == 3)
+    int nm = 2;
+    bool shared() const { return nm == 3; }
+    float* dshared = nullptr;  // the shared head's output gradient: policy dX + critic dX
     int64_t nparams = 0, nhalf = 0;
     float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr;
     uint16_t* half = nullptr;
@@ -117,7 +124,7 @@ struct rlgpu_ppo {
     // set by init / refresh_half / the optimizer step, cleared when forward_train re-splits.  With
     // the whole iteration as one batch the planes are rebuilt once per optimizer step, not per
     // minibatch.
-    bool split_dirty[2] = {true, true};
+    bool split_dirty[3] = {true, true, true};
     int64_t step = 0;
     int hmax = 0;
     float *scratch = nullptr;  // clip partials + coefficients
@@ -406,27 +413,44 @@ inline int dout_ld(int out) { return out > 1 ? (out + 3) / 4 * 4 : out; }
 
 // H3 operand scale slots (null in the other modes): slot k of model m, and the gathered obs
 inline float* amax_slot(Model& m, int k) { return m.mode == RLGPU_GEMM_F16X3 ? m.amax + (int64_t)k * 64 : nullptr; }
-inline float* amax_x(rlgpu_ppo* h, const Model& m) { return m.mode == RLGPU_GEMM_F16X3 ? h->x_amax : nullptr; }
 inline const float* wscale_at(const Model& m, int64_t off) {
     return m.mode == RLGPU_GEMM_F16X3 ? m.wscale + off : nullptr;
 }
 
-// fp32 training forward; keeps activations; writes the output layer to `out`.  X is the
-// gathered, zero-padded minibatch copy (row stride h->x_ld).
-void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipStream_t s) {
+// A training model's input: rows of ld floats, their H3 scale shards (null outside H3), and whether
+// the rows are zero-padded past the model input to a multiple of 4 (16-byte loads across the row end).
+struct Input {
+    const float* X;
+    int64_t ld;
+    const float* amax;
+    bool tail_ok;
+};
+// the gathered minibatch obs (rows of x_ld floats, zero-padded)
+inline Input obs_input(rlgpu_ppo* h) { return {h->x0, h->x_ld, h->x_amax, true}; }
+// what model mi reads: the obs, or the shared head's last activation (PPOLearner.cpp:403,474)
+inline Input model_input(rlgpu_ppo* h, int mi) {
+    if (mi == 2 || !h->shared()) return obs_input(h);
+    Model& sm = h->M[2];
+    const int l = nhid(sm) - 1;
+    return {sm.act[l], sm.L[l].out, amax_slot(sm, l), false};
+}
+
+// fp32 training forward of model mi on x; keeps activations; writes the output layer to `out` (the
+// shared head has none: its last activation stays in m.act).
+void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipStream_t s) {
     Model& m = h->M[mi];
     const float* P = h->params;
     if (h->split_dirty[mi]) {
         split_weights(P, m, s);
         h->split_dirty[mi] = false;
     }
-    int nh = (int)m.L.size() - 1;
-    const float* in = X;
-    const float* in_amax = amax_x(h, m);
-    int64_t ld = h->x_ld;
-    bool tail_ok = true;
-    const Layer& O = m.L[nh];
-    const bool head1 = O.out == 1 && nh > 0;  // rank-1 head fused into the last LayerNorm forward
+    const int nh = nhid(m);
+    const float* in = x.X;
+    const float* in_amax = x.amax;
+    int64_t ld = x.ld;
+    bool tail_ok = x.tail_ok;
+    const Layer* O = m.head_only ? nullptr : &m.L[nh];
+    const bool head1 = O && O->out == 1 && nh > 0;  // rank-1 head fused into the last LayerNorm forward
     for (int l = 0; l < nh; l++) {
         const Layer& L = m.L[l];
         if (L.sf >= 0)
@@ -434,102 +458,117 @@ void forward_train(rlgpu_ppo* h, int mi, const float* X, int n, float* out, hipS
                         L.in, s, tail_ok, in_amax, wscale_at(m, L.sfs));
         else
             gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s,
-                     tail_ok);
+                     tail_ok, false, in_amax);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool fuse = head1 && l == nh - 1;
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
-                           amax_slot(m, l), fuse ? P + O.w : nullptr, fuse ? P + O.b : nullptr, fuse ? out : nullptr);
+                           amax_slot(m, l), fuse ? P + O->w : nullptr, fuse ? P + O->b : nullptr, fuse ? out : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = m.act[l];
         in_amax = amax_slot(m, l);
         ld = L.out;
         tail_ok = false;
     }
-    if (head1) return;
-    if (O.out == 1) {  // rank-1 head (critic value) of a model without hidden layers: wave-per-row dot products
-        if (ld != O.in)
+    if (!O || head1) return;
+    if (O->out == 1) {  // rank-1 head (critic value) of a model without hidden layers: wave-per-row dot products
+        if (ld != O->in)
             throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "a rank-1 model without hidden layers needs obs_size % 4 == 0");
-        hipLaunchKernelGGL(mlp::head1_fwd_any(O.in), dim3(ceil_div(n, mlp::H1_ROWS)), dim3(256), 0, s, in, P + O.w, P + O.b, n,
-                           O.in, out);
+        hipLaunchKernelGGL(mlp::head1_fwd_any(O->in), dim3(ceil_div(n, mlp::H1_ROWS)), dim3(256), 0, s, in, P + O->w, P + O->b, n,
+                           O->in, out);
         RLGPU_CHECK_HIP(hipGetLastError());
         return;
     }
-    if (O.sf >= 0)
-        gemm_x6_pre(in, ld, m.wsplit + O.sf, O.sf_ld, (int64_t)O.sf_rows * O.sf_ld, out, O.out, P + O.b, n, O.out, O.in, s,
-                    false, in_amax, wscale_at(m, O.sfs));
+    if (O->sf >= 0)
+        gemm_x6_pre(in, ld, m.wsplit + O->sf, O->sf_ld, (int64_t)O->sf_rows * O->sf_ld, out, O->out, P + O->b, n, O->out, O->in, s,
+                    tail_ok, in_amax, wscale_at(m, O->sfs));
     else
-        gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + O.w, O.in, out, O.out, P + O.b, n, O.out, O.in, 1, s);
+        gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + O->w, O->in, out, O->out, P + O->b, n, O->out, O->in, 1, s, tail_ok,
+                 false, in_amax);
 }
 
-// backward from dout [n, out] into the grad buffer (accumulating).  dout_part: optional per-block
-// column partials of dout (dout_nblk rows of `out` floats, written by the loss kernel) for the
-// output bias, instead of a separate column-sum pass.  H3: dout's max |x| is in slot kAmaxOut.
-void backward(rlgpu_ppo* h, int mi, const float* X, int n, const float* dout, hipStream_t s,
+// backward of model mi (input x) from dout into the grad buffer (accumulating).  dout: the loss
+// gradient [n, out] of the output layer, or -- the shared head -- the gradient of its last
+// activation [n, H].  dout_part: optional per-block column partials of dout (dout_nblk rows of `out`
+// floats, written by the loss kernel) for the output bias, instead of a separate column-sum pass.
+// H3: dout's max |x| is in slot kAmaxOut.  When m.dX is set (a model behind the shared head) the
+// gradient w.r.t. the model input is written there too.
+void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hipStream_t s,
               const float* dout_part = nullptr, int dout_nblk = 0) {
     Model& m = h->M[mi];
     const float* P = h->params;
     float* G = h->grads;
-    int nh = (int)m.L.size() - 1;
-    const Layer& O = m.L[nh];
-    if (O.out == 1 && nh == 0) {  // rank-1 head on the input: dA = dv w^T, dw / db partials in one pass
-        if (h->x_ld != O.in)
+    const int nh = nhid(m);
+    const float* dA_top = m.dA;  // gradient of the last hidden layer's activation
+    bool rank1 = false;          // rank-1 output layer folded into the last LayerNorm backward
+    const Layer* O = m.head_only ? nullptr : &m.L[nh];
+    if (!O) {
+        dA_top = dout;
+    } else if (O->out == 1 && nh == 0) {  // rank-1 head on the input: dA = dv w^T, dw / db partials in one pass
+        if (x.ld != O->in)
             throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "a rank-1 model without hidden layers needs obs_size % 4 == 0");
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
-        hipLaunchKernelGGL(mlp::head1_bwd_any(O.in), dim3(nb), dim3(256), 0, s, X, P + O.w, dout, n, O.in, m.dA, m.cpart);
+        hipLaunchKernelGGL(mlp::head1_bwd_any(O->in), dim3(nb), dim3(256), 0, s, x.X, P + O->w, dout, n, O->in,
+                           m.dX ? m.dX : m.dA, m.cpart);
         RLGPU_CHECK_HIP(hipGetLastError());
-        reduce_partials(m, m.cpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous in the flat buffer
-    } else if (O.out == 1) {
+        reduce_partials(m, m.cpart, nb, O->in + 1, O->in + 1, G + O->w, s);  // [w | b] contiguous in the flat buffer
+        return;
+    } else if (O->out == 1) {
         // rank-1 head after a LayerNorm: its backward recomputes dA = dv w^T and the activation, and
         // emits the head's dw / db partials (m.hpart) beside its own -- no separate head pass
+        rank1 = true;
     } else {
         if (m.mode == RLGPU_GEMM_F16X3 && !dout_part)
             throw rlgpu::Error(RLGPU_ERR_STATE, "H3 backward: the loss kernel must provide dout's scale");
         // dout rows of dld floats (the policy loss pads them with zeros to a multiple of 4)
-        const int dld = dout_ld(O.out);
-        weight_grad(m, dout, O.out, m.act[nh - 1], O.in, O.in, n, G + O.w, s, false, amax_slot(m, kAmaxOut),
-                    amax_slot(m, nh - 1), dld);
+        const int dld = dout_ld(O->out);
+        const Input a = nh > 0 ? Input{m.act[nh - 1], O->in, amax_slot(m, nh - 1), false} : x;
+        weight_grad(m, dout, O->out, a.X, a.ld, O->in, n, G + O->w, s, a.tail_ok, amax_slot(m, kAmaxOut), a.amax, dld);
         if (dout_part)
-            reduce_partials(m, dout_part, dout_nblk, O.out, O.out, G + O.b, s);
-        else if (dld == O.out)
-            colsum_into(m, dout, n, O.out, G + O.b, s);
+            reduce_partials(m, dout_part, dout_nblk, O->out, O->out, G + O->b, s);
+        else if (dld == O->out)
+            colsum_into(m, dout, n, O->out, G + O->b, s);
         else
             throw rlgpu::Error(RLGPU_ERR_STATE, "backward: padded dout needs the loss kernel's bias partials");
-        // dA = dout . W_out
-        if (O.sb >= 0)
-            gemm_x6_pre(dout, dld, m.wsplit + O.sb, O.sb_ld, (int64_t)O.sb_rows * O.sb_ld, m.dA, O.in, nullptr, n, O.in,
-                        O.out, s, dld > O.out, amax_slot(m, kAmaxOut), wscale_at(m, O.sbs));
-        else
-            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dout, dld, P + O.w, O.in, m.dA, O.in, nullptr, n, O.in, O.out, 1, s,
-                     dld > O.out);
+        // dA = dout . W_out (into the input gradient when the output layer reads the model input)
+        float* dA = nh > 0 ? m.dA : m.dX;
+        if (dA) {
+            if (O->sb >= 0)
+                gemm_x6_pre(dout, dld, m.wsplit + O->sb, O->sb_ld, (int64_t)O->sb_rows * O->sb_ld, dA, O->in, nullptr, n, O->in,
+                            O->out, s, dld > O->out, amax_slot(m, kAmaxOut), wscale_at(m, O->sbs));
+            else
+                gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dout, dld, P + O->w, O->in, dA, O->in, nullptr, n, O->in, O->out, 1, s,
+                         dld > O->out, false, amax_slot(m, kAmaxOut), nullptr);
+        }
     }
     for (int l = nh - 1; l >= 0; l--) {
         const Layer& L = m.L[l];
         int nb = (int)ceil_div(n, mlp::LNB_ROWS);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
-        const bool rank1 = O.out == 1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
-        hipLaunchKernelGGL(rank1 ? mlp::ln_act_bwd_head_any(L.out) : mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, rank1 ? nullptr : m.dA, m.xhat[l],
+        const bool r1 = rank1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
+        const float* dA_in = l == nh - 1 ? dA_top : m.dA;
+        hipLaunchKernelGGL(r1 ? mlp::ln_act_bwd_head_any(L.out) : mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
                            reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
-                           h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), rank1 ? dout : nullptr,
-                           rank1 ? P + O.w : nullptr, rank1 ? m.hpart : nullptr);
+                           h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
+                           r1 ? P + O->w : nullptr, r1 ? m.hpart : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
-        if (rank1) reduce_partials(m, m.hpart, nb, O.in + 1, O.in + 1, G + O.w, s);  // [w | b] contiguous
+        if (r1) reduce_partials(m, m.hpart, nb, O->in + 1, O->in + 1, G + O->w, s);  // [w | b] contiguous
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
         reduce_partials(m, m.cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
         RLGPU_CHECK_HIP(hipGetLastError());
-        if (l == 0)
-            weight_grad(m, m.dZ, L.out, X, h->x_ld, L.in, n, G + L.w, s, true, amax_slot(m, kAmaxDZ + l), amax_x(h, m));
-        else
-            weight_grad(m, m.dZ, L.out, m.act[l - 1], L.in, L.in, n, G + L.w, s, false, amax_slot(m, kAmaxDZ + l),
-                        amax_slot(m, l - 1));
-        if (l > 0 && L.sb >= 0)
-            gemm_x6_pre(m.dZ, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, m.dA, L.in, nullptr, n, L.in,
+        const Input a = l > 0 ? Input{m.act[l - 1], L.in, amax_slot(m, l - 1), false} : x;
+        weight_grad(m, m.dZ, L.out, a.X, a.ld, L.in, n, G + L.w, s, a.tail_ok, amax_slot(m, kAmaxDZ + l), a.amax);
+        float* dA = l > 0 ? m.dA : m.dX;  // the first layer's only when the input gradient is wanted
+        if (!dA) continue;
+        if (L.sb >= 0)
+            gemm_x6_pre(m.dZ, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, dA, L.in, nullptr, n, L.in,
                         L.out, s, false, amax_slot(m, kAmaxDZ + l), wscale_at(m, L.sbs));
-        else if (l > 0)
-            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, m.dA, L.in, nullptr, n, L.in, L.out, 1, s);
+        else
+            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, dA, L.in, nullptr, n, L.in, L.out, 1, s, false,
+                     false, amax_slot(m, kAmaxDZ + l), nullptr);
     }
 }
 
@@ -542,27 +581,45 @@ void gather_obs(rlgpu_ppo* h, const float* obs, const int32_t* idx, int64_t star
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
-// bf16 inference forward of n rows; result in h->logits_h [n, out] (bf16).  Model::Forward with
-// halfPrec (Models.cpp:42-68): every module runs on the bf16 copy, activations rounded to bf16.
-void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, const uint16_t* weights = nullptr) {
-    Model& m = h->M[mi];
+// The Linear layers a 16-bit forward of model mi runs through: the shared head's first (for the
+// policy / critic), then the model's -- Model::Forward chained as InferPolicyProbsFromModels /
+// InferCritic do (PPOLearner.cpp:90-91,188-191).  The shared head's f32 output re-enters the policy
+// as bf16 (Models.cpp:64), which is exact, so the chain is one 16-bit network.
+struct Link {
+    const Layer* L;
+    bool hidden;  // [Linear -> LayerNorm -> LeakyReLU]; false: the output Linear
+};
+std::vector<Link> chain(const rlgpu_ppo* h, int mi) {
+    std::vector<Link> c;
+    if (mi != 2 && h->shared())
+        for (auto& L : h->M[2].L) c.push_back({&L, true});
+    const Model& m = h->M[mi];
+    for (size_t l = 0; l < m.L.size(); l++) c.push_back({&m.L[l], m.head_only || l + 1 < m.L.size()});
+    return c;
+}
+
+// bf16 inference forward of n rows through chain(mi); returns the 16-bit result [n, out] (h->logits_h
+// after an output Linear, else the last activation buffer).  Model::Forward with halfPrec
+// (Models.cpp:42-68): every module runs on the bf16 copy, activations rounded to bf16.
+const uint16_t* forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, const uint16_t* weights = nullptr) {
     const uint16_t* P = weights ? weights : h->half;
-    int nh = (int)m.L.size() - 1;
+    const auto c = chain(h, mi);
     {
         int64_t e = (int64_t)n * h->xh_ld;
-        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, m.in, n, h->xh, h->xh_ld);
+        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, h->cfg.obs_size, n, h->xh,
+                         h->xh_ld);
         RLGPU_CHECK_HIP(hipGetLastError());
     }
     const uint16_t* in = h->xh;
     int64_t ld = h->xh_ld;
     int cur = 0;
-    for (int l = 0; l <= nh; l++) {
-        const Layer& L = m.L[l];
+    for (const Link& k : c) {
+        const Layer& L = *k.L;
         mlp::HGemmArgs g;
         g.A = in;
         g.B = P + L.hw;
         g.bias = P + L.hb;
-        g.C = l < nh ? h->zh : h->logits_h;
+        g.C = k.hidden ? h->zh : h->logits_h;
         g.lda = ld;
         g.ldb = L.in_pad;
         g.ldc = L.out;
@@ -573,7 +630,7 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, co
         g.gy = (int)ceil_div(n, mlp::BM);
         RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::gemm_bf16, dim3(g.gx * g.gy), dim3(256), 0, s, g);
         RLGPU_CHECK_HIP(hipGetLastError());
-        if (l == nh) break;
+        if (!k.hidden) return h->logits_h;
         const uint16_t* gg = L.hg >= 0 ? P + L.hg : nullptr;
         const uint16_t* bb = L.hbe >= 0 ? P + L.hbe : nullptr;
         hipLaunchKernelGGL(h->cfg.infer_fp16 ? mlp::ln_act_fwd_bf16_any<true>(L.out) : mlp::ln_act_fwd_bf16_any<false>(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
@@ -583,6 +640,7 @@ void forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStream_t s, co
         ld = L.out;
         cur ^= 1;
     }
+    return in;
 }
 
 // Fused inference (infer::mlp_infer): one launch per forward when every layer fits the kernel's
@@ -592,11 +650,11 @@ unsigned long long* g_infer_trace = nullptr;  // rlgpu_debug_infer_trace
 bool fused_ok(const rlgpu_ppo* h, int mi) {
     const char* e = getenv("RLGPU_FUSED_INFER");
     if (e && atoi(e) == 0) return false;
-    const Model& m = h->M[mi];
-    if ((int)m.L.size() > infer::kMaxLinear) return false;
-    for (size_t l = 0; l < m.L.size(); l++) {
-        if (m.L[l].in > infer::IMAX) return false;
-        if (m.L[l].out > (l + 1 < m.L.size() ? infer::IMAX : infer::IOUT)) return false;
+    const auto c = chain(h, mi);
+    if ((int)c.size() > infer::kMaxLinear || c.back().hidden) return false;  // the kernel ends on an output Linear
+    for (size_t l = 0; l < c.size(); l++) {
+        if (c[l].L->in > infer::IMAX) return false;
+        if (c[l].L->out > (l + 1 < c.size() ? infer::IMAX : infer::IOUT)) return false;
     }
     return true;
 }
@@ -606,17 +664,17 @@ bool fused_ok(const rlgpu_ppo* h, int mi) {
 void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode, float* out_f,
                  const uint8_t* masks, int det, uint64_t step, int32_t* act, float* logp, const uint8_t* row_sel, int sel,
                  hipStream_t s) {
-    const Model& m = h->M[mi];
+    const auto c = chain(h, mi);
     infer::InferArgs a{};
     a.X = X;
     a.n = n;
-    a.in = m.in;
+    a.in = h->cfg.obs_size;
     a.P = ver ? h->half_ver : h->half;
     a.F = ver ? h->frag_ver : h->frag;
-    a.nl = (int)m.L.size();
-    a.width[0] = m.in;
+    a.nl = (int)c.size();
+    a.width[0] = a.in;
     for (int l = 0; l < a.nl; l++) {
-        const Layer& L = m.L[l];
+        const Layer& L = *c[l].L;
         a.width[l + 1] = L.out;
         a.fw[l] = L.fw;
         a.hb[l] = L.hb;
@@ -640,9 +698,14 @@ void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
-void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, int out, float lr) {
+// Model layout in the flat buffers.  out = 0: the shared head (hidden layers only, PPOLearner.cpp:56-64);
+// input_grad: the model reads the shared head's output, so its first layer also gets the transposed
+// weight planes for the input gradient.
+void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, int out, float lr, bool input_grad = false) {
+    m.head_only = out == 0;
+    if (m.head_only) nl--;  // the last hidden layer takes the output layer's slot in the loop below
     m.in = in;
-    m.out = out;
+    m.out = m.head_only ? layers[nl] : out;
     m.lr = lr;
     m.mode = h->cfg.train_gemm;
     m.off = h->nparams;
@@ -650,13 +713,14 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
     for (int l = 0; l <= nl; l++) {
         Layer L;
         L.in = prev;
-        L.out = l < nl ? layers[l] : out;
+        const bool hidden = l < nl || m.head_only;
+        L.out = l < nl ? layers[l] : m.out;
         L.w = h->nparams;
         h->nparams += (int64_t)L.in * L.out;
         L.b = h->nparams;
         h->nparams += L.out;
         L.g = L.be = -1;
-        if (l < nl && h->cfg.layer_norm) {
+        if (hidden && h->cfg.layer_norm) {
             L.g = h->nparams;
             h->nparams += L.out;
             L.be = h->nparams;
@@ -688,7 +752,7 @@ void build_model(rlgpu_ppo* h, Model& m, int in, const int32_t* layers, int nl, 
             m.nsplit += np * (int64_t)L.sf_rows * L.sf_ld;
             L.sfs = m.nscale;
             m.nscale += L.sf_rows;
-            if (l > 0) {  // dA of the first layer is never needed
+            if (l > 0 || input_grad) {  // dA of the first layer only behind the shared head
                 L.sb_rows = (int)ceil_div(L.in, rpad) * rpad;
                 L.sb_ld = (int)ceil_div(L.out, mlp::XKMAX) * mlp::XKMAX;
                 L.sb = m.nsplit;
@@ -729,8 +793,10 @@ void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, uint16_t* 
 }
 
 void refresh_half(rlgpu_ppo* h, hipStream_t s) {
-    for (int mi = 0; mi < 2; mi++) half_from(h, mi, h->params + h->M[mi].off, h->half, h->frag, s);
-    h->split_dirty[0] = h->split_dirty[1] = true;
+    for (int mi = 0; mi < h->nm; mi++) {
+        half_from(h, mi, h->params + h->M[mi].off, h->half, h->frag, s);
+        h->split_dirty[mi] = true;
+    }
 }
 
 }  // namespace
@@ -748,12 +814,25 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             RLGPU_REQUIRE(cfg->policy_layers[i] > 0 && cfg->policy_layers[i] <= 2048, "hidden sizes must be in [1, 2048]");
         for (int i = 0; i < cfg->n_critic_layers; i++)
             RLGPU_REQUIRE(cfg->critic_layers[i] > 0 && cfg->critic_layers[i] <= 2048, "hidden sizes must be in [1, 2048]");
+        RLGPU_REQUIRE(cfg->n_shared_layers >= 0 && cfg->n_shared_layers <= RLGPU_MAX_LAYERS, "0..8 shared-head layers");
+        for (int i = 0; i < cfg->n_shared_layers; i++)
+            RLGPU_REQUIRE(cfg->shared_layers[i] > 0 && cfg->shared_layers[i] <= 2048, "hidden sizes must be in [1, 2048]");
         auto* h = new rlgpu_ppo();
         try {
             h->cfg = *cfg;
-            build_model(h, h->M[0], cfg->obs_size, cfg->policy_layers, cfg->n_policy_layers, cfg->num_actions, cfg->policy_lr);
+            const bool sh = cfg->n_shared_layers > 0;
+            h->nm = sh ? 3 : 2;
+            // PPOLearner::MakeModels (PPOLearner.cpp:42-74): behind a shared head the policy / critic
+            // take its last width as input
+            const int min = sh ? cfg->shared_layers[cfg->n_shared_layers - 1] : cfg->obs_size;
+            build_model(h, h->M[0], min, cfg->policy_layers, cfg->n_policy_layers, cfg->num_actions, cfg->policy_lr, sh);
             h->nparams = (h->nparams + 63) / 64 * 64;  // 256-byte aligned model start: float4 weight rows
-            build_model(h, h->M[1], cfg->obs_size, cfg->critic_layers, cfg->n_critic_layers, 1, cfg->critic_lr);
+            build_model(h, h->M[1], min, cfg->critic_layers, cfg->n_critic_layers, 1, cfg->critic_lr, sh);
+            if (sh) {  // shared head LR = min(policy, critic) (PPOLearner::SetLearningRates, :652-663)
+                h->nparams = (h->nparams + 63) / 64 * 64;
+                build_model(h, h->M[2], cfg->obs_size, cfg->shared_layers, cfg->n_shared_layers, 0,
+                            std::min(cfg->policy_lr, cfg->critic_lr));
+            }
             int64_t P = h->nparams, R = cfg->max_rows;
             h->params = h->alloc<float>(P);
             h->grads = h->alloc<float>(P);
@@ -767,8 +846,9 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             RLGPU_CHECK_HIP(hipMemset(h->grads, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->exp_avg, 0, P * 4));
             RLGPU_CHECK_HIP(hipMemset(h->exp_avg_sq, 0, P * 4));
-            for (auto& m : h->M) {
-                int nh = (int)m.L.size() - 1;
+            for (int mi = 0; mi < h->nm; mi++) {
+                Model& m = h->M[mi];
+                const int nh = nhid(m);
                 for (int l = 0; l < nh; l++) {
                     m.xhat.push_back(h->alloc<float>(R * m.L[l].out));
                     m.act.push_back(h->alloc<float>(R * m.L[l].out));
@@ -787,16 +867,21 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 }
                 g_cus = cus;
             }
-            for (auto& m : h->M)
-                for (auto& L : m.L) {
+            for (int mi = 0; mi < h->nm; mi++)
+                for (auto& L : h->M[mi].L) {
+                    const Model& m = h->M[mi];
                     wmax = std::max<int64_t>(wmax, (int64_t)L.in * L.out);
                     // splits_for is non-decreasing in the row count, and z = ceil(n / chunk) <= splits
                     wpart_max = std::max<int64_t>(wpart_max, (int64_t)splits_for(m.mode, (int)R, L.out, L.in) * L.in * L.out);
                 }
             int64_t nb = ceil_div(R, std::min(std::min(mlp::LNB_ROWS, mlp::CS_ROWS), ppo::PL_ROWS));
-            for (auto& m : h->M) {
-                m.y = h->alloc<float>(R * omax);
-                m.dy = h->alloc<float>(R * ((omax + 3) / 4 * 4));
+            for (int mi = 0; mi < h->nm; mi++) {
+                Model& m = h->M[mi];
+                if (!m.head_only) {
+                    m.y = h->alloc<float>(R * omax);
+                    m.dy = h->alloc<float>(R * ((omax + 3) / 4 * 4));
+                }
+                if (sh && mi < 2) m.dX = h->alloc<float>(R * (int64_t)m.in);  // input gradient behind the shared head
                 m.dA = h->alloc<float>(R * H);
                 m.dZ = h->alloc<float>(R * H);
                 m.wpart = h->alloc<float>(wpart_max);
@@ -806,13 +891,13 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 if (m.nsplit) m.wsplit = h->alloc<uint16_t>(m.nsplit);
                 if (m.mode == RLGPU_GEMM_F16X3 && m.nscale) m.wscale = h->alloc<float>(m.nscale);
             }
-            if (cfg->train_gemm == RLGPU_GEMM_F16X3) {  // operand-scale shards: both models' slots + the obs
-                h->amax_count = (2 * (int64_t)kAmaxSlots + 1) * 64;
+            if (sh) h->dshared = h->alloc<float>(R * (int64_t)h->M[2].out);
+            if (cfg->train_gemm == RLGPU_GEMM_F16X3) {  // operand-scale shards: every model's slots + the obs
+                h->amax_count = (3 * (int64_t)kAmaxSlots + 1) * 64;
                 h->amax_all = h->alloc<float>(h->amax_count);
                 RLGPU_CHECK_HIP(hipMemset(h->amax_all, 0, h->amax_count * sizeof(float)));
-                h->M[0].amax = h->amax_all;
-                h->M[1].amax = h->amax_all + (int64_t)kAmaxSlots * 64;
-                h->x_amax = h->amax_all + 2 * (int64_t)kAmaxSlots * 64;
+                for (int mi = 0; mi < 3; mi++) h->M[mi].amax = h->amax_all + (int64_t)mi * kAmaxSlots * 64;
+                h->x_amax = h->amax_all + 3 * (int64_t)kAmaxSlots * 64;
             }
             RLGPU_CHECK_HIP(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
             RLGPU_CHECK_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -858,9 +943,10 @@ extern "C" int rlgpu_ppo_buffers(rlgpu_ppo* h, float** d_params, float** d_grads
 
 extern "C" int rlgpu_ppo_model_range(rlgpu_ppo* h, int32_t model, int64_t* offset, int64_t* count) {
     return rlgpu::guarded([&] {
-        RLGPU_REQUIRE(h && (model == 0 || model == 1), "model must be 0 (policy) or 1 (critic)");
-        if (offset) *offset = h->M[model].off;
-        if (count) *count = h->M[model].count;
+        RLGPU_REQUIRE(h && model >= 0 && model <= 2, "model must be 0 (policy), 1 (critic) or 2 (shared head)");
+        const bool present = model < h->nm;
+        if (offset) *offset = present ? h->M[model].off : h->nparams;
+        if (count) *count = present ? h->M[model].count : 0;
     });
 }
 
@@ -868,9 +954,9 @@ extern "C" int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream) 
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h, "null handle");
         hipStream_t s = rlgpu::as_stream(stream);
-        uint32_t sid = 0;
-        for (auto& m : h->M)
-            for (auto& L : m.L) {
+        uint32_t sid = 0;  // Philox stream per tensor, in model order (policy, critic, shared head)
+        for (int mi = 0; mi < h->nm; mi++)
+            for (auto& L : h->M[mi].L) {
                 float bound = 1.f / std::sqrt((float)L.in);
                 int64_t nw = (int64_t)L.in * L.out;
                 hipLaunchKernelGGL(ppo::init_uniform, dim3(ceil_div(nw, 256)), dim3(256), 0, s, h->params + L.w, nw, bound, seed,
@@ -900,19 +986,24 @@ extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision,
                                  void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h && d_in && d_out, "null argument");
-        RLGPU_REQUIRE(model == 0 || model == 1, "model must be 0 or 1");
+        RLGPU_REQUIRE(model >= 0 && model < h->nm, "model must be 0, 1 or (with a shared head) 2");
         RLGPU_REQUIRE(n >= 0 && n <= h->cfg.max_rows, "n must be in [0, max_rows]");
         if (n == 0) return;
         hipStream_t s = rlgpu::as_stream(stream);
+        const int64_t e = (int64_t)n * h->M[model].out;
         if (precision == 0) {
             gather_obs(h, d_in, nullptr, 0, n, s);
-            forward_train(h, model, h->x0, n, d_out, s);
+            if (h->shared()) forward_train(h, 2, obs_input(h), n, nullptr, s);
+            if (model == 2) {  // the shared head's last activation
+                RLGPU_CHECK_HIP(hipMemcpyAsync(d_out, model_input(h, 0).X, e * sizeof(float), hipMemcpyDeviceToDevice, s));
+            } else {
+                forward_train(h, model, model_input(h, model), n, d_out, s);
+            }
         } else if (fused_ok(h, model)) {
             infer_fused(h, model, false, d_in, n, 0, d_out, nullptr, 0, 0, nullptr, nullptr, nullptr, 0, s);
         } else {
-            forward_half(h, model, d_in, n, s);
-            int64_t e = (int64_t)n * h->M[model].out;
-            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, h->logits_h, d_out, e);
+            const uint16_t* y = forward_half(h, model, d_in, n, s);
+            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, y, d_out, e);
             RLGPU_CHECK_HIP(hipGetLastError());
         }
     });
@@ -950,7 +1041,10 @@ extern "C" int rlgpu_debug_infer_trace(void* d_buf) {
 extern "C" int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h && d_policy_params, "rlgpu_ppo_set_version: null argument");
-        half_from(h, 0, d_policy_params, h->half_ver, h->frag_ver, rlgpu::as_stream(stream));
+        hipStream_t s = rlgpu::as_stream(stream);
+        half_from(h, 0, d_policy_params, h->half_ver, h->frag_ver, s);
+        // the version's shared head follows its policy (GetPolicyModels, PPOLearner.cpp:665-674)
+        if (h->shared()) half_from(h, 2, d_policy_params + h->M[0].count, h->half_ver, h->frag_ver, s);
         h->has_ver = true;
     });
 }
@@ -1031,6 +1125,9 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         float bsr = (float)n / (float)batch_size;  // PPOLearner.cpp:374
         int A = h->cfg.num_actions;
         gather_obs(h, d_obs, d_index, start, n, s);  // one gathered, padded copy serves both models
+        // the shared head's forward once per minibatch (PPOLearner.cpp:395-398); policy and critic read it
+        const Input obs_in = obs_input(h), xin = model_input(h, 0);
+        if (h->shared()) forward_train(h, 2, obs_in, n, nullptr, s);
         // the critic's pass runs on the auxiliary stream (disjoint parameters, gradients, workspace
         // and metric slots), overlapping the policy's; the caller's stream waits for both
         static const bool serial = getenv("RLGPU_SERIAL_MINIBATCH") != nullptr;  // experiment switch
@@ -1041,21 +1138,27 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         }
         Model& pm = h->M[0];
         Model& cm = h->M[1];
-        forward_train(h, 1, h->x0, n, cm.y, cs);
+        forward_train(h, 1, xin, n, cm.y, cs);
         hipLaunchKernelGGL(ppo::critic_loss, dim3(ceil_div(n, 256)), dim3(256), 0, cs, cm.y, d_target, d_index, start, n,
                            bsr, cm.dy, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 1, h->x0, n, cm.dy, cs);
+        backward(h, 1, xin, n, cm.dy, cs);
         if (!serial) RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
         // policy on the caller's stream
-        forward_train(h, 0, h->x0, n, pm.y, s);
+        forward_train(h, 0, xin, n, pm.y, s);
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
         hipLaunchKernelGGL(ppo::policy_loss_any(A), dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
                            d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
                            1.f / std::log((float)A), pm.dy, dout_ld(A), d_metrics, pm.cpart, amax_slot(pm, kAmaxOut));
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 0, h->x0, n, pm.dy, s, pm.cpart, pl_blocks);
+        backward(h, 0, xin, n, pm.dy, s, pm.cpart, pl_blocks);
         if (!serial) RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
+        if (h->shared()) {  // (ppoLoss + criticLoss).backward() through the shared features (:498)
+            const int64_t e = (int64_t)n * h->M[2].out;
+            hipLaunchKernelGGL(ppo::add2, dim3(ceil_div(ceil_div(e, 4), 256)), dim3(256), 0, s, pm.dX, cm.dX, h->dshared, e);
+            RLGPU_CHECK_HIP(hipGetLastError());
+            backward(h, 2, obs_in, n, h->dshared, s);
+        }
     });
 }
 
@@ -1067,10 +1170,11 @@ extern "C" int rlgpu_ppo_optimizer_step(rlgpu_ppo* h, float* d_metrics, void* st
         const auto& c = h->cfg;
         double bc1 = 1.0 - std::pow((double)c.beta1, (double)h->step);
         double bc2 = 1.0 - std::pow((double)c.beta2, (double)h->step);
-        for (int mi = 0; mi < 2; mi++) {
+        const int slot[3] = {RLGPU_M_GRAD_NORM_POLICY, RLGPU_M_GRAD_NORM_CRITIC, RLGPU_M_GRAD_NORM_SHARED};
+        for (int mi = 0; mi < h->nm; mi++) {
             Model& m = h->M[mi];
             float* coef = h->scratch + 600 + mi;
-            float* norm_out = d_metrics ? d_metrics + (mi == 0 ? RLGPU_M_GRAD_NORM_POLICY : RLGPU_M_GRAD_NORM_CRITIC) : nullptr;
+            float* norm_out = d_metrics ? d_metrics + slot[mi] : nullptr;
             sumsq_coef(h, h->grads + m.off, m.count, c.max_grad_norm, coef, norm_out, s);
             double lr = m.lr;
             float decay_mul = (float)(1.0 - lr * (double)c.weight_decay);

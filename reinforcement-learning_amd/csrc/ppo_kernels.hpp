@@ -334,6 +334,21 @@ __global__ void critic_loss(const float* vals, const float* target, const int32_
     if ((threadIdx.x & 63) == 0 && metrics) atomicAdd(&metrics[3], contrib);
 }
 
+// out = a + b over n floats (the shared head's output gradient: policy + critic input gradients),
+// 4 per thread where the three spans are 16-byte aligned
+__global__ void add2(const float* a, const float* b, float* out, int64_t n) {
+    const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (e >= n) return;
+    const bool vec = e + 4 <= n && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                                     reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    if (vec) {
+        const float4 x = *reinterpret_cast<const float4*>(a + e), y = *reinterpret_cast<const float4*>(b + e);
+        *reinterpret_cast<float4*>(out + e) = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+        return;
+    }
+    for (int64_t k = e; k < e + 4 && k < n; k++) out[k] = a[k] + b[k];
+}
+
 // sum of squares partials (fixed grid -> deterministic)
 __global__ void __launch_bounds__(256) sumsq_partial(const float* x, int64_t n, float* part) {
     __shared__ float red[4];

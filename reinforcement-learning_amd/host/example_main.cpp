@@ -3,10 +3,13 @@
 // ExampleMain builds the 2v2 EnvSet (AdvancedObs, DefaultAction, the 13 weighted rewards,
 // NoTouch(8) + ScoreLimit(3), KickoffState; ExampleMain.cpp:128-226), sets the LearnerConfig /
 // PPOLearnerConfig of ExampleMain.cpp:340-430 and calls Learner::Start.  Here the plugin set is
-// the one built into the env kernel and the config is rlgpu_learner_default_config; the loop is
-// GGL::Learner::Start over a fixed number of iterations, printing the reference's report keys.
+// the one built into the env kernel and the config is rlgpu_learner_default_config with
+// ExampleMain's model topology: shared head [384, 384], policy and critic [384] x 3 (the sizes its
+// log prints, run_out.log:25-28; ExampleMain.cpp:478-522); --c2-model selects BASELINE config C2's
+// [512, 512] actor / critic without a shared head.  The loop is GGL::Learner::Start over a fixed
+// number of iterations, printing the reference's report keys.
 //
-//   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--f32-gemm]
+//   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--f32-gemm] [--c2-model]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,13 +21,21 @@ int main(int argc, char** argv) {
     rlgpu_learner_config cfg;
     rlgpu_learner_default_config(&cfg);
     long iterations = 3;
+    cfg.n_shared_layers = 2;
+    cfg.shared_layers[0] = cfg.shared_layers[1] = 384;
+    cfg.n_policy_layers = cfg.n_critic_layers = 3;
+    for (int l = 0; l < 3; l++) cfg.policy_layers[l] = cfg.critic_layers[l] = 384;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "--iterations") && i + 1 < argc) iterations = std::atol(argv[++i]);
         else if (!std::strcmp(argv[i], "--arenas") && i + 1 < argc) cfg.num_arenas = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rollout") && i + 1 < argc) cfg.rollout_len = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--f32-gemm")) cfg.train_gemm = RLGPU_GEMM_F32;
-        else {
-            std::fprintf(stderr, "usage: %s [--iterations N] [--arenas A] [--rollout T] [--f32-gemm]\n", argv[0]);
+        else if (!std::strcmp(argv[i], "--c2-model")) {
+            cfg.n_shared_layers = 0;
+            cfg.n_policy_layers = cfg.n_critic_layers = 2;
+            for (int l = 0; l < 2; l++) cfg.policy_layers[l] = cfg.critic_layers[l] = 512;
+        } else {
+            std::fprintf(stderr, "usage: %s [--iterations N] [--arenas A] [--rollout T] [--f32-gemm] [--c2-model]\n", argv[0]);
             return 2;
         }
     }
@@ -32,6 +43,19 @@ int main(int argc, char** argv) {
         hipStream_t s = nullptr;
         if (hipStreamCreate(&s) != hipSuccess) throw std::runtime_error("hipStreamCreate failed");
         GGL::Learner learner(cfg, nullptr, s);
+        {  // "Model parameter counts:" (PPOLearner.cpp:24-33; ModelSet order: critic, policy, shared_head)
+            int64_t cnt[3] = {0, 0, 0}, total = 0;
+            for (int m = 0; m < 3; m++) RLGC::RlgpuCheck(rlgpu_ppo_model_range(learner.ppo().handle(), m, nullptr, &cnt[m]), "model range");
+            std::printf("Model parameter counts:\n");
+            const int order[3] = {1, 0, 2};
+            const char* names[3] = {"policy", "critic", "shared_head"};
+            for (int m : order)
+                if (cnt[m]) {
+                    std::printf("\t\"%s\": %lld\n", names[m], (long long)cnt[m]);
+                    total += cnt[m];
+                }
+            std::printf("\t[Total]: %lld\n", (long long)total);
+        }
         for (long it = 0; it < iterations; it++) {
             rlgpu_learner_report r = learner.Iterate();
             const double total = r.collect_s + r.consume_s + r.learn_s;

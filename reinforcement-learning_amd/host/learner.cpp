@@ -217,6 +217,8 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     pc.n_policy_layers = cfg.n_policy_layers;
     std::memcpy(pc.critic_layers, cfg.critic_layers, sizeof(pc.critic_layers));
     pc.n_critic_layers = cfg.n_critic_layers;
+    std::memcpy(pc.shared_layers, cfg.shared_layers, sizeof(pc.shared_layers));
+    pc.n_shared_layers = cfg.n_shared_layers;
     pc.layer_norm = 1;
     pc.leaky_slope = 0.01f;
     pc.policy_lr = cfg.policy_lr;

@@ -30,7 +30,7 @@ import shutil
 import warnings
 
 STATS_FILE = "RUNNING_STATS.json"          # Learner.cpp:221
-MODEL_NAMES = ("policy", "critic")         # PPOLearner model names (PPOLearner.cpp:13-74)
+MODEL_NAMES = ("policy", "critic", "shared_head")  # PPOLearner model names (PPOLearner.cpp:42-74)
 OPTIM_FILE = "RLGPU_OPTIM.safetensors"
 
 
@@ -128,7 +128,8 @@ def read_model_state(path):
 
 def save(learner, folder, keep=8):
     """Learner::Save: <folder>/<total_timesteps>/{RUNNING_STATS.json, POLICY.lt, CRITIC.lt,
-    RLGPU_OPTIM.safetensors}, then prune to `keep` checkpoints (-1 keeps all).  Returns the path."""
+    [SHARED_HEAD.lt,] RLGPU_OPTIM.safetensors}, then prune to `keep` checkpoints (-1 keeps all).
+    Returns the path."""
     import torch
     from safetensors.torch import save_file
     path = os.path.join(folder, str(int(learner.total_steps)))
@@ -138,11 +139,12 @@ def save(learner, folder, keep=8):
     with open(os.path.join(path, STATS_FILE), "w") as f:
         json.dump(stats, f, indent=4)
     ppo = learner.ppo
-    for mi, name in enumerate(MODEL_NAMES):
-        write_model(ppo.torch_module(mi), model_path(path, name))
+    for mi in ppo.models:
+        write_model(ppo.torch_module(mi), model_path(path, MODEL_NAMES[mi]))
     step, m, v = ppo.optimizer_state()
     t = {"step": torch.tensor([step], dtype=torch.int64)}
-    for mi, name in enumerate(MODEL_NAMES):
+    for mi in ppo.models:
+        name = MODEL_NAMES[mi]
         o, c = ppo.model_range(mi)
         t[name + ".exp_avg"] = m[o:o + c].detach().cpu().contiguous()
         t[name + ".exp_avg_sq"] = v[o:o + c].detach().cpu().contiguous()
@@ -171,7 +173,8 @@ def load(learner, folder, allow_missing_models=True):
     if "return_stat" in j:
         learner.return_stat.read_json(j["return_stat"])
     ppo = learner.ppo
-    for mi, name in enumerate(MODEL_NAMES):
+    for mi in ppo.models:
+        name = MODEL_NAMES[mi]
         p = model_path(path, name)
         if not os.path.exists(p):
             if allow_missing_models:
@@ -192,9 +195,10 @@ def load(learner, folder, allow_missing_models=True):
         from safetensors.torch import load_file
         t = load_file(op)
         step, m, v = ppo.optimizer_state()
-        for mi, name in enumerate(MODEL_NAMES):
+        for mi in ppo.models:
+            name = MODEL_NAMES[mi]
             o, c = ppo.model_range(mi)
-            if t[name + ".exp_avg"].numel() != c:
+            if name + ".exp_avg" not in t or t[name + ".exp_avg"].numel() != c:
                 raise ValueError(f"optimizer state in {op} does not match the model sizes")
             m[o:o + c].copy_(t[name + ".exp_avg"].to(m.device))
             v[o:o + c].copy_(t[name + ".exp_avg_sq"].to(v.device))

@@ -119,10 +119,18 @@ def moments_mean_std(m3):
 
 
 def broadcast_(t, group=None):
-    """Rank 0's tensor into `t` on every rank, in place (RCCL for device tensors on nccl; through the
-    host for gloo)."""
+    """Rank 0's tensor into `t` on every rank, in place: RCCL for device tensors on nccl, whose host
+    tensors (the header, version timestamps) travel through the current device; gloo through the
+    host."""
     backend = dist.get_backend(group)
-    if t.device.type == "cpu" or backend == "nccl":
+    if backend == "nccl":
+        if t.device.type == "cuda":
+            dist.broadcast(t, 0, group=group)
+        else:  # RCCL cannot take host buffers
+            d = t.to(torch.device("cuda", torch.cuda.current_device()))
+            dist.broadcast(d, 0, group=group)
+            t.copy_(d.cpu())
+    elif t.device.type == "cpu":
         dist.broadcast(t, 0, group=group)
     else:
         c = t.cpu()

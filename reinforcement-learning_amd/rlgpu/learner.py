@@ -109,34 +109,39 @@ def sample_finished_rows(seed, rank, iteration, ends, n):
     return out[:m.value]
 
 
-def sync_from_rank0(learner, group=None):
+def sync_from_rank0(learner, group=None, error=None):
     """Every rank takes rank 0's training state: parameters, AdamW moments and step, step counters,
     return statistics and the old policy versions.  Only rank 0 reads the checkpoint folder
     (Learner.cpp:145-153 loads in the single-process reference); the ranks need not share a
-    filesystem, and replicas can never start diverged."""
+    filesystem, and replicas can never start diverged.  `error`: rank 0's load failure -- the
+    header carries it first, so every rank raises together instead of waiting in a broadcast rank 0
+    never reaches."""
     import torch
     from .dist import broadcast_
     st = learner._stats()
     ppo = learner.ppo
     step, m, v = ppo.optimizer_state()
     vers = learner.versions.versions if learner.versions is not None else []
-    hdr = torch.tensor([float(learner.last_checkpoint is not None), st.total_steps, st.iteration, st.return_n,
-                        st.return_mean, st.return_m2, step, len(vers)], dtype=torch.float64)
+    hdr = torch.tensor([float(error is None), float(learner.last_checkpoint is not None), st.total_steps,
+                        st.iteration, st.return_n, st.return_mean, st.return_m2, step, len(vers)], dtype=torch.float64)
     broadcast_(hdr, group)
-    loaded, total, it, rn, rmean, rm2, step, nv = hdr.tolist()
-    if not loaded:
-        return
-    for t in (ppo.params, m, v):
-        broadcast_(t, group)
-    st.total_steps, st.iteration, st.return_n = int(total), int(it), int(rn)
-    st.return_mean, st.return_m2 = rmean, rm2
-    learner._set_stats(st)
-    ppo.set_optimizer_step(int(step))
-    ppo.refresh_half()
+    ok, loaded, total, it, rn, rmean, rm2, step, nv = hdr.tolist()
+    if not ok:
+        raise RuntimeError(f"rank 0 failed to load the checkpoint: {error!r}" if error is not None else
+                           "rank 0 failed to load the checkpoint (see its log)")
+    if loaded:
+        for t in (ppo.params, m, v):
+            broadcast_(t, group)
+        st.total_steps, st.iteration, st.return_n = int(total), int(it), int(rn)
+        st.return_mean, st.return_m2 = rmean, rm2
+        learner._set_stats(st)
+        ppo.set_optimizer_step(int(step))
+        ppo.refresh_half()
+    # old versions whenever rank 0 holds any (policy_versions/ may exist without a checkpoint)
     if learner.versions is not None and int(nv) > 0:
         ts = torch.tensor([float(x.timesteps) for x in vers] if vers else [0.0] * int(nv), dtype=torch.float64)
         broadcast_(ts, group)
-        like = ppo.model_slice(0)
+        like = ppo.policy_version()
         params = [x.params for x in vers] if vers else [torch.empty_like(like) for _ in range(int(nv))]
         for t in params:
             broadcast_(t, group)
@@ -169,6 +174,7 @@ class LearnerConfig:
         self.return_samples = 150         # Learner.cpp:959-967
         self.policy_layers = (512, 512)
         self.critic_layers = (512, 512)
+        self.shared_layers = ()            # PPOLearnerConfig::sharedHead ((384, 384) in the reference's run log)
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
         self.train_gemm = 2               # rlgpu_ppo_config.train_gemm: 2 = f32 via scaled fp16 split (H3), 0 = bf16 x6 split, 1 = f32 MFMA
@@ -203,7 +209,8 @@ class _CConfig(ctypes.Structure):
                 ("deterministic", ctypes.c_int32), ("train_gemm", ctypes.c_int32), ("infer_fp16", ctypes.c_int32),
                 ("frame_stack", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
-                ("mesh_object_ntris", ctypes.c_void_p)]
+                ("mesh_object_ntris", ctypes.c_void_p),
+                ("shared_layers", ctypes.c_int32 * MAX_LAYERS), ("n_shared_layers", ctypes.c_int32)]
 
 
 class _CRollout(ctypes.Structure):
@@ -291,6 +298,9 @@ class Learner:
         for i, v in enumerate(cfg.critic_layers):
             c.critic_layers[i] = v
         c.n_policy_layers, c.n_critic_layers = len(cfg.policy_layers), len(cfg.critic_layers)
+        for i, v in enumerate(cfg.shared_layers):
+            c.shared_layers[i] = v
+        c.n_shared_layers = len(cfg.shared_layers)
         c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
         c.frame_stack = cfg.frame_stack
         c.rank, c.world = rank, world
@@ -309,7 +319,8 @@ class Learner:
         self.env = EnvSet.wrap(eh.value, self.device, cfg.tick_skip, cfg.action_delay, owner=self)
         max_rows = max(min(cfg.mini_batch_size, cfg.rollout_len * 4 * cfg.num_arenas), min(4 * cfg.num_arenas, 65536))
         self.ppo = PPO.wrap(ph.value, self.device, cfg.policy_layers, cfg.critic_layers, max_rows,
-                            obs_size=OBS * max(1, cfg.frame_stack), metrics_source=self._metrics, owner=self)
+                            obs_size=OBS * max(1, cfg.frame_stack), metrics_source=self._metrics, owner=self,
+                            shared_layers=cfg.shared_layers)
         r = _CRollout()
         _lib.check(L.rlgpu_learner_rollout(h, ctypes.byref(r)), "rlgpu_learner_rollout")
         T, P, W = r.T, r.P, r.obs_width
@@ -345,12 +356,18 @@ class Learner:
         self.last_checkpoint = None
         if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-153)
             from . import checkpoint as _ckpt
+            err = None
             if rank == 0:  # rank 0 reads the folder, every other rank receives its state
-                self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
-                if self.versions is not None:
-                    self.versions.load_versions(self.total_steps)
+                try:
+                    self.last_checkpoint = _ckpt.load(self, cfg.checkpoint_folder)
+                    if self.versions is not None:
+                        self.versions.load_versions(self.total_steps)
+                except Exception as e:  # noqa: BLE001 -- re-raised below, on every rank
+                    err = e
             if world > 1:
-                sync_from_rank0(self, group)
+                sync_from_rank0(self, group, err)
+            elif err is not None:
+                raise err
 
     def close(self):
         if getattr(self, "_h", None):

@@ -3,7 +3,8 @@ GGL::PPOLearner (GigaLearnCPP/src/private/GigaLearnCPP/PPO/PPOLearner.h:41-59) a
 GGL::Model (Util/Models.h:21-163).
 
 Method map (reference -> here):
-    Model(name, ModelConfig)                         -> part of PPO(...) (policy = 0, critic = 1)
+    Model(name, ModelConfig)                         -> part of PPO(...) (policy = 0, critic = 1,
+                                                        shared_head = 2 when shared_layers is given)
     PPOLearner::InferActions(obs, masks, ...)        -> infer_actions(obs, masks, step)
     PPOLearner::InferCritic / InferCriticBatched     -> infer_critic(obs)
     PPOLearner::Learn per-minibatch body (:341-475)  -> minibatch(...)
@@ -19,7 +20,8 @@ from ._lib import alias
 MAX_LAYERS = 8
 NUM_METRICS = 16
 METRICS = ("entropy", "kl", "policy_loss", "critic_loss", "ratio", "clip_fraction", "count",
-           "grad_norm_policy", "grad_norm_critic")
+           "grad_norm_policy", "grad_norm_critic", "grad_norm_shared")
+MODEL_NAMES = ("policy", "critic", "shared_head")  # GGL::Model::modelName (PPOLearner.cpp:66-72)
 
 
 class _Cfg(ctypes.Structure):
@@ -32,7 +34,8 @@ class _Cfg(ctypes.Structure):
                 ("weight_decay", ctypes.c_float), ("clip_range", ctypes.c_float),
                 ("entropy_scale", ctypes.c_float), ("max_grad_norm", ctypes.c_float),
                 ("max_rows", ctypes.c_int32), ("seed", ctypes.c_uint64), ("train_gemm", ctypes.c_int32),
-                ("infer_fp16", ctypes.c_int32)]
+                ("infer_fp16", ctypes.c_int32), ("shared_layers", ctypes.c_int32 * MAX_LAYERS),
+                ("n_shared_layers", ctypes.c_int32)]
 
 GEMM_F32X6, GEMM_F32, GEMM_F16X3 = 0, 1, 2  # rlgpu_ppo_config.train_gemm (include/rlgpu_ppo.h)
 
@@ -70,7 +73,8 @@ def _bind():
 
 
 def param_count(obs_size, num_actions, layers, out=None, layer_norm=True):
-    """Parameter count of a GGL::Model (Linear [+LayerNorm] per hidden layer + output Linear)."""
+    """Parameter count of a GGL::Model (Linear [+LayerNorm] per hidden layer + output Linear;
+    out=0: no output layer, the shared head)."""
     n, prev = 0, obs_size
     for h in layers:
         n += prev * h + h + (2 * h if layer_norm else 0)
@@ -80,13 +84,14 @@ def param_count(obs_size, num_actions, layers, out=None, layer_norm=True):
 
 
 class PPO:
-    """Policy + critic (no shared head), AdamW, fp32 training / bf16 inference, all in HBM."""
+    """Policy + critic (+ an optional shared head in front of both: PPOLearnerConfig::sharedHead),
+    AdamW, fp32 training / bf16 inference, all in HBM."""
 
     def __init__(self, obs_size=167, num_actions=90, policy_layers=(512, 512), critic_layers=(512, 512),
                  layer_norm=True, policy_lr=2.5e-4, critic_lr=2.5e-4, clip_range=0.2, entropy_scale=0.035,
                  max_grad_norm=0.5, max_rows=50_000, seed=42, init=True, device="cuda:0",
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, leaky_slope=0.01, train_gemm=GEMM_F16X3,
-                 infer_fp16=False):
+                 infer_fp16=False, shared_layers=()):
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("PPO needs an MI355X: the product path has no CPU fallback")
@@ -100,6 +105,9 @@ class PPO:
             c.policy_layers[i] = v
         for i, v in enumerate(critic_layers):
             c.critic_layers[i] = v
+        c.n_shared_layers = len(shared_layers)
+        for i, v in enumerate(shared_layers):
+            c.shared_layers[i] = v
         c.layer_norm, c.leaky_slope = int(layer_norm), leaky_slope
         self.leaky_slope = leaky_slope
         c.policy_lr, c.critic_lr = policy_lr, critic_lr
@@ -114,6 +122,7 @@ class PPO:
         self.cfg = c
         self.obs_size, self.num_actions = obs_size, num_actions
         self.policy_layers, self.critic_layers, self.layer_norm = tuple(policy_layers), tuple(critic_layers), layer_norm
+        self.shared_layers = tuple(shared_layers)
         self.max_rows = max_rows
         p, g, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         _lib.check(L.rlgpu_ppo_buffers(h, ctypes.byref(p), ctypes.byref(g), ctypes.byref(n)), "rlgpu_ppo_buffers")
@@ -127,7 +136,7 @@ class PPO:
 
     @classmethod
     def wrap(cls, handle, device, policy_layers, critic_layers, max_rows, obs_size=167, num_actions=90,
-             layer_norm=True, leaky_slope=0.01, metrics_source=None, owner=None):
+             layer_norm=True, leaky_slope=0.01, metrics_source=None, owner=None, shared_layers=()):
         """A PPO view of a handle owned elsewhere (the C++ Learner's PPOLearner): not destroyed
         by this object.  metrics_source(reset) -> (sums, count) replaces the own metric buffer."""
         import torch
@@ -137,6 +146,7 @@ class PPO:
         self.device = torch.device(device)
         self.obs_size, self.num_actions = obs_size, num_actions
         self.policy_layers, self.critic_layers, self.layer_norm = tuple(policy_layers), tuple(critic_layers), layer_norm
+        self.shared_layers = tuple(shared_layers)
         self.leaky_slope, self.max_rows = leaky_slope, max_rows
         p, g, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         _lib.check(L.rlgpu_ppo_buffers(self._h, ctypes.byref(p), ctypes.byref(g), ctypes.byref(n)), "rlgpu_ppo_buffers")
@@ -173,11 +183,28 @@ class PPO:
         off, cnt = self.model_range(model)
         return (self.grads if grads else self.params)[off:off + cnt]
 
+    @property
+    def models(self):
+        """Model indices present: policy, critic (and the shared head)."""
+        return (0, 1, 2) if self.shared_layers else (0, 1)
+
     def flat(self, grads=False):
         """Concatenation of the models' parameters (or gradients) in torch parameters() order,
-        without the alignment gap between models."""
+        without the alignment gap between models (policy, critic, shared head)."""
         import torch
-        return torch.cat([self.model_slice(0, grads), self.model_slice(1, grads)])
+        return torch.cat([self.model_slice(m, grads) for m in self.models])
+
+    def policy_version(self):
+        """The flat parameters an old policy version holds: the policy's, then the shared head's
+        (PolicyVersionManager versions GetPolicyModels(), PPOLearner.cpp:665-674)."""
+        import torch
+        return torch.cat([self.model_slice(m) for m in self.models if m != 1])
+
+    def model_in(self, model):
+        return self.shared_layers[-1] if (self.shared_layers and model != 2) else self.obs_size
+
+    def model_out(self, model):
+        return (self.num_actions, 1, self.shared_layers[-1] if self.shared_layers else 0)[model]
 
     def init_params(self, seed):
         _lib.check(_lib.lib().rlgpu_ppo_init_params(self._h, seed, _lib.stream_ptr()), "init_params")
@@ -189,9 +216,9 @@ class PPO:
         """An equivalent torch.nn.Sequential (torch parameters() order = the flat layout), on CPU,
         holding a copy of the current parameters: checkpoint export and test reference."""
         import torch
-        layers = self.policy_layers if model == 0 else self.critic_layers
-        out = self.num_actions if model == 0 else 1
-        seq = make_sequential(self.obs_size, out, layers, self.layer_norm, self.leaky_slope)
+        layers = (self.policy_layers, self.critic_layers, self.shared_layers)[model]
+        out = None if model == 2 else self.model_out(model)
+        seq = make_sequential(self.model_in(model), out, layers, self.layer_norm, self.leaky_slope)
         flat = self.model_slice(model).detach().cpu()
         o = 0
         with torch.no_grad():
@@ -199,6 +226,13 @@ class PPO:
                 prm.copy_(flat[o:o + prm.numel()].view_as(prm))
                 o += prm.numel()
         return seq
+
+    def torch_chain(self, model):
+        """shared head -> model as one torch.nn.Sequential (the module chain the reference's
+        InferPolicyProbsFromModels / InferCritic run, PPOLearner.cpp:90-91,188-191)."""
+        import torch
+        mods = list(self.torch_module(2)) if (self.shared_layers and model != 2) else []
+        return torch.nn.Sequential(*(mods + list(self.torch_module(model))))
 
     def load_torch_module(self, model, seq):
         import torch
@@ -212,7 +246,7 @@ class PPO:
     def forward(self, model, x, half=False, out=None):
         import torch
         n = x.shape[0]
-        width = self.num_actions if model == 0 else 1
+        width = self.model_out(model)
         out = torch.empty((n, width), device=self.device) if out is None else out
         _lib.check(_lib.lib().rlgpu_ppo_forward(self._h, model, int(half), _lib.ptr(x.contiguous()), n, _lib.ptr(out),
                                                 _lib.stream_ptr()), "rlgpu_ppo_forward")
@@ -229,8 +263,9 @@ class PPO:
         return actions, logp
 
     def set_version(self, policy_params):
-        """bf16 inference copy of an old policy version (flat fp32 policy parameters on the device)."""
-        _, cnt = self.model_range(0)
+        """bf16 inference copy of an old policy version (flat fp32 parameters on the device: the
+        policy's, then the shared head's -- policy_version())."""
+        cnt = sum(self.model_range(m)[1] for m in self.models if m != 1)
         if policy_params.numel() != cnt:
             raise _lib.RLGPUError("policy version has the wrong parameter count")
         _lib.check(_lib.lib().rlgpu_ppo_set_version(self._h, _lib.ptr(policy_params.contiguous()), _lib.stream_ptr()),
@@ -284,12 +319,12 @@ class PPO:
             cnt = max(cnt, 1)
             return {"Policy Entropy": m[0] / cnt, "Mean KL Divergence": m[1] / cnt, "Policy Loss": m[2] / cnt,
                     "Critic Loss": m[3] / cnt, "Ratio": m[4] / cnt, "SB3 Clip Fraction": m[5] / cnt,
-                    "Policy Grad Norm": m[7], "Critic Grad Norm": m[8]}
+                    "Policy Grad Norm": m[7], "Critic Grad Norm": m[8], "Shared Head Grad Norm": m[9]}
         m = self.metrics.cpu().tolist()
         cnt = max(self._count, 1)
         rep = {"Policy Entropy": m[0] / cnt, "Mean KL Divergence": m[1] / cnt, "Policy Loss": m[2] / cnt,
                "Critic Loss": m[3] / cnt, "Ratio": m[4] / cnt, "SB3 Clip Fraction": m[5] / cnt,
-               "Policy Grad Norm": m[7], "Critic Grad Norm": m[8]}
+               "Policy Grad Norm": m[7], "Critic Grad Norm": m[8], "Shared Head Grad Norm": m[9]}
         if reset:
             self.metrics.zero_()
             self._count = 0
@@ -313,7 +348,8 @@ class PPO:
 
 def make_sequential(obs_size, out, layers, layer_norm=True, leaky_slope=0.01):
     """GGL::Model's module list (Models.cpp:7-33): per hidden layer Linear [, LayerNorm],
-    LeakyReLU; then the output Linear.  CPU, torch default init."""
+    LeakyReLU; then the output Linear (none when out is None: the shared head, addOutputLayer
+    false).  CPU, torch default init."""
     import torch
     mods, prev = [], obs_size
     for hdim in layers:
@@ -322,7 +358,8 @@ def make_sequential(obs_size, out, layers, layer_norm=True, leaky_slope=0.01):
             mods.append(torch.nn.LayerNorm(hdim))
         mods.append(torch.nn.LeakyReLU(leaky_slope))
         prev = hdim
-    mods.append(torch.nn.Linear(prev, out))
+    if out is not None:
+        mods.append(torch.nn.Linear(prev, out))
     return torch.nn.Sequential(*mods)
 
 

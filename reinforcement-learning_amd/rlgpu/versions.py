@@ -12,7 +12,9 @@ Reference map:
     LearnerConfig                         LearnerConfig.h:62-68 (tsPerVersion 25M, maxOldVersions 32,
                                           trainAgainstOldVersions, trainAgainstOldChance 0.15)
 
-Versions are the policy's flat fp32 parameters kept in HBM (1.6 MB each at [512, 512]); the active
+Versions are the policy's flat fp32 parameters -- followed by the shared head's when the model has
+one, as the reference versions GetPolicyModels() (PPOLearner.cpp:665-674) and saves POLICY.lt +
+SHARED_HEAD.lt per version -- kept in HBM (1.6 MB each at [512, 512]); the active
 one is converted once per iteration into the PPO handle's second bf16 inference copy
 (rlgpu_ppo_set_version) and used by the mixed-policy inference of the Learner.  The skill/ELO
 tracker is not part of this tier (SURVEY.md 8f-3 lists it as optional); STATS.json carries an
@@ -28,7 +30,7 @@ from . import checkpoint as _ckpt
 class PolicyVersion:
     def __init__(self, timesteps, params, ratings=None):
         self.timesteps = int(timesteps)
-        self.params = params            # device tensor, flat fp32 policy parameters
+        self.params = params            # device tensor, flat fp32 policy (+ shared head) parameters
         self.ratings = dict(ratings or {})
 
 
@@ -44,7 +46,7 @@ class PolicyVersionManager:
 
     def add_version(self, timesteps, params=None):
         """AddVersion: a copy of the current policy (or of `params`)."""
-        src = self.ppo.model_slice(0) if params is None else params
+        src = self.ppo.policy_version() if params is None else params
         v = PolicyVersion(timesteps, src.detach().clone())
         self.versions.append(v)
         self.versions.sort(key=lambda x: x.timesteps)
@@ -68,33 +70,39 @@ class PolicyVersionManager:
                 continue
             d = os.path.join(self.save_folder, str(v.timesteps))
             os.makedirs(d, exist_ok=True)
-            seq = self.ppo.torch_module(0)
-            o = 0
             import torch
             flat = v.params.detach().cpu()
-            with torch.no_grad():
-                for p in seq.parameters():
-                    p.copy_(flat[o:o + p.numel()].view_as(p))
-                    o += p.numel()
-            _ckpt.write_model(seq, _ckpt.model_path(d, "policy"))
+            o = 0
+            for mi in self._models():  # ModelSet::Save(folder, false): no optimizer files
+                seq = self.ppo.torch_module(mi)
+                with torch.no_grad():
+                    for p in seq.parameters():
+                        p.copy_(flat[o:o + p.numel()].view_as(p))
+                        o += p.numel()
+                _ckpt.write_model(seq, _ckpt.model_path(d, _ckpt.MODEL_NAMES[mi]))
             with open(os.path.join(d, "STATS.json"), "w") as f:
                 json.dump({"skill_ratings": v.ratings}, f, indent=4)
+
+    def _models(self):
+        return [m for m in self.ppo.models if m != 1]  # GetPolicyModels: policy (+ shared head)
 
     def load_versions(self, cur_timesteps):
         import torch
         self.versions = []
         if not self.save_folder:
             return
-        want = self.ppo.model_sizes(0)
         for ts in sorted(_ckpt.numbered_dirs(self.save_folder)):
             if ts > cur_timesteps:
                 raise ValueError(f"Tried to load saved policy version that is newer than our current model "
                                  f"({ts} > {cur_timesteps})")
             d = os.path.join(self.save_folder, str(ts))
-            tensors = _ckpt.read_model_state(_ckpt.model_path(d, "policy"))
-            if [t.numel() for t in tensors] != want:
-                raise ValueError(f"saved policy version in {d} has a different size than the current model")
-            flat = torch.cat([t.reshape(-1) for t in tensors]).to(self.ppo.params.device)
+            parts = []
+            for mi in self._models():
+                tensors = _ckpt.read_model_state(_ckpt.model_path(d, _ckpt.MODEL_NAMES[mi]))
+                if [t.numel() for t in tensors] != self.ppo.model_sizes(mi):
+                    raise ValueError(f"saved policy version in {d} has a different size than the current model")
+                parts += [t.reshape(-1) for t in tensors]
+            flat = torch.cat(parts).to(self.ppo.params.device)
             v = self.add_version(ts, flat)
             p = os.path.join(d, "STATS.json")
             if os.path.exists(p):

@@ -148,3 +148,32 @@ def test_model_reader_matches_parameters(tmp_path):
     assert [t.shape for t in got] == [w.shape for w in want]
     for g, w in zip(got, want):
         assert torch.equal(g, w.detach())
+
+
+def test_shared_head_file_loads_in_libtorch(harness, tmp_path):
+    """SHARED_HEAD.lt (Models.h:114-128, the shared head of PPOLearner::MakeModels: hidden layers,
+    no output Linear) loads into libtorch's Sequential built with addOutputLayer = false, and a
+    libtorch-written shared head reads back here."""
+    import torch
+    torch.manual_seed(4)
+    seq = make_sequential(ARCH["obs"], None, (64, 32), True)
+    p = str(tmp_path / "SHARED_HEAD.lt")
+    assert ckpt.model_path(str(tmp_path), "shared_head") == p
+    ckpt.write_model(seq, p)
+    x = np.random.default_rng(2).standard_normal((5, ARCH["obs"])).astype(np.float32)
+    x.tofile(tmp_path / "x.f32")
+    args = [str(ARCH["obs"]), "0", "1", "64", "32"]
+    r = subprocess.run([harness, "load", p, str(tmp_path / "x.f32"), "5", str(tmp_path / "y.f32"), *args],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    y = np.fromfile(tmp_path / "y.f32", np.float32).reshape(5, 32)
+    with torch.no_grad():
+        np.testing.assert_allclose(y, seq(torch.from_numpy(x)).numpy(), rtol=1e-5, atol=1e-6)
+    n = sum(q.numel() for q in seq.parameters())
+    flat = np.random.default_rng(3).standard_normal(n).astype(np.float32)
+    flat.tofile(tmp_path / "p.f32")
+    q = str(tmp_path / "LT_SHARED_HEAD.lt")
+    r = subprocess.run([harness, "save", str(tmp_path / "p.f32"), q, *args], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    got = torch.cat([t.reshape(-1) for t in ckpt.read_model_state(q)]).numpy()
+    np.testing.assert_array_equal(got, flat)

@@ -176,15 +176,21 @@ class _FakePPO:
     def model_slice(self, model):
         return self.params[:self.policy]
 
+    def policy_version(self):
+        return self.params[:self.policy]
+
 
 class _FakeLearner:
-    def __init__(self, rank):
+    def __init__(self, rank, loaded=True):
         from rlgpu.versions import PolicyVersionManager
         self.ppo = _FakePPO(10, 4)
         self.versions = PolicyVersionManager(self.ppo)
         self.st = _FakeStats()
         self.last_checkpoint = None
-        if rank == 0:  # what checkpoint.load + load_versions leave on rank 0
+        if rank == 0 and not loaded:  # no checkpoint, but policy_versions/ held two versions
+            self.versions.add_version(100, torch.full((4,), 1.0))
+            self.versions.add_version(200, torch.full((4,), 2.0))
+        elif rank == 0:  # what checkpoint.load + load_versions leave on rank 0
             self.last_checkpoint = "/ckpt/300"
             self.ppo.params.copy_(torch.arange(10.0))
             self.ppo.m.fill_(0.5)
@@ -202,14 +208,21 @@ class _FakeLearner:
         self.st = st
 
 
-def _sync_worker(rank, world, port, q):
+def _sync_worker(rank, world, port, q, case="loaded"):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd"))
     from rlgpu.learner import sync_from_rank0
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        L = _FakeLearner(rank)
+        L = _FakeLearner(rank, loaded=case == "loaded")
+        if case == "error":  # rank 0's load raised: every rank raises, none hangs
+            try:
+                sync_from_rank0(L, None, ValueError("truncated archive") if rank == 0 else None)
+                q.put((rank, "no error"))
+            except RuntimeError as e:
+                q.put((rank, "raised" if "failed to load" in str(e) else repr(e)))
+            return
         sync_from_rank0(L)
         s = L.st
         q.put((rank, L.ppo.params.tolist(), L.ppo.m.tolist(), L.ppo.v.tolist(), L.ppo.step, L.ppo.refreshed,
@@ -237,3 +250,31 @@ def test_checkpoint_state_broadcast_from_rank0():
     assert res[1][1] == list(np.arange(10.0)) and res[1][4] == 7 and res[1][5]
     assert res[1][6] == (300, 3, 450, 1.25, 9.5)
     assert res[1][7] == [(100, [1.0] * 4), (200, [2.0] * 4)]
+
+
+def _run_sync(case):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, q, case)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.timeout(120)
+def test_checkpoint_load_error_raises_on_every_rank():
+    """a failing rank-0 load is broadcast in the header, so all ranks raise together."""
+    assert _run_sync("error") == [(0, "raised"), (1, "raised")]
+
+
+@pytest.mark.timeout(120)
+def test_versions_broadcast_without_checkpoint():
+    """rank 0's policy versions reach the other ranks even when no checkpoint was loaded."""
+    res = _run_sync("versions")
+    assert res[1][7] == res[0][7] == [(100, [1.0] * 4), (200, [2.0] * 4)]
+    assert res[1][6] == (0, 0, 0, 0.0, 0.0) and not res[1][5]

@@ -182,6 +182,9 @@ def test_example_main_binary(gpu):
     assert r.returncode == 0, r.stderr
     lines = [x for x in r.stdout.splitlines() if x.startswith("iteration")]
     assert len(lines) == 2 and "Total Timesteps 4096" in lines[-1], r.stdout
+    # ExampleMain's model topology by default: the reference log's parameter counts (run_out.log:36-39)
+    for want in ('"critic": 446209', '"policy": 480474', '"shared_head": 213888', "[Total]: 1140571"):
+        assert want in r.stdout, r.stdout
 
 
 def test_return_samples_finished_trajectories_and_welford_state(gpu):

@@ -1,7 +1,8 @@
 // lt_load_check.cpp -- checkpoint-compatibility harness (test tool, linked against libtorch).
 //
 // Builds the reference's model the way GGL::Model's constructor does (Models.cpp:7-33: per hidden
-// layer Linear, LayerNorm if enabled, the activation; then the output Linear), loads a <NAME>.lt
+// layer Linear, LayerNorm if enabled, the activation; then the output Linear -- none when out is 0,
+// the shared head's addOutputLayer = false, Models.cpp:24-28), loads a <NAME>.lt
 // file with torch::load(seq, stream) as Model::Load does (Models.cpp:130-166, including its
 // parameter-size check), runs the float forward on the rows of an input file and writes the
 // outputs -- or, with "save", writes the module with torch::save(seq, stream) (Models.cpp:116-120)
@@ -26,7 +27,7 @@ static torch::nn::Sequential make_model(int obs, int out, bool ln, const std::ve
         last = h;
         seq->push_back(torch::nn::LeakyReLU());
     }
-    seq->push_back(torch::nn::Linear(last, out));
+    if (out > 0) seq->push_back(torch::nn::Linear(last, out));
     return seq;
 }
 
