@@ -112,4 +112,90 @@ RLGPU_HD float rs_atan2f(float y, float x) {
 /* asin(x) = atan2(x, sqrt(1 - x^2)) (sqrt is correctly rounded on both sides). */
 RLGPU_HD float rs_asinf(float x, float sqrt_one_minus_x2) { return rs_atan2f(x, sqrt_one_minus_x2); }
 
+/* The action sampler's exp / log (the reference's torch::softmax and .log(), PPOLearner.cpp:97-113,
+ * 131-141): the same Cephes-style kernels on both sides so the sampled action indices and log probs
+ * of the GPU and the CPU oracle agree bit for bit.  The device sampler compiles them under
+ * "#pragma clang fp contract(off)" (no FMA contraction), the oracle with -ffp-contract=off. */
+RLGPU_HD float rs_bits_float(unsigned int u) {
+    union {
+        unsigned int u;
+        float f;
+    } c;
+    c.u = u;
+    return c.f;
+}
+RLGPU_HD unsigned int rs_float_bits(float f) {
+    union {
+        unsigned int u;
+        float f;
+    } c;
+    c.f = f;
+    return c.u;
+}
+
+/* e^x (Cephes expf: x = n ln2 + r with a 2-part ln2, degree-6 polynomial, exact scaling by 2^n).
+ * Results below FLT_MIN are flushed to +0 (x < -87.33: a softmax term that small is clamped to the
+ * 1e-11 floor anyway); x > 88.72 gives +inf; NaN stays NaN. */
+RLGPU_HD float rs_expf(float x) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    if (x != x) return x;
+    if (x > 88.72283905206835f) return rs_bits_float(0x7f800000u);
+    if (x < -87.33654475055310898657f) return 0.0f;
+    float fx = 1.44269504088896341f * x + 0.5f;
+    int n = (int)fx;
+    if ((float)n > fx) n -= 1; /* floor */
+    const float z0 = (float)n;
+    float r = x - z0 * 0.693359375f;
+    r = r - z0 * -2.12194440e-4f;
+    const float z = r * r;
+    float y = ((((1.9875691500E-4f * r + 1.3981999507E-3f) * r + 8.3334519073E-3f) * r + 4.1665795894E-2f) * r +
+               1.6666665459E-1f) * r + 5.0000001201E-1f;
+    y = y * z + r + 1.0f;
+    /* n is in [-126, 128] over the accepted x range; 2^n is built exactly from its bits (n = 128 as
+     * 2 * 2^127), so the result is one correctly rounded IEEE product on both sides */
+    if (n > 127) {
+        y = y * 2.0f;
+        n -= 1;
+    }
+    return y * rs_bits_float((unsigned int)(n + 127) << 23);
+}
+
+/* natural log (Cephes logf: x = m 2^e, m in [sqrt(1/2), sqrt(2)), degree-9 polynomial in m - 1,
+ * 2-part ln2).  x <= 0 gives -inf (0) or NaN. */
+RLGPU_HD float rs_logf(float xin) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    if (xin != xin) return xin;
+    if (xin <= 0.0f) return xin == 0.0f ? rs_bits_float(0xff800000u) : rs_bits_float(0x7fc00000u);
+    if (xin == rs_bits_float(0x7f800000u)) return xin;
+    float x = xin;
+    int ebias = 0;
+    if (x < 1.17549435e-38f) { /* subnormal: scale into the normal range (exact) */
+        x = x * 33554432.0f;   /* 2^25 */
+        ebias = -25;
+    }
+    const unsigned int b = rs_float_bits(x);
+    int e = (int)((b >> 23) & 0xffu) - 126 + ebias;
+    x = rs_bits_float((b & 0x807fffffu) | 0x3f000000u); /* mantissa in [0.5, 1) */
+    if (x < 0.707106781186547524f) {
+        e -= 1;
+        x = (x + x) - 1.0f;
+    } else {
+        x = x - 1.0f;
+    }
+    const float z = x * x;
+    float y = ((((((((7.0376836292E-2f * x - 1.1514610310E-1f) * x + 1.1676998740E-1f) * x - 1.2420140846E-1f) * x +
+                   1.4249322787E-1f) * x - 1.6668057665E-1f) * x + 2.0000714765E-1f) * x - 2.4999993993E-1f) * x +
+               3.3333331174E-1f) * x * z;
+    const float fe = (float)e;
+    y += -2.12194440e-4f * fe;
+    y += -0.5f * z;
+    float r = x + y;
+    r += 0.693359375f * fe;
+    return r;
+}
+
 #endif

@@ -174,3 +174,31 @@ def pad_map():
     m = np.zeros(PADS, np.int32)
     lib().oracle_pad_map(_p(m))
     return m
+
+
+# ------------------------------------------------------------------ action sampler (sampler_ref.c)
+def sample_actions(logits16, masks, deterministic, seed, step, row0=0, f16=False, with_logp=True):
+    """oracle_sample_actions: PPOLearner.cpp:78-184 in the GPU sampler's operation order.
+    logits16: uint16 [n, A] bf16 (or fp16) bit patterns.  Returns (actions int32 [n], logp f32 [n])."""
+    lg = np.ascontiguousarray(logits16, np.uint16)
+    mk = np.ascontiguousarray(masks, np.uint8)
+    n, A = lg.shape
+    act = np.empty(n, np.int32)
+    lp = np.empty(n, np.float32) if with_logp else None
+    f = lib().oracle_sample_actions
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                  ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    f(_p(lg), _p(mk), n, A, int(deterministic), seed, step, row0, int(f16), _p(act), _p(lp))
+    return act, lp
+
+
+def detmath_exp_log(x):
+    """rs_expf / rs_logf (include/rlgpu_detmath.h) over an array."""
+    x = np.ascontiguousarray(x, np.float32)
+    ex, lg = np.empty_like(x), np.empty_like(x)
+    f = lib().oracle_detmath_exp_log
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    f(_p(x), x.size, _p(ex), _p(lg))
+    return ex, lg

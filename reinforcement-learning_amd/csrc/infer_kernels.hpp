@@ -76,6 +76,7 @@ struct InferArgs {
     const uint8_t* masks;          // mode 1: [n][out]
     int det;
     uint64_t seed, step;
+    int64_t row0;                  // global row number of X's row 0 (the sampler's Philox counter)
     int32_t* act;
     float* logp;                   // may be null
     const uint8_t* row_sel;        // mode 1, optional: only rows with (row_sel != 0) == sel are written
@@ -416,7 +417,7 @@ __global__ void __launch_bounds__(IT, 1) mlp_infer(InferArgs a) {
             row[g] = r0 + r;
             ok[g] = Sel[r] != 0;
         }
-        ppo::sample_rows<IRW, F16>(lg, mk, N, a.det, a.seed, a.step, row, ok, lane, a.act, a.logp);
+        ppo::sample_rows<IRW, F16>(lg, mk, N, a.det, a.seed, a.step, a.row0, row, ok, lane, a.act, a.logp);
     }
     INFER_MARK(15);
 }

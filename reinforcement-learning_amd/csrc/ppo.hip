@@ -663,7 +663,7 @@ bool fused_ok(const rlgpu_ppo* h, int mi) {
 // mode 1 samples actions (masks, act, logp; row_sel / sel as ppo::sample_actions)
 void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode, float* out_f,
                  const uint8_t* masks, int det, uint64_t step, int32_t* act, float* logp, const uint8_t* row_sel, int sel,
-                 hipStream_t s) {
+                 hipStream_t s, int64_t row0 = 0) {
     const auto c = chain(h, mi);
     infer::InferArgs a{};
     a.X = X;
@@ -689,6 +689,7 @@ void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode
     a.det = det;
     a.seed = h->cfg.seed;
     a.step = step;
+    a.row0 = row0;
     a.act = act;
     a.logp = logp;
     a.row_sel = row_sel;
@@ -1021,13 +1022,13 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
             int m = (int)std::min<int64_t>(R, n - b);
             if (fused_ok(h, 0)) {
                 infer_fused(h, 0, false, d_obs + b * h->cfg.obs_size, m, 1, nullptr, d_masks + b * h->cfg.num_actions,
-                            deterministic, rng_step, d_actions + b, d_logp ? d_logp + b : nullptr, nullptr, 0, s);
+                            deterministic, rng_step, d_actions + b, d_logp ? d_logp + b : nullptr, nullptr, 0, s, b);
                 continue;
             }
             forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s);
             RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
-                               rng_step, d_actions + b, d_logp ? d_logp + b : nullptr);
+                               rng_step, b, d_actions + b, d_logp ? d_logp + b : nullptr);
             RLGPU_CHECK_HIP(hipGetLastError());
         }
     });
@@ -1064,13 +1065,13 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
                 if (fused_ok(h, 0)) {
                     infer_fused(h, 0, old != 0, d_obs + b * h->cfg.obs_size, m, 1, nullptr,
                                 d_masks + b * h->cfg.num_actions, deterministic, rng_step, d_actions + b,
-                                (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old, s);
+                                (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old, s, b);
                     continue;
                 }
                 forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s, old ? h->half_ver : h->half);
                 RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                    d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
-                                   rng_step, d_actions + b, (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
+                                   rng_step, b, d_actions + b, (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
                 RLGPU_CHECK_HIP(hipGetLastError());
             }
         }

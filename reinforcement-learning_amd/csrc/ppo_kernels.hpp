@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/rlgpu_detmath.h"
 #include "mlp_kernels.hpp"
 
 namespace ppo {
@@ -46,6 +47,11 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 
 // InferActions: logits bf16 [n, A] -> action (int32), log prob.  Inverse-CDF multinomial on the
 // clamped probs (torch.multinomial normalises by their sum); argmax when deterministic.
+// Bit-exact against the CPU oracle (oracle/sampler_ref.c): IEEE + - * / only, exp / log by the
+// shared rs_expf / rs_logf (include/rlgpu_detmath.h), no FMA contraction, and every reduction in a
+// fixed order the oracle restates (xor-butterfly max / sum = pairwise tree, Hillis-Steele scan).
+// The Philox counter is (row0 + row, step): global row numbers, so chunked launches draw the same
+// uniforms as one launch.
 // row_sel (optional): only rows with (row_sel[row] != 0) == sel are written (mixed-policy inference).
 // RG rows, one wave, interleaved (each cross-lane step issues for all RG rows before the next, so
 // one wave hides the shuffle latency of RG independent rows): lg[g] = row g's A logits (global or
@@ -54,8 +60,10 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 // same, so both draw the same actions from the same logits.
 template <int RG, bool F16>
 __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], const uint8_t* const (&mk)[RG], int A,
-                                            int deterministic, uint64_t seed, uint64_t step, const int (&row)[RG],
-                                            const bool (&ok)[RG], int lane, int32_t* act, float* logp) {
+                                            int deterministic, uint64_t seed, uint64_t step, int64_t row0,
+                                            const int (&row)[RG], const bool (&ok)[RG], int lane, int32_t* act,
+                                            float* logp) {
+#pragma clang fp contract(off)
     const int a0 = 2 * lane, a1 = 2 * lane + 1;
     const bool in0 = a0 < A, in1 = a1 < A;
     float z0[RG], z1[RG], m[RG], s[RG], p0[RG], p1[RG];
@@ -74,8 +82,8 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
     for (int g = 0; g < RG; g++) m[g] = mlp::wave_max_x(m[g]);
 #pragma unroll
     for (int g = 0; g < RG; g++) {
-        z0[g] = in0 ? __expf(z0[g] - m[g]) : 0.f;  // e0, e1
-        z1[g] = in1 ? __expf(z1[g] - m[g]) : 0.f;
+        z0[g] = in0 ? rs_expf(z0[g] - m[g]) : 0.f;  // e0, e1
+        z1[g] = in1 ? rs_expf(z1[g] - m[g]) : 0.f;
         s[g] = z0[g] + z1[g];
     }
 #pragma unroll
@@ -119,7 +127,7 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
 #pragma unroll
         for (int g = 0; g < RG; g++) {
             float total = __shfl(inc[g], 63, 64);
-            float u = (float)(philox(seed, (uint32_t)row[g], (uint32_t)step) >> 8) * (1.f / 16777216.f) * total;
+            float u = (float)(philox(seed, (uint32_t)(row0 + row[g]), (uint32_t)step) >> 8) * (1.f / 16777216.f) * total;
             float excl = inc[g] - pair[g];
             bool hit = (u < inc[g]) && (u >= excl) && pair[g] > 0.f;
             const unsigned long long bal = __ballot(hit), nz = __ballot(pair[g] > 0.f);
@@ -135,14 +143,15 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
         float pp0 = __shfl(p0[g], pick[g] >> 1, 64), pp1 = __shfl(p1[g], pick[g] >> 1, 64);
         if (lane == 0 && ok[g]) {
             act[row[g]] = pick[g];
-            if (logp) logp[row[g]] = __logf((pick[g] & 1) ? pp1 : pp0);
+            if (logp) logp[row[g]] = rs_logf((pick[g] & 1) ? pp1 : pp0);
         }
     }
 }
 template <bool F16>
 __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
-                                                     int deterministic, uint64_t seed, uint64_t step, int32_t* act,
-                                                     float* logp, const uint8_t* row_sel = nullptr, int sel = 0) {
+                                                     int deterministic, uint64_t seed, uint64_t step, int64_t row0,
+                                                     int32_t* act, float* logp, const uint8_t* row_sel = nullptr,
+                                                     int sel = 0) {
     int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= n) return;
     if (row_sel && ((row_sel[row] != 0) != (sel != 0))) return;
@@ -150,7 +159,7 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
     const uint8_t* const mk[1] = {masks + (int64_t)row * A};
     const int rw[1] = {row};
     const bool ok[1] = {true};
-    sample_rows<1, F16>(lg, mk, A, deterministic, seed, step, rw, ok, lane, act, logp);
+    sample_rows<1, F16>(lg, mk, A, deterministic, seed, step, row0, rw, ok, lane, act, logp);
 }
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.
