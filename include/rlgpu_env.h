@@ -10,10 +10,15 @@
  *     ResetArena(int) / Reset()            EnvSet.cpp:275-354  -> rlgpu_envset_reset_arena / _reset
  *     state.{obs,actionMasks,rewards,terminals,arenaPlayerStartIdx}
  *                                          EnvSet.h:35-65      -> rlgpu_envset_buffers
- * with the plugin set of src/ExampleMain.cpp:128-226 built in: AdvancedObs, DefaultAction,
- * KickoffState, the 13 weighted rewards and NoTouchCondition(8) + ScoreLimitCondition(3).
+ * The EnvCreateFn's plugin set (EnvCreateResult, EnvSet.h:14-24) is AdvancedObs, DefaultAction and
+ * KickoffState, plus a device registry of weighted rewards and terminal conditions
+ * (rlgpu_reward_spec / rlgpu_terminal_spec lists in rlgpu_envset_config; NULL lists = src/ExampleMain.cpp:
+ * 128-226: the 13 weighted rewards and NoTouchCondition(8) + ScoreLimitCondition(3)).
  *
- * Arena state lives on the device as struct-of-arrays; one env step is ONE kernel launch
+ * Arena state lives on the device as one 2,304-byte record per arena (array of structs: a
+ * workgroup stages whole records into LDS with coalesced 16-byte loads, runs the step there and
+ * writes them back once, so the record is read and written exactly once per step whatever the
+ * access pattern inside -- DESIGN.md section 3); one env step is ONE kernel launch
  * (7 ticks with the previous controls, action parse, 1 tick, builders, reset-if-terminal)
  * when rlgpu_envset_step() is used, or two launches through the two-half API.
  *
@@ -37,6 +42,61 @@ extern "C" {
 #define RLGPU_OBS 167         /* AdvancedObs 9+8+34+29*4 (AdvancedObs.cpp:193-270) */
 #define RLGPU_ACTIONS 90      /* DefaultAction table (DefaultAction.cpp:3-89) */
 #define RLGPU_REWARDS 13      /* ExampleMain reward list (src/ExampleMain.cpp:132-177) */
+#define RLGPU_MAX_REWARDS 32  /* weighted rewards per env set (device registry) */
+#define RLGPU_MAX_TERMINALS 8 /* terminal conditions per env set */
+
+/* Reward plugins of the device registry: RLGymCPP's CommonRewards (RG/Rewards/CommonRewards.h),
+ * KickoffProximityReward2v2Enhanced (RG/Rewards/KickoffProximityReward2v2Enhanced.h) and ExampleMain's
+ * LosingPenaltyReward (src/ExampleMain.cpp:84-124).  params[] are the constructor arguments, 0 meaning
+ * the reference default where noted.  The first 13 ids are ExampleMain's list in its order. */
+enum {
+    RLGPU_RW_AIR = 0,                     /* AirReward */
+    RLGPU_RW_WAVEDASH = 1,                /* WavedashReward */
+    RLGPU_RW_KICKOFF_PROXIMITY_2V2 = 2,   /* KickoffProximityReward2v2Enhanced */
+    RLGPU_RW_VELOCITY_PLAYER_TO_BALL = 3, /* VelocityPlayerToBallReward */
+    RLGPU_RW_STRONG_TOUCH = 4,            /* StrongTouchReward(params[0] minSpeedKPH, params[1] maxSpeedKPH) */
+    RLGPU_RW_TOUCH_ACCEL = 5,             /* TouchAccelReward */
+    RLGPU_RW_VELOCITY_BALL_TO_GOAL = 6,   /* VelocityBallToGoalReward(params[0] ownGoal != 0) */
+    RLGPU_RW_PICKUP_BOOST = 7,            /* PickupBoostReward */
+    RLGPU_RW_SAVE_BOOST = 8,              /* SaveBoostReward(params[0] exponent) */
+    RLGPU_RW_BUMP = 9,                    /* BumpReward (PlayerDataEventReward<bump>) */
+    RLGPU_RW_DEMO = 10,                   /* DemoReward */
+    RLGPU_RW_GOAL = 11,                   /* GoalReward(params[0] concedeScale) */
+    RLGPU_RW_LOSING_PENALTY = 12,         /* LosingPenaltyReward(params[0] penaltyPerGoalBehind) */
+    RLGPU_RW_BUMPED_PENALTY = 13,         /* BumpedPenalty */
+    RLGPU_RW_DEMOED_PENALTY = 14,         /* DemoedPenalty */
+    RLGPU_RW_VELOCITY = 15,               /* VelocityReward(params[0] isNegative != 0) */
+    RLGPU_RW_FACE_BALL = 16,              /* FaceBallReward */
+    RLGPU_RW_TOUCH_BALL = 17,             /* TouchBallReward */
+    RLGPU_RW_SPEED = 18,                  /* SpeedReward */
+    RLGPU_NUM_REWARD_TYPES = 19
+};
+/* One WeightedReward {Reward*, weight} (EnvSet.h:14-18).  zero_sum != 0: the reward is wrapped in
+ * ZeroSumReward(child, zero_sum_team_spirit, zero_sum_opponent_scale) -- accepted for the API, and a
+ * pass-through exactly as in the reference: ZeroSumReward overrides only GetAllRewards, while the hot
+ * path calls GetAllRewardsInPlace, which runs the child's GetReward (ZeroSumReward.cpp:3-48,
+ * Reward.h:43-48). */
+typedef struct {
+    int32_t type;      /* RLGPU_RW_* */
+    float weight;
+    float params[3];
+    int32_t zero_sum;
+    float zero_sum_team_spirit, zero_sum_opponent_scale;
+} rlgpu_reward_spec;
+
+/* Terminal conditions (RG/TerminalConditions/NoTouchCondition.h, GoalScoreCondition.h, src/ExampleMain.cpp:46-82).  The list is merged as
+ * EnvSet::StepSecondHalf does: any condition sets the arena's terminal, NORMAL dominating TRUNCATED
+ * (EnvSet.cpp:167-180). */
+enum {
+    RLGPU_TC_NO_TOUCH = 0,     /* NoTouchCondition(param maxTime s): truncation */
+    RLGPU_TC_SCORE_LIMIT = 1,  /* ScoreLimitCondition(param goals): normal */
+    RLGPU_TC_GOAL_SCORE = 2,   /* GoalScoreCondition: normal */
+    RLGPU_NUM_TERMINAL_TYPES = 3
+};
+typedef struct {
+    int32_t type;  /* RLGPU_TC_* */
+    float param;
+} rlgpu_terminal_spec;
 
 /* One contact point (btManifoldPoint subset, bullet units). */
 typedef struct {
@@ -151,6 +211,16 @@ typedef struct {
     int32_t mesh_ntris;
     int32_t mesh_objects;
     const int32_t* mesh_object_ntris;
+    /* The EnvCreateFn's rewards and terminal conditions (EnvCreateResult, EnvSet.h:14-24), host
+     * memory copied at create.  rewards == NULL: ExampleMain's 13 weighted rewards
+     * (src/ExampleMain.cpp:132-177); terminals == NULL: NoTouchCondition(8) + ScoreLimitCondition(3)
+     * (:181-187).  An unknown type, a list longer than the RLGPU_MAX_* limits or a bad parameter is
+     * rejected by rlgpu_envset_create with RLGPU_ERR_UNSUPPORTED / RLGPU_ERR_INVALID_ARG and a
+     * message naming it (rlgpu_last_error) -- a user's own C++ plugin class has no device code here. */
+    const rlgpu_reward_spec* rewards;
+    int32_t n_rewards;
+    const rlgpu_terminal_spec* terminals;
+    int32_t n_terminals;
 } rlgpu_envset_config;
 
 /* Experience-append destinations of the fused step (Learner.cpp:823-861); any may be NULL. */
@@ -170,10 +240,13 @@ typedef struct {
     uint8_t* action_masks;   /* [num_players][RLGPU_ACTIONS] */
     float* rewards;          /* [num_players] */
     uint8_t* terminals;      /* [num_arenas]: 0, 1 NORMAL, 2 TRUNCATED */
-    float* last_rewards;     /* [num_arenas][RLGPU_REWARDS] (if save_rewards) */
+    float* last_rewards;     /* [num_arenas][num_rewards]: each reward's value for player 0 (if save_rewards;
+                                EnvState::lastRewards, EnvSet.cpp:224-242) */
     float* trunc_obs;        /* [num_players][RLGPU_OBS] pre-reset obs of truncated arenas */
     int32_t num_players;
     int32_t num_arenas;
+    int32_t num_rewards;     /* length of the reward list */
+    int32_t* arena_player_start; /* [num_arenas] EnvState::arenaPlayerStartIdx (4 * arena, 2v2) */
 } rlgpu_envset_buffers;
 
 /* Creates the set, resets every arena to a random kickoff (EnvSet.cpp:105-110). */
@@ -244,6 +317,12 @@ int rlgpu_envset_enable_step_metrics(rlgpu_envset* env, int32_t enable);
 int rlgpu_envset_step_metrics(rlgpu_envset* env, double* h_total, uint64_t* h_count, int32_t reset, void* stream);
 /* The raw per-arena slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] (tests, custom reductions). */
 int rlgpu_envset_step_metric_slots(rlgpu_envset* env, double* h_out, void* stream);
+
+/* The registry lists ExampleMain's EnvCreateFn builds (src/ExampleMain.cpp:132-187), the defaults of
+ * NULL config lists: writes up to RLGPU_MAX_REWARDS / RLGPU_MAX_TERMINALS entries (any output may be
+ * NULL). */
+int rlgpu_envset_default_plugins(rlgpu_reward_spec* rewards, int32_t* n_rewards, rlgpu_terminal_spec* terminals,
+                                 int32_t* n_terminals);
 
 /* Static sizes for binding checks. */
 int rlgpu_arena_state_size(void);

@@ -78,6 +78,12 @@ typedef struct {
     /* PPOLearnerConfig::sharedHead (rlgpu_ppo_config.shared_layers); n_shared_layers = 0: none */
     int32_t shared_layers[RLGPU_MAX_LAYERS];
     int32_t n_shared_layers;
+    /* the EnvCreateFn's reward / terminal lists (rlgpu_envset_config.rewards / terminals; NULL =
+     * ExampleMain's), host memory copied at create */
+    const rlgpu_reward_spec* rewards;
+    int32_t n_rewards;
+    const rlgpu_terminal_spec* terminals;
+    int32_t n_terminals;
 } rlgpu_learner_config;
 
 /* Fills ExampleMain's values (src/ExampleMain.cpp:340-430) for a C2 rank: 4096 arenas, T = 128,

@@ -68,7 +68,7 @@ def gae_rollout(rews, terms, vals, trunc_vals, boot_vals, gamma, lam, return_std
 
 
 # ------------------------------------------------------------------ env (rsim_ref.cpp + env_ref.cpp)
-OBS, ACTIONS, REWARDS, PADS = 167, 90, 13, 34
+OBS, ACTIONS, REWARDS, PADS, MAX_REWARDS = 167, 90, 13, 34, 32
 
 
 def arena_state_size():
@@ -79,9 +79,11 @@ class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0,
-                 mesh=None):
+                 mesh=None, rewards=None, terminals=None):
         """mesh: (tris [N, 9] float32 bullet units, object_ntris int32 [K]) or an object with
-        .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh."""
+        .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh.
+        rewards / terminals: structured arrays of rlgpu_reward_spec / rlgpu_terminal_spec records
+        (include/rlgpu_env.h), None = ExampleMain's lists (the oracle restates them itself)."""
         L = lib()
         L.oracle_env_create.restype = ctypes.c_void_p
         L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -104,6 +106,17 @@ class EnvSet:
             self._mesh = (np.ascontiguousarray(tris, np.float32).reshape(-1, 9), np.ascontiguousarray(objs, np.int32))
             L.oracle_env_set_mesh.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
             L.oracle_env_set_mesh(self.h, _p(self._mesh[0]), len(self._mesh[0]), _p(self._mesh[1]), len(self._mesh[1]))
+        self.num_rewards = REWARDS
+        if rewards is not None or terminals is not None:
+            L.oracle_env_set_plugins.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+            self._rw = None if rewards is None else np.ascontiguousarray(rewards)
+            self._tc = None if terminals is None else np.ascontiguousarray(terminals)
+            nr = 0 if self._rw is None else self._rw.size
+            nt = 0 if self._tc is None else self._tc.size
+            L.oracle_env_set_plugins(self.h, None if self._rw is None else self._rw.ctypes.data, nr,
+                                     None if self._tc is None else self._tc.ctypes.data, nt)
+            if self._rw is not None:
+                self.num_rewards = nr
         self.traj_terms = np.zeros(4 * num_arenas, np.int8)
         P = 4 * num_arenas
         self.obs = np.zeros((P, OBS), np.float32)
@@ -111,7 +124,7 @@ class EnvSet:
         self.rewards = np.zeros(P, np.float32)
         self.terminals = np.zeros(num_arenas, np.uint8)
         self.trunc_obs = np.zeros((P, OBS), np.float32)
-        self.last_rewards = np.zeros((num_arenas, REWARDS), np.float32)
+        self._last_rewards = np.zeros((num_arenas, MAX_REWARDS), np.float32)
         self.read()
 
     def __del__(self):
@@ -123,7 +136,8 @@ class EnvSet:
         if hasattr(self, "traj_terms"):
             self.L.oracle_env_read_traj_terms(self.h, _p(self.traj_terms))
         self.L.oracle_env_read(self.h, _p(self.obs), _p(self.masks), _p(self.rewards), _p(self.terminals),
-                               _p(self.trunc_obs), _p(self.last_rewards))
+                               _p(self.trunc_obs), _p(self._last_rewards))
+        self.last_rewards = self._last_rewards[:, :self.num_rewards]
 
     def step_first_half(self):
         self.L.oracle_env_step_first_half(self.h)

@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -367,15 +368,123 @@ struct KickoffReward {
     }
 };
 
+// ------------------------------------------------------------------ reward / terminal plugins
+// The EnvCreateFn's WeightedReward list and TerminalCondition list (EnvSet.h:14-24), as the
+// rlgpu_envset_config registry describes them.
+struct Plugins {
+    std::vector<rlgpu_reward_spec> rw;
+    std::vector<rlgpu_terminal_spec> tc;
+};
+// src/ExampleMain.cpp:132-187
+static Plugins example_main_plugins() {
+    Plugins p;
+    auto R = [&](int type, float w, float p0 = 0, float p1 = 0) {
+        rlgpu_reward_spec r;
+        std::memset(&r, 0, sizeof r);
+        r.type = type;
+        r.weight = w;
+        r.params[0] = p0;
+        r.params[1] = p1;
+        p.rw.push_back(r);
+    };
+    R(RLGPU_RW_AIR, 0.25f);
+    R(RLGPU_RW_WAVEDASH, 0.12f);
+    R(RLGPU_RW_KICKOFF_PROXIMITY_2V2, 5.f);
+    R(RLGPU_RW_VELOCITY_PLAYER_TO_BALL, 4.f);
+    R(RLGPU_RW_STRONG_TOUCH, 60, 20, 120);
+    R(RLGPU_RW_TOUCH_ACCEL, 6.f);
+    R(RLGPU_RW_VELOCITY_BALL_TO_GOAL, 8.0f, 0);
+    R(RLGPU_RW_PICKUP_BOOST, 0.1f);
+    R(RLGPU_RW_SAVE_BOOST, 0.010f, 0.5f);
+    R(RLGPU_RW_BUMP, 20);
+    R(RLGPU_RW_DEMO, 80);
+    R(RLGPU_RW_GOAL, 150, -1);
+    R(RLGPU_RW_LOSING_PENALTY, 1.0f, 0.02f);
+    p.tc.push_back(rlgpu_terminal_spec{RLGPU_TC_NO_TOUCH, 8.f});
+    p.tc.push_back(rlgpu_terminal_spec{RLGPU_TC_SCORE_LIMIT, 3.f});
+    return p;
+}
+
+// SaveBoostReward's powf(boost / 100, exponent): 0.5 as sqrtf (ExampleMain), else exp(b log a) on the
+// deterministic kernels shared with the device (include/rlgpu_detmath.h)
+static float powf_det(float a, float b) {
+    if (b == 0.5f) return std::sqrt(a);
+    if (b == 0.f) return 1.f;
+    if (a == 0.f) return b > 0.f ? 0.f : std::numeric_limits<float>::infinity();
+    return rs_expf(b * rs_logf(a));
+}
+
+// Reward::GetReward of one registry entry (CommonRewards.h:8-203, KickoffProximityReward2v2Enhanced.h,
+// ExampleMain.cpp:84-124) for player i; CAR_MAX_SPEED 2300, BALL_MAX_SPEED 6000 (CommonValues.h)
+static float reward_of(const rlgpu_reward_spec& rs, int i, const PlayerView* P, const rlgpu_env_extra& e, V bpos,
+                       V bvel, V prev_bvel, bool goal) {
+    const PlayerView& pl = P[i];
+    const float KPH = 250.f / 9.f;  // Math::KPHToVel
+    switch (rs.type) {
+        case RLGPU_RW_AIR: return !pl.on_ground;
+        case RLGPU_RW_WAVEDASH: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1 : 0;
+        case RLGPU_RW_KICKOFF_PROXIMITY_2V2: return KickoffReward::reward(i, P, bpos, bvel);
+        case RLGPU_RW_VELOCITY_PLAYER_TO_BALL: {
+            V dir = rs_norm(bpos - pl.pos);
+            V nv = rs_div(pl.vel, 2300.f);
+            return dot(dir, nv);
+        }
+        case RLGPU_RW_STRONG_TOUCH: {
+            const float minv = rs.params[0] * KPH, maxv = rs.params[1] * KPH;
+            if (!pl.touched) return 0;
+            float hit = rs_len(bvel - prev_bvel);
+            return hit < minv ? 0 : std::min(1.f, hit / maxv);
+        }
+        case RLGPU_RW_TOUCH_ACCEL: {
+            const float MAXS = 110 * KPH;
+            if (!pl.touched) return 0;
+            float pf = std::min(1.f, rs_len(prev_bvel) / MAXS);
+            float cf = std::min(1.f, rs_len(bvel) / MAXS);
+            return cf > pf ? (cf - pf) : 0;
+        }
+        case RLGPU_RW_VELOCITY_BALL_TO_GOAL: {
+            bool orange_goal = pl.orange == false;
+            if (rs.params[0] != 0) orange_goal = !orange_goal;
+            V tgt = orange_goal ? V(0, 6000, 642.775f / 2) : V(0, -6000, 642.775f / 2);
+            V d = rs_norm(tgt - bpos);
+            return dot(d, rs_div(bvel, 6000.f));
+        }
+        case RLGPU_RW_PICKUP_BOOST:
+            return pl.boost > e.prev_boost[i] ? std::sqrt(pl.boost / 100.f) - std::sqrt(e.prev_boost[i] / 100.f) : 0;
+        case RLGPU_RW_SAVE_BOOST: return std::min(std::max(powf_det(pl.boost / 100, rs.params[0]), 0.f), 1.f);
+        case RLGPU_RW_BUMP: return e.ev_bump[i];
+        case RLGPU_RW_DEMO: return e.ev_demo[i];
+        case RLGPU_RW_BUMPED_PENALTY: return -(float)e.ev_bumped[i];
+        case RLGPU_RW_DEMOED_PENALTY: return -(float)e.ev_demoed[i];
+        case RLGPU_RW_GOAL: {
+            if (!goal) return 0;
+            bool ball_team_orange = !(bpos.y < 0);  // RS_TEAM_FROM_Y
+            return (pl.orange != ball_team_orange) ? 1.f : rs.params[0];
+        }
+        case RLGPU_RW_LOSING_PENALTY: {
+            int own = pl.orange ? e.penalty_orange : e.penalty_blue;
+            int opp = pl.orange ? e.penalty_blue : e.penalty_orange;
+            int deficit = opp - own;
+            return deficit > 0 ? -rs.params[0] * (float)deficit : 0.f;
+        }
+        case RLGPU_RW_VELOCITY: return rs_len(pl.vel) / 2300.f * (float)(1 - 2 * (rs.params[0] != 0));
+        case RLGPU_RW_FACE_BALL: return dot(pl.fwd, rs_norm(bpos - pl.pos));
+        case RLGPU_RW_TOUCH_BALL: return pl.touched ? 1.f : 0.f;
+        case RLGPU_RW_SPEED: return rs_len(pl.vel) / 2300.f;
+    }
+    return 0;
+}
+
 // ------------------------------------------------------------------ env step halves
 struct StepOut {
     float* obs;
     uint8_t* masks;
     float* rewards;
     uint8_t* terminal;
-    float* last_rewards;  // [RLGPU_REWARDS] of player 0 (may be null)
+    float* last_rewards;  // [number of rewards] of player 0 (may be null)
     int8_t* traj_term;    // [4] trajectory codes (Learner.cpp:829-861), may be null
     int max_episode_steps;
+    const Plugins* plug;
 };
 
 // GameState::UpdateFromArena + terminals + rewards + obs/masks (EnvSet.cpp:157-270)
@@ -394,25 +503,38 @@ void second_half_builders(rlgpu_arena_state& s, const StepOut& out, int tick_ski
     bool goal = std::fabs(s.ball.pos[1] * BT_TO_UU) > (5124.25f + 91.25f);  // Arena::IsBallScored
     PlayerView P[4];
     for (int i = 0; i < 4; i++) P[i] = view_player(s.cars[i], i, touched[i]);
-    // terminal conditions: NoTouchCondition(8), ScoreLimitCondition(3)
+    // terminal conditions of the list (EnvSet.cpp:163-181).  Every instance of NoTouchCondition
+    // (NoTouchCondition.h:17-28) keeps the same timeSinceTouch and every ScoreLimitCondition
+    // (ExampleMain.cpp:55-68) the same goal counts -- IsTerminal runs for all of them each step -- so
+    // the arena holds one copy of each, updated every step.
     uint8_t term = 0;
     {
         bool any = touched[0] || touched[1] || touched[2] || touched[3];
-        bool t_notouch;
-        if (any) {
-            e.no_touch_time = 0;
-            t_notouch = false;
-        } else {
-            e.no_touch_time += delta_time;
-            t_notouch = e.no_touch_time >= 8.f;
-        }
+        if (any) e.no_touch_time = 0;
+        else e.no_touch_time += delta_time;
         if (goal) {
             if (bpos.y > 0) e.score_blue++;
             else e.score_orange++;
         }
-        bool t_score = (e.score_blue >= 3) || (e.score_orange >= 3);
-        if (t_notouch) term = 2;
-        if (t_score) term = 1;  // NORMAL dominates (EnvSet.cpp:167-180)
+        for (const rlgpu_terminal_spec& c : out.plug->tc) {
+            bool terminal = false, truncation = false;
+            switch (c.type) {
+                case RLGPU_TC_NO_TOUCH:
+                    terminal = !any && e.no_touch_time >= c.param;
+                    truncation = true;
+                    break;
+                case RLGPU_TC_SCORE_LIMIT: {
+                    int limit = (int)c.param;
+                    terminal = (e.score_blue >= limit) || (e.score_orange >= limit);
+                    break;
+                }
+                case RLGPU_TC_GOAL_SCORE: terminal = goal; break;  // GoalScoreCondition.h
+            }
+            if (!terminal) continue;
+            uint8_t t = truncation ? 2 : 1;
+            if (term == 0) term = t;
+            else if (t == 1) term = 1;  // NORMAL dominates
+        }
     }
     e.terminal = term;
     // trajectory-level code: maxEpisodeLength truncates without an arena reset (Learner.cpp:848-850)
@@ -427,80 +549,16 @@ void second_half_builders(rlgpu_arena_state& s, const StepOut& out, int tick_ski
         if (bpos.y > 0) e.penalty_blue++;
         else e.penalty_orange++;
     }
-    // rewards (ExampleMain.cpp:132-177); allRewards[i] += out[i] * weight in list order
-    const float W[RLGPU_REWARDS] = {0.25f, 0.12f, 5.f, 4.f, 60, 6.f, 8.0f, 0.1f, 0.010f, 20, 80, 150, 1.0f};
+    // rewards of the list; allRewards[i] += out[i] * weight in list order (EnvSet.cpp:183-222); lastRewards
+    // holds each reward's value for the lowest car id, player 0 (:224-242; ZeroSumReward's inner rewards
+    // stay empty on this path, so the value is the child's)
     float all[4] = {0, 0, 0, 0};
     V prev_bvel = ld3v(e.prev_ball_vel);
-    const float KPH = 250.f / 9.f;
-    for (int r = 0; r < RLGPU_REWARDS; r++) {
+    const std::vector<rlgpu_reward_spec>& rw = out.plug->rw;
+    for (size_t r = 0; r < rw.size(); r++) {
         float o[4];
-        for (int i = 0; i < 4; i++) {
-            const PlayerView& pl = P[i];
-            float v = 0;
-            switch (r) {
-                case 0: v = !pl.on_ground; break;  // AirReward
-                case 1:                             // WavedashReward
-                    v = (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1 : 0;
-                    break;
-                case 2: v = KickoffReward::reward(i, P, bpos, bvel); break;
-                case 3: {  // VelocityPlayerToBallReward
-                    V dir = rs_norm(bpos - pl.pos);
-                    V nv = rs_div(pl.vel, 2300.f);
-                    v = dot(dir, nv);
-                    break;
-                }
-                case 4: {  // StrongTouchReward(20, 120)
-                    float minv = 20 * KPH, maxv = 120 * KPH;
-                    if (pl.touched) {
-                        float hit = rs_len(bvel - prev_bvel);
-                        v = hit < minv ? 0 : std::min(1.f, hit / maxv);
-                    }
-                    break;
-                }
-                case 5: {  // TouchAccelReward
-                    const float MAXS = 110 * KPH;
-                    if (pl.touched) {
-                        float pf = std::min(1.f, rs_len(prev_bvel) / MAXS);
-                        float cf = std::min(1.f, rs_len(bvel) / MAXS);
-                        v = cf > pf ? (cf - pf) : 0;
-                    }
-                    break;
-                }
-                case 6: {  // ZeroSum(VelocityBallToGoalReward) -> pass-through
-                    V tgt = !pl.orange ? V(0, 6000, 642.775f / 2) : V(0, -6000, 642.775f / 2);
-                    V d = rs_norm(tgt - bpos);
-                    v = dot(d, rs_div(bvel, 6000.f));
-                    break;
-                }
-                case 7:  // PickupBoostReward
-                    v = pl.boost > e.prev_boost[i] ? std::sqrt(pl.boost / 100.f) - std::sqrt(e.prev_boost[i] / 100.f) : 0;
-                    break;
-                case 8: {  // SaveBoostReward(0.5): powf(b/100, 0.5) evaluated as sqrtf
-                    float x = std::sqrt(pl.boost / 100);
-                    v = std::min(std::max(x, 0.f), 1.f);
-                    break;
-                }
-                case 9: v = e.ev_bump[i]; break;   // ZeroSum(BumpReward) pass-through
-                case 10: v = e.ev_demo[i]; break;  // ZeroSum(DemoReward) pass-through
-                case 11: {                         // ZeroSum(GoalReward) pass-through
-                    if (goal) {
-                        bool team_from_y_orange = !(bpos.y < 0);
-                        bool scored = pl.orange != team_from_y_orange;
-                        v = scored ? 1.f : -1.f;
-                    }
-                    break;
-                }
-                case 12: {  // LosingPenaltyReward(0.02)
-                    int own = pl.orange ? e.penalty_orange : e.penalty_blue;
-                    int opp = pl.orange ? e.penalty_blue : e.penalty_orange;
-                    int deficit = opp - own;
-                    v = deficit > 0 ? -0.02f * (float)deficit : 0.f;
-                    break;
-                }
-            }
-            o[i] = v;
-        }
-        for (int i = 0; i < 4; i++) all[i] += o[i] * W[r];
+        for (int i = 0; i < 4; i++) o[i] = reward_of(rw[r], i, P, e, bpos, bvel, prev_bvel, goal);
+        for (int i = 0; i < 4; i++) all[i] += o[i] * rw[r].weight;
         if (out.last_rewards) out.last_rewards[r] = o[0];
     }
     for (int i = 0; i < 4; i++) out.rewards[i] = all[i];
@@ -617,6 +675,7 @@ struct EnvSet {
     std::vector<uint8_t> masks, terminals;
     std::vector<int8_t> traj_terms;
     int max_episode_steps = 0;
+    Plugins plug = example_main_plugins();
     Pool* pool = nullptr;
     World* own_world = nullptr;     // set by oracle_env_set_mesh
     const World* w = &world();
@@ -635,7 +694,7 @@ struct EnvSet {
     }
     StepOut out(int i) {
         return {&obs[(size_t)i * 4 * RLGPU_OBS], &masks[(size_t)i * 4 * RLGPU_ACTIONS], &rewards[(size_t)i * 4], &terminals[i],
-                &last_rewards[(size_t)i * RLGPU_REWARDS], &traj_terms[(size_t)i * 4], max_episode_steps};
+                &last_rewards[(size_t)i * RLGPU_MAX_REWARDS], &traj_terms[(size_t)i * 4], max_episode_steps, &plug};
     }
 };
 
@@ -657,7 +716,7 @@ void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action
     e->trunc_obs.assign((size_t)num_arenas * 4 * RLGPU_OBS, 0.f);
     e->masks.assign((size_t)num_arenas * 4 * RLGPU_ACTIONS, 0);
     e->rewards.assign((size_t)num_arenas * 4, 0.f);
-    e->last_rewards.assign((size_t)num_arenas * RLGPU_REWARDS, 0.f);
+    e->last_rewards.assign((size_t)num_arenas * RLGPU_MAX_REWARDS, 0.f);
     e->terminals.assign(num_arenas, 0);
     e->traj_terms.assign((size_t)num_arenas * 4, 0);
     if (threads > 1) e->pool = new Pool(threads);
@@ -751,6 +810,15 @@ void oracle_env_read(void* h, float* obs, uint8_t* masks, float* rewards, uint8_
 }
 
 void oracle_env_set_max_episode_steps(void* h, int n) { ((EnvSet*)h)->max_episode_steps = n; }
+
+// The reward / terminal lists (rlgpu_envset_config.rewards / terminals; NULL keeps ExampleMain's).
+// last_rewards rows are RLGPU_MAX_REWARDS wide, the first n_rewards used.
+void oracle_env_set_plugins(void* h, const rlgpu_reward_spec* rw, int nr, const rlgpu_terminal_spec* tc, int nt) {
+    EnvSet* e = (EnvSet*)h;
+    Plugins def = example_main_plugins();
+    e->plug.rw = rw ? std::vector<rlgpu_reward_spec>(rw, rw + nr) : def.rw;
+    e->plug.tc = tc ? std::vector<rlgpu_terminal_spec>(tc, tc + nt) : def.tc;
+}
 
 // Arena collision meshes for this set (rlgpu_envset_config.mesh_*): ntris x 9 floats (bullet
 // units), object k owns the next obj_ntris[k] triangles (obj_ntris NULL: one object).

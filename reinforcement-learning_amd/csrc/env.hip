@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "common.hpp"
@@ -42,6 +43,7 @@ struct StepArgs {
     MeshView mesh;
     double* metrics;           // [n][RLGPU_STEP_METRIC_SLOTS] StepCallback sums (build steps) or null
     int metrics_players;       // this call is one of ExampleMain's every-4th "expensive" calls
+    const Plugins* plug;       // the set's reward / terminal registry (device)
 };
 
 // ExampleMain's StepCallback (src/ExampleMain.cpp:233-283) on this arena's GameState as the
@@ -428,22 +430,34 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
             float by = A->s.ball.pos[1] * kBT2UU;
             bool goal = fabsf(by) > (5124.25f + 91.25f);
             A->a.goal = goal;
-            bool t_notouch;
-            if (any) {
-                e.no_touch_time = 0;
-                t_notouch = false;
-            } else {
-                e.no_touch_time += delta_time;
-                t_notouch = e.no_touch_time >= 8.f;
-            }
+            // the conditions' state: NoTouchCondition::timeSinceTouch and ScoreLimitCondition's goal
+            // counts evolve identically in every instance (each IsTerminal is called every step), so one
+            // copy serves any number of instances with different limits
+            if (any) e.no_touch_time = 0;
+            else e.no_touch_time += delta_time;
             if (goal) {
                 if (by > 0) e.score_blue++;
                 else e.score_orange++;
             }
-            bool t_score = (e.score_blue >= 3) || (e.score_orange >= 3);
+            // terminal merge over the registry's list (EnvSet.cpp:167-180): NORMAL dominates
             uint8_t tt = 0;
-            if (t_notouch) tt = 2;
-            if (t_score) tt = 1;
+            for (int k = 0; k < g.plug->nt; k++) {
+                const rlgpu_terminal_spec& tc = g.plug->tc[k];
+                bool hit = false, trunc = false;
+                if (tc.type == RLGPU_TC_NO_TOUCH) {
+                    hit = !any && e.no_touch_time >= tc.param;
+                    trunc = true;
+                } else if (tc.type == RLGPU_TC_SCORE_LIMIT) {
+                    const int lim = (int)tc.param;
+                    hit = (e.score_blue >= lim) || (e.score_orange >= lim);
+                } else if (tc.type == RLGPU_TC_GOAL_SCORE) {
+                    hit = goal;
+                }
+                if (hit) {
+                    const uint8_t cur = trunc ? 2 : 1;
+                    if (tt == 0 || cur == 1) tt = cur;
+                }
+            }
             e.terminal = tt;
             if (goal) {
                 if (by > 0) e.penalty_blue++;
@@ -461,11 +475,13 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
         if (valid && l < 4) {
             const PView me = view_player(A, l);  // the other players' views are read where used
             v3 bp = ld3(A->s.ball.pos) * kBT2UU, bv = ld3(A->s.ball.vel) * kBT2UU, pbv = ld3(A->s.env.prev_ball_vel);
-            float all = 0.f;
-            for (int r = 0; r < RLGPU_REWARDS; r++) {
-                float o = reward_value(A, r, l, me, bp, bv, pbv, A->a.goal != 0);
-                all += o * C.reward_w[r];
-                if (l == 0 && g.last_rewards) g.last_rewards[(size_t)arena * RLGPU_REWARDS + r] = o;
+            float all = 0.f;  // allRewards[i] += out[i] * weight in list order (EnvSet.cpp:199-222)
+            const int nr = g.plug->nr;
+            for (int r = 0; r < nr; r++) {
+                const rlgpu_reward_spec& rs = g.plug->rw[r];
+                float o = reward_value(A, rs, l, me, bp, bv, pbv, A->a.goal != 0);
+                all += o * rs.weight;
+                if (l == 0 && g.last_rewards) g.last_rewards[(size_t)arena * nr + r] = o;
             }
             A->a.all_rewards[l] = all;
         }
@@ -685,8 +701,6 @@ static EnvConst make_env_const() {
             if (i < ng && x[0] == x[6] && ((x[3] != 0) == (x[7] != 0))) k.mask_air[i] = 1;
         }
     }
-    const float W[RLGPU_REWARDS] = {0.25f, 0.12f, 5.f, 4.f, 60, 6.f, 8.0f, 0.1f, 0.010f, 20, 80, 150, 1.0f};
-    std::memcpy(k.reward_w, W, sizeof W);
     return k;
 }
 
@@ -704,7 +718,102 @@ struct rlgpu_envset {
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
     void *d_tri = nullptr, *d_cell_start = nullptr, *d_cell_tris = nullptr;  // arena mesh (MeshView)
     rl::MeshView mesh{};
+    rl::Plugins plug{};                 // host copy of the reward / terminal registry
+    rl::Plugins* d_plug = nullptr;      // its device copy (StepArgs::plug)
+    int32_t* d_player_start = nullptr;  // EnvState::arenaPlayerStartIdx
 };
+
+namespace {
+// src/ExampleMain.cpp:132-187: the 13 weighted rewards and NoTouchCondition(8) + ScoreLimitCondition(3)
+void example_main_plugins(rl::Plugins& p) {
+    std::memset(&p, 0, sizeof p);
+    struct R {
+        int type;
+        float w, p0, p1;
+        int zs;
+        float ts, os;
+    };
+    const R list[RLGPU_REWARDS] = {
+        {RLGPU_RW_AIR, 0.25f, 0, 0, 0, 0, 0},
+        {RLGPU_RW_WAVEDASH, 0.12f, 0, 0, 0, 0, 0},
+        {RLGPU_RW_KICKOFF_PROXIMITY_2V2, 5.f, 0, 0, 0, 0, 0},
+        {RLGPU_RW_VELOCITY_PLAYER_TO_BALL, 4.f, 0, 0, 0, 0, 0},
+        {RLGPU_RW_STRONG_TOUCH, 60, 20, 120, 0, 0, 0},
+        {RLGPU_RW_TOUCH_ACCEL, 6.f, 0, 0, 0, 0, 0},
+        {RLGPU_RW_VELOCITY_BALL_TO_GOAL, 8.0f, 0, 0, 1, 1, 1},   // ZeroSumReward(child, 1)
+        {RLGPU_RW_PICKUP_BOOST, 0.1f, 0, 0, 0, 0, 0},
+        {RLGPU_RW_SAVE_BOOST, 0.010f, 0.5f, 0, 0, 0, 0},
+        {RLGPU_RW_BUMP, 20, 0, 0, 1, 0.5f, 1},                   // ZeroSumReward(child, 0.5f)
+        {RLGPU_RW_DEMO, 80, 0, 0, 1, 0.5f, 1},
+        {RLGPU_RW_GOAL, 150, -1, 0, 1, 1, 1},                    // GoalReward() concedeScale -1
+        {RLGPU_RW_LOSING_PENALTY, 1.0f, 0.02f, 0, 0, 0, 0}};
+    p.nr = RLGPU_REWARDS;
+    for (int i = 0; i < RLGPU_REWARDS; i++) {
+        rlgpu_reward_spec& r = p.rw[i];
+        r.type = list[i].type;
+        r.weight = list[i].w;
+        r.params[0] = list[i].p0;
+        r.params[1] = list[i].p1;
+        r.zero_sum = list[i].zs;
+        r.zero_sum_team_spirit = list[i].ts;
+        r.zero_sum_opponent_scale = list[i].os;
+    }
+    p.nt = 2;
+    p.tc[0] = rlgpu_terminal_spec{RLGPU_TC_NO_TOUCH, 8.f};
+    p.tc[1] = rlgpu_terminal_spec{RLGPU_TC_SCORE_LIMIT, 3.f};
+}
+
+// the config's lists, validated (before any device work: a rejected config allocates nothing)
+rl::Plugins plugins_from(const rlgpu_envset_config* cfg) {
+    rl::Plugins p;
+    example_main_plugins(p);
+    if (cfg->rewards) {
+        RLGPU_REQUIRE(cfg->n_rewards >= 0 && cfg->n_rewards <= RLGPU_MAX_REWARDS,
+                      "rlgpu_envset_create: n_rewards must be in [0, " + std::to_string(RLGPU_MAX_REWARDS) + "]");
+        p.nr = cfg->n_rewards;
+        for (int i = 0; i < p.nr; i++) {
+            const rlgpu_reward_spec& r = cfg->rewards[i];
+            if (r.type < 0 || r.type >= RLGPU_NUM_REWARD_TYPES)
+                throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED,
+                                   "rlgpu_envset_create: reward " + std::to_string(i) + " has unknown type " +
+                                       std::to_string(r.type) + " (the device registry holds types 0.." +
+                                       std::to_string(RLGPU_NUM_REWARD_TYPES - 1) + ", include/rlgpu_env.h RLGPU_RW_*)");
+            p.rw[i] = r;
+        }
+    } else {
+        RLGPU_REQUIRE(cfg->n_rewards == 0, "rlgpu_envset_create: n_rewards without a rewards list");
+    }
+    if (cfg->terminals) {
+        RLGPU_REQUIRE(cfg->n_terminals >= 0 && cfg->n_terminals <= RLGPU_MAX_TERMINALS,
+                      "rlgpu_envset_create: n_terminals must be in [0, " + std::to_string(RLGPU_MAX_TERMINALS) + "]");
+        p.nt = cfg->n_terminals;
+        for (int i = 0; i < p.nt; i++) {
+            const rlgpu_terminal_spec& t = cfg->terminals[i];
+            if (t.type < 0 || t.type >= RLGPU_NUM_TERMINAL_TYPES)
+                throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED,
+                                   "rlgpu_envset_create: terminal condition " + std::to_string(i) + " has unknown type " +
+                                       std::to_string(t.type) + " (the device registry holds types 0.." +
+                                       std::to_string(RLGPU_NUM_TERMINAL_TYPES - 1) + ", include/rlgpu_env.h RLGPU_TC_*)");
+            p.tc[i] = t;
+        }
+    } else {
+        RLGPU_REQUIRE(cfg->n_terminals == 0, "rlgpu_envset_create: n_terminals without a terminals list");
+    }
+    return p;
+}
+}  // namespace
+
+extern "C" int rlgpu_envset_default_plugins(rlgpu_reward_spec* rewards, int32_t* n_rewards, rlgpu_terminal_spec* terminals,
+                                            int32_t* n_terminals) {
+    return rlgpu::guarded([&] {
+        rl::Plugins p;
+        example_main_plugins(p);
+        if (rewards) std::memcpy(rewards, p.rw, sizeof(rlgpu_reward_spec) * p.nr);
+        if (n_rewards) *n_rewards = p.nr;
+        if (terminals) std::memcpy(terminals, p.tc, sizeof(rlgpu_terminal_spec) * p.nt);
+        if (n_terminals) *n_terminals = p.nt;
+    });
+}
 
 namespace {
 bool g_const_ready = false;
@@ -729,6 +838,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.max_episode_steps = e->cfg.max_episode_steps;
     g.prof = e->d_prof;
     g.mesh = e->mesh;
+    g.plug = e->d_plug;
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
         g.metrics_players = (++e->metric_calls % 4) == 0;
@@ -755,6 +865,7 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         RLGPU_REQUIRE(cfg->action_delay >= 0 && cfg->action_delay <= cfg->tick_skip,
                       "actionDelay must be in [0, tickSkip] (EnvSet.cpp:49)");
         RLGPU_REQUIRE(cfg->mesh_tris == nullptr || cfg->mesh_ntris > 0, "mesh_ntris must be > 0 with mesh_tris");
+        const rl::Plugins plug = plugins_from(cfg);
         ensure_const();
         // arena meshes (Arena::_SetupArenaCollisionShapes): triangle table + grid index in HBM
         std::vector<float> builtin;
@@ -771,6 +882,11 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         e->cfg = *cfg;
         e->cfg.mesh_tris = nullptr;  // host pointers are not kept
         e->cfg.mesh_object_ntris = nullptr;
+        e->cfg.rewards = nullptr;
+        e->cfg.terminals = nullptr;
+        e->plug = plug;
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_plug, sizeof(rl::Plugins)));
+        RLGPU_CHECK_HIP(hipMemcpy(e->d_plug, &e->plug, sizeof(rl::Plugins), hipMemcpyHostToDevice));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_tri, grid.tri.size() * sizeof(float)));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_start, grid.cell_start.size() * sizeof(int)));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_tris, std::max<size_t>(grid.cell_tris.size(), 1) * sizeof(int)));
@@ -798,13 +914,19 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         RLGPU_CHECK_HIP(hipMalloc(&e->d_obs, P * RLGPU_OBS * sizeof(float)));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_trunc_obs, P * RLGPU_OBS * sizeof(float)));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_rewards, P * sizeof(float)));
-        RLGPU_CHECK_HIP(hipMalloc(&e->d_last_rewards, (size_t)n * RLGPU_REWARDS * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_last_rewards, (size_t)n * std::max(plug.nr, 1) * sizeof(float)));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_masks, P * RLGPU_ACTIONS));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_terminals, (size_t)n));
         RLGPU_CHECK_HIP(hipMemset(e->d_terminals, 0, (size_t)n));
         RLGPU_CHECK_HIP(hipMemset(e->d_rewards, 0, P * sizeof(float)));
         RLGPU_CHECK_HIP(hipMemset(e->d_trunc_obs, 0, P * RLGPU_OBS * sizeof(float)));
-        RLGPU_CHECK_HIP(hipMemset(e->d_last_rewards, 0, (size_t)n * RLGPU_REWARDS * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMemset(e->d_last_rewards, 0, (size_t)n * std::max(plug.nr, 1) * sizeof(float)));
+        {  // EnvState::arenaPlayerStartIdx (EnvSet.h:35-65): 4 players per arena
+            std::vector<int32_t> start(n);
+            for (int i = 0; i < n; i++) start[i] = 4 * i;
+            RLGPU_CHECK_HIP(hipMalloc(&e->d_player_start, (size_t)n * sizeof(int32_t)));
+            RLGPU_CHECK_HIP(hipMemcpy(e->d_player_start, start.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+        }
         // initial records: Arena ctor + AddCar defaults (Arena.cpp:429-562, Car.cpp:195-277)
         std::vector<char> host((size_t)n * rl::kRec, 0);
         rl::EnvConst k = rl::make_env_const();
@@ -921,6 +1043,8 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_tri);
         (void)hipFree(e->d_cell_start);
         (void)hipFree(e->d_cell_tris);
+        (void)hipFree(e->d_plug);
+        (void)hipFree(e->d_player_start);
         delete e;
     });
 }
@@ -936,6 +1060,8 @@ extern "C" int rlgpu_envset_buffers_get(rlgpu_envset* e, rlgpu_envset_buffers* o
         out->trunc_obs = e->d_trunc_obs;
         out->num_players = e->num_players;
         out->num_arenas = e->cfg.num_arenas;
+        out->num_rewards = e->plug.nr;
+        out->arena_player_start = e->d_player_start;
     });
 }
 

@@ -246,56 +246,77 @@ DEV float kickoff_reward(ArenaLDS* A, int pi, const PView& pl, v3 bpos, v3 bvel)
     return clampf(tot, -0.8f, 0.8f);
 }
 
-// one reward of the ExampleMain list for player i (src/ExampleMain.cpp:132-177)
-DEV float reward_value(ArenaLDS* A, int r, int i, const PView& pl, v3 bpos, v3 bvel, v3 prev_bvel, bool goal) {
+// a^b for SaveBoostReward's powf (CommonRewards.h:136-145): b = 0.5 as sqrtf (correctly rounded on
+// both sides, the ExampleMain case), otherwise exp(b log a) on the shared deterministic kernels
+DEV float reward_powf(float a, float b) {
+    if (b == 0.5f) return sqrtf(a);
+    if (b == 0.f) return 1.f;
+    if (a == 0.f) return b > 0.f ? 0.f : __int_as_float(0x7f800000);
+    return rs_expf(b * rs_logf(a));
+}
+
+// one weighted reward of the registry for player i (CommonRewards.h:8-203,
+// KickoffProximityReward2v2Enhanced.h, src/ExampleMain.cpp:84-124); CommonValues CAR_MAX_SPEED 2300,
+// BALL_MAX_SPEED 6000, goal backs (0, +-6000, 642.775 / 2) (CommonValues.h)
+DEV float reward_value(ArenaLDS* A, const rlgpu_reward_spec& rs, int i, const PView& pl, v3 bpos, v3 bvel, v3 prev_bvel,
+                       bool goal) {
     const rlgpu_env_extra& e = A->s.env;
-    const float KPH = 250.f / 9.f;
+    const float KPH = 250.f / 9.f;  // Math::KPHToVel (RG/Math.h:12-14)
     bool touched = A->a.touched[i] != 0;
-    switch (r) {
-        case 0: return !pl.on_ground;
-        case 1: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1.f : 0.f;
-        case 2: return kickoff_reward(A, i, pl, bpos, bvel);
-        case 3: {
+    switch (rs.type) {
+        case RLGPU_RW_AIR: return !pl.on_ground;
+        case RLGPU_RW_WAVEDASH: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1.f : 0.f;
+        case RLGPU_RW_KICKOFF_PROXIMITY_2V2: return kickoff_reward(A, i, pl, bpos, bvel);
+        case RLGPU_RW_VELOCITY_PLAYER_TO_BALL: {
             v3 dir = rs_norm(bpos - pl.pos);
             v3 nv = rs_div(pl.vel, 2300.f);
             return dot(dir, nv);
         }
-        case 4: {
-            float minv = 20 * KPH, maxv = 120 * KPH;
+        case RLGPU_RW_STRONG_TOUCH: {
+            float minv = rs.params[0] * KPH, maxv = rs.params[1] * KPH;
             if (!touched) return 0.f;
             float hit = rs_len(bvel - prev_bvel);
             return hit < minv ? 0.f : stdmin(1.f, hit / maxv);
         }
-        case 5: {
+        case RLGPU_RW_TOUCH_ACCEL: {
             const float MAXS = 110 * KPH;
             if (!touched) return 0.f;
             float pf = stdmin(1.f, rs_len(prev_bvel) / MAXS);
             float cf = stdmin(1.f, rs_len(bvel) / MAXS);
             return cf > pf ? (cf - pf) : 0.f;
         }
-        case 6: {
-            v3 tgt = !pl.orange ? v3{0, 6000, 642.775f / 2} : v3{0, -6000, 642.775f / 2};
+        case RLGPU_RW_VELOCITY_BALL_TO_GOAL: {
+            bool target_orange = !pl.orange;
+            if (rs.params[0] != 0.f) target_orange = !target_orange;  // ownGoal
+            v3 tgt = target_orange ? v3{0, 6000, 642.775f / 2} : v3{0, -6000, 642.775f / 2};
             v3 d = rs_norm(tgt - bpos);
             return dot(d, rs_div(bvel, 6000.f));
         }
-        case 7: return pl.boost > e.prev_boost[i] ? sqrtf(pl.boost / 100.f) - sqrtf(e.prev_boost[i] / 100.f) : 0.f;
-        case 8: {
-            float x = sqrtf(pl.boost / 100);
-            return stdmin(stdmax(x, 0.f), 1.f);
+        case RLGPU_RW_PICKUP_BOOST:
+            return pl.boost > e.prev_boost[i] ? sqrtf(pl.boost / 100.f) - sqrtf(e.prev_boost[i] / 100.f) : 0.f;
+        case RLGPU_RW_SAVE_BOOST: {
+            float x = reward_powf(pl.boost / 100, rs.params[0]);
+            return stdmin(stdmax(x, 0.f), 1.f);  // RS_CLAMP
         }
-        case 9: return e.ev_bump[i];
-        case 10: return e.ev_demo[i];
-        case 11: {
+        case RLGPU_RW_BUMP: return e.ev_bump[i];
+        case RLGPU_RW_DEMO: return e.ev_demo[i];
+        case RLGPU_RW_BUMPED_PENALTY: return -(float)e.ev_bumped[i];
+        case RLGPU_RW_DEMOED_PENALTY: return -(float)e.ev_demoed[i];
+        case RLGPU_RW_GOAL: {
             if (!goal) return 0.f;
-            bool team_from_y_orange = !(bpos.y < 0);
-            return (pl.orange != team_from_y_orange) ? 1.f : -1.f;
+            bool team_from_y_orange = !(bpos.y < 0);  // RS_TEAM_FROM_Y
+            return (pl.orange != team_from_y_orange) ? 1.f : rs.params[0];  // concedeScale
         }
-        case 12: {
+        case RLGPU_RW_LOSING_PENALTY: {
             int own = pl.orange ? e.penalty_orange : e.penalty_blue;
             int opp = pl.orange ? e.penalty_blue : e.penalty_orange;
             int deficit = opp - own;
-            return deficit > 0 ? -0.02f * (float)deficit : 0.f;
+            return deficit > 0 ? -rs.params[0] * (float)deficit : 0.f;
         }
+        case RLGPU_RW_VELOCITY: return rs_len(pl.vel) / 2300.f * (float)(1 - 2 * (rs.params[0] != 0.f));
+        case RLGPU_RW_FACE_BALL: return dot(pl.fwd, rs_norm(bpos - pl.pos));
+        case RLGPU_RW_TOUCH_BALL: return touched ? 1.f : 0.f;
+        case RLGPU_RW_SPEED: return rs_len(pl.vel) / 2300.f;
     }
     return 0.f;
 }

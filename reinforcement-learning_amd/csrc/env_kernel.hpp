@@ -69,7 +69,14 @@ struct EnvConst {
     v3 boost_loc[RLGPU_PADS];          // CommonValues::BOOST_LOCATIONS (uu)
     float action[RLGPU_ACTIONS][8];    // DefaultAction table
     uint8_t mask_ground[RLGPU_ACTIONS], mask_air[RLGPU_ACTIONS], mask_jump[RLGPU_ACTIONS], mask_boost[RLGPU_ACTIONS];
-    float reward_w[RLGPU_REWARDS];
+};
+
+// The env set's reward / terminal registry (rlgpu_envset_config rewards / terminals), one device copy
+// per set, read with uniform (scalar) loads by every workgroup.
+struct Plugins {
+    int nr, nt;
+    rlgpu_reward_spec rw[RLGPU_MAX_REWARDS];
+    rlgpu_terminal_spec tc[RLGPU_MAX_TERMINALS];
 };
 
 struct WheelT {

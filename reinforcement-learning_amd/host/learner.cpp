@@ -204,6 +204,10 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     ec.mesh_ntris = cfg.mesh_ntris;
     ec.mesh_objects = cfg.mesh_objects;
     ec.mesh_object_ntris = cfg.mesh_object_ntris;
+    ec.rewards = cfg.rewards;
+    ec.n_rewards = cfg.n_rewards;
+    ec.terminals = cfg.terminals;
+    ec.n_terminals = cfg.n_terminals;
     env_ = new RLGC::EnvSetGPU(ec, s_);
     // ExampleMain registers its StepCallback (ExampleMain.cpp:233-283, 592): restated on the device
     RlgpuCheck(rlgpu_envset_enable_step_metrics(env_->handle(), 1), "step metrics");

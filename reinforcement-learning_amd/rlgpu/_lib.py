@@ -31,6 +31,11 @@ def lib():
     return _lib
 
 
+def last_error():
+    """rlgpu_last_error() of this thread."""
+    return lib().rlgpu_last_error().decode(errors="replace")
+
+
 def check(status, what=""):
     if status != 0:
         msg = lib().rlgpu_last_error().decode(errors="replace")

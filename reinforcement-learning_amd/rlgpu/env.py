@@ -27,7 +27,8 @@ class _Config(ctypes.Structure):
     _fields_ = [("num_arenas", ctypes.c_int32), ("tick_skip", ctypes.c_int32), ("action_delay", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("save_rewards", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32),
                 ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
-                ("mesh_object_ntris", ctypes.c_void_p)]
+                ("mesh_object_ntris", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("n_rewards", ctypes.c_int32),
+                ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32)]
 
 
 class StepOutputs(ctypes.Structure):
@@ -47,7 +48,8 @@ class StepOutputs(ctypes.Structure):
 class _Buffers(ctypes.Structure):
     _fields_ = [("obs", ctypes.c_void_p), ("action_masks", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
                 ("terminals", ctypes.c_void_p), ("last_rewards", ctypes.c_void_p), ("trunc_obs", ctypes.c_void_p),
-                ("num_players", ctypes.c_int32), ("num_arenas", ctypes.c_int32)]
+                ("num_players", ctypes.c_int32), ("num_arenas", ctypes.c_int32), ("num_rewards", ctypes.c_int32),
+                ("arena_player_start", ctypes.c_void_p)]
 
 
 _bound = False
@@ -85,13 +87,15 @@ def arena_state_size():
 
 
 class EnvSet:
-    """Vectorised 2v2 arena set resident in HBM (ExampleMain plugin set: AdvancedObs,
-    DefaultAction, 13 rewards, NoTouch(8 s) + GoalScore(3) terminals, KickoffState)."""
+    """Vectorised 2v2 arena set resident in HBM (AdvancedObs, DefaultAction, KickoffState, and a
+    reward / terminal list from the device registry -- ExampleMain's 13 rewards and NoTouch(8 s) +
+    ScoreLimit(3) by default)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, save_rewards=True, device="cuda:0",
-                 max_episode_steps=0, mesh=None):
+                 max_episode_steps=0, mesh=None, rewards=None, terminals=None):
         """mesh: an rlgpu.mesh.ArenaMesh (e.g. ArenaMesh.from_folder("collision_meshes")), or None for
-        the built-in synthetic arena mesh."""
+        the built-in synthetic arena mesh.  rewards / terminals: lists of rlgpu.plugins.reward(...) /
+        terminal(...) specs (or structured arrays), None = ExampleMain's."""
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("EnvSet needs an MI355X: the product path has no CPU fallback")
@@ -104,6 +108,16 @@ class EnvSet:
             cfg.mesh_ntris = mesh.num_tris
             cfg.mesh_objects = mesh.num_objects
             cfg.mesh_object_ntris = mesh.object_ntris.ctypes.data
+        from . import plugins
+        # a non-NULL list pointer selects the given list, even an empty one (a 1-record buffer then)
+        if rewards is not None:
+            rw = rewards if isinstance(rewards, np.ndarray) else plugins.rewards_array(rewards)
+            self._rw = np.ascontiguousarray(rw if rw.size else np.zeros(1, plugins.REWARD_SPEC))
+            cfg.rewards, cfg.n_rewards = self._rw.ctypes.data, rw.size
+        if terminals is not None:
+            tc = terminals if isinstance(terminals, np.ndarray) else plugins.terminals_array(terminals)
+            self._tc = np.ascontiguousarray(tc if tc.size else np.zeros(1, plugins.TERMINAL_SPEC))
+            cfg.terminals, cfg.n_terminals = self._tc.ctypes.data, tc.size
         h = ctypes.c_void_p()
         _lib.check(L.rlgpu_envset_create(ctypes.byref(cfg), ctypes.byref(h)), "rlgpu_envset_create")
         self._h = h
@@ -128,14 +142,15 @@ class EnvSet:
         import torch
         b = _Buffers()
         _lib.check(L.rlgpu_envset_buffers_get(self._h, ctypes.byref(b)), "rlgpu_envset_buffers_get")
-        self.num_arenas, self.num_players = b.num_arenas, b.num_players
+        self.num_arenas, self.num_players, self.num_rewards = b.num_arenas, b.num_players, b.num_rewards
         P, N, dev = b.num_players, b.num_arenas, self.device
         self.obs = _alias(b.obs, (P, OBS), torch.float32, dev)
         self.action_masks = _alias(b.action_masks, (P, ACTIONS), torch.uint8, dev)
         self.rewards = _alias(b.rewards, (P,), torch.float32, dev)
         self.terminals = _alias(b.terminals, (N,), torch.uint8, dev)
-        self.last_rewards = _alias(b.last_rewards, (N, REWARDS), torch.float32, dev)
+        self.last_rewards = _alias(b.last_rewards, (N, self.num_rewards), torch.float32, dev)
         self.trunc_obs = _alias(b.trunc_obs, (P, OBS), torch.float32, dev)
+        self.arena_player_start = _alias(b.arena_player_start, (N,), torch.int32, dev)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -175,6 +175,8 @@ class LearnerConfig:
         self.policy_layers = (512, 512)
         self.critic_layers = (512, 512)
         self.shared_layers = ()            # PPOLearnerConfig::sharedHead ((384, 384) in the reference's run log)
+        self.rewards = None                # EnvCreateFn reward list (rlgpu.plugins.reward specs); None = ExampleMain's
+        self.terminals = None              # terminal conditions (rlgpu.plugins.terminal specs); None = ExampleMain's
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
         self.train_gemm = 2               # rlgpu_ppo_config.train_gemm: 2 = f32 via scaled fp16 split (H3), 0 = bf16 x6 split, 1 = f32 MFMA
@@ -210,7 +212,9 @@ class _CConfig(ctypes.Structure):
                 ("frame_stack", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
                 ("mesh_object_ntris", ctypes.c_void_p),
-                ("shared_layers", ctypes.c_int32 * MAX_LAYERS), ("n_shared_layers", ctypes.c_int32)]
+                ("shared_layers", ctypes.c_int32 * MAX_LAYERS), ("n_shared_layers", ctypes.c_int32),
+                ("rewards", ctypes.c_void_p), ("n_rewards", ctypes.c_int32),
+                ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32)]
 
 
 class _CRollout(ctypes.Structure):
@@ -301,6 +305,15 @@ class Learner:
         for i, v in enumerate(cfg.shared_layers):
             c.shared_layers[i] = v
         c.n_shared_layers = len(cfg.shared_layers)
+        from . import plugins
+        if cfg.rewards is not None:
+            rw = plugins.rewards_array(cfg.rewards)
+            self._rw = np.ascontiguousarray(rw if rw.size else np.zeros(1, plugins.REWARD_SPEC))
+            c.rewards, c.n_rewards = self._rw.ctypes.data, rw.size
+        if cfg.terminals is not None:
+            tc = plugins.terminals_array(cfg.terminals)
+            self._tc = np.ascontiguousarray(tc if tc.size else np.zeros(1, plugins.TERMINAL_SPEC))
+            c.terminals, c.n_terminals = self._tc.ctypes.data, tc.size
         c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
         c.frame_stack = cfg.frame_stack
         c.rank, c.world = rank, world
