@@ -54,6 +54,19 @@ int rlgpu_gae_rollout(const float* d_rews, const int8_t* d_terms, const float* d
                       float* d_adv, float* d_target, float* d_ret, float* d_clip_partials,
                       void* stream);
 
+/* Complete trajectories of a flat batch -- the reference's combinedTraj (Learner.cpp:823-861), whose
+ * every trajectory ends in its only nonzero code: segment k covers rows [d_seg_off[k],
+ * d_seg_off[k] + d_seg_len[k]), d_seg_tidx[k] is its index into d_trunc_vals when it ends TRUNCATED
+ * (else -1).  One lane per segment walks it backwards in GAE::Compute's operation order
+ * (GAE.cpp:169-193).  This equals rlgpu_gae_flat's sequential reference over the concatenation BIT
+ * FOR BIT whenever no reward is -0: across a terminal the recursion's carry is multiplied by
+ * notDoneNotTrunc = 0, so only a -0 reward could expose the carry's sign (the env's weighted reward
+ * sums start at +0 and are never -0).  d_clip_partials as rlgpu_gae_rollout. */
+int rlgpu_gae_segments(const float* d_rews, const int8_t* d_terms, const float* d_vals, const float* d_trunc_vals,
+                       const int64_t* d_seg_off, const int32_t* d_seg_len, const int32_t* d_seg_tidx,
+                       int64_t num_segments, float gamma, float lambda, float return_std, float clip_range,
+                       float* d_adv, float* d_target, float* d_ret, float* d_clip_partials, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

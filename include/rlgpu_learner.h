@@ -84,7 +84,21 @@ typedef struct {
     int32_t n_rewards;
     const rlgpu_terminal_spec* terminals;
     int32_t n_terminals;
+    /* Experience scheduling.  RLGPU_EXP_ROLLOUT (0, default): a fixed [T, P] rollout trained in full,
+     * the unfinished tail bootstrapped from V(obs_T) (the engine's fast path, BASELINE configs).
+     * RLGPU_EXP_TRAJECTORIES (1): the reference's -- steps are kept per player until the trajectory
+     * ends, only complete trajectories are trained (in the order they end: combinedTraj), unfinished ones
+     * carry over to the next iteration, and collection runs until ts_per_itr steps of complete
+     * trajectories are held (Learner.cpp:504-547,823-861), then GAE runs over the trajectories with
+     * their truncation values (GAE.cpp:7-208) -- needs max_episode_duration > 0. */
+    int32_t experience_mode;
+    int64_t ts_per_itr;            /* PPOLearnerConfig::tsPerItr (mode 1); 0 = rollout_len * 4 * num_arenas */
+    int32_t experience_capacity;   /* mode 1: store rows (steps kept per player); 0 = maxEpisodeLength +
+                                      2 * ceil(ts_per_itr / players) + 64.  Collection also stops when
+                                      the store would overwrite a live step (documented divergence). */
 } rlgpu_learner_config;
+
+enum { RLGPU_EXP_ROLLOUT = 0, RLGPU_EXP_TRAJECTORIES = 1 };
 
 /* Fills ExampleMain's values (src/ExampleMain.cpp:340-430) for a C2 rank: 4096 arenas, T = 128,
  * [512, 512] actor / critic (BASELINE config C2, no shared head), world 1.  ExampleMain's own
@@ -100,6 +114,17 @@ typedef struct {
     int (*allreduce_sum_f64)(void* user, double* h_buf, int64_t n);          /* host buffer, in place */
     int (*allgather_f32)(void* user, const float* h_in, int64_t n, float* h_out); /* host, out [world * n] */
 } rlgpu_collective;
+
+/* The collective over a native RCCL communicator (one rank per GPU, RCCL over xGMI; host/
+ * rccl_collective.cpp): the gradient all-reduce is enqueued on `stream` (the learner's), the fp64
+ * moments and return samples are staged through the device.  Rank 0 makes the 128-byte unique id and
+ * the launcher hands it to every rank (rlgpu_train: a file; Python: any side channel); every rank then
+ * calls create with its rank and the world size (ncclCommInitRank, collective across the ranks).
+ * destroy frees the communicator and zeroes the struct. */
+#define RLGPU_RCCL_ID_BYTES 128
+int rlgpu_rccl_unique_id(uint8_t* out, int32_t out_bytes);
+int rlgpu_rccl_collective_create(const uint8_t* id, int32_t rank, int32_t world, void* stream, rlgpu_collective* out);
+int rlgpu_rccl_collective_destroy(rlgpu_collective* c);
 
 /* Device views of the rollout (ExperienceBuffer) in HBM, [T, P] time-major, P = 4 * num_arenas.
  * W = obs_width = RLGPU_OBS * max(1, frame_stack). */
@@ -119,6 +144,29 @@ typedef struct {
     int32_t T, P;
     int32_t obs_width;   /* W */
 } rlgpu_rollout_view;
+
+/* The trained batch of RLGPU_EXP_TRAJECTORIES (valid after consume, until the next collect): the
+ * complete trajectories of the iteration concatenated in the order they ended (combinedTraj), their
+ * critic values / GAE outputs, the truncation list (nextTruncStates and their values, in the same
+ * order), and the trajectory records. */
+typedef struct {
+    float* obs;          /* [num_rows][obs_width] */
+    uint8_t* masks;      /* [num_rows][RLGPU_ACTIONS] */
+    int32_t* actions;
+    float* logp, *rewards;
+    int8_t* terms;       /* 0 inside a trajectory, its code (1 / 2) on its last step */
+    float* values, *adv, *target, *ret;
+    int64_t num_rows;
+    float* trunc_obs;    /* [num_truncs][obs_width] */
+    float* trunc_vals;   /* [num_truncs] */
+    int64_t num_truncs;
+    int32_t *seg_player, *seg_start, *seg_len, *seg_code, *seg_tidx; /* [num_segments] */
+    int64_t* seg_off;    /* first row of each trajectory in the batch */
+    int64_t num_segments;
+    int32_t store_rows;  /* the per-player step store's rows (circular) */
+    int32_t steps;       /* env steps collected this iteration */
+    int64_t first_step;  /* global index of its first step; store row = step % store_rows */
+} rlgpu_batch_view;
 
 /* Host-side statistics (checkpoint RUNNING_STATS.json, Learner.cpp:224-279). */
 typedef struct {
@@ -146,6 +194,8 @@ int rlgpu_learner_destroy(rlgpu_learner* h);
 /* The owned env set and PPO handles (valid until destroy). */
 int rlgpu_learner_handles(rlgpu_learner* h, rlgpu_envset** env, rlgpu_ppo** ppo);
 int rlgpu_learner_rollout(rlgpu_learner* h, rlgpu_rollout_view* out);
+/* The trained batch of RLGPU_EXP_TRAJECTORIES (RLGPU_ERR_STATE in the rollout mode). */
+int rlgpu_learner_batch(rlgpu_learner* h, rlgpu_batch_view* out);
 
 /* One iteration = collect + consume + learn + finish (Learner::Start loop body). */
 int rlgpu_learner_iterate(rlgpu_learner* h, rlgpu_learner_report* rep);

@@ -328,7 +328,83 @@ __global__ void __launch_bounds__(256) k_gae_rollout(const float* __restrict__ r
     }
 }
 
+// One lane per complete trajectory of a flat batch (rlgpu_gae_segments): the same recursion as
+// k_gae_rollout over rows off + len - 1 .. off, the segment's terminal bootstrapped from trunc_vals[tidx]
+// (code 2) or 0 (code 1), prevLambda / prevRet starting at 0.
+__global__ void __launch_bounds__(256) k_gae_segments(const float* __restrict__ rews, const int8_t* __restrict__ terms,
+                                                      const float* __restrict__ vals, const float* __restrict__ trunc_vals,
+                                                      const int64_t* __restrict__ seg_off, const int32_t* __restrict__ seg_len,
+                                                      const int32_t* __restrict__ seg_tidx, int64_t K, float gamma,
+                                                      float gamma_lambda, float inv_std, int normalize, int clip,
+                                                      float clip_range, float* __restrict__ adv, float* __restrict__ target,
+                                                      float* __restrict__ ret, float* clip_sums) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float sabs = 0.f, sclip = 0.f;
+    if (k < K) {
+        const int64_t off = seg_off[k];
+        const int L = seg_len[k], tidx = seg_tidx[k];
+        float prevLambda = 0.f, prevRet = 0.f;
+        for (int j = L - 1; j >= 0; --j) {
+            const int64_t i = off + j;
+            const int8_t term = terms[i];
+            const float rew = rews[i];
+            float cur = rew;
+            if (normalize) {
+                cur = rew * inv_std;
+                sabs += fabsf(cur);
+                if (clip) cur = fminf(fmaxf(cur, -clip_range), clip_range);
+                sclip += fabsf(cur);
+            }
+            const float done = (term == kNormal) ? 1.f : 0.f;
+            const float trunc = (term == kTruncated) ? 1.f : 0.f;
+            const float nd = (1.f - done) * (1.f - trunc);
+            float nextVal;
+            if (term == kNormal) nextVal = 0.f;
+            else if (term == kTruncated) nextVal = (trunc_vals && tidx >= 0) ? trunc_vals[tidx] : 0.f;
+            else nextVal = vals[i + 1];  // a segment's non-final rows are never its last row
+            const float v = vals[i];
+            const float predReturn = cur + gamma * nextVal;
+            const float delta = predReturn - v;
+            const float curReturn = rew + prevRet * gamma * nd;
+            ret[i] = curReturn;
+            prevLambda = delta + gamma_lambda * nd * prevLambda;
+            adv[i] = prevLambda;
+            target[i] = v + prevLambda;
+            prevRet = curReturn;
+        }
+    }
+    if (clip_sums && normalize) {
+        for (int o = 32; o > 0; o >>= 1) {
+            sabs += __shfl_down(sabs, o, 64);
+            sclip += __shfl_down(sclip, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&clip_sums[0], sabs);
+            atomicAdd(&clip_sums[1], sclip);
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int rlgpu_gae_segments(const float* d_rews, const int8_t* d_terms, const float* d_vals, const float* d_trunc_vals,
+                                  const int64_t* d_seg_off, const int32_t* d_seg_len, const int32_t* d_seg_tidx,
+                                  int64_t num_segments, float gamma, float lambda, float return_std, float clip_range,
+                                  float* d_adv, float* d_target, float* d_ret, float* d_clip_partials, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(num_segments >= 0, "rlgpu_gae_segments: negative segment count");
+        if (num_segments == 0) return;
+        RLGPU_REQUIRE(d_rews && d_terms && d_vals && d_seg_off && d_seg_len && d_seg_tidx && d_adv && d_target && d_ret,
+                      "rlgpu_gae_segments: null argument");
+        hipStream_t s = rlgpu::as_stream(stream);
+        const bool normalize = (return_std != 0.f && return_std != 1.f);  // GAE.cpp:47-49
+        const float inv_std = normalize ? 1.f / return_std : 1.f;
+        hipLaunchKernelGGL(k_gae_segments, dim3(rlgpu::ceil_div(num_segments, 256)), dim3(256), 0, s, d_rews, d_terms, d_vals,
+                           d_trunc_vals, d_seg_off, d_seg_len, d_seg_tidx, num_segments, gamma, gamma * lambda, inv_std,
+                           (int)normalize, (int)(clip_range > 0.f), clip_range, d_adv, d_target, d_ret, d_clip_partials);
+        RLGPU_CHECK_HIP(hipGetLastError());
+    });
+}
 
 extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const float* d_vals,
                               const float* d_trunc_vals, int64_t num_returns, int64_t num_truncs, float gamma,

@@ -126,6 +126,117 @@ __global__ void k_stack_frames(const float* cur, const float* trunc, const int8_
     }
 }
 
+// one workgroup walks the players in chunks of 1024: block-wide exclusive scans of the end /
+// truncation flags give each ending trajectory its record slot, truncation slot and combined offset in
+// (player) order after the records of earlier steps
+constexpr int kTrajThreads = 1024;
+__global__ void __launch_bounds__(kTrajThreads) k_traj_step(const int8_t* codes, int row, int Tmax, const uint8_t* track,
+                                                            int P, int32_t* start, int32_t* len, TrajRecs R,
+                                                            int64_t* cnt, int32_t* trnew) {
+    typedef hipcub::BlockScan<int, kTrajThreads> Scan;
+    typedef hipcub::BlockScan<int64_t, kTrajThreads> Scan64;
+    __shared__ typename Scan::TempStorage ts;
+    __shared__ typename Scan64::TempStorage ts64;
+    __shared__ int64_t base[3];
+    __shared__ int newtr;
+    const int t = threadIdx.x;
+    if (t == 0) {
+        base[0] = cnt[kTcRecs];
+        base[1] = cnt[kTcTruncs];
+        base[2] = cnt[kTcSteps];
+        newtr = 0;
+    }
+    __syncthreads();
+    const int next = (row + 1) % Tmax;
+    for (int c0 = 0; c0 < P; c0 += kTrajThreads) {
+        const int p = c0 + t;
+        const bool on = p < P && (!track || track[p]);
+        const int code = on ? codes[p] : 0;
+        const int l = on ? len[p] + 1 : 0;
+        const int e = code != 0, tr = code == 2;
+        int eo, to, etot, ttot;
+        int64_t lo, ltot;
+        Scan(ts).ExclusiveSum(e, eo, etot);
+        __syncthreads();
+        Scan(ts).ExclusiveSum(tr, to, ttot);
+        __syncthreads();
+        Scan64(ts64).ExclusiveSum(e ? (int64_t)l : (int64_t)0, lo, ltot);
+        __syncthreads();
+        if (e) {
+            const int64_t k = base[0] + eo;
+            R.p[k] = p;
+            R.start[k] = start[p];
+            R.len[k] = l;
+            R.code[k] = code;
+            R.tidx[k] = tr ? (int32_t)(base[1] + to) : -1;
+            R.off[k] = base[2] + lo;
+            if (tr) trnew[newtr + to] = p;
+            start[p] = next;
+            len[p] = 0;
+        } else if (on) {
+            len[p] = l;
+        }
+        __syncthreads();
+        if (t == 0) {
+            base[0] += etot;
+            base[1] += ttot;
+            base[2] += ltot;
+            newtr += ttot;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        cnt[kTcRecs] = base[0];
+        cnt[kTcTruncs] = base[1];
+        cnt[kTcSteps] = base[2];
+        cnt[kTcNewTruncs] = newtr;
+    }
+}
+
+__global__ void k_traj_trunc_copy(const float* src, int W, const int64_t* cnt, const int32_t* trnew, float* dst) {
+    const int64_t nnew = cnt[kTcNewTruncs], first = cnt[kTcTruncs] - nnew;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnew * W; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = e / W;
+        const int c = (int)(e - j * W);
+        dst[(first + j) * W + c] = src[(int64_t)trnew[j] * W + c];
+    }
+}
+
+__global__ void k_traj_restart(const uint8_t* mask, int P, int row, int32_t* start, int32_t* len) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P && mask[p]) {
+        start[p] = row;
+        len[p] = 0;
+    }
+}
+
+// one workgroup per record: its steps' rows, 16-byte vectors where the obs rows allow
+__global__ void __launch_bounds__(256) k_traj_gather(TrajRecs R, int Tmax, int P, int W, int A, const float* obs,
+                                                     const uint8_t* masks, const int32_t* acts, const float* logp,
+                                                     const float* rews, const int8_t* terms, float* c_obs,
+                                                     uint8_t* c_masks, int32_t* c_acts, float* c_logp, float* c_rews,
+                                                     int8_t* c_terms) {
+    const int64_t k = blockIdx.x;
+    const int p = R.p[k], st = R.start[k], L = R.len[k];
+    const int64_t off = R.off[k];
+    for (int j = threadIdx.x; j < L; j += blockDim.x) {
+        const int64_t src = (int64_t)((st + j) % Tmax) * P + p, dst = off + j;
+        c_acts[dst] = acts[src];
+        c_logp[dst] = logp[src];
+        c_rews[dst] = rews[src];
+        c_terms[dst] = terms[src];
+    }
+    for (int j = 0; j < L; j++) {
+        const int64_t src = (int64_t)((st + j) % Tmax) * P + p, dst = off + j;
+        const float* so = obs + src * W;
+        float* d = c_obs + dst * W;
+        for (int c = threadIdx.x; c < W; c += blockDim.x) d[c] = so[c];
+        const uint8_t* sm = masks + src * A;
+        uint8_t* dm = c_masks + dst * A;
+        for (int c = threadIdx.x; c < A; c += blockDim.x) dm[c] = sm[c];
+    }
+}
+
 struct IsTrunc {
     const int8_t* t;
     __device__ bool operator()(const int32_t& i) const { return t[i] == 2; }
@@ -180,6 +291,29 @@ void stack_frames(const float* cur, const float* trunc, const int8_t* codes, flo
     const int64_t n = (int64_t)P * obs;
     hipLaunchKernelGGL(k_stack_frames, dim3(ceil_div(n, 256)), dim3(256), 0, s, cur, trunc, codes, hist, K, P, obs, out,
                        out_trunc);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+void traj_step(const int8_t* codes, int row, int Tmax, const uint8_t* track, int P, int32_t* start, int32_t* len,
+               TrajRecs recs, int64_t* counters, int32_t* trnew, hipStream_t s) {
+    hipLaunchKernelGGL(k_traj_step, dim3(1), dim3(kTrajThreads), 0, s, codes, row, Tmax, track, P, start, len, recs, counters,
+                       trnew);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void traj_trunc_copy(const float* src, int W, const int64_t* counters, const int32_t* trnew, float* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_traj_trunc_copy, dim3(256), dim3(256), 0, s, src, W, counters, trnew, dst);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void traj_restart(const uint8_t* mask, int P, int row, int32_t* start, int32_t* len, hipStream_t s) {
+    hipLaunchKernelGGL(k_traj_restart, dim3(ceil_div(P, 256)), dim3(256), 0, s, mask, P, row, start, len);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+void traj_gather(TrajRecs recs, int64_t K, int Tmax, int P, int W, int A, const float* obs, const uint8_t* masks,
+                 const int32_t* acts, const float* logp, const float* rews, const int8_t* terms, float* c_obs,
+                 uint8_t* c_masks, int32_t* c_acts, float* c_logp, float* c_rews, int8_t* c_terms, hipStream_t s) {
+    if (K <= 0) return;
+    hipLaunchKernelGGL(k_traj_gather, dim3((unsigned)K), dim3(256), 0, s, recs, Tmax, P, W, A, obs, masks, acts, logp, rews,
+                       terms, c_obs, c_masks, c_acts, c_logp, c_rews, c_terms);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 

@@ -31,4 +31,34 @@ void select_trunc(const int8_t* terms, int64_t n, void* scratch, size_t scratch_
 // hist [K-1][P][OBS].  codes == null: initialise (every stack = the current frame repeated).
 void stack_frames(const float* cur, const float* trunc, const int8_t* codes, float* hist, int K, int P, int obs,
                   float* out, float* out_trunc, hipStream_t s);
+
+// ---- reference experience mode (complete trajectories with carry-over, Learner.cpp:504-547,823-861)
+// Trajectory records, structure of arrays (capacity rows each), appended in the reference's order:
+// by the step a trajectory ends, then by player index (combinedTraj.Append in the newPlayerIndices loop).
+struct TrajRecs {
+    int32_t* p;      // player
+    int32_t* start;  // circular store row of its first step
+    int32_t* len;    // steps
+    int32_t* code;   // its last step's code: 1 NORMAL / 2 TRUNCATED
+    int32_t* tidx;   // index into the truncation list (code 2), else -1
+    int64_t* off;    // first row in the combined (flat) batch
+};
+// counters (device int64 [8]): [0] records, [1] truncations, [2] combined steps (finished), [3] this
+// step's truncations (players in trnew)
+enum { kTcRecs = 0, kTcTruncs = 1, kTcSteps = 2, kTcNewTruncs = 3, kTcCount = 8 };
+// One env step's bookkeeping: for every tracked player (track[p] != 0; null = all) the step at store
+// row `row` (codes[p]) extends its trajectory; a nonzero code ends it -- a record is appended and the
+// next trajectory starts at row + 1 (mod Tmax).  trnew[j] = the j-th truncating player of this step.
+void traj_step(const int8_t* codes, int row, int Tmax, const uint8_t* track, int P, int32_t* start, int32_t* len,
+               TrajRecs recs, int64_t* counters, int32_t* trnew, hipStream_t s);
+// the pre-reset obs rows of this step's truncations (src [P][W]) to dst rows counters[1] - counters[3] + j
+void traj_trunc_copy(const float* src, int W, const int64_t* counters, const int32_t* trnew, float* dst, hipStream_t s);
+// restart the trajectories of players with mask[p] != 0 at store row `row` (self-play: a team that acted
+// with an old version)
+void traj_restart(const uint8_t* mask, int P, int row, int32_t* start, int32_t* len, hipStream_t s);
+// the combined batch: record k's len steps (store rows start .. start + len - 1 mod Tmax, column p) to
+// combined rows off .. off + len - 1 (obs W floats, masks A bytes, action, log prob, reward, code)
+void traj_gather(TrajRecs recs, int64_t K, int Tmax, int P, int W, int A, const float* obs, const uint8_t* masks,
+                 const int32_t* acts, const float* logp, const float* rews, const int8_t* terms, float* c_obs,
+                 uint8_t* c_masks, int32_t* c_acts, float* c_logp, float* c_rews, int8_t* c_terms, hipStream_t s);
 }  // namespace lk

@@ -9,11 +9,20 @@
 // [512, 512] actor / critic without a shared head.  The loop is GGL::Learner::Start over a fixed
 // number of iterations, printing the reference's report keys.
 //
+// Multi-GPU: one process per GPU (--rank r --world N --rccl-id FILE): rank 0 writes RCCL's unique id
+// to FILE, the other ranks read it, every rank trains its own arenas and the Learner's exchanges run
+// over the native RCCL communicator (host/rccl_collective.cpp).
+//
 //   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--f32-gemm] [--c2-model]
+//               [--rank r --world N --rccl-id FILE]
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <fstream>
+#include <string>
+#include <thread>
 
 #include "learner.hpp"
 
@@ -21,6 +30,7 @@ int main(int argc, char** argv) {
     rlgpu_learner_config cfg;
     rlgpu_learner_default_config(&cfg);
     long iterations = 3;
+    std::string idFile;
     cfg.n_shared_layers = 2;
     cfg.shared_layers[0] = cfg.shared_layers[1] = 384;
     cfg.n_policy_layers = cfg.n_critic_layers = 3;
@@ -30,6 +40,9 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--arenas") && i + 1 < argc) cfg.num_arenas = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rollout") && i + 1 < argc) cfg.rollout_len = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--f32-gemm")) cfg.train_gemm = RLGPU_GEMM_F32;
+        else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) cfg.rank = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) cfg.world = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--rccl-id") && i + 1 < argc) idFile = argv[++i];
         else if (!std::strcmp(argv[i], "--c2-model")) {
             cfg.n_shared_layers = 0;
             cfg.n_policy_layers = cfg.n_critic_layers = 2;
@@ -40,9 +53,33 @@ int main(int argc, char** argv) {
         }
     }
     try {
+        if (cfg.world > 1) {  // one GPU per rank (local rank = rank on one node)
+            int ndev = 0;
+            if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw std::runtime_error("no GPU");
+            if (hipSetDevice(cfg.rank % ndev) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
+        }
         hipStream_t s = nullptr;
         if (hipStreamCreate(&s) != hipSuccess) throw std::runtime_error("hipStreamCreate failed");
-        GGL::Learner learner(cfg, nullptr, s);
+        rlgpu_collective coll{};
+        if (cfg.world > 1) {
+            if (idFile.empty()) throw std::runtime_error("--world > 1 needs --rccl-id FILE");
+            uint8_t id[RLGPU_RCCL_ID_BYTES];
+            if (cfg.rank == 0) {  // write then rename: readers never see a partial id
+                RLGC::RlgpuCheck(rlgpu_rccl_unique_id(id, sizeof id), "RCCL unique id");
+                const std::string tmp = idFile + ".tmp";
+                std::ofstream(tmp, std::ios::binary).write((const char*)id, sizeof id);
+                if (std::rename(tmp.c_str(), idFile.c_str()) != 0) throw std::runtime_error("cannot write " + idFile);
+            } else {
+                for (int tries = 0;; tries++) {
+                    std::ifstream f(idFile, std::ios::binary);
+                    if (f && f.read((char*)id, sizeof id) && f.gcount() == (std::streamsize)sizeof id) break;
+                    if (tries > 6000) throw std::runtime_error("timed out waiting for " + idFile);
+                    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+                }
+            }
+            RLGC::RlgpuCheck(rlgpu_rccl_collective_create(id, cfg.rank, cfg.world, s, &coll), "RCCL communicator");
+        }
+        GGL::Learner learner(cfg, cfg.world > 1 ? &coll : nullptr, s);
         {  // "Model parameter counts:" (PPOLearner.cpp:24-33; ModelSet order: critic, policy, shared_head)
             int64_t cnt[3] = {0, 0, 0}, total = 0;
             for (int m = 0; m < 3; m++) RLGC::RlgpuCheck(rlgpu_ppo_model_range(learner.ppo().handle(), m, nullptr, &cnt[m]), "model range");
@@ -71,6 +108,7 @@ int main(int argc, char** argv) {
             for (int k = 0; k < RLGPU_NUM_STEP_METRICS; k++)
                 if (cnt[k]) std::printf("  %s: %.4g\n", rlgpu_step_metric_name(k), tot[k] / (double)cnt[k]);
         }
+        if (cfg.world > 1) RLGC::RlgpuCheck(rlgpu_rccl_collective_destroy(&coll), "RCCL communicator");
         (void)hipStreamDestroy(s);
     } catch (const std::exception& e) {  // ExampleMain.cpp:603-612
         std::fprintf(stderr, "Exception thrown: %s\n", e.what());

@@ -100,7 +100,28 @@ std::vector<std::pair<int64_t, int64_t>> BatchRanges(int64_t expSize, int64_t ba
     return out;
 }
 
-void ExperienceBuffer::Allocate(int T_, int P_, int W_) {
+template <class T>
+void DevArray<T>::Reserve(int64_t n, hipStream_t s, bool keep) {
+    if (n <= cap) return;
+    const int64_t ncap = std::max<int64_t>(n, cap + cap / 2);
+    T* q = nullptr;
+    hipCheck(hipMalloc((void**)&q, (size_t)ncap * sizeof(T) + 16), "DevArray alloc");
+    if (keep && p && cap > 0) hipCheck(hipMemcpyAsync(q, p, (size_t)cap * sizeof(T), hipMemcpyDeviceToDevice, s), "DevArray copy");
+    if (p) {
+        hipCheck(hipStreamSynchronize(s), "sync");
+        (void)hipFree(p);
+    }
+    p = q;
+    cap = ncap;
+}
+template <class T>
+void DevArray<T>::Free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+void ExperienceBuffer::Allocate(int T_, int P_, int W_, bool rollout_outputs) {
     T = T_;
     P = P_;
     W = W_;
@@ -112,18 +133,19 @@ void ExperienceBuffer::Allocate(int T_, int P_, int W_) {
         return p;
     };
     const size_t TP = (size_t)T * P, T1P = (size_t)(T + 1) * P;
+    const size_t OP = rollout_outputs ? TP : (size_t)P, O1P = rollout_outputs ? T1P : (size_t)P;
     v.obs = (float*)A(T1P * W * 4);
     v.masks = (uint8_t*)A(T1P * ACT);
     v.actions = (int32_t*)A(TP * 4);
     v.logp = (float*)A(TP * 4);
     v.rewards = (float*)A(TP * 4);
     v.terms = (int8_t*)A(TP);
-    v.trunc_obs = (float*)A(TP * W * 4);
-    v.values = (float*)A(T1P * 4);
-    v.trunc_vals = (float*)A(TP * 4);
-    v.adv = (float*)A(TP * 4);
-    v.target = (float*)A(TP * 4);
-    v.ret = (float*)A(TP * 4);
+    v.trunc_obs = (float*)A(OP * W * 4);
+    v.values = (float*)A(O1P * 4);
+    v.trunc_vals = (float*)A(OP * 4);
+    v.adv = (float*)A(OP * 4);
+    v.target = (float*)A(OP * 4);
+    v.ret = (float*)A(OP * 4);
     v.T = T;
     v.P = P;
     v.obs_width = W;
@@ -235,7 +257,9 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     pc.entropy_scale = cfg.entropy_scale;
     pc.max_grad_norm = 0.5f;
     const int64_t TP = (int64_t)T * P;
-    pc.max_rows = (int32_t)std::max<int64_t>(std::min<int64_t>(cfg.mini_batch_size, TP), std::min<int64_t>(P, 65536));
+    // minibatch rows: the rollout's T * P caps them in mode 0; complete-trajectory batches can be larger
+    const int64_t rowsCap = cfg.experience_mode == RLGPU_EXP_TRAJECTORIES ? (int64_t)cfg.mini_batch_size : TP;
+    pc.max_rows = (int32_t)std::max<int64_t>(std::min<int64_t>(cfg.mini_batch_size, rowsCap), std::min<int64_t>(P, 65536));
     pc.seed = cfg.seed;
     pc.train_gemm = cfg.train_gemm;
     pc.infer_fp16 = cfg.infer_fp16;
@@ -251,7 +275,33 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
             throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: parameter broadcast failed");
         RlgpuCheck(rlgpu_ppo_refresh_half(ppo_->handle(), s_), "refresh half");
     }
-    exp_.Allocate(T, P, W);
+    if (trajMode()) {  // the reference's experience scheduling (RLGPU_EXP_TRAJECTORIES)
+        RLGPU_REQUIRE(ec.max_episode_steps > 0, "Learner: experience_mode 1 needs max_episode_duration > 0");
+        TrajectoryStore& J = traj;
+        J.maxLen = ec.max_episode_steps;
+        // every rank collects its share of the iteration's complete-trajectory steps
+        const int64_t total = cfg.ts_per_itr > 0 ? cfg.ts_per_itr : (int64_t)T * P * cfg.world;
+        J.tsPerItr = (total + cfg.world - 1) / cfg.world;
+        const int64_t perStep = P;  // steps per env step (all players tracked at most)
+        J.Tmax = cfg.experience_capacity > 0 ? cfg.experience_capacity
+                                              : (int)(J.maxLen + 2 * ((J.tsPerItr + perStep - 1) / perStep) + 64);
+        RLGPU_REQUIRE(J.Tmax > J.maxLen + 1, "Learner: experience_capacity must exceed the max episode length + 1");
+        exp_.Allocate(J.Tmax, P, W, false);
+        J.start = Alloc<int32_t>(P);
+        J.len = Alloc<int32_t>(P);
+        J.trnew = Alloc<int32_t>(P);
+        J.counters = Alloc<int64_t>(lk::kTcCount);
+        hipCheck(hipMemset(J.start, 0, (size_t)P * 4), "traj start");
+        hipCheck(hipMemset(J.len, 0, (size_t)P * 4), "traj len");
+        hipCheck(hipHostMalloc((void**)&J.hcounters, lk::kTcCount * sizeof(int64_t)), "pinned counters");
+        if (K_ > 1) J.truncStage = Alloc<float>((size_t)P * W);
+        const int64_t rc = 4 * (int64_t)P;
+        for (auto* a : {&J.rp, &J.rstart, &J.rlen, &J.rcode, &J.rtidx}) a->Reserve(rc, s_);
+        J.roff.Reserve(rc, s_);
+        J.truncObs.Reserve(4 * (int64_t)P * W, s_);
+    } else {
+        exp_.Allocate(T, P, W);
+    }
     // rollout row 0 = the env's initial obs (stacked: the first frame repeated) / masks
     const rlgpu_envset_buffers& st = env_->state();
     if (K_ > 1) {
@@ -281,6 +331,7 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     ends_ = Alloc<int32_t>(P);
     hostEnds_.assign(P, -1);
     mom_ = (double*)Alloc<char>(4 * sizeof(double) + lk::moments_scratch_bytes());
+    clipSums_ = Alloc<float>(2);
     hipCheck(hipStreamSynchronize(s_), "Learner init");
 }
 
@@ -290,12 +341,24 @@ Learner::~Learner() {
     for (void* p : allocs_) (void)hipFree(p);
     if (truncObsC_) (void)hipFree(truncObsC_);
     if (truncValC_) (void)hipFree(truncValC_);
+    if (traj.hcounters) (void)hipHostFree(traj.hcounters);
+    for (auto* a : {&traj.rp, &traj.rstart, &traj.rlen, &traj.rcode, &traj.rtidx, &traj.cActs}) a->Free();
+    traj.roff.Free();
+    for (auto* a : {&traj.truncObs, &traj.truncVals, &traj.cObs, &traj.cLogp, &traj.cRews, &traj.cVals, &traj.cAdv,
+                    &traj.cTarget, &traj.cRet})
+        a->Free();
+    traj.cMasks.Free();
+    traj.cTerms.Free();
     exp_.Free();
     delete ppo_;
     delete env_;
 }
 
 void Learner::Collect() {
+    if (trajMode()) {
+        CollectTrajectories();
+        return;
+    }
     const int T = exp_.T, P = exp_.P;
     const rlgpu_rollout_view& v = exp_.v;
     const uint8_t* old = oldTeam_ >= 0 ? oldRows_[oldTeam_] : nullptr;
@@ -325,6 +388,10 @@ void Learner::Collect() {
 }
 
 void Learner::Consume() {
+    if (trajMode()) {
+        ConsumeTrajectories();
+        return;
+    }
     const int T = exp_.T, P = exp_.P;
     const int64_t TP = (int64_t)T * P;
     const rlgpu_rollout_view& v = exp_.v;
@@ -366,10 +433,17 @@ void Learner::Consume() {
     int32_t m = 0;
     RlgpuCheck(rlgpu_sample_finished_rows(cfg_.seed, cfg_.rank, stats.iteration, hostEnds_.data(), P, k, idx.data(), &m),
                "return samples");
+    FeedReturnStat(v.ret, idx, m);
+}
+
+// WelfordStat::Increment over the sampled returns (Learner.cpp:959-967); ranks may hold different
+// sample counts, so the samples are all-gathered as (count, k padded samples) and every rank adds all
+void Learner::FeedReturnStat(const float* d_ret, const std::vector<int64_t>& idx, int32_t m) {
+    const int k = cfg_.return_samples;
     std::vector<float> hs((size_t)std::max(m, 1));
     if (m > 0) {
         hipCheck(hipMemcpyAsync(sampleIdx_, idx.data(), m * sizeof(int64_t), hipMemcpyHostToDevice, s_), "sample idx");
-        lk::gather_samples(v.ret, sampleIdx_, m, samples_, s_);
+        lk::gather_samples(d_ret, sampleIdx_, m, samples_, s_);
         hipCheck(hipMemcpyAsync(hs.data(), samples_, m * sizeof(float), hipMemcpyDeviceToHost, s_), "samples");
         hipCheck(hipStreamSynchronize(s_), "sync");
     }
@@ -421,12 +495,33 @@ void Learner::BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int6
 
 void Learner::Learn() {
     const int T = exp_.T, P = exp_.P;
-    const rlgpu_rollout_view& v = exp_.v;
-    const bool rows = oldTeam_ >= 0;
-    const int64_t M = rows ? (int64_t)T * (P / 2) : (int64_t)T * P;
-    const int64_t globalM = M * cfg_.world;
+    rlgpu_rollout_view v = exp_.v;
+    // the trajectory mode trains the combined batch (complete trajectories of the current policy's
+    // players only, so no row selection)
+    const bool rows = oldTeam_ >= 0 && !trajMode();
+    int64_t M = rows ? (int64_t)T * (P / 2) : (int64_t)T * P;
+    if (trajMode()) {
+        M = traj.nrows;
+        v.obs = traj.cObs.p;
+        v.masks = traj.cMasks.p;
+        v.actions = traj.cActs.p;
+        v.logp = traj.cLogp.p;
+        v.adv = traj.cAdv.p;
+        v.target = traj.cTarget.p;
+        if (M <= 0 && !hasColl_) return;  // with ranks, an empty one still joins every collective
+    }
+    int64_t globalM = M * cfg_.world;
+    if (trajMode() && hasColl_) {  // ranks hold different complete-trajectory counts: the true total
+        double m = (double)M;
+        if (coll_.allreduce_sum_f64(coll_.user, &m, 1) != 0)
+            throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: batch-size all-reduce failed");
+        globalM = (int64_t)m;
+    }
     const int64_t batch = cfg_.batch_size > 0 ? cfg_.batch_size : globalM;
-    const int64_t localBatch = cfg_.batch_size > 0 ? std::max<int64_t>(1, cfg_.batch_size / cfg_.world) : M;
+    int64_t localBatch = cfg_.batch_size > 0 ? std::max<int64_t>(1, cfg_.batch_size / cfg_.world) : M;
+    // with several ranks every rank must take the same number of optimizer steps (one all-reduce each):
+    // the trajectory mode trains each rank's whole batch as one batch per epoch
+    if (trajMode() && hasColl_) localBatch = M;
     if (rows) lk::train_rows(T, P, 1 - oldTeam_, trainRows_, s_);
     for (int epoch = 0; epoch < cfg_.epochs; epoch++) {
         RlgpuCheck(rlgpu_permutation(M, cfg_.seed + (uint64_t)cfg_.rank, (uint64_t)(stats.iteration * cfg_.epochs + epoch),
@@ -437,7 +532,9 @@ void Learner::Learn() {
             lk::compose(trainRows_, perm_, M, permRows_, s_);
             order = permRows_;
         }
-        for (auto [b0, b1] : BatchRanges(M, localBatch, cfg_.overbatching != 0)) {
+        auto ranges = BatchRanges(M, localBatch, cfg_.overbatching != 0);
+        if (trajMode() && hasColl_ && ranges.empty()) ranges.emplace_back(0, 0);
+        for (auto [b0, b1] : ranges) {
             const bool whole = !rows && b0 == 0 && b1 == M;
             BatchAdvantageStats(v.adv, whole ? nullptr : order + b0, b1 - b0);
             for (int64_t s0 = b0; s0 < b1; s0 += cfg_.mini_batch_size) {
@@ -454,11 +551,100 @@ void Learner::FinishIteration() {
     const int T = exp_.T, P = exp_.P;
     const rlgpu_rollout_view& v = exp_.v;
     const size_t W = (size_t)exp_.W;
+    const int64_t realPlayers = oldTeam_ < 0 ? P : P / 2;  // numRealPlayers (Learner.cpp:629)
+    stats.iteration++;
+    if (trajMode()) {  // stepsCollected (Learner.cpp:651): every step of the iteration, finished or not
+        stats.total_steps += (int64_t)traj.steps * realPlayers * cfg_.world;
+        return;
+    }
     hipCheck(hipMemcpyAsync(v.obs, v.obs + (size_t)T * P * W, (size_t)P * W * 4, hipMemcpyDeviceToDevice, s_), "obs");
     hipCheck(hipMemcpyAsync(v.masks, v.masks + (size_t)T * P * ACT, (size_t)P * ACT, hipMemcpyDeviceToDevice, s_), "masks");
-    stats.iteration++;
-    const int64_t realPlayers = oldTeam_ < 0 ? P : P / 2;  // numRealPlayers (Learner.cpp:629)
     stats.total_steps += (int64_t)T * realPlayers * cfg_.world;
+}
+
+// ---- RLGPU_EXP_TRAJECTORIES: the reference's trajectory loop (Learner.cpp:643-861)
+void Learner::CollectTrajectories() {
+    TrajectoryStore& J = traj;
+    const int P = exp_.P, W = exp_.W, Tm = J.Tmax;
+    const rlgpu_rollout_view& v = exp_.v;
+    const rlgpu_envset_buffers& st = env_->state();
+    // the players of the current policy; a team that acted with an old version last iteration starts
+    // fresh trajectories (the reference freezes them and resumes them later across the gap)
+    const uint8_t* track = oldTeam_ >= 0 ? oldRows_[1 - oldTeam_] : nullptr;
+    if (J.lastOldTeam >= 0) lk::traj_restart(oldRows_[J.lastOldTeam], P, (int)(J.step % Tm), J.start, J.len, s_);
+    J.lastOldTeam = oldTeam_;
+    const uint8_t* old = oldTeam_ >= 0 ? oldRows_[oldTeam_] : nullptr;
+    hipCheck(hipMemsetAsync(J.counters, 0, lk::kTcCount * sizeof(int64_t), s_), "traj counters");
+    J.firstStep = J.step;
+    J.steps = 0;
+    J.nrec = J.ntrunc = J.nrows = 0;
+    for (;;) {
+        // room for this step's records and truncation rows (at most one per player)
+        const int64_t need = std::max(J.nrec, J.ntrunc) + P;
+        if (J.rp.cap < need) {
+            for (auto* a : {&J.rp, &J.rstart, &J.rlen, &J.rcode, &J.rtidx}) a->Reserve(2 * need, s_, true);
+            J.roff.Reserve(2 * need, s_, true);
+        }
+        J.truncObs.Reserve((J.ntrunc + P) * (int64_t)W, s_, true);
+        const int r = (int)(J.step % Tm), rn = (int)((J.step + 1) % Tm);
+        const size_t row = (size_t)r * P, rown = (size_t)rn * P;
+        ppo_->InferActions(v.obs + row * W, v.masks + row * ACT, P, cfg_.deterministic != 0, (uint64_t)stats.rng_step,
+                           v.actions + row, v.logp + row, old);
+        stats.rng_step++;
+        rlgpu_step_outputs o{K_ > 1 ? nullptr : v.obs + rown * OBS, v.masks + rown * ACT, v.rewards + row, v.terms + row,
+                             nullptr};
+        env_->Step(v.actions + row, &o);
+        if (K_ > 1)
+            lk::stack_frames(st.obs, st.trunc_obs, v.terms + row, hist_, K_, P, OBS, v.obs + rown * W, J.truncStage, s_);
+        lk::TrajRecs R{J.rp.p, J.rstart.p, J.rlen.p, J.rcode.p, J.rtidx.p, J.roff.p};
+        lk::traj_step(v.terms + row, r, Tm, track, P, J.start, J.len, R, J.counters, J.trnew, s_);
+        lk::traj_trunc_copy(K_ > 1 ? J.truncStage : st.trunc_obs, W, J.counters, J.trnew, J.truncObs.p, s_);
+        J.step++;
+        J.steps++;
+        hipCheck(hipMemcpyAsync(J.hcounters, J.counters, lk::kTcCount * sizeof(int64_t), hipMemcpyDeviceToHost, s_),
+                 "traj counters");
+        hipCheck(hipStreamSynchronize(s_), "sync");
+        J.nrec = J.hcounters[lk::kTcRecs];
+        J.ntrunc = J.hcounters[lk::kTcTruncs];
+        J.nrows = J.hcounters[lk::kTcSteps];
+        if (J.nrows >= J.tsPerItr) break;  // combinedTraj.Length() >= tsPerItr (Learner.cpp:651)
+        // the store holds maxLen steps of every live trajectory plus this iteration's: stop before the
+        // next step could overwrite a live one
+        if (J.steps + J.maxLen + 2 >= Tm) break;
+    }
+}
+
+void Learner::ConsumeTrajectories() {
+    TrajectoryStore& J = traj;
+    const int P = exp_.P, W = exp_.W;
+    const rlgpu_rollout_view& v = exp_.v;
+    const int64_t M = J.nrows, K = J.nrec, ntr = J.ntrunc;
+    J.cObs.Reserve(std::max<int64_t>(M, 1) * W, s_);
+    J.cMasks.Reserve(std::max<int64_t>(M, 1) * ACT, s_);
+    for (auto* a : {&J.cLogp, &J.cRews, &J.cVals, &J.cAdv, &J.cTarget, &J.cRet}) a->Reserve(std::max<int64_t>(M, 1), s_);
+    J.cActs.Reserve(std::max<int64_t>(M, 1), s_);
+    J.cTerms.Reserve(std::max<int64_t>(M, 1), s_);
+    J.truncVals.Reserve(std::max<int64_t>(ntr, 1), s_);
+    if (M == 0) return;
+    // combinedTraj -> tensors (Learner.cpp:863-912): the complete trajectories in the order they ended
+    lk::TrajRecs R{J.rp.p, J.rstart.p, J.rlen.p, J.rcode.p, J.rtidx.p, J.roff.p};
+    lk::traj_gather(R, K, J.Tmax, P, W, ACT, v.obs, v.masks, v.actions, v.logp, v.rewards, v.terms, J.cObs.p, J.cMasks.p,
+                    J.cActs.p, J.cLogp.p, J.cRews.p, J.cTerms.p, s_);
+    ppo_->InferCritic(J.cObs.p, M, J.cVals.p);  // InferCriticBatched (Learner.cpp:936)
+    if (ntr > 0) ppo_->InferCritic(J.truncObs.p, ntr, J.truncVals.p);  // nextTruncStates (:939-941)
+    const float std_ = (float)returnStat.GetSTD();
+    hipCheck(hipMemsetAsync(clipSums_, 0, 2 * sizeof(float), s_), "clip sums");
+    RlgpuCheck(rlgpu_gae_segments(J.cRews.p, J.cTerms.p, J.cVals.p, ntr > 0 ? J.truncVals.p : nullptr, J.roff.p, J.rlen.p,
+                                  J.rtidx.p, K, cfg_.gamma, cfg_.gae_lambda, std_, cfg_.reward_clip_range, J.cAdv.p,
+                                  J.cTarget.p, J.cRet.p, clipSums_, s_),
+               "GAE");
+    // return-std samples: torch::randint over every combined return (Learner.cpp:959-967)
+    const int k = cfg_.return_samples;
+    if (k <= 0) return;
+    const int32_t m = (int32_t)std::min<int64_t>(k, M);
+    std::vector<int64_t> idx((size_t)std::max(m, 1));
+    if (m > 0) RlgpuCheck(rlgpu_sample_indices(cfg_.seed, cfg_.rank, stats.iteration, M, m, idx.data()), "return samples");
+    FeedReturnStat(J.cRet.p, idx, m);
 }
 
 rlgpu_learner_report Learner::Iterate() {
@@ -481,15 +667,16 @@ rlgpu_learner_report Learner::Iterate() {
     r.collect_s = secs(t0, t1);
     r.consume_s = secs(t1, t2);
     r.learn_s = secs(t2, t3);
-    r.env_steps = (int64_t)exp_.T * cfg_.num_arenas;
+    r.env_steps = (int64_t)(trajMode() ? traj.steps : exp_.T) * cfg_.num_arenas;
     if (envTiming_ && !ev_.empty()) {
         double ms = 0;
-        for (int t = 0; t < exp_.T; t++) {
+        const int nt = trajMode() ? 0 : exp_.T;  // the trajectory mode records no per-step events
+        for (int t = 0; t < nt; t++) {
             float x = 0;
             hipCheck(hipEventElapsedTime(&x, ev_[2 * t], ev_[2 * t + 1]), "elapsed");
             ms += x;
         }
-        r.env_kernel_ms = ms / exp_.T;
+        r.env_kernel_ms = nt ? ms / nt : 0.0;
     }
     return r;
 }
@@ -576,6 +763,41 @@ extern "C" int rlgpu_learner_rollout(rlgpu_learner* h, rlgpu_rollout_view* out) 
         *out = h->L->exp().v;
     });
 }
+extern "C" int rlgpu_learner_batch(rlgpu_learner* h, rlgpu_batch_view* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        RLGPU_REQUIRE(out, "null output");
+        RLGPU_REQUIRE(h->L->config().experience_mode == RLGPU_EXP_TRAJECTORIES,
+                      "rlgpu_learner_batch: the learner runs the rollout experience mode");
+        const GGL::TrajectoryStore& J = h->L->traj;
+        rlgpu_batch_view& b = *out;
+        b.obs = J.cObs.p;
+        b.masks = J.cMasks.p;
+        b.actions = J.cActs.p;
+        b.logp = J.cLogp.p;
+        b.rewards = J.cRews.p;
+        b.terms = J.cTerms.p;
+        b.values = J.cVals.p;
+        b.adv = J.cAdv.p;
+        b.target = J.cTarget.p;
+        b.ret = J.cRet.p;
+        b.num_rows = J.nrows;
+        b.trunc_obs = J.truncObs.p;
+        b.trunc_vals = J.truncVals.p;
+        b.num_truncs = J.ntrunc;
+        b.seg_player = J.rp.p;
+        b.seg_start = J.rstart.p;
+        b.seg_len = J.rlen.p;
+        b.seg_code = J.rcode.p;
+        b.seg_tidx = J.rtidx.p;
+        b.seg_off = J.roff.p;
+        b.num_segments = J.nrec;
+        b.store_rows = J.Tmax;
+        b.steps = J.steps;
+        b.first_step = J.firstStep;
+    });
+}
+
 extern "C" int rlgpu_learner_iterate(rlgpu_learner* h, rlgpu_learner_report* rep) {
     return rlgpu::guarded([&] {
         RLGPU_LEARNER(h);

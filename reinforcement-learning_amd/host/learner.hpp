@@ -79,12 +79,47 @@ std::vector<std::pair<int64_t, int64_t>> BatchRanges(int64_t expSize, int64_t ba
 
 // The rollout ([T, P] time-major) in HBM; every collected step is trained in the iteration that
 // collected it (the unfinished tail bootstrapped from V(obs_T), DESIGN.md Deviations 5).
+// In RLGPU_EXP_TRAJECTORIES the same arrays are a circular per-player step store of T rows (obs row r
+// = the state the step at row r acted on) and the outputs (values, GAE, truncation rows) live in the
+// combined batch instead (rollout_outputs = false).
 struct ExperienceBuffer {
     int T = 0, P = 0, W = 0;  // W: obs row width (RLGPU_OBS x frames)
     rlgpu_rollout_view v{};
     std::vector<void*> allocs;
-    void Allocate(int T, int P, int W);
+    void Allocate(int T, int P, int W, bool rollout_outputs = true);
     void Free();
+};
+
+// Device arrays that grow on demand (kept across iterations).
+template <class T>
+struct DevArray {
+    T* p = nullptr;
+    int64_t cap = 0;
+    void Reserve(int64_t n, hipStream_t s, bool keep = false);
+    void Free();
+};
+
+// RLGPU_EXP_TRAJECTORIES state: per-player trajectories, this iteration's records, truncation list and
+// the combined batch (the reference's combinedTraj)
+struct TrajectoryStore {
+    int Tmax = 0, maxLen = 0;
+    int64_t tsPerItr = 0;
+    int64_t step = 0;           // global step counter (store row = step % Tmax)
+    int64_t firstStep = 0;      // this iteration's first step
+    int steps = 0;              // steps collected this iteration
+    int lastOldTeam = -1;
+    int32_t *start = nullptr, *len = nullptr, *trnew = nullptr;
+    int64_t* counters = nullptr;      // device lk::kTcCount
+    int64_t* hcounters = nullptr;     // pinned host copy
+    DevArray<int32_t> rp, rstart, rlen, rcode, rtidx;
+    DevArray<int64_t> roff;
+    DevArray<float> truncObs, truncVals;
+    DevArray<float> cObs, cLogp, cRews, cVals, cAdv, cTarget, cRet;
+    DevArray<uint8_t> cMasks;
+    DevArray<int32_t> cActs;
+    DevArray<int8_t> cTerms;
+    float* truncStage = nullptr;  // [P][W] stacked pre-reset rows (frame stacking)
+    int64_t nrec = 0, ntrunc = 0, nrows = 0;
 };
 
 // PPOLearner (PPOLearner.h:41-59) over rlgpu_ppo.
@@ -148,6 +183,10 @@ public:
 private:
     void AllReduceGrads();
     void BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int64_t n);
+    void CollectTrajectories();
+    void ConsumeTrajectories();
+    void FeedReturnStat(const float* d_ret, const std::vector<int64_t>& idx, int32_t m);
+    bool trajMode() const { return cfg_.experience_mode == RLGPU_EXP_TRAJECTORIES; }
     hipStream_t s_;
     rlgpu_learner_config cfg_;
     rlgpu_collective coll_{};
@@ -178,6 +217,10 @@ private:
     int32_t* ends_ = nullptr;          // [P] last trajectory end per column (return sampling)
     std::vector<int32_t> hostEnds_;
     double* mom_ = nullptr;   // [3] + scratch
+    float* clipSums_ = nullptr;  // [2] GAE clip-portion partial sums
+  public:
+    TrajectoryStore traj;      // RLGPU_EXP_TRAJECTORIES
+  private:
     std::vector<void*> allocs_;
     template <class T>
     T* Alloc(size_t count);

@@ -107,6 +107,49 @@ class TorchCollective:
         return self._c
 
 
+class RcclCollective:
+    """The rlgpu_collective over a native RCCL communicator (include/rlgpu_learner.h rlgpu_rccl_*,
+    host/rccl_collective.cpp): the C++ Learner's exchanges run in C++ on RCCL, no Python callback in
+    the loop.  Rank 0's unique id reaches the other ranks through `group` (torch.distributed, any
+    backend) -- or pass `unique_id` bytes from another channel."""
+
+    def __init__(self, rank, world, stream=None, group=None, unique_id=None):
+        from . import _lib
+        L = _lib.lib()
+        L.rlgpu_rccl_unique_id.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.rlgpu_rccl_collective_create.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                                   ctypes.POINTER(CCollective)]
+        L.rlgpu_rccl_collective_destroy.argtypes = [ctypes.POINTER(CCollective)]
+        uid = np.zeros(128, np.uint8)
+        if unique_id is not None:
+            uid[:] = np.frombuffer(bytes(unique_id), np.uint8)
+        else:
+            if rank == 0:
+                _lib.check(L.rlgpu_rccl_unique_id(uid.ctypes.data, 128), "rlgpu_rccl_unique_id")
+            if world > 1:
+                t = torch.from_numpy(uid.astype(np.int64))
+                broadcast_(t, group)
+                uid[:] = t.numpy().astype(np.uint8)
+        self.unique_id = uid.tobytes()
+        self._c = CCollective()
+        _lib.check(L.rlgpu_rccl_collective_create(uid.ctypes.data, rank, world, _lib.stream_ptr(stream),
+                                                  ctypes.byref(self._c)), "rlgpu_rccl_collective_create")
+
+    def c_struct(self):
+        return self._c
+
+    def close(self):
+        if getattr(self, "_c", None) is not None and self._c.user:
+            from . import _lib
+            _lib.check(_lib.lib().rlgpu_rccl_collective_destroy(ctypes.byref(self._c)), "rlgpu_rccl_collective_destroy")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def moments_mean_std(m3):
     """rlgpu_moments_mean_std: (mean, unbiased std) float32 from fp64 (sum, sum sq, count)."""
     from . import _lib

@@ -175,6 +175,10 @@ class LearnerConfig:
         self.policy_layers = (512, 512)
         self.critic_layers = (512, 512)
         self.shared_layers = ()            # PPOLearnerConfig::sharedHead ((384, 384) in the reference's run log)
+        self.experience_mode = 0           # 0: fixed [T, P] rollout; 1: the reference's complete trajectories
+                                           # with carry-over (rlgpu_learner_config.experience_mode)
+        self.ts_per_itr = 0                # mode 1: PPOLearnerConfig::tsPerItr (0 = rollout_len * players)
+        self.experience_capacity = 0       # mode 1: per-player step store rows (0 = automatic)
         self.rewards = None                # EnvCreateFn reward list (rlgpu.plugins.reward specs); None = ExampleMain's
         self.terminals = None              # terminal conditions (rlgpu.plugins.terminal specs); None = ExampleMain's
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
@@ -214,7 +218,20 @@ class _CConfig(ctypes.Structure):
                 ("mesh_object_ntris", ctypes.c_void_p),
                 ("shared_layers", ctypes.c_int32 * MAX_LAYERS), ("n_shared_layers", ctypes.c_int32),
                 ("rewards", ctypes.c_void_p), ("n_rewards", ctypes.c_int32),
-                ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32)]
+                ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32),
+                ("experience_mode", ctypes.c_int32), ("ts_per_itr", ctypes.c_int64),
+                ("experience_capacity", ctypes.c_int32)]
+
+
+class _CBatch(ctypes.Structure):
+    """rlgpu_batch_view (include/rlgpu_learner.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("obs", "masks", "actions", "logp", "rewards", "terms", "values", "adv",
+                                               "target", "ret")] + \
+               [("num_rows", ctypes.c_int64), ("trunc_obs", ctypes.c_void_p), ("trunc_vals", ctypes.c_void_p),
+                ("num_truncs", ctypes.c_int64)] + \
+               [(n, ctypes.c_void_p) for n in ("seg_player", "seg_start", "seg_len", "seg_code", "seg_tidx", "seg_off")] + \
+               [("num_segments", ctypes.c_int64), ("store_rows", ctypes.c_int32), ("steps", ctypes.c_int32),
+                ("first_step", ctypes.c_int64)]
 
 
 class _CRollout(ctypes.Structure):
@@ -241,6 +258,7 @@ def _bind():
     L.rlgpu_learner_destroy.argtypes = [vp]
     L.rlgpu_learner_handles.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
     L.rlgpu_learner_rollout.argtypes = [vp, ctypes.POINTER(_CRollout)]
+    L.rlgpu_learner_batch.argtypes = [vp, ctypes.POINTER(_CBatch)]
     L.rlgpu_learner_iterate.argtypes = [vp, ctypes.POINTER(_CReport)]
     for f in ("collect", "consume", "learn", "finish_iteration"):
         getattr(L, "rlgpu_learner_" + f).argtypes = [vp]
@@ -278,7 +296,10 @@ class _ReturnStat:
 class Learner:
     """GGL::Learner for one rank (the C++ host Learner) with torch views of its HBM rollout."""
 
-    def __init__(self, cfg, device="cuda:0", rank=0, world=1, group=None):
+    def __init__(self, cfg, device="cuda:0", rank=0, world=1, group=None, native_rccl=False):
+        """world > 1: the C++ Learner's exchanges go through rlgpu.dist.TorchCollective (torch.distributed,
+        RCCL for the nccl backend), or with native_rccl through its own RCCL communicator
+        (rlgpu.dist.RcclCollective: no Python in the exchange path)."""
         import torch
         from .env import EnvSet
         from .ppo import PPO
@@ -316,12 +337,17 @@ class Learner:
             c.terminals, c.n_terminals = self._tc.ctypes.data, tc.size
         c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
         c.frame_stack = cfg.frame_stack
+        c.experience_mode, c.ts_per_itr, c.experience_capacity = cfg.experience_mode, cfg.ts_per_itr, cfg.experience_capacity
         c.rank, c.world = rank, world
         self._coll = None
         coll = None
         if world > 1:
-            from .dist import TorchCollective
-            self._coll = TorchCollective(group, self.device)
+            if native_rccl:
+                from .dist import RcclCollective
+                self._coll = RcclCollective(rank, world, group=group)
+            else:
+                from .dist import TorchCollective
+                self._coll = TorchCollective(group, self.device)
             coll = ctypes.byref(self._coll.c_struct())
         h = ctypes.c_void_p()
         _lib.check(L.rlgpu_learner_create(ctypes.byref(c), coll, _lib.stream_ptr(), ctypes.byref(h)),
@@ -330,7 +356,8 @@ class Learner:
         eh, ph = ctypes.c_void_p(), ctypes.c_void_p()
         _lib.check(L.rlgpu_learner_handles(h, ctypes.byref(eh), ctypes.byref(ph)), "rlgpu_learner_handles")
         self.env = EnvSet.wrap(eh.value, self.device, cfg.tick_skip, cfg.action_delay, owner=self)
-        max_rows = max(min(cfg.mini_batch_size, cfg.rollout_len * 4 * cfg.num_arenas), min(4 * cfg.num_arenas, 65536))
+        rows_cap = cfg.mini_batch_size if cfg.experience_mode == 1 else cfg.rollout_len * 4 * cfg.num_arenas
+        max_rows = max(min(cfg.mini_batch_size, rows_cap), min(4 * cfg.num_arenas, 65536))  # host/learner.cpp
         self.ppo = PPO.wrap(ph.value, self.device, cfg.policy_layers, cfg.critic_layers, max_rows,
                             obs_size=OBS * max(1, cfg.frame_stack), metrics_source=self._metrics, owner=self,
                             shared_layers=cfg.shared_layers)
@@ -457,6 +484,33 @@ class Learner:
 
     def learn(self):
         _lib.check(_lib.lib().rlgpu_learner_learn(self._h), "rlgpu_learner_learn")
+
+    def batch(self):
+        """The trained batch of experience_mode 1 (after consume): combined complete trajectories,
+        their values / GAE outputs, the truncation list and the trajectory records, as torch views."""
+        import torch
+        b = _CBatch()
+        _lib.check(_lib.lib().rlgpu_learner_batch(self._h, ctypes.byref(b)), "rlgpu_learner_batch")
+        d, M, K, nt, W = self.device, max(b.num_rows, 1), max(b.num_segments, 1), max(b.num_truncs, 1), self.W
+
+        def a(ptr, shape, dtype, dev):  # arrays are allocated at the first consume
+            return _lib.alias(ptr, shape, dtype, dev) if ptr else torch.empty((0,) + tuple(shape[1:]), dtype=dtype, device=dev)
+        f32, i32 = torch.float32, torch.int32
+        out = {"obs": a(b.obs, (M, W), f32, d), "masks": a(b.masks, (M, ACTIONS), torch.uint8, d),
+               "actions": a(b.actions, (M,), i32, d), "logp": a(b.logp, (M,), f32, d),
+               "rewards": a(b.rewards, (M,), f32, d), "terms": a(b.terms, (M,), torch.int8, d),
+               "values": a(b.values, (M,), f32, d), "adv": a(b.adv, (M,), f32, d), "target": a(b.target, (M,), f32, d),
+               "ret": a(b.ret, (M,), f32, d), "trunc_obs": a(b.trunc_obs, (nt, W), f32, d),
+               "trunc_vals": a(b.trunc_vals, (nt,), f32, d)}
+        for k in ("seg_player", "seg_start", "seg_len", "seg_code", "seg_tidx"):
+            out[k] = a(getattr(b, k), (K,), i32, d)[:b.num_segments]
+        out["seg_off"] = a(b.seg_off, (K,), torch.int64, d)[:b.num_segments]
+        for k in ("obs", "masks", "actions", "logp", "rewards", "terms", "values", "adv", "target", "ret"):
+            out[k] = out[k][:b.num_rows]
+        out["trunc_obs"], out["trunc_vals"] = out["trunc_obs"][:b.num_truncs], out["trunc_vals"][:b.num_truncs]
+        out.update(num_rows=b.num_rows, num_truncs=b.num_truncs, num_segments=b.num_segments, store_rows=b.store_rows,
+                   steps=b.steps, first_step=b.first_step)
+        return out
 
     def finish_iteration(self):
         _lib.check(_lib.lib().rlgpu_learner_finish_iteration(self._h), "rlgpu_learner_finish_iteration")

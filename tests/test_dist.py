@@ -278,3 +278,32 @@ def test_versions_broadcast_without_checkpoint():
     res = _run_sync("versions")
     assert res[1][7] == res[0][7] == [(100, [1.0] * 4), (200, [2.0] * 4)]
     assert res[1][6] == (0, 0, 0, 0.0, 0.0) and not res[1][5]
+
+
+@pytest.mark.gpu
+def test_native_rccl_collective_single_rank():
+    """rlgpu_rccl_* (host/rccl_collective.cpp): a one-rank RCCL communicator on the learner's stream;
+    the three callbacks the C++ Learner calls -- device f32 all-reduce, host f64 all-reduce, host f32
+    all-gather -- return their inputs (sum / gather over one rank).  Two ranks cannot share one GPU
+    under RCCL ("Duplicate GPU detected"), so the multi-rank path runs on the driver's 8-GPU node."""
+    import ctypes
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reinforcement-learning_amd"))
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rlgpu.dist import RcclCollective
+    c = RcclCollective(0, 1)
+    s = c.c_struct()
+    x = torch.arange(1000, dtype=torch.float32, device="cuda:0")
+    assert s.allreduce_sum_f32(s.user, x.data_ptr(), x.numel()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32))
+    m = np.array([1.5, -2.25, 3.0])
+    assert s.allreduce_sum_f64(s.user, m.ctypes.data, 3) == 0
+    np.testing.assert_array_equal(m, [1.5, -2.25, 3.0])
+    a = np.float32([1, 2, 3, 4])
+    out = np.zeros(4, np.float32)
+    assert s.allgather_f32(s.user, a.ctypes.data, 4, out.ctypes.data) == 0
+    np.testing.assert_array_equal(out, a)
+    c.close()
+    assert not c.c_struct().user
