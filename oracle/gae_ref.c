@@ -50,18 +50,33 @@ int oracle_gae_flat(const float* rews, const int8_t* terms, const float* vals, c
         }
         if (t == TERM_TRUNCATED) trunc_seen++;
     }
-    /* :104-167 normalisation + clip; sums accumulated in float as the reference does
-       (the reference unrolls by 8; this sequential sum differs only in rounding). */
+    /* :104-167 normalisation + clip; the clip-portion sums in float in the reference's order: groups
+       of 8 summed left to right, each group added to the running total (:113-141), then the
+       remainder one by one (:153-162). */
     float tot = 0.0f, tot_clip = 0.0f;
-    for (int64_t i = 0; i < num_returns; i++) {
-        float n = rews[i];
-        if (should_normalize) {
-            n = rews[i] * inv_std;
+    if (should_normalize) {
+        const int64_t unroll_end = num_returns - (num_returns % 8);
+        int64_t i = 0;
+        for (; i < unroll_end; i += 8) {
+            float n[8];
+            for (int k = 0; k < 8; k++) n[k] = rews[i + k] * inv_std;
+            tot += fabsf(n[0]) + fabsf(n[1]) + fabsf(n[2]) + fabsf(n[3]) + fabsf(n[4]) + fabsf(n[5]) + fabsf(n[6]) +
+                   fabsf(n[7]);
+            if (should_clip)
+                for (int k = 0; k < 8; k++) n[k] = fminf(fmaxf(n[k], -clip_range), clip_range);
+            tot_clip += fabsf(n[0]) + fabsf(n[1]) + fabsf(n[2]) + fabsf(n[3]) + fabsf(n[4]) + fabsf(n[5]) + fabsf(n[6]) +
+                        fabsf(n[7]);
+            for (int k = 0; k < 8; k++) nrew[i + k] = n[k];
+        }
+        for (; i < num_returns; i++) {
+            float n = rews[i] * inv_std;
             tot += fabsf(n);
             if (should_clip) n = fminf(fmaxf(n, -clip_range), clip_range);
             tot_clip += fabsf(n);
+            nrew[i] = n;
         }
-        nrew[i] = n;
+    } else {
+        for (int64_t i = 0; i < num_returns; i++) nrew[i] = rews[i];
     }
     /* :169-193 backward recursion */
     float prev_lambda = 0.0f, prev_ret = 0.0f;

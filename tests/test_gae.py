@@ -176,3 +176,35 @@ def test_c1_cpu_loop_runs():
     r = run_c1(seconds=0.01, arenas=4, rollout=4, threads=2)
     assert r["iterations"] >= 1 and r["agent_steps"] == 4 * 4 * 4 * r["iterations"]
     assert r["ppo_s_per_1M_agent_steps"] > 0
+
+
+def test_clip_portion_follows_the_reference_unroll():
+    """GAE.cpp:113-162: |r/std| summed in groups of 8 (left to right, each group then added to the
+    running float total), the remainder one by one -- restated exactly, so the clipped-reward portion
+    carries the reference's rounding (values chosen so a plain sequential sum rounds differently)."""
+    r = np.float32([2e8, 0, 0, 0, 0, 0, 0, 0] + [6] * 8 + [7, 5, 2])
+    std, clip = 2.0, 1e7
+    m = r.size
+    _, _, _, cp, st = oracle.gae_flat(r, np.zeros(m, np.int8), np.zeros(m, np.float32), None, 0.99, 0.95, std, clip)
+    n = r * np.float32(1 / std)
+    c = np.clip(n, -clip, clip)
+
+    def ref_sum(x):
+        tot = np.float32(0)
+        for g in range(0, 16, 8):
+            s = np.float32(0) + x[g]
+            for k in range(1, 8):
+                s = np.float32(s + x[g + k])
+            tot = np.float32(tot + s)
+        for v in x[16:]:
+            tot = np.float32(tot + v)
+        return tot
+
+    def seq_sum(x):
+        tot = np.float32(0)
+        for v in x:
+            tot = np.float32(tot + v)
+        return tot
+    tot, totc = ref_sum(np.abs(n)), ref_sum(np.abs(c))
+    assert st == 0 and np.float32(cp) == np.float32((tot - totc) / max(tot, np.float32(1e-7)))
+    assert ref_sum(np.abs(n)) != seq_sum(np.abs(n))  # the order is observable on this input
