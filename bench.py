@@ -24,6 +24,8 @@ sys.path.insert(0, os.path.join(ROOT, "reinforcement-learning_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
+MFMA_F16_TFS = 2500.0   # dense fp16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
+H3_TFS = MFMA_F16_TFS / 3  # fp32 GEMM ceiling of the H3 split: three fp16 MFMAs per fp32 product
 ARENAS_PER_GPU = 4096   # BASELINE configs[1] (C2)
 
 
@@ -37,18 +39,31 @@ def env_bytes_per_step(arena_state_size, append=True):
     return b
 
 
-def pmc_traffic(kernel_ms, arenas):
+def pmc_traffic(kernel_ms, arenas, mesh_name):
     """HBM traffic of the env kernel from the committed rocprofv3 PMC passes (profiles/*_env_pmc.json,
     made by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE runs of this bench at its
     default ARENAS_PER_GPU arenas), as GB/s over the average launch duration measured here; None when
-    no summary is present or this run steps another arena count (the bytes were counted for that one)."""
+    no summary is present or this run steps another arena count or mesh (the bytes were counted for that one)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_pmc.json")))
     if not files or arenas != ARENAS_PER_GPU:
         return None, None
+    files = [f for f in files if json.load(open(f)).get("mesh", "synthetic") == mesh_name]
+    if not files:
+        return None, None
     d = json.load(open(files[-1]))
     b = d["hbm_bytes_per_launch"]
     return b / (kernel_ms * 1e-3) / 1e9, {"bytes_per_launch": b, "source": os.path.relpath(files[-1], ROOT)}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(seconds=12.0, arenas=256):
@@ -70,8 +85,23 @@ def cpu_baseline(seconds=12.0, arenas=256):
         if el >= seconds:
             break
     out = {"value": arenas * steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+           "cpu_model": cpu_model(),
            "sample": f"env only: {arenas} arenas x {steps} env steps of the oracle/ CPU restatement "
-                     f"({cores} threads, uniform valid actions)"}
+                     f"({cores} threads, uniform valid actions, synthetic 36-triangle arena: the oracle scans every "
+                     f"triangle, so the SOCCAR-sized mesh would measure its brute force, not the reference's BVH)"}
+    # one thread, one 2v2 arena: physics ticks/s beside RocketSim's published 114,481 ticks/s
+    # (v2.1.0, i5-11400); the oracle runs tickSkip 8 ticks per env step plus the builders
+    one = oracle.EnvSet(1, seed=99, threads=1)
+    steps1 = 0
+    t1 = time.perf_counter()
+    while time.perf_counter() - t1 < 4.0:
+        m1 = one.masks.astype(bool)
+        one.step(np.argmax(rng.random(m1.shape) * m1, axis=1).astype(np.int32), True)
+        steps1 += 1
+    el1 = time.perf_counter() - t1
+    out["one_thread"] = {"ticks_per_s": 8 * steps1 / el1, "env_steps_per_s": steps1 / el1,
+                         "reference_published_ticks_per_s": 114481,
+                         "sample": f"1 arena x {steps1} env steps (8 ticks + obs / reward builders each), 1 thread"}
     # BASELINE config C1 on CPU (PPO wall-clock per 1M agent-steps with the C1 model):
     # 64 arenas, actor / critic [256, 256], oracle env + torch CPU fp32 MLP / PPO, bounded sample
     from oracle.ppo_cpu import run_c1
@@ -83,6 +113,32 @@ def cpu_baseline(seconds=12.0, arenas=256):
     return out
 
 
+def learn_roofline(L, train_gemm):
+    """Per kernel class of the learn phase: achieved TF/s (fp32-equivalent flops 2*I*J*K of the GEMMs)
+    against the H3 ceiling, or GB/s (algorithmic bytes of the LayerNorm kernels) against HBM, from
+    one iteration timed per launch."""
+    import torch
+    from rlgpu.ppo import kernel_timing, kernel_timing_read
+    kernel_timing(True)
+    L.iterate()
+    torch.cuda.synchronize()
+    t = kernel_timing_read()
+    kernel_timing(False)
+    peak = H3_TFS if train_gemm == "h3" else (MFMA_F16_TFS / 6 if train_gemm == "x6" else MFMA_F16_TFS / 16)
+    out = {"method": "HIP events around each launch on its own stream, one untimed PPO iteration after the timed ones",
+           "gemm_peak_note": f"{train_gemm}: fp32-equivalent ceiling {peak:.0f} TF/s of the {MFMA_F16_TFS:.0f} TF/s dense 16-bit MFMA peak"}
+    for name, (ms, work, n) in t.items():
+        if n == 0:
+            continue
+        gemm = "GEMM" in name
+        ach = work / (ms * 1e-3) / (1e12 if gemm else 1e9)
+        p = peak if gemm else HBM_PEAK_GBS
+        out[name] = {"bound": "mfma" if gemm else "hbm", "achieved": ach, "peak": p, "unit": "TF/s" if gemm else "GB/s",
+                     "frac": ach / p, "launches": n, "ms_total": ms, "avg_us": ms * 1e3 / n,
+                     ("flops_total" if gemm else "bytes_total"): work}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -91,6 +147,9 @@ def main():
     ap.add_argument("--arenas", type=int, default=ARENAS_PER_GPU)
     ap.add_argument("--rollout", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mesh", choices=("procedural", "synthetic"), default="procedural",
+                    help="arena collision mesh: the SOCCAR-sized procedural stand-in (16 objects, 8,800 triangles: "
+                         "rlgpu.mesh.procedural_soccar) or the 36-triangle synthetic arena")
     ap.add_argument("--train-gemm", choices=("h3", "x6", "f32"), default="h3",
                     help="fp32 training GEMM arithmetic (include/rlgpu_ppo.h rlgpu_gemm modes)")
     args = ap.parse_args()
@@ -120,8 +179,10 @@ def main():
     # the same work; the mixed-policy path is covered by tests/test_learner_gpu.py
     from rlgpu.ppo import GEMM_F16X3, GEMM_F32, GEMM_F32X6
     train_gemm = {"h3": GEMM_F16X3, "x6": GEMM_F32X6, "f32": GEMM_F32}[args.train_gemm]
+    from rlgpu.mesh import procedural_soccar
+    mesh = procedural_soccar() if args.mesh == "procedural" else None
     cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False,
-                        train_gemm=train_gemm)
+                        train_gemm=train_gemm, mesh=mesh)
     L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
     L.set_env_timing(True)  # HIP events around every fused env step, on the learner's stream
 
@@ -155,7 +216,7 @@ def main():
     kern_ms = sum(kern) / len(kern)
     b_env = env_bytes_per_step(arena_state_size())
     achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kern_ms, args.arenas)
+    traffic, traffic_src = pmc_traffic(kern_ms, args.arenas, args.mesh)
     out = {
         "metric": "env-steps/sec (whole node) at 32768 arenas; PPO wall-clock per 1M steps",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -168,7 +229,10 @@ def main():
                                "LayerNorm+LeakyReLU, bf16 inference / fp32 training, T=128, 2 epochs, minibatch 50k",
                    "arenas_per_gpu": args.arenas, "agents_per_gpu": 4 * args.arenas, "rollout_len": cfg.rollout_len,
                    "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32",
-                   "train_gemm": args.train_gemm},
+                   "train_gemm": args.train_gemm,
+                   "mesh": (f"procedural SOCCAR stand-in: {mesh.num_objects} objects, {mesh.num_tris} triangles "
+                            "(quarter pipes, rounded corners, goal boxes; floor / walls / ceiling are static planes)"
+                            if mesh is not None else "synthetic arena: 1 object, 36 triangles (include/rlgpu_arena_mesh.h)")},
         "agent_steps_per_s": agent_steps / el,
         "ppo_s_per_1M_agent_steps": el / agent_steps * 1e6,
         "phase_s_per_iteration": {k: v / args.steps for k, v in phase.items()},
@@ -180,6 +244,9 @@ def main():
                      "units_per_launch": args.arenas,
                      "algorithmic_bytes_per_launch": b_env * args.arenas},
     }
+    # learn-phase roofline: one more (untimed) iteration with HIP events around every training GEMM
+    # and LayerNorm launch, on the stream each runs on (rlgpu_kernel_timing)
+    out["learn_roofline"] = learn_roofline(L, args.train_gemm)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

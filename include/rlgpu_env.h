@@ -279,8 +279,9 @@ int rlgpu_envset_build_obs(rlgpu_envset* env, void* stream);
  * the shader cycles thread 0 of each workgroup spends per phase (0-10 tick phases, 11 load/halves
  * prelude, 12 builders, 13 obs rows, 14 resets, 15 store, 16-22 solver sub-phases) to
  * d_counters[phase] (all workgroups) and to d_counters[64 + 24 * workgroup + phase].  NULL disables
- * (the default). */
-int rlgpu_envset_set_profile(rlgpu_envset* env, unsigned long long* d_counters);
+ * (the default).  capacity: entries of d_counters (>= 64 + 24 * workgroups, else
+ * RLGPU_ERR_INVALID_ARG). */
+int rlgpu_envset_set_profile(rlgpu_envset* env, unsigned long long* d_counters, int64_t capacity);
 
 /* ExampleMain's StepCallback metrics on the device.  Replaces the StepCallbackFn that
  * Learner::Start calls after every StepSecondHalf (GL/public/GigaLearnCPP/Learner.h:11,

@@ -108,8 +108,16 @@ int rlgpu_ppo_init_params(rlgpu_ppo* h, uint64_t seed, void* stream);
 int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream);
 
 /* Diagnostics: while d_buf != NULL, every fused inference launch writes 16 wall-clock (100 MHz)
- * phase marks per 64-row workgroup into d_buf (uint64 [workgroups * 16]; tools/infer_trace.py). */
-int rlgpu_debug_infer_trace(void* d_buf);
+ * phase marks per 64-row workgroup into d_buf (uint64 [workgroups * 16] within `capacity` entries;
+ * a launch needing more fails with RLGPU_ERR_INVALID_ARG; tools/infer_trace.py). */
+int rlgpu_debug_infer_trace(void* d_buf, int64_t capacity);
+/* Diagnostics: learn-phase kernel timing.  While enabled, HIP events bracket every training GEMM
+ * and LayerNorm launch on the stream it is launched on; rlgpu_kernel_timing_read sums, per slot
+ * (0 forward / input-gradient GEMMs, 1 weight-gradient GEMMs, 2 LayerNorm forward, 3 LayerNorm
+ * backward), the milliseconds, the work (flops for GEMMs, algorithmic bytes for the row kernels)
+ * and the launch count since the last rlgpu_kernel_timing call (it waits for the events). */
+int rlgpu_kernel_timing(int32_t enable);
+int rlgpu_kernel_timing_read(double* ms, double* work, int64_t* count, int32_t nslots);
 
 /* Plain forward of one model on n rows (n <= max_rows): precision 0 = fp32 (training path,
  * no activations kept), 1 = bf16 inference path.  d_out [n, out_size] fp32.  With a shared head,

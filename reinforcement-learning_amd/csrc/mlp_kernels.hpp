@@ -1019,6 +1019,168 @@ __global__ void __launch_bounds__(256, 2) gemm_h3w(GemmArgs g) {
     }
 }
 
+// ---- H3 GEMM on an LDS-DMA ring (gemm_h3r): C = A . B^T + bias with A_IK fp32 (k contiguous) and
+// B the pre-split fp16 planes -- the forward and input-gradient GEMMs of training.  128 x 128 tile,
+// 4 waves of 64 x 64, one workgroup per CU.  Both operands travel global -> LDS by
+// global_load_lds_dwordx4 (no VGPR round trip, no staging VALU) into a ring of NS stages of RK k;
+// the ring keeps NS - 1 stages in flight across the raw barriers (counted vmcnt, never 0 inside the
+// loop), so the loads of a stage have NS - 1 stages of MFMAs to land instead of one.  A stays fp32
+// in LDS and each wave splits its own fragments after ds_read (split2h, the same scaled fp16 pair
+// as the staged kernels), so the products, their order (per 16-deep k step: l.h, h.l, h.h into the
+// one accumulator) and the epilogue are gemm_x6's H3 path: the results are bit-identical.
+// LDS images are lane-linear per DMA instruction; bank conflicts are removed by an XOR swizzle of
+// the 16-byte slot within a row (rswz), applied on the DMA's global source address and on the read.
+template <int RK>
+struct RingGeom {
+    static constexpr int AROW = RK * 4, BROW = RK * 2;                      // bytes per LDS row
+    static constexpr int ABYTES = BM * AROW, BPLANE = BN * BROW;
+    static constexpr int STAGE = ABYTES + 2 * BPLANE;
+    static constexpr int AINS = ABYTES / 1024 / 4, BINS = 2 * BPLANE / 1024 / 4;  // DMAs per wave and stage
+    static constexpr int ARPI = 1024 / AROW, BRPI = 1024 / BROW;           // rows per DMA
+};
+// physical 16-byte slot of logical slot s in row r of an LDS image with ROWB-byte rows (<= 256):
+// the rows sharing one 256-byte bank row, and the 16 lanes of a ds_read_b128 group (rows {0-3,
+// 12-15, 20-27} + 32 u), land on 16 distinct slots
+template <int ROWB>
+DEV int rswz(int r, int s) {
+    constexpr int S = ROWB / 16, Q = 256 / ROWB;
+    return s ^ ((r / Q) & (S - 1));
+}
+DEV void glds16(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+template <int RK, int NS>
+__global__ void __launch_bounds__(256, NS * RingGeom<RK>::STAGE <= 80 * 1024 ? 2 : 1) gemm_h3r(GemmArgs g) {
+    using G = RingGeom<RK>;
+    static_assert(NS * G::STAGE <= 160 * 1024, "ring exceeds the CU's LDS");
+    constexpr int NV = (G::AINS + G::BINS) * (NS - 2);  // DMAs per wave allowed in flight at a stage's wait
+    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * G::STAGE];  // the kernel's only LDS object
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const Tile tl = xcd_tile(g.gx, g.gy, 1);
+    const int i0 = tl.y * BM, j0 = tl.x * BN;
+    const int K = g.K;
+    // operand scale first: its load retires before the first DMA is issued
+    const int pa = h3_pow(shard_max_bits(g.amax_a));
+    const float sa = pow2f(pa);
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+    const float* zero = reinterpret_cast<const float*>(g_zero_row);
+    // per-lane DMA sources, fixed for the whole K loop: row base + swizzled chunk (stage k0 added)
+    const float* asrc[G::AINS];
+    int akc[G::AINS];  // first k of the lane's chunk within a stage
+#pragma unroll
+    for (int q = 0; q < G::AINS; q++) {
+        const int r = (w * G::AINS + q) * G::ARPI + lane / (G::AROW / 16);
+        const int c = rswz<G::AROW>(r, lane % (G::AROW / 16));
+        akc[q] = 4 * c;
+        asrc[q] = (i0 + r < g.I) ? g.A + (int64_t)(i0 + r) * g.lda + 4 * c : nullptr;
+    }
+    const uint16_t* bsrc[G::BINS];
+#pragma unroll
+    for (int q = 0; q < G::BINS; q++) {
+        constexpr int PER_PLANE = G::BPLANE / 1024;
+        const int e = w * G::BINS + q, p = e / PER_PLANE;
+        const int r = (e % PER_PLANE) * G::BRPI + lane / (G::BROW / 16);
+        const int c = rswz<G::BROW>(r, lane % (G::BROW / 16));
+        bsrc[q] = Bp + p * g.bplane + (int64_t)(j0 + r) * g.ldb + 8 * c;
+    }
+    const int nst = (K + RK - 1) / RK;
+    // stage s into ring slot s % NS (a stage past the last reads the zero row: the in-flight count
+    // stays NS - 1 to the end, so every wait is the same constant)
+    auto issue = [&](int s) {
+        uint8_t* dst = ring + (s % NS) * G::STAGE;
+        const int k0 = s * RK;
+        const bool live = s < nst;
+#pragma unroll
+        for (int q = 0; q < G::AINS; q++) {
+            const bool ok = live && asrc[q] && (k0 + akc[q] < K);
+            glds16(ok ? asrc[q] + k0 : zero, dst + (w * G::AINS + q) * 1024);
+        }
+#pragma unroll
+        for (int q = 0; q < G::BINS; q++)
+            glds16(live ? (const void*)(bsrc[q] + k0) : (const void*)zero, dst + G::ABYTES + (w * G::BINS + q) * 1024);
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS - 1; s++) issue(s);
+    const int l32 = lane & 31, hk = lane >> 5;
+    for (int it = 0; it < nst; it++) {
+        // this wave's DMAs of stage it have landed (NS - 2 younger stages may still fly); the barrier
+        // extends that to every wave's, and retires every wave's reads of the slot refilled next
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NV) : "memory");
+        issue(it + NS - 1);
+        const uint8_t* As = ring + (it % NS) * G::STAGE;
+        const uint8_t* Bs = As + G::ABYTES;
+#pragma unroll
+        for (int ks = 0; ks < RK / 16; ks++) {
+            h16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int ra = wm * 64 + 32 * u + l32, sa0 = ks * 4 + 2 * hk;
+                f32x4_t v[2];
+                v[0] = *(const f32x4_t*)(As + ra * G::AROW + rswz<G::AROW>(ra, sa0) * 16);
+                v[1] = *(const f32x4_t*)(As + ra * G::AROW + rswz<G::AROW>(ra, sa0 + 1) * 16);
+                u32x4_t h, l;
+                split2h(v, sa, h, l);
+                ah[u] = __builtin_bit_cast(h16x8, h);
+                al[u] = __builtin_bit_cast(h16x8, l);
+                const int rb = wn * 64 + 32 * u + l32;
+                const int ob = rb * G::BROW + rswz<G::BROW>(rb, ks * 2 + hk) * 16;
+                bh[u] = *(const h16x8*)(Bs + ob);
+                bl[u] = *(const h16x8*)(Bs + G::BPLANE + ob);
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++) {
+                    f32x16 c = acc[ti][tj];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ti], bh[tj], c, 0, 0, 0);  // l h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ti], bl[tj], c, 0, 0, 0);  // h l
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ti], bh[tj], c, 0, 0, 0);  // h h
+                }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-row DMAs past the last stage
+    const int h = hk;
+    float csc[2];
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++) csc[tj] = g.bscale[j0 + wn * 64 + tj * 32 + l32];
+    if (i0 + BM <= g.I && j0 + BN <= g.J) {
+        float* cb = g.C + (int64_t)(i0 + wm * 64 + 4 * h) * g.ldc + j0 + wn * 64 + l32;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                const float bj = g.bias ? g.bias[j0 + wn * 64 + tj * 32 + l32] : 0.f;
+                float* ct = cb + (int64_t)(ti * 32) * g.ldc + tj * 32;
+#pragma unroll
+                for (int r = 0; r < 16; r++)
+                    ct[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = ldexpf(acc[ti][tj][r] * csc[tj], -pa) + bj;
+            }
+        return;
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+        for (int tj = 0; tj < 2; tj++) {
+            const int j = j0 + wn * 64 + tj * 32 + l32;
+            if (j >= g.J) continue;
+            const float bj = g.bias ? g.bias[j] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (i < g.I) g.C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * csc[tj], -pa) + bj;
+            }
+        }
+}
+
 // ---- bf16 inference GEMM: C[i,j] = bf16( sum_k A[i,k] W[j,k] + bias[j] ) on
 // v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  A [I][lda] and W [J][ldb] bf16, k contiguous,
 // 16-byte aligned rows, K a multiple of 8 with zero padding (the padded inference copy of the

@@ -94,6 +94,20 @@ inline bool h3_wide(int J) {
     }();
     return on && J > mlp::BN;
 }
+// Forward / input-gradient H3 GEMMs (A_IK x pre-split B) on the LDS-DMA ring kernel mlp::gemm_h3r when
+// RLGPU_H3_RING = 1 (32-deep stages, 4-stage ring), 2 (64-deep, 2 stages), 3 (32-deep, 3 stages) or 4
+// (32-deep, 2 stages, two workgroups per CU); 0 (default): the register-staged gemm_x6 path.  Same
+// bits either way.  Measured in the C2 learn phase (tools/learn_bench.py, 50k minibatch): 1.58 ms per
+// minibatch on gemm_x6, 1.81 (ring 1 / 2) and 1.63 (ring 4) -- one wave per SIMD cannot hide the
+// per-wave split of the fp32 A fragments, so the ring stays an experiment.
+inline int h3_ring() {
+    static const int v = [] {
+        const char* e = getenv("RLGPU_H3_RING");
+        const int x = e ? atoi(e) : 0;
+        return (x >= 0 && x <= 4) ? x : 0;
+    }();
+    return v;
+}
 inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
 inline bool split_mode_(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
 inline int gemm_slots(int mode) {
@@ -150,6 +164,57 @@ struct rlgpu_ppo {
 };
 
 namespace {
+
+// ---- learn-phase kernel timing (rlgpu_kernel_timing / rlgpu_kernel_timing_read): HIP events
+// around the training GEMM and LayerNorm launches, recorded on the stream each launch goes to (the
+// policy's and the critic's passes run on two streams).  Off unless enabled; bench.py reports the
+// learn phase's roofline from it.  Work per launch: flops (GEMMs) or algorithmic bytes (row kernels).
+namespace ktime {
+enum { FWD_GEMM = 0, WGRAD_GEMM = 1, LN_FWD = 2, LN_BWD = 3, NSLOT = 4 };
+struct Rec {
+    hipEvent_t a, b;
+    int slot;
+    double work;
+};
+struct State {
+    bool on = false;
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;  // events of cleared records, reused
+};
+State g;
+hipEvent_t event() {
+    hipEvent_t e;
+    if (!g.pool.empty()) {
+        e = g.pool.back();
+        g.pool.pop_back();
+    } else {
+        RLGPU_CHECK_HIP(hipEventCreate(&e));
+    }
+    return e;
+}
+void clear() {
+    for (auto& r : g.recs) {
+        g.pool.push_back(r.a);
+        g.pool.push_back(r.b);
+    }
+    g.recs.clear();
+}
+// brackets one launch on stream s
+struct Span {
+    int idx = -1;
+    hipStream_t s;
+    Span(int slot, double work, hipStream_t s_) : s(s_) {
+        if (!g.on) return;
+        Rec r{event(), event(), slot, work};
+        RLGPU_CHECK_HIP(hipEventRecord(r.a, s));
+        g.recs.push_back(r);
+        idx = (int)g.recs.size() - 1;
+    }
+    ~Span() {
+        if (idx >= 0) (void)hipEventRecord(g.recs[idx].b, s);
+    }
+};
+}  // namespace ktime
 
 // C[I,J] (+ bias) = A . B with the layouts of mlp::gemm_f32.  *_tail_ok: the operand's rows are
 // zero-padded up to a multiple of 4 past the bound (so float4 loads may straddle it).
@@ -277,6 +342,7 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
 void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int64_t bplane, float* C, int64_t ldc,
                  const float* bias, int I, int J, int K, hipStream_t s, bool a_tail_ok = false,
                  const float* amax_a = nullptr, const float* bscale = nullptr) {
+    ktime::Span span(ktime::FWD_GEMM, 2.0 * I * J * K, s);
     mlp::GemmArgs g{};
     g.amax_a = amax_a;
     g.bscale = bscale;
@@ -310,7 +376,14 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
         return;
     }
     dim3 grid(g.gx * g.gy), blk(256);
-    if (h3) {
+    if (h3 && av && h3_ring() != 0) {  // LDS-DMA ring kernel (bit-identical to gemm_x6's H3 path)
+        switch (h3_ring()) {
+            case 2: hipLaunchKernelGGL((mlp::gemm_h3r<64, 2>), grid, blk, 0, s, g); break;
+            case 3: hipLaunchKernelGGL((mlp::gemm_h3r<32, 3>), grid, blk, 0, s, g); break;
+            case 4: hipLaunchKernelGGL((mlp::gemm_h3r<32, 2>), grid, blk, 0, s, g); break;
+            default: hipLaunchKernelGGL((mlp::gemm_h3r<32, 4>), grid, blk, 0, s, g); break;
+        }
+    } else if (h3) {
         if (av)
             x6_launch_v<mlp::A_IK, mlp::B_JK, true, true, true, true>(grid, blk, s, g);
         else
@@ -374,8 +447,11 @@ void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx
     int chunk = (int)ceil_div(ceil_div(n, splits), kgran(m.mode)) * kgran(m.mode);
     int z = (int)ceil_div(n, chunk);
     // ldz > out: dZ rows zero-padded to ldz floats (16-byte loads across the row end)
+    {
+    ktime::Span span(ktime::WGRAD_GEMM, 2.0 * out * in * (double)n, s);
     gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, ldz ? ldz : out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s,
              ldz > out, x_tail_ok, amax_dz, amax_x);
+    }
     int64_t e = (int64_t)out * in;
     if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)m.wpart & 15) == 0)
         hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
@@ -462,6 +538,8 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool fuse = head1 && l == nh - 1;
+        // bytes: z read, act written, (mean, rstd) written
+        ktime::Span span(ktime::LN_FWD, (double)n * (8.0 * L.out + 8.0), s);
         hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
                            amax_slot(m, l), fuse ? P + O->w : nullptr, fuse ? P + O->b : nullptr, fuse ? out : nullptr);
@@ -549,11 +627,15 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool r1 = rank1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
         const float* dA_in = l == nh - 1 ? dA_top : m.dA;
+        {
+        // bytes: dA (recomputed for the rank-1 head: its dv instead), z, stats read; dZ written
+        ktime::Span span(ktime::LN_BWD, (double)n * ((r1 ? 4.0 : 4.0 * L.out) + 8.0 * L.out + 8.0), s);
         hipLaunchKernelGGL(r1 ? mlp::ln_act_bwd_head_any(L.out) : mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
                            reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
                            h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
                            r1 ? P + O->w : nullptr, r1 ? m.hpart : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
+        }
         if (r1) reduce_partials(m, m.hpart, nb, O->in + 1, O->in + 1, G + O->w, s);  // [w | b] contiguous
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
@@ -647,6 +729,7 @@ const uint16_t* forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStr
 // LDS tile (inputs / hidden widths <= 512, outputs <= 128); RLGPU_FUSED_INFER=0 selects the
 // layer-by-layer path (forward_half), which computes the same bits.
 unsigned long long* g_infer_trace = nullptr;  // rlgpu_debug_infer_trace
+int64_t g_infer_trace_cap = 0;             // its capacity (uint64 entries)
 bool fused_ok(const rlgpu_ppo* h, int mi) {
     const char* e = getenv("RLGPU_FUSED_INFER");
     if (e && atoi(e) == 0) return false;
@@ -695,6 +778,9 @@ void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode
     a.row_sel = row_sel;
     a.sel = sel;
     a.trace = g_infer_trace;
+    if (a.trace && ceil_div(n, infer::IR) * 16 > g_infer_trace_cap)
+        throw rlgpu::Error(RLGPU_ERR_INVALID_ARG, "rlgpu_debug_infer_trace: buffer of " + std::to_string(g_infer_trace_cap) +
+                                                      " entries, this launch needs " + std::to_string(ceil_div(n, infer::IR) * 16));
     RLGPU_H16_LAUNCH(h->cfg.infer_fp16, infer::mlp_infer, dim3(ceil_div(n, infer::IR)), dim3(infer::IT), 0, s, a);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
@@ -1034,9 +1120,12 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
     });
 }
 
-extern "C" int rlgpu_debug_infer_trace(void* d_buf) {
-    g_infer_trace = (unsigned long long*)d_buf;
-    return 0;
+extern "C" int rlgpu_debug_infer_trace(void* d_buf, int64_t capacity) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(!d_buf || capacity >= 16, "rlgpu_debug_infer_trace: capacity below one workgroup's 16 marks");
+        g_infer_trace = (unsigned long long*)d_buf;
+        g_infer_trace_cap = d_buf ? capacity : 0;
+    });
 }
 
 extern "C" int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stream) {
@@ -1311,5 +1400,31 @@ extern "C" int rlgpu_gemm_f32(int32_t a_layout, int32_t b_layout, const float* d
         RLGPU_REQUIRE((a_layout == 0 && (b_layout == 0 || b_layout == 1)) || (a_layout == 1 && b_layout == 1),
                       "rlgpu_gemm_f32: unsupported layout pair");
         gemm_f32(RLGPU_GEMM_F32, a_layout, b_layout, d_A, lda, d_B, ldb, d_C, ldc, d_bias, I, J, K, splits, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_kernel_timing(int32_t enable) {
+    return rlgpu::guarded([&] {
+        ktime::clear();
+        ktime::g.on = enable != 0;
+    });
+}
+
+extern "C" int rlgpu_kernel_timing_read(double* ms, double* work, int64_t* count, int32_t nslots) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(ms && work && count && nslots >= 0, "rlgpu_kernel_timing_read: null argument");
+        for (int i = 0; i < nslots; i++) {
+            ms[i] = work[i] = 0.0;
+            count[i] = 0;
+        }
+        for (auto& r : ktime::g.recs) {
+            if (r.slot >= nslots) continue;
+            RLGPU_CHECK_HIP(hipEventSynchronize(r.b));
+            float t = 0.f;
+            RLGPU_CHECK_HIP(hipEventElapsedTime(&t, r.a, r.b));
+            ms[r.slot] += t;
+            work[r.slot] += r.work;
+            count[r.slot]++;
+        }
     });
 }

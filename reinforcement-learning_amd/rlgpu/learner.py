@@ -181,6 +181,7 @@ class LearnerConfig:
         self.experience_capacity = 0       # mode 1: per-player step store rows (0 = automatic)
         self.rewards = None                # EnvCreateFn reward list (rlgpu.plugins.reward specs); None = ExampleMain's
         self.terminals = None              # terminal conditions (rlgpu.plugins.terminal specs); None = ExampleMain's
+        self.mesh = None                   # arena collision meshes (rlgpu.mesh.ArenaMesh); None = the built-in synthetic arena
         self.max_episode_duration = 300.0  # seconds (ExampleMain)
         self.deterministic = False
         self.train_gemm = 2               # rlgpu_ppo_config.train_gemm: 2 = f32 via scaled fp16 split (H3), 0 = bf16 x6 split, 1 = f32 MFMA
@@ -335,6 +336,10 @@ class Learner:
             tc = plugins.terminals_array(cfg.terminals)
             self._tc = np.ascontiguousarray(tc if tc.size else np.zeros(1, plugins.TERMINAL_SPEC))
             c.terminals, c.n_terminals = self._tc.ctypes.data, tc.size
+        if cfg.mesh is not None:  # copied by the env set at create
+            self._mesh = cfg.mesh
+            c.mesh_tris, c.mesh_ntris = cfg.mesh.tris.ctypes.data, cfg.mesh.num_tris
+            c.mesh_objects, c.mesh_object_ntris = cfg.mesh.num_objects, cfg.mesh.object_ntris.ctypes.data
         c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
         c.frame_stack = cfg.frame_stack
         c.experience_mode, c.ts_per_itr, c.experience_capacity = cfg.experience_mode, cfg.ts_per_itr, cfg.experience_capacity

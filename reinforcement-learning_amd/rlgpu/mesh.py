@@ -113,3 +113,69 @@ def cmf_bytes(vertices, triangles):
     v = np.ascontiguousarray(vertices, "<f4").reshape(-1, 3)
     t = np.ascontiguousarray(triangles, "<i4").reshape(-1, 3)
     return np.array([len(t), len(v)], "<i4").tobytes() + t.tobytes() + v.tobytes()
+
+
+def procedural_soccar(arc_segments=10, length_segments=36, goal_segments=10):
+    """A SOCCAR-sized stand-in for the absent game meshes (the reference loads 16 .cmf objects,
+    ~9k triangles, RocketSim.cpp:100-170 / Arena.cpp:1015-1058; the .cmf files are not in the
+    checkout).  It has their structure and density: the floor, ceiling and flat walls stay the
+    reference's static planes (Arena.cpp:1052-1100), and the mesh covers what the planes do not --
+    quarter-pipe transitions (radius 256 uu) from the floor and the ceiling into the side and back
+    walls, rounded vertical corners, and the two goal boxes (back net, side nets, roof) -- split
+    into 16 objects.  Vertices in bullet units (uu / 50).  ~9k triangles at the defaults."""
+    s = 1.0 / 50.0
+    X, Y, H, R, C = 4096.0, 5120.0, 2044.0, 256.0, 1152.0
+    GW, GH, NET = 892.755, 642.775, 6000.0
+    objs = []
+
+    def grid(P):  # P [a, b, 3] vertex grid -> triangles [2 (a-1)(b-1), 9]
+        a, b = P.shape[:2]
+        t = []
+        for i in range(a - 1):
+            for j in range(b - 1):
+                p00, p01, p10, p11 = P[i, j], P[i, j + 1], P[i + 1, j], P[i + 1, j + 1]
+                t += [np.concatenate([p00, p10, p11]), np.concatenate([p00, p11, p01])]
+        return np.array(t, np.float32)
+
+    th = np.linspace(0.0, np.pi / 2, arc_segments + 1)
+    # side-wall quarter pipes (floor and ceiling, both sides): along y, the arc in the x-z plane
+    for side in (-1.0, 1.0):
+        for top in (0, 1):
+            ys = np.linspace(-(Y - C), Y - C, length_segments + 1)
+            cx, cz = side * (X - R), (H - R) if top else R
+            # floor: theta 0 at the floor (z = 0) -> pi/2 on the wall (z = R); ceiling: theta 0 at
+            # the ceiling (z = H) -> pi/2 on the wall (z = H - R)
+            px = cx + side * R * np.sin(th)
+            pz = cz + (R * np.cos(th) if top else -R * np.cos(th))
+            P = np.stack(np.broadcast_arrays(px[:, None], ys[None, :], pz[:, None]), -1)
+            objs.append(grid(P * s))
+    # back-wall quarter pipes (floor and ceiling, both ends), left and right of the goal mouth
+    for end in (-1.0, 1.0):
+        for top in (0, 1):
+            parts = []
+            for x0, x1 in ((-(X - C), -GW), (GW, X - C)):
+                xs = np.linspace(x0, x1, length_segments // 2 + 1)
+                cy, cz = end * (Y - R), (H - R) if top else R
+                py = cy + end * R * np.sin(th)
+                pz = cz + (R * np.cos(th) if top else -R * np.cos(th))
+                P = np.stack(np.broadcast_arrays(xs[None, :], py[:, None], pz[:, None]), -1)
+                parts.append(grid(P * s))
+            objs.append(np.concatenate(parts))
+    # rounded vertical corners (45-degree corner region as a quarter-round, radius C)
+    for sx in (-1.0, 1.0):
+        for sy in (-1.0, 1.0):
+            zs = np.linspace(0.0, H, length_segments // 2 + 1)
+            cx, cy = sx * (X - C), sy * (Y - C)
+            px, py = cx + sx * C * np.cos(th), cy + sy * C * np.sin(th)
+            P = np.stack(np.broadcast_arrays(px[:, None], py[:, None], zs[None, :]), -1)
+            objs.append(grid(P * s))
+    # goal boxes: back net + roof, and the two side nets (two objects per goal)
+    for end in (-1.0, 1.0):
+        xs, zs, ys = np.linspace(-GW, GW, goal_segments + 1), np.linspace(0.0, GH, goal_segments + 1), \
+            np.linspace(end * Y, end * NET, goal_segments + 1)
+        net = np.stack(np.broadcast_arrays(xs[:, None], end * NET, zs[None, :]), -1)
+        roof = np.stack(np.broadcast_arrays(xs[:, None], ys[None, :], GH), -1)
+        objs.append(np.concatenate([grid(net * s), grid(roof * s)]))
+        sides = [np.stack(np.broadcast_arrays(gx, ys[:, None], zs[None, :]), -1) for gx in (-GW, GW)]
+        objs.append(np.concatenate([grid(p * s) for p in sides]))
+    return ArenaMesh(objs)

@@ -67,6 +67,8 @@ def _bind():
     L.rlgpu_ppo_set_version.argtypes = [vp, vp, vp]
     L.rlgpu_ppo_infer_actions_mixed.argtypes = [vp, vp, vp, i32, i32, u64, vp, vp, vp, vp]
     L.rlgpu_permutation.argtypes = [i64, u64, u64, vp, vp]
+    L.rlgpu_kernel_timing.argtypes = [i32]
+    L.rlgpu_kernel_timing_read.argtypes = [vp, vp, vp, i32]
     _ = f32
     _bound = True
     return L
@@ -361,6 +363,27 @@ def make_sequential(obs_size, out, layers, layer_norm=True, leaky_slope=0.01):
     if out is not None:
         mods.append(torch.nn.Linear(prev, out))
     return torch.nn.Sequential(*mods)
+
+
+KERNEL_TIMING_SLOTS = ("forward / input-gradient GEMMs", "weight-gradient GEMMs", "LayerNorm forward",
+                       "LayerNorm backward")
+
+
+def kernel_timing(enable):
+    """Start (clearing earlier records) or stop the learn-phase kernel timing (rlgpu_kernel_timing)."""
+    _bind()
+    _lib.check(_lib.lib().rlgpu_kernel_timing(1 if enable else 0), "rlgpu_kernel_timing")
+
+
+def kernel_timing_read():
+    """{slot name: (ms summed, work summed -- flops or bytes --, launches)} since kernel_timing(True)."""
+    import numpy as np
+    _bind()
+    n = len(KERNEL_TIMING_SLOTS)
+    ms, work, cnt = np.zeros(n), np.zeros(n), np.zeros(n, np.int64)
+    _lib.check(_lib.lib().rlgpu_kernel_timing_read(ms.ctypes.data, work.ctypes.data, cnt.ctypes.data, n),
+               "rlgpu_kernel_timing_read")
+    return {k: (float(ms[i]), float(work[i]), int(cnt[i])) for i, k in enumerate(KERNEL_TIMING_SLOTS)}
 
 
 def permutation(n, seed, counter, out=None, device="cuda:0"):

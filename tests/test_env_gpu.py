@@ -153,6 +153,39 @@ def test_env_custom_mesh_parity(gpu):
         _check_step(g, o, f"mesh perturbed step {t}")
 
 
+def test_env_procedural_soccar_mesh_parity(gpu):
+    """The bench's SOCCAR-sized workload mesh (rlgpu.mesh.procedural_soccar: 16 objects, 8,800
+    triangles -- quarter pipes, rounded corners, goal boxes): cars driven and balls thrown into the
+    curved transitions and goals, bit-exact vs the oracle's scan of every triangle."""
+    import torch
+    from rlgpu.env import EnvSet
+    from rlgpu.mesh import procedural_soccar
+    from rlgpu.state import ARENA
+    mesh = procedural_soccar()
+    assert (mesh.num_objects, mesh.num_tris) == (16, 8800)
+    n = 64
+    g, o = EnvSet(n, seed=21, device=gpu, mesh=mesh), oracle.EnvSet(n, seed=21, mesh=mesh, threads=8)
+    _check(g, o, "create")
+    rng = np.random.default_rng(8)
+    st = np.frombuffer(o.get_arenas().tobytes(), ARENA).copy()
+    for i in range(n):  # aim every ball at a transition, corner or goal; send cars at the walls
+        tgt = np.float32([rng.choice([-1, 1]) * rng.uniform(3000, 4096), rng.choice([-1, 1]) * rng.uniform(3500, 5900),
+                          rng.uniform(0, 2000)]) / 50.0
+        d = tgt - st["ball"][i]["pos"]
+        st["ball"][i]["vel"] = (d / np.linalg.norm(d) * rng.uniform(50, 110)).astype(np.float32)
+        for k in range(4):
+            v = rng.normal(size=3) * [1, 1, 0.2]
+            st["cars"][i]["body"]["vel"][k] = (v / np.linalg.norm(v) * rng.uniform(20, 46)).astype(np.float32)
+    buf = np.frombuffer(st.tobytes(), np.uint8)
+    o.set_arenas(buf)
+    g.set_arenas(buf)
+    for t in range(60):
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True)
+        _check_step(g, o, f"procedural soccar step {t}")
+
+
 def test_env_reset_arenas_mask(gpu):
     import torch
     n = 12

@@ -18,7 +18,12 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 8  # env steps before profiling (late-episode states)
 dev = torch.device("cuda:0")
-env = EnvSet(n, seed=1234, device=dev)
+mesh_name = sys.argv[4] if len(sys.argv) > 4 else "synthetic"
+if mesh_name == "procedural":
+    from rlgpu.mesh import procedural_soccar
+    env = EnvSet(n, seed=1234, device=dev, mesh=procedural_soccar())
+else:
+    env = EnvSet(n, seed=1234, device=dev)
 gen = torch.Generator(device=dev).manual_seed(7)
 acts = torch.empty(4 * n, dtype=torch.int32, device=dev)
 for i in range(warm):
@@ -29,8 +34,8 @@ KP, KW = 24, 64  # env_kernel.hpp kProfPhases, kProfWG
 prof = torch.zeros(KW + wg * KP, dtype=torch.int64, device=dev)
 spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
 L = _lib.lib()
-L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-_lib.check(L.rlgpu_envset_set_profile(env._h, ctypes.c_void_p(prof.data_ptr())), "set_profile")
+L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+_lib.check(L.rlgpu_envset_set_profile(env._h, ctypes.c_void_p(prof.data_ptr()), prof.numel()), "set_profile")
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 tot_ms = 0.0
 for i in range(steps):
@@ -47,7 +52,7 @@ for i in range(steps):
     prof[KW:].zero_()
 c = prof.cpu().tolist()
 total = sum(c[:23])
-print(f"{n} arenas, {steps} steps, {tot_ms / steps:.3f} ms/step (profiled build)")
+print(f"{n} arenas, {steps} steps, {mesh_name} mesh, {tot_ms / steps:.3f} ms/step (profiled build)")
 ticks = steps * 8
 print(f"  per tick (workgroup 0, arena 0): candidates {c[24] / ticks / wg:.2f}, mode-1 ranks {c[27] / ticks / wg:.2f}, "
       f"refresh-needing ranks {c[25] / ticks / wg:.2f}, live ranks {c[26] / ticks / wg:.2f}")

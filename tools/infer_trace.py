@@ -39,7 +39,7 @@ def report(tag, tr, nblk):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
     lib = _lib.lib()
-    lib.rlgpu_debug_infer_trace.argtypes = [ctypes.c_void_p]
+    lib.rlgpu_debug_infer_trace.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     p = PPO(max_rows=50_000, seed=1)
     g = torch.Generator().manual_seed(0)
     obs = torch.randn(max(n, 50_000), 167, generator=g).cuda()
@@ -53,10 +53,10 @@ def main():
     for tag, fn, rows in (("policy sample", lambda: p.infer_actions(obs[:n], masks), n),
                           ("critic values", lambda: p.infer_critic(obs[:50_000]), 50_000)):
         tr.zero_()
-        lib.rlgpu_debug_infer_trace(ctypes.c_void_p(tr.data_ptr()))
+        lib.rlgpu_debug_infer_trace(ctypes.c_void_p(tr.data_ptr()), tr.numel())
         fn()
         torch.cuda.synchronize()
-        lib.rlgpu_debug_infer_trace(None)
+        lib.rlgpu_debug_infer_trace(None, 0)
         report(tag, tr.cpu().numpy(), (rows + 63) // 64)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
