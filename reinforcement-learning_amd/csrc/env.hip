@@ -716,7 +716,7 @@ struct rlgpu_envset {
     unsigned long long* d_prof = nullptr;
     double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
-    void *d_tri = nullptr, *d_cell_start = nullptr, *d_cell_tris = nullptr;  // arena mesh (MeshView)
+    void *d_cell_tri = nullptr, *d_cell_start = nullptr;  // arena mesh (MeshView)
     rl::MeshView mesh{};
     rl::Plugins plug{};                 // host copy of the reward / terminal registry
     rl::Plugins* d_plug = nullptr;      // its device copy (StepArgs::plug)
@@ -887,18 +887,15 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         e->plug = plug;
         RLGPU_CHECK_HIP(hipMalloc(&e->d_plug, sizeof(rl::Plugins)));
         RLGPU_CHECK_HIP(hipMemcpy(e->d_plug, &e->plug, sizeof(rl::Plugins), hipMemcpyHostToDevice));
-        RLGPU_CHECK_HIP(hipMalloc(&e->d_tri, grid.tri.size() * sizeof(float)));
         RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_start, grid.cell_start.size() * sizeof(int)));
-        RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_tris, std::max<size_t>(grid.cell_tris.size(), 1) * sizeof(int)));
-        RLGPU_CHECK_HIP(hipMemcpy(e->d_tri, grid.tri.data(), grid.tri.size() * sizeof(float), hipMemcpyHostToDevice));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_cell_tri, std::max<size_t>(grid.cell_tri.size(), 12) * sizeof(float)));
         RLGPU_CHECK_HIP(hipMemcpy(e->d_cell_start, grid.cell_start.data(), grid.cell_start.size() * sizeof(int),
                                   hipMemcpyHostToDevice));
-        if (!grid.cell_tris.empty())
-            RLGPU_CHECK_HIP(hipMemcpy(e->d_cell_tris, grid.cell_tris.data(), grid.cell_tris.size() * sizeof(int),
+        if (!grid.cell_tri.empty())
+            RLGPU_CHECK_HIP(hipMemcpy(e->d_cell_tri, grid.cell_tri.data(), grid.cell_tri.size() * sizeof(float),
                                       hipMemcpyHostToDevice));
-        e->mesh.tri = (const float4*)e->d_tri;
+        e->mesh.cell_tri = (const float4*)e->d_cell_tri;
         e->mesh.cell_start = (const int*)e->d_cell_start;
-        e->mesh.cell_tris = (const int*)e->d_cell_tris;
         e->mesh.ox = grid.ox;
         e->mesh.oy = grid.oy;
         e->mesh.oz = grid.oz;
@@ -1044,9 +1041,8 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_last_rewards);
         (void)hipFree(e->d_masks);
         (void)hipFree(e->d_terminals);
-        (void)hipFree(e->d_tri);
+        (void)hipFree(e->d_cell_tri);
         (void)hipFree(e->d_cell_start);
-        (void)hipFree(e->d_cell_tris);
         (void)hipFree(e->d_plug);
         (void)hipFree(e->d_player_start);
         delete e;

@@ -153,36 +153,43 @@ DEV int grid_cell(float x, float o, float inv, int n) {
     f = fminf(fmaxf(f, 0.f), (float)(n - 1));
     return (int)f;
 }
-DEV void load_tri(const MeshView& M, int t, v3& v0, v3& v1, v3& v2, int& obj) {
-    const float4 a = M.tri[3 * t], b = M.tri[3 * t + 1], c = M.tri[3 * t + 2];
-    v0 = v3{a.x, a.y, a.z};
-    v1 = v3{b.x, b.y, b.z};
-    v2 = v3{c.x, c.y, c.z};
-    obj = __float_as_int(a.w);
-}
+constexpr int kGridBatch = 4;  // grid entries whose loads are issued together
 // Calls f(t, v0, v1, v2, obj) once for every triangle whose AABB overlaps [qmn, qmx] (the exact
 // test of the linear scan it replaces), in no particular order.  A triangle is listed in every
 // cell its AABB touches; it is visited only from the cell max(query lo, triangle lo) per axis,
 // which lies in both cell ranges whenever the boxes overlap (grid_cell is monotone).  Entries
-// are dealt round-robin over `parts` callers.
+// are dealt round-robin over `parts` callers.  Entries hold their triangle inline (no index
+// indirection), and kGridBatch entries' loads are issued before the first is tested: the walk is
+// latency-bound (one dependent L2 round trip per entry otherwise).
 template <class F>
 DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& f) {
     const int x0 = grid_cell(qmn.x, M.ox, M.inv_cell, M.nx), x1 = grid_cell(qmx.x, M.ox, M.inv_cell, M.nx);
     const int y0 = grid_cell(qmn.y, M.oy, M.inv_cell, M.ny), y1 = grid_cell(qmx.y, M.oy, M.inv_cell, M.ny);
     const int z0 = grid_cell(qmn.z, M.oz, M.inv_cell, M.nz), z1 = grid_cell(qmx.z, M.oz, M.inv_cell, M.nz);
     int seen = 0;
+    // the cells x0..x1 of one (y, z) row are consecutive, so their entries are one contiguous range
+    // (each entry carries its cell's x in v2.w for the visit-once rule)
     for (int cz = z0; cz <= z1; cz++)
-        for (int cy = y0; cy <= y1; cy++)
-            for (int cx = x0; cx <= x1; cx++) {
-                const int cell = (cz * M.ny + cy) * M.nx + cx;
-                const int b = M.cell_start[cell], e = M.cell_start[cell + 1];
-                int k = b + ((part - seen % parts) + parts) % parts;
-                seen += e - b;
-                for (; k < e; k += parts) {
-                    const int t = M.cell_tris[k];
-                    v3 v0, v1, v2;
-                    int obj;
-                    load_tri(M, t, v0, v1, v2, obj);
+        for (int cy = y0; cy <= y1; cy++) {
+            const int row = (cz * M.ny + cy) * M.nx;
+            const int b = M.cell_start[row + x0], e = M.cell_start[row + x1 + 1];
+            int k = b + ((part - seen % parts) + parts) % parts;
+            seen += e - b;
+            for (; k < e; k += kGridBatch * parts) {
+                float4 q[kGridBatch][3];
+#pragma unroll
+                for (int j = 0; j < kGridBatch; j++) {  // past the range's end: the last entry again (not visited)
+                    const float4* p = M.cell_tri + 3 * (size_t)min(k + j * parts, e - 1);
+                    q[j][0] = p[0];
+                    q[j][1] = p[1];
+                    q[j][2] = p[2];
+                }
+#pragma unroll
+                for (int j = 0; j < kGridBatch; j++) {
+                    if (k + j * parts >= e) break;
+                    const v3 v0 = v3{q[j][0].x, q[j][0].y, q[j][0].z}, v1 = v3{q[j][1].x, q[j][1].y, q[j][1].z},
+                             v2 = v3{q[j][2].x, q[j][2].y, q[j][2].z};
+                    const int obj = __float_as_int(q[j][0].w), t = __float_as_int(q[j][1].w), cx = __float_as_int(q[j][2].w);
                     const v3 tmn = v3{fminf(v0.x, fminf(v1.x, v2.x)), fminf(v0.y, fminf(v1.y, v2.y)), fminf(v0.z, fminf(v1.z, v2.z))};
                     const v3 tmx = v3{fmaxf(v0.x, fmaxf(v1.x, v2.x)), fmaxf(v0.y, fmaxf(v1.y, v2.y)), fmaxf(v0.z, fmaxf(v1.z, v2.z))};
                     if (!aabb_overlap(qmn, qmx, tmn, tmx)) continue;
@@ -193,6 +200,7 @@ DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& 
                     f(t, v0, v1, v2, obj);
                 }
             }
+        }
 }
 
 // ------------------------------------------------------------------ ray cast (btCollisionWorld::rayTest)

@@ -98,9 +98,9 @@ struct Cand {
 // on every triangle the grid returns, so results equal a scan of all triangles.
 constexpr int kMaxTris = 1 << 20;   // triangle index fits the low 20 bits of Cand::order
 struct MeshView {
-    const float4* tri;       // [ntris * 3]
+    const float4* cell_tri;  // [entries * 3]: the triangles of every cell inline, ascending index
+                             // (v0 | object, v1 | triangle index, v2 | cell x; mesh.hpp MeshGrid)
     const int* cell_start;   // [ncell + 1]
-    const int* cell_tris;    // triangle indices, ascending within a cell
     float ox, oy, oz, inv_cell;
     int nx, ny, nz, ntris;
 };

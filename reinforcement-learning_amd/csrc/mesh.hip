@@ -85,9 +85,11 @@ MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntr
                 mn[a] = std::fmin(mn[a], x);
                 mx[a] = std::fmax(mx[a], x);
             }
-    // cells of >= 256 uu (5.12 bullet units): a car or ball query touches at most 2 cells per axis
+    // cells of >= 128 uu (2.56 bullet units): a wheel ray touches one or two cells per axis, a car
+    // or ball two or three; a SOCCAR-density mesh (quarter pipes of 10 x 36 segments) lists ~10
+    // triangles in a cell it crosses
     float ext = std::fmax(mx[0] - mn[0], std::fmax(mx[1] - mn[1], mx[2] - mn[2]));
-    float cell = std::fmax(5.12f, ext / 96.f);
+    float cell = std::fmax(2.56f, ext / 128.f);
     g.inv_cell = 1.f / cell;
     g.ox = mn[0];
     g.oy = mn[1];
@@ -119,22 +121,23 @@ MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntr
     }
     g.cell_start.assign(ncell + 1, 0);
     for (size_t c = 0; c < ncell; c++) g.cell_start[c + 1] = g.cell_start[c] + count[c];
-    g.cell_tris.assign((size_t)g.cell_start[ncell], 0);
+    RLGPU_REQUIRE(g.cell_start[ncell] < (1 << 26), "mesh: grid index too large");
+    g.cell_tri.assign((size_t)g.cell_start[ncell] * 12, 0.f);
     std::vector<int> fill(g.cell_start.begin(), g.cell_start.end() - 1);
     for (int t = 0; t < ntris; t++) {  // ascending t within every cell
         int lo[3], hi[3];
         cell_range(t, lo, hi);
+        const float* p = tris + (size_t)t * 9;
         for (int z = lo[2]; z <= hi[2]; z++)
             for (int y = lo[1]; y <= hi[1]; y++)
-                for (int x = lo[0]; x <= hi[0]; x++) g.cell_tris[fill[((size_t)z * g.ny + y) * g.nx + x]++] = t;
-    }
-    g.tri.assign((size_t)ntris * 12, 0.f);
-    for (int t = 0; t < ntris; t++) {
-        float* d = &g.tri[(size_t)t * 12];
-        const float* p = tris + (size_t)t * 9;
-        for (int v = 0; v < 3; v++)
-            for (int a = 0; a < 3; a++) d[v * 4 + a] = p[v * 3 + a];
-        std::memcpy(&d[3], &obj[t], sizeof(int));
+                for (int x = lo[0]; x <= hi[0]; x++) {
+                    float* d = &g.cell_tri[(size_t)fill[((size_t)z * g.ny + y) * g.nx + x]++ * 12];
+                    for (int v = 0; v < 3; v++)
+                        for (int a = 0; a < 3; a++) d[v * 4 + a] = p[v * 3 + a];
+                    std::memcpy(&d[3], &obj[t], sizeof(int));
+                    std::memcpy(&d[7], &t, sizeof(int));
+                    std::memcpy(&d[11], &x, sizeof(int));
+                }
     }
     return g;
 }

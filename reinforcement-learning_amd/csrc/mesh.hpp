@@ -7,8 +7,10 @@
 namespace rlgpu {
 
 struct MeshGrid {
-    std::vector<float> tri;  // ntris x 12 floats: v0.xyz | object id bits, v1.xyz | 0, v2.xyz | 0
-    std::vector<int> cell_start, cell_tris;
+    // one entry per (cell, triangle) listing, ascending triangle index within a cell, the triangle
+    // inline: 12 floats = v0.xyz | object id bits, v1.xyz | triangle index bits, v2.xyz | cell x bits
+    std::vector<float> cell_tri;
+    std::vector<int> cell_start;
     float ox = 0, oy = 0, oz = 0, inv_cell = 1;
     int nx = 1, ny = 1, nz = 1, ntris = 0;
 };
