@@ -38,6 +38,14 @@ int rlgpu_cmf_parse(const void* data, int64_t size, float* out_tris, int32_t max
  * reference only warns about unknown or duplicate meshes, RocketSim.cpp:140-155). */
 int rlgpu_mesh_known_hash(int32_t game_mode, uint32_t hash);
 
+/* The internal-edge records the env set builds for its mesh at create (RocketSim.cpp:166-170:
+ * btGenerateInternalEdgeInfo per collision object; used by btAdjustInternalEdgeContacts in the contact
+ * callback, Arena.cpp:275-279).  tris / object_ntris as rlgpu_envset_config.mesh_* (object_ntris NULL:
+ * one object).  out: ntris x 4 floats = m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle (2 pi = no
+ * neighbour) and the flags as int32 bits (TRI_INFO_* convex 1/2/4, swap 8/16/32; bit 30 = the triangle
+ * has a record, 0 = none).  Host only. */
+int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects, float* out);
+
 #ifdef __cplusplus
 }
 #endif

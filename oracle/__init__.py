@@ -216,3 +216,16 @@ def detmath_exp_log(x):
     f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
     f(_p(x), x.size, _p(ex), _p(lg))
     return ex, lg
+
+
+def mesh_edge_info(tris, object_ntris=None):
+    """oracle_mesh_edge_info: btGenerateInternalEdgeInfo restated (edge_ref.hpp) -> [ntris, 4] float32
+    (m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle, flags bits | 1 << 30 with a record)."""
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    objs = None if object_ntris is None else np.ascontiguousarray(object_ntris, np.int32)
+    out = np.zeros((len(tris), 4), np.float32)
+    f = lib().oracle_mesh_edge_info
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    f(_p(tris), len(tris), _p(objs), 0 if objs is None else len(objs), _p(out))
+    return out

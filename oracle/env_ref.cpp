@@ -822,6 +822,21 @@ void oracle_env_set_plugins(void* h, const rlgpu_reward_spec* rw, int nr, const 
 
 // Arena collision meshes for this set (rlgpu_envset_config.mesh_*): ntris x 9 floats (bullet
 // units), object k owns the next obj_ntris[k] triangles (obj_ntris NULL: one object).
+// internal-edge records of a mesh (btGenerateInternalEdgeInfo restated, edge_ref.hpp): ntris x 4 floats
+// (3 angles, flags bits | 1 << 30 when the triangle has a record), the library's rlgpu_mesh_edge_info layout
+void oracle_mesh_edge_info(const float* tris, int ntris, const int* obj_ntris, int nobj, float* out) {
+    World wd;
+    wd.set_mesh(tris, ntris, obj_ntris, nobj);
+    for (int t = 0; t < ntris; t++) {
+        const TriInfo& ti = wd.tri_info[t];
+        int flags = ti.flags | (ti.present ? (1 << 30) : 0);
+        out[4 * t] = ti.e01;
+        out[4 * t + 1] = ti.e12;
+        out[4 * t + 2] = ti.e20;
+        std::memcpy(&out[4 * t + 3], &flags, sizeof(int));
+    }
+}
+
 void oracle_env_set_mesh(void* h, const float* tris, int ntris, const int* obj_ntris, int nobj) {
     EnvSet* e = (EnvSet*)h;
     delete e->own_world;

@@ -196,6 +196,7 @@ void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) 
         for (int k = 0; k < nobjects; k++)
             for (int i = 0; i < obj_ntris[k] && t < n; i++) tri_obj[t++] = k;
     }
+    tri_info = edge::gen_edge_info(tri, tri_obj);  // RocketSim.cpp:166-170
 }
 
 const World& world() {
@@ -1145,8 +1146,9 @@ struct Sim {
         return best;
     }
 
-    // btManifoldResult::addContactPoint + contact-added callback (Arena.cpp:218-281)
-    void add_contact(int key, V normal_b, V point_b, float depth) {
+    // btManifoldResult::addContactPoint + contact-added callback (Arena.cpp:218-281); t >= 0: the
+    // mesh triangle of the point (btAdjustInternalEdgeContacts ends the callback, Arena.cpp:275-279)
+    void add_contact(int key, V normal_b, V point_b, float depth, int t = -1) {
         int a, bb;
         key_bodies(key, a, bb);
         float cbt = pair_cbt(a, bb);
@@ -1184,6 +1186,13 @@ struct Sim {
         if (idx < 0) idx = 0;
         m->pts[idx] = c;
         contact_callback(a, bb, m->pts[idx]);
+        if (t >= 0) {
+            rlgpu_contact& cp = m->pts[idx];
+            V n = ld3(cp.normalB), lb = ld3(cp.localB);
+            edge::adjust_edge(&w.tri[(size_t)t * 3], w.tri_info[t], n, lb, pa, cp.dist);
+            st3(cp.normalB, n);
+            st3(cp.localB, lb);
+        }
     }
 
     // Arena::_BulletContactAddedCallback (Arena.cpp:218-281): bodies ordered car < ball < world
@@ -1360,7 +1369,7 @@ struct Sim {
             if (!aabb_overlap(c - V(ext, ext, ext), c + V(ext, ext, ext), w.tri_min[t], w.tri_max[t])) continue;
             V pt, nrm;
             float depth;
-            if (sphere_triangle(c, r, t, cbt, pt, nrm, depth)) add_contact(key, nrm, pt, depth);
+            if (sphere_triangle(c, r, t, cbt, pt, nrm, depth)) add_contact(key, nrm, pt, depth, t);
         }
     }
     static bool aabb_overlap(V a0, V a1, V b0, V b1) {
@@ -1526,7 +1535,7 @@ struct Sim {
             if (!aabb_overlap(mn, mx, w.tri_min[t], w.tri_max[t])) continue;
             V n, pb;
             float d;
-            if (box_triangle(bi, t, cbt, n, pb, d)) add_contact(key, n, pb, d);
+            if (box_triangle(bi, t, cbt, n, pb, d)) add_contact(key, n, pb, d, t);
         }
     }
     // btSphereBoxCollisionAlgorithm::getSphereDistance (box = the car), manifold A = ball, B = car

@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "../include/rlgpu_env.h"
+#include "edge_ref.hpp"
 #include "rsim_math.hpp"
 
 namespace orc {
@@ -22,6 +23,7 @@ struct World {
     int ntris = 0, nobj = 1;
     std::vector<V> tri, tri_min, tri_max;
     std::vector<int> tri_obj;
+    std::vector<TriInfo> tri_info;  // internal-edge records (btGenerateInternalEdgeInfo, edge_ref.hpp)
     void set_mesh(const float* tris_bt, int n, const int* obj_ntris, int nobjects);
     float kick_x[5], kick_y[5];
     M kick_rot[2][5];

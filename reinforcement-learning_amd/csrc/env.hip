@@ -193,7 +193,7 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
     sync();
     P.mark(5);
     if (valid && l == 0) {
-        commit_contacts(A, &P);
+        commit_contacts(A, M, &P);
         if (threadIdx.x == 0) P.mark(16);
     }
     sync();
@@ -716,7 +716,7 @@ struct rlgpu_envset {
     unsigned long long* d_prof = nullptr;
     double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
-    void *d_cell_tri = nullptr, *d_cell_start = nullptr;  // arena mesh (MeshView)
+    void *d_cell_tri = nullptr, *d_cell_start = nullptr, *d_tri = nullptr, *d_edge = nullptr;  // arena mesh (MeshView)
     rl::MeshView mesh{};
     rl::Plugins plug{};                 // host copy of the reward / terminal registry
     rl::Plugins* d_plug = nullptr;      // its device copy (StepArgs::plug)
@@ -896,6 +896,12 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
                                       hipMemcpyHostToDevice));
         e->mesh.cell_tri = (const float4*)e->d_cell_tri;
         e->mesh.cell_start = (const int*)e->d_cell_start;
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_tri, grid.tri.size() * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMalloc(&e->d_edge, grid.edge.size() * sizeof(float)));
+        RLGPU_CHECK_HIP(hipMemcpy(e->d_tri, grid.tri.data(), grid.tri.size() * sizeof(float), hipMemcpyHostToDevice));
+        RLGPU_CHECK_HIP(hipMemcpy(e->d_edge, grid.edge.data(), grid.edge.size() * sizeof(float), hipMemcpyHostToDevice));
+        e->mesh.tri = (const float4*)e->d_tri;
+        e->mesh.edge = (const float4*)e->d_edge;
         e->mesh.ox = grid.ox;
         e->mesh.oy = grid.oy;
         e->mesh.oz = grid.oz;
@@ -1042,6 +1048,8 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_masks);
         (void)hipFree(e->d_terminals);
         (void)hipFree(e->d_cell_tri);
+        (void)hipFree(e->d_tri);
+        (void)hipFree(e->d_edge);
         (void)hipFree(e->d_cell_start);
         (void)hipFree(e->d_plug);
         (void)hipFree(e->d_player_start);

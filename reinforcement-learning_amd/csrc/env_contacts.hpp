@@ -2,6 +2,7 @@
 // sequential-impulse solver of the env kernel.  Reference map in env_kernel.hpp; each
 // function cites the Bullet / RocketSim code it restates.
 #pragma once
+#include "edge_info.hpp"
 #include "env_device.hpp"
 
 namespace rl {
@@ -198,8 +199,9 @@ DEV void contact_callback(ArenaLDS* A, int a, int b, rlgpu_contact& cp) {
     }
 }
 
-// btManifoldResult::addContactPoint (btManifoldResult.cpp:110-200)
-DEV void add_contact(ArenaLDS* A, int key, v3 normal_b, v3 point_b, float depth) {
+// btManifoldResult::addContactPoint (btManifoldResult.cpp:110-200); tri >= 0: the mesh triangle the
+// point lies on (its internal-edge adjustment ends the contact callback, Arena.cpp:275-279)
+DEV void add_contact(ArenaLDS* A, const MeshView& M, int key, v3 normal_b, v3 point_b, float depth, int tri) {
     int a, b;
     key_bodies(key, a, b);
     float cbt = pair_cbt(a, b);
@@ -236,6 +238,15 @@ DEV void add_contact(ArenaLDS* A, int key, v3 normal_b, v3 point_b, float depth)
     if (idx < 0) idx = 0;
     m->pts[idx] = c;
     contact_callback(A, a, b, m->pts[idx]);
+    if (tri >= 0) {  // btAdjustInternalEdgeContacts on the stored point (mesh at the identity transform)
+        rlgpu_contact& cp = m->pts[idx];
+        const float4 t0 = M.tri[3 * tri], t1 = M.tri[3 * tri + 1], t2 = M.tri[3 * tri + 2], ei = M.edge[tri];
+        const EdgeInfo info{ei.x, ei.y, ei.z, __float_as_int(ei.w)};
+        v3 n = ld3(cp.normalB), pb = ld3(cp.localB);
+        adjust_edge_contact(v3{t0.x, t0.y, t0.z}, v3{t1.x, t1.y, t1.z}, v3{t2.x, t2.y, t2.z}, info, n, pb, pa, cp.dist);
+        st3(cp.normalB, n);
+        st3(cp.localB, pb);
+    }
 }
 
 // btPersistentManifold::refreshContactPoints (btPersistentManifold.cpp:265-330)
@@ -576,7 +587,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
 // single lane: commit this tick's candidates in canonical order -- per pair (key): add its points
 // (contact callbacks fire here), then refresh its manifold, as Bullet's dispatch loop does
 // (btCollisionDispatcher::dispatchAllCollisionPairs, processCollision -> refreshContactPoints)
-DEV void commit_contacts(ArenaLDS* A, Prof* P = nullptr) {
+DEV void commit_contacts(ArenaLDS* A, const MeshView& M, Prof* P = nullptr) {
     int n = A->a.ncand;
     if (n > kMaxCand) {
         A->s.env.manifold_overflow += (uint32_t)(n - kMaxCand);
@@ -615,7 +626,11 @@ DEV void commit_contacts(ArenaLDS* A, Prof* P = nullptr) {
             if (cur >= 0) refresh(A, cur);
             cur = c.key;
         }
-        add_contact(A, c.key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth);
+        // mesh-object keys carry their triangle in the low bits of the commit order
+        int ka, kb;
+        key_bodies(c.key, ka, kb);
+        const int tri = (c.key < kDynKey && kb - 10 < kMaxObj) ? (c.order & (kMaxTris - 1)) : -1;
+        add_contact(A, M, c.key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth, tri);
     }
     if (cur >= 0) refresh(A, cur);
     if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[26], (unsigned long long)A->a.nmf);

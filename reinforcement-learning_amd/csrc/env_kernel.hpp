@@ -101,6 +101,8 @@ struct MeshView {
     const float4* cell_tri;  // [entries * 3]: the triangles of every cell inline, ascending index
                              // (v0 | object, v1 | triangle index, v2 | cell x; mesh.hpp MeshGrid)
     const int* cell_start;   // [ncell + 1]
+    const float4* tri;       // [ntris * 3]: v0 | object, v1, v2 of triangle t (load order)
+    const float4* edge;      // [ntris]: internal-edge record (edge_info.hpp EdgeInfo)
     float ox, oy, oz, inv_cell;
     int nx, ny, nz, ntris;
 };

@@ -11,6 +11,7 @@
 #include "../../include/rlgpu_env.h"
 #include "../../include/rlgpu_mesh.h"
 #include "common.hpp"
+#include "edge_info.hpp"
 
 namespace rlgpu {
 
@@ -139,7 +140,60 @@ MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntr
                     std::memcpy(&d[11], &x, sizeof(int));
                 }
     }
+    g.tri.assign((size_t)ntris * 12, 0.f);
+    for (int t = 0; t < ntris; t++) {
+        float* d = &g.tri[(size_t)t * 12];
+        const float* p = tris + (size_t)t * 9;
+        for (int v = 0; v < 3; v++)
+            for (int a = 0; a < 3; a++) d[v * 4 + a] = p[v * 3 + a];
+        std::memcpy(&d[3], &obj[t], sizeof(int));
+    }
+    g.edge = mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1);
     return g;
+}
+
+// btGenerateInternalEdgeInfo per collision object (one btBvhTriangleMeshShape per object, partId 0):
+// for every triangle A, every other triangle B of the object whose AABB overlaps A's, in index order
+// (the reference: the BVH's overlap query, btInternalEdgeUtility.cpp:300-356)
+std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* object_ntris, int nobjects) {
+    std::vector<float> out((size_t)ntris * 4, 0.f);
+    auto vert = [&](int t, int k) {
+        const float* p = tris + (size_t)t * 9 + 3 * k;
+        return rl::v3{p[0], p[1], p[2]};
+    };
+    int t0 = 0;
+    for (int o = 0; o < nobjects; o++) {
+        const int n = object_ntris ? object_ntris[o] : ntris;
+        std::vector<rl::v3> mn(n), mx(n);
+        for (int i = 0; i < n; i++) {
+            rl::v3 a = vert(t0 + i, 0), b = vert(t0 + i, 1), c = vert(t0 + i, 2);
+            mn[i] = rl::v3{std::fmin(a.x, std::fmin(b.x, c.x)), std::fmin(a.y, std::fmin(b.y, c.y)), std::fmin(a.z, std::fmin(b.z, c.z))};
+            mx[i] = rl::v3{std::fmax(a.x, std::fmax(b.x, c.x)), std::fmax(a.y, std::fmax(b.y, c.y)), std::fmax(a.z, std::fmax(b.z, c.z))};
+        }
+        for (int i = 0; i < n; i++) {
+            const rl::v3 va[3] = {vert(t0 + i, 0), vert(t0 + i, 1), vert(t0 + i, 2)};
+            rl::EdgeInfo info{rl::kEdge2Pi, rl::kEdge2Pi, rl::kEdge2Pi, 0};
+            for (int j = 0; j < n; j++) {
+                if (j == i) continue;  // self
+                // AABB overlap grown by 2e-4 (twice the shared-vertex distance): a neighbour whose shared
+                // vertices differ by less than the threshold always passes, as in the BVH's
+                // conservative (quantized) query
+                const float g = 2e-4f;
+                if (mn[j].x > mx[i].x + g || mx[j].x < mn[i].x - g || mn[j].y > mx[i].y + g || mx[j].y < mn[i].y - g ||
+                    mn[j].z > mx[i].z + g || mx[j].z < mn[i].z - g)
+                    continue;
+                const rl::v3 vb[3] = {vert(t0 + j, 0), vert(t0 + j, 1), vert(t0 + j, 2)};
+                rl::edge_connect(va, vb, info);
+            }
+            float* d = &out[(size_t)(t0 + i) * 4];
+            d[0] = info.a01;
+            d[1] = info.a12;
+            d[2] = info.a20;
+            std::memcpy(&d[3], &info.flags, sizeof(int));
+        }
+        t0 += n;
+    }
+    return out;
 }
 
 }  // namespace rlgpu
@@ -174,6 +228,24 @@ extern "C" int rlgpu_cmf_parse(const void* data, int64_t size, float* out_tris, 
                 for (int i = 0; i < 3; i++)
                     for (int j = 0; j < 3; j++) out_tris[(size_t)t * 9 + i * 3 + j] = verts[(size_t)idx[(size_t)t * 3 + i] * 3 + j];
         }
+    });
+}
+
+extern "C" int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects,
+                                    float* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(tris && out && ntris > 0, "rlgpu_mesh_edge_info: null argument or no triangles");
+        if (object_ntris) {
+            RLGPU_REQUIRE(nobjects >= 1, "rlgpu_mesh_edge_info: nobjects must be >= 1");
+            int64_t sum = 0;
+            for (int k = 0; k < nobjects; k++) {
+                RLGPU_REQUIRE(object_ntris[k] >= 0, "rlgpu_mesh_edge_info: negative object triangle count");
+                sum += object_ntris[k];
+            }
+            RLGPU_REQUIRE(sum == ntris, "rlgpu_mesh_edge_info: object triangle counts do not add up to ntris");
+        }
+        const std::vector<float> e = rlgpu::mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1);
+        std::memcpy(out, e.data(), e.size() * sizeof(float));
     });
 }
 

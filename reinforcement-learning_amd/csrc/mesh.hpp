@@ -11,6 +11,9 @@ struct MeshGrid {
     // inline: 12 floats = v0.xyz | object id bits, v1.xyz | triangle index bits, v2.xyz | cell x bits
     std::vector<float> cell_tri;
     std::vector<int> cell_start;
+    // per triangle in load order: 12 floats = v0.xyz | object id bits, v1.xyz | 0, v2.xyz | 0, and its
+    // internal-edge record (edge_info.hpp EdgeInfo: 3 angles | flags bits)
+    std::vector<float> tri, edge;
     float ox = 0, oy = 0, oz = 0, inv_cell = 1;
     int nx = 1, ny = 1, nz = 1, ntris = 0;
 };
@@ -18,6 +21,10 @@ struct MeshGrid {
 // tris_bt: ntris x 9 floats (bullet units); object k owns the next object_ntris[k] triangles
 // (object_ntris == nullptr: one object).  Throws rlgpu::Error on invalid input.
 MeshGrid build_mesh_grid(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects);
+
+// btGenerateInternalEdgeInfo over every object of a mesh (edge_info.hpp): ntris x 4 floats
+// (m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle, flags bits; flags 0 = no record)
+std::vector<float> mesh_edge_info(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects);
 
 // The built-in synthetic arena mesh (include/rlgpu_arena_mesh.h) in bullet units (uu / 50).
 std::vector<float> builtin_mesh_bt();

@@ -405,11 +405,21 @@ DEV void xs_load(f32x4_t (&v)[XK / 16][2], const RowPtrs& rows, const float* bas
         }
     }
 }
-template <bool KMAJ, int XK, bool H3>
-DEV void xs_store(uint16_t (*lds)[BM][XK + XPAD], const f32x4_t (&v)[XK / 16][2], float sc) {
+// Unpadded 32-deep planes (row pitch P == XK == 32 halves, 64 B) are XOR-swizzled instead of padded:
+// the 16-byte chunk c of row r sits at chunk c ^ ((r >> 2) & 3).  Then both the staging stores
+// (ds_write_b128: 8 lanes = 2 rows x 4 chunks, one 128-byte span) and the fragment reads
+// (ds_read_b128: 16 lanes = rows {0-3, 12-15, 20-27} + 32 u, one chunk) are conflict-free; the
+// padded pitch (80 B) left the stores 2-way conflicted.
+template <int P, int XK>
+DEV int xchunk(int row, int c) {  // physical chunk of logical chunk c
+    static_assert(P != XK || XK == 32, "swizzled planes are 32 deep");
+    return P == XK ? (c ^ ((row >> 2) & 3)) : c;
+}
+template <bool KMAJ, int XK, bool H3, int P = XK + XPAD>
+DEV void xs_store(uint16_t (*lds)[BM][P], const f32x4_t (&v)[XK / 16][2], float sc) {
 #pragma unroll
     for (int q = 0; q < XK / 16; q++) {
-        const int row = xs_row<KMAJ, XK>(q), c = xs_kg<KMAJ, XK>(q) * 8;
+        const int row = xs_row<KMAJ, XK>(q), c = xchunk<P, XK>(row, xs_kg<KMAJ, XK>(q)) * 8;
         if (H3) {
             u32x4_t h, l;
             split2h(v[q], sc, h, l);
@@ -443,14 +453,15 @@ DEV void xp_load(u32x4_t (&v)[NP][XK / 16], const uint16_t* B, int64_t ldb, int6
             v[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? B + p * plane + off : reinterpret_cast<const uint16_t*>(g_zero_row));
     }
 }
-template <int XK, int NP>
-DEV void xp_store(uint16_t (*lds)[BM][XK + XPAD], const u32x4_t (&v)[NP][XK / 16]) {
+template <int XK, int NP, int P = XK + XPAD>
+DEV void xp_store(uint16_t (*lds)[BM][P], const u32x4_t (&v)[NP][XK / 16]) {
     constexpr int KG = XK / 8;
 #pragma unroll
     for (int q = 0; q < XK / 16; q++) {
         const int e = threadIdx.x + 256 * q;
+        const int c = xchunk<P, XK>(e / KG, e % KG) * 8;
 #pragma unroll
-        for (int p = 0; p < NP; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e / KG][(e % KG) * 8]) = v[p][q];
+        for (int p = 0; p < NP; p++) *reinterpret_cast<u32x4_t*>(&lds[p][e / KG][c]) = v[p][q];
     }
 }
 
@@ -636,12 +647,12 @@ DEV h16x8 tr_frag(const uint16_t* plane, int ob, int kof0, int lane) {
     return __builtin_bit_cast(h16x8, r);
 }
 
-template <int XK, bool TA = false, bool TB = false>
-DEV void h3_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
+template <int XK, bool TA = false, bool TB = false, int P = XK + XPAD>
+DEV void h3_mfma_stage(const uint16_t (*As)[BM][P], const uint16_t (*Bs)[BN][P], int ra, int rb, int lane,
                        f32x16 (&acc)[2][2], f32x16 (&cor)[2][2]) {
 #pragma unroll
     for (int ks = 0; ks < XK / 16; ks++) {
-        const int kof = ks * 16 + 8 * (lane >> 5);
+        const int kc = 2 * ks + (lane >> 5);  // logical 16-byte chunk of this lane's 8 k
         h16x8 a[2][2], b[2][2];
 #pragma unroll
         for (int p = 0; p < 2; p++)
@@ -649,9 +660,9 @@ DEV void h3_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)
             for (int u = 0; u < 2; u++) {
                 // ra / rb: this lane's row; (ra & ~31) the wave's 32-row block base
                 a[p][u] = TA ? tr_frag(&As[p][0][0], (ra & ~31) + 32 * u, ks * 16, lane)
-                             : *(const h16x8*)&As[p][ra + 32 * u][kof];
+                             : *(const h16x8*)&As[p][ra + 32 * u][xchunk<P, XK>(ra + 32 * u, kc) * 8];
                 b[p][u] = TB ? tr_frag(&Bs[p][0][0], (rb & ~31) + 32 * u, ks * 16, lane)
-                             : *(const h16x8*)&Bs[p][rb + 32 * u][kof];
+                             : *(const h16x8*)&Bs[p][rb + 32 * u][xchunk<P, XK>(rb + 32 * u, kc) * 8];
             }
         // one accumulator: the corrections, then the leading product, enter the running f32 sum (the
         // rounding count of an f32 FMA chain; a separate correction accumulator would cost 64
@@ -674,8 +685,11 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
     // H3 with 32-deep stages: row-index-contiguous operands staged k-major (xt_load / tr_frag)
     constexpr bool TA = H3 && !AK && XK == 32, TB = H3 && !BPRE && !BKM && XK == 32;
-    __shared__ uint16_t As[NB][NP][BM][XK + XPAD];
-    __shared__ uint16_t Bs[NB][NP][BN][XK + XPAD];
+    // H3 with both operands k-contiguous, default variant: unpadded XOR-swizzled planes (xchunk)
+    constexpr bool SWZ = H3 && !TA && !TB && XK == 32 && V == 0;
+    constexpr int P = SWZ ? XK : XK + XPAD;
+    __shared__ uint16_t As[NB][NP][BM][P];
+    __shared__ uint16_t Bs[NB][NP][BN][P];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wm = w >> 1, wn = w & 1;
     const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
@@ -725,24 +739,24 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
                 *reinterpret_cast<f32x4_t*>(&As[buf][0][row][c]) = va[q][0];
                 *reinterpret_cast<f32x4_t*>(&As[buf][1][row][c]) = va[q][1];
             }
-            if (BPRE) xp_store<XK, NP>(Bs[buf], vp);
+            if (BPRE) xp_store<XK, NP, P>(Bs[buf], vp);
             return;
         }
         if constexpr (TA)
             xt_store(As[buf], va, sa);
         else
-            xs_store<AK, XK, H3>(As[buf], va, sa);
+            xs_store<AK, XK, H3, P>(As[buf], va, sa);
         if (BPRE)
-            xp_store<XK, NP>(Bs[buf], vp);
+            xp_store<XK, NP, P>(Bs[buf], vp);
         else if constexpr (TB)
             xt_store(Bs[buf], vb, sb);
         else
-            xs_store<BKM, XK, H3>(Bs[buf], vb, sb);
+            xs_store<BKM, XK, H3, P>(Bs[buf], vb, sb);
     };
     auto mfma_stage = [&](int buf) {
         if (V == 9 || V == 10) return;
-        if (H3)
-            h3_mfma_stage<XK, TA, TB>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
+        if constexpr (H3)
+            h3_mfma_stage<XK, TA, TB, P>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
         else
             x6_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
     };
@@ -1449,7 +1463,7 @@ template <int MAXH>
 constexpr int lnf_rf() {
     return MAXH <= 8 ? 4 : (MAXH <= 16 ? 2 : 1);
 }
-template <int MAXH>
+template <int MAXH, int ROWS = LNF_ROWS, int RFX = lnf_rf<MAXH>()>
 __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const float* gamma, const float* beta, int R, int H,
                                                      float slope, int use_ln, float* act, float2* stats, float* amax,
                                                      const float* head_w = nullptr, const float* head_b = nullptr,
@@ -1464,13 +1478,13 @@ __global__ void __launch_bounds__(256) ln_act_fwd_f32(const float* Z, const floa
         g[q] = (use_ln && c < H) ? gamma[c] : 1.f;
         b[q] = (use_ln && c < H) ? beta[c] : 0.f;
     }
-    constexpr int RF = lnf_rf<MAXH>();
-    for (int i0 = 0; i0 < LNF_ROWS / 4; i0 += RF) {
+    constexpr int RF = RFX;
+    for (int i0 = 0; i0 < ROWS / 4; i0 += RF) {
         int row[RF];
         float v[RF][MAXH];
 #pragma unroll
         for (int r = 0; r < RF; r++) {  // all RF rows' loads first (a row past R reloads row R-1)
-            row[r] = blockIdx.x * LNF_ROWS + (i0 + r) * 4 + wv;
+            row[r] = blockIdx.x * ROWS + (i0 + r) * 4 + wv;
             const float* z = Z + (int64_t)min(row[r], R - 1) * H;
             if (vec) {
 #pragma unroll
@@ -1638,7 +1652,10 @@ __global__ void __launch_bounds__(256) ln_act_fwd_bf16(const uint16_t* Z, const 
 // Columns per lane: lcol (float4 loads / stores); gamma / beta stay in registers; each of the 4
 // waves walks LNB_ROWS/4 rows.
 constexpr int LNB_ROWS = 32;
-template <int MAXH, bool HEAD = false>
+constexpr int LNB_ROWS_MIN = 16;  // fewest rows per block of any variant (partial buffers are sized for it)
+// ROWS rows per block, PR rows per wave and pass (loads issued before the reductions); every wave
+// adds its rows to its partials in ascending order whatever PR is, so PR changes no bit
+template <int MAXH, bool HEAD = false, int ROWS = LNB_ROWS, int PR = 2>
 __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* Z, const float2* stats, const float* gamma,
                                                  const float* beta, int R, int H, float slope, int use_ln, float* dZ,
                                                  float* part, float* amax, const float* head_dv = nullptr,
@@ -1658,17 +1675,18 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
         hw[q] = (!dA && c < H) ? head_w[c] : 0.f;
         pg[q] = pb[q] = pz[q] = ph[q] = 0.f;
     }
-    const int r0 = blockIdx.x * LNB_ROWS;
-    // two rows per wave and pass: both rows' loads are issued before either row's reductions
-    for (int rr = w; rr < LNB_ROWS; rr += 8) {
-        float xs[2][MAXH], as[2][MAXH];
-        float2 sts[2];
-        float dvs[2] = {0.f, 0.f};
+    const int r0 = blockIdx.x * ROWS;
+    // PR rows per wave and pass: all their loads are issued before any row's reductions
+    for (int rr = w; rr < ROWS; rr += 4 * PR) {
+        float xs[PR][MAXH], as[PR][MAXH];
+        float2 sts[PR];
+        float dvs[PR];
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < PR; j++) {
+            dvs[j] = 0.f;
             const int row = r0 + rr + 4 * j;
             const bool ok = row < R;
-            const int rw = ok ? row : r0 + rr;  // a valid row (its values are not used)
+            const int rw = ok ? row : R - 1;  // a valid row (its values are not used)
             const float* da = dA + (int64_t)rw * H;
             const float* xh = Z + (int64_t)rw * H;  // pre-norm z; xhat recomputed below
             sts[j] = stats[rw];
@@ -1701,7 +1719,7 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
             }
         }
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < PR; j++) {
         const int row = r0 + rr + 4 * j;
         if (row >= R) break;
         const float2 st = sts[j];
@@ -1816,6 +1834,30 @@ inline decltype(&ln_act_bwd<16, true>) ln_act_bwd_head_any(int H) {
     if (H <= 512) return &ln_act_bwd<8, true>;
     if (H <= 1024) return &ln_act_bwd<16, true>;
     return &ln_act_bwd<32, true>;
+}
+
+// Row-shape variants of the H in (256, 512] kernels (host: RLGPU_LNF_VARIANT / RLGPU_LNB_VARIANT):
+// rows per block and rows in flight per wave.  Same bits for any forward variant; a backward
+// variant with other rows per block regroups the column partials (fp32 sums in another order).
+inline decltype(&ln_act_fwd_f32<8>) ln_act_fwd_f32_pick(int H, int v, int* rows) {
+    *rows = LNF_ROWS;
+    if (H > 256 && H <= 512) switch (v) {
+            case 1: *rows = 32; return &ln_act_fwd_f32<8, 32, 4>;
+            case 2: *rows = 8; return &ln_act_fwd_f32<8, 8, 2>;
+            case 3: *rows = 64; return &ln_act_fwd_f32<8, 64, 4>;
+            default: break;
+        }
+    return ln_act_fwd_f32_any(H);
+}
+inline decltype(&ln_act_bwd<8>) ln_act_bwd_pick(int H, bool head, int v, int* rows) {
+    *rows = LNB_ROWS;
+    if (H > 256 && H <= 512) switch (v) {
+            case 1: *rows = 16; return head ? &ln_act_bwd<8, true, 16, 2> : &ln_act_bwd<8, false, 16, 2>;
+            case 2: return head ? &ln_act_bwd<8, true, 32, 4> : &ln_act_bwd<8, false, 32, 4>;
+            case 3: *rows = 64; return head ? &ln_act_bwd<8, true, 64, 4> : &ln_act_bwd<8, false, 64, 4>;
+            default: break;
+        }
+    return head ? ln_act_bwd_head_any(H) : ln_act_bwd_any(H);
 }
 
 // Rank-1 output layer (the critic's Linear(H, 1)): GEMM tiles would be 1/128 occupied, so the

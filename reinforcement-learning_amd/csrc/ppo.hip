@@ -109,6 +109,19 @@ inline int h3_ring() {
     return v;
 }
 inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
+// LayerNorm row-shape variants (mlp::ln_act_fwd_f32_pick / ln_act_bwd_pick), for microbenchmarks
+inline int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+inline int lnf_variant() {
+    static const int v = env_int("RLGPU_LNF_VARIANT", 0);
+    return v;
+}
+inline int lnb_variant() {
+    static const int v = env_int("RLGPU_LNB_VARIANT", 0);
+    return v;
+}
 inline bool split_mode_(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
 inline int gemm_slots(int mode) {
     // H3 variant 0: 146 / 156 VGPRs (forward / weight-gradient instances), 40 KB LDS -> three
@@ -540,7 +553,9 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
         const bool fuse = head1 && l == nh - 1;
         // bytes: z read, act written, (mean, rstd) written
         ktime::Span span(ktime::LN_FWD, (double)n * (8.0 * L.out + 8.0), s);
-        hipLaunchKernelGGL(mlp::ln_act_fwd_f32_any(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
+        int lnf_rows = 0;
+        const auto lnf = mlp::ln_act_fwd_f32_pick(L.out, lnf_variant(), &lnf_rows);
+        hipLaunchKernelGGL(lnf, dim3(ceil_div(n, lnf_rows)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
                            amax_slot(m, l), fuse ? P + O->w : nullptr, fuse ? P + O->b : nullptr, fuse ? out : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
@@ -622,15 +637,17 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
     }
     for (int l = nh - 1; l >= 0; l--) {
         const Layer& L = m.L[l];
-        int nb = (int)ceil_div(n, mlp::LNB_ROWS);
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool r1 = rank1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
+        int lnb_rows = 0;
+        const auto lnb = mlp::ln_act_bwd_pick(L.out, r1, lnb_variant(), &lnb_rows);
+        const int nb = (int)ceil_div(n, lnb_rows);
         const float* dA_in = l == nh - 1 ? dA_top : m.dA;
         {
         // bytes: dA (recomputed for the rank-1 head: its dv instead), z, stats read; dZ written
         ktime::Span span(ktime::LN_BWD, (double)n * ((r1 ? 4.0 : 4.0 * L.out) + 8.0 * L.out + 8.0), s);
-        hipLaunchKernelGGL(r1 ? mlp::ln_act_bwd_head_any(L.out) : mlp::ln_act_bwd_any(L.out), dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
+        hipLaunchKernelGGL(lnb, dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
                            reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
                            h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
                            r1 ? P + O->w : nullptr, r1 ? m.hpart : nullptr);
@@ -961,7 +978,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                     // splits_for is non-decreasing in the row count, and z = ceil(n / chunk) <= splits
                     wpart_max = std::max<int64_t>(wpart_max, (int64_t)splits_for(m.mode, (int)R, L.out, L.in) * L.in * L.out);
                 }
-            int64_t nb = ceil_div(R, std::min(std::min(mlp::LNB_ROWS, mlp::CS_ROWS), ppo::PL_ROWS));
+            int64_t nb = ceil_div(R, std::min(std::min(mlp::LNB_ROWS_MIN, mlp::CS_ROWS), ppo::PL_ROWS));
             for (int mi = 0; mi < h->nm; mi++) {
                 Model& m = h->M[mi];
                 if (!m.head_only) {

@@ -179,3 +179,15 @@ def procedural_soccar(arc_segments=10, length_segments=36, goal_segments=10):
         sides = [np.stack(np.broadcast_arrays(gx, ys[:, None], zs[None, :]), -1) for gx in (-GW, GW)]
         objs.append(np.concatenate([grid(p * s) for p in sides]))
     return ArenaMesh(objs)
+
+
+def edge_info(mesh):
+    """The internal-edge records the env set builds for `mesh` (rlgpu_mesh_edge_info): [ntris, 4]
+    float32 -- the angle to the neighbour across edges V0V1, V1V2, V2V0 (2 pi: no neighbour) and the
+    TRI_INFO_* flags as int32 bits (1 << 30: the triangle has a record)."""
+    L = _bind()
+    L.rlgpu_mesh_edge_info.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    out = np.zeros((mesh.num_tris, 4), np.float32)
+    _lib.check(L.rlgpu_mesh_edge_info(mesh.tris.ctypes.data, mesh.num_tris, mesh.object_ntris.ctypes.data,
+                                      mesh.num_objects, out.ctypes.data), "rlgpu_mesh_edge_info")
+    return out

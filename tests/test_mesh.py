@@ -136,3 +136,49 @@ def test_oracle_car_ball_hit_registers():
     vb = s2["ball"][0]["vel"] * BT_TO_UU
     vc = s2["cars"][0]["body"]["vel"][0] * BT_TO_UU
     assert vb[1] > vc[1] + 300, (vb, vc)
+
+
+def _edge_flags(info):
+    return info[:, 3].view(np.int32)
+
+
+@pytest.mark.parametrize("which", ["procedural_soccar", "test_mesh"])
+def test_internal_edge_info_matches_oracle(which):
+    """btGenerateInternalEdgeInfo (RocketSim.cpp:166-170, btInternalEdgeUtility.cpp:50-358): the
+    library's records (built at env-set create for the kernel) equal the oracle's independent
+    restatement bit for bit, on the SOCCAR-sized procedural mesh and the test mesh."""
+    from rlgpu.mesh import edge_info, procedural_soccar
+    if which == "procedural_soccar":
+        mesh = procedural_soccar()
+    else:
+        t, o = mesh_from_objects(procedural_arena_mesh())
+        mesh = ArenaMesh([t[s:e] for s, e in zip(np.r_[0, np.cumsum(o)[:-1]], np.cumsum(o))])
+    got = edge_info(mesh)
+    want = oracle.mesh_edge_info(mesh.tris, mesh.object_ntris)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    flags = _edge_flags(got)
+    assert (flags & (1 << 30)).mean() > 0.95  # tessellated surfaces: almost every triangle has a neighbour
+
+
+def test_internal_edge_info_known_answers():
+    """Two triangles of a flat quad: the shared diagonal has angle 0 (planar); a 90-degree fold: the
+    angle is +-pi/2 with the convex flag when the fold is convex; edges without a neighbour keep 2 pi."""
+    from rlgpu.mesh import edge_info
+    two_pi = np.float32(2 * np.float32(np.pi))
+    quad = np.float32([[0, 0, 0, 1, 0, 0, 1, 1, 0], [0, 0, 0, 1, 1, 0, 0, 1, 0]])
+    info = edge_info(ArenaMesh([quad]))
+    # triangle 0 shares V0 and V2 with triangle 1: its V2V0 edge; triangle 1 shares its V0V1 edge
+    assert info[0, 2] == 0 and info[1, 0] == 0
+    assert info[0, 0] == two_pi and info[0, 1] == two_pi
+    # convex fold: floor triangle + wall triangle rising along the shared edge x = 1 (a box corner seen
+    # from outside) vs concave fold (a wall rising from the floor's far edge, seen from inside)
+    floor = [0, 0, 0, 1, 0, 0, 1, 1, 0]
+    convex = np.float32([floor, [1, 0, 0, 1, 0, -1, 1, 1, 0]])
+    concave = np.float32([floor, [1, 0, 0, 1, 1, 0, 1, 0, 1]])
+    for tris, is_convex in ((convex, True), (concave, False)):
+        info = edge_info(ArenaMesh([tris]))
+        want = oracle.mesh_edge_info(tris)
+        np.testing.assert_array_equal(info.view(np.uint32), want.view(np.uint32))
+        a = info[0, 1]  # triangle 0's V1V2 edge is the fold
+        assert abs(abs(a) - np.pi / 2) < 1e-5, a
+        assert bool(_edge_flags(info)[0] & 2) == is_convex  # TRI_INFO_V1V2_CONVEX
