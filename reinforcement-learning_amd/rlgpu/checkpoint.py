@@ -18,11 +18,13 @@ Linear), which libtorch's torch::load(seq, stream) reads into the reference's Se
 (verified by tools/lt_load_check.cpp, tests/test_checkpoint.py), so a GPU-trained policy loads in
 the reference's InferUnit / RLBotClient; reference-written POLICY.lt / CRITIC.lt load here.
 
-Optimizer state: the reference writes <NAME>_OPTIM.lt with torch::optim::AdamW::save, keyed by
-tensor addresses; it tolerates the file being absent (warns and resets the optimizer,
-Models.cpp:168-186).  This module keeps the exact AdamW state (step, exp_avg, exp_avg_sq in the
-flat torch parameter order) in RLGPU_OPTIM.safetensors next to the model files, which the
-reference ignores; loading a checkpoint without it resets the optimizer, as the reference does.
+Optimizer state: the reference writes <NAME>_OPTIM.lt with torch::optim::AdamW::save into a
+torch::serialize archive (Models.cpp:116-126) and reads it back with AdamW::load (state keyed by
+parameter address, mapped back by parameter order; a missing file resets the optimizer with a
+warning, Models.cpp:168-186).  Here the same archives are written and read by libtorch itself
+(rlgpu/rlgpu_optim_lt, host/optim_archive.cpp), so a reference checkpoint resumes with its AdamW state
+and a GPU checkpoint resumes in the reference with ours.  The exact state (step, exp_avg, exp_avg_sq
+in the flat torch parameter order) is also kept in RLGPU_OPTIM.safetensors, which load() prefers.
 """
 import json
 import os
@@ -32,6 +34,7 @@ import warnings
 STATS_FILE = "RUNNING_STATS.json"          # Learner.cpp:221
 MODEL_NAMES = ("policy", "critic", "shared_head")  # PPOLearner model names (PPOLearner.cpp:42-74)
 OPTIM_FILE = "RLGPU_OPTIM.safetensors"
+OPTIM_TOOL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rlgpu_optim_lt")
 
 
 def model_path(folder, name, suffix=""):
@@ -44,6 +47,57 @@ def numbered_dirs(base):
     if not os.path.isdir(base):
         return set()
     return {int(n) for n in os.listdir(base) if n.isdigit() and os.path.isdir(os.path.join(base, n))}
+
+
+def _shape_args(shapes):
+    return ["x".join(str(int(d)) for d in s) for s in shapes]
+
+
+def write_optim_archive(path, shapes, step, lr, betas, eps, weight_decay, exp_avg, exp_avg_sq):
+    """<NAME>_OPTIM.lt via libtorch's AdamW::save (Models.cpp:122-125).  shapes: the model's parameter
+    shapes in parameters() order; exp_avg / exp_avg_sq: their moments, flat in that order."""
+    import subprocess
+    import tempfile
+
+    import numpy as np
+    if not os.path.exists(OPTIM_TOOL):
+        raise FileNotFoundError(f"{OPTIM_TOOL} is not built (__graft_entry__.build / make optim)")
+    state = np.concatenate([np.asarray(exp_avg, np.float32).ravel(), np.asarray(exp_avg_sq, np.float32).ravel()])
+    with tempfile.NamedTemporaryFile(suffix=".f32", delete=False) as f:
+        state.tofile(f)
+        tmp = f.name
+    try:
+        r = subprocess.run([OPTIM_TOOL, "save", path, tmp, str(int(step)), repr(float(lr)), repr(float(betas[0])),
+                            repr(float(betas[1])), repr(float(eps)), repr(float(weight_decay)), *_shape_args(shapes)],
+                           capture_output=True, text=True)
+    finally:
+        os.unlink(tmp)
+    if r.returncode != 0:
+        raise RuntimeError(f"writing {path} failed: {r.stderr.strip()}")
+
+
+def read_optim_archive(path, shapes):
+    """(step, exp_avg, exp_avg_sq) of a <NAME>_OPTIM.lt read by libtorch's AdamW::load
+    (Models.cpp:177-180) into parameters of `shapes`; parameters without state read as zeros."""
+    import subprocess
+    import tempfile
+
+    import numpy as np
+    if not os.path.exists(OPTIM_TOOL):
+        raise FileNotFoundError(f"{OPTIM_TOOL} is not built (__graft_entry__.build / make optim)")
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        tmp = f.name
+    try:
+        r = subprocess.run([OPTIM_TOOL, "load", path, tmp, *_shape_args(shapes)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reading {path} failed: {r.stderr.strip()}")
+        raw = open(tmp, "rb").read()
+    finally:
+        os.unlink(tmp)
+    n = sum(int(np.prod(s)) for s in shapes)
+    step = int(np.frombuffer(raw[:8], np.int64)[0])
+    v = np.frombuffer(raw[8:], np.float32)
+    return step, v[:n].copy(), v[n:2 * n].copy()
 
 
 def write_model(seq, path):
@@ -128,7 +182,8 @@ def read_model_state(path):
 
 def save(learner, folder, keep=8):
     """Learner::Save: <folder>/<total_timesteps>/{RUNNING_STATS.json, POLICY.lt, CRITIC.lt,
-    [SHARED_HEAD.lt,] RLGPU_OPTIM.safetensors}, then prune to `keep` checkpoints (-1 keeps all).
+    [SHARED_HEAD.lt,] POLICY_OPTIM.lt, CRITIC_OPTIM.lt, [SHARED_HEAD_OPTIM.lt,] RLGPU_OPTIM.safetensors}, then
+    prune to `keep` checkpoints (-1 keeps all).
     Returns the path."""
     import torch
     from safetensors.torch import save_file
@@ -139,8 +194,11 @@ def save(learner, folder, keep=8):
     with open(os.path.join(path, STATS_FILE), "w") as f:
         json.dump(stats, f, indent=4)
     ppo = learner.ppo
+    shapes = {}
     for mi in ppo.models:
-        write_model(ppo.torch_module(mi), model_path(path, MODEL_NAMES[mi]))
+        mod = ppo.torch_module(mi)
+        shapes[mi] = [tuple(p.shape) for p in mod.parameters()]
+        write_model(mod, model_path(path, MODEL_NAMES[mi]))
     step, m, v = ppo.optimizer_state()
     t = {"step": torch.tensor([step], dtype=torch.int64)}
     for mi in ppo.models:
@@ -149,6 +207,15 @@ def save(learner, folder, keep=8):
         t[name + ".exp_avg"] = m[o:o + c].detach().cpu().contiguous()
         t[name + ".exp_avg_sq"] = v[o:o + c].detach().cpu().contiguous()
     save_file(t, os.path.join(path, OPTIM_FILE))
+    # the reference's <NAME>_OPTIM.lt (Model::Save with saveOptim)
+    opts = getattr(ppo, "optim_options", None)
+    if opts is None or not os.path.exists(OPTIM_TOOL):
+        warnings.warn("*_OPTIM.lt archives not written (no optimizer options or rlgpu_optim_lt not built)")
+    else:
+        for mi in ppo.models:
+            name = MODEL_NAMES[mi]
+            write_optim_archive(model_path(path, name, "_OPTIM"), shapes[mi], step, opts["lr"][mi], opts["betas"], opts["eps"],
+                                opts["weight_decay"], t[name + ".exp_avg"].numpy(), t[name + ".exp_avg_sq"].numpy())
     if keep != -1:
         dirs = numbered_dirs(folder)
         while len(dirs) > keep:
@@ -203,6 +270,26 @@ def load(learner, folder, allow_missing_models=True):
             m[o:o + c].copy_(t[name + ".exp_avg"].to(m.device))
             v[o:o + c].copy_(t[name + ".exp_avg_sq"].to(v.device))
         ppo.set_optimizer_step(int(t["step"][0]))
+    elif any(os.path.exists(model_path(path, MODEL_NAMES[mi], "_OPTIM")) for mi in ppo.models):
+        # a reference checkpoint: its AdamW archives (Model::Load, Models.cpp:168-186); a model
+        # without one resets its moments, as the reference resets that model's optimizer
+        step, m, v = ppo.optimizer_state()
+        steps = []
+        for mi in ppo.models:
+            name = MODEL_NAMES[mi]
+            o, c = ppo.model_range(mi)
+            p = model_path(path, name, "_OPTIM")
+            if not os.path.exists(p) or os.path.getsize(p) == 0:
+                warnings.warn(f"no optimizer found at {p}, optimizer will be reset")
+                m[o:o + c].zero_()
+                v[o:o + c].zero_()
+                continue
+            shapes = [tuple(q.shape) for q in ppo.torch_module(mi).parameters()]
+            s_, ea, eas = read_optim_archive(p, shapes)
+            m[o:o + c].copy_(torch.from_numpy(ea).to(m.device))
+            v[o:o + c].copy_(torch.from_numpy(eas).to(v.device))
+            steps.append(s_)
+        ppo.set_optimizer_step(max(steps) if steps else 0)
     else:
         warnings.warn(f"no optimizer state found in {path}, optimizer will be reset")
         step, m, v = ppo.optimizer_state()

@@ -365,7 +365,9 @@ class Learner:
         max_rows = max(min(cfg.mini_batch_size, rows_cap), min(4 * cfg.num_arenas, 65536))  # host/learner.cpp
         self.ppo = PPO.wrap(ph.value, self.device, cfg.policy_layers, cfg.critic_layers, max_rows,
                             obs_size=OBS * max(1, cfg.frame_stack), metrics_source=self._metrics, owner=self,
-                            shared_layers=cfg.shared_layers)
+                            shared_layers=cfg.shared_layers,
+                            optim_options={"lr": (cfg.policy_lr, cfg.critic_lr, min(cfg.policy_lr, cfg.critic_lr)),
+                                           "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 1e-2})
         r = _CRollout()
         _lib.check(L.rlgpu_learner_rollout(h, ctypes.byref(r)), "rlgpu_learner_rollout")
         T, P, W = r.T, r.P, r.obs_width

@@ -122,6 +122,9 @@ class PPO:
         _lib.check(L.rlgpu_ppo_create(ctypes.byref(c), ctypes.byref(h)), "rlgpu_ppo_create")
         self._h = h
         self.cfg = c
+        # AdamW options per model (checkpoint.py's *_OPTIM.lt): the shared head steps at min(LR)
+        self.optim_options = {"lr": (policy_lr, critic_lr, min(policy_lr, critic_lr)), "betas": tuple(betas), "eps": eps,
+                              "weight_decay": weight_decay}
         self.obs_size, self.num_actions = obs_size, num_actions
         self.policy_layers, self.critic_layers, self.layer_norm = tuple(policy_layers), tuple(critic_layers), layer_norm
         self.shared_layers = tuple(shared_layers)
@@ -138,7 +141,7 @@ class PPO:
 
     @classmethod
     def wrap(cls, handle, device, policy_layers, critic_layers, max_rows, obs_size=167, num_actions=90,
-             layer_norm=True, leaky_slope=0.01, metrics_source=None, owner=None, shared_layers=()):
+             layer_norm=True, leaky_slope=0.01, metrics_source=None, owner=None, shared_layers=(), optim_options=None):
         """A PPO view of a handle owned elsewhere (the C++ Learner's PPOLearner): not destroyed
         by this object.  metrics_source(reset) -> (sums, count) replaces the own metric buffer."""
         import torch
@@ -150,6 +153,7 @@ class PPO:
         self.policy_layers, self.critic_layers, self.layer_norm = tuple(policy_layers), tuple(critic_layers), layer_norm
         self.shared_layers = tuple(shared_layers)
         self.leaky_slope, self.max_rows = leaky_slope, max_rows
+        self.optim_options = optim_options
         p, g, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         _lib.check(L.rlgpu_ppo_buffers(self._h, ctypes.byref(p), ctypes.byref(g), ctypes.byref(n)), "rlgpu_ppo_buffers")
         self.num_params = n.value
@@ -162,6 +166,7 @@ class PPO:
 
     _owned = True
     _metrics_source = None
+    optim_options = None
 
     def close(self):
         if getattr(self, "_h", None):

@@ -177,3 +177,50 @@ def test_shared_head_file_loads_in_libtorch(harness, tmp_path):
     assert r.returncode == 0, r.stderr
     got = torch.cat([t.reshape(-1) for t in ckpt.read_model_state(q)]).numpy()
     np.testing.assert_array_equal(got, flat)
+
+
+def _shapes():
+    import torch
+    from rlgpu.ppo import make_sequential
+    seq = make_sequential(ARCH["obs"], ARCH["out"], ARCH["layers"], bool(ARCH["ln"]))
+    return [tuple(p.shape) for p in seq.parameters()]
+
+
+def test_reference_optimizer_archive_reads(harness, tmp_path):
+    """A reference-written <NAME>_OPTIM.lt (libtorch AdamW after 3 steps, saved as Model::Save does,
+    Models.cpp:122-125) reads back through rlgpu's reader -- libtorch's AdamW::load, as Model::Load
+    (Models.cpp:177-180) -- with the exact step and moments, mapped by parameter order."""
+    import numpy as np
+    from rlgpu.checkpoint import OPTIM_TOOL, read_optim_archive
+    if not os.path.exists(OPTIM_TOOL):
+        pytest.skip("rlgpu_optim_lt not built")
+    p, dump = str(tmp_path / "POLICY_OPTIM.lt"), str(tmp_path / "dump.bin")
+    r = subprocess.run([harness, "optim", p, dump, "3", *_args()], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    raw = open(dump, "rb").read()
+    shapes = _shapes()
+    n = sum(int(np.prod(s)) for s in shapes)
+    want_step, want = int(np.frombuffer(raw[:8], np.int64)[0]), np.frombuffer(raw[8:], np.float32)
+    step, m, v = read_optim_archive(p, shapes)
+    assert step == want_step == 3
+    np.testing.assert_array_equal(m, want[:n])
+    np.testing.assert_array_equal(v, want[n:])
+
+
+def test_optimizer_archive_round_trip(tmp_path):
+    """rlgpu's <NAME>_OPTIM.lt writer (libtorch AdamW::save) and reader (AdamW::load) round-trip the
+    step and both moments bit for bit."""
+    import numpy as np
+    from rlgpu.checkpoint import OPTIM_TOOL, read_optim_archive, write_optim_archive
+    if not os.path.exists(OPTIM_TOOL):
+        pytest.skip("rlgpu_optim_lt not built")
+    shapes = _shapes()
+    n = sum(int(np.prod(s)) for s in shapes)
+    rng = np.random.default_rng(2)
+    m, v = rng.standard_normal(n).astype(np.float32), rng.random(n).astype(np.float32)
+    p = str(tmp_path / "CRITIC_OPTIM.lt")
+    write_optim_archive(p, shapes, 41, 2.5e-4, (0.9, 0.999), 1e-8, 1e-2, m, v)
+    step, m2, v2 = read_optim_archive(p, shapes)
+    assert step == 41
+    np.testing.assert_array_equal(m2, m)
+    np.testing.assert_array_equal(v2, v)

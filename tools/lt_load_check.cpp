@@ -10,6 +10,10 @@
 //
 // usage: lt_load_check load <model.lt> <in.f32> <rows> <out.f32> <obs> <out> <ln 0|1> <h1> [h2 ...]
 //        lt_load_check save <params.f32> <model.lt> <obs> <out> <ln 0|1> <h1> [h2 ...]
+//        lt_load_check optim <NAME_OPTIM.lt> <dump.bin> <steps> <obs> <out> <ln 0|1> <h1> [h2 ...]
+// optim: an AdamW over the model's parameters (Models.h:40-56) takes <steps> steps on a seeded loss,
+// then Model::Save's optimizer branch writes the archive (Models.cpp:122-125); dump.bin gets the
+// step (int64) and every parameter's exp_avg, then exp_avg_sq, in parameters() order.
 #include <torch/torch.h>
 
 #include <cstdio>
@@ -42,13 +46,41 @@ int main(int argc, char** argv) {
     if (argc < 2) return 2;
     std::string mode = argv[1];
     bool load = mode == "load";
-    int a = load ? 6 : 4;
+    int a = load ? 6 : (mode == "optim" ? 5 : 4);
     if (argc < a + 4) return 2;
     int obs = std::atoi(argv[a]), out = std::atoi(argv[a + 1]);
     bool ln = std::atoi(argv[a + 2]) != 0;
     std::vector<int> layers;
     for (int i = a + 3; i < argc; i++) layers.push_back(std::atoi(argv[i]));
     torch::nn::Sequential seq = make_model(obs, out, ln, layers);
+    if (mode == "optim") {
+        torch::manual_seed(5);
+        torch::optim::AdamW opt(seq->parameters(), torch::optim::AdamWOptions(2.5e-4));
+        for (int k = 0; k < std::atoi(argv[4]); k++) {
+            auto loss = seq->forward(torch::randn({8, obs})).square().sum();
+            opt.zero_grad();
+            loss.backward();
+            opt.step();
+        }
+        torch::serialize::OutputArchive ar;
+        opt.save(ar);
+        ar.save_to(argv[2]);
+        std::vector<float> m, v;
+        int64_t step = 0;
+        for (auto& p : seq->parameters()) {
+            auto& st = static_cast<torch::optim::AdamWParamState&>(*opt.state().at(p.unsafeGetTensorImpl()));
+            step = st.step();
+            auto a_ = st.exp_avg().contiguous(), b_ = st.exp_avg_sq().contiguous();
+            m.insert(m.end(), a_.data_ptr<float>(), a_.data_ptr<float>() + a_.numel());
+            v.insert(v.end(), b_.data_ptr<float>(), b_.data_ptr<float>() + b_.numel());
+        }
+        FILE* g = std::fopen(argv[3], "wb");
+        std::fwrite(&step, 8, 1, g);
+        std::fwrite(m.data(), 4, m.size(), g);
+        std::fwrite(v.data(), 4, v.size(), g);
+        std::fclose(g);
+        return 0;
+    }
     if (load) {
         auto before = seq_sizes(seq);
         std::ifstream in(argv[2], std::ios::binary);
