@@ -200,6 +200,15 @@ T* Learner::Alloc(size_t count) {
     allocs_.push_back(p);
     return (T*)p;
 }
+void Learner::Release(void* p) {  // an Alloc'd buffer, freed before the destructor
+    for (auto& q : allocs_)
+        if (q == p) {
+            (void)hipFree(q);
+            q = allocs_.back();
+            allocs_.pop_back();
+            return;
+        }
+}
 
 Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, hipStream_t stream)
     : s_(stream), cfg_(cfg) {
@@ -322,6 +331,7 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     perm_ = Alloc<int32_t>(TP);
     permRows_ = Alloc<int32_t>(TP);
     badv_ = Alloc<float>(TP);
+    permCap_ = TP;
     truncRows_ = Alloc<int32_t>(TP);
     truncCount_ = Alloc<int32_t>(1);
     selBytes_ = lk::select_trunc_scratch_bytes(TP);
@@ -493,6 +503,18 @@ void Learner::BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int6
     hipCheck(hipStreamSynchronize(s_), "sync");
 }
 
+// the per-row learn scratch (shuffle, row selection, batch advantages) for M rows
+void Learner::ReserveLearnRows(int64_t M) {
+    if (M <= permCap_) return;
+    const int64_t cap = std::max<int64_t>(M, permCap_ + permCap_ / 2);
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    for (void* p : {(void*)perm_, (void*)permRows_, (void*)badv_}) Release(p);
+    perm_ = Alloc<int32_t>(cap);
+    permRows_ = Alloc<int32_t>(cap);
+    badv_ = Alloc<float>(cap);
+    permCap_ = cap;
+}
+
 void Learner::Learn() {
     const int T = exp_.T, P = exp_.P;
     rlgpu_rollout_view v = exp_.v;
@@ -510,6 +532,7 @@ void Learner::Learn() {
         v.target = traj.cTarget.p;
         if (M <= 0 && !hasColl_) return;  // with ranks, an empty one still joins every collective
     }
+    ReserveLearnRows(M);
     int64_t globalM = M * cfg_.world;
     if (trajMode() && hasColl_) {  // ranks hold different complete-trajectory counts: the true total
         double m = (double)M;

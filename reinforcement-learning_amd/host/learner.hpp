@@ -202,9 +202,11 @@ private:
     // device scratch
     uint8_t* oldRows_[2] = {nullptr, nullptr};
     int32_t* trainRows_ = nullptr;
-    int32_t* perm_ = nullptr;
-    int32_t* permRows_ = nullptr;
-    float* badv_ = nullptr;
+    int32_t* perm_ = nullptr;     // the shuffle, its row-selected form and the gathered batch advantages:
+    int32_t* permRows_ = nullptr; // permCap_ rows each (T * P; grown to the combined batch in the
+    float* badv_ = nullptr;       // trajectory mode, whose row count has no fixed bound)
+    int64_t permCap_ = 0;
+    void ReserveLearnRows(int64_t M);
     int32_t* truncRows_ = nullptr;
     int32_t* truncCount_ = nullptr;
     void* selScratch_ = nullptr;
@@ -224,6 +226,7 @@ private:
     std::vector<void*> allocs_;
     template <class T>
     T* Alloc(size_t count);
+    void Release(void* p);
 };
 
 }  // namespace GGL

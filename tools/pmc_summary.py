@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (run separately, as
 MI355X_MICROARCH.md prescribes) into per-launch HBM bytes for one kernel.
 
-usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel substring> <min grid threads> <out.json>
+usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel substring> <min grid threads> <out.json> [mesh]
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
 coalesced streaming reads -> doubled; WRITE_SIZE is taken as is.  Both counters are in KB.
@@ -19,13 +19,14 @@ def per_launch(path, kernel, min_grid):
 
 def main():
     fdir, wdir, kernel, min_grid, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    mesh = sys.argv[6] if len(sys.argv) > 6 else "synthetic"
     nf, fetch_kb = per_launch(f"{fdir}/run_counter_collection.csv", kernel, min_grid)
     nw, write_kb = per_launch(f"{wdir}/run_counter_collection.csv", kernel, min_grid)
     res = {"kernel": kernel, "launches": [nf, nw], "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
            "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1; KB = 1024 B",
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1; KB = 1024 B", "mesh": mesh,
            "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --output-format csv -- python3 bench.py --steps 1 "
-                      "--warmup 0 --no-cpu-baseline (two separate passes)"}
+                      f"--warmup 0 --no-cpu-baseline --mesh {mesh} (two separate passes)"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
