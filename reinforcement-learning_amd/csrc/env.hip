@@ -100,7 +100,15 @@ DEV void load_pad_regs(PadRegs& R, int l) {
 }
 
 // ------------------------------------------------------------------ one tick (Arena::Step body)
-DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R) {
+// Inlined into the tick loop (RLGPU_TICK_ATTR).  Inlined, the compiler hoists the launch-invariant
+// constant-buffer values of all phases out of the loop (408 VGPR + AGPR, one wave per SIMD);
+// called (__noinline__) the kernel needs 248 VGPRs and could run two waves per SIMD, but measured
+// slower: 870 -> 938 us per launch at 4 arenas per wave, and 2 arenas per wave (two waves per
+// SIMD) 1.7x slower per arena.
+#ifndef RLGPU_TICK_ATTR
+#define RLGPU_TICK_ATTR DEV
+#endif
+RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R) {
     if (valid && l == 0) {
         rlgpu_arena_state& s = A->s;
         bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
@@ -345,7 +353,7 @@ DEV void copy_rows(ArenaLDS* A, int l, int arena, float* obs, uint8_t* masks) {
     }
 }
 
-__global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
+__global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
     __shared__ ArenaLDS lds[kArenas];
     const int team = threadIdx.x >> 4, l = threadIdx.x & 15;
     const int arena = blockIdx.x * kArenas + team;
@@ -357,7 +365,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
         int first = blockIdx.x * kArenas;
         int cnt = g.n - first < kArenas ? g.n - first : kArenas;
         const int chunks = kRec / 16;
-        for (int k = threadIdx.x; k < cnt * chunks; k += 64) {
+        for (int k = threadIdx.x; k < cnt * chunks; k += kWG) {
             int a = k / chunks, c = k % chunks;
             const uint4* src = (const uint4*)(g.arenas + (size_t)(first + a) * kRec) + c;
             uint4* dst = (uint4*)&lds[a] + c;
@@ -553,7 +561,7 @@ __global__ void __launch_bounds__(64) env_kernel(StepArgs g) {
         int first = blockIdx.x * kArenas;
         int cnt = g.n - first < kArenas ? g.n - first : kArenas;
         const int chunks = kRec / 16;
-        for (int k = threadIdx.x; k < cnt * chunks; k += 64) {
+        for (int k = threadIdx.x; k < cnt * chunks; k += kWG) {
             int a = k / chunks, c = k % chunks;
             uint4* dst = (uint4*)(g.arenas + (size_t)(first + a) * kRec) + c;
             const uint4* src = (const uint4*)&lds[a] + c;
@@ -844,7 +852,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
         g.metrics_players = (++e->metric_calls % 4) == 0;
     }
     unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
-    hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(64), 0, s, g);
+    hipLaunchKernelGGL(rl::env_kernel, dim3(blocks), dim3(rl::kWG), 0, s, g);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 

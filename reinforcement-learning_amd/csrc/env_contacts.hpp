@@ -969,7 +969,7 @@ DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
     pmark(P, 20);
     int nlev = valid ? S.nlev : 0;  // workgroup-uniform: the max over its arenas
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) nlev = stdmax(nlev, __shfl_xor(nlev, o, 64));
+    for (int o = kWG / 2; o > 0; o >>= 1) nlev = stdmax(nlev, __shfl_xor(nlev, o, 64));
     const bool mine = valid && l < S.nrows;
     const int lv = mine ? S.lvl[l] : -1;
     // this lane's contact and friction rows stay in registers for the sweeps (only the bodies'

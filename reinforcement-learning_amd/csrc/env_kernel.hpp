@@ -33,7 +33,12 @@
 namespace rl {
 
 constexpr int kTeam = 16;           // lanes per arena
-constexpr int kArenas = 4;          // arenas per 64-thread workgroup
+#ifndef RLGPU_ENV_ARENAS_PER_WG
+#define RLGPU_ENV_ARENAS_PER_WG 4
+#endif
+constexpr int kArenas = RLGPU_ENV_ARENAS_PER_WG;  // arenas per workgroup (one wavefront)
+constexpr int kWG = kArenas * kTeam;               // threads per workgroup
+static_assert(kWG <= 64, "one wavefront per workgroup");
 constexpr int kMaxCand = 64;        // narrowphase candidates per tick per arena
 constexpr int kMaxRows = RLGPU_MAX_SOLVER_ROWS;  // solver contact rows per arena (+ as many friction rows)
 constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic work items ("ranks")

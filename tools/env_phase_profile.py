@@ -29,7 +29,8 @@ acts = torch.empty(4 * n, dtype=torch.int32, device=dev)
 for i in range(warm):
     acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
     env.step(acts, True)
-wg = (n + 3) // 4
+APW = int(os.environ.get("RLGPU_ENV_APW", "4"))  # arenas per workgroup of the built library (env_kernel.hpp)
+wg = (n + APW - 1) // APW
 KP, KW = 24, 64  # env_kernel.hpp kProfPhases, kProfWG
 prof = torch.zeros(KW + wg * KP, dtype=torch.int64, device=dev)
 spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
