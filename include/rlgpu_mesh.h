@@ -46,6 +46,17 @@ int rlgpu_mesh_known_hash(int32_t game_mode, uint32_t hash);
  * has a record, 0 = none).  Host only. */
 int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects, float* out);
 
+/* The car-hitbox vs mesh-triangle narrowphase of the env kernel on its own (the GJK / EPA query of
+ * btConvexTriangleCallback::processTriangle -> btConvexConvexAlgorithm -> btGjkPairDetector with
+ * btGjkEpaPenetrationDepthSolver, btConvexConcaveCollisionAlgorithm.cpp:71-138 and
+ * btGjkPairDetector.cpp:686-959), on the device, one query per lane: n queries of device arrays rot
+ * [n][9] (box basis rows), centre [n][3] (hitbox child origin), tri [n][9] (three vertices), cbt [n]
+ * (contact breaking threshold); the box is the Octane hitbox.  d_out [n][8] = {hit, normal xyz,
+ * point xyz, depth} (the arguments of btManifoldResult::addContactPoint; zeros when no point).
+ * Asynchronous on `stream`; scratch for the penetration solver is allocated per call. */
+int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
+                               const float* d_cbt, float* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -229,3 +229,45 @@ def mesh_edge_info(tris, object_ntris=None):
     f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     f(_p(tris), len(tris), _p(objs), 0 if objs is None else len(objs), _p(out))
     return out
+
+
+def car_box_shape():
+    """The Octane hitbox as btBoxShape holds it -> (implicit half extents [3], margin, half extents with
+    margin [3]) (btBoxShape.cpp:18-26 + setSafeMargin, btConvexInternalShape.h:63-78)."""
+    impl, half, m = np.zeros(3, np.float32), np.zeros(3, np.float32), np.zeros(1, np.float32)
+    f = lib().oracle_car_box_shape
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p] * 3
+    f(_p(impl), _p(m), _p(half))
+    return impl, float(m[0]), half
+
+
+def box_triangle(rot, centre, tri, cbt):
+    """oracle_box_triangle (gjk_ref.hpp): n car-hitbox vs triangle queries as Bullet runs them (normal
+    early out, GJK with margins, GJK/EPA penetration solver, normal fix).  rot [n,3,3] rows, centre [n,3],
+    tri [n,3,3], cbt [n] -> (out [n,8] = hit, normal, point, depth; counts [2] = GJK queries, penetration-
+    solver calls)."""
+    rot = np.ascontiguousarray(rot, np.float32).reshape(-1, 9)
+    n = len(rot)
+    centre = np.ascontiguousarray(centre, np.float32).reshape(n, 3)
+    tri = np.ascontiguousarray(tri, np.float32).reshape(n, 9)
+    cbt = np.ascontiguousarray(np.broadcast_to(np.asarray(cbt, np.float32), (n,)))
+    out = np.zeros((n, 8), np.float32)
+    counts = np.zeros(2, np.uint64)
+    f = lib().oracle_box_triangle
+    f.restype = None
+    f.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 6
+    f(n, _p(rot), _p(centre), _p(tri), _p(cbt), _p(out), _p(counts))
+    return out, counts
+
+
+def gjk_counts():
+    """This thread's box-triangle GJK queries, penetration-solver calls, EPA runs, EPA iterations, most
+    iterations of one EPA run and most polytope faces one run took, inside oracle arena steps and
+    box_triangle() calls since the last call (diagnostics)."""
+    c = np.zeros(6, np.uint64)
+    f = lib().oracle_gjk_counts
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p]
+    f(_p(c))
+    return c

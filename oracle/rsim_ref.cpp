@@ -20,8 +20,8 @@
 // Documented deviations from the reference (also in DESIGN.md):
 //   * synthetic arena mesh (include/rlgpu_arena_mesh.h) by default; real .cmf meshes can be
 //     loaded (World::set_mesh), one collision object per file;
-//   * box-triangle and box-box contacts use SAT (1 point) instead of GJK/EPA / btBoxBoxDetector;
-//   * internal-edge normal adjustment (btAdjustInternalEdgeContacts) is not applied;
+//   * box-box (car-car) contacts use SAT (1 point) instead of btBoxBoxDetector (box-triangle runs
+//     Bullet's GJK / EPA, gjk_ref.hpp);
 //   * time-based deactivation (btRigidBody.h:531-545) is not modelled -- only the zero-velocity
 //     ball sleep of Arena.cpp:722-727;
 //   * pairs are processed in a canonical order (per body: mesh objects, planes; then the dynamic
@@ -35,8 +35,12 @@
 
 #include "../include/rlgpu_arena_mesh.h"
 #include "../include/rlgpu_detmath.h"
+#include "gjk_ref.hpp"
 
 namespace orc {
+
+// diagnostics: box-triangle GJK queries and penetration-solver (EPA) calls on this thread
+thread_local uint64_t gjk_evals[2] = {0, 0};
 
 // ------------------------------------------------------------------ constants (RLConst.h)
 const float UU_TO_BT = 1.f / 50.f;  // BulletLink.h:15
@@ -89,8 +93,22 @@ World::World() {
     // Octane (CarConfig.cpp:20-70): box half extents through btBoxShape margin handling
     V hs = V(120.507f, 86.6994f, 38.6591f) * UU_TO_BT;
     V h(hs.x / 2.f, hs.y / 2.f, hs.z / 2.f);
-    const float margin = 0.04f;
-    car_half = V((h.x - margin) + margin, (h.y - margin) + margin, (h.z - margin) + margin);
+    // btBoxShape(halfExtents) (btBoxShape.cpp:18-26): implicit = half - 0.04 (CONVEX_DISTANCE_MARGIN), then
+    // setSafeMargin(half) (btConvexInternalShape.h:63-78) lowers the margin to 0.1 x the smallest half
+    // extent when that is below 0.04 (Octane: 0.0386591) and btBoxShape::setMargin (btBoxShape.h:84-92)
+    // moves the difference into the implicit dimensions
+    const float m0 = 0.04f;
+    V impl((h.x - m0), (h.y - m0), (h.z - m0));
+    float mn_half = h[h.x < h.y ? (h.x < h.z ? 0 : 2) : (h.y < h.z ? 1 : 2)];  // btVector3::minAxis
+    float safe = 0.1f * mn_half;
+    car_margin = m0;
+    if (safe < car_margin) {
+        V with_m = impl + V(m0, m0, m0);
+        car_margin = safe;
+        impl = with_m - V(safe, safe, safe);
+    }
+    car_impl = impl;
+    car_half = car_impl + V(car_margin, car_margin, car_margin);  // getHalfExtentsWithMargin
     car_offset = V(13.87566f, 0.f, 20.755f) * UU_TO_BT;
     float lx = 2.f * car_half.x, ly = 2.f * car_half.y, lz = 2.f * car_half.z;  // btBoxShape.cpp
     V inertia = V(ly * ly + lz * lz, lx * lx + lz * lz, lx * lx + ly * ly) * (CAR_MASS / 12.f);
@@ -1475,57 +1493,17 @@ struct Sim {
         V on_plane = vtx - n * dist;
         if (dist < pair_cbt(bi, 10)) add_contact(key, n, on_plane, dist);
     }
-    // SAT separation of an OBB and a triangle; returns false if separated beyond cbt.
-    bool box_triangle(int bi, int t, float cbt, V& nrm, V& point_b, float& depth) const {
-        const M& R = b[bi].rot;
-        V c = car_box_center(bi);
-        V ax[3] = {R.col(0), R.col(1), R.col(2)};
+    // box vs one triangle: btConvexTriangleCallback::processTriangle's normal early out, then GJK with
+    // margins and the GJK/EPA penetration solver (gjk_ref.hpp)
+    bool box_triangle(int bi, int t, float cbt, V& nrm, V& point_b, float& depth) {
+        gjk::Shapes sh;
+        sh.impl = w.car_impl;
+        sh.margin = w.car_margin;
         const V* v = &w.tri[(size_t)t * 3];
-        V e[3] = {v[1] - v[0], v[2] - v[1], v[0] - v[2]};
-        V tn = cross(e[0], v[2] - v[0]);
-        V axes[13];
-        int na = 0;
-        axes[na++] = tn;
-        for (int i = 0; i < 3; i++) axes[na++] = ax[i];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) axes[na++] = cross(ax[i], e[j]);
-        float best = 1e30f;
-        V best_n;
-        for (int k = 0; k < na; k++) {
-            float l2 = len2(axes[k]);
-            if (l2 < 1e-10f) continue;
-            V L = axes[k] / std::sqrt(l2);
-            float r = w.car_half.x * std::fabs(dot(ax[0], L)) + w.car_half.y * std::fabs(dot(ax[1], L)) +
-                      w.car_half.z * std::fabs(dot(ax[2], L));
-            float p0 = dot(v[0], L), p1 = dot(v[1], L), p2 = dot(v[2], L);
-            float tmin = std::min(p0, std::min(p1, p2)), tmax = std::max(p0, std::max(p1, p2));
-            float cl = dot(c, L);
-            float pen_pos = tmax - (cl - r);  // push box along +L
-            float pen_neg = (cl + r) - tmin;  // push box along -L
-            float pen;
-            V n;
-            if (pen_pos < pen_neg) {
-                pen = pen_pos;
-                n = L;
-            } else {
-                pen = pen_neg;
-                n = -L;
-            }
-            if (-pen > cbt) return false;  // separated on this axis
-            if (pen < best) {
-                best = pen;
-                best_n = n;
-            }
-        }
-        nrm = best_n;  // normal on B (triangle) pointing to A (box)
-        depth = -best;
-        // deepest box vertex along -n, then the point on B
-        V dl = vmul(-nrm, R);
-        V lv(dl.x >= 0 ? w.car_half.x : -w.car_half.x, dl.y >= 0 ? w.car_half.y : -w.car_half.y,
-             dl.z >= 0 ? w.car_half.z : -w.car_half.z);
-        V pa = R * lv + c;
-        point_b = pa - nrm * depth;
-        return true;
+        sh.tri[0] = v[0];
+        sh.tri[1] = v[1];
+        sh.tri[2] = v[2];
+        return gjk::box_triangle(b[bi].rot, car_box_center(bi), sh, cbt, nrm, point_b, depth, gjk_evals);
     }
     void collide_box_mesh(int key, int bi, int t0, int t1) {
         V mn, mx;
@@ -1542,8 +1520,8 @@ struct Sim {
     void collide_car_ball(int key, int bi) {
         const M& R = b[bi].rot;
         V c = car_box_center(bi);
-        const float margin = 0.04f;
-        V he((w.car_half.x - margin), (w.car_half.y - margin), (w.car_half.z - margin));
+        const float margin = w.car_margin;  // boxShape->getMargin() (btSphereBoxCollisionAlgorithm.cpp:82-90)
+        V he = w.car_impl;                  // getHalfExtentsWithoutMargin
         V rel = vmul(b[0].pos - c, R);
         V cp(std::max(-he.x, std::min(he.x, rel.x)), std::max(-he.y, std::min(he.y, rel.y)),
              std::max(-he.z, std::min(he.z, rel.z)));
@@ -2225,3 +2203,60 @@ void arena_step(const World& w, rlgpu_arena_state& s, uint64_t seed, int arena_i
 }
 
 }  // namespace orc
+
+// ---------------------------------------------------------------- checker entry points (tests only)
+extern "C" {
+// The Octane hitbox as btBoxShape holds it: implicit half extents, margin, half extents with margin.
+void oracle_car_box_shape(float* impl3, float* margin, float* half3) {
+    const orc::World& w = orc::world();
+    for (int i = 0; i < 3; i++) {
+        impl3[i] = w.car_impl[i];
+        half3[i] = w.car_half[i];
+    }
+    *margin = w.car_margin;
+}
+// n box-triangle queries (gjk_ref.hpp box_triangle): per query rot[9] (rows), centre[3], tri[9] (3
+// vertices), cbt; the box shape is the Octane's.  out[8 per query] = {hit, normal xyz, point xyz, depth}.
+// counts[2] (optional) += GJK queries and penetration-solver calls.
+void oracle_box_triangle(int n, const float* rot, const float* centre, const float* tri, const float* cbt, float* out,
+                         uint64_t* counts) {
+    const orc::World& w = orc::world();
+    orc::gjk::Shapes sh;
+    sh.impl = w.car_impl;
+    sh.margin = w.car_margin;
+    uint64_t ev[2] = {0, 0};
+    for (int i = 0; i < n; i++) {
+        orc::M R;
+        for (int r = 0; r < 3; r++) R.r[r] = orc::V(rot[9 * i + 3 * r], rot[9 * i + 3 * r + 1], rot[9 * i + 3 * r + 2]);
+        orc::V c(centre[3 * i], centre[3 * i + 1], centre[3 * i + 2]);
+        for (int k = 0; k < 3; k++) sh.tri[k] = orc::V(tri[9 * i + 3 * k], tri[9 * i + 3 * k + 1], tri[9 * i + 3 * k + 2]);
+        orc::V nrm, pt;
+        float d = 0;
+        bool hit = orc::gjk::box_triangle(R, c, sh, cbt[i], nrm, pt, d, ev);
+        float* o = out + 8 * i;
+        o[0] = hit ? 1.f : 0.f;
+        o[1] = hit ? nrm.x : 0.f;
+        o[2] = hit ? nrm.y : 0.f;
+        o[3] = hit ? nrm.z : 0.f;
+        o[4] = hit ? pt.x : 0.f;
+        o[5] = hit ? pt.y : 0.f;
+        o[6] = hit ? pt.z : 0.f;
+        o[7] = hit ? d : 0.f;
+    }
+    if (counts) {
+        counts[0] += ev[0];
+        counts[1] += ev[1];
+    }
+}
+// this thread's box-triangle GJK queries / penetration-solver calls inside arena steps, then EPA runs, EPA
+// iterations, most iterations of one run, most faces one run took (reset after reading)
+void oracle_gjk_counts(uint64_t* out6) {
+    out6[0] = orc::gjk_evals[0];
+    out6[1] = orc::gjk_evals[1];
+    orc::gjk_evals[0] = orc::gjk_evals[1] = 0;
+    for (int i = 0; i < 4; i++) {
+        out6[2 + i] = orc::gjk::epa_stats[i];
+        orc::gjk::epa_stats[i] = 0;
+    }
+}
+}  // extern "C"

@@ -15,6 +15,8 @@ extern const float UU_TO_BT, BT_TO_UU, TICK_TIME, CAR_MASS, BALL_MASS;
 struct World {
     float ball_radius, ball_inv_mass, car_inv_mass, ball_cbt, car_cbt, ball_damp, susp_travel;
     V ball_inv_inertia, car_half, car_offset, car_inv_inertia, gravity;
+    V car_impl;        // btBoxShape m_implicitShapeDimensions (half extents without the margin)
+    float car_margin;  // btBoxShape margin after setSafeMargin (0.1 x the smallest half extent)
     V wheel_conn[4];
     float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
     V plane_n[4], plane_p[4];

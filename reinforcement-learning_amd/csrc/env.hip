@@ -589,8 +589,22 @@ static EnvConst make_env_const() {
     k.ball_inv_mass = 1.f / kBallMass;
     v3 hs = v3{120.507f, 86.6994f, 38.6591f} * UU;  // Octane hitbox (CarConfig.cpp:20-70)
     v3 h = v3{hs.x / 2.f, hs.y / 2.f, hs.z / 2.f};
-    const float margin = 0.04f;
-    k.car_half = v3{(h.x - margin) + margin, (h.y - margin) + margin, (h.z - margin) + margin};
+    // btBoxShape (btBoxShape.cpp:18-26): implicit = half - 0.04, then setSafeMargin(half)
+    // (btConvexInternalShape.h:63-78) lowers the margin to 0.1 x the smallest half extent (Octane:
+    // 0.0386591) and btBoxShape::setMargin (btBoxShape.h:84-92) moves the difference into the implicit
+    // half extents
+    const float m0 = 0.04f;
+    v3 impl = v3{h.x - m0, h.y - m0, h.z - m0};
+    const float mn_half = h.x < h.y ? (h.x < h.z ? h.x : h.z) : (h.y < h.z ? h.y : h.z);  // btVector3::minAxis
+    const float safe = 0.1f * mn_half;
+    k.car_margin = m0;
+    if (safe < k.car_margin) {
+        const v3 with_m = impl + v3{m0, m0, m0};
+        k.car_margin = safe;
+        impl = with_m - v3{safe, safe, safe};
+    }
+    k.car_impl = impl;
+    k.car_half = impl + v3{k.car_margin, k.car_margin, k.car_margin};  // getHalfExtentsWithMargin
     k.car_offset = v3{13.87566f, 0.f, 20.755f} * UU;
     float lx = 2.f * k.car_half.x, ly = 2.f * k.car_half.y, lz = 2.f * k.car_half.z;
     v3 inertia = v3{ly * ly + lz * lz, lx * lx + lz * lz, lx * lx + ly * ly} * (kCarMass / 12.f);
@@ -725,6 +739,7 @@ struct rlgpu_envset {
     double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
     void *d_cell_tri = nullptr, *d_cell_start = nullptr, *d_tri = nullptr, *d_edge = nullptr;  // arena mesh (MeshView)
+    void* d_gjk = nullptr;  // per-lane box-triangle penetration-solver scratch (MeshView::gjk)
     rl::MeshView mesh{};
     rl::Plugins plug{};                 // host copy of the reward / terminal registry
     rl::Plugins* d_plug = nullptr;      // its device copy (StepArgs::plug)
@@ -919,6 +934,11 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         e->mesh.nz = grid.nz;
         e->mesh.ntris = grid.ntris;
         int n = cfg->num_arenas;
+        {  // one GjkScratch per lane of the env kernel's grid (touched only by penetration-solver calls)
+            const size_t lanes = (size_t)rlgpu::ceil_div(n, rl::kArenas) * rl::kWG;
+            RLGPU_CHECK_HIP(hipMalloc(&e->d_gjk, lanes * sizeof(rl::gjk::GjkScratch)));
+            e->mesh.gjk = (rl::gjk::GjkScratch*)e->d_gjk;
+        }
         e->num_players = 4 * n;
         size_t P = (size_t)e->num_players;
         RLGPU_CHECK_HIP(hipMalloc(&e->d_arenas, (size_t)n * rl::kRec));
@@ -1058,6 +1078,7 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_cell_tri);
         (void)hipFree(e->d_tri);
         (void)hipFree(e->d_edge);
+        (void)hipFree(e->d_gjk);
         (void)hipFree(e->d_cell_start);
         (void)hipFree(e->d_plug);
         (void)hipFree(e->d_player_start);
@@ -1180,5 +1201,48 @@ extern "C" int rlgpu_envset_set_arenas(rlgpu_envset* e, int32_t first, int32_t c
         RLGPU_CHECK_HIP(hipDeviceSynchronize());
         RLGPU_CHECK_HIP(hipMemcpy2D(e->d_arenas + (size_t)first * rl::kRec, rl::kRec, h_in, sizeof(rlgpu_arena_state),
                                     sizeof(rlgpu_arena_state), count, hipMemcpyHostToDevice));
+    });
+}
+
+// ------------------------------------------------------------------ box-triangle queries (tests)
+namespace rl {
+__global__ void __launch_bounds__(64) box_triangle_kernel(int n, const float* rot, const float* centre, const float* tri,
+                                                          const float* cbt, float* out, gjk::GjkScratch* scratch) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const float* r = rot + 9 * (size_t)i;
+    const m3 R = m3{v3{r[0], r[1], r[2]}, v3{r[3], r[4], r[5]}, v3{r[6], r[7], r[8]}};
+    const v3 c = v3{centre[3 * (size_t)i], centre[3 * (size_t)i + 1], centre[3 * (size_t)i + 2]};
+    const float* t = tri + 9 * (size_t)i;
+    const gjk::Shape sh{C.car_impl, C.car_margin, v3{t[0], t[1], t[2]}, v3{t[3], t[4], t[5]}, v3{t[6], t[7], t[8]}};
+    v3 nrm, pt;
+    float d = 0.f;
+    const bool hit = gjk::box_triangle(R, c, sh, cbt[i], scratch + i, nrm, pt, d);
+    float* o = out + 8 * (size_t)i;
+    o[0] = hit ? 1.f : 0.f;
+    o[1] = hit ? nrm.x : 0.f;
+    o[2] = hit ? nrm.y : 0.f;
+    o[3] = hit ? nrm.z : 0.f;
+    o[4] = hit ? pt.x : 0.f;
+    o[5] = hit ? pt.y : 0.f;
+    o[6] = hit ? pt.z : 0.f;
+    o[7] = hit ? d : 0.f;
+}
+}  // namespace rl
+
+extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
+                                          const float* d_cbt, float* d_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(n >= 0, "rlgpu_box_triangle_queries: n must be >= 0");
+        if (n == 0) return;
+        RLGPU_REQUIRE(d_rot && d_centre && d_tri && d_cbt && d_out, "rlgpu_box_triangle_queries: null argument");
+        ensure_const();
+        hipStream_t s = (hipStream_t)stream;
+        void* scratch = nullptr;
+        RLGPU_CHECK_HIP(hipMallocAsync(&scratch, (size_t)n * sizeof(rl::gjk::GjkScratch), s));
+        hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 64)), dim3(64), 0, s, n, d_rot, d_centre, d_tri,
+                           d_cbt, d_out, (rl::gjk::GjkScratch*)scratch);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
     });
 }

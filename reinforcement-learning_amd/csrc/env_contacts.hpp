@@ -392,52 +392,6 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
                dl.z >= 0 ? C.car_half.z : -C.car_half.z};
     return R * lv + c;
 }
-// box (car) vs triangle: SAT (stand-in for GJK/EPA)
-DEV bool box_triangle(ArenaLDS* A, int bi, v3 v0, v3 v1, v3 v2, float cbt, v3& nrm, v3& point_b, float& depth) {
-    m3 R = brot(A, bi);
-    v3 c = car_box_center(A, bi);
-    // the axes as named registers picked by selects (a k-indexed private array lives in scratch)
-    const v3 ax0 = col(R, 0), ax1 = col(R, 1), ax2 = col(R, 2);
-    const v3 e0 = v1 - v0, e1 = v2 - v1, e2 = v0 - v2;
-    float best = 1e30f;
-    v3 best_n = zero3();
-    for (int k = 0; k < 13; k++) {
-        v3 axis;
-        if (k == 0) axis = cross(e0, v2 - v0);
-        else if (k < 4) axis = sel3(ax0, ax1, ax2, k - 1);
-        else axis = cross(sel3(ax0, ax1, ax2, (k - 4) / 3), sel3(e0, e1, e2, (k - 4) % 3));
-        float l2 = len2(axis);
-        if (l2 < 1e-10f) continue;
-        v3 L = axis / sqrtf(l2);
-        float r = C.car_half.x * fabsf(dot(ax0, L)) + C.car_half.y * fabsf(dot(ax1, L)) +
-                  C.car_half.z * fabsf(dot(ax2, L));
-        float p0 = dot(v0, L), p1 = dot(v1, L), p2 = dot(v2, L);
-        float tmin = stdmin(p0, stdmin(p1, p2)), tmax = stdmax(p0, stdmax(p1, p2));
-        float cl = dot(c, L);
-        float pen_pos = tmax - (cl - r);
-        float pen_neg = (cl + r) - tmin;
-        float pen;
-        v3 n;
-        if (pen_pos < pen_neg) {
-            pen = pen_pos;
-            n = L;
-        } else {
-            pen = pen_neg;
-            n = -L;
-        }
-        if (-pen > cbt) return false;
-        if (pen < best) {
-            best = pen;
-            best_n = n;
-        }
-    }
-    nrm = best_n;
-    depth = -best;
-    v3 pa = box_support(R, c, -nrm);
-    point_b = pa - nrm * depth;
-    return true;
-}
-
 // runs the narrowphase of one canonical pair rank and emits candidates; returns 1 when it ran.
 // Body-vs-mesh ranks are split over `parts` lanes (grid entries dealt round-robin); candidates
 // carry (rank, triangle), so the commit order does not depend on the split.
@@ -477,10 +431,14 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                 v3 mn, mx;
                 body_aabb(bi, bpos(A, bi), R, mn, mx);
                 float cbt = pair_cbt(bi, 10);
+                // Bullet's GJK / EPA per triangle (gjk.hpp); this lane's penetration-solver scratch
+                const v3 c = car_box_center(A, bi);
+                gjk::GjkScratch* S = M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x);
                 grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) {
+                    const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2};
                     v3 n, pb;
                     float d;
-                    if (box_triangle(A, bi, v0, v1, v2, cbt, n, pb, d)) emit(A, rank, t, mesh_key(bi, obj), n, pb, d);
+                    if (gjk::box_triangle(R, c, sh, cbt, S, n, pb, d)) emit(A, rank, t, mesh_key(bi, obj), n, pb, d);
                 });
             }
         }
@@ -502,8 +460,8 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
     if (B_ == 0) {  // btSphereBoxCollisionAlgorithm::getSphereDistance, A = car, B = ball
         m3 R = brot(A, A_);
         v3 c = car_box_center(A, A_);
-        const float margin = 0.04f;
-        v3 he = v3{(C.car_half.x - margin), (C.car_half.y - margin), (C.car_half.z - margin)};
+        const float margin = C.car_margin;  // boxShape->getMargin() (btSphereBoxCollisionAlgorithm.cpp:82-90)
+        const v3 he = C.car_impl;          // getHalfExtentsWithoutMargin
         v3 rel = vmul(bpos(A, 0) - c, R);
         v3 cp = v3{stdmax(-he.x, stdmin(he.x, rel.x)), stdmax(-he.y, stdmin(he.y, rel.y)), stdmax(-he.z, stdmin(he.z, rel.z))};
         float r = C.ball_radius;

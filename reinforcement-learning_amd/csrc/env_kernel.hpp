@@ -29,6 +29,7 @@
 
 #include "../../include/rlgpu_env.h"
 #include "dmath.hpp"
+#include "gjk.hpp"
 
 namespace rl {
 
@@ -61,6 +62,8 @@ constexpr float kBallMass = kCarMass / 6.f;
 struct EnvConst {
     float ball_radius, ball_inv_mass, car_inv_mass, ball_cbt, car_cbt, ball_damp, susp_travel;
     v3 ball_inv_inertia, car_half, car_offset, car_inv_inertia, gravity;
+    v3 car_impl;       // btBoxShape implicit half extents (without the margin)
+    float car_margin;  // btBoxShape margin after setSafeMargin
     v3 wheel_conn[4];
     float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
     v3 plane_n[4], plane_p[4];
@@ -108,6 +111,7 @@ struct MeshView {
     const int* cell_start;   // [ncell + 1]
     const float4* tri;       // [ntris * 3]: v0 | object, v1, v2 of triangle t (load order)
     const float4* edge;      // [ntris]: internal-edge record (edge_info.hpp EdgeInfo)
+    gjk::GjkScratch* gjk;    // [grid lanes]: box-triangle penetration-solver scratch (gjk.hpp)
     float ox, oy, oz, inv_cell;
     int nx, ny, nz, ntris;
 };

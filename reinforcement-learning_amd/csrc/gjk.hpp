@@ -1,0 +1,1121 @@
+// gjk.hpp -- car hitbox (box) vs arena-mesh triangle narrowphase on the device, as Bullet 3.24 runs it
+// for RocketSim (the reference's call chain, all in GigaLearnCPP/RLGymCPP/RocketSim/libsrc/bullet3-3.24/
+// BulletCollision):
+//   CollisionDispatch/btConvexConcaveCollisionAlgorithm.cpp:71-138   per triangle: normal early out on
+//       both sides, then btConvexConvexAlgorithm (body 0 = box, body 1 = triangle)
+//   CollisionDispatch/btConvexConvexAlgorithm.cpp:268-513           no polyhedral features, no perturbation:
+//       one btGjkPairDetector query with maximum distance margin + contact breaking threshold
+//   NarrowPhaseCollision/btGjkPairDetector.cpp:686-959              GJK on the margin-free shapes with the
+//       Voronoi sub-distance solver (btVoronoiSimplexSolver.cpp:34-577), degenerate-case catch, the
+//       penetration solver (btGjkEpaPenetrationDepthSolver.cpp:22-79 -> btGjkEpa2.cpp GJK + EPA with
+//       margins, nine guesses, Distance fallback) and the AABB-centre normal-direction fix
+//
+// Layout: the Voronoi GJK state lives in registers (fixed-index arrays, runtime slots picked by selects);
+// the penetration solver's GJK / EPA work set (132 support vertices, 256 polytope faces and their lists,
+// the horizon flood-fill stack) lives in a per-lane GjkScratch in HBM (12 KB; MeshView::gjk), touched only
+// when a query needs the penetration solver.  EPA's face lists are index-linked, in Bullet's list order
+// (the stock list's untouched tail is implicit), its recursions (EncloseOrigin, expand) are iterative.
+// Every float operation is Bullet's, in its order (dmath.hpp conventions); the CPU oracle
+// (oracle/gjk_ref.hpp) is an independent restatement and the two agree bit for bit.
+#pragma once
+#include "dmath.hpp"
+
+#ifndef DEV
+#define DEV __device__ __forceinline__
+#endif
+
+namespace rl {
+namespace gjk {
+
+constexpr float kLarge = 1e18f;          // BT_LARGE_FLOAT
+constexpr float kRelError2 = 1.0e-6f;    // btGjkPairDetector.cpp:35
+constexpr float kEqualVertex = 0.0001f;  // VORONOI_DEFAULT_EQUAL_VERTEX_THRESHOLD
+constexpr int kGjkMaxIter = 128;         // GJK_MAX_ITERATIONS
+constexpr float kGjkAccuracy = 0.0001f, kGjkMinDistance = 0.0001f, kGjkDuplicatedEps = 0.0001f;
+constexpr int kEpaMaxVertices = 128, kEpaMaxFaces = 256, kEpaMaxIterations = 255;
+constexpr float kEpaAccuracy = 0.0001f, kEpaPlaneEps = 0.00001f;
+constexpr int kSV = 4 + kEpaMaxVertices;  // support vertices: GJK store 0..3, EPA store 4..131
+constexpr uint16_t kNone = 0xffff;
+
+struct SSV {
+    v3 d, w;
+};
+struct SFace {
+    v3 n;
+    float d;
+    uint8_t c[3];  // support vertices
+    uint8_t f[3];  // adjacent faces
+    uint8_t e[3];  // adjacent faces' edge indices
+    uint8_t pass;
+    uint16_t l[2];  // list links (prev, next)
+};
+struct GjkScratch {
+    SSV sv[kSV];
+    SFace fc[kEpaMaxFaces];
+    uint32_t stack[kEpaMaxFaces + 8];  // expand() frames: face | edge << 8 | stage << 10
+};
+
+// ---------------------------------------------------------------- shapes
+struct Shape {
+    v3 impl;       // box half extents without margin
+    float margin;  // box margin
+    v3 t0, t1, t2;  // triangle (mesh space = world: identity transform)
+};
+DEV v3 box_nm(const Shape& s, v3 d) {
+    return v3{d.x >= 0 ? s.impl.x : -s.impl.x, d.y >= 0 ? s.impl.y : -s.impl.y, d.z >= 0 ? s.impl.z : -s.impl.z};
+}
+DEV v3 tri_nm(const Shape& s, v3 d) {  // dot3 + btVector3::maxAxis
+    const float a = dot(d, s.t0), b = dot(d, s.t1), c = dot(d, s.t2);
+    const int k = a < b ? (b < c ? 2 : 1) : (a < c ? 2 : 0);
+    return sel3(s.t0, s.t1, s.t2, k);
+}
+DEV v3 unit_dir(v3 d) {  // localGetSupportVertexNonVirtual's normalisation
+    if (len2(d) < kEps * kEps) d = v3{-1.f, -1.f, -1.f};
+    return d * (1.f / sqrtf(len2(d)));
+}
+DEV v3 xf(const m3& b, v3 o, v3 x) { return b * x + o; }
+DEV m3 transpose_times(const m3& a, const m3& m) {  // btMatrix3x3::transposeTimes
+    m3 r;
+    r.r0 = v3{a.r0.x * m.r0.x + a.r1.x * m.r1.x + a.r2.x * m.r2.x, a.r0.x * m.r0.y + a.r1.x * m.r1.y + a.r2.x * m.r2.y,
+              a.r0.x * m.r0.z + a.r1.x * m.r1.z + a.r2.x * m.r2.z};
+    r.r1 = v3{a.r0.y * m.r0.x + a.r1.y * m.r1.x + a.r2.y * m.r2.x, a.r0.y * m.r0.y + a.r1.y * m.r1.y + a.r2.y * m.r2.y,
+              a.r0.y * m.r0.z + a.r1.y * m.r1.z + a.r2.y * m.r2.z};
+    r.r2 = v3{a.r0.z * m.r0.x + a.r1.z * m.r1.x + a.r2.z * m.r2.x, a.r0.z * m.r0.y + a.r1.z * m.r1.y + a.r2.z * m.r2.y,
+              a.r0.z * m.r0.z + a.r1.z * m.r1.z + a.r2.z * m.r2.z};
+    return r;
+}
+
+// runtime slot of a 4-entry register array, as selects / predicated writes
+template <typename T>
+DEV T get4(const T (&a)[4], int i) {
+    return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
+}
+template <typename T>
+DEV void put4(T (&a)[4], int i, const T& v) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k == i) a[k] = v;
+}
+
+// ---------------------------------------------------------------- btVoronoiSimplexSolver (registers)
+struct Voronoi {
+    v3 W[4], P[4], Q[4];
+    int n;
+    v3 lastW, cP1, cP2, cV;
+    bool u[4];
+    float bc[4];
+    bool degenerate, needs_update, valid;
+};
+DEV void bc_reset(Voronoi& s) {
+    s.degenerate = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        s.bc[k] = 0.f;
+        s.u[k] = false;
+    }
+}
+DEV bool bc_valid(const Voronoi& s) { return s.bc[0] >= 0.f && s.bc[1] >= 0.f && s.bc[2] >= 0.f && s.bc[3] >= 0.f; }
+DEV void vor_reset(Voronoi& s) {
+    s.valid = false;
+    s.n = 0;
+    s.needs_update = true;
+    s.lastW = v3{kLarge, kLarge, kLarge};
+    bc_reset(s);
+}
+template <int I>
+DEV void vor_remove(Voronoi& s) {  // removeVertex(I): the last vertex moves into slot I
+    const int last = s.n - 1;
+    s.W[I] = get4(s.W, last);
+    s.P[I] = get4(s.P, last);
+    s.Q[I] = get4(s.Q, last);
+    s.n = last;
+}
+DEV void vor_reduce(Voronoi& s) {
+    if (s.n >= 4 && !s.u[3]) vor_remove<3>(s);
+    if (s.n >= 3 && !s.u[2]) vor_remove<2>(s);
+    if (s.n >= 2 && !s.u[1]) vor_remove<1>(s);
+    if (s.n >= 1 && !s.u[0]) vor_remove<0>(s);
+}
+// closestPtPointTriangle with p = origin (btVoronoiSimplexSolver.cpp:313-408)
+DEV void closest_tri(v3 a, v3 b, v3 c, v3& pt, bool& u0, bool& u1, bool& u2, float& w0, float& w1, float& w2) {
+    const v3 p = zero3();
+    u0 = u1 = u2 = false;
+    const v3 ab = b - a, ac = c - a, ap = p - a;
+    const float d1 = dot(ab, ap), d2 = dot(ac, ap);
+    if (d1 <= 0.f && d2 <= 0.f) {
+        pt = a; u0 = true; w0 = 1; w1 = 0; w2 = 0;
+        return;
+    }
+    const v3 bp = p - b;
+    const float d3 = dot(ab, bp), d4 = dot(ac, bp);
+    if (d3 >= 0.f && d4 <= d3) {
+        pt = b; u1 = true; w0 = 0; w1 = 1; w2 = 0;
+        return;
+    }
+    const float vc = d1 * d4 - d3 * d2;
+    if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+        const float v = d1 / (d1 - d3);
+        pt = a + v * ab; u0 = u1 = true; w0 = 1 - v; w1 = v; w2 = 0;
+        return;
+    }
+    const v3 cp = p - c;
+    const float d5 = dot(ab, cp), d6 = dot(ac, cp);
+    if (d6 >= 0.f && d5 <= d6) {
+        pt = c; u2 = true; w0 = 0; w1 = 0; w2 = 1;
+        return;
+    }
+    const float vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+        const float w = d2 / (d2 - d6);
+        pt = a + w * ac; u0 = u2 = true; w0 = 1 - w; w1 = 0; w2 = w;
+        return;
+    }
+    const float va = d3 * d6 - d5 * d4;
+    if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+        const float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        pt = b + w * (c - b); u1 = u2 = true; w0 = 0; w1 = 1 - w; w2 = w;
+        return;
+    }
+    const float denom = 1.f / (va + vb + vc);
+    const float v = vb * denom, w = vc * denom;
+    pt = a + ab * v + ac * w;
+    u0 = u1 = u2 = true;
+    w0 = 1 - v - w; w1 = v; w2 = w;
+}
+DEV int outside_plane(v3 a, v3 b, v3 c, v3 d) {  // pointOutsideOfPlane with p = origin
+    const v3 p = zero3();
+    const v3 nrm = cross(b - a, c - a);
+    const float signp = dot(p - a, nrm), signd = dot(d - a, nrm);
+    if (signd * signd < (1e-4f * 1e-4f)) return -1;
+    return signp * signd < 0.f;
+}
+// closestPtPointTetrahedron (cpp:437-577) into the solver's bc / u / degenerate
+DEV bool closest_tetra(Voronoi& s) {
+    const v3 a = s.W[0], b = s.W[1], c = s.W[2], d = s.W[3];
+    s.u[0] = s.u[1] = s.u[2] = s.u[3] = true;
+    const int oABC = outside_plane(a, b, c, d), oACD = outside_plane(a, c, d, b), oADB = outside_plane(a, d, b, c),
+              oBDC = outside_plane(b, d, c, a);
+    if (oABC < 0 || oACD < 0 || oADB < 0 || oBDC < 0) {
+        s.degenerate = true;
+        return false;
+    }
+    if (!oABC && !oACD && !oADB && !oBDC) return false;
+    float best = 3.40282346638528859812e+38f;  // FLT_MAX
+    const v3 o = zero3();
+    v3 q;
+    bool t0, t1, t2;
+    float w0, w1, w2;
+    if (oABC) {
+        closest_tri(a, b, c, q, t0, t1, t2, w0, w1, w2);
+        const float sq = dot(q - o, q - o);
+        if (sq < best) {
+            best = sq;
+            s.u[0] = t0; s.u[1] = t1; s.u[2] = t2; s.u[3] = false;
+            s.bc[0] = w0; s.bc[1] = w1; s.bc[2] = w2; s.bc[3] = 0;
+        }
+    }
+    if (oACD) {
+        closest_tri(a, c, d, q, t0, t1, t2, w0, w1, w2);
+        const float sq = dot(q - o, q - o);
+        if (sq < best) {
+            best = sq;
+            s.u[0] = t0; s.u[1] = false; s.u[2] = t1; s.u[3] = t2;
+            s.bc[0] = w0; s.bc[1] = 0; s.bc[2] = w1; s.bc[3] = w2;
+        }
+    }
+    if (oADB) {
+        closest_tri(a, d, b, q, t0, t1, t2, w0, w1, w2);
+        const float sq = dot(q - o, q - o);
+        if (sq < best) {
+            best = sq;
+            s.u[0] = t0; s.u[1] = t2; s.u[2] = false; s.u[3] = t1;
+            s.bc[0] = w0; s.bc[1] = w2; s.bc[2] = 0; s.bc[3] = w1;
+        }
+    }
+    if (oBDC) {
+        closest_tri(b, d, c, q, t0, t1, t2, w0, w1, w2);
+        const float sq = dot(q - o, q - o);
+        if (sq < best) {
+            best = sq;
+            s.u[0] = false; s.u[1] = t0; s.u[2] = t2; s.u[3] = t1;
+            s.bc[0] = 0; s.bc[1] = w0; s.bc[2] = w2; s.bc[3] = w1;
+        }
+    }
+    return true;
+}
+// updateClosestVectorAndPoints (cpp:81-233)
+DEV bool vor_update(Voronoi& s) {
+    if (s.needs_update) {
+        bc_reset(s);
+        s.needs_update = false;
+        if (s.n == 1) {
+            s.cP1 = s.P[0];
+            s.cP2 = s.Q[0];
+            s.cV = s.cP1 - s.cP2;
+            bc_reset(s);
+            s.bc[0] = 1.f;
+            s.valid = bc_valid(s);
+        } else if (s.n == 2) {
+            const v3 from = s.W[0], to = s.W[1];
+            v3 diff = zero3() - from;
+            const v3 v = to - from;
+            float t = dot(v, diff);
+            if (t > 0) {
+                const float vv = dot(v, v);
+                if (t < vv) {
+                    t /= vv;
+                    diff -= t * v;
+                    s.u[0] = s.u[1] = true;
+                } else {
+                    t = 1;
+                    diff -= v;
+                    s.u[1] = true;
+                }
+            } else {
+                t = 0;
+                s.u[0] = true;
+            }
+            s.bc[0] = 1 - t; s.bc[1] = t; s.bc[2] = 0; s.bc[3] = 0;
+            s.cP1 = s.P[0] + t * (s.P[1] - s.P[0]);
+            s.cP2 = s.Q[0] + t * (s.Q[1] - s.Q[0]);
+            s.cV = s.cP1 - s.cP2;
+            vor_reduce(s);
+            s.valid = bc_valid(s);
+        } else if (s.n == 3) {
+            v3 pt;
+            closest_tri(s.W[0], s.W[1], s.W[2], pt, s.u[0], s.u[1], s.u[2], s.bc[0], s.bc[1], s.bc[2]);
+            s.cP1 = s.P[0] * s.bc[0] + s.P[1] * s.bc[1] + s.P[2] * s.bc[2];
+            s.cP2 = s.Q[0] * s.bc[0] + s.Q[1] * s.bc[1] + s.Q[2] * s.bc[2];
+            s.cV = s.cP1 - s.cP2;
+            vor_reduce(s);
+            s.valid = bc_valid(s);
+        } else if (s.n == 4) {
+            if (closest_tetra(s)) {
+                s.cP1 = s.P[0] * s.bc[0] + s.P[1] * s.bc[1] + s.P[2] * s.bc[2] + s.P[3] * s.bc[3];
+                s.cP2 = s.Q[0] * s.bc[0] + s.Q[1] * s.bc[1] + s.Q[2] * s.bc[2] + s.Q[3] * s.bc[3];
+                s.cV = s.cP1 - s.cP2;
+                vor_reduce(s);
+                s.valid = bc_valid(s);
+            } else if (s.degenerate) {
+                s.valid = false;
+            } else {
+                s.valid = true;
+                s.cV = zero3();
+            }
+        } else {
+            s.valid = false;
+        }
+    }
+    return s.valid;
+}
+DEV bool vor_in_simplex(const Voronoi& s, v3 w) {
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < s.n && len2(w - s.W[k]) <= kEqualVertex) found = true;
+    if (w.x == s.lastW.x && w.y == s.lastW.y && w.z == s.lastW.z) return true;
+    return found;
+}
+
+// ---------------------------------------------------------------- btGjkEpa2 in the lane's scratch
+struct Mink {
+    Shape s;
+    m3 toshape1, b0;  // b0 / o0: toshape0
+    v3 o0;
+    bool margins;
+};
+DEV Mink make_mink(const Shape& s, const m3& tb0, v3 to0, const m3& tb1, v3 to1, bool margins) {
+    Mink m;
+    m.s = s;
+    m.toshape1 = transpose_times(tb1, tb0);
+    m.b0 = transpose_times(tb0, tb1);  // btTransform::inverseTimes
+    m.o0 = vmul(to1 - to0, tb0);
+    m.margins = margins;
+    return m;
+}
+DEV v3 support0(const Mink& m, v3 d) {
+    if (m.margins) {
+        const v3 n = unit_dir(d);
+        return box_nm(m.s, n) + m.s.margin * n;
+    }
+    return box_nm(m.s, d);
+}
+DEV v3 support1(const Mink& m, v3 d) {
+    const v3 dd = m.toshape1 * d;
+    v3 sup;
+    if (m.margins) {
+        const v3 n = unit_dir(dd);
+        sup = tri_nm(m.s, n) + 0.f * n;
+    } else {
+        sup = tri_nm(m.s, dd);
+    }
+    return xf(m.b0, m.o0, sup);
+}
+DEV v3 support(const Mink& m, v3 d) { return support0(m, d) - support1(m, -d); }
+
+// the GJK of btGjkEpa2 (cpp:155-552): simplex vertex indices packed 8 bits each, store in scratch
+struct Simp {
+    uint32_t c;  // c[k] = (c >> 8k) & 255
+    float p[4];
+    int rank;
+};
+DEV int sc(const Simp& s, int k) { return (int)((s.c >> (8 * k)) & 255u); }
+DEV void sc_set(Simp& s, int k, int v) { s.c = (s.c & ~(255u << (8 * k))) | ((uint32_t)v << (8 * k)); }
+struct Gjk2 {
+    Simp cs, ns;     // current / next simplex (swapped when Bullet flips m_current)
+    uint32_t freev;  // free list: 4 slots of 8 bits
+    int nfree;
+    v3 ray;
+    int status;  // Valid 0, Inside 1, Failed 2
+};
+DEV void getsupport(GjkScratch* S, const Mink& m, v3 d, int idx) {
+    const v3 dn = d / len(d);
+    S->sv[idx].d = dn;
+    S->sv[idx].w = support(m, dn);
+}
+DEV void g2_append(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 v) {
+    put4(s.p, s.rank, 0.f);
+    g.nfree--;
+    const int idx = (int)((g.freev >> (8 * g.nfree)) & 255u);
+    sc_set(s, s.rank, idx);
+    s.rank++;
+    getsupport(S, m, v, idx);
+}
+DEV void g2_remove(Gjk2& g, Simp& s) {
+    s.rank--;
+    const int idx = sc(s, s.rank);
+    g.freev = (g.freev & ~(255u << (8 * g.nfree))) | ((uint32_t)idx << (8 * g.nfree));
+    g.nfree++;
+}
+DEV float det3(v3 a, v3 b, v3 c) {
+    return (a.y * b.z * c.x + a.z * b.x * c.y - a.x * b.z * c.y - a.y * b.x * c.z + a.x * b.y * c.z - a.z * b.y * c.x);
+}
+DEV float project2(v3 a, v3 b, float* w, uint32_t& m) {
+    const v3 d = b - a;
+    const float l = len2(d);
+    if (l > 0.f) {
+        const float t = l > 0 ? -dot(a, d) / l : 0;
+        if (t >= 1) {
+            w[0] = 0; w[1] = 1; m = 2;
+            return len2(b);
+        } else if (t <= 0) {
+            w[0] = 1; w[1] = 0; m = 1;
+            return len2(a);
+        } else {
+            w[1] = t;
+            w[0] = 1 - t;
+            m = 3;
+            return len2(a + d * t);
+        }
+    }
+    return -1;
+}
+DEV float project3(v3 a, v3 b, v3 c, float* w, uint32_t& m) {
+    const v3 dl0 = a - b, dl1 = b - c, dl2 = c - a;
+    const v3 n = cross(dl0, dl1);
+    const float l = len2(n);
+    if (l > 0.f) {
+        float mindist = -1;
+        float subw[2] = {0.f, 0.f};
+        uint32_t subm = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const v3 vi = sel3(a, b, c, i), dli = sel3(dl0, dl1, dl2, i);
+            if (dot(vi, cross(dli, n)) > 0) {
+                const int j = i == 2 ? 0 : i + 1;
+                const float subd = project2(vi, sel3(a, b, c, j), subw, subm);
+                if ((mindist < 0) || (subd < mindist)) {
+                    mindist = subd;
+                    m = ((subm & 1) ? 1u << i : 0u) + ((subm & 2) ? 1u << j : 0u);
+                    w[i] = subw[0];
+                    w[j] = subw[1];
+                    w[j == 2 ? 0 : j + 1] = 0;
+                }
+            }
+        }
+        if (mindist < 0) {
+            const float d = dot(a, n);
+            const float s = sqrtf(l);
+            const v3 p = n * (d / l);
+            mindist = len2(p);
+            m = 7;
+            w[0] = len(cross(dl1, b - p)) / s;
+            w[1] = len(cross(dl2, c - p)) / s;
+            w[2] = 1 - (w[0] + w[1]);
+        }
+        return mindist;
+    }
+    return -1;
+}
+DEV float project4(v3 a, v3 b, v3 c, v3 d, float* w, uint32_t& m) {
+    const v3 dl0 = a - d, dl1 = b - d, dl2 = c - d;
+    const float vl = det3(dl0, dl1, dl2);
+    const bool ng = (vl * dot(a, cross(b - c, a - b))) <= 0;
+    if (ng && (fabsf(vl) > 0.f)) {
+        float mindist = -1;
+        float subw[3] = {0.f, 0.f, 0.f};
+        uint32_t subm = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int j = i == 2 ? 0 : i + 1;
+            const float s = vl * dot(d, cross(sel3(dl0, dl1, dl2, i), sel3(dl0, dl1, dl2, j)));
+            if (s > 0) {
+                const float subd = project3(sel3(a, b, c, i), sel3(a, b, c, j), d, subw, subm);
+                if ((mindist < 0) || (subd < mindist)) {
+                    mindist = subd;
+                    m = (subm & 1 ? 1u << i : 0u) + (subm & 2 ? 1u << j : 0u) + (subm & 4 ? 8u : 0u);
+                    w[i] = subw[0];
+                    w[j] = subw[1];
+                    w[j == 2 ? 0 : j + 1] = 0;
+                    w[3] = subw[2];
+                }
+            }
+        }
+        if (mindist < 0) {
+            mindist = 0;
+            m = 15;
+            w[0] = det3(c, b, d) / vl;
+            w[1] = det3(a, c, d) / vl;
+            w[2] = det3(b, a, d) / vl;
+            w[3] = 1 - (w[0] + w[1] + w[2]);
+        }
+        return mindist;
+    }
+    return -1;
+}
+DEV v3 svw(const GjkScratch* S, int i) { return S->sv[i].w; }
+// GJK::Evaluate (cpp:201-337); on return g.cs is m_simplex
+DEV int g2_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, v3 guess) {
+    unsigned iterations = 0;
+    float sqdist = 0, alpha = 0;
+    v3 lastw[4];
+    int clastw = 0;
+    g.freev = 0u | (1u << 8) | (2u << 16) | (3u << 24);
+    g.nfree = 4;
+    g.status = 0;
+    g.cs.rank = 0;
+    g.cs.c = 0;
+    g.ns.c = 0;
+    g.ns.rank = 0;
+    g.ray = guess;
+    const float sqrl = len2(g.ray);
+    g2_append(S, m, g, g.cs, sqrl > 0 ? -g.ray : v3{1, 0, 0});
+    g.cs.p[0] = 1;
+    g.ray = svw(S, sc(g.cs, 0));
+    sqdist = sqrl;
+    lastw[0] = lastw[1] = lastw[2] = lastw[3] = g.ray;
+    do {
+        const float rl = len(g.ray);
+        if (rl < kGjkMinDistance) {
+            g.status = 1;
+            break;
+        }
+        g2_append(S, m, g, g.cs, -g.ray);
+        const v3 w = svw(S, sc(g.cs, g.cs.rank - 1));
+        bool found = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (len2(w - lastw[i]) < kGjkDuplicatedEps) found = true;
+        if (found) {
+            g2_remove(g, g.cs);
+            break;
+        }
+        clastw = (clastw + 1) & 3;
+        put4(lastw, clastw, w);
+        const float omega = dot(g.ray, w) / rl;
+        alpha = omega > alpha ? omega : alpha;
+        if (((rl - alpha) - (kGjkAccuracy * rl)) <= 0) {
+            g2_remove(g, g.cs);
+            break;
+        }
+        float weights[4];
+        uint32_t mask = 0;
+        const v3 w0 = svw(S, sc(g.cs, 0)), w1 = svw(S, sc(g.cs, 1));
+        if (g.cs.rank == 2) {
+            sqdist = project2(w0, w1, weights, mask);
+        } else if (g.cs.rank == 3) {
+            sqdist = project3(w0, w1, svw(S, sc(g.cs, 2)), weights, mask);
+        } else if (g.cs.rank == 4) {
+            sqdist = project4(w0, w1, svw(S, sc(g.cs, 2)), svw(S, sc(g.cs, 3)), weights, mask);
+        }
+        if (sqdist >= 0) {
+            g.ns.rank = 0;
+            g.ns.c = 0;
+            g.ray = zero3();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (i < g.cs.rank) {
+                    const int ci = sc(g.cs, i);
+                    if (mask & (1u << i)) {
+                        sc_set(g.ns, g.ns.rank, ci);
+                        put4(g.ns.p, g.ns.rank, weights[i]);
+                        g.ns.rank++;
+                        g.ray += svw(S, ci) * weights[i];
+                    } else {
+                        g.freev = (g.freev & ~(255u << (8 * g.nfree))) | ((uint32_t)ci << (8 * g.nfree));
+                        g.nfree++;
+                    }
+                }
+            }
+            const Simp t = g.cs;  // m_current = next
+            g.cs = g.ns;
+            g.ns = t;
+            if (mask == 15) g.status = 1;
+        } else {
+            g2_remove(g, g.cs);
+            break;
+        }
+        g.status = ((++iterations) < (unsigned)kGjkMaxIter) ? g.status : 2;
+    } while (g.status == 0);
+    return g.status;
+}
+// GJK::EncloseOrigin (cpp:338-402), its recursion unrolled by rank
+DEV bool enclose4(const GjkScratch* S, const Simp& s) {
+    const v3 w3 = svw(S, sc(s, 3));
+    return fabsf(det3(svw(S, sc(s, 0)) - w3, svw(S, sc(s, 1)) - w3, svw(S, sc(s, 2)) - w3)) > 0;
+}
+DEV bool enclose3(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
+    const v3 w0 = svw(S, sc(s, 0));
+    const v3 n = cross(svw(S, sc(s, 1)) - w0, svw(S, sc(s, 2)) - w0);
+    if (len2(n) > 0) {
+        g2_append(S, m, g, s, n);
+        if (enclose4(S, s)) return true;
+        g2_remove(g, s);
+        g2_append(S, m, g, s, -n);
+        if (enclose4(S, s)) return true;
+        g2_remove(g, s);
+    }
+    return false;
+}
+DEV bool enclose2(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
+    const v3 d = svw(S, sc(s, 1)) - svw(S, sc(s, 0));
+    for (int i = 0; i < 3; ++i) {
+        v3 axis = zero3();
+        set_comp(axis, i, 1.f);
+        const v3 p = cross(d, axis);
+        if (len2(p) > 0) {
+            g2_append(S, m, g, s, p);
+            if (enclose3(S, m, g, s)) return true;
+            g2_remove(g, s);
+            g2_append(S, m, g, s, -p);
+            if (enclose3(S, m, g, s)) return true;
+            g2_remove(g, s);
+        }
+    }
+    return false;
+}
+DEV bool enclose_origin(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
+    if (s.rank == 1) {
+        for (int i = 0; i < 3; ++i) {
+            v3 axis = zero3();
+            set_comp(axis, i, 1.f);
+            g2_append(S, m, g, s, axis);
+            if (enclose2(S, m, g, s)) return true;
+            g2_remove(g, s);
+            g2_append(S, m, g, s, -axis);
+            if (enclose2(S, m, g, s)) return true;
+            g2_remove(g, s);
+        }
+        return false;
+    }
+    if (s.rank == 2) return enclose2(S, m, g, s);
+    if (s.rank == 3) return enclose3(S, m, g, s);
+    if (s.rank == 4) return enclose4(S, s);
+    return false;
+}
+
+// ---- EPA (cpp:555-901) over scratch faces
+struct Epa {
+    uint16_t hull;    // hull list root
+    int hull_count;
+    uint16_t stock;   // recycled faces (pushed at the stock's front)
+    int fresh;        // stock tail: faces fresh..255 never taken, in index order (EPA::Initialize)
+    int status;       // Valid 0 .. Failed 9 (EPA::eStatus order)
+    int nextsv;
+};
+DEV void list_append(GjkScratch* S, uint16_t& root, int face) {
+    SFace& f = S->fc[face];
+    f.l[0] = kNone;
+    f.l[1] = root;
+    if (root != kNone) S->fc[root].l[0] = (uint16_t)face;
+    root = (uint16_t)face;
+}
+DEV void list_remove(GjkScratch* S, uint16_t& root, int face) {
+    SFace& f = S->fc[face];
+    if (f.l[1] != kNone) S->fc[f.l[1]].l[0] = f.l[0];
+    if (f.l[0] != kNone) S->fc[f.l[0]].l[1] = f.l[1];
+    if (face == root) root = f.l[1];
+}
+DEV void stock_push(GjkScratch* S, Epa& E, int face) { list_append(S, E.stock, face); }
+DEV void bind(GjkScratch* S, int fa, int ea, int fb, int eb) {
+    S->fc[fa].e[ea] = (uint8_t)eb;
+    S->fc[fa].f[ea] = (uint8_t)fb;
+    S->fc[fb].e[eb] = (uint8_t)ea;
+    S->fc[fb].f[eb] = (uint8_t)fa;
+}
+DEV bool getedgedist(const GjkScratch* S, v3 fn, int a, int b, float& dist) {
+    const v3 aw = svw(S, a), bw = svw(S, b);
+    const v3 ba = bw - aw;
+    const v3 n_ab = cross(ba, fn);
+    const float a_dot_nab = dot(aw, n_ab);
+    if (a_dot_nab < 0) {
+        const float ba_l2 = len2(ba);
+        const float a_dot_ba = dot(aw, ba);
+        const float b_dot_ba = dot(bw, ba);
+        if (a_dot_ba > 0) {
+            dist = len(aw);
+        } else if (b_dot_ba < 0) {
+            dist = len(bw);
+        } else {
+            const float a_dot_b = dot(aw, bw);
+            const float q = (len2(aw) * len2(bw) - a_dot_b * a_dot_b) / ba_l2;
+            dist = sqrtf(q > 0.f ? q : 0.f);
+        }
+        return true;
+    }
+    return false;
+}
+// EPA::newface; returns the face or -1
+DEV int newface(GjkScratch* S, Epa& E, int a, int b, int c, bool forced) {
+    int face;
+    if (E.stock != kNone) {
+        face = E.stock;
+        list_remove(S, E.stock, face);
+    } else if (E.fresh < kEpaMaxFaces) {
+        face = E.fresh++;
+    } else {
+        E.status = 5;  // OutOfFaces (the stock is empty)
+        return -1;
+    }
+    list_append(S, E.hull, face);
+    E.hull_count++;
+    SFace& F = S->fc[face];
+    F.pass = 0;
+    F.c[0] = (uint8_t)a;
+    F.c[1] = (uint8_t)b;
+    F.c[2] = (uint8_t)c;
+    const v3 aw = svw(S, a);
+    v3 n = cross(svw(S, b) - aw, svw(S, c) - aw);
+    const float l = len(n);
+    if (l > kEpaAccuracy) {
+        float d;
+        if (!(getedgedist(S, n, a, b, d) || getedgedist(S, n, b, c, d) || getedgedist(S, n, c, a, d))) d = dot(aw, n) / l;
+        n = n / l;
+        F.n = n;
+        F.d = d;
+        if (forced || (d >= -kEpaPlaneEps)) return face;
+        E.status = 3;  // NonConvex
+    } else {
+        F.n = n;
+        E.status = 2;  // Degenerated
+    }
+    list_remove(S, E.hull, face);
+    E.hull_count--;
+    stock_push(S, E, face);
+    return -1;
+}
+DEV int findbest(const GjkScratch* S, const Epa& E) {
+    int minf = E.hull;
+    float mind = S->fc[minf].d * S->fc[minf].d;
+    for (int f = S->fc[minf].l[1]; f != kNone; f = S->fc[f].l[1]) {
+        const float sqd = S->fc[f].d * S->fc[f].d;
+        if (sqd < mind) {
+            minf = f;
+            mind = sqd;
+        }
+    }
+    return minf;
+}
+// EPA::expand (cpp:864-900) as an explicit-stack walk: frame = face | edge << 8 | stage << 10
+DEV bool expand(GjkScratch* S, Epa& E, unsigned pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
+    int sp = 0;
+    S->stack[sp++] = (uint32_t)f0 | ((uint32_t)e0 << 8);
+    bool ret = false;
+    while (sp > 0) {
+        const uint32_t fr = S->stack[sp - 1];
+        const int f = (int)(fr & 255u), e = (int)((fr >> 8) & 3u), stage = (int)(fr >> 10);
+        const int e1 = e == 2 ? 0 : e + 1, e2 = e == 0 ? 2 : e - 1;
+        if (stage == 0) {
+            SFace& F = S->fc[f];
+            if (F.pass != (uint8_t)pass) {
+                if ((dot(F.n, svw(S, w)) - F.d) < -kEpaPlaneEps) {
+                    const int nf = newface(S, E, F.c[e1], F.c[e], w, false);
+                    ret = false;
+                    if (nf >= 0) {
+                        bind(S, nf, 0, f, e);
+                        if (hcf >= 0)
+                            bind(S, hcf, 1, nf, 2);
+                        else
+                            hff = nf;
+                        hcf = nf;
+                        ++hnf;
+                        ret = true;
+                    }
+                    sp--;
+                } else {
+                    F.pass = (uint8_t)pass;
+                    S->stack[sp - 1] = fr | (1u << 10);
+                    S->stack[sp++] = (uint32_t)F.f[e1] | ((uint32_t)F.e[e1] << 8);
+                }
+            } else {
+                ret = false;
+                sp--;
+            }
+        } else if (stage == 1) {
+            if (!ret) {
+                sp--;
+            } else {
+                const SFace& F = S->fc[f];
+                S->stack[sp - 1] = (fr & 1023u) | (2u << 10);
+                S->stack[sp++] = (uint32_t)F.f[e2] | ((uint32_t)F.e[e2] << 8);
+            }
+        } else {
+            if (ret) {
+                list_remove(S, E.hull, f);
+                E.hull_count--;
+                stock_push(S, E, f);
+            }
+            sp--;
+        }
+    }
+    return ret;
+}
+// EPA::Evaluate (cpp:648-768) on the GJK's simplex s; out: normal, depth, result (rank, c, p)
+DEV int epa_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v3& normal, float& depth, Simp& res) {
+    Epa E;
+    E.hull = kNone;
+    E.hull_count = 0;
+    E.stock = kNone;
+    E.fresh = 0;
+    E.status = 9;
+    E.nextsv = 0;
+    if ((s.rank > 1) && enclose_origin(S, m, g, s)) {
+        E.status = 0;
+        E.nextsv = 0;
+        {
+            const v3 w3 = svw(S, sc(s, 3));
+            if (det3(svw(S, sc(s, 0)) - w3, svw(S, sc(s, 1)) - w3, svw(S, sc(s, 2)) - w3) < 0) {
+                const int c0 = sc(s, 0), c1 = sc(s, 1);
+                sc_set(s, 0, c1);
+                sc_set(s, 1, c0);
+                const float p0 = s.p[0];
+                s.p[0] = s.p[1];
+                s.p[1] = p0;
+            }
+        }
+        const int s0 = sc(s, 0), s1 = sc(s, 1), s2 = sc(s, 2), s3 = sc(s, 3);
+        const int t0 = newface(S, E, s0, s1, s2, true);
+        const int t1 = newface(S, E, s1, s0, s3, true);
+        const int t2 = newface(S, E, s2, s1, s3, true);
+        const int t3 = newface(S, E, s0, s2, s3, true);
+        if (E.hull_count == 4) {
+            int best = findbest(S, E);
+            SFace outer = S->fc[best];
+            unsigned pass = 0;
+            bind(S, t0, 0, t1, 0);
+            bind(S, t0, 1, t2, 0);
+            bind(S, t0, 2, t3, 0);
+            bind(S, t1, 1, t3, 2);
+            bind(S, t1, 2, t2, 1);
+            bind(S, t2, 2, t3, 1);
+            E.status = 0;
+            for (int iterations = 0; iterations < kEpaMaxIterations; ++iterations) {
+                if (E.nextsv < kEpaMaxVertices) {
+                    int hcf = -1, hff = -1, hnf = 0;
+                    const int w = 4 + E.nextsv++;
+                    bool valid = true;
+                    S->fc[best].pass = (uint8_t)(++pass);
+                    const v3 bn = S->fc[best].n;
+                    const float bd = S->fc[best].d;
+                    getsupport(S, m, bn, w);
+                    const float wdist = dot(bn, svw(S, w)) - bd;
+                    if (wdist > kEpaAccuracy) {
+                        for (int j = 0; (j < 3) && valid; ++j)
+                            valid &= expand(S, E, pass, w, S->fc[best].f[j], S->fc[best].e[j], hcf, hff, hnf);
+                        if (valid && (hnf >= 3)) {
+                            bind(S, hcf, 1, hff, 2);
+                            list_remove(S, E.hull, best);
+                            E.hull_count--;
+                            stock_push(S, E, best);
+                            best = findbest(S, E);
+                            outer = S->fc[best];
+                        } else {
+                            E.status = 4;  // InvalidHull
+                            break;
+                        }
+                    } else {
+                        E.status = 7;  // AccuraryReached
+                        break;
+                    }
+                } else {
+                    E.status = 6;  // OutOfVertices
+                    break;
+                }
+            }
+            const v3 projection = outer.n * outer.d;
+            normal = outer.n;
+            depth = outer.d;
+            res.rank = 3;
+            res.c = 0;
+            sc_set(res, 0, outer.c[0]);
+            sc_set(res, 1, outer.c[1]);
+            sc_set(res, 2, outer.c[2]);
+            const v3 o0 = svw(S, outer.c[0]), o1 = svw(S, outer.c[1]), o2 = svw(S, outer.c[2]);
+            res.p[0] = len(cross(o1 - projection, o2 - projection));
+            res.p[1] = len(cross(o2 - projection, o0 - projection));
+            res.p[2] = len(cross(o0 - projection, o1 - projection));
+            const float sum = res.p[0] + res.p[1] + res.p[2];
+            res.p[0] /= sum;
+            res.p[1] /= sum;
+            res.p[2] /= sum;
+            return E.status;
+        }
+    }
+    E.status = 8;  // FallBack
+    normal = -guess;
+    const float nl = len(normal);
+    if (nl > 0)
+        normal = normal / nl;
+    else
+        normal = v3{1, 0, 0};
+    depth = 0;
+    res.rank = 1;
+    res.c = 0;
+    sc_set(res, 0, sc(s, 0));
+    res.p[0] = 1;
+    return E.status;
+}
+
+// btGjkEpaSolver2::Penetration (cpp:973-1017) with margins; t0 / t1 = (basis, origin)
+DEV bool penetration(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
+                     v3& nrm) {
+    const Mink m = make_mink(sh, b0, o0, b1, o1, true);
+    Gjk2 g;
+    if (g2_evaluate(S, m, g, -guess) != 1) return false;
+    v3 en;
+    float ed;
+    Simp res;
+    const int es = epa_evaluate(S, m, g, g.cs, -guess, en, ed, res);
+    if (es == 9) return false;
+    v3 w0 = zero3();
+    for (int i = 0; i < res.rank; ++i) w0 += support0(m, S->sv[sc(res, i)].d) * get4(res.p, i);
+    wA = xf(b0, o0, w0);
+    wB = xf(b0, o0, w0 - en * ed);
+    nrm = -en;
+    return true;
+}
+// btGjkEpaSolver2::Distance (cpp:937-970), margins off
+DEV bool distance(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
+                  v3& nrm) {
+    const Mink m = make_mink(sh, b0, o0, b1, o1, false);
+    Gjk2 g;
+    if (g2_evaluate(S, m, g, guess) != 0) return false;
+    v3 w0 = zero3(), w1 = zero3();
+    for (int i = 0; i < g.cs.rank; ++i) {
+        const float p = get4(g.cs.p, i);
+        const v3 d = S->sv[sc(g.cs, i)].d;
+        w0 += support0(m, d) * p;
+        w1 += support1(m, -d) * p;
+    }
+    wA = xf(b0, o0, w0);
+    wB = xf(b0, o0, w1);
+    nrm = w0 - w1;
+    const float dist = len(nrm);
+    nrm = nrm / (dist > kGjkMinDistance ? dist : 1);
+    return true;
+}
+// btGjkEpaPenetrationDepthSolver::calcPenDepth (cpp:22-79); called, not inlined: the rare path stays out
+// of the narrowphase's hot code
+__device__ __noinline__ bool calc_pen_depth(GjkScratch* S, const Shape& sh, const m3& bA, v3 oA, const m3& bB, v3 oB, v3& v, v3& wA, v3& wB) {
+    for (int i = 0; i < 9; i++) {
+        v3 g;
+        if (i == 0) g = safe_normalized(oB - oA);
+        else if (i == 1) g = safe_normalized(oA - oB);
+        else if (i == 2) g = v3{0, 0, 1};
+        else if (i == 3) g = v3{0, 1, 0};
+        else if (i == 4) g = v3{1, 0, 0};
+        else if (i == 5) g = v3{1, 1, 0};
+        else if (i == 6) g = v3{1, 1, 1};
+        else if (i == 7) g = v3{0, 1, 1};
+        else g = v3{1, 0, 1};
+        if (penetration(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return true;
+        if (distance(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return false;
+    }
+    wA = wB = v = zero3();
+    return false;
+}
+
+// One box-triangle query (the caller did the AABB test).  R / c: the hitbox child's world basis and
+// origin; cbt: the pair manifold's contact breaking threshold.  True when Bullet would call
+// btManifoldResult::addContactPoint(normal, point, depth).  S: this lane's penetration-solver scratch.
+DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, GjkScratch* S, v3& normal, v3& point, float& depth) {
+    // normal early out, both sides (btConvexConcaveCollisionAlgorithm.cpp:101-136)
+    {
+        const v3 half = s.impl + v3{s.margin, s.margin, s.margin};
+        const m3 inv = inverse(R);
+        v3 tn = cross(s.t1 - s.t0, s.t2 - s.t0);
+        tn = tn * (1.f / sqrtf(len2(tn)));
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            const v3 ld = inv * tn;
+            const v3 lp = v3{ld.x >= 0 ? half.x : -half.x, ld.y >= 0 ? half.y : -half.y, ld.z >= 0 ? half.z : -half.z};
+            const v3 wp = R * lp + c;
+            const float dist = dot(tn, s.t0) - dot(tn, wp);
+            if (dist > cbt) return false;
+            tn = tn * -1.f;
+        }
+    }
+    const float maxd = s.margin + 0.f + cbt;
+    const float max2 = maxd * maxd;
+    const m3 I = ident3();
+    const v3 po = (c + zero3()) * 0.5f;
+    const v3 oA = c - po, oB = zero3() - po;
+    const float mA = s.margin, mB = 0.f;
+    float distance_ = 0.f;
+    v3 nB = zero3(), pA = zero3(), pB = zero3();
+    v3 v = v3{0.f, 1.f, 0.f};
+    bool valid = false, check = false;
+    int degen = 0, iter = 0;
+    float sqd = kLarge, delta = 0.f;
+    const float margin = mA + mB;
+    Voronoi vs;
+    vor_reset(vs);
+    while (true) {
+        const v3 sa = vmul(-v, R), sb = vmul(v, I);
+        const v3 pw = xf(R, oA, box_nm(s, sa)), qw = xf(I, oB, tri_nm(s, sb));
+        const v3 w = pw - qw;
+        delta = dot(v, w);
+        if ((delta > 0.f) && (delta * delta > sqd * max2)) {
+            degen = 10;
+            check = true;
+            break;
+        }
+        if (vor_in_simplex(vs, w)) {
+            degen = 1;
+            check = true;
+            break;
+        }
+        const float f0 = sqd - delta, f1 = sqd * kRelError2;
+        if (f0 <= f1) {
+            degen = f0 <= 0.f ? 2 : 11;
+            check = true;
+            break;
+        }
+        vs.lastW = w;  // addVertex
+        vs.needs_update = true;
+        put4(vs.W, vs.n, w);
+        put4(vs.P, vs.n, pw);
+        put4(vs.Q, vs.n, qw);
+        vs.n++;
+        const bool ok = vor_update(vs);
+        const v3 nv = vs.cV;
+        if (!ok) {
+            degen = 3;
+            check = true;
+            break;
+        }
+        if (len2(nv) < kRelError2) {
+            v = nv;
+            degen = 6;
+            check = true;
+            break;
+        }
+        const float prev = sqd;
+        sqd = len2(nv);
+        if (prev - sqd <= kEps * prev) {
+            check = true;
+            degen = 12;
+            break;
+        }
+        v = nv;
+        if (iter++ > 1000) break;
+        if (vs.n == 4) {
+            degen = 13;
+            break;
+        }
+    }
+    if (check) {
+        vor_update(vs);  // compute_points
+        pA = vs.cP1;
+        pB = vs.cP2;
+        nB = v;
+        const float l2 = len2(v);
+        if ((double)l2 < 0.0001) degen = 5;
+        if (l2 > kEps * kEps) {
+            const float rlen = 1.f / sqrtf(l2);
+            nB *= rlen;
+            const float sq = sqrtf(sqd);
+            pA -= v * (mA / sq);
+            pB += v * (mB / sq);
+            distance_ = (1.f / rlen) - margin;
+            valid = true;
+        }
+    }
+    const bool catch_degen = degen && ((double)(distance_ + margin) < 0.01);
+    if (!valid || catch_degen) {
+        v3 tA, tB;
+        v = zero3();
+        const bool ok2 = calc_pen_depth(S, s, R, oA, I, oB, v, tA, tB);
+        if (ok2) {
+            v3 tn = tB - tA;
+            float l2 = len2(tn);
+            if (l2 <= kEps * kEps) {
+                tn = v;
+                l2 = len2(v);
+            }
+            if (l2 > kEps * kEps) {
+                tn = tn / sqrtf(l2);
+                const float d2 = -len(tA - tB);
+                if (!valid || d2 < distance_) {
+                    distance_ = d2;
+                    pA = tA;
+                    pB = tB;
+                    nB = tn;
+                    valid = true;
+                }
+            }
+        } else if (len2(v) > 0.f) {
+            const float d2 = len(tA - tB) - margin;
+            if (!valid || d2 < distance_) {
+                distance_ = d2;
+                pA = tA;
+                pB = tB;
+                pA -= v * mA;
+                pB += v * mB;
+                nB = v * (1.f / sqrtf(len2(v)));
+                valid = true;
+            }
+        }
+    }
+    if (!(valid && ((distance_ < 0) || (distance_ * distance_ < max2)))) return false;
+    // normal-direction fix from the two AABB centres (btGjkPairDetector.cpp:930-949)
+    v3 posA, posB;
+    {
+        const v3 hwm = s.impl + v3{s.margin, s.margin, s.margin};
+        const v3 ext = v3{dot(hwm, v3{fabsf(R.r0.x), fabsf(R.r0.y), fabsf(R.r0.z)}),
+                          dot(hwm, v3{fabsf(R.r1.x), fabsf(R.r1.y), fabsf(R.r1.z)}),
+                          dot(hwm, v3{fabsf(R.r2.x), fabsf(R.r2.y), fabsf(R.r2.z)})};
+        const v3 mn = oA - ext, mx = oA + ext;
+        posA = (mx + mn) * 0.5f;
+        v3 tmn, tmx;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            v3 vec = zero3();
+            set_comp(vec, i, 1.f);
+            v3 t = xf(I, oB, tri_nm(s, vmul(vec, I)));
+            set_comp(tmx, i, comp(t, i) + 0.f);
+            set_comp(vec, i, -1.f);
+            t = xf(I, oB, tri_nm(s, vmul(vec, I)));
+            set_comp(tmn, i, comp(t, i) - 0.f);
+        }
+        posB = (tmn + tmx) * 0.5f;
+    }
+    if (dot(posA - posB, nB) < 0.f) nB *= -1.f;
+    normal = nB;
+    point = pB + po;
+    depth = distance_;
+    return true;
+}
+
+}  // namespace gjk
+}  // namespace rl

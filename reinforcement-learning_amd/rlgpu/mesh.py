@@ -191,3 +191,22 @@ def edge_info(mesh):
     _lib.check(L.rlgpu_mesh_edge_info(mesh.tris.ctypes.data, mesh.num_tris, mesh.object_ntris.ctypes.data,
                                       mesh.num_objects, out.ctypes.data), "rlgpu_mesh_edge_info")
     return out
+
+
+def box_triangle_queries(rot, centre, tri, cbt):
+    """The env kernel's car-hitbox vs triangle narrowphase (Bullet's GJK / EPA query, include/rlgpu_mesh.h
+    rlgpu_box_triangle_queries) on the device, one query per lane.  CUDA tensors: rot [n,3,3] (basis rows),
+    centre [n,3], tri [n,3,3], cbt [n] -> [n,8] float32 (hit, normal xyz, point xyz, depth)."""
+    import torch
+    rot = rot.reshape(-1, 9).contiguous().float()
+    n = rot.shape[0]
+    centre = centre.reshape(n, 3).contiguous().float()
+    tri = tri.reshape(n, 9).contiguous().float()
+    cbt = cbt.reshape(n).contiguous().float()
+    out = torch.zeros((n, 8), dtype=torch.float32, device=rot.device)
+    L = _bind()
+    L.rlgpu_box_triangle_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 6
+    _lib.check(L.rlgpu_box_triangle_queries(n, rot.data_ptr(), centre.data_ptr(), tri.data_ptr(), cbt.data_ptr(),
+                                            out.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+               "rlgpu_box_triangle_queries")
+    return out
