@@ -53,9 +53,11 @@ int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object
  * [n][9] (box basis rows), centre [n][3] (hitbox child origin), tri [n][9] (three vertices), cbt [n]
  * (contact breaking threshold); the box is the Octane hitbox.  d_out [n][8] = {hit, normal xyz,
  * point xyz, depth} (the arguments of btManifoldResult::addContactPoint; zeros when no point).
- * Asynchronous on `stream`; scratch for the penetration solver is allocated per call. */
+ * lds_first != 0: the penetration solver first runs in a small LDS work set per lane (24 support
+ * vertices, 28 live faces), rerun in the lane's HBM set when it overflows -- the env kernel's policy;
+ * 0: HBM only.  Asynchronous on `stream`; the HBM sets are allocated per call. */
 int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
-                               const float* d_cbt, float* d_out, void* stream);
+                               const float* d_cbt, float* d_out, int32_t lds_first, void* stream);
 
 #ifdef __cplusplus
 }

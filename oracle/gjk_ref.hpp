@@ -34,6 +34,8 @@ constexpr float REL_ERROR2 = 1.0e-6f;  // btGjkPairDetector.cpp:35
 constexpr float EQUAL_VERTEX_THRESHOLD = 0.0001f;  // VORONOI_DEFAULT_EQUAL_VERTEX_THRESHOLD
 // diagnostics (this thread): EPA runs, EPA iterations, max iterations of one run, max faces taken
 inline thread_local uint64_t epa_stats[4] = {0, 0, 0, 0};
+// diagnostics (this thread): btGjkEpa2 GJK evaluations, their iterations, most iterations of one
+inline thread_local uint64_t gjk2_stats[3] = {0, 0, 0};
 
 struct Tr {  // btTransform: basis rows + origin
     M b;
@@ -555,6 +557,9 @@ struct GJK {
             status = ((++iterations) < (unsigned)GJK_MAX_ITERATIONS) ? status : 2;
         } while (status == 0);
         simplex = &simplices[current];
+        gjk2_stats[0]++;
+        gjk2_stats[1] += iterations;
+        if (iterations > gjk2_stats[2]) gjk2_stats[2] = iterations;
         if (status == 0) distance = len(ray);
         else if (status == 1) distance = 0;
         return status;

@@ -2250,6 +2250,12 @@ void oracle_box_triangle(int n, const float* rot, const float* centre, const flo
 }
 // this thread's box-triangle GJK queries / penetration-solver calls inside arena steps, then EPA runs, EPA
 // iterations, most iterations of one run, most faces one run took (reset after reading)
+void oracle_gjk2_counts(uint64_t* out3) {
+    for (int i = 0; i < 3; i++) {
+        out3[i] = orc::gjk::gjk2_stats[i];
+        orc::gjk::gjk2_stats[i] = 0;
+    }
+}
 void oracle_gjk_counts(uint64_t* out6) {
     out6[0] = orc::gjk_evals[0];
     out6[1] = orc::gjk_evals[1];

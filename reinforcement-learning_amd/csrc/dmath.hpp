@@ -34,7 +34,9 @@ HD v3& operator-=(v3& a, v3 b) { a = a - b; return a; }
 HD v3& operator*=(v3& a, float s) { a = a * s; return a; }
 HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 // one of three vectors by a runtime index, as selects (keeps small vector tables in registers)
-HD v3 sel3(const v3& a, const v3& b, const v3& c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
+HD v3 sel3(v3 a, v3 b, v3 c, int i) {  // per component (a select of lvalues would select addresses)
+    return v3{i == 0 ? a.x : (i == 1 ? b.x : c.x), i == 0 ? a.y : (i == 1 ? b.y : c.y), i == 0 ? a.z : (i == 1 ? b.z : c.z)};
+}
 HD v3 cross(v3 a, v3 b) { return v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 HD float len2(v3 a) { return dot(a, a); }
 HD float len(v3 a) { return sqrtf(len2(a)); }
@@ -67,7 +69,7 @@ HD v3 rs_norm(v3 a) {
 struct m3 {
     v3 r0, r1, r2;
 };
-HD v3 row(const m3& m, int i) { return i == 0 ? m.r0 : (i == 1 ? m.r1 : m.r2); }
+HD v3 row(const m3& m, int i) { return sel3(m.r0, m.r1, m.r2, i); }
 HD v3 col(const m3& m, int i) { return v3{comp(m.r0, i), comp(m.r1, i), comp(m.r2, i)}; }
 HD m3 ident3() { return m3{v3{1, 0, 0}, v3{0, 1, 0}, v3{0, 0, 1}}; }
 HD v3 operator*(const m3& m, v3 v) { return v3{dot(m.r0, v), dot(m.r1, v), dot(m.r2, v)}; }

@@ -378,6 +378,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         A->a.torque[l] = zero3();
         update_inertia(A, l);
     }
+    if (l == 0) A->a.epa_lock = A->a.npen = 0;
     sync(); P.mark(11);
     // ---- StepFirstHalf (EnvSet.cpp:113-130) prelude
     if (g.ticks_first > 0) {
@@ -569,6 +570,10 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         }
     }
     P.mark(15);
+    if (g.prof && valid && l == 0 && A->a.npen) {  // penetration-solver calls: total and this workgroup's
+        atomicAdd(&g.prof[28], (unsigned long long)A->a.npen);
+        atomicAdd(&g.prof[kProfWG + (size_t)blockIdx.x * kProfPhases + 23], (unsigned long long)A->a.npen);
+    }
 }
 
 // ------------------------------------------------------------------ host: constants
@@ -1206,9 +1211,14 @@ extern "C" int rlgpu_envset_set_arenas(rlgpu_envset* e, int32_t first, int32_t c
 
 // ------------------------------------------------------------------ box-triangle queries (tests)
 namespace rl {
-__global__ void __launch_bounds__(64) box_triangle_kernel(int n, const float* rot, const float* centre, const float* tri,
-                                                          const float* cbt, float* out, gjk::GjkScratch* scratch) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
+// lds != 0: each lane first tries a small LDS work set of its own, as the env kernel's lanes do
+__global__ void __launch_bounds__(16) box_triangle_kernel(int n, const float* rot, const float* centre, const float* tri,
+                                                          const float* cbt, float* out, gjk::GjkScratch* scratch,
+                                                          int lds) {
+    __shared__ char small[16][gjk::kSmallBytes];
+    __shared__ int lock[16];
+    const int i = blockIdx.x * 16 + threadIdx.x;
+    lock[threadIdx.x] = 0;
     if (i >= n) return;
     const float* r = rot + 9 * (size_t)i;
     const m3 R = m3{v3{r[0], r[1], r[2]}, v3{r[3], r[4], r[5]}, v3{r[6], r[7], r[8]}};
@@ -1217,7 +1227,9 @@ __global__ void __launch_bounds__(64) box_triangle_kernel(int n, const float* ro
     const gjk::Shape sh{C.car_impl, C.car_margin, v3{t[0], t[1], t[2]}, v3{t[3], t[4], t[5]}, v3{t[6], t[7], t[8]}};
     v3 nrm, pt;
     float d = 0.f;
-    const bool hit = gjk::box_triangle(R, c, sh, cbt[i], scratch + i, nrm, pt, d);
+    gjk::Scr slow = gjk::hbm_view(scratch + i);
+    gjk::Scr fast = gjk::lds_view(small[threadIdx.x]);
+    const bool hit = gjk::box_triangle(R, c, sh, cbt[i], lds ? &fast : nullptr, &lock[threadIdx.x], slow, nrm, pt, d);
     float* o = out + 8 * (size_t)i;
     o[0] = hit ? 1.f : 0.f;
     o[1] = hit ? nrm.x : 0.f;
@@ -1231,7 +1243,7 @@ __global__ void __launch_bounds__(64) box_triangle_kernel(int n, const float* ro
 }  // namespace rl
 
 extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
-                                          const float* d_cbt, float* d_out, void* stream) {
+                                          const float* d_cbt, float* d_out, int32_t lds_first, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(n >= 0, "rlgpu_box_triangle_queries: n must be >= 0");
         if (n == 0) return;
@@ -1240,8 +1252,8 @@ extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const f
         hipStream_t s = (hipStream_t)stream;
         void* scratch = nullptr;
         RLGPU_CHECK_HIP(hipMallocAsync(&scratch, (size_t)n * sizeof(rl::gjk::GjkScratch), s));
-        hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 64)), dim3(64), 0, s, n, d_rot, d_centre, d_tri,
-                           d_cbt, d_out, (rl::gjk::GjkScratch*)scratch);
+        hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 16)), dim3(16), 0, s, n, d_rot, d_centre, d_tri,
+                           d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)(lds_first != 0));
         RLGPU_CHECK_HIP(hipGetLastError());
         RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
     });

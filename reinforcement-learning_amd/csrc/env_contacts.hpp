@@ -431,14 +431,18 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                 v3 mn, mx;
                 body_aabb(bi, bpos(A, bi), R, mn, mx);
                 float cbt = pair_cbt(bi, 10);
-                // Bullet's GJK / EPA per triangle (gjk.hpp); this lane's penetration-solver scratch
+                // Bullet's GJK / EPA per triangle (gjk.hpp).  Penetration-solver work sets: the arena's
+                // small LDS set past the candidate list (free during the narrowphase), one lane at a time,
+                // else this lane's HBM scratch
                 const v3 c = car_box_center(A, bi);
-                gjk::GjkScratch* S = M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x);
+                gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
+                gjk::Scr fast = gjk::lds_view((char*)&A->u.cand[kMaxCand]);
                 grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) {
                     const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2};
                     v3 n, pb;
                     float d;
-                    if (gjk::box_triangle(R, c, sh, cbt, S, n, pb, d)) emit(A, rank, t, mesh_key(bi, obj), n, pb, d);
+                    if (gjk::box_triangle(R, c, sh, cbt, &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
+                        emit(A, rank, t, mesh_key(bi, obj), n, pb, d);
                 });
             }
         }

@@ -155,6 +155,8 @@ struct Aux {
     v3 snap_vel[5], snap_ang[5];
     int active[5];
     int ball_awake, ball_sleep, ncand, nmf;
+    int epa_lock;  // the arena's LDS penetration-solver set is in use (gjk.hpp box_triangle)
+    int npen;      // penetration-solver calls this launch (profiling: prof[28], per-workgroup slot 23)
     int locked[RLGPU_PADS];
     int touched[4];
     int goal;
@@ -165,6 +167,8 @@ struct Aux {
 union Scratch {
     WheelT wt[16];
     Cand cand[kMaxCand];
+    // narrowphase: the candidates, then the small penetration-solver set (gjk::lds_view)
+    char narrow[sizeof(Cand) * kMaxCand + gjk::kSmallBytes];
     Solver sv;
     struct {
         float obs[4][RLGPU_OBS];

@@ -11,9 +11,11 @@
 //       margins, nine guesses, Distance fallback) and the AABB-centre normal-direction fix
 //
 // Layout: the Voronoi GJK state lives in registers (fixed-index arrays, runtime slots picked by selects);
-// the penetration solver's GJK / EPA work set (132 support vertices, 256 polytope faces and their lists,
-// the horizon flood-fill stack) lives in a per-lane GjkScratch in HBM (12 KB; MeshView::gjk), touched only
-// when a query needs the penetration solver.  EPA's face lists are index-linked, in Bullet's list order
+// the penetration solver's GJK / EPA work set (support vertices, polytope faces and their lists, the
+// horizon flood-fill stack) first runs in a small set in the arena's LDS (24 vertices, 28 live faces:
+// every EPA run of the bench workload fits), and only when that overflows, or another lane of the arena
+// holds it, in the lane's full-capacity GjkScratch in HBM (12 KB; MeshView::gjk; Bullet's 128 vertices /
+// 256 faces).  EPA's face lists are index-linked, in Bullet's list order
 // (the stock list's untouched tail is implicit), its recursions (EncloseOrigin, expand) are iterative.
 // Every float operation is Bullet's, in its order (dmath.hpp conventions); the CPU oracle
 // (oracle/gjk_ref.hpp) is an independent restatement and the two agree bit for bit.
@@ -23,6 +25,9 @@
 #ifndef DEV
 #define DEV __device__ __forceinline__
 #endif
+// the penetration solver's big, rarely-run pieces are called, not inlined, and their loops are not
+// unrolled: one copy of each keeps the instruction footprint (and its cache misses) small
+#define GJK_CALLED DEV
 
 namespace rl {
 namespace gjk {
@@ -54,6 +59,26 @@ struct GjkScratch {
     SFace fc[kEpaMaxFaces];
     uint32_t stack[kEpaMaxFaces + 8];  // expand() frames: face | edge << 8 | stage << 10
 };
+// A penetration-solver work set: the full-capacity per-lane HBM scratch, or a small one in the arena's
+// LDS (the narrowphase-time free tail of ArenaLDS::u).  A small set that would need more support
+// vertices, live faces or expand() depth than it holds sets `overflow`; the query is then rerun on the
+// HBM set from the start (every run is deterministic, so the rerun gives Bullet's result).
+struct Scr {
+    SSV* sv;
+    SFace* fc;
+    uint32_t* stack;
+    int max_sv, max_fc, max_stack;
+    int overflow;
+};
+DEV Scr hbm_view(GjkScratch* g) { return Scr{g->sv, g->fc, g->stack, kSV, kEpaMaxFaces, kEpaMaxFaces + 8, 0}; }
+// small set carved from `bytes` of LDS: 24 support vertices (20 EPA iterations), 28 live faces, depth 24
+constexpr int kSmallSV = 24, kSmallFaces = 28, kSmallStack = 24;
+constexpr int kSmallBytes = kSmallSV * (int)sizeof(SSV) + kSmallFaces * (int)sizeof(SFace) + kSmallStack * 4;
+DEV Scr lds_view(char* base) {
+    return Scr{(SSV*)base, (SFace*)(base + kSmallSV * sizeof(SSV)),
+               (uint32_t*)(base + kSmallSV * sizeof(SSV) + kSmallFaces * sizeof(SFace)), kSmallSV, kSmallFaces,
+               kSmallStack, 0};
+}
 
 // ---------------------------------------------------------------- shapes
 struct Shape {
@@ -86,15 +111,19 @@ DEV m3 transpose_times(const m3& a, const m3& m) {  // btMatrix3x3::transposeTim
 }
 
 // runtime slot of a 4-entry register array, as selects / predicated writes
+DEV float pick(bool c, float a, float b) { return c ? a : b; }
+DEV v3 pick(bool c, v3 a, v3 b) { return v3{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
 template <typename T>
-DEV T get4(const T (&a)[4], int i) {
-    return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
+DEV T get4(const T (&a)[4], int i) {  // selects of values (a select of lvalues selects addresses)
+    const T x0 = a[0], x1 = a[1], x2 = a[2], x3 = a[3];
+    return pick(i == 0, x0, pick(i == 1, x1, pick(i == 2, x2, x3)));
 }
+// every slot is rewritten with a select: a conditional store would become a store through a selected
+// pointer, which keeps the array in private (scratch) memory
 template <typename T>
 DEV void put4(T (&a)[4], int i, const T& v) {
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (k == i) a[k] = v;
+    for (int k = 0; k < 4; k++) a[k] = pick(k == i, v, a[k]);
 }
 
 // ---------------------------------------------------------------- btVoronoiSimplexSolver (registers)
@@ -368,12 +397,12 @@ struct Gjk2 {
     v3 ray;
     int status;  // Valid 0, Inside 1, Failed 2
 };
-DEV void getsupport(GjkScratch* S, const Mink& m, v3 d, int idx) {
+DEV void getsupport(Scr& S, const Mink& m, v3 d, int idx) {
     const v3 dn = d / len(d);
-    S->sv[idx].d = dn;
-    S->sv[idx].w = support(m, dn);
+    S.sv[idx].d = dn;
+    S.sv[idx].w = support(m, dn);
 }
-DEV void g2_append(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 v) {
+DEV void g2_append(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 v) {
     put4(s.p, s.rank, 0.f);
     g.nfree--;
     const int idx = (int)((g.freev >> (8 * g.nfree)) & 255u);
@@ -483,9 +512,9 @@ DEV float project4(v3 a, v3 b, v3 c, v3 d, float* w, uint32_t& m) {
     }
     return -1;
 }
-DEV v3 svw(const GjkScratch* S, int i) { return S->sv[i].w; }
+DEV v3 svw(const Scr& S, int i) { return S.sv[i].w; }
 // GJK::Evaluate (cpp:201-337); on return g.cs is m_simplex
-DEV int g2_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, v3 guess) {
+GJK_CALLED int g2_evaluate(Scr& S, const Mink& m, Gjk2& g, v3 guess) {
     unsigned iterations = 0;
     float sqdist = 0, alpha = 0;
     v3 lastw[4];
@@ -570,11 +599,11 @@ DEV int g2_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, v3 guess) {
     return g.status;
 }
 // GJK::EncloseOrigin (cpp:338-402), its recursion unrolled by rank
-DEV bool enclose4(const GjkScratch* S, const Simp& s) {
+DEV bool enclose4(const Scr& S, const Simp& s) {
     const v3 w3 = svw(S, sc(s, 3));
     return fabsf(det3(svw(S, sc(s, 0)) - w3, svw(S, sc(s, 1)) - w3, svw(S, sc(s, 2)) - w3)) > 0;
 }
-DEV bool enclose3(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
+GJK_CALLED bool enclose3(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
     const v3 w0 = svw(S, sc(s, 0));
     const v3 n = cross(svw(S, sc(s, 1)) - w0, svw(S, sc(s, 2)) - w0);
     if (len2(n) > 0) {
@@ -587,8 +616,9 @@ DEV bool enclose3(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
     }
     return false;
 }
-DEV bool enclose2(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
+GJK_CALLED bool enclose2(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
     const v3 d = svw(S, sc(s, 1)) - svw(S, sc(s, 0));
+#pragma unroll 1
     for (int i = 0; i < 3; ++i) {
         v3 axis = zero3();
         set_comp(axis, i, 1.f);
@@ -604,8 +634,9 @@ DEV bool enclose2(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
     }
     return false;
 }
-DEV bool enclose_origin(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s) {
+DEV bool enclose_origin(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
     if (s.rank == 1) {
+#pragma unroll 1
         for (int i = 0; i < 3; ++i) {
             v3 axis = zero3();
             set_comp(axis, i, 1.f);
@@ -633,27 +664,27 @@ struct Epa {
     int status;       // Valid 0 .. Failed 9 (EPA::eStatus order)
     int nextsv;
 };
-DEV void list_append(GjkScratch* S, uint16_t& root, int face) {
-    SFace& f = S->fc[face];
+DEV void list_append(Scr& S, uint16_t& root, int face) {
+    SFace& f = S.fc[face];
     f.l[0] = kNone;
     f.l[1] = root;
-    if (root != kNone) S->fc[root].l[0] = (uint16_t)face;
+    if (root != kNone) S.fc[root].l[0] = (uint16_t)face;
     root = (uint16_t)face;
 }
-DEV void list_remove(GjkScratch* S, uint16_t& root, int face) {
-    SFace& f = S->fc[face];
-    if (f.l[1] != kNone) S->fc[f.l[1]].l[0] = f.l[0];
-    if (f.l[0] != kNone) S->fc[f.l[0]].l[1] = f.l[1];
+DEV void list_remove(Scr& S, uint16_t& root, int face) {
+    SFace& f = S.fc[face];
+    if (f.l[1] != kNone) S.fc[f.l[1]].l[0] = f.l[0];
+    if (f.l[0] != kNone) S.fc[f.l[0]].l[1] = f.l[1];
     if (face == root) root = f.l[1];
 }
-DEV void stock_push(GjkScratch* S, Epa& E, int face) { list_append(S, E.stock, face); }
-DEV void bind(GjkScratch* S, int fa, int ea, int fb, int eb) {
-    S->fc[fa].e[ea] = (uint8_t)eb;
-    S->fc[fa].f[ea] = (uint8_t)fb;
-    S->fc[fb].e[eb] = (uint8_t)ea;
-    S->fc[fb].f[eb] = (uint8_t)fa;
+DEV void stock_push(Scr& S, Epa& E, int face) { list_append(S, E.stock, face); }
+DEV void bind(Scr& S, int fa, int ea, int fb, int eb) {
+    S.fc[fa].e[ea] = (uint8_t)eb;
+    S.fc[fa].f[ea] = (uint8_t)fb;
+    S.fc[fb].e[eb] = (uint8_t)ea;
+    S.fc[fb].f[eb] = (uint8_t)fa;
 }
-DEV bool getedgedist(const GjkScratch* S, v3 fn, int a, int b, float& dist) {
+DEV bool getedgedist(const Scr& S, v3 fn, int a, int b, float& dist) {
     const v3 aw = svw(S, a), bw = svw(S, b);
     const v3 ba = bw - aw;
     const v3 n_ab = cross(ba, fn);
@@ -676,20 +707,23 @@ DEV bool getedgedist(const GjkScratch* S, v3 fn, int a, int b, float& dist) {
     return false;
 }
 // EPA::newface; returns the face or -1
-DEV int newface(GjkScratch* S, Epa& E, int a, int b, int c, bool forced) {
+DEV int newface(Scr& S, Epa& E, int a, int b, int c, bool forced) {
     int face;
     if (E.stock != kNone) {
         face = E.stock;
         list_remove(S, E.stock, face);
-    } else if (E.fresh < kEpaMaxFaces) {
+    } else if (E.fresh < S.max_fc) {
         face = E.fresh++;
+    } else if (E.hull_count >= kEpaMaxFaces) {
+        E.status = 5;  // OutOfFaces (Bullet's stock is empty: all 256 faces are in the hull)
+        return -1;
     } else {
-        E.status = 5;  // OutOfFaces (the stock is empty)
+        S.overflow = 1;  // Bullet still has stock faces: too small a work set
         return -1;
     }
     list_append(S, E.hull, face);
     E.hull_count++;
-    SFace& F = S->fc[face];
+    SFace& F = S.fc[face];
     F.pass = 0;
     F.c[0] = (uint8_t)a;
     F.c[1] = (uint8_t)b;
@@ -714,11 +748,11 @@ DEV int newface(GjkScratch* S, Epa& E, int a, int b, int c, bool forced) {
     stock_push(S, E, face);
     return -1;
 }
-DEV int findbest(const GjkScratch* S, const Epa& E) {
+DEV int findbest(const Scr& S, const Epa& E) {
     int minf = E.hull;
-    float mind = S->fc[minf].d * S->fc[minf].d;
-    for (int f = S->fc[minf].l[1]; f != kNone; f = S->fc[f].l[1]) {
-        const float sqd = S->fc[f].d * S->fc[f].d;
+    float mind = S.fc[minf].d * S.fc[minf].d;
+    for (int f = S.fc[minf].l[1]; f != kNone; f = S.fc[f].l[1]) {
+        const float sqd = S.fc[f].d * S.fc[f].d;
         if (sqd < mind) {
             minf = f;
             mind = sqd;
@@ -727,19 +761,20 @@ DEV int findbest(const GjkScratch* S, const Epa& E) {
     return minf;
 }
 // EPA::expand (cpp:864-900) as an explicit-stack walk: frame = face | edge << 8 | stage << 10
-DEV bool expand(GjkScratch* S, Epa& E, unsigned pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
+GJK_CALLED bool expand(Scr& S, Epa& E, unsigned pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
     int sp = 0;
-    S->stack[sp++] = (uint32_t)f0 | ((uint32_t)e0 << 8);
+    S.stack[sp++] = (uint32_t)f0 | ((uint32_t)e0 << 8);
     bool ret = false;
     while (sp > 0) {
-        const uint32_t fr = S->stack[sp - 1];
+        const uint32_t fr = S.stack[sp - 1];
         const int f = (int)(fr & 255u), e = (int)((fr >> 8) & 3u), stage = (int)(fr >> 10);
         const int e1 = e == 2 ? 0 : e + 1, e2 = e == 0 ? 2 : e - 1;
         if (stage == 0) {
-            SFace& F = S->fc[f];
+            SFace& F = S.fc[f];
             if (F.pass != (uint8_t)pass) {
                 if ((dot(F.n, svw(S, w)) - F.d) < -kEpaPlaneEps) {
                     const int nf = newface(S, E, F.c[e1], F.c[e], w, false);
+                    if (S.overflow) return false;
                     ret = false;
                     if (nf >= 0) {
                         bind(S, nf, 0, f, e);
@@ -754,8 +789,12 @@ DEV bool expand(GjkScratch* S, Epa& E, unsigned pass, int w, int f0, int e0, int
                     sp--;
                 } else {
                     F.pass = (uint8_t)pass;
-                    S->stack[sp - 1] = fr | (1u << 10);
-                    S->stack[sp++] = (uint32_t)F.f[e1] | ((uint32_t)F.e[e1] << 8);
+                    if (sp >= S.max_stack) {
+                        S.overflow = 1;
+                        return false;
+                    }
+                    S.stack[sp - 1] = fr | (1u << 10);
+                    S.stack[sp++] = (uint32_t)F.f[e1] | ((uint32_t)F.e[e1] << 8);
                 }
             } else {
                 ret = false;
@@ -765,9 +804,13 @@ DEV bool expand(GjkScratch* S, Epa& E, unsigned pass, int w, int f0, int e0, int
             if (!ret) {
                 sp--;
             } else {
-                const SFace& F = S->fc[f];
-                S->stack[sp - 1] = (fr & 1023u) | (2u << 10);
-                S->stack[sp++] = (uint32_t)F.f[e2] | ((uint32_t)F.e[e2] << 8);
+                const SFace& F = S.fc[f];
+                if (sp >= S.max_stack) {
+                    S.overflow = 1;
+                    return false;
+                }
+                S.stack[sp - 1] = (fr & 1023u) | (2u << 10);
+                S.stack[sp++] = (uint32_t)F.f[e2] | ((uint32_t)F.e[e2] << 8);
             }
         } else {
             if (ret) {
@@ -781,7 +824,7 @@ DEV bool expand(GjkScratch* S, Epa& E, unsigned pass, int w, int f0, int e0, int
     return ret;
 }
 // EPA::Evaluate (cpp:648-768) on the GJK's simplex s; out: normal, depth, result (rank, c, p)
-DEV int epa_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v3& normal, float& depth, Simp& res) {
+GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v3& normal, float& depth, Simp& res) {
     Epa E;
     E.hull = kNone;
     E.hull_count = 0;
@@ -808,9 +851,10 @@ DEV int epa_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
         const int t1 = newface(S, E, s1, s0, s3, true);
         const int t2 = newface(S, E, s2, s1, s3, true);
         const int t3 = newface(S, E, s0, s2, s3, true);
+        if (S.overflow) return 9;
         if (E.hull_count == 4) {
             int best = findbest(S, E);
-            SFace outer = S->fc[best];
+            SFace outer = S.fc[best];
             unsigned pass = 0;
             bind(S, t0, 0, t1, 0);
             bind(S, t0, 1, t2, 0);
@@ -821,24 +865,30 @@ DEV int epa_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
             E.status = 0;
             for (int iterations = 0; iterations < kEpaMaxIterations; ++iterations) {
                 if (E.nextsv < kEpaMaxVertices) {
+                    if (4 + E.nextsv >= S.max_sv) {
+                        S.overflow = 1;
+                        return 9;
+                    }
                     int hcf = -1, hff = -1, hnf = 0;
                     const int w = 4 + E.nextsv++;
                     bool valid = true;
-                    S->fc[best].pass = (uint8_t)(++pass);
-                    const v3 bn = S->fc[best].n;
-                    const float bd = S->fc[best].d;
+                    S.fc[best].pass = (uint8_t)(++pass);
+                    const v3 bn = S.fc[best].n;
+                    const float bd = S.fc[best].d;
                     getsupport(S, m, bn, w);
                     const float wdist = dot(bn, svw(S, w)) - bd;
                     if (wdist > kEpaAccuracy) {
-                        for (int j = 0; (j < 3) && valid; ++j)
-                            valid &= expand(S, E, pass, w, S->fc[best].f[j], S->fc[best].e[j], hcf, hff, hnf);
+                        for (int j = 0; (j < 3) && valid; ++j) {
+                            valid &= expand(S, E, pass, w, S.fc[best].f[j], S.fc[best].e[j], hcf, hff, hnf);
+                            if (S.overflow) return 9;
+                        }
                         if (valid && (hnf >= 3)) {
                             bind(S, hcf, 1, hff, 2);
                             list_remove(S, E.hull, best);
                             E.hull_count--;
                             stock_push(S, E, best);
                             best = findbest(S, E);
-                            outer = S->fc[best];
+                            outer = S.fc[best];
                         } else {
                             E.status = 4;  // InvalidHull
                             break;
@@ -887,7 +937,7 @@ DEV int epa_evaluate(GjkScratch* S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
 }
 
 // btGjkEpaSolver2::Penetration (cpp:973-1017) with margins; t0 / t1 = (basis, origin)
-DEV bool penetration(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
+DEV bool penetration(Scr& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
                      v3& nrm) {
     const Mink m = make_mink(sh, b0, o0, b1, o1, true);
     Gjk2 g;
@@ -896,16 +946,16 @@ DEV bool penetration(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const 
     float ed;
     Simp res;
     const int es = epa_evaluate(S, m, g, g.cs, -guess, en, ed, res);
-    if (es == 9) return false;
+    if (es == 9 || S.overflow) return false;
     v3 w0 = zero3();
-    for (int i = 0; i < res.rank; ++i) w0 += support0(m, S->sv[sc(res, i)].d) * get4(res.p, i);
+    for (int i = 0; i < res.rank; ++i) w0 += support0(m, S.sv[sc(res, i)].d) * get4(res.p, i);
     wA = xf(b0, o0, w0);
     wB = xf(b0, o0, w0 - en * ed);
     nrm = -en;
     return true;
 }
 // btGjkEpaSolver2::Distance (cpp:937-970), margins off
-DEV bool distance(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
+DEV bool distance(Scr& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
                   v3& nrm) {
     const Mink m = make_mink(sh, b0, o0, b1, o1, false);
     Gjk2 g;
@@ -913,7 +963,7 @@ DEV bool distance(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const m3&
     v3 w0 = zero3(), w1 = zero3();
     for (int i = 0; i < g.cs.rank; ++i) {
         const float p = get4(g.cs.p, i);
-        const v3 d = S->sv[sc(g.cs, i)].d;
+        const v3 d = S.sv[sc(g.cs, i)].d;
         w0 += support0(m, d) * p;
         w1 += support1(m, -d) * p;
     }
@@ -926,7 +976,8 @@ DEV bool distance(GjkScratch* S, const Shape& sh, const m3& b0, v3 o0, const m3&
 }
 // btGjkEpaPenetrationDepthSolver::calcPenDepth (cpp:22-79); called, not inlined: the rare path stays out
 // of the narrowphase's hot code
-__device__ __noinline__ bool calc_pen_depth(GjkScratch* S, const Shape& sh, const m3& bA, v3 oA, const m3& bB, v3 oB, v3& v, v3& wA, v3& wB) {
+__device__ __noinline__ bool calc_pen_depth(Scr& S, const Shape& sh, const m3& bA, v3 oA, const m3& bB, v3 oB, v3& v, v3& wA, v3& wB) {
+#pragma unroll 1
     for (int i = 0; i < 9; i++) {
         v3 g;
         if (i == 0) g = safe_normalized(oB - oA);
@@ -939,6 +990,7 @@ __device__ __noinline__ bool calc_pen_depth(GjkScratch* S, const Shape& sh, cons
         else if (i == 7) g = v3{0, 1, 1};
         else g = v3{1, 0, 1};
         if (penetration(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return true;
+        if (S.overflow) return false;
         if (distance(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return false;
     }
     wA = wB = v = zero3();
@@ -948,7 +1000,10 @@ __device__ __noinline__ bool calc_pen_depth(GjkScratch* S, const Shape& sh, cons
 // One box-triangle query (the caller did the AABB test).  R / c: the hitbox child's world basis and
 // origin; cbt: the pair manifold's contact breaking threshold.  True when Bullet would call
 // btManifoldResult::addContactPoint(normal, point, depth).  S: this lane's penetration-solver scratch.
-DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, GjkScratch* S, v3& normal, v3& point, float& depth) {
+// fast / lock: a small LDS work set and the lock that serialises it among the arena's lanes (null: HBM
+// only); slow: this lane's HBM set.
+DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, int* lock, Scr& slow, v3& normal,
+                      v3& point, float& depth, int* pen_count = nullptr) {
     // normal early out, both sides (btConvexConcaveCollisionAlgorithm.cpp:101-136)
     {
         const v3 half = s.impl + v3{s.margin, s.margin, s.margin};
@@ -1055,7 +1110,20 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, GjkScratch* 
     if (!valid || catch_degen) {
         v3 tA, tB;
         v = zero3();
-        const bool ok2 = calc_pen_depth(S, s, R, oA, I, oB, v, tA, tB);
+        bool ok2;
+        if (pen_count) atomicAdd(pen_count, 1);
+        if (fast && atomicCAS(lock, 0, 1) == 0) {
+            fast->overflow = 0;
+            ok2 = calc_pen_depth(*fast, s, R, oA, I, oB, v, tA, tB);
+            const bool redo = fast->overflow != 0;
+            atomicExch(lock, 0);
+            if (redo) {
+                v = zero3();
+                ok2 = calc_pen_depth(slow, s, R, oA, I, oB, v, tA, tB);
+            }
+        } else {
+            ok2 = calc_pen_depth(slow, s, R, oA, I, oB, v, tA, tB);
+        }
         if (ok2) {
             v3 tn = tB - tA;
             float l2 = len2(tn);

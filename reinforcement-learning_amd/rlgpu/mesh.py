@@ -193,10 +193,11 @@ def edge_info(mesh):
     return out
 
 
-def box_triangle_queries(rot, centre, tri, cbt):
+def box_triangle_queries(rot, centre, tri, cbt, lds_first=True):
     """The env kernel's car-hitbox vs triangle narrowphase (Bullet's GJK / EPA query, include/rlgpu_mesh.h
     rlgpu_box_triangle_queries) on the device, one query per lane.  CUDA tensors: rot [n,3,3] (basis rows),
-    centre [n,3], tri [n,3,3], cbt [n] -> [n,8] float32 (hit, normal xyz, point xyz, depth)."""
+    centre [n,3], tri [n,3,3], cbt [n] -> [n,8] float32 (hit, normal xyz, point xyz, depth).  lds_first: the
+    penetration solver runs in a small LDS set first (the env kernel's policy), else in HBM only."""
     import torch
     rot = rot.reshape(-1, 9).contiguous().float()
     n = rot.shape[0]
@@ -205,8 +206,9 @@ def box_triangle_queries(rot, centre, tri, cbt):
     cbt = cbt.reshape(n).contiguous().float()
     out = torch.zeros((n, 8), dtype=torch.float32, device=rot.device)
     L = _bind()
-    L.rlgpu_box_triangle_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 6
+    L.rlgpu_box_triangle_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 5 + [ctypes.c_int32, ctypes.c_void_p]
     _lib.check(L.rlgpu_box_triangle_queries(n, rot.data_ptr(), centre.data_ptr(), tri.data_ptr(), cbt.data_ptr(),
-                                            out.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                                            out.data_ptr(), int(bool(lds_first)),
+                                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
                "rlgpu_box_triangle_queries")
     return out

@@ -115,8 +115,10 @@ def test_device_box_triangle_bit_exact(gpu):
     from rlgpu.mesh import box_triangle_queries
     R, c, t, cbt = make_cases(20000, seed=7)
     want, counts = oracle.box_triangle(R, c, t, cbt)
-    got = box_triangle_queries(torch.from_numpy(R).to(gpu), torch.from_numpy(c).to(gpu), torch.from_numpy(t).to(gpu),
-                               torch.from_numpy(cbt).to(gpu)).cpu().numpy()
-    bad = np.nonzero(np.any(_canon(got) != _canon(want), axis=1))[0]
     assert counts[1] > 1000
-    assert len(bad) == 0, f"{len(bad)} of {len(R)} differ; first {bad[:5]}: got {got[bad[:2]]} want {want[bad[:2]]}"
+    args = [torch.from_numpy(a).to(gpu) for a in (R, c, t, cbt)]
+    for lds_first in (False, True):  # full-capacity HBM sets; small LDS sets with the HBM rerun
+        got = box_triangle_queries(*args, lds_first=lds_first).cpu().numpy()
+        bad = np.nonzero(np.any(_canon(got) != _canon(want), axis=1))[0]
+        assert len(bad) == 0, f"lds_first={lds_first}: {len(bad)} of {len(R)} differ; first {bad[:5]}: " \
+                              f"got {got[bad[:2]]} want {want[bad[:2]]}"

@@ -3,6 +3,7 @@ import ctypes
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -39,6 +40,7 @@ L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.
 _lib.check(L.rlgpu_envset_set_profile(env._h, ctypes.c_void_p(prof.data_ptr()), prof.numel()), "set_profile")
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 tot_ms = 0.0
+pen_rows = []  # per step: penetration-solver calls in all / the busiest / the slowest workgroup
 for i in range(steps):
     acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
     e0.record()
@@ -50,6 +52,8 @@ for i in range(steps):
     tots = per.sum(1)
     k = int(tots.argmax())
     spread.append((tots.max().item(), tots.mean().item(), per[k].cpu(), per.mean(0).cpu()))
+    pens = prof[KW:].view(wg, KP)[:, 23]
+    pen_rows.append((int(pens.sum()), int(pens.max()), int(pens[k])))
     prof[KW:].zero_()
 c = prof.cpu().tolist()
 total = sum(c[:23])
@@ -70,3 +74,6 @@ mean = sum(x[3] for x in spread) / len(spread)
 order = sorted(range(23), key=lambda k: -(slow[k] - mean[k]).item())
 for k in order[:8]:
     print(f"    {NAMES[k]:28s} slowest {slow[k].item():10.0f}  mean {mean[k].item():10.0f}  excess {slow[k].item() - mean[k].item():10.0f}")
+pr = np.array(pen_rows)
+print(f"  penetration-solver (EPA) calls per step: mean {pr[:, 0].mean():.1f} over all workgroups, busiest workgroup "
+      f"{pr[:, 1].mean():.1f} (max {pr[:, 1].max()}), slowest workgroup {pr[:, 2].mean():.1f}")

@@ -20,13 +20,11 @@ pen = np.zeros(len(R), bool)
 for i in range(len(R)):
     _, cnt = oracle.box_triangle(R[i:i + 1], c[i:i + 1], t[i:i + 1], cbt[i:i + 1])
     pen[i] = cnt[1] > 0
-sets = {"gjk-only": np.nonzero(~pen & (out[:, 0] == 1))[0], "penetration": np.nonzero(pen)[0],
+sets = {"empty": np.zeros(0, int), "gjk-only": np.nonzero(~pen & (out[:, 0] == 1))[0], "penetration": np.nonzero(pen)[0],
         "no-hit": np.nonzero(out[:, 0] == 0)[0]}
 for name, idx in sets.items():
-    for n in (64, 1024, 4096):
-        if len(idx) == 0:
-            continue
-        sel = np.resize(idx, n)
+    for n in (1, 16, 64, 1024):
+        sel = np.resize(idx, n) if len(idx) else np.resize(np.nonzero(out[:, 0] == 0)[0], n)
         args = [torch.from_numpy(np.ascontiguousarray(a[sel])).to(dev) for a in (R, c, t, cbt)]
         for _ in range(3):
             box_triangle_queries(*args)
@@ -38,4 +36,12 @@ for name, idx in sets.items():
             box_triangle_queries(*args)
         e1.record()
         torch.cuda.synchronize()
-        print(f"{name:12s} n={n:5d}: {e0.elapsed_time(e1) / reps * 1e3:9.1f} us per launch (incl. scratch alloc)", flush=True)
+        t_lds = e0.elapsed_time(e1) / reps * 1e3
+        e0.record()
+        for _ in range(reps):
+            box_triangle_queries(*args, lds_first=False)
+        e1.record()
+        torch.cuda.synchronize()
+        t_hbm = e0.elapsed_time(e1) / reps * 1e3
+        print(f"{name:12s} n={n:5d}: {t_lds:9.1f} us per launch LDS-first, {t_hbm:9.1f} us HBM only (incl. scratch alloc)",
+              flush=True)

@@ -1,0 +1,59 @@
+// Micro-benchmark of one box-triangle query on one lane (gjk.hpp): in-kernel clock64 cycles of the whole
+// query, for a shallow (GJK only) and a deep (penetration solver) pose, LDS-first and HBM work sets.
+// Built with different flags by tools/micro/run_gjk_micro.sh (experiments, not product code).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#include "../../reinforcement-learning_amd/csrc/gjk.hpp"
+
+using namespace rl;
+
+__global__ void __launch_bounds__(64) k(int mode, float gap, unsigned long long* out, float* res, gjk::GjkScratch* hbm) {
+    __shared__ char small[gjk::kSmallBytes];
+    __shared__ int lock;
+    lock = 0;
+    if (threadIdx.x != 0) return;
+    const v3 impl = v3{1.1664109f, 0.8283349f, 0.3479319f};
+    const float margin = 0.0386591f;
+    gjk::Shape sh{impl, margin, v3{-50.f, -50.f, 0.f}, v3{50.f, -50.f, 0.f}, v3{0.f, 60.f, 0.f}};
+    const float c0 = 0.3f, s0 = 0.2f;  // a tilted box
+    m3 R = m3{v3{1, 0, 0}, v3{0, c0 / sqrtf(c0 * c0 + s0 * s0), -s0 / sqrtf(c0 * c0 + s0 * s0)},
+              v3{0, s0 / sqrtf(c0 * c0 + s0 * s0), c0 / sqrtf(c0 * c0 + s0 * s0)}};
+    float ext = fabsf(R.r2.x) * (impl.x + margin) + fabsf(R.r2.y) * (impl.y + margin) + fabsf(R.r2.z) * (impl.z + margin);
+    v3 c = v3{0.1f, 0.2f, ext + gap};
+    gjk::Scr slow = gjk::hbm_view(hbm);
+    gjk::Scr fast = gjk::lds_view(small);
+    v3 n, p;
+    float d = 0;
+    int pen = 0;
+    long long t0 = clock64();
+    bool hit = gjk::box_triangle(R, c, sh, 0.02f, mode ? &fast : nullptr, &lock, slow, n, p, d, &pen);
+    long long t1 = clock64();
+    out[0] = (unsigned long long)(t1 - t0);
+    out[1] = (unsigned long long)pen;
+    res[0] = hit;
+    res[1] = d;
+}
+
+int main() {
+    unsigned long long* out;
+    float* res;
+    gjk::GjkScratch* hbm;
+    hipMalloc(&out, 16);
+    hipMalloc(&res, 8);
+    hipMalloc(&hbm, sizeof(gjk::GjkScratch));
+    for (int mode = 0; mode < 2; mode++)
+        for (float gap : {0.01f, -0.02f, -0.1f, -0.3f}) {
+            unsigned long long best = ~0ull, o[2];
+            float r[2];
+            for (int rep = 0; rep < 5; rep++) {
+                hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, mode, gap, out, res, hbm);
+                hipMemcpy(o, out, 16, hipMemcpyDeviceToHost);
+                hipMemcpy(r, res, 8, hipMemcpyDeviceToHost);
+                if (o[0] < best) best = o[0];
+            }
+            printf("%s gap %+.2f: %8llu cycles (pen-solver calls %llu, hit %.0f depth %+.5f)\n", mode ? "LDS-first" : "HBM-only ",
+                   gap, best, o[1], r[0], r[1]);
+        }
+    return 0;
+}
