@@ -184,6 +184,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
         }
         A->a.ball_awake = awake;
         A->a.ncand = 0;
+        A->a.nq = 0;
     }
     sync();
     P.mark(4);
@@ -198,6 +199,8 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
                 narrow_pair(A, M, j < 20 ? (j / 4) * 5 + 1 + (j % 4) : 25 + (j - 20));
             }
         }
+    sync();
+    if (valid) narrow_queue(A, M, l);
     sync();
     P.mark(5);
     if (valid && l == 0) {

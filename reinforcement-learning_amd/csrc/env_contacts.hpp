@@ -392,6 +392,31 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
                dl.z >= 0 ? C.car_half.z : -C.car_half.z};
     return R * lv + c;
 }
+// One car hitbox vs mesh triangle: Bullet's GJK / EPA query (gjk.hpp) and its candidate.  Penetration-
+// solver work sets: the arena's small LDS set past the candidate list (free during the narrowphase), one
+// lane at a time, else this lane's HBM scratch.
+DEV void box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2) {
+    const m3 R = brot(A, bi);
+    const v3 c = car_box_center(A, bi);
+    gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
+    gjk::Scr fast = gjk::lds_view((char*)&A->u.cand[kMaxCand]);
+    const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2};
+    v3 n, pb;
+    float d;
+    if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
+        emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
+}
+// the queued box-triangle queries, dealt round-robin over the arena's lanes
+DEV void narrow_queue(ArenaLDS* A, const MeshView& M, int l) {
+    const int nq = stdmin(A->a.nq, kQueue);
+    for (int k = l; k < nq; k += kTeam) {
+        const uint32_t e = A->a.q[k];
+        const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)(e >> 25);
+        const float4 a = M.tri[3 * (size_t)t], b = M.tri[3 * (size_t)t + 1], c = M.tri[3 * (size_t)t + 2];
+        box_tri_query(A, M, bi, t, obj, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{c.x, c.y, c.z});
+    }
+}
+
 // runs the narrowphase of one canonical pair rank and emits candidates; returns 1 when it ran.
 // Body-vs-mesh ranks are split over `parts` lanes (grid entries dealt round-robin); candidates
 // carry (rank, triangle), so the commit order does not depend on the split.
@@ -431,18 +456,14 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                 v3 mn, mx;
                 body_aabb(bi, bpos(A, bi), R, mn, mx);
                 float cbt = pair_cbt(bi, 10);
-                // Bullet's GJK / EPA per triangle (gjk.hpp).  Penetration-solver work sets: the arena's
-                // small LDS set past the candidate list (free during the narrowphase), one lane at a time,
-                // else this lane's HBM scratch
-                const v3 c = car_box_center(A, bi);
-                gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
-                gjk::Scr fast = gjk::lds_view((char*)&A->u.cand[kMaxCand]);
+                // triangles past the AABB test are queued for Bullet's GJK / EPA query (box_tri_query),
+                // which the arena's 16 lanes then share evenly (narrow_queue); a full queue runs them here
                 grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) {
-                    const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2};
-                    v3 n, pb;
-                    float d;
-                    if (gjk::box_triangle(R, c, sh, cbt, &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
-                        emit(A, rank, t, mesh_key(bi, obj), n, pb, d);
+                    const int slot = atomicAdd(&A->a.nq, 1);
+                    if (slot < kQueue)
+                        A->a.q[slot] = (uint32_t)t | ((uint32_t)obj << 20) | ((uint32_t)bi << 25);
+                    else
+                        box_tri_query(A, M, bi, t, obj, v0, v1, v2);
                 });
             }
         }

@@ -44,6 +44,7 @@ constexpr int kMaxCand = 64;        // narrowphase candidates per tick per arena
 constexpr int kMaxRows = RLGPU_MAX_SOLVER_ROWS;  // solver contact rows per arena (+ as many friction rows)
 constexpr int kPairs = 35;          // 25 dynamic-static + 10 dynamic-dynamic work items ("ranks")
 constexpr int kMeshChunks = 6;      // lanes per body-vs-mesh pair in the narrowphase
+constexpr int kQueue = 64;          // box-triangle queries queued per arena and tick (more run at once)
 // Manifold keys, ascending in Bullet's pair order (rsim_ref.cpp pair_key restates the same):
 //   dynamic-static  body * kStat + s, s = mesh object 0..kMaxObj-1, then kMaxObj + plane 0..3
 //                   (meshes are created before the planes, Arena.cpp:1015-1100, and a cell's static
@@ -157,6 +158,8 @@ struct Aux {
     int ball_awake, ball_sleep, ncand, nmf;
     int epa_lock;  // the arena's LDS penetration-solver set is in use (gjk.hpp box_triangle)
     int npen;      // penetration-solver calls this launch (profiling: prof[28], per-workgroup slot 23)
+    int nq;        // this tick's queued box-triangle queries (q: triangle | object << 20 | body << 25)
+    uint32_t q[kQueue];
     int locked[RLGPU_PADS];
     int touched[4];
     int goal;
