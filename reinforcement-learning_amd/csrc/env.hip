@@ -108,7 +108,8 @@ DEV void load_pad_regs(PadRegs& R, int l) {
 #ifndef RLGPU_TICK_ATTR
 #define RLGPU_TICK_ATTR DEV
 #endif
-RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R) {
+RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R,
+                          int nvalid) {
     if (valid && l == 0) {
         rlgpu_arena_state& s = A->s;
         bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
@@ -200,7 +201,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
             }
         }
     sync();
-    if (valid) narrow_queue(A, M, l);
+    narrow_queue(A - (threadIdx.x >> 4), nvalid, M);
     sync();
     P.mark(5);
     if (valid && l == 0) {
@@ -421,7 +422,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
                 sync(); P.mark(11);
             }
             if (t >= t1 + t2) break;
-            tick(A, g.mesh, l, valid, g.seed, arena, P, pregs);
+            tick(A, g.mesh, l, valid, g.seed, arena, P, pregs, stdmin(kArenas, g.n - (int)blockIdx.x * kArenas));
         }
     }
     // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks

@@ -406,11 +406,23 @@ DEV void box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v
     if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
         emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
 }
-// the queued box-triangle queries, dealt round-robin over the arena's lanes
-DEV void narrow_queue(ArenaLDS* A, const MeshView& M, int l) {
-    const int nq = stdmin(A->a.nq, kQueue);
-    for (int k = l; k < nq; k += kTeam) {
-        const uint32_t e = A->a.q[k];
+// the queued box-triangle queries of the workgroup's arenas, dealt round-robin over all its lanes (an
+// arena with many triangle contacts borrows the lanes of quiet ones); base = the workgroup's arenas,
+// nvalid = how many of them exist
+DEV void narrow_queue(ArenaLDS* base, int nvalid, const MeshView& M) {
+    int start[kArenas + 1];
+    start[0] = 0;
+#pragma unroll
+    for (int a = 0; a < kArenas; a++) start[a + 1] = start[a] + (a < nvalid ? stdmin(base[a].a.nq, kQueue) : 0);
+    for (int k = threadIdx.x; k < start[kArenas]; k += kWG) {
+        int ar = 0;
+#pragma unroll
+        for (int j = 1; j < kArenas; j++) ar += k >= start[j] ? 1 : 0;
+        int off = start[0];
+#pragma unroll
+        for (int j = 1; j < kArenas; j++) off = ar == j ? start[j] : off;
+        ArenaLDS* A = base + ar;
+        const uint32_t e = A->a.q[k - off];
         const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)(e >> 25);
         const float4 a = M.tri[3 * (size_t)t], b = M.tri[3 * (size_t)t + 1], c = M.tri[3 * (size_t)t + 2];
         box_tri_query(A, M, bi, t, obj, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{c.x, c.y, c.z});
