@@ -59,6 +59,14 @@ int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object
 int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
                                const float* d_cbt, float* d_out, int32_t lds_first, void* stream);
 
+/* The car-vs-car hitbox narrowphase of the env kernel on its own (btBoxBoxDetector::getClosestPoints ->
+ * dBoxBox2, btBoxBoxDetector.cpp:267-767), on the device, one query per lane: n queries of device arrays
+ * rot_a / rot_b [n][9] (basis rows), centre_a / centre_b [n][3] (hitbox child origins), both boxes the
+ * Octane hitbox.  d_out [n][29] = {count, then up to 4 x (normal on B xyz, point xyz, depth)} (the
+ * btManifoldResult::addContactPoint calls in order).  Asynchronous on `stream`. */
+int rlgpu_box_box_queries(int32_t n, const float* d_rot_a, const float* d_centre_a, const float* d_rot_b,
+                          const float* d_centre_b, float* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -271,3 +271,19 @@ def gjk_counts():
     f.argtypes = [ctypes.c_void_p]
     f(_p(c))
     return c
+
+
+def box_box(rot_a, centre_a, rot_b, centre_b):
+    """oracle_box_box (boxbox_ref.hpp, btBoxBoxDetector / dBoxBox2): n car-vs-car hitbox queries ->
+    [n, 29] float32 = count, then up to 4 x (normal on B xyz, point xyz, depth)."""
+    rot_a = np.ascontiguousarray(rot_a, np.float32).reshape(-1, 9)
+    n = len(rot_a)
+    rot_b = np.ascontiguousarray(rot_b, np.float32).reshape(n, 9)
+    centre_a = np.ascontiguousarray(centre_a, np.float32).reshape(n, 3)
+    centre_b = np.ascontiguousarray(centre_b, np.float32).reshape(n, 3)
+    out = np.zeros((n, 29), np.float32)
+    f = lib().oracle_box_box
+    f.restype = None
+    f.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 5
+    f(n, _p(rot_a), _p(centre_a), _p(rot_b), _p(centre_b), _p(out))
+    return out

@@ -1,0 +1,405 @@
+// boxbox_ref.hpp -- ORACLE (test infrastructure only; never linked into the product).
+//
+// Car hitbox vs car hitbox as Bullet 3.24 runs it for RocketSim: btCompoundCompoundCollisionAlgorithm's
+// one child pair -> btBoxBoxCollisionAlgorithm (BulletCollision/CollisionDispatch/
+// btBoxBoxCollisionAlgorithm.cpp:44-71, persistent contacts, the shared manifold) -> btBoxBoxDetector::
+// getClosestPoints (btBoxBoxDetector.cpp:730-767) -> ODE's dBoxBox2 (:267-728): the 15-axis separating-
+// axis test with its fudge factors, then either one edge-edge point (dLineClosestApproach, :84-108) or the
+// incident face clipped against the reference face (intersectRectQuad2, :116-175), the penetrating
+// points kept, culled to 4 by angle about the centroid (cullPoints2, :187-265).  Sides are 2 x the half
+// extents with margin; every point goes to btManifoldResult::addContactPoint(-normal, point, -depth).
+// btAtan2 is the deterministic rs_atan2f (include/rlgpu_detmath.h), as for every transcendental here.
+// Scalar order is ODE's (dDOTpq and friends, restated below); the product's independent restatement is
+// reinforcement-learning_amd/csrc/boxbox.hpp.
+#pragma once
+#include <cstring>
+
+#include "rsim_math.hpp"
+
+namespace orc {
+namespace boxbox {
+
+// ODE dMatrix3 view of a btMatrix3x3 (R[4 i + j] = row i, column j)
+struct OM {
+    float m[12];
+    explicit OM(const M& b) {
+        std::memset(m, 0, sizeof m);
+        for (int j = 0; j < 3; j++) {
+            m[0 + 4 * j] = b.r[j].x;
+            m[1 + 4 * j] = b.r[j].y;
+            m[2 + 4 * j] = b.r[j].z;
+        }
+    }
+};
+inline float dDOTpq(const float* a, const float* b, int p, int q) { return a[0] * b[0] + a[p] * b[q] + a[2 * p] * b[2 * q]; }
+inline float dDOT(const float* a, const float* b) { return dDOTpq(a, b, 1, 1); }
+inline float dDOT44(const float* a, const float* b) { return dDOTpq(a, b, 4, 4); }
+inline float dDOT41(const float* a, const float* b) { return dDOTpq(a, b, 4, 1); }
+inline float dDOT14(const float* a, const float* b) { return dDOTpq(a, b, 1, 4); }
+
+inline void line_closest_approach(const float* pa, const float* ua, const float* pb, const float* ub, float* alpha,
+                                  float* beta) {
+    float p[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    float uaub = dDOT(ua, ub);
+    float q1 = dDOT(ua, p);
+    float q2 = -dDOT(ub, p);
+    float d = 1 - uaub * uaub;
+    if (d <= 0.0001f) {
+        *alpha = 0;
+        *beta = 0;
+    } else {
+        d = 1.f / d;
+        *alpha = (q1 + uaub * q2) * d;
+        *beta = (uaub * q1 + q2) * d;
+    }
+}
+
+inline int intersect_rect_quad2(const float h[2], float p[8], float ret[16]) {
+    int nq = 4, nr = 0;
+    float buffer[16];
+    float* q = p;
+    float* r = ret;
+    for (int dir = 0; dir <= 1; dir++) {
+        for (int sign = -1; sign <= 1; sign += 2) {
+            float* pq = q;
+            float* pr = r;
+            nr = 0;
+            for (int i = nq; i > 0; i--) {
+                if (sign * pq[dir] < h[dir]) {
+                    pr[0] = pq[0];
+                    pr[1] = pq[1];
+                    pr += 2;
+                    nr++;
+                    if (nr & 8) {
+                        q = r;
+                        goto done;
+                    }
+                }
+                float* nextq = (i > 1) ? pq + 2 : q;
+                if ((sign * pq[dir] < h[dir]) ^ (sign * nextq[dir] < h[dir])) {
+                    pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * h[dir] - pq[dir]);
+                    pr[dir] = sign * h[dir];
+                    pr += 2;
+                    nr++;
+                    if (nr & 8) {
+                        q = r;
+                        goto done;
+                    }
+                }
+                pq += 2;
+            }
+            q = r;
+            r = (q == ret) ? buffer : ret;
+            nq = nr;
+        }
+    }
+done:
+    if (q != ret) std::memcpy(ret, q, nr * 2 * sizeof(float));
+    return nr;
+}
+
+constexpr float kPi = 3.14159265f;  // M__PI
+
+inline void cull_points2(int n, const float p[], int m, int i0, int iret[]) {
+    int i, j;
+    float a, cx, cy, q;
+    if (n == 1) {
+        cx = p[0];
+        cy = p[1];
+    } else if (n == 2) {
+        cx = 0.5f * (p[0] + p[2]);
+        cy = 0.5f * (p[1] + p[3]);
+    } else {
+        a = 0;
+        cx = 0;
+        cy = 0;
+        for (i = 0; i < (n - 1); i++) {
+            q = p[i * 2] * p[i * 2 + 3] - p[i * 2 + 2] * p[i * 2 + 1];
+            a += q;
+            cx += q * (p[i * 2] + p[i * 2 + 2]);
+            cy += q * (p[i * 2 + 1] + p[i * 2 + 3]);
+        }
+        q = p[n * 2 - 2] * p[1] - p[0] * p[n * 2 - 1];
+        if (std::fabs(a + q) > SIMD_EPSILON)
+            a = 1.f / (3.0f * (a + q));
+        else
+            a = 1e18f;  // BT_LARGE_FLOAT
+        cx = a * (cx + q * (p[n * 2 - 2] + p[0]));
+        cy = a * (cy + q * (p[n * 2 - 1] + p[1]));
+    }
+    float A[8];
+    for (i = 0; i < n; i++) A[i] = rs_atan2f(p[i * 2 + 1] - cy, p[i * 2] - cx);
+    int avail[8];
+    for (i = 0; i < n; i++) avail[i] = 1;
+    avail[i0] = 0;
+    iret[0] = i0;
+    iret++;
+    for (j = 1; j < m; j++) {
+        a = float(j) * (2 * kPi / m) + A[i0];
+        if (a > kPi) a -= 2 * kPi;
+        float maxdiff = 1e9f, diff;
+        *iret = i0;
+        for (i = 0; i < n; i++) {
+            if (avail[i]) {
+                diff = std::fabs(A[i] - a);
+                if (diff > kPi) diff = 2 * kPi - diff;
+                if (diff < maxdiff) {
+                    maxdiff = diff;
+                    *iret = i;
+                }
+            }
+        }
+        avail[*iret] = 0;
+        iret++;
+    }
+}
+
+// dBoxBox2 with maxc = 4.  emit(normal_on_b, point, depth) per contact; returns the contact count.
+template <typename Emit>
+int box_box(V p1v, const M& B1, V side1, V p2v, const M& B2, V side2, Emit&& emit) {
+    const OM o1(B1), o2(B2);
+    const float* R1 = o1.m;
+    const float* R2 = o2.m;
+    const float p1[3] = {p1v.x, p1v.y, p1v.z}, p2[3] = {p2v.x, p2v.y, p2v.z};
+    const float fudge_factor = 1.05f;
+    float p[3], pp[3], normalC[3] = {0.f, 0.f, 0.f};
+    const float* normalR = nullptr;
+    float A[3], B[3], R11, R12, R13, R21, R22, R23, R31, R32, R33, Q11, Q12, Q13, Q21, Q22, Q23, Q31, Q32, Q33, s, s2, l;
+    int i, j, invert_normal, code;
+    for (i = 0; i < 3; i++) p[i] = p2[i] - p1[i];
+    pp[0] = dDOT41(R1 + 0, p);
+    pp[1] = dDOT41(R1 + 1, p);
+    pp[2] = dDOT41(R1 + 2, p);
+    A[0] = side1[0] * 0.5f;
+    A[1] = side1[1] * 0.5f;
+    A[2] = side1[2] * 0.5f;
+    B[0] = side2[0] * 0.5f;
+    B[1] = side2[1] * 0.5f;
+    B[2] = side2[2] * 0.5f;
+    R11 = dDOT44(R1 + 0, R2 + 0);
+    R12 = dDOT44(R1 + 0, R2 + 1);
+    R13 = dDOT44(R1 + 0, R2 + 2);
+    R21 = dDOT44(R1 + 1, R2 + 0);
+    R22 = dDOT44(R1 + 1, R2 + 1);
+    R23 = dDOT44(R1 + 1, R2 + 2);
+    R31 = dDOT44(R1 + 2, R2 + 0);
+    R32 = dDOT44(R1 + 2, R2 + 1);
+    R33 = dDOT44(R1 + 2, R2 + 2);
+    Q11 = std::fabs(R11);
+    Q12 = std::fabs(R12);
+    Q13 = std::fabs(R13);
+    Q21 = std::fabs(R21);
+    Q22 = std::fabs(R22);
+    Q23 = std::fabs(R23);
+    Q31 = std::fabs(R31);
+    Q32 = std::fabs(R32);
+    Q33 = std::fabs(R33);
+    s = -FLT_MAX;
+    invert_normal = 0;
+    code = 0;
+    auto face = [&](float e1, float e2, const float* norm, int cc) {
+        s2 = std::fabs(e1) - e2;
+        if (s2 > 0) return false;
+        if (s2 > s) {
+            s = s2;
+            normalR = norm;
+            invert_normal = e1 < 0;
+            code = cc;
+        }
+        return true;
+    };
+    if (!face(pp[0], (A[0] + B[0] * Q11 + B[1] * Q12 + B[2] * Q13), R1 + 0, 1)) return 0;
+    if (!face(pp[1], (A[1] + B[0] * Q21 + B[1] * Q22 + B[2] * Q23), R1 + 1, 2)) return 0;
+    if (!face(pp[2], (A[2] + B[0] * Q31 + B[1] * Q32 + B[2] * Q33), R1 + 2, 3)) return 0;
+    if (!face(dDOT41(R2 + 0, p), (A[0] * Q11 + A[1] * Q21 + A[2] * Q31 + B[0]), R2 + 0, 4)) return 0;
+    if (!face(dDOT41(R2 + 1, p), (A[0] * Q12 + A[1] * Q22 + A[2] * Q32 + B[1]), R2 + 1, 5)) return 0;
+    if (!face(dDOT41(R2 + 2, p), (A[0] * Q13 + A[1] * Q23 + A[2] * Q33 + B[2]), R2 + 2, 6)) return 0;
+    auto edge = [&](float e1, float e2, float n1, float n2, float n3, int cc) {
+        s2 = std::fabs(e1) - e2;
+        if (s2 > SIMD_EPSILON) return false;
+        l = std::sqrt(n1 * n1 + n2 * n2 + n3 * n3);
+        if (l > SIMD_EPSILON) {
+            s2 /= l;
+            if (s2 * fudge_factor > s) {
+                s = s2;
+                normalR = nullptr;
+                normalC[0] = n1 / l;
+                normalC[1] = n2 / l;
+                normalC[2] = n3 / l;
+                invert_normal = e1 < 0;
+                code = cc;
+            }
+        }
+        return true;
+    };
+    const float fudge2 = 1.0e-5f;
+    Q11 += fudge2;
+    Q12 += fudge2;
+    Q13 += fudge2;
+    Q21 += fudge2;
+    Q22 += fudge2;
+    Q23 += fudge2;
+    Q31 += fudge2;
+    Q32 += fudge2;
+    Q33 += fudge2;
+    if (!edge(pp[2] * R21 - pp[1] * R31, (A[1] * Q31 + A[2] * Q21 + B[1] * Q13 + B[2] * Q12), 0, -R31, R21, 7)) return 0;
+    if (!edge(pp[2] * R22 - pp[1] * R32, (A[1] * Q32 + A[2] * Q22 + B[0] * Q13 + B[2] * Q11), 0, -R32, R22, 8)) return 0;
+    if (!edge(pp[2] * R23 - pp[1] * R33, (A[1] * Q33 + A[2] * Q23 + B[0] * Q12 + B[1] * Q11), 0, -R33, R23, 9)) return 0;
+    if (!edge(pp[0] * R31 - pp[2] * R11, (A[0] * Q31 + A[2] * Q11 + B[1] * Q23 + B[2] * Q22), R31, 0, -R11, 10)) return 0;
+    if (!edge(pp[0] * R32 - pp[2] * R12, (A[0] * Q32 + A[2] * Q12 + B[0] * Q23 + B[2] * Q21), R32, 0, -R12, 11)) return 0;
+    if (!edge(pp[0] * R33 - pp[2] * R13, (A[0] * Q33 + A[2] * Q13 + B[0] * Q22 + B[1] * Q21), R33, 0, -R13, 12)) return 0;
+    if (!edge(pp[1] * R11 - pp[0] * R21, (A[0] * Q21 + A[1] * Q11 + B[1] * Q33 + B[2] * Q32), -R21, R11, 0, 13)) return 0;
+    if (!edge(pp[1] * R12 - pp[0] * R22, (A[0] * Q22 + A[1] * Q12 + B[0] * Q33 + B[2] * Q31), -R22, R12, 0, 14)) return 0;
+    if (!edge(pp[1] * R13 - pp[0] * R23, (A[0] * Q23 + A[1] * Q13 + B[0] * Q32 + B[1] * Q31), -R23, R13, 0, 15)) return 0;
+    if (!code) return 0;
+    float normal[3];
+    if (normalR) {
+        normal[0] = normalR[0];
+        normal[1] = normalR[4];
+        normal[2] = normalR[8];
+    } else {
+        normal[0] = dDOT(R1 + 0, normalC);
+        normal[1] = dDOT(R1 + 4, normalC);
+        normal[2] = dDOT(R1 + 8, normalC);
+    }
+    if (invert_normal) {
+        normal[0] = -normal[0];
+        normal[1] = -normal[1];
+        normal[2] = -normal[2];
+    }
+    const float depth = -s;
+    const V nOut(-normal[0], -normal[1], -normal[2]);
+    if (code > 6) {
+        float pa[3], pb[3], sign;
+        for (i = 0; i < 3; i++) pa[i] = p1[i];
+        for (j = 0; j < 3; j++) {
+            sign = (dDOT14(normal, R1 + j) > 0) ? 1.0f : -1.0f;
+            for (i = 0; i < 3; i++) pa[i] += sign * A[j] * R1[i * 4 + j];
+        }
+        for (i = 0; i < 3; i++) pb[i] = p2[i];
+        for (j = 0; j < 3; j++) {
+            sign = (dDOT14(normal, R2 + j) > 0) ? -1.0f : 1.0f;
+            for (i = 0; i < 3; i++) pb[i] += sign * B[j] * R2[i * 4 + j];
+        }
+        float alpha, beta, ua[3], ub[3];
+        for (i = 0; i < 3; i++) ua[i] = R1[((code)-7) / 3 + i * 4];
+        for (i = 0; i < 3; i++) ub[i] = R2[((code)-7) % 3 + i * 4];
+        line_closest_approach(pa, ua, pb, ub, &alpha, &beta);
+        for (i = 0; i < 3; i++) pa[i] += ua[i] * alpha;
+        for (i = 0; i < 3; i++) pb[i] += ub[i] * beta;
+        emit(nOut, V(pb[0], pb[1], pb[2]), -depth);
+        return 1;
+    }
+    const float *Ra, *Rb, *pa, *pb, *Sa, *Sb;
+    if (code <= 3) {
+        Ra = R1; Rb = R2; pa = p1; pb = p2; Sa = A; Sb = B;
+    } else {
+        Ra = R2; Rb = R1; pa = p2; pb = p1; Sa = B; Sb = A;
+    }
+    float normal2[3], nr[3], anr[3];
+    if (code <= 3) {
+        normal2[0] = normal[0]; normal2[1] = normal[1]; normal2[2] = normal[2];
+    } else {
+        normal2[0] = -normal[0]; normal2[1] = -normal[1]; normal2[2] = -normal[2];
+    }
+    nr[0] = dDOT41(Rb + 0, normal2);
+    nr[1] = dDOT41(Rb + 1, normal2);
+    nr[2] = dDOT41(Rb + 2, normal2);
+    anr[0] = std::fabs(nr[0]);
+    anr[1] = std::fabs(nr[1]);
+    anr[2] = std::fabs(nr[2]);
+    int lanr, a1, a2;
+    if (anr[1] > anr[0]) {
+        if (anr[1] > anr[2]) { a1 = 0; lanr = 1; a2 = 2; }
+        else { a1 = 0; a2 = 1; lanr = 2; }
+    } else {
+        if (anr[0] > anr[2]) { lanr = 0; a1 = 1; a2 = 2; }
+        else { a1 = 0; a2 = 1; lanr = 2; }
+    }
+    float center[3];
+    if (nr[lanr] < 0) {
+        for (i = 0; i < 3; i++) center[i] = pb[i] - pa[i] + Sb[lanr] * Rb[i * 4 + lanr];
+    } else {
+        for (i = 0; i < 3; i++) center[i] = pb[i] - pa[i] - Sb[lanr] * Rb[i * 4 + lanr];
+    }
+    int codeN, code1, code2;
+    codeN = code <= 3 ? code - 1 : code - 4;
+    if (codeN == 0) { code1 = 1; code2 = 2; }
+    else if (codeN == 1) { code1 = 0; code2 = 2; }
+    else { code1 = 0; code2 = 1; }
+    float quad[8], c1, c2, m11, m12, m21, m22;
+    c1 = dDOT14(center, Ra + code1);
+    c2 = dDOT14(center, Ra + code2);
+    m11 = dDOT44(Ra + code1, Rb + a1);
+    m12 = dDOT44(Ra + code1, Rb + a2);
+    m21 = dDOT44(Ra + code2, Rb + a1);
+    m22 = dDOT44(Ra + code2, Rb + a2);
+    {
+        float k1 = m11 * Sb[a1], k2 = m21 * Sb[a1], k3 = m12 * Sb[a2], k4 = m22 * Sb[a2];
+        quad[0] = c1 - k1 - k3;
+        quad[1] = c2 - k2 - k4;
+        quad[2] = c1 - k1 + k3;
+        quad[3] = c2 - k2 + k4;
+        quad[4] = c1 + k1 + k3;
+        quad[5] = c2 + k2 + k4;
+        quad[6] = c1 + k1 - k3;
+        quad[7] = c2 + k2 - k4;
+    }
+    const float rect[2] = {Sa[code1], Sa[code2]};
+    float ret[16];
+    int n = intersect_rect_quad2(rect, quad, ret);
+    if (n < 1) return 0;
+    float point[3 * 8], dep[8];
+    float det1 = 1.f / (m11 * m22 - m12 * m21);
+    m11 *= det1;
+    m12 *= det1;
+    m21 *= det1;
+    m22 *= det1;
+    int cnum = 0;
+    for (j = 0; j < n; j++) {
+        float k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
+        float k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
+        for (i = 0; i < 3; i++) point[cnum * 3 + i] = center[i] + k1 * Rb[i * 4 + a1] + k2 * Rb[i * 4 + a2];
+        dep[cnum] = Sa[codeN] - dDOT(normal2, point + cnum * 3);
+        if (dep[cnum] >= 0) {
+            ret[cnum * 2] = ret[j * 2];
+            ret[cnum * 2 + 1] = ret[j * 2 + 1];
+            cnum++;
+        }
+    }
+    if (cnum < 1) return 0;
+    int maxc = 4;
+    if (maxc > cnum) maxc = cnum;
+    if (cnum <= maxc) {
+        for (j = 0; j < cnum; j++) {
+            float w[3];
+            if (code < 4)
+                for (i = 0; i < 3; i++) w[i] = point[j * 3 + i] + pa[i];
+            else
+                for (i = 0; i < 3; i++) w[i] = point[j * 3 + i] + pa[i] - normal[i] * dep[j];
+            emit(nOut, V(w[0], w[1], w[2]), -dep[j]);
+        }
+    } else {
+        int i1 = 0;
+        float maxdepth = dep[0];
+        for (i = 1; i < cnum; i++)
+            if (dep[i] > maxdepth) {
+                maxdepth = dep[i];
+                i1 = i;
+            }
+        int iret[8];
+        cull_points2(cnum, ret, maxc, i1, iret);
+        for (j = 0; j < maxc; j++) {
+            V w(point[iret[j] * 3] + pa[0], point[iret[j] * 3 + 1] + pa[1], point[iret[j] * 3 + 2] + pa[2]);
+            if (code < 4)
+                emit(nOut, w, -dep[iret[j]]);
+            else
+                emit(nOut, w - V(normal[0], normal[1], normal[2]) * dep[iret[j]], -dep[iret[j]]);
+        }
+        cnum = maxc;
+    }
+    return cnum;
+}
+
+}  // namespace boxbox
+}  // namespace orc

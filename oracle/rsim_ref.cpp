@@ -20,8 +20,7 @@
 // Documented deviations from the reference (also in DESIGN.md):
 //   * synthetic arena mesh (include/rlgpu_arena_mesh.h) by default; real .cmf meshes can be
 //     loaded (World::set_mesh), one collision object per file;
-//   * box-box (car-car) contacts use SAT (1 point) instead of btBoxBoxDetector (box-triangle runs
-//     Bullet's GJK / EPA, gjk_ref.hpp);
+//   * (box-triangle runs Bullet's GJK / EPA, gjk_ref.hpp; box-box btBoxBoxDetector, boxbox_ref.hpp)
 //   * time-based deactivation (btRigidBody.h:531-545) is not modelled -- only the zero-velocity
 //     ball sleep of Arena.cpp:722-727;
 //   * pairs are processed in a canonical order (per body: mesh objects, planes; then the dynamic
@@ -35,6 +34,7 @@
 
 #include "../include/rlgpu_arena_mesh.h"
 #include "../include/rlgpu_detmath.h"
+#include "boxbox_ref.hpp"
 #include "gjk_ref.hpp"
 
 namespace orc {
@@ -1558,54 +1558,12 @@ struct Sim {
         // (btSphereBoxCollisionAlgorithm.cpp:30-37,66-75, btManifoldResult.cpp:118-135)
         add_contact(key, nw, point_on_box, pen);
     }
-    // OBB vs OBB SAT (1 point), A = car a, B = car b
+    // car hitbox vs car hitbox: btBoxBoxDetector / dBoxBox2 (boxbox_ref.hpp), A = car a, B = car b; sides
+    // 2 x the half extents with margin (btBoxBoxDetector.cpp:758-766); up to 4 points
     void collide_car_car(int key, int ba, int bb) {
-        const M& Ra = b[ba].rot;
-        const M& Rb = b[bb].rot;
-        V ca = car_box_center(ba), cb = car_box_center(bb);
-        V A[3] = {Ra.col(0), Ra.col(1), Ra.col(2)}, B[3] = {Rb.col(0), Rb.col(1), Rb.col(2)};
-        V h = w.car_half;
-        float cbt = pair_cbt(ba, bb);
-        V axes[15];
-        int na = 0;
-        for (int i = 0; i < 3; i++) axes[na++] = A[i];
-        for (int i = 0; i < 3; i++) axes[na++] = B[i];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) axes[na++] = cross(A[i], B[j]);
-        float best = 1e30f;
-        V best_n;
-        int best_k = -1;
-        for (int k = 0; k < na; k++) {
-            float l2 = len2(axes[k]);
-            if (l2 < 1e-10f) continue;
-            V L = axes[k] / std::sqrt(l2);
-            float ra = h.x * std::fabs(dot(A[0], L)) + h.y * std::fabs(dot(A[1], L)) + h.z * std::fabs(dot(A[2], L));
-            float rb = h.x * std::fabs(dot(B[0], L)) + h.y * std::fabs(dot(B[1], L)) + h.z * std::fabs(dot(B[2], L));
-            float d = dot(ca - cb, L);
-            float pen = ra + rb - std::fabs(d);
-            if (-pen > cbt) return;
-            if (pen < best) {
-                best = pen;
-                best_n = d >= 0 ? L : -L;  // from B towards A
-                best_k = k;
-            }
-        }
-        float depth = -best;
-        V n = best_n;
-        V point_b;
-        if (best_k >= 3 && best_k < 6) {
-            // face of B: deepest vertex of A along -n
-            V dl = vmul(-n, Ra);
-            V lv(dl.x >= 0 ? h.x : -h.x, dl.y >= 0 ? h.y : -h.y, dl.z >= 0 ? h.z : -h.z);
-            V pa = Ra * lv + ca;
-            point_b = pa - n * depth;
-        } else {
-            // face of A or edge-edge: deepest vertex of B along +n
-            V dl = vmul(n, Rb);
-            V lv(dl.x >= 0 ? h.x : -h.x, dl.y >= 0 ? h.y : -h.y, dl.z >= 0 ? h.z : -h.z);
-            point_b = Rb * lv + cb;
-        }
-        add_contact(key, n, point_b, depth);
+        const V side = w.car_half * 2.f;
+        boxbox::box_box(car_box_center(ba), b[ba].rot, side, car_box_center(bb), b[bb].rot, side,
+                        [&](V n, V p, float d) { add_contact(key, n, p, d); });
     }
 
     void collision_detection(bool ball_awake) {
@@ -2263,6 +2221,33 @@ void oracle_gjk_counts(uint64_t* out6) {
     for (int i = 0; i < 4; i++) {
         out6[2 + i] = orc::gjk::epa_stats[i];
         orc::gjk::epa_stats[i] = 0;
+    }
+}
+}  // extern "C"
+
+extern "C" {
+// n car-vs-car hitbox queries (boxbox_ref.hpp): per query rot_a[9], centre_a[3], rot_b[9], centre_b[3];
+// the Octane box for both.  out[n][1 + 4 * 7] = {count, then per point: normal xyz, point xyz, depth}.
+void oracle_box_box(int n, const float* rot_a, const float* centre_a, const float* rot_b, const float* centre_b,
+                    float* out) {
+    const orc::World& w = orc::world();
+    const orc::V side = w.car_half * 2.f;
+    for (int i = 0; i < n; i++) {
+        orc::M Ra, Rb;
+        for (int r = 0; r < 3; r++) {
+            Ra.r[r] = orc::V(rot_a[9 * i + 3 * r], rot_a[9 * i + 3 * r + 1], rot_a[9 * i + 3 * r + 2]);
+            Rb.r[r] = orc::V(rot_b[9 * i + 3 * r], rot_b[9 * i + 3 * r + 1], rot_b[9 * i + 3 * r + 2]);
+        }
+        orc::V ca(centre_a[3 * i], centre_a[3 * i + 1], centre_a[3 * i + 2]);
+        orc::V cb(centre_b[3 * i], centre_b[3 * i + 1], centre_b[3 * i + 2]);
+        float* o = out + (size_t)i * 29;
+        for (int k = 0; k < 29; k++) o[k] = 0.f;
+        int cnt = 0;
+        orc::boxbox::box_box(ca, Ra, side, cb, Rb, side, [&](orc::V nn, orc::V p, float d) {
+            float* q = o + 1 + 7 * cnt++;
+            q[0] = nn.x; q[1] = nn.y; q[2] = nn.z; q[3] = p.x; q[4] = p.y; q[5] = p.z; q[6] = d;
+        });
+        o[0] = (float)cnt;
     }
 }
 }  // extern "C"

@@ -1262,3 +1262,39 @@ extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const f
         RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
     });
 }
+
+// ------------------------------------------------------------------ box-box queries (tests)
+namespace rl {
+__global__ void __launch_bounds__(64) box_box_kernel(int n, const float* ra, const float* ca, const float* rb,
+                                                     const float* cb, float* out) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const float* a = ra + 9 * (size_t)i;
+    const float* b = rb + 9 * (size_t)i;
+    const m3 Ra = m3{v3{a[0], a[1], a[2]}, v3{a[3], a[4], a[5]}, v3{a[6], a[7], a[8]}};
+    const m3 Rb = m3{v3{b[0], b[1], b[2]}, v3{b[3], b[4], b[5]}, v3{b[6], b[7], b[8]}};
+    const v3 pa = v3{ca[3 * (size_t)i], ca[3 * (size_t)i + 1], ca[3 * (size_t)i + 2]};
+    const v3 pb = v3{cb[3 * (size_t)i], cb[3 * (size_t)i + 1], cb[3 * (size_t)i + 2]};
+    float* o = out + 29 * (size_t)i;
+    for (int k = 0; k < 29; k++) o[k] = 0.f;
+    int cnt = 0;
+    boxbox::box_box(pa, Ra, C.car_half, pb, Rb, C.car_half, [&](v3 nn, v3 p, float d) {
+        float* q = o + 1 + 7 * cnt++;
+        q[0] = nn.x; q[1] = nn.y; q[2] = nn.z; q[3] = p.x; q[4] = p.y; q[5] = p.z; q[6] = d;
+    });
+    o[0] = (float)cnt;
+}
+}  // namespace rl
+
+extern "C" int rlgpu_box_box_queries(int32_t n, const float* d_rot_a, const float* d_centre_a, const float* d_rot_b,
+                                     const float* d_centre_b, float* d_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(n >= 0, "rlgpu_box_box_queries: n must be >= 0");
+        if (n == 0) return;
+        RLGPU_REQUIRE(d_rot_a && d_centre_a && d_rot_b && d_centre_b && d_out, "rlgpu_box_box_queries: null argument");
+        ensure_const();
+        hipLaunchKernelGGL(rl::box_box_kernel, dim3(rlgpu::ceil_div(n, 64)), dim3(64), 0, (hipStream_t)stream, n, d_rot_a,
+                           d_centre_a, d_rot_b, d_centre_b, d_out);
+        RLGPU_CHECK_HIP(hipGetLastError());
+    });
+}

@@ -2,6 +2,7 @@
 // sequential-impulse solver of the env kernel.  Reference map in env_kernel.hpp; each
 // function cites the Bullet / RocketSim code it restates.
 #pragma once
+#include "boxbox.hpp"
 #include "edge_info.hpp"
 #include "env_device.hpp"
 
@@ -536,45 +537,12 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
         emit(A, rank, 0, key, nw, point_on_box, pen);
         return 1;
     }
-    // OBB vs OBB SAT (stand-in for btBoxBoxDetector), A = car ka, B = car kb
+    // car vs car: btBoxBoxDetector / dBoxBox2 (boxbox.hpp), A = car ka, B = car kb, up to 4 points in
+    // emission order (the point index orders them at the commit)
     {
-        m3 Ra = brot(A, A_), Rb = brot(A, B_);
-        v3 ca = car_box_center(A, A_), cb = car_box_center(A, B_);
-        const v3 A0 = col(Ra, 0), A1 = col(Ra, 1), A2 = col(Ra, 2), B0 = col(Rb, 0), B1 = col(Rb, 1), B2 = col(Rb, 2);
-        v3 h = C.car_half;
-        float cbt = pair_cbt(A_, B_);
-        float best = 1e30f;
-        v3 best_n = zero3();
-        int best_k = -1;
-        for (int k = 0; k < 15; k++) {
-            v3 axis;
-            if (k < 3) axis = sel3(A0, A1, A2, k);
-            else if (k < 6) axis = sel3(B0, B1, B2, k - 3);
-            else axis = cross(sel3(A0, A1, A2, (k - 6) / 3), sel3(B0, B1, B2, (k - 6) % 3));
-            float l2 = len2(axis);
-            if (l2 < 1e-10f) continue;
-            v3 L = axis / sqrtf(l2);
-            float ra = h.x * fabsf(dot(A0, L)) + h.y * fabsf(dot(A1, L)) + h.z * fabsf(dot(A2, L));
-            float rb = h.x * fabsf(dot(B0, L)) + h.y * fabsf(dot(B1, L)) + h.z * fabsf(dot(B2, L));
-            float d = dot(ca - cb, L);
-            float pen = ra + rb - fabsf(d);
-            if (-pen > cbt) return 1;
-            if (pen < best) {
-                best = pen;
-                best_n = d >= 0 ? L : -L;
-                best_k = k;
-            }
-        }
-        float depth = -best;
-        v3 n = best_n;
-        v3 point_b;
-        if (best_k >= 3 && best_k < 6) {
-            v3 pa = box_support(Ra, ca, -n);
-            point_b = pa - n * depth;
-        } else {
-            point_b = box_support(Rb, cb, n);
-        }
-        emit(A, rank, 0, key, n, point_b, depth);
+        int j = 0;
+        boxbox::box_box(car_box_center(A, A_), brot(A, A_), C.car_half, car_box_center(A, B_), brot(A, B_), C.car_half,
+                        [&](v3 n, v3 p, float d) { emit(A, rank, j++, key, n, p, d); });
     }
     return 1;
 }

@@ -212,3 +212,20 @@ def box_triangle_queries(rot, centre, tri, cbt, lds_first=True):
                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
                "rlgpu_box_triangle_queries")
     return out
+
+
+def box_box_queries(rot_a, centre_a, rot_b, centre_b):
+    """The env kernel's car-vs-car hitbox narrowphase (btBoxBoxDetector / dBoxBox2, include/rlgpu_mesh.h
+    rlgpu_box_box_queries) on the device.  CUDA tensors rot_* [n,3,3], centre_* [n,3] -> [n,29] float32
+    (count, then up to 4 x normal on B, point, depth)."""
+    import torch
+    rot_a = rot_a.reshape(-1, 9).contiguous().float()
+    n = rot_a.shape[0]
+    args = [rot_a, centre_a.reshape(n, 3).contiguous().float(), rot_b.reshape(n, 9).contiguous().float(),
+            centre_b.reshape(n, 3).contiguous().float()]
+    out = torch.zeros((n, 29), dtype=torch.float32, device=rot_a.device)
+    L = _bind()
+    L.rlgpu_box_box_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 6
+    _lib.check(L.rlgpu_box_box_queries(n, *[a.data_ptr() for a in args], out.data_ptr(),
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "rlgpu_box_box_queries")
+    return out
