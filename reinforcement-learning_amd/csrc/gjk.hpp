@@ -1084,6 +1084,9 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
         }
         v = nv;
         if (iter++ > 1000) break;
+#ifdef RLGPU_GJK_TRACE
+        RLGPU_GJK_TRACE(iter);
+#endif
         if (vs.n == 4) {
             degen = 13;
             break;

@@ -4,6 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
+__device__ long long g_trace[64];
+__device__ int g_ntrace;
+#define RLGPU_GJK_TRACE(it) { if (g_ntrace < 64) g_trace[g_ntrace++] = clock64(); }
+
 #include "../../reinforcement-learning_amd/csrc/gjk.hpp"
 
 using namespace rl;
@@ -26,11 +30,16 @@ __global__ void __launch_bounds__(64) k(int mode, float gap, unsigned long long*
     v3 n, p;
     float d = 0;
     int pen = 0;
+    g_ntrace = 0;
     long long t0 = clock64();
     bool hit = gjk::box_triangle(R, c, sh, 0.02f, mode ? &fast : nullptr, &lock, slow, n, p, d, &pen);
     long long t1 = clock64();
     out[0] = (unsigned long long)(t1 - t0);
     out[1] = (unsigned long long)pen;
+    out[2] = (unsigned long long)g_ntrace;
+    out[3] = g_ntrace ? (unsigned long long)(g_trace[0] - t0) : 0;
+    out[4] = g_ntrace > 1 ? (unsigned long long)((g_trace[g_ntrace - 1] - g_trace[0]) / (g_ntrace - 1)) : 0;
+    out[5] = g_ntrace ? (unsigned long long)(t1 - g_trace[g_ntrace - 1]) : 0;
     res[0] = hit;
     res[1] = d;
 }
@@ -39,21 +48,22 @@ int main() {
     unsigned long long* out;
     float* res;
     gjk::GjkScratch* hbm;
-    hipMalloc(&out, 16);
+    hipMalloc(&out, 64);
     hipMalloc(&res, 8);
     hipMalloc(&hbm, sizeof(gjk::GjkScratch));
     for (int mode = 0; mode < 2; mode++)
         for (float gap : {0.01f, -0.02f, -0.1f, -0.3f}) {
-            unsigned long long best = ~0ull, o[2];
+            unsigned long long best = ~0ull, o[8];
             float r[2];
             for (int rep = 0; rep < 5; rep++) {
                 hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, mode, gap, out, res, hbm);
-                hipMemcpy(o, out, 16, hipMemcpyDeviceToHost);
+                hipMemcpy(o, out, 64, hipMemcpyDeviceToHost);
                 hipMemcpy(r, res, 8, hipMemcpyDeviceToHost);
                 if (o[0] < best) best = o[0];
             }
-            printf("%s gap %+.2f: %8llu cycles (pen-solver calls %llu, hit %.0f depth %+.5f)\n", mode ? "LDS-first" : "HBM-only ",
-                   gap, best, o[1], r[0], r[1]);
+            printf("%s gap %+.2f: %8llu cycles (pen-solver calls %llu, hit %.0f depth %+.5f) GJK iterations %llu: first %llu, "
+                   "per iteration %llu, after the loop %llu\n", mode ? "LDS-first" : "HBM-only ", gap, best, o[1], r[0], r[1], o[2],
+                   o[3], o[4], o[5]);
         }
     return 0;
 }
