@@ -396,7 +396,7 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
 // One car hitbox vs mesh triangle: Bullet's GJK / EPA query (gjk.hpp) and its candidate.  Penetration-
 // solver work sets: the arena's small LDS set past the candidate list (free during the narrowphase), one
 // lane at a time, else this lane's HBM scratch.
-DEV void box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2) {
+__device__ __noinline__ void box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2) {
     const m3 R = brot(A, bi);
     const v3 c = car_box_center(A, bi);
     gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
