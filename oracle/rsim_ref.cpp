@@ -23,8 +23,9 @@
 //   * (box-triangle runs Bullet's GJK / EPA, gjk_ref.hpp; box-box btBoxBoxDetector, boxbox_ref.hpp)
 //   * time-based deactivation (btRigidBody.h:531-545) is not modelled -- only the zero-velocity
 //     ball sleep of Arena.cpp:722-727;
-//   * pairs are processed in a canonical order (per body: mesh objects, planes; then the dynamic
-//     pairs) instead of the broadphase cells' insertion order; wheels resting on another dynamic
+//   * pairs are processed in btRSBroadphase's order (per dynamic proxy: its statics, then its pairs with
+//     later bodies), except that a cell's dynamic list is taken in body order rather than its insertion
+//     history; wheels resting on another dynamic
 //     body read that body's tick-start velocity (the reference's order is unordered_set order);
 //   * transcendentals use include/rlgpu_detmath.h (shared with the kernels) instead of libm.
 #include "rsim_ref.hpp"
@@ -1568,33 +1569,34 @@ struct Sim {
 
     void collision_detection(bool ball_awake) {
         nmf = 0;  // last tick's pairs (and manifolds) were removed by the broadphase
-        // dynamic-static pairs: per body, the mesh objects then the 4 planes; skipped when the body
-        // is inactive (needsCollision(inactive, static) == false)
+        // the broadphase's pair order (btRSBroadphase.cpp:392-465): per dynamic proxy in creation order
+        // (ball, cars 1-4), its static pairs (mesh objects, then the 4 planes; skipped when the body is
+        // inactive, needsCollision(inactive, static) == false), then its dynamic pairs with the later
+        // bodies (the cell list's insertion history taken as body order) while the AABBs overlap
         for (int bi = 0; bi < 5; bi++) {
             bool active = bi == 0 ? ball_awake : b[bi].active;
-            if (!active) continue;
-            for (int o = 0, t0 = 0; o < w.nobj; o++) {
-                int t1 = t0;
-                while (t1 < w.ntris && w.tri_obj[t1] == o) t1++;
-                int key = bi * KSTAT + o;
-                if (bi == 0)
-                    collide_sphere_mesh(key, t0, t1);
-                else
-                    collide_box_mesh(key, bi, t0, t1);
-                refresh(key);
-                t0 = t1;
+            if (active) {
+                for (int o = 0, t0 = 0; o < w.nobj; o++) {
+                    int t1 = t0;
+                    while (t1 < w.ntris && w.tri_obj[t1] == o) t1++;
+                    int key = bi * KSTAT + o;
+                    if (bi == 0)
+                        collide_sphere_mesh(key, t0, t1);
+                    else
+                        collide_box_mesh(key, bi, t0, t1);
+                    refresh(key);
+                    t0 = t1;
+                }
+                for (int p = 0; p < 4; p++) {
+                    int key = bi * KSTAT + KOBJ + p;
+                    if (bi == 0)
+                        collide_sphere_plane(key, p);
+                    else
+                        collide_box_plane(key, bi, p);
+                    refresh(key);
+                }
             }
-            for (int p = 0; p < 4; p++) {
-                int key = bi * KSTAT + KOBJ + p;
-                if (bi == 0)
-                    collide_sphere_plane(key, p);
-                else
-                    collide_box_plane(key, bi, p);
-                refresh(key);
-            }
-        }
-        // dynamic-dynamic pairs: ball-car then car-car, only while broadphase AABBs overlap
-        for (int a = 0; a < 5; a++)
+            const int a = bi;
             for (int c2 = a + 1; c2 < 5; c2++) {
                 int ka = a == 0 ? c2 : a, kb = a == 0 ? 0 : c2;  // the car first for ball pairs
                 int key = KDYN + a * 8 + c2;
@@ -1612,6 +1614,7 @@ struct Sim {
                     collide_car_car(key, ka, kb);
                 refresh(key);
             }
+        }
     }
 
     // -------------------------------------------------------------------- solver

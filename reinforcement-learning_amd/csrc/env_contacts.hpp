@@ -291,6 +291,17 @@ DEV bool refresh(ArenaLDS* A, int key) {
 }
 
 // ------------------------------------------------------------------ narrowphase (candidates)
+// Commit (= manifold = solver) order of a work item: btRSBroadphase::calculateOverlappingPairs
+// (btRSBroadphase.cpp:392-465) walks the dynamic proxies in creation order (ball, then cars 1-4) and adds,
+// for each, its pairs with the cell's static proxies (meshes, then planes: creation order), then its
+// pairs with the cell's other dynamic proxies not paired yet; the pair cache dispatches in that order.
+// Within one proxy's dynamic pairs the cell list's order (insertion history) is taken as body order.
+DEV int commit_rank(int rank) {
+    if (rank < 25) return (rank / 5) * 9 + rank % 5;  // body * 9 + (0 mesh objects, 1-4 planes)
+    int a, b;
+    dyn_pair(rank, a, b);
+    return a * 9 + 5 + (b - a - 1);  // body a's pairs with the later bodies
+}
 DEV void emit(ArenaLDS* A, int rank, int tri, int key, v3 n, v3 p, float depth) {
     int slot = atomicAdd(&A->a.ncand, 1);
     if (slot >= kMaxCand) return;  // counted by the committing lane
@@ -298,7 +309,7 @@ DEV void emit(ArenaLDS* A, int rank, int tri, int key, v3 n, v3 p, float depth) 
     c.n[0] = n.x; c.n[1] = n.y; c.n[2] = n.z;
     c.p[0] = p.x; c.p[1] = p.y; c.p[2] = p.z;
     c.depth = depth;
-    c.order = (rank << 20) | tri;
+    c.order = (commit_rank(rank) << 20) | tri;
     c.key = key;
 }
 
@@ -547,7 +558,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
     return 1;
 }
 
-// single lane: commit this tick's candidates in canonical order -- per pair (key): add its points
+// single lane: commit this tick's candidates in the broadphase's pair order -- per pair (key): add its points
 // (contact callbacks fire here), then refresh its manifold, as Bullet's dispatch loop does
 // (btCollisionDispatcher::dispatchAllCollisionPairs, processCollision -> refreshContactPoints)
 DEV void commit_contacts(ArenaLDS* A, const MeshView& M, Prof* P = nullptr) {
