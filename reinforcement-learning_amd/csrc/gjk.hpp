@@ -25,6 +25,11 @@
 #ifndef DEV
 #define DEV __device__ __forceinline__
 #endif
+#ifdef RLGPU_GJK_TRACE
+#define GJK_MARK(k) RLGPU_GJK_TRACE(k)
+#else
+#define GJK_MARK(k)
+#endif
 // the penetration solver's big, rarely-run pieces are called, not inlined, and their loops are not
 // unrolled: one copy of each keeps the instruction footprint (and its cache misses) small
 #define GJK_CALLED DEV
@@ -63,13 +68,54 @@ struct GjkScratch {
 // LDS (the narrowphase-time free tail of ArenaLDS::u).  A small set that would need more support
 // vertices, live faces or expand() depth than it holds sets `overflow`; the query is then rerun on the
 // HBM set from the start (every run is deterministic, so the rerun gives Bullet's result).
-struct Scr {
+// AS: the address space the work set's pointers carry (1 global, 3 LDS), so that every access compiles
+// to global_* / ds_* instructions instead of flat ones (a flat access to LDS pays the vector-memory path)
+template <int AS>
+struct ScrT {
+    __attribute__((address_space(AS))) SSV* sv;
+    __attribute__((address_space(AS))) SFace* fc;
+    __attribute__((address_space(AS))) uint32_t* stack;
+    int max_sv, max_fc, max_stack;
+    int overflow;
+};
+struct Scr {  // the generic view handed around by the narrowphase
     SSV* sv;
     SFace* fc;
     uint32_t* stack;
     int max_sv, max_fc, max_stack;
     int overflow;
 };
+template <int AS>
+DEV ScrT<AS> in_space(const Scr& s) {
+    return ScrT<AS>{(__attribute__((address_space(AS))) SSV*)s.sv, (__attribute__((address_space(AS))) SFace*)s.fc,
+                    (__attribute__((address_space(AS))) uint32_t*)s.stack, s.max_sv, s.max_fc, s.max_stack, 0};
+}
+// v3 members of work-set records are read / written component-wise (an address-space-qualified v3
+// cannot bind the generic copy constructor / assignment)
+template <typename R>
+DEV v3 ldv(const R& r) {
+    return v3{r.x, r.y, r.z};
+}
+template <typename R>
+DEV void stv(R& r, v3 v) {
+    r.x = v.x;
+    r.y = v.y;
+    r.z = v.z;
+}
+template <typename F>
+DEV void copy_face(SFace& o, const F& f) {
+    o.n = ldv(f.n);
+    o.d = f.d;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        o.c[k] = f.c[k];
+        o.f[k] = f.f[k];
+        o.e[k] = f.e[k];
+    }
+    o.pass = f.pass;
+    o.l[0] = f.l[0];
+    o.l[1] = f.l[1];
+}
 DEV Scr hbm_view(GjkScratch* g) { return Scr{g->sv, g->fc, g->stack, kSV, kEpaMaxFaces, kEpaMaxFaces + 8, 0}; }
 // small set carved from `bytes` of LDS: 24 support vertices (20 EPA iterations), 28 live faces, depth 24
 constexpr int kSmallSV = 24, kSmallFaces = 28, kSmallStack = 24;
@@ -397,12 +443,14 @@ struct Gjk2 {
     v3 ray;
     int status;  // Valid 0, Inside 1, Failed 2
 };
-DEV void getsupport(Scr& S, const Mink& m, v3 d, int idx) {
+template <int AS>
+DEV void getsupport(ScrT<AS>& S, const Mink& m, v3 d, int idx) {
     const v3 dn = d / len(d);
-    S.sv[idx].d = dn;
-    S.sv[idx].w = support(m, dn);
+    stv(S.sv[idx].d, dn);
+    stv(S.sv[idx].w, support(m, dn));
 }
-DEV void g2_append(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 v) {
+template <int AS>
+DEV void g2_append(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 v) {
     put4(s.p, s.rank, 0.f);
     g.nfree--;
     const int idx = (int)((g.freev >> (8 * g.nfree)) & 255u);
@@ -512,9 +560,11 @@ DEV float project4(v3 a, v3 b, v3 c, v3 d, float* w, uint32_t& m) {
     }
     return -1;
 }
-DEV v3 svw(const Scr& S, int i) { return S.sv[i].w; }
+template <int AS>
+DEV v3 svw(const ScrT<AS>& S, int i) { return ldv(S.sv[i].w); }
 // GJK::Evaluate (cpp:201-337); on return g.cs is m_simplex
-GJK_CALLED int g2_evaluate(Scr& S, const Mink& m, Gjk2& g, v3 guess) {
+template <int AS>
+GJK_CALLED int g2_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, v3 guess) {
     unsigned iterations = 0;
     float sqdist = 0, alpha = 0;
     v3 lastw[4];
@@ -599,11 +649,13 @@ GJK_CALLED int g2_evaluate(Scr& S, const Mink& m, Gjk2& g, v3 guess) {
     return g.status;
 }
 // GJK::EncloseOrigin (cpp:338-402), its recursion unrolled by rank
-DEV bool enclose4(const Scr& S, const Simp& s) {
+template <int AS>
+DEV bool enclose4(const ScrT<AS>& S, const Simp& s) {
     const v3 w3 = svw(S, sc(s, 3));
     return fabsf(det3(svw(S, sc(s, 0)) - w3, svw(S, sc(s, 1)) - w3, svw(S, sc(s, 2)) - w3)) > 0;
 }
-GJK_CALLED bool enclose3(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
+template <int AS>
+GJK_CALLED bool enclose3(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s) {
     const v3 w0 = svw(S, sc(s, 0));
     const v3 n = cross(svw(S, sc(s, 1)) - w0, svw(S, sc(s, 2)) - w0);
     if (len2(n) > 0) {
@@ -616,7 +668,8 @@ GJK_CALLED bool enclose3(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
     }
     return false;
 }
-GJK_CALLED bool enclose2(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
+template <int AS>
+GJK_CALLED bool enclose2(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s) {
     const v3 d = svw(S, sc(s, 1)) - svw(S, sc(s, 0));
 #pragma unroll 1
     for (int i = 0; i < 3; ++i) {
@@ -634,7 +687,8 @@ GJK_CALLED bool enclose2(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
     }
     return false;
 }
-DEV bool enclose_origin(Scr& S, const Mink& m, Gjk2& g, Simp& s) {
+template <int AS>
+DEV bool enclose_origin(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s) {
     if (s.rank == 1) {
 #pragma unroll 1
         for (int i = 0; i < 3; ++i) {
@@ -664,27 +718,32 @@ struct Epa {
     int status;       // Valid 0 .. Failed 9 (EPA::eStatus order)
     int nextsv;
 };
-DEV void list_append(Scr& S, uint16_t& root, int face) {
-    SFace& f = S.fc[face];
+template <int AS>
+DEV void list_append(ScrT<AS>& S, uint16_t& root, int face) {
+    auto& f = S.fc[face];
     f.l[0] = kNone;
     f.l[1] = root;
     if (root != kNone) S.fc[root].l[0] = (uint16_t)face;
     root = (uint16_t)face;
 }
-DEV void list_remove(Scr& S, uint16_t& root, int face) {
-    SFace& f = S.fc[face];
+template <int AS>
+DEV void list_remove(ScrT<AS>& S, uint16_t& root, int face) {
+    auto& f = S.fc[face];
     if (f.l[1] != kNone) S.fc[f.l[1]].l[0] = f.l[0];
     if (f.l[0] != kNone) S.fc[f.l[0]].l[1] = f.l[1];
     if (face == root) root = f.l[1];
 }
-DEV void stock_push(Scr& S, Epa& E, int face) { list_append(S, E.stock, face); }
-DEV void bind(Scr& S, int fa, int ea, int fb, int eb) {
+template <int AS>
+DEV void stock_push(ScrT<AS>& S, Epa& E, int face) { list_append(S, E.stock, face); }
+template <int AS>
+DEV void bind(ScrT<AS>& S, int fa, int ea, int fb, int eb) {
     S.fc[fa].e[ea] = (uint8_t)eb;
     S.fc[fa].f[ea] = (uint8_t)fb;
     S.fc[fb].e[eb] = (uint8_t)ea;
     S.fc[fb].f[eb] = (uint8_t)fa;
 }
-DEV bool getedgedist(const Scr& S, v3 fn, int a, int b, float& dist) {
+template <int AS>
+DEV bool getedgedist(const ScrT<AS>& S, v3 fn, int a, int b, float& dist) {
     const v3 aw = svw(S, a), bw = svw(S, b);
     const v3 ba = bw - aw;
     const v3 n_ab = cross(ba, fn);
@@ -707,7 +766,8 @@ DEV bool getedgedist(const Scr& S, v3 fn, int a, int b, float& dist) {
     return false;
 }
 // EPA::newface; returns the face or -1
-DEV int newface(Scr& S, Epa& E, int a, int b, int c, bool forced) {
+template <int AS>
+DEV int newface(ScrT<AS>& S, Epa& E, int a, int b, int c, bool forced) {
     int face;
     if (E.stock != kNone) {
         face = E.stock;
@@ -723,7 +783,7 @@ DEV int newface(Scr& S, Epa& E, int a, int b, int c, bool forced) {
     }
     list_append(S, E.hull, face);
     E.hull_count++;
-    SFace& F = S.fc[face];
+    auto& F = S.fc[face];
     F.pass = 0;
     F.c[0] = (uint8_t)a;
     F.c[1] = (uint8_t)b;
@@ -735,12 +795,12 @@ DEV int newface(Scr& S, Epa& E, int a, int b, int c, bool forced) {
         float d;
         if (!(getedgedist(S, n, a, b, d) || getedgedist(S, n, b, c, d) || getedgedist(S, n, c, a, d))) d = dot(aw, n) / l;
         n = n / l;
-        F.n = n;
+        stv(F.n, n);
         F.d = d;
         if (forced || (d >= -kEpaPlaneEps)) return face;
         E.status = 3;  // NonConvex
     } else {
-        F.n = n;
+        stv(F.n, n);
         E.status = 2;  // Degenerated
     }
     list_remove(S, E.hull, face);
@@ -748,7 +808,8 @@ DEV int newface(Scr& S, Epa& E, int a, int b, int c, bool forced) {
     stock_push(S, E, face);
     return -1;
 }
-DEV int findbest(const Scr& S, const Epa& E) {
+template <int AS>
+DEV int findbest(const ScrT<AS>& S, const Epa& E) {
     int minf = E.hull;
     float mind = S.fc[minf].d * S.fc[minf].d;
     for (int f = S.fc[minf].l[1]; f != kNone; f = S.fc[f].l[1]) {
@@ -761,7 +822,8 @@ DEV int findbest(const Scr& S, const Epa& E) {
     return minf;
 }
 // EPA::expand (cpp:864-900) as an explicit-stack walk: frame = face | edge << 8 | stage << 10
-GJK_CALLED bool expand(Scr& S, Epa& E, unsigned pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
+template <int AS>
+GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
     int sp = 0;
     S.stack[sp++] = (uint32_t)f0 | ((uint32_t)e0 << 8);
     bool ret = false;
@@ -770,9 +832,9 @@ GJK_CALLED bool expand(Scr& S, Epa& E, unsigned pass, int w, int f0, int e0, int
         const int f = (int)(fr & 255u), e = (int)((fr >> 8) & 3u), stage = (int)(fr >> 10);
         const int e1 = e == 2 ? 0 : e + 1, e2 = e == 0 ? 2 : e - 1;
         if (stage == 0) {
-            SFace& F = S.fc[f];
+            auto& F = S.fc[f];
             if (F.pass != (uint8_t)pass) {
-                if ((dot(F.n, svw(S, w)) - F.d) < -kEpaPlaneEps) {
+                if ((dot(ldv(F.n), svw(S, w)) - F.d) < -kEpaPlaneEps) {
                     const int nf = newface(S, E, F.c[e1], F.c[e], w, false);
                     if (S.overflow) return false;
                     ret = false;
@@ -804,7 +866,7 @@ GJK_CALLED bool expand(Scr& S, Epa& E, unsigned pass, int w, int f0, int e0, int
             if (!ret) {
                 sp--;
             } else {
-                const SFace& F = S.fc[f];
+                const auto& F = S.fc[f];
                 if (sp >= S.max_stack) {
                     S.overflow = 1;
                     return false;
@@ -824,7 +886,8 @@ GJK_CALLED bool expand(Scr& S, Epa& E, unsigned pass, int w, int f0, int e0, int
     return ret;
 }
 // EPA::Evaluate (cpp:648-768) on the GJK's simplex s; out: normal, depth, result (rank, c, p)
-GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v3& normal, float& depth, Simp& res) {
+template <int AS>
+GJK_CALLED int epa_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v3& normal, float& depth, Simp& res) {
     Epa E;
     E.hull = kNone;
     E.hull_count = 0;
@@ -854,7 +917,8 @@ GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
         if (S.overflow) return 9;
         if (E.hull_count == 4) {
             int best = findbest(S, E);
-            SFace outer = S.fc[best];
+            SFace outer;
+            copy_face(outer, S.fc[best]);
             unsigned pass = 0;
             bind(S, t0, 0, t1, 0);
             bind(S, t0, 1, t2, 0);
@@ -864,6 +928,7 @@ GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
             bind(S, t2, 2, t3, 1);
             E.status = 0;
             for (int iterations = 0; iterations < kEpaMaxIterations; ++iterations) {
+                GJK_MARK(4);
                 if (E.nextsv < kEpaMaxVertices) {
                     if (4 + E.nextsv >= S.max_sv) {
                         S.overflow = 1;
@@ -873,7 +938,7 @@ GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
                     const int w = 4 + E.nextsv++;
                     bool valid = true;
                     S.fc[best].pass = (uint8_t)(++pass);
-                    const v3 bn = S.fc[best].n;
+                    const v3 bn = ldv(S.fc[best].n);
                     const float bd = S.fc[best].d;
                     getsupport(S, m, bn, w);
                     const float wdist = dot(bn, svw(S, w)) - bd;
@@ -888,7 +953,7 @@ GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
                             E.hull_count--;
                             stock_push(S, E, best);
                             best = findbest(S, E);
-                            outer = S.fc[best];
+                            copy_face(outer, S.fc[best]);
                         } else {
                             E.status = 4;  // InvalidHull
                             break;
@@ -937,25 +1002,30 @@ GJK_CALLED int epa_evaluate(Scr& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v
 }
 
 // btGjkEpaSolver2::Penetration (cpp:973-1017) with margins; t0 / t1 = (basis, origin)
-DEV bool penetration(Scr& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
+template <int AS>
+DEV bool penetration(ScrT<AS>& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
                      v3& nrm) {
     const Mink m = make_mink(sh, b0, o0, b1, o1, true);
     Gjk2 g;
+    GJK_MARK(2);
     if (g2_evaluate(S, m, g, -guess) != 1) return false;
+    GJK_MARK(3);
     v3 en;
     float ed;
     Simp res;
     const int es = epa_evaluate(S, m, g, g.cs, -guess, en, ed, res);
+    GJK_MARK(5);
     if (es == 9 || S.overflow) return false;
     v3 w0 = zero3();
-    for (int i = 0; i < res.rank; ++i) w0 += support0(m, S.sv[sc(res, i)].d) * get4(res.p, i);
+    for (int i = 0; i < res.rank; ++i) w0 += support0(m, ldv(S.sv[sc(res, i)].d)) * get4(res.p, i);
     wA = xf(b0, o0, w0);
     wB = xf(b0, o0, w0 - en * ed);
     nrm = -en;
     return true;
 }
 // btGjkEpaSolver2::Distance (cpp:937-970), margins off
-DEV bool distance(Scr& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
+template <int AS>
+DEV bool distance(ScrT<AS>& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
                   v3& nrm) {
     const Mink m = make_mink(sh, b0, o0, b1, o1, false);
     Gjk2 g;
@@ -963,7 +1033,7 @@ DEV bool distance(Scr& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3
     v3 w0 = zero3(), w1 = zero3();
     for (int i = 0; i < g.cs.rank; ++i) {
         const float p = get4(g.cs.p, i);
-        const v3 d = S.sv[sc(g.cs, i)].d;
+        const v3 d = ldv(S.sv[sc(g.cs, i)].d);
         w0 += support0(m, d) * p;
         w1 += support1(m, -d) * p;
     }
@@ -976,7 +1046,8 @@ DEV bool distance(Scr& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3
 }
 // btGjkEpaPenetrationDepthSolver::calcPenDepth (cpp:22-79); called, not inlined: the rare path stays out
 // of the narrowphase's hot code
-__device__ __noinline__ bool calc_pen_depth(Scr& S, const Shape& sh, const m3& bA, v3 oA, const m3& bB, v3 oB, v3& v, v3& wA, v3& wB) {
+template <int AS>
+__device__ __noinline__ bool calc_pen_depth(ScrT<AS>& S, const Shape& sh, const m3& bA, v3 oA, const m3& bB, v3 oB, v3& v, v3& wA, v3& wB) {
 #pragma unroll 1
     for (int i = 0; i < 9; i++) {
         v3 g;
@@ -1084,9 +1155,7 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
         }
         v = nv;
         if (iter++ > 1000) break;
-#ifdef RLGPU_GJK_TRACE
-        RLGPU_GJK_TRACE(iter);
-#endif
+        GJK_MARK(1);
         if (vs.n == 4) {
             degen = 13;
             break;
@@ -1115,17 +1184,18 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
         v = zero3();
         bool ok2;
         if (pen_count) atomicAdd(pen_count, 1);
+        ScrT<1> slow1 = in_space<1>(slow);
         if (fast && atomicCAS(lock, 0, 1) == 0) {
-            fast->overflow = 0;
-            ok2 = calc_pen_depth(*fast, s, R, oA, I, oB, v, tA, tB);
-            const bool redo = fast->overflow != 0;
+            ScrT<3> fast3 = in_space<3>(*fast);
+            ok2 = calc_pen_depth(fast3, s, R, oA, I, oB, v, tA, tB);
+            const bool redo = fast3.overflow != 0;
             atomicExch(lock, 0);
             if (redo) {
                 v = zero3();
-                ok2 = calc_pen_depth(slow, s, R, oA, I, oB, v, tA, tB);
+                ok2 = calc_pen_depth(slow1, s, R, oA, I, oB, v, tA, tB);
             }
         } else {
-            ok2 = calc_pen_depth(slow, s, R, oA, I, oB, v, tA, tB);
+            ok2 = calc_pen_depth(slow1, s, R, oA, I, oB, v, tA, tB);
         }
         if (ok2) {
             v3 tn = tB - tA;

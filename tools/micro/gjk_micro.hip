@@ -5,8 +5,9 @@
 #include <cstdio>
 
 __device__ long long g_trace[64];
+__device__ int g_tid[64];
 __device__ int g_ntrace;
-#define RLGPU_GJK_TRACE(it) { if (g_ntrace < 64) g_trace[g_ntrace++] = clock64(); }
+#define RLGPU_GJK_TRACE(id) { if (g_ntrace < 64) { g_tid[g_ntrace] = (id); g_trace[g_ntrace++] = clock64(); } }
 
 #include "../../reinforcement-learning_amd/csrc/gjk.hpp"
 
@@ -60,6 +61,16 @@ int main() {
                 hipMemcpy(o, out, 64, hipMemcpyDeviceToHost);
                 hipMemcpy(r, res, 8, hipMemcpyDeviceToHost);
                 if (o[0] < best) best = o[0];
+            }
+            if (mode == 1 && gap < -0.05f) {
+                long long tr[64];
+                int id[64], nt;
+                hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_trace), sizeof tr);
+                hipMemcpyFromSymbol(id, HIP_SYMBOL(g_tid), sizeof id);
+                hipMemcpyFromSymbol(&nt, HIP_SYMBOL(g_ntrace), sizeof nt);
+                printf("  trace:");
+                for (int k = 1; k < nt; k++) printf(" %d:%lld", id[k], tr[k] - tr[k - 1]);
+                printf("\n");
             }
             printf("%s gap %+.2f: %8llu cycles (pen-solver calls %llu, hit %.0f depth %+.5f) GJK iterations %llu: first %llu, "
                    "per iteration %llu, after the loop %llu\n", mode ? "LDS-first" : "HBM-only ", gap, best, o[1], r[0], r[1], o[2],
