@@ -46,6 +46,15 @@ int rlgpu_mesh_known_hash(int32_t game_mode, uint32_t hash);
  * has a record, 0 = none).  Host only. */
 int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects, float* out);
 
+/* The order in which the reference's per-object quantized BVH (btBvhTriangleMeshShape with quantized
+ * AABB compression, RocketSim.cpp:167; btOptimizedBvh::build, btOptimizedBvh.cpp:28-160, and
+ * btQuantizedBvh::buildTree, btQuantizedBvh.cpp:116-305) hands overlapping triangles to the narrowphase:
+ * out[k] = the mesh triangle visited k-th (objects in order, each object's triangles permuted within its
+ * own range).  The env kernel commits mesh contacts in this order.  tris / object_ntris as
+ * rlgpu_mesh_edge_info.  Host only. */
+int rlgpu_mesh_bvh_order(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects,
+                         int32_t* out);
+
 /* The car-hitbox vs mesh-triangle narrowphase of the env kernel on its own (the GJK / EPA query of
  * btConvexTriangleCallback::processTriangle -> btConvexConvexAlgorithm -> btGjkPairDetector with
  * btGjkEpaPenetrationDepthSolver, btConvexConcaveCollisionAlgorithm.cpp:71-138 and

@@ -287,3 +287,24 @@ def box_box(rot_a, centre_a, rot_b, centre_b):
     f.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 5
     f(n, _p(rot_a), _p(centre_a), _p(rot_b), _p(centre_b), _p(out))
     return out
+
+
+def bvh_order(tris, object_ntris=None):
+    """oracle_bvh_order (bvh_ref.hpp): per collision object, the order its quantized BVH visits the
+    triangles -> [ntris] int32, out[k] = the mesh triangle visited k-th (each object's range permuted
+    within itself)."""
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    counts = [len(tris)] if object_ntris is None else [int(c) for c in object_ntris]
+    out = np.zeros(len(tris), np.int32)
+    f = lib().oracle_bvh_order
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    t0 = 0
+    for c in counts:
+        if c:
+            part = np.ascontiguousarray(tris[t0:t0 + c])
+            o = np.zeros(c, np.int32)
+            f(_p(part), c, _p(o))
+            out[t0:t0 + c] = o + t0
+        t0 += c
+    return out

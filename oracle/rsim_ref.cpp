@@ -20,7 +20,8 @@
 // Documented deviations from the reference (also in DESIGN.md):
 //   * synthetic arena mesh (include/rlgpu_arena_mesh.h) by default; real .cmf meshes can be
 //     loaded (World::set_mesh), one collision object per file;
-//   * (box-triangle runs Bullet's GJK / EPA, gjk_ref.hpp; box-box btBoxBoxDetector, boxbox_ref.hpp)
+//   * (box-triangle runs Bullet's GJK / EPA, gjk_ref.hpp; box-box btBoxBoxDetector, boxbox_ref.hpp;
+//     mesh triangles are visited in the quantized BVH's order, bvh_ref.hpp)
 //   * time-based deactivation (btRigidBody.h:531-545) is not modelled -- only the zero-velocity
 //     ball sleep of Arena.cpp:722-727;
 //   * pairs are processed in btRSBroadphase's order (per dynamic proxy: its statics, then its pairs with
@@ -36,6 +37,7 @@
 #include "../include/rlgpu_arena_mesh.h"
 #include "../include/rlgpu_detmath.h"
 #include "boxbox_ref.hpp"
+#include "bvh_ref.hpp"
 #include "gjk_ref.hpp"
 
 namespace orc {
@@ -216,6 +218,15 @@ void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) 
             for (int i = 0; i < obj_ntris[k] && t < n; i++) tri_obj[t++] = k;
     }
     tri_info = edge::gen_edge_info(tri, tri_obj);  // RocketSim.cpp:166-170
+    // btBvhTriangleMeshShape per object (RocketSim.cpp:167): the order its quantized BVH visits the triangles
+    tri_visit.resize(n);
+    for (int t0 = 0; t0 < n;) {
+        int t1 = t0;
+        while (t1 < n && tri_obj[t1] == tri_obj[t0]) t1++;
+        std::vector<int> order = bvh::leaf_order(p + (size_t)t0 * 9, t1 - t0);
+        for (int k = 0; k < t1 - t0; k++) tri_visit[t0 + k] = t0 + order[k];
+        t0 = t1;
+    }
 }
 
 const World& world() {
@@ -1384,7 +1395,8 @@ struct Sim {
         float r = w.ball_radius;
         float ext = r + 0.08f;
         float cbt = pair_cbt(0, 10);
-        for (int t = t0; t < t1; t++) {
+        for (int k = t0; k < t1; k++) {  // the object's triangles in BVH visit order
+            const int t = w.tri_visit[k];
             if (!aabb_overlap(c - V(ext, ext, ext), c + V(ext, ext, ext), w.tri_min[t], w.tri_max[t])) continue;
             V pt, nrm;
             float depth;
@@ -1510,7 +1522,8 @@ struct Sim {
         V mn, mx;
         body_aabb(bi, b[bi].pos, b[bi].rot, mn, mx);
         float cbt = pair_cbt(bi, 10);
-        for (int t = t0; t < t1; t++) {
+        for (int k = t0; k < t1; k++) {  // the object's triangles in BVH visit order
+            const int t = w.tri_visit[k];
             if (!aabb_overlap(mn, mx, w.tri_min[t], w.tri_max[t])) continue;
             V n, pb;
             float d;
@@ -2252,5 +2265,13 @@ void oracle_box_box(int n, const float* rot_a, const float* centre_a, const floa
         });
         o[0] = (float)cnt;
     }
+}
+}  // extern "C"
+
+extern "C" {
+// Bullet's BVH visit order of one mesh's triangles (bvh_ref.hpp): out[k] = triangle visited k-th.
+void oracle_bvh_order(const float* tris, int ntris, int32_t* out) {
+    std::vector<int> o = orc::bvh::leaf_order(tris, ntris);
+    for (int k = 0; k < ntris; k++) out[k] = o[k];
 }
 }  // extern "C"

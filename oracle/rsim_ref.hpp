@@ -26,6 +26,7 @@ struct World {
     std::vector<V> tri, tri_min, tri_max;
     std::vector<int> tri_obj;
     std::vector<TriInfo> tri_info;  // internal-edge records (btGenerateInternalEdgeInfo, edge_ref.hpp)
+    std::vector<int> tri_visit;     // each object's triangles in Bullet's BVH visit order (bvh_ref.hpp)
     void set_mesh(const float* tris_bt, int n, const int* obj_ntris, int nobjects);
     float kick_x[5], kick_y[5];
     M kick_rot[2][5];

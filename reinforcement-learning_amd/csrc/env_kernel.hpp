@@ -96,7 +96,7 @@ struct WheelT {
 
 struct Cand {
     float n[3], p[3], depth;
-    int order;  // (pair rank << 20) | triangle: commit order
+    int order;  // (pair rank << 20) | triangle's BVH visit position: commit order
     int key;    // manifold key
 };
 
@@ -112,6 +112,8 @@ struct MeshView {
     const int* cell_start;   // [ncell + 1]
     const float4* tri;       // [ntris * 3]: v0 | object, v1, v2 of triangle t (load order)
     const float4* edge;      // [ntris]: internal-edge record (edge_info.hpp EdgeInfo)
+    const int* visit;        // [2 * ntris]: triangle -> position in its object's BVH walk, then the
+                             // inverse (mesh.hpp MeshGrid::visit_pos / visit_tri)
     gjk::GjkScratch* gjk;    // [grid lanes]: box-triangle penetration-solver scratch (gjk.hpp)
     float ox, oy, oz, inv_cell;
     int nx, ny, nz, ntris;

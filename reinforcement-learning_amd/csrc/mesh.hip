@@ -149,7 +149,120 @@ MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntr
         std::memcpy(&d[3], &obj[t], sizeof(int));
     }
     g.edge = mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1);
+    g.visit_pos.assign(ntris, 0);
+    g.visit_tri.assign(ntris, 0);
+    for (int t0 = 0; t0 < ntris;) {  // one btBvhTriangleMeshShape per object
+        int t1 = t0;
+        while (t1 < ntris && obj[t1] == obj[t0]) t1++;
+        const std::vector<int> order = bvh_visit_order(tris + (size_t)t0 * 9, t1 - t0);
+        for (int k = 0; k < t1 - t0; k++) {
+            g.visit_tri[t0 + k] = t0 + order[k];
+            g.visit_pos[t0 + order[k]] = t0 + k;
+        }
+        t0 = t1;
+    }
     return g;
+}
+
+namespace {
+// btQuantizedBvh's quantizer (btQuantizedBvh.h:331-415): bounds, scale, 16-bit snapped coordinates
+struct BvhQuant {
+    float lo[3], hi[3], scale[3];
+    void rescale() {
+        for (int a = 0; a < 3; a++) scale[a] = 65533.f / (hi[a] - lo[a]);
+    }
+    uint16_t q(float x, int a, bool upper) const {
+        const float v = (x - lo[a]) * scale[a];
+        return upper ? (uint16_t)((uint16_t)(v + 1.f) | 1) : (uint16_t)((uint16_t)v & 0xfffe);
+    }
+    float uq(uint16_t x, int a) const { return (float)x / scale[a] + lo[a]; }
+};
+}  // namespace
+
+std::vector<int> bvh_visit_order(const float* tris, int n) {
+    std::vector<int> out(n);
+    if (n <= 0) return out;
+    // btTriangleMeshShape::recalcLocalAabb: support vertices along +-axes (a vertex replaces the best
+    // only with a strictly larger dot), margin 0
+    float best_hi[3], best_lo[3];
+    for (int a = 0; a < 3; a++) best_hi[a] = best_lo[a] = -1e18f;
+    for (int i = 0; i < 3 * n; i++)
+        for (int a = 0; a < 3; a++) {
+            const float c = tris[3 * i + a];
+            if (c > best_hi[a]) best_hi[a] = c;
+            if (-c > best_lo[a]) best_lo[a] = -c;
+        }
+    BvhQuant Q;
+    for (int a = 0; a < 3; a++) {  // setQuantizationValues(min, max, 1.0) with its two refinements
+        Q.lo[a] = (-best_lo[a] - 0.f) - 1.f;
+        Q.hi[a] = (best_hi[a] + 0.f) + 1.f;
+    }
+    Q.rescale();
+    for (int a = 0; a < 3; a++) {
+        const float v = Q.uq(Q.q(Q.lo[a], a, false), a) - 1.f;
+        Q.lo[a] = Q.lo[a] < v ? Q.lo[a] : v;
+    }
+    Q.rescale();
+    for (int a = 0; a < 3; a++) {
+        const float v = Q.uq(Q.q(Q.hi[a], a, true), a) + 1.f;
+        Q.hi[a] = Q.hi[a] > v ? Q.hi[a] : v;
+    }
+    Q.rescale();
+    // leaves: quantized vertex AABBs widened to 0.002 (btOptimizedBvh.cpp:118-150); the partitioning
+    // only ever needs each leaf's unquantized centre, 0.5 * (max + min)
+    struct L {
+        float c[3];
+        int t;
+    };
+    std::vector<L> leaf(n);
+    for (int t = 0; t < n; t++) {
+        for (int a = 0; a < 3; a++) {
+            float mn = 1e18f, mx = -1e18f;
+            for (int k = 0; k < 3; k++) {
+                const float c = tris[9 * t + 3 * k + a];
+                mn = c < mn ? c : mn;
+                mx = mx < c ? c : mx;
+            }
+            if (mx - mn < 0.002f) {
+                mx = mx + 0.001f;
+                mn = mn - 0.001f;
+            }
+            const float umax = Q.uq(Q.q(mx, a, true), a), umin = Q.uq(Q.q(mn, a, false), a);
+            leaf[t].c[a] = (umax + umin) * 0.5f;
+        }
+        leaf[t].t = t;
+    }
+    // buildTree (btQuantizedBvh.cpp:116-305) without the nodes: ranges split depth first, left first
+    std::vector<std::pair<int, int>> todo{{0, n}};
+    while (!todo.empty()) {
+        const auto [s, e] = todo.back();
+        todo.pop_back();
+        const int m = e - s;
+        if (m <= 1) continue;
+        float mean[3] = {0.f, 0.f, 0.f}, var[3] = {0.f, 0.f, 0.f};
+        for (int i = s; i < e; i++)
+            for (int a = 0; a < 3; a++) mean[a] += leaf[i].c[a];
+        const float inv = 1.f / (float)m;
+        for (int a = 0; a < 3; a++) mean[a] *= inv;
+        for (int i = s; i < e; i++)
+            for (int a = 0; a < 3; a++) {
+                const float d = leaf[i].c[a] - mean[a];
+                var[a] += d * d;
+            }
+        const float inv1 = 1.f / ((float)m - 1);
+        for (int a = 0; a < 3; a++) var[a] *= inv1;
+        const int axis = var[0] < var[1] ? (var[1] < var[2] ? 2 : 1) : (var[0] < var[2] ? 2 : 0);
+        // sortAndCalcSplittingIndex recomputes the means (same operations, same value)
+        const float split = mean[axis];
+        int k = s;
+        for (int i = s; i < e; i++)
+            if (leaf[i].c[axis] > split) std::swap(leaf[i], leaf[k++]);
+        if (k <= s + m / 3 || k >= e - 1 - m / 3) k = s + (m >> 1);
+        todo.push_back({k, e});  // right after left
+        todo.push_back({s, k});
+    }
+    for (int i = 0; i < n; i++) out[i] = leaf[i].t;
+    return out;
 }
 
 // btGenerateInternalEdgeInfo per collision object (one btBvhTriangleMeshShape per object, partId 0):
@@ -246,6 +359,15 @@ extern "C" int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int3
         }
         const std::vector<float> e = rlgpu::mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1);
         std::memcpy(out, e.data(), e.size() * sizeof(float));
+    });
+}
+
+extern "C" int rlgpu_mesh_bvh_order(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects,
+                                    int32_t* out) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(out, "rlgpu_mesh_bvh_order: null argument");
+        const rlgpu::MeshGrid g = rlgpu::build_mesh_grid(tris, ntris, object_ntris, nobjects);
+        std::copy(g.visit_tri.begin(), g.visit_tri.end(), out);
     });
 }
 

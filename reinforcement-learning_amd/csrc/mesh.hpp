@@ -14,6 +14,9 @@ struct MeshGrid {
     // per triangle in load order: 12 floats = v0.xyz | object id bits, v1.xyz | 0, v2.xyz | 0, and its
     // internal-edge record (edge_info.hpp EdgeInfo: 3 angles | flags bits)
     std::vector<float> tri, edge;
+    // Bullet's BVH visit order (bvh_visit_order): visit position of each triangle (object start + rank
+    // within its object) and the triangle at each position
+    std::vector<int> visit_pos, visit_tri;
     float ox = 0, oy = 0, oz = 0, inv_cell = 1;
     int nx = 1, ny = 1, nz = 1, ntris = 0;
 };
@@ -25,6 +28,11 @@ MeshGrid build_mesh_grid(const float* tris_bt, int ntris, const int32_t* object_
 // btGenerateInternalEdgeInfo over every object of a mesh (edge_info.hpp): ntris x 4 floats
 // (m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle, flags bits; flags 0 = no record)
 std::vector<float> mesh_edge_info(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects);
+
+// The order in which Bullet's quantized BVH of one mesh visits its triangles (btBvhTriangleMeshShape with
+// quantized AABB compression, RocketSim.cpp:167; btOptimizedBvh::build, btQuantizedBvh::buildTree and the
+// stackless walk, btQuantizedBvh.cpp:76-305,676-740): out[k] = the triangle visited k-th.
+std::vector<int> bvh_visit_order(const float* tris_bt, int ntris);
 
 // The built-in synthetic arena mesh (include/rlgpu_arena_mesh.h) in bullet units (uu / 50).
 std::vector<float> builtin_mesh_bt();

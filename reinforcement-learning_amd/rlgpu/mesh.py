@@ -193,6 +193,17 @@ def edge_info(mesh):
     return out
 
 
+def bvh_order(mesh):
+    """The order the reference's per-object quantized BVH visits the triangles of `mesh`
+    (rlgpu_mesh_bvh_order): [ntris] int32, out[k] = the triangle visited k-th."""
+    L = _bind()
+    L.rlgpu_mesh_bvh_order.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    out = np.zeros(mesh.num_tris, np.int32)
+    _lib.check(L.rlgpu_mesh_bvh_order(mesh.tris.ctypes.data, mesh.num_tris, mesh.object_ntris.ctypes.data,
+                                      mesh.num_objects, out.ctypes.data), "rlgpu_mesh_bvh_order")
+    return out
+
+
 def box_triangle_queries(rot, centre, tri, cbt, lds_first=True):
     """The env kernel's car-hitbox vs triangle narrowphase (Bullet's GJK / EPA query, include/rlgpu_mesh.h
     rlgpu_box_triangle_queries) on the device, one query per lane.  CUDA tensors: rot [n,3,3] (basis rows),

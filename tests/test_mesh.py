@@ -182,3 +182,43 @@ def test_internal_edge_info_known_answers():
         a = info[0, 1]  # triangle 0's V1V2 edge is the fold
         assert abs(abs(a) - np.pi / 2) < 1e-5, a
         assert bool(_edge_flags(info)[0] & 2) == is_convex  # TRI_INFO_V1V2_CONVEX
+
+
+@pytest.mark.parametrize("which", ["procedural_soccar", "test_mesh", "random"])
+def test_bvh_visit_order_matches_oracle(which):
+    """btOptimizedBvh::build / btQuantizedBvh::buildTree (btOptimizedBvh.cpp:28-160, btQuantizedBvh.cpp:
+    116-305): the triangle order of each object's quantized BVH walk, which the env kernel commits mesh
+    contacts in, equals the oracle's independent restatement (bvh_ref.hpp) exactly."""
+    from rlgpu.mesh import bvh_order, procedural_soccar
+    if which == "procedural_soccar":
+        mesh = procedural_soccar()
+    elif which == "test_mesh":
+        t, o = mesh_from_objects(procedural_arena_mesh())
+        mesh = ArenaMesh([t[s:e] for s, e in zip(np.r_[0, np.cumsum(o)[:-1]], np.cumsum(o))])
+    else:  # ragged objects of scattered triangles, one flat in z (the 0.002 widening), one of a single triangle
+        rng = np.random.default_rng(7)
+        objs = [rng.uniform(-50, 50, (n, 9)).astype(np.float32) for n in (257, 1, 40)]
+        objs[2][:, 2::3] = 3.0
+        mesh = ArenaMesh(objs)
+    got = bvh_order(mesh)
+    want = oracle.bvh_order(mesh.tris, mesh.object_ntris)
+    np.testing.assert_array_equal(got, want)
+    t0 = 0
+    for c in mesh.object_ntris:  # a permutation of each object's own range
+        assert sorted(got[t0:t0 + c]) == list(range(t0, t0 + c))
+        t0 += c
+    if which != "random":
+        assert (got != np.arange(mesh.num_tris)).any()
+
+
+def test_bvh_visit_order_known_answers():
+    """Hand-worked buildTree partitions: two triangles -> the one whose centre is above the mean first
+    (the 1/3 balance fallback splits 1 + 1); five triangles in a row along x -> visited in descending x
+    (mean split 2 + 3, then the fallbacks)."""
+    from rlgpu.mesh import bvh_order
+    tri = np.float32([0, 0, 0, 1, 0, 0, 0, 1, 0])
+    row = lambda xs: np.stack([tri + np.float32([x, 0, 0] * 3) for x in xs])
+    assert list(bvh_order(ArenaMesh([row([0, 10])]))) == [1, 0]
+    assert list(bvh_order(ArenaMesh([row([0, 10, 20, 30, 40])]))) == [4, 3, 2, 1, 0]
+    assert list(bvh_order(ArenaMesh([row([40, 0, 30, 10, 20])]))) == list(oracle.bvh_order(row([40, 0, 30, 10, 20])))
+    assert list(bvh_order(ArenaMesh([tri[None]]))) == [0]
