@@ -404,8 +404,10 @@ struct Sim {
                 nrm = da > 0.f ? w.plane_n[p] : -w.plane_n[p];
             }
         }
-        // mesh triangles (btTriangleRaycastCallback::processTriangle)
-        for (int t = 0; t < w.ntris; t++) {
+        // mesh triangles in BVH visit order (btTriangleRaycastCallback::processTriangle keeps a strictly
+        // closer hit, so the first visited wins a tie)
+        for (int k = 0; k < w.ntris; k++) {
+            const int t = w.tri_visit[k];
             const V& v0 = w.tri[(size_t)t * 3];
             const V& v1 = w.tri[(size_t)t * 3 + 1];
             const V& v2 = w.tri[(size_t)t * 3 + 2];
@@ -1389,7 +1391,7 @@ struct Sim {
         float cbt = pair_cbt(0, 10);
         if (dist < cbt) add_contact(key, n, on_plane, dist);
     }
-    // triangles [t0, t1) of one mesh object, in index order (btConvexTriangleCallback)
+    // triangles [t0, t1) of one mesh object, in BVH visit order (btConvexTriangleCallback)
     void collide_sphere_mesh(int key, int t0, int t1) {
         V c = b[0].pos;
         float r = w.ball_radius;

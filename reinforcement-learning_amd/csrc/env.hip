@@ -747,7 +747,7 @@ struct rlgpu_envset {
     unsigned long long* d_prof = nullptr;
     double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
-    void *d_cell_tri = nullptr, *d_cell_start = nullptr, *d_tri = nullptr, *d_edge = nullptr, *d_visit = nullptr;  // arena mesh (MeshView)
+    void *d_cell_tri = nullptr, *d_cell_start = nullptr, *d_tri = nullptr, *d_edge = nullptr;  // arena mesh (MeshView)
     void* d_gjk = nullptr;  // per-lane box-triangle penetration-solver scratch (MeshView::gjk)
     rl::MeshView mesh{};
     rl::Plugins plug{};                 // host copy of the reward / terminal registry
@@ -934,12 +934,6 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         RLGPU_CHECK_HIP(hipMemcpy(e->d_edge, grid.edge.data(), grid.edge.size() * sizeof(float), hipMemcpyHostToDevice));
         e->mesh.tri = (const float4*)e->d_tri;
         e->mesh.edge = (const float4*)e->d_edge;
-        RLGPU_CHECK_HIP(hipMalloc(&e->d_visit, 2 * grid.visit_pos.size() * sizeof(int)));
-        RLGPU_CHECK_HIP(hipMemcpy(e->d_visit, grid.visit_pos.data(), grid.visit_pos.size() * sizeof(int),
-                                  hipMemcpyHostToDevice));
-        RLGPU_CHECK_HIP(hipMemcpy((int*)e->d_visit + grid.visit_pos.size(), grid.visit_tri.data(),
-                                  grid.visit_tri.size() * sizeof(int), hipMemcpyHostToDevice));
-        e->mesh.visit = (const int*)e->d_visit;
         e->mesh.ox = grid.ox;
         e->mesh.oy = grid.oy;
         e->mesh.oz = grid.oz;
@@ -1092,7 +1086,6 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_terminals);
         (void)hipFree(e->d_cell_tri);
         (void)hipFree(e->d_tri);
-        (void)hipFree(e->d_visit);
         (void)hipFree(e->d_edge);
         (void)hipFree(e->d_gjk);
         (void)hipFree(e->d_cell_start);

@@ -416,7 +416,7 @@ __device__ __noinline__ void box_tri_query(ArenaLDS* A, const MeshView& M, int b
     v3 n, pb;
     float d;
     if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
-        emit(A, bi * 5, M.visit[t], mesh_key(bi, obj), n, pb, d);
+        emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
 }
 // the queued box-triangle queries of the workgroup's arenas, dealt round-robin over all its lanes (an
 // arena with many triangle contacts borrows the lanes of quiet ones); base = the workgroup's arenas,
@@ -465,7 +465,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                     v3 pt, nrm;
                     float depth;
                     if (sphere_triangle(c, r, v0, v1, v2, cbt, pt, nrm, depth))
-                        emit(A, rank, M.visit[t], mesh_key(0, obj), nrm, pt, depth);
+                        emit(A, rank, t, mesh_key(0, obj), nrm, pt, depth);
                 });
             }
         } else {
@@ -600,10 +600,10 @@ DEV void commit_contacts(ArenaLDS* A, const MeshView& M, Prof* P = nullptr) {
             if (cur >= 0) refresh(A, cur);
             cur = c.key;
         }
-        // mesh-object keys carry their triangle's BVH visit position in the low bits of the commit order
+        // mesh-object keys carry their triangle in the low bits of the commit order
         int ka, kb;
         key_bodies(c.key, ka, kb);
-        const int tri = (c.key < kDynKey && kb - 10 < kMaxObj) ? M.visit[M.ntris + (c.order & (kMaxTris - 1))] : -1;
+        const int tri = (c.key < kDynKey && kb - 10 < kMaxObj) ? (c.order & (kMaxTris - 1)) : -1;
         add_contact(A, M, c.key, v3{c.n[0], c.n[1], c.n[2]}, v3{c.p[0], c.p[1], c.p[2]}, c.depth, tri);
     }
     if (cur >= 0) refresh(A, cur);

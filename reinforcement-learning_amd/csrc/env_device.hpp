@@ -225,8 +225,9 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
     const float kRayCull = 0.1f;
     const v3 smin = v3{fminf(from.x, to.x) - kRayCull, fminf(from.y, to.y) - kRayCull, fminf(from.z, to.z) - kRayCull};
     const v3 smax = v3{fmaxf(from.x, to.x) + kRayCull, fmaxf(from.y, to.y) + kRayCull, fmaxf(from.z, to.z) + kRayCull};
-    // closest hit over the mesh = the first minimum of the reference's index-order scan: ties in
-    // f go to the lower triangle index, and a plane hit at the same f is kept (strict <)
+    // closest hit over the mesh = the first minimum of the reference's walk (btTriangleRaycastCallback keeps
+    // a hit only when strictly closer): ties in f go to the lower triangle index = the earlier BVH visit
+    // position (mesh.hpp), and a plane hit at the same f is kept
     int best_t = -1;
     grid_query(M, smin, smax, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int) {
         v3 tn = cross(v1 - v0, v2 - v0);

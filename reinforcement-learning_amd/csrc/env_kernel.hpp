@@ -96,7 +96,7 @@ struct WheelT {
 
 struct Cand {
     float n[3], p[3], depth;
-    int order;  // (pair rank << 20) | triangle's BVH visit position: commit order
+    int order;  // (pair rank << 20) | triangle (= its BVH visit position, mesh.hpp): commit order
     int key;    // manifold key
 };
 
@@ -110,10 +110,8 @@ struct MeshView {
     const float4* cell_tri;  // [entries * 3]: the triangles of every cell inline, ascending index
                              // (v0 | object, v1 | triangle index, v2 | cell x; mesh.hpp MeshGrid)
     const int* cell_start;   // [ncell + 1]
-    const float4* tri;       // [ntris * 3]: v0 | object, v1, v2 of triangle t (load order)
+    const float4* tri;       // [ntris * 3]: v0 | object, v1, v2 of triangle t (BVH visit order, mesh.hpp)
     const float4* edge;      // [ntris]: internal-edge record (edge_info.hpp EdgeInfo)
-    const int* visit;        // [2 * ntris]: triangle -> position in its object's BVH walk, then the
-                             // inverse (mesh.hpp MeshGrid::visit_pos / visit_tri)
     gjk::GjkScratch* gjk;    // [grid lanes]: box-triangle penetration-solver scratch (gjk.hpp)
     float ox, oy, oz, inv_cell;
     int nx, ny, nz, ntris;

@@ -57,8 +57,8 @@ std::vector<float> builtin_mesh_bt() {
     return out;
 }
 
-MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntris, int nobjects) {
-    RLGPU_REQUIRE(tris && ntris > 0, "mesh: no triangles");
+MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_ntris, int nobjects) {
+    RLGPU_REQUIRE(tris_in && ntris > 0, "mesh: no triangles");
     RLGPU_REQUIRE(ntris < (1 << 20), "mesh: more than 2^20 - 1 triangles");
     if (!object_ntris) nobjects = 1;
     RLGPU_REQUIRE(nobjects >= 1 && nobjects <= RLGPU_MAX_MESH_OBJECTS,
@@ -77,12 +77,33 @@ MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntr
         for (int k = 0; k < nobjects; k++)
             for (int i = 0; i < object_ntris[k]; i++) obj[t++] = k;
     }
+    for (size_t i = 0; i < (size_t)ntris * 9; i++)
+        RLGPU_REQUIRE(std::isfinite(tris_in[i]), "mesh: non-finite vertex coordinate");
+    // The device tables number the triangles in Bullet's BVH visit order (one btBvhTriangleMeshShape per
+    // object): a triangle's index is its visit position, so every "lower index first" rule of the kernel
+    // (grid cells list ascending indices, the commit sorts candidates by (pair, index), ray ties go to the
+    // lower index) follows the reference's walk.  visit_tri maps a position back to the load order.
+    g.visit_pos.assign(ntris, 0);
+    g.visit_tri.assign(ntris, 0);
+    for (int t0 = 0; t0 < ntris;) {
+        int t1 = t0;
+        while (t1 < ntris && obj[t1] == obj[t0]) t1++;
+        const std::vector<int> order = bvh_visit_order(tris_in + (size_t)t0 * 9, t1 - t0);
+        for (int k = 0; k < t1 - t0; k++) {
+            g.visit_tri[t0 + k] = t0 + order[k];
+            g.visit_pos[t0 + order[k]] = t0 + k;
+        }
+        t0 = t1;
+    }
+    std::vector<float> visit_tris((size_t)ntris * 9);
+    for (int p = 0; p < ntris; p++)
+        std::memcpy(&visit_tris[(size_t)p * 9], tris_in + (size_t)g.visit_tri[p] * 9, 9 * sizeof(float));
+    const float* tris = visit_tris.data();  // obj[] is unchanged: objects keep their ranges
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int t = 0; t < ntris; t++)
         for (int v = 0; v < 3; v++)
             for (int a = 0; a < 3; a++) {
                 float x = tris[(size_t)t * 9 + v * 3 + a];
-                RLGPU_REQUIRE(std::isfinite(x), "mesh: non-finite vertex coordinate");
                 mn[a] = std::fmin(mn[a], x);
                 mx[a] = std::fmax(mx[a], x);
             }
@@ -148,19 +169,10 @@ MeshGrid build_mesh_grid(const float* tris, int ntris, const int32_t* object_ntr
             for (int a = 0; a < 3; a++) d[v * 4 + a] = p[v * 3 + a];
         std::memcpy(&d[3], &obj[t], sizeof(int));
     }
-    g.edge = mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1);
-    g.visit_pos.assign(ntris, 0);
-    g.visit_tri.assign(ntris, 0);
-    for (int t0 = 0; t0 < ntris;) {  // one btBvhTriangleMeshShape per object
-        int t1 = t0;
-        while (t1 < ntris && obj[t1] == obj[t0]) t1++;
-        const std::vector<int> order = bvh_visit_order(tris + (size_t)t0 * 9, t1 - t0);
-        for (int k = 0; k < t1 - t0; k++) {
-            g.visit_tri[t0 + k] = t0 + order[k];
-            g.visit_pos[t0 + order[k]] = t0 + k;
-        }
-        t0 = t1;
-    }
+    // internal-edge records of the mesh as loaded (neighbour order = load order), moved with their triangles
+    const std::vector<float> edge = mesh_edge_info(tris_in, ntris, object_ntris, object_ntris ? nobjects : 1);
+    g.edge.resize(edge.size());
+    for (int p = 0; p < ntris; p++) std::memcpy(&g.edge[(size_t)p * 4], &edge[(size_t)g.visit_tri[p] * 4], 4 * sizeof(float));
     return g;
 }
 

@@ -1,5 +1,5 @@
 // mesh.hpp -- host-side construction of the env kernel's MeshView (env_kernel.hpp): the triangle
-// table in load order and its uniform-grid index.  Implemented in mesh.hip.
+// table in Bullet's BVH visit order and its uniform-grid index.  Implemented in mesh.hip.
 #pragma once
 #include <cstdint>
 #include <vector>
@@ -11,7 +11,7 @@ struct MeshGrid {
     // inline: 12 floats = v0.xyz | object id bits, v1.xyz | triangle index bits, v2.xyz | cell x bits
     std::vector<float> cell_tri;
     std::vector<int> cell_start;
-    // per triangle in load order: 12 floats = v0.xyz | object id bits, v1.xyz | 0, v2.xyz | 0, and its
+    // per triangle in BVH visit order: 12 floats = v0.xyz | object id bits, v1.xyz | 0, v2.xyz | 0, and its
     // internal-edge record (edge_info.hpp EdgeInfo: 3 angles | flags bits)
     std::vector<float> tri, edge;
     // Bullet's BVH visit order (bvh_visit_order): visit position of each triangle (object start + rank
