@@ -9,8 +9,9 @@
 // Called by RocketSim for every arena mesh (RocketSim.cpp:166-170) and at the end of the contact-added
 // callback (Arena.cpp:275-279).  Meshes are static at the identity transform (local = world frame).
 // Neighbour candidates of a triangle: the other triangles of its collision object whose AABB, grown
-// by 2e-4, overlaps its own, in index order (the reference walks its quantized BVH; the two orders
-// differ only for edges shared by three or more triangles -- the engine's documented choice).
+// by 2e-4, overlaps its own, in the order the object's quantized BVH visits them (`visit`, bvh_ref.hpp;
+// the reference's processAllTriangles query, btInternalEdgeUtility.cpp:340-356) -- the last neighbour
+// sharing an edge writes its record.
 #pragma once
 #include <cmath>
 #include <map>
@@ -142,7 +143,9 @@ inline void process_triangle(const V* A, const V* B, TriInfo& info) {
 }
 
 // btGenerateInternalEdgeInfo over every collision object of a mesh (tri: 3 vertices per triangle)
-inline std::vector<TriInfo> gen_edge_info(const std::vector<V>& tri, const std::vector<int>& tri_obj) {
+// visit: the mesh's triangles in BVH visit order (each object's range permuted within itself)
+inline std::vector<TriInfo> gen_edge_info(const std::vector<V>& tri, const std::vector<int>& tri_obj,
+                                          const std::vector<int>& visit) {
     const int n = (int)tri_obj.size();
     std::vector<TriInfo> out(n);
     std::vector<V> mn(n), mx(n);
@@ -156,7 +159,8 @@ inline std::vector<TriInfo> gen_edge_info(const std::vector<V>& tri, const std::
     }
     const float g = 2e-4f;
     for (int a = 0; a < n; a++)
-        for (int b = 0; b < n; b++) {
+        for (int k = 0; k < n; k++) {
+            const int b = visit[k];
             if (b == a || tri_obj[b] != tri_obj[a]) continue;
             bool apart = false;
             for (int k = 0; k < 3; k++) apart |= mn[b][k] > mx[a][k] + g || mx[b][k] < mn[a][k] - g;

@@ -217,7 +217,6 @@ void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) 
         for (int k = 0; k < nobjects; k++)
             for (int i = 0; i < obj_ntris[k] && t < n; i++) tri_obj[t++] = k;
     }
-    tri_info = edge::gen_edge_info(tri, tri_obj);  // RocketSim.cpp:166-170
     // btBvhTriangleMeshShape per object (RocketSim.cpp:167): the order its quantized BVH visits the triangles
     tri_visit.resize(n);
     for (int t0 = 0; t0 < n;) {
@@ -227,6 +226,7 @@ void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) 
         for (int k = 0; k < t1 - t0; k++) tri_visit[t0 + k] = t0 + order[k];
         t0 = t1;
     }
+    tri_info = edge::gen_edge_info(tri, tri_obj, tri_visit);  // RocketSim.cpp:166-170
 }
 
 const World& world() {

@@ -13,8 +13,8 @@
 // identity transform, so the triangle-local frame is the world frame (the reference's basis products
 // with the identity are skipped: they only turn a -0 component into +0).
 // Neighbour order: a triangle's edge info is written by every neighbour that shares the edge, the last
-// one winning; the reference visits neighbours in its quantized BVH's traversal order, here in index
-// order (they differ only on edges shared by three or more triangles).
+// one winning; neighbours are visited in the quantized BVH's traversal order, as the reference does
+// (mesh.hip mesh_edge_info; it matters on edges shared by three or more triangles).
 #pragma once
 #include "dmath.hpp"
 

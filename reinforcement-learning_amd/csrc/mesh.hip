@@ -278,8 +278,9 @@ std::vector<int> bvh_visit_order(const float* tris, int n) {
 }
 
 // btGenerateInternalEdgeInfo per collision object (one btBvhTriangleMeshShape per object, partId 0):
-// for every triangle A, every other triangle B of the object whose AABB overlaps A's, in index order
-// (the reference: the BVH's overlap query, btInternalEdgeUtility.cpp:300-356)
+// for every triangle A, every other triangle B of the object whose AABB overlaps A's, in the order the
+// object's quantized BVH visits them (the reference's overlap query, btInternalEdgeUtility.cpp:300-356:
+// the last neighbour sharing an edge writes A's record)
 std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* object_ntris, int nobjects) {
     std::vector<float> out((size_t)ntris * 4, 0.f);
     auto vert = [&](int t, int k) {
@@ -290,6 +291,7 @@ std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* o
     for (int o = 0; o < nobjects; o++) {
         const int n = object_ntris ? object_ntris[o] : ntris;
         std::vector<rl::v3> mn(n), mx(n);
+        const std::vector<int> visit = bvh_visit_order(tris + (size_t)t0 * 9, n);
         for (int i = 0; i < n; i++) {
             rl::v3 a = vert(t0 + i, 0), b = vert(t0 + i, 1), c = vert(t0 + i, 2);
             mn[i] = rl::v3{std::fmin(a.x, std::fmin(b.x, c.x)), std::fmin(a.y, std::fmin(b.y, c.y)), std::fmin(a.z, std::fmin(b.z, c.z))};
@@ -298,7 +300,8 @@ std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* o
         for (int i = 0; i < n; i++) {
             const rl::v3 va[3] = {vert(t0 + i, 0), vert(t0 + i, 1), vert(t0 + i, 2)};
             rl::EdgeInfo info{rl::kEdge2Pi, rl::kEdge2Pi, rl::kEdge2Pi, 0};
-            for (int j = 0; j < n; j++) {
+            for (int k = 0; k < n; k++) {
+                const int j = visit[k];
                 if (j == i) continue;  // self
                 // AABB overlap grown by 2e-4 (twice the shared-vertex distance): a neighbour whose shared
                 // vertices differ by less than the threshold always passes, as in the BVH's

@@ -222,3 +222,24 @@ def test_bvh_visit_order_known_answers():
     assert list(bvh_order(ArenaMesh([row([0, 10, 20, 30, 40])]))) == [4, 3, 2, 1, 0]
     assert list(bvh_order(ArenaMesh([row([40, 0, 30, 10, 20])]))) == list(oracle.bvh_order(row([40, 0, 30, 10, 20])))
     assert list(bvh_order(ArenaMesh([tri[None]]))) == [0]
+
+
+@pytest.mark.parametrize("perm", [(0, 1, 2), (0, 2, 1), (2, 1, 0)])
+def test_internal_edge_info_bvh_neighbour_order(perm):
+    """An edge shared by three triangles (floor A, its planar continuation B, a wall C): A's record is
+    written by the neighbour the object's BVH query visits last (btInternalEdgeUtility.cpp:340-356),
+    0 for B, +-pi/2 for C -- library and oracle agree for every listing order, and the BVH (built from the
+    geometry) visits C after B in each of them, so the record does not depend on the listing (an index-
+    order walk would give 0 for the (0, 2, 1) listing)."""
+    from rlgpu.mesh import bvh_order, edge_info
+    base = [np.float32([0, 0, 0, 1, 0, 0, 1, 1, 0]),        # A: the edge (1,0,0)-(1,1,0) is its V1V2
+            np.float32([1, 0, 0, 2, 0.5, 0, 1, 1, 0]),      # B: coplanar across the edge
+            np.float32([1, 0, 0, 1, 1, 0, 1, 0.5, 1])]     # C: wall rising from the edge
+    tris = np.stack([base[i] for i in perm])
+    got = edge_info(ArenaMesh([tris]))
+    np.testing.assert_array_equal(got.view(np.uint32), oracle.mesh_edge_info(tris).view(np.uint32))
+    order = list(bvh_order(ArenaMesh([tris])))
+    a, b, c = (perm.index(i) for i in range(3))
+    ang = got[a, 1]
+    assert order.index(c) > order.index(b), order
+    assert abs(abs(ang) - np.pi / 2) < 1e-5, ang
