@@ -15,7 +15,7 @@
  * (rlgpu_reward_spec / rlgpu_terminal_spec lists in rlgpu_envset_config; NULL lists = src/ExampleMain.cpp:
  * 128-226: the 13 weighted rewards and NoTouchCondition(8) + ScoreLimitCondition(3)).
  *
- * Arena state lives on the device as one 2,304-byte record per arena (array of structs: a
+ * Arena state lives on the device as one 2,312-byte record per arena (array of structs: a
  * workgroup stages whole records into LDS with coalesced 16-byte loads, runs the step there and
  * writes them back once, so the record is read and written exactly once per step whatever the
  * access pattern inside -- DESIGN.md section 3); one env step is ONE kernel launch
@@ -180,7 +180,12 @@ typedef struct {
     uint32_t rng_counter;        /* Philox counter for this arena's draws */
     uint32_t manifold_overflow;  /* contacts dropped by a build limit (manifolds, candidates, rows) */
     int32_t episode_steps;       /* steps in the current trajectory (Learner maxEpisodeLength) */
-    int32_t reserved0;
+    /* btRSBroadphase cell-list history (btRSBroadphase.cpp:160-176,284-320), per dynamic body (ball, cars
+     * 1-4): its home cell + 1 (0 = not placed yet) and its rank in the order the bodies last entered their
+     * cells, which is every cell's dynamic-list order (all 0 = creation order, as a fresh arena has) */
+    uint16_t bp_cell[RLGPU_CARS + 1];
+    uint8_t bp_rank[RLGPU_CARS + 1];
+    uint8_t pad1;
 } rlgpu_env_extra;
 
 /* Complete serialised arena (the wire format of rlgpu_envset_get/set_arenas). */

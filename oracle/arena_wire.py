@@ -221,6 +221,8 @@ def _fresh(rec):
         c["ball_hit_extra_tick"] = -1
     rec["ball_vel_impulse_cache"] = 0
     rec["ball_sleeping"] = 0
+    rec["env"]["bp_cell"] = 0  # a new broadphase: cell lists in creation order (btRSBroadphase::createProxy)
+    rec["env"]["bp_rank"] = 0
 
 
 def deserialize(data, rec):

@@ -1582,12 +1582,44 @@ struct Sim {
                         [&](V n, V p, float d) { add_contact(key, n, p, d); });
     }
 
+    // btRSBroadphase's grid (Arena.cpp:466-471 with ArenaConfig.h:20-29, HEAVY; btRSBroadphase.cpp:43-84) and
+    // GetCellIndices (btRSBroadphase.h:90-99): the home cell of a dynamic proxy is the cell of its AABB min
+    int home_cell(V mn) const {
+        const float uu = 1.f / 50.f;
+        const V lo(-4500.f * uu, -6000.f * uu, 0.f * uu), hi(4500.f * uu, 6000.f * uu, 2500.f * uu);
+        const float cs = 370.f * uu * 1.f;
+        const V range = hi - lo;
+        int n[3];
+        for (int a = 0; a < 3; a++) n[a] = std::max(1, (int)std::ceil(range[a] / cs));
+        const V f = (mn - lo) * (1.f / cs);
+        int c[3];
+        for (int a = 0; a < 3; a++) c[a] = std::min(std::max((int)f[a], 0), n[a] - 1);
+        return (c[0] * n[1] + c[1]) * n[2] + c[2];
+    }
+    // The cells' dynamic lists (btRSBroadphase.cpp:160-176, 284-320): setAabb (from updateAabbs, bodies in
+    // creation order) removes a proxy whose home cell changed from the 27 cells around the old one and appends
+    // it to the 27 around the new one, so each list is in the order of the members' last home change --
+    // kept as s.env.bp_rank (all zero: creation order) with s.env.bp_cell = home cell + 1 (0: not placed).
+    int list_key(int bi) const { return s.env.bp_rank[bi] * 8 + bi; }
+    void broadphase_update() {
+        for (int bi = 0; bi < 5; bi++) {
+            V mn, mx;
+            broad_aabb(bi, mn, mx);
+            const int cell = home_cell(mn) + 1;
+            if (cell == s.env.bp_cell[bi]) continue;
+            s.env.bp_cell[bi] = (uint16_t)cell;
+            std::vector<std::pair<int, int>> order;  // (list key, body); bi goes to the end
+            for (int c = 0; c < 5; c++) order.push_back({c == bi ? 1000 : list_key(c), c});
+            std::sort(order.begin(), order.end());
+            for (int r = 0; r < 5; r++) s.env.bp_rank[order[r].second] = (uint8_t)r;
+        }
+    }
     void collision_detection(bool ball_awake) {
         nmf = 0;  // last tick's pairs (and manifolds) were removed by the broadphase
         // the broadphase's pair order (btRSBroadphase.cpp:392-465): per dynamic proxy in creation order
         // (ball, cars 1-4), its static pairs (mesh objects, then the 4 planes; skipped when the body is
         // inactive, needsCollision(inactive, static) == false), then its dynamic pairs with the later
-        // bodies (the cell list's insertion history taken as body order) while the AABBs overlap
+        // bodies, in its home cell's dynamic-list order, while the AABBs overlap
         for (int bi = 0; bi < 5; bi++) {
             bool active = bi == 0 ? ball_awake : b[bi].active;
             if (active) {
@@ -1612,7 +1644,11 @@ struct Sim {
                 }
             }
             const int a = bi;
-            for (int c2 = a + 1; c2 < 5; c2++) {
+            std::vector<std::pair<int, int>> later;  // (list key, body) of the later bodies
+            for (int c = a + 1; c < 5; c++) later.push_back({list_key(c), c});
+            std::sort(later.begin(), later.end());
+            for (const auto& lc : later) {
+                const int c2 = lc.second;
                 int ka = a == 0 ? c2 : a, kb = a == 0 ? 0 : c2;  // the car first for ball pairs
                 int key = KDYN + a * 8 + c2;
                 bool dem = (ka >= 1 && !b[ka].active) || (kb >= 1 && !b[kb].active);
@@ -2013,6 +2049,7 @@ struct Sim {
                 integrate_transform(b[i].pos, b[i].rot, b[i].vel, b[i].ang, TICK_TIME, b[i].pred_pos, b[i].pred_rot);
             }
         }
+        broadphase_update();  // updateAabbs -> btRSBroadphase::setAabb
         // ball island activity: awake if moving, or sharing an island (overlapping broadphase pair)
         bool ball_awake = !ball_sleep;
         if (ball_sleep) {

@@ -172,6 +172,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     sync();
     P.mark(3);
     if (valid && l == 0) {
+        bp_update(A);  // updateAabbs -> btRSBroadphase::setAabb
         bool awake = !A->a.ball_sleep;
         if (!awake) {
             v3 m0, m1;
@@ -613,6 +614,16 @@ static EnvConst make_env_const() {
         impl = with_m - v3{safe, safe, safe};
     }
     k.car_impl = impl;
+    {  // btRSBroadphase(minPos * UU_TO_BT, maxPos * UU_TO_BT, maxAABBLen * UU_TO_BT * 1 (HEAVY)), btRSBroadphase.cpp:43-84
+        const v3 mn = v3{-4500.f * UU, -6000.f * UU, 0.f * UU}, mx = v3{4500.f * UU, 6000.f * UU, 2500.f * UU};
+        const float cell = 370.f * UU * 1.f;
+        const v3 range = mx - mn;
+        k.bp_min = mn;
+        k.bp_inv_cell = 1.f / cell;
+        k.bp_cells[0] = std::max(1, (int)std::ceil(range.x / cell));
+        k.bp_cells[1] = std::max(1, (int)std::ceil(range.y / cell));
+        k.bp_cells[2] = std::max(1, (int)std::ceil(range.z / cell));
+    }
     k.car_half = impl + v3{k.car_margin, k.car_margin, k.car_margin};  // getHalfExtentsWithMargin
     k.car_offset = v3{13.87566f, 0.f, 20.755f} * UU;
     float lx = 2.f * k.car_half.x, ly = 2.f * k.car_half.y, lz = 2.f * k.car_half.z;

@@ -295,12 +295,50 @@ DEV bool refresh(ArenaLDS* A, int key) {
 // (btRSBroadphase.cpp:392-465) walks the dynamic proxies in creation order (ball, then cars 1-4) and adds,
 // for each, its pairs with the cell's static proxies (meshes, then planes: creation order), then its
 // pairs with the cell's other dynamic proxies not paired yet; the pair cache dispatches in that order.
-// Within one proxy's dynamic pairs the cell list's order (insertion history) is taken as body order.
-DEV int commit_rank(int rank) {
+// Within one proxy's dynamic pairs, the order of its home cell's dynamic list (bp_update).
+// btRSBroadphase's cell lists (btRSBroadphase.cpp:90-110,160-176,284-320): a dynamic proxy's home cell is the
+// grid cell of its AABB min and the proxy sits in the 27 cells around it, appended when created and re-appended
+// whenever its home cell changes (setAabb, called by updateAabbs for the bodies in creation order); so every
+// cell lists its dynamic proxies in the order of their last home change.  bp_rank keeps that order per arena.
+DEV int bp_home(v3 mn) {
+    const v3 f = (mn - C.bp_min) * C.bp_inv_cell;  // (pos - minPos) / cellSize = * (1 / cellSize)
+    const int i = min(max((int)f.x, 0), C.bp_cells[0] - 1);
+    const int j = min(max((int)f.y, 0), C.bp_cells[1] - 1);
+    const int k = min(max((int)f.z, 0), C.bp_cells[2] - 1);
+    return (i * C.bp_cells[1] + j) * C.bp_cells[2] + k;
+}
+DEV int bp_key(const ArenaLDS* A, int b) { return A->s.env.bp_rank[b] * 8 + b; }  // list position (ties: creation)
+// one lane per arena, on this tick's broadphase AABBs (after predictUnconstraintMotion)
+DEV void bp_update(ArenaLDS* A) {
+#pragma unroll 1
+    for (int bi = 0; bi < 5; bi++) {
+        v3 mn, mx;
+        broad_aabb(A, bi, mn, mx);
+        const int cell = bp_home(mn) + 1;
+        if (cell == A->s.env.bp_cell[bi]) continue;
+        A->s.env.bp_cell[bi] = (uint16_t)cell;
+        int key[5];
+#pragma unroll
+        for (int c = 0; c < 5; c++) key[c] = c == bi ? 64 : bp_key(A, c);  // bi moves to the lists' end
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            int r = 0;
+#pragma unroll
+            for (int d = 0; d < 5; d++) r += key[d] < key[c];
+            A->s.env.bp_rank[c] = (uint8_t)r;
+        }
+    }
+}
+DEV int commit_rank(const ArenaLDS* A, int rank) {
     if (rank < 25) return (rank / 5) * 9 + rank % 5;  // body * 9 + (0 mesh objects, 1-4 planes)
     int a, b;
     dyn_pair(rank, a, b);
-    return a * 9 + 5 + (b - a - 1);  // body a's pairs with the later bodies
+    // body a's pairs with the later bodies, in its home cell's list order
+    const int kb = bp_key(A, b);
+    int pos = 0;
+#pragma unroll
+    for (int c = 1; c < 5; c++) pos += c > a && bp_key(A, c) < kb;
+    return a * 9 + 5 + pos;
 }
 DEV void emit(ArenaLDS* A, int rank, int tri, int key, v3 n, v3 p, float depth) {
     int slot = atomicAdd(&A->a.ncand, 1);
@@ -309,7 +347,7 @@ DEV void emit(ArenaLDS* A, int rank, int tri, int key, v3 n, v3 p, float depth) 
     c.n[0] = n.x; c.n[1] = n.y; c.n[2] = n.z;
     c.p[0] = p.x; c.p[1] = p.y; c.p[2] = p.z;
     c.depth = depth;
-    c.order = (commit_rank(rank) << 20) | tri;
+    c.order = (commit_rank(A, rank) << 20) | tri;
     c.key = key;
 }
 

@@ -65,6 +65,9 @@ struct EnvConst {
     v3 ball_inv_inertia, car_half, car_offset, car_inv_inertia, gravity;
     v3 car_impl;       // btBoxShape implicit half extents (without the margin)
     float car_margin;  // btBoxShape margin after setSafeMargin
+    v3 bp_min;         // btRSBroadphase grid (Arena.cpp:466-471, ArenaConfig.h:20-29): minPos, 1 / cellSize, cells
+    float bp_inv_cell;
+    int bp_cells[3];
     v3 wheel_conn[4];
     float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
     v3 plane_n[4], plane_p[4];

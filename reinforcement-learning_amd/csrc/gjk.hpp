@@ -942,11 +942,13 @@ GJK_CALLED int epa_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 gue
                     const float bd = S.fc[best].d;
                     getsupport(S, m, bn, w);
                     const float wdist = dot(bn, svw(S, w)) - bd;
+                    GJK_MARK(6);
                     if (wdist > kEpaAccuracy) {
                         for (int j = 0; (j < 3) && valid; ++j) {
                             valid &= expand(S, E, pass, w, S.fc[best].f[j], S.fc[best].e[j], hcf, hff, hnf);
                             if (S.overflow) return 9;
                         }
+                        GJK_MARK(7);
                         if (valid && (hnf >= 3)) {
                             bind(S, hcf, 1, hff, 2);
                             list_remove(S, E.hull, best);
@@ -954,6 +956,7 @@ GJK_CALLED int epa_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 gue
                             stock_push(S, E, best);
                             best = findbest(S, E);
                             copy_face(outer, S.fc[best]);
+                            GJK_MARK(8);
                         } else {
                             E.status = 4;  // InvalidHull
                             break;

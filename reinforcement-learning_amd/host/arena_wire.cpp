@@ -342,7 +342,8 @@ void arena_fields(S& s, A& a) {
 
 // DeserializeNew builds a new arena: what the stream does not carry starts as a new car / ball has
 // it (CarState() and BallHitInfo() defaults, Car / Ball::SetState's cleared impulse caches, new
-// wheels: Car.h:17-100, BallHitInfo.h:11-22, Car.cpp:23-36, Ball.cpp:35-49, Arena.cpp:703-714)
+// wheels: Car.h:17-100, BallHitInfo.h:11-22, Car.cpp:23-36, Ball.cpp:35-49, Arena.cpp:703-714) and
+// a new broadphase's cell lists
 void fresh_engine_state(rlgpu_arena_state& s) {
     for (rlgpu_car& c : s.cars) {
         c.is_supersonic = 0;
@@ -363,6 +364,9 @@ void fresh_engine_state(rlgpu_arena_state& s) {
     }
     std::memset(s.ball_vel_impulse_cache, 0, sizeof s.ball_vel_impulse_cache);
     s.ball_sleeping = 0;
+    // a new broadphase: cell lists in creation order (btRSBroadphase::createProxy)
+    std::memset(s.env.bp_cell, 0, sizeof s.env.bp_cell);
+    std::memset(s.env.bp_rank, 0, sizeof s.env.bp_rank);
 }
 
 void check(int st) {

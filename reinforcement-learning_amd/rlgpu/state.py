@@ -35,7 +35,8 @@ ENV = np.dtype([
     ("pad", "u1", 2), ("prev_action", "<f4", (4, 8)), ("no_touch_time", "<f4"),
     ("score_blue", "<i4"), ("score_orange", "<i4"), ("penalty_blue", "<i4"), ("penalty_orange", "<i4"),
     ("ev_bump", "u1", 4), ("ev_bumped", "u1", 4), ("ev_demo", "u1", 4), ("ev_demoed", "u1", 4),
-    ("rng_counter", "<u4"), ("manifold_overflow", "<u4"), ("episode_steps", "<i4"), ("reserved0", "<i4"),
+    ("rng_counter", "<u4"), ("manifold_overflow", "<u4"), ("episode_steps", "<i4"),
+    ("bp_cell", "<u2", 5), ("bp_rank", "u1", 5), ("pad1", "u1"),
 ], align=True)
 ARENA = np.dtype([("ball", BODY), ("ball_vel_impulse_cache", "<f4", 3), ("ball_sleeping", "<i4"),
                   ("cars", CAR, 4), ("pads", PAD, 34), ("env", ENV)], align=True)

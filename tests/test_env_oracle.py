@@ -194,3 +194,30 @@ def test_oracle_deterministic(seed):
         b.step(act, True)
     assert a.get_arenas().tobytes() == b.get_arenas().tobytes()
     np.testing.assert_array_equal(a.obs, b.obs)
+
+
+def test_broadphase_cell_lists_follow_home_cell_changes():
+    """btRSBroadphase (btRSBroadphase.cpp:160-176,284-320): a body whose home cell changes is re-appended to
+    its cells' dynamic lists, so it moves to the end of the list order (bp_rank) while the others keep theirs;
+    a body that stays in its cell keeps its place.  Cars 1-4 teleport at kickoff, ball stays: creation order."""
+    env = oracle.EnvSet(2, seed=5)
+    noop = np.full(8, 8, np.int32)
+    for _ in range(2):
+        env.step(noop)
+    s = _state(env)
+    for a in range(2):
+        assert sorted(s["env"][a]["bp_rank"]) == [0, 1, 2, 3, 4]
+        assert (s["env"][a]["bp_cell"] > 0).all()
+    before = s.copy()
+    car = s["cars"][0][1]  # body 2
+    car["body"]["pos"][0] += -30.0 if car["body"]["pos"][0] > 0 else 30.0  # bullet units: several cells
+    env.set_arenas(np.frombuffer(s.tobytes(), np.uint8))
+    env.step(noop)
+    t = _state(env)
+    cells0, cells1 = before["env"][0]["bp_cell"], t["env"][0]["bp_cell"]
+    assert cells1[2] != cells0[2]
+    others = [0, 1, 3, 4]
+    np.testing.assert_array_equal(cells1[others], cells0[others])  # nobody else changed cell
+    r0, r1 = before["env"][0]["bp_rank"], t["env"][0]["bp_rank"]
+    assert r1[2] == 4
+    assert list(np.argsort(r1[others])) == list(np.argsort(r0[others]))
