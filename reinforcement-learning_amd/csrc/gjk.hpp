@@ -821,21 +821,30 @@ DEV int findbest(const ScrT<AS>& S, const Epa& E) {
     }
     return minf;
 }
-// EPA::expand (cpp:864-900) as an explicit-stack walk: frame = face | edge << 8 | stage << 10
+// EPA::expand (cpp:864-900) as an explicit-stack walk: frame = face | edge << 8 | stage << 10.  The top
+// frame lives in a register (the stack holds the frames below it), and a frame's face fields are loaded
+// together before they are tested: the walk is a chain of dependent scratch round trips otherwise.  Same
+// visits, same tests, same new faces and the same overflow decisions as the recursion.
 template <int AS>
 GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
-    int sp = 0;
-    S.stack[sp++] = (uint32_t)f0 | ((uint32_t)e0 << 8);
+    const v3 wv = svw(S, w);
+    int sp = 1;
+    uint32_t top = (uint32_t)f0 | ((uint32_t)e0 << 8);  // frame sp - 1
     bool ret = false;
     while (sp > 0) {
-        const uint32_t fr = S.stack[sp - 1];
+        const uint32_t fr = top;
         const int f = (int)(fr & 255u), e = (int)((fr >> 8) & 3u), stage = (int)(fr >> 10);
         const int e1 = e == 2 ? 0 : e + 1, e2 = e == 0 ? 2 : e - 1;
+        bool pop = false;
         if (stage == 0) {
             auto& F = S.fc[f];
-            if (F.pass != (uint8_t)pass) {
-                if ((dot(ldv(F.n), svw(S, w)) - F.d) < -kEpaPlaneEps) {
-                    const int nf = newface(S, E, F.c[e1], F.c[e], w, false);
+            const uint8_t fpass = F.pass;
+            const v3 fn = ldv(F.n);
+            const float fd = F.d;
+            const int ce1 = F.c[e1], ce = F.c[e], nb = F.f[e1], nbe = F.e[e1];
+            if (fpass != (uint8_t)pass) {
+                if ((dot(fn, wv) - fd) < -kEpaPlaneEps) {
+                    const int nf = newface(S, E, ce1, ce, w, false);
                     if (S.overflow) return false;
                     ret = false;
                     if (nf >= 0) {
@@ -848,7 +857,7 @@ GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0
                         ++hnf;
                         ret = true;
                     }
-                    sp--;
+                    pop = true;
                 } else {
                     F.pass = (uint8_t)pass;
                     if (sp >= S.max_stack) {
@@ -856,15 +865,16 @@ GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0
                         return false;
                     }
                     S.stack[sp - 1] = fr | (1u << 10);
-                    S.stack[sp++] = (uint32_t)F.f[e1] | ((uint32_t)F.e[e1] << 8);
+                    sp++;
+                    top = (uint32_t)nb | ((uint32_t)nbe << 8);
                 }
             } else {
                 ret = false;
-                sp--;
+                pop = true;
             }
         } else if (stage == 1) {
             if (!ret) {
-                sp--;
+                pop = true;
             } else {
                 const auto& F = S.fc[f];
                 if (sp >= S.max_stack) {
@@ -872,7 +882,8 @@ GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0
                     return false;
                 }
                 S.stack[sp - 1] = (fr & 1023u) | (2u << 10);
-                S.stack[sp++] = (uint32_t)F.f[e2] | ((uint32_t)F.e[e2] << 8);
+                sp++;
+                top = (uint32_t)F.f[e2] | ((uint32_t)F.e[e2] << 8);
             }
         } else {
             if (ret) {
@@ -880,8 +891,9 @@ GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0
                 E.hull_count--;
                 stock_push(S, E, f);
             }
-            sp--;
+            pop = true;
         }
+        if (pop && --sp > 0) top = S.stack[sp - 1];
     }
     return ret;
 }
