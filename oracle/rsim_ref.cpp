@@ -384,6 +384,33 @@ struct Sim {
     }
 
     // ---------------------------------------------------------------- ray tests
+    // btVector3::setInterpolate3 (btVector3.h:496-520)
+    static V interpolate3(V v0, V v1, float rt) {
+        const float s = 1.f - rt;
+        return V(s * v0.x + rt * v1.x, s * v0.y + rt * v1.y, s * v0.z + rt * v1.z);
+    }
+    // btTriangleRaycastCallback::processTriangle (btRaycastCallback.cpp:35-117), flags 0: the fraction of a
+    // hit inside the triangle (edge tolerance) strictly closer than `best`, else -1; n faces `from`
+    static float ray_triangle(const V& v0, const V& v1, const V& v2, V from, V to, float best, V& n) {
+        const V tn = cross(v1 - v0, v2 - v0);
+        const float dist = dot(v0, tn);
+        const float da = dot(tn, from) - dist;
+        const float db = dot(tn, to) - dist;
+        if (da * db >= 0.f) return -1.f;
+        const float f = da / (da - db);
+        if (!(f < best)) return -1.f;
+        const float tol = len2(tn) * -0.0001f;
+        const V pt = interpolate3(from, to, f);
+        const V v0p = v0 - pt, v1p = v1 - pt;
+        if (!(dot(cross(v0p, v1p), tn) >= tol)) return -1.f;
+        const V v2p = v2 - pt;
+        if (!(dot(cross(v1p, v2p), tn) >= tol)) return -1.f;
+        const V cp2 = cross(v2p, v0p);
+        if (!(dot(cp2, tn) >= tol)) return -1.f;
+        const V u = normalized(tn);  // triangleNormal.normalize()
+        n = da <= 0.f ? -u : u;
+        return f;
+    }
     // Closest hit of segment [from,to] against the world (btCollisionWorld::rayTest +
     // ClosestRayResultCallback), ignoring body `self`.  Returns hit object id:
     // -1 none, 0 ball, 1..4 car, 10 static.  (btDefaultVehicleRaycaster.cpp:32-52)
@@ -392,40 +419,52 @@ struct Sim {
         int obj = -1;
         V nrm;
         V d = to - from;
-        // static planes (btStaticPlaneShape as triangles -> plane intersection)
-        for (int p = 0; p < 4; p++) {
-            float da = dot(w.plane_n[p], from - w.plane_p[p]);
-            float db = dot(w.plane_n[p], to - w.plane_p[p]);
-            if (da * db >= 0.f) continue;
-            float f = da / (da - db);
-            if (f < best) {
-                best = f;
-                obj = 10;
-                nrm = da > 0.f ? w.plane_n[p] : -w.plane_n[p];
-            }
-        }
-        // mesh triangles in BVH visit order (btTriangleRaycastCallback::processTriangle keeps a strictly
-        // closer hit, so the first visited wins a tie)
+        // the ray cell's statics in creation order (btRSBroadphase::rayTest): mesh objects, then planes;
+        // every object keeps a hit only when strictly closer, so the first one wins a tie
+        // mesh triangles in BVH visit order (btBvhTriangleMeshShape::performRaycast)
         for (int k = 0; k < w.ntris; k++) {
             const int t = w.tri_visit[k];
-            const V& v0 = w.tri[(size_t)t * 3];
-            const V& v1 = w.tri[(size_t)t * 3 + 1];
-            const V& v2 = w.tri[(size_t)t * 3 + 2];
-            V tn = cross(v1 - v0, v2 - v0);
-            float dist = dot(v0, tn);
-            float da = dot(tn, from) - dist;
-            float db = dot(tn, to) - dist;
-            if (da * db >= 0.f) continue;
-            float f = da / (da - db);
-            if (f < best) {
-                float tol = len2(tn) * -0.0001f;
-                V pt = from + d * f;
-                V v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
-                if (dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol) {
+            V n;
+            const float f = ray_triangle(w.tri[(size_t)t * 3], w.tri[(size_t)t * 3 + 1], w.tri[(size_t)t * 3 + 2], from, to,
+                                         best, n);
+            if (f >= 0.f) {
+                best = f;
+                obj = 10;
+                nrm = n;
+            }
+        }
+        // static planes: btStaticPlaneShape(normal, 0) at plane_p (identity basis); processAllTriangles
+        // (btStaticPlaneShape.cpp:56-82) spans two triangles over the ray's AABB in the plane's frame
+        for (int p = 0; p < 4; p++) {
+            const V pn = w.plane_n[p], fl = from - w.plane_p[p], tl = to - w.plane_p[p];
+            V amn = fl, amx = fl;
+            for (int a = 0; a < 3; a++) {
+                if (tl[a] < amn[a]) amn[a] = tl[a];  // btSetMin
+                if (amx[a] < tl[a]) amx[a] = tl[a];  // btSetMax
+            }
+            const V he = (amx - amn) * 0.5f;
+            const float radius = std::sqrt(he.x * he.x + he.y * he.y + he.z * he.z);  // length()
+            const V c = (amx + amn) * 0.5f;
+            V t0, t1;
+            if (std::fabs(pn.z) > 0.7071067811865475244008443621048490f) {  // btPlaneSpace1
+                const float a = pn.y * pn.y + pn.z * pn.z, k = 1.f / std::sqrt(a);
+                t0 = V(0.f, -pn.z * k, pn.y * k);
+                t1 = V(a * k, -pn.x * t0.z, pn.x * t0.y);
+            } else {
+                const float a = pn.x * pn.x + pn.y * pn.y, k = 1.f / std::sqrt(a);
+                t0 = V(-pn.y * k, pn.x * k, 0.f);
+                t1 = V(-pn.z * t0.y, pn.z * t0.x, a * k);
+            }
+            const V pc = c - pn * ((pn.x * c.x + pn.y * c.y + pn.z * c.z) - 0.f);
+            const V ta = t0 * radius, tb = t1 * radius;
+            const V tri[2][3] = {{(pc + ta) + tb, (pc + ta) - tb, (pc - ta) - tb}, {(pc - ta) - tb, (pc - ta) + tb, (pc + ta) + tb}};
+            for (int q = 0; q < 2; q++) {
+                V n;
+                const float f = ray_triangle(tri[q][0], tri[q][1], tri[q][2], fl, tl, best, n);
+                if (f >= 0.f) {
                     best = f;
                     obj = 10;
-                    V n = normalized(tn);
-                    nrm = da <= 0.f ? -n : n;
+                    nrm = n;
                 }
             }
         }
@@ -486,7 +525,7 @@ struct Sim {
         }
         if (obj < 0) return -1;
         frac = best;
-        hit_point = from + d * best;  // setInterpolate3
+        hit_point = interpolate3(from, to, best);  // ClosestRayResultCallback: setInterpolate3
         hit_normal = normalized(nrm);
         if (obj >= 1 && obj <= 4 && !b[obj].active) return -1;  // CF_NO_CONTACT_RESPONSE
         return obj;

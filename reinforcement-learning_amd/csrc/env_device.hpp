@@ -204,51 +204,94 @@ DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& 
 }
 
 // ------------------------------------------------------------------ ray cast (btCollisionWorld::rayTest)
+// btVector3::setInterpolate3 (btVector3.h:496-520): (1 - rt) * v0 + rt * v1
+DEV v3 lerp3(v3 v0, v3 v1, float rt) {
+    const float s = 1.f - rt;
+    return v3{s * v0.x + rt * v1.x, s * v0.y + rt * v1.y, s * v0.z + rt * v1.z};
+}
+// btTriangleRaycastCallback::processTriangle (btRaycastCallback.cpp:35-117, ClosestRayResultCallback flags 0):
+// the hit fraction of [from, to] on the triangle when it lies inside (with the edge tolerance) and is
+// closer than `best` (or equal, when `tie`), else -1; n = the unit normal facing `from`
+DEV float ray_tri(v3 v0, v3 v1, v3 v2, v3 from, v3 to, float best, bool tie, v3& n) {
+    const v3 tn = cross(v1 - v0, v2 - v0);
+    const float dist = dot(v0, tn);
+    const float da = dot(tn, from) - dist, db = dot(tn, to) - dist;
+    if (da * db >= 0.f) return -1.f;
+    const float f = da / (da - db);
+    if (!(f < best || (tie && f == best))) return -1.f;
+    const float tol = len2(tn) * -0.0001f;
+    const v3 pt = lerp3(from, to, f);
+    const v3 v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
+    if (!(dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol))
+        return -1.f;
+    const v3 u = normalized(tn);
+    n = da <= 0.f ? -u : u;
+    return f;
+}
+// btPlaneSpace1 (btVector3.h:1266-1294)
+DEV void plane_space1(v3 n, v3& p, v3& q) {
+    if (fabsf(n.z) > 0.7071067811865475244008443621048490f) {
+        const float a = n.y * n.y + n.z * n.z, k = 1.f / sqrtf(a);
+        p = v3{0.f, -n.z * k, n.y * k};
+        q = v3{a * k, -n.x * p.z, n.x * p.y};
+    } else {
+        const float a = n.x * n.x + n.y * n.y, k = 1.f / sqrtf(a);
+        p = v3{-n.y * k, n.x * k, 0.f};
+        q = v3{-n.z * p.y, n.z * p.x, a * k};
+    }
+}
 DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& hit_point, v3& hit_normal) {
     float best = 1.0f;
     int obj = -1;
     v3 nrm = zero3();
     v3 d = to - from;
-    for (int p = 0; p < 4; p++) {
-        float da = dot(C.plane_n[p], from - C.plane_p[p]);
-        float db = dot(C.plane_n[p], to - C.plane_p[p]);
-        if (da * db >= 0.f) continue;
-        float f = da / (da - db);
-        if (f < best) {
-            best = f;
-            obj = 10;
-            nrm = da > 0.f ? C.plane_n[p] : -C.plane_n[p];
-        }
-    }
-    // segment AABB, grown by a margin well above the edge-test tolerance below: a triangle whose
-    // (grown) AABB misses it cannot be hit, so skipping it changes no result
+    // the ray cell's static proxies in creation order (btRSBroadphase::rayTest, btRSBroadphase.cpp:325-336):
+    // the mesh objects, then the planes, then the dynamic bodies; each object keeps a hit only when strictly
+    // closer than the best so far (btTriangleRaycastCallback, the convex casts), so the first one wins a tie.
+    // Mesh: segment AABB grown by a margin well above the edge-test tolerance (a triangle whose grown AABB
+    // misses it cannot be hit); ties in f go to the lower triangle index = the earlier BVH visit position
     const float kRayCull = 0.1f;
     const v3 smin = v3{fminf(from.x, to.x) - kRayCull, fminf(from.y, to.y) - kRayCull, fminf(from.z, to.z) - kRayCull};
     const v3 smax = v3{fmaxf(from.x, to.x) + kRayCull, fmaxf(from.y, to.y) + kRayCull, fmaxf(from.z, to.z) + kRayCull};
-    // closest hit over the mesh = the first minimum of the reference's walk (btTriangleRaycastCallback keeps
-    // a hit only when strictly closer): ties in f go to the lower triangle index = the earlier BVH visit
-    // position (mesh.hpp), and a plane hit at the same f is kept
     int best_t = -1;
     grid_query(M, smin, smax, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int) {
-        v3 tn = cross(v1 - v0, v2 - v0);
-        float dist = dot(v0, tn);
-        float da = dot(tn, from) - dist;
-        float db = dot(tn, to) - dist;
-        if (da * db >= 0.f) return;
-        float f = da / (da - db);
-        if (f < best || (f == best && best_t >= 0 && t < best_t)) {
-            float tol = len2(tn) * -0.0001f;
-            v3 pt = from + d * f;
-            v3 v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
-            if (dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol) {
-                best = f;
-                best_t = t;
-                obj = 10;
-                v3 n = normalized(tn);
-                nrm = da <= 0.f ? -n : n;
-            }
-        }
+        v3 n;
+        const float f = ray_tri(v0, v1, v2, from, to, best, best_t >= 0 && t < best_t, n);
+        if (f < 0.f) return;
+        best = f;
+        best_t = t;
+        obj = 10;
+        nrm = n;
     });
+    // planes: btStaticPlaneShape (normal, constant 0) at plane_p with the identity basis; the ray in its frame
+    // (x - plane_p) gives the AABB from which processAllTriangles (btStaticPlaneShape.cpp:56-82) builds two
+    // triangles, each through processTriangle
+    for (int p = 0; p < 4; p++) {
+        const v3 pn = C.plane_n[p], fl = from - C.plane_p[p], tl = to - C.plane_p[p];
+        const v3 amn = v3{tl.x < fl.x ? tl.x : fl.x, tl.y < fl.y ? tl.y : fl.y, tl.z < fl.z ? tl.z : fl.z};
+        const v3 amx = v3{fl.x < tl.x ? tl.x : fl.x, fl.y < tl.y ? tl.y : fl.y, fl.z < tl.z ? tl.z : fl.z};
+        const v3 he = (amx - amn) * 0.5f;
+        const float radius = sqrtf(he.x * he.x + he.y * he.y + he.z * he.z);
+        const v3 c = (amx + amn) * 0.5f;
+        v3 t0, t1;
+        plane_space1(pn, t0, t1);
+        const v3 pc = c - pn * ((pn.x * c.x + pn.y * c.y + pn.z * c.z) - 0.f);
+        const v3 ta = t0 * radius, tb = t1 * radius;
+        const v3 ppp = (pc + ta) + tb, ppm = (pc + ta) - tb, pmm = (pc - ta) - tb, pmp = (pc - ta) + tb;
+        v3 n;
+        float f = ray_tri(ppp, ppm, pmm, fl, tl, best, false, n);
+        if (f >= 0.f) {
+            best = f;
+            obj = 10;
+            nrm = n;
+        }
+        f = ray_tri(pmm, pmp, ppp, fl, tl, best, false, n);
+        if (f >= 0.f) {
+            best = f;
+            obj = 10;
+            nrm = n;
+        }
+    }
     {
         v3 bp = bpos(A, 0);
         v3 oc = from - bp;
@@ -307,8 +350,8 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
         }
     }
     if (obj < 0) return -1;
-    hit_point = from + d * best;
-    hit_normal = normalized(nrm);
+    hit_point = lerp3(from, to, best);  // ClosestRayResultCallback::addSingleResult
+    hit_normal = normalized(nrm);       // btDefaultVehicleRaycaster::castRay
     if (obj >= 1 && obj <= 4 && !A->a.active[obj]) return -1;
     return obj;
 }
