@@ -659,6 +659,13 @@ static EnvConst make_env_const() {
     k.plane_p[2] = v3{-4096, 0, 2048 / 2} * UU;
     k.plane_n[3] = v3{-1, 0, 0};
     k.plane_p[3] = v3{4096, 0, 2048 / 2} * UU;
+    for (int p = 0; p < 4; p++) {
+        const v3 n = k.plane_n[p];
+        k.plane_axis[p] = -1;
+        if (std::fabs(n.x) == 1.f && n.y == 0.f && n.z == 0.f) k.plane_axis[p] = 0;
+        if (n.x == 0.f && std::fabs(n.y) == 1.f && n.z == 0.f) k.plane_axis[p] = 1;
+        if (n.x == 0.f && n.y == 0.f && std::fabs(n.z) == 1.f) k.plane_axis[p] = 2;
+    }
     const float sx[5] = {-2048, 2048, -256, 256, 0}, sy[5] = {-2560, -2560, -3840, -3840, -4608};
     const float syaw[5] = {(float)(M_PI_4 * 1), (float)(M_PI_4 * 3), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2), (float)(M_PI_4 * 2)};
     for (int i = 0; i < 5; i++) {  // RLConst.h:297-303, orange mirrored (Arena.cpp:183-186)

@@ -268,6 +268,14 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
     // triangles, each through processTriangle
     for (int p = 0; p < 4; p++) {
         const v3 pn = C.plane_n[p], fl = from - C.plane_p[p], tl = to - C.plane_p[p];
+        // an axis plane's triangles lie exactly in the plane (the normal coordinate of every vertex is 0, the
+        // normal is +-C e_k), so processTriangle's dist_a / dist_b are C * fl_k / C * tl_k: unless fl_k and
+        // tl_k have strictly opposite signs, dist_a * dist_b >= 0 and neither triangle can be hit
+        const int ax = C.plane_axis[p];
+        if (ax >= 0) {
+            const float a = comp(fl, ax), b = comp(tl, ax);
+            if (!((a < 0.f && b > 0.f) || (a > 0.f && b < 0.f))) continue;
+        }
         const v3 amn = v3{tl.x < fl.x ? tl.x : fl.x, tl.y < fl.y ? tl.y : fl.y, tl.z < fl.z ? tl.z : fl.z};
         const v3 amx = v3{fl.x < tl.x ? tl.x : fl.x, fl.y < tl.y ? tl.y : fl.y, fl.z < tl.z ? tl.z : fl.z};
         const v3 he = (amx - amn) * 0.5f;

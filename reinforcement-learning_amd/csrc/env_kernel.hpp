@@ -71,6 +71,7 @@ struct EnvConst {
     v3 wheel_conn[4];
     float wheel_rest[4], wheel_radius[4], wheel_force_scale[4];
     v3 plane_n[4], plane_p[4];
+    int plane_axis[4];  // k when plane_n[p] is the unit axis +-e_k, else -1 (ray_cast's side test)
     float kick_x[5], kick_y[5];
     m3 kick_rot[2][5];
     float respawn_x[4], respawn_y[4];
