@@ -28,6 +28,7 @@
 #define RLGPU_ENV_H
 
 #include <stdint.h>
+#include "rlgpu_arith.h"
 #include "rlgpu_core.h"
 
 #ifdef __cplusplus
@@ -226,6 +227,10 @@ typedef struct {
     int32_t n_rewards;
     const rlgpu_terminal_spec* terminals;
     int32_t n_terminals;
+    /* The reference build whose Bullet arithmetic the step follows (RLGPU_ARITH_*, include/rlgpu_arith.h):
+     * 0 = RLGPU_ARITH_MSVC_X64, the reference's own build (build.ps1); RLGPU_ARITH_GCC_X64; RLGPU_ARITH_SCALAR.
+     * The x86 modes read this host's rsqrtss table at create (RLGPU_ERR_UNSUPPORTED on a host without one). */
+    int32_t arith;
 } rlgpu_envset_config;
 
 /* Experience-append destinations of the fused step (Learner.cpp:823-861); any may be NULL. */

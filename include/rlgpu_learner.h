@@ -96,6 +96,8 @@ typedef struct {
     int32_t experience_capacity;   /* mode 1: store rows (steps kept per player); 0 = maxEpisodeLength +
                                       2 * ceil(ts_per_itr / players) + 64.  Collection also stops when
                                       the store would overwrite a live step (documented divergence). */
+    int32_t arith;                 /* rlgpu_envset_config.arith: the reference build's Bullet arithmetic
+                                      (include/rlgpu_arith.h; 0 = build.ps1's MSVC x64) */
 } rlgpu_learner_config;
 
 enum { RLGPU_EXP_ROLLOUT = 0, RLGPU_EXP_TRAJECTORIES = 1 };

@@ -15,6 +15,7 @@
 #define RLGPU_MESH_H
 
 #include <stdint.h>
+#include "rlgpu_arith.h"
 #include "rlgpu_core.h"
 
 #ifdef __cplusplus
@@ -43,8 +44,11 @@ int rlgpu_mesh_known_hash(int32_t game_mode, uint32_t hash);
  * callback, Arena.cpp:275-279).  tris / object_ntris as rlgpu_envset_config.mesh_* (object_ntris NULL:
  * one object).  out: ntris x 4 floats = m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle (2 pi = no
  * neighbour) and the flags as int32 bits (TRI_INFO_* convex 1/2/4, swap 8/16/32; bit 30 = the triangle
- * has a record, 0 = none).  Host only. */
-int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects, float* out);
+ * has a record, 0 = none).  arith: the RLGPU_ARITH_* mode the records are built in (the connectivity
+ * processor normalises with btVector3::normalize and rotates with quatRotate, btInternalEdgeUtility.cpp:
+ * 159-271, whose arithmetic is the build's, include/rlgpu_arith.h).  Host only. */
+int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects, int32_t arith,
+                         float* out);
 
 /* The order in which the reference's per-object quantized BVH (btBvhTriangleMeshShape with quantized
  * AABB compression, RocketSim.cpp:167; btOptimizedBvh::build, btOptimizedBvh.cpp:28-160, and
@@ -64,9 +68,10 @@ int rlgpu_mesh_bvh_order(const float* tris, int32_t ntris, const int32_t* object
  * point xyz, depth} (the arguments of btManifoldResult::addContactPoint; zeros when no point).
  * lds_first != 0: the penetration solver first runs in a small LDS work set per lane (24 support
  * vertices, 28 live faces), rerun in the lane's HBM set when it overflows -- the env kernel's policy;
- * 0: HBM only.  Asynchronous on `stream`; the HBM sets are allocated per call. */
+ * 0: HBM only.  arith: RLGPU_ARITH_* (the normalisations follow that build, include/rlgpu_arith.h).
+ * Asynchronous on `stream`; the HBM sets are allocated per call. */
 int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
-                               const float* d_cbt, float* d_out, int32_t lds_first, void* stream);
+                               const float* d_cbt, float* d_out, int32_t lds_first, int32_t arith, void* stream);
 
 /* The car-vs-car hitbox narrowphase of the env kernel on its own (btBoxBoxDetector::getClosestPoints ->
  * dBoxBox2, btBoxBoxDetector.cpp:267-767), on the device, one query per lane: n queries of device arrays

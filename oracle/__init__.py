@@ -79,11 +79,13 @@ class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0,
-                 mesh=None, rewards=None, terminals=None):
+                 mesh=None, rewards=None, terminals=None, arith=0):
         """mesh: (tris [N, 9] float32 bullet units, object_ntris int32 [K]) or an object with
         .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh.
         rewards / terminals: structured arrays of rlgpu_reward_spec / rlgpu_terminal_spec records
-        (include/rlgpu_env.h), None = ExampleMain's lists (the oracle restates them itself)."""
+        (include/rlgpu_env.h), None = ExampleMain's lists (the oracle restates them itself).
+        arith: the reference build's Bullet arithmetic (include/rlgpu_arith.h: 0 MSVC x64, 1 GCC x86-64,
+        2 scalar)."""
         L = lib()
         L.oracle_env_create.restype = ctypes.c_void_p
         L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -101,6 +103,8 @@ class EnvSet:
         L.oracle_env_set_max_episode_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.oracle_env_read_traj_terms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_env_set_max_episode_steps(self.h, max_episode_steps)
+        L.oracle_env_set_arith.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_env_set_arith(self.h, int(arith))
         if mesh is not None:
             tris, objs = (mesh.tris, mesh.object_ntris) if hasattr(mesh, "tris") else mesh
             self._mesh = (np.ascontiguousarray(tris, np.float32).reshape(-1, 9), np.ascontiguousarray(objs, np.int32))
@@ -218,7 +222,7 @@ def detmath_exp_log(x):
     return ex, lg
 
 
-def mesh_edge_info(tris, object_ntris=None):
+def mesh_edge_info(tris, object_ntris=None, arith=0):
     """oracle_mesh_edge_info: btGenerateInternalEdgeInfo restated (edge_ref.hpp) -> [ntris, 4] float32
     (m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle, flags bits | 1 << 30 with a record)."""
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
@@ -226,8 +230,8 @@ def mesh_edge_info(tris, object_ntris=None):
     out = np.zeros((len(tris), 4), np.float32)
     f = lib().oracle_mesh_edge_info
     f.restype = None
-    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
-    f(_p(tris), len(tris), _p(objs), 0 if objs is None else len(objs), _p(out))
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    f(_p(tris), len(tris), _p(objs), 0 if objs is None else len(objs), int(arith), _p(out))
     return out
 
 
@@ -242,7 +246,7 @@ def car_box_shape():
     return impl, float(m[0]), half
 
 
-def box_triangle(rot, centre, tri, cbt):
+def box_triangle(rot, centre, tri, cbt, arith=0):
     """oracle_box_triangle (gjk_ref.hpp): n car-hitbox vs triangle queries as Bullet runs them (normal
     early out, GJK with margins, GJK/EPA penetration solver, normal fix).  rot [n,3,3] rows, centre [n,3],
     tri [n,3,3], cbt [n] -> (out [n,8] = hit, normal, point, depth; counts [2] = GJK queries, penetration-
@@ -256,8 +260,8 @@ def box_triangle(rot, centre, tri, cbt):
     counts = np.zeros(2, np.uint64)
     f = lib().oracle_box_triangle
     f.restype = None
-    f.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 6
-    f(n, _p(rot), _p(centre), _p(tri), _p(cbt), _p(out), _p(counts))
+    f.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 6 + [ctypes.c_int]
+    f(n, _p(rot), _p(centre), _p(tri), _p(cbt), _p(out), _p(counts), int(arith))
     return out, counts
 
 
@@ -307,4 +311,55 @@ def bvh_order(tris, object_ntris=None):
             f(_p(part), c, _p(o))
             out[t0:t0 + c] = o + t0
         t0 += c
+    return out
+
+
+# ------------------------------------------------------------------ x86 arithmetic (rsim_math.hpp)
+def rsqrtss(x):
+    """This host's rsqrtss instruction over an array (btVector3::normalize's estimate)."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    f = lib().oracle_rsqrtss
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    f(_p(x), x.size, _p(out))
+    return out
+
+
+def has_sse41_fma3():
+    return bool(lib().oracle_has_sse41_fma3())
+
+
+def dpps(a, b, restated=False):
+    """_mm_dp_ps(a, b, 0x7f) on [n, 3] rows (the instruction), or its restatement (x + y) + (z + 0)."""
+    a = np.ascontiguousarray(a, np.float32).reshape(-1, 3)
+    b = np.ascontiguousarray(b, np.float32).reshape(-1, 3)
+    out = np.empty(len(a), np.float32)
+    f = lib().oracle_dpps_restated if restated else lib().oracle_dpps
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int64, ctypes.c_void_p]
+    f(_p(a), _p(b), len(a), _p(out))
+    return out
+
+
+def fmadd(a, b, c, restated=False):
+    """_mm_fmadd_ss (the instruction) or std::fma over arrays."""
+    a, b, c = (np.ascontiguousarray(v, np.float32) for v in (a, b, c))
+    out = np.empty_like(a)
+    f = lib().oracle_fma_restated if restated else lib().oracle_fmadd
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p]
+    f(_p(a), _p(b), _p(c), a.size, _p(out))
+    return out
+
+
+def linear_math(op, arith, inp):
+    """oracle_linear_math: the mode-dependent LinearMath operation `op` (0 normalize, 1 setRotation,
+    2 getRotation, 3 quaternion product, 4 integrateTransform) on rows of 24 floats -> [n, 12]."""
+    inp = np.ascontiguousarray(inp, np.float32).reshape(-1, 24)
+    out = np.zeros((len(inp), 12), np.float32)
+    f = lib().oracle_linear_math
+    f.restype = None
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    f(int(op), int(arith), _p(inp), len(inp), _p(out))
     return out

@@ -40,7 +40,7 @@ inline float get_angle(V edgeA, V normalA, V normalB) {  // btGetAngle
     return rs_atan2f(dot(normalB, edgeA), dot(normalB, normalA));
 }
 inline V calc_normal(V a, V b, V c) {  // btTriangleShape::calcNormal
-    return normalized(cross(b - a, c - a));
+    return bt_normalize(cross(b - a, c - a));
 }
 inline V quat_rotate(Q r, V w) {  // quatRotate: (r * w) *= r.inverse()
     Q q{r.w * w.x + r.y * w.z - r.z * w.y, r.w * w.y + r.z * w.x - r.x * w.z, r.w * w.z + r.x * w.y - r.y * w.x,
@@ -88,13 +88,13 @@ inline void process_triangle(const V* A, const V* B, TriInfo& info) {
     int otherIndexB = 3 - (sharedVertsB[0] + sharedVertsB[1]);
     V normalA = calc_normal(A[0], A[1], A[2]);
     V normalB = calc_normal(B[sharedVertsB[1]], B[sharedVertsB[0]], B[otherIndexB]);
-    edgeVec = normalized(edgeVec);
-    V edgeCrossA = normalized(cross(edgeVec, normalA));
+    edgeVec = bt_normalize(edgeVec);
+    V edgeCrossA = bt_normalize(cross(edgeVec, normalA));
     {
         V tmp = A[otherIndexA] - A[sharedVertsA[0]];
         if (dot(edgeCrossA, tmp) < 0) edgeCrossA *= -1;
     }
-    V edgeCrossB = normalized(cross(edgeVec, normalB));
+    V edgeCrossB = bt_normalize(cross(edgeVec, normalB));
     {
         V tmp = B[otherIndexB] - B[sharedVertsB[0]];
         if (dot(edgeCrossB, tmp) < 0) edgeCrossB *= -1;
@@ -106,8 +106,8 @@ inline void process_triangle(const V* A, const V* B, TriInfo& info) {
     if (len2e < PLANAR_EPS) {
         // angle2 = ang4 = 0
     } else {
-        calculatedEdge = normalized(calculatedEdge);
-        V calculatedNormalA = normalized(cross(calculatedEdge, edgeCrossA));
+        calculatedEdge = bt_normalize(calculatedEdge);
+        V calculatedNormalA = bt_normalize(cross(calculatedEdge, edgeCrossA));
         float angle2 = get_angle(calculatedNormalA, edgeCrossA, edgeCrossB);
         float ang4 = PI - angle2;
         float dotA = dot(normalA, edgeCrossB);
@@ -180,7 +180,7 @@ inline V nearest_point_in_line_segment(V point, V line0, V line1) {
 }
 
 inline bool clamp_normal(V edgeV, V tri_normal, V localContactNormalOnB, float correctedEdgeAngle, V& clamped) {
-    V edgeCross = normalized(cross(edgeV, tri_normal));
+    V edgeCross = bt_normalize(cross(edgeV, tri_normal));
     float curAngle = get_angle(edgeCross, tri_normal, localContactNormalOnB);
     if (correctedEdgeAngle < 0) {
         if (curAngle < correctedEdgeAngle) {
@@ -210,7 +210,7 @@ inline void adjust_edge(const V* tv, const TriInfo& info, V& n, V& localB, V pos
     V contact = localB;
     bool isNearEdge = false;
     int numConcaveEdgeHits = 0;
-    V localContactNormalOnB = normalized(n);
+    V localContactNormalOnB = bt_normalize(n);
     int bestedge = -1;
     float disttobestedge = 1e18f;  // BT_LARGE_FLOAT
     if (std::fabs(info.e01) < MAX_EDGE_ANGLE) {

@@ -677,20 +677,37 @@ struct EnvSet {
     int max_episode_steps = 0;
     Plugins plug = example_main_plugins();
     Pool* pool = nullptr;
+    int arith = RLGPU_ARITH_MSVC_X64;  // the reference build's arithmetic (oracle_env_set_arith)
     World* own_world = nullptr;     // set by oracle_env_set_mesh
-    const World* w = &world();
+    std::vector<float> mesh_tris;   // its mesh, rebuilt when the arithmetic changes
+    std::vector<int> mesh_obj;
+    const World* w = &world(RLGPU_ARITH_MSVC_X64);
     ~EnvSet() {
         delete pool;
         delete own_world;
     }
     void par(std::function<void(int)> f) {
         if (!pool) {
+            ArithScope scope(arith);
             for (int i = 0; i < n; i++) f(i);
             return;
         }
         pool->run(n, [&](int b0, int b1) {
+            ArithScope scope(arith);
             for (int i = b0; i < b1; i++) f(i);
         });
+    }
+    void rebuild_world() {
+        delete own_world;
+        own_world = nullptr;
+        if (mesh_tris.empty()) {
+            w = &world(arith);
+            return;
+        }
+        own_world = new World(arith);
+        own_world->set_mesh(mesh_tris.data(), (int)(mesh_tris.size() / 9), mesh_obj.empty() ? nullptr : mesh_obj.data(),
+                            (int)mesh_obj.size());
+        w = own_world;
     }
     StepOut out(int i) {
         return {&obs[(size_t)i * 4 * RLGPU_OBS], &masks[(size_t)i * 4 * RLGPU_ACTIONS], &rewards[(size_t)i * 4], &terminals[i],
@@ -824,8 +841,8 @@ void oracle_env_set_plugins(void* h, const rlgpu_reward_spec* rw, int nr, const 
 // units), object k owns the next obj_ntris[k] triangles (obj_ntris NULL: one object).
 // internal-edge records of a mesh (btGenerateInternalEdgeInfo restated, edge_ref.hpp): ntris x 4 floats
 // (3 angles, flags bits | 1 << 30 when the triangle has a record), the library's rlgpu_mesh_edge_info layout
-void oracle_mesh_edge_info(const float* tris, int ntris, const int* obj_ntris, int nobj, float* out) {
-    World wd;
+void oracle_mesh_edge_info(const float* tris, int ntris, const int* obj_ntris, int nobj, int arith, float* out) {
+    World wd(arith);
     wd.set_mesh(tris, ntris, obj_ntris, nobj);
     for (int t = 0; t < ntris; t++) {
         const TriInfo& ti = wd.tri_info[t];
@@ -839,10 +856,18 @@ void oracle_mesh_edge_info(const float* tris, int ntris, const int* obj_ntris, i
 
 void oracle_env_set_mesh(void* h, const float* tris, int ntris, const int* obj_ntris, int nobj) {
     EnvSet* e = (EnvSet*)h;
-    delete e->own_world;
-    e->own_world = new World();
-    e->own_world->set_mesh(tris, ntris, obj_ntris, nobj);
-    e->w = e->own_world;
+    e->mesh_tris.assign(tris, tris + (size_t)ntris * 9);
+    if (obj_ntris) e->mesh_obj.assign(obj_ntris, obj_ntris + nobj);
+    else e->mesh_obj.clear();
+    e->rebuild_world();
+}
+
+// The reference build's arithmetic (RLGPU_ARITH_*, include/rlgpu_arith.h) for every later step; the set's
+// edge records are rebuilt in it.
+void oracle_env_set_arith(void* h, int arith) {
+    EnvSet* e = (EnvSet*)h;
+    e->arith = arith;
+    e->rebuild_world();
 }
 
 void oracle_env_read_traj_terms(void* h, int8_t* out) {

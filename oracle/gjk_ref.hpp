@@ -51,7 +51,7 @@ inline M transpose_times(const M& a, const M& m) {
     return r;
 }
 inline int max_axis(V d) { return d.x < d.y ? (d.y < d.z ? 2 : 1) : (d.x < d.z ? 2 : 0); }  // btVector3::maxAxis
-inline V normalize(V a) { return a * (1.f / std::sqrt(len2(a))); }  // btVector3::normalize
+inline V normalize(V a) { return bt_normalize(a); }  // btVector3::normalize (rsim_math.hpp: rsqrtss + Newton in the x86 builds)
 
 struct Shapes {
     V impl;       // box half extents without margin (m_implicitShapeDimensions)

@@ -8,7 +8,8 @@
 //                          .../Sim/BoostPad/BoostPadGrid/BoostPadGrid.cpp:5-25
 //   contact callbacks      Arena.cpp:218-427
 //   Bullet subset          btDiscreteDynamicsWorld.cpp:325-437, btRigidBody.cpp:95-420,
-//                          btSequentialImpulseConstraintSolver.cpp:440-1900 (scalar path),
+//                          btSequentialImpulseConstraintSolver.cpp:440-1900 (the row functions and the
+//                          LinearMath branches of the build selected by g_arith, rsim_math.hpp),
 //                          btPersistentManifold.cpp:100-330, btManifoldResult.cpp:110-200,
 //                          SphereTriangleDetector.cpp:88-240, btSphereBoxCollisionAlgorithm.cpp,
 //                          btConvexPlaneCollisionAlgorithm.cpp:53-90, btContactConstraint.cpp:60-150
@@ -87,7 +88,7 @@ const Curve BUMP_VEL_AMOUNT_AIR = {3, {0, 1400, 2200}, {5.f / 6.f, 1390.f, 1945.
 const Curve BUMP_UPWARD_VEL_AMOUNT = {3, {0, 1400, 2200}, {2.f / 6.f, 278.f, 417.f}};
 
 // -------------------------------------------------------------------- static world
-World::World() {
+World::World(int arith_) : arith(arith_) {
     ball_radius = BALL_RADIUS_UU * UU_TO_BT;
     // btSphereShape::calculateLocalInertia (btSphereShape.cpp:61-65)
     float elem = 0.4f * BALL_MASS * ball_radius * ball_radius;
@@ -226,12 +227,13 @@ void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) 
         for (int k = 0; k < t1 - t0; k++) tri_visit[t0 + k] = t0 + order[k];
         t0 = t1;
     }
+    ArithScope scope(arith);
     tri_info = edge::gen_edge_info(tri, tri_obj, tri_visit);  // RocketSim.cpp:166-170
 }
 
-const World& world() {
-    static World w;
-    return w;
+const World& world(int arith) {
+    static const World w0(RLGPU_ARITH_MSVC_X64), w1(RLGPU_ARITH_GCC_X64), w2(RLGPU_ARITH_SCALAR);
+    return arith == RLGPU_ARITH_SCALAR ? w2 : (arith == RLGPU_ARITH_GCC_X64 ? w1 : w0);
 }
 
 // ------------------------------------------------------------------ Philox 4x32-10
@@ -407,7 +409,7 @@ struct Sim {
         if (!(dot(cross(v1p, v2p), tn) >= tol)) return -1.f;
         const V cp2 = cross(v2p, v0p);
         if (!(dot(cp2, tn) >= tol)) return -1.f;
-        const V u = normalized(tn);  // triangleNormal.normalize()
+        const V u = bt_normalize(tn);  // triangleNormal.normalize()
         n = da <= 0.f ? -u : u;
         return f;
     }
@@ -479,7 +481,7 @@ struct Sim {
                     if (f >= 0.f && f < best) {
                         best = f;
                         obj = 0;
-                        nrm = normalized((from + d * f) - b[0].pos);
+                        nrm = bt_normalize((from + d * f) - b[0].pos);
                     }
                 }
             }
@@ -526,7 +528,7 @@ struct Sim {
         if (obj < 0) return -1;
         frac = best;
         hit_point = interpolate3(from, to, best);  // ClosestRayResultCallback: setInterpolate3
-        hit_normal = normalized(nrm);
+        hit_normal = bt_normalize(nrm);
         if (obj >= 1 && obj <= 4 && !b[obj].active) return -1;  // CF_NO_CONTACT_RESPONSE
         return obj;
     }
@@ -1483,7 +1485,7 @@ struct Sim {
         if (!(d2 < rwt * rwt)) return false;
         if (d2 > SIMD_EPSILON) {
             float d = std::sqrt(d2);
-            normal_out = normalized(c2c);
+            normal_out = bt_normalize(c2c);
             point = cp;
             depth = -(radius - d);
         } else {
@@ -1951,42 +1953,89 @@ struct Sim {
             add_friction(i, 5, tmp, rel1, rel2, cidx, tmp.friction);
         }
 
+        // The row functions the reference build selects (setupSolverFunctions, btSequentialImpulseConstraintSolver.cpp:
+        // 359-382): _scalar_reference (:46-100, 283-313) without SSE; _sse2 (:149-177, 207-233, 315-350) on x86;
+        // MSVC on an SSE4.1 + FMA3 CPU replaces the contact and friction rows by _sse4_1_fma3 (:180-205, 235-260).
+        // The dots: btSimdDot3 x + (y + z) (:106-110) in _sse2, _mm_dp_ps(.., 0x7f) = (x + y) + (z + 0) in
+        // _sse4_1_fma3, btVector3::dot (x + y) + z in the scalar rows.
+        const int ar = g_arith;
+        auto rdot = [](V a, V b, int how) {
+            const float x = a.x * b.x, y = a.y * b.y, z = a.z * b.z;
+            if (how == 1) return x + (y + z);
+            if (how == 2) return (x + y) + (z + 0.f);
+            return (x + y) + z;
+        };
         auto resolve_lower = [&](Row& c, bool generic) {
             SBody& A = sb[c.a];
             SBody& B = sb[c.bb];
+            const bool fma3 = ar == RLGPU_ARITH_MSVC_X64;
+            const int how = fma3 ? 2 : (ar == RLGPU_ARITH_GCC_X64 ? 1 : 0);
             float di = c.rhs - c.applied * c.cfm;
-            float dv1 = dot(c.n1, A.dlin) + dot(c.rc1, A.dang);
-            float dv2 = dot(c.n2, B.dlin) + dot(c.rc2, B.dang);
-            di -= dv1 * c.jinv;
-            di -= dv2 * c.jinv;
-            float sum = c.applied + di;
-            if (sum < c.lower) {
-                di = c.lower - c.applied;
+            float dv1 = rdot(c.n1, A.dlin, how) + rdot(c.rc1, A.dang, how);
+            float dv2 = rdot(c.n2, B.dlin, how) + rdot(c.rc2, B.dang, how);
+            if (fma3) {  // FMNADD(deltaVelDotn, jacDiagABInv, deltaImpulse) = -(a * b) + c, one rounding
+                di = std::fma(-dv1, c.jinv, di);
+                di = std::fma(-dv2, c.jinv, di);
+            } else {
+                di -= dv1 * c.jinv;
+                di -= dv2 * c.jinv;
+            }
+            const float applied = c.applied, sum = applied + di;
+            if (fma3) {
+                // masks sum > lower and upper > sum; _mm_blendv_ps keeps the in-range values
+                const bool above = sum > c.lower, below = !generic || c.upper > sum;
+                di = above ? (below ? di : c.upper - applied) : c.lower - applied;
+                c.applied = above ? (below ? sum : c.upper) : c.lower;
+            } else if (ar == RLGPU_ARITH_GCC_X64) {
+                // resultLowerLess = sum < lower, resultUpperLess = sum < upper, applied as and / andnot selects
+                const bool low = sum < c.lower;
+                float d = low ? c.lower - applied : di, ap = low ? c.lower : sum;
+                if (generic && !(sum < c.upper)) {
+                    d = c.upper - applied;
+                    ap = c.upper;
+                }
+                di = d;
+                c.applied = ap;
+            } else if (sum < c.lower) {
+                di = c.lower - applied;
                 c.applied = c.lower;
             } else if (generic && sum > c.upper) {
-                di = c.upper - c.applied;
+                di = c.upper - applied;
                 c.applied = c.upper;
             } else {
                 c.applied = sum;
             }
-            if (A.real) {
-                A.dlin += c.n1 * A.inv_mass * di;
-                A.dang += c.angA * di;
+            if (fma3) {  // FMADD(n * invMass, deltaImpulse, deltaLinearVelocity), FMADD(angularComponent, ...)
+                if (A.real) {
+                    const V la = c.n1 * A.inv_mass;
+                    A.dlin = V(std::fma(la.x, di, A.dlin.x), std::fma(la.y, di, A.dlin.y), std::fma(la.z, di, A.dlin.z));
+                    A.dang = V(std::fma(c.angA.x, di, A.dang.x), std::fma(c.angA.y, di, A.dang.y), std::fma(c.angA.z, di, A.dang.z));
+                }
+                if (B.real) {
+                    const V lb = c.n2 * B.inv_mass;
+                    B.dlin = V(std::fma(lb.x, di, B.dlin.x), std::fma(lb.y, di, B.dlin.y), std::fma(lb.z, di, B.dlin.z));
+                    B.dang = V(std::fma(c.angB.x, di, B.dang.x), std::fma(c.angB.y, di, B.dang.y), std::fma(c.angB.z, di, B.dang.z));
+                }
+            } else {
+                if (A.real) {
+                    A.dlin += c.n1 * A.inv_mass * di;
+                    A.dang += c.angA * di;
+                }
+                if (B.real) {
+                    B.dlin += c.n2 * B.inv_mass * di;
+                    B.dang += c.angB * di;
+                }
             }
-            if (B.real) {
-                B.dlin += c.n2 * B.inv_mass * di;
-                B.dang += c.angB * di;
-            }
-            return di * (1.f / c.jinv);
         };
-        auto resolve_split = [&](Row& c) {
+        auto resolve_split = [&](Row& c) {  // _scalar_reference or _sse2: only the dot order differs
             float di = 0.f;
             if (c.rhs_pen != 0.f) {
                 SBody& A = sb[c.a];
                 SBody& B = sb[c.bb];
+                const int how = ar == RLGPU_ARITH_SCALAR ? 0 : 1;
                 di = c.rhs_pen - c.applied_push * c.cfm;
-                float dv1 = dot(c.n1, A.push) + dot(c.rc1, A.turn);
-                float dv2 = dot(c.n2, B.push) + dot(c.rc2, B.turn);
+                float dv1 = rdot(c.n1, A.push, how) + rdot(c.rc1, A.turn, how);
+                float dv2 = rdot(c.n2, B.push, how) + rdot(c.rc2, B.turn, how);
                 di -= dv1 * c.jinv;
                 di -= dv2 * c.jinv;
                 float sum = c.applied_push + di;
@@ -2005,7 +2054,7 @@ struct Sim {
                     B.turn += c.angB * di;
                 }
             }
-            return di * (1.f / c.jinv);
+            return (float)((double)di * (1. / (double)c.jinv));  // deltaImpulse * (1. / m_jacDiagABInv)
         };
         // split-impulse iterations (btSequentialImpulseConstraintSolver.cpp:1762-1795)
         for (int it = 0; it < 10; it++) {
@@ -2143,8 +2192,8 @@ struct Sim {
                     st3(cs.vel_impulse_cache, V());
                 }
                 const float maxv = 2300.f * UU_TO_BT;
-                if (len2(c.vel) > maxv * maxv) c.vel = normalized(c.vel) * maxv;
-                if (len2(c.ang) > 5.5f * 5.5f) c.ang = normalized(c.ang) * 5.5f;
+                if (len2(c.vel) > maxv * maxv) c.vel = bt_normalize(c.vel) * maxv;
+                if (len2(c.ang) > 5.5f * 5.5f) c.ang = bt_normalize(c.ang) * 5.5f;
             }
             // BoostPadGrid::CheckCollision (BoostPadGrid.cpp:5-25)
             if (cs.is_demoed || cs.boost >= 100) continue;
@@ -2194,8 +2243,8 @@ struct Sim {
                 st3(s.ball_vel_impulse_cache, V());
             }
             const float maxv = 6000.f * UU_TO_BT;
-            if (len2(ball.vel) > maxv * maxv) ball.vel = normalized(ball.vel) * maxv;
-            if (len2(ball.ang) > 6.f * 6.f) ball.ang = normalized(ball.ang) * 6.f;
+            if (len2(ball.vel) > maxv * maxv) ball.vel = bt_normalize(ball.vel) * maxv;
+            if (len2(ball.ang) > 6.f * 6.f) ball.ang = bt_normalize(ball.ang) * 6.f;
         }
         s.env.tick_count++;
     }
@@ -2271,7 +2320,8 @@ void oracle_car_box_shape(float* impl3, float* margin, float* half3) {
 // vertices), cbt; the box shape is the Octane's.  out[8 per query] = {hit, normal xyz, point xyz, depth}.
 // counts[2] (optional) += GJK queries and penetration-solver calls.
 void oracle_box_triangle(int n, const float* rot, const float* centre, const float* tri, const float* cbt, float* out,
-                         uint64_t* counts) {
+                         uint64_t* counts, int arith) {
+    orc::ArithScope scope(arith);
     const orc::World& w = orc::world();
     orc::gjk::Shapes sh;
     sh.impl = w.car_impl;
@@ -2351,5 +2401,74 @@ extern "C" {
 void oracle_bvh_order(const float* tris, int ntris, int32_t* out) {
     std::vector<int> o = orc::bvh::leaf_order(tris, ntris);
     for (int k = 0; k < ntris; k++) out[k] = o[k];
+}
+}  // extern "C"
+
+// ---------------------------------------------------------------- x86 instruction checks (tests only)
+// The x86 modes restate three instructions: rsqrtss (executed here, looked up from this host's table on the
+// device), DPPS with mask 0x7f ((x + y) + (z + 0)) and the FMA3 fused multiply-add (std::fma).  These run
+// the instructions themselves on arrays so the tests can compare them with the restatements.
+#include <immintrin.h>
+extern "C" {
+void oracle_rsqrtss(const float* x, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = orc::x86_rsqrtss(x[i]);
+}
+// 1 when the host has SSE4.1 and FMA3 (the MSVC build's _sse4_1_fma3 rows run only there)
+int oracle_has_sse41_fma3() { return __builtin_cpu_supports("sse4.1") && __builtin_cpu_supports("fma") ? 1 : 0; }
+__attribute__((target("sse4.1"))) void oracle_dpps(const float* a, const float* b, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++) {
+        const __m128 va = _mm_set_ps(0.f, a[3 * i + 2], a[3 * i + 1], a[3 * i]);
+        const __m128 vb = _mm_set_ps(0.f, b[3 * i + 2], b[3 * i + 1], b[3 * i]);
+        out[i] = _mm_cvtss_f32(_mm_dp_ps(va, vb, 0x7f));
+    }
+}
+__attribute__((target("fma"))) void oracle_fmadd(const float* a, const float* b, const float* c, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = _mm_cvtss_f32(_mm_fmadd_ss(_mm_set_ss(a[i]), _mm_set_ss(b[i]), _mm_set_ss(c[i])));
+}
+// the restatements, for comparison: DPPS order and std::fma
+void oracle_dpps_restated(const float* a, const float* b, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++) {
+        const float x = a[3 * i] * b[3 * i], y = a[3 * i + 1] * b[3 * i + 1], z = a[3 * i + 2] * b[3 * i + 2];
+        out[i] = (x + y) + (z + 0.f);
+    }
+}
+void oracle_fma_restated(const float* a, const float* b, const float* c, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = std::fma(a[i], b[i], c[i]);
+}
+// LinearMath operations of one arithmetic mode (rsim_math.hpp) on arrays, for the device comparison
+// (rlgpu_linear_math_queries, dmath.hpp): op 0 normalize v[3] -> v[3]; 1 setRotation q[4] -> m[9];
+// 2 getRotation m[9] -> q[4]; 3 quaternion product a[4] b[4] -> q[4]; 4 integrateTransform of rot[9] pos[3]
+// linvel[3] angvel[3] over 1/120 s -> pos[3] rot[9].  Input stride 24 floats, output stride 12.
+void oracle_linear_math(int op, int arith, const float* in, int64_t n, float* out) {
+    orc::ArithScope scope(arith);
+    using orc::V;
+    using orc::M;
+    using orc::Q;
+    for (int64_t i = 0; i < n; i++) {
+        const float* p = in + 24 * i;
+        float* o = out + 12 * i;
+        M m;
+        for (int r = 0; r < 3; r++) m.r[r] = V(p[3 * r], p[3 * r + 1], p[3 * r + 2]);
+        if (op == 0) {
+            const V v = orc::bt_normalize(V(p[0], p[1], p[2]));
+            o[0] = v.x, o[1] = v.y, o[2] = v.z;
+        } else if (op == 1) {
+            const M r = orc::mat_from_quat(Q{p[0], p[1], p[2], p[3]});
+            for (int k = 0; k < 9; k++) o[k] = r.r[k / 3][k % 3];
+        } else if (op == 2) {
+            const Q q = orc::quat_from_mat(m);
+            o[0] = q.x, o[1] = q.y, o[2] = q.z, o[3] = q.w;
+        } else if (op == 3) {
+            const Q q = orc::qmul(Q{p[0], p[1], p[2], p[3]}, Q{p[4], p[5], p[6], p[7]});
+            o[0] = q.x, o[1] = q.y, o[2] = q.z, o[3] = q.w;
+        } else {
+            V np;
+            M nr;
+            orc::integrate_transform(V(p[9], p[10], p[11]), m, V(p[12], p[13], p[14]), V(p[15], p[16], p[17]), 1.f / 120.f,
+                                     np, nr);
+            o[0] = np.x, o[1] = np.y, o[2] = np.z;
+            for (int k = 0; k < 9; k++) o[3 + k] = nr.r[k / 3][k % 3];
+        }
+    }
 }
 }  // extern "C"

@@ -27,6 +27,7 @@ struct World {
     std::vector<int> tri_obj;
     std::vector<TriInfo> tri_info;  // internal-edge records (btGenerateInternalEdgeInfo, edge_ref.hpp)
     std::vector<int> tri_visit;     // each object's triangles in Bullet's BVH visit order (bvh_ref.hpp)
+    int arith = RLGPU_ARITH_MSVC_X64;  // the build whose arithmetic the edge records are made in (rsim_math.hpp)
     void set_mesh(const float* tris_bt, int n, const int* obj_ntris, int nobjects);
     float kick_x[5], kick_y[5];
     M kick_rot[2][5];
@@ -35,9 +36,10 @@ struct World {
     V pad_pos_uu[RLGPU_PADS], pad_pos_bt[RLGPU_PADS], pad_box_min[RLGPU_PADS], pad_box_max[RLGPU_PADS];
     bool pad_big[RLGPU_PADS];
     int pad_cell_x[RLGPU_PADS], pad_cell_y[RLGPU_PADS];
-    World();
+    explicit World(int arith = RLGPU_ARITH_MSVC_X64);
 };
-const World& world();
+// the built-in world of an arithmetic mode (synthetic mesh; its edge records depend on the mode)
+const World& world(int arith = g_arith);
 
 inline V ld3(const float* p) { return V(p[0], p[1], p[2]); }
 inline V ld3v(const float* p) { return V(p[0], p[1], p[2]); }

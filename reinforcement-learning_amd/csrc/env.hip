@@ -44,6 +44,7 @@ struct StepArgs {
     double* metrics;           // [n][RLGPU_STEP_METRIC_SLOTS] StepCallback sums (build steps) or null
     int metrics_players;       // this call is one of ExampleMain's every-4th "expensive" calls
     const Plugins* plug;       // the set's reward / terminal registry (device)
+    int arith;                 // RLGPU_ARITH_* (rlgpu_envset_config.arith): copied into Aux::arith at launch
 };
 
 // ExampleMain's StepCallback (src/ExampleMain.cpp:233-283) on this arena's GameState as the
@@ -166,7 +167,8 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
             A->a.pred_pos[0] = bpos(A, 0) + bvel(A, 0) * kTick;
             A->a.pred_rot[0] = brot(A, 0);
         } else {
-            integrate_transform(bpos(A, l), brot(A, l), bvel(A, l), bang(A, l), kTick, A->a.pred_pos[l], A->a.pred_rot[l]);
+            integrate_transform(bpos(A, l), brot(A, l), bvel(A, l), bang(A, l), kTick, A->a.pred_pos[l], A->a.pred_rot[l],
+                                arith(A));
         }
     }
     sync();
@@ -222,7 +224,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
             } else {
                 v3 np;
                 m3 nr;
-                integrate_transform(ld3(b->pos), ldm(b->rot), ld3(b->vel), ld3(b->angvel), kTick, np, nr);
+                integrate_transform(ld3(b->pos), ldm(b->rot), ld3(b->vel), ld3(b->angvel), kTick, np, nr, arith(A));
                 st3(b->pos, np);
                 stm(b->rot, nr);
             }
@@ -255,8 +257,8 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
                 st3(cs.vel_impulse_cache, zero3());
             }
             const float maxv = 2300.f * kUU2BT;
-            if (len2(v) > maxv * maxv) v = normalized(v) * maxv;
-            if (len2(w) > 5.5f * 5.5f) w = normalized(w) * 5.5f;
+            if (len2(v) > maxv * maxv) v = bt_normalize(v, arith(A)) * maxv;  // vel.normalized() (Car.cpp:183-186)
+            if (len2(w) > 5.5f * 5.5f) w = bt_normalize(w, arith(A)) * 5.5f;
             st3(b->vel, v);
             st3(b->angvel, w);
         }
@@ -334,8 +336,8 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
             st3(A->s.ball_vel_impulse_cache, zero3());
         }
         const float maxv = 6000.f * kUU2BT;
-        if (len2(v) > maxv * maxv) v = normalized(v) * maxv;
-        if (len2(w) > 6.f * 6.f) w = normalized(w) * 6.f;
+        if (len2(v) > maxv * maxv) v = bt_normalize(v, arith(A)) * maxv;  // vel.normalized() (Ball.cpp:128-131)
+        if (len2(w) > 6.f * 6.f) w = bt_normalize(w, arith(A)) * 6.f;
         st3(b->vel, v);
         st3(b->angvel, w);
         A->s.env.tick_count++;
@@ -383,7 +385,10 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         A->a.torque[l] = zero3();
         update_inertia(A, l);
     }
-    if (l == 0) A->a.epa_lock = A->a.npen = 0;
+    if (l == 0) {
+        A->a.epa_lock = A->a.npen = 0;
+        A->a.arith = g.arith;
+    }
     sync(); P.mark(11);
     // ---- StepFirstHalf (EnvSet.cpp:113-130) prelude
     if (g.ticks_first > 0) {
@@ -867,6 +872,21 @@ extern "C" int rlgpu_envset_default_plugins(rlgpu_reward_spec* rewards, int32_t*
 
 namespace {
 bool g_const_ready = false;
+bool g_rsqrt_ready = false;
+
+// the x86 modes' rsqrtss: this host's table (host/x86_arith.cpp) in device memory, its pointer in the
+// kernels' kRsqrtLut (once per process; the table is the host CPU's, the same for every set)
+void ensure_rsqrt() {
+    if (g_rsqrt_ready) return;
+    int bits = 0;
+    const std::vector<uint32_t>& t = rlgpu::x86_rsqrt_table_or_throw(&bits);
+    uint32_t* d = nullptr;
+    RLGPU_CHECK_HIP(hipMalloc(&d, t.size() * sizeof(uint32_t)));
+    RLGPU_CHECK_HIP(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const rl::RsqrtLut L{d, bits};
+    RLGPU_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rl::kRsqrtLut), &L, sizeof L));
+    g_rsqrt_ready = true;
+}
 
 void ensure_const() {
     if (g_const_ready) return;
@@ -889,6 +909,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.prof = e->d_prof;
     g.mesh = e->mesh;
     g.plug = e->d_plug;
+    g.arith = e->cfg.arith;
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
         g.metrics_players = (++e->metric_calls % 4) == 0;
@@ -915,8 +936,11 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         RLGPU_REQUIRE(cfg->action_delay >= 0 && cfg->action_delay <= cfg->tick_skip,
                       "actionDelay must be in [0, tickSkip] (EnvSet.cpp:49)");
         RLGPU_REQUIRE(cfg->mesh_tris == nullptr || cfg->mesh_ntris > 0, "mesh_ntris must be > 0 with mesh_tris");
+        RLGPU_REQUIRE(cfg->arith >= 0 && cfg->arith < RLGPU_NUM_ARITH,
+                      "rlgpu_envset_create: unknown arithmetic mode " + std::to_string(cfg->arith) + " (RLGPU_ARITH_*)");
         const rl::Plugins plug = plugins_from(cfg);
         ensure_const();
+        if (rl::sse_api(cfg->arith)) ensure_rsqrt();
         // arena meshes (Arena::_SetupArenaCollisionShapes): triangle table + grid index in HBM
         std::vector<float> builtin;
         const float* tris = cfg->mesh_tris;
@@ -927,7 +951,7 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
             ntris = (int)(builtin.size() / 9);
         }
         rlgpu::MeshGrid grid = rlgpu::build_mesh_grid(tris, ntris, cfg->mesh_tris ? cfg->mesh_object_ntris : nullptr,
-                                                      cfg->mesh_tris ? cfg->mesh_objects : 1);
+                                                      cfg->mesh_tris ? cfg->mesh_objects : 1, cfg->arith);
         auto* e = new rlgpu_envset();
         e->cfg = *cfg;
         e->cfg.mesh_tris = nullptr;  // host pointers are not kept
@@ -1236,7 +1260,7 @@ namespace rl {
 // lds != 0: each lane first tries a small LDS work set of its own, as the env kernel's lanes do
 __global__ void __launch_bounds__(16) box_triangle_kernel(int n, const float* rot, const float* centre, const float* tri,
                                                           const float* cbt, float* out, gjk::GjkScratch* scratch,
-                                                          int lds) {
+                                                          int lds, int ar) {
     __shared__ char small[16][gjk::kSmallBytes];
     __shared__ int lock[16];
     const int i = blockIdx.x * 16 + threadIdx.x;
@@ -1246,7 +1270,7 @@ __global__ void __launch_bounds__(16) box_triangle_kernel(int n, const float* ro
     const m3 R = m3{v3{r[0], r[1], r[2]}, v3{r[3], r[4], r[5]}, v3{r[6], r[7], r[8]}};
     const v3 c = v3{centre[3 * (size_t)i], centre[3 * (size_t)i + 1], centre[3 * (size_t)i + 2]};
     const float* t = tri + 9 * (size_t)i;
-    const gjk::Shape sh{C.car_impl, C.car_margin, v3{t[0], t[1], t[2]}, v3{t[3], t[4], t[5]}, v3{t[6], t[7], t[8]}};
+    const gjk::Shape sh{C.car_impl, C.car_margin, v3{t[0], t[1], t[2]}, v3{t[3], t[4], t[5]}, v3{t[6], t[7], t[8]}, ar};
     v3 nrm, pt;
     float d = 0.f;
     gjk::Scr slow = gjk::hbm_view(scratch + i);
@@ -1265,19 +1289,69 @@ __global__ void __launch_bounds__(16) box_triangle_kernel(int n, const float* ro
 }  // namespace rl
 
 extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
-                                          const float* d_cbt, float* d_out, int32_t lds_first, void* stream) {
+                                          const float* d_cbt, float* d_out, int32_t lds_first, int32_t arith, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(n >= 0, "rlgpu_box_triangle_queries: n must be >= 0");
+        RLGPU_REQUIRE(arith >= 0 && arith < RLGPU_NUM_ARITH, "rlgpu_box_triangle_queries: unknown arithmetic mode");
         if (n == 0) return;
         RLGPU_REQUIRE(d_rot && d_centre && d_tri && d_cbt && d_out, "rlgpu_box_triangle_queries: null argument");
         ensure_const();
+        if (rl::sse_api(arith)) ensure_rsqrt();
         hipStream_t s = (hipStream_t)stream;
         void* scratch = nullptr;
         RLGPU_CHECK_HIP(hipMallocAsync(&scratch, (size_t)n * sizeof(rl::gjk::GjkScratch), s));
         hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 16)), dim3(16), 0, s, n, d_rot, d_centre, d_tri,
-                           d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)(lds_first != 0));
+                           d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)(lds_first != 0), (int)arith);
         RLGPU_CHECK_HIP(hipGetLastError());
         RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
+    });
+}
+
+// ------------------------------------------------------------------ LinearMath queries (tests)
+namespace rl {
+// one query per lane of dmath.hpp's mode-dependent operations (rlgpu_linear_math_queries)
+__global__ void __launch_bounds__(64) linear_math_kernel(int op, int ar, const float* in, int n, float* out) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const float* p = in + 24 * (size_t)i;
+    float* o = out + 12 * (size_t)i;
+    const m3 m = m3{v3{p[0], p[1], p[2]}, v3{p[3], p[4], p[5]}, v3{p[6], p[7], p[8]}};
+    auto put9 = [&](const m3& r, float* q) {
+        q[0] = r.r0.x; q[1] = r.r0.y; q[2] = r.r0.z;
+        q[3] = r.r1.x; q[4] = r.r1.y; q[5] = r.r1.z;
+        q[6] = r.r2.x; q[7] = r.r2.y; q[8] = r.r2.z;
+    };
+    if (op == 0) {
+        const v3 v = bt_normalize(v3{p[0], p[1], p[2]}, ar);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z;
+    } else if (op == 1) {
+        put9(mat_from_quat(quat{p[0], p[1], p[2], p[3]}, ar), o);
+    } else if (op == 2) {
+        const quat q = quat_from_mat(m, ar);
+        o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.w;
+    } else if (op == 3) {
+        const quat q = qmul(quat{p[0], p[1], p[2], p[3]}, quat{p[4], p[5], p[6], p[7]}, ar);
+        o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.w;
+    } else {
+        v3 np;
+        m3 nr;
+        integrate_transform(v3{p[9], p[10], p[11]}, m, v3{p[12], p[13], p[14]}, v3{p[15], p[16], p[17]}, kTick, np, nr, ar);
+        o[0] = np.x; o[1] = np.y; o[2] = np.z;
+        put9(nr, o + 3);
+    }
+}
+}  // namespace rl
+
+extern "C" int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(op >= 0 && op <= 4, "rlgpu_linear_math_queries: op must be in [0, 4]");
+        RLGPU_REQUIRE(arith >= 0 && arith < RLGPU_NUM_ARITH, "rlgpu_linear_math_queries: unknown arithmetic mode");
+        RLGPU_REQUIRE(n >= 0 && (n == 0 || (d_in && d_out)), "rlgpu_linear_math_queries: bad argument");
+        if (n == 0) return;
+        if (rl::sse_api(arith)) ensure_rsqrt();
+        hipLaunchKernelGGL(rl::linear_math_kernel, dim3(rlgpu::ceil_div(n, 64)), dim3(64), 0, (hipStream_t)stream, (int)op,
+                           (int)arith, d_in, (int)n, d_out);
+        RLGPU_CHECK_HIP(hipGetLastError());
     });
 }
 

@@ -244,7 +244,8 @@ DEV void add_contact(ArenaLDS* A, const MeshView& M, int key, v3 normal_b, v3 po
         const float4 t0 = M.tri[3 * tri], t1 = M.tri[3 * tri + 1], t2 = M.tri[3 * tri + 2], ei = M.edge[tri];
         const EdgeInfo info{ei.x, ei.y, ei.z, __float_as_int(ei.w)};
         v3 n = ld3(cp.normalB), pb = ld3(cp.localB);
-        adjust_edge_contact(v3{t0.x, t0.y, t0.z}, v3{t1.x, t1.y, t1.z}, v3{t2.x, t2.y, t2.z}, info, n, pb, pa, cp.dist);
+        adjust_edge_contact(v3{t0.x, t0.y, t0.z}, v3{t1.x, t1.y, t1.z}, v3{t2.x, t2.y, t2.z}, info, n, pb, pa, cp.dist,
+                            arith(A));
         st3(cp.normalB, n);
         st3(cp.localB, pb);
     }
@@ -392,7 +393,7 @@ DEV v3 closest_point_triangle(v3 p, v3 a, v3 b, v3 c) {
     return a + ab * vv + ac * ww;
 }
 DEV bool sphere_triangle(v3 center, float radius, v3 v0, v3 v1, v3 v2, float cbt, v3& point, v3& normal_out,
-                         float& depth) {
+                         float& depth, int ar) {
     float rwt = radius + cbt;
     v3 normal = cross(v1 - v0, v2 - v0);
     float l2 = len2(normal);
@@ -426,7 +427,7 @@ DEV bool sphere_triangle(v3 center, float radius, v3 v0, v3 v1, v3 v2, float cbt
     if (!(d2 < rwt * rwt)) return false;
     if (d2 > kEps) {
         float d = sqrtf(d2);
-        normal_out = normalized(c2c);
+        normal_out = bt_normalize(c2c, ar);  // resultNormal.normalize() (SphereTriangleDetector.cpp:228)
         point = cp;
         depth = -(radius - d);
     } else {
@@ -450,7 +451,7 @@ __device__ __noinline__ void box_tri_query(ArenaLDS* A, const MeshView& M, int b
     const v3 c = car_box_center(A, bi);
     gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
     gjk::Scr fast = gjk::lds_view((char*)&A->u.cand[kMaxCand]);
-    const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2};
+    const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2, arith(A)};
     v3 n, pb;
     float d;
     if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
@@ -483,6 +484,7 @@ DEV void narrow_queue(ArenaLDS* base, int nvalid, const MeshView& M) {
 // Body-vs-mesh ranks are split over `parts` lanes (grid entries dealt round-robin); candidates
 // carry (rank, triangle), so the commit order does not depend on the split.
 DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int parts = 1) {
+    const int ar = arith(A);
     if (rank < 25) {
         const int bi = rank / 5, st = rank % 5;
         bool active = bi == 0 ? A->a.ball_awake != 0 : A->a.active[bi] != 0;
@@ -502,7 +504,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                 grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) {
                     v3 pt, nrm;
                     float depth;
-                    if (sphere_triangle(c, r, v0, v1, v2, cbt, pt, nrm, depth))
+                    if (sphere_triangle(c, r, v0, v1, v2, cbt, pt, nrm, depth, ar))
                         emit(A, rank, t, mesh_key(0, obj), nrm, pt, depth);
                 });
             }
@@ -757,43 +759,97 @@ DEV void add_friction(ArenaLDS* A, Solver& S, int ia, int ib, const rlgpu_contac
     f.upper = friction;
 }
 
+// A row's dot with a body's velocity deltas, in the order of the row function the reference build runs:
+// the _sse2 rows' btSimdDot3 x + (y + z) (btSequentialImpulseConstraintSolver.cpp:106-110), the MSVC
+// _sse4_1_fma3 rows' _mm_dp_ps(a, b, 0x7f) -- products, then lanes (0 + 1) + (2 + 3) with lane 3 zeroed --
+// i.e. (x + y) + (z + 0) (:122-124), and the scalar rows' btVector3::dot (x + y) + z.
+enum { kDotScalar = 0, kDotSse2 = 1, kDotDpps = 2 };
+DEV float row_dot(v3 a, v3 b, int how) {
+    const float x = a.x * b.x, y = a.y * b.y, z = a.z * b.z;
+    if (how == kDotSse2) return x + (y + z);
+    if (how == kDotDpps) return (x + y) + (z + 0.f);
+    return (x + y) + z;
+}
+
+// One contact (lower limit only) or friction (generic) row: gResolveSingleConstraintRow{LowerLimit,Generic}_
+// scalar_reference (:46-100), _sse2 (:149-177, 207-233) or _sse4_1_fma3 (:180-205, 235-260) by the set's
+// arithmetic mode.  The x86 rows differ from the scalar one in the dot order, in the clamp at equality
+// (_sse2 clamps to the upper limit when sum == upper; _sse4_1_fma3 clamps when sum <= lower or sum >= upper)
+// and, for _sse4_1_fma3, in fused multiply-adds for the delta and the velocity updates.  Static / inactive
+// bodies are not updated: the reference adds (n * 0) * di to its fixed body's zero deltas, which stay +0.
 template <class Row>
-DEV float resolve_row(Solver& S, Row& c, float lower, float upper, bool generic) {
+DEV void resolve_row(Solver& S, Row& c, float lower, float upper, bool generic, int ar) {
     SB& A = S.sb[c.a];
     SB& B = S.sb[c.b];
+    const bool fma3 = ar == RLGPU_ARITH_MSVC_X64;
+    const int how = fma3 ? kDotDpps : (ar == RLGPU_ARITH_GCC_X64 ? kDotSse2 : kDotScalar);
     float di = c.rhs - c.applied * 0.f;
-    float dv1 = dot(c.n1, A.dlin) + dot(c.rc1, A.dang);
-    float dv2 = dot(c.n2, B.dlin) + dot(c.rc2, B.dang);
-    di -= dv1 * c.jinv;
-    di -= dv2 * c.jinv;
-    float sum = c.applied + di;
-    if (sum < lower) {
-        di = lower - c.applied;
+    const float dv1 = row_dot(c.n1, A.dlin, how) + row_dot(c.rc1, A.dang, how);
+    const float dv2 = row_dot(c.n2, B.dlin, how) + row_dot(c.rc2, B.dang, how);
+    if (fma3) {  // FMNADD: -(dv * jac) + di, fused
+        di = fmaf(-dv1, c.jinv, di);
+        di = fmaf(-dv2, c.jinv, di);
+    } else {
+        di -= dv1 * c.jinv;
+        di -= dv2 * c.jinv;
+    }
+    const float applied = c.applied, sum = applied + di;
+    if (fma3) {  // blendv on sum > lower and upper > sum
+        const bool above = sum > lower, below = !generic || upper > sum;
+        di = above ? (below ? di : upper - applied) : lower - applied;
+        c.applied = above ? (below ? sum : upper) : lower;
+    } else if (ar == RLGPU_ARITH_GCC_X64) {  // and / andnot selects on sum < lower, then sum < upper
+        const bool low = sum < lower;
+        float d = low ? lower - applied : di, ap = low ? lower : sum;
+        if (generic && !(sum < upper)) {
+            d = upper - applied;
+            ap = upper;
+        }
+        di = d;
+        c.applied = ap;
+    } else if (sum < lower) {
+        di = lower - applied;
         c.applied = lower;
     } else if (generic && sum > upper) {
-        di = upper - c.applied;
+        di = upper - applied;
         c.applied = upper;
     } else {
         c.applied = sum;
     }
-    if (A.real) {
-        A.dlin += c.n1 * v3{A.inv_mass, A.inv_mass, A.inv_mass} * di;
-        A.dang += c.angA * di;
+    if (fma3) {  // FMADD(n * invMass, di, delta), FMADD(angular component, di, delta)
+        if (A.real) {
+            const v3 la = c.n1 * v3{A.inv_mass, A.inv_mass, A.inv_mass};
+            A.dlin = v3{fmaf(la.x, di, A.dlin.x), fmaf(la.y, di, A.dlin.y), fmaf(la.z, di, A.dlin.z)};
+            A.dang = v3{fmaf(c.angA.x, di, A.dang.x), fmaf(c.angA.y, di, A.dang.y), fmaf(c.angA.z, di, A.dang.z)};
+        }
+        if (B.real) {
+            const v3 lb = c.n2 * v3{B.inv_mass, B.inv_mass, B.inv_mass};
+            B.dlin = v3{fmaf(lb.x, di, B.dlin.x), fmaf(lb.y, di, B.dlin.y), fmaf(lb.z, di, B.dlin.z)};
+            B.dang = v3{fmaf(c.angB.x, di, B.dang.x), fmaf(c.angB.y, di, B.dang.y), fmaf(c.angB.z, di, B.dang.z)};
+        }
+    } else {
+        if (A.real) {
+            A.dlin += c.n1 * v3{A.inv_mass, A.inv_mass, A.inv_mass} * di;
+            A.dang += c.angA * di;
+        }
+        if (B.real) {
+            B.dlin += c.n2 * v3{B.inv_mass, B.inv_mass, B.inv_mass} * di;
+            B.dang += c.angB * di;
+        }
     }
-    if (B.real) {
-        B.dlin += c.n2 * v3{B.inv_mass, B.inv_mass, B.inv_mass} * di;
-        B.dang += c.angB * di;
-    }
-    return di * (1.f / c.jinv);
 }
-DEV float resolve_split(Solver& S, CRow& c) {
+// gResolveSplitPenetrationImpulse_scalar_reference (:283-313) / _sse2 (:315-350; both x86 builds, MSVC has no
+// fused split row): only the dot order differs.  The residual is deltaImpulse * (1. / jacDiagABInv) in
+// double, returned as float.
+DEV float resolve_split(Solver& S, CRow& c, int ar) {
     float di = 0.f;
     if (c.rhs_pen != 0.f) {
         SB& A = S.sb[c.a];
         SB& B = S.sb[c.b];
+        const int how = sse_api(ar) ? kDotSse2 : kDotScalar;
         di = c.rhs_pen - c.applied_push * 0.f;
-        float dv1 = dot(c.n1, A.push) + dot(c.rc1, A.turn);
-        float dv2 = dot(c.n2, B.push) + dot(c.rc2, B.turn);
+        float dv1 = row_dot(c.n1, A.push, how) + row_dot(c.rc1, A.turn, how);
+        float dv2 = row_dot(c.n2, B.push, how) + row_dot(c.rc2, B.turn, how);
         di -= dv1 * c.jinv;
         di -= dv2 * c.jinv;
         float sum = c.applied_push + di;
@@ -812,7 +868,7 @@ DEV float resolve_split(Solver& S, CRow& c) {
             B.turn += c.angB * di;
         }
     }
-    return di * (1.f / c.jinv);
+    return (float)((double)di * (1. / (double)c.jinv));
 }
 
 // max over the 16 lanes of an arena (xor partners stay inside the 16-lane group)
@@ -833,6 +889,7 @@ DEV float group16_max(float v) {
 // Called by all threads of the workgroup (it synchronises); `valid`: this lane's arena exists.
 DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
     Solver& S = A->u.sv;
+    const int ar = arith(A);
     static_assert(kMaxRows <= kTeam, "one lane per solver row");
     if (valid && l < 5) {  // bodies (btSolverBody init), one per lane
         const int i = l;
@@ -998,7 +1055,7 @@ DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
         float lsr = 0.f;
         for (int L = 0; L < nlev; L++) {
             if (!done && lv == L) {
-                float res = resolve_split(S, cr);
+                float res = resolve_split(S, cr, ar);
                 lsr = stdmax(lsr, res * res);
             }
             sync();
@@ -1011,7 +1068,7 @@ DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
     const bool special = mine && cr.special;
     for (int it = 0; it < 10; it++) {
         for (int L = 0; L < nlev; L++) {
-            if (lv == L && !special) resolve_row(S, cr, 0.f, 1e10f, false);
+            if (lv == L && !special) resolve_row(S, cr, 0.f, 1e10f, false, ar);
             sync();
         }
         for (int L = 0; L < nlev; L++) {
@@ -1020,7 +1077,7 @@ DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
                 if (total > 0.f) {
                     fr.lower = -(fr.friction * total);
                     fr.upper = fr.friction * total;
-                    resolve_row(S, fr, fr.lower, fr.upper, true);
+                    resolve_row(S, fr, fr.lower, fr.upper, true, ar);
                 }
             }
             sync();
@@ -1040,7 +1097,7 @@ DEV void solve_lanes(ArenaLDS* A, int l, bool valid, Prof* P = nullptr) {
             } else {
                 v3 np;
                 m3 nr;
-                integrate_transform(ld3(bd->pos), ldm(bd->rot), x.push, x.turn * 0.1f, kTick, np, nr);
+                integrate_transform(ld3(bd->pos), ldm(bd->rot), x.push, x.turn * 0.1f, kTick, np, nr, ar);
                 st3(bd->pos, np);
                 stm(bd->rot, nr);
             }

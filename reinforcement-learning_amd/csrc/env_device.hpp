@@ -28,6 +28,7 @@ DEV v3 bpos(ArenaLDS* A, int i) { return ld3(body(A, i)->pos); }
 DEV v3 bvel(ArenaLDS* A, int i) { return ld3(body(A, i)->vel); }
 DEV v3 bang(ArenaLDS* A, int i) { return ld3(body(A, i)->angvel); }
 DEV m3 brot(ArenaLDS* A, int i) { return ldm(body(A, i)->rot); }
+DEV int arith(const ArenaLDS* A) { return A->a.arith; }  // the set's RLGPU_ARITH_* mode
 DEV float binv_mass(int i) { return i == 0 ? C.ball_inv_mass : C.car_inv_mass; }
 DEV v3 binv_iner(int i) { return i == 0 ? C.ball_inv_inertia : C.car_inv_inertia; }
 DEV v3 vel_at(ArenaLDS* A, int i, v3 rel) { return bvel(A, i) + cross(bang(A, i), rel); }
@@ -212,7 +213,7 @@ DEV v3 lerp3(v3 v0, v3 v1, float rt) {
 // btTriangleRaycastCallback::processTriangle (btRaycastCallback.cpp:35-117, ClosestRayResultCallback flags 0):
 // the hit fraction of [from, to] on the triangle when it lies inside (with the edge tolerance) and is
 // closer than `best` (or equal, when `tie`), else -1; n = the unit normal facing `from`
-DEV float ray_tri(v3 v0, v3 v1, v3 v2, v3 from, v3 to, float best, bool tie, v3& n) {
+DEV float ray_tri(v3 v0, v3 v1, v3 v2, v3 from, v3 to, float best, bool tie, v3& n, int ar) {
     const v3 tn = cross(v1 - v0, v2 - v0);
     const float dist = dot(v0, tn);
     const float da = dot(tn, from) - dist, db = dot(tn, to) - dist;
@@ -224,7 +225,7 @@ DEV float ray_tri(v3 v0, v3 v1, v3 v2, v3 from, v3 to, float best, bool tie, v3&
     const v3 v0p = v0 - pt, v1p = v1 - pt, v2p = v2 - pt;
     if (!(dot(cross(v0p, v1p), tn) >= tol && dot(cross(v1p, v2p), tn) >= tol && dot(cross(v2p, v0p), tn) >= tol))
         return -1.f;
-    const v3 u = normalized(tn);
+    const v3 u = bt_normalize(tn, ar);  // triangleNormal.normalize() (btRaycastCallback.cpp:102)
     n = da <= 0.f ? -u : u;
     return f;
 }
@@ -254,9 +255,10 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
     const v3 smin = v3{fminf(from.x, to.x) - kRayCull, fminf(from.y, to.y) - kRayCull, fminf(from.z, to.z) - kRayCull};
     const v3 smax = v3{fmaxf(from.x, to.x) + kRayCull, fmaxf(from.y, to.y) + kRayCull, fmaxf(from.z, to.z) + kRayCull};
     int best_t = -1;
+    const int ar = arith(A);
     grid_query(M, smin, smax, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int) {
         v3 n;
-        const float f = ray_tri(v0, v1, v2, from, to, best, best_t >= 0 && t < best_t, n);
+        const float f = ray_tri(v0, v1, v2, from, to, best, best_t >= 0 && t < best_t, n, ar);
         if (f < 0.f) return;
         best = f;
         best_t = t;
@@ -287,13 +289,13 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
         const v3 ta = t0 * radius, tb = t1 * radius;
         const v3 ppp = (pc + ta) + tb, ppm = (pc + ta) - tb, pmm = (pc - ta) - tb, pmp = (pc - ta) + tb;
         v3 n;
-        float f = ray_tri(ppp, ppm, pmm, fl, tl, best, false, n);
+        float f = ray_tri(ppp, ppm, pmm, fl, tl, best, false, n, ar);
         if (f >= 0.f) {
             best = f;
             obj = 10;
             nrm = n;
         }
-        f = ray_tri(pmm, pmp, ppp, fl, tl, best, false, n);
+        f = ray_tri(pmm, pmp, ppp, fl, tl, best, false, n, ar);
         if (f >= 0.f) {
             best = f;
             obj = 10;
@@ -311,7 +313,7 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
                 if (f >= 0.f && f < best) {
                     best = f;
                     obj = 0;
-                    nrm = normalized((from + d * f) - bp);
+                    nrm = bt_normalize((from + d * f) - bp, ar);
                 }
             }
         }
@@ -359,7 +361,7 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
     }
     if (obj < 0) return -1;
     hit_point = lerp3(from, to, best);  // ClosestRayResultCallback::addSingleResult
-    hit_normal = normalized(nrm);       // btDefaultVehicleRaycaster::castRay
+    hit_normal = bt_normalize(nrm, ar);  // btDefaultVehicleRaycaster::castRay (btDefaultVehicleRaycaster.cpp:47)
     if (obj >= 1 && obj <= 4 && !A->a.active[obj]) return -1;
     return obj;
 }
@@ -377,7 +379,7 @@ DEV void wheel_phase(ArenaLDS* A, const MeshView& M, int ci, int i) {
     v3 axle = R * v3{0, -1, 0};
     v3 up = -W.wheel_dir;
     quat q = quat_axis_angle(up, cs.wheel_steer[i]);
-    m3 steer = mat_from_quat(q);
+    m3 steer = mat_from_quat(q, arith(A));
     W.wt_col1 = steer * (-axle);
     // rayCast
     W.in_contact = 0;

@@ -169,6 +169,7 @@ struct Aux {
     int goal;
     int traj_term;
     float all_rewards[4];
+    int arith;     // the set's arithmetic mode (rlgpu_envset_config.arith, include/rlgpu_arith.h)
 };
 
 union Scratch {

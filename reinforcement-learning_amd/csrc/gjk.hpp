@@ -131,6 +131,7 @@ struct Shape {
     v3 impl;       // box half extents without margin
     float margin;  // box margin
     v3 t0, t1, t2;  // triangle (mesh space = world: identity transform)
+    int ar;         // the set's arithmetic mode (include/rlgpu_arith.h): btVector3::normalize is bt_normalize
 };
 DEV v3 box_nm(const Shape& s, v3 d) {
     return v3{d.x >= 0 ? s.impl.x : -s.impl.x, d.y >= 0 ? s.impl.y : -s.impl.y, d.z >= 0 ? s.impl.z : -s.impl.z};
@@ -140,9 +141,9 @@ DEV v3 tri_nm(const Shape& s, v3 d) {  // dot3 + btVector3::maxAxis
     const int k = a < b ? (b < c ? 2 : 1) : (a < c ? 2 : 0);
     return sel3(s.t0, s.t1, s.t2, k);
 }
-DEV v3 unit_dir(v3 d) {  // localGetSupportVertexNonVirtual's normalisation
+DEV v3 unit_dir(v3 d, int ar) {  // localGetSupportVertexNonVirtual's localDirNorm.normalize() (btConvexShape.cpp:186-193)
     if (len2(d) < kEps * kEps) d = v3{-1.f, -1.f, -1.f};
-    return d * (1.f / sqrtf(len2(d)));
+    return bt_normalize(d, ar);
 }
 DEV v3 xf(const m3& b, v3 o, v3 x) { return b * x + o; }
 DEV m3 transpose_times(const m3& a, const m3& m) {  // btMatrix3x3::transposeTimes
@@ -410,7 +411,7 @@ DEV Mink make_mink(const Shape& s, const m3& tb0, v3 to0, const m3& tb1, v3 to1,
 }
 DEV v3 support0(const Mink& m, v3 d) {
     if (m.margins) {
-        const v3 n = unit_dir(d);
+        const v3 n = unit_dir(d, m.s.ar);
         return box_nm(m.s, n) + m.s.margin * n;
     }
     return box_nm(m.s, d);
@@ -419,7 +420,7 @@ DEV v3 support1(const Mink& m, v3 d) {
     const v3 dd = m.toshape1 * d;
     v3 sup;
     if (m.margins) {
-        const v3 n = unit_dir(dd);
+        const v3 n = unit_dir(dd, m.s.ar);
         sup = tri_nm(m.s, n) + 0.f * n;
     } else {
         sup = tri_nm(m.s, dd);
@@ -1095,7 +1096,7 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
         const v3 half = s.impl + v3{s.margin, s.margin, s.margin};
         const m3 inv = inverse(R);
         v3 tn = cross(s.t1 - s.t0, s.t2 - s.t0);
-        tn = tn * (1.f / sqrtf(len2(tn)));
+        tn = bt_normalize(tn, s.ar);  // triangle_normal_world.normalize() (btConvexConcaveCollisionAlgorithm.cpp:111)
 #pragma unroll
         for (int side = 0; side < 2; side++) {
             const v3 ld = inv * tn;
@@ -1238,7 +1239,7 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
                 pB = tB;
                 pA -= v * mA;
                 pB += v * mB;
-                nB = v * (1.f / sqrtf(len2(v)));
+                nB = bt_normalize(v, s.ar);  // normalInB.normalize() (btGjkPairDetector.cpp:914)
                 valid = true;
             }
         }

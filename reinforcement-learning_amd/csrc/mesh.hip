@@ -57,7 +57,7 @@ std::vector<float> builtin_mesh_bt() {
     return out;
 }
 
-MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_ntris, int nobjects) {
+MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_ntris, int nobjects, int arith) {
     RLGPU_REQUIRE(tris_in && ntris > 0, "mesh: no triangles");
     RLGPU_REQUIRE(ntris < (1 << 20), "mesh: more than 2^20 - 1 triangles");
     if (!object_ntris) nobjects = 1;
@@ -170,7 +170,7 @@ MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_
         std::memcpy(&d[3], &obj[t], sizeof(int));
     }
     // internal-edge records of the mesh as loaded (neighbour order = load order), moved with their triangles
-    const std::vector<float> edge = mesh_edge_info(tris_in, ntris, object_ntris, object_ntris ? nobjects : 1);
+    const std::vector<float> edge = mesh_edge_info(tris_in, ntris, object_ntris, object_ntris ? nobjects : 1, arith);
     g.edge.resize(edge.size());
     for (int p = 0; p < ntris; p++) std::memcpy(&g.edge[(size_t)p * 4], &edge[(size_t)g.visit_tri[p] * 4], 4 * sizeof(float));
     return g;
@@ -281,7 +281,7 @@ std::vector<int> bvh_visit_order(const float* tris, int n) {
 // for every triangle A, every other triangle B of the object whose AABB overlaps A's, in the order the
 // object's quantized BVH visits them (the reference's overlap query, btInternalEdgeUtility.cpp:300-356:
 // the last neighbour sharing an edge writes A's record)
-std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* object_ntris, int nobjects) {
+std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* object_ntris, int nobjects, int arith) {
     std::vector<float> out((size_t)ntris * 4, 0.f);
     auto vert = [&](int t, int k) {
         const float* p = tris + (size_t)t * 9 + 3 * k;
@@ -311,7 +311,7 @@ std::vector<float> mesh_edge_info(const float* tris, int ntris, const int32_t* o
                     mn[j].z > mx[i].z + g || mx[j].z < mn[i].z - g)
                     continue;
                 const rl::v3 vb[3] = {vert(t0 + j, 0), vert(t0 + j, 1), vert(t0 + j, 2)};
-                rl::edge_connect(va, vb, info);
+                rl::edge_connect(va, vb, info, arith);
             }
             float* d = &out[(size_t)(t0 + i) * 4];
             d[0] = info.a01;
@@ -360,9 +360,10 @@ extern "C" int rlgpu_cmf_parse(const void* data, int64_t size, float* out_tris, 
 }
 
 extern "C" int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int32_t* object_ntris, int32_t nobjects,
-                                    float* out) {
+                                    int32_t arith, float* out) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(tris && out && ntris > 0, "rlgpu_mesh_edge_info: null argument or no triangles");
+        RLGPU_REQUIRE(arith >= 0 && arith < RLGPU_NUM_ARITH, "rlgpu_mesh_edge_info: unknown arithmetic mode");
         if (object_ntris) {
             RLGPU_REQUIRE(nobjects >= 1, "rlgpu_mesh_edge_info: nobjects must be >= 1");
             int64_t sum = 0;
@@ -372,7 +373,7 @@ extern "C" int rlgpu_mesh_edge_info(const float* tris, int32_t ntris, const int3
             }
             RLGPU_REQUIRE(sum == ntris, "rlgpu_mesh_edge_info: object triangle counts do not add up to ntris");
         }
-        const std::vector<float> e = rlgpu::mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1);
+        const std::vector<float> e = rlgpu::mesh_edge_info(tris, ntris, object_ntris, object_ntris ? nobjects : 1, arith);
         std::memcpy(out, e.data(), e.size() * sizeof(float));
     });
 }
@@ -381,7 +382,7 @@ extern "C" int rlgpu_mesh_bvh_order(const float* tris, int32_t ntris, const int3
                                     int32_t* out) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(out, "rlgpu_mesh_bvh_order: null argument");
-        const rlgpu::MeshGrid g = rlgpu::build_mesh_grid(tris, ntris, object_ntris, nobjects);
+        const rlgpu::MeshGrid g = rlgpu::build_mesh_grid(tris, ntris, object_ntris, nobjects, RLGPU_ARITH_SCALAR);
         std::copy(g.visit_tri.begin(), g.visit_tri.end(), out);
     });
 }

@@ -23,11 +23,11 @@ struct MeshGrid {
 
 // tris_bt: ntris x 9 floats (bullet units); object k owns the next object_ntris[k] triangles
 // (object_ntris == nullptr: one object).  Throws rlgpu::Error on invalid input.
-MeshGrid build_mesh_grid(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects);
+MeshGrid build_mesh_grid(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects, int arith);
 
 // btGenerateInternalEdgeInfo over every object of a mesh (edge_info.hpp): ntris x 4 floats
 // (m_edgeV0V1Angle, m_edgeV1V2Angle, m_edgeV2V0Angle, flags bits; flags 0 = no record)
-std::vector<float> mesh_edge_info(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects);
+std::vector<float> mesh_edge_info(const float* tris_bt, int ntris, const int32_t* object_ntris, int nobjects, int arith);
 
 // The order in which Bullet's quantized BVH of one mesh visits its triangles (btBvhTriangleMeshShape with
 // quantized AABB compression, RocketSim.cpp:167; btOptimizedBvh::build, btQuantizedBvh::buildTree and the
@@ -36,6 +36,10 @@ std::vector<int> bvh_visit_order(const float* tris_bt, int ntris);
 
 // The built-in synthetic arena mesh (include/rlgpu_arena_mesh.h) in bullet units (uu / 50).
 std::vector<float> builtin_mesh_bt();
+
+// This host's rsqrtss table for the x86 arithmetic modes (host/x86_arith.cpp, rlgpu_arith.h): 2 << *bits
+// entries; throws rlgpu::Error(RLGPU_ERR_UNSUPPORTED) when the host has none usable.
+const std::vector<uint32_t>& x86_rsqrt_table_or_throw(int* bits);
 
 // Axis cell of a coordinate, the same IEEE operations as the device's grid_cell.
 inline int grid_cell_host(float x, float o, float inv, int n) {

@@ -14,7 +14,7 @@
 // over the native RCCL communicator (host/rccl_collective.cpp).
 //
 //   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--f32-gemm] [--c2-model]
-//               [--rank r --world N --rccl-id FILE]
+//               [--rank r --world N --rccl-id FILE [--rccl-nonce STR]]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
     rlgpu_learner_config cfg;
     rlgpu_learner_default_config(&cfg);
     long iterations = 3;
-    std::string idFile;
+    std::string idFile, nonce;
     cfg.n_shared_layers = 2;
     cfg.shared_layers[0] = cfg.shared_layers[1] = 384;
     cfg.n_policy_layers = cfg.n_critic_layers = 3;
@@ -43,6 +43,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) cfg.rank = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) cfg.world = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rccl-id") && i + 1 < argc) idFile = argv[++i];
+        else if (!std::strcmp(argv[i], "--rccl-nonce") && i + 1 < argc) nonce = argv[++i];
         else if (!std::strcmp(argv[i], "--c2-model")) {
             cfg.n_shared_layers = 0;
             cfg.n_policy_layers = cfg.n_critic_layers = 2;
@@ -63,17 +64,37 @@ int main(int argc, char** argv) {
         rlgpu_collective coll{};
         if (cfg.world > 1) {
             if (idFile.empty()) throw std::runtime_error("--world > 1 needs --rccl-id FILE");
+            // The file carries the launch's nonce (--rccl-nonce, else $RLGPU_RUN_ID, else
+            // $TORCHELASTIC_RUN_ID) before the id: a reader accepts only a file of its own launch, so an
+            // id left over from an earlier run is never taken.
+            if (nonce.empty())
+                for (const char* e : {"RLGPU_RUN_ID", "TORCHELASTIC_RUN_ID"})
+                    if (const char* v = std::getenv(e); v && *v) {
+                        nonce = v;
+                        break;
+                    }
+            const std::string header = "RLGPUID1:" + nonce + "\n";
             uint8_t id[RLGPU_RCCL_ID_BYTES];
-            if (cfg.rank == 0) {  // write then rename: readers never see a partial id
+            if (cfg.rank == 0) {  // remove, write, check, rename: readers never see a partial or stale id
+                std::remove(idFile.c_str());
                 RLGC::RlgpuCheck(rlgpu_rccl_unique_id(id, sizeof id), "RCCL unique id");
                 const std::string tmp = idFile + ".tmp";
-                std::ofstream(tmp, std::ios::binary).write((const char*)id, sizeof id);
+                {
+                    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+                    f.write(header.data(), (std::streamsize)header.size());
+                    f.write((const char*)id, sizeof id);
+                    f.close();
+                    if (!f) throw std::runtime_error("cannot write " + tmp);
+                }
                 if (std::rename(tmp.c_str(), idFile.c_str()) != 0) throw std::runtime_error("cannot write " + idFile);
             } else {
                 for (int tries = 0;; tries++) {
                     std::ifstream f(idFile, std::ios::binary);
-                    if (f && f.read((char*)id, sizeof id) && f.gcount() == (std::streamsize)sizeof id) break;
-                    if (tries > 6000) throw std::runtime_error("timed out waiting for " + idFile);
+                    std::string h(header.size(), '\0');
+                    if (f && f.read(h.data(), (std::streamsize)h.size()) && h == header && f.read((char*)id, sizeof id) &&
+                        f.gcount() == (std::streamsize)sizeof id)
+                        break;
+                    if (tries > 6000) throw std::runtime_error("timed out waiting for " + idFile + " of this launch");
                     std::this_thread::sleep_for(std::chrono::milliseconds(10));
                 }
             }

@@ -239,6 +239,7 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     ec.n_rewards = cfg.n_rewards;
     ec.terminals = cfg.terminals;
     ec.n_terminals = cfg.n_terminals;
+    ec.arith = cfg.arith;
     env_ = new RLGC::EnvSetGPU(ec, s_);
     // ExampleMain registers its StepCallback (ExampleMain.cpp:233-283, 592): restated on the device
     RlgpuCheck(rlgpu_envset_enable_step_metrics(env_->handle(), 1), "step metrics");
@@ -541,10 +542,17 @@ void Learner::Learn() {
         globalM = (int64_t)m;
     }
     const int64_t batch = cfg_.batch_size > 0 ? cfg_.batch_size : globalM;
-    int64_t localBatch = cfg_.batch_size > 0 ? std::max<int64_t>(1, cfg_.batch_size / cfg_.world) : M;
-    // with several ranks every rank must take the same number of optimizer steps (one all-reduce each):
-    // the trajectory mode trains each rank's whole batch as one batch per epoch
-    if (trajMode() && hasColl_) localBatch = M;
+    const int64_t localBatch = cfg_.batch_size > 0 ? std::max<int64_t>(1, cfg_.batch_size / cfg_.world) : M;
+    // with several ranks in the trajectory mode the ranks hold different row counts, yet every rank
+    // must take the same optimizer steps (one all-reduce each): the batches are the reference's
+    // GetAllBatchesShuffled split of the global combined batch (ExperienceBuffer.cpp:117-162), and
+    // rank-local batch i is the same fraction [g0 / globalM, g1 / globalM) of this rank's rows
+    std::vector<std::pair<int64_t, int64_t>> trajRanges;
+    if (trajMode() && hasColl_) {
+        for (auto [g0, g1] : BatchRanges(globalM, batch, cfg_.overbatching != 0))
+            trajRanges.emplace_back(globalM ? g0 * M / globalM : 0, globalM ? g1 * M / globalM : 0);
+        if (trajRanges.empty()) trajRanges.emplace_back(0, 0);
+    }
     if (rows) lk::train_rows(T, P, 1 - oldTeam_, trainRows_, s_);
     for (int epoch = 0; epoch < cfg_.epochs; epoch++) {
         RlgpuCheck(rlgpu_permutation(M, cfg_.seed + (uint64_t)cfg_.rank, (uint64_t)(stats.iteration * cfg_.epochs + epoch),
@@ -555,8 +563,7 @@ void Learner::Learn() {
             lk::compose(trainRows_, perm_, M, permRows_, s_);
             order = permRows_;
         }
-        auto ranges = BatchRanges(M, localBatch, cfg_.overbatching != 0);
-        if (trajMode() && hasColl_ && ranges.empty()) ranges.emplace_back(0, 0);
+        const auto ranges = trajMode() && hasColl_ ? trajRanges : BatchRanges(M, localBatch, cfg_.overbatching != 0);
         for (auto [b0, b1] : ranges) {
             const bool whole = !rows && b0 == 0 && b1 == M;
             BatchAdvantageStats(v.adv, whole ? nullptr : order + b0, b1 - b0);
@@ -648,7 +655,11 @@ void Learner::ConsumeTrajectories() {
     J.cActs.Reserve(std::max<int64_t>(M, 1), s_);
     J.cTerms.Reserve(std::max<int64_t>(M, 1), s_);
     J.truncVals.Reserve(std::max<int64_t>(ntr, 1), s_);
-    if (M == 0) return;
+    if (M == 0) {
+        // a rank without finished rows still joins the return-sample all-gather the others make
+        if (hasColl_ && cfg_.return_samples > 0) FeedReturnStat(J.cRet.p, {}, 0);
+        return;
+    }
     // combinedTraj -> tensors (Learner.cpp:863-912): the complete trajectories in the order they ended
     lk::TrajRecs R{J.rp.p, J.rstart.p, J.rlen.p, J.rcode.p, J.rtidx.p, J.roff.p};
     lk::traj_gather(R, K, J.Tmax, P, W, ACT, v.obs, v.masks, v.actions, v.logp, v.rewards, v.terms, J.cObs.p, J.cMasks.p,

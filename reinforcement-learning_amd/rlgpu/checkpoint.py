@@ -279,8 +279,11 @@ def load(learner, folder, allow_missing_models=True):
             name = MODEL_NAMES[mi]
             o, c = ppo.model_range(mi)
             p = model_path(path, name, "_OPTIM")
-            if not os.path.exists(p) or os.path.getsize(p) == 0:
-                warnings.warn(f"no optimizer found at {p}, optimizer will be reset")
+            if not os.path.exists(p) or os.path.getsize(p) == 0 or not os.path.exists(OPTIM_TOOL):
+                # the reference resets a model's optimizer whose state it cannot use (Models.cpp:168-186)
+                usable = os.path.exists(p) and os.path.getsize(p) > 0
+                why = "readable (rlgpu_optim_lt is not built)" if usable else "found"
+                warnings.warn(f"no optimizer {why} at {p}, optimizer will be reset")
                 m[o:o + c].zero_()
                 v[o:o + c].zero_()
                 continue

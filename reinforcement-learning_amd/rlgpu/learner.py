@@ -179,6 +179,7 @@ class LearnerConfig:
                                            # with carry-over (rlgpu_learner_config.experience_mode)
         self.ts_per_itr = 0                # mode 1: PPOLearnerConfig::tsPerItr (0 = rollout_len * players)
         self.experience_capacity = 0       # mode 1: per-player step store rows (0 = automatic)
+        self.arith = 0                     # the reference build's Bullet arithmetic (rlgpu.arith; 0 = MSVC x64)
         self.rewards = None                # EnvCreateFn reward list (rlgpu.plugins.reward specs); None = ExampleMain's
         self.terminals = None              # terminal conditions (rlgpu.plugins.terminal specs); None = ExampleMain's
         self.mesh = None                   # arena collision meshes (rlgpu.mesh.ArenaMesh); None = the built-in synthetic arena
@@ -221,7 +222,7 @@ class _CConfig(ctypes.Structure):
                 ("rewards", ctypes.c_void_p), ("n_rewards", ctypes.c_int32),
                 ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32),
                 ("experience_mode", ctypes.c_int32), ("ts_per_itr", ctypes.c_int64),
-                ("experience_capacity", ctypes.c_int32)]
+                ("experience_capacity", ctypes.c_int32), ("arith", ctypes.c_int32)]
 
 
 class _CBatch(ctypes.Structure):
@@ -343,6 +344,7 @@ class Learner:
         c.deterministic, c.train_gemm, c.infer_fp16 = int(cfg.deterministic), cfg.train_gemm, int(cfg.infer_fp16)
         c.frame_stack = cfg.frame_stack
         c.experience_mode, c.ts_per_itr, c.experience_capacity = cfg.experience_mode, cfg.ts_per_itr, cfg.experience_capacity
+        c.arith = cfg.arith
         c.rank, c.world = rank, world
         self._coll = None
         coll = None

@@ -181,15 +181,17 @@ def procedural_soccar(arc_segments=10, length_segments=36, goal_segments=10):
     return ArenaMesh(objs)
 
 
-def edge_info(mesh):
+def edge_info(mesh, arith=0):
     """The internal-edge records the env set builds for `mesh` (rlgpu_mesh_edge_info): [ntris, 4]
     float32 -- the angle to the neighbour across edges V0V1, V1V2, V2V0 (2 pi: no neighbour) and the
-    TRI_INFO_* flags as int32 bits (1 << 30: the triangle has a record)."""
+    TRI_INFO_* flags as int32 bits (1 << 30: the triangle has a record).  arith: RLGPU_ARITH_* (the
+    build whose arithmetic the records are made in; 0 = the reference's MSVC x64 build)."""
     L = _bind()
-    L.rlgpu_mesh_edge_info.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    L.rlgpu_mesh_edge_info.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p]
     out = np.zeros((mesh.num_tris, 4), np.float32)
     _lib.check(L.rlgpu_mesh_edge_info(mesh.tris.ctypes.data, mesh.num_tris, mesh.object_ntris.ctypes.data,
-                                      mesh.num_objects, out.ctypes.data), "rlgpu_mesh_edge_info")
+                                      mesh.num_objects, int(arith), out.ctypes.data), "rlgpu_mesh_edge_info")
     return out
 
 
@@ -204,11 +206,12 @@ def bvh_order(mesh):
     return out
 
 
-def box_triangle_queries(rot, centre, tri, cbt, lds_first=True):
+def box_triangle_queries(rot, centre, tri, cbt, lds_first=True, arith=0):
     """The env kernel's car-hitbox vs triangle narrowphase (Bullet's GJK / EPA query, include/rlgpu_mesh.h
     rlgpu_box_triangle_queries) on the device, one query per lane.  CUDA tensors: rot [n,3,3] (basis rows),
     centre [n,3], tri [n,3,3], cbt [n] -> [n,8] float32 (hit, normal xyz, point xyz, depth).  lds_first: the
-    penetration solver runs in a small LDS set first (the env kernel's policy), else in HBM only."""
+    penetration solver runs in a small LDS set first (the env kernel's policy), else in HBM only.  arith:
+    RLGPU_ARITH_* (include/rlgpu_arith.h)."""
     import torch
     rot = rot.reshape(-1, 9).contiguous().float()
     n = rot.shape[0]
@@ -217,9 +220,10 @@ def box_triangle_queries(rot, centre, tri, cbt, lds_first=True):
     cbt = cbt.reshape(n).contiguous().float()
     out = torch.zeros((n, 8), dtype=torch.float32, device=rot.device)
     L = _bind()
-    L.rlgpu_box_triangle_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 5 + [ctypes.c_int32, ctypes.c_void_p]
+    L.rlgpu_box_triangle_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 5 + [ctypes.c_int32, ctypes.c_int32,
+                                                                                     ctypes.c_void_p]
     _lib.check(L.rlgpu_box_triangle_queries(n, rot.data_ptr(), centre.data_ptr(), tri.data_ptr(), cbt.data_ptr(),
-                                            out.data_ptr(), int(bool(lds_first)),
+                                            out.data_ptr(), int(bool(lds_first)), int(arith),
                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
                "rlgpu_box_triangle_queries")
     return out

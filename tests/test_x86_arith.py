@@ -1,0 +1,267 @@
+"""The reference's x86 Bullet arithmetic (include/rlgpu_arith.h).
+
+Every x86 build of the reference compiles Bullet with BT_USE_SSE_IN_API (btScalar.h:113-137 MSVC,
+:217-223 GCC x86-64): btVector3::normalize is rsqrtss + one Newton step, the quaternion dot / product and
+btMatrix3x3::setRotation / getRotation take SSE branches, and the solver runs the _sse2 rows -- or, in
+build.ps1's MSVC build on an SSE4.1 + FMA3 CPU, the _sse4_1_fma3 contact and friction rows.  The oracle
+restates those branches (oracle/rsim_math.hpp, rsim_ref.cpp) and executes rsqrtss itself; the kernels
+(csrc/dmath.hpp, env_contacts.hpp) follow the same operation order and look rsqrtss up in this host's
+table.
+
+CPU: the table against the instruction over every input of [1, 4) and every exponent; the DPPS / FMA3
+restatements against the instructions; the modes really differ; edge records per mode.
+GPU: every mode-dependent LinearMath operation, the box-triangle narrowphase and whole env trajectories
+bit-exact against the oracle in each mode, and a >= 10k arena-step run reporting the largest relative
+error of obs / rewards / GAE advantages against the x86 oracle.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from tests_util import arena_diff, random_actions
+
+MODES = (0, 1, 2)  # RLGPU_ARITH_MSVC_X64, GCC_X64, SCALAR
+
+
+def _bits(x):
+    return np.ascontiguousarray(x, np.float32).view(np.uint32)
+
+
+# ------------------------------------------------------------------ CPU
+def test_rsqrt_table_equals_the_instruction_everywhere():
+    """The kernels' table lookup == this host's rsqrtss on all 2^24 inputs of [1, 4), on random inputs of
+    every exponent and on the special values (zero, denormal, inf, NaN, negative)."""
+    from rlgpu import arith
+    table = arith.rsqrt_table()
+    assert table[1] >= 1 and table[0].size == 2 << table[1]
+    u = np.arange(1 << 24, dtype=np.uint32)
+    x = (((127 + (u >> 23)) << 23) | (u & 0x7fffff)).astype(np.uint32).view(np.float32)
+    np.testing.assert_array_equal(_bits(arith.rsqrtss_emulated(x, table)), _bits(oracle.rsqrtss(x)))
+    rng = np.random.default_rng(0)
+    r = rng.integers(0x00800000, 0x7f800000, 1 << 20, dtype=np.uint32).view(np.float32)
+    np.testing.assert_array_equal(_bits(arith.rsqrtss_emulated(r, table)), _bits(oracle.rsqrtss(r)))
+    sp = np.array([0x0, 0x80000000, 0x1, 0x7fffff, 0x80400000, 0x7f800000, 0xff800000, 0x7fc00000, 0xbf800000,
+                   0x00800000, 0x7f7fffff], np.uint32).view(np.float32)
+    got, want = arith.rsqrtss_emulated(sp, table), oracle.rsqrtss(sp)
+    same = (_bits(got) == _bits(want)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), (sp[~same], got[~same], want[~same])
+    c = arith.rsqrtss_emulated_c(r[:2000])  # the library's host copy of the emulation
+    np.testing.assert_array_equal(_bits(c), _bits(oracle.rsqrtss(r[:2000])))
+
+
+def test_dpps_and_fma_restatements_equal_the_instructions():
+    """_mm_dp_ps(a, b, 0x7f) == (x + y) + (z + 0) and _mm_fmadd_ss == std::fma, bit for bit (the MSVC
+    _sse4_1_fma3 rows); includes signed zeros and cancellations."""
+    if not oracle.has_sse41_fma3():
+        pytest.skip("host without SSE4.1 / FMA3")
+    rng = np.random.default_rng(1)
+    a = rng.standard_normal((200000, 3)).astype(np.float32) * np.float32(rng.choice([1e-20, 1, 1e20], (200000, 1)))
+    b = rng.standard_normal((200000, 3)).astype(np.float32)
+    a[:1000] = -0.0
+    b[1000:2000, 2] = -b[1000:2000, 0] * a[1000:2000, 0] / np.where(a[1000:2000, 2] == 0, 1, a[1000:2000, 2])
+    np.testing.assert_array_equal(_bits(oracle.dpps(a, b)), _bits(oracle.dpps(a, b, restated=True)))
+    x, y, z = (rng.standard_normal(500000).astype(np.float32) for _ in range(3))
+    z[:1000] = -(x[:1000] * y[:1000])
+    np.testing.assert_array_equal(_bits(oracle.fmadd(x, y, z)), _bits(oracle.fmadd(x, y, z, restated=True)))
+
+
+def _lm_inputs(n, seed):
+    """Rows of 24 floats for oracle.linear_math / rlgpu_linear_math_queries: random vectors, quaternions
+    (unit and not), rotation matrices from them and velocities."""
+    rng = np.random.default_rng(seed)
+    x = np.zeros((n, 24), np.float32)
+    q = rng.standard_normal((n, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True).astype(np.float32)
+    q[: n // 4] *= rng.uniform(0.5, 2.0, (n // 4, 1)).astype(np.float32)
+    x[:, :4] = q
+    x[:, 4:8] = rng.standard_normal((n, 4)).astype(np.float32)
+    R = oracle.linear_math(1, 2, x)[:, :9]  # scalar setRotation: rotations for ops 2 and 4
+    return x, R, rng
+
+
+def test_oracle_x86_modes_differ_from_scalar_within_rounding():
+    """The SSE branches are different operation orders of the same math: results agree with the scalar
+    ones to a few ulps, and differ in the last bits on a good share of inputs (the modes are live)."""
+    x, R, rng = _lm_inputs(20000, 2)
+    y = x.copy()
+    y[:, :9] = R
+    y[:, 9:12] = rng.uniform(-50, 50, (len(y), 3)).astype(np.float32)
+    y[:, 12:15] = rng.uniform(-40, 40, (len(y), 3)).astype(np.float32)
+    y[:, 15:18] = rng.uniform(-6, 6, (len(y), 3)).astype(np.float32)
+    v = x.copy()
+    v[:, :3] = rng.standard_normal((len(v), 3)).astype(np.float32) * 30
+    for op, inp, k in ((0, v, 3), (1, x, 9), (2, y, 4), (3, x, 4), (4, y, 12)):
+        s = oracle.linear_math(op, 2, inp)[:, :k]
+        m = oracle.linear_math(op, 0, inp)[:, :k]
+        g = oracle.linear_math(op, 1, inp)[:, :k]
+        np.testing.assert_array_equal(_bits(m), _bits(g), err_msg=f"op {op}: MSVC and GCC LinearMath are the same")
+        assert np.abs(m - s).max() <= 4e-6 * max(1.0, np.abs(s).max()), f"op {op}"
+        frac = (_bits(m) != _bits(s)).any(axis=1).mean()
+        assert frac > 0.01, f"op {op}: the SSE branch never changed a bit ({frac})"
+
+
+def test_edge_records_per_mode_library_equals_oracle():
+    """btGenerateInternalEdgeInfo normalises with btVector3::normalize and rotates with quatRotate, so the
+    records depend on the build: the library's equal the oracle's in every mode."""
+    from rlgpu.mesh import edge_info, procedural_soccar
+    mesh = procedural_soccar()
+    for mode in MODES:
+        got = edge_info(mesh, mode)
+        want = oracle.mesh_edge_info(mesh.tris, mesh.object_ntris, mode)
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg=f"mode {mode}")
+    assert not np.array_equal(edge_info(mesh, 0).view(np.uint32), edge_info(mesh, 2).view(np.uint32))
+
+
+def test_oracle_env_modes_diverge():
+    """Whole arena steps: the three builds give different trajectories (scalar vs SSE LinearMath, _sse2 vs
+    _sse4_1_fma3 rows), so a parity test in one mode says nothing about another."""
+    from rlgpu.state import ARENA
+    n, steps = 16, 60
+    envs = [oracle.EnvSet(n, seed=9, arith=m) for m in MODES]
+    rng = np.random.default_rng(3)
+    for _ in range(steps):
+        a = random_actions(envs[0].masks, rng)
+        for e in envs:
+            e.step(a, True)
+    st = [np.frombuffer(e.get_arenas().tobytes(), ARENA) for e in envs]
+    assert arena_diff(st[0], st[2]), "MSVC x64 and scalar arithmetic gave identical arenas"
+    assert arena_diff(st[0], st[1]), "_sse4_1_fma3 and _sse2 rows gave identical arenas"
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_linear_math_device_equals_oracle(gpu, mode):
+    """normalize, setRotation, getRotation, quaternion product and integrateTransform: the kernels'
+    dmath.hpp == the oracle's rsim_math.hpp bit for bit in every mode (20,000 inputs each)."""
+    import torch
+    from rlgpu import arith
+    x, R, rng = _lm_inputs(20000, 4)
+    y = x.copy()
+    y[:, :9] = R
+    y[:, 9:12] = rng.uniform(-50, 50, (len(y), 3)).astype(np.float32)
+    y[:, 12:15] = rng.uniform(-40, 40, (len(y), 3)).astype(np.float32)
+    y[:, 15:18] = rng.uniform(-6, 6, (len(y), 3)).astype(np.float32)
+    y[::7, 15:18] *= 1e-4  # small angular velocities: the Taylor branch
+    v = x.copy()
+    v[:, :3] = rng.standard_normal((len(v), 3)).astype(np.float32) * np.float32(10.0) ** rng.integers(-20, 20, (len(v), 1))
+    for op, inp, k in ((0, v, 3), (1, x, 9), (2, y, 4), (3, x, 4), (4, y, 12)):
+        want = oracle.linear_math(op, mode, inp)[:, :k]
+        got = arith.linear_math_queries(op, mode, torch.from_numpy(inp).to(gpu)).cpu().numpy()[:, :k]
+        bad = np.nonzero((_bits(got) != _bits(want)).any(axis=1))[0]
+        assert bad.size == 0, f"op {op} mode {mode}: {bad.size} rows differ, first {bad[:4]}: {got[bad[:2]]} vs {want[bad[:2]]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", (0, 2))
+def test_box_triangle_per_mode(gpu, mode):
+    """The GJK / EPA box-triangle query normalises the triangle normal, the margin support directions and
+    the fallback normal with btVector3::normalize: bit-exact against the oracle per mode."""
+    import torch
+    from rlgpu.mesh import box_triangle_queries
+    rng = np.random.default_rng(11)
+    n = 6000
+    q = rng.standard_normal((n, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    inp = np.zeros((n, 24), np.float32)
+    inp[:, :4] = q
+    rot = oracle.linear_math(1, 2, inp)[:, :9]
+    centre = rng.uniform(-1, 1, (n, 3)).astype(np.float32) * 0.6
+    tri = (rng.uniform(-1.5, 1.5, (n, 9)) + np.repeat(rng.uniform(-0.4, 0.4, (n, 3)), 3, axis=1)).astype(np.float32)
+    cbt = np.full(n, 0.042, np.float32)
+    want, _ = oracle.box_triangle(rot, centre, tri, cbt, arith=mode)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    got = box_triangle_queries(t(rot), t(centre), t(tri), t(cbt), True, mode).cpu().numpy()
+    assert want[:, 0].sum() > 100
+    bad = np.nonzero((_bits(got) != _bits(want)).any(axis=1))[0]
+    assert bad.size == 0, f"mode {mode}: {bad.size} queries differ, first {bad[:4]}"
+
+
+def _run_pair(gpu, mode, n, steps, seed, mesh=None, perturb_at=None):
+    """Env trajectories, kernel vs oracle in `mode`, bit-exact every step; returns the number of arena-steps."""
+    import torch
+    from rlgpu.env import EnvSet
+    from rlgpu.state import ARENA
+    g = EnvSet(n, seed=seed, device=gpu, mesh=mesh, arith=mode)
+    o = oracle.EnvSet(n, seed=seed, mesh=mesh, arith=mode, threads=8)
+    rng = np.random.default_rng(seed)
+    for t in range(steps):
+        if perturb_at is not None and t == perturb_at:  # throw the balls at the cars, cars at each other
+            st = np.frombuffer(o.get_arenas().tobytes(), ARENA).copy()
+            for i in range(n):
+                c = st["cars"][i]["body"]["pos"][i % 4]
+                d = c - st["ball"][i]["pos"]
+                st["ball"][i]["vel"] = (d / (np.linalg.norm(d) + 1e-6) * rng.uniform(10, 110)).astype(np.float32)
+                st["ball"][i]["angvel"] = rng.uniform(-6, 6, 3).astype(np.float32)
+            buf = np.frombuffer(st.tobytes(), np.uint8)
+            o.set_arenas(buf)
+            g.set_arenas(buf)
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True)
+        torch.cuda.synchronize()
+        d = arena_diff(np.frombuffer(g.get_arenas().tobytes(), ARENA), np.frombuffer(o.get_arenas().tobytes(), ARENA))
+        assert not d, f"mode {mode} step {t}: " + "\n".join(d)
+        np.testing.assert_array_equal(_bits(g.obs.cpu().numpy()), _bits(o.obs), err_msg=f"mode {mode} step {t}: obs")
+        np.testing.assert_array_equal(_bits(g.rewards.cpu().numpy()), _bits(o.rewards), err_msg=f"step {t}: rewards")
+        np.testing.assert_array_equal(g.terminals.cpu().numpy(), o.terminals, err_msg=f"step {t}: terminals")
+        np.testing.assert_array_equal(g.action_masks.cpu().numpy(), o.masks, err_msg=f"step {t}: masks")
+    return n * steps
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", (1, 2))
+def test_env_parity_other_modes(gpu, mode):
+    """The GCC x86-64 build and the scalar build (regression harness of rounds 1-3) on the procedural
+    SOCCAR mesh, kickoff then thrown balls: bit-exact every step.  (The default MSVC mode is what every
+    other env test runs.)"""
+    from rlgpu.mesh import procedural_soccar
+    _run_pair(gpu, mode, 64, 80, 17, mesh=procedural_soccar(), perturb_at=40)
+
+
+@pytest.mark.gpu
+def test_x86_env_relative_error_report(gpu):
+    """>= 10k arena-steps in the reference's own build (MSVC x64 arithmetic) on the procedural SOCCAR mesh --
+    kickoff, late game and perturbed contacts -- plus GAE over the collected rewards: the largest relative
+    error of obs, rewards and advantages against the oracle must be <= 1e-5 (north_star), masks and
+    terminals bit-exact.  The kernel follows the oracle's operations exactly, so the error is 0."""
+    import torch
+    from rlgpu import GAE
+    from rlgpu.env import EnvSet
+    from rlgpu.mesh import procedural_soccar
+    n, steps = 128, 100
+    mesh = procedural_soccar()
+    g = EnvSet(n, seed=23, device=gpu, mesh=mesh, arith=0)
+    o = oracle.EnvSet(n, seed=23, mesh=mesh, arith=0, threads=8)
+    rng = np.random.default_rng(23)
+    rel = {"obs": 0.0, "rewards": 0.0, "adv": 0.0}
+    R_g, R_o, T_o = [], [], []
+    from rlgpu.state import ARENA
+    for t in range(steps):
+        if t == 60:
+            st = np.frombuffer(o.get_arenas().tobytes(), ARENA).copy()
+            st["ball"]["vel"] = rng.uniform(-60, 60, st["ball"]["vel"].shape).astype(np.float32)
+            buf = np.frombuffer(st.tobytes(), np.uint8)
+            o.set_arenas(buf)
+            g.set_arenas(buf)
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True)
+        torch.cuda.synchronize()
+        go, gr = g.obs.cpu().numpy(), g.rewards.cpu().numpy()
+        rel["obs"] = max(rel["obs"], float((np.abs(go - o.obs) / np.maximum(np.abs(o.obs), 1e-30)).max()))
+        rel["rewards"] = max(rel["rewards"], float((np.abs(gr - o.rewards) / np.maximum(np.abs(o.rewards), 1e-30)).max()))
+        np.testing.assert_array_equal(g.terminals.cpu().numpy(), o.terminals)
+        np.testing.assert_array_equal(g.action_masks.cpu().numpy(), o.masks)
+        R_g.append(gr.copy())
+        R_o.append(o.rewards.copy())
+        T_o.append(np.repeat(o.terminals, 4).astype(np.int8))
+    rg, ro, tt = np.stack(R_g), np.stack(R_o), np.stack(T_o)
+    vals = np.random.default_rng(5).standard_normal(rg.shape).astype(np.float32)
+    ga, _, _ = GAE.compute_rollout(torch.from_numpy(rg).to(gpu), torch.from_numpy(tt).to(gpu),
+                                   torch.from_numpy(vals).to(gpu), None, None, 0.99, 0.95, 1.0, 0.0)
+    oa, _, _ = oracle.gae_rollout(ro, tt, vals, None, None, 0.99, 0.95, 1.0, 0.0)
+    rel["adv"] = float((np.abs(ga.cpu().numpy() - oa) / np.maximum(np.abs(oa), 1e-30)).max())
+    print(f"x86 (MSVC x64) arithmetic, {n * steps} arena-steps: max relative error {rel}")
+    assert n * steps >= 10000
+    assert all(v <= 1e-5 for v in rel.values()), rel
