@@ -231,6 +231,10 @@ typedef struct {
      * 0 = RLGPU_ARITH_MSVC_X64, the reference's own build (build.ps1); RLGPU_ARITH_GCC_X64; RLGPU_ARITH_SCALAR.
      * The x86 modes read this host's rsqrtss table at create (RLGPU_ERR_UNSUPPORTED on a host without one). */
     int32_t arith;
+    /* global index of arena 0 for the arenas' Philox streams (key seed, counter (arena, draw)): rank r of a
+     * data-parallel job passes r x num_arenas, so its arenas are the ones a single device holding every
+     * arena would step (0 for one device) */
+    int32_t arena_offset;
 } rlgpu_envset_config;
 
 /* Experience-append destinations of the fused step (Learner.cpp:823-861); any may be NULL. */

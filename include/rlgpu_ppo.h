@@ -66,6 +66,9 @@ typedef struct {
      * min(policy_lr, critic_lr) (PPOLearner::SetLearningRates, PPOLearner.cpp:652-663). */
     int32_t shared_layers[RLGPU_MAX_LAYERS];
     int32_t n_shared_layers;
+    /* global row number of this handle's row 0 for the sampler's Philox counter (row, step): rank r of a
+     * data-parallel job passes r x its rows, so the ranks draw what one device holding every row draws */
+    int64_t sample_row_offset;
 } rlgpu_ppo_config;
 
 /* fp32 GEMM arithmetic of the training path (libtorch fp32 Linear forward / backward in the

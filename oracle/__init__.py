@@ -79,16 +79,16 @@ class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0,
-                 mesh=None, rewards=None, terminals=None, arith=0):
+                 mesh=None, rewards=None, terminals=None, arith=0, arena_offset=0):
         """mesh: (tris [N, 9] float32 bullet units, object_ntris int32 [K]) or an object with
         .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh.
         rewards / terminals: structured arrays of rlgpu_reward_spec / rlgpu_terminal_spec records
         (include/rlgpu_env.h), None = ExampleMain's lists (the oracle restates them itself).
         arith: the reference build's Bullet arithmetic (include/rlgpu_arith.h: 0 MSVC x64, 1 GCC x86-64,
-        2 scalar)."""
+        2 scalar).  arena_offset: global index of arena 0 (rlgpu_envset_config.arena_offset)."""
         L = lib()
         L.oracle_env_create.restype = ctypes.c_void_p
-        L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for n in ("oracle_env_destroy", "oracle_env_step_first_half", "oracle_env_reset", "oracle_env_build_obs"):
             getattr(L, n).argtypes = [ctypes.c_void_p]
         L.oracle_env_step_second_half.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -99,7 +99,7 @@ class EnvSet:
         L.oracle_env_read.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
         self.L = L
         self.n = num_arenas
-        self.h = L.oracle_env_create(num_arenas, seed, tick_skip, action_delay, threads)
+        self.h = L.oracle_env_create(num_arenas, seed, tick_skip, action_delay, threads, arena_offset)
         L.oracle_env_set_max_episode_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.oracle_env_read_traj_terms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_env_set_max_episode_steps(self.h, max_episode_steps)
@@ -209,6 +209,21 @@ def sample_actions(logits16, masks, deterministic, seed, step, row0=0, f16=False
                   ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     f(_p(lg), _p(mk), n, A, int(deterministic), seed, step, row0, int(f16), _p(act), _p(lp))
     return act, lp
+
+
+def sampler_probs(logits16, masks, seed, step, row0=0, f16=False):
+    """The clamped probs [n, A] the sampler draws from and each row's uniform r [n] (oracle_sampler_probs)."""
+    lg = np.ascontiguousarray(logits16, np.uint16)
+    mk = np.ascontiguousarray(masks, np.uint8)
+    n, A = lg.shape
+    pr = np.empty((n, A), np.float32)
+    r = np.empty(n, np.float32)
+    f = lib().oracle_sampler_probs
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                  ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    f(_p(lg), _p(mk), n, A, seed, step, row0, int(f16), _p(pr), _p(r))
+    return pr, r
 
 
 def detmath_exp_log(x):

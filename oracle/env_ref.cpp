@@ -678,6 +678,7 @@ struct EnvSet {
     Plugins plug = example_main_plugins();
     Pool* pool = nullptr;
     int arith = RLGPU_ARITH_MSVC_X64;  // the reference build's arithmetic (oracle_env_set_arith)
+    int arena_offset = 0;              // global index of arena 0 (the arenas' Philox streams)
     World* own_world = nullptr;     // set by oracle_env_set_mesh
     std::vector<float> mesh_tris;   // its mesh, rebuilt when the arithmetic changes
     std::vector<int> mesh_obj;
@@ -721,8 +722,9 @@ using namespace orc;
 
 extern "C" {
 
-void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action_delay, int threads) {
+void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action_delay, int threads, int arena_offset) {
     EnvSet* e = new EnvSet();
+    e->arena_offset = arena_offset;
     e->n = num_arenas;
     e->seed = seed;
     e->tick_skip = tick_skip;
@@ -746,7 +748,7 @@ void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action
         for (int p = 0; p < RLGPU_PADS; p++) s.pads[p].is_active = 1;
     }
     // EnvSet ctor: reset all arenas (EnvSet.cpp:105-110)
-    e->par([&](int i) { reset_arena(e->arenas[i], e->seed, i, e->out(i).obs, e->out(i).masks); });
+    e->par([&](int i) { reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks); });
     return e;
 }
 
@@ -766,13 +768,13 @@ void oracle_env_set_arenas(void* h, int first, int count, const rlgpu_arena_stat
 
 void oracle_env_step_first_half(void* h) {
     EnvSet* e = (EnvSet*)h;
-    e->par([&](int i) { first_half(*e->w, e->arenas[i], e->seed, i, e->action_delay); });
+    e->par([&](int i) { first_half(*e->w, e->arenas[i], e->seed, i + e->arena_offset, e->action_delay); });
 }
 
 void oracle_env_step_second_half(void* h, const int32_t* actions) {
     EnvSet* e = (EnvSet*)h;
     e->par([&](int i) {
-        second_half(*e->w, e->arenas[i], e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, e->out(i));
+        second_half(*e->w, e->arenas[i], e->seed, i + e->arena_offset, e->tick_skip - e->action_delay, actions + 4 * i, e->out(i));
     });
 }
 
@@ -782,7 +784,7 @@ void oracle_env_reset(void* h) {
     e->par([&](int i) {
         if (e->terminals[i]) {
             e->terminals[i] = 0;
-            reset_arena(e->arenas[i], e->seed, i, e->out(i).obs, e->out(i).masks);
+            reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks);
         }
     });
 }
@@ -790,7 +792,7 @@ void oracle_env_reset(void* h) {
 void oracle_env_reset_arenas(void* h, const uint8_t* mask) {
     EnvSet* e = (EnvSet*)h;
     e->par([&](int i) {
-        if (!mask || mask[i]) reset_arena(e->arenas[i], e->seed, i, e->out(i).obs, e->out(i).masks);
+        if (!mask || mask[i]) reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks);
     });
 }
 
@@ -799,11 +801,11 @@ void oracle_env_step(void* h, const int32_t* actions, int reset_terminated) {
     EnvSet* e = (EnvSet*)h;
     e->par([&](int i) {
         rlgpu_arena_state& s = e->arenas[i];
-        first_half(*e->w, s, e->seed, i, e->action_delay);
+        first_half(*e->w, s, e->seed, i + e->arena_offset, e->action_delay);
         StepOut o = e->out(i);
-        second_half(*e->w, s, e->seed, i, e->tick_skip - e->action_delay, actions + 4 * i, o);
+        second_half(*e->w, s, e->seed, i + e->arena_offset, e->tick_skip - e->action_delay, actions + 4 * i, o);
         if (o.traj_term[0] == 2) std::memcpy(&e->trunc_obs[(size_t)i * 4 * RLGPU_OBS], o.obs, sizeof(float) * 4 * RLGPU_OBS);
-        if (reset_terminated && *o.terminal) reset_arena(s, e->seed, i, o.obs, o.masks);
+        if (reset_terminated && *o.terminal) reset_arena(s, e->seed, i + e->arena_offset, o.obs, o.masks);
     });
 }
 
@@ -864,6 +866,9 @@ void oracle_env_set_mesh(void* h, const float* tris, int ntris, const int* obj_n
 
 // The reference build's arithmetic (RLGPU_ARITH_*, include/rlgpu_arith.h) for every later step; the set's
 // edge records are rebuilt in it.
+// Global index of arena 0 for the arenas' Philox streams (rlgpu_envset_config.arena_offset).
+void oracle_env_set_arena_offset(void* h, int off) { ((EnvSet*)h)->arena_offset = off; }
+
 void oracle_env_set_arith(void* h, int arith) {
     EnvSet* e = (EnvSet*)h;
     e->arith = arith;

@@ -45,6 +45,7 @@ struct StepArgs {
     int metrics_players;       // this call is one of ExampleMain's every-4th "expensive" calls
     const Plugins* plug;       // the set's reward / terminal registry (device)
     int arith;                 // RLGPU_ARITH_* (rlgpu_envset_config.arith): copied into Aux::arith at launch
+    int arena_offset;          // global index of arena 0 (the arenas' Philox streams)
 };
 
 // ExampleMain's StepCallback (src/ExampleMain.cpp:233-283) on this arena's GameState as the
@@ -428,7 +429,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
                 sync(); P.mark(11);
             }
             if (t >= t1 + t2) break;
-            tick(A, g.mesh, l, valid, g.seed, arena, P, pregs, stdmin(kArenas, g.n - (int)blockIdx.x * kArenas));
+            tick(A, g.mesh, l, valid, g.seed, arena + g.arena_offset, P, pregs, stdmin(kArenas, g.n - (int)blockIdx.x * kArenas));
         }
     }
     // ---- builders: GameState::UpdateFromArena, terminals, rewards, obs, masks
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         }
         sync(); P.mark(13);
         if (g.reset_mode == 1) {
-            if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena);
+            if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena + g.arena_offset);
             sync(); P.mark(14);
             if (fused_reset && l < 4) build_obs_row(A, l);
             sync(); P.mark(14);
@@ -557,7 +558,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         }
         sync(); P.mark(14);
         if (do_reset && l == 0) {
-            kickoff_reset(A, g.seed, arena);
+            kickoff_reset(A, g.seed, arena + g.arena_offset);
             if (g.reset_mode == 2) g.terminals[arena] = 0;
         }
         sync(); P.mark(14);
@@ -910,6 +911,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.mesh = e->mesh;
     g.plug = e->d_plug;
     g.arith = e->cfg.arith;
+    g.arena_offset = e->cfg.arena_offset;
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
         g.metrics_players = (++e->metric_calls % 4) == 0;

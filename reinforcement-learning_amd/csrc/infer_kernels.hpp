@@ -42,6 +42,9 @@ constexpr int IT = 64 * IW;        // threads
 constexpr int IRW = IR / IW;       // rows per wave in the row-parallel phases
 constexpr int IMAX = 512;          // widest layer input / hidden layer
 constexpr int IPITCH = IMAX + 8;   // LDS row pitch (16-bit): 1040 B, rows 4 banks apart
+// the sampler's probs (ppo::sample_rows) in each row of Xs past its <= kMaxA 16-bit logits
+constexpr int kSampleProbs = 128;
+static_assert(ppo::kMaxA <= kSampleProbs && kSampleProbs * 2 + ppo::kMaxA * 4 <= IPITCH * 2, "probs fit a row of Xs");
 constexpr int IOUT = 128;          // widest output layer (4 x 32-column tiles)
 constexpr int kMaxLinear = 9;      // RLGPU_MAX_LAYERS hidden + the output layer
 
@@ -407,6 +410,7 @@ __global__ void __launch_bounds__(IT, 1) mlp_infer(InferArgs a) {
     {
         const uint16_t* lg[IRW];
         const uint8_t* mk[IRW];
+        float* pr[IRW];
         int row[IRW];
         bool ok[IRW];
 #pragma unroll
@@ -414,10 +418,11 @@ __global__ void __launch_bounds__(IT, 1) mlp_infer(InferArgs a) {
             const int r = w + IW * g;
             lg[g] = Xs[r];
             mk[g] = Ms + r * N;
+            pr[g] = reinterpret_cast<float*>(&Xs[r][kSampleProbs]);  // the row past its logits: the probs
             row[g] = r0 + r;
             ok[g] = Sel[r] != 0;
         }
-        ppo::sample_rows<IRW, F16>(lg, mk, N, a.det, a.seed, a.step, a.row0, row, ok, lane, a.act, a.logp);
+        ppo::sample_rows<IRW, F16>(lg, mk, pr, N, a.det, a.seed, a.step, a.row0, row, ok, lane, a.act, a.logp);
     }
     INFER_MARK(15);
 }

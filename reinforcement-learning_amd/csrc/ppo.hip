@@ -1125,13 +1125,14 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
             int m = (int)std::min<int64_t>(R, n - b);
             if (fused_ok(h, 0)) {
                 infer_fused(h, 0, false, d_obs + b * h->cfg.obs_size, m, 1, nullptr, d_masks + b * h->cfg.num_actions,
-                            deterministic, rng_step, d_actions + b, d_logp ? d_logp + b : nullptr, nullptr, 0, s, b);
+                            deterministic, rng_step, d_actions + b, d_logp ? d_logp + b : nullptr, nullptr, 0, s,
+                            b + h->cfg.sample_row_offset);
                 continue;
             }
             forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s);
             RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
-                               rng_step, b, d_actions + b, d_logp ? d_logp + b : nullptr);
+                               rng_step, b + h->cfg.sample_row_offset, d_actions + b, d_logp ? d_logp + b : nullptr);
             RLGPU_CHECK_HIP(hipGetLastError());
         }
     });
@@ -1171,13 +1172,15 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
                 if (fused_ok(h, 0)) {
                     infer_fused(h, 0, old != 0, d_obs + b * h->cfg.obs_size, m, 1, nullptr,
                                 d_masks + b * h->cfg.num_actions, deterministic, rng_step, d_actions + b,
-                                (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old, s, b);
+                                (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old, s,
+                                b + h->cfg.sample_row_offset);
                     continue;
                 }
                 forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s, old ? h->half_ver : h->half);
                 RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                    d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
-                                   rng_step, b, d_actions + b, (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
+                                   rng_step, b + h->cfg.sample_row_offset, d_actions + b,
+                                   (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
                 RLGPU_CHECK_HIP(hipGetLastError());
             }
         }

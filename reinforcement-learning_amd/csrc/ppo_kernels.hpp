@@ -45,24 +45,27 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
     p1 = e1 / s;
 }
 
-// InferActions: logits bf16 [n, A] -> action (int32), log prob.  Inverse-CDF multinomial on the
-// clamped probs (torch.multinomial normalises by their sum); argmax when deterministic.
-// Bit-exact against the CPU oracle (oracle/sampler_ref.c): IEEE + - * / only, exp / log by the
-// shared rs_expf / rs_logf (include/rlgpu_detmath.h), no FMA contraction, and every reduction in a
-// fixed order the oracle restates (xor-butterfly max / sum = pairwise tree, Hillis-Steele scan).
-// The Philox counter is (row0 + row, step): global row numbers, so chunked launches draw the same
-// uniforms as one launch.
+// InferActions: logits bf16 [n, A] -> action (int32), log prob (PPOLearner.cpp:78-184).  The probs are the
+// masked softmax clamped to [1e-11, 1]; deterministic: argmax (lowest index on ties); otherwise the
+// reference's CPU sampler (PPOLearner.cpp:157-178): r uniform in [0, 1), the first action whose running sum
+// of the clamped probs, accumulated in column order, reaches r (r <= running), the last column when none
+// does, and log(max(1e-12, p)) of the pick.  The uniform is a Philox draw of (seed, row0 + row, step) --
+// global row numbers, so chunked launches draw the same uniforms as one launch -- where the reference uses
+// an unseeded thread-local mt19937.
+// Bit-exact against the CPU oracle (oracle/sampler_ref.c): IEEE + - * / only, exp / log by the shared
+// rs_expf / rs_logf (include/rlgpu_detmath.h), no FMA contraction, max / sum by xor butterflies (= pairwise
+// trees), and the running sum sequential: one lane per row walks the row's probs staged in LDS.
 // row_sel (optional): only rows with (row_sel[row] != 0) == sel are written (mixed-policy inference).
 // RG rows, one wave, interleaved (each cross-lane step issues for all RG rows before the next, so
 // one wave hides the shuffle latency of RG independent rows): lg[g] = row g's A logits (global or
-// LDS), mk[g] its masks; writes act[row[g]], logp[row[g]] where ok[g].  sample_actions runs it with
-// RG = 1, the fused inference kernel (infer_kernels.hpp) with RG = 8 -- the per-row arithmetic is the
-// same, so both draw the same actions from the same logits.
+// LDS), mk[g] its masks, pr[g] A floats of LDS scratch for its probs; writes act[row[g]], logp[row[g]]
+// where ok[g].  sample_actions runs it with RG = 1, the fused inference kernel (infer_kernels.hpp) with
+// RG = 8 -- the per-row arithmetic is the same, so both draw the same actions from the same logits.
 template <int RG, bool F16>
-__device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], const uint8_t* const (&mk)[RG], int A,
-                                            int deterministic, uint64_t seed, uint64_t step, int64_t row0,
-                                            const int (&row)[RG], const bool (&ok)[RG], int lane, int32_t* act,
-                                            float* logp) {
+__device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], const uint8_t* const (&mk)[RG],
+                                            float* const (&pr)[RG], int A, int deterministic, uint64_t seed,
+                                            uint64_t step, int64_t row0, const int (&row)[RG], const bool (&ok)[RG],
+                                            int lane, int32_t* act, float* logp) {
 #pragma clang fp contract(off)
     const int a0 = 2 * lane, a1 = 2 * lane + 1;
     const bool in0 = a0 < A, in1 = a1 < A;
@@ -114,36 +117,46 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
 #pragma unroll
         for (int g = 0; g < RG; g++) pick[g] = bi[g];
     } else {
-        float pair[RG], inc[RG];
-#pragma unroll
-        for (int g = 0; g < RG; g++) inc[g] = pair[g] = p0[g] + p1[g];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1)
-#pragma unroll
-            for (int g = 0; g < RG; g++) {
-                float up = __shfl_up(inc[g], o, 64);
-                if (lane >= o) inc[g] += up;
-            }
+        // the probs into LDS (lane l holds actions 2l, 2l + 1), then lane g < RG walks row g
 #pragma unroll
         for (int g = 0; g < RG; g++) {
-            float total = __shfl(inc[g], 63, 64);
-            float u = (float)(philox(seed, (uint32_t)(row0 + row[g]), (uint32_t)step) >> 8) * (1.f / 16777216.f) * total;
-            float excl = inc[g] - pair[g];
-            bool hit = (u < inc[g]) && (u >= excl) && pair[g] > 0.f;
-            const unsigned long long bal = __ballot(hit), nz = __ballot(pair[g] > 0.f);
-            // no hit: u landed past the last positive pair by rounding -- take the last valid action
-            const int lsel = bal ? __ffsll((long long)bal) - 1 : 63 - __clzll((long long)nz);
-            int c = 2 * lsel;
-            float e = __shfl(excl, lsel, 64), q0 = __shfl(p0[g], lsel, 64), q1 = __shfl(p1[g], lsel, 64);
-            pick[g] = (u < e + q0 || q1 == 0.f) ? c : c + 1;
+            if (in0) pr[g][a0] = p0[g];
+            if (in1) pr[g][a1] = p1[g];
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int mine = A - 1;  // picked = cols - 1 when no running sum reaches r
+        if (lane < RG) {
+            const float* p = pr[0];
+            int rw = row[0];
+#pragma unroll
+            for (int g = 1; g < RG; g++)
+                if (lane == g) {
+                    p = pr[g];
+                    rw = row[g];
+                }
+            const float r = (float)(philox(seed, (uint32_t)(row0 + rw), (uint32_t)step) >> 8) * (1.f / 16777216.f);
+            float running = 0.f;
+            bool found = false;
+            for (int j = 0; j < A; j++) {
+                running += p[j];
+                if (!found && r <= running) {
+                    mine = j;
+                    found = true;
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < RG; g++) pick[g] = __shfl(mine, g, 64);
     }
 #pragma unroll
     for (int g = 0; g < RG; g++) {
         float pp0 = __shfl(p0[g], pick[g] >> 1, 64), pp1 = __shfl(p1[g], pick[g] >> 1, 64);
         if (lane == 0 && ok[g]) {
             act[row[g]] = pick[g];
-            if (logp) logp[row[g]] = rs_logf((pick[g] & 1) ? pp1 : pp0);
+            const float pp = (pick[g] & 1) ? pp1 : pp0;
+            if (logp) logp[row[g]] = rs_logf(1e-12f < pp ? pp : 1e-12f);  // log(std::max(1e-12f, p))
         }
     }
 }
@@ -152,14 +165,16 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
                                                      int deterministic, uint64_t seed, uint64_t step, int64_t row0,
                                                      int32_t* act, float* logp, const uint8_t* row_sel = nullptr,
                                                      int sel = 0) {
+    __shared__ float probs[4][kMaxA];  // one row of probs per wave (sample_rows' running sum)
     int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= n) return;
     if (row_sel && ((row_sel[row] != 0) != (sel != 0))) return;
     const uint16_t* const lg[1] = {logits + (int64_t)row * A};
     const uint8_t* const mk[1] = {masks + (int64_t)row * A};
+    float* const pr[1] = {probs[threadIdx.x >> 6]};
     const int rw[1] = {row};
     const bool ok[1] = {true};
-    sample_rows<1, F16>(lg, mk, A, deterministic, seed, step, row0, rw, ok, lane, act, logp);
+    sample_rows<1, F16>(lg, mk, pr, A, deterministic, seed, step, row0, rw, ok, lane, act, logp);
 }
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.

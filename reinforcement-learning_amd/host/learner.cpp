@@ -228,7 +228,9 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     ec.num_arenas = N;
     ec.tick_skip = cfg.tick_skip;
     ec.action_delay = cfg.action_delay;
-    ec.seed = cfg.seed * 1000003ull + (uint64_t)cfg.rank;
+    // one arena stream space for the whole job: rank r's arenas are arenas [r N, (r + 1) N) of it
+    ec.seed = cfg.seed * 1000003ull;
+    ec.arena_offset = cfg.rank * N;
     ec.save_rewards = 1;
     ec.max_episode_steps = (int32_t)(cfg.max_episode_duration * (120.0f / (float)cfg.tick_skip));
     ec.mesh_tris = cfg.mesh_tris;
@@ -271,6 +273,7 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     const int64_t rowsCap = cfg.experience_mode == RLGPU_EXP_TRAJECTORIES ? (int64_t)cfg.mini_batch_size : TP;
     pc.max_rows = (int32_t)std::max<int64_t>(std::min<int64_t>(cfg.mini_batch_size, rowsCap), std::min<int64_t>(P, 65536));
     pc.seed = cfg.seed;
+    pc.sample_row_offset = (int64_t)cfg.rank * P;  // rank r's players are players [r P, (r + 1) P) of the job
     pc.train_gemm = cfg.train_gemm;
     pc.infer_fp16 = cfg.infer_fp16;
     ppo_ = new PPOLearnerGPU(pc, s_);
@@ -440,11 +443,54 @@ void Learner::Consume() {
     hipCheck(hipStreamSynchronize(s_), "sync");
     if (oldTeam_ >= 0)
         for (int p = oldTeam_; p < P; p += 2) hostEnds_[p] = -1;  // team of player p is p % 2
-    std::vector<int64_t> idx(k);
+    if (!hasColl_) {
+        std::vector<int64_t> idx(k);
+        int32_t m = 0;
+        RlgpuCheck(rlgpu_sample_finished_rows(cfg_.seed, 0, stats.iteration, hostEnds_.data(), P, k, idx.data(), &m),
+                   "return samples");
+        FeedReturnStat(v.ret, idx, m);
+        return;
+    }
+    // Several ranks: the draws are made over the job's rows -- every rank's columns in rank order, as one
+    // device holding all of them would number them -- with one rank-independent generator, so a job of any
+    // world size feeds the WelfordStat the same returns in the same order.  Each rank fills the draws that
+    // fall in its own columns; an fp64 all-reduce of the draw vector (zeros elsewhere, exact) hands every
+    // rank all of them.
+    const int world = cfg_.world;
+    std::vector<float> mine((size_t)P), all((size_t)P * world);
+    for (int p = 0; p < P; p++) mine[p] = (float)hostEnds_[p];  // exact: ends < 2^24
+    if (coll_.allgather_f32(coll_.user, mine.data(), P, all.data()) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: trajectory-end all-gather failed");
+    std::vector<int32_t> gends((size_t)P * world);
+    for (size_t i = 0; i < gends.size(); i++) gends[i] = (int32_t)all[i];
+    const int64_t GP = (int64_t)P * world;
+    std::vector<int64_t> gidx(k), idx;
+    std::vector<int32_t> slot;
     int32_t m = 0;
-    RlgpuCheck(rlgpu_sample_finished_rows(cfg_.seed, cfg_.rank, stats.iteration, hostEnds_.data(), P, k, idx.data(), &m),
+    RlgpuCheck(rlgpu_sample_finished_rows(cfg_.seed, 0, stats.iteration, gends.data(), (int32_t)GP, k, gidx.data(), &m),
                "return samples");
-    FeedReturnStat(v.ret, idx, m);
+    for (int32_t i = 0; i < m; i++) {  // global row t * GP + gp -> this rank's row t * P + (gp - rank P)
+        const int64_t t = gidx[i] / GP, gp = gidx[i] % GP;
+        if (gp / P == cfg_.rank) {
+            idx.push_back(t * P + (gp - (int64_t)cfg_.rank * P));
+            slot.push_back(i);
+        }
+    }
+    std::vector<float> hs(std::max<size_t>(idx.size(), 1));
+    if (!idx.empty()) {
+        hipCheck(hipMemcpyAsync(sampleIdx_, idx.data(), idx.size() * sizeof(int64_t), hipMemcpyHostToDevice, s_),
+                 "sample idx");
+        lk::gather_samples(v.ret, sampleIdx_, (int32_t)idx.size(), samples_, s_);
+        hipCheck(hipMemcpyAsync(hs.data(), samples_, idx.size() * sizeof(float), hipMemcpyDeviceToHost, s_), "samples");
+        hipCheck(hipStreamSynchronize(s_), "sync");
+    }
+    std::vector<double> draw((size_t)std::max(m, 1), 0.0);
+    for (size_t j = 0; j < idx.size(); j++) draw[slot[j]] = (double)hs[j];
+    if (m > 0 && coll_.allreduce_sum_f64(coll_.user, draw.data(), m) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: return-sample all-reduce failed");
+    std::vector<float> got((size_t)std::max(m, 1));
+    for (int32_t i = 0; i < m; i++) got[i] = (float)draw[i];
+    returnStat.Increment(got.data(), m);
 }
 
 // WelfordStat::Increment over the sampled returns (Learner.cpp:959-967); ranks may hold different

@@ -35,7 +35,7 @@ class _Cfg(ctypes.Structure):
                 ("entropy_scale", ctypes.c_float), ("max_grad_norm", ctypes.c_float),
                 ("max_rows", ctypes.c_int32), ("seed", ctypes.c_uint64), ("train_gemm", ctypes.c_int32),
                 ("infer_fp16", ctypes.c_int32), ("shared_layers", ctypes.c_int32 * MAX_LAYERS),
-                ("n_shared_layers", ctypes.c_int32)]
+                ("n_shared_layers", ctypes.c_int32), ("sample_row_offset", ctypes.c_int64)]
 
 GEMM_F32X6, GEMM_F32, GEMM_F16X3 = 0, 1, 2  # rlgpu_ppo_config.train_gemm (include/rlgpu_ppo.h)
 

@@ -1,11 +1,14 @@
 """Action sampling (PPOLearner::InferActionsFromModels, GigaLearnCPP/src/private/GigaLearnCPP/PPO/
-PPOLearner.cpp:78-184): the GPU sampler against the CPU oracle (oracle/sampler_ref.c), which restates
-the kernel's operation order.  Given the same 16-bit logits, masks and Philox uniforms the action
-indices and log probs must agree BIT FOR BIT (north_star: discrete action indices bit-exact) -- for
-the fused inference kernel, the layer-by-layer path, max_rows chunking, a shared head and fp16.
+PPOLearner.cpp:78-184): the GPU sampler against the CPU oracle (oracle/sampler_ref.c).  The draw is the
+reference's CPU sampler (PPOLearner.cpp:157-178: sequential running sum of the clamped probs, the first
+column with r <= running, cols - 1 when none, log(max(1e-12, p))); the softmax is in the kernel's
+operation order.  Given the same 16-bit logits, masks and Philox uniforms the action indices and log
+probs must agree BIT FOR BIT (north_star: discrete action indices bit-exact) -- for the fused inference
+kernel, the layer-by-layer path, max_rows chunking, a shared head and fp16.
 
-CPU part: the shared exp / log kernels against libm (known answers) and the oracle sampler's
-semantics (argmax, masks, frequencies).
+CPU part: the shared exp / log kernels against libm (known answers), the oracle's draw against a numpy
+transcription of the reference loop on the same probs and uniforms, and the sampler's semantics
+(argmax, masks, frequencies).
 """
 import numpy as np
 import pytest
@@ -62,6 +65,44 @@ def test_oracle_sampler_semantics():
     # the global row counter: a chunk at row0 draws what the whole batch draws for those rows
     b, _ = oracle.sample_actions(logits[1000:], masks[1000:], False, 42, 3, row0=1000)
     np.testing.assert_array_equal(b, a[1000:])
+
+
+def reference_cpu_draw(pr, r):
+    """PPOLearner.cpp:157-178 in float32: running += p in column order, first j with r <= running, else the
+    last column; log(std::max(1e-12f, p))."""
+    n, A = pr.shape
+    act = np.full(n, A - 1, np.int64)
+    for i in range(n):
+        running = np.float32(0)
+        for j in range(A):
+            running = np.float32(running + pr[i, j])
+            if r[i] <= running:
+                act[i] = j
+                break
+    p = pr[np.arange(n), act]
+    return act, np.log(np.maximum(np.float32(1e-12), p).astype(np.float64)).astype(np.float32)
+
+
+def test_oracle_draw_is_the_reference_cpu_loop():
+    """Zero disagreement with the reference's CPU inverse CDF on 16,384 rows x 4 steps given the same
+    probs and uniforms, including rows whose uniform lands past the probs' rounded
+    total (picked = the last column, as the reference does)."""
+    rng = np.random.default_rng(3)
+    n, A = 16384, 90
+    logits = _bf16_bits(rng.standard_normal((n, A)) * 3)
+    masks = (rng.random((n, A)) < 0.6).astype(np.uint8)
+    masks[:, 0] = 1
+    for step in (0, 1, 2, 12345):
+        a, lp = oracle.sample_actions(logits, masks, False, 77, step)
+        pr, r = oracle.sampler_probs(logits, masks, 77, step)
+        ra, rlp = reference_cpu_draw(pr, r)
+        np.testing.assert_array_equal(a, ra)
+        np.testing.assert_allclose(lp, rlp, rtol=3e-7, atol=1e-7)  # rs_logf vs libm log: <= 2 ulp
+    # a uniform past every running sum takes the last column (here: masked) -- the reference's fallback
+    pr = np.full((1, A), np.float32(1e-11))
+    pr[0, 0] = np.float32(0.5)
+    ra, _ = reference_cpu_draw(pr, np.float32([0.75]))
+    assert ra[0] == A - 1
 
 
 def _gpu_logits16(p, o, fp16):
