@@ -531,6 +531,7 @@ void Learner::AllReduceGrads() {
 void Learner::BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int64_t n) {
     if (!hasColl_) {
         if (d_idx) {
+            NeedLearnRows(n, "the batch-advantage gather");
             lk::gather_f32(d_adv, d_idx, n, badv_, s_);
             ppo_->AdvantageStats(badv_, n);
         } else {
@@ -548,6 +549,14 @@ void Learner::BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int6
     MomentsMeanStd(m, st);
     hipCheck(hipMemcpyAsync(ppo_->adv_stats(), st, sizeof(st), hipMemcpyHostToDevice, s_), "adv stats");
     hipCheck(hipStreamSynchronize(s_), "sync");
+}
+
+// Every consumer of the per-row learn scratch checks its row count against the capacity first: an
+// undersized buffer is an RLGPU_ERR_INVALID_ARG naming the consumer, never a device fault.
+void Learner::NeedLearnRows(int64_t n, const char* what) const {
+    if (n > permCap_)
+        throw rlgpu::Error(RLGPU_ERR_INVALID_ARG, std::string("Learner: ") + what + " needs " + std::to_string(n) +
+                                                      " rows of learn scratch, " + std::to_string(permCap_) + " reserved");
 }
 
 // the per-row learn scratch (shuffle, row selection, batch advantages) for M rows
@@ -601,11 +610,14 @@ void Learner::Learn() {
     }
     if (rows) lk::train_rows(T, P, 1 - oldTeam_, trainRows_, s_);
     for (int epoch = 0; epoch < cfg_.epochs; epoch++) {
+        NeedLearnRows(M, "the shuffle");
         RlgpuCheck(rlgpu_permutation(M, cfg_.seed + (uint64_t)cfg_.rank, (uint64_t)(stats.iteration * cfg_.epochs + epoch),
                                      perm_, s_),
                    "shuffle");
         const int32_t* order = perm_;
         if (rows) {
+            NeedLearnRows(M, "the team row selection");
+            if (M > (int64_t)T * (P / 2)) throw rlgpu::Error(RLGPU_ERR_INVALID_ARG, "Learner: team rows exceed T * P / 2");
             lk::compose(trainRows_, perm_, M, permRows_, s_);
             order = permRows_;
         }

@@ -206,6 +206,7 @@ private:
     int32_t* permRows_ = nullptr; // permCap_ rows each (T * P; grown to the combined batch in the
     float* badv_ = nullptr;       // trajectory mode, whose row count has no fixed bound)
     int64_t permCap_ = 0;
+    void NeedLearnRows(int64_t n, const char* what) const;
     void ReserveLearnRows(int64_t M);
     int32_t* truncRows_ = nullptr;
     int32_t* truncCount_ = nullptr;

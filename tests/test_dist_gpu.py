@@ -1,0 +1,107 @@
+"""Data parallelism through the real C++ Learner (host/learner.cpp), ranks on one GPU over gloo.
+
+* 2 ranks x 64 arenas equal 1 rank x 128 arenas: the arenas' and the sampler's random streams are global
+  (rlgpu_envset_config.arena_offset, rlgpu_ppo_config.sample_row_offset), and the return samples are drawn
+  over the job's rows with one generator, so the two jobs collect the same rollouts and feed the
+  WelfordStat the same returns (identical statistics); the parameters after the iterations agree to fp32
+  summation order (the minibatches of the two jobs hold different rows; AdamW's first steps move each
+  parameter by +-lr, so a flipped sign of a near-zero gradient component shows as a 2 lr difference).
+  PPOLearner.cpp:360-374,521-526; SURVEY.md 8e.
+* the trajectory mode (experience_mode 1) with a rank that finishes no trajectory in an iteration: it
+  still joins the return-sample all-gather and every batch's all-reduces, so nothing hangs
+  and the ranks stay identical.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q, kw, iters):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "reinforcement-learning_amd"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rlgpu.learner import Learner, LearnerConfig
+        k = dict(kw)
+        per_rank = k.pop("per_rank", {})
+        k.update(per_rank.get(rank, {}))
+        L = Learner(LearnerConfig(train_against_old_versions=False, **k), device="cuda:0", rank=rank, world=world)
+        out = {"rank": rank, "rewards": [], "ret": []}
+        for _ in range(iters):
+            L.iterate()
+            torch.cuda.synchronize()
+            if k.get("experience_mode", 0) == 0:
+                out["rewards"].append(L.rewards.cpu().numpy().copy())
+            out["ret"].append((L.return_stat.n, L.return_stat.mean, L.return_stat.m2))
+        out["params"] = L.ppo.flat().cpu().numpy().copy()
+        out["steps"] = L.total_steps
+        q.put(out)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _run(world, kw, iters):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kw, iters)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=280) for _ in range(world)], key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.timeout(400)
+def test_two_ranks_equal_one_rank(gpu):
+    import torch  # noqa: F401
+    kw = dict(num_arenas=64, rollout_len=16, mini_batch_size=1024, seed=5)
+    two = _run(2, kw, 2)
+    one = _run(1, dict(kw, num_arenas=128), 2)[0]
+    # the same rollouts: rank r's players are players [256 r, 256 (r + 1)) of the one-rank job
+    for it in range(2):
+        got = np.concatenate([two[0]["rewards"][it], two[1]["rewards"][it]], axis=1)
+        np.testing.assert_array_equal(got.view(np.uint32), one["rewards"][it].view(np.uint32), err_msg=f"iteration {it}")
+    # the same return statistics (the same samples in the same order), bit for bit
+    for it in range(2):
+        assert two[0]["ret"][it] == two[1]["ret"][it] == one["ret"][it], (it, two[0]["ret"][it], one["ret"][it])
+    assert two[0]["steps"] == two[1]["steps"] == one["steps"]
+    np.testing.assert_array_equal(two[0]["params"], two[1]["params"])
+    d = np.abs(two[0]["params"] - one["params"])
+    lr = 2.5e-4
+    close = d <= 1e-6 + 1e-5 * np.abs(one["params"])
+    print(f"2 x 64 vs 1 x 128 arenas: {close.mean():.5f} of {d.size} parameters within 1e-5, max |diff| {d.max():.3g}")
+    assert d.max() <= 4 * lr * 1.01
+    assert close.mean() >= 0.98
+
+
+@pytest.mark.timeout(400)
+def test_trajectory_mode_rank_without_finished_rows(gpu):
+    """Rank 0's episodes cannot end inside its small step store (300 s episodes, 80 rows), so it brings no
+    rows; rank 1's (0.2 s episodes) do.  Both ranks run 3 iterations to the end with the same parameters
+    and return statistics."""
+    kw = dict(num_arenas=16, experience_mode=1, experience_capacity=80, ts_per_itr=512, mini_batch_size=512, seed=7,
+              per_rank={0: dict(max_episode_duration=300.0), 1: dict(max_episode_duration=0.2)})
+    res = _run(2, kw, 3)
+    np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
+    assert res[0]["ret"] == res[1]["ret"]
+    assert res[1]["ret"][-1][0] > 0  # rank 1's samples reached both ranks' statistics
