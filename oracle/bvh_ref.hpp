@@ -15,6 +15,7 @@
 //     their mean, leaves with centre > split swapped to the front in order, the 1/3 balance fallback.
 // Returns order[k] = the triangle (index within the mesh) visited k-th.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <utility>
 #include <vector>
@@ -92,17 +93,52 @@ struct Builder {
         if (k <= s + bal || k >= e - 1 - bal) k = s + (n >> 1);
         return k;
     }
+    // buildTree's nodes in the order it emits them (depth first, left first): node i covers leaf positions
+    // [ns[i], ne[i]), nskip[i] = the node after its subtree (the stackless walk's escape index)
+    std::vector<int> ns, ne, nskip;
     void build(int s, int e) {
-        if (e - s == 1) return;
-        const int axis = split_axis(s, e);
-        const int k = split_index(s, e, axis);
-        build(s, k);
-        build(k, e);
+        const int me = (int)ns.size();
+        ns.push_back(s);
+        ne.push_back(e);
+        nskip.push_back(0);
+        if (e - s > 1) {
+            const int axis = split_axis(s, e);
+            const int k = split_index(s, e, axis);
+            build(s, k);
+            build(k, e);
+        }
+        nskip[me] = (int)ns.size();
     }
 };
 
-// tris: ntris x 9 floats (bullet units), one mesh (collision object)
-inline std::vector<int> leaf_order(const float* tris, int ntris) {
+// The walk of one mesh's BVH (walkStacklessQuantizedTree / ...AgainstRay, btQuantizedBvh.cpp:676-740,
+// 479-590): nodes in array order, a subtree skipped (escape index) when its box misses the query, the
+// overlapping leaves reported in leaf order.  Bullet tests quantized node boxes, which contain the exact ones,
+// and processTriangle then applies the exact triangle AABB test (btConvexConcaveCollisionAlgorithm.cpp:71-138);
+// testing exact boxes here drops the same triangles earlier, so the reported set and order are Bullet's.
+struct Tree {
+    std::vector<int> ns, ne, nskip;  // node -> leaf positions [ns, ne), escape index
+    std::vector<V> mn, mx;           // node boxes: the union of their triangles' exact AABBs
+    // calls f(k) for every leaf position k whose triangle box overlaps [qmn, qmx], in leaf order
+    template <class F>
+    void walk(V qmn, V qmx, F&& f) const {
+        const int n = (int)ns.size();
+        for (int i = 0; i < n;) {
+            const bool hit = !(qmn.x > mx[i].x || qmx.x < mn[i].x || qmn.y > mx[i].y || qmx.y < mn[i].y ||
+                               qmn.z > mx[i].z || qmx.z < mn[i].z);
+            if (!hit) {
+                i = nskip[i];
+                continue;
+            }
+            if (ne[i] - ns[i] == 1) f(ns[i]);
+            i++;
+        }
+    }
+};
+
+// tris: ntris x 9 floats (bullet units), one mesh (collision object); tree (optional): the node hierarchy
+// over the leaf positions with exact triangle boxes
+inline std::vector<int> leaf_order(const float* tris, int ntris, Tree* tree = nullptr) {
     std::vector<int> order;
     if (ntris <= 0) return order;
     V lo(1e18f, 1e18f, 1e18f), hi(-1e18f, -1e18f, -1e18f);
@@ -143,6 +179,36 @@ inline std::vector<int> leaf_order(const float* tris, int ntris) {
     b.build(0, ntris);
     order.resize(ntris);
     for (int k = 0; k < ntris; k++) order[k] = b.leaves[k].tri;
+    if (tree) {
+        tree->ns = b.ns;
+        tree->ne = b.ne;
+        tree->nskip = b.nskip;
+        const int nn = (int)b.ns.size();
+        std::vector<V> lmn(ntris), lmx(ntris);  // exact triangle boxes by leaf position
+        for (int k = 0; k < ntris; k++) {
+            const float* p = tris + 9 * (size_t)order[k];
+            V a(p[0], p[1], p[2]), z = a;
+            for (int v = 1; v < 3; v++)
+                for (int i = 0; i < 3; i++) {
+                    a[i] = std::min(a[i], p[3 * v + i]);
+                    z[i] = std::max(z[i], p[3 * v + i]);
+                }
+            lmn[k] = a;
+            lmx[k] = z;
+        }
+        tree->mn.assign(nn, V());
+        tree->mx.assign(nn, V());
+        for (int i = nn - 1; i >= 0; i--) {  // children follow their parent: fold leaves bottom-up per node
+            V a = lmn[b.ns[i]], z = lmx[b.ns[i]];
+            for (int k = b.ns[i] + 1; k < b.ne[i]; k++)
+                for (int c = 0; c < 3; c++) {
+                    a[c] = std::min(a[c], lmn[k][c]);
+                    z[c] = std::max(z[c], lmx[k][c]);
+                }
+            tree->mn[i] = a;
+            tree->mx[i] = z;
+        }
+    }
     return order;
 }
 

@@ -220,11 +220,15 @@ void World::set_mesh(const float* p, int n, const int* obj_ntris, int nobjects) 
     }
     // btBvhTriangleMeshShape per object (RocketSim.cpp:167): the order its quantized BVH visits the triangles
     tri_visit.resize(n);
+    obj_t0.assign(nobj, 0);
+    obj_tree.assign(nobj, bvh::Tree());  // an object without triangles keeps an empty tree
     for (int t0 = 0; t0 < n;) {
         int t1 = t0;
         while (t1 < n && tri_obj[t1] == tri_obj[t0]) t1++;
-        std::vector<int> order = bvh::leaf_order(p + (size_t)t0 * 9, t1 - t0);
+        const int o = tri_obj[t0];
+        std::vector<int> order = bvh::leaf_order(p + (size_t)t0 * 9, t1 - t0, &obj_tree[o]);
         for (int k = 0; k < t1 - t0; k++) tri_visit[t0 + k] = t0 + order[k];
+        obj_t0[o] = t0;
         t0 = t1;
     }
     ArithScope scope(arith);
@@ -423,18 +427,23 @@ struct Sim {
         V d = to - from;
         // the ray cell's statics in creation order (btRSBroadphase::rayTest): mesh objects, then planes;
         // every object keeps a hit only when strictly closer, so the first one wins a tie
-        // mesh triangles in BVH visit order (btBvhTriangleMeshShape::performRaycast)
-        for (int k = 0; k < w.ntris; k++) {
-            const int t = w.tri_visit[k];
-            V n;
-            const float f = ray_triangle(w.tri[(size_t)t * 3], w.tri[(size_t)t * 3 + 1], w.tri[(size_t)t * 3 + 2], from, to,
-                                         best, n);
-            if (f >= 0.f) {
-                best = f;
-                obj = 10;
-                nrm = n;
-            }
-        }
+        // mesh triangles in BVH visit order (btBvhTriangleMeshShape::performRaycast ->
+        // walkStacklessQuantizedTreeAgainstRay), objects in creation order; the walk is pruned by the
+        // segment's box grown by 0.1 (more than the edge tolerance can reach outside a triangle)
+        const V rmn(std::min(from.x, to.x) - 0.1f, std::min(from.y, to.y) - 0.1f, std::min(from.z, to.z) - 0.1f);
+        const V rmx(std::max(from.x, to.x) + 0.1f, std::max(from.y, to.y) + 0.1f, std::max(from.z, to.z) + 0.1f);
+        for (size_t o = 0; o < w.obj_tree.size(); o++)
+            w.obj_tree[o].walk(rmn, rmx, [&](int k) {
+                const int t = w.tri_visit[w.obj_t0[o] + k];
+                V n;
+                const float f = ray_triangle(w.tri[(size_t)t * 3], w.tri[(size_t)t * 3 + 1], w.tri[(size_t)t * 3 + 2],
+                                             from, to, best, n);
+                if (f >= 0.f) {
+                    best = f;
+                    obj = 10;
+                    nrm = n;
+                }
+            });
         // static planes: btStaticPlaneShape(normal, 0) at plane_p (identity basis); processAllTriangles
         // (btStaticPlaneShape.cpp:56-82) spans two triangles over the ray's AABB in the plane's frame
         for (int p = 0; p < 4; p++) {
@@ -1433,18 +1442,18 @@ struct Sim {
         if (dist < cbt) add_contact(key, n, on_plane, dist);
     }
     // triangles [t0, t1) of one mesh object, in BVH visit order (btConvexTriangleCallback)
-    void collide_sphere_mesh(int key, int t0, int t1) {
+    void collide_sphere_mesh(int key, int o) {
         V c = b[0].pos;
         float r = w.ball_radius;
         float ext = r + 0.08f;
         float cbt = pair_cbt(0, 10);
-        for (int k = t0; k < t1; k++) {  // the object's triangles in BVH visit order
-            const int t = w.tri_visit[k];
-            if (!aabb_overlap(c - V(ext, ext, ext), c + V(ext, ext, ext), w.tri_min[t], w.tri_max[t])) continue;
+        // the object's triangles whose box overlaps the sphere's, in BVH visit order
+        w.obj_tree[o].walk(c - V(ext, ext, ext), c + V(ext, ext, ext), [&](int k) {
+            const int t = w.tri_visit[w.obj_t0[o] + k];
             V pt, nrm;
             float depth;
             if (sphere_triangle(c, r, t, cbt, pt, nrm, depth)) add_contact(key, nrm, pt, depth, t);
-        }
+        });
     }
     static bool aabb_overlap(V a0, V a1, V b0, V b1) {
         return !(a0.x > b1.x || a1.x < b0.x || a0.y > b1.y || a1.y < b0.y || a0.z > b1.z || a1.z < b0.z);
@@ -1561,17 +1570,17 @@ struct Sim {
         sh.tri[2] = v[2];
         return gjk::box_triangle(b[bi].rot, car_box_center(bi), sh, cbt, nrm, point_b, depth, gjk_evals);
     }
-    void collide_box_mesh(int key, int bi, int t0, int t1) {
+    void collide_box_mesh(int key, int bi, int o) {
         V mn, mx;
         body_aabb(bi, b[bi].pos, b[bi].rot, mn, mx);
         float cbt = pair_cbt(bi, 10);
-        for (int k = t0; k < t1; k++) {  // the object's triangles in BVH visit order
-            const int t = w.tri_visit[k];
-            if (!aabb_overlap(mn, mx, w.tri_min[t], w.tri_max[t])) continue;
+        // the object's triangles whose box overlaps the body's, in BVH visit order
+        w.obj_tree[o].walk(mn, mx, [&](int k) {
+            const int t = w.tri_visit[w.obj_t0[o] + k];
             V n, pb;
             float d;
             if (box_triangle(bi, t, cbt, n, pb, d)) add_contact(key, n, pb, d, t);
-        }
+        });
     }
     // btSphereBoxCollisionAlgorithm::getSphereDistance (box = the car), manifold A = ball, B = car
     void collide_car_ball(int key, int bi) {
@@ -1664,16 +1673,13 @@ struct Sim {
         for (int bi = 0; bi < 5; bi++) {
             bool active = bi == 0 ? ball_awake : b[bi].active;
             if (active) {
-                for (int o = 0, t0 = 0; o < w.nobj; o++) {
-                    int t1 = t0;
-                    while (t1 < w.ntris && w.tri_obj[t1] == o) t1++;
+                for (int o = 0; o < w.nobj; o++) {
                     int key = bi * KSTAT + o;
                     if (bi == 0)
-                        collide_sphere_mesh(key, t0, t1);
+                        collide_sphere_mesh(key, o);
                     else
-                        collide_box_mesh(key, bi, t0, t1);
+                        collide_box_mesh(key, bi, o);
                     refresh(key);
-                    t0 = t1;
                 }
                 for (int p = 0; p < 4; p++) {
                     int key = bi * KSTAT + KOBJ + p;

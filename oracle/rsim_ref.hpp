@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "../include/rlgpu_env.h"
+#include "bvh_ref.hpp"
 #include "edge_ref.hpp"
 #include "rsim_math.hpp"
 
@@ -27,6 +28,8 @@ struct World {
     std::vector<int> tri_obj;
     std::vector<TriInfo> tri_info;  // internal-edge records (btGenerateInternalEdgeInfo, edge_ref.hpp)
     std::vector<int> tri_visit;     // each object's triangles in Bullet's BVH visit order (bvh_ref.hpp)
+    std::vector<int> obj_t0;        // first triangle of each object
+    std::vector<bvh::Tree> obj_tree;  // each object's BVH nodes (the walk that finds a query's triangles)
     int arith = RLGPU_ARITH_MSVC_X64;  // the build whose arithmetic the edge records are made in (rsim_math.hpp)
     void set_mesh(const float* tris_bt, int n, const int* obj_ntris, int nobjects);
     float kick_x[5], kick_y[5];

@@ -3,7 +3,7 @@
 * C2 / C3 per GPU (4,096 arenas): the env kernel against the CPU oracle, bit for bit on every arena
   record, obs row, mask, reward, terminal and trajectory code, for 100 steps from kickoff and 100
   steps of a late-game stretch (the GPU alone runs ~600 steps first, then both sides continue from
-  its state).
+  its state), on the synthetic arena and on the bench's procedural SOCCAR mesh.
 * C4 per GPU (4,096 arenas, frame_stack = 4): a Learner rollout whose stacked rows hold the oracle
   env's obs in frame 0 bit for bit, then consume + learn.
 * C5 per GPU (8,192 arenas, actor / critic [2048] x 4, fp16 inference): a Learner iteration at a
@@ -49,13 +49,18 @@ def _check_step(g, o, what, terms=None):
         np.testing.assert_array_equal(terms.cpu().numpy(), o.traj_terms, err_msg=what + ": trajectory codes")
 
 
-def test_c2_env_parity_4096_arenas(gpu):
-    """4,096 arenas: 100 kickoff steps and a 100-step late-game stretch, bit-exact vs the oracle."""
+@pytest.mark.parametrize("mesh_kind", ["synthetic", "procedural"])
+def test_c2_env_parity_4096_arenas(gpu, mesh_kind):
+    """4,096 arenas: 100 kickoff steps and a 100-step late-game stretch, bit-exact vs the oracle -- on the
+    built-in 36-triangle arena and on the bench's own 8,800-triangle procedural SOCCAR stand-in (the oracle
+    walks each object's BVH as Bullet does, oracle/bvh_ref.hpp)."""
     import torch
     from rlgpu.env import EnvSet, StepOutputs
+    from rlgpu.mesh import procedural_soccar
     n, seed = 4096, 1234
-    g = EnvSet(n, seed=seed, device=gpu)
-    o = oracle.EnvSet(n, seed=seed, threads=THREADS)
+    mesh = procedural_soccar() if mesh_kind == "procedural" else None
+    g = EnvSet(n, seed=seed, device=gpu, mesh=mesh)
+    o = oracle.EnvSet(n, seed=seed, threads=THREADS, mesh=mesh)
     rng = np.random.default_rng(0)
     terms = torch.empty(4 * n, dtype=torch.int8, device=gpu)
     saw = set()
