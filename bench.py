@@ -66,13 +66,14 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(seconds=12.0, arenas=256):
+def cpu_baseline(mesh=None, mesh_name="synthetic", seconds=12.0, arenas=1024):
     """The CPU restatement (oracle/, reference threading model: contiguous arena chunks over a
-    pool) timed on this box's host cores on a bounded sample of the same env workload."""
+    pool) timed on this box's host cores on a bounded sample of the same env workload: the bench's
+    own arena mesh, whose objects the oracle queries through their BVHs as Bullet does."""
     import numpy as np
     import oracle
     cores = min(16, os.cpu_count() or 1)  # the box's CPU share is 16 (gpurun)
-    env = oracle.EnvSet(arenas, seed=1234, threads=cores)
+    env = oracle.EnvSet(arenas, seed=1234, threads=cores, mesh=mesh)
     rng = np.random.default_rng(7)
     steps = 0
     t0 = time.perf_counter()
@@ -87,11 +88,11 @@ def cpu_baseline(seconds=12.0, arenas=256):
     out = {"value": arenas * steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
            "cpu_model": cpu_model(),
            "sample": f"env only: {arenas} arenas x {steps} env steps of the oracle/ CPU restatement "
-                     f"({cores} threads, uniform valid actions, synthetic 36-triangle arena: the oracle scans every "
-                     f"triangle, so the SOCCAR-sized mesh would measure its brute force, not the reference's BVH)"}
+                     f"({cores} threads, uniform valid actions, the reference's x86 (MSVC x64) arithmetic, "
+                     f"the bench's {mesh_name} mesh walked through each object's BVH)"}
     # one thread, one 2v2 arena: physics ticks/s beside RocketSim's published 114,481 ticks/s
     # (v2.1.0, i5-11400); the oracle runs tickSkip 8 ticks per env step plus the builders
-    one = oracle.EnvSet(1, seed=99, threads=1)
+    one = oracle.EnvSet(1, seed=99, threads=1, mesh=mesh)
     steps1 = 0
     t1 = time.perf_counter()
     while time.perf_counter() - t1 < 4.0:
@@ -248,7 +249,7 @@ def main():
     # and LayerNorm launch, on the stream each runs on (rlgpu_kernel_timing)
     out["learn_roofline"] = learn_roofline(L, args.train_gemm)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline()
+        out["cpu_baseline"] = cpu_baseline(mesh, args.mesh)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -11,6 +11,7 @@
 #include "common.hpp"
 #include "env_builders.hpp"
 #include "mesh.hpp"
+#include "../../include/rlgpu_gamestate.h"
 
 namespace rl {
 
@@ -46,6 +47,7 @@ struct StepArgs {
     const Plugins* plug;       // the set's reward / terminal registry (device)
     int arith;                 // RLGPU_ARITH_* (rlgpu_envset_config.arith): copied into Aux::arith at launch
     int arena_offset;          // global index of arena 0 (the arenas' Philox streams)
+    float* reward_values;      // [players][nr] each reward's value before its weight, or null
 };
 
 // ExampleMain's StepCallback (src/ExampleMain.cpp:233-283) on this arena's GameState as the
@@ -502,6 +504,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
                 float o = reward_value(A, rs, l, me, bp, bv, pbv, A->a.goal != 0);
                 all += o * rs.weight;
                 if (l == 0 && g.last_rewards) g.last_rewards[(size_t)arena * nr + r] = o;
+                if (g.reward_values) g.reward_values[((size_t)arena * 4 + l) * nr + r] = o;
             }
             A->a.all_rewards[l] = all;
         }
@@ -761,6 +764,14 @@ static EnvConst make_env_const() {
 
 }  // namespace rl
 
+namespace rlgpu {
+void boost_pad_index_map(int out[RLGPU_PADS_FOR_MAP]) {
+    static_assert(RLGPU_PADS_FOR_MAP == RLGPU_PADS, "pad count");
+    const rl::EnvConst k = rl::make_env_const();
+    for (int i = 0; i < RLGPU_PADS; i++) out[i] = k.pad_map[i];
+}
+}  // namespace rlgpu
+
 // ------------------------------------------------------------------ C ABI
 struct rlgpu_envset {
     rlgpu_envset_config cfg;
@@ -777,6 +788,7 @@ struct rlgpu_envset {
     rl::Plugins plug{};                 // host copy of the reward / terminal registry
     rl::Plugins* d_plug = nullptr;      // its device copy (StepArgs::plug)
     int32_t* d_player_start = nullptr;  // EnvState::arenaPlayerStartIdx
+    float* d_reward_values = nullptr;   // [players][nr] per-reward values (rlgpu_envset_enable_reward_values) or null
 };
 
 namespace {
@@ -912,6 +924,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.plug = e->d_plug;
     g.arith = e->cfg.arith;
     g.arena_offset = e->cfg.arena_offset;
+    g.reward_values = g.build ? e->d_reward_values : nullptr;
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
         g.metrics_players = (++e->metric_calls % 4) == 0;
@@ -1135,7 +1148,38 @@ extern "C" int rlgpu_envset_destroy(rlgpu_envset* e) {
         (void)hipFree(e->d_cell_start);
         (void)hipFree(e->d_plug);
         (void)hipFree(e->d_player_start);
+        if (e->d_reward_values) (void)hipFree(e->d_reward_values);
         delete e;
+    });
+}
+
+extern "C" int rlgpu_envset_enable_reward_values(rlgpu_envset* e, int32_t enable) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        RLGPU_CHECK_HIP(hipDeviceSynchronize());
+        if (e->d_reward_values) (void)hipFree(e->d_reward_values);
+        e->d_reward_values = nullptr;
+        if (enable) {
+            const size_t n = (size_t)e->num_players * std::max(e->plug.nr, 1);
+            RLGPU_CHECK_HIP(hipMalloc(&e->d_reward_values, n * sizeof(float)));
+            RLGPU_CHECK_HIP(hipMemset(e->d_reward_values, 0, n * sizeof(float)));
+        }
+    });
+}
+
+extern "C" float* rlgpu_envset_reward_values(rlgpu_envset* e) { return e ? e->d_reward_values : nullptr; }
+
+extern "C" int rlgpu_envset_download_gamestates(rlgpu_envset* e, int32_t first, int32_t count, rlgpu_gamestate* h_out,
+                                                void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && h_out, "rlgpu_envset_download_gamestates: null argument");
+        RLGPU_REQUIRE(first >= 0 && count >= 0 && first + count <= e->cfg.num_arenas, "arena range out of bounds");
+        if (count == 0) return;
+        RLGPU_CHECK_HIP(hipStreamSynchronize((hipStream_t)stream));
+        std::vector<rlgpu_arena_state> rec((size_t)count);
+        RLGPU_CHECK_HIP(hipMemcpy2D(rec.data(), sizeof(rlgpu_arena_state), e->d_arenas + (size_t)first * rl::kRec, rl::kRec,
+                                    sizeof(rlgpu_arena_state), count, hipMemcpyDeviceToHost));
+        rlgpu::gamestates_from_arenas(rec.data(), count, e->cfg.tick_skip, h_out);
     });
 }
 

@@ -4,6 +4,8 @@
 #include <cstdint>
 #include <vector>
 
+#define RLGPU_PADS_FOR_MAP 34
+
 namespace rlgpu {
 
 struct MeshGrid {
@@ -40,6 +42,14 @@ std::vector<float> builtin_mesh_bt();
 // This host's rsqrtss table for the x86 arithmetic modes (host/x86_arith.cpp, rlgpu_arith.h): 2 << *bits
 // entries; throws rlgpu::Error(RLGPU_ERR_UNSUPPORTED) when the host has none usable.
 const std::vector<uint32_t>& x86_rsqrt_table_or_throw(int* bits);
+
+// GameState::UpdateFromArena on arena records (host/gamestate.cpp, include/rlgpu_gamestate.h), and the
+// pad index map it reads (GameState.cpp:11-51: CommonValues::BOOST_LOCATIONS[i] -> arena pad, env.hip)
+void boost_pad_index_map(int out[RLGPU_PADS_FOR_MAP]);
+}  // namespace rlgpu
+#include "../../include/rlgpu_gamestate.h"
+namespace rlgpu {
+void gamestates_from_arenas(const rlgpu_arena_state* rec, int count, int tick_skip, rlgpu_gamestate* out);
 
 // Axis cell of a coordinate, the same IEEE operations as the device's grid_cell.
 inline int grid_cell_host(float x, float o, float inv, int n) {

@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import alias as _alias
-from .state import ARENA
+from .state import ARENA, GAMESTATE
 
 OBS, ACTIONS, REWARDS, PADS, CARS = 167, 90, 13, 34, 4
 
@@ -82,12 +82,33 @@ def _bind():
     L.rlgpu_envset_enable_step_metrics.argtypes = [vp, i32]
     L.rlgpu_envset_step_metrics.argtypes = [vp, vp, vp, i32, vp]
     L.rlgpu_envset_step_metric_slots.argtypes = [vp, vp, vp]
+    L.rlgpu_envset_download_gamestates.argtypes = [vp, i32, i32, vp, vp]
+    L.rlgpu_gamestates_from_arenas.argtypes = [vp, i32, i32, vp]
+    L.rlgpu_envset_enable_reward_values.argtypes = [vp, i32]
+    L.rlgpu_envset_reward_values.argtypes = [vp]
+    L.rlgpu_envset_reward_values.restype = vp
     _bound = True
     return L
 
 
 def arena_state_size():
     return _lib.lib().rlgpu_arena_state_size()
+
+
+def gamestate_size():
+    return _lib.lib().rlgpu_gamestate_size()
+
+
+def gamestates_from_arenas(buf, tick_skip=8):
+    """GameState records (numpy GAMESTATE array) of wire-format arena records (rlgpu_gamestates_from_arenas,
+    GameState::UpdateFromArena on the record)."""
+    L = _bind()
+    buf = np.ascontiguousarray(buf, np.uint8)
+    count = buf.size // ARENA.itemsize
+    out = np.zeros(count, GAMESTATE)
+    _lib.check(L.rlgpu_gamestates_from_arenas(buf.ctypes.data_as(ctypes.c_void_p), count, int(tick_skip),
+                                              out.ctypes.data_as(ctypes.c_void_p)), "rlgpu_gamestates_from_arenas")
+    return out
 
 
 class EnvSet:
@@ -226,6 +247,27 @@ class EnvSet:
         count = buf.size // ARENA.itemsize
         _lib.check(_lib.lib().rlgpu_envset_set_arenas(self._h, first, count, buf.ctypes.data_as(ctypes.c_void_p)),
                    "set_arenas")
+
+    def gamestates(self, first=0, count=None, stream=None):
+        """RLGC::GameState records (numpy GAMESTATE array, rlgpu.state) of arenas [first, first+count) as the
+        last step left them: what the reference hands a StepCallbackFn (Learner.cpp:796-797)."""
+        count = self.num_arenas - first if count is None else count
+        out = np.zeros(count, GAMESTATE)
+        _lib.check(_bind().rlgpu_envset_download_gamestates(self._h, first, count, out.ctypes.data_as(ctypes.c_void_p),
+                                                            _lib.stream_ptr(stream)), "download_gamestates")
+        return out
+
+    def enable_reward_values(self, on=True):
+        """Every later builders launch writes each reward's value before its weight: reward_values() is then
+        a [num_players, num_rewards] device tensor (None while disabled)."""
+        _lib.check(_bind().rlgpu_envset_enable_reward_values(self._h, int(on)), "enable_reward_values")
+
+    def reward_values(self):
+        import torch
+        p = _bind().rlgpu_envset_reward_values(self._h)
+        if not p:
+            return None
+        return _alias(p, (self.num_players, max(self.num_rewards, 1)), torch.float32, self.device)
 
     # ---- ExampleMain's StepCallback metrics (include/rlgpu_env.h rlgpu_envset_step_metrics)
     STEP_METRIC_SLOTS = 32

@@ -49,3 +49,35 @@ def view(buf):
 
 def to_bytes(arr):
     return np.frombuffer(arr.tobytes(), np.uint8).copy()
+
+
+# RLGC::GameState records (rlgpu_gamestate, include/rlgpu_gamestate.h): RocketSim GetState units (uu, uu/s,
+# rad/s), rot = RotMat forward, right, up
+CAR_STATE = np.dtype([
+    ("pos", "<f4", 3), ("rot", "<f4", 9), ("vel", "<f4", 3), ("ang_vel", "<f4", 3),
+    ("is_on_ground", "u1"), ("has_jumped", "u1"), ("has_double_jumped", "u1"), ("has_flipped", "u1"),
+    ("is_flipping", "u1"), ("is_jumping", "u1"), ("is_supersonic", "u1"), ("is_auto_flipping", "u1"),
+    ("is_demoed", "u1"), ("world_contact_has_contact", "u1"), ("ball_hit_is_valid", "u1"), ("pad0", "u1"),
+    ("wheels_with_contact", "u1", 4), ("flip_rel_torque", "<f4", 3),
+    ("jump_time", "<f4"), ("flip_time", "<f4"), ("air_time", "<f4"), ("air_time_since_jump", "<f4"),
+    ("boost", "<f4"), ("time_spent_boosting", "<f4"), ("supersonic_time", "<f4"), ("handbrake_val", "<f4"),
+    ("auto_flip_timer", "<f4"), ("auto_flip_torque_scale", "<f4"), ("demo_respawn_timer", "<f4"),
+    ("world_contact_normal", "<f4", 3), ("car_contact_other_car_id", "<u4"), ("car_contact_cooldown_timer", "<f4"),
+    ("ball_hit_relative_pos_on_ball", "<f4", 3), ("ball_hit_ball_pos", "<f4", 3), ("ball_hit_extra_hit_vel", "<f4", 3),
+    ("ball_hit_tick_count_when_hit", "<i8"), ("ball_hit_tick_count_when_extra_impulse_applied", "<i8"),
+    ("last_controls", "<f4", 8),
+], align=True)
+PLAYER_STATE = np.dtype([
+    ("car", CAR_STATE), ("index", "<i4"), ("car_id", "<u4"), ("team", "<i4"),
+    ("events", "u1", 9), ("ball_touched_step", "u1"), ("ball_touched_tick", "u1"), ("pad0", "u1"),
+    ("prev_action", "<f4", 8),
+], align=True)
+# PlayerEventState order of PLAYER_STATE["events"]
+EVENTS = ("goal", "save", "assist", "shot", "shot_pass", "bump", "bumped", "demo", "demoed")
+GAMESTATE = np.dtype([
+    ("delta_time", "<f4"), ("goal_scored", "<i4"), ("last_touch_car_id", "<i4"), ("last_tick_count", "<u8"),
+    ("ball", np.dtype([("pos", "<f4", 3), ("rot", "<f4", 9), ("vel", "<f4", 3), ("ang_vel", "<f4", 3)], align=True)),
+    ("players", PLAYER_STATE, 4),
+    ("boost_pads", "u1", 34), ("boost_pads_inv", "u1", 34),
+    ("boost_pad_timers", "<f4", 34), ("boost_pad_timers_inv", "<f4", 34),
+], align=True)

@@ -1,0 +1,139 @@
+"""The reference-side plugin surface: RLGC::EnvCreateResult -> device registry translation and the host fallback
+for user plugins (reinforcement-learning_amd/facade/EnvSetGPU.hpp), and the GameState records a StepCallbackFn
+reads (include/rlgpu_gamestate.h).
+
+* translate (CPU): ExampleMain's EnvCreateFunc (src/ExampleMain.cpp:128-226) written against facade/RLGC.hpp
+  translates to the registry's default lists byte for byte; user classes go to the host (facade_test.cpp).
+* gamestates_from_arenas (CPU): GameState::UpdateFromArena (GameState.cpp:60-131) / Player::UpdateFromCar
+  (Player.cpp:8-25) on synthetic arena records: uu units, RotMat columns, ids / teams, ballTouchedStep's window,
+  the boost pads' inverted arrays.
+* fallback (GPU): an env set whose rewards / conditions are registry classes and one where user classes with the
+  same bodies run on the host step in lockstep; rewards, terminals and obs agree bit for bit, resets included.
+* download / reward values (GPU): rlgpu_envset_download_gamestates equals the restatement on get_arenas, and the
+  per-reward values' list-order weighted sum is the step's reward bit for bit (EnvSet.cpp:199-222).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "reinforcement-learning_amd", "rlgpu", "rlgpu_facade_test")
+
+
+def _run(*args, timeout=120):
+    if not os.path.exists(BIN):
+        pytest.fail(f"{BIN} is not built (make -C reinforcement-learning_amd)")
+    r = subprocess.run([BIN, *args], capture_output=True, text=True, timeout=timeout)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    return r
+
+
+def test_translate_example_main():
+    r = _run("translate")
+    assert r.returncode == 0 and "translate: ok" in r.stdout
+
+
+def _records(n, seed=0):
+    from rlgpu.state import ARENA
+    rng = np.random.default_rng(seed)
+    rec = np.zeros(n, ARENA)
+    raw = rec.view(np.uint8).reshape(n, -1)
+    raw[:] = rng.integers(0, 256, raw.shape, dtype=np.uint8)
+    f = lambda shape: rng.standard_normal(shape).astype(np.float32)  # noqa: E731
+    rec["ball"]["pos"] = f((n, 3))
+    rec["ball"]["rot"] = f((n, 9))
+    rec["ball"]["vel"] = f((n, 3))
+    rec["ball"]["angvel"] = f((n, 3))
+    for k, s in (("pos", 3), ("rot", 9), ("vel", 3), ("angvel", 3)):
+        rec["cars"]["body"][k] = f((n, 4, s))
+    rec["cars"]["boost"] = rng.uniform(0, 100, (n, 4)).astype(np.float32)
+    rec["cars"]["ball_hit_valid"] = rng.integers(0, 2, (n, 4))
+    rec["env"]["tick_count"] = rng.integers(100, 10_000, n)
+    # hits inside, at the edge of and outside the 8-tick window
+    rec["cars"]["ball_hit_tick"] = rec["env"]["tick_count"][:, None] - rng.integers(0, 12, (n, 4))
+    rec["pads"]["is_active"] = rng.integers(0, 2, (n, 34))
+    rec["pads"]["cooldown"] = rng.uniform(0, 10, (n, 34)).astype(np.float32)
+    for k in ("ev_bump", "ev_bumped", "ev_demo", "ev_demoed"):
+        rec["env"][k] = rng.integers(0, 2, (n, 4))
+    rec["env"]["prev_action"] = f((n, 4, 8))
+    return rec
+
+
+def test_gamestates_from_arenas_restates_update_from_arena():
+    from rlgpu import env
+    from rlgpu.state import GAMESTATE, EVENTS
+    assert env.gamestate_size() == GAMESTATE.itemsize
+    n, tick_skip = 64, 8
+    rec = _records(n)
+    gs = env.gamestates_from_arenas(rec.view(np.uint8), tick_skip)
+    assert gs.shape == (n,)
+    np.testing.assert_array_equal(gs["delta_time"], np.float32(tick_skip * np.float32(1 / 120)))
+    np.testing.assert_array_equal(gs["last_tick_count"], rec["env"]["tick_count"])
+    np.testing.assert_array_equal(gs["ball"]["pos"], rec["ball"]["pos"] * np.float32(50))
+    np.testing.assert_array_equal(gs["ball"]["vel"], rec["ball"]["vel"] * np.float32(50))
+    np.testing.assert_array_equal(gs["ball"]["ang_vel"], rec["ball"]["angvel"])
+    # RotMat forward / right / up = the btMatrix3x3's columns
+    np.testing.assert_array_equal(gs["ball"]["rot"].reshape(n, 3, 3), rec["ball"]["rot"].reshape(n, 3, 3).transpose(0, 2, 1))
+    P, C = gs["players"], rec["cars"]
+    np.testing.assert_array_equal(P["car"]["pos"], C["body"]["pos"] * np.float32(50))
+    np.testing.assert_array_equal(P["car"]["vel"], C["body"]["vel"] * np.float32(50))
+    np.testing.assert_array_equal(P["car"]["ang_vel"], C["body"]["angvel"])
+    np.testing.assert_array_equal(P["car"]["rot"].reshape(n, 4, 3, 3), C["body"]["rot"].reshape(n, 4, 3, 3).transpose(0, 1, 3, 2))
+    np.testing.assert_array_equal(P["car"]["boost"], C["boost"])
+    np.testing.assert_array_equal(P["car"]["wheels_with_contact"], C["wheel_contact"])
+    np.testing.assert_array_equal(P["index"], np.arange(4)[None].repeat(n, 0))
+    np.testing.assert_array_equal(P["car_id"], np.arange(1, 5)[None].repeat(n, 0))
+    np.testing.assert_array_equal(P["team"], (np.arange(4) & 1)[None].repeat(n, 0))
+    for k, e in (("bump", "ev_bump"), ("bumped", "ev_bumped"), ("demo", "ev_demo"), ("demoed", "ev_demoed")):
+        np.testing.assert_array_equal(P["events"][:, :, EVENTS.index(k)], rec["env"][e])
+    np.testing.assert_array_equal(P["prev_action"], rec["env"]["prev_action"])
+    # Player.cpp:17-22: touched this step = a valid hit at tick >= tickCount - tickSkip
+    tick = rec["env"]["tick_count"][:, None]
+    hit = C["ball_hit_tick"]
+    valid = C["ball_hit_valid"] != 0
+    np.testing.assert_array_equal(P["ball_touched_step"] != 0, valid & (hit >= tick - tick_skip))
+    np.testing.assert_array_equal(P["ball_touched_tick"] != 0, valid & (hit == tick - 1))
+    last = np.where(P["ball_touched_step"].any(1), 0, -1)
+    for i in range(4):  # the last toucher in player order
+        last = np.where(P["ball_touched_step"][:, i] != 0, i + 1, last)
+    np.testing.assert_array_equal(gs["last_touch_car_id"], last)
+    # the pads: a permutation of the arena's pads, the inverted arrays mirrored (GameState.cpp:109-126)
+    assert (np.sort(gs["boost_pad_timers"], 1) == np.sort(rec["pads"]["cooldown"], 1)).all()
+    np.testing.assert_array_equal(gs["boost_pads_inv"], gs["boost_pads"][:, ::-1])
+    np.testing.assert_array_equal(gs["boost_pad_timers_inv"], gs["boost_pad_timers"][:, ::-1])
+    np.testing.assert_array_equal(gs["goal_scored"] != 0, np.abs(rec["ball"]["pos"][:, 1] * np.float32(50)) > 5215.5)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_host_fallback_matches_registry(gpu):
+    r = _run("fallback", "256", "300", timeout=280)
+    assert r.returncode == 0 and "fallback:" in r.stdout and "FAIL" not in r.stdout
+
+
+@pytest.mark.gpu
+def test_download_gamestates_and_reward_values(gpu):
+    import torch
+    from rlgpu import env, plugins
+    E = env.EnvSet(64, seed=3)
+    E.enable_reward_values(True)
+    weights = plugins.example_main()[0]["weight"]
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for s in range(40):
+        a = torch.randint(0, env.ACTIONS, (E.num_players,), generator=g, dtype=torch.int32).to(gpu)
+        E.step_first_half()
+        E.step_second_half(a)
+        torch.cuda.synchronize()
+        gs = E.gamestates()
+        ref = env.gamestates_from_arenas(E.get_arenas(), E.tick_skip)
+        assert gs.tobytes() == ref.tobytes(), f"step {s}"
+        vals = E.reward_values().cpu().numpy()
+        assert vals.shape == (E.num_players, weights.size)
+        tot = np.zeros(E.num_players, np.float32)
+        for k in range(weights.size):  # allRewards[i] += out[i] * weight, list order
+            tot = (tot + vals[:, k] * weights[k]).astype(np.float32)
+        np.testing.assert_array_equal(tot.view(np.uint32), E.rewards.cpu().numpy().view(np.uint32))
+        E.reset()
+    E.close()
