@@ -111,6 +111,12 @@ def cpu_baseline(mesh=None, mesh_name="synthetic", seconds=12.0, arenas=1024):
                      "env_steps_per_s": c1["env_steps_per_s"], "cores": cores,
                      "sample": f"C1: 64 arenas, [256,256] actor/critic, T=64, {c1['iterations']} PPO iterations "
                                f"({c1['agent_steps']} agent-steps) of oracle env + torch CPU fp32 PPO"}
+    # the GAE microbenchmark's inputs through the CPU restatement of GAE::Compute (oracle/gae_ref.c), 1 thread
+    for lg in (21, 24):
+        r, t, v, tv = gae_inputs(lg)
+        t2 = time.perf_counter()
+        oracle.gae_flat(r, t, v, tv, 0.99, 0.95, 1.7, 200.0)
+        out.setdefault("gae_flat_ms", {})[f"M=2^{lg}"] = (time.perf_counter() - t2) * 1e3
     return out
 
 
@@ -137,6 +143,59 @@ def learn_roofline(L, train_gemm):
         out[name] = {"bound": "mfma" if gemm else "hbm", "achieved": ach, "peak": p, "unit": "TF/s" if gemm else "GB/s",
                      "frac": ach / p, "launches": n, "ms_total": ms, "avg_us": ms * 1e3 / n,
                      ("flops_total" if gemm else "bytes_total"): work}
+    return out
+
+
+def gae_inputs(lg):
+    """SURVEY.md 8d's GAE microbenchmark inputs: r ~ N(0,1), V ~ N(0,1), terminal NORMAL with p = 1/128 and
+    TRUNCATED with p = 1/512, seed 7, M = 2^lg agent-steps, one truncation value per TRUNCATED step."""
+    import numpy as np
+    M = 1 << lg
+    rng = np.random.default_rng(7)
+    r = rng.standard_normal(M).astype(np.float32)
+    v = rng.standard_normal(M).astype(np.float32)
+    u = rng.random(M)
+    t = np.where(u < 1 / 128, 1, np.where(u < 1 / 128 + 1 / 512, 2, 0)).astype(np.int8)
+    tv = rng.standard_normal(int((t == 2).sum())).astype(np.float32)
+    return r, t, v, tv
+
+
+def gae_micro(dev, reps=20):
+    """The GAE microbenchmark (gae_inputs) at M = 2^21 and 2^24: 21 algorithmic bytes per agent-step (r, V, A,
+    target, R f32 + the terminal byte; the truncation values are ~M/512 more floats).  The flat
+    episode-concatenated layout (GAE::Compute's own, rlgpu_gae_flat, which returns the clip portion to the
+    host) and the engine's [T = 128, N] rollout layout (rlgpu_gae_rollout); HIP events around each call on the
+    stream it runs on, inputs resident in HBM, median of `reps`."""
+    import torch
+    from rlgpu.gae import GAE
+    out = {"bytes_per_agent_step": 21, "peak_GBps": HBM_PEAK_GBS}
+    for lg in (21, 24):
+        r, t, v, tv = gae_inputs(lg)
+        M, ntr = r.size, tv.size
+        dr, dv, dt = (torch.from_numpy(x).to(dev) for x in (r, v, t))
+        dtv = torch.from_numpy(tv).to(dev) if ntr else None
+        row = {"M": M, "truncations": ntr}
+        T = 128
+        N = M // T
+        boot = torch.zeros(N, device=dev)
+        trv = torch.zeros(M, device=dev)
+        for name, call in (
+                ("flat", lambda: GAE.compute(dr, dt, dv, dtv, 0.99, 0.95, 1.7, 200.0)),
+                ("rollout", lambda: GAE.compute_rollout(dr.view(T, N), dt.view(T, N), dv.view(T, N), trv.view(T, N),
+                                                        boot, 0.99, 0.95, 1.7, 200.0))):
+            call()
+            torch.cuda.synchronize()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+            for i in range(reps):
+                ev[2 * i].record()
+                call()
+                ev[2 * i + 1].record()
+            torch.cuda.synchronize()
+            ms = sorted(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps))[reps // 2]
+            gbs = 21 * M / (ms * 1e-3) / 1e9
+            row[name] = {"ms_median": ms, "agent_steps_per_s": M / (ms * 1e-3), "achieved_GBps": gbs,
+                         "frac": gbs / HBM_PEAK_GBS}
+        out[f"M=2^{lg}"] = row
     return out
 
 
@@ -248,6 +307,8 @@ def main():
     # learn-phase roofline: one more (untimed) iteration with HIP events around every training GEMM
     # and LayerNorm launch, on the stream each runs on (rlgpu_kernel_timing)
     out["learn_roofline"] = learn_roofline(L, args.train_gemm)
+    if rank == 0 and world == 1:
+        out["gae_micro"] = gae_micro(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(mesh, args.mesh)
     if rank == 0:

@@ -53,7 +53,10 @@ float rlgpu_x86_rsqrtss_emulated(float x);
  * compare them with the oracle's restatement): op 0 btVector3::normalize v[3] -> v[3]; 1
  * btMatrix3x3::setRotation q[4] -> m[9]; 2 btMatrix3x3::getRotation m[9] -> q[4]; 3 btQuaternion product
  * a[4] b[4] -> q[4]; 4 btTransformUtil::integrateTransform of rot[9] pos[3] linvel[3] angvel[3] over 1/120 s
- * -> pos[3] rot[9].  d_in [n][24], d_out [n][12] floats (device).  Asynchronous on `stream`. */
+ * -> pos[3] rot[9]; 5 a wheel ray's btSubsimplexConvexCast (btCollisionWorld.cpp:277-310) of the segment
+ * from[3] (at 9) to[3] (at 12) against a resting body of basis rot[9] (at 0) and origin o[3] (at 15), a box of
+ * half extents h[3] (at 18, with its margin) or a sphere of radius r (at 21, > 0) -> hit, fraction, normal[3].
+ * d_in [n][24], d_out [n][12] floats (device).  Asynchronous on `stream`. */
 int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream);
 
 #ifdef __cplusplus

@@ -45,6 +45,8 @@ extern "C" {
 #define RLGPU_REWARDS 13      /* ExampleMain reward list (src/ExampleMain.cpp:132-177) */
 #define RLGPU_MAX_REWARDS 32  /* weighted rewards per env set (device registry) */
 #define RLGPU_MAX_TERMINALS 8 /* terminal conditions per env set */
+#define RLGPU_SS_KICKOFF 0        /* KickoffState */
+#define RLGPU_SS_FUZZED_KICKOFF 1 /* FuzzedKickoffState */
 
 /* Reward plugins of the device registry: RLGymCPP's CommonRewards (RG/Rewards/CommonRewards.h),
  * KickoffProximityReward2v2Enhanced (RG/Rewards/KickoffProximityReward2v2Enhanced.h) and ExampleMain's
@@ -235,6 +237,11 @@ typedef struct {
      * data-parallel job passes r x num_arenas, so its arenas are the ones a single device holding every
      * arena would step (0 for one device) */
     int32_t arena_offset;
+    /* EnvCreateResult::stateSetter (RLGPU_SS_*): KickoffState (RG/StateSetters/KickoffState.h), or
+     * FuzzedKickoffState (FuzzedKickoffState.h:7-26: the kickoff, then every car's position moved by
+     * RandFloat(-0.1, 0.1) uu per axis through CarState, RS/Sim/Car/Car.cpp:23-36) -- the skill tracker's
+     * (PolicyVersionManager.cpp:24-31).  The fuzz draws are the arena's Philox stream after the kickoff's. */
+    int32_t state_setter;
 } rlgpu_envset_config;
 
 /* Experience-append destinations of the fused step (Learner.cpp:823-861); any may be NULL. */

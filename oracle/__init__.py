@@ -79,16 +79,18 @@ class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0,
-                 mesh=None, rewards=None, terminals=None, arith=0, arena_offset=0):
+                 mesh=None, rewards=None, terminals=None, arith=0, arena_offset=0, state_setter=0):
         """mesh: (tris [N, 9] float32 bullet units, object_ntris int32 [K]) or an object with
         .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh.
         rewards / terminals: structured arrays of rlgpu_reward_spec / rlgpu_terminal_spec records
         (include/rlgpu_env.h), None = ExampleMain's lists (the oracle restates them itself).
         arith: the reference build's Bullet arithmetic (include/rlgpu_arith.h: 0 MSVC x64, 1 GCC x86-64,
-        2 scalar).  arena_offset: global index of arena 0 (rlgpu_envset_config.arena_offset)."""
+        2 scalar).  arena_offset: global index of arena 0 (rlgpu_envset_config.arena_offset).
+        state_setter: 0 KickoffState, 1 FuzzedKickoffState (rlgpu_envset_config.state_setter)."""
         L = lib()
         L.oracle_env_create.restype = ctypes.c_void_p
-        L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int]
         for n in ("oracle_env_destroy", "oracle_env_step_first_half", "oracle_env_reset", "oracle_env_build_obs"):
             getattr(L, n).argtypes = [ctypes.c_void_p]
         L.oracle_env_step_second_half.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -99,7 +101,7 @@ class EnvSet:
         L.oracle_env_read.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
         self.L = L
         self.n = num_arenas
-        self.h = L.oracle_env_create(num_arenas, seed, tick_skip, action_delay, threads, arena_offset)
+        self.h = L.oracle_env_create(num_arenas, seed, tick_skip, action_delay, threads, arena_offset, int(state_setter))
         L.oracle_env_set_max_episode_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.oracle_env_read_traj_terms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_env_set_max_episode_steps(self.h, max_episode_steps)
@@ -370,7 +372,8 @@ def fmadd(a, b, c, restated=False):
 
 def linear_math(op, arith, inp):
     """oracle_linear_math: the mode-dependent LinearMath operation `op` (0 normalize, 1 setRotation,
-    2 getRotation, 3 quaternion product, 4 integrateTransform) on rows of 24 floats -> [n, 12]."""
+    2 getRotation, 3 quaternion product, 4 integrateTransform, 5 wheel-ray convex cast) on rows of 24 floats
+    -> [n, 12]."""
     inp = np.ascontiguousarray(inp, np.float32).reshape(-1, 24)
     out = np.zeros((len(inp), 12), np.float32)
     f = lib().oracle_linear_math

@@ -599,8 +599,8 @@ void second_half(const World& w, rlgpu_arena_state& s, uint64_t seed, int idx, i
 }
 
 // EnvSet::ResetArena (EnvSet.cpp:275-304)
-void reset_arena(rlgpu_arena_state& s, uint64_t seed, int idx, float* obs, uint8_t* masks) {
-    kickoff(s, seed, idx);
+void reset_arena(rlgpu_arena_state& s, uint64_t seed, int idx, float* obs, uint8_t* masks, bool fuzz) {
+    kickoff(s, seed, idx, fuzz);
     rlgpu_env_extra& e = s.env;
     e.last_tick_count = e.tick_count;  // new GameState(arena)
     e.no_touch_time = 0;
@@ -679,6 +679,7 @@ struct EnvSet {
     Pool* pool = nullptr;
     int arith = RLGPU_ARITH_MSVC_X64;  // the reference build's arithmetic (oracle_env_set_arith)
     int arena_offset = 0;              // global index of arena 0 (the arenas' Philox streams)
+    bool fuzz = false;                 // FuzzedKickoffState (rlgpu_envset_config.state_setter)
     World* own_world = nullptr;     // set by oracle_env_set_mesh
     std::vector<float> mesh_tris;   // its mesh, rebuilt when the arithmetic changes
     std::vector<int> mesh_obj;
@@ -722,9 +723,11 @@ using namespace orc;
 
 extern "C" {
 
-void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action_delay, int threads, int arena_offset) {
+void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action_delay, int threads, int arena_offset,
+                        int state_setter) {
     EnvSet* e = new EnvSet();
     e->arena_offset = arena_offset;
+    e->fuzz = state_setter == 1;
     e->n = num_arenas;
     e->seed = seed;
     e->tick_skip = tick_skip;
@@ -748,7 +751,7 @@ void* oracle_env_create(int num_arenas, uint64_t seed, int tick_skip, int action
         for (int p = 0; p < RLGPU_PADS; p++) s.pads[p].is_active = 1;
     }
     // EnvSet ctor: reset all arenas (EnvSet.cpp:105-110)
-    e->par([&](int i) { reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks); });
+    e->par([&](int i) { reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks, e->fuzz); });
     return e;
 }
 
@@ -784,7 +787,7 @@ void oracle_env_reset(void* h) {
     e->par([&](int i) {
         if (e->terminals[i]) {
             e->terminals[i] = 0;
-            reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks);
+            reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks, e->fuzz);
         }
     });
 }
@@ -792,7 +795,7 @@ void oracle_env_reset(void* h) {
 void oracle_env_reset_arenas(void* h, const uint8_t* mask) {
     EnvSet* e = (EnvSet*)h;
     e->par([&](int i) {
-        if (!mask || mask[i]) reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks);
+        if (!mask || mask[i]) reset_arena(e->arenas[i], e->seed, i + e->arena_offset, e->out(i).obs, e->out(i).masks, e->fuzz);
     });
 }
 
@@ -805,7 +808,7 @@ void oracle_env_step(void* h, const int32_t* actions, int reset_terminated) {
         StepOut o = e->out(i);
         second_half(*e->w, s, e->seed, i + e->arena_offset, e->tick_skip - e->action_delay, actions + 4 * i, o);
         if (o.traj_term[0] == 2) std::memcpy(&e->trunc_obs[(size_t)i * 4 * RLGPU_OBS], o.obs, sizeof(float) * 4 * RLGPU_OBS);
-        if (reset_terminated && *o.terminal) reset_arena(s, e->seed, i + e->arena_offset, o.obs, o.masks);
+        if (reset_terminated && *o.terminal) reset_arena(s, e->seed, i + e->arena_offset, o.obs, o.masks, e->fuzz);
     });
 }
 
@@ -868,6 +871,8 @@ void oracle_env_set_mesh(void* h, const float* tris, int ntris, const int* obj_n
 // edge records are rebuilt in it.
 // Global index of arena 0 for the arenas' Philox streams (rlgpu_envset_config.arena_offset).
 void oracle_env_set_arena_offset(void* h, int off) { ((EnvSet*)h)->arena_offset = off; }
+// The state setter (RLGPU_SS_*): 1 = FuzzedKickoffState.  Resets from now on use it.
+void oracle_env_set_state_setter(void* h, int ss) { ((EnvSet*)h)->fuzz = ss == 1; }
 
 void oracle_env_set_arith(void* h, int arith) {
     EnvSet* e = (EnvSet*)h;

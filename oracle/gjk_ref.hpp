@@ -22,6 +22,7 @@
 // The product's restatement is reinforcement-learning_amd/csrc/gjk.hpp (independent code, index-based
 // EPA lists in per-lane scratch); the two agree bit for bit.
 #pragma once
+#include <cfloat>
 #include <cstdint>
 
 #include "rsim_math.hpp"
@@ -1100,5 +1101,72 @@ inline bool box_triangle(const M& R, V c, const Shapes& s, float cbt, V& normal,
     return true;
 }
 
+
+// ------------------------------------------------------------------ btSubsimplexConvexCast (wheel rays)
+// The convex branch of btCollisionWorld::rayTestSingleInternal (btCollisionWorld.cpp:277-310): the ray's point
+// shape (btSphereShape(0), margin 0, identity basis) cast from `from` to `to` against a resting convex body with
+// basis R and origin o by btSubsimplexConvexCast::calcTimeOfImpact (btSubSimplexConvexCast.cpp:30-153;
+// btConvexCast.h:25-29: 32 iterations, epsilon 0.0001, allowed penetration 0).  sphere_r > 0: btSphereShape
+// (margin = radius, btSphereShape.cpp:37-48); otherwise btBoxShape with half extents h including its margin
+// (btBoxShape.h:47-56).  True when Bullet reports the cast (fraction, normal = n.normalized()).
+inline V sphere_support(V d, float radius) {
+    V vn;
+    if (len2(d) < FLT_EPSILON * FLT_EPSILON)
+        vn = bt_normalize(V(-1.f, -1.f, -1.f));  // the static invalidVecNorm
+    else
+        vn = bt_normalize(d);
+    return vn * radius;  // getMargin() * vecnorm
+}
+inline V box_support(V d, V h) {  // btFsels(d, h, -h)
+    return V(d.x >= 0.f ? h.x : -h.x, d.y >= 0.f ? h.y : -h.y, d.z >= 0.f ? h.z : -h.z);
+}
+inline V interp3(V v0, V v1, float rt) {  // btVector3::setInterpolate3
+    const float s = 1.f - rt;
+    return V(s * v0.x + rt * v1.x, s * v0.y + rt * v1.y, s * v0.z + rt * v1.z);
+}
+inline bool ray_convex_cast(V from, V to, float sphere_r, V h, const M& R, V o, float& frac, V& normal) {
+    const M I = M::ident();
+    auto supA = [&](V d, V org) { return I * sphere_support(vmul(d, I), 0.f) + org; };
+    auto supB = [&](V d, V org) {
+        const V l = vmul(d, R);
+        return R * (sphere_r > 0.f ? sphere_support(l, sphere_r) : box_support(l, h)) + org;
+    };
+    Voronoi vs;
+    vs.reset();
+    const V linA = to - from, linB = o - o;
+    float lambda = 0.f;
+    V iA = from, iB = o;
+    const V r = linA - linB;
+    V sa = supA(-r, iA), sb = supB(r, iB);
+    V v = sa - sb;
+    int max_iter = 32;
+    V n(0.f, 0.f, 0.f);
+    float dist2 = len2(v);
+    while ((dist2 > 0.0001f) && max_iter--) {
+        sa = supA(-v, iA);
+        sb = supB(v, iB);
+        V w = sa - sb;
+        const float vdw = dot(v, w);
+        if (lambda > 1.f) return false;
+        if (vdw > 0.f) {
+            const float vdr = dot(v, r);
+            if (vdr >= -(FLT_EPSILON * FLT_EPSILON)) return false;
+            lambda = lambda - vdw / vdr;
+            iA = interp3(from, to, lambda);
+            iB = interp3(o, o, lambda);
+            w = sa - sb;
+            n = v;
+        }
+        if (!vs.in_simplex(w)) vs.add(w, sa, sb);
+        if (vs.closest(v))
+            dist2 = len2(v);
+        else
+            dist2 = 0.f;
+    }
+    frac = lambda;
+    normal = len2(n) >= FLT_EPSILON * FLT_EPSILON ? bt_normalize(n) : V(0.f, 0.f, 0.f);
+    if (dot(normal, r) >= -0.f) return false;
+    return true;
+}
 }  // namespace gjk
 }  // namespace orc

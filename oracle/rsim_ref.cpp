@@ -424,7 +424,6 @@ struct Sim {
         float best = 1.0f;
         int obj = -1;
         V nrm;
-        V d = to - from;
         // the ray cell's statics in creation order (btRSBroadphase::rayTest): mesh objects, then planes;
         // every object keeps a hit only when strictly closer, so the first one wins a tie
         // mesh triangles in BVH visit order (btBvhTriangleMeshShape::performRaycast ->
@@ -479,60 +478,25 @@ struct Sim {
                 }
             }
         }
-        // ball sphere (analytic; hits only from outside)
-        {
-            V oc = from - b[0].pos;
-            float a = dot(d, d), bb = dot(oc, d), c = dot(oc, oc) - w.ball_radius * w.ball_radius;
-            if (c > 0.f) {
-                float disc = bb * bb - a * c;
-                if (disc >= 0.f && bb < 0.f) {
-                    float f = (-bb - std::sqrt(disc)) / a;
-                    if (f >= 0.f && f < best) {
-                        best = f;
-                        obj = 0;
-                        nrm = bt_normalize((from + d * f) - b[0].pos);
-                    }
-                }
-            }
-        }
-        // other cars (OBB slab test, from outside); demoed cars still block (no response -> miss)
-        for (int ci = 1; ci <= 4; ci++) {
-            if (ci == self) continue;
-            V c = car_box_center(ci);
-            const M& R = b[ci].rot;
-            V lo = vmul(from - c, R), ld = vmul(d, R);  // into box frame (R^T * v)
-            float tmin = 0.f, tmax = best;
-            int axis = -1;
-            float sgn = 0.f;
-            bool ok = true;
-            for (int k = 0; k < 3 && ok; k++) {
-                float h = w.car_half[k];
-                if (std::fabs(ld[k]) < 1e-12f) {
-                    if (lo[k] < -h || lo[k] > h) ok = false;
-                    continue;
-                }
-                float inv = 1.f / ld[k];
-                float t1 = (-h - lo[k]) * inv, t2 = (h - lo[k]) * inv;
-                float s1 = -1.f;
-                if (t1 > t2) {
-                    std::swap(t1, t2);
-                    s1 = 1.f;
-                }
-                if (t1 > tmin) {
-                    tmin = t1;
-                    axis = k;
-                    sgn = s1;
-                }
-                if (t2 < tmax) tmax = t2;
-                if (tmin > tmax) ok = false;
-            }
-            if (ok && axis >= 0 && tmin < best) {
-                best = tmin;
-                obj = ci;
-                V ln;
-                ln[axis] = sgn;
-                nrm = R * ln;
-            }
+        // the dynamic bodies of the ray's cell in the cell list's order (list_key), the wheel's own car skipped
+        // (ClosestRayResultCallback's ignore object): btSubsimplexConvexCast of the ray's point against the ball's
+        // sphere or the car compound's box child (childWorldTrans = the body's transform * the hitbox offset,
+        // btCollisionWorld.cpp:339-400 without a dynamic AABB tree), kept when strictly closer and its normal is
+        // long enough (btCollisionWorld.cpp:285-307).  Every dynamic within reach is in the cell's list: a body
+        // sits in the 3x3x3 cells around its home cell (btRSBroadphase.cpp:182-200), wider than any wheel ray.
+        int order[5] = {0, 1, 2, 3, 4};
+        std::sort(order, order + 5, [&](int x, int y) { return list_key(x) < list_key(y); });
+        for (int k = 0; k < 5; k++) {
+            const int bi = order[k];
+            if (bi == self || best == 0.f) continue;  // btSingleRayCallback::process stops at fraction 0
+            float f;
+            V n;
+            const bool hit = bi == 0 ? gjk::ray_convex_cast(from, to, w.ball_radius, V(), b[0].rot, b[0].pos, f, n)
+                                     : gjk::ray_convex_cast(from, to, 0.f, w.car_half, b[bi].rot, car_box_center(bi), f, n);
+            if (!hit || !(len2(n) > 0.0001f) || !(f < best)) continue;
+            best = f;
+            obj = bi;
+            nrm = bt_normalize(n);  // castResult.m_normal.normalize()
         }
         if (obj < 0) return -1;
         frac = best;
@@ -2272,8 +2236,11 @@ void default_car(rlgpu_car& cs) {
     cs.ball_hit_extra_tick = -1;
 }
 
-// Arena::ResetToRandomKickoff (Arena.cpp:112-216) with Philox draws for std::shuffle.
-void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index) {
+// Arena::ResetToRandomKickoff (Arena.cpp:112-216) with Philox draws for std::shuffle; fuzz: then
+// FuzzedKickoffState::ResetArena (FuzzedKickoffState.h:17-25): per car GetState (pos, vel x BT_TO_UU),
+// pos += RandFloat(-0.1, 0.1) per axis (Math.cpp:54-57, a 24-bit Philox fraction in place of the engine's),
+// SetState (x UU_TO_BT, Car.cpp:23-36).
+void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index, bool fuzz) {
     const World& W = world();
     int order[5] = {0, 1, 2, 3, 4};
     for (int i = 4; i > 0; i--) {  // Fisher-Yates
@@ -2291,6 +2258,16 @@ void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index) {
             sim.set_car_state(ci, pos, W.kick_rot[team][k], 100.f / 3.f, true);
         }
     }
+    if (fuzz)
+        for (int ci = 0; ci < 4; ci++) {
+            Body& c = sim.b[ci + 1];
+            for (int k = 0; k < 3; k++) {
+                const float u = (float)(rng_next(seed, arena_index, s.env) >> 8) * (1.f / 16777216.f);
+                const float r = -0.1f + u * (0.1f - -0.1f);
+                c.pos[k] = (c.pos[k] * BT_TO_UU + r) * UU_TO_BT;
+                c.vel[k] = (c.vel[k] * BT_TO_UU) * UU_TO_BT;
+            }
+        }
     // ball: BallState() at rest (pos 0,0,BALL_REST_Z)
     sim.b[0].pos = V(0, 0, 93.15f) * UU_TO_BT;
     sim.b[0].rot = M::ident();
@@ -2467,13 +2444,19 @@ void oracle_linear_math(int op, int arith, const float* in, int64_t n, float* ou
         } else if (op == 3) {
             const Q q = orc::qmul(Q{p[0], p[1], p[2], p[3]}, Q{p[4], p[5], p[6], p[7]});
             o[0] = q.x, o[1] = q.y, o[2] = q.z, o[3] = q.w;
-        } else {
+        } else if (op == 4) {
             V np;
             M nr;
             orc::integrate_transform(V(p[9], p[10], p[11]), m, V(p[12], p[13], p[14]), V(p[15], p[16], p[17]), 1.f / 120.f,
                                      np, nr);
             o[0] = np.x, o[1] = np.y, o[2] = np.z;
             for (int k = 0; k < 9; k++) o[3 + k] = nr.r[k / 3][k % 3];
+        } else {  // a wheel ray's btSubsimplexConvexCast (layout: rlgpu_linear_math_queries op 5)
+            float f = 0.f;
+            V n(0.f, 0.f, 0.f);
+            const bool hit = orc::gjk::ray_convex_cast(V(p[9], p[10], p[11]), V(p[12], p[13], p[14]), p[21],
+                                                       V(p[18], p[19], p[20]), m, V(p[15], p[16], p[17]), f, n);
+            o[0] = hit ? 1.f : 0.f, o[1] = f, o[2] = n.x, o[3] = n.y, o[4] = n.z;
         }
     }
 }

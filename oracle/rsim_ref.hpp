@@ -67,7 +67,7 @@ inline void stm(float* p, const M& m) {
 void philox(uint64_t key, uint32_t c0, uint32_t c1, uint32_t out[4]);
 uint32_t rng_next(uint64_t seed, int arena, rlgpu_env_extra& env);
 void default_car(rlgpu_car& cs);
-void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index);
+void kickoff(rlgpu_arena_state& s, uint64_t seed, int arena_index, bool fuzz = false);
 void arena_step(const World& w, rlgpu_arena_state& s, uint64_t seed, int arena_index, int ticks);
 
 }  // namespace orc

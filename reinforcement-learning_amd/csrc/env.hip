@@ -48,6 +48,7 @@ struct StepArgs {
     int arith;                 // RLGPU_ARITH_* (rlgpu_envset_config.arith): copied into Aux::arith at launch
     int arena_offset;          // global index of arena 0 (the arenas' Philox streams)
     float* reward_values;      // [players][nr] each reward's value before its weight, or null
+    int fuzz;                  // FuzzedKickoffState (rlgpu_envset_config.state_setter)
 };
 
 // ExampleMain's StepCallback (src/ExampleMain.cpp:233-283) on this arena's GameState as the
@@ -540,7 +541,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         }
         sync(); P.mark(13);
         if (g.reset_mode == 1) {
-            if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena + g.arena_offset);
+            if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena + g.arena_offset, g.fuzz != 0);
             sync(); P.mark(14);
             if (fused_reset && l < 4) build_obs_row(A, l);
             sync(); P.mark(14);
@@ -561,7 +562,7 @@ __global__ void __launch_bounds__(kWG) env_kernel(StepArgs g) {
         }
         sync(); P.mark(14);
         if (do_reset && l == 0) {
-            kickoff_reset(A, g.seed, arena + g.arena_offset);
+            kickoff_reset(A, g.seed, arena + g.arena_offset, g.fuzz != 0);
             if (g.reset_mode == 2) g.terminals[arena] = 0;
         }
         sync(); P.mark(14);
@@ -924,6 +925,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.plug = e->d_plug;
     g.arith = e->cfg.arith;
     g.arena_offset = e->cfg.arena_offset;
+    g.fuzz = e->cfg.state_setter == RLGPU_SS_FUZZED_KICKOFF;
     g.reward_values = g.build ? e->d_reward_values : nullptr;
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
@@ -953,6 +955,8 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         RLGPU_REQUIRE(cfg->mesh_tris == nullptr || cfg->mesh_ntris > 0, "mesh_ntris must be > 0 with mesh_tris");
         RLGPU_REQUIRE(cfg->arith >= 0 && cfg->arith < RLGPU_NUM_ARITH,
                       "rlgpu_envset_create: unknown arithmetic mode " + std::to_string(cfg->arith) + " (RLGPU_ARITH_*)");
+        RLGPU_REQUIRE(cfg->state_setter == RLGPU_SS_KICKOFF || cfg->state_setter == RLGPU_SS_FUZZED_KICKOFF,
+                      "rlgpu_envset_create: unknown state setter " + std::to_string(cfg->state_setter) + " (RLGPU_SS_*)");
         const rl::Plugins plug = plugins_from(cfg);
         ensure_const();
         if (rl::sse_api(cfg->arith)) ensure_rsqrt();
@@ -1378,19 +1382,27 @@ __global__ void __launch_bounds__(64) linear_math_kernel(int op, int ar, const f
     } else if (op == 3) {
         const quat q = qmul(quat{p[0], p[1], p[2], p[3]}, quat{p[4], p[5], p[6], p[7]}, ar);
         o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.w;
-    } else {
+    } else if (op == 4) {
         v3 np;
         m3 nr;
         integrate_transform(v3{p[9], p[10], p[11]}, m, v3{p[12], p[13], p[14]}, v3{p[15], p[16], p[17]}, kTick, np, nr, ar);
         o[0] = np.x; o[1] = np.y; o[2] = np.z;
         put9(nr, o + 3);
+    } else {
+        // a wheel ray's btSubsimplexConvexCast: R = p[0..8], from p[9..11], to p[12..14], body origin p[15..17],
+        // box half extents p[18..20], sphere radius p[21] (> 0: sphere)
+        float f = 0.f;
+        v3 n = zero3();
+        const bool hit = gjk::ray_convex_cast(v3{p[9], p[10], p[11]}, v3{p[12], p[13], p[14]}, p[21],
+                                              v3{p[18], p[19], p[20]}, m, v3{p[15], p[16], p[17]}, ar, f, n);
+        o[0] = hit ? 1.f : 0.f; o[1] = f; o[2] = n.x; o[3] = n.y; o[4] = n.z;
     }
 }
 }  // namespace rl
 
 extern "C" int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream) {
     return rlgpu::guarded([&] {
-        RLGPU_REQUIRE(op >= 0 && op <= 4, "rlgpu_linear_math_queries: op must be in [0, 4]");
+        RLGPU_REQUIRE(op >= 0 && op <= 5, "rlgpu_linear_math_queries: op must be in [0, 5]");
         RLGPU_REQUIRE(arith >= 0 && arith < RLGPU_NUM_ARITH, "rlgpu_linear_math_queries: unknown arithmetic mode");
         RLGPU_REQUIRE(n >= 0 && (n == 0 || (d_in && d_out)), "rlgpu_linear_math_queries: bad argument");
         if (n == 0) return;

@@ -322,7 +322,7 @@ DEV float reward_value(ArenaLDS* A, const rlgpu_reward_spec& rs, int i, const PV
 }
 
 // Arena::ResetToRandomKickoff (Arena.cpp:112-216) + EnvSet::ResetArena state (EnvSet.cpp:275-304), one lane
-DEV void kickoff_reset(ArenaLDS* A, uint64_t seed, int arena) {
+DEV void kickoff_reset(ArenaLDS* A, uint64_t seed, int arena, bool fuzz) {
     int order[5] = {0, 1, 2, 3, 4};
     for (int i = 4; i > 0; i--) {
         int j = (int)(rng_next(A, seed, arena) % (uint32_t)(i + 1));
@@ -337,6 +337,16 @@ DEV void kickoff_reset(ArenaLDS* A, uint64_t seed, int arena) {
             v3 pos = v3{C.kick_x[k], C.kick_y[k], 17.f};
             if (team == 1) pos = pos * v3{-1, -1, 1};
             set_car_state(A, ci, pos, C.kick_rot[team][k], 100.f / 3.f, true);
+        }
+    }
+    if (fuzz) {  // FuzzedKickoffState::ResetArena: GetState, pos += RandFloat(-0.1, 0.1) uu, SetState
+        for (int ci = 0; ci < 4; ci++) {
+            rlgpu_body& b = A->s.cars[ci].body;
+            for (int k = 0; k < 3; k++) {
+                const float r = -0.1f + rng_uniform(A, seed, arena) * (0.1f - -0.1f);
+                b.pos[k] = (b.pos[k] * kBT2UU + r) * kUU2BT;
+                b.vel[k] = (b.vel[k] * kBT2UU) * kUU2BT;
+            }
         }
     }
     st3(A->s.ball.pos, v3{0, 0, 93.15f} * kUU2BT);

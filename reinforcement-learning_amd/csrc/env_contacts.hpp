@@ -308,7 +308,7 @@ DEV int bp_home(v3 mn) {
     const int k = min(max((int)f.z, 0), C.bp_cells[2] - 1);
     return (i * C.bp_cells[1] + j) * C.bp_cells[2] + k;
 }
-DEV int bp_key(const ArenaLDS* A, int b) { return A->s.env.bp_rank[b] * 8 + b; }  // list position (ties: creation)
+// bp_key (env_device.hpp): a body's position in every cell's dynamic list
 // one lane per arena, on this tick's broadphase AABBs (after predictUnconstraintMotion)
 DEV void bp_update(ArenaLDS* A) {
 #pragma unroll 1

@@ -117,6 +117,10 @@ DEV uint32_t philox0(uint64_t key, uint32_t c0, uint32_t c1) {
     return x0;
 }
 DEV uint32_t rng_next(ArenaLDS* A, uint64_t seed, int arena) { return philox0(seed, (uint32_t)arena, A->s.env.rng_counter++); }
+// a uniform float in [0, 1) from the next draw (24 bits): RocketSim's RandFloat fraction e() / e.max()
+DEV float rng_uniform(ArenaLDS* A, uint64_t seed, int arena) {
+    return (float)(rng_next(A, seed, arena) >> 8) * (1.f / 16777216.f);
+}
 
 // ------------------------------------------------------------------ shapes / AABBs
 DEV v3 car_box_center(ArenaLDS* A, int bi) { return bpos(A, bi) + brot(A, bi) * C.car_offset; }
@@ -241,6 +245,8 @@ DEV void plane_space1(v3 n, v3& p, v3& q) {
         q = v3{-n.z * p.y, n.z * p.x, a * k};
     }
 }
+// a dynamic body's position in every cell's dynamic list (ties: creation order); env_contacts.hpp keeps the ranks
+DEV int bp_key(const ArenaLDS* A, int b) { return A->s.env.bp_rank[b] * 8 + b; }  // list position (ties: creation)
 DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& hit_point, v3& hit_normal) {
     float best = 1.0f;
     int obj = -1;
@@ -302,61 +308,35 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
             nrm = n;
         }
     }
+    // the dynamic bodies of the ray's cell in the cell list's order (bp_key), the wheel's own car skipped
+    // (ClosestRayResultCallback's ignore object): btSubsimplexConvexCast of the ray's point against the ball's
+    // sphere or the car compound's box child (btCollisionWorld.cpp:277-310,339-400), kept when strictly closer
+    // and its normal long enough.  A body is in the cells around its home cell (btRSBroadphase.cpp:182-200),
+    // wider than any wheel ray, so every body within reach is listed; a body whose bounding sphere the
+    // segment misses by more than the cast's tolerances cannot be hit and is skipped without the cast.
     {
-        v3 bp = bpos(A, 0);
-        v3 oc = from - bp;
-        float a = dot(d, d), bb = dot(oc, d), c = dot(oc, oc) - C.ball_radius * C.ball_radius;
-        if (c > 0.f) {
-            float disc = bb * bb - a * c;
-            if (disc >= 0.f && bb < 0.f) {
-                float f = (-bb - sqrtf(disc)) / a;
-                if (f >= 0.f && f < best) {
-                    best = f;
-                    obj = 0;
-                    nrm = bt_normalize((from + d * f) - bp, ar);
+        int done = 0;
+        for (int k = 0; k < 5; k++) {
+            int bi = -1, key = 1 << 30;
+            for (int c = 0; c < 5; c++)
+                if (!(done >> c & 1) && bp_key(A, c) < key) {
+                    key = bp_key(A, c);
+                    bi = c;
                 }
-            }
-        }
-    }
-    for (int ci = 1; ci <= 4; ci++) {
-        if (ci == self) continue;
-        v3 c = car_box_center(A, ci);
-        m3 R = brot(A, ci);
-        v3 lo = vmul(from - c, R), ldir = vmul(d, R);
-        float tmin = 0.f, tmax = best;
-        int axis = -1;
-        float sg = 0.f;
-        bool ok = true;
-        for (int k = 0; k < 3 && ok; k++) {
-            float h = comp(C.car_half, k);
-            float lk = comp(ldir, k), ok_ = comp(lo, k);
-            if (fabsf(lk) < 1e-12f) {
-                if (ok_ < -h || ok_ > h) ok = false;
-                continue;
-            }
-            float inv = 1.f / lk;
-            float t1 = (-h - ok_) * inv, t2 = (h - ok_) * inv;
-            float s1 = -1.f;
-            if (t1 > t2) {
-                float tt = t1;
-                t1 = t2;
-                t2 = tt;
-                s1 = 1.f;
-            }
-            if (t1 > tmin) {
-                tmin = t1;
-                axis = k;
-                sg = s1;
-            }
-            if (t2 < tmax) tmax = t2;
-            if (tmin > tmax) ok = false;
-        }
-        if (ok && axis >= 0 && tmin < best) {
-            best = tmin;
-            obj = ci;
-            v3 ln = zero3();
-            set_comp(ln, axis, sg);
-            nrm = R * ln;
+            done |= 1 << bi;
+            if (bi == self || best == 0.f) continue;  // btSingleRayCallback::process stops at fraction 0
+            const v3 c = bi == 0 ? bpos(A, 0) : car_box_center(A, bi);
+            const float reach = bi == 0 ? C.ball_radius : len(C.car_half);
+            const float t = fminf(fmaxf(dot(c - from, d) / fmaxf(dot(d, d), 1e-30f), 0.f), 1.f);
+            if (len2(from + d * t - c) > (reach + 0.05f) * (reach + 0.05f)) continue;
+            float f;
+            v3 n;
+            const bool hit = bi == 0 ? gjk::ray_convex_cast(from, to, C.ball_radius, zero3(), brot(A, 0), c, ar, f, n)
+                                     : gjk::ray_convex_cast(from, to, 0.f, C.car_half, brot(A, bi), c, ar, f, n);
+            if (!hit || !(len2(n) > 0.0001f) || !(f < best)) continue;
+            best = f;
+            obj = bi;
+            nrm = bt_normalize(n, ar);  // castResult.m_normal.normalize()
         }
     }
     if (obj < 0) return -1;

@@ -393,6 +393,77 @@ DEV bool vor_in_simplex(const Voronoi& s, v3 w) {
     return found;
 }
 
+// ---------------------------------------------------------------- btSubsimplexConvexCast (wheel rays)
+// The convex branch of btCollisionWorld::rayTestSingleInternal (btCollisionWorld.cpp:277-310): the ray's point
+// shape (btSphereShape(0), margin 0, identity basis) cast from `from` to `to` against a resting convex body with
+// basis R and origin o by btSubsimplexConvexCast::calcTimeOfImpact (btSubSimplexConvexCast.cpp:30-153;
+// btConvexCast.h:25-29: 32 iterations, epsilon 0.0001, allowed penetration 0).  sphere_r > 0: btSphereShape
+// (margin = radius, btSphereShape.cpp:37-48); otherwise btBoxShape with half extents h including its margin
+// (btBoxShape.h:47-56).  True when Bullet reports the cast (fraction, normal = n.normalized()).  The simplex
+// state is the GJK's register Voronoi solver; the oracle (oracle/gjk_ref.hpp) restates the same.
+constexpr float kSimdEps = 1.1920928955078125e-07f;  // SIMD_EPSILON = FLT_EPSILON
+DEV v3 sphere_support(v3 d, float radius, int ar) {
+    const v3 vn = len2(d) < kSimdEps * kSimdEps ? bt_normalize(v3{-1.f, -1.f, -1.f}, ar) : bt_normalize(d, ar);
+    return radius * vn;  // getMargin() * vecnorm
+}
+DEV v3 box_support(v3 d, v3 h) {  // btFsels(d, h, -h)
+    return v3{d.x >= 0.f ? h.x : -h.x, d.y >= 0.f ? h.y : -h.y, d.z >= 0.f ? h.z : -h.z};
+}
+DEV v3 interp3(v3 v0, v3 v1, float rt) {  // btVector3::setInterpolate3
+    const float s = 1.f - rt;
+    return v3{s * v0.x + rt * v1.x, s * v0.y + rt * v1.y, s * v0.z + rt * v1.z};
+}
+DEV bool ray_convex_cast(v3 from, v3 to, float sphere_r, v3 h, m3 R, v3 o, int ar, float& frac,
+                                             v3& normal) {
+    const m3 I = m3{v3{1.f, 0.f, 0.f}, v3{0.f, 1.f, 0.f}, v3{0.f, 0.f, 1.f}};
+    auto supA = [&](v3 d, v3 org) { return I * sphere_support(vmul(d, I), 0.f, ar) + org; };
+    auto supB = [&](v3 d, v3 org) {
+        const v3 l = vmul(d, R);
+        return R * (sphere_r > 0.f ? sphere_support(l, sphere_r, ar) : box_support(l, h)) + org;
+    };
+    Voronoi vs;
+    vor_reset(vs);
+    const v3 linA = to - from, linB = o - o;
+    float lambda = 0.f;
+    v3 iA = from, iB = o;
+    const v3 r = linA - linB;
+    v3 sa = supA(-r, iA), sb = supB(r, iB);
+    v3 v = sa - sb;
+    int max_iter = 32;
+    v3 n = zero3();
+    float dist2 = len2(v);
+    while ((dist2 > 0.0001f) && max_iter--) {
+        sa = supA(-v, iA);
+        sb = supB(v, iB);
+        v3 w = sa - sb;
+        const float vdw = dot(v, w);
+        if (lambda > 1.f) return false;
+        if (vdw > 0.f) {
+            const float vdr = dot(v, r);
+            if (vdr >= -(kSimdEps * kSimdEps)) return false;
+            lambda = lambda - vdw / vdr;
+            iA = interp3(from, to, lambda);
+            iB = interp3(o, o, lambda);
+            w = sa - sb;
+            n = v;
+        }
+        if (!vor_in_simplex(vs, w)) {  // addVertex
+            vs.lastW = w;
+            vs.needs_update = true;
+            put4(vs.W, vs.n, w);
+            put4(vs.P, vs.n, sa);
+            put4(vs.Q, vs.n, sb);
+            vs.n++;
+        }
+        const bool ok = vor_update(vs);  // closest(v)
+        v = vs.cV;
+        dist2 = ok ? len2(v) : 0.f;
+    }
+    frac = lambda;
+    normal = len2(n) >= kSimdEps * kSimdEps ? bt_normalize(n, ar) : zero3();
+    return !(dot(normal, r) >= -0.f);
+}
+
 // ---------------------------------------------------------------- btGjkEpa2 in the lane's scratch
 struct Mink {
     Shape s;

@@ -56,6 +56,7 @@ struct PluginPlan {
     std::vector<int> rewardSlot;                        // per EnvCreateResult::rewards entry: device index, -1 = host
     std::vector<int> hostTerminals;                     // indices into terminalConditions that run on the host
     std::vector<std::string> hostNames;                 // host plugins' type names (the log line)
+    int32_t stateSetter = RLGPU_SS_KICKOFF;             // KickoffState / FuzzedKickoffState
     int NumHostRewards() const {
         int n = 0;
         for (int s : rewardSlot) n += s < 0;
@@ -171,7 +172,7 @@ inline bool SameSpec(const rlgpu_reward_spec& a, const rlgpu_reward_spec& b) {
 }  // namespace detail
 
 // One arena's EnvCreateResult.  Throws std::invalid_argument for what neither side can run: a builder other
-// than AdvancedObs / DefaultAction / KickoffState (the kernels' own), a registry class with a field the
+// than AdvancedObs / DefaultAction / KickoffState / FuzzedKickoffState (the kernels' own), a registry class with a field the
 // registry cannot hold, or lists longer than RLGPU_MAX_REWARDS / RLGPU_MAX_TERMINALS.
 inline PluginPlan TranslatePlugins(const EnvCreateResult& r) {
     if (r.obsBuilder && typeid(*r.obsBuilder) != typeid(AdvancedObs))
@@ -180,10 +181,11 @@ inline PluginPlan TranslatePlugins(const EnvCreateResult& r) {
     if (r.actionParser && typeid(*r.actionParser) != typeid(DefaultAction))
         throw std::invalid_argument(std::string("EnvCreateResult: action parser ") + typeid(*r.actionParser).name() +
                                     " (the kernels parse DefaultAction)");
-    if (r.stateSetter && typeid(*r.stateSetter) != typeid(KickoffState))
+    if (r.stateSetter && typeid(*r.stateSetter) != typeid(KickoffState) && typeid(*r.stateSetter) != typeid(FuzzedKickoffState))
         throw std::invalid_argument(std::string("EnvCreateResult: state setter ") + typeid(*r.stateSetter).name() +
-                                    " (the kernels reset to KickoffState)");
+                                    " (the kernels reset to KickoffState or FuzzedKickoffState)");
     PluginPlan p;
+    if (r.stateSetter && typeid(*r.stateSetter) == typeid(FuzzedKickoffState)) p.stateSetter = RLGPU_SS_FUZZED_KICKOFF;
     for (const WeightedReward& w : r.rewards) {
         if (!w.reward) throw std::invalid_argument("EnvCreateResult: null reward");
         rlgpu_reward_spec s{};
@@ -215,7 +217,7 @@ inline PluginPlan TranslatePlugins(const EnvCreateResult& r) {
 // The arenas share one registry list: EnvCreateFn must give every arena the same classes and fields in the
 // same order (the host plugin objects themselves stay per arena).
 inline void RequireSamePlan(const PluginPlan& a, const PluginPlan& b, int index) {
-    bool same = a.rewardSlot == b.rewardSlot && a.hostTerminals == b.hostTerminals &&
+    bool same = a.rewardSlot == b.rewardSlot && a.hostTerminals == b.hostTerminals && a.stateSetter == b.stateSetter &&
                 a.deviceRewards.size() == b.deviceRewards.size() && a.deviceTerminals.size() == b.deviceTerminals.size();
     for (size_t i = 0; same && i < a.deviceRewards.size(); i++) same = detail::SameSpec(a.deviceRewards[i], b.deviceRewards[i]);
     for (size_t i = 0; same && i < a.deviceTerminals.size(); i++)
@@ -407,6 +409,7 @@ class EnvSetGPU {
         if (!cfg.terminals) cfg.terminals = &kNoTerminals;
         cfg.arith = o.arith;
         cfg.arena_offset = o.arenaOffset;
+        cfg.state_setter = plan.stateSetter;
         RlgpuCheck(rlgpu_envset_create(&cfg, &h), "EnvSet");
         RlgpuCheck(rlgpu_envset_buffers_get(h, &state), "EnvSet buffers");
         fallbackStats.hostRewards = plan.NumHostRewards();

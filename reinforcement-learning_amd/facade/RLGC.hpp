@@ -334,6 +334,10 @@ class StateSetter {
 class AdvancedObs : public ObsBuilder {};
 class DefaultAction : public ActionParser {};
 class KickoffState : public StateSetter {};
+class FuzzedKickoffState : public StateSetter {  // RG/StateSetters/FuzzedKickoffState.h
+  public:
+    constexpr static float FUZZ_POS_RANGE = 0.1f;
+};
 
 struct EnvCreateResult {  // RG/EnvSet/EnvSet.h:14-24
     void* arena = nullptr;  // the device builds the 2v2 SOCCAR arena itself

@@ -234,14 +234,14 @@ static EnvCreateResult DeviceEnv(int) {
     EnvCreateResult r;
     r.rewards = {{new SpeedReward(), 2.f}, {new AirReward(), 0.5f}, {new TouchBallReward(), 3.f},
                  {new ZeroSumReward(new GoalReward(), 1), 150.f}};
-    r.terminalConditions = {new NoTouchCondition(0.75f), new GoalScoreCondition()};
+    r.terminalConditions = {new NoTouchCondition(3.0f), new GoalScoreCondition()};
     return r;
 }
 static EnvCreateResult HostEnv(int) {
     EnvCreateResult r;
     r.rewards = {{new MySpeedReward(), 2.f}, {new AirReward(), 0.5f}, {new MyTouchBallReward(), 3.f},
                  {new ZeroSumReward(new GoalReward(), 1), 150.f}};
-    r.terminalConditions = {new MyNoTouchCondition(0.75f), new MyGoalCondition()};
+    r.terminalConditions = {new MyNoTouchCondition(3.0f), new MyGoalCondition()};
     return r;
 }
 static EnvCreateResult FinalEnv(int) {
@@ -276,7 +276,9 @@ static int Fallback(int arenas, int steps) {
         CHECK(std::memcmp(oa.data(), ob.data(), oa.size() * 4) == 0, "obs differ %s step %d", when, step);
     };
     for (int s = 0; s < steps && !g_fail; s++) {
-        for (auto& x : act) x = (int32_t)(rng() % RLGPU_ACTIONS);
+        // mostly full throttle + boost straight ahead (DefaultAction row 18): kickoff cars face the ball, so
+        // touches, goals and no-touch timeouts all happen
+        for (auto& x : act) x = (int32_t)(rng() % 10 < 7 ? 18 : rng() % RLGPU_ACTIONS);
         RlgpuCheckHip(hipMemcpy(dAct, act.data(), act.size() * 4, hipMemcpyHostToDevice), "actions");
         for (EnvSetGPU* e : {&A, &B, &F}) {
             e->StepFirstHalf(false);

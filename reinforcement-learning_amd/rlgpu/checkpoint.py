@@ -191,6 +191,9 @@ def save(learner, folder, keep=8):
     os.makedirs(path, exist_ok=True)
     stats = {"total_timesteps": int(learner.total_steps), "total_iterations": int(learner.iteration),
              "return_stat": learner.return_stat.to_json()}
+    skill = getattr(learner, "skill", None)
+    if skill is not None:  # PolicyVersionManager::AddRunningStatsToJSON
+        stats["skill_ratings"] = skill.cur_ratings.to_json()
     with open(os.path.join(path, STATS_FILE), "w") as f:
         json.dump(stats, f, indent=4)
     ppo = learner.ppo
@@ -239,6 +242,10 @@ def load(learner, folder, allow_missing_models=True):
     learner.iteration = int(j["total_iterations"])
     if "return_stat" in j:
         learner.return_stat.read_json(j["return_stat"])
+    skill = getattr(learner, "skill", None)
+    if skill is not None and "skill_ratings" in j:  # LoadRunningStatsFromJSON
+        from .skill import SkillRating
+        skill.cur_ratings = SkillRating.from_json(j["skill_ratings"])
     ppo = learner.ppo
     for mi in ppo.models:
         name = MODEL_NAMES[mi]

@@ -29,10 +29,12 @@ class _Config(ctypes.Structure):
                 ("mesh_tris", ctypes.c_void_p), ("mesh_ntris", ctypes.c_int32), ("mesh_objects", ctypes.c_int32),
                 ("mesh_object_ntris", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("n_rewards", ctypes.c_int32),
                 ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32), ("arith", ctypes.c_int32),
-                ("arena_offset", ctypes.c_int32)]
+                ("arena_offset", ctypes.c_int32), ("state_setter", ctypes.c_int32)]
 
 # the reference build whose Bullet arithmetic the arenas follow (include/rlgpu_arith.h)
 ARITH_MSVC_X64, ARITH_GCC_X64, ARITH_SCALAR = 0, 1, 2
+# EnvCreateResult::stateSetter (include/rlgpu_env.h RLGPU_SS_*)
+KICKOFF_STATE, FUZZED_KICKOFF_STATE = 0, 1
 
 
 class StepOutputs(ctypes.Structure):
@@ -117,12 +119,14 @@ class EnvSet:
     ScoreLimit(3) by default)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, save_rewards=True, device="cuda:0",
-                 max_episode_steps=0, mesh=None, rewards=None, terminals=None, arith=ARITH_MSVC_X64, arena_offset=0):
+                 max_episode_steps=0, mesh=None, rewards=None, terminals=None, arith=ARITH_MSVC_X64, arena_offset=0,
+                 state_setter=KICKOFF_STATE):
         """mesh: an rlgpu.mesh.ArenaMesh (e.g. ArenaMesh.from_folder("collision_meshes")), or None for
         the built-in synthetic arena mesh.  rewards / terminals: lists of rlgpu.plugins.reward(...) /
         terminal(...) specs (or structured arrays), None = ExampleMain's.  arith: the reference build
         whose Bullet arithmetic the step follows (ARITH_MSVC_X64 = build.ps1's, ARITH_GCC_X64, ARITH_SCALAR).
-        arena_offset: global index of arena 0 for the arenas' random streams (a rank's first arena)."""
+        arena_offset: global index of arena 0 for the arenas' random streams (a rank's first arena).
+        state_setter: KICKOFF_STATE, or FUZZED_KICKOFF_STATE (the skill tracker's, rlgpu.skill)."""
         import torch
         if not torch.cuda.is_available():
             raise _lib.RLGPUError("EnvSet needs an MI355X: the product path has no CPU fallback")
@@ -132,6 +136,7 @@ class EnvSet:
         cfg = _Config(num_arenas, tick_skip, action_delay, seed, int(save_rewards), max_episode_steps)
         cfg.arith = int(arith)
         cfg.arena_offset = int(arena_offset)
+        cfg.state_setter = int(state_setter)
         self.arith = int(arith)
         if mesh is not None:
             cfg.mesh_tris = mesh.tris.ctypes.data

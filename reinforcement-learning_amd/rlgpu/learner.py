@@ -197,6 +197,9 @@ class LearnerConfig:
         self.train_against_old_chance = 0.15
         self.ts_per_version = 25_000_000
         self.max_old_versions = 32
+        # ELO skill matches against the old versions (LearnerConfig.h:70, SkillTrackerConfig.h): a
+        # rlgpu.skill.SkillTrackerConfig, or None = disabled
+        self.skill_tracker = None
         for k, v in kw.items():
             if not hasattr(self, k):
                 raise AttributeError(f"unknown LearnerConfig field {k}")
@@ -397,11 +400,17 @@ class Learner:
         self.versions = None
         self.old_version, self.old_team = None, 0
         self._vrng = np.random.default_rng(cfg.seed + 104729)
-        if cfg.train_against_old_versions:
+        self.skill = None
+        # rank 0 plays the skill matches (ratings are a report; every rank holds the same versions)
+        if cfg.skill_tracker is not None and cfg.skill_tracker.enabled and rank == 0:  # PolicyVersionManager.cpp:24-31
+            from .skill import SkillTracker
+            self.skill = SkillTracker(cfg.skill_tracker, self.ppo, self.device, cfg.tick_skip, cfg.action_delay,
+                                      seed=cfg.seed, mesh=cfg.mesh, arith=cfg.arith)
+        if cfg.train_against_old_versions or self.skill is not None:  # Learner.cpp:131-142
             import os
             from .versions import PolicyVersionManager
             vf = os.path.join(cfg.checkpoint_folder, "policy_versions") if cfg.checkpoint_folder else None
-            self.versions = PolicyVersionManager(self.ppo, vf, cfg.max_old_versions, cfg.ts_per_version)
+            self.versions = PolicyVersionManager(self.ppo, vf, cfg.max_old_versions, cfg.ts_per_version, self.skill)
         self.last_checkpoint = None
         if cfg.checkpoint_folder:  # Learner ctor: load the most recent checkpoint (Learner.cpp:145-153)
             from . import checkpoint as _ckpt
@@ -422,6 +431,8 @@ class Learner:
         if getattr(self, "_h", None):
             import torch
             torch.cuda.synchronize(self.device)
+            if self.skill is not None:
+                self.skill.close()
             self.env.close()
             self.ppo.close()
             _lib.check(_lib.lib().rlgpu_learner_destroy(self._h), "rlgpu_learner_destroy")
@@ -529,7 +540,7 @@ class Learner:
         import torch
         t0 = time.perf_counter()
         self.old_version = None
-        if self.versions is not None and self.versions.versions:  # Learner.cpp:587-627
+        if self.cfg.train_against_old_versions and self.versions is not None and self.versions.versions:  # Learner.cpp:587-627
             if self._vrng.random() < self.cfg.train_against_old_chance:
                 self.old_version = self.versions.versions[int(self._vrng.integers(0, len(self.versions.versions)))]
                 self.old_team = int(self._vrng.integers(0, 2))
@@ -539,10 +550,11 @@ class Learner:
         prev = self.total_steps
         rep = _CReport()
         _lib.check(_lib.lib().rlgpu_learner_iterate(self._h, ctypes.byref(rep)), "rlgpu_learner_iterate")
+        report = {}
         if self.versions is not None:
-            self.versions.on_iteration(self.total_steps, prev)
+            self.versions.on_iteration(self.total_steps, prev, report)
         torch.cuda.synchronize(self.device)
-        out = {"iteration_s": time.perf_counter() - t0, "collect_s": rep.collect_s, "consume_s": rep.consume_s,
+        out = {"report": report, "iteration_s": time.perf_counter() - t0, "collect_s": rep.collect_s, "consume_s": rep.consume_s,
                "learn_s": rep.learn_s, "learn_issue_s": rep.learn_issue_s, "collect_issue_s": rep.collect_issue_s, "env_kernel_ms": rep.env_kernel_ms,
                "old_version": None if self.old_version is None else (self.old_version.timesteps, self.old_team)}
         if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)

@@ -16,27 +16,30 @@ Versions are the policy's flat fp32 parameters -- followed by the shared head's 
 one, as the reference versions GetPolicyModels() (PPOLearner.cpp:665-674) and saves POLICY.lt +
 SHARED_HEAD.lt per version -- kept in HBM (1.6 MB each at [512, 512]); the active
 one is converted once per iteration into the PPO handle's second bf16 inference copy
-(rlgpu_ppo_set_version) and used by the mixed-policy inference of the Learner.  The skill/ELO
-tracker is not part of this tier (SURVEY.md 8f-3 lists it as optional); STATS.json carries an
-empty "skill_ratings" object so the reference's loader accepts the directories.
+(rlgpu_ppo_set_version) and used by the mixed-policy inference of the Learner.  With a skill tracker
+(rlgpu.skill, LearnerConfig.skill_tracker) every version carries its ELO ratings (a copy of the current
+ratings when it is added, PolicyVersionManager.cpp:47), STATS.json stores them under "skill_ratings", and
+OnIteration runs the skill matches every update_interval iterations (PolicyVersionManager.cpp:302-315).
 """
 import json
 import os
 import shutil
 
 from . import checkpoint as _ckpt
+from .skill import SkillRating
 
 
 class PolicyVersion:
     def __init__(self, timesteps, params, ratings=None):
         self.timesteps = int(timesteps)
         self.params = params            # device tensor, flat fp32 policy (+ shared head) parameters
-        self.ratings = dict(ratings or {})
+        self.ratings = ratings.copy() if isinstance(ratings, SkillRating) else SkillRating(ratings)
 
 
 class PolicyVersionManager:
-    def __init__(self, ppo, save_folder=None, max_versions=32, ts_per_version=25_000_000):
+    def __init__(self, ppo, save_folder=None, max_versions=32, ts_per_version=25_000_000, skill=None):
         self.ppo = ppo
+        self.skill = skill  # rlgpu.skill.SkillTracker or None
         self.save_folder = save_folder
         self.max_versions = max_versions
         self.ts_per_version = ts_per_version
@@ -47,16 +50,23 @@ class PolicyVersionManager:
     def add_version(self, timesteps, params=None):
         """AddVersion: a copy of the current policy (or of `params`)."""
         src = self.ppo.policy_version() if params is None else params
-        v = PolicyVersion(timesteps, src.detach().clone())
+        v = PolicyVersion(timesteps, src.detach().clone(), self.skill.cur_ratings if self.skill is not None else None)
         self.versions.append(v)
         self.versions.sort(key=lambda x: x.timesteps)
         while len(self.versions) > self.max_versions:
             self.versions.pop(0)
         return v
 
-    def on_iteration(self, total_timesteps, prev_timesteps):
+    def on_iteration(self, total_timesteps, prev_timesteps, report=None):
+        """OnIteration: a version every ts_per_version timesteps (and after the first iteration), then the skill
+        matches every update_interval iterations once a version exists."""
         if total_timesteps // self.ts_per_version > prev_timesteps // self.ts_per_version or prev_timesteps == 0:
             self.add_version(total_timesteps)
+        if self.skill is not None and self.skill.cfg.enabled:
+            self.skill.iterations_since_ran += 1
+            if self.skill.iterations_since_ran >= self.skill.cfg.update_interval and self.versions:
+                self.skill.iterations_since_ran = 0
+                self.skill.run(self.versions, report)
 
     def save_versions(self):
         if not self.save_folder:
@@ -81,7 +91,7 @@ class PolicyVersionManager:
                         o += p.numel()
                 _ckpt.write_model(seq, _ckpt.model_path(d, _ckpt.MODEL_NAMES[mi]))
             with open(os.path.join(d, "STATS.json"), "w") as f:
-                json.dump({"skill_ratings": v.ratings}, f, indent=4)
+                json.dump({"skill_ratings": v.ratings.to_json()}, f, indent=4)
 
     def _models(self):
         return [m for m in self.ppo.models if m != 1]  # GetPolicyModels: policy (+ shared head)
@@ -107,4 +117,4 @@ class PolicyVersionManager:
             p = os.path.join(d, "STATS.json")
             if os.path.exists(p):
                 with open(p) as f:
-                    v.ratings = json.load(f).get("skill_ratings", {})
+                    v.ratings = SkillRating.from_json(json.load(f).get("skill_ratings", {}))

@@ -73,17 +73,19 @@ def _run(world, kw, iters):
 
 @pytest.mark.timeout(400)
 def test_two_ranks_equal_one_rank(gpu):
+    """One iteration from the same initial parameters: the rollouts and return statistics are identical, the
+    parameters after the update agree to fp32 summation order.  (A second iteration would infer with those
+    slightly different parameters, so its sampled actions -- and rollouts -- may differ where two actions
+    are nearly tied.)"""
     import torch  # noqa: F401
     kw = dict(num_arenas=64, rollout_len=16, mini_batch_size=1024, seed=5)
-    two = _run(2, kw, 2)
-    one = _run(1, dict(kw, num_arenas=128), 2)[0]
+    two = _run(2, kw, 1)
+    one = _run(1, dict(kw, num_arenas=128), 1)[0]
     # the same rollouts: rank r's players are players [256 r, 256 (r + 1)) of the one-rank job
-    for it in range(2):
-        got = np.concatenate([two[0]["rewards"][it], two[1]["rewards"][it]], axis=1)
-        np.testing.assert_array_equal(got.view(np.uint32), one["rewards"][it].view(np.uint32), err_msg=f"iteration {it}")
+    got = np.concatenate([two[0]["rewards"][0], two[1]["rewards"][0]], axis=1)
+    np.testing.assert_array_equal(got.view(np.uint32), one["rewards"][0].view(np.uint32))
     # the same return statistics (the same samples in the same order), bit for bit
-    for it in range(2):
-        assert two[0]["ret"][it] == two[1]["ret"][it] == one["ret"][it], (it, two[0]["ret"][it], one["ret"][it])
+    assert two[0]["ret"][0] == two[1]["ret"][0] == one["ret"][0], (two[0]["ret"][0], one["ret"][0])
     assert two[0]["steps"] == two[1]["steps"] == one["steps"]
     np.testing.assert_array_equal(two[0]["params"], two[1]["params"])
     d = np.abs(two[0]["params"] - one["params"])

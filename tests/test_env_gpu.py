@@ -112,6 +112,52 @@ def test_env_perturbed_contacts_parity(gpu):
         _check_step(g, o, f"perturbed step {t}")
 
 
+def _stacked_states(st, rng):
+    """Cars parked on the ball and on each other, high above the floor: their wheel rays end on the ball's
+    sphere or another car's box (btSubsimplexConvexCast, btCollisionWorld.cpp:277-310)."""
+    n = st.shape[0]
+    for i in range(n):
+        x, y = rng.uniform(-30, 30), rng.uniform(-40, 40)
+        st["ball"]["pos"][i] = (x, y, 6.0)
+        st["ball"]["vel"][i] = 0
+        st["ball"]["angvel"][i] = rng.uniform(-1, 1, 3)
+        for k in range(4):
+            body = st["cars"]["body"][i, k]
+            body["vel"] = rng.uniform(-0.2, 0.2, 3)
+            body["angvel"] = rng.uniform(-0.3, 0.3, 3)
+            a = rng.uniform(-0.2, 0.2)
+            body["rot"] = np.array([np.cos(a), -np.sin(a), 0, np.sin(a), np.cos(a), 0, 0, 0, 1], np.float32)
+        cars = st["cars"]["body"]["pos"][i]
+        cars[0] = (x + rng.uniform(-0.4, 0.4), y + rng.uniform(-0.4, 0.4), 6.0 + 1.825 + rng.uniform(0.35, 0.7))
+        cars[1] = (x + 12, y, 5.0)
+        cars[2] = (x + 12 + rng.uniform(-0.5, 0.5), y + rng.uniform(-0.5, 0.5), 5.0 + rng.uniform(0.9, 1.3))
+        cars[3] = (x - 12, y + rng.uniform(-2, 2), 0.4)
+    return st
+
+
+def test_env_wheel_rays_on_dynamic_bodies_parity(gpu):
+    import torch
+    from rlgpu.state import ARENA
+    n = 64
+    g, o = _mk(n, 31, gpu)
+    rng = np.random.default_rng(5)
+    st = _stacked_states(np.frombuffer(o.get_arenas().tobytes(), ARENA).copy(), rng)
+    buf = np.frombuffer(st.tobytes(), np.uint8)
+    o.set_arenas(buf)
+    g.set_arenas(buf)
+    elevated_contacts = 0
+    for t in range(30):
+        a = random_actions(o.masks, rng)
+        o.step(a, False)
+        g.step(torch.from_numpy(a).to(gpu), False)
+        _check_step(g, o, f"stacked step {t}")
+        s = _state(o)
+        high = s["cars"]["body"]["pos"][..., 2] > 2.5
+        elevated_contacts += int((s["cars"]["wheel_contact"].any(-1) & high).sum())
+    assert elevated_contacts > 0, "no wheel ray reached the ball or a car"
+    print(f"wheel contacts of cars standing on the ball / a car: {elevated_contacts}")
+
+
 def test_env_custom_mesh_parity(gpu):
     """A dense 8-object collision mesh loaded from .cmf images (bumpy heightfield floor, side
     ramps, back walls; 3.5k triangles): wheel rays, ball and car contacts against the uniform-grid
