@@ -199,6 +199,39 @@ def gae_micro(dev, reps=20):
     return out
 
 
+def extra_leg(dev, name, mesh, iters=1, **kw):
+    """One more workload on a fresh C++ Learner, beside the headline (rank 0, N = 1 only): one untimed and
+    `iters` timed PPO iterations, their per-phase times and the learn-phase roofline of one more iteration.
+    SURVEY.md 8d: C5 = 8,192 arenas, actor / critic [2048] x 4, fp16 inference (the MFMA-bound regime); x6 =
+    the C2 workload with the exact fp32 GEMM split (rlgpu_ppo.h GEMM_F32X6) instead of H3."""
+    import torch
+    from rlgpu.learner import Learner, LearnerConfig
+    cfg = LearnerConfig(train_against_old_versions=False, mesh=mesh, **kw)
+    L = Learner(cfg, device=dev)
+    L.iterate()
+    torch.cuda.synchronize()
+    ph = {"collect": 0.0, "consume": 0.0, "learn": 0.0}
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        rep = L.iterate()
+        for k in ph:
+            ph[k] += rep[k + "_s"]
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / iters
+    env_steps = cfg.num_arenas * cfg.rollout_len
+    gemm = {2: "h3", 0: "x6", 1: "f32"}[cfg.train_gemm]
+    out = {"leg": name, "arenas": cfg.num_arenas, "policy_layers": list(cfg.policy_layers),
+           "critic_layers": list(cfg.critic_layers), "train_gemm": gemm, "infer_fp16": bool(cfg.infer_fp16),
+           "ms_per_iteration": el * 1e3, "env_steps_per_s": env_steps / el,
+           "ppo_s_per_1M_agent_steps": el / (4 * env_steps) * 1e6, "iterations": iters,
+           "phase_s_per_iteration": {k: v / iters for k, v in ph.items()},
+           "learn_roofline": learn_roofline(L, gemm)}
+    L.close()
+    del L
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,11 +240,15 @@ def main():
     ap.add_argument("--arenas", type=int, default=ARENAS_PER_GPU)
     ap.add_argument("--rollout", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the C5 and exact-GEMM (x6) legs")
     ap.add_argument("--mesh", choices=("procedural", "synthetic"), default="procedural",
                     help="arena collision mesh: the SOCCAR-sized procedural stand-in (16 objects, 8,800 triangles: "
                          "rlgpu.mesh.procedural_soccar) or the 36-triangle synthetic arena")
     ap.add_argument("--train-gemm", choices=("h3", "x6", "f32"), default="h3",
                     help="fp32 training GEMM arithmetic (include/rlgpu_ppo.h rlgpu_gemm modes)")
+    ap.add_argument("--arith", choices=("msvc_x64", "gcc_x64", "scalar"), default="msvc_x64",
+                    help="the reference build whose Bullet arithmetic the arenas follow (include/rlgpu_arith.h; "
+                         "msvc_x64 = build.ps1's, the reference's own)")
     args = ap.parse_args()
 
     import torch
@@ -241,8 +278,9 @@ def main():
     train_gemm = {"h3": GEMM_F16X3, "x6": GEMM_F32X6, "f32": GEMM_F32}[args.train_gemm]
     from rlgpu.mesh import procedural_soccar
     mesh = procedural_soccar() if args.mesh == "procedural" else None
+    arith = {"msvc_x64": 0, "gcc_x64": 1, "scalar": 2}[args.arith]
     cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False,
-                        train_gemm=train_gemm, mesh=mesh)
+                        train_gemm=train_gemm, mesh=mesh, arith=arith)
     L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
     L.set_env_timing(True)  # HIP events around every fused env step, on the learner's stream
 
@@ -289,7 +327,7 @@ def main():
                                "LayerNorm+LeakyReLU, bf16 inference / fp32 training, T=128, 2 epochs, minibatch 50k",
                    "arenas_per_gpu": args.arenas, "agents_per_gpu": 4 * args.arenas, "rollout_len": cfg.rollout_len,
                    "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32",
-                   "train_gemm": args.train_gemm,
+                   "train_gemm": args.train_gemm, "arith": args.arith,
                    "mesh": (f"procedural SOCCAR stand-in: {mesh.num_objects} objects, {mesh.num_tris} triangles "
                             "(quarter pipes, rounded corners, goal boxes; floor / walls / ceiling are static planes)"
                             if mesh is not None else "synthetic arena: 1 object, 36 triangles (include/rlgpu_arena_mesh.h)")},
@@ -309,6 +347,16 @@ def main():
     out["learn_roofline"] = learn_roofline(L, args.train_gemm)
     if rank == 0 and world == 1:
         out["gae_micro"] = gae_micro(dev)
+    if rank == 0 and world == 1 and not args.no_legs:
+        L.close()
+        torch.cuda.empty_cache()
+        from rlgpu.ppo import GEMM_F32X6 as _X6
+        out["legs"] = [
+            extra_leg(dev, "C5 per GPU", mesh, num_arenas=8192, policy_layers=(2048,) * 4, critic_layers=(2048,) * 4,
+                      infer_fp16=True, arith=arith),
+            extra_leg(dev, "C2 exact fp32 split (x6)", mesh, num_arenas=args.arenas, rollout_len=args.rollout,
+                      train_gemm=_X6, arith=arith),
+        ]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(mesh, args.mesh)
     if rank == 0:

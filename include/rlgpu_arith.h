@@ -48,6 +48,11 @@ int rlgpu_x86_rsqrt_table(uint32_t* h_table, int64_t cap, int32_t* bits);
 /* The table-driven rsqrtss emulation the kernels use, evaluated on the host (tests compare it with the
  * instruction). */
 float rlgpu_x86_rsqrtss_emulated(float x);
+/* When every table entry is 1 / sqrt(the midpoint of its input interval) rounded to nearest-even at the
+ * entries' significant bits (Intel's rsqrtss, with a margin far above double rounding), the kernels compute
+ * the entry in double instead of reading the table: returns those significant bits (12 on Intel), 0 when
+ * the kernels read the table (RLGPU_RSQRT_LUT=1 forces it), -1 without a table. */
+int rlgpu_x86_rsqrt_formula_bits(void);
 
 /* The mode-dependent LinearMath operations of the arena kernels on the device, one query per lane (tests
  * compare them with the oracle's restatement): op 0 btVector3::normalize v[3] -> v[3]; 1
@@ -55,7 +60,8 @@ float rlgpu_x86_rsqrtss_emulated(float x);
  * a[4] b[4] -> q[4]; 4 btTransformUtil::integrateTransform of rot[9] pos[3] linvel[3] angvel[3] over 1/120 s
  * -> pos[3] rot[9]; 5 a wheel ray's btSubsimplexConvexCast (btCollisionWorld.cpp:277-310) of the segment
  * from[3] (at 9) to[3] (at 12) against a resting body of basis rot[9] (at 0) and origin o[3] (at 15), a box of
- * half extents h[3] (at 18, with its margin) or a sphere of radius r (at 21, > 0) -> hit, fraction, normal[3].
+ * half extents h[3] (at 18, with its margin) or a sphere of radius r (at 21, > 0) -> hit, fraction, normal[3];
+ * 6 the kernels' rsqrtss of the row's first 12 floats -> 12 floats.
  * d_in [n][24], d_out [n][12] floats (device).  Asynchronous on `stream`. */
 int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream);
 

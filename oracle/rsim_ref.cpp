@@ -2451,6 +2451,8 @@ void oracle_linear_math(int op, int arith, const float* in, int64_t n, float* ou
                                      np, nr);
             o[0] = np.x, o[1] = np.y, o[2] = np.z;
             for (int k = 0; k < 9; k++) o[3 + k] = nr.r[k / 3][k % 3];
+        } else if (op == 6) {  // rsqrtss itself
+            for (int k = 0; k < 12; k++) o[k] = orc::x86_rsqrtss(p[k]);
         } else {  // a wheel ray's btSubsimplexConvexCast (layout: rlgpu_linear_math_queries op 5)
             float f = 0.f;
             V n(0.f, 0.f, 0.f);

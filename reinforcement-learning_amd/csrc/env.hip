@@ -892,12 +892,12 @@ bool g_rsqrt_ready = false;
 // kernels' kRsqrtLut (once per process; the table is the host CPU's, the same for every set)
 void ensure_rsqrt() {
     if (g_rsqrt_ready) return;
-    int bits = 0;
-    const std::vector<uint32_t>& t = rlgpu::x86_rsqrt_table_or_throw(&bits);
+    int bits = 0, sig = 0;
+    const std::vector<uint32_t>& t = rlgpu::x86_rsqrt_table_or_throw(&bits, &sig);
     uint32_t* d = nullptr;
     RLGPU_CHECK_HIP(hipMalloc(&d, t.size() * sizeof(uint32_t)));
     RLGPU_CHECK_HIP(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    const rl::RsqrtLut L{d, bits};
+    const rl::RsqrtLut L{d, bits, sig};
     RLGPU_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rl::kRsqrtLut), &L, sizeof L));
     g_rsqrt_ready = true;
 }
@@ -1388,6 +1388,8 @@ __global__ void __launch_bounds__(64) linear_math_kernel(int op, int ar, const f
         integrate_transform(v3{p[9], p[10], p[11]}, m, v3{p[12], p[13], p[14]}, v3{p[15], p[16], p[17]}, kTick, np, nr, ar);
         o[0] = np.x; o[1] = np.y; o[2] = np.z;
         put9(nr, o + 3);
+    } else if (op == 6) {  // rsqrtss of the first 12 floats of the row (the table or its formula)
+        for (int k = 0; k < 12; k++) o[k] = x86_rsqrtss(p[k]);
     } else {
         // a wheel ray's btSubsimplexConvexCast: R = p[0..8], from p[9..11], to p[12..14], body origin p[15..17],
         // box half extents p[18..20], sphere radius p[21] (> 0: sphere)
@@ -1402,7 +1404,7 @@ __global__ void __launch_bounds__(64) linear_math_kernel(int op, int ar, const f
 
 extern "C" int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream) {
     return rlgpu::guarded([&] {
-        RLGPU_REQUIRE(op >= 0 && op <= 5, "rlgpu_linear_math_queries: op must be in [0, 5]");
+        RLGPU_REQUIRE(op >= 0 && op <= 6, "rlgpu_linear_math_queries: op must be in [0, 6]");
         RLGPU_REQUIRE(arith >= 0 && arith < RLGPU_NUM_ARITH, "rlgpu_linear_math_queries: unknown arithmetic mode");
         RLGPU_REQUIRE(n >= 0 && (n == 0 || (d_in && d_out)), "rlgpu_linear_math_queries: bad argument");
         if (n == 0) return;

@@ -1971,6 +1971,98 @@ __global__ void __launch_bounds__(256) colsum_partial(const float* X, int R, int
     }
 }
 
+// The column sums of one tile of reduce_cols (block (x, y) of a G-group grid): the same loads in the same
+// order, so reduce_batch's column jobs give reduce_cols's bits.
+DEV void reduce_cols_tile(const float* part, int nblk, int64_t stride, int n, int x, int y, int G, float* out,
+                          int64_t out_stride, int accumulate, float (*red)[64]) {
+    const int cl = threadIdx.x & 63, gi = threadIdx.x >> 6;
+    const int c = x * 64 + cl;
+    float s = 0.f;
+    if (c < n) {
+        const int step = 16 * G;
+        for (int b = y + G * gi; b < nblk; b += 8 * step) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int bk = b + k * step;
+                v[k] = part[(int64_t)(bk < nblk ? bk : b) * stride + c];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (b + k * step < nblk) s += v[k];
+        }
+    }
+    red[gi][cl] = s;
+    __syncthreads();
+    if (gi == 0 && c < n) {
+        float tot = 0.f;
+        for (int k = 0; k < 16; k++) tot += red[k][cl];
+        float* o = out + (int64_t)y * out_stride + c;
+        *o = accumulate ? *o + tot : tot;
+    }
+}
+
+// Every reduction of one backward pass in one launch per level (instead of one or two launches per
+// reduction).  Job k: dst[c] += sum over nblk partial rows (stride floats apart) of column c < n.
+//   vec = 1: split-K weight-gradient partials (few rows, many columns): 4 columns per thread, rows in
+//            order -- reduce_splits4's sums; vec = 2: one column per thread -- reduce_splits's.
+//   vec = 0: per-block column partials: reduce_cols's scheme, level 1 over G row groups into mid[y][c]
+//            (or straight into dst when G = 1), level 2 over mid's G rows into dst.
+// Blocks of 1024 threads; b.tile0[k] = first block of job k at this level (a job with no tiles at a
+// level is skipped).  Same bits as the separate launches.
+constexpr int kRedJobs = 16;
+struct RedJob {
+    const float* part;
+    float* dst;
+    float* mid;
+    int64_t stride;
+    int nblk, n, G, vec;
+};
+struct RedBatch {
+    RedJob j[kRedJobs];
+    int tile0[kRedJobs + 1];
+    int njobs, level;
+};
+__global__ void __launch_bounds__(1024) reduce_batch(RedBatch b) {
+    __shared__ float red[16][64];
+    const int t = blockIdx.x;
+    int k = 0;
+    while (k + 1 < b.njobs && b.tile0[k + 1] <= t) k++;
+    const RedJob& J = b.j[k];
+    const int r = t - b.tile0[k];
+    if (J.vec == 1) {
+        const int64_t e = ((int64_t)r * 1024 + threadIdx.x) * 4;
+        if (e >= J.n) return;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+        for (int q = 0; q < J.nblk; q++) {
+            const float4 v = *reinterpret_cast<const float4*>(J.part + q * J.stride + e);
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        float4* o = reinterpret_cast<float4*>(J.dst + e);
+        const float4 v = *o;
+        *o = make_float4(v.x + s.x, v.y + s.y, v.z + s.z, v.w + s.w);
+        return;
+    }
+    if (J.vec == 2) {
+        const int64_t e = (int64_t)r * 1024 + threadIdx.x;
+        if (e >= J.n) return;
+        float s = 0.f;
+        for (int q = 0; q < J.nblk; q++) s += J.part[q * J.stride + e];
+        J.dst[e] = J.dst[e] + s;
+        return;
+    }
+    const int cx = (J.n + 63) / 64;
+    if (b.level == 1)
+        reduce_cols_tile(J.part, J.nblk, J.stride, J.n, r % cx, r / cx, J.G, J.G > 1 ? J.mid : J.dst, J.n, J.G > 1 ? 0 : 1,
+                         red);
+    else
+        reduce_cols_tile(J.mid, J.G, J.n, J.n, r, 0, 1, J.dst, 0, 1, red);
+}
+
 // Column reduction of per-block partials, deterministic, two levels:
 //   stage 1 (grid ceil(n/64) x G): block (x, y) sums partial rows b = y, y+G, ... of 64 columns
 //            (16 row groups of 64 threads, combined in LDS in a fixed order) -> out2[y][c]

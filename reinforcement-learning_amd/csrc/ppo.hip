@@ -47,6 +47,12 @@ struct Model {
     std::vector<float*> xhat, act, rstd;
     float *y = nullptr, *dy = nullptr, *dA = nullptr, *dZ = nullptr, *wpart = nullptr, *cpart = nullptr, *mid = nullptr;  // y: model output
     float* hpart = nullptr;  // rank-1 head dw / db partials, written by the last LayerNorm backward
+    // per-layer partial buffers of the deferred reductions (so a backward pass reduces them all at its end):
+    // split-K weight-gradient partials of layer l, LayerNorm-backward column partials of hidden layer l, and
+    // the loss kernel's output-bias partials
+    std::vector<float*> wpart_l, cpart_l;
+    float* lpart = nullptr;
+    int64_t midn = 0;  // floats per row of a reduction's level-1 sums (m.mid holds kRedJobs x 16 rows)
     uint16_t* wsplit = nullptr;  // split weight planes (x6 / H3 modes)
     int64_t nsplit = 0;
     float* wscale = nullptr;     // H3: per-row inverse scales of the weight planes
@@ -453,23 +459,85 @@ int splits_for(int mode, int rows, int out, int in) {
     return s < 1 ? 1 : s;
 }
 
-// dW (+)= dZ^T . X  over n rows (split-K over rows, fixed-order reduction into grad)
+// The reductions of one backward pass, launched together at its end: one mlp::reduce_batch launch per level
+// for all of them instead of one or two launches each (the partial buffers are per layer, so nothing is
+// overwritten before the flush).  Same summation orders, same bits as the separate launches.
+struct Reducer {
+    mlp::RedBatch b{};
+    Model* m = nullptr;
+    void add(const float* part, int nblk, int64_t stride, int n, float* dst, bool splits, hipStream_t s) {
+        if (b.njobs == mlp::kRedJobs) flush(s);
+        mlp::RedJob& J = b.j[b.njobs];
+        J.part = part;
+        J.dst = dst;
+        J.stride = stride;
+        J.nblk = nblk;
+        J.n = n;
+        J.mid = m->mid + (int64_t)b.njobs * 16 * m->midn;
+        if (splits) {
+            J.G = 1;
+            J.vec = (n % 4 == 0 && stride % 4 == 0 && ((uintptr_t)part & 15) == 0 && ((uintptr_t)dst & 15) == 0) ? 1 : 2;
+        } else {
+            J.G = nblk >= 256 ? 16 : 1;
+            J.vec = 0;
+            if ((int64_t)n > m->midn) throw rlgpu::Error(RLGPU_ERR_STATE, "reduction wider than its level-1 buffer");
+        }
+        b.njobs++;
+    }
+    void flush(hipStream_t s) {
+        if (!b.njobs) return;
+        bool two = false;
+        int t = 0;
+        for (int k = 0; k < b.njobs; k++) {
+            const mlp::RedJob& J = b.j[k];
+            b.tile0[k] = t;
+            t += J.vec == 1 ? (int)ceil_div(J.n, 4096) : J.vec == 2 ? (int)ceil_div(J.n, 1024) : (int)ceil_div(J.n, 64) * J.G;
+            two |= J.vec == 0 && J.G > 1;
+        }
+        b.tile0[b.njobs] = t;
+        b.level = 1;
+        hipLaunchKernelGGL(mlp::reduce_batch, dim3(t), dim3(1024), 0, s, b);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        if (two) {
+            t = 0;
+            for (int k = 0; k < b.njobs; k++) {
+                const mlp::RedJob& J = b.j[k];
+                b.tile0[k] = t;
+                t += (J.vec == 0 && J.G > 1) ? (int)ceil_div(J.n, 64) : 0;
+            }
+            b.tile0[b.njobs] = t;
+            b.level = 2;
+            hipLaunchKernelGGL(mlp::reduce_batch, dim3(t), dim3(1024), 0, s, b);
+            RLGPU_CHECK_HIP(hipGetLastError());
+        }
+        b.njobs = 0;
+    }
+};
+
+// dW (+)= dZ^T . X  over n rows (split-K over rows into `wpart`, fixed-order reduction into grad: now, or
+// through R at the end of the pass)
 void weight_grad(Model& m, const float* dZ, int out, const float* X, int64_t ldx, int in, int n, float* gW, hipStream_t s,
-                 bool x_tail_ok = false, const float* amax_dz = nullptr, const float* amax_x = nullptr, int64_t ldz = 0) {
+                 bool x_tail_ok = false, const float* amax_dz = nullptr, const float* amax_x = nullptr, int64_t ldz = 0,
+                 Reducer* R = nullptr, float* wpart = nullptr) {
+    if (!wpart) wpart = m.wpart;
     int splits = splits_for(m.mode, n, out, in);
     int chunk = (int)ceil_div(ceil_div(n, splits), kgran(m.mode)) * kgran(m.mode);
     int z = (int)ceil_div(n, chunk);
     // ldz > out: dZ rows zero-padded to ldz floats (16-byte loads across the row end)
     {
     ktime::Span span(ktime::WGRAD_GEMM, 2.0 * out * in * (double)n, s);
-    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, ldz ? ldz : out, X, ldx, m.wpart, in, nullptr, out, in, n, splits, s,
+    gemm_f32(m.mode, mlp::A_KI, mlp::B_KJ, dZ, ldz ? ldz : out, X, ldx, wpart, in, nullptr, out, in, n, splits, s,
              ldz > out, x_tail_ok, amax_dz, amax_x);
     }
     int64_t e = (int64_t)out * in;
-    if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)m.wpart & 15) == 0)
-        hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
+    if (R) {
+        R->add(wpart, z, e, (int)e, gW, true, s);
+        return;
+    }
+    if (e % 4 == 0 && ((uintptr_t)gW & 15) == 0 && ((uintptr_t)wpart & 15) == 0)
+        hipLaunchKernelGGL(mlp::reduce_splits4, dim3(ceil_div(e / 4, 256)), dim3(256), 0, s, wpart, z, e, e, gW, 1);
     else
-        hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, m.wpart, z, e, e, gW, 1);
+        hipLaunchKernelGGL(mlp::reduce_splits, dim3(ceil_div(e, 256)), dim3(256), 0, s, wpart, z, e, e, gW, 1);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -595,6 +663,15 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
     const int nh = nhid(m);
     const float* dA_top = m.dA;  // gradient of the last hidden layer's activation
     bool rank1 = false;          // rank-1 output layer folded into the last LayerNorm backward
+    // the pass's bias / LayerNorm / weight-gradient reductions, launched together at its end
+    // (RLGPU_BATCH_REDUCE=0: each right after its producer, as before)
+    static const bool batch = [] {
+        const char* e = getenv("RLGPU_BATCH_REDUCE");
+        return !(e && e[0] == '0');
+    }();
+    Reducer red;
+    red.m = &m;
+    Reducer* R = batch ? &red : nullptr;
     const Layer* O = m.head_only ? nullptr : &m.L[nh];
     if (!O) {
         dA_top = dout;
@@ -617,8 +694,11 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         // dout rows of dld floats (the policy loss pads them with zeros to a multiple of 4)
         const int dld = dout_ld(O->out);
         const Input a = nh > 0 ? Input{m.act[nh - 1], O->in, amax_slot(m, nh - 1), false} : x;
-        weight_grad(m, dout, O->out, a.X, a.ld, O->in, n, G + O->w, s, a.tail_ok, amax_slot(m, kAmaxOut), a.amax, dld);
-        if (dout_part)
+        weight_grad(m, dout, O->out, a.X, a.ld, O->in, n, G + O->w, s, a.tail_ok, amax_slot(m, kAmaxOut), a.amax, dld, R,
+                    m.wpart_l[nh]);
+        if (dout_part && R)
+            R->add(dout_part, dout_nblk, O->out, O->out, G + O->b, false, s);
+        else if (dout_part)
             reduce_partials(m, dout_part, dout_nblk, O->out, O->out, G + O->b, s);
         else if (dld == O->out)
             colsum_into(m, dout, n, O->out, G + O->b, s);
@@ -649,17 +729,23 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         ktime::Span span(ktime::LN_BWD, (double)n * ((r1 ? 4.0 : 4.0 * L.out) + 8.0 * L.out + 8.0), s);
         hipLaunchKernelGGL(lnb, dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
                            reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
-                           h->cfg.layer_norm, m.dZ, m.cpart, amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
+                           h->cfg.layer_norm, m.dZ, m.cpart_l[l], amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
                            r1 ? P + O->w : nullptr, r1 ? m.hpart : nullptr);
         RLGPU_CHECK_HIP(hipGetLastError());
         }
-        if (r1) reduce_partials(m, m.hpart, nb, O->in + 1, O->in + 1, G + O->w, s);  // [w | b] contiguous
-        // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b)
+        // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b); the rank-1
+        // head's [w | b] are contiguous too
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
-        reduce_partials(m, m.cpart, nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
-        RLGPU_CHECK_HIP(hipGetLastError());
+        if (R) {
+            if (r1) R->add(m.hpart, nb, O->in + 1, O->in + 1, G + O->w, false, s);
+            R->add(m.cpart_l[l], nb, 3 * (int64_t)L.out, ncol, G + L.b, false, s);
+        } else {
+            if (r1) reduce_partials(m, m.hpart, nb, O->in + 1, O->in + 1, G + O->w, s);
+            reduce_partials(m, m.cpart_l[l], nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
+        }
         const Input a = l > 0 ? Input{m.act[l - 1], L.in, amax_slot(m, l - 1), false} : x;
-        weight_grad(m, m.dZ, L.out, a.X, a.ld, L.in, n, G + L.w, s, a.tail_ok, amax_slot(m, kAmaxDZ + l), a.amax);
+        weight_grad(m, m.dZ, L.out, a.X, a.ld, L.in, n, G + L.w, s, a.tail_ok, amax_slot(m, kAmaxDZ + l), a.amax, 0, R,
+                    m.wpart_l[l]);
         float* dA = l > 0 ? m.dA : m.dX;  // the first layer's only when the input gradient is wanted
         if (!dA) continue;
         if (L.sb >= 0)
@@ -669,6 +755,7 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
             gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, dA, L.in, nullptr, n, L.in, L.out, 1, s, false,
                      false, amax_slot(m, kAmaxDZ + l), nullptr);
     }
+    red.flush(s);
 }
 
 void gather_obs(rlgpu_ppo* h, const float* obs, const int32_t* idx, int64_t start, int n, hipStream_t s) {
@@ -991,7 +1078,14 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
                 m.wpart = h->alloc<float>(wpart_max);
                 m.cpart = h->alloc<float>(nb * 3 * std::max(H, omax) + nb);
                 m.hpart = h->alloc<float>(nb * ((int64_t)H + 1));
-                m.mid = h->alloc<float>(16 * 3 * (int64_t)std::max(std::max(H, omax) + 1, 1024));
+                // the deferred reductions' per-layer partials and level-1 rows (Reducer)
+                for (auto& L : m.L) {
+                    m.wpart_l.push_back(h->alloc<float>((int64_t)splits_for(m.mode, (int)R, L.out, L.in) * L.in * L.out));
+                    m.cpart_l.push_back(h->alloc<float>(nb * 3 * (int64_t)L.out));
+                }
+                m.lpart = h->alloc<float>(nb * (int64_t)omax);
+                m.midn = 3 * (int64_t)std::max(std::max(H, omax) + 1, 1024);
+                m.mid = h->alloc<float>((int64_t)mlp::kRedJobs * 16 * m.midn);
                 if (m.nsplit) m.wsplit = h->alloc<uint16_t>(m.nsplit);
                 if (m.mode == RLGPU_GEMM_F16X3 && m.nscale) m.wscale = h->alloc<float>(m.nscale);
             }
@@ -1259,9 +1353,9 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
         hipLaunchKernelGGL(ppo::policy_loss_any(A), dim3(pl_blocks), dim3(256), 0, s, pm.y, d_masks, d_actions, d_old_logp, d_adv,
                            d_index, start, n, A, d_adv_stats, bsr, h->cfg.clip_range, h->cfg.entropy_scale,
-                           1.f / std::log((float)A), pm.dy, dout_ld(A), d_metrics, pm.cpart, amax_slot(pm, kAmaxOut));
+                           1.f / std::log((float)A), pm.dy, dout_ld(A), d_metrics, pm.lpart, amax_slot(pm, kAmaxOut));
         RLGPU_CHECK_HIP(hipGetLastError());
-        backward(h, 0, xin, n, pm.dy, s, pm.cpart, pl_blocks);
+        backward(h, 0, xin, n, pm.dy, s, pm.lpart, pl_blocks);
         if (!serial) RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
         if (h->shared()) {  // (ppoLoss + criticLoss).backward() through the shared features (:498)
             const int64_t e = (int64_t)n * h->M[2].out;

@@ -64,11 +64,24 @@ def _run(world, kw, iters):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, kw, iters)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=280) for _ in range(world)], key=lambda r: r["rank"])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    return res
+    import queue
+    import time
+    res, deadline = [], time.time() + 280
+    try:
+        while len(res) < world:  # a rank that dies must fail the test now, not after the queue's timeout
+            try:
+                res.append(q.get(timeout=5))
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                assert not dead, f"a rank exited with {dead}"
+                assert time.time() < deadline, "ranks did not finish in time"
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    return sorted(res, key=lambda r: r["rank"])
 
 
 @pytest.mark.timeout(400)
@@ -98,11 +111,11 @@ def test_two_ranks_equal_one_rank(gpu):
 
 @pytest.mark.timeout(400)
 def test_trajectory_mode_rank_without_finished_rows(gpu):
-    """Rank 0's episodes cannot end inside its small step store (300 s episodes, 80 rows), so it brings no
-    rows; rank 1's (0.2 s episodes) do.  Both ranks run 3 iterations to the end with the same parameters
-    and return statistics."""
+    """Rank 0's episodes (4.5 s = 67 steps, inside its 80-row step store) cannot end in the few collection
+    steps rank 1's 0.2 s episodes need to fill an iteration, so rank 0 brings no rows; rank 1 does.  Both
+    ranks run 3 iterations to the end with the same parameters and return statistics."""
     kw = dict(num_arenas=16, experience_mode=1, experience_capacity=80, ts_per_itr=512, mini_batch_size=512, seed=7,
-              per_rank={0: dict(max_episode_duration=300.0), 1: dict(max_episode_duration=0.2)})
+              per_rank={0: dict(max_episode_duration=4.5), 1: dict(max_episode_duration=0.2)})
     res = _run(2, kw, 3)
     np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
     assert res[0]["ret"] == res[1]["ret"]

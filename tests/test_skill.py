@@ -161,7 +161,7 @@ def test_skill_run_mixed_version_rollout_oracle_checked(gpu):
     dd = arena_diff(_arenas(tr.env), _arenas(o))
     assert not dd, "after the run:\n" + "\n".join(dd)
     log = tr.log[-1]
-    assert steps[0] == tr.steps_run and steps[0] > 10
+    assert steps[0] == tr.steps_run and steps[0] >= 5
     assert len(goals) == len(oracle_goals) and len(goals) >= 4, (len(goals), len(oracle_goals))
     # an independent fp32 replay of the ratings from the oracle's goals
     new_team = log["new_team"]

@@ -265,3 +265,49 @@ def test_x86_env_relative_error_report(gpu):
     print(f"x86 (MSVC x64) arithmetic, {n * steps} arena-steps: max relative error {rel}")
     assert n * steps >= 10000
     assert all(v <= 1e-5 for v in rel.values()), rel
+
+
+def test_rsqrt_formula_detection():
+    """On an Intel host every table entry is RNE-12(1 / sqrt(interval midpoint)): the kernels compute it
+    (formula_bits 12) instead of reading the table; a numpy restatement of the formula reproduces the table."""
+    from rlgpu import arith
+    t, bits = arith.rsqrt_table()
+    fb = arith.formula_bits()
+    assert fb >= 0
+    if fb == 0:
+        pytest.skip("this host's rsqrtss is not the midpoint formula: the kernels read the table")
+    idx = np.arange(t.size, dtype=np.uint32)
+    p, h = idx >> bits, idx & ((1 << bits) - 1)
+    xm = (((127 + p) << 23) | (h << (23 - bits)) | (1 << (22 - bits))).astype(np.uint32).view(np.float32)
+    y = (1.0 / np.sqrt(xm.astype(np.float64))).view(np.uint64)
+    drop = np.uint64(52 - fb)
+    half = np.uint64(1) << (drop - np.uint64(1))
+    r = (y + (half - np.uint64(1)) + ((y >> drop) & np.uint64(1))) & ~((np.uint64(1) << drop) - np.uint64(1))
+    np.testing.assert_array_equal(r.view(np.float64).astype(np.float32).view(np.uint32), t)
+
+
+@pytest.mark.gpu
+def test_device_rsqrtss_every_input_of_one_binade_pair(gpu):
+    """The kernels' rsqrtss (the computed entries, or the table) == the instruction on all 2^24 inputs of
+    [1, 4), on random inputs of every exponent and on the special values."""
+    import torch
+    from rlgpu import arith
+    u = np.arange(1 << 24, dtype=np.uint32)
+    x = (((127 + (u >> 23)) << 23) | (u & 0x7fffff)).astype(np.uint32).view(np.float32)
+    rng = np.random.default_rng(5)
+    r = rng.integers(0x00800000, 0x7f800000, 1 << 20, dtype=np.uint32).view(np.float32)
+    sp = np.array([0x0, 0x80000000, 0x1, 0x7fffff, 0x80400000, 0x7f800000, 0xff800000, 0xbf800000, 0x00800000,
+                   0x7f7fffff, 0x3f800000, 0x40800000], np.uint32).view(np.float32)
+    allx = np.concatenate([x, r, sp])
+    pad = (-allx.size) % 12
+    allx = np.concatenate([allx, np.ones(pad, np.float32)])
+    rows = np.zeros((allx.size // 12, 24), np.float32)
+    rows[:, :12] = allx.reshape(-1, 12)
+    got = np.empty((len(rows), 12), np.float32)
+    for s in range(0, len(rows), 1 << 18):
+        got[s:s + (1 << 18)] = arith.linear_math_queries(6, 0, torch.from_numpy(rows[s:s + (1 << 18)]).to(gpu)).cpu().numpy()
+    got = got.reshape(-1)
+    want = oracle.rsqrtss(allx)
+    same = (_bits(got) == _bits(want)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), (allx[~same][:4], got[~same][:4], want[~same][:4])
+    print(f"device rsqrtss == the instruction on {allx.size} inputs (formula bits {arith.formula_bits()})")

@@ -20,11 +20,12 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 8  # env steps before profiling (late-episode states)
 dev = torch.device("cuda:0")
 mesh_name = sys.argv[4] if len(sys.argv) > 4 else "synthetic"
+arith = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # include/rlgpu_arith.h mode
 if mesh_name == "procedural":
     from rlgpu.mesh import procedural_soccar
-    env = EnvSet(n, seed=1234, device=dev, mesh=procedural_soccar())
+    env = EnvSet(n, seed=1234, device=dev, mesh=procedural_soccar(), arith=arith)
 else:
-    env = EnvSet(n, seed=1234, device=dev)
+    env = EnvSet(n, seed=1234, device=dev, arith=arith)
 gen = torch.Generator(device=dev).manual_seed(7)
 acts = torch.empty(4 * n, dtype=torch.int32, device=dev)
 for i in range(warm):
