@@ -48,11 +48,6 @@ int rlgpu_x86_rsqrt_table(uint32_t* h_table, int64_t cap, int32_t* bits);
 /* The table-driven rsqrtss emulation the kernels use, evaluated on the host (tests compare it with the
  * instruction). */
 float rlgpu_x86_rsqrtss_emulated(float x);
-/* When every table entry is 1 / sqrt(the midpoint of its input interval) rounded to nearest-even at the
- * entries' significant bits (Intel's rsqrtss, with a margin far above double rounding), the kernels compute
- * the entry in double instead of reading the table: returns those significant bits (12 on Intel), 0 when
- * the kernels read the table (RLGPU_RSQRT_LUT=1 forces it), -1 without a table. */
-int rlgpu_x86_rsqrt_formula_bits(void);
 
 /* The mode-dependent LinearMath operations of the arena kernels on the device, one query per lane (tests
  * compare them with the oracle's restatement): op 0 btVector3::normalize v[3] -> v[3]; 1

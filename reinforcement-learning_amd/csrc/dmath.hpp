@@ -27,7 +27,6 @@ namespace rl {
 struct RsqrtLut {
     const uint32_t* t;  // [2 << bits]
     int bits;
-    int sig;  // > 0: the entries are computed (rlgpu_x86_rsqrt_formula_bits), not read
 };
 static __constant__ RsqrtLut kRsqrtLut;
 
@@ -42,21 +41,8 @@ HD float x86_rsqrtss(float x) {
     if (e == 0xffu) return m ? __uint_as_float(u | 0x400000u) : ((u >> 31) ? __uint_as_float(0xffc00000u) : 0.f);
     if (u >> 31) return __uint_as_float(0xffc00000u);
     const int E = (int)e - 127, p = E & 1, q = (E - p) / 2;
-    const int bits = kRsqrtLut.bits, sig = kRsqrtLut.sig;
-    uint32_t r;
-    if (sig > 0) {
-        // the entry without a memory read: 1 / sqrt(x_mid) in double, rounded to nearest-even at `sig` bits
-        // (exact for this host's table, checked entry by entry at load, x86_arith.cpp formula_sig)
-        const float xm = __uint_as_float(((127u + (uint32_t)p) << 23) | ((m >> (23 - bits)) << (23 - bits)) | (1u << (22 - bits)));
-        const double y = 1.0 / sqrt((double)xm);
-        const uint64_t u = (uint64_t)__double_as_longlong(y);
-        const int drop = 52 - sig;
-        const uint64_t half = 1ull << (drop - 1);
-        const uint64_t rr = (u + (half - 1) + ((u >> drop) & 1ull)) & ~((1ull << drop) - 1);
-        r = __float_as_uint((float)__longlong_as_double((long long)rr));
-    } else {
-        r = kRsqrtLut.t[((uint32_t)p << bits) | (m >> (23 - bits))];
-    }
+    const int bits = kRsqrtLut.bits;
+    const uint32_t r = kRsqrtLut.t[((uint32_t)p << bits) | (m >> (23 - bits))];
     return __uint_as_float((uint32_t)((int32_t)r - q * (1 << 23)));
 #elif defined(__x86_64__) || defined(__i386__)
     return _mm_cvtss_f32(_mm_rsqrt_ss(_mm_set_ss(x)));

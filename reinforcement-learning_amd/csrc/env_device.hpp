@@ -6,7 +6,9 @@
 
 namespace rl {
 
-extern __constant__ EnvConst C;
+// the env set constants (make_env_const): one copy per translation unit, each uploaded by env.hip
+// (ensure_const: its own for the test kernels, the specialised env kernels' through env_kN_upload)
+static __constant__ EnvConst C;
 
 #define DEV __device__ __forceinline__
 
@@ -28,7 +30,12 @@ DEV v3 bpos(ArenaLDS* A, int i) { return ld3(body(A, i)->pos); }
 DEV v3 bvel(ArenaLDS* A, int i) { return ld3(body(A, i)->vel); }
 DEV v3 bang(ArenaLDS* A, int i) { return ld3(body(A, i)->angvel); }
 DEV m3 brot(ArenaLDS* A, int i) { return ldm(body(A, i)->rot); }
-DEV int arith(const ArenaLDS* A) { return A->a.arith; }  // the set's RLGPU_ARITH_* mode
+// the set's RLGPU_ARITH_* mode: a constant in the specialised env kernels (env_step.hpp), else the arena's
+#ifdef RLGPU_ENV_ARITH
+DEV int arith(const ArenaLDS*) { return RLGPU_ENV_ARITH; }
+#else
+DEV int arith(const ArenaLDS* A) { return A->a.arith; }
+#endif
 DEV float binv_mass(int i) { return i == 0 ? C.ball_inv_mass : C.car_inv_mass; }
 DEV v3 binv_iner(int i) { return i == 0 ? C.ball_inv_inertia : C.car_inv_inertia; }
 DEV v3 vel_at(ArenaLDS* A, int i, v3 rel) { return bvel(A, i) + cross(bang(A, i), rel); }

@@ -57,7 +57,8 @@ struct SFace {
     uint8_t f[3];  // adjacent faces
     uint8_t e[3];  // adjacent faces' edge indices
     uint8_t pass;
-    uint16_t l[2];  // list links (prev, next)
+    uint16_t l[2];  // stock-list links (prev, next)
+    uint16_t seq;   // > 0: in the hull, appended seq-th (0: not in the hull; findbest)
 };
 struct GjkScratch {
     SSV sv[kSV];
@@ -783,8 +784,9 @@ DEV bool enclose_origin(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s) {
 
 // ---- EPA (cpp:555-901) over scratch faces
 struct Epa {
-    uint16_t hull;    // hull list root
+    uint16_t hull;    // hull list root (unused: the hull is the faces with seq > 0)
     int hull_count;
+    int seq;          // hull appends so far (the newest face is the hull list's root in Bullet)
     uint16_t stock;   // recycled faces (pushed at the stock's front)
     int fresh;        // stock tail: faces fresh..255 never taken, in index order (EPA::Initialize)
     int status;       // Valid 0 .. Failed 9 (EPA::eStatus order)
@@ -807,6 +809,19 @@ DEV void list_remove(ScrT<AS>& S, uint16_t& root, int face) {
 }
 template <int AS>
 DEV void stock_push(ScrT<AS>& S, Epa& E, int face) { list_append(S, E.stock, face); }
+// The hull as Bullet keeps it, a list appended at its root, is only ever walked by findbest from the root;
+// the walk's order is newest first, so each face's append number stands in for the links (no list updates,
+// and findbest reads independent slots instead of chasing links)
+template <int AS>
+DEV void hull_append(ScrT<AS>& S, Epa& E, int face) {
+    S.fc[face].seq = (uint16_t)(++E.seq);
+    E.hull_count++;
+}
+template <int AS>
+DEV void hull_remove(ScrT<AS>& S, Epa& E, int face) {
+    S.fc[face].seq = 0;
+    E.hull_count--;
+}
 template <int AS>
 DEV void bind(ScrT<AS>& S, int fa, int ea, int fb, int eb) {
     S.fc[fa].e[ea] = (uint8_t)eb;
@@ -853,8 +868,7 @@ DEV int newface(ScrT<AS>& S, Epa& E, int a, int b, int c, bool forced) {
         S.overflow = 1;  // Bullet still has stock faces: too small a work set
         return -1;
     }
-    list_append(S, E.hull, face);
-    E.hull_count++;
+    hull_append(S, E, face);
     auto& F = S.fc[face];
     F.pass = 0;
     F.c[0] = (uint8_t)a;
@@ -875,20 +889,26 @@ DEV int newface(ScrT<AS>& S, Epa& E, int a, int b, int c, bool forced) {
         stv(F.n, n);
         E.status = 2;  // Degenerated
     }
-    list_remove(S, E.hull, face);
-    E.hull_count--;
+    hull_remove(S, E, face);
     stock_push(S, E, face);
     return -1;
 }
+// EPA::findbest (cpp:840-862): the first face of least d^2 on the walk from the hull's root, i.e. of the
+// faces of least d^2 the one appended last.  Every allocated slot is read (independent loads, several in
+// flight) instead of following the links one dependent load at a time.
 template <int AS>
 DEV int findbest(const ScrT<AS>& S, const Epa& E) {
-    int minf = E.hull;
-    float mind = S.fc[minf].d * S.fc[minf].d;
-    for (int f = S.fc[minf].l[1]; f != kNone; f = S.fc[f].l[1]) {
-        const float sqd = S.fc[f].d * S.fc[f].d;
-        if (sqd < mind) {
+    int minf = -1, bestseq = 0;
+    float mind = 0.f;
+#pragma unroll 4
+    for (int f = 0; f < E.fresh; f++) {
+        const int sq = S.fc[f].seq;
+        const float d = S.fc[f].d;
+        const float sqd = d * d;
+        if (sq > 0 && (minf < 0 || sqd < mind || (sqd == mind && sq > bestseq))) {
             minf = f;
             mind = sqd;
+            bestseq = sq;
         }
     }
     return minf;
@@ -959,8 +979,7 @@ GJK_CALLED bool expand(ScrT<AS>& S, Epa& E, unsigned pass, int w, int f0, int e0
             }
         } else {
             if (ret) {
-                list_remove(S, E.hull, f);
-                E.hull_count--;
+                hull_remove(S, E, f);
                 stock_push(S, E, f);
             }
             pop = true;
@@ -975,6 +994,7 @@ GJK_CALLED int epa_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 gue
     Epa E;
     E.hull = kNone;
     E.hull_count = 0;
+    E.seq = 0;
     E.stock = kNone;
     E.fresh = 0;
     E.status = 9;
@@ -1035,8 +1055,7 @@ GJK_CALLED int epa_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 gue
                         GJK_MARK(7);
                         if (valid && (hnf >= 3)) {
                             bind(S, hcf, 1, hff, 2);
-                            list_remove(S, E.hull, best);
-                            E.hull_count--;
+                            hull_remove(S, E, best);
                             stock_push(S, E, best);
                             best = findbest(S, E);
                             copy_face(outer, S.fc[best]);

@@ -41,7 +41,7 @@ std::vector<float> builtin_mesh_bt();
 
 // This host's rsqrtss table for the x86 arithmetic modes (host/x86_arith.cpp, rlgpu_arith.h): 2 << *bits
 // entries; throws rlgpu::Error(RLGPU_ERR_UNSUPPORTED) when the host has none usable.
-const std::vector<uint32_t>& x86_rsqrt_table_or_throw(int* bits, int* sig);
+const std::vector<uint32_t>& x86_rsqrt_table_or_throw(int* bits);
 
 // GameState::UpdateFromArena on arena records (host/gamestate.cpp, include/rlgpu_gamestate.h), and the
 // pad index map it reads (GameState.cpp:11-51: CommonValues::BOOST_LOCATIONS[i] -> arena pad, env.hip)

@@ -28,7 +28,6 @@ namespace {
 struct RsqrtTable {
     bool ok = false;
     int bits = 0;
-    int sig = 0;  // > 0: every entry is 1/sqrt(its interval's midpoint) rounded to sig mantissa bits (formula_sig)
     std::vector<uint32_t> t;  // [2 << bits]
     std::string why;
 };
@@ -64,36 +63,6 @@ float emulate(const RsqrtTable& T, float x) {
     const int E = (int)e - 127, p = E & 1, q = (E - p) / 2;
     const uint32_t r = T.t[((uint32_t)p << T.bits) | (m >> (23 - T.bits))];
     return bitsf((uint32_t)((int32_t)r - q * (1 << 23)));
-}
-
-// The entries of an Intel rsqrtss table are 1 / sqrt(x_mid), x_mid the midpoint of the entry's input
-// interval, rounded to nearest-even at the entries' significant bits.  When that holds for every entry with
-// a margin far above double rounding (2^-40 relative to the rounding boundary), the kernels compute the
-// entry in double instead of loading it (no table read on the normalize path); otherwise (another vendor's
-// approximation) they keep the table.  Returns the significant bits, or 0.
-int formula_sig(const RsqrtTable& T) {
-    int tz = 23;
-    for (uint32_t r : T.t)
-        if (r & 0x7fffffu) tz = std::min(tz, __builtin_ctz(r & 0x7fffffu));
-    const int sig = 23 - tz;
-    if (sig < 1 || sig > 22) return 0;
-    const int drop = 52 - sig;
-    for (uint32_t i = 0; i < T.t.size(); i++) {
-        const uint32_t p = i >> T.bits, h = i & ((1u << T.bits) - 1u);
-        const float xm = bitsf(((127u + p) << 23) | (h << (23 - T.bits)) | (1u << (22 - T.bits)));
-        const double y = 1.0 / std::sqrt((double)xm);
-        uint64_t u;
-        std::memcpy(&u, &y, 8);
-        const uint64_t low = u & ((1ull << drop) - 1), half = 1ull << (drop - 1);
-        // the margin to the halfway point, in units of the double's last place
-        const uint64_t dist = low > half ? low - half : half - low;
-        if (dist < (1ull << (52 - 40))) return 0;
-        const uint64_t r = (u + (half - 1) + ((u >> drop) & 1)) & ~((1ull << drop) - 1);
-        double rd;
-        std::memcpy(&rd, &r, 8);
-        if (fbits((float)rd) != T.t[i]) return 0;
-    }
-    return sig;
 }
 
 RsqrtTable capture() {
@@ -142,7 +111,6 @@ RsqrtTable capture() {
         }
     }
     T.ok = true;
-    T.sig = formula_sig(T);
     return T;
 #endif
 }
@@ -156,16 +124,11 @@ const RsqrtTable& rsqrt_table() {
     return T;
 }
 
-// for env.hip: the table, or an RLGPU_ERR_UNSUPPORTED error naming why the host's cannot be used; *sig: the
-// formula's significant bits (0: the kernels read the table; RLGPU_RSQRT_LUT=1 forces the table)
-const std::vector<uint32_t>& x86_rsqrt_table_or_throw(int* bits, int* sig) {
+// for env.hip: the table, or an RLGPU_ERR_UNSUPPORTED error naming why the host's cannot be used
+const std::vector<uint32_t>& x86_rsqrt_table_or_throw(int* bits) {
     const RsqrtTable& T = rsqrt_table();
     if (!T.ok) throw Error(RLGPU_ERR_UNSUPPORTED, "x86 arithmetic modes need this host's rsqrtss table: " + T.why);
     *bits = T.bits;
-    if (sig) {
-        const char* e = getenv("RLGPU_RSQRT_LUT");
-        *sig = (e && e[0] == '1') ? 0 : T.sig;
-    }
     return T.t;
 }
 
@@ -175,18 +138,13 @@ extern "C" int rlgpu_x86_rsqrt_table(uint32_t* h_table, int64_t cap, int32_t* bi
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(bits, "rlgpu_x86_rsqrt_table: null bits");
         int b = 0;
-        const std::vector<uint32_t>& t = rlgpu::x86_rsqrt_table_or_throw(&b, nullptr);
+        const std::vector<uint32_t>& t = rlgpu::x86_rsqrt_table_or_throw(&b);
         *bits = b;
         if (h_table) {
             RLGPU_REQUIRE(cap >= (int64_t)t.size(), "rlgpu_x86_rsqrt_table: table needs 2 << bits entries");
             std::memcpy(h_table, t.data(), t.size() * sizeof(uint32_t));
         }
     });
-}
-
-extern "C" int rlgpu_x86_rsqrt_formula_bits(void) {
-    const rlgpu::RsqrtTable& T = rlgpu::rsqrt_table();
-    return T.ok ? T.sig : -1;
 }
 
 extern "C" float rlgpu_x86_rsqrtss_emulated(float x) {

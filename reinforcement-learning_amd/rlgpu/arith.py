@@ -27,13 +27,6 @@ def rsqrt_table():
     return t, bits.value
 
 
-def formula_bits():
-    """The significant bits of the kernels' computed rsqrtss entries (rlgpu_x86_rsqrt_formula_bits): > 0 when
-    every table entry is 1 / sqrt(its interval midpoint) rounded there (the kernels then read no table), 0 when
-    they read the table, -1 without one."""
-    return int(_lib.lib().rlgpu_x86_rsqrt_formula_bits())
-
-
 def rsqrtss_emulated(x, table=None):
     """The kernels' table lookup (dmath.hpp x86_rsqrtss) in numpy, for float32 arrays."""
     t, bits = rsqrt_table() if table is None else table

@@ -267,28 +267,9 @@ def test_x86_env_relative_error_report(gpu):
     assert all(v <= 1e-5 for v in rel.values()), rel
 
 
-def test_rsqrt_formula_detection():
-    """On an Intel host every table entry is RNE-12(1 / sqrt(interval midpoint)): the kernels compute it
-    (formula_bits 12) instead of reading the table; a numpy restatement of the formula reproduces the table."""
-    from rlgpu import arith
-    t, bits = arith.rsqrt_table()
-    fb = arith.formula_bits()
-    assert fb >= 0
-    if fb == 0:
-        pytest.skip("this host's rsqrtss is not the midpoint formula: the kernels read the table")
-    idx = np.arange(t.size, dtype=np.uint32)
-    p, h = idx >> bits, idx & ((1 << bits) - 1)
-    xm = (((127 + p) << 23) | (h << (23 - bits)) | (1 << (22 - bits))).astype(np.uint32).view(np.float32)
-    y = (1.0 / np.sqrt(xm.astype(np.float64))).view(np.uint64)
-    drop = np.uint64(52 - fb)
-    half = np.uint64(1) << (drop - np.uint64(1))
-    r = (y + (half - np.uint64(1)) + ((y >> drop) & np.uint64(1))) & ~((np.uint64(1) << drop) - np.uint64(1))
-    np.testing.assert_array_equal(r.view(np.float64).astype(np.float32).view(np.uint32), t)
-
-
 @pytest.mark.gpu
 def test_device_rsqrtss_every_input_of_one_binade_pair(gpu):
-    """The kernels' rsqrtss (the computed entries, or the table) == the instruction on all 2^24 inputs of
+    """The kernels' rsqrtss (this host's table, uploaded to the device) == the instruction on all 2^24 inputs of
     [1, 4), on random inputs of every exponent and on the special values."""
     import torch
     from rlgpu import arith
@@ -310,4 +291,4 @@ def test_device_rsqrtss_every_input_of_one_binade_pair(gpu):
     want = oracle.rsqrtss(allx)
     same = (_bits(got) == _bits(want)) | (np.isnan(got) & np.isnan(want))
     assert same.all(), (allx[~same][:4], got[~same][:4], want[~same][:4])
-    print(f"device rsqrtss == the instruction on {allx.size} inputs (formula bits {arith.formula_bits()})")
+    print(f"device rsqrtss == the instruction on {allx.size} inputs (table of {arith.rsqrt_table()[0].size} entries)")
