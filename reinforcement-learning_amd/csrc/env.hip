@@ -777,6 +777,57 @@ __global__ void __launch_bounds__(16) box_triangle_kernel(int n, const float* ro
     o[6] = hit ? pt.z : 0.f;
     o[7] = hit ? d : 0.f;
 }
+// lds == 2: the env kernel's narrowphase scheme -- 64 lanes each run a query with the penetration solver
+// deferred, then the whole wave runs the deferred queries one at a time with the wave-mode EPA
+__device__ __forceinline__ void bt_load(int i, const float* rot, const float* centre, const float* tri, int ar, m3& R, v3& c,
+                                        gjk::Shape& sh) {
+    const float* r = rot + 9 * (size_t)i;
+    R = m3{v3{r[0], r[1], r[2]}, v3{r[3], r[4], r[5]}, v3{r[6], r[7], r[8]}};
+    c = v3{centre[3 * (size_t)i], centre[3 * (size_t)i + 1], centre[3 * (size_t)i + 2]};
+    const float* t = tri + 9 * (size_t)i;
+    sh = gjk::Shape{C.car_impl, C.car_margin, v3{t[0], t[1], t[2]}, v3{t[3], t[4], t[5]}, v3{t[6], t[7], t[8]}, ar};
+}
+__device__ __forceinline__ void bt_store(float* out, int i, bool hit, v3 nrm, v3 pt, float d) {
+    float* o = out + 8 * (size_t)i;
+    o[0] = hit ? 1.f : 0.f;
+    o[1] = hit ? nrm.x : 0.f;
+    o[2] = hit ? nrm.y : 0.f;
+    o[3] = hit ? nrm.z : 0.f;
+    o[4] = hit ? pt.x : 0.f;
+    o[5] = hit ? pt.y : 0.f;
+    o[6] = hit ? pt.z : 0.f;
+    o[7] = hit ? d : 0.f;
+}
+__global__ void __launch_bounds__(64) box_triangle_wave_kernel(int n, const float* rot, const float* centre, const float* tri,
+                                                               const float* cbt, float* out, gjk::GjkScratch* scratch, int ar) {
+    __shared__ char small[gjk::kSmallBytes];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    gjk::Scr slow = gjk::hbm_view(scratch + i);  // scratch holds a set for every lane of the grid
+    bool deferred = false;
+    if (i < n) {
+        m3 R;
+        v3 c, nrm, pt;
+        gjk::Shape sh;
+        float d = 0.f;
+        bt_load(i, rot, centre, tri, ar, R, c, sh);
+        const bool hit = gjk::box_triangle(R, c, sh, cbt[i], nullptr, nullptr, slow, nrm, pt, d, nullptr, gjk::kPenDefer,
+                                           &deferred);
+        if (!deferred) bt_store(out, i, hit, nrm, pt, d);
+    }
+    uint64_t m = __ballot(deferred);
+    while (m) {
+        const int q = blockIdx.x * 64 + gjk::lowbit(m);
+        m &= m - 1ull;
+        m3 R;
+        v3 c, nrm, pt;
+        gjk::Shape sh;
+        float d = 0.f;
+        bt_load(q, rot, centre, tri, ar, R, c, sh);
+        gjk::Scr wave = gjk::wave_view(small);
+        const bool hit = gjk::box_triangle(R, c, sh, cbt[q], &wave, nullptr, slow, nrm, pt, d, nullptr, gjk::kPenWave);
+        if (threadIdx.x == 0) bt_store(out, q, hit, nrm, pt, d);
+    }
+}
 }  // namespace rl
 
 extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
@@ -789,10 +840,16 @@ extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const f
         ensure_const();
         if (rl::sse_api(arith)) ensure_rsqrt();
         hipStream_t s = (hipStream_t)stream;
+        RLGPU_REQUIRE(lds_first >= 0 && lds_first <= 2, "rlgpu_box_triangle_queries: lds_first must be 0, 1 or 2");
         void* scratch = nullptr;
-        RLGPU_CHECK_HIP(hipMallocAsync(&scratch, (size_t)n * sizeof(rl::gjk::GjkScratch), s));
-        hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 16)), dim3(16), 0, s, n, d_rot, d_centre, d_tri,
-                           d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)(lds_first != 0), (int)arith);
+        const int lanes = lds_first == 2 ? rlgpu::ceil_div(n, 64) * 64 : n;
+        RLGPU_CHECK_HIP(hipMallocAsync(&scratch, (size_t)lanes * sizeof(rl::gjk::GjkScratch), s));
+        if (lds_first == 2)
+            hipLaunchKernelGGL(rl::box_triangle_wave_kernel, dim3(lanes / 64), dim3(64), 0, s, n, d_rot, d_centre, d_tri,
+                               d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)arith);
+        else
+            hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 16)), dim3(16), 0, s, n, d_rot, d_centre,
+                               d_tri, d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)lds_first, (int)arith);
         RLGPU_CHECK_HIP(hipGetLastError());
         RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
     });

@@ -309,13 +309,12 @@ DEV int bp_home(v3 mn) {
     return (i * C.bp_cells[1] + j) * C.bp_cells[2] + k;
 }
 // bp_key (env_device.hpp): a body's position in every cell's dynamic list
-// one lane per arena, on this tick's broadphase AABBs (after predictUnconstraintMotion)
+// one lane per arena, on this tick's broadphase AABBs (after predictUnconstraintMotion) and the home cells the
+// body lanes computed into A->u.bp.cell: setAabb for the bodies in creation order
 DEV void bp_update(ArenaLDS* A) {
 #pragma unroll 1
     for (int bi = 0; bi < 5; bi++) {
-        v3 mn, mx;
-        broad_aabb(A, bi, mn, mx);
-        const int cell = bp_home(mn) + 1;
+        const int cell = A->u.bp.cell[bi];
         if (cell == A->s.env.bp_cell[bi]) continue;
         A->s.env.bp_cell[bi] = (uint16_t)cell;
         int key[5];
@@ -443,10 +442,12 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
                dl.z >= 0 ? C.car_half.z : -C.car_half.z};
     return R * lv + c;
 }
-// One car hitbox vs mesh triangle: Bullet's GJK / EPA query (gjk.hpp) and its candidate.  Penetration-
-// solver work sets: the arena's small LDS set past the candidate list (free during the narrowphase), one
-// lane at a time, else this lane's HBM scratch.
-__device__ __noinline__ void box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2) {
+// One car hitbox vs mesh triangle: Bullet's GJK / EPA query (gjk.hpp) and its candidate.  defer: a query
+// that needs the penetration solver stops there and returns true (narrow_deferred reruns it on the whole
+// wave); else the solver runs here, in the arena's small LDS set past the candidate list (free during the
+// narrowphase), one lane at a time, or in this lane's HBM scratch.
+__device__ __noinline__ bool box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2,
+                                           bool defer) {
     const m3 R = brot(A, bi);
     const v3 c = car_box_center(A, bi);
     gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
@@ -454,12 +455,32 @@ __device__ __noinline__ void box_tri_query(ArenaLDS* A, const MeshView& M, int b
     const gjk::Shape sh{C.car_impl, C.car_margin, v0, v1, v2, arith(A)};
     v3 n, pb;
     float d;
-    if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen))
+    bool deferred = false;
+    if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen,
+                          defer ? gjk::kPenDefer : gjk::kPenInline, &deferred))
         emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
+    return deferred;
 }
+// A deferred query (queue entry e) on every lane of the wave: the penetration solver's EPA keeps its
+// polytope in the wave's registers (gjk::epa_wave), its support vertices in the arena's small LDS set
+__device__ __noinline__ void box_tri_query_wave(ArenaLDS* A, const MeshView& M, uint32_t e) {
+    const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)((e >> 25) & 7u);
+    const float4 a = M.tri[3 * (size_t)t], b = M.tri[3 * (size_t)t + 1], cc = M.tri[3 * (size_t)t + 2];
+    const m3 R = brot(A, bi);
+    const v3 c = car_box_center(A, bi);
+    gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
+    gjk::Scr wave = gjk::wave_view((char*)&A->u.cand[kMaxCand]);
+    const gjk::Shape sh{C.car_impl, C.car_margin, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{cc.x, cc.y, cc.z}, arith(A)};
+    v3 n, pb;
+    float d;
+    const bool hit = gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &wave, nullptr, slow, n, pb, d, &A->a.npen, gjk::kPenWave);
+    if (hit && threadIdx.x == 0) emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
+}
+constexpr uint32_t kDeferred = 0x80000000u;  // queue entry flag: the query waits for narrow_deferred
 // the queued box-triangle queries of the workgroup's arenas, dealt round-robin over all its lanes (an
 // arena with many triangle contacts borrows the lanes of quiet ones); base = the workgroup's arenas,
-// nvalid = how many of them exist
+// nvalid = how many of them exist.  Queries that need the penetration solver are flagged for
+// narrow_deferred (a full wave: kWG == 64), else run it in place.
 DEV void narrow_queue(ArenaLDS* base, int nvalid, const MeshView& M) {
     int start[kArenas + 1];
     start[0] = 0;
@@ -476,7 +497,26 @@ DEV void narrow_queue(ArenaLDS* base, int nvalid, const MeshView& M) {
         const uint32_t e = A->a.q[k - off];
         const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)(e >> 25);
         const float4 a = M.tri[3 * (size_t)t], b = M.tri[3 * (size_t)t + 1], c = M.tri[3 * (size_t)t + 2];
-        box_tri_query(A, M, bi, t, obj, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{c.x, c.y, c.z});
+        if (box_tri_query(A, M, bi, t, obj, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{c.x, c.y, c.z}, kWG == 64))
+            A->a.q[k - off] = e | kDeferred;
+    }
+}
+// the flagged queries, arena by arena and in queue order, each on the whole wave (every lane calls this)
+DEV void narrow_deferred(ArenaLDS* base, int nvalid, const MeshView& M) {
+    if (kWG != 64) return;
+    for (int ar = 0; ar < nvalid; ar++) {
+        ArenaLDS* A = base + ar;
+        const int nq = stdmin(A->a.nq, kQueue);
+        for (int k0 = 0; k0 < nq; k0 += kWG) {
+            const int k = k0 + (int)threadIdx.x;
+            const uint32_t e = k < nq ? A->a.q[k] : 0u;
+            uint64_t m = __ballot((e & kDeferred) != 0);
+            while (m) {
+                const uint32_t ej = gjk::rdl(e, gjk::lowbit(m));
+                m &= m - 1ull;
+                box_tri_query_wave(A, M, ej & ~kDeferred);
+            }
+        }
     }
 }
 
@@ -527,7 +567,7 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                     if (slot < kQueue)
                         A->a.q[slot] = (uint32_t)t | ((uint32_t)obj << 20) | ((uint32_t)bi << 25);
                     else
-                        box_tri_query(A, M, bi, t, obj, v0, v1, v2);
+                        box_tri_query(A, M, bi, t, obj, v0, v1, v2, false);
                 });
             }
         }
@@ -598,44 +638,39 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
     return 1;
 }
 
-// single lane: commit this tick's candidates in the broadphase's pair order -- per pair (key): add its points
-// (contact callbacks fire here), then refresh its manifold, as Bullet's dispatch loop does
-// (btCollisionDispatcher::dispatchAllCollisionPairs, processCollision -> refreshContactPoints)
+// the commit order of this tick's candidates, on the arena's 16 lanes: candidate i goes to position
+// #{j : order_j < order_i, or order_j == order_i and j < i} -- the stable order the single-lane insertion sort
+// gave -- written as a permutation into the narrowphase's free LDS tail (the penetration solver's small set)
+DEV uint8_t* cand_perm(ArenaLDS* A) { return (uint8_t*)&A->u.cand[kMaxCand]; }
+DEV void sort_candidates(ArenaLDS* A, int l) {
+    const int n = min(A->a.ncand, kMaxCand);
+    uint8_t* perm = cand_perm(A);
+    for (int i = l; i < n; i += kTeam) {
+        const int oi = A->u.cand[i].order;
+        int r = 0;
+        for (int j = 0; j < n; j++) {
+            const int oj = A->u.cand[j].order;
+            r += (oj < oi) || (oj == oi && j < i);
+        }
+        perm[r] = (uint8_t)i;
+    }
+}
+// single lane: commit this tick's candidates in the broadphase's pair order (sort_candidates) -- per pair
+// (key): add its points (contact callbacks fire here), then refresh its manifold, as Bullet's dispatch loop
+// does (btCollisionDispatcher::dispatchAllCollisionPairs, processCollision -> refreshContactPoints)
 DEV void commit_contacts(ArenaLDS* A, const MeshView& M, Prof* P = nullptr) {
     int n = A->a.ncand;
     if (n > kMaxCand) {
         A->s.env.manifold_overflow += (uint32_t)(n - kMaxCand);
         n = kMaxCand;
     }
-    // insertion sort by commit order (few elements)
-    // (the element being inserted is held field by field: a Cand temporary is a private-memory copy)
-    for (int i = 1; i < n; i++) {
-        const Cand& ci = A->u.cand[i];
-        const float xn0 = ci.n[0], xn1 = ci.n[1], xn2 = ci.n[2], xp0 = ci.p[0], xp1 = ci.p[1], xp2 = ci.p[2];
-        const float xd = ci.depth;
-        const int xo = ci.order, xk = ci.key;
-        int j = i - 1;
-        while (j >= 0 && A->u.cand[j].order > xo) {
-            A->u.cand[j + 1] = A->u.cand[j];
-            j--;
-        }
-        Cand& d = A->u.cand[j + 1];
-        d.n[0] = xn0;
-        d.n[1] = xn1;
-        d.n[2] = xn2;
-        d.p[0] = xp0;
-        d.p[1] = xp1;
-        d.p[2] = xp2;
-        d.depth = xd;
-        d.order = xo;
-        d.key = xk;
-    }
+    const uint8_t* perm = cand_perm(A);
     pmark(P, 17);
     if (P && P->p && threadIdx.x == 0) atomicAdd(&P->p[24], (unsigned long long)n);
     A->a.nmf = 0;  // the previous tick's manifolds were destroyed with their pairs
     int cur = -1;
     for (int ci = 0; ci < n; ci++) {
-        const Cand& c = A->u.cand[ci];
+        const Cand& c = A->u.cand[perm[ci]];
         if (c.key != cur) {
             if (cur >= 0) refresh(A, cur);
             cur = c.key;

@@ -174,6 +174,10 @@ struct Aux {
 
 union Scratch {
     WheelT wt[16];
+    struct {
+        v3 mn[5], mx[5];  // T4: the bodies' broadphase AABBs
+        int cell[5];      //     and home cells + 1 (bp_home), one lane per body
+    } bp;
     Cand cand[kMaxCand];
     // narrowphase: the candidates, then the small penetration-solver set (gjk::lds_view)
     char narrow[sizeof(Cand) * kMaxCand + gjk::kSmallBytes];

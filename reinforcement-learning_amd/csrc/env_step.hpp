@@ -172,17 +172,22 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     }
     sync();
     P.mark(3);
+    if (valid && l < 5) {  // updateAabbs: the broadphase AABB and home cell of body l (one lane per body)
+        v3 mn, mx;
+        broad_aabb(A, l, mn, mx);
+        A->u.bp.mn[l] = mn;
+        A->u.bp.mx[l] = mx;
+        A->u.bp.cell[l] = bp_home(mn) + 1;
+    }
+    sync();
     if (valid && l == 0) {
-        bp_update(A);  // updateAabbs -> btRSBroadphase::setAabb
+        bp_update(A);  // btRSBroadphase::setAabb in body order
         bool awake = !A->a.ball_sleep;
         if (!awake) {
-            v3 m0, m1;
-            broad_aabb(A, 0, m0, m1);
+            const v3 m0 = A->u.bp.mn[0], m1 = A->u.bp.mx[0];
             for (int ci = 1; ci <= 4; ci++) {
                 if (!A->a.active[ci]) continue;
-                v3 n0, n1;
-                broad_aabb(A, ci, n0, n1);
-                if (aabb_overlap(m0, m1, n0, n1)) awake = true;
+                if (aabb_overlap(m0, m1, A->u.bp.mn[ci], A->u.bp.mx[ci])) awake = true;
             }
         }
         A->a.ball_awake = awake;
@@ -205,7 +210,11 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     sync();
     narrow_queue(A - (threadIdx.x >> 4), nvalid, M);
     sync();
+    narrow_deferred(A - (threadIdx.x >> 4), nvalid, M);
+    sync();
     P.mark(5);
+    if (valid) sort_candidates(A, l);
+    sync();
     if (valid && l == 0) {
         commit_contacts(A, M, &P);
         if (threadIdx.x == 0) P.mark(16);

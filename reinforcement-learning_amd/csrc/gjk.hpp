@@ -118,9 +118,13 @@ DEV void copy_face(SFace& o, const F& f) {
     o.l[1] = f.l[1];
 }
 DEV Scr hbm_view(GjkScratch* g) { return Scr{g->sv, g->fc, g->stack, kSV, kEpaMaxFaces, kEpaMaxFaces + 8, 0}; }
+// wave mode's set (epa_wave): support vertices only, in the same bytes
+constexpr int kWaveSV = 64;
+DEV Scr wave_view(char* base) { return Scr{(SSV*)base, nullptr, nullptr, kWaveSV, 0, 0, 0}; }
 // small set carved from `bytes` of LDS: 24 support vertices (20 EPA iterations), 28 live faces, depth 24
 constexpr int kSmallSV = 24, kSmallFaces = 28, kSmallStack = 24;
 constexpr int kSmallBytes = kSmallSV * (int)sizeof(SSV) + kSmallFaces * (int)sizeof(SFace) + kSmallStack * 4;
+static_assert(kWaveSV * (int)sizeof(SSV) <= kSmallBytes, "the wave-mode set fits the small set's bytes");
 DEV Scr lds_view(char* base) {
     return Scr{(SSV*)base, (SFace*)(base + kSmallSV * sizeof(SSV)),
                (uint32_t*)(base + kSmallSV * sizeof(SSV) + kSmallFaces * sizeof(SFace)), kSmallSV, kSmallFaces,
@@ -829,9 +833,8 @@ DEV void bind(ScrT<AS>& S, int fa, int ea, int fb, int eb) {
     S.fc[fb].e[eb] = (uint8_t)ea;
     S.fc[fb].f[eb] = (uint8_t)fa;
 }
-template <int AS>
-DEV bool getedgedist(const ScrT<AS>& S, v3 fn, int a, int b, float& dist) {
-    const v3 aw = svw(S, a), bw = svw(S, b);
+// EPA::getedgedist on the edge's two support points (already in registers: newface loads each vertex once)
+DEV bool getedgedist(v3 fn, v3 aw, v3 bw, float& dist) {
     const v3 ba = bw - aw;
     const v3 n_ab = cross(ba, fn);
     const float a_dot_nab = dot(aw, n_ab);
@@ -851,6 +854,16 @@ DEV bool getedgedist(const ScrT<AS>& S, v3 fn, int a, int b, float& dist) {
         return true;
     }
     return false;
+}
+// EPA::newface's plane of (a, b, c): false when degenerate (|n| <= EPA_ACCURACY); else n normalised and d
+// the distance of the nearest edge (getedgedist) or of the plane
+DEV bool face_plane(v3 aw, v3 bw, v3 cw, v3& n, float& d) {
+    n = cross(bw - aw, cw - aw);
+    const float l = len(n);
+    if (!(l > kEpaAccuracy)) return false;
+    if (!(getedgedist(n, aw, bw, d) || getedgedist(n, bw, cw, d) || getedgedist(n, cw, aw, d))) d = dot(aw, n) / l;
+    n = n / l;
+    return true;
 }
 // EPA::newface; returns the face or -1
 template <int AS>
@@ -874,13 +887,9 @@ DEV int newface(ScrT<AS>& S, Epa& E, int a, int b, int c, bool forced) {
     F.c[0] = (uint8_t)a;
     F.c[1] = (uint8_t)b;
     F.c[2] = (uint8_t)c;
-    const v3 aw = svw(S, a);
-    v3 n = cross(svw(S, b) - aw, svw(S, c) - aw);
-    const float l = len(n);
-    if (l > kEpaAccuracy) {
-        float d;
-        if (!(getedgedist(S, n, a, b, d) || getedgedist(S, n, b, c, d) || getedgedist(S, n, c, a, d))) d = dot(aw, n) / l;
-        n = n / l;
+    v3 n;
+    float d;
+    if (face_plane(svw(S, a), svw(S, b), svw(S, c), n, d)) {
         stv(F.n, n);
         F.d = d;
         if (forced || (d >= -kEpaPlaneEps)) return face;
@@ -1107,8 +1116,289 @@ GJK_CALLED int epa_evaluate(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 gue
     return E.status;
 }
 
-// btGjkEpaSolver2::Penetration (cpp:973-1017) with margins; t0 / t1 = (basis, origin)
+// ---- EPA on the whole wave (wave mode: every lane of the wavefront runs the same query, in lockstep)
+// The polytope lives in registers: face slot k is lane k's WFace, so the hull holds at most one face per
+// lane.  Per iteration the lanes test every face against the new support point at once (one ballot), the
+// walk of Bullet's expand recursion runs on those bits and the faces' adjacency words read across lanes
+// (uniform, scalar), the horizon's new faces are built in parallel (one lane each, in the free slots),
+// and findbest is a wave reduction.  Same faces, same order (append numbers), same tests, same failures:
+//   * expand's first `false` (a face met twice) ends Bullet's iteration with InvalidHull and nothing after
+//     it has any effect, so the walk stops there;
+//   * a newface that fails (Degenerated / NonConvex) also ends the iteration with InvalidHull, and the
+//     walk that Bullet would have cut short changes nothing else: the new faces are computed after the
+//     walk and any failure among them ends the iteration the same way;
+//   * the walk reads adjacency that expand's own binds never touch (binds change only new faces and the
+//     horizon's non-visible faces, which expand never walks through).
+// More support vertices than the set holds, more faces than lanes, a deeper walk than 64 frames: overflow,
+// and the caller reruns the query on the full-capacity HBM set (scalar epa_evaluate).
+struct WFace {
+    v3 n;
+    float d;
+    uint32_t c;    // support vertices c0 | c1 << 8 | c2 << 16
+    uint32_t adj;  // adjacent faces f0 | f1 << 8 | f2 << 16, their edges e0 << 24 | e1 << 26 | e2 << 28
+    uint32_t seq;  // > 0: in the hull, appended seq-th
+};
+DEV uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+DEV float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+DEV v3 rdl(v3 v, int l) { return v3{rdl(v.x, l), rdl(v.y, l), rdl(v.z, l)}; }
+DEV uint32_t wrl(uint32_t v, int l, uint32_t x) { return __lane_id() == l ? x : v; }  // lane l of v = x
+DEV uint32_t rdfirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+DEV uint32_t lane_perm(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_ds_bpermute(l << 2, (int)v); }
+DEV uint32_t wmin(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
+        v = u < v ? u : v;
+    }
+    return rdfirst(v);
+}
+DEV uint32_t wmax(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
+        v = u > v ? u : v;
+    }
+    return rdfirst(v);
+}
+DEV int lowbit(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+DEV int highbit(uint64_t m) { return 63 - __clzll((long long)m); }
+// findbest over the lanes: least d^2, ties to the newest face
+DEV int wfindbest(const WFace& F) {
+    const int L = __lane_id();
+    const bool alive = F.seq != 0;
+    const uint32_t key = alive ? __float_as_uint(F.d * F.d) : 0xffffffffu;
+    const uint32_t mk = wmin(key);
+    const uint64_t tie = __ballot(alive && key == mk);
+    if (__popcll(tie) == 1) return lowbit(tie);
+    const bool in = (tie >> L) & 1;
+    const uint32_t ms = wmax(in ? F.seq : 0u);
+    return lowbit(__ballot(in && F.seq == ms));
+}
+DEV int adj_f(uint32_t adj, int e) { return (int)((adj >> (8 * e)) & 255u); }
+DEV int adj_e(uint32_t adj, int e) { return (int)((adj >> (24 + 2 * e)) & 3u); }
+// Bullet's expand from best's three edges over the visible-face bits `vis`.  Returns 1 when every call
+// returned true, 0 at the first false, -1 on overflow.  Out: the horizon edges in creation order (lane j of
+// H = face | edge << 8 of the j-th), their count, and the visible faces the walk removes.
+DEV int wexpand(const WFace& F, int best, uint64_t vis, uint64_t lanes, uint32_t& H, int& nh, uint64_t& removed) {
+    uint64_t visited = 1ull << best;
+    removed = 0;
+    nh = 0;
+    uint32_t stk = 0;  // walk frames below the top, frame k in lane k: face | edge << 8 | stage << 10
+    const uint32_t badj = rdl(F.adj, best);
+    for (int j = 0; j < 3; j++) {
+        uint32_t top = (uint32_t)adj_f(badj, j) | ((uint32_t)adj_e(badj, j) << 8);
+        int sp = 0;
+        while (true) {
+            const int f = (int)(top & 255u), e = (int)((top >> 8) & 3u), stage = (int)(top >> 10);
+            bool pop = false;
+            if (stage == 0) {
+                if ((visited >> f) & 1) return 0;  // f->pass == pass: expand returns false
+                if (!((vis >> f) & 1)) {           // the face sees w below it: a horizon edge, newface(c[e1], c[e], w)
+                    if (nh >= 64 || ((lanes >> nh) & 1) == 0) return -1;
+                    H = wrl(H, nh, top);
+                    nh++;
+                    pop = true;
+                } else {  // visible: mark it, walk its edge e1, then e2, then remove it
+                    visited |= 1ull << f;
+                    if (sp >= 64 || ((lanes >> sp) & 1) == 0) return -1;
+                    stk = wrl(stk, sp, top | (1u << 10));
+                    sp++;
+                    const int e1 = e == 2 ? 0 : e + 1;
+                    const uint32_t adj = rdl(F.adj, f);
+                    top = (uint32_t)adj_f(adj, e1) | ((uint32_t)adj_e(adj, e1) << 8);
+                }
+            } else if (stage == 1) {
+                stk = wrl(stk, sp, (top & 1023u) | (2u << 10));
+                sp++;
+                const int e2 = e == 0 ? 2 : e - 1;
+                const uint32_t adj = rdl(F.adj, f);
+                top = (uint32_t)adj_f(adj, e2) | ((uint32_t)adj_e(adj, e2) << 8);
+            } else {
+                removed |= 1ull << f;
+                pop = true;
+            }
+            if (pop) {
+                if (sp == 0) break;
+                top = rdl(stk, --sp);
+            }
+        }
+    }
+    return 1;
+}
+// EPA::Evaluate (cpp:648-768) in wave mode; same contract as epa_evaluate (S: support vertices only)
 template <int AS>
+GJK_CALLED int epa_wave(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, v3& normal, float& depth, Simp& res) {
+    const int L = __lane_id();
+    const uint64_t lanes = __ballot(1);
+    if ((s.rank > 1) && enclose_origin(S, m, g, s)) {
+        {
+            const v3 w3 = svw(S, sc(s, 3));
+            if (det3(svw(S, sc(s, 0)) - w3, svw(S, sc(s, 1)) - w3, svw(S, sc(s, 2)) - w3) < 0) {
+                const int c0 = sc(s, 0), c1 = sc(s, 1);
+                sc_set(s, 0, c1);
+                sc_set(s, 1, c0);
+                const float p0 = s.p[0];
+                s.p[0] = s.p[1];
+                s.p[1] = p0;
+            }
+        }
+        const int s0 = sc(s, 0), s1 = sc(s, 1), s2 = sc(s, 2), s3 = sc(s, 3);
+        // the tetrahedron: lane k builds t_k = newface(..., forced) and its binds
+        const int ta = L == 1 ? s1 : (L == 2 ? s2 : s0);
+        const int tb = L == 0 ? s1 : (L == 1 ? s0 : (L == 2 ? s1 : s2));
+        const int tc = L == 0 ? s2 : s3;
+        // adjacency after bind(t0,0,t1,0) bind(t0,1,t2,0) bind(t0,2,t3,0) bind(t1,1,t3,2) bind(t1,2,t2,1) bind(t2,2,t3,1)
+        const uint32_t tadj = L == 0 ? (1u | 2u << 8 | 3u << 16)
+                              : L == 1 ? (0u | 3u << 8 | 2u << 16 | 0u << 24 | 2u << 26 | 1u << 28)
+                              : L == 2 ? (0u | 1u << 8 | 3u << 16 | 1u << 24 | 2u << 26 | 1u << 28)
+                                       : (0u | 2u << 8 | 1u << 16 | 2u << 24 | 2u << 26 | 1u << 28);
+        WFace F;
+        F.n = zero3();
+        F.d = 0.f;
+        F.c = 0;
+        F.adj = 0;
+        F.seq = 0;
+        bool ok = true;
+        if (L < 4) {
+            v3 n;
+            float d;
+            ok = face_plane(svw(S, ta), svw(S, tb), svw(S, tc), n, d);
+            F.n = n;
+            F.d = d;
+            F.c = (uint32_t)ta | ((uint32_t)tb << 8) | ((uint32_t)tc << 16);
+            F.adj = tadj;
+            F.seq = (uint32_t)(L + 1);
+        }
+        if (__ballot(L < 4 && !ok) == 0) {  // all four made: m_hull.count == 4
+            int best = wfindbest(F);
+            v3 on = rdl(F.n, best);
+            float od = rdl(F.d, best);
+            uint32_t oc = rdl(F.c, best);
+            uint32_t seq = 4;
+            int nextsv = 0, status = 0;
+            for (int iterations = 0; iterations < kEpaMaxIterations; ++iterations) {
+                if (nextsv >= kEpaMaxVertices) {
+                    status = 6;  // OutOfVertices
+                    break;
+                }
+                if (4 + nextsv >= S.max_sv) {
+                    S.overflow = 1;
+                    return 9;
+                }
+                GJK_MARK(4);
+                const int w = 4 + nextsv++;
+                const v3 bn = rdl(F.n, best);
+                const float bd = rdl(F.d, best);
+                getsupport(S, m, bn, w);
+                const v3 wv = svw(S, w);
+                const float wdist = dot(bn, wv) - bd;
+                GJK_MARK(6);
+                if (!(wdist > kEpaAccuracy)) {
+                    status = 7;  // AccuraryReached
+                    break;
+                }
+                const uint64_t vis = __ballot(F.seq != 0 && !((dot(F.n, wv) - F.d) < -kEpaPlaneEps));
+                uint32_t H = 0;
+                int nh;
+                uint64_t removed;
+                const int walk = wexpand(F, best, vis, lanes, H, nh, removed);
+                GJK_MARK(7);
+                if (walk < 0) {
+                    S.overflow = 1;
+                    return 9;
+                }
+                if (walk == 0 || nh < 3) {
+                    status = 4;  // InvalidHull
+                    break;
+                }
+                // the new faces, in horizon order, take the free slots in ascending order
+                const uint64_t keep = __ballot(F.seq != 0) & ~removed & ~(1ull << best);
+                const uint64_t freem = lanes & ~keep;
+                if (__popcll(freem) < nh) {
+                    S.overflow = 1;
+                    return 9;
+                }
+                const uint64_t below = (1ull << L) - 1ull;
+                const bool in_free = (freem >> L) & 1;
+                const int r = __popcll(freem & below);
+                const bool host = in_free && r < nh;
+                const uint32_t h = lane_perm(H, host ? r : 0);
+                const int hf = (int)(h & 255u), he = (int)((h >> 8) & 3u), he1 = he == 2 ? 0 : he + 1;
+                const uint32_t hc = lane_perm(F.c, hf);
+                const int na = (int)((hc >> (8 * he1)) & 255u), nb = (int)((hc >> (8 * he)) & 255u);
+                v3 nn = zero3();
+                float nd = 0.f;
+                bool nok = true;
+                if (host) nok = face_plane(svw(S, na), svw(S, nb), wv, nn, nd) && (nd >= -kEpaPlaneEps);
+                if (__ballot(host && !nok) != 0) {
+                    status = 4;  // a newface failed (Degenerated / NonConvex): expand false, InvalidHull
+                    break;
+                }
+                const int first = lowbit(freem);
+                const int last = lowbit(__ballot(host && r == nh - 1));
+                const uint64_t above = freem & ~below & ~(1ull << L);
+                const int nxt = r + 1 < nh ? lowbit(above) : first;
+                const int prv = r > 0 ? highbit(freem & below) : last;
+                if (host) {  // bind(nf, 0, f, e); bind(prev, 1, nf, 2); bind(nf, 1, next, 2)
+                    F.n = nn;
+                    F.d = nd;
+                    F.c = (uint32_t)na | ((uint32_t)nb << 8) | ((uint32_t)w << 16);
+                    F.seq = seq + 1u + (uint32_t)r;
+                    F.adj = (uint32_t)hf | ((uint32_t)nxt << 8) | ((uint32_t)prv << 16) | ((uint32_t)he << 24) |
+                            (2u << 26) | (1u << 28);
+                } else if (!((keep >> L) & 1)) {
+                    F.seq = 0;  // removed (the best face and the walk's visible faces)
+                }
+                uint64_t fm = freem;
+                for (int j = 0; j < nh; j++) {  // the horizon's faces: edge e now borders the new face
+                    const int sj = lowbit(fm);
+                    fm &= fm - 1ull;
+                    const uint32_t hj = rdl(H, j);
+                    const int fj = (int)(hj & 255u), ej = (int)((hj >> 8) & 3u);
+                    if (L == fj)
+                        F.adj = (F.adj & ~(255u << (8 * ej)) & ~(3u << (24 + 2 * ej))) | ((uint32_t)sj << (8 * ej));
+                }
+                seq += (uint32_t)nh;
+                GJK_MARK(9);
+                best = wfindbest(F);
+                on = rdl(F.n, best);
+                od = rdl(F.d, best);
+                oc = rdl(F.c, best);
+                GJK_MARK(8);
+            }
+            const v3 projection = on * od;
+            normal = on;
+            depth = od;
+            res.rank = 3;
+            res.c = oc & 0xffffffu;
+            const v3 o0 = svw(S, (int)(oc & 255u)), o1 = svw(S, (int)((oc >> 8) & 255u)),
+                     o2 = svw(S, (int)((oc >> 16) & 255u));
+            res.p[0] = len(cross(o1 - projection, o2 - projection));
+            res.p[1] = len(cross(o2 - projection, o0 - projection));
+            res.p[2] = len(cross(o0 - projection, o1 - projection));
+            const float sum = res.p[0] + res.p[1] + res.p[2];
+            res.p[0] /= sum;
+            res.p[1] /= sum;
+            res.p[2] /= sum;
+            return status;
+        }
+    }
+    normal = -guess;  // FallBack
+    const float nl = len(normal);
+    if (nl > 0)
+        normal = normal / nl;
+    else
+        normal = v3{1, 0, 0};
+    depth = 0;
+    res.rank = 1;
+    res.c = 0;
+    sc_set(res, 0, sc(s, 0));
+    res.p[0] = 1;
+    return 8;
+}
+
+// btGjkEpaSolver2::Penetration (cpp:973-1017) with margins; t0 / t1 = (basis, origin); W: wave-mode EPA
+template <int AS, bool W>
 DEV bool penetration(ScrT<AS>& S, const Shape& sh, const m3& b0, v3 o0, const m3& b1, v3 o1, v3 guess, v3& wA, v3& wB,
                      v3& nrm) {
     const Mink m = make_mink(sh, b0, o0, b1, o1, true);
@@ -1119,7 +1409,7 @@ DEV bool penetration(ScrT<AS>& S, const Shape& sh, const m3& b0, v3 o0, const m3
     v3 en;
     float ed;
     Simp res;
-    const int es = epa_evaluate(S, m, g, g.cs, -guess, en, ed, res);
+    const int es = W ? epa_wave(S, m, g, g.cs, -guess, en, ed, res) : epa_evaluate(S, m, g, g.cs, -guess, en, ed, res);
     GJK_MARK(5);
     if (es == 9 || S.overflow) return false;
     v3 w0 = zero3();
@@ -1152,7 +1442,7 @@ DEV bool distance(ScrT<AS>& S, const Shape& sh, const m3& b0, v3 o0, const m3& b
 }
 // btGjkEpaPenetrationDepthSolver::calcPenDepth (cpp:22-79); called, not inlined: the rare path stays out
 // of the narrowphase's hot code
-template <int AS>
+template <int AS, bool W = false>
 __device__ __noinline__ bool calc_pen_depth(ScrT<AS>& S, const Shape& sh, const m3& bA, v3 oA, const m3& bB, v3 oB, v3& v, v3& wA, v3& wB) {
 #pragma unroll 1
     for (int i = 0; i < 9; i++) {
@@ -1166,7 +1456,7 @@ __device__ __noinline__ bool calc_pen_depth(ScrT<AS>& S, const Shape& sh, const 
         else if (i == 6) g = v3{1, 1, 1};
         else if (i == 7) g = v3{0, 1, 1};
         else g = v3{1, 0, 1};
-        if (penetration(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return true;
+        if (penetration<AS, W>(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return true;
         if (S.overflow) return false;
         if (distance(S, sh, bA, oA, bB, oB, g, wA, wB, v)) return false;
     }
@@ -1179,8 +1469,13 @@ __device__ __noinline__ bool calc_pen_depth(ScrT<AS>& S, const Shape& sh, const 
 // btManifoldResult::addContactPoint(normal, point, depth).  S: this lane's penetration-solver scratch.
 // fast / lock: a small LDS work set and the lock that serialises it among the arena's lanes (null: HBM
 // only); slow: this lane's HBM set.
+// mode: kPenInline runs the penetration solver where the query needs it; kPenDefer stops there instead
+// (returns false and sets *deferred: the caller reruns the query in wave mode); kPenWave, called by every
+// lane of the wavefront with the same query, runs it with the wave-mode EPA on `fast` (support vertices
+// only, kWaveSV of them).
+constexpr int kPenInline = 0, kPenDefer = 1, kPenWave = 2;
 DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, int* lock, Scr& slow, v3& normal,
-                      v3& point, float& depth, int* pen_count = nullptr) {
+                      v3& point, float& depth, int* pen_count = nullptr, int mode = kPenInline, bool* deferred = nullptr) {
     // normal early out, both sides (btConvexConcaveCollisionAlgorithm.cpp:101-136)
     {
         const v3 half = s.impl + v3{s.margin, s.margin, s.margin};
@@ -1289,9 +1584,20 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
         v3 tA, tB;
         v = zero3();
         bool ok2;
-        if (pen_count) atomicAdd(pen_count, 1);
+        if (mode == kPenDefer) {
+            *deferred = true;
+            return false;
+        }
+        if (pen_count && (mode != kPenWave || __lane_id() == 0)) atomicAdd(pen_count, 1);
         ScrT<1> slow1 = in_space<1>(slow);
-        if (fast && atomicCAS(lock, 0, 1) == 0) {
+        if (mode == kPenWave) {
+            ScrT<3> wave3 = in_space<3>(*fast);
+            ok2 = calc_pen_depth<3, true>(wave3, s, R, oA, I, oB, v, tA, tB);
+            if (wave3.overflow != 0) {
+                v = zero3();
+                ok2 = calc_pen_depth(slow1, s, R, oA, I, oB, v, tA, tB);
+            }
+        } else if (fast && atomicCAS(lock, 0, 1) == 0) {
             ScrT<3> fast3 = in_space<3>(*fast);
             ok2 = calc_pen_depth(fast3, s, R, oA, I, oB, v, tA, tB);
             const bool redo = fast3.overflow != 0;

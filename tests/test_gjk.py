@@ -9,7 +9,8 @@ penetration solver (EPA) takes over exactly where btGjkPairDetector's degenerate
 below 0.01).  Parity unpinned beyond these: the reference cannot be built here.
 GPU: the device restatement (csrc/gjk.hpp, rlgpu_box_triangle_queries) bit for bit against the oracle
 on 20,000 seeded poses spanning separated, touching, shallow and deep (EPA) contacts on faces, edges
-and vertices of small and large triangles.
+and vertices of small and large triangles, for each work-set policy (HBM, LDS first, and the env kernel's
+deferred queries run by the whole wavefront with the polytope in its registers, gjk.hpp epa_wave).
 """
 import numpy as np
 import pytest
@@ -117,7 +118,8 @@ def test_device_box_triangle_bit_exact(gpu):
     want, counts = oracle.box_triangle(R, c, t, cbt)
     assert counts[1] > 1000
     args = [torch.from_numpy(a).to(gpu) for a in (R, c, t, cbt)]
-    for lds_first in (False, True):  # full-capacity HBM sets; small LDS sets with the HBM rerun
+    # full-capacity HBM sets; small LDS sets with the HBM rerun; the env kernel's deferred wave-mode EPA
+    for lds_first in (False, True, "wave"):
         got = box_triangle_queries(*args, lds_first=lds_first).cpu().numpy()
         bad = np.nonzero(np.any(_canon(got) != _canon(want), axis=1))[0]
         assert len(bad) == 0, f"lds_first={lds_first}: {len(bad)} of {len(R)} differ; first {bad[:5]}: " \

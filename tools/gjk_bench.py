@@ -30,18 +30,16 @@ for name, idx in sets.items():
             box_triangle_queries(*args)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        reps = 10
-        for _ in range(reps):
-            box_triangle_queries(*args)
-        e1.record()
-        torch.cuda.synchronize()
-        t_lds = e0.elapsed_time(e1) / reps * 1e3
-        e0.record()
-        for _ in range(reps):
-            box_triangle_queries(*args, lds_first=False)
-        e1.record()
-        torch.cuda.synchronize()
-        t_hbm = e0.elapsed_time(e1) / reps * 1e3
-        print(f"{name:12s} n={n:5d}: {t_lds:9.1f} us per launch LDS-first, {t_hbm:9.1f} us HBM only (incl. scratch alloc)",
-              flush=True)
+        tm = {}
+        for mode in (True, False, "wave"):
+            box_triangle_queries(*args, lds_first=mode)
+            torch.cuda.synchronize()
+            e0.record()
+            reps = 10
+            for _ in range(reps):
+                box_triangle_queries(*args, lds_first=mode)
+            e1.record()
+            torch.cuda.synchronize()
+            tm[mode] = e0.elapsed_time(e1) / reps * 1e3
+        print(f"{name:12s} n={n:5d}: {tm[True]:9.1f} us per launch LDS-first, {tm[False]:9.1f} us HBM only, "
+              f"{tm['wave']:9.1f} us wave-mode EPA (incl. scratch alloc)", flush=True)
