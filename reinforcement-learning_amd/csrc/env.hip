@@ -804,6 +804,7 @@ __global__ void __launch_bounds__(64) box_triangle_wave_kernel(int n, const floa
     const int i = blockIdx.x * 64 + threadIdx.x;
     gjk::Scr slow = gjk::hbm_view(scratch + i);  // scratch holds a set for every lane of the grid
     bool deferred = false;
+    gjk::PenState st{};
     if (i < n) {
         m3 R;
         v3 c, nrm, pt;
@@ -811,12 +812,12 @@ __global__ void __launch_bounds__(64) box_triangle_wave_kernel(int n, const floa
         float d = 0.f;
         bt_load(i, rot, centre, tri, ar, R, c, sh);
         const bool hit = gjk::box_triangle(R, c, sh, cbt[i], nullptr, nullptr, slow, nrm, pt, d, nullptr, gjk::kPenDefer,
-                                           &deferred);
+                                           &deferred, &st);
         if (!deferred) bt_store(out, i, hit, nrm, pt, d);
     }
     uint64_t m = __ballot(deferred);
     while (m) {
-        const int q = blockIdx.x * 64 + gjk::lowbit(m);
+        const int j = gjk::lowbit(m), q = blockIdx.x * 64 + j;
         m &= m - 1ull;
         m3 R;
         v3 c, nrm, pt;
@@ -824,7 +825,11 @@ __global__ void __launch_bounds__(64) box_triangle_wave_kernel(int n, const floa
         float d = 0.f;
         bt_load(q, rot, centre, tri, ar, R, c, sh);
         gjk::Scr wave = gjk::wave_view(small);
-        const bool hit = gjk::box_triangle(R, c, sh, cbt[q], &wave, nullptr, slow, nrm, pt, d, nullptr, gjk::kPenWave);
+        // even queries resume from the deferring lane's saved state, odd ones start over (both env paths)
+        const gjk::PenState rs{gjk::rdl(st.pA, j), gjk::rdl(st.pB, j), gjk::rdl(st.nB, j), gjk::rdl(st.dist, j),
+                               (int)gjk::rdl((uint32_t)st.valid, j)};
+        const bool hit = gjk::box_triangle(R, c, sh, cbt[q], &wave, nullptr, slow, nrm, pt, d, nullptr, gjk::kPenWave,
+                                           nullptr, nullptr, (q & 1) ? nullptr : &rs);
         if (threadIdx.x == 0) bt_store(out, q, hit, nrm, pt, d);
     }
 }

@@ -442,12 +442,21 @@ DEV v3 box_support(const m3& R, v3 c, v3 dir_world) {
                dl.z >= 0 ? C.car_half.z : -C.car_half.z};
     return R * lv + c;
 }
+// Deferred box-triangle queries (narrow_queue -> narrow_deferred): a queue entry's top 4 bits tag it --
+// 0 not deferred, 1..kPenSave its saved GJK state's slot + 1, kPenNoSave deferred without one (the rerun
+// starts over).  The states sit in the workgroup's LDS (kPenSave x 44 B fits the allocation's rounding).
+constexpr int kPenSave = 8;
+constexpr uint32_t kPenTagShift = 28, kPenNoSave = 15;
+struct PenSave {
+    gjk::PenState st[kPenSave];
+    int n;
+};
+static __shared__ PenSave g_pen_save;
 // One car hitbox vs mesh triangle: Bullet's GJK / EPA query (gjk.hpp) and its candidate.  defer: a query
-// that needs the penetration solver stops there and returns true (narrow_deferred reruns it on the whole
+// that needs the penetration solver stops there and returns its tag (narrow_deferred reruns it on the whole
 // wave); else the solver runs here, in the arena's small LDS set past the candidate list (free during the
 // narrowphase), one lane at a time, or in this lane's HBM scratch.
-__device__ __noinline__ bool box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2,
-                                           bool defer) {
+__device__ __noinline__ uint32_t box_tri_query(ArenaLDS* A, const MeshView& M, int bi, int t, int obj, v3 v0, v3 v1, v3 v2, bool defer) {
     const m3 R = brot(A, bi);
     const v3 c = car_box_center(A, bi);
     gjk::Scr slow = gjk::hbm_view(M.gjk + ((size_t)blockIdx.x * kWG + threadIdx.x));
@@ -456,14 +465,20 @@ __device__ __noinline__ bool box_tri_query(ArenaLDS* A, const MeshView& M, int b
     v3 n, pb;
     float d;
     bool deferred = false;
+    gjk::PenState st;
     if (gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &fast, &A->a.epa_lock, slow, n, pb, d, &A->a.npen,
-                          defer ? gjk::kPenDefer : gjk::kPenInline, &deferred))
+                          defer ? gjk::kPenDefer : gjk::kPenInline, &deferred, &st))
         emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
-    return deferred;
+    if (!deferred) return 0u;
+    const int slot = atomicAdd(&g_pen_save.n, 1);
+    if (slot >= kPenSave) return kPenNoSave;
+    g_pen_save.st[slot] = st;
+    return (uint32_t)slot + 1u;
 }
-// A deferred query (queue entry e) on every lane of the wave: the penetration solver's EPA keeps its
-// polytope in the wave's registers (gjk::epa_wave), its support vertices in the arena's small LDS set
-__device__ __noinline__ void box_tri_query_wave(ArenaLDS* A, const MeshView& M, uint32_t e) {
+// A deferred query (queue entry e, tag stripped; saved: its GJK state or null) on every lane of the wave:
+// the penetration solver's EPA keeps its polytope in the wave's registers (gjk::epa_wave), its support
+// vertices in the arena's small LDS set
+__device__ __noinline__ void box_tri_query_wave(ArenaLDS* A, const MeshView& M, uint32_t e, const gjk::PenState* saved) {
     const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)((e >> 25) & 7u);
     const float4 a = M.tri[3 * (size_t)t], b = M.tri[3 * (size_t)t + 1], cc = M.tri[3 * (size_t)t + 2];
     const m3 R = brot(A, bi);
@@ -473,14 +488,16 @@ __device__ __noinline__ void box_tri_query_wave(ArenaLDS* A, const MeshView& M, 
     const gjk::Shape sh{C.car_impl, C.car_margin, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{cc.x, cc.y, cc.z}, arith(A)};
     v3 n, pb;
     float d;
-    const bool hit = gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &wave, nullptr, slow, n, pb, d, &A->a.npen, gjk::kPenWave);
+    const bool hit = gjk::box_triangle(R, c, sh, pair_cbt(bi, 10), &wave, nullptr, slow, n, pb, d, &A->a.npen, gjk::kPenWave,
+                                       nullptr, nullptr, saved);
     if (hit && threadIdx.x == 0) emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
 }
-constexpr uint32_t kDeferred = 0x80000000u;  // queue entry flag: the query waits for narrow_deferred
 // the queued box-triangle queries of the workgroup's arenas, dealt round-robin over all its lanes (an
 // arena with many triangle contacts borrows the lanes of quiet ones); base = the workgroup's arenas,
 // nvalid = how many of them exist.  Queries that need the penetration solver are flagged for
-// narrow_deferred (a full wave: kWG == 64), else run it in place.
+// narrow_deferred (a full wave: kWG == 64), else run it in place.  Each query is a call (inlining the
+// queue's loop into one called function instead costs 1.08 -> 1.13 ms and 59 -> 89 MB of scratch writes
+// per launch: the kernel's whole live state is saved around it every tick).
 DEV void narrow_queue(ArenaLDS* base, int nvalid, const MeshView& M) {
     int start[kArenas + 1];
     start[0] = 0;
@@ -495,10 +512,10 @@ DEV void narrow_queue(ArenaLDS* base, int nvalid, const MeshView& M) {
         for (int j = 1; j < kArenas; j++) off = ar == j ? start[j] : off;
         ArenaLDS* A = base + ar;
         const uint32_t e = A->a.q[k - off];
-        const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)(e >> 25);
+        const int t = (int)(e & 0xFFFFFu), obj = (int)((e >> 20) & 31u), bi = (int)((e >> 25) & 7u);
         const float4 a = M.tri[3 * (size_t)t], b = M.tri[3 * (size_t)t + 1], c = M.tri[3 * (size_t)t + 2];
-        if (box_tri_query(A, M, bi, t, obj, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{c.x, c.y, c.z}, kWG == 64))
-            A->a.q[k - off] = e | kDeferred;
+        const uint32_t tag = box_tri_query(A, M, bi, t, obj, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, v3{c.x, c.y, c.z}, kWG == 64);
+        if (tag) A->a.q[k - off] = e | (tag << kPenTagShift);
     }
 }
 // the flagged queries, arena by arena and in queue order, each on the whole wave (every lane calls this)
@@ -510,11 +527,12 @@ DEV void narrow_deferred(ArenaLDS* base, int nvalid, const MeshView& M) {
         for (int k0 = 0; k0 < nq; k0 += kWG) {
             const int k = k0 + (int)threadIdx.x;
             const uint32_t e = k < nq ? A->a.q[k] : 0u;
-            uint64_t m = __ballot((e & kDeferred) != 0);
+            uint64_t m = __ballot((e >> kPenTagShift) != 0);
             while (m) {
                 const uint32_t ej = gjk::rdl(e, gjk::lowbit(m));
                 m &= m - 1ull;
-                box_tri_query_wave(A, M, ej & ~kDeferred);
+                const uint32_t tag = ej >> kPenTagShift;
+                box_tri_query_wave(A, M, ej & ((1u << kPenTagShift) - 1u), tag <= kPenSave ? &g_pen_save.st[tag - 1] : nullptr);
             }
         }
     }

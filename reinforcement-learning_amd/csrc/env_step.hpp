@@ -194,6 +194,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
         A->a.ncand = 0;
         A->a.nq = 0;
     }
+    if (threadIdx.x == 0) g_pen_save.n = 0;
     sync();
     P.mark(4);
     if (valid)
@@ -210,9 +211,10 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     sync();
     narrow_queue(A - (threadIdx.x >> 4), nvalid, M);
     sync();
+    P.mark(5);
     narrow_deferred(A - (threadIdx.x >> 4), nvalid, M);
     sync();
-    P.mark(5);
+    P.mark(18);
     if (valid) sort_candidates(A, l);
     sync();
     if (valid && l == 0) {

@@ -1469,13 +1469,18 @@ __device__ __noinline__ bool calc_pen_depth(ScrT<AS>& S, const Shape& sh, const 
 // btManifoldResult::addContactPoint(normal, point, depth).  S: this lane's penetration-solver scratch.
 // fast / lock: a small LDS work set and the lock that serialises it among the arena's lanes (null: HBM
 // only); slow: this lane's HBM set.
-// mode: kPenInline runs the penetration solver where the query needs it; kPenDefer stops there instead
-// (returns false and sets *deferred: the caller reruns the query in wave mode); kPenWave, called by every
-// lane of the wavefront with the same query, runs it with the wave-mode EPA on `fast` (support vertices
-// only, kWaveSV of them).
 constexpr int kPenInline = 0, kPenDefer = 1, kPenWave = 2;
-DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, int* lock, Scr& slow, v3& normal,
-                      v3& point, float& depth, int* pen_count = nullptr, int mode = kPenInline, bool* deferred = nullptr) {
+// btGjkPairDetector's state where it may hand over to the penetration solver (what the rest of the query
+// reads): a deferred query (kPenDefer) keeps it, the wave-mode rerun resumes from it
+struct PenState {
+    v3 pA, pB, nB;
+    float dist;
+    int valid;
+};
+// the query up to the penetration solver: 0 no contact (early out), 1 GJK's result stands, 2 the
+// penetration solver runs (btGjkPairDetector.cpp:847-851: no valid result, or a degenerate one with the
+// core distance below 0.01)
+DEV int box_triangle_gjk(const m3& R, v3 c, const Shape& s, float cbt, PenState& st) {
     // normal early out, both sides (btConvexConcaveCollisionAlgorithm.cpp:101-136)
     {
         const v3 half = s.impl + v3{s.margin, s.margin, s.margin};
@@ -1488,7 +1493,7 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
             const v3 lp = v3{ld.x >= 0 ? half.x : -half.x, ld.y >= 0 ? half.y : -half.y, ld.z >= 0 ? half.z : -half.z};
             const v3 wp = R * lp + c;
             const float dist = dot(tn, s.t0) - dot(tn, wp);
-            if (dist > cbt) return false;
+            if (dist > cbt) return 0;
             tn = tn * -1.f;
         }
     }
@@ -1580,11 +1585,45 @@ DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, i
         }
     }
     const bool catch_degen = degen && ((double)(distance_ + margin) < 0.01);
-    if (!valid || catch_degen) {
+    st.pA = pA;
+    st.pB = pB;
+    st.nB = nB;
+    st.dist = distance_;
+    st.valid = valid ? 1 : 0;
+    return (!valid || catch_degen) ? 2 : 1;
+}
+// mode: kPenInline runs the penetration solver where the query needs it; kPenDefer stops there instead
+// (returns false, sets *deferred and *save: the caller reruns the query in wave mode); kPenWave, called by
+// every lane of the wavefront with the same query, runs it with the wave-mode EPA on `fast` (support vertices
+// only, kWaveSV of them), from `resume` (a deferred query's saved state) when given.
+DEV bool box_triangle(const m3& R, v3 c, const Shape& s, float cbt, Scr* fast, int* lock, Scr& slow, v3& normal,
+                      v3& point, float& depth, int* pen_count = nullptr, int mode = kPenInline, bool* deferred = nullptr,
+                      PenState* save = nullptr, const PenState* resume = nullptr) {
+    PenState st;
+    int stage;
+    if (resume) {
+        st = *resume;
+        stage = 2;
+    } else {
+        stage = box_triangle_gjk(R, c, s, cbt, st);
+        if (stage == 0) return false;
+    }
+    const float maxd = s.margin + 0.f + cbt;
+    const float max2 = maxd * maxd;
+    const m3 I = ident3();
+    const v3 po = (c + zero3()) * 0.5f;
+    const v3 oA = c - po, oB = zero3() - po;
+    const float mA = s.margin, mB = 0.f;
+    const float margin = mA + mB;
+    float distance_ = st.dist;
+    v3 nB = st.nB, pA = st.pA, pB = st.pB, v;
+    bool valid = st.valid != 0;
+    if (stage == 2) {
         v3 tA, tB;
         v = zero3();
         bool ok2;
         if (mode == kPenDefer) {
+            if (save) *save = st;
             *deferred = true;
             return false;
         }

@@ -20,7 +20,8 @@ __global__ void __launch_bounds__(64) k(int mode, float gap, unsigned long long*
     if (mode < 2 && threadIdx.x != 0) return;  // mode 2: the whole wave runs the query (wave-mode EPA)
     const v3 impl = v3{1.1664109f, 0.8283349f, 0.3479319f};
     const float margin = 0.0386591f;
-    gjk::Shape sh{impl, margin, v3{-50.f, -50.f, 0.f}, v3{50.f, -50.f, 0.f}, v3{0.f, 60.f, 0.f}};
+    // RLGPU_ARITH_SCALAR (2): no rsqrtss table on the device in this program
+    gjk::Shape sh{impl, margin, v3{-50.f, -50.f, 0.f}, v3{50.f, -50.f, 0.f}, v3{0.f, 60.f, 0.f}, 2};
     const float c0 = 0.3f, s0 = 0.2f;  // a tilted box
     m3 R = m3{v3{1, 0, 0}, v3{0, c0 / sqrtf(c0 * c0 + s0 * s0), -s0 / sqrtf(c0 * c0 + s0 * s0)},
               v3{0, s0 / sqrtf(c0 * c0 + s0 * s0), c0 / sqrtf(c0 * c0 + s0 * s0)}};
