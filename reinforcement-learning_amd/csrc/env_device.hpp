@@ -338,8 +338,10 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
             if (len2(from + d * t - c) > (reach + 0.05f) * (reach + 0.05f)) continue;
             float f;
             v3 n;
-            const bool hit = bi == 0 ? gjk::ray_convex_cast(from, to, C.ball_radius, zero3(), brot(A, 0), c, ar, f, n)
-                                     : gjk::ray_convex_cast(from, to, 0.f, C.car_half, brot(A, bi), c, ar, f, n);
+            // one inlined cast for both shapes (the sphere radius or the box half extents select its support)
+            const bool ball = bi == 0;
+            const bool hit = gjk::ray_convex_cast(from, to, ball ? C.ball_radius : 0.f, ball ? zero3() : C.car_half,
+                                                  brot(A, bi), c, ar, f, n);
             if (!hit || !(len2(n) > 0.0001f) || !(f < best)) continue;
             best = f;
             obj = bi;
