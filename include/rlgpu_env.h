@@ -296,11 +296,12 @@ int rlgpu_envset_set_arenas(rlgpu_envset* env, int32_t first, int32_t count, con
 /* Rebuild obs/masks of all arenas from the current state (no physics). */
 int rlgpu_envset_build_obs(rlgpu_envset* env, void* stream);
 
-/* Diagnostics: when d_counters (uint64, device, 64 + 24 x workgroups) is non-NULL, every launch adds
- * the shader cycles thread 0 of each workgroup spends per phase (0-10 tick phases, 11 load/halves
- * prelude, 12 builders, 13 obs rows, 14 resets, 15 store, 16-22 solver sub-phases) to
- * d_counters[phase] (all workgroups) and to d_counters[64 + 24 * workgroup + phase].  NULL disables
- * (the default).  capacity: entries of d_counters (>= 64 + 24 * workgroups, else
+/* Diagnostics: when d_counters (uint64, device, 64 + 24 x workgroups + arenas) is non-NULL, every launch
+ * adds the shader cycles thread 0 of each workgroup spends per phase (0-10 tick phases, 11 load/halves
+ * prelude, 12 builders, 13 obs rows, 14 resets, 15 store, 16-22 solver sub-phases, 18 the deferred
+ * penetration queries) to d_counters[phase] (all workgroups) and to d_counters[64 + 24 * workgroup + phase];
+ * slot 23 of a workgroup and d_counters[64 + 24 * workgroups + arena] count penetration-solver calls.
+ * NULL disables (the default).  capacity: entries of d_counters (>= 64 + 24 * workgroups + arenas, else
  * RLGPU_ERR_INVALID_ARG). */
 int rlgpu_envset_set_profile(rlgpu_envset* env, unsigned long long* d_counters, int64_t capacity);
 

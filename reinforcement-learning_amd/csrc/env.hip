@@ -499,8 +499,8 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
 extern "C" int rlgpu_envset_set_profile(rlgpu_envset* e, unsigned long long* d_counters, int64_t capacity) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(e, "null envset");
-        // 64 totals + 24 per workgroup of the step launch
-        const int64_t need = 64 + 24 * (int64_t)rlgpu::ceil_div(e->cfg.num_arenas, rl::kArenas);
+        // 64 totals + 24 per workgroup of the step launch + one per arena (penetration-solver calls)
+        const int64_t need = 64 + 24 * (int64_t)rlgpu::ceil_div(e->cfg.num_arenas, rl::kArenas) + e->cfg.num_arenas;
         RLGPU_REQUIRE(!d_counters || capacity >= need,
                       "rlgpu_envset_set_profile: buffer of " + std::to_string(capacity) + " counters, needs " + std::to_string(need));
         e->d_prof = d_counters;

@@ -594,6 +594,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
     if (g.prof && valid && l == 0 && A->a.npen) {  // penetration-solver calls: total and this workgroup's
         atomicAdd(&g.prof[28], (unsigned long long)A->a.npen);
         atomicAdd(&g.prof[kProfWG + (size_t)blockIdx.x * kProfPhases + 23], (unsigned long long)A->a.npen);
+        atomicAdd(&g.prof[kProfWG + (size_t)gridDim.x * kProfPhases + arena], (unsigned long long)A->a.npen);
     }
 }
 #endif  // RLGPU_ENV_KERNEL

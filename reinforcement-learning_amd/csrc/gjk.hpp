@@ -1178,7 +1178,8 @@ DEV int adj_f(uint32_t adj, int e) { return (int)((adj >> (8 * e)) & 255u); }
 DEV int adj_e(uint32_t adj, int e) { return (int)((adj >> (24 + 2 * e)) & 3u); }
 // Bullet's expand from best's three edges over the visible-face bits `vis`.  Returns 1 when every call
 // returned true, 0 at the first false, -1 on overflow.  Out: the horizon edges in creation order (lane j of
-// H = face | edge << 8 of the j-th), their count, and the visible faces the walk removes.
+// H = face | edge << 8 | c[e1] << 16 | c[e] << 24 of the j-th: the face and its new face's first two
+// vertices), their count, and the visible faces the walk removes.
 DEV int wexpand(const WFace& F, int best, uint64_t vis, uint64_t lanes, uint32_t& H, int& nh, uint64_t& removed) {
     uint64_t visited = 1ull << best;
     removed = 0;
@@ -1195,7 +1196,9 @@ DEV int wexpand(const WFace& F, int best, uint64_t vis, uint64_t lanes, uint32_t
                 if ((visited >> f) & 1) return 0;  // f->pass == pass: expand returns false
                 if (!((vis >> f) & 1)) {           // the face sees w below it: a horizon edge, newface(c[e1], c[e], w)
                     if (nh >= 64 || ((lanes >> nh) & 1) == 0) return -1;
-                    H = wrl(H, nh, top);
+                    const uint32_t fc = rdl(F.c, f);
+                    const int e1 = e == 2 ? 0 : e + 1;
+                    H = wrl(H, nh, top | (((fc >> (8 * e1)) & 255u) << 16) | (((fc >> (8 * e)) & 255u) << 24));
                     nh++;
                     pop = true;
                 } else {  // visible: mark it, walk its edge e1, then e2, then remove it
@@ -1323,9 +1326,8 @@ GJK_CALLED int epa_wave(ScrT<AS>& S, const Mink& m, Gjk2& g, Simp& s, v3 guess, 
                 const int r = __popcll(freem & below);
                 const bool host = in_free && r < nh;
                 const uint32_t h = lane_perm(H, host ? r : 0);
-                const int hf = (int)(h & 255u), he = (int)((h >> 8) & 3u), he1 = he == 2 ? 0 : he + 1;
-                const uint32_t hc = lane_perm(F.c, hf);
-                const int na = (int)((hc >> (8 * he1)) & 255u), nb = (int)((hc >> (8 * he)) & 255u);
+                const int hf = (int)(h & 255u), he = (int)((h >> 8) & 3u);
+                const int na = (int)((h >> 16) & 255u), nb = (int)(h >> 24);
                 v3 nn = zero3();
                 float nd = 0.f;
                 bool nok = true;

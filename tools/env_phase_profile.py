@@ -34,7 +34,7 @@ for i in range(warm):
 APW = int(os.environ.get("RLGPU_ENV_APW", "4"))  # arenas per workgroup of the built library (env_kernel.hpp)
 wg = (n + APW - 1) // APW
 KP, KW = 24, 64  # env_kernel.hpp kProfPhases, kProfWG
-prof = torch.zeros(KW + wg * KP, dtype=torch.int64, device=dev)
+prof = torch.zeros(KW + wg * KP + n, dtype=torch.int64, device=dev)  # + per-arena penetration-solver calls
 spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
 L = _lib.lib()
 L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
@@ -42,6 +42,7 @@ _lib.check(L.rlgpu_envset_set_profile(env._h, ctypes.c_void_p(prof.data_ptr()), 
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 tot_ms = 0.0
 pen_rows = []  # per step: penetration-solver calls in all / the busiest / the slowest workgroup
+arena_rows, slow_arenas = [], []  # per step: workgroups with >= 2 arenas calling it; the slowest one's per-arena calls
 for i in range(steps):
     acts.copy_(torch.argmax(torch.rand((4 * n, 90), device=dev, generator=gen) * env.action_masks, 1))
     e0.record()
@@ -49,12 +50,16 @@ for i in range(steps):
     e1.record()
     torch.cuda.synchronize()
     tot_ms += e0.elapsed_time(e1)
-    per = prof[KW:].view(wg, KP)[:, :23].double()
+    per = prof[KW:KW + wg * KP].view(wg, KP)[:, :23].double()
     tots = per.sum(1)
     k = int(tots.argmax())
     spread.append((tots.max().item(), tots.mean().item(), per[k].cpu(), per.mean(0).cpu()))
-    pens = prof[KW:].view(wg, KP)[:, 23]
+    pens = prof[KW:KW + wg * KP].view(wg, KP)[:, 23]
     pen_rows.append((int(pens.sum()), int(pens.max()), int(pens[k])))
+    pa = prof[KW + wg * KP:].view(-1)
+    pa = torch.nn.functional.pad(pa, (0, wg * APW - n)).view(wg, APW)
+    arena_rows.append(((pa > 0).sum(1) >= 2).sum().item())  # workgroups with two or more arenas calling the solver
+    slow_arenas.append(pa[k].cpu().tolist())
     prof[KW:].zero_()
 c = prof.cpu().tolist()
 total = sum(c[:23])
@@ -78,3 +83,5 @@ for k in order[:8]:
 pr = np.array(pen_rows)
 print(f"  penetration-solver (EPA) calls per step: mean {pr[:, 0].mean():.1f} over all workgroups, busiest workgroup "
       f"{pr[:, 1].mean():.1f} (max {pr[:, 1].max()}), slowest workgroup {pr[:, 2].mean():.1f}")
+print(f"  workgroups with two or more arenas calling the penetration solver, per step: {np.mean(arena_rows):.1f}; "
+      f"the slowest workgroup's calls per arena, first steps: {slow_arenas[:6]}")
