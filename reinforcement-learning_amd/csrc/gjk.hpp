@@ -833,35 +833,26 @@ DEV void bind(ScrT<AS>& S, int fa, int ea, int fb, int eb) {
     S.fc[fb].e[eb] = (uint8_t)ea;
     S.fc[fb].f[eb] = (uint8_t)fa;
 }
-// EPA::getedgedist on the edge's two support points (already in registers: newface loads each vertex once)
-DEV bool getedgedist(v3 fn, v3 aw, v3 bw, float& dist) {
-    const v3 ba = bw - aw;
-    const v3 n_ab = cross(ba, fn);
-    const float a_dot_nab = dot(aw, n_ab);
-    if (a_dot_nab < 0) {
-        const float ba_l2 = len2(ba);
-        const float a_dot_ba = dot(aw, ba);
-        const float b_dot_ba = dot(bw, ba);
-        if (a_dot_ba > 0) {
-            dist = len(aw);
-        } else if (b_dot_ba < 0) {
-            dist = len(bw);
-        } else {
-            const float a_dot_b = dot(aw, bw);
-            const float q = (len2(aw) * len2(bw) - a_dot_b * a_dot_b) / ba_l2;
-            dist = sqrtf(q > 0.f ? q : 0.f);
-        }
-        return true;
-    }
-    return false;
-}
 // EPA::newface's plane of (a, b, c): false when degenerate (|n| <= EPA_ACCURACY); else n normalised and d
-// the distance of the nearest edge (getedgedist) or of the plane
+// the distance of the nearest edge (EPA::getedgedist, btGjkEpa2.cpp) or of the plane
+// Straight-line form (no divergent branches for the wave-mode EPA's lanes): the first edge of (ab, bc, ca)
+// whose getedgedist test holds is selected, and its distance -- |a|, |b| or sqrt(max(q, 0)) -- or the
+// plane's dot(a, n) / l is one select of operands for one division and one square root: the same
+// operations on the same values as the short-circuit calls.
 DEV bool face_plane(v3 aw, v3 bw, v3 cw, v3& n, float& d) {
     n = cross(bw - aw, cw - aw);
     const float l = len(n);
     if (!(l > kEpaAccuracy)) return false;
-    if (!(getedgedist(n, aw, bw, d) || getedgedist(n, bw, cw, d) || getedgedist(n, cw, aw, d))) d = dot(aw, n) / l;
+    const bool t0 = dot(aw, cross(bw - aw, n)) < 0, t1 = dot(bw, cross(cw - bw, n)) < 0, t2 = dot(cw, cross(aw - cw, n)) < 0;
+    const bool edge = t0 || t1 || t2;
+    const v3 ea = t0 ? aw : (t1 ? bw : cw), eb = t0 ? bw : (t1 ? cw : aw);
+    const v3 ba = eb - ea;
+    const float a_dot_ba = dot(ea, ba), b_dot_ba = dot(eb, ba);
+    const float a_dot_b = dot(ea, eb);
+    const bool use_a = a_dot_ba > 0, use_b = !use_a && b_dot_ba < 0;
+    const float q = (edge ? (len2(ea) * len2(eb) - a_dot_b * a_dot_b) : dot(aw, n)) / (edge ? len2(ba) : l);
+    const float root = sqrtf(use_a ? len2(ea) : (use_b ? len2(eb) : (q > 0.f ? q : 0.f)));
+    d = edge ? root : q;
     n = n / l;
     return true;
 }
@@ -1144,22 +1135,25 @@ DEV v3 rdl(v3 v, int l) { return v3{rdl(v.x, l), rdl(v.y, l), rdl(v.z, l)}; }
 DEV uint32_t wrl(uint32_t v, int l, uint32_t x) { return __lane_id() == l ? x : v; }  // lane l of v = x
 DEV uint32_t rdfirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint32_t lane_perm(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_ds_bpermute(l << 2, (int)v); }
-DEV uint32_t wmin(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
-        v = u < v ? u : v;
-    }
+// wave min / max without the LDS crossbar: xor-32 / xor-16 by v_permlane32_swap / v_permlane16_swap,
+// then DPP row_ror 8 / 4 / 2 / 1 (mlp_kernels.hpp wave_max_x); every lane ends with the wave's result
+template <int CTRL>
+DEV uint32_t dpp_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false); }
+template <bool MX>
+DEV uint32_t wred(uint32_t v) {
+    auto pick2 = [](uint32_t a, uint32_t b) { return MX ? (a > b ? a : b) : (a < b ? a : b); };
+    auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = pick2(r[0], r[1]);
+    r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = pick2(r[0], r[1]);
+    v = pick2(v, dpp_u<0x128>(v));
+    v = pick2(v, dpp_u<0x124>(v));
+    v = pick2(v, dpp_u<0x122>(v));
+    v = pick2(v, dpp_u<0x121>(v));
     return rdfirst(v);
 }
-DEV uint32_t wmax(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
-        v = u > v ? u : v;
-    }
-    return rdfirst(v);
-}
+DEV uint32_t wmin(uint32_t v) { return wred<false>(v); }
+DEV uint32_t wmax(uint32_t v) { return wred<true>(v); }
 DEV int lowbit(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 DEV int highbit(uint64_t m) { return 63 - __clzll((long long)m); }
 // findbest over the lanes: least d^2, ties to the newest face
