@@ -65,46 +65,50 @@ DEV void add_player_obs(float* o, const PView& pl, bool inv, v3 bp, v3 bv) {
 }
 
 // AdvancedObs::BuildObs + DefaultAction::GetActionMask for player pi, into LDS rows
-DEV void build_obs_row(ArenaLDS* A, int pi) {
+// One quarter of player pi's AdvancedObs row and action mask (AdvancedObs.cpp, DefaultAction masks), so
+// that the arena's 16 lanes build its 4 rows together: part 0 the ball, previous action and self block,
+// part 1 the boost pads, part 2 the teammate and the first opponent, part 3 the second opponent and the
+// mask.  Every element is the same expression as in a whole-row build; only the lane that writes it differs.
+DEV void build_obs_row(ArenaLDS* A, int pi, int part) {
     // player views are read from LDS where used: an array of them indexed by the lane's player
     // would live in private (scratch) memory
-    const PView me = view_player(A, pi);
+    const bool inv = pi & 1;  // the player's team (orange = index & 1)
     float* o = A->u.out.obs[pi];
-    bool inv = me.orange;
-    v3 bp = inv_if(ld3(A->s.ball.pos) * kBT2UU, inv), bv = inv_if(ld3(A->s.ball.vel) * kBT2UU, inv),
-       ba = inv_if(ld3(A->s.ball.angvel), inv);
-    const float BPOS = 1 / 5000.f, BVEL = 1 / 2300.f, BANG = 1 / 3.f;  // AdvancedObs.h:10-13
-    o[0] = bp.x * BPOS; o[1] = bp.y * BPOS; o[2] = bp.z * BPOS;
-    o[3] = bv.x * BVEL; o[4] = bv.y * BVEL; o[5] = bv.z * BVEL;
-    o[6] = ba.x * BANG; o[7] = ba.y * BANG; o[8] = ba.z * BANG;
-    for (int k = 0; k < 8; k++) o[9 + k] = A->s.env.prev_action[pi][k];
-    for (int k = 0; k < RLGPU_PADS; k++) {
-        int act_idx = inv ? C.pad_map[RLGPU_PADS - k - 1] : C.pad_map[k];
-        int tim_idx = inv ? C.pad_map[k] : C.pad_map[RLGPU_PADS - k - 1];  // GameState.h:60 quirk
-        bool active = A->s.pads[act_idx].is_active;
-        float timer = A->s.pads[tim_idx].cooldown;
-        o[17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
-    }
-    float* q = o + 51;
-    add_player_obs(q, me, inv, bp, bv);
-    q += 29;
-    for (int j = 0; j < 4; j++)
-        if (j != pi && (j & 1) == (pi & 1)) {  // teammates (orange = j & 1)
-            add_player_obs(q, view_player(A, j), inv, bp, bv);
-            q += 29;
+    v3 bp = inv_if(ld3(A->s.ball.pos) * kBT2UU, inv), bv = inv_if(ld3(A->s.ball.vel) * kBT2UU, inv);
+    if (part == 0) {
+        const v3 ba = inv_if(ld3(A->s.ball.angvel), inv);
+        const float BPOS = 1 / 5000.f, BVEL = 1 / 2300.f, BANG = 1 / 3.f;  // AdvancedObs.h:10-13
+        o[0] = bp.x * BPOS; o[1] = bp.y * BPOS; o[2] = bp.z * BPOS;
+        o[3] = bv.x * BVEL; o[4] = bv.y * BVEL; o[5] = bv.z * BVEL;
+        o[6] = ba.x * BANG; o[7] = ba.y * BANG; o[8] = ba.z * BANG;
+        for (int k = 0; k < 8; k++) o[9 + k] = A->s.env.prev_action[pi][k];
+        add_player_obs(o + 51, view_player(A, pi), inv, bp, bv);
+    } else if (part == 1) {
+        for (int k = 0; k < RLGPU_PADS; k++) {
+            int act_idx = inv ? C.pad_map[RLGPU_PADS - k - 1] : C.pad_map[k];
+            int tim_idx = inv ? C.pad_map[k] : C.pad_map[RLGPU_PADS - k - 1];  // GameState.h:60 quirk
+            bool active = A->s.pads[act_idx].is_active;
+            float timer = A->s.pads[tim_idx].cooldown;
+            o[17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
         }
-    for (int j = 0; j < 4; j++)
-        if ((j & 1) != (pi & 1)) {  // opponents
-            add_player_obs(q, view_player(A, j), inv, bp, bv);
-            q += 29;
+    } else if (part == 2) {
+        // the teammate (the other player of this team), then the first opponent (player of the other
+        // team with the lower index)
+        add_player_obs(o + 51 + 29, view_player(A, pi ^ 2), inv, bp, bv);
+        add_player_obs(o + 51 + 58, view_player(A, (pi & 1) ^ 1), inv, bp, bv);
+    } else {
+        add_player_obs(o + 51 + 87, view_player(A, ((pi & 1) ^ 1) + 2), inv, bp, bv);
+        const rlgpu_car& c = A->s.cars[pi];
+        const bool on_ground = c.is_on_ground;
+        const bool hfj = c.is_on_ground || (!c.has_flipped && !c.has_double_jumped && c.air_time_since_jump < 1.25f);
+        uint8_t* m = A->u.out.masks[pi];
+        bool turtled = c.world_contact && c.world_contact_normal[2] > 0.9f;
+        for (int k = 0; k < RLGPU_ACTIONS; k++) {
+            uint8_t r = on_ground ? C.mask_ground[k] : C.mask_air[k];
+            if (c.boost == 0) r &= (uint8_t)~C.mask_boost[k];
+            if (hfj || turtled) r |= C.mask_jump[k];
+            m[k] = r & 1;
         }
-    uint8_t* m = A->u.out.masks[pi];
-    bool turtled = me.world_contact && me.wc_z > 0.9f;
-    for (int k = 0; k < RLGPU_ACTIONS; k++) {
-        uint8_t r = me.on_ground ? C.mask_ground[k] : C.mask_air[k];
-        if (me.boost == 0) r &= (uint8_t)~C.mask_boost[k];
-        if (me.hfj || turtled) r |= C.mask_jump[k];
-        m[k] = r & 1;
     }
 }
 

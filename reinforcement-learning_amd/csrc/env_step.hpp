@@ -110,21 +110,27 @@ DEV void load_pad_regs(PadRegs& R, int l) {
 #endif
 RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R,
                           int nvalid) {
-    if (valid && l == 0) {
+    if (valid) {  // per body / car on lanes 0-4: independent fields, read before the respawns below write
         rlgpu_arena_state& s = A->s;
-        bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
-        s.ball_sleeping = sleep;
-        A->a.ball_sleep = sleep;
-        A->a.active[0] = 1;
-        for (int c = 0; c < 4; c++) {
+        if (l == 0) {
+            bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
+            s.ball_sleeping = sleep;
+            A->a.ball_sleep = sleep;
+            A->a.active[0] = 1;
+        } else if (l < 5) {
+            const int c = l - 1;
             A->a.active[c + 1] = !s.cars[c].is_demoed;
             float* ctl = s.cars[c].controls;  // CarControls::ClampFix
             for (int k = 0; k < 5; k++) ctl[k] = stdclamp(ctl[k], -1.f, 1.f);
         }
-        for (int i = 0; i < 5; i++) {
-            A->a.snap_vel[i] = bvel(A, i);
-            A->a.snap_ang[i] = bang(A, i);
+        if (l < 5) {
+            A->a.snap_vel[l] = bvel(A, l);
+            A->a.snap_ang[l] = bang(A, l);
         }
+    }
+    sync();
+    if (valid && l == 0) {
+        rlgpu_arena_state& s = A->s;
         // demo timer / respawn (Car.cpp:66-84), RNG draws in car order
         for (int c = 0; c < 4; c++) {
             rlgpu_car& cs = s.cars[c];
@@ -535,7 +541,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
             A->s.env.last_tick_count = A->s.env.tick_count;
         }
         const bool fused_reset = g.reset_mode == 1 && valid && term != 0;
-        if (valid && l < 4) build_obs_row(A, l);
+        if (valid) build_obs_row(A, l & 3, l >> 2);
         sync(); P.mark(13);
         if (valid) {
             copy_rows(A, l, arena, g.obs, g.masks);
@@ -549,7 +555,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
         if (g.reset_mode == 1) {
             if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena + g.arena_offset, g.fuzz != 0);
             sync(); P.mark(14);
-            if (fused_reset && l < 4) build_obs_row(A, l);
+            if (fused_reset) build_obs_row(A, l & 3, l >> 2);
             sync(); P.mark(14);
             if (fused_reset) {
                 copy_rows(A, l, arena, g.obs, g.masks);
@@ -573,7 +579,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
         }
         sync(); P.mark(14);
         bool rebuild = do_reset || (valid && g.reset_mode == 5);
-        if (rebuild && l < 4) build_obs_row(A, l);
+        if (rebuild) build_obs_row(A, l & 3, l >> 2);
         sync(); P.mark(14);
         if (rebuild) copy_rows(A, l, arena, g.obs, g.masks);
         sync(); P.mark(14);
