@@ -69,7 +69,8 @@ int rlgpu_mesh_bvh_order(const float* tris, int32_t ntris, const int32_t* object
  * lds_first != 0: the penetration solver first runs in a small LDS work set per lane (24 support
  * vertices, 28 live faces), rerun in the lane's HBM set when it overflows; 0: HBM only; 2: the env
  * kernel's policy -- 64 lanes each stop at the penetration solver, then the whole wavefront runs those
- * queries one at a time with the polytope in its registers (gjk.hpp epa_wave), HBM rerun on overflow.  arith: RLGPU_ARITH_* (the normalisations follow that build, include/rlgpu_arith.h).
+ * queries one at a time with the polytope in its registers (gjk.hpp epa_wave), HBM rerun on overflow;
+ * 3: as 2 with a 6-vertex wave set, so that the EPA overflows and reruns (tests of that path).  arith: RLGPU_ARITH_* (the normalisations follow that build, include/rlgpu_arith.h).
  * Asynchronous on `stream`; the HBM sets are allocated per call. */
 int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const float* d_centre, const float* d_tri,
                                const float* d_cbt, float* d_out, int32_t lds_first, int32_t arith, void* stream);

@@ -221,6 +221,8 @@ struct rlgpu_envset {
     rl::Plugins* d_plug = nullptr;      // its device copy (StepArgs::plug)
     int32_t* d_player_start = nullptr;  // EnvState::arenaPlayerStartIdx
     float* d_reward_values = nullptr;   // [players][nr] per-reward values (rlgpu_envset_enable_reward_values) or null
+    int pen_slots = rl::kPenSave;       // saved deferred penetration queries per workgroup and tick (tests:
+                                        // RLGPU_DEBUG_PEN_SAVE_SLOTS at create, 0..kPenSave, exercises the restart path)
 };
 
 namespace {
@@ -363,6 +365,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.arith = e->cfg.arith;
     g.arena_offset = e->cfg.arena_offset;
     g.fuzz = e->cfg.state_setter == RLGPU_SS_FUZZED_KICKOFF;
+    g.pen_slots = e->pen_slots;
     g.reward_values = g.build ? e->d_reward_values : nullptr;
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
@@ -413,6 +416,7 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         rlgpu::MeshGrid grid = rlgpu::build_mesh_grid(tris, ntris, cfg->mesh_tris ? cfg->mesh_object_ntris : nullptr,
                                                       cfg->mesh_tris ? cfg->mesh_objects : 1, cfg->arith);
         auto* e = new rlgpu_envset();
+        if (const char* v = getenv("RLGPU_DEBUG_PEN_SAVE_SLOTS")) e->pen_slots = std::max(0, std::min(atoi(v), rl::kPenSave));
         e->cfg = *cfg;
         e->cfg.mesh_tris = nullptr;  // host pointers are not kept
         e->cfg.mesh_object_ntris = nullptr;
@@ -778,7 +782,8 @@ __global__ void __launch_bounds__(16) box_triangle_kernel(int n, const float* ro
     o[7] = hit ? d : 0.f;
 }
 // lds == 2: the env kernel's narrowphase scheme -- 64 lanes each run a query with the penetration solver
-// deferred, then the whole wave runs the deferred queries one at a time with the wave-mode EPA
+// deferred, then the whole wave runs the deferred queries one at a time with the wave-mode EPA; lds == 3:
+// the same with a 6-vertex wave set, so that EPA runs overflow and rerun on the HBM set
 __device__ __forceinline__ void bt_load(int i, const float* rot, const float* centre, const float* tri, int ar, m3& R, v3& c,
                                         gjk::Shape& sh) {
     const float* r = rot + 9 * (size_t)i;
@@ -799,7 +804,8 @@ __device__ __forceinline__ void bt_store(float* out, int i, bool hit, v3 nrm, v3
     o[7] = hit ? d : 0.f;
 }
 __global__ void __launch_bounds__(64) box_triangle_wave_kernel(int n, const float* rot, const float* centre, const float* tri,
-                                                               const float* cbt, float* out, gjk::GjkScratch* scratch, int ar) {
+                                                               const float* cbt, float* out, gjk::GjkScratch* scratch, int ar,
+                                                               int tiny) {
     __shared__ char small[gjk::kSmallBytes];
     const int i = blockIdx.x * 64 + threadIdx.x;
     gjk::Scr slow = gjk::hbm_view(scratch + i);  // scratch holds a set for every lane of the grid
@@ -825,6 +831,7 @@ __global__ void __launch_bounds__(64) box_triangle_wave_kernel(int n, const floa
         float d = 0.f;
         bt_load(q, rot, centre, tri, ar, R, c, sh);
         gjk::Scr wave = gjk::wave_view(small);
+        if (tiny) wave.max_sv = 6;  // two EPA vertices, then the overflow rerun on the HBM set
         // even queries resume from the deferring lane's saved state, odd ones start over (both env paths)
         const gjk::PenState rs{gjk::rdl(st.pA, j), gjk::rdl(st.pB, j), gjk::rdl(st.nB, j), gjk::rdl(st.dist, j),
                                (int)gjk::rdl((uint32_t)st.valid, j)};
@@ -845,13 +852,13 @@ extern "C" int rlgpu_box_triangle_queries(int32_t n, const float* d_rot, const f
         ensure_const();
         if (rl::sse_api(arith)) ensure_rsqrt();
         hipStream_t s = (hipStream_t)stream;
-        RLGPU_REQUIRE(lds_first >= 0 && lds_first <= 2, "rlgpu_box_triangle_queries: lds_first must be 0, 1 or 2");
+        RLGPU_REQUIRE(lds_first >= 0 && lds_first <= 3, "rlgpu_box_triangle_queries: lds_first must be 0 .. 3");
         void* scratch = nullptr;
-        const int lanes = lds_first == 2 ? rlgpu::ceil_div(n, 64) * 64 : n;
+        const int lanes = lds_first >= 2 ? rlgpu::ceil_div(n, 64) * 64 : n;
         RLGPU_CHECK_HIP(hipMallocAsync(&scratch, (size_t)lanes * sizeof(rl::gjk::GjkScratch), s));
-        if (lds_first == 2)
+        if (lds_first >= 2)
             hipLaunchKernelGGL(rl::box_triangle_wave_kernel, dim3(lanes / 64), dim3(64), 0, s, n, d_rot, d_centre, d_tri,
-                               d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)arith);
+                               d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)arith, (int)(lds_first == 3));
         else
             hipLaunchKernelGGL(rl::box_triangle_kernel, dim3(rlgpu::ceil_div(n, 16)), dim3(16), 0, s, n, d_rot, d_centre,
                                d_tri, d_cbt, d_out, (rl::gjk::GjkScratch*)scratch, (int)lds_first, (int)arith);

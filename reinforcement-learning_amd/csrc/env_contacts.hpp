@@ -450,6 +450,7 @@ constexpr uint32_t kPenTagShift = 28, kPenNoSave = 15;
 struct PenSave {
     gjk::PenState st[kPenSave];
     int n;
+    int cap;  // slots in use this launch (StepArgs::pen_slots: kPenSave, fewer to test the restart path)
 };
 static __shared__ PenSave g_pen_save;
 // One car hitbox vs mesh triangle: Bullet's GJK / EPA query (gjk.hpp) and its candidate.  defer: a query
@@ -471,7 +472,7 @@ __device__ __noinline__ uint32_t box_tri_query(ArenaLDS* A, const MeshView& M, i
         emit(A, bi * 5, t, mesh_key(bi, obj), n, pb, d);
     if (!deferred) return 0u;
     const int slot = atomicAdd(&g_pen_save.n, 1);
-    if (slot >= kPenSave) return kPenNoSave;
+    if (slot >= g_pen_save.cap) return kPenNoSave;
     g_pen_save.st[slot] = st;
     return (uint32_t)slot + 1u;
 }

@@ -42,6 +42,7 @@ struct StepArgs {
     int arena_offset;          // global index of arena 0 (the arenas' Philox streams)
     float* reward_values;      // [players][nr] each reward's value before its weight, or null
     int fuzz;                  // FuzzedKickoffState (rlgpu_envset_config.state_setter)
+    int pen_slots;             // deferred penetration queries whose GJK state is saved (kPenSave; tests: fewer)
 };
 
 #ifdef RLGPU_ENV_KERNEL
@@ -405,6 +406,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
         A->a.epa_lock = A->a.npen = 0;
         A->a.arith = g.arith;
     }
+    if (threadIdx.x == 0) g_pen_save.cap = g.pen_slots;
     sync(); P.mark(11);
     // ---- StepFirstHalf (EnvSet.cpp:113-130) prelude
     if (g.ticks_first > 0) {

@@ -211,7 +211,8 @@ def box_triangle_queries(rot, centre, tri, cbt, lds_first=True, arith=0):
     rlgpu_box_triangle_queries) on the device, one query per lane.  CUDA tensors: rot [n,3,3] (basis rows),
     centre [n,3], tri [n,3,3], cbt [n] -> [n,8] float32 (hit, normal xyz, point xyz, depth).  lds_first: the
     penetration solver runs in a small LDS set first, else (False) in HBM only; "wave": the env kernel's
-    policy (penetration queries deferred, then run by the whole wavefront).  arith: RLGPU_ARITH_*
+    policy (penetration queries deferred, then run by the whole wavefront); "wave-overflow": the same with a
+    6-vertex wave set (every longer EPA reruns on the HBM set).  arith: RLGPU_ARITH_*
     (include/rlgpu_arith.h)."""
     import torch
     rot = rot.reshape(-1, 9).contiguous().float()
@@ -224,7 +225,8 @@ def box_triangle_queries(rot, centre, tri, cbt, lds_first=True, arith=0):
     L.rlgpu_box_triangle_queries.argtypes = [ctypes.c_int32] + [ctypes.c_void_p] * 5 + [ctypes.c_int32, ctypes.c_int32,
                                                                                      ctypes.c_void_p]
     _lib.check(L.rlgpu_box_triangle_queries(n, rot.data_ptr(), centre.data_ptr(), tri.data_ptr(), cbt.data_ptr(),
-                                            out.data_ptr(), 2 if lds_first == "wave" else int(bool(lds_first)), int(arith),
+                                            out.data_ptr(), {"wave": 2, "wave-overflow": 3}.get(lds_first, None) if isinstance(lds_first, str)
+                                            else int(bool(lds_first)), int(arith),
                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
                "rlgpu_box_triangle_queries")
     return out

@@ -199,18 +199,29 @@ def test_env_custom_mesh_parity(gpu):
         _check_step(g, o, f"mesh perturbed step {t}")
 
 
-def test_env_procedural_soccar_mesh_parity(gpu):
+@pytest.mark.parametrize("pen_slots", [None, 0])
+def test_env_procedural_soccar_mesh_parity(gpu, pen_slots, monkeypatch):
     """The bench's SOCCAR-sized workload mesh (rlgpu.mesh.procedural_soccar: 16 objects, 8,800
     triangles -- quarter pipes, rounded corners, goal boxes): cars driven and balls thrown into the
-    curved transitions and goals, bit-exact vs the oracle's scan of every triangle."""
+    curved transitions and goals, bit-exact vs the oracle's scan of every triangle.  The run goes through
+    the penetration solver (counted by the env set's profile counters); pen_slots = 0 takes the deferred
+    queries' restart path (no saved pair-GJK state) instead of the resume path."""
+    import ctypes
     import torch
+    from rlgpu import _lib
     from rlgpu.env import EnvSet
     from rlgpu.mesh import procedural_soccar
     from rlgpu.state import ARENA
     mesh = procedural_soccar()
     assert (mesh.num_objects, mesh.num_tris) == (16, 8800)
     n = 64
+    if pen_slots is not None:
+        monkeypatch.setenv("RLGPU_DEBUG_PEN_SAVE_SLOTS", str(pen_slots))
     g, o = EnvSet(n, seed=21, device=gpu, mesh=mesh), oracle.EnvSet(n, seed=21, mesh=mesh, threads=8)
+    prof = torch.zeros(64 + 24 * (n // 4) + n, dtype=torch.int64, device=gpu)
+    L = _lib.lib()
+    L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    _lib.check(L.rlgpu_envset_set_profile(g._h, ctypes.c_void_p(prof.data_ptr()), prof.numel()), "set_profile")
     _check(g, o, "create")
     rng = np.random.default_rng(8)
     st = np.frombuffer(o.get_arenas().tobytes(), ARENA).copy()
@@ -230,6 +241,10 @@ def test_env_procedural_soccar_mesh_parity(gpu):
         o.step(a, True)
         g.step(torch.from_numpy(a).to(gpu), True)
         _check_step(g, o, f"procedural soccar step {t}")
+    torch.cuda.synchronize()
+    pen = int(prof[28])
+    assert pen > 0 and int(prof[64 + 24 * (n // 4):].sum()) == pen, pen  # the penetration solver ran
+    _lib.check(L.rlgpu_envset_set_profile(g._h, None, 0), "set_profile")
 
 
 def test_env_reset_arenas_mask(gpu):

@@ -119,7 +119,7 @@ def test_device_box_triangle_bit_exact(gpu):
     assert counts[1] > 1000
     args = [torch.from_numpy(a).to(gpu) for a in (R, c, t, cbt)]
     # full-capacity HBM sets; small LDS sets with the HBM rerun; the env kernel's deferred wave-mode EPA
-    for lds_first in (False, True, "wave"):
+    for lds_first in (False, True, "wave", "wave-overflow"):
         got = box_triangle_queries(*args, lds_first=lds_first).cpu().numpy()
         bad = np.nonzero(np.any(_canon(got) != _canon(want), axis=1))[0]
         assert len(bad) == 0, f"lds_first={lds_first}: {len(bad)} of {len(R)} differ; first {bad[:5]}: " \
