@@ -254,7 +254,10 @@ DEV void plane_space1(v3 n, v3& p, v3& q) {
 }
 // a dynamic body's position in every cell's dynamic list (ties: creation order); env_contacts.hpp keeps the ranks
 DEV int bp_key(const ArenaLDS* A, int b) { return A->s.env.bp_rank[b] * 8 + b; }  // list position (ties: creation)
-DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& hit_point, v3& hit_normal) {
+// btCollisionWorld::rayTest of a wheel ray, first half: the closest hit among the static objects (mesh
+// triangles, planes) into W.rc_*, and a cast job per dynamic body the ray may reach (wheel_casts runs them
+// on all lanes; ray_cast_finish combines them in the cell list's order)
+DEV void ray_cast_static(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, int wheel, WheelT& W) {
     float best = 1.0f;
     int obj = -1;
     v3 nrm = zero3();
@@ -320,33 +323,81 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
     // sphere or the car compound's box child (btCollisionWorld.cpp:277-310,339-400), kept when strictly closer
     // and its normal long enough.  A body is in the cells around its home cell (btRSBroadphase.cpp:182-200),
     // wider than any wheel ray, so every body within reach is listed; a body whose bounding sphere the
-    // segment misses by more than the cast's tolerances cannot be hit and is skipped without the cast.
-    {
-        int done = 0;
-        for (int k = 0; k < 5; k++) {
-            int bi = -1, key = 1 << 30;
-            for (int c = 0; c < 5; c++)
-                if (!(done >> c & 1) && bp_key(A, c) < key) {
-                    key = bp_key(A, c);
-                    bi = c;
-                }
-            done |= 1 << bi;
-            if (bi == self || best == 0.f) continue;  // btSingleRayCallback::process stops at fraction 0
-            const v3 c = bi == 0 ? bpos(A, 0) : car_box_center(A, bi);
-            const float reach = bi == 0 ? C.ball_radius : len(C.car_half);
-            const float t = fminf(fmaxf(dot(c - from, d) / fmaxf(dot(d, d), 1e-30f), 0.f), 1.f);
-            if (len2(from + d * t - c) > (reach + 0.05f) * (reach + 0.05f)) continue;
-            float f;
-            v3 n;
-            // one inlined cast for both shapes (the sphere radius or the box half extents select its support)
-            const bool ball = bi == 0;
-            const bool hit = gjk::ray_convex_cast(from, to, ball ? C.ball_radius : 0.f, ball ? zero3() : C.car_half,
-                                                  brot(A, bi), c, ar, f, n);
-            if (!hit || !(len2(n) > 0.0001f) || !(f < best)) continue;
-            best = f;
-            obj = bi;
-            nrm = bt_normalize(n, ar);  // castResult.m_normal.normalize()
-        }
+    // segment misses by more than the cast's tolerances cannot be hit and gets no job (the oracle casts
+    // against every body: the env parity tests check that this skip is exact).  Jobs go in list order;
+    // none after a fraction-0 static hit (btSingleRayCallback::process stops at fraction 0).
+    W.rc_best = best;
+    W.rc_obj = obj;
+    W.rc_nrm = nrm;
+    if (best == 0.f) return;
+    int done = 0;
+    for (int k = 0; k < 5; k++) {
+        int bi = -1, key = 1 << 30;
+        for (int c = 0; c < 5; c++)
+            if (!(done >> c & 1) && bp_key(A, c) < key) {
+                key = bp_key(A, c);
+                bi = c;
+            }
+        done |= 1 << bi;
+        if (bi == self) continue;
+        const v3 c = bi == 0 ? bpos(A, 0) : car_box_center(A, bi);
+        const float reach = bi == 0 ? C.ball_radius : len(C.car_half);
+        const float t = fminf(fmaxf(dot(c - from, d) / fmaxf(dot(d, d), 1e-30f), 0.f), 1.f);
+        if (len2(from + d * t - c) > (reach + 0.05f) * (reach + 0.05f)) continue;
+        const int slot = atomicAdd(&A->u.wc.njob, 1);
+        CastJob& J = A->u.wc.job[slot];
+        J.wheel = (uint8_t)wheel;
+        J.body = (uint8_t)bi;
+    }
+}
+// the cast jobs of the workgroup's arenas (base, nvalid of them), dealt over all its lanes
+DEV void wheel_casts(ArenaLDS* base, int nvalid) {
+    int start[kArenas + 1];
+    start[0] = 0;
+#pragma unroll
+    for (int a = 0; a < kArenas; a++) start[a + 1] = start[a] + (a < nvalid ? base[a].u.wc.njob : 0);
+    for (int k = threadIdx.x; k < start[kArenas]; k += kWG) {
+        int ar = 0;
+#pragma unroll
+        for (int j = 1; j < kArenas; j++) ar += k >= start[j] ? 1 : 0;
+        int off = start[0];
+#pragma unroll
+        for (int j = 1; j < kArenas; j++) off = ar == j ? start[j] : off;
+        ArenaLDS* A = base + ar;
+        CastJob& J = A->u.wc.job[k - off];
+        const WheelT& W = A->u.wt[J.wheel];
+        const int bi = J.body;
+        const v3 c = bi == 0 ? bpos(A, 0) : car_box_center(A, bi);
+        // one inlined cast for both shapes (the sphere radius or the box half extents select its support);
+        // the ray: the wheel's hard point to its contact point as first set (the target)
+        const bool ball = bi == 0;
+        float f = 0.f;
+        v3 n = zero3();
+        const bool hit = gjk::ray_convex_cast(W.hard_point, W.contact_point, ball ? C.ball_radius : 0.f,
+                                              ball ? zero3() : C.car_half, brot(A, bi), c, arith(A), f, n);
+        J.f = f;
+        J.nx = n.x;
+        J.ny = n.y;
+        J.nz = n.z;
+        J.hit = hit ? 1 : 0;
+    }
+}
+// second half: this ray's cast results in list order (kept when strictly closer and the normal is long
+// enough, none after a fraction-0 hit), then ClosestRayResultCallback's point and normal
+DEV int ray_cast_finish(ArenaLDS* A, v3 from, v3 to, int wheel, const WheelT& W, v3& hit_point, v3& hit_normal) {
+    float best = W.rc_best;
+    int obj = W.rc_obj;
+    v3 nrm = W.rc_nrm;
+    const int ar = arith(A);
+    const int nj = A->u.wc.njob;
+    for (int s = 0; s < nj; s++) {
+        const CastJob& J = A->u.wc.job[s];
+        if (J.wheel != wheel || best == 0.f) continue;
+        const v3 n = v3{J.nx, J.ny, J.nz};
+        if (!J.hit || !(len2(n) > 0.0001f) || !(J.f < best)) continue;
+        best = J.f;
+        obj = J.body;
+        nrm = bt_normalize(n, ar);  // castResult.m_normal.normalize()
     }
     if (obj < 0) return -1;
     hit_point = lerp3(from, to, best);  // ClosestRayResultCallback::addSingleResult
@@ -356,7 +407,8 @@ DEV int ray_cast(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int self, v3& h
 }
 
 // ------------------------------------------------------------------ vehicle, one wheel per lane
-// btVehicleRL::updateWheelTransform + rayCast (btVehicleRL.cpp:64-207)
+// btVehicleRL::updateWheelTransform + rayCast (btVehicleRL.cpp:64-207).  First half of the wheel phase (btVehicleRL::updateVehicle, btVehicleRL.cpp:64-190): the wheel's
+// transform and its ray against the static objects, cast jobs for the dynamic bodies
 DEV void wheel_phase(ArenaLDS* A, const MeshView& M, int ci, int i) {
     rlgpu_car& cs = A->s.cars[ci];
     WheelT& W = A->u.wt[ci * 4 + i];
@@ -379,8 +431,18 @@ DEV void wheel_phase(ArenaLDS* A, const MeshView& M, int ci, int i) {
     v3 target = source + W.wheel_dir * ray_len;
     W.contact_point = target;
     W.ground = -1;
+    ray_cast_static(A, M, source, target, bi, ci * 4 + i, W);
+}
+// Second half of the wheel phase (after wheel_casts): the ray's hit, suspension, friction impulses
+DEV void wheel_phase_b(ArenaLDS* A, int ci, int i) {
+    rlgpu_car& cs = A->s.cars[ci];
+    WheelT& W = A->u.wt[ci * 4 + i];
+    int bi = ci + 1;
+    m3 R = brot(A, bi);
+    v3 P = bpos(A, bi);
+    float rest = C.wheel_rest[i], radius = C.wheel_radius[i], travel = C.susp_travel;
     v3 hp, hn;
-    int obj = ray_cast(A, M, source, target, bi, hp, hn);
+    int obj = ray_cast_finish(A, W.hard_point, W.contact_point, ci * 4 + i, W, hp, hn);
     v3 upv = col(R, 2);
     if (obj >= 0) {
         W.contact_point = hp;

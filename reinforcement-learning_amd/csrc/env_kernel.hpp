@@ -96,7 +96,17 @@ struct WheelT {
     v3 hard_point, wheel_dir, contact_point, contact_normal, wt_col1, impulse;
     float susp_len, susp_rel_vel, clipped_inv;
     int ground, in_contact, contact_world;
+    v3 rc_nrm;     // the ray's closest static hit before the dynamic bodies' casts: normal,
+    float rc_best; // fraction (1: none)
+    int rc_obj;    // and object (-1: none)
 };
+// A wheel ray's convex cast against one dynamic body (ball / car), dealt over the workgroup's lanes
+// between the two halves of the wheel phase (wheel_casts)
+struct CastJob {
+    float f, nx, ny, nz;
+    uint8_t wheel, body, hit, pad_;
+};
+constexpr int kCastJobs = 16 * 4;  // 16 rays x (ball + 3 other cars)
 
 struct Cand {
     float n[3], p[3], depth;
@@ -174,6 +184,11 @@ struct Aux {
 
 union Scratch {
     WheelT wt[16];
+    struct {
+        WheelT wt_[16];  // = wt
+        CastJob job[kCastJobs];
+        int njob;
+    } wc;
     struct {
         v3 mn[5], mx[5];  // T4: the bodies' broadphase AABBs
         int cell[5];      //     and home cells + 1 (bp_home), one lane per body

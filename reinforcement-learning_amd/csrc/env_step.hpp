@@ -114,6 +114,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     if (valid) {  // per body / car on lanes 0-4: independent fields, read before the respawns below write
         rlgpu_arena_state& s = A->s;
         if (l == 0) {
+            A->u.wc.njob = 0;  // this tick's wheel-ray cast jobs
             bool sleep = len2(ld3(s.ball.vel)) == 0 && len2(ld3(s.ball.angvel)) == 0;  // Arena.cpp:722-727
             s.ball_sleeping = sleep;
             A->a.ball_sleep = sleep;
@@ -149,6 +150,10 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     sync();
     P.mark(0);
     if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase(A, M, l >> 2, l & 3);
+    sync();
+    wheel_casts(A - (threadIdx.x >> 4), nvalid);
+    sync();
+    if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase_b(A, l >> 2, l & 3);
     sync();
     P.mark(1);
     if (valid) {
