@@ -221,6 +221,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
             }
         }
     sync();
+    P.mark(22);
     narrow_queue(A - (threadIdx.x >> 4), nvalid, M);
     sync();
     P.mark(5);

@@ -12,9 +12,9 @@ from rlgpu import _lib  # noqa: E402
 from rlgpu.env import EnvSet  # noqa: E402
 
 NAMES = ["T0 sleep/demo/snapshot", "T1 wheels (16 lanes)", "T2 car logic + pads pre", "T3 gravity/predict",
-         "T4 ball awake", "T5 narrowphase", "T6 commit + solve (lane 0)", "T7 integrate", "T8 car post/finish",
+         "T4 ball awake", "T5 narrowphase (queue GJK)", "T6 commit + solve (lane 0)", "T7 integrate", "T8 car post/finish",
          "T9 pad collide", "T10 pad post + ball finish", "prelude / halves", "builders", "obs rows", "resets", "store", "T6 commit loop", "T6 commit sort",
-         "T5 deferred EPA (wave)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T6 solve writeback"]
+         "T5 deferred EPA (wave)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T5 narrow pairs (grid walks)"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 8  # env steps before profiling (late-episode states)
