@@ -107,11 +107,13 @@ MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_
                 mn[a] = std::fmin(mn[a], x);
                 mx[a] = std::fmax(mx[a], x);
             }
-    // cells of >= 128 uu (2.56 bullet units): a wheel ray touches one or two cells per axis, a car
-    // or ball two or three; a SOCCAR-density mesh (quarter pipes of 10 x 36 segments) lists ~10
-    // triangles in a cell it crosses
+    // cells of >= 160 uu (3.2 bullet units): a wheel ray touches one or two cells per axis, a car
+    // or ball two or three; a SOCCAR-density mesh (quarter pipes of 10 x 36 segments) lists ~15
+    // triangles in a cell it crosses.  Measured on the procedural SOCCAR mesh (env kernel per launch):
+    // 1.5 bt 1.071 ms, 2.56 bt 1.066, 3.2 bt 1.054-1.057, 4.0 bt 1.061, 5.12 bt 1.075
+    // (profiles/r04ad_env_ab.txt)
     float ext = std::fmax(mx[0] - mn[0], std::fmax(mx[1] - mn[1], mx[2] - mn[2]));
-    float cell = std::fmax(2.56f, ext / 128.f);
+    float cell = std::fmax(3.2f, ext / 128.f);
     g.inv_cell = 1.f / cell;
     g.ox = mn[0];
     g.oy = mn[1];
