@@ -39,21 +39,42 @@ def env_bytes_per_step(arena_state_size, append=True):
     return b
 
 
-def pmc_traffic(kernel_ms, arenas, mesh_name):
-    """HBM traffic of the env kernel from the committed rocprofv3 PMC passes (profiles/*_env_pmc.json,
-    made by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE runs of this bench at its
-    default ARENAS_PER_GPU arenas), as GB/s over the average launch duration measured here; None when
-    no summary is present or this run steps another arena count or mesh (the bytes were counted for that one)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_pmc.json")))
-    if not files or arenas != ARENAS_PER_GPU:
+# The env kernel's PMC summary of the committed HEAD (tools/pmc_summary.py over separate FETCH_SIZE /
+# WRITE_SIZE rocprofv3 passes of this bench, procedural mesh, ARENAS_PER_GPU arenas).  Named explicitly and
+# updated with every re-measurement -- never picked by file-name order.
+ENV_PMC_FILE = "profiles/r05_env_pmc.json"
+
+
+def pmc_traffic(kernel_ms, arenas, mesh_name, pmc_file):
+    """HBM traffic of the env kernel from the named PMC summary, as GB/s over the average launch
+    duration measured here; None when the file is absent or this run steps another arena count or mesh
+    (the bytes were counted for that one)."""
+    path = os.path.join(ROOT, pmc_file)
+    if arenas != ARENAS_PER_GPU or not os.path.exists(path):
         return None, None
-    files = [f for f in files if json.load(open(f)).get("mesh", "synthetic") == mesh_name]
-    if not files:
+    d = json.load(open(path))
+    if d.get("mesh", "synthetic") != mesh_name:
         return None, None
-    d = json.load(open(files[-1]))
     b = d["hbm_bytes_per_launch"]
-    return b / (kernel_ms * 1e-3) / 1e9, {"bytes_per_launch": b, "source": os.path.relpath(files[-1], ROOT)}
+    src = {"bytes_per_launch": b, "source": pmc_file, "fetch_bytes_per_launch": 2 * d["fetch_size_kb_raw"] * 1024,
+           "write_bytes_per_launch": d["write_size_kb"] * 1024}
+    if d.get("kernel_us_rocprof"):  # the same profiling session's own kernel duration
+        src["pmc_kernel_us"] = d["kernel_us_rocprof"]
+        src["traffic_at_pmc_kernel_us"] = b / (d["kernel_us_rocprof"] * 1e-6) / 1e9
+    return b / (kernel_ms * 1e-3) / 1e9, src
+
+
+def cpu_cores():
+    """The host cores this process may actually use: its affinity set, capped by the cgroup CPU quota
+    (gpurun boxes show the whole machine in os.cpu_count() but grant a share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_model():
@@ -72,7 +93,7 @@ def cpu_baseline(mesh=None, mesh_name="synthetic", seconds=12.0, arenas=1024):
     own arena mesh, whose objects the oracle queries through their BVHs as Bullet does."""
     import numpy as np
     import oracle
-    cores = min(16, os.cpu_count() or 1)  # the box's CPU share is 16 (gpurun)
+    cores = cpu_cores()
     env = oracle.EnvSet(arenas, seed=1234, threads=cores, mesh=mesh)
     rng = np.random.default_rng(7)
     steps = 0
@@ -86,7 +107,7 @@ def cpu_baseline(mesh=None, mesh_name="synthetic", seconds=12.0, arenas=1024):
         if el >= seconds:
             break
     out = {"value": arenas * steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
-           "cpu_model": cpu_model(),
+           "cpu_model": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
            "sample": f"env only: {arenas} arenas x {steps} env steps of the oracle/ CPU restatement "
                      f"({cores} threads, uniform valid actions, the reference's x86 (MSVC x64) arithmetic, "
                      f"the bench's {mesh_name} mesh walked through each object's BVH)"}
@@ -240,6 +261,8 @@ def main():
     ap.add_argument("--arenas", type=int, default=ARENAS_PER_GPU)
     ap.add_argument("--rollout", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-file", default=ENV_PMC_FILE,
+                    help="the env kernel's PMC summary (tools/pmc_summary.py) that roofline.traffic comes from")
     ap.add_argument("--no-legs", action="store_true", help="skip the C5 and exact-GEMM (x6) legs")
     ap.add_argument("--mesh", choices=("procedural", "synthetic"), default="procedural",
                     help="arena collision mesh: the SOCCAR-sized procedural stand-in (16 objects, 8,800 triangles: "
@@ -314,7 +337,7 @@ def main():
     kern_ms = sum(kern) / len(kern)
     b_env = env_bytes_per_step(arena_state_size())
     achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kern_ms, args.arenas, args.mesh)
+    traffic, traffic_src = pmc_traffic(kern_ms, args.arenas, args.mesh, args.pmc_file)
     out = {
         "metric": "env-steps/sec (whole node) at 32768 arenas; PPO wall-clock per 1M steps",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -328,6 +351,8 @@ def main():
                    "arenas_per_gpu": args.arenas, "agents_per_gpu": 4 * args.arenas, "rollout_len": cfg.rollout_len,
                    "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32",
                    "train_gemm": args.train_gemm, "arith": args.arith,
+                   "self_play": "off (trainAgainstOldVersions = false: every timed iteration does the same work; "
+                                "the old-version path is tested in tests/test_learner_gpu.py)",
                    "mesh": (f"procedural SOCCAR stand-in: {mesh.num_objects} objects, {mesh.num_tris} triangles "
                             "(quarter pipes, rounded corners, goal boxes; floor / walls / ceiling are static planes)"
                             if mesh is not None else "synthetic arena: 1 object, 36 triangles (include/rlgpu_arena_mesh.h)")},

@@ -55,7 +55,9 @@ extern "C" {
 enum {
     RLGPU_RW_AIR = 0,                     /* AirReward */
     RLGPU_RW_WAVEDASH = 1,                /* WavedashReward */
-    RLGPU_RW_KICKOFF_PROXIMITY_2V2 = 2,   /* KickoffProximityReward2v2Enhanced */
+    RLGPU_RW_KICKOFF_PROXIMITY_2V2 = 2,   /* KickoffProximityReward2v2Enhanced: params[2] != 0 -> params[0] goerReward,
+                                             params[1] rotationPrepWeight (else the class defaults 1.2 / 0.2;
+                                             cheaterReward / dynamicWeight are never read by its GetReward) */
     RLGPU_RW_VELOCITY_PLAYER_TO_BALL = 3, /* VelocityPlayerToBallReward */
     RLGPU_RW_STRONG_TOUCH = 4,            /* StrongTouchReward(params[0] minSpeedKPH, params[1] maxSpeedKPH) */
     RLGPU_RW_TOUCH_ACCEL = 5,             /* TouchAccelReward */

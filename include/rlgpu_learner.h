@@ -213,6 +213,20 @@ int rlgpu_learner_finish_iteration(rlgpu_learner* h);
  * rlgpu_ppo_set_version (its rows are simulated but not trained or counted); -1 = off. */
 int rlgpu_learner_set_old_team(rlgpu_learner* h, int32_t team);
 
+/* Host plugins and a StepCallbackFn inside the collection loop (Learner.cpp:676-861; EnvSet.cpp:163-255).
+ * With a hook set, every collection step runs: the env step WITHOUT resetting terminated arenas, then
+ * fn(user, RLGPU_HOOK_AFTER_STEP) -- the env set (rlgpu_learner_handles) holds the post-step, pre-reset state;
+ * the hook may download GameStates, run user plugins and rewrite the env's rewards [players] / terminals
+ * [arenas] buffers (device, rlgpu_envset_buffers) -- then the trajectory codes (the merged terminal, else the
+ * max-episode-length truncation), rewards and truncation rows are appended, every arena whose terminal is
+ * set is reset (rlgpu_envset_reset), fn(user, RLGPU_HOOK_AFTER_RESET) runs (the plugins' Reset on the new
+ * states), and the post-reset obs / masks are appended.  fn returns 0, else the iteration fails with
+ * RLGPU_ERR_STATE.  fn == NULL restores the fused step.  Without host changes the two paths are
+ * bit-identical. */
+enum { RLGPU_HOOK_AFTER_STEP = 0, RLGPU_HOOK_AFTER_RESET = 1 };
+typedef int (*rlgpu_step_hook_fn)(void* user, int32_t phase);
+int rlgpu_learner_set_step_hook(rlgpu_learner* h, rlgpu_step_hook_fn fn, void* user);
+
 int rlgpu_learner_get_stats(rlgpu_learner* h, rlgpu_learner_stats* out);
 int rlgpu_learner_set_stats(rlgpu_learner* h, const rlgpu_learner_stats* in);
 /* PPO report metrics accumulated since the last reset (PPOLearner.cpp:537-566): h_out receives

@@ -209,7 +209,8 @@ struct KickoffReward {
     static V blue_back() { return V(0, -6000, 642.775f / 2); }
     static V orange_back() { return V(0, 6000, 642.775f / 2); }
     static float clampf(float v, float lo, float hi) { return std::min(std::max(v, lo), hi); }
-    static float reward(int pi, const PlayerView* P, V bpos, V bvel) {
+    // goer = goerReward (KickoffProximityReward2v2Enhanced.h:9,135), rpw = rotationPrepWeight (:12,175)
+    static float reward(int pi, const PlayerView* P, V bpos, V bvel, float goer, float rpw) {
         // IsKickoffActive
         float bspeed = rs_len(bvel);
         V b2(bpos.x, bpos.y, 0.f);
@@ -257,7 +258,7 @@ struct KickoffReward {
         float spawn = (adiff > (3.14159f / 3.f)) ? 1.f : 0.f;
         float total = dscore + sscore + bscore + spawn * 0.1f;
         if (total >= 0.5f) {  // GOER
-            float base = (pdist < an.closest_opp) ? 1.2f : -1.2f * 0.5f;
+            float base = (pdist < an.closest_opp) ? goer : -goer * 0.5f;
             V to_b = rs_norm(bpos - pl.pos);
             float pvel = dot(pl.vel, to_b);
             float speed_bonus = clampf(pvel / 2300.f, -0.3f, 0.3f);
@@ -344,7 +345,7 @@ struct KickoffReward {
             float ready = 1.f - clampf(dts / 1000.f, 0.f, 1.f);
             V tos = rs_norm(sup - pl.pos);
             float align = std::max(0.f, dot(rs_norm(pl.vel), tos));
-            rot = (ready * 0.7f + align * 0.3f) * 0.2f;
+            rot = (ready * 0.7f + align * 0.3f) * rpw;
         }
         float aware;
         {
@@ -423,7 +424,9 @@ static float reward_of(const rlgpu_reward_spec& rs, int i, const PlayerView* P, 
     switch (rs.type) {
         case RLGPU_RW_AIR: return !pl.on_ground;
         case RLGPU_RW_WAVEDASH: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1 : 0;
-        case RLGPU_RW_KICKOFF_PROXIMITY_2V2: return KickoffReward::reward(i, P, bpos, bvel);
+        case RLGPU_RW_KICKOFF_PROXIMITY_2V2:
+            return KickoffReward::reward(i, P, bpos, bvel, rs.params[2] != 0.f ? rs.params[0] : 1.2f,
+                                         rs.params[2] != 0.f ? rs.params[1] : 0.2f);
         case RLGPU_RW_VELOCITY_PLAYER_TO_BALL: {
             V dir = rs_norm(bpos - pl.pos);
             V nv = rs_div(pl.vel, 2300.f);

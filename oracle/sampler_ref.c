@@ -24,6 +24,9 @@
 #define NL 64
 static const float kMinProb = 1e-11f, kDisabled = -1e10f;
 
+/* the sampler's key: the step's high 32 bits folded into the seed (ppo_kernels.hpp sample_key) */
+static uint64_t sample_key(uint64_t seed, uint64_t step) { return seed ^ ((step >> 32) * 0x9E3779B97F4A7C15ull); }
+
 static uint32_t philox(uint64_t key, uint32_t c0, uint32_t c1) {
     uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
     uint32_t x0 = c0, x1 = c1, x2 = 0x2545F491u, x3 = 0x4F6CDD1Du;
@@ -102,7 +105,7 @@ void oracle_sample_actions(const uint16_t* logits, const uint8_t* masks, int64_t
                 }
             }
         } else {  /* PPOLearner.cpp:157-173 */
-            const float r = (float)(philox(seed, (uint32_t)(row0 + row), (uint32_t)step) >> 8) * (1.f / 16777216.f);
+            const float r = (float)(philox(sample_key(seed, step), (uint32_t)(row0 + row), (uint32_t)step) >> 8) * (1.f / 16777216.f);
             float running = 0.f;
             pick = A - 1;
             for (int j = 0; j < A; j++) {
@@ -147,7 +150,7 @@ void oracle_sampler_probs(const uint16_t* logits, const uint8_t* masks, int64_t 
             const float e = (a & 1) ? z1[a >> 1] : z0[a >> 1];
             probs[row * A + a] = fminf(fmaxf(e / s, kMinProb), 1.f);
         }
-        r[row] = (float)(philox(seed, (uint32_t)(row0 + row), (uint32_t)step) >> 8) * (1.f / 16777216.f);
+        r[row] = (float)(philox(sample_key(seed, step), (uint32_t)(row0 + row), (uint32_t)step) >> 8) * (1.f / 16777216.f);
     }
 }
 

@@ -112,8 +112,9 @@ DEV void build_obs_row(ArenaLDS* A, int pi, int part) {
     }
 }
 
-// KickoffProximityReward2v2Enhanced (KickoffProximityReward2v2Enhanced.h:14-366)
-DEV float kickoff_reward(ArenaLDS* A, int pi, const PView& pl, v3 bpos, v3 bvel) {
+// KickoffProximityReward2v2Enhanced (KickoffProximityReward2v2Enhanced.h:14-366).  goer = goerReward (:9, used at
+// :135), rpw = rotationPrepWeight (:12, used at :175); cheaterReward / dynamicWeight are never read by GetReward.
+DEV float kickoff_reward(ArenaLDS* A, int pi, const PView& pl, v3 bpos, v3 bvel, float goer, float rpw) {
     float bspeed = rs_len(bvel);
     v3 b2 = v3{bpos.x, bpos.y, 0.f};
     if (!(bspeed < 2.f && bpos.z < 150.f && rs_len(b2) < 50.f)) return 0.f;
@@ -157,7 +158,7 @@ DEV float kickoff_reward(ArenaLDS* A, int pi, const PView& pl, v3 bpos, v3 bvel)
     float spawn = (adiff > (3.14159f / 3.f)) ? 1.f : 0.f;
     float total = dscore + sscore + bscore + spawn * 0.1f;
     if (total >= 0.5f) {
-        float base = (pdist < closest) ? 1.2f : -1.2f * 0.5f;
+        float base = (pdist < closest) ? goer : -goer * 0.5f;
         v3 to_b = rs_norm(bpos - pl.pos);
         float pvel = dot(pl.vel, to_b);
         float speed_bonus = clampf(pvel / 2300.f, -0.3f, 0.3f);
@@ -227,7 +228,7 @@ DEV float kickoff_reward(ArenaLDS* A, int pi, const PView& pl, v3 bpos, v3 bvel)
         float ready = 1.f - clampf(dts / 1000.f, 0.f, 1.f);
         v3 tos = rs_norm(sup - pl.pos);
         float align = stdmax(0.f, dot(rs_norm(pl.vel), tos));
-        rot = (ready * 0.7f + align * 0.3f) * 0.2f;
+        rot = (ready * 0.7f + align * 0.3f) * rpw;
     }
     float aware;
     {
@@ -270,7 +271,9 @@ DEV float reward_value(ArenaLDS* A, const rlgpu_reward_spec& rs, int i, const PV
     switch (rs.type) {
         case RLGPU_RW_AIR: return !pl.on_ground;
         case RLGPU_RW_WAVEDASH: return (pl.on_ground && (e.prev_is_flipping[i] && !e.prev_on_ground[i])) ? 1.f : 0.f;
-        case RLGPU_RW_KICKOFF_PROXIMITY_2V2: return kickoff_reward(A, i, pl, bpos, bvel);
+        case RLGPU_RW_KICKOFF_PROXIMITY_2V2:  // params[2] != 0: params[0..1] hold the tunables, else the defaults
+            return kickoff_reward(A, i, pl, bpos, bvel, rs.params[2] != 0.f ? rs.params[0] : 1.2f,
+                                  rs.params[2] != 0.f ? rs.params[1] : 0.2f);
         case RLGPU_RW_VELOCITY_PLAYER_TO_BALL: {
             v3 dir = rs_norm(bpos - pl.pos);
             v3 nv = rs_div(pl.vel, 2300.f);

@@ -126,6 +126,27 @@ __global__ void k_stack_frames(const float* cur, const float* trunc, const int8_
     }
 }
 
+// After a step hook (host plugins, Learner.cpp:780-861): one thread per (player, obs column).  The
+// player's code becomes the arena's merged terminal (the hook's NORMAL-over-TRUNCATED merge of device and
+// host conditions) or, where that is 0, the device's own code (the max-episode-length truncation); column 0
+// also takes the step's (host-rebuilt) reward.  A code-2 row's pre-reset obs goes to the truncation rows.
+__global__ void k_host_step_finish(const uint8_t* arena_terms, int8_t* codes, const float* rewards, float* rew_out,
+                                   const float* obs, float* trunc_env, float* trunc_out, int P, int obs_w) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)P * obs_w) return;
+    const int p = (int)(e / obs_w), c = (int)(e % obs_w);
+    const int m = arena_terms[p / 4];
+    const int code = m ? m : codes[p];
+    if (code == 2) {
+        trunc_env[e] = obs[e];
+        if (trunc_out) trunc_out[e] = obs[e];
+    }
+    if (c == 0) {  // idempotent: a thread of the row that reads codes[p] after this write computes the same code
+        codes[p] = (int8_t)code;
+        if (rew_out) rew_out[p] = rewards[p];
+    }
+}
+
 // one workgroup walks the players in chunks of 1024: block-wide exclusive scans of the end /
 // truncation flags give each ending trajectory its record slot, truncation slot and combined offset in
 // (player) order after the records of earlier steps
@@ -291,6 +312,14 @@ void stack_frames(const float* cur, const float* trunc, const int8_t* codes, flo
     const int64_t n = (int64_t)P * obs;
     hipLaunchKernelGGL(k_stack_frames, dim3(ceil_div(n, 256)), dim3(256), 0, s, cur, trunc, codes, hist, K, P, obs, out,
                        out_trunc);
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+void host_step_finish(const uint8_t* arena_terms, int8_t* codes, const float* rewards, float* rew_out, const float* obs,
+                      float* trunc_env, float* trunc_out, int P, int obs_w, hipStream_t s) {
+    const int64_t n = (int64_t)P * obs_w;
+    hipLaunchKernelGGL(k_host_step_finish, dim3(ceil_div(n, 256)), dim3(256), 0, s, arena_terms, codes, rewards, rew_out,
+                       obs, trunc_env, trunc_out, P, obs_w);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 

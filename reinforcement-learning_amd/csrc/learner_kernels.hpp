@@ -32,6 +32,12 @@ void select_trunc(const int8_t* terms, int64_t n, void* scratch, size_t scratch_
 void stack_frames(const float* cur, const float* trunc, const int8_t* codes, float* hist, int K, int P, int obs,
                   float* out, float* out_trunc, hipStream_t s);
 
+// After a step hook (host plugins / StepCallbackFn): codes[p] = arena_terms[p / 4] (the merged terminal) or,
+// where 0, the device's code; rew_out[p] = rewards[p] (rew_out may be null); the pre-reset obs rows of code-2
+// players (obs [P][obs_w]) to trunc_env and trunc_out (may be null)
+void host_step_finish(const uint8_t* arena_terms, int8_t* codes, const float* rewards, float* rew_out, const float* obs,
+                      float* trunc_env, float* trunc_out, int P, int obs_w, hipStream_t s);
+
 // ---- reference experience mode (complete trajectories with carry-over, Learner.cpp:504-547,823-861)
 // Trajectory records, structure of arrays (capacity rows each), appended in the reference's order:
 // by the step a trajectory ends, then by player index (combinedTraj.Append in the newPlayerIndices loop).

@@ -19,6 +19,13 @@ constexpr float kMinProb = 1e-11f;        // ACTION_MIN_PROB
 constexpr float kDisabledLogit = -1e10f;  // ACTION_DISABLED_LOGIT
 constexpr int kMaxA = 128;                // actions per row: 2 per lane
 
+// The sampler's Philox key for a draw step: the seed, with the step's high 32 bits folded in (the counter carries its
+// low 32), so streams on separate step ranges -- the skill matches' 2^40 + k (rlgpu/skill.py) against the rollout's
+// k -- never share uniforms; steps below 2^32 keep key = seed.
+__host__ __device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint64_t step) {
+    return seed ^ ((step >> 32) * 0x9E3779B97F4A7C15ull);
+}
+
 __device__ __forceinline__ uint32_t philox(uint64_t key, uint32_t c0, uint32_t c1) {
     uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
     uint32_t x0 = c0, x1 = c1, x2 = 0x2545F491u, x3 = 0x4F6CDD1Du;
@@ -136,7 +143,8 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
                     p = pr[g];
                     rw = row[g];
                 }
-            const float r = (float)(philox(seed, (uint32_t)(row0 + rw), (uint32_t)step) >> 8) * (1.f / 16777216.f);
+            const float r = (float)(philox(sample_key(seed, step), (uint32_t)(row0 + rw), (uint32_t)step) >> 8) *
+                            (1.f / 16777216.f);
             float running = 0.f;
             bool found = false;
             for (int j = 0; j < A; j++) {

@@ -111,11 +111,14 @@ inline bool RegistryReward(Reward* r, rlgpu_reward_spec& s) {
     else if (Is<WavedashReward>(r, t)) s.type = RLGPU_RW_WAVEDASH;
     else if (Is<KickoffProximityReward2v2Enhanced>(r, t)) {
         auto* k = static_cast<KickoffProximityReward2v2Enhanced*>(r);
-        // the kernel holds the class's default tunables (RG/Rewards/KickoffProximityReward2v2Enhanced.h:8-11)
-        if (k->goerReward != 1.2f || k->cheaterReward != 0.6f || k->dynamicWeight != 0.3f || k->rotationPrepWeight != 0.2f)
-            throw std::invalid_argument("KickoffProximityReward2v2Enhanced: only the default goerReward / cheaterReward / "
-                                        "dynamicWeight / rotationPrepWeight are in the device registry");
+        // the tunables GetReward reads (KickoffProximityReward2v2Enhanced.h:9,12,135,175); cheaterReward and
+        // dynamicWeight are declared but never read by it
         s.type = RLGPU_RW_KICKOFF_PROXIMITY_2V2;
+        if (k->goerReward != 1.2f || k->rotationPrepWeight != 0.2f) {  // defaults stay the registry's zero params
+            s.params[0] = k->goerReward;
+            s.params[1] = k->rotationPrepWeight;
+            s.params[2] = 1.f;
+        }
     } else if (Is<VelocityPlayerToBallReward>(r, t)) s.type = RLGPU_RW_VELOCITY_PLAYER_TO_BALL;
     else if (Is<StrongTouchReward>(r, t)) {
         auto* st = static_cast<StrongTouchReward*>(r);

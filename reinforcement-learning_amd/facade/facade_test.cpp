@@ -189,20 +189,25 @@ static int Translate() {
         CHECK(q.hostNames.size() == 5, "names");
         FreeResult(r);
     }
-    // refused: registry fields it cannot hold, foreign builders, differing arenas
+    // KickoffProximityReward2v2Enhanced's tunables are device parameters (goerReward, rotationPrepWeight)
     {
         EnvCreateResult r;
         auto* k = new KickoffProximityReward2v2Enhanced();
         k->goerReward = 2.f;
-        r.rewards = {{k, 1.f}};
-        bool threw = false;
-        try {
-            TranslatePlugins(r);
-        } catch (const std::invalid_argument&) {
-            threw = true;
+        k->rotationPrepWeight = 0.35f;
+        r.rewards = {{k, 1.f}, {new KickoffProximityReward2v2Enhanced(), 2.f}};
+        PluginPlan q = TranslatePlugins(r);
+        CHECK(!q.HasHost() && q.deviceRewards.size() == 2, "kickoff tunables");
+        if (q.deviceRewards.size() == 2) {
+            CHECK(q.deviceRewards[0].params[0] == 2.f && q.deviceRewards[0].params[1] == 0.35f &&
+                      q.deviceRewards[0].params[2] == 1.f, "kickoff tunables in params");
+            CHECK(q.deviceRewards[1].params[2] == 0.f, "default kickoff tunables are the registry's zero params");
         }
-        CHECK(threw, "non-default kickoff tunables accepted");
         FreeResult(r);
+    }
+    // refused: foreign builders, differing arenas
+    {
+        bool threw = false;
         EnvCreateResult o;
         o.obsBuilder = new MyObs();
         threw = false;

@@ -393,12 +393,41 @@ void Learner::Collect() {
         rlgpu_step_outputs o{K_ > 1 ? nullptr : v.obs + (r + P) * OBS, v.masks + (r + P) * ACT, v.rewards + r,
                              v.terms + r, K_ > 1 ? nullptr : v.trunc_obs + r * OBS};
         if (envTiming_) hipCheck(hipEventRecord(ev_[2 * t], s_), "event");
-        env_->Step(v.actions + r, &o);
+        StepEnv(v.actions + r, o);
         if (envTiming_) hipCheck(hipEventRecord(ev_[2 * t + 1], s_), "event");
         if (K_ > 1)
             lk::stack_frames(st.obs, st.trunc_obs, v.terms + r, hist_, K_, P, OBS, v.obs + (r + P) * W, v.trunc_obs + r * W,
                              s_);
     }
+}
+
+// One env step with the experience append.  Without a hook: the fused kernel (step, reset of terminated
+// arenas, append).  With one (host plugins / a StepCallbackFn): the step without its reset, then the hook
+// (phase 0: the post-step GameStates; it may rewrite the env's rewards / terminals -- EnvSet::StepSecondHalf's
+// host plugins and Learner.cpp:796-797's callback), the merged codes / rewards / truncation rows, the reset of
+// the arenas whose merged terminal is set (EnvSet::Reset at the next step's start, Learner.cpp:676), the
+// hook's phase 1 (the plugins' Reset on the new states), then the post-reset obs / masks appended.  With no
+// host change this is bit-identical to the fused step (same kickoff draws, same builders).
+void Learner::StepEnv(const int32_t* d_actions, const rlgpu_step_outputs& o) {
+    if (!hook_) {
+        env_->Step(d_actions, &o);
+        return;
+    }
+    rlgpu_envset* e = env_->handle();
+    const rlgpu_envset_buffers& st = env_->state();
+    const int P = st.num_players;
+    rlgpu_step_outputs pre{nullptr, nullptr, nullptr, o.terminals, nullptr};
+    RlgpuCheck(rlgpu_envset_step(e, d_actions, 0, &pre, s_), "EnvSet step (hooked)");
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    if (hook_(hookUser_, RLGPU_HOOK_AFTER_STEP) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, std::string("Learner: step hook failed: ") + rlgpu_last_error());
+    lk::host_step_finish(st.terminals, o.terminals, st.rewards, o.rewards, st.obs, st.trunc_obs, o.trunc_obs, P, OBS, s_);
+    RlgpuCheck(rlgpu_envset_reset(e, s_), "EnvSet reset (hooked)");
+    hipCheck(hipStreamSynchronize(s_), "sync");
+    if (hook_(hookUser_, RLGPU_HOOK_AFTER_RESET) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, std::string("Learner: step hook failed: ") + rlgpu_last_error());
+    if (o.obs) hipCheck(hipMemcpyAsync(o.obs, st.obs, (size_t)P * OBS * 4, hipMemcpyDeviceToDevice, s_), "obs append");
+    if (o.masks) hipCheck(hipMemcpyAsync(o.masks, st.action_masks, (size_t)P * ACT, hipMemcpyDeviceToDevice, s_), "mask append");
 }
 
 void Learner::Consume() {
@@ -681,7 +710,7 @@ void Learner::CollectTrajectories() {
         stats.rng_step++;
         rlgpu_step_outputs o{K_ > 1 ? nullptr : v.obs + rown * OBS, v.masks + rown * ACT, v.rewards + row, v.terms + row,
                              nullptr};
-        env_->Step(v.actions + row, &o);
+        StepEnv(v.actions + row, o);
         if (K_ > 1)
             lk::stack_frames(st.obs, st.trunc_obs, v.terms + row, hist_, K_, P, OBS, v.obs + rown * W, J.truncStage, s_);
         lk::TrajRecs R{J.rp.p, J.rstart.p, J.rlen.p, J.rcode.p, J.rtidx.p, J.roff.p};
@@ -978,6 +1007,13 @@ extern "C" int rlgpu_moments_mean_std(const double* m3, float* out2) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(m3 && out2 && m3[2] > 1, "rlgpu_moments_mean_std: bad argument");
         GGL::MomentsMeanStd(m3, out2);
+    });
+}
+
+extern "C" int rlgpu_learner_set_step_hook(rlgpu_learner* h, rlgpu_step_hook_fn fn, void* user) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->SetStepHook(fn, user);
     });
 }
 

@@ -171,6 +171,10 @@ public:
     void Start(int64_t iterations);  // Learner::Start loop (Learner.cpp:482-1056), a fixed count
 
     void SetOldTeam(int team) { oldTeam_ = team; }
+    void SetStepHook(rlgpu_step_hook_fn fn, void* user) {
+        hook_ = fn;
+        hookUser_ = user;
+    }
     void SetEnvTiming(bool on) { envTiming_ = on; }
 
     const rlgpu_learner_config& config() const { return cfg_; }
@@ -181,6 +185,7 @@ public:
     WelfordStat returnStat;
 
 private:
+    void StepEnv(const int32_t* d_actions, const rlgpu_step_outputs& o);
     void AllReduceGrads();
     void BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int64_t n);
     void CollectTrajectories();
@@ -196,6 +201,8 @@ private:
     ExperienceBuffer exp_;
     int oldTeam_ = -1;
     bool envTiming_ = false;
+    rlgpu_step_hook_fn hook_ = nullptr;  // host plugins / StepCallbackFn (rlgpu_learner_set_step_hook)
+    void* hookUser_ = nullptr;
     int K_ = 1;                 // frames stacked (config C4)
     float* hist_ = nullptr;     // [K-1][P][OBS] frame history
     std::vector<hipEvent_t> ev_;

@@ -49,8 +49,22 @@ class UnknownPlugin(KeyError):
     pass
 
 
-def reward(name, weight, *params):
-    """WeightedReward{new <name>(*params), weight}."""
+# KickoffProximityReward2v2Enhanced's public tunables (KickoffProximityReward2v2Enhanced.h:9-12): the two its
+# GetReward reads (:135, :175) are device parameters; cheaterReward / dynamicWeight are never read
+KICKOFF_TUNABLES = {"goer_reward": 1.2, "rotation_prep_weight": 0.2}
+
+
+def reward(name, weight, *params, **tunables):
+    """WeightedReward{new <name>(*params), weight}.  KickoffProximityReward2v2Enhanced also takes the keyword
+    tunables goer_reward / rotation_prep_weight (its member fields; defaults 1.2 / 0.2)."""
+    if tunables:
+        if name != "KickoffProximityReward2v2Enhanced" or set(tunables) - set(KICKOFF_TUNABLES):
+            raise TypeError(f"{name} takes no keyword tunables {sorted(tunables)}")
+        t = dict(KICKOFF_TUNABLES, **tunables)
+        r = reward(name, weight)
+        if (np.float32(t["goer_reward"]), np.float32(t["rotation_prep_weight"])) != (np.float32(1.2), np.float32(0.2)):
+            r["params"][:] = (t["goer_reward"], t["rotation_prep_weight"], 1.0)
+        return r
     if name not in REWARDS:
         raise UnknownPlugin(f"reward class {name!r} has no device implementation (registry: {sorted(REWARDS)})")
     rid, defaults = REWARDS[name]

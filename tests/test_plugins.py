@@ -88,7 +88,18 @@ CUSTOM_REWARDS = [
     plugins.reward("BumpReward", 9.0),
     plugins.reward("DemoReward", 12.0),
     plugins.reward("AirReward", -0.05),  # a type twice
+    # its member tunables (KickoffProximityReward2v2Enhanced.h:9-12) as device parameters
+    plugins.reward("KickoffProximityReward2v2Enhanced", 2.5, goer_reward=1.7, rotation_prep_weight=0.35),
 ]
+
+
+def test_kickoff_tunables_spec():
+    r = plugins.reward("KickoffProximityReward2v2Enhanced", 2.5, goer_reward=1.7, rotation_prep_weight=0.35)
+    assert list(r["params"]) == [np.float32(1.7), np.float32(0.35), 1.0]
+    d = plugins.reward("KickoffProximityReward2v2Enhanced", 2.5, goer_reward=1.2)  # the defaults: registry zeros
+    assert list(d["params"]) == [0.0, 0.0, 0.0]
+    with pytest.raises(TypeError):
+        plugins.reward("AirReward", 1.0, goer_reward=1.0)
 CUSTOM_TERMINALS = [plugins.terminal("NoTouchCondition", 2.5), plugins.terminal("GoalScoreCondition"),
                     plugins.terminal("ScoreLimitCondition", 2), plugins.terminal("NoTouchCondition", 4.0)]
 

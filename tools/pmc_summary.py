@@ -2,6 +2,10 @@
 MI355X_MICROARCH.md prescribes) into per-launch HBM bytes for one kernel.
 
 usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel substring> <min grid threads> <out.json> [mesh]
+                                  [kernel_stats.csv] [round tag]
+
+The optional kernel-stats CSV (rocprofv3 --kernel-trace --stats of the same bench command) adds the kernel's
+average duration (kernel_us_rocprof), so bench.py can report the traffic at the profiler's own kernel time.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
 coalesced streaming reads -> doubled; WRITE_SIZE is taken as is.  Both counters are in KB.
@@ -20,6 +24,8 @@ def per_launch(path, kernel, min_grid):
 def main():
     fdir, wdir, kernel, min_grid, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
     mesh = sys.argv[6] if len(sys.argv) > 6 else "synthetic"
+    stats = sys.argv[7] if len(sys.argv) > 7 else None
+    tag = sys.argv[8] if len(sys.argv) > 8 else None
     nf, fetch_kb = per_launch(f"{fdir}/run_counter_collection.csv", kernel, min_grid)
     nw, write_kb = per_launch(f"{wdir}/run_counter_collection.csv", kernel, min_grid)
     res = {"kernel": kernel, "launches": [nf, nw], "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
@@ -27,6 +33,14 @@ def main():
            "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1; KB = 1024 B", "mesh": mesh,
            "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --output-format csv -- python3 bench.py --steps 1 "
                       f"--warmup 0 --no-cpu-baseline --mesh {mesh} (two separate passes)"}
+    if stats:
+        for r in csv.DictReader(open(stats)):
+            if kernel in r["Name"]:
+                res["kernel_us_rocprof"] = float(r["AverageNs"]) / 1e3
+                res["kernel_stats_source"] = stats
+                break
+    if tag:
+        res["round"] = tag
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
