@@ -98,7 +98,15 @@ typedef struct {
                                       the store would overwrite a live step (documented divergence). */
     int32_t arith;                 /* rlgpu_envset_config.arith: the reference build's Bullet arithmetic
                                       (include/rlgpu_arith.h; 0 = build.ps1's MSVC x64) */
+    int32_t activation;            /* PartialModelConfig::activationType of every model: RLGPU_ACT_LEAKY_RELU (0,
+                                      torch::nn::LeakyReLU, slope 0.01) or RLGPU_ACT_RELU */
+    int32_t optimizer;             /* PartialModelConfig::optimType of every model (Models.h:40-56):
+                                      RLGPU_OPT_ADAMW (0, libtorch AdamW: weight decay 1e-2) or RLGPU_OPT_ADAM
+                                      (libtorch Adam: no weight decay) */
 } rlgpu_learner_config;
+
+enum { RLGPU_ACT_LEAKY_RELU = 0, RLGPU_ACT_RELU = 1 };
+enum { RLGPU_OPT_ADAMW = 0, RLGPU_OPT_ADAM = 1 };
 
 enum { RLGPU_EXP_ROLLOUT = 0, RLGPU_EXP_TRAJECTORIES = 1 };
 
@@ -254,6 +262,12 @@ int rlgpu_moments_mean_std(const double* moments3, float* out2);
 /* The return-sample indices of one iteration: n draws in [0, range) from a counter-based
  * generator keyed by (seed, rank, iteration) -- every language binding reproduces the same draws. */
 int rlgpu_sample_indices(uint64_t seed, int32_t rank, int64_t iteration, int64_t range, int32_t n, int64_t* out);
+/* The host picks of self-play and the skill matches (RocketSim::Math::RandFloat / RandInt in the reference:
+ * Learner.cpp:589-600, PolicyVersionManager.cpp:181-186): a counter-based uniform in [0, 1) of (seed, stream,
+ * counter), so every binding (the C++ trainer facade, Python) makes the same picks.  Streams in use: 1 = the
+ * self-play draw of iteration i at counters 3 i .. 3 i + 2 (old-version chance, version, team); 2 = skill run r
+ * at 2 r, 2 r + 1 (version, new team). */
+double rlgpu_host_uniform(uint64_t seed, uint64_t stream, uint64_t counter);
 /* The return-sample rows of one iteration, drawn only from steps of FINISHED trajectories -- the
  * reference samples tReturns of combinedTraj, which holds complete trajectories only
  * (Learner.cpp:823-861, 959-967).  ends[p] = the last step t of column p whose trajectory code is

@@ -138,9 +138,11 @@ inline bool RegistryReward(Reward* r, rlgpu_reward_spec& s) {
     else if (Is<GoalReward>(r, t)) {
         s.type = RLGPU_RW_GOAL;
         s.params[0] = static_cast<GoalReward*>(r)->concedeScale;
+#ifndef RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES  // else ExampleMain's own class: a host plugin
     } else if (Is<LosingPenaltyReward>(r, t)) {
         s.type = RLGPU_RW_LOSING_PENALTY;
         s.params[0] = static_cast<LosingPenaltyReward*>(r)->penaltyScale;
+#endif
     } else if (Is<BumpedPenalty>(r, t)) s.type = RLGPU_RW_BUMPED_PENALTY;
     else if (Is<DemoedPenalty>(r, t)) s.type = RLGPU_RW_DEMOED_PENALTY;
     else if (Is<VelocityReward>(r, t)) {
@@ -159,9 +161,11 @@ inline bool RegistryTerminal(TerminalCondition* c, rlgpu_terminal_spec& s) {
     if (Is<NoTouchCondition>(c, t)) {
         s.type = RLGPU_TC_NO_TOUCH;
         s.param = static_cast<NoTouchCondition*>(c)->maxTime;
+#ifndef RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES
     } else if (Is<ScoreLimitCondition>(c, t)) {
         s.type = RLGPU_TC_SCORE_LIMIT;
         s.param = (float)static_cast<ScoreLimitCondition*>(c)->limit;
+#endif
     } else if (Is<GoalScoreCondition>(c, t)) s.type = RLGPU_TC_GOAL_SCORE;
     else return false;
     return true;
@@ -381,15 +385,7 @@ class EnvSetGPU {
     int obsSize = RLGPU_OBS, numActions = RLGPU_ACTIONS;
 
     EnvSetGPU(const EnvSetConfig& c, const EnvSetGPUOptions& o = {}, hipStream_t s = nullptr) : config(c), stream(s) {
-        if (!c.envCreateFn) throw std::invalid_argument("EnvSetConfig: no envCreateFn");
-        if (c.numArenas <= 0) throw std::invalid_argument("EnvSetConfig: numArenas must be positive");
-        results.reserve(c.numArenas);
-        for (int i = 0; i < c.numArenas; i++) {
-            results.push_back(c.envCreateFn(i));
-            PluginPlan p = TranslatePlugins(results.back());
-            if (i == 0) plan = p;
-            else RequireSamePlan(plan, p, i);
-        }
+        plan = CreateEnvs(c, results);
         rlgpu_envset_config cfg{};
         cfg.num_arenas = c.numArenas;
         cfg.tick_skip = c.tickSkip;
@@ -415,6 +411,39 @@ class EnvSetGPU {
         cfg.state_setter = plan.stateSetter;
         RlgpuCheck(rlgpu_envset_create(&cfg, &h), "EnvSet");
         RlgpuCheck(rlgpu_envset_buffers_get(h, &state), "EnvSet buffers");
+        InitHost();
+    }
+    // Attached to a device env set made by someone else from this plan's registry lists (the trainer facade: the
+    // C++ Learner owns the env set, the plugin objects and the host fallback live here).  Not destroyed here.
+    EnvSetGPU(const EnvSetConfig& c, std::vector<EnvCreateResult>&& res, const PluginPlan& p, rlgpu_envset* attached,
+              hipStream_t s)
+        : config(c), h(attached), stream(s), results(std::move(res)), plan(p), owns(false) {
+        if (!h) throw std::invalid_argument("EnvSetGPU: null env set to attach to");
+        RlgpuCheck(rlgpu_envset_buffers_get(h, &state), "EnvSet buffers");
+        if (state.num_arenas != c.numArenas) throw std::invalid_argument("EnvSetGPU: attached env set has another arena count");
+        InitHost();
+    }
+
+    // EnvSet ctor (EnvSet.cpp:46-111): one EnvCreateFn call per arena, each result's arena checked against the
+    // device's and its plugins translated; every arena must give the same plan.  Returns it.
+    static PluginPlan CreateEnvs(const EnvSetConfig& c, std::vector<EnvCreateResult>& results) {
+        if (!c.envCreateFn) throw std::invalid_argument("EnvSetConfig: no envCreateFn");
+        if (c.numArenas <= 0) throw std::invalid_argument("EnvSetConfig: numArenas must be positive");
+        PluginPlan plan;
+        results.reserve(c.numArenas);
+        for (int i = 0; i < c.numArenas; i++) {
+            results.push_back(c.envCreateFn(i));
+            RequireDeviceArena(results.back().arena, i);
+            PluginPlan p = TranslatePlugins(results.back());
+            if (i == 0) plan = p;
+            else RequireSamePlan(plan, p, i);
+        }
+        return plan;
+    }
+
+  private:
+    void InitHost() {
+        const EnvSetConfig& c = config;
         fallbackStats.hostRewards = plan.NumHostRewards();
         fallbackStats.hostTerminals = (int)plan.hostTerminals.size();
         if (plan.HasHost()) {
@@ -432,12 +461,16 @@ class EnvSetGPU {
             HostReset(all);
         }
     }
+
+  public:
     EnvSetGPU(const EnvSetGPU&) = delete;
     EnvSetGPU& operator=(const EnvSetGPU&) = delete;
     ~EnvSetGPU() {
-        rlgpu_envset_destroy(h);
+        if (owns) rlgpu_envset_destroy(h);
         if (dMask) (void)hipFree(dMask);
+        if (dActions) (void)hipFree(dActions);
         for (auto& r : results) {
+            delete r.arena;  // EnvSet owns its arenas (EnvSet.h:67-124)
             for (auto& w : r.rewards) delete w.reward;
             for (auto* t : r.terminalConditions) delete t;
             delete r.obsBuilder;
@@ -459,7 +492,36 @@ class EnvSetGPU {
         if (!async) Sync();
     }
 
+    // EnvSet::StepSecondHalf(const IList& actionIndices, bool async) (EnvSet.h:106): host action indices, one per
+    // player, uploaded to the device
+    void StepSecondHalf(const IList& actions, bool async) {
+        if ((int)actions.size() != state.num_players)
+            throw std::invalid_argument("StepSecondHalf: " + std::to_string(actions.size()) + " actions for " +
+                                        std::to_string(state.num_players) + " players");
+        if (!dActions) RlgpuCheckHip(hipMalloc(&dActions, (size_t)state.num_players * sizeof(int32_t)), "actions");
+        static_assert(sizeof(int) == sizeof(int32_t), "IList holds int32 action indices");
+        RlgpuCheckHip(hipMemcpyAsync(dActions, actions.data(), actions.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream),
+                      "actions");
+        StepSecondHalf(dActions, async);
+    }
+
     void Sync() { RlgpuCheck(rlgpu_envset_sync(h, stream), "Sync"); }
+
+    // The trainer facade's step hook (rlgpu_learner_set_step_hook) on an attached set: after the device step, the
+    // host plugins as StepSecondHalf runs them (the previous states kept as StepFirstHalf does); after the reset,
+    // the plugins' Reset on the arenas whose merged terminal reset them.
+    void HostAfterStep() {
+        if (!plan.HasHost()) return;
+        for (int a = 0; a < config.numArenas; a++) prevGameStates[a] = gameStates[a];
+        HostStep();
+    }
+    void HostAfterReset() {
+        if (!plan.HasHost()) return;
+        std::vector<int> reset;
+        for (int a = 0; a < config.numArenas; a++)
+            if (hostTerms[a]) reset.push_back(a);
+        if (!reset.empty()) HostReset(reset);
+    }
 
     // EnvSet::Reset: every arena whose terminal is set (the merged host + device terminal)
     void Reset() {
@@ -494,7 +556,9 @@ class EnvSetGPU {
     }
 
   private:
+    bool owns = true;
     uint8_t* dMask = nullptr;
+    int32_t* dActions = nullptr;
     std::vector<rlgpu_gamestate> recs;
     std::vector<uint8_t> hostTerms;
     std::vector<float> hostRewards, rewardValues;

@@ -12,17 +12,42 @@
 // body: the device evaluates them (EnvSetGPU translates them to rlgpu_reward_spec / rlgpu_terminal_spec).  A
 // class of the user's own -- anything the translator's dynamic_casts do not recognise -- runs on the host,
 // through its own virtuals, exactly as EnvSet::StepSecondHalf calls them (EnvSet.cpp:163-250).
+//
+// The arena an EnvCreateFn builds (RocketSim's Arena::Create / AddCar, RS/Sim/Arena/Arena.h:71,111) is restated as
+// a record of what was asked for -- game mode, tick rate, cars (team, config), mutators -- which the facade
+// checks against the one arena the kernels simulate (2v2 SOCCAR, Octanes added blue, orange, blue, orange at
+// 120 Hz) and refuses with a named error otherwise.
+//
+// RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES: the including translation unit defines ExampleMain's own
+// ScoreLimitCondition / LosingPenaltyReward (src/ExampleMain.cpp:46-124, compiled verbatim): they are then the
+// user's classes (host plugins through their own virtuals), not this header's registry declarations.
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <filesystem>
+#include <fstream>
 #include <functional>
+#include <iostream>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <typeinfo>
 #include <vector>
 
+// RocketSim's Framework.h helpers
+#ifndef RS_MAX
+#define RS_MAX(a, b) ((a) > (b) ? (a) : (b))
+#define RS_MIN(a, b) ((a) < (b) ? (a) : (b))
+#endif
+
 namespace RLGC {
+
+typedef std::vector<float> FList;  // RG/BasicTypes/Lists.h
+typedef std::vector<int> IList;
 
 // RocketSim's Vec (MathTypes.h:8-160): float components, Length = sqrtf(x*x + y*y + z*z), Normalized safe
 struct Vec {
@@ -74,6 +99,66 @@ struct RotMat {
 
 enum class Team : uint8_t { BLUE = 0, ORANGE = 1 };
 #define RS_TEAM_FROM_Y(y) ((y) < 0 ? RLGC::Team::BLUE : RLGC::Team::ORANGE)
+
+// ---- the arena an EnvCreateFn asks for (RS/Sim/GameMode.h, Arena.h, CarConfig.h) ----
+enum class GameMode : uint8_t { SOCCAR, HOOPS, HEATSEEKER, SNOWDAY, DROPSHOT, THE_VOID };
+struct CarConfig {  // the preset the hitbox and wheels come from (CarConfig.h:21-43)
+    int preset;
+    const char* name;
+};
+inline const CarConfig CAR_CONFIG_OCTANE{0, "Octane"}, CAR_CONFIG_DOMINUS{1, "Dominus"}, CAR_CONFIG_PLANK{2, "Plank"},
+    CAR_CONFIG_BREAKOUT{3, "Breakout"}, CAR_CONFIG_HYBRID{4, "Hybrid"}, CAR_CONFIG_MERC{5, "Merc"};
+struct MutatorConfig {};
+struct ArenaConfig {};
+struct Car {
+    uint32_t id = 0;
+    Team team = Team::BLUE;
+    CarConfig config = CAR_CONFIG_OCTANE;
+};
+class Arena {
+  public:
+    GameMode gameMode = GameMode::SOCCAR;
+    float tickRate = 120;
+    bool mutatorsSet = false;
+    std::vector<std::unique_ptr<Car>> cars;
+    static Arena* Create(GameMode mode, const ArenaConfig& = {}, float tickRate = 120) {
+        auto* a = new Arena();
+        a->gameMode = mode;
+        a->tickRate = tickRate;
+        return a;
+    }
+    Car* AddCar(Team team, const CarConfig& config = CAR_CONFIG_OCTANE) {
+        cars.emplace_back(new Car{(uint32_t)cars.size() + 1, team, config});  // car ids start at 1 (Arena.cpp)
+        return cars.back().get();
+    }
+    void SetMutatorConfig(const MutatorConfig&) { mutatorsSet = true; }
+    std::vector<Car*> GetCars() const {
+        std::vector<Car*> v;
+        for (auto& c : cars) v.push_back(c.get());
+        return v;
+    }
+};
+
+// The arena the kernels simulate: 2v2 SOCCAR at 120 Hz, Octanes added blue, orange, blue, orange (creation order
+// is the player order: team of player p = p % 2).  Throws std::invalid_argument naming what differs.
+inline void RequireDeviceArena(const Arena* a, int index) {
+    if (!a) return;  // no arena: the device's own
+    auto fail = [&](const std::string& what) {
+        throw std::invalid_argument("EnvCreateFn(" + std::to_string(index) + "): " + what +
+                                    " (the device simulates 2v2 SOCCAR at 120 Hz with Octanes added blue, orange, "
+                                    "blue, orange)");
+    };
+    if (a->gameMode != GameMode::SOCCAR) fail("game mode " + std::to_string((int)a->gameMode) + " is not SOCCAR");
+    if (a->tickRate != 120.f) fail("tick rate " + std::to_string(a->tickRate) + " is not 120");
+    if (a->mutatorsSet) fail("mutators are set");
+    if (a->cars.size() != 4) fail(std::to_string(a->cars.size()) + " cars instead of 4");
+    for (size_t i = 0; i < a->cars.size(); i++) {
+        if (a->cars[i]->team != (i % 2 ? Team::ORANGE : Team::BLUE))
+            fail("car " + std::to_string(i) + " is on the wrong team for the blue, orange, blue, orange order");
+        if (a->cars[i]->config.preset != CAR_CONFIG_OCTANE.preset)
+            fail(std::string("car ") + std::to_string(i) + " is a " + a->cars[i]->config.name + ", not an Octane");
+    }
+}
 
 struct CarControls {  // RS/Sim/CarControls.h:7-20
     float throttle = 0, steer = 0, pitch = 0, yaw = 0, roll = 0;
@@ -286,6 +371,7 @@ class KickoffProximityReward2v2Enhanced : public Reward {
   public:
     float goerReward = 1.2f, cheaterReward = 0.6f, dynamicWeight = 0.3f, rotationPrepWeight = 0.2f;
 };
+#ifndef RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES
 // src/ExampleMain.cpp:84-124 (its fields are private there; a translator in the reference tree needs them
 // public or an accessor -- INTEGRATION.md section 3)
 class LosingPenaltyReward : public Reward {
@@ -294,6 +380,7 @@ class LosingPenaltyReward : public Reward {
     float penaltyScale;
     int blueScore = 0, orangeScore = 0;
 };
+#endif
 
 class NoTouchCondition : public TerminalCondition {
   public:
@@ -308,6 +395,7 @@ class GoalScoreCondition : public TerminalCondition {
     bool IsTerminal(const GameState& s) override { return s.goalScored; }
     bool IsTruncation() override { return false; }
 };
+#ifndef RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES
 // src/ExampleMain.cpp:46-82
 class ScoreLimitCondition : public TerminalCondition {
   public:
@@ -317,6 +405,7 @@ class ScoreLimitCondition : public TerminalCondition {
     int limit;
     int blueScore = 0, orangeScore = 0;
 };
+#endif
 
 // ---- builders the kernels implement (AdvancedObs.cpp, DefaultAction.cpp, KickoffState.cpp) ----
 class ObsBuilder {
@@ -332,15 +421,22 @@ class StateSetter {
     virtual ~StateSetter() {}
 };
 class AdvancedObs : public ObsBuilder {};
+class DefaultObs : public ObsBuilder {};        // RG/ObsBuilders/DefaultObs.h (declared; the kernels build AdvancedObs)
 class DefaultAction : public ActionParser {};
 class KickoffState : public StateSetter {};
+class RandomState : public StateSetter {        // RG/StateSetters/RandomState.h (declared; not a device state setter)
+  public:
+    bool randBallSpeed = true, randCarSpeed = true, carsOnGround = true;
+    RandomState(bool randBallSpeed = true, bool randCarSpeed = true, bool carsOnGround = true)
+        : randBallSpeed(randBallSpeed), randCarSpeed(randCarSpeed), carsOnGround(carsOnGround) {}
+};
 class FuzzedKickoffState : public StateSetter {  // RG/StateSetters/FuzzedKickoffState.h
   public:
     constexpr static float FUZZ_POS_RANGE = 0.1f;
 };
 
 struct EnvCreateResult {  // RG/EnvSet/EnvSet.h:14-24
-    void* arena = nullptr;  // the device builds the 2v2 SOCCAR arena itself
+    Arena* arena = nullptr;  // checked by RequireDeviceArena; null = the device's 2v2 SOCCAR arena
     std::vector<WeightedReward> rewards;
     std::vector<TerminalCondition*> terminalConditions;
     ObsBuilder* obsBuilder = nullptr;
@@ -360,3 +456,22 @@ struct EnvSetConfig {  // RG/EnvSet/EnvSet.h:27-34
 };
 
 }  // namespace RLGC
+
+// RocketSim::Init (RS/RocketSim.cpp:12-100): the collision meshes of a folder of .cmf files.  The facade keeps the
+// folder; the Learner loads its meshes into the env set when it exists (rlgpu_cmf_parse), else the built-in arena.
+namespace RocketSim {
+using RLGC::Arena;
+using RLGC::CarConfig;
+using RLGC::GameMode;
+using RLGC::Team;
+inline std::string& MeshFolder() {
+    static std::string folder;
+    return folder;
+}
+inline void Init(const std::filesystem::path& collisionMeshesFolder, bool silent = false) {
+    MeshFolder() = collisionMeshesFolder.string();
+    if (!silent && !std::filesystem::is_directory(collisionMeshesFolder))
+        std::fprintf(stderr, "RocketSim::Init: no collision mesh folder at \"%s\": the built-in arena mesh is used\n",
+                     MeshFolder().c_str());
+}
+}  // namespace RocketSim

@@ -1,0 +1,3 @@
+// compat <RLGymCPP/OBSBuilders/DefaultObs.h>: the declarations restated in facade/RLGC.hpp (device registry classes and builders)
+#pragma once
+#include "RLGC.hpp"

@@ -1,0 +1,3 @@
+// compat <RLGymCPP/StateSetters/KickoffState.h>: the declarations restated in facade/RLGC.hpp (device registry classes and builders)
+#pragma once
+#include "RLGC.hpp"

@@ -205,6 +205,42 @@ static int Translate() {
         }
         FreeResult(r);
     }
+    // the arena an EnvCreateFn builds must be the device's: 2v2 SOCCAR, Octanes added blue, orange, blue, orange
+    {
+        auto arena = [](GameMode mode, std::vector<Team> teams, const CarConfig& car = CAR_CONFIG_OCTANE) {
+            Arena* a = Arena::Create(mode);
+            for (Team t : teams) a->AddCar(t, car);
+            return a;
+        };
+        const std::vector<Team> ok2v2 = {Team::BLUE, Team::ORANGE, Team::BLUE, Team::ORANGE};
+        struct Case {
+            Arena* a;
+            const char* why;
+        } bad[] = {{arena(GameMode::SOCCAR, {Team::BLUE, Team::ORANGE}), "1v1"},
+                   {arena(GameMode::HOOPS, ok2v2), "HOOPS"},
+                   {arena(GameMode::SOCCAR, {Team::BLUE, Team::BLUE, Team::ORANGE, Team::ORANGE}), "team order"},
+                   {arena(GameMode::SOCCAR, ok2v2, CAR_CONFIG_DOMINUS), "Dominus"},
+                   {Arena::Create(GameMode::SOCCAR, {}, 60), "60 Hz"}};
+        for (auto& c : bad) {
+            bool threw = false;
+            try {
+                RequireDeviceArena(c.a, 3);
+            } catch (const std::invalid_argument& e) {
+                threw = std::string(e.what()).find("EnvCreateFn(3)") != std::string::npos;
+            }
+            CHECK(threw, "arena accepted: %s", c.why);
+            delete c.a;
+        }
+        Arena* good = arena(GameMode::SOCCAR, ok2v2);
+        bool threw = false;
+        try {
+            RequireDeviceArena(good, 0);
+        } catch (const std::exception&) {
+            threw = true;
+        }
+        CHECK(!threw, "ExampleMain's 2v2 arena refused");
+        delete good;
+    }
     // refused: foreign builders, differing arenas
     {
         bool threw = false;

@@ -257,14 +257,18 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     pc.n_critic_layers = cfg.n_critic_layers;
     std::memcpy(pc.shared_layers, cfg.shared_layers, sizeof(pc.shared_layers));
     pc.n_shared_layers = cfg.n_shared_layers;
+    RLGPU_REQUIRE(cfg.activation == RLGPU_ACT_LEAKY_RELU || cfg.activation == RLGPU_ACT_RELU,
+                  "Learner: activation must be RLGPU_ACT_LEAKY_RELU or RLGPU_ACT_RELU");
+    RLGPU_REQUIRE(cfg.optimizer == RLGPU_OPT_ADAMW || cfg.optimizer == RLGPU_OPT_ADAM,
+                  "Learner: optimizer must be RLGPU_OPT_ADAMW or RLGPU_OPT_ADAM");
     pc.layer_norm = 1;
-    pc.leaky_slope = 0.01f;
+    pc.leaky_slope = cfg.activation == RLGPU_ACT_RELU ? 0.f : 0.01f;
     pc.policy_lr = cfg.policy_lr;
     pc.critic_lr = cfg.critic_lr;
     pc.beta1 = 0.9f;
     pc.beta2 = 0.999f;
     pc.eps = 1e-8f;
-    pc.weight_decay = 1e-2f;
+    pc.weight_decay = cfg.optimizer == RLGPU_OPT_ADAM ? 0.f : 1e-2f;  // Adam == AdamW without decoupled decay
     pc.clip_range = cfg.clip_range;
     pc.entropy_scale = cfg.entropy_scale;
     pc.max_grad_norm = 0.5f;
@@ -1086,4 +1090,9 @@ extern "C" int rlgpu_sample_indices(uint64_t seed, int32_t rank, int64_t iterati
             out[i] = (int64_t)(((unsigned __int128)x * (unsigned __int128)(uint64_t)range) >> 64);
         }
     });
+}
+
+extern "C" double rlgpu_host_uniform(uint64_t seed, uint64_t stream, uint64_t counter) {
+    const uint64_t x = splitmix64(seed ^ splitmix64((stream << 48) ^ splitmix64(counter)));
+    return (double)(x >> 11) * (1.0 / 9007199254740992.0);  // 53 bits
 }

@@ -5,8 +5,16 @@
 // address, mapped back by parameter order on load).  Built against the libtorch of the installed
 // PyTorch (plumbing); rlgpu/checkpoint.py drives it.
 //
+// It also writes and reads the model archives <NAME>.lt (GGL::Model::Save / Load, Models.cpp:116-166): the
+// Sequential GGL::Model builds (Models.cpp:7-33: per hidden layer Linear, LayerNorm, LeakyReLU; then the output
+// Linear unless out is 0, the shared head's addOutputLayer = false) saved with torch::save(seq, stream) and
+// read with torch::load(seq, stream), with Model::Load's parameter-size check.
+//
 // usage: rlgpu_optim_lt save <out.lt> <state.f32> <step> <lr> <beta1> <beta2> <eps> <weight_decay> <shape>...
 //        rlgpu_optim_lt load <in.lt> <state.f32> <shape>...
+//        rlgpu_optim_lt model-save <out.lt> <params.f32> <obs> <out> <h1> [h2 ...]
+//        rlgpu_optim_lt model-load <in.lt> <params.f32> <obs> <out> <h1> [h2 ...]
+//   params.f32: the model's parameters flat in parameters() order (model-load writes them).
 //   shape: dimensions joined by 'x' (e.g. 384x167), one per model parameter in parameters() order;
 //   state.f32: every parameter's exp_avg (flat, parameter order), then every exp_avg_sq.  load writes
 //   it preceded by the step as an int64 (0 and zero moments for parameters without state).
@@ -39,12 +47,81 @@ std::vector<torch::Tensor> make_params(char** shapes, int n) {
     return ps;
 }
 
+torch::nn::Sequential make_model(int obs, int out, const std::vector<int>& layers) {
+    torch::nn::Sequential seq;
+    int last = obs;
+    for (int h : layers) {
+        seq->push_back(torch::nn::Linear(last, h));
+        seq->push_back(torch::nn::LayerNorm(torch::nn::LayerNormOptions({(int64_t)h})));
+        last = h;
+        seq->push_back(torch::nn::LeakyReLU());
+    }
+    if (out > 0) seq->push_back(torch::nn::Linear(last, out));
+    return seq;
+}
+
+std::vector<int64_t> seq_sizes(torch::nn::Sequential& seq) {  // GetSeqSizes (Models.cpp:79-87)
+    std::vector<int64_t> r;
+    for (size_t i = 0; i < seq->size(); i++)
+        for (auto& p : seq[i]->parameters()) r.push_back(p.numel());
+    return r;
+}
+
+int model_mode(bool save, int argc, char** argv) {
+    if (argc < 7) return 2;
+    std::vector<int> layers;
+    for (int i = 6; i < argc; i++) layers.push_back(std::atoi(argv[i]));
+    torch::nn::Sequential seq = make_model(std::atoi(argv[4]), std::atoi(argv[5]), layers);
+    torch::NoGradGuard ng;
+    int64_t total = 0;
+    for (auto& p : seq->parameters()) total += p.numel();
+    std::vector<float> buf((size_t)total);
+    if (save) {
+        std::ifstream in(argv[3], std::ios::binary);
+        in.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(buf.size() * sizeof(float)));
+        if (!in) {
+            std::cerr << "parameter file too short\n";
+            return 3;
+        }
+        int64_t off = 0;
+        for (auto& p : seq->parameters()) {
+            p.copy_(torch::from_blob(buf.data() + off, p.sizes(), torch::kFloat32));
+            off += p.numel();
+        }
+        std::ofstream out(argv[2], std::ios::binary);  // Model::Save (Models.cpp:116-120)
+        torch::save(seq, out);
+        return out ? 0 : 3;
+    }
+    const auto before = seq_sizes(seq);
+    std::ifstream in(argv[2], std::ios::binary);  // Model::Load (Models.cpp:130-166)
+    in >> std::noskipws;
+    if (!in.good()) {
+        std::cerr << "cannot open " << argv[2] << "\n";
+        return 3;
+    }
+    torch::load(seq, in);
+    if (seq_sizes(seq) != before) {
+        std::cerr << "Saved model has different size than current model, cannot load model from " << argv[2] << "\n";
+        return 5;
+    }
+    int64_t off = 0;
+    for (auto& p : seq->parameters()) {
+        auto c = p.to(torch::kCPU).to(torch::kFloat32).contiguous();
+        std::copy(c.data_ptr<float>(), c.data_ptr<float>() + c.numel(), buf.begin() + off);
+        off += p.numel();
+    }
+    std::ofstream out(argv[3], std::ios::binary);
+    out.write(reinterpret_cast<const char*>(buf.data()), (std::streamsize)(buf.size() * sizeof(float)));
+    return out ? 0 : 3;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     try {
         if (argc < 4) return 2;
         const std::string mode = argv[1];
+        if (mode == "model-save" || mode == "model-load") return model_mode(mode == "model-save", argc, argv);
         if (mode == "save") {
             if (argc < 10) return 2;
             const int64_t step = std::atoll(argv[4]);

@@ -72,6 +72,15 @@ class WelfordStat:
         self.n, self.mean, self.m2 = int(j["count"]), float(j["mean"]), float(j["var"])
 
 
+def host_uniform(seed, stream, counter):
+    """rlgpu_host_uniform: the counter-based host draw of the self-play / skill-match picks (include/rlgpu_learner.h),
+    the same in the C++ trainer facade."""
+    L = _host_lib()
+    L.rlgpu_host_uniform.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+    L.rlgpu_host_uniform.restype = ctypes.c_double
+    return float(L.rlgpu_host_uniform(seed & (2**64 - 1), stream, counter))
+
+
 def batch_ranges(exp_size, batch_size, overbatching=True):
     """ExperienceBuffer::GetAllBatchesShuffled batch boundaries (ExperienceBuffer.cpp:117-162),
     from the C++ ExperienceBuffer (GGL::BatchRanges)."""
@@ -225,7 +234,8 @@ class _CConfig(ctypes.Structure):
                 ("rewards", ctypes.c_void_p), ("n_rewards", ctypes.c_int32),
                 ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32),
                 ("experience_mode", ctypes.c_int32), ("ts_per_itr", ctypes.c_int64),
-                ("experience_capacity", ctypes.c_int32), ("arith", ctypes.c_int32)]
+                ("experience_capacity", ctypes.c_int32), ("arith", ctypes.c_int32),
+                ("activation", ctypes.c_int32), ("optimizer", ctypes.c_int32)]
 
 
 class _CBatch(ctypes.Structure):
@@ -399,7 +409,6 @@ class Learner:
         # players use the current policy); the draw is rank-independent so every rank agrees
         self.versions = None
         self.old_version, self.old_team = None, 0
-        self._vrng = np.random.default_rng(cfg.seed + 104729)
         self.skill = None
         # rank 0 plays the skill matches (ratings are a report; every rank holds the same versions)
         if cfg.skill_tracker is not None and cfg.skill_tracker.enabled and rank == 0:  # PolicyVersionManager.cpp:24-31
@@ -541,9 +550,10 @@ class Learner:
         t0 = time.perf_counter()
         self.old_version = None
         if self.cfg.train_against_old_versions and self.versions is not None and self.versions.versions:  # Learner.cpp:587-627
-            if self._vrng.random() < self.cfg.train_against_old_chance:
-                self.old_version = self.versions.versions[int(self._vrng.integers(0, len(self.versions.versions)))]
-                self.old_team = int(self._vrng.integers(0, 2))
+            it, n = self.iteration, len(self.versions.versions)
+            if host_uniform(self.cfg.seed, 1, 3 * it) < self.cfg.train_against_old_chance:  # the C++ facade's picks
+                self.old_version = self.versions.versions[min(n - 1, int(host_uniform(self.cfg.seed, 1, 3 * it + 1) * n))]
+                self.old_team = min(1, int(host_uniform(self.cfg.seed, 1, 3 * it + 2) * 2))
                 self.ppo.set_version(self.old_version.params)
         team = -1 if self.old_version is None else self.old_team
         _lib.check(_lib.lib().rlgpu_learner_set_old_team(self._h, team), "rlgpu_learner_set_old_team")

@@ -9,9 +9,11 @@ them), StepFirstHalf, one mixed-policy inference over every player -- the curren
 players, the old version (rlgpu_ppo_set_version) for the other team's (rlgpu_ppo_infer_actions_mixed; the
 reference runs the two models on index-selected rows, PPOLearner::InferActionsFromModels) -- and
 StepSecondHalf; every arena whose GameState has goalScored then updates the two ratings with ELO math in arena
-order, in fp32 as the reference computes them.  The random picks (old version, new team) use a NumPy
-generator in place of RocketSim's Math::RandInt; the policy's multinomial draws use the PPO handle's Philox
-stream on a counter range of their own.
+order, in fp32 as the reference computes them.  The random picks (old version, new team) are the library's
+counter-based host draws (rlgpu_host_uniform, stream 2: the C++ facade's PolicyVersionManager makes the same
+picks) in place of RocketSim's Math::RandInt; the policy's multinomial draws use the PPO handle's Philox
+stream on a step range of their own (2^40 + k: the step's high bits are folded into the Philox key, so these
+uniforms never repeat the rollout's).
 """
 import numpy as np
 
@@ -108,7 +110,8 @@ class SkillTracker:
         self.prev_new_team = 0
         self.prev_sim_time = np.float32(0)
         self.iterations_since_ran = 0
-        self.rng = np.random.default_rng(seed + 65537)
+        self.seed = seed
+        self.runs = 0  # rlgpu_host_uniform counter: run r draws 2 r (version) and 2 r + 1 (team)
         self.steps_run = 0
         self.log = []  # (old version index, new team, goal events) per run, for reports and tests
 
@@ -125,10 +128,13 @@ class SkillTracker:
             assert self.prev_old_version_index < len(versions)
             old_index, new_team, total = self.prev_old_version_index, self.prev_new_team, f(self.prev_sim_time)
         else:
-            old_index = int(self.rng.integers(0, len(versions)))
-            new_team = int(self.rng.integers(0, 2))
+            from .learner import host_uniform
+            n = len(versions)
+            old_index = min(n - 1, int(host_uniform(self.seed, 2, 2 * self.runs) * n))
+            new_team = min(1, int(host_uniform(self.seed, 2, 2 * self.runs + 1) * 2))
             total = f(0)
             E.reset()
+        self.runs += 1
         self.do_continuation = False
         old = versions[old_index]
         self.ppo.set_version(old.params)

@@ -105,6 +105,22 @@ def test_oracle_draw_is_the_reference_cpu_loop():
     assert ra[0] == A - 1
 
 
+def test_skill_steps_draw_their_own_uniforms():
+    """The skill matches sample at steps 2^40 + k (rlgpu/skill.py); the step's high 32 bits are folded into the
+    Philox key (ppo_kernels.hpp sample_key), so their uniforms differ from the rollout's at step k on the same rows
+    (a uint32 counter alone made them identical)."""
+    rng = np.random.default_rng(5)
+    n, A = 4096, 90
+    logits = _bf16_bits(rng.standard_normal((n, A)))
+    masks = np.ones((n, A), np.uint8)
+    for k in (0, 3, 1000):
+        _, r0 = oracle.sampler_probs(logits, masks, 77, k)
+        _, r1 = oracle.sampler_probs(logits, masks, 77, 2**40 + k)
+        assert (r0 != r1).mean() > 0.99
+        _, r2 = oracle.sampler_probs(logits, masks, 77, k)
+        np.testing.assert_array_equal(r0, r2)
+
+
 def _gpu_logits16(p, o, fp16):
     """The policy's 16-bit logits exactly as the sampler reads them (forward(..., half=True) returns
     their exact f32 values)."""
@@ -138,7 +154,7 @@ def test_sampler_bit_exact_vs_oracle(gpu, monkeypatch, kw, fp16, fused, chunk):
     o, m = torch.from_numpy(obs).to(gpu), torch.from_numpy(masks).to(gpu)
     logits = np.concatenate([_gpu_logits16(p, o[i:i + p.max_rows], fp16) for i in range(0, n, p.max_rows)])
     for det in (True, False):
-        for step in (0, 1, 77, 2**31 + 5):
+        for step in (0, 1, 77, 2**31 + 5, 2**40 + 5):  # 2^40 + k: the skill matches' step range
             a, lp = p.infer_actions(o, m, step=step, deterministic=det)
             wa, wlp = oracle.sample_actions(logits, masks, det, p.cfg.seed, step, 0, fp16)
             ga, glp = a.cpu().numpy(), lp.cpu().numpy()
