@@ -18,9 +18,9 @@
 // checks against the one arena the kernels simulate (2v2 SOCCAR, Octanes added blue, orange, blue, orange at
 // 120 Hz) and refuses with a named error otherwise.
 //
-// RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES: the including translation unit defines ExampleMain's own
-// ScoreLimitCondition / LosingPenaltyReward (src/ExampleMain.cpp:46-124, compiled verbatim): they are then the
-// user's classes (host plugins through their own virtuals), not this header's registry declarations.
+// RLGPU_FACADE_USER_EXAMPLEMAIN_CLASSES: the including translation unit defines its own ScoreLimitCondition /
+// LosingPenaltyReward, as src/ExampleMain.cpp:46-124 does: they are then the user's classes (host plugins through
+// their own virtuals), not this header's registry declarations.
 #pragma once
 #include <algorithm>
 #include <cmath>
