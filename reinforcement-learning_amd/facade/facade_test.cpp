@@ -4,6 +4,10 @@
 //                           RLGC.hpp translates to exactly rlgpu_envset_default_plugins' registry lists; user
 //                           classes, subclasses of registry classes and ZeroSumReward over a user class go to
 //                           the host; fields the registry cannot hold and foreign builders are refused.
+//   facade_test learner     (GPU) two trainer-facade GGL::Learners (GigaLearn.hpp) on the same seed: one whose
+//                           EnvCreateFn gives registry classes (the fused env step), one with the user classes
+//                           on the host plus a StepCallbackFn (the hooked step): the same parameters bit for bit
+//                           after every iteration, and the callback saw every step's GameStates.
 //   facade_test fallback    (GPU) two env sets in lockstep on the same seed and actions: one whose plugins are
 //                           all registry classes, one where user classes restating the same rewards and
 //                           conditions run on the host.  Rewards, terminals and obs must agree bit for bit over
@@ -12,7 +16,7 @@
 #include <cstring>
 #include <random>
 
-#include "EnvSetGPU.hpp"
+#include "GigaLearn.hpp"
 
 using namespace RLGC;
 
@@ -378,13 +382,74 @@ static int Fallback(int arenas, int steps) {
     return g_fail ? 1 : 0;
 }
 
+// ---- GPU: the trainer facade with host plugins + a StepCallbackFn vs the registry-only Learner ----
+static int LearnerMode(int arenas, int iters) {
+    using namespace GGL;
+    LearnerConfig cfg = {};
+    cfg.numGames = arenas;
+    cfg.randomSeed = 7;
+    cfg.ppo.tsPerItr = 24 * 4 * arenas;
+    cfg.ppo.batchSize = cfg.ppo.tsPerItr;
+    cfg.ppo.miniBatchSize = cfg.ppo.tsPerItr / 2;
+    cfg.ppo.maxEpisodeDuration = 2.0;
+    cfg.ppo.sharedHead.layerSizes = {64};
+    cfg.ppo.policy.layerSizes = {64, 64};
+    cfg.ppo.critic.layerSizes = {64, 64};
+    for (PartialModelConfig* m : {&cfg.ppo.policy, &cfg.ppo.critic, &cfg.ppo.sharedHead}) {
+        m->activationType = ModelActivationType::LEAKY_RELU;
+        m->optimType = ModelOptimType::ADAMW;
+    }
+    cfg.checkpointFolder.clear();
+    cfg.trainAgainstOldVersions = false;
+    cfg.sendMetrics = false;
+    LearnerGPUOptions o;
+    o.quitKeyThread = false;
+    o.displayReport = false;
+    uint64_t calls = 0, players = 0;
+    Learner A(DeviceEnv, cfg, nullptr, o);
+    Learner B(HostEnv, cfg,
+              [&](Learner*, const std::vector<GameState>& states, Report& report) {
+                  calls++;
+                  for (auto& s : states)
+                      for (auto& p : s.players) {
+                          players++;
+                          report.AddAvg("Player/Speed", p.vel.Length());
+                      }
+              },
+              o);
+    CHECK(B.envSet->plan.HasHost(), "the user classes did not go to the host");
+    for (int it = 0; it < iters && !g_fail; it++) {
+        Report ra, rb;
+        A.Iterate(ra);
+        B.Iterate(rb);
+        CHECK(A.totalTimesteps == B.totalTimesteps, "iteration %d: %llu vs %llu timesteps", it,
+              (unsigned long long)A.totalTimesteps, (unsigned long long)B.totalTimesteps);
+        for (auto& m : A.models) {
+            const std::vector<float> a = A.ModelParams(m.index), b = B.ModelParams(m.index);
+            int bad = 0;
+            for (size_t i = 0; i < a.size(); i++) bad += std::memcmp(&a[i], &b[i], 4) != 0;
+            CHECK(a.size() == b.size() && bad == 0, "iteration %d: %s: %d of %zu parameters differ", it, m.name, bad, a.size());
+        }
+        rb.Finish();
+        CHECK(rb.Has("Player/Speed"), "the StepCallbackFn's report is missing");
+    }
+    CHECK(calls > 0 && players == calls * (uint64_t)arenas * 4, "callback calls %llu, players %llu",
+          (unsigned long long)calls, (unsigned long long)players);
+    std::printf("learner: %d arenas x %d iterations, %llu timesteps, %llu callback calls, host reward calls %llu: %s\n",
+                arenas, iters, (unsigned long long)A.totalTimesteps, (unsigned long long)calls,
+                (unsigned long long)B.envSet->fallbackStats.rewardCalls, g_fail ? "FAILED" : "ok");
+    return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::printf("usage: facade_test translate | fallback [arenas] [steps]\n");
+        std::printf("usage: facade_test translate | fallback [arenas] [steps] | learner [arenas] [iterations]\n");
         return 2;
     }
     try {
         if (!std::strcmp(argv[1], "translate")) return Translate();
+        if (!std::strcmp(argv[1], "learner"))
+            return LearnerMode(argc > 2 ? std::atoi(argv[2]) : 64, argc > 3 ? std::atoi(argv[3]) : 2);
         if (!std::strcmp(argv[1], "fallback"))
             return Fallback(argc > 2 ? std::atoi(argv[2]) : 256, argc > 3 ? std::atoi(argv[3]) : 300);
     } catch (const std::exception& e) {

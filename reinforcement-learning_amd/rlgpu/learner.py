@@ -488,6 +488,30 @@ class Learner:
                    "rlgpu_learner_step_metrics")
         return {k: float(t) / int(c) for k, t, c in zip(EnvSet.step_metric_names(), tot, cnt) if c}
 
+    _HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32)
+
+    def set_step_hook(self, fn):
+        """rlgpu_learner_set_step_hook: fn(phase) after every collection step (0: post-step, pre-reset -- it may
+        rewrite self.env's rewards / terminals; 1: after the arenas whose terminal is set were reset); None restores
+        the fused step.  An exception in fn fails the iteration."""
+        L = _lib.lib()
+        if fn is None:
+            self._hook = None
+            _lib.check(L.rlgpu_learner_set_step_hook(self._h, None, None), "rlgpu_learner_set_step_hook")
+            return
+
+        def thunk(_user, phase):
+            try:
+                fn(int(phase))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported by the iteration's failure
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._hook = self._HOOK(thunk)  # kept alive with the learner
+        L.rlgpu_learner_set_step_hook.argtypes = [ctypes.c_void_p, self._HOOK, ctypes.c_void_p]
+        _lib.check(L.rlgpu_learner_set_step_hook(self._h, self._hook, None), "rlgpu_learner_set_step_hook")
+
     def set_env_timing(self, on=True):
         _lib.check(_lib.lib().rlgpu_learner_set_env_timing(self._h, int(on)), "rlgpu_learner_set_env_timing")
 

@@ -114,6 +114,16 @@ def test_host_fallback_matches_registry(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_trainer_facade_host_plugins_and_step_callback(gpu):
+    """GGL::Learner(EnvCreateFn, LearnerConfig, StepCallbackFn) (facade/GigaLearn.hpp, Learner.h:42): user plugin
+    classes on the host plus a StepCallbackFn (the hooked env step) train the same parameters, bit for bit, as the
+    registry classes on the fused step."""
+    r = _run("learner", "64", "2", timeout=280)
+    assert r.returncode == 0 and "learner:" in r.stdout and "FAIL" not in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
 def test_download_gamestates_and_reward_values(gpu):
     import torch
     from rlgpu import env, plugins

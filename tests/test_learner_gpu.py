@@ -269,3 +269,57 @@ def test_c4_frame_stack_rollout(gpu):
     L.learn()
     torch.cuda.synchronize()
     assert torch.isfinite(L.ppo.flat()).all()
+
+
+def _bits(t):
+    import torch
+    return t.contiguous().view(torch.int32) if t.dtype == torch.float32 else t
+
+
+def test_step_hook_split_step_is_the_fused_step(gpu):
+    """rlgpu_learner_set_step_hook (host plugins / a StepCallbackFn in the loop, Learner.cpp:676-861): with a hook
+    that changes nothing, the split step (env step without reset, hook, merged codes / rewards / truncation rows,
+    EnvSet::Reset, hook, append) collects and trains bit for bit what the fused step does."""
+    import torch
+    A = _learner(gpu, max_episode_duration=1.2, train_against_old_versions=False)
+    B = _learner(gpu, max_episode_duration=1.2, train_against_old_versions=False)
+    calls = []
+    B.set_step_hook(calls.append)
+    for L in (A, B):
+        L.iterate()
+    torch.cuda.synchronize()
+    assert calls == [0, 1] * A.T
+    assert (A.terms == 2).any()  # max-episode truncations (their pre-reset rows are appended)
+    for name in ("obs", "masks", "actions", "logp", "rewards", "terms", "values", "adv", "target"):
+        assert torch.equal(_bits(getattr(A, name)), _bits(getattr(B, name))), name
+    sel = A.terms == 2
+    assert torch.equal(_bits(A.trunc_obs[sel]), _bits(B.trunc_obs[sel]))
+    assert torch.equal(_bits(A.ppo.params), _bits(B.ppo.params))
+
+
+def test_step_hook_host_rewards_and_terminals(gpu):
+    """A hook that adds 1 to every reward and ends arena 0 (NORMAL) every 5th step, as a host plugin would: the
+    rollout takes the host rewards, arena 0's codes are the merged terminal and it is reset; every other arena is
+    the fused run's, reward + 1."""
+    import torch
+    C = _learner(gpu, train_against_old_versions=False)
+    D = _learner(gpu, train_against_old_versions=False)
+    n = [0]
+
+    def hook(phase):
+        if phase == 0:
+            C.env.rewards.add_(1.0)
+            if n[0] % 5 == 4:
+                C.env.terminals[0] = 1
+            n[0] += 1
+        torch.cuda.synchronize()
+    C.set_step_hook(hook)
+    C.collect()
+    D.collect()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(C.rewards[:, 4:].cpu().numpy(), D.rewards[:, 4:].cpu().numpy() + np.float32(1))
+    assert torch.equal(C.terms[:, 4:], D.terms[:, 4:])
+    assert torch.equal(_bits(C.obs[:, 4:]), _bits(D.obs[:, 4:]))
+    forced = C.terms[4::5, :4].cpu().numpy()
+    assert (forced == 1).all(), forced
+    assert not torch.equal(_bits(C.obs[5, :4]), _bits(D.obs[5, :4]))  # arena 0 restarted from a kickoff after t = 4
