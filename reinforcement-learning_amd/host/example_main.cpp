@@ -21,7 +21,11 @@
 //   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--trajectories] [--f32-gemm] [--c2-model] [--seed S]
 //               [--checkpoint-folder DIR [--ts-per-save N] [--resave-to DIR2]] [--self-play]
 //               [--rank r --world N --rccl-id FILE [--rccl-nonce STR]]
+#include <execinfo.h>
+#include <signal.h>
+
 #include <chrono>
+#include <csignal>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -101,7 +105,21 @@ static void ReadOrWriteRcclId(int rank, const std::string& idFile, std::string n
     }
 }
 
+// a crash prints the host backtrace to stderr before the default action (diagnostics for a test run)
+static void OnCrash(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "rlgpu_train: fatal signal, host backtrace:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char** argv) {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);
+    signal(SIGSEGV, OnCrash);
+    signal(SIGABRT, OnCrash);
     LearnerConfig cfg = {};
     LearnerGPUOptions opt;
     opt.experienceMode = RLGPU_EXP_ROLLOUT;  // the engine's fixed [T, P] rollout (the bench's); --trajectories: the reference's

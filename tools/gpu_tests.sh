@@ -1,5 +1,8 @@
-# GPU test run: every -m gpu test (or the pytest selection given as arguments), then smoke().
+# GPU test run: the -m gpu tests of the given files (default: all), then smoke().  TAG names gpurun_out/<TAG>.
 export TMPDIR=/tmp
-mkdir -p gpurun_out/t
-timeout -k 10 900 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t/gpu_tests.log 2>&1 && \
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/t/smoke.log 2>&1
+O=gpurun_out/${TAG:-t}
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest ${@:-tests} -m gpu -x -v -s --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -3 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+echo smoke ok
