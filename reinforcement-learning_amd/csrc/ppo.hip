@@ -10,6 +10,7 @@
 #include "common.hpp"
 #include "mlp_kernels.hpp"
 #include "ppo_kernels.hpp"
+#include "row_gemm.hpp"
 #include "infer_kernels.hpp"
 
 namespace {
@@ -119,6 +120,13 @@ inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
 inline int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
+}
+// Full-row H3 GEMMs (mlp::gemm_row, row_gemm.hpp): the training forward's Linear + LayerNorm + LeakyReLU of a
+// hidden layer with 256 or 512 outputs in one kernel.  RLGPU_ROW_GEMM: 0 off (the 128 x 128 GEMM + ln_act_fwd),
+// 1 (default) on.
+inline int row_gemm() {
+    static const int v = env_int("RLGPU_ROW_GEMM", 1);
+    return v;
 }
 inline int lnf_variant() {
     static const int v = env_int("RLGPU_LNF_VARIANT", 0);
@@ -610,15 +618,53 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
     const bool head1 = O && O->out == 1 && nh > 0;  // rank-1 head fused into the last LayerNorm forward
     for (int l = 0; l < nh; l++) {
         const Layer& L = m.L[l];
+        const float* gg = L.g >= 0 ? P + L.g : nullptr;
+        const float* bb = L.be >= 0 ? P + L.be : nullptr;
+        const bool fuse = head1 && l == nh - 1;
+        // the full-row kernel: Linear + LayerNorm + LeakyReLU in one pass (row_gemm.hpp)
+        if (row_gemm() && m.mode == RLGPU_GEMM_F16X3 && L.sf >= 0 && gg && !fuse && (L.out == 512 || L.out == 256) &&
+            ld % 4 == 0 && (L.in % 4 == 0 || tail_ok)) {
+            mlp::RowArgs a{};
+            a.A = in;
+            a.lda = ld;
+            a.B = m.wsplit + L.sf;
+            a.ldb = L.sf_ld;
+            a.bplane = (int64_t)L.sf_rows * L.sf_ld;
+            a.bscale = wscale_at(m, L.sfs);
+            a.amax_a = in_amax;
+            a.bias = P + L.b;
+            a.C = m.xhat[l];
+            a.ldc = L.out;
+            a.I = n;
+            a.N = L.out;
+            a.K = L.in;
+            a.gamma = gg;
+            a.beta = bb;
+            a.slope = h->cfg.leaky_slope;
+            a.act = m.act[l];
+            a.stats = reinterpret_cast<float2*>(m.rstd[l]);
+            a.amax_out = amax_slot(m, l);
+            {
+                // flops of the GEMM (the LayerNorm's bytes ride along in the same launch)
+                ktime::Span span(ktime::FWD_GEMM, 2.0 * n * (double)L.out * L.in, s);
+                if (L.out == 512)
+                    hipLaunchKernelGGL((mlp::gemm_row<32, 2, 4, mlp::ROW_LN>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
+                else
+                    hipLaunchKernelGGL((mlp::gemm_row<32, 2, 2, mlp::ROW_LN>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
+                RLGPU_CHECK_HIP(hipGetLastError());
+            }
+            in = m.act[l];
+            in_amax = amax_slot(m, l);
+            ld = L.out;
+            tail_ok = false;
+            continue;
+        }
         if (L.sf >= 0)
             gemm_x6_pre(in, ld, m.wsplit + L.sf, L.sf_ld, (int64_t)L.sf_rows * L.sf_ld, m.xhat[l], L.out, P + L.b, n, L.out,
                         L.in, s, tail_ok, in_amax, wscale_at(m, L.sfs));
         else
             gemm_f32(m.mode, mlp::A_IK, mlp::B_JK, in, ld, P + L.w, L.in, m.xhat[l], L.out, P + L.b, n, L.out, L.in, 1, s,
                      tail_ok, false, in_amax);
-        const float* gg = L.g >= 0 ? P + L.g : nullptr;
-        const float* bb = L.be >= 0 ? P + L.be : nullptr;
-        const bool fuse = head1 && l == nh - 1;
         // bytes: z read, act written, (mean, rstd) written
         ktime::Span span(ktime::LN_FWD, (double)n * (8.0 * L.out + 8.0), s);
         int lnf_rows = 0;
@@ -673,6 +719,46 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
     red.m = &m;
     Reducer* R = batch ? &red : nullptr;
     const Layer* O = m.head_only ? nullptr : &m.L[nh];
+    // The full-row input-gradient GEMM with hidden layer l's LayerNorm backward in its epilogue (row_gemm.hpp
+    // ROW_LNB): dA of layer l = A . src^T (src: the layer above, its pre-split transposed planes), then dZ_l into
+    // dst and layer l's column partials.  fusedDZ[l]: where dZ_l went (the fused layers ping-pong between m.dZ
+    // and m.dA, which the fused path no longer needs).
+    std::vector<float*> fusedDZ((size_t)std::max(nh, 1), nullptr);
+    auto row_lnb_ok = [&](int l, const Layer& src, int64_t lda) {
+        const Layer& L = m.L[l];
+        return row_gemm() && m.mode == RLGPU_GEMM_F16X3 && src.sb >= 0 && L.g >= 0 && L.be >= 0 &&
+               (L.out == 512 || L.out == 256) && lda % 4 == 0;
+    };
+    auto launch_lnb = [&](int l, const float* A, int64_t lda, const float* a_amax, const Layer& src, float* dst) {
+        const Layer& L = m.L[l];
+        mlp::RowArgs a{};
+        a.A = A;
+        a.lda = lda;
+        a.B = m.wsplit + src.sb;
+        a.ldb = src.sb_ld;
+        a.bplane = (int64_t)src.sb_rows * src.sb_ld;
+        a.bscale = wscale_at(m, src.sbs);
+        a.amax_a = a_amax;
+        a.C = dst;
+        a.ldc = L.out;
+        a.I = n;
+        a.N = L.out;
+        a.K = src.out;
+        a.gamma = P + L.g;
+        a.beta = P + L.be;
+        a.slope = h->cfg.leaky_slope;
+        a.stats = reinterpret_cast<float2*>(m.rstd[l]);
+        a.amax_out = amax_slot(m, kAmaxDZ + l);
+        a.Z = m.xhat[l];
+        a.part = m.cpart_l[l];
+        ktime::Span span(ktime::FWD_GEMM, 2.0 * n * (double)L.out * src.out, s);
+        if (L.out == 512)
+            hipLaunchKernelGGL((mlp::gemm_row<32, 2, 4, mlp::ROW_LNB>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((mlp::gemm_row<32, 2, 2, mlp::ROW_LNB>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        fusedDZ[l] = dst;
+    };
     if (!O) {
         dA_top = dout;
     } else if (O->out == 1 && nh == 0) {  // rank-1 head on the input: dA = dv w^T, dw / db partials in one pass
@@ -706,7 +792,9 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
             throw rlgpu::Error(RLGPU_ERR_STATE, "backward: padded dout needs the loss kernel's bias partials");
         // dA = dout . W_out (into the input gradient when the output layer reads the model input)
         float* dA = nh > 0 ? m.dA : m.dX;
-        if (dA) {
+        if (nh > 0 && row_lnb_ok(nh - 1, *O, dld)) {
+            launch_lnb(nh - 1, dout, dld, amax_slot(m, kAmaxOut), *O, m.dZ);
+        } else if (dA) {
             if (O->sb >= 0)
                 gemm_x6_pre(dout, dld, m.wsplit + O->sb, O->sb_ld, (int64_t)O->sb_rows * O->sb_ld, dA, O->in, nullptr, n, O->in,
                             O->out, s, dld > O->out, amax_slot(m, kAmaxOut), wscale_at(m, O->sbs));
@@ -722,9 +810,10 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         const bool r1 = rank1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
         int lnb_rows = 0;
         const auto lnb = mlp::ln_act_bwd_pick(L.out, r1, lnb_variant(), &lnb_rows);
-        const int nb = (int)ceil_div(n, lnb_rows);
         const float* dA_in = l == nh - 1 ? dA_top : m.dA;
-        {
+        float* dz = fusedDZ[l] ? fusedDZ[l] : m.dZ;  // this layer's dZ
+        const int nb = fusedDZ[l] ? (int)ceil_div(n, mlp::RM) : (int)ceil_div(n, lnb_rows);
+        if (!fusedDZ[l]) {
         // bytes: dA (recomputed for the rank-1 head: its dv instead), z, stats read; dZ written
         ktime::Span span(ktime::LN_BWD, (double)n * ((r1 ? 4.0 : 4.0 * L.out) + 8.0 * L.out + 8.0), s);
         hipLaunchKernelGGL(lnb, dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
@@ -744,15 +833,19 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
             reduce_partials(m, m.cpart_l[l], nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
         }
         const Input a = l > 0 ? Input{m.act[l - 1], L.in, amax_slot(m, l - 1), false} : x;
-        weight_grad(m, m.dZ, L.out, a.X, a.ld, L.in, n, G + L.w, s, a.tail_ok, amax_slot(m, kAmaxDZ + l), a.amax, 0, R,
+        weight_grad(m, dz, L.out, a.X, a.ld, L.in, n, G + L.w, s, a.tail_ok, amax_slot(m, kAmaxDZ + l), a.amax, 0, R,
                     m.wpart_l[l]);
         float* dA = l > 0 ? m.dA : m.dX;  // the first layer's only when the input gradient is wanted
         if (!dA) continue;
+        if (l > 0 && row_lnb_ok(l - 1, L, L.out)) {  // layer l - 1's LayerNorm backward inside its dA GEMM
+            launch_lnb(l - 1, dz, L.out, amax_slot(m, kAmaxDZ + l), L, dz == m.dZ ? m.dA : m.dZ);
+            continue;
+        }
         if (L.sb >= 0)
-            gemm_x6_pre(m.dZ, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, dA, L.in, nullptr, n, L.in,
+            gemm_x6_pre(dz, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, dA, L.in, nullptr, n, L.in,
                         L.out, s, false, amax_slot(m, kAmaxDZ + l), wscale_at(m, L.sbs));
         else
-            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, m.dZ, L.out, P + L.w, L.in, dA, L.in, nullptr, n, L.in, L.out, 1, s, false,
+            gemm_f32(m.mode, mlp::A_IK, mlp::B_KJ, dz, L.out, P + L.w, L.in, dA, L.in, nullptr, n, L.in, L.out, 1, s, false,
                      false, amax_slot(m, kAmaxDZ + l), nullptr);
     }
     red.flush(s);

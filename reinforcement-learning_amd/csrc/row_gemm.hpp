@@ -6,6 +6,14 @@
 //                                                    layer's pre-split scaled fp16 planes, mlp::split_weight_h3)
 //   act[i, :] = LeakyReLU(LayerNorm(z[i, :]) * gamma + beta),  stats[i] = (mean, rstd)   (EPI = ROW_LN)
 //
+// and the input-gradient GEMM of a hidden layer with the backward of its LayerNorm + LeakyReLU (EPI = ROW_LNB):
+//   dA[i, c]  = sum_o dZ'[i, o] W'[o, c]              (the next layer's dX: dZ' its pre-activation gradient,
+//                                                      W' its pre-split transposed planes)
+//   dZ[i, :]  = rstd (dH g - mean(dH g) - xhat mean(dH g xhat)),  dH = dA * LeakyReLU'(h)   (mlp::ln_act_bwd's
+//               formulas on xhat = (z - mean) rstd recomputed from this layer's z and stats)
+//   part[blk] = per-column sums over the block's 64 rows of dZ, dH xhat, dH (the Linear.bias / LayerNorm.weight /
+//               LayerNorm.bias gradient partials, ln_act_bwd's [blk][3][H] layout, reduced by mlp::reduce_batch)
+//
 // Arithmetic is the H3 scheme of mlp::gemm_x6 (A scaled by its tensor's power of two and split into fp16 h + l,
 // products l.h, h.l, h.h into one f32 accumulator per 16-deep k step, the same epilogue scaling), so z is
 // bit-identical to the 128 x 128 kernels'.  The LayerNorm reduces each row across the 4 waves (two passes: mean,
@@ -22,7 +30,7 @@
 namespace mlp {
 
 constexpr int RM = 64;  // rows per workgroup
-enum { ROW_PLAIN = 0, ROW_LN = 1 };
+enum { ROW_PLAIN = 0, ROW_LN = 1, ROW_LNB = 2 };
 
 struct RowArgs {
     const float* A;          // [I][lda] fp32, k contiguous
@@ -35,13 +43,16 @@ struct RowArgs {
     float* C;                // z [I][ldc]
     int64_t ldc;
     int I, N, K;
-    // ROW_LN
+    // ROW_LN / ROW_LNB
     const float* gamma;
     const float* beta;
     float slope;
-    float* act;              // [I][N]
-    float2* stats;           // [I] (mean, rstd)
-    float* amax_out;         // 64 shards of max |act| (the next GEMM's operand scale), or null
+    float* act;              // ROW_LN: [I][N]
+    float2* stats;           // [I] (mean, rstd): ROW_LN writes them, ROW_LNB reads them
+    float* amax_out;         // 64 shards of max |act| (ROW_LN) or |dZ| (ROW_LNB) for the next H3 GEMM, or null
+    // ROW_LNB: this layer's pre-norm z [I][N] and the column partials [gridDim][3][N]; C receives dZ
+    const float* Z;
+    float* part;
 };
 
 template <int RK, int NBJ>
@@ -169,17 +180,100 @@ __global__ void __launch_bounds__(256, 1) gemm_row(RowArgs g) {
             for (int r = 0; r < 16; r++) acc[ti][tj][r] = ldexpf(acc[ti][tj][r] * csc, -pa) + bj[tj];
     }
     auto rowof = [&](int ti, int r) { return 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * hk; };
+    if constexpr (EPI != ROW_LNB) {
 #pragma unroll
-    for (int ti = 0; ti < 2; ti++)
+        for (int ti = 0; ti < 2; ti++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int i = i0 + rowof(ti, r);
-            if (i < g.I) {
-                float* zr = g.C + (int64_t)i * g.ldc + cw0 + l32;
+            for (int r = 0; r < 16; r++) {
+                const int i = i0 + rowof(ti, r);
+                if (i < g.I) {
+                    float* zr = g.C + (int64_t)i * g.ldc + cw0 + l32;
 #pragma unroll
-                for (int tj = 0; tj < NBJ; tj++) zr[32 * tj] = acc[ti][tj][r];
+                    for (int tj = 0; tj < NBJ; tj++) zr[32 * tj] = acc[ti][tj][r];
+                }
+            }
+    }
+    if constexpr (EPI == ROW_LNB) {
+        // acc holds dA.  Pass 1: dH = dA * LeakyReLU'(h) (kept in acc), row sums of dH g and dH g xhat; pass 2:
+        // dZ, its column partials.  z is read twice (the second time from the cache), xhat recomputed with the
+        // forward's operations.
+        const float invN = 1.f / (float)G::N;
+        float gj[NBJ], bt[NBJ];
+#pragma unroll
+        for (int tj = 0; tj < NBJ; tj++) {
+            gj[tj] = g.gamma[cw0 + 32 * tj + l32];
+            bt[tj] = g.beta[cw0 + 32 * tj + l32];
+        }
+        __shared__ float red2[4][RM];
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int i = min(i0 + rowof(ti, r), g.I - 1);  // a row past I recomputes row I - 1 (not stored)
+                const float2 st = g.stats[i];
+                const float* zr = g.Z + (int64_t)i * G::N + cw0 + l32;
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int tj = 0; tj < NBJ; tj++) {
+                    const float xh = (zr[32 * tj] - st.x) * st.y;
+                    const float h = xh * gj[tj] + bt[tj];
+                    const float dh = h > 0.f ? acc[ti][tj][r] : acc[ti][tj][r] * g.slope;
+                    acc[ti][tj][r] = dh;
+                    const float gg = dh * gj[tj];
+                    s1 += gg;
+                    s2 += gg * xh;
+                }
+                s1 = half_sum(s1);
+                s2 = half_sum(s2);
+                if (l32 == 0) {
+                    red[w][rowof(ti, r)] = s1;
+                    red2[w][rowof(ti, r)] = s2;
+                }
+            }
+        __syncthreads();
+        float pz[NBJ], pg[NBJ], pb[NBJ];
+#pragma unroll
+        for (int tj = 0; tj < NBJ; tj++) pz[tj] = pg[tj] = pb[tj] = 0.f;
+        uint32_t vmax = 0;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = rowof(ti, r), i = i0 + row;
+                if (i >= g.I) continue;
+                const float m1 = (((red[0][row] + red[1][row]) + red[2][row]) + red[3][row]) * invN;
+                const float m2 = (((red2[0][row] + red2[1][row]) + red2[2][row]) + red2[3][row]) * invN;
+                const float2 st = g.stats[i];
+                const float* zr = g.Z + (int64_t)i * G::N + cw0 + l32;
+                float* dz = g.C + (int64_t)i * g.ldc + cw0 + l32;
+#pragma unroll
+                for (int tj = 0; tj < NBJ; tj++) {
+                    const float xh = (zr[32 * tj] - st.x) * st.y;
+                    const float dh = acc[ti][tj][r];
+                    const float d = st.y * (dh * gj[tj] - m1 - xh * m2);
+                    dz[32 * tj] = d;
+                    pz[tj] += d;
+                    pg[tj] += dh * xh;
+                    pb[tj] += dh;
+                    const uint32_t b = abs_bits(d);
+                    vmax = b > vmax ? b : vmax;
+                }
+            }
+        // the two half-waves hold the same columns' other rows
+        float* out = g.part + (int64_t)blockIdx.x * 3 * G::N + cw0 + l32;
+#pragma unroll
+        for (int tj = 0; tj < NBJ; tj++) {
+            const float z2 = pz[tj] + __shfl_xor(pz[tj], 32, 64);
+            const float g2 = pg[tj] + __shfl_xor(pg[tj], 32, 64);
+            const float b2 = pb[tj] + __shfl_xor(pb[tj], 32, 64);
+            if (hk == 0) {
+                out[32 * tj] = z2;
+                out[G::N + 32 * tj] = g2;
+                out[2 * G::N + 32 * tj] = b2;
             }
         }
+        if (g.amax_out) h3_amax_commit(g.amax_out, vmax);
+    }
     if constexpr (EPI == ROW_LN) {
         const float invN = 1.f / (float)G::N;
         float mean[2][16], rs[2][16];
