@@ -12,16 +12,19 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
-_lib = None
+# variant "libm": the same restatement with the host libm in place of the deterministic sin / cos / atan /
+# atan2 / asin kernels (include/rlgpu_detmath.h RLGPU_DETMATH_LIBM), for tests/test_detmath_bound.py only
+LIB_PATHS = {"": LIB_PATH, "libm": os.path.join(_HERE, "build", "liboracle_libm.so")}
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
-        _lib = ctypes.CDLL(LIB_PATH)
-    return _lib
+def lib(variant=""):
+    if variant not in _libs:
+        path = LIB_PATHS[variant]
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        _libs[variant] = ctypes.CDLL(path)
+    return _libs[variant]
 
 
 def _p(a):
@@ -79,15 +82,16 @@ class EnvSet:
     """CPU restatement of RLGC::EnvSet with the ExampleMain plugin set (2v2, tickSkip 8, actionDelay 7)."""
 
     def __init__(self, num_arenas, seed=1234, tick_skip=8, action_delay=7, threads=1, max_episode_steps=0,
-                 mesh=None, rewards=None, terminals=None, arith=0, arena_offset=0, state_setter=0):
+                 mesh=None, rewards=None, terminals=None, arith=0, arena_offset=0, state_setter=0, variant=""):
         """mesh: (tris [N, 9] float32 bullet units, object_ntris int32 [K]) or an object with
         .tris / .object_ntris (rlgpu.mesh.ArenaMesh); None = the built-in synthetic mesh.
         rewards / terminals: structured arrays of rlgpu_reward_spec / rlgpu_terminal_spec records
         (include/rlgpu_env.h), None = ExampleMain's lists (the oracle restates them itself).
         arith: the reference build's Bullet arithmetic (include/rlgpu_arith.h: 0 MSVC x64, 1 GCC x86-64,
         2 scalar).  arena_offset: global index of arena 0 (rlgpu_envset_config.arena_offset).
-        state_setter: 0 KickoffState, 1 FuzzedKickoffState (rlgpu_envset_config.state_setter)."""
-        L = lib()
+        state_setter: 0 KickoffState, 1 FuzzedKickoffState (rlgpu_envset_config.state_setter).
+        variant: "" the oracle, "libm" its host-libm twin (lib())."""
+        L = lib(variant)
         L.oracle_env_create.restype = ctypes.c_void_p
         L.oracle_env_create.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int]
@@ -226,6 +230,22 @@ def sampler_probs(logits16, masks, seed, step, row0=0, f16=False):
                   ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     f(_p(lg), _p(mk), n, A, seed, step, row0, int(f16), _p(pr), _p(r))
     return pr, r
+
+
+TRIG_OPS = {"sin": 0, "cos": 1, "atan2": 2, "asin": 3, "atan": 4}
+
+
+def detmath_trig(op, x, y=None, variant=""):
+    """rs_sinf / rs_cosf / rs_atan2f(y, x) / rs_asinf / rs_atanf (include/rlgpu_detmath.h) over an array;
+    variant "libm" gives the host libm's sinf / cosf / atan2f / asinf / atanf instead."""
+    x = np.ascontiguousarray(x, np.float32)
+    yy = np.ascontiguousarray(x if y is None else y, np.float32)
+    out = np.empty_like(x)
+    f = lib(variant).oracle_detmath_trig
+    f.restype = None
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    f(TRIG_OPS[op], _p(x), _p(yy), x.size, _p(out))
+    return out
 
 
 def detmath_exp_log(x):

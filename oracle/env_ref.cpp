@@ -409,6 +409,9 @@ static Plugins example_main_plugins() {
 // SaveBoostReward's powf(boost / 100, exponent): 0.5 as sqrtf (ExampleMain), else exp(b log a) on the
 // deterministic kernels shared with the device (include/rlgpu_detmath.h)
 static float powf_det(float a, float b) {
+#ifdef RLGPU_DETMATH_LIBM
+    return powf(a, b);  // the reference's call, host libm (tests/test_detmath_bound.py)
+#endif
     if (b == 0.5f) return std::sqrt(a);
     if (b == 0.f) return 1.f;
     if (a == 0.f) return b > 0.f ? 0.f : std::numeric_limits<float>::infinity();

@@ -155,6 +155,24 @@ void oracle_sampler_probs(const uint16_t* logits, const uint8_t* masks, int64_t 
 }
 
 /* rs_expf / rs_logf over arrays (known-answer tests of the shared kernels against libm) */
+/* rs_sinf / rs_cosf / rs_atan2f / rs_asinf over arrays (op 0 sin x, 1 cos x, 2 atan2(y, x), 3 asin x with
+ * sqrtf(1 - x^2) as the simulator forms it, 4 atan x); liboracle_libm.so returns the host libm's values */
+void oracle_detmath_trig(int op, const float* x, const float* y, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++) {
+        switch (op) {
+        case 0: out[i] = rs_sinf(x[i]); break;
+        case 1: out[i] = rs_cosf(x[i]); break;
+        case 2: out[i] = rs_atan2f(y[i], x[i]); break;
+        case 3: {
+            const float t = 1.f - x[i] * x[i];
+            out[i] = rs_asinf(x[i], sqrtf(t > 0.f ? t : 0.f));
+            break;
+        }
+        default: out[i] = rs_atanf(x[i]); break;
+        }
+    }
+}
+
 void oracle_detmath_exp_log(const float* x, int64_t n, float* ex, float* lg) {
     for (int64_t i = 0; i < n; i++) {
         if (ex) ex[i] = rs_expf(x[i]);

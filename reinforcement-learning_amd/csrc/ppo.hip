@@ -128,6 +128,18 @@ inline int row_gemm() {
     static const int v = env_int("RLGPU_ROW_GEMM", 1);
     return v;
 }
+// the full-row kernel's ring: RLGPU_ROW_GEMM=1 -> 2 stages of 32 k, 2 -> 4 stages of 16 k (3 in flight)
+template <int EPI>
+void launch_row(int N, int n, hipStream_t s, const mlp::RowArgs& a) {
+    const dim3 grid(ceil_div(n, mlp::RM)), blk(256);
+    if (row_gemm() == 2) {
+        if (N == 512) hipLaunchKernelGGL((mlp::gemm_row<16, 4, 4, EPI>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((mlp::gemm_row<16, 4, 2, EPI>), grid, blk, 0, s, a);
+    } else {
+        if (N == 512) hipLaunchKernelGGL((mlp::gemm_row<32, 2, 4, EPI>), grid, blk, 0, s, a);
+        else hipLaunchKernelGGL((mlp::gemm_row<32, 2, 2, EPI>), grid, blk, 0, s, a);
+    }
+}
 inline int lnf_variant() {
     static const int v = env_int("RLGPU_LNF_VARIANT", 0);
     return v;
@@ -647,10 +659,7 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
             {
                 // flops of the GEMM (the LayerNorm's bytes ride along in the same launch)
                 ktime::Span span(ktime::FWD_GEMM, 2.0 * n * (double)L.out * L.in, s);
-                if (L.out == 512)
-                    hipLaunchKernelGGL((mlp::gemm_row<32, 2, 4, mlp::ROW_LN>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
-                else
-                    hipLaunchKernelGGL((mlp::gemm_row<32, 2, 2, mlp::ROW_LN>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
+                launch_row<mlp::ROW_LN>(L.out, n, s, a);
                 RLGPU_CHECK_HIP(hipGetLastError());
             }
             in = m.act[l];
@@ -752,10 +761,7 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         a.Z = m.xhat[l];
         a.part = m.cpart_l[l];
         ktime::Span span(ktime::FWD_GEMM, 2.0 * n * (double)L.out * src.out, s);
-        if (L.out == 512)
-            hipLaunchKernelGGL((mlp::gemm_row<32, 2, 4, mlp::ROW_LNB>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((mlp::gemm_row<32, 2, 2, mlp::ROW_LNB>), dim3(ceil_div(n, mlp::RM)), dim3(256), 0, s, a);
+        launch_row<mlp::ROW_LNB>(L.out, n, s, a);
         RLGPU_CHECK_HIP(hipGetLastError());
         fusedDZ[l] = dst;
     };
