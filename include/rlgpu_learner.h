@@ -235,6 +235,14 @@ enum { RLGPU_HOOK_AFTER_STEP = 0, RLGPU_HOOK_AFTER_RESET = 1 };
 typedef int (*rlgpu_step_hook_fn)(void* user, int32_t phase);
 int rlgpu_learner_set_step_hook(rlgpu_learner* h, rlgpu_step_hook_fn fn, void* user);
 
+/* Gradient tap (monitoring / tests; PPOLearner.cpp:990-1000's point between the all-reduce and
+ * clip_grad_norm_): after each batch's gradients are summed over the ranks and before they are clipped
+ * and stepped, fn receives the device pointer of the flat fp32 gradient [n] (the stream synchronised; the
+ * buffer is read-only for fn), the epoch and the batch's index within it.  A non-zero return fails the
+ * iteration.  fn null removes the tap. */
+typedef int (*rlgpu_grad_hook_fn)(void* user, const float* grads, int64_t n, int32_t epoch, int32_t batch);
+int rlgpu_learner_set_grad_hook(rlgpu_learner* h, rlgpu_grad_hook_fn fn, void* user);
+
 int rlgpu_learner_get_stats(rlgpu_learner* h, rlgpu_learner_stats* out);
 int rlgpu_learner_set_stats(rlgpu_learner* h, const rlgpu_learner_stats* in);
 /* PPO report metrics accumulated since the last reset (PPOLearner.cpp:537-566): h_out receives

@@ -2,6 +2,7 @@
 //
 // One launch = one (half) env step for every arena: LDS-resident arena records, quarter-wave
 // teams per arena (env_kernel.hpp), phases of Arena::Step separated by workgroup barriers.
+#include <mutex>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -318,13 +319,23 @@ extern "C" int rlgpu_envset_default_plugins(rlgpu_reward_spec* rewards, int32_t*
 }
 
 namespace {
-bool g_const_ready = false;
-bool g_rsqrt_ready = false;
+// the kernels' __constant__ symbols live once per device: uploaded the first time a set is created on a
+// device, under one lock (sets may be created from several threads, on several devices of one process)
+std::mutex g_init_mu;
+std::vector<char> g_const_ready, g_rsqrt_ready;  // indexed by HIP device
+
+bool device_flag(std::vector<char>& v, int* dev) {
+    RLGPU_CHECK_HIP(hipGetDevice(dev));
+    if ((int)v.size() <= *dev) v.resize(*dev + 1, 0);
+    return v[*dev] != 0;
+}
 
 // the x86 modes' rsqrtss: this host's table (host/x86_arith.cpp) in device memory, its pointer in the
-// kernels' kRsqrtLut (once per process; the table is the host CPU's, the same for every set)
+// kernels' kRsqrtLut (once per device; the table is the host CPU's, the same for every set)
 void ensure_rsqrt() {
-    if (g_rsqrt_ready) return;
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    int dev = 0;
+    if (device_flag(g_rsqrt_ready, &dev)) return;
     int bits = 0;
     const std::vector<uint32_t>& t = rlgpu::x86_rsqrt_table_or_throw(&bits);
     uint32_t* d = nullptr;
@@ -335,17 +346,19 @@ void ensure_rsqrt() {
     const rl::EnvConst k = rl::make_env_const();
     rl::env_k0_upload(k, &L);
     rl::env_k1_upload(k, &L);
-    g_rsqrt_ready = true;
+    g_rsqrt_ready[dev] = 1;
 }
 
 void ensure_const() {
-    if (g_const_ready) return;
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    int dev = 0;
+    if (device_flag(g_const_ready, &dev)) return;
     rl::EnvConst k = rl::make_env_const();
     RLGPU_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rl::C), &k, sizeof k));
     rl::env_k0_upload(k, nullptr);
     rl::env_k1_upload(k, nullptr);
     rl::env_k2_upload(k, nullptr);
-    g_const_ready = true;
+    g_const_ready[dev] = 1;
 }
 
 void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {

@@ -17,18 +17,15 @@
 //     kernel (21 B per agent-step algorithmic).
 //   * flat (episode-concatenated, the reference's own input): A_t = d_t + c_t*A_{t+1} is a
 //     composition of affine maps, (cL,dL)o(cR,dR) = (cL*cR, dL + cL*dR).  Terminals make c=0,
-//     so one non-segmented reverse scan is exactly the segmented GAE.  Chunked 3-pass scan:
-//     trunc counts -> chunk summaries -> chunk carries -> apply.  Within a chunk every lane
-//     composes 8 contiguous elements, a 64-lane shuffle suffix-scan combines lanes and LDS
-//     combines the 4 waves of a 256-thread workgroup.
+//     so one non-segmented reverse scan is exactly the segmented GAE.  Three streaming passes
+//     over 4096-element tiles (tile summaries with the truncation value left symbolic -> one
+//     workgroup resolves truncation indices and tile carries -> apply), float4 accesses, a
+//     fixed composition order (the same result on every run); see k_flat_summary.
 #include "common.hpp"
 #include "../../include/rlgpu_gae.h"
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kPerThread = 8;
-constexpr int kChunk = kThreads * kPerThread;  // 2048 elements per workgroup
 constexpr int8_t kNormal = 1, kTruncated = 2;   // RLGC::TerminalType (TerminalCondition.h:6-11)
 
 struct Aff {
@@ -52,6 +49,70 @@ struct GaeParams {
     float clip_range;
 };
 
+// ---- flat layout: three passes, each a streaming pass over 4096-element tiles ---------------------------------
+// A tile is 4 rounds of 1024 elements; in a round thread l owns elements 4l .. 4l + 3 (one float4 of each
+// array: every load and store of a wave is one contiguous 1 KB).  Pass 1 (k_flat_summary) composes each
+// tile's maps and counts its truncations; pass 2 (k_flat_carry, one workgroup) turns the counts into each
+// tile's first truncation index and the maps into the value entering each tile from the right; pass 3
+// (k_flat_apply) rebuilds the maps with the exact truncation values and writes A, target, R.  The
+// composition order is fixed by the tiling, so the result is the same on every run.
+//
+// The summary cannot know its truncation values (their index is a forward count over the tiles to its
+// left), so it composes maps of the form x -> c x + d + b T, T = the value of the tile's first truncation:
+// the tile's first terminal zeroes every coefficient to its right, so only that T can survive.
+constexpr int kFT = 256, kFV = 4, kFRounds = 4;
+constexpr int kFRound = kFT * kFV, kFTile = kFRound * kFRounds;
+constexpr int kCT = 1024;  // the carry pass's workgroup
+
+struct Aff3 {
+    float c, d, b;
+};
+__device__ __forceinline__ Aff3 compose3(Aff3 L, Aff3 R) { return {L.c * R.c, L.d + L.c * R.d, L.b + L.c * R.b}; }
+
+// one thread's 4 elements of a round starting at i0 (tail elements past M load as NORMAL zeros: their
+// maps are never applied and the tile's real maps end before them)
+struct Quad {
+    float r[kFV], v[kFV];
+    int8_t t[kFV];
+    float vnext;  // vals[i0 + 4] (0 past the end)
+};
+template <bool VEC>
+__device__ __forceinline__ void load_quad(const GaeParams& p, int64_t i0, Quad& q) {
+    if (VEC && i0 + kFV <= p.M) {
+        const float4 r = *reinterpret_cast<const float4*>(p.rews + i0);
+        const float4 v = *reinterpret_cast<const float4*>(p.vals + i0);
+        const uint32_t t = *reinterpret_cast<const uint32_t*>(p.terms + i0);
+        q.r[0] = r.x, q.r[1] = r.y, q.r[2] = r.z, q.r[3] = r.w;
+        q.v[0] = v.x, q.v[1] = v.y, q.v[2] = v.z, q.v[3] = v.w;
+#pragma unroll
+        for (int j = 0; j < kFV; j++) q.t[j] = (int8_t)(t >> (8 * j));
+    } else {
+#pragma unroll
+        for (int j = 0; j < kFV; j++) {
+            const bool in = i0 + j < p.M;
+            q.r[j] = in ? p.rews[i0 + j] : 0.f;
+            q.v[j] = in ? p.vals[i0 + j] : 0.f;
+            q.t[j] = in ? p.terms[i0 + j] : kNormal;
+        }
+    }
+    // the next element's value: the right neighbour lane's first, lane 63 (and the array's end) from memory
+    const float nb = __shfl_down(q.v[0], 1, 64);
+    q.vnext = ((threadIdx.x & 63) != 63) ? nb : (i0 + kFV < p.M ? p.vals[i0 + kFV] : 0.f);
+    if (i0 + kFV >= p.M) q.vnext = 0.f;
+}
+
+__device__ __forceinline__ float norm_rew(const GaeParams& p, float rew) {
+    float n = rew;
+    if (p.normalize) {
+        n = rew * p.inv_std;
+        if (p.clip) n = fminf(fmaxf(n, -p.clip_range), p.clip_range);
+    }
+    return n;
+}
+
+// the next value of element j of the quad (non-terminal: V[i + 1], 0 on the array's last step)
+__device__ __forceinline__ float next_val(const Quad& q, int j) { return j + 1 < kFV ? q.v[j + 1] : q.vnext; }
+
 // Inclusive suffix scan over the 64 lanes of a wave: S_l = f_l o ... o f_63.
 __device__ __forceinline__ Aff wave_suffix_inclusive(Aff a, int lane) {
 #pragma unroll
@@ -62,215 +123,303 @@ __device__ __forceinline__ Aff wave_suffix_inclusive(Aff a, int lane) {
     return a;
 }
 
-// Exclusive forward prefix sum of an int over a 256-thread block.
-__device__ __forceinline__ int block_excl_prefix_int(int v, int* smem4) {
-    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int inc = v;
+// ordered wave reduction (lane 0 receives f_0 o f_1 o ... o f_63)
+__device__ __forceinline__ Aff3 wave_reduce3(Aff3 a) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        int o = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += o;
+        Aff3 o{__shfl_down(a.c, off, 64), __shfl_down(a.d, off, 64), __shfl_down(a.b, off, 64)};
+        if ((threadIdx.x & 63) + off < 64) a = compose3(a, o);
     }
-    if (lane == 63) smem4[wave] = inc;
-    __syncthreads();
-    int base = 0;
-    for (int w = 0; w < wave; ++w) base += smem4[w];
-    __syncthreads();
-    return base + inc - v;
+    return a;
+}
+__device__ __forceinline__ Aff wave_reduce(Aff a) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        Aff o = shfl_down_aff(a, off);
+        if ((threadIdx.x & 63) + off < 64) a = compose(a, o);
+    }
+    return a;
 }
 
-// Block-wide exclusive suffix composition for two affine maps (adv + ret chains).
-// Returns for this thread the composition of all threads to its right in the block.
-__device__ __forceinline__ void block_suffix_excl(Aff& a, Aff& r, Aff* smem_a, Aff* smem_r) {
-    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    Aff sa = wave_suffix_inclusive(a, lane);
-    Aff sr = wave_suffix_inclusive(r, lane);
+// Pass 1: per tile, the composed adv map (c, d, b), the composed return map, the truncation count and the
+// clip-portion partial sums (sum |r / std|, sum |clip(r / std)|).
+template <bool VEC>
+__global__ void __launch_bounds__(kFT) k_flat_summary(GaeParams p, float4* sumA, float2* sumR, int* cnt, float2* clipp) {
+    __shared__ Aff3 sa[kFRounds][kFT / 64];
+    __shared__ Aff sr[kFRounds][kFT / 64];
+    __shared__ float sc[3][kFT / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t0 = (int64_t)blockIdx.x * kFTile;
+    int c = 0;
+    float sabs = 0.f, sclip = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFRounds; q++) {
+        const int64_t i0 = t0 + (int64_t)q * kFRound + threadIdx.x * kFV;
+        Quad e;
+        load_quad<VEC>(p, i0, e);
+        Aff3 A{1.f, 0.f, 0.f};
+        Aff R{1.f, 0.f};
+#pragma unroll
+        for (int j = kFV - 1; j >= 0; j--) {
+            const int8_t t = e.t[j];
+            const float n = norm_rew(p, e.r[j]);
+            if (p.normalize && i0 + j < p.M) {
+                sabs += fabsf(e.r[j] * p.inv_std);
+                sclip += fabsf(n);
+            }
+            const bool term = t == kNormal || t == kTruncated;
+            const float nd = term ? 0.f : 1.f;
+            Aff3 f;
+            if (t == kTruncated) {
+                f = {0.f, n - e.v[j], p.gamma};  // (n + gamma T) - V with T symbolic
+                c += i0 + j < p.M;
+            } else {
+                const float next = t == kNormal ? 0.f : next_val(e, j);
+                f = {p.gamma_lambda * nd, (n + p.gamma * next) - e.v[j], 0.f};
+            }
+            A = compose3(f, A);
+            R = compose(Aff{p.gamma * nd, e.r[j]}, R);
+        }
+        A = wave_reduce3(A);
+        R = wave_reduce(R);
+        if (lane == 0) {
+            sa[q][w] = A;
+            sr[q][w] = R;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_down(c, o, 64);
+        sabs += __shfl_down(sabs, o, 64);
+        sclip += __shfl_down(sclip, o, 64);
+    }
+    if (lane == 0) {
+        sc[0][w] = (float)c;
+        sc[1][w] = sabs;
+        sc[2][w] = sclip;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Aff3 A{1.f, 0.f, 0.f};
+        Aff R{1.f, 0.f};
+        for (int q = kFRounds - 1; q >= 0; q--)
+            for (int ww = kFT / 64 - 1; ww >= 0; ww--) {
+                A = compose3(sa[q][ww], A);
+                R = compose(sr[q][ww], R);
+            }
+        sumA[blockIdx.x] = make_float4(A.c, A.d, A.b, 0.f);
+        sumR[blockIdx.x] = make_float2(R.c, R.d);
+        float cs = 0.f, s1 = 0.f, s2 = 0.f;
+        for (int ww = 0; ww < kFT / 64; ww++) {
+            cs += sc[0][ww];
+            s1 += sc[1][ww];
+            s2 += sc[2][ww];
+        }
+        cnt[blockIdx.x] = (int)cs;
+        clipp[blockIdx.x] = make_float2(s1, s2);
+    }
+}
+
+struct FlatResult {
+    int64_t total;  // truncations found (GAE.cpp:196-197 checks it against the values given)
+    float sabs, sclip;
+};
+
+// Pass 2 (one workgroup): base[t] = truncations before tile t (base[n] = total), carry[t] = (A, R) entering
+// tile t from its right neighbour, the clip sums; all in a fixed order.
+__global__ void __launch_bounds__(kCT) k_flat_carry(const float4* sumA, const float2* sumR, const int* cnt,
+                                                    const float2* clipp, int n, const float* trunc_vals,
+                                                    int64_t num_truncs, int64_t* base, float2* carry, FlatResult* res) {
+    __shared__ int64_t s_cnt[kCT / 64];
+    __shared__ Aff s_a[kCT / 64], s_r[kCT / 64];
+    __shared__ float s_c[2][kCT / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int per = (n + kCT - 1) / kCT, b0 = threadIdx.x * per, b1 = min(b0 + per, n);
+    // forward exclusive prefix of the counts
+    int64_t mine = 0;
+    float s1 = 0.f, s2 = 0.f;
+    for (int b = b0; b < b1; b++) {
+        mine += cnt[b];
+        const float2 cp = clipp[b];
+        s1 += cp.x;
+        s2 += cp.y;
+    }
+    int64_t inc = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t o = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += o;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_down(s1, o, 64);
+        s2 += __shfl_down(s2, o, 64);
+    }
+    if (lane == 63) s_cnt[w] = inc;
+    if (lane == 0) {
+        s_c[0][w] = s1;
+        s_c[1][w] = s2;
+    }
+    __syncthreads();
+    int64_t run = inc - mine;
+    for (int ww = 0; ww < w; ww++) run += s_cnt[ww];
+    // the tiles' resolved maps, composed right to left over this thread's range
+    Aff ta{1.f, 0.f}, tr{1.f, 0.f};
+    {
+        int64_t k = run;
+        for (int b = b0; b < b1; b++) {
+            base[b] = k;
+            k += cnt[b];
+        }
+        if (b0 < n && b1 == n) {
+            base[n] = k;
+            float a1 = 0.f, a2 = 0.f;
+            for (int ww = 0; ww < kCT / 64; ww++) {
+                a1 += s_c[0][ww];
+                a2 += s_c[1][ww];
+            }
+            res->total = k;
+            res->sabs = a1;
+            res->sclip = a2;
+        }
+    }
+    auto resolved = [&](int b, int64_t kb) {
+        const float4 s = sumA[b];
+        const float T = (s.z != 0.f && kb < num_truncs) ? trunc_vals[kb] : 0.f;
+        return Aff{s.x, s.y + s.z * T};
+    };
+    for (int b = b1 - 1; b >= b0; b--) {
+        ta = compose(resolved(b, base[b]), ta);
+        const float2 r = sumR[b];
+        tr = compose(Aff{r.x, r.y}, tr);
+    }
+    // exclusive suffix over the threads: the composition of every range to this one's right
+    Aff sa = wave_suffix_inclusive(ta, lane), sr = wave_suffix_inclusive(tr, lane);
     Aff ea = shfl_down_aff(sa, 1), er = shfl_down_aff(sr, 1);
     if (lane == 63) ea = er = Aff{1.f, 0.f};
     if (lane == 0) {
-        smem_a[wave] = sa;
-        smem_r[wave] = sr;
+        s_a[w] = sa;
+        s_r[w] = sr;
     }
     __syncthreads();
-    Aff ta{1.f, 0.f}, tr{1.f, 0.f};
-    for (int w = (kThreads / 64) - 1; w > wave; --w) {
-        ta = compose(smem_a[w], ta);
-        tr = compose(smem_r[w], tr);
+    Aff xa{1.f, 0.f}, xr{1.f, 0.f};
+    for (int ww = kCT / 64 - 1; ww > w; ww--) {
+        xa = compose(s_a[ww], xa);
+        xr = compose(s_r[ww], xr);
     }
-    __syncthreads();
-    a = compose(ea, ta);
-    r = compose(er, tr);
-}
-
-// Builds the 8 per-element maps of this thread.  trunc_base = global index of the first
-// truncation at or after this thread's first element.
-__device__ __forceinline__ void element_maps(const GaeParams& p, int64_t i0, int64_t trunc_base,
-                                             Aff* fa, Aff* fr, float* nrew) {
-    int64_t k = trunc_base;
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-        int64_t i = i0 + j;
-        if (i >= p.M) {
-            fa[j] = fr[j] = Aff{1.f, 0.f};
-            nrew[j] = 0.f;
-            continue;
-        }
-        int8_t t = p.terms[i];
-        float rew = p.rews[i];
-        float n = rew;
-        if (p.normalize) {
-            n = rew * p.inv_std;
-            if (p.clip) n = fminf(fmaxf(n, -p.clip_range), p.clip_range);
-        }
-        nrew[j] = n;
-        float nd = (t == kNormal || t == kTruncated) ? 0.f : 1.f;
-        float next;
-        if (t == kNormal) next = 0.f;
-        else if (t == kTruncated) next = (k < p.num_truncs) ? p.trunc_vals[k] : 0.f;
-        else if (i < p.M - 1) next = p.vals[i + 1];
-        else next = 0.f;
-        if (t == kTruncated) ++k;
-        float delta = (n + p.gamma * next) - p.vals[i];
-        fa[j] = Aff{p.gamma_lambda * nd, delta};
-        fr[j] = Aff{p.gamma * nd, rew};
-    }
-}
-
-__global__ void __launch_bounds__(kThreads) k_trunc_count(const int8_t* terms, int64_t M, int* counts) {
-    __shared__ int s[4];
-    int64_t i0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPerThread;
-    int c = 0;
-    for (int j = 0; j < kPerThread; ++j)
-        if (i0 + j < M && terms[i0 + j] == kTruncated) ++c;
-    int excl = block_excl_prefix_int(c, s);
-    if (threadIdx.x == kThreads - 1) counts[blockIdx.x] = excl + c;
-}
-
-// Single workgroup: exclusive prefix of chunk trunc counts (sequential per thread segment).
-__global__ void __launch_bounds__(kThreads) k_scan_counts(const int* counts, int nchunks, int64_t* offsets,
-                                                          int64_t* total) {
-    __shared__ int s[4];
-    int per = (nchunks + kThreads - 1) / kThreads;
-    int b0 = threadIdx.x * per;
-    int local = 0;
-    for (int b = b0; b < b0 + per && b < nchunks; ++b) local += counts[b];
-    int base = block_excl_prefix_int(local, s);
-    int64_t run = base;
-    for (int b = b0; b < b0 + per && b < nchunks; ++b) {
-        offsets[b] = run;
-        run += counts[b];
-    }
-    if (threadIdx.x == kThreads - 1) *total = run;
-}
-
-// Pass 1: per-chunk composed maps (adv chain, return chain).
-__global__ void __launch_bounds__(kThreads) k_chunk_summary(GaeParams p, const int64_t* trunc_offsets,
-                                                            float4* summaries) {
-    __shared__ int s_int[4];
-    __shared__ Aff s_a[4], s_r[4];
-    int64_t i0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPerThread;
-    int c = 0;
-    for (int j = 0; j < kPerThread; ++j)
-        if (i0 + j < p.M && p.terms[i0 + j] == kTruncated) ++c;
-    int64_t tb = trunc_offsets[blockIdx.x] + block_excl_prefix_int(c, s_int);
-    Aff fa[kPerThread], fr[kPerThread];
-    float nrew[kPerThread];
-    element_maps(p, i0, tb, fa, fr, nrew);
-    Aff ta{1.f, 0.f}, tr{1.f, 0.f};
-#pragma unroll
-    for (int j = kPerThread - 1; j >= 0; --j) {
-        ta = compose(fa[j], ta);
-        tr = compose(fr[j], tr);
-    }
-    // Composition of the whole chunk = thread 0's map composed with everything to its right.
-    Aff ea = ta, er = tr;
-    block_suffix_excl(ea, er, s_a, s_r);
-    if (threadIdx.x == 0) {
-        Aff A = compose(ta, ea), R = compose(tr, er);
-        summaries[blockIdx.x] = make_float4(A.c, A.d, R.c, R.d);
-    }
-}
-
-// Pass 2 (single workgroup): carry-in value of each chunk = (chunks to the right)(0).
-__global__ void __launch_bounds__(kThreads) k_chunk_carry(const float4* summaries, int nchunks, float2* carry) {
-    __shared__ Aff s_a[4], s_r[4];
-    int per = (nchunks + kThreads - 1) / kThreads;
-    int b0 = threadIdx.x * per;
-    Aff ta{1.f, 0.f}, tr{1.f, 0.f};
-    for (int b = min(b0 + per, nchunks) - 1; b >= b0; --b) {
-        float4 s = summaries[b];
-        ta = compose(Aff{s.x, s.y}, ta);
-        tr = compose(Aff{s.z, s.w}, tr);
-    }
-    Aff ea = ta, er = tr;
-    block_suffix_excl(ea, er, s_a, s_r);
-    // Value entering this thread's right edge: (everything right of it)(0).
-    float va = ea.d, vr = er.d;
-    for (int b = min(b0 + per, nchunks) - 1; b >= b0; --b) {
+    ea = compose(ea, xa);
+    er = compose(er, xr);
+    float va = ea.d, vr = er.d;  // the value entering this range's right edge (0 past the array's end)
+    for (int b = b1 - 1; b >= b0; b--) {
         carry[b] = make_float2(va, vr);
-        float4 s = summaries[b];
-        va = s.y + s.x * va;
-        vr = s.w + s.z * vr;
+        const Aff a = resolved(b, base[b]);
+        const float2 r = sumR[b];
+        va = a.d + a.c * va;
+        vr = r.y + r.x * vr;
     }
 }
 
-// Pass 3: apply carries and write A, target, R; accumulate clip-portion sums.
-__global__ void __launch_bounds__(kThreads) k_apply(GaeParams p, const int64_t* trunc_offsets, const float2* carry,
-                                                    float* adv, float* target, float* ret, float* clip_sums) {
-    __shared__ int s_int[4];
-    __shared__ Aff s_a[4], s_r[4];
-    __shared__ float s_sum[2][4];
-    int64_t i0 = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kPerThread;
-    int c = 0;
-    for (int j = 0; j < kPerThread; ++j)
-        if (i0 + j < p.M && p.terms[i0 + j] == kTruncated) ++c;
-    int64_t tb = trunc_offsets[blockIdx.x] + block_excl_prefix_int(c, s_int);
-    Aff fa[kPerThread], fr[kPerThread];
-    float nrew[kPerThread];
-    element_maps(p, i0, tb, fa, fr, nrew);
-    Aff ta{1.f, 0.f}, tr{1.f, 0.f};
+// block-wide inclusive suffix sum of an int (threads l .. kFT - 1)
+__device__ __forceinline__ int block_suffix_int(int v, int* s4) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = kPerThread - 1; j >= 0; --j) {
-        ta = compose(fa[j], ta);
-        tr = compose(fr[j], tr);
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_down(v, off, 64);
+        if (lane + off < 64) v += o;
     }
-    Aff ea = ta, er = tr;
-    block_suffix_excl(ea, er, s_a, s_r);
+    if (lane == 0) s4[w] = v;
+    __syncthreads();
+    for (int ww = kFT / 64 - 1; ww > w; ww--) v += s4[ww];
+    return v;
+}
+
+// Pass 3: per tile, rounds right to left; exact maps (the truncation values by their forward index), the
+// carry composed in, A / target / R written as float4s.
+template <bool VEC>
+__global__ void __launch_bounds__(kFT) k_flat_apply(GaeParams p, const int64_t* base, const float2* carry, float* adv,
+                                                    float* target, float* ret) {
+    __shared__ int s_cnt[kFRounds][kFT / 64];
+    __shared__ Aff s_a[kFRounds][kFT / 64], s_r[kFRounds][kFT / 64];
+    __shared__ float2 s_x[kFRounds];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t0 = (int64_t)blockIdx.x * kFTile;
+    const int64_t knext = base[blockIdx.x + 1];  // truncations before the next tile
     float2 cin = carry[blockIdx.x];
-    float xa = ea.d + ea.c * cin.x;
-    float xr = er.d + er.c * cin.y;
-    float sabs = 0.f, sclip = 0.f;
+    int after = 0;  // truncations in this tile's rounds to the right of the current one
+    for (int q = kFRounds - 1; q >= 0; q--) {
+        const int64_t i0 = t0 + (int64_t)q * kFRound + threadIdx.x * kFV;
+        Quad e;
+        load_quad<VEC>(p, i0, e);
+        int c = 0;
 #pragma unroll
-    for (int j = kPerThread - 1; j >= 0; --j) {
-        int64_t i = i0 + j;
-        xa = fa[j].d + fa[j].c * xa;
-        xr = fr[j].d + fr[j].c * xr;
-        if (i < p.M) {
-            adv[i] = xa;
-            ret[i] = xr;
-            target[i] = p.vals[i] + xa;
-            if (p.normalize) {
-                float raw = p.rews[i] * p.inv_std;
-                sabs += fabsf(raw);
-                sclip += fabsf(nrew[j]);
-            }
+        for (int j = 0; j < kFV; j++) c += (e.t[j] == kTruncated && i0 + j < p.M);
+        const int suf = block_suffix_int(c, s_cnt[q]);  // truncations at this thread's first element or later
+        int k_after = after + suf - c;  // truncations after this thread's 4 elements within the tile
+        Aff fa[kFV], fr[kFV];
+        float n[kFV];
+#pragma unroll
+        for (int j = kFV - 1; j >= 0; j--) {
+            const int8_t t = e.t[j];
+            n[j] = norm_rew(p, e.r[j]);
+            const bool term = t == kNormal || t == kTruncated;
+            const float nd = term ? 0.f : 1.f;
+            float next;
+            if (t == kNormal) next = 0.f;
+            else if (t == kTruncated) {
+                k_after += i0 + j < p.M;
+                const int64_t k = knext - k_after;  // the forward index of this truncation
+                next = (k >= 0 && k < p.num_truncs) ? p.trunc_vals[k] : 0.f;
+            } else next = next_val(e, j);
+            fa[j] = Aff{p.gamma_lambda * nd, (n[j] + p.gamma * next) - e.v[j]};
+            fr[j] = Aff{p.gamma * nd, e.r[j]};
         }
-    }
-    if (clip_sums && p.normalize) {
-        for (int off = 32; off > 0; off >>= 1) {
-            sabs += __shfl_down(sabs, off, 64);
-            sclip += __shfl_down(sclip, off, 64);
+        Aff ta{1.f, 0.f}, tr{1.f, 0.f};
+#pragma unroll
+        for (int j = kFV - 1; j >= 0; j--) {
+            ta = compose(fa[j], ta);
+            tr = compose(fr[j], tr);
         }
-        int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        // exclusive suffix over the block's threads, then the round's carry
+        Aff sa = wave_suffix_inclusive(ta, lane), sr = wave_suffix_inclusive(tr, lane);
+        Aff ea = shfl_down_aff(sa, 1), er = shfl_down_aff(sr, 1);
+        if (lane == 63) ea = er = Aff{1.f, 0.f};
         if (lane == 0) {
-            s_sum[0][wave] = sabs;
-            s_sum[1][wave] = sclip;
+            s_a[q][w] = sa;
+            s_r[q][w] = sr;
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            atomicAdd(&clip_sums[0], s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3]);
-            atomicAdd(&clip_sums[1], s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3]);
+        Aff xa{1.f, 0.f}, xr{1.f, 0.f};
+        for (int ww = kFT / 64 - 1; ww > w; ww--) {
+            xa = compose(s_a[q][ww], xa);
+            xr = compose(s_r[q][ww], xr);
         }
+        ea = compose(ea, xa);
+        er = compose(er, xr);
+        float va = ea.d + ea.c * cin.x, vr = er.d + er.c * cin.y;
+        float oa[kFV], ot[kFV], orr[kFV];
+#pragma unroll
+        for (int j = kFV - 1; j >= 0; j--) {
+            va = fa[j].d + fa[j].c * va;
+            vr = fr[j].d + fr[j].c * vr;
+            oa[j] = va;
+            ot[j] = e.v[j] + va;
+            orr[j] = vr;
+        }
+        if (VEC && i0 + kFV <= p.M) {
+            *reinterpret_cast<float4*>(adv + i0) = make_float4(oa[0], oa[1], oa[2], oa[3]);
+            *reinterpret_cast<float4*>(target + i0) = make_float4(ot[0], ot[1], ot[2], ot[3]);
+            *reinterpret_cast<float4*>(ret + i0) = make_float4(orr[0], orr[1], orr[2], orr[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < kFV; j++)
+                if (i0 + j < p.M) {
+                    adv[i0 + j] = oa[j];
+                    target[i0 + j] = ot[j];
+                    ret[i0 + j] = orr[j];
+                }
+        }
+        if (threadIdx.x == 0) s_x[q] = make_float2(va, vr);  // the value at the round's first element
+        __syncthreads();
+        cin = s_x[q];
+        after += s_cnt[q][0] + s_cnt[q][1] + s_cnt[q][2] + s_cnt[q][3];  // the round's truncations
     }
 }
 
@@ -419,27 +568,27 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
         RLGPU_REQUIRE(d_rews && d_terms && d_vals && d_adv && d_target && d_ret, "rlgpu_gae_flat: null pointer");
         RLGPU_REQUIRE(num_truncs == 0 || d_trunc_vals, "rlgpu_gae_flat: trunc values missing");
         hipStream_t s = rlgpu::as_stream(stream);
-        int nchunks = (int)rlgpu::ceil_div(num_returns, kChunk);
-        // scratch: counts(int) | offsets(i64) | total(i64) | summaries(f4) | carry(f2) | clip sums(f2)
+        const int n = (int)rlgpu::ceil_div(num_returns, kFTile);
+        // scratch: tile maps (f4, f2) | counts (i32) | clip partials (f2) | bases (i64, n + 1) | carries (f2) | result
         size_t bytes = 0;
-        auto take = [&](size_t n, size_t align) {
-            bytes = (bytes + align - 1) / align * align;
-            size_t off = bytes;
-            bytes += n;
+        auto take = [&](size_t sz) {
+            bytes = (bytes + 15) / 16 * 16;
+            const size_t off = bytes;
+            bytes += sz;
             return off;
         };
-        size_t o_counts = take(sizeof(int) * nchunks, 16), o_offs = take(sizeof(int64_t) * nchunks, 16),
-               o_total = take(sizeof(int64_t), 16), o_sum = take(sizeof(float4) * nchunks, 16),
-               o_carry = take(sizeof(float2) * nchunks, 16), o_clip = take(sizeof(float) * 2, 16);
+        const size_t o_a = take(sizeof(float4) * n), o_r = take(sizeof(float2) * n), o_c = take(sizeof(int) * n),
+                     o_p = take(sizeof(float2) * n), o_b = take(sizeof(int64_t) * (n + 1)),
+                     o_x = take(sizeof(float2) * n), o_res = take(sizeof(FlatResult));
         char* scratch = nullptr;
         RLGPU_CHECK_HIP(hipMallocAsync((void**)&scratch, bytes, s));
-        int* counts = (int*)(scratch + o_counts);
-        int64_t* offs = (int64_t*)(scratch + o_offs);
-        int64_t* total = (int64_t*)(scratch + o_total);
-        float4* sums = (float4*)(scratch + o_sum);
-        float2* carry = (float2*)(scratch + o_carry);
-        float* clip = (float*)(scratch + o_clip);
-        RLGPU_CHECK_HIP(hipMemsetAsync(clip, 0, sizeof(float) * 2, s));
+        float4* sumA = (float4*)(scratch + o_a);
+        float2* sumR = (float2*)(scratch + o_r);
+        int* cnt = (int*)(scratch + o_c);
+        float2* clipp = (float2*)(scratch + o_p);
+        int64_t* base = (int64_t*)(scratch + o_b);
+        float2* carry = (float2*)(scratch + o_x);
+        FlatResult* res = (FlatResult*)(scratch + o_res);
 
         GaeParams p;
         p.rews = d_rews;
@@ -455,18 +604,23 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
         p.gamma_lambda = gamma * lambda;
         p.clip_range = clip_range;
 
-        hipLaunchKernelGGL(k_trunc_count, dim3(nchunks), dim3(kThreads), 0, s, d_terms, num_returns, counts);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kThreads), 0, s, counts, nchunks, offs, total);
-        hipLaunchKernelGGL(k_chunk_summary, dim3(nchunks), dim3(kThreads), 0, s, p, offs, sums);
-        hipLaunchKernelGGL(k_chunk_carry, dim3(1), dim3(kThreads), 0, s, sums, nchunks, carry);
-        hipLaunchKernelGGL(k_apply, dim3(nchunks), dim3(kThreads), 0, s, p, offs, carry, d_adv, d_target, d_ret, clip);
+        // float4 / 4-byte accesses when every array is aligned for them (torch allocations are)
+        auto al = [](const void* q, uintptr_t a) { return ((uintptr_t)q % a) == 0; };
+        const bool vec = al(d_rews, 16) && al(d_vals, 16) && al(d_terms, 4) && al(d_adv, 16) && al(d_target, 16) &&
+                         al(d_ret, 16);
+        if (vec) hipLaunchKernelGGL(k_flat_summary<true>, dim3(n), dim3(kFT), 0, s, p, sumA, sumR, cnt, clipp);
+        else hipLaunchKernelGGL(k_flat_summary<false>, dim3(n), dim3(kFT), 0, s, p, sumA, sumR, cnt, clipp);
+        hipLaunchKernelGGL(k_flat_carry, dim3(1), dim3(kCT), 0, s, sumA, sumR, cnt, clipp, n, d_trunc_vals, num_truncs, base,
+                           carry, res);
+        if (vec) hipLaunchKernelGGL(k_flat_apply<true>, dim3(n), dim3(kFT), 0, s, p, base, carry, d_adv, d_target, d_ret);
+        else hipLaunchKernelGGL(k_flat_apply<false>, dim3(n), dim3(kFT), 0, s, p, base, carry, d_adv, d_target, d_ret);
         RLGPU_CHECK_HIP(hipGetLastError());
-        int64_t h_total = 0;
-        float h_clip[2] = {0.f, 0.f};
-        RLGPU_CHECK_HIP(hipMemcpyAsync(&h_total, total, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        RLGPU_CHECK_HIP(hipMemcpyAsync(h_clip, clip, sizeof(h_clip), hipMemcpyDeviceToHost, s));
+        FlatResult h{};
+        RLGPU_CHECK_HIP(hipMemcpyAsync(&h, res, sizeof h, hipMemcpyDeviceToHost, s));
         RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
         RLGPU_CHECK_HIP(hipStreamSynchronize(s));
+        const int64_t h_total = h.total;
+        const float h_clip[2] = {h.sabs, h.sclip};
         // GAE.cpp:196-197: truncation count must match the provided bootstrap values.
         if (num_truncs > 0 && h_total != num_truncs)
             throw rlgpu::Error(RLGPU_ERR_INVALID_ARG, "GAE: truncation count mismatch (" + std::to_string(h_total) +

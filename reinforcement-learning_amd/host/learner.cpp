@@ -552,11 +552,13 @@ void Learner::FeedReturnStat(const float* d_ret, const std::vector<int64_t>& idx
     }
 }
 
-void Learner::AllReduceGrads() {
-    if (!hasColl_) return;
+void Learner::AllReduceGrads(int epoch, int batch) {
+    if (!hasColl_ && !gradHook_) return;
     hipCheck(hipStreamSynchronize(s_), "sync");
-    if (coll_.allreduce_sum_f32(coll_.user, ppo_->grads(), ppo_->num_params()) != 0)
+    if (hasColl_ && coll_.allreduce_sum_f32(coll_.user, ppo_->grads(), ppo_->num_params()) != 0)
         throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: gradient all-reduce failed");
+    if (gradHook_ && gradHook_(gradHookUser_, ppo_->grads(), ppo_->num_params(), epoch, batch) != 0)
+        throw rlgpu::Error(RLGPU_ERR_STATE, "Learner: the gradient hook failed");
 }
 
 // batch advantage normalisation (PPOLearner.cpp:360-371): (mean, unbiased std) of the batch's
@@ -655,6 +657,7 @@ void Learner::Learn() {
             order = permRows_;
         }
         const auto ranges = trajMode() && hasColl_ ? trajRanges : BatchRanges(M, localBatch, cfg_.overbatching != 0);
+        int bi = 0;
         for (auto [b0, b1] : ranges) {
             const bool whole = !rows && b0 == 0 && b1 == M;
             BatchAdvantageStats(v.adv, whole ? nullptr : order + b0, b1 - b0);
@@ -662,7 +665,7 @@ void Learner::Learn() {
                 const int n = (int)std::min<int64_t>(cfg_.mini_batch_size, b1 - s0);
                 ppo_->Minibatch(v.obs, v.masks, v.actions, v.logp, v.adv, v.target, order, s0, n, batch);
             }
-            AllReduceGrads();  // RCCL over xGMI (via the collective), before clip_grad_norm_
+            AllReduceGrads(epoch, bi++);  // RCCL over xGMI (via the collective), before clip_grad_norm_
             ppo_->OptimizerStep();
         }
     }
@@ -1018,6 +1021,13 @@ extern "C" int rlgpu_learner_set_step_hook(rlgpu_learner* h, rlgpu_step_hook_fn 
     return rlgpu::guarded([&] {
         RLGPU_LEARNER(h);
         h->L->SetStepHook(fn, user);
+    });
+}
+
+extern "C" int rlgpu_learner_set_grad_hook(rlgpu_learner* h, rlgpu_grad_hook_fn fn, void* user) {
+    return rlgpu::guarded([&] {
+        RLGPU_LEARNER(h);
+        h->L->SetGradHook(fn, user);
     });
 }
 

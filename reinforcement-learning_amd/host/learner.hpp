@@ -171,6 +171,10 @@ public:
     void Start(int64_t iterations);  // Learner::Start loop (Learner.cpp:482-1056), a fixed count
 
     void SetOldTeam(int team) { oldTeam_ = team; }
+    void SetGradHook(rlgpu_grad_hook_fn fn, void* user) {
+        gradHook_ = fn;
+        gradHookUser_ = user;
+    }
     void SetStepHook(rlgpu_step_hook_fn fn, void* user) {
         hook_ = fn;
         hookUser_ = user;
@@ -186,7 +190,7 @@ public:
 
 private:
     void StepEnv(const int32_t* d_actions, const rlgpu_step_outputs& o);
-    void AllReduceGrads();
+    void AllReduceGrads(int epoch, int batch);
     void BatchAdvantageStats(const float* d_adv, const int32_t* d_idx, int64_t n);
     void CollectTrajectories();
     void ConsumeTrajectories();
@@ -203,6 +207,8 @@ private:
     bool envTiming_ = false;
     rlgpu_step_hook_fn hook_ = nullptr;  // host plugins / StepCallbackFn (rlgpu_learner_set_step_hook)
     void* hookUser_ = nullptr;
+    rlgpu_grad_hook_fn gradHook_ = nullptr;
+    void* gradHookUser_ = nullptr;
     int K_ = 1;                 // frames stacked (config C4)
     float* hist_ = nullptr;     // [K-1][P][OBS] frame history
     std::vector<hipEvent_t> ev_;

@@ -286,11 +286,14 @@ def load(learner, folder, allow_missing_models=True):
             name = MODEL_NAMES[mi]
             o, c = ppo.model_range(mi)
             p = model_path(path, name, "_OPTIM")
-            if not os.path.exists(p) or os.path.getsize(p) == 0 or not os.path.exists(OPTIM_TOOL):
+            usable = os.path.exists(p) and os.path.getsize(p) > 0
+            if usable and not os.path.exists(OPTIM_TOOL):
+                # a readable archive this build cannot parse: resetting would silently drop the saved moments
+                raise RuntimeError(f"{p} holds optimizer state but {OPTIM_TOOL} is not built (make -C "
+                                   "reinforcement-learning_amd optim)")
+            if not usable:
                 # the reference resets a model's optimizer whose state it cannot use (Models.cpp:168-186)
-                usable = os.path.exists(p) and os.path.getsize(p) > 0
-                why = "readable (rlgpu_optim_lt is not built)" if usable else "found"
-                warnings.warn(f"no optimizer {why} at {p}, optimizer will be reset")
+                warnings.warn(f"no optimizer found at {p}, optimizer will be reset")
                 m[o:o + c].zero_()
                 v[o:o + c].zero_()
                 continue

@@ -489,6 +489,8 @@ class Learner:
         return {k: float(t) / int(c) for k, t, c in zip(EnvSet.step_metric_names(), tot, cnt) if c}
 
     _HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32)
+    _GRAD_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                  ctypes.c_int32)
 
     def set_step_hook(self, fn):
         """rlgpu_learner_set_step_hook: fn(phase) after every collection step (0: post-step, pre-reset -- it may
@@ -511,6 +513,30 @@ class Learner:
         self._hook = self._HOOK(thunk)  # kept alive with the learner
         L.rlgpu_learner_set_step_hook.argtypes = [ctypes.c_void_p, self._HOOK, ctypes.c_void_p]
         _lib.check(L.rlgpu_learner_set_step_hook(self._h, self._hook, None), "rlgpu_learner_set_step_hook")
+
+    def set_grad_hook(self, fn):
+        """rlgpu_learner_set_grad_hook: fn(grads, epoch, batch) after each batch's gradient all-reduce, before
+        clip_grad_norm_ / AdamW; grads is a torch view of the flat fp32 gradient in HBM (valid during the call,
+        read-only).  None removes the tap.  An exception in fn fails the iteration."""
+        import torch
+        from ._lib import alias
+        L = _lib.lib()
+        if fn is None:
+            self._ghook = None
+            _lib.check(L.rlgpu_learner_set_grad_hook(self._h, None, None), "rlgpu_learner_set_grad_hook")
+            return
+
+        def thunk(_user, ptr, n, epoch, batch):
+            try:
+                fn(alias(ptr, (n,), torch.float32, self.device), int(epoch), int(batch))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported by the iteration's failure
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._ghook = self._GRAD_HOOK(thunk)
+        L.rlgpu_learner_set_grad_hook.argtypes = [ctypes.c_void_p, self._GRAD_HOOK, ctypes.c_void_p]
+        _lib.check(L.rlgpu_learner_set_grad_hook(self._h, self._ghook, None), "rlgpu_learner_set_grad_hook")
 
     def set_env_timing(self, on=True):
         _lib.check(_lib.lib().rlgpu_learner_set_env_timing(self._h, int(on)), "rlgpu_learner_set_env_timing")

@@ -224,3 +224,51 @@ def test_optimizer_archive_round_trip(tmp_path):
     assert step == 41
     np.testing.assert_array_equal(m2, m)
     np.testing.assert_array_equal(v2, v)
+
+
+def test_optimizer_archive_without_reader_raises(tmp_path, monkeypatch):
+    """A checkpoint holding <NAME>_OPTIM.lt but no RLGPU_OPTIM.safetensors, loaded by a build without
+    rlgpu_optim_lt: the load fails instead of silently resetting the saved AdamW moments."""
+    import json
+    import torch
+    seq = make_sequential(ARCH["obs"], ARCH["out"], ARCH["layers"], True)
+    d = tmp_path / "100"
+    d.mkdir()
+    ckpt.write_model(seq, str(d / "POLICY.lt"))
+    (d / "POLICY_OPTIM.lt").write_bytes(b"PK\x03\x04 not empty")
+    (d / ckpt.STATS_FILE).write_text(json.dumps({"total_timesteps": 100, "total_iterations": 1}))
+    n = sum(p.numel() for p in seq.parameters())
+
+    class _PPO:
+        models = (0,)
+        params = torch.zeros(n)
+
+        def model_sizes(self, mi):
+            return [p.numel() for p in seq.parameters()]
+
+        def model_range(self, mi):
+            return 0, n
+
+        def refresh_half(self):
+            pass
+
+        def optimizer_state(self):
+            return 0, torch.ones(n), torch.ones(n)
+
+        def set_optimizer_step(self, step):
+            assert step == 0
+
+    class _Learner:
+        total_steps = iteration = 0
+        return_stat = None
+        ppo = _PPO()
+
+    monkeypatch.setattr(ckpt, "OPTIM_TOOL", str(tmp_path / "no_such_tool"))
+    with pytest.raises(RuntimeError, match="holds optimizer state"):
+        ckpt.load(_Learner(), str(tmp_path))
+    # an empty archive is the reference's "cannot use": that model's optimizer resets, with a warning
+    (d / "POLICY_OPTIM.lt").write_bytes(b"")
+    L = _Learner()
+    with pytest.warns(UserWarning, match="optimizer will be reset"):
+        ckpt.load(L, str(tmp_path))
+    assert L.ppo.optimizer_state()[1].sum() == n  # a fresh tensor each call: nothing else touched

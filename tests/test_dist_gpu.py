@@ -41,7 +41,9 @@ def _worker(rank, world, port, q, kw, iters):
         per_rank = k.pop("per_rank", {})
         k.update(per_rank.get(rank, {}))
         L = Learner(LearnerConfig(train_against_old_versions=False, **k), device="cuda:0", rank=rank, world=world)
-        out = {"rank": rank, "rewards": [], "ret": []}
+        out = {"rank": rank, "rewards": [], "ret": [], "grads": []}
+        # the all-reduced flat gradient of each batch, before clip_grad_norm_ / AdamW (rlgpu_learner_set_grad_hook)
+        L.set_grad_hook(lambda g, epoch, batch: out["grads"].append((epoch, batch, g.cpu().numpy().copy())))
         for _ in range(iters):
             L.iterate()
             torch.cuda.synchronize()
@@ -86,8 +88,10 @@ def _run(world, kw, iters):
 
 @pytest.mark.timeout(400)
 def test_two_ranks_equal_one_rank(gpu):
-    """One iteration from the same initial parameters: the rollouts and return statistics are identical, the
-    parameters after the update agree to fp32 summation order.  (A second iteration would infer with those
+    """One iteration from the same initial parameters: the rollouts and return statistics are identical; the
+    first batch's all-reduced gradient (before clip_grad_norm_ / AdamW, the whole rollout in both jobs) agrees
+    normwise to 1e-5 -- the same rows, summed in a different order -- and the parameters after the update agree
+    to fp32 summation order.  (A second iteration would infer with those
     slightly different parameters, so its sampled actions -- and rollouts -- may differ where two actions
     are nearly tied.)"""
     import torch  # noqa: F401
@@ -100,6 +104,14 @@ def test_two_ranks_equal_one_rank(gpu):
     # the same return statistics (the same samples in the same order), bit for bit
     assert two[0]["ret"][0] == two[1]["ret"][0] == one["ret"][0], (two[0]["ret"][0], one["ret"][0])
     assert two[0]["steps"] == two[1]["steps"] == one["steps"]
+    # the gradient both jobs clip and step first: the sum over the ranks of each rank's rows' gradients
+    (e2, b2, g2), (e1, b1, g1) = two[0]["grads"][0], one["grads"][0]
+    assert (e2, b2) == (e1, b1) == (0, 0)
+    np.testing.assert_array_equal(g2, two[1]["grads"][0][2])  # every rank steps the same reduced gradient
+    assert len(two[0]["grads"]) == len(one["grads"])
+    rel = float(np.linalg.norm(g2.astype(np.float64) - g1) / np.linalg.norm(g1.astype(np.float64)))
+    print(f"first all-reduced gradient, 2 x 64 vs 1 x 128 arenas: ||diff|| / ||g|| = {rel:.3g}")
+    assert np.linalg.norm(g1) > 0 and rel <= 1e-5, rel
     np.testing.assert_array_equal(two[0]["params"], two[1]["params"])
     d = np.abs(two[0]["params"] - one["params"])
     lr = 2.5e-4

@@ -125,7 +125,7 @@ def test_gpu_flat_matches_golden(gpu, path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("m", [1, 7, 2048, 2049, 1 << 21])
+@pytest.mark.parametrize("m", [1, 7, 2048, 2049, 4095, 4096, 4097, 12289, 1 << 21, 1 << 24])
 def test_gpu_flat_sizes_and_edges(gpu, m):
     import torch
     from rlgpu import GAE
@@ -138,6 +138,42 @@ def test_gpu_flat_sizes_and_edges(gpu, m):
     np.testing.assert_allclose(adv.cpu().numpy(), ea, rtol=1e-5, atol=1e-5 * (np.abs(ea).max() + 1))
     np.testing.assert_allclose(ret.cpu().numpy(), er, rtol=1e-5, atol=1e-5 * (np.abs(er).max() + 1))
     assert cp == pytest.approx(ecp, rel=1e-4, abs=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_flat_tile_boundaries_unaligned_and_deterministic(gpu):
+    """The flat scan's 4096-element tiles: one episode running across many tiles with no terminal, truncations
+    on a tile's first and last elements and on adjacent steps, and the same inputs one element off 16-byte
+    alignment (the scalar-access variant); two calls agree bit for bit (a fixed composition order)."""
+    import torch
+    from rlgpu import GAE
+    m = 5 * 4096 + 77
+    rng = np.random.default_rng(3)
+    r = rng.standard_normal(m).astype(np.float32)
+    v = rng.standard_normal(m).astype(np.float32)
+    t = np.zeros(m, np.int8)
+    for i in (4096, 8191, 8192, 8193, 12288 + 4095, 16384, 16385, m - 1):
+        t[i] = 2
+    t[9000] = 1
+    tv = rng.standard_normal(int((t == 2).sum())).astype(np.float32)
+    ea, et, er, ecp, st = oracle.gae_flat(r, t, v, tv, 0.99, 0.95, 1.7, 5.0)
+    assert st == 0
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    outs = []
+    for off in (0, 1):
+        pad = lambda a: np.concatenate([np.zeros(off, a.dtype), a])  # noqa: E731
+        rr, tt, vv = d(pad(r))[off:], d(pad(t))[off:], d(pad(v))[off:]
+        for _ in range(2):
+            adv, tgt, ret, cp = GAE.compute(rr, tt, vv, d(tv), 0.99, 0.95, 1.7, 5.0)
+            np.testing.assert_allclose(adv.cpu().numpy(), ea, rtol=1e-5, atol=1e-5 * (np.abs(ea).max() + 1))
+            np.testing.assert_allclose(ret.cpu().numpy(), er, rtol=1e-5, atol=1e-5 * (np.abs(er).max() + 1))
+            np.testing.assert_allclose(tgt.cpu().numpy(), et, rtol=1e-5, atol=1e-5 * (np.abs(et).max() + 1))
+            assert cp == pytest.approx(ecp, rel=1e-4, abs=1e-6)
+            outs.append((adv.cpu().numpy(), ret.cpu().numpy(), cp))
+    for a, b in ((0, 1), (2, 3)):
+        np.testing.assert_array_equal(outs[a][0], outs[b][0])
+        np.testing.assert_array_equal(outs[a][1], outs[b][1])
+        assert outs[a][2] == outs[b][2]
 
 
 @pytest.mark.gpu
