@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace mlp {
 
 #define DEV __device__ __forceinline__
@@ -1805,6 +1807,229 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
     if (amax) h3_amax_commit(amax, vmax);
 }
 
+// Wide rows (H > 512, H % 4 == 0; C5's 2048): the wave-per-row kernels above hold a whole row per lane set
+// (32 columns per lane at H = 2048: spills, 1 workgroup per CU).  Here a workgroup walks LNW_ROWS rows,
+// LNW_RB at a time, each thread owning the float4 column groups 4 t + 1024 k (every load / store of a wave
+// is one contiguous 1 KB), the row sums reduced over the 4 waves through LDS in a fixed order.  Same
+// arguments as the wave-per-row kernels (the rank-1 head options are not taken: those layers keep them).
+constexpr int LNW_ROWS = 32;
+// RLGPU_WIDE_LN=0: the wave-per-row kernels at every width; 2: the wide kernels with 2 rows per pass (A/B)
+inline int wide_ln_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("RLGPU_WIDE_LN");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+inline bool wide_ln() { return wide_ln_mode() != 0; }
+DEV int wcol(int k) { return 4 * (int)threadIdx.x + 1024 * k; }
+DEV float4 ld4(const float* p, int c, int H) { return c < H ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f); }
+
+template <int NV, int LNW_RB = 4>
+__global__ void __launch_bounds__(256) ln_act_fwd_wide(const float* Z, const float* gamma, const float* beta, int R, int H,
+                                                      float slope, int use_ln, float* act, float2* stats, float* amax,
+                                                      const float*, const float*, float*) {
+    __shared__ float red[2][LNW_RB][4];
+    const int w = threadIdx.x >> 6;
+    uint32_t vmax = 0;
+    float4 g[NV], b[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        g[k] = use_ln ? ld4(gamma, wcol(k), H) : make_float4(1.f, 1.f, 1.f, 1.f);
+        b[k] = use_ln ? ld4(beta, wcol(k), H) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int r_end = min(R, (int)(blockIdx.x + 1) * LNW_ROWS);
+    for (int r0 = blockIdx.x * LNW_ROWS; r0 < r_end; r0 += LNW_RB) {
+        float4 v[LNW_RB][NV];
+#pragma unroll
+        for (int j = 0; j < LNW_RB; j++) {
+            const float* z = Z + (int64_t)min(r0 + j, R - 1) * H;
+#pragma unroll
+            for (int k = 0; k < NV; k++) v[j][k] = ld4(z, wcol(k), H);
+        }
+        float mean[LNW_RB], rs[LNW_RB];
+#pragma unroll
+        for (int j = 0; j < LNW_RB; j++) {
+            mean[j] = 0.f;
+            rs[j] = 1.f;
+        }
+        if (use_ln) {
+#pragma unroll
+            for (int j = 0; j < LNW_RB; j++) {
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < NV; k++) s += ((v[j][k].x + v[j][k].y) + v[j][k].z) + v[j][k].w;
+                s = wave_sum_x(s);
+                if ((threadIdx.x & 63) == 0) red[0][j][w] = s;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < LNW_RB; j++) {
+                mean[j] = (((red[0][j][0] + red[0][j][1]) + red[0][j][2]) + red[0][j][3]) / (float)H;
+                float s2 = 0.f;
+#pragma unroll
+                for (int k = 0; k < NV; k++) {
+                    const bool in = wcol(k) < H;
+                    const float dx = v[j][k].x - mean[j], dy = v[j][k].y - mean[j], dz = v[j][k].z - mean[j],
+                                dw = v[j][k].w - mean[j];
+                    s2 += in ? ((dx * dx + dy * dy) + dz * dz) + dw * dw : 0.f;
+                }
+                s2 = wave_sum_x(s2);
+                if ((threadIdx.x & 63) == 0) red[1][j][w] = s2;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < LNW_RB; j++)
+                rs[j] = 1.f / sqrtf((((red[1][j][0] + red[1][j][1]) + red[1][j][2]) + red[1][j][3]) / (float)H + 1e-5f);
+        }
+#pragma unroll
+        for (int j = 0; j < LNW_RB; j++) {
+            const int row = r0 + j;
+            if (row >= R) break;
+            float* ao = act + (int64_t)row * H;
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const int c = wcol(k);
+                if (c >= H) continue;
+                float a[4];
+                const float vv[4] = {v[j][k].x, v[j][k].y, v[j][k].z, v[j][k].w};
+                const float gg[4] = {g[k].x, g[k].y, g[k].z, g[k].w}, bb[4] = {b[k].x, b[k].y, b[k].z, b[k].w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const float xh = use_ln ? (vv[e] - mean[j]) * rs[j] : vv[e];
+                    const float hv = use_ln ? xh * gg[e] + bb[e] : xh;
+                    a[e] = hv > 0.f ? hv : hv * slope;
+                    const uint32_t bits = abs_bits(a[e]);
+                    vmax = bits > vmax ? bits : vmax;
+                }
+                *reinterpret_cast<float4*>(ao + c) = make_float4(a[0], a[1], a[2], a[3]);
+            }
+            if (threadIdx.x == 0) stats[row] = make_float2(mean[j], rs[j]);
+        }
+    }
+    if (amax) h3_amax_commit(amax, vmax);
+}
+
+template <int NV, int LNW_RB = 4>
+__global__ void __launch_bounds__(256) ln_act_bwd_wide(const float* dA, const float* Z, const float2* stats, const float* gamma,
+                                                      const float* beta, int R, int H, float slope, int use_ln, float* dZ,
+                                                      float* part, float* amax, const float*, const float*, float*) {
+    __shared__ float red[2][2][LNW_RB][4];  // [pass parity][s1 | s2][row][wave]
+    const int w = threadIdx.x >> 6;
+    uint32_t vmax = 0;
+    float4 g[NV], b[NV], pz[NV], pg[NV], pb[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        g[k] = use_ln ? ld4(gamma, wcol(k), H) : make_float4(1.f, 1.f, 1.f, 1.f);
+        b[k] = use_ln ? ld4(beta, wcol(k), H) : make_float4(0.f, 0.f, 0.f, 0.f);
+        pz[k] = pg[k] = pb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int r_end = min(R, (int)(blockIdx.x + 1) * LNW_ROWS);
+    int par = 0;
+    for (int r0 = blockIdx.x * LNW_ROWS; r0 < r_end; r0 += LNW_RB, par ^= 1) {
+        float x[LNW_RB][NV][4], dh[LNW_RB][NV][4];
+        float2 st[LNW_RB];
+#pragma unroll
+        for (int j = 0; j < LNW_RB; j++) {
+            const int rw = min(r0 + j, R - 1);
+            st[j] = stats[rw];
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const float4 z = ld4(Z + (int64_t)rw * H, wcol(k), H);
+                const float4 a = ld4(dA + (int64_t)rw * H, wcol(k), H);
+                x[j][k][0] = z.x, x[j][k][1] = z.y, x[j][k][2] = z.z, x[j][k][3] = z.w;
+                dh[j][k][0] = a.x, dh[j][k][1] = a.y, dh[j][k][2] = a.z, dh[j][k][3] = a.w;
+            }
+        }
+        float m1[LNW_RB], m2[LNW_RB];
+#pragma unroll
+        for (int j = 0; j < LNW_RB; j++) {
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const float gg[4] = {g[k].x, g[k].y, g[k].z, g[k].w}, bb[4] = {b[k].x, b[k].y, b[k].z, b[k].w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    if (use_ln) x[j][k][e] = (x[j][k][e] - st[j].x) * st[j].y;  // the forward's xhat, same ops
+                    const float h = x[j][k][e] * gg[e] + bb[e];
+                    dh[j][k][e] = h > 0.f ? dh[j][k][e] : dh[j][k][e] * slope;
+                    const float t = dh[j][k][e] * gg[e];
+                    s1 += t;
+                    s2 += t * x[j][k][e];
+                }
+            }
+            m1[j] = m2[j] = 0.f;
+            if (use_ln) {
+                s1 = wave_sum_x(s1);
+                s2 = wave_sum_x(s2);
+                if ((threadIdx.x & 63) == 0) {
+                    red[par][0][j][w] = s1;
+                    red[par][1][j][w] = s2;
+                }
+            }
+        }
+        if (use_ln) {
+            __syncthreads();  // parity buffers: the next pass writes the other half, so one barrier per pass
+#pragma unroll
+            for (int j = 0; j < LNW_RB; j++) {
+                m1[j] = (((red[par][0][j][0] + red[par][0][j][1]) + red[par][0][j][2]) + red[par][0][j][3]) / (float)H;
+                m2[j] = (((red[par][1][j][0] + red[par][1][j][1]) + red[par][1][j][2]) + red[par][1][j][3]) / (float)H;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < LNW_RB; j++) {
+            const int row = r0 + j;
+            if (row >= R) break;
+            float* dz = dZ + (int64_t)row * H;
+#pragma unroll
+            for (int k = 0; k < NV; k++) {
+                const int c = wcol(k);
+                if (c >= H) continue;
+                const float gg[4] = {g[k].x, g[k].y, g[k].z, g[k].w};
+                float d[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    d[e] = use_ln ? st[j].y * (dh[j][k][e] * gg[e] - m1[j] - x[j][k][e] * m2[j]) : dh[j][k][e];
+                    const uint32_t bits = abs_bits(d[e]);
+                    vmax = bits > vmax ? bits : vmax;
+                }
+                *reinterpret_cast<float4*>(dz + c) = make_float4(d[0], d[1], d[2], d[3]);
+                pz[k].x += d[0], pz[k].y += d[1], pz[k].z += d[2], pz[k].w += d[3];
+                pg[k].x += dh[j][k][0] * x[j][k][0], pg[k].y += dh[j][k][1] * x[j][k][1];
+                pg[k].z += dh[j][k][2] * x[j][k][2], pg[k].w += dh[j][k][3] * x[j][k][3];
+                pb[k].x += dh[j][k][0], pb[k].y += dh[j][k][1], pb[k].z += dh[j][k][2], pb[k].w += dh[j][k][3];
+            }
+        }
+    }
+    // this thread's columns' partials over the workgroup's rows, in row order: part[blk][dbias | dgamma | dbeta]
+    float* out = part + (int64_t)blockIdx.x * 3 * H;
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        const int c = wcol(k);
+        if (c >= H) continue;
+        *reinterpret_cast<float4*>(out + c) = pz[k];
+        *reinterpret_cast<float4*>(out + H + c) = pg[k];
+        *reinterpret_cast<float4*>(out + 2 * H + c) = pb[k];
+    }
+    if (amax) h3_amax_commit(amax, vmax);
+}
+
+// the wide kernels for H in (512, 4096] with H % 4 == 0 (null: not applicable)
+inline decltype(&ln_act_fwd_wide<2>) ln_act_fwd_wide_any(int H) {
+    if (H <= 512 || H % 4 != 0 || H > 4096) return nullptr;
+    const bool r2 = wide_ln_mode() == 2;
+    if (H <= 1024) return r2 ? &ln_act_fwd_wide<1, 2> : &ln_act_fwd_wide<1>;
+    if (H <= 2048) return r2 ? &ln_act_fwd_wide<2, 2> : &ln_act_fwd_wide<2>;
+    return r2 ? &ln_act_fwd_wide<4, 2> : &ln_act_fwd_wide<4>;
+}
+inline decltype(&ln_act_bwd_wide<2>) ln_act_bwd_wide_any(int H) {
+    if (H <= 512 || H % 4 != 0 || H > 4096) return nullptr;
+    const bool r2 = wide_ln_mode() == 2;
+    if (H <= 1024) return r2 ? &ln_act_bwd_wide<1, 2> : &ln_act_bwd_wide<1>;
+    if (H <= 2048) return r2 ? &ln_act_bwd_wide<2, 2> : &ln_act_bwd_wide<2>;
+    return r2 ? &ln_act_bwd_wide<4, 2> : &ln_act_bwd_wide<4>;
+}
+
 // NPER (columns per lane) dispatch: H <= 64 * NPER
 #define RLGPU_NPER_DISPATCH(NAME)                                  \
     inline decltype(&NAME<16>) NAME##_any(int H) {                 \
@@ -1839,8 +2064,13 @@ inline decltype(&ln_act_bwd<16, true>) ln_act_bwd_head_any(int H) {
 // Row-shape variants of the H in (256, 512] kernels (host: RLGPU_LNF_VARIANT / RLGPU_LNB_VARIANT):
 // rows per block and rows in flight per wave.  Same bits for any forward variant; a backward
 // variant with other rows per block regroups the column partials (fp32 sums in another order).
-inline decltype(&ln_act_fwd_f32<8>) ln_act_fwd_f32_pick(int H, int v, int* rows) {
+inline decltype(&ln_act_fwd_f32<8>) ln_act_fwd_f32_pick(int H, int v, int* rows, bool head = false) {
     *rows = LNF_ROWS;
+    if (!head && wide_ln())
+        if (auto f = ln_act_fwd_wide_any(H)) {
+            *rows = LNW_ROWS;
+            return f;
+        }
     if (H > 256 && H <= 512) switch (v) {
             case 1: *rows = 32; return &ln_act_fwd_f32<8, 32, 4>;
             case 2: *rows = 8; return &ln_act_fwd_f32<8, 8, 2>;
@@ -1851,6 +2081,11 @@ inline decltype(&ln_act_fwd_f32<8>) ln_act_fwd_f32_pick(int H, int v, int* rows)
 }
 inline decltype(&ln_act_bwd<8>) ln_act_bwd_pick(int H, bool head, int v, int* rows) {
     *rows = LNB_ROWS;
+    if (!head && wide_ln())
+        if (auto f = ln_act_bwd_wide_any(H)) {
+            *rows = LNW_ROWS;
+            return f;
+        }
     if (H > 256 && H <= 512) switch (v) {
             case 1: *rows = 16; return head ? &ln_act_bwd<8, true, 16, 2> : &ln_act_bwd<8, false, 16, 2>;
             case 2: return head ? &ln_act_bwd<8, true, 32, 4> : &ln_act_bwd<8, false, 32, 4>;

@@ -122,10 +122,12 @@ inline int env_int(const char* name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 // Full-row H3 GEMMs (mlp::gemm_row, row_gemm.hpp): the training forward's Linear + LayerNorm + LeakyReLU of a
-// hidden layer with 256 or 512 outputs in one kernel.  RLGPU_ROW_GEMM: 0 off (the 128 x 128 GEMM + ln_act_fwd),
-// 1 (default) on.
+// hidden layer with 256 or 512 outputs in one kernel, and the dA GEMM with the LayerNorm backward.
+// RLGPU_ROW_GEMM: 0 (default) off (the 128 x 128 GEMM + ln_act_fwd / ln_act_bwd), 1 on (ring of 2 stages x 32 k),
+// 2 on (4 stages x 16 k).
 inline int row_gemm() {
-    static const int v = env_int("RLGPU_ROW_GEMM", 1);
+    // off by default: measured slower than gemm_x6 + the LayerNorm passes (profiles/r05h_row_gemm_ab.txt)
+    static const int v = env_int("RLGPU_ROW_GEMM", 0);
     return v;
 }
 // the full-row kernel's ring: RLGPU_ROW_GEMM=1 -> 2 stages of 32 k, 2 -> 4 stages of 16 k (3 in flight)
@@ -677,7 +679,7 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
         // bytes: z read, act written, (mean, rstd) written
         ktime::Span span(ktime::LN_FWD, (double)n * (8.0 * L.out + 8.0), s);
         int lnf_rows = 0;
-        const auto lnf = mlp::ln_act_fwd_f32_pick(L.out, lnf_variant(), &lnf_rows);
+        const auto lnf = mlp::ln_act_fwd_f32_pick(L.out, lnf_variant(), &lnf_rows, fuse);
         hipLaunchKernelGGL(lnf, dim3(ceil_div(n, lnf_rows)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
                            amax_slot(m, l), fuse ? P + O->w : nullptr, fuse ? P + O->b : nullptr, fuse ? out : nullptr);

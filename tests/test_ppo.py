@@ -439,3 +439,23 @@ def test_c5_minibatch_grads_match_torch(gpu):
     p.zero_grad()
     p.minibatch(d["obs"], d["masks"], d["acts"], d["old"], d["adv"], d["tgt"], None, 0, n, n)
     assert_grads_close(p.flat(grads=True).cpu(), pol, crit, rel_tol=1e-4, frac=1.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_row_gemm_option_keeps_the_gradients(gpu, variant):
+    """The full-row H3 GEMMs (RLGPU_ROW_GEMM=1 / 2, csrc/row_gemm.hpp; off by default, slower) still pass the
+    forward and minibatch-gradient tests against torch fp32: the knob is read once per process, so they run in a
+    child process with it set."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RLGPU_ROW_GEMM=variant)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_ppo.py"), "-k",
+                        "(minibatch_grads_match_torch and h3) or forward_fp32_h3"],
+                       env=env, capture_output=True, text=True, timeout=360, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout

@@ -4,7 +4,8 @@ buffer, shuffled, then the optimizer step -- the PPOLearner::Learn inner loop (P
 without the env.  Prints ms per minibatch (HIP events); run under rocprofv3 --kernel-trace --stats
 for per-kernel durations.
 
-usage: python tools/learn_bench.py [minibatches=24] [train_gemm=h3|x6|f32]
+usage: python tools/learn_bench.py [minibatches=24] [train_gemm=h3|x6|f32] [width=512] [depth=2]
+(width 2048, depth 4 = the C5 leg's model)
 """
 import os
 import sys
@@ -28,7 +29,10 @@ acts = torch.multinomial(masks.float(), 1, generator=g).squeeze(1).to(torch.int3
 old = -torch.rand((N,), device=dev, generator=g) * 4
 adv = torch.randn((N,), device=dev, generator=g)
 tgt = torch.randn((N,), device=dev, generator=g)
-p = PPO(max_rows=MB, seed=123, train_gemm=mode)
+width = int(sys.argv[3]) if len(sys.argv) > 3 else 512
+depth = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+layers = (width,) * depth
+p = PPO(max_rows=MB, seed=123, train_gemm=mode, policy_layers=layers, critic_layers=layers)
 p.adv_normalizer(adv)
 idx = permutation(N, 7, 0)
 
@@ -49,7 +53,7 @@ e0.record()
 run(nmb)
 e1.record()
 torch.cuda.synchronize()
-print(f"learn_bench: {e0.elapsed_time(e1) / nmb:.3f} ms per 50k minibatch (+ optimizer step every {N // MB}), "
+print(f"learn_bench {layers}: {e0.elapsed_time(e1) / nmb:.3f} ms per 50k minibatch (+ optimizer step every {N // MB}), "
       f"mode {sys.argv[2] if len(sys.argv) > 2 else 'h3'}, {nmb} minibatches", flush=True)
 print("metrics finite:", bool(np.isfinite(p.metrics.cpu().numpy()).all()))
 kernel_timing(True)
