@@ -209,6 +209,18 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     if (threadIdx.x == 0) g_pen_save.n = 0;
     sync();
     P.mark(4);
+#if RLGPU_MESH_DEAL
+    // the bodies' mesh queries planned by lanes 0..4 of each arena, the 30 light pairs (planes, dynamic
+    // pairs) on the arena's lanes; then the mesh entries of all four arenas dealt over the workgroup
+    if (valid) {
+        mesh_plan(A, M, l);
+        for (int j = l; j < 30; j += kTeam) narrow_pair(A, M, j < 20 ? (j / 4) * 5 + 1 + (j % 4) : 25 + (j - 20));
+    }
+    sync();
+    narrow_mesh(A - (threadIdx.x >> 4), nvalid, M);
+    sync();
+    if (valid && l == 0) A->a.epa_lock = 0;  // the plan's bytes are the small solver set again
+#else
     if (valid)
         // work items: the 5 body-vs-mesh pairs split into kMeshChunks parts each (the heavy items,
         // spread over distinct lanes first), then the 30 light pairs
@@ -220,6 +232,7 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
                 narrow_pair(A, M, j < 20 ? (j / 4) * 5 + 1 + (j % 4) : 25 + (j - 20));
             }
         }
+#endif
     sync();
     P.mark(22);
     narrow_queue(A - (threadIdx.x >> 4), nvalid, M);

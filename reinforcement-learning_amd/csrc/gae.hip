@@ -424,6 +424,7 @@ __global__ void __launch_bounds__(kFT) k_flat_apply(GaeParams p, const int64_t* 
 }
 
 // Rollout layout: one lane per agent column, exact reference order (GAE.cpp:169-193).
+constexpr int kGaeU = 8;
 __global__ void __launch_bounds__(256) k_gae_rollout(const float* __restrict__ rews, const int8_t* __restrict__ terms,
                                                      const float* __restrict__ vals, const float* __restrict__ trunc_vals,
                                                      const float* __restrict__ boot_vals, int T, int N, float gamma,
@@ -434,35 +435,52 @@ __global__ void __launch_bounds__(256) k_gae_rollout(const float* __restrict__ r
     int n = blockIdx.x * blockDim.x + threadIdx.x;
     float sabs = 0.f, sclip = 0.f;
     if (n < N) {
+        // kGaeU steps' loads are issued before their recursion (the loads do not depend on it; one
+        // global-load latency per kGaeU steps instead of per step); V[t + 1] is the previous step's V
         float prevLambda = 0.f, prevRet = 0.f;
-        for (int t = T - 1; t >= 0; --t) {
-            int64_t i = (int64_t)t * N + n;
-            int8_t term = terms[i];
-            float rew = rews[i];
-            float cur = rew;
-            if (normalize) {
-                cur = rew * inv_std;
-                sabs += fabsf(cur);
-                if (clip) cur = fminf(fmaxf(cur, -clip_range), clip_range);
-                sclip += fabsf(cur);
+        float vnext = boot_vals ? boot_vals[n] : 0.f;  // the value after the last step
+        for (int t1 = T - 1; t1 >= 0; t1 -= kGaeU) {
+            float rr[kGaeU], vv[kGaeU];
+            int8_t tt[kGaeU];
+#pragma unroll
+            for (int u = 0; u < kGaeU; u++) {
+                const int64_t i = (int64_t)max(t1 - u, 0) * N + n;
+                rr[u] = rews[i];
+                vv[u] = vals[i];
+                tt[u] = terms[i];
             }
-            float done = (term == kNormal) ? 1.f : 0.f;
-            float trunc = (term == kTruncated) ? 1.f : 0.f;
-            float nd = (1.f - done) * (1.f - trunc);
-            float nextVal;
-            if (term == kNormal) nextVal = 0.f;
-            else if (term == kTruncated) nextVal = trunc_vals ? trunc_vals[i] : 0.f;
-            else if (t < T - 1) nextVal = vals[i + N];
-            else nextVal = boot_vals ? boot_vals[n] : 0.f;
-            float v = vals[i];
-            float predReturn = cur + gamma * nextVal;
-            float delta = predReturn - v;
-            float curReturn = rew + prevRet * gamma * nd;
-            ret[i] = curReturn;
-            prevLambda = delta + gamma_lambda * nd * prevLambda;
-            adv[i] = prevLambda;
-            target[i] = v + prevLambda;
-            prevRet = curReturn;
+#pragma unroll
+            for (int u = 0; u < kGaeU; u++) {
+                const int t = t1 - u;
+                if (t < 0) break;
+                const int64_t i = (int64_t)t * N + n;
+                const int8_t term = tt[u];
+                const float rew = rr[u];
+                float cur = rew;
+                if (normalize) {
+                    cur = rew * inv_std;
+                    sabs += fabsf(cur);
+                    if (clip) cur = fminf(fmaxf(cur, -clip_range), clip_range);
+                    sclip += fabsf(cur);
+                }
+                float done = (term == kNormal) ? 1.f : 0.f;
+                float trunc = (term == kTruncated) ? 1.f : 0.f;
+                float nd = (1.f - done) * (1.f - trunc);
+                float nextVal;
+                if (term == kNormal) nextVal = 0.f;
+                else if (term == kTruncated) nextVal = trunc_vals ? trunc_vals[i] : 0.f;
+                else nextVal = vnext;  // V[t + 1], or the bootstrap value at t = T - 1
+                float v = vv[u];
+                float predReturn = cur + gamma * nextVal;
+                float delta = predReturn - v;
+                float curReturn = rew + prevRet * gamma * nd;
+                ret[i] = curReturn;
+                prevLambda = delta + gamma_lambda * nd * prevLambda;
+                adv[i] = prevLambda;
+                target[i] = v + prevLambda;
+                prevRet = curReturn;
+                vnext = v;
+            }
         }
     }
     if (clip_sums && normalize) {
