@@ -18,9 +18,12 @@
 //   * flat (episode-concatenated, the reference's own input): A_t = d_t + c_t*A_{t+1} is a
 //     composition of affine maps, (cL,dL)o(cR,dR) = (cL*cR, dL + cL*dR).  Terminals make c=0,
 //     so one non-segmented reverse scan is exactly the segmented GAE.  Three streaming passes
-//     over 4096-element tiles (tile summaries with the truncation value left symbolic -> one
+//     over 8192-element tiles (tile summaries with the truncation value left symbolic -> one
 //     workgroup resolves truncation indices and tile carries -> apply), float4 accesses, a
 //     fixed composition order (the same result on every run); see k_flat_summary.
+#include <mutex>
+#include <vector>
+
 #include "common.hpp"
 #include "../../include/rlgpu_gae.h"
 
@@ -49,8 +52,8 @@ struct GaeParams {
     float clip_range;
 };
 
-// ---- flat layout: three passes, each a streaming pass over 4096-element tiles ---------------------------------
-// A tile is 4 rounds of 1024 elements; in a round thread l owns elements 4l .. 4l + 3 (one float4 of each
+// ---- flat layout: three passes, each a streaming pass over 8192-element tiles ---------------------------------
+// A tile is 8 rounds of 1024 elements; in a round thread l owns elements 4l .. 4l + 3 (one float4 of each
 // array: every load and store of a wave is one contiguous 1 KB).  Pass 1 (k_flat_summary) composes each
 // tile's maps and counts its truncations; pass 2 (k_flat_carry, one workgroup) turns the counts into each
 // tile's first truncation index and the maps into the value entering each tile from the right; pass 3
@@ -60,7 +63,7 @@ struct GaeParams {
 // The summary cannot know its truncation values (their index is a forward count over the tiles to its
 // left), so it composes maps of the form x -> c x + d + b T, T = the value of the tile's first truncation:
 // the tile's first terminal zeroes every coefficient to its right, so only that T can survive.
-constexpr int kFT = 256, kFV = 4, kFRounds = 4;
+constexpr int kFT = 256, kFV = 4, kFRounds = 8;
 constexpr int kFRound = kFT * kFV, kFTile = kFRound * kFRounds;
 constexpr int kCT = 1024;  // the carry pass's workgroup
 
@@ -218,6 +221,13 @@ __global__ void __launch_bounds__(kFT) k_flat_summary(GaeParams p, float4* sumA,
         clipp[blockIdx.x] = make_float2(s1, s2);
     }
 }
+
+struct FlatScratch {
+    char* p = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_flat_mu;
+std::vector<FlatScratch> g_flat_scratch;  // rlgpu_gae_flat's tile summaries, per device
 
 struct FlatResult {
     int64_t total;  // truncations found (GAE.cpp:196-197 checks it against the values given)
@@ -598,8 +608,20 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
         const size_t o_a = take(sizeof(float4) * n), o_r = take(sizeof(float2) * n), o_c = take(sizeof(int) * n),
                      o_p = take(sizeof(float2) * n), o_b = take(sizeof(int64_t) * (n + 1)),
                      o_x = take(sizeof(float2) * n), o_res = take(sizeof(FlatResult));
-        char* scratch = nullptr;
-        RLGPU_CHECK_HIP(hipMallocAsync((void**)&scratch, bytes, s));
+        // one scratch buffer per device, grown on demand and held for the call (the call ends synchronised)
+        std::lock_guard<std::mutex> lock(g_flat_mu);
+        int dev = 0;
+        RLGPU_CHECK_HIP(hipGetDevice(&dev));
+        if ((int)g_flat_scratch.size() <= dev) g_flat_scratch.resize(dev + 1);
+        FlatScratch& sc = g_flat_scratch[dev];
+        if (sc.bytes < bytes) {
+            if (sc.p) RLGPU_CHECK_HIP(hipFree(sc.p));
+            sc.p = nullptr;
+            sc.bytes = 0;
+            RLGPU_CHECK_HIP(hipMalloc((void**)&sc.p, bytes));
+            sc.bytes = bytes;
+        }
+        char* scratch = sc.p;
         float4* sumA = (float4*)(scratch + o_a);
         float2* sumR = (float2*)(scratch + o_r);
         int* cnt = (int*)(scratch + o_c);
@@ -635,7 +657,6 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
         RLGPU_CHECK_HIP(hipGetLastError());
         FlatResult h{};
         RLGPU_CHECK_HIP(hipMemcpyAsync(&h, res, sizeof h, hipMemcpyDeviceToHost, s));
-        RLGPU_CHECK_HIP(hipFreeAsync(scratch, s));
         RLGPU_CHECK_HIP(hipStreamSynchronize(s));
         const int64_t h_total = h.total;
         const float h_clip[2] = {h.sabs, h.sclip};

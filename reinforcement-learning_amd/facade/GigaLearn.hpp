@@ -98,6 +98,26 @@ struct PPOLearnerConfig {
     }
 };
 
+// PPO/TransferLearnConfig.h: the fields of Learner::StartTransferLearn's configuration (distilling an old policy
+// with its own obs builder / action parser into the current one, Learner.cpp:290-470, PPOLearner.cpp:583-637).
+// Restated so a caller's source compiles; the engine does not run that mode (StartTransferLearn says so).
+using MakeObsFn = std::function<RLGC::ObsBuilder*()>;
+using MakeActFn = std::function<RLGC::ActionParser*()>;
+struct TransferLearnConfig {
+    MakeObsFn makeOldObsFn;
+    MakeActFn makeOldActFn;
+    std::function<std::vector<int>(const RLGC::Player&, const RLGC::GameState&)> mapActsFn = nullptr;
+    PartialModelConfig oldPolicyConfig;
+    PartialModelConfig oldSharedHeadConfig;
+    std::filesystem::path oldModelsPath;
+    float lr = 3e-4f;
+    int batchSize = 50'000;
+    int epochs = 5;
+    bool useKLDiv = false;
+    float lossScale = 500.f;
+    float lossExponent = 1.f;
+};
+
 struct SkillTrackerConfig {
     bool enabled = false;
     int numArenas = 16;
@@ -613,6 +633,11 @@ class Learner {
     Learner& operator=(const Learner&) = delete;
 
     void Start();
+    // Learner::StartTransferLearn (Learner.h:45): not part of the engine's path; refused by name
+    [[noreturn]] void StartTransferLearn(const TransferLearnConfig&) {
+        throw std::runtime_error("GGL::Learner::StartTransferLearn: transfer learning (PPOLearner::TransferLearn) is not "
+                                 "implemented by the rlgpu engine");
+    }
     // one Start() loop body (collection, consumption, learning, versions) into `report`; returns the timesteps
     // before it (engine extension: Start() without the loop)
     int64_t Iterate(Report& report);

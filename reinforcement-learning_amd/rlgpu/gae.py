@@ -41,9 +41,8 @@ class GAE:
         n = rews.numel()
         nt = 0 if trunc_val_preds is None else trunc_val_preds.numel()
         tv = None if trunc_val_preds is None else trunc_val_preds.contiguous().float()
-        adv = torch.empty(n, dtype=torch.float32, device=rews.device)
-        tgt = torch.empty_like(adv)
-        ret = torch.empty_like(adv)
+        # one allocation; rows padded to 4 floats so each output starts 16-byte aligned (the kernels' float4 path)
+        adv, tgt, ret = torch.empty((3, (n + 3) // 4 * 4), dtype=torch.float32, device=rews.device)[:, :n]
         clip = ctypes.c_float(0.0)
         f, _ = _sig()
         check(f(ptr(rews), ptr(terminals), ptr(val_preds), ptr(tv), n, nt, gamma, lam, return_std,
