@@ -53,8 +53,9 @@ struct GaeParams {
 };
 
 // ---- flat layout: three passes, each a streaming pass over 8192-element tiles ---------------------------------
-// A tile is 8 rounds of 1024 elements; in a round thread l owns elements 4l .. 4l + 3 (one float4 of each
-// array: every load and store of a wave is one contiguous 1 KB).  Pass 1 (k_flat_summary) composes each
+// The apply pass walks a tile in 8 rounds of 1024 elements, thread l owning elements 4l .. 4l + 3 of a round
+// (one float4 of each array: every load and store of a wave is one contiguous 1 KB); the summary pass in 4
+// rounds of 2048, 8 elements per thread (8 per thread in the apply pass measured 65 -> 69 us at 2^24).  Pass 1 (k_flat_summary) composes each
 // tile's maps and counts its truncations; pass 2 (k_flat_carry, one workgroup) turns the counts into each
 // tile's first truncation index and the maps into the value entering each tile from the right; pass 3
 // (k_flat_apply) rebuilds the maps with the exact truncation values and writes A, target, R.  The
@@ -63,8 +64,9 @@ struct GaeParams {
 // The summary cannot know its truncation values (their index is a forward count over the tiles to its
 // left), so it composes maps of the form x -> c x + d + b T, T = the value of the tile's first truncation:
 // the tile's first terminal zeroes every coefficient to its right, so only that T can survive.
-constexpr int kFT = 256, kFV = 4, kFRounds = 8;
-constexpr int kFRound = kFT * kFV, kFTile = kFRound * kFRounds;
+constexpr int kFT = 256, kFV = 4;
+constexpr int kFTile = 8192;
+constexpr int kFRound = kFT * kFV, kFRounds = kFTile / kFRound;  // the apply pass: rounds of 1024
 constexpr int kCT = 1024;  // the carry pass's workgroup
 
 struct Aff3 {
@@ -80,7 +82,7 @@ struct Quad {
     float vnext;  // vals[i0 + 4] (0 past the end)
 };
 template <bool VEC>
-__device__ __forceinline__ void load_quad(const GaeParams& p, int64_t i0, Quad& q) {
+__device__ __forceinline__ void load_quad_raw(const GaeParams& p, int64_t i0, Quad& q) {
     if (VEC && i0 + kFV <= p.M) {
         const float4 r = *reinterpret_cast<const float4*>(p.rews + i0);
         const float4 v = *reinterpret_cast<const float4*>(p.vals + i0);
@@ -98,10 +100,26 @@ __device__ __forceinline__ void load_quad(const GaeParams& p, int64_t i0, Quad& 
             q.t[j] = in ? p.terms[i0 + j] : kNormal;
         }
     }
-    // the next element's value: the right neighbour lane's first, lane 63 (and the array's end) from memory
-    const float nb = __shfl_down(q.v[0], 1, 64);
-    q.vnext = ((threadIdx.x & 63) != 63) ? nb : (i0 + kFV < p.M ? p.vals[i0 + kFV] : 0.f);
-    if (i0 + kFV >= p.M) q.vnext = 0.f;
+}
+// the value after element i0 + span - 1 when the next lane's first element is i0 + span: its v0, lane 63 (and
+// the array's end) from memory
+__device__ __forceinline__ float next_lane_val(const GaeParams& p, int64_t i0, int span, float v0) {
+    const float nb = __shfl_down(v0, 1, 64);
+    if (i0 + span >= p.M) return 0.f;
+    return ((threadIdx.x & 63) != 63) ? nb : p.vals[i0 + span];
+}
+template <bool VEC>
+__device__ __forceinline__ void load_quad(const GaeParams& p, int64_t i0, Quad& q) {
+    load_quad_raw<VEC>(p, i0, q);
+    q.vnext = next_lane_val(p, i0, kFV, q.v[0]);
+}
+// elements i0 .. i0 + 7 of a thread whose next lane starts at i0 + 8
+template <bool VEC>
+__device__ __forceinline__ void load_octet(const GaeParams& p, int64_t i0, Quad (&e)[2]) {
+    load_quad_raw<VEC>(p, i0, e[0]);
+    load_quad_raw<VEC>(p, i0 + kFV, e[1]);
+    e[0].vnext = i0 + kFV < p.M ? e[1].v[0] : 0.f;
+    e[1].vnext = next_lane_val(p, i0, 2 * kFV, e[0].v[0]);
 }
 
 __device__ __forceinline__ float norm_rew(const GaeParams& p, float rew) {
@@ -145,43 +163,50 @@ __device__ __forceinline__ Aff wave_reduce(Aff a) {
 }
 
 // Pass 1: per tile, the composed adv map (c, d, b), the composed return map, the truncation count and the
-// clip-portion partial sums (sum |r / std|, sum |clip(r / std)|).
+// clip-portion partial sums (sum |r / std|, sum |clip(r / std)|).  Rounds of 2048 elements, 8 per thread (two
+// float4 of each array; 4 per thread took twice the cross-lane reductions: 45.6 -> 37.8 us at 2^24).
+constexpr int kSRound = kFT * 2 * kFV, kSRounds = kFTile / kSRound;
 template <bool VEC>
 __global__ void __launch_bounds__(kFT) k_flat_summary(GaeParams p, float4* sumA, float2* sumR, int* cnt, float2* clipp) {
-    __shared__ Aff3 sa[kFRounds][kFT / 64];
-    __shared__ Aff sr[kFRounds][kFT / 64];
+    __shared__ Aff3 sa[kSRounds][kFT / 64];
+    __shared__ Aff sr[kSRounds][kFT / 64];
     __shared__ float sc[3][kFT / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t t0 = (int64_t)blockIdx.x * kFTile;
     int c = 0;
     float sabs = 0.f, sclip = 0.f;
 #pragma unroll
-    for (int q = 0; q < kFRounds; q++) {
-        const int64_t i0 = t0 + (int64_t)q * kFRound + threadIdx.x * kFV;
-        Quad e;
-        load_quad<VEC>(p, i0, e);
+    for (int q = 0; q < kSRounds; q++) {
+        const int64_t i0 = t0 + (int64_t)q * kSRound + threadIdx.x * 2 * kFV;
+        Quad e2[2];
+        load_octet<VEC>(p, i0, e2);
         Aff3 A{1.f, 0.f, 0.f};
         Aff R{1.f, 0.f};
 #pragma unroll
-        for (int j = kFV - 1; j >= 0; j--) {
-            const int8_t t = e.t[j];
-            const float n = norm_rew(p, e.r[j]);
-            if (p.normalize && i0 + j < p.M) {
-                sabs += fabsf(e.r[j] * p.inv_std);
-                sclip += fabsf(n);
+        for (int h = 1; h >= 0; h--) {
+            const Quad& e = e2[h];
+            const int64_t j0 = i0 + h * kFV;
+#pragma unroll
+            for (int j = kFV - 1; j >= 0; j--) {
+                const int8_t t = e.t[j];
+                const float n = norm_rew(p, e.r[j]);
+                if (p.normalize && j0 + j < p.M) {
+                    sabs += fabsf(e.r[j] * p.inv_std);
+                    sclip += fabsf(n);
+                }
+                const bool term = t == kNormal || t == kTruncated;
+                const float nd = term ? 0.f : 1.f;
+                Aff3 f;
+                if (t == kTruncated) {
+                    f = {0.f, n - e.v[j], p.gamma};  // (n + gamma T) - V with T symbolic
+                    c += j0 + j < p.M;
+                } else {
+                    const float next = t == kNormal ? 0.f : next_val(e, j);
+                    f = {p.gamma_lambda * nd, (n + p.gamma * next) - e.v[j], 0.f};
+                }
+                A = compose3(f, A);
+                R = compose(Aff{p.gamma * nd, e.r[j]}, R);
             }
-            const bool term = t == kNormal || t == kTruncated;
-            const float nd = term ? 0.f : 1.f;
-            Aff3 f;
-            if (t == kTruncated) {
-                f = {0.f, n - e.v[j], p.gamma};  // (n + gamma T) - V with T symbolic
-                c += i0 + j < p.M;
-            } else {
-                const float next = t == kNormal ? 0.f : next_val(e, j);
-                f = {p.gamma_lambda * nd, (n + p.gamma * next) - e.v[j], 0.f};
-            }
-            A = compose3(f, A);
-            R = compose(Aff{p.gamma * nd, e.r[j]}, R);
         }
         A = wave_reduce3(A);
         R = wave_reduce(R);
@@ -204,7 +229,7 @@ __global__ void __launch_bounds__(kFT) k_flat_summary(GaeParams p, float4* sumA,
     if (threadIdx.x == 0) {
         Aff3 A{1.f, 0.f, 0.f};
         Aff R{1.f, 0.f};
-        for (int q = kFRounds - 1; q >= 0; q--)
+        for (int q = kSRounds - 1; q >= 0; q--)
             for (int ww = kFT / 64 - 1; ww >= 0; ww--) {
                 A = compose3(sa[q][ww], A);
                 R = compose(sr[q][ww], R);

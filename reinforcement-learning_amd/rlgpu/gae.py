@@ -4,6 +4,7 @@
 csrc/gae.hip through the C ABI (include/rlgpu_gae.h).
 """
 import ctypes
+import functools
 
 import torch
 
@@ -15,7 +16,8 @@ TERMINAL_NORMAL = 1      # RLGC::TerminalType::NORMAL (TerminalCondition.h:8)
 TERMINAL_TRUNCATED = 2   # RLGC::TerminalType::TRUNCATED (TerminalCondition.h:9)
 
 
-def _sig():
+@functools.lru_cache(maxsize=None)
+def _sig():  # the prototypes, set once
     L = lib()
     f = L.rlgpu_gae_flat
     f.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int64] + [ctypes.c_float] * 4 + \

@@ -247,6 +247,39 @@ def test_env_procedural_soccar_mesh_parity(gpu, pen_slots, monkeypatch):
     _lib.check(L.rlgpu_envset_set_profile(g._h, None, 0), "set_profile")
 
 
+@pytest.mark.parametrize("n", [1, 6, 39])
+def test_env_ragged_workgroup_parity(gpu, n):
+    """Arena counts that leave the last workgroup partly empty (1 of 4, 2 of 4, 3 of 4 arenas): the
+    workgroup-wide phases (the wheel rays' casts, the queued box-triangle queries, the deferred penetration
+    queries) deal only over the valid arenas, on the procedural SOCCAR mesh with balls and cars thrown at
+    its transitions, bit-exact for 80 steps."""
+    import torch
+    from rlgpu.env import EnvSet
+    from rlgpu.mesh import procedural_soccar
+    from rlgpu.state import ARENA
+    mesh = procedural_soccar()
+    g, o = EnvSet(n, seed=31 + n, device=gpu, mesh=mesh), oracle.EnvSet(n, seed=31 + n, mesh=mesh, threads=4)
+    _check(g, o, "create")
+    rng = np.random.default_rng(n)
+    st = np.frombuffer(o.get_arenas().tobytes(), ARENA).copy()
+    for i in range(n):
+        tgt = np.float32([rng.choice([-1, 1]) * rng.uniform(3000, 4096), rng.choice([-1, 1]) * rng.uniform(3500, 5900),
+                          rng.uniform(0, 2000)]) / 50.0
+        d = tgt - st["ball"][i]["pos"]
+        st["ball"][i]["vel"] = (d / np.linalg.norm(d) * rng.uniform(50, 110)).astype(np.float32)
+        for k in range(4):
+            v = rng.normal(size=3) * [1, 1, 0.2]
+            st["cars"][i]["body"]["vel"][k] = (v / np.linalg.norm(v) * rng.uniform(20, 46)).astype(np.float32)
+    buf = np.frombuffer(st.tobytes(), np.uint8)
+    o.set_arenas(buf)
+    g.set_arenas(buf)
+    for t in range(80):
+        a = random_actions(o.masks, rng)
+        o.step(a, True)
+        g.step(torch.from_numpy(a).to(gpu), True)
+        _check_step(g, o, f"ragged n={n} step {t}")
+
+
 def test_env_reset_arenas_mask(gpu):
     import torch
     n = 12

@@ -125,7 +125,7 @@ def test_gpu_flat_matches_golden(gpu, path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("m", [1, 7, 2048, 2049, 4095, 4096, 4097, 8191, 8192, 8193, 12289, 1 << 21, 1 << 24])
+@pytest.mark.parametrize("m", [1, 7, 2047, 2048, 2049, 4095, 4096, 4097, 8191, 8192, 8193, 12289, 1 << 21, 1 << 24])
 def test_gpu_flat_sizes_and_edges(gpu, m):
     import torch
     from rlgpu import GAE
@@ -152,7 +152,7 @@ def test_gpu_flat_tile_boundaries_unaligned_and_deterministic(gpu):
     r = rng.standard_normal(m).astype(np.float32)
     v = rng.standard_normal(m).astype(np.float32)
     t = np.zeros(m, np.int8)
-    for i in (1023, 1024, 4096, 8191, 8192, 8193, 12288 + 4095, 16383, 16384, 16385, 24575, 24576, m - 1):
+    for i in (1023, 1024, 2047, 2048, 4096, 8191, 8192, 8193, 12288 + 4095, 16383, 16384, 16385, 24575, 24576, m - 1):
         t[i] = 2
     t[9000] = 1
     tv = rng.standard_normal(int((t == 2).sum())).astype(np.float32)

@@ -9,6 +9,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 find $O/prof -type f ! -name '*kernel_stats.csv' -delete
 python tools/kstats.py $O/prof/run_kernel_stats.csv 1 12
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gae.py tests/test_trajectories.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+  timeout -k 10 600 python -u -m pytest tests/test_gae.py tests/test_trajectories.py ${MORE_TESTS} -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
   tail -2 $O/tests.log
 fi
