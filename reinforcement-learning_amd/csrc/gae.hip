@@ -250,6 +250,7 @@ __global__ void __launch_bounds__(kFT) k_flat_summary(GaeParams p, float4* sumA,
 struct FlatScratch {
     char* p = nullptr;
     size_t bytes = 0;
+    void* host = nullptr;  // pinned, mapped: the carry pass writes the FlatResult straight to the host
 };
 std::mutex g_flat_mu;
 std::vector<FlatScratch> g_flat_scratch;  // rlgpu_gae_flat's tile summaries, per device
@@ -653,7 +654,10 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
         float2* clipp = (float2*)(scratch + o_p);
         int64_t* base = (int64_t*)(scratch + o_b);
         float2* carry = (float2*)(scratch + o_x);
-        FlatResult* res = (FlatResult*)(scratch + o_res);
+        if (!sc.host) RLGPU_CHECK_HIP(hipHostMalloc(&sc.host, sizeof(FlatResult), hipHostMallocMapped));
+        FlatResult* res = nullptr;
+        RLGPU_CHECK_HIP(hipHostGetDevicePointer((void**)&res, sc.host, 0));
+        (void)o_res;
 
         GaeParams p;
         p.rews = d_rews;
@@ -680,9 +684,12 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
         if (vec) hipLaunchKernelGGL(k_flat_apply<true>, dim3(n), dim3(kFT), 0, s, p, base, carry, d_adv, d_target, d_ret);
         else hipLaunchKernelGGL(k_flat_apply<false>, dim3(n), dim3(kFT), 0, s, p, base, carry, d_adv, d_target, d_ret);
         RLGPU_CHECK_HIP(hipGetLastError());
-        FlatResult h{};
-        RLGPU_CHECK_HIP(hipMemcpyAsync(&h, res, sizeof h, hipMemcpyDeviceToHost, s));
         RLGPU_CHECK_HIP(hipStreamSynchronize(s));
+        const volatile FlatResult* hv = reinterpret_cast<volatile FlatResult*>(sc.host);
+        FlatResult h;
+        h.total = hv->total;
+        h.sabs = hv->sabs;
+        h.sclip = hv->sclip;
         const int64_t h_total = h.total;
         const float h_clip[2] = {h.sabs, h.sclip};
         // GAE.cpp:196-197: truncation count must match the provided bootstrap values.
