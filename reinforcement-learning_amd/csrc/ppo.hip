@@ -91,15 +91,16 @@ inline int h3_variant() {
     }();
     return v;
 }
-// H3 GEMMs with more than 128 output columns on the 128 x 256 tile kernel (mlp::gemm_h3w) when
-// RLGPU_H3_WIDE=1 (experiment: 50000 x 512 x 512 took 134 us against 111 us on gemm_x6's 128 x 128
-// tiles at three workgroups per CU)
+// H3 GEMMs on the 128 x 256 tile kernel (mlp::gemm_h3w): by default for 1024 or more output columns (the C5
+// leg's 2048-wide layers: 32.8 -> 31.6 ms per 50k minibatch, profiles/r05u_h3_wide_ab.txt); at 512 columns the
+// 128 x 128 gemm_x6 at three workgroups per CU is faster (1.57 vs 1.81 ms per C2 minibatch).  RLGPU_H3_WIDE=0:
+// never, 1: for every width above 128.
 inline bool h3_wide(int J) {
-    static const bool on = [] {
-        const char* e = getenv("RLGPU_H3_WIDE");  // measured slower (254 VGPRs, 2 WGs / CU): off by default
-        return e && atoi(e) == 1;
+    static const int mode = [] {
+        const char* e = getenv("RLGPU_H3_WIDE");
+        return e ? atoi(e) : -1;
     }();
-    return on && J > mlp::BN;
+    return mode == 1 ? J > mlp::BN : (mode == 0 ? false : J >= 1024);
 }
 // Forward / input-gradient H3 GEMMs (A_IK x pre-split B) on the LDS-DMA ring kernel mlp::gemm_h3r when
 // RLGPU_H3_RING = 1 (32-deep stages, 4-stage ring), 2 (64-deep, 2 stages), 3 (32-deep, 3 stages) or 4
