@@ -45,15 +45,15 @@ def env_bytes_per_step(arena_state_size, append=True):
 ENV_PMC_FILE = "profiles/r05m_env_pmc.json"
 
 
-def pmc_traffic(kernel_ms, arenas, mesh_name, pmc_file):
+def pmc_traffic(kernel_ms, launch_arenas, mesh_name, pmc_file):
     """HBM traffic of the env kernel from the named PMC summary, as GB/s over the average launch
-    duration measured here; None when the file is absent or this run steps another arena count or mesh
-    (the bytes were counted for that one)."""
+    duration measured here; None when the file is absent or was counted for launches of another arena count
+    or another mesh."""
     path = os.path.join(ROOT, pmc_file)
-    if arenas != ARENAS_PER_GPU or not os.path.exists(path):
+    if not os.path.exists(path):
         return None, None
     d = json.load(open(path))
-    if d.get("mesh", "synthetic") != mesh_name:
+    if d.get("mesh", "synthetic") != mesh_name or d.get("arenas_per_launch", ARENAS_PER_GPU) != launch_arenas:
         return None, None
     b = d["hbm_bytes_per_launch"]
     src = {"bytes_per_launch": b, "source": pmc_file, "fetch_bytes_per_launch": 2 * d["fetch_size_kb_raw"] * 1024,
@@ -303,7 +303,8 @@ def main():
     mesh = procedural_soccar() if args.mesh == "procedural" else None
     arith = {"msvc_x64": 0, "gcc_x64": 1, "scalar": 2}[args.arith]
     cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False,
-                        train_gemm=train_gemm, mesh=mesh, arith=arith)
+                        train_gemm=train_gemm, mesh=mesh, arith=arith,
+                        collect_groups=int(os.environ.get("RLGPU_BENCH_COLLECT_GROUPS", "0")))  # 0: automatic
     L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
     L.set_env_timing(True)  # HIP events around every fused env step, on the learner's stream
 
@@ -324,6 +325,7 @@ def main():
         phase["learn_issue"] += rep["learn_issue_s"]
         phase["collect_issue"] += rep["collect_issue_s"]
         kern.append(rep["env_kernel_ms"])
+        launch_arenas = rep["env_launch_arenas"]  # arenas per env launch (the collection's arena groups)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -336,8 +338,8 @@ def main():
     value = env_steps / el
     kern_ms = sum(kern) / len(kern)
     b_env = env_bytes_per_step(arena_state_size())
-    achieved = b_env * args.arenas / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kern_ms, args.arenas, args.mesh, args.pmc_file)
+    achieved = b_env * launch_arenas / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(kern_ms, launch_arenas, args.mesh, args.pmc_file)
     out = {
         "metric": "env-steps/sec (whole node) at 32768 arenas; PPO wall-clock per 1M steps",
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -364,8 +366,8 @@ def main():
         "roofline": {"bound": "hbm", "limiter": "latency (per-arena serial physics phases)", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_pmc": traffic_src,
                      "kernel": "rl::env_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": b_env,
-                     "units_per_launch": args.arenas,
-                     "algorithmic_bytes_per_launch": b_env * args.arenas},
+                     "units_per_launch": launch_arenas, "collection_groups": args.arenas // launch_arenas,
+                     "algorithmic_bytes_per_launch": b_env * launch_arenas},
     }
     # learn-phase roofline: one more (untimed) iteration with HIP events around every training GEMM
     # and LayerNorm launch, on the stream each runs on (rlgpu_kernel_timing)

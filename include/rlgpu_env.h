@@ -290,6 +290,15 @@ int rlgpu_envset_step_second_half(rlgpu_envset* env, const int32_t* d_actions, v
  * pre-reset rows of trajectories ending TRUNCATED.  Requires action_delay > 0. */
 int rlgpu_envset_step(rlgpu_envset* env, const int32_t* d_actions, int32_t reset_terminated,
                       const rlgpu_step_outputs* out, void* stream);
+/* The fused step of the arenas [first, first + count) only (first a multiple of 4): d_actions holds those
+ * arenas' players' actions and `out` those players' rows.  Ranges of one set with disjoint arenas may run
+ * concurrently on different streams -- the C++ Learner's collection runs arena groups on their own streams,
+ * so one group's launch tail (a launch lasts as long as its slowest workgroup) overlaps the other groups'
+ * work.  Every arena's results are the full-set step's bit for bit.  ExampleMain's StepCallback cadence
+ * (every 4th step for the player metrics) advances at the range that starts at arena 0.  Not with the
+ * per-phase profile (rlgpu_envset_set_profile). */
+int rlgpu_envset_step_range(rlgpu_envset* env, int32_t first, int32_t count, const int32_t* d_actions,
+                            int32_t reset_terminated, const rlgpu_step_outputs* out, void* stream);
 int rlgpu_envset_sync(rlgpu_envset* env, void* stream);
 
 /* Wire-format state transfer (host <-> device), for GameState snapshots, tests and replay. */

@@ -103,6 +103,10 @@ typedef struct {
     int32_t optimizer;             /* PartialModelConfig::optimType of every model (Models.h:40-56):
                                       RLGPU_OPT_ADAMW (0, libtorch AdamW: weight decay 1e-2) or RLGPU_OPT_ADAM
                                       (libtorch Adam: no weight decay) */
+    int32_t collect_groups;        /* the rollout collection's arena groups, each stepped and inferred on its own
+                                      stream so one group's launch tail overlaps the others' work (same results
+                                      bit for bit); 0 = automatic (4 when the policy runs on the fused inference
+                                      kernel, without host plugins or frame stacking, and 16 | num_arenas), 1 = one */
 } rlgpu_learner_config;
 
 enum { RLGPU_ACT_LEAKY_RELU = 0, RLGPU_ACT_RELU = 1 };
@@ -194,6 +198,7 @@ typedef struct {
     double learn_issue_s;                   /* host time to enqueue the learn phase (before its sync):
                                                close to learn_s means the phase is launch-bound */
     double collect_issue_s;                 /* the same for the collection phase */
+    int32_t env_launch_arenas;              /* arenas per timed env launch (num_arenas / collection groups) */
 } rlgpu_learner_report;
 
 typedef struct rlgpu_learner rlgpu_learner;

@@ -149,6 +149,16 @@ int rlgpu_ppo_set_version(rlgpu_ppo* h, const float* d_policy_params, void* stre
 int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n,
                                   int32_t deterministic, uint64_t rng_step, const uint8_t* d_old_rows,
                                   int32_t* d_actions, float* d_logp, void* stream);
+/* rlgpu_ppo_infer_actions (d_old_rows NULL) or _mixed over n rows that are rows [row0, row0 + n) of this rank's
+ * players (the sampler's Philox row index is row0 + i; d_obs / d_masks / d_actions / d_logp / d_old_rows point
+ * at those rows).  Calls on disjoint rows may run concurrently on different streams (the C++ Learner's arena
+ * groups): only on the fused inference kernel, which keeps no per-handle row buffers -- otherwise
+ * RLGPU_ERR_UNSUPPORTED (rlgpu_ppo_fused_infer tells beforehand). */
+int rlgpu_ppo_infer_actions_rows(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n, int64_t row0,
+                                 int32_t deterministic, uint64_t rng_step, const uint8_t* d_old_rows,
+                                 int32_t* d_actions, float* d_logp, void* stream);
+/* 1 when model `model` (0 policy, 1 critic) runs on the fused inference kernel, else 0. */
+int rlgpu_ppo_fused_infer(rlgpu_ppo* h, int32_t model);
 /* InferCriticBatched: bf16 critic forward over n rows (any n; chunked by max_rows). */
 int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t n, float* d_values, void* stream);
 

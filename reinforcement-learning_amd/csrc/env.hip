@@ -215,6 +215,7 @@ struct rlgpu_envset {
     unsigned long long* d_prof = nullptr;
     double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
+    bool metric_players = false;   // this step's player-metrics flag (rlgpu_envset_step_range)
     void *d_cell_tri = nullptr, *d_cell_start = nullptr, *d_tri = nullptr, *d_edge = nullptr;  // arena mesh (MeshView)
     void* d_gjk = nullptr;  // per-lane box-triangle penetration-solver scratch (MeshView::gjk)
     rl::MeshView mesh{};
@@ -386,6 +387,42 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     }
     unsigned blocks = rlgpu::ceil_div(g.n, rl::kArenas);
     switch (e->cfg.arith) {  // the kernel specialised for the set's arithmetic
+        case RLGPU_ARITH_MSVC_X64: rl::env_k0_launch(g, blocks, s); break;
+        case RLGPU_ARITH_GCC_X64: rl::env_k1_launch(g, blocks, s); break;
+        default: rl::env_k2_launch(g, blocks, s); break;
+    }
+    RLGPU_CHECK_HIP(hipGetLastError());
+}
+
+// the arenas [first, first + count) of the set (first % kArenas == 0): every per-arena / per-player pointer
+// moved to the range, the arenas' Philox streams and the penetration-solver scratch of their workgroups kept
+void launch_range(rlgpu_envset* e, rl::StepArgs g, int first, int count, bool metrics_players, hipStream_t s) {
+    const size_t P0 = (size_t)first * 4;
+    g.arenas = e->d_arenas + (size_t)first * rl::kRec;
+    g.n = count;
+    g.obs = e->d_obs + P0 * RLGPU_OBS;
+    g.masks = e->d_masks + P0 * RLGPU_ACTIONS;
+    g.rewards = e->d_rewards + P0;
+    g.terminals = e->d_terminals + first;
+    g.last_rewards = e->cfg.save_rewards ? e->d_last_rewards + (size_t)first * e->plug.nr : nullptr;
+    g.trunc_obs = e->d_trunc_obs + P0 * RLGPU_OBS;
+    g.seed = e->cfg.seed;
+    g.max_episode_steps = e->cfg.max_episode_steps;
+    g.prof = nullptr;
+    g.mesh = e->mesh;
+    g.mesh.gjk = e->mesh.gjk ? e->mesh.gjk + (size_t)(first / rl::kArenas) * rl::kWG : nullptr;
+    g.plug = e->d_plug;
+    g.arith = e->cfg.arith;
+    g.arena_offset = e->cfg.arena_offset + first;
+    g.fuzz = e->cfg.state_setter == RLGPU_SS_FUZZED_KICKOFF;
+    g.pen_slots = e->pen_slots;
+    g.reward_values = g.build && e->d_reward_values ? e->d_reward_values + P0 * e->plug.nr : nullptr;
+    if (g.build && e->d_metrics) {
+        g.metrics = e->d_metrics + (size_t)first * RLGPU_STEP_METRIC_SLOTS;
+        g.metrics_players = metrics_players;
+    }
+    const unsigned blocks = rlgpu::ceil_div(count, rl::kArenas);
+    switch (e->cfg.arith) {
         case RLGPU_ARITH_MSVC_X64: rl::env_k0_launch(g, blocks, s); break;
         case RLGPU_ARITH_GCC_X64: rl::env_k1_launch(g, blocks, s); break;
         default: rl::env_k2_launch(g, blocks, s); break;
@@ -722,6 +759,32 @@ extern "C" int rlgpu_envset_step(rlgpu_envset* e, const int32_t* d_actions, int3
             g.out_trunc = out->trunc_obs;
         }
         launch(e, g, rlgpu::as_stream(stream));
+    });
+}
+
+extern "C" int rlgpu_envset_step_range(rlgpu_envset* e, int32_t first, int32_t count, const int32_t* d_actions,
+                                       int32_t reset_terminated, const rlgpu_step_outputs* out, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e && d_actions, "rlgpu_envset_step_range: null argument");
+        RLGPU_REQUIRE(e->cfg.action_delay > 0, "fused step needs actionDelay > 0");
+        RLGPU_REQUIRE(first >= 0 && count > 0 && first + count <= e->cfg.num_arenas && first % rl::kArenas == 0,
+                      "rlgpu_envset_step_range: the range must lie in the set and start at a multiple of 4");
+        RLGPU_REQUIRE(!e->d_prof, "rlgpu_envset_step_range: not with the per-phase profile");
+        rl::StepArgs g = blank();
+        g.ticks_first = e->cfg.action_delay;
+        g.actions = d_actions;
+        g.ticks_second = e->cfg.tick_skip - e->cfg.action_delay;
+        g.build = 1;
+        g.reset_mode = reset_terminated ? 1 : 0;
+        if (out) {
+            g.out_obs = out->obs;
+            g.out_masks = out->masks;
+            g.out_rew = out->rewards;
+            g.out_term = out->terminals;
+            g.out_trunc = out->trunc_obs;
+        }
+        if (first == 0 && e->d_metrics) e->metric_players = (++e->metric_calls % 4) == 0;  // one StepCallback call
+        launch_range(e, g, first, count, e->metric_players, rlgpu::as_stream(stream));
     });
 }
 

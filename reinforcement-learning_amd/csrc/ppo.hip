@@ -1383,6 +1383,31 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
     });
 }
 
+extern "C" int rlgpu_ppo_infer_actions_rows(rlgpu_ppo* h, const float* d_obs, const uint8_t* d_masks, int32_t n, int64_t row0,
+                                            int32_t deterministic, uint64_t rng_step, const uint8_t* d_old_rows,
+                                            int32_t* d_actions, float* d_logp, void* stream) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(h && d_obs && d_masks && d_actions, "null argument");
+        RLGPU_REQUIRE(n >= 0 && row0 >= 0, "n and row0 must be >= 0");
+        RLGPU_REQUIRE(!d_old_rows || h->has_ver, "rlgpu_ppo_infer_actions_rows: old rows without a version set");
+        if (!fused_ok(h, 0))
+            throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "rlgpu_ppo_infer_actions_rows: the policy is not on the fused kernel");
+        hipStream_t s = rlgpu::as_stream(stream);
+        // the fused kernel keeps no per-row buffers: one launch per pass over all n rows (no max_rows chunks)
+        const int64_t r0 = row0 + h->cfg.sample_row_offset;
+        if (!d_old_rows) {
+            infer_fused(h, 0, false, d_obs, n, 1, nullptr, d_masks, deterministic, rng_step, d_actions, d_logp, nullptr, 0, s,
+                        r0);
+            return;
+        }
+        for (int old = 0; old < 2; old++)  // current policy rows, then the old version's rows
+            infer_fused(h, 0, old != 0, d_obs, n, 1, nullptr, d_masks, deterministic, rng_step, d_actions,
+                        (d_logp && !old) ? d_logp : nullptr, d_old_rows, old, s, r0);
+    });
+}
+
+extern "C" int rlgpu_ppo_fused_infer(rlgpu_ppo* h, int32_t model) { return h && fused_ok(h, model) ? 1 : 0; }
+
 extern "C" int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t n, float* d_values, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h && d_obs && d_values, "null argument");

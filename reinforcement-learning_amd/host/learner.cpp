@@ -355,6 +355,12 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
 
 Learner::~Learner() {
     if (s_) (void)hipStreamSynchronize(s_);
+    for (auto s : gs_) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+    }
+    for (auto e : gsEnd_) (void)hipEventDestroy(e);
+    if (gsStart_) (void)hipEventDestroy(gsStart_);
     for (auto e : ev_) (void)hipEventDestroy(e);
     for (void* p : allocs_) (void)hipFree(p);
     if (truncObsC_) (void)hipFree(truncObsC_);
@@ -372,11 +378,77 @@ Learner::~Learner() {
     delete env_;
 }
 
+// Arena groups for the rollout collection: a launch lasts as long as its slowest workgroup, so with the
+// arenas split into groups stepped (and inferred) on their own streams, one group's launch tail overlaps the
+// other groups' work (tools/env_streams.py: 0.84 -> 0.75 ms per env step of 4,096 arenas with 4 groups).
+// Each arena's step and each player's draw are the same as in one launch (the arenas' Philox streams and the
+// sampler's rows are global), so the rollout is bit-identical.  Only for the fused inference kernel (no
+// per-handle row buffers), without a step hook or stacked frames, and for whole workgroups of arenas.
+int Learner::CollectGroups() const {
+    const int want = cfg_.collect_groups > 0 ? cfg_.collect_groups : 4;
+    if (want <= 1 || hook_ || K_ > 1 || trajMode() || !rlgpu_ppo_fused_infer(ppo_->handle(), 0)) return 1;
+    if (cfg_.num_arenas % (4 * want) != 0) return 1;
+    return want;
+}
+
+void Learner::CollectGrouped(int G) {
+    const int T = exp_.T, P = exp_.P, W = exp_.W;
+    const rlgpu_rollout_view& v = exp_.v;
+    const uint8_t* old = oldTeam_ >= 0 ? oldRows_[oldTeam_] : nullptr;
+    const int Na = cfg_.num_arenas / G, Pg = 4 * Na;
+    if ((int)gs_.size() != G) {
+        for (auto s : gs_) (void)hipStreamDestroy(s);
+        for (auto e : gsEnd_) (void)hipEventDestroy(e);
+        gs_.assign(G, nullptr);
+        gsEnd_.assign(G, nullptr);
+        for (int g = 0; g < G; g++) {
+            hipCheck(hipStreamCreateWithFlags(&gs_[g], hipStreamNonBlocking), "group stream");
+            hipCheck(hipEventCreateWithFlags(&gsEnd_[g], hipEventDisableTiming), "group event");
+        }
+        if (!gsStart_) hipCheck(hipEventCreateWithFlags(&gsStart_, hipEventDisableTiming), "group event");
+    }
+    if (envTiming_ && ev_.size() < (size_t)2 * T * G) {
+        for (auto e : ev_) (void)hipEventDestroy(e);
+        ev_.assign((size_t)2 * T * G, nullptr);
+        for (auto& e : ev_) hipCheck(hipEventCreate(&e), "event");
+    }
+    hipCheck(hipEventRecord(gsStart_, s_), "group start");
+    for (int g = 0; g < G; g++) hipCheck(hipStreamWaitEvent(gs_[g], gsStart_, 0), "group wait");
+    rlgpu_ppo* ph = ppo_->handle();
+    rlgpu_envset* eh = env_->handle();
+    for (int t = 0; t < T; t++) {
+        const size_t r = (size_t)t * P;
+        for (int g = 0; g < G; g++) {  // group 0 first: it advances the StepCallback cadence (rlgpu_envset_step_range)
+            const size_t p0 = (size_t)g * Pg, a = r + p0;
+            RlgpuCheck(rlgpu_ppo_infer_actions_rows(ph, v.obs + a * W, v.masks + a * ACT, Pg, (int64_t)p0,
+                                                    cfg_.deterministic != 0, (uint64_t)stats.rng_step,
+                                                    old ? old + p0 : nullptr, v.actions + a, v.logp + a, gs_[g]),
+                       "InferActions (group)");
+            rlgpu_step_outputs o{v.obs + (a + P) * OBS, v.masks + (a + P) * ACT, v.rewards + a, v.terms + a,
+                                 v.trunc_obs + a * OBS};
+            if (envTiming_) hipCheck(hipEventRecord(ev_[2 * ((size_t)t * G + g)], gs_[g]), "event");
+            RlgpuCheck(rlgpu_envset_step_range(eh, g * Na, Na, v.actions + a, 1, &o, gs_[g]), "EnvSet step (group)");
+            if (envTiming_) hipCheck(hipEventRecord(ev_[2 * ((size_t)t * G + g) + 1], gs_[g]), "event");
+        }
+        stats.rng_step++;
+    }
+    for (int g = 0; g < G; g++) {
+        hipCheck(hipEventRecord(gsEnd_[g], gs_[g]), "group end");
+        hipCheck(hipStreamWaitEvent(s_, gsEnd_[g], 0), "group join");
+    }
+}
+
 void Learner::Collect() {
     if (trajMode()) {
         CollectTrajectories();
         return;
     }
+    if (const int G = CollectGroups(); G > 1) {
+        collectGroupsUsed_ = G;
+        CollectGrouped(G);
+        return;
+    }
+    collectGroupsUsed_ = 1;
     const int T = exp_.T, P = exp_.P;
     const rlgpu_rollout_view& v = exp_.v;
     const uint8_t* old = oldTeam_ >= 0 ? oldRows_[oldTeam_] : nullptr;
@@ -796,9 +868,11 @@ rlgpu_learner_report Learner::Iterate() {
     r.consume_s = secs(t1, t2);
     r.learn_s = secs(t2, t3);
     r.env_steps = (int64_t)(trajMode() ? traj.steps : exp_.T) * cfg_.num_arenas;
+    r.env_launch_arenas = cfg_.num_arenas / std::max(1, collectGroupsUsed_);
     if (envTiming_ && !ev_.empty()) {
         double ms = 0;
-        const int nt = trajMode() ? 0 : exp_.T;  // the trajectory mode records no per-step events
+        // per env launch: T per group (the trajectory mode records no per-step events)
+        const int nt = trajMode() ? 0 : exp_.T * std::max(1, collectGroupsUsed_);
         for (int t = 0; t < nt; t++) {
             float x = 0;
             hipCheck(hipEventElapsedTime(&x, ev_[2 * t], ev_[2 * t + 1]), "elapsed");

@@ -212,6 +212,14 @@ private:
     int K_ = 1;                 // frames stacked (config C4)
     float* hist_ = nullptr;     // [K-1][P][OBS] frame history
     std::vector<hipEvent_t> ev_;
+    // the rollout collection in arena groups (rlgpu_learner_config.collect_groups): one stream per group, joined
+    // to s_ by events at the phase's start and end
+    std::vector<hipStream_t> gs_;
+    std::vector<hipEvent_t> gsEnd_;
+    hipEvent_t gsStart_ = nullptr;
+    int CollectGroups() const;
+    int collectGroupsUsed_ = 1;
+    void CollectGrouped(int G);
     // device scratch
     uint8_t* oldRows_[2] = {nullptr, nullptr};
     int32_t* trainRows_ = nullptr;

@@ -197,6 +197,7 @@ class LearnerConfig:
         self.train_gemm = 2               # rlgpu_ppo_config.train_gemm: 2 = f32 via scaled fp16 split (H3), 0 = bf16 x6 split, 1 = f32 MFMA
         self.infer_fp16 = False           # rlgpu_ppo_config.infer_fp16: fp16 inference copy (C5) instead of bf16
         self.frame_stack = 1              # K >= 2: stacked AdvancedObs frames (C4; no reference counterpart)
+        self.collect_groups = 0           # rollout collection in arena groups on their own streams (0 = automatic)
         # checkpoints (LearnerConfig.h:31-38): None = no save / load
         self.checkpoint_folder = None
         self.ts_per_save = 10_000_000     # 0 = every iteration (Learner.cpp:44-45)
@@ -235,7 +236,7 @@ class _CConfig(ctypes.Structure):
                 ("terminals", ctypes.c_void_p), ("n_terminals", ctypes.c_int32),
                 ("experience_mode", ctypes.c_int32), ("ts_per_itr", ctypes.c_int64),
                 ("experience_capacity", ctypes.c_int32), ("arith", ctypes.c_int32),
-                ("activation", ctypes.c_int32), ("optimizer", ctypes.c_int32)]
+                ("activation", ctypes.c_int32), ("optimizer", ctypes.c_int32), ("collect_groups", ctypes.c_int32)]
 
 
 class _CBatch(ctypes.Structure):
@@ -263,7 +264,7 @@ class _CStats(ctypes.Structure):
 class _CReport(ctypes.Structure):
     _fields_ = [("collect_s", ctypes.c_double), ("consume_s", ctypes.c_double), ("learn_s", ctypes.c_double),
                 ("env_kernel_ms", ctypes.c_double), ("env_steps", ctypes.c_int64), ("learn_issue_s", ctypes.c_double),
-                ("collect_issue_s", ctypes.c_double)]
+                ("collect_issue_s", ctypes.c_double), ("env_launch_arenas", ctypes.c_int32)]
 
 
 def _bind():
@@ -358,6 +359,7 @@ class Learner:
         c.frame_stack = cfg.frame_stack
         c.experience_mode, c.ts_per_itr, c.experience_capacity = cfg.experience_mode, cfg.ts_per_itr, cfg.experience_capacity
         c.arith = cfg.arith
+        c.collect_groups = cfg.collect_groups
         c.rank, c.world = rank, world
         self._coll = None
         coll = None
@@ -616,6 +618,7 @@ class Learner:
         torch.cuda.synchronize(self.device)
         out = {"report": report, "iteration_s": time.perf_counter() - t0, "collect_s": rep.collect_s, "consume_s": rep.consume_s,
                "learn_s": rep.learn_s, "learn_issue_s": rep.learn_issue_s, "collect_issue_s": rep.collect_issue_s, "env_kernel_ms": rep.env_kernel_ms,
+               "env_launch_arenas": rep.env_launch_arenas,
                "old_version": None if self.old_version is None else (self.old_version.timesteps, self.old_team)}
         if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)
             per = self.cfg.ts_per_save or self.T * self.P * self.world

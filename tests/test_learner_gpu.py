@@ -323,3 +323,23 @@ def test_step_hook_host_rewards_and_terminals(gpu):
     forced = C.terms[4::5, :4].cpu().numpy()
     assert (forced == 1).all(), forced
     assert not torch.equal(_bits(C.obs[5, :4]), _bits(D.obs[5, :4]))  # arena 0 restarted from a kickoff after t = 4
+
+
+def test_collect_groups_bit_identical(gpu):
+    """rlgpu_learner_config.collect_groups: the rollout collected in 4 arena groups, each inferred and stepped on
+    its own stream (rlgpu_ppo_infer_actions_rows + rlgpu_envset_step_range), equals the one-launch collection bit
+    for bit -- obs, masks, actions, log-probs, rewards, trajectory codes, truncation rows -- and so do the
+    parameters after learning, over two iterations the second of which plays one team with an old version."""
+    import torch
+    Ls = [_learner(gpu, num_arenas=64, collect_groups=g, max_episode_duration=1.2, train_against_old_chance=1.0)
+          for g in (1, 4)]
+    for it in range(2):
+        reps = [L.iterate() for L in Ls]
+        torch.cuda.synchronize()
+        assert [r["env_launch_arenas"] for r in reps] == [64, 16]
+        assert (reps[0]["old_version"] is None) == (it == 0) and reps[0]["old_version"] == reps[1]["old_version"]
+        for name in ("obs", "masks", "actions", "logp", "rewards", "terms", "trunc_obs"):
+            a, b = getattr(Ls[0], name), getattr(Ls[1], name)
+            assert torch.equal(a.view(torch.uint8) if a.dtype == torch.float32 else a,
+                               b.view(torch.uint8) if b.dtype == torch.float32 else b), (it, name)
+        assert torch.equal(Ls[0].ppo.flat(), Ls[1].ppo.flat()), it

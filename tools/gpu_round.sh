@@ -25,7 +25,7 @@ python tools/kstats.py $O/ks/run_kernel_stats.csv 4 40 > $O/kstats.txt
 echo "kernel trace done"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex env_kernel --output-format csv -d $O/fetch -o run -- python3 bench.py $B1 > $O/fetch.log 2>&1 || { tail -5 $O/fetch.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex env_kernel --output-format csv -d $O/write -o run -- python3 bench.py $B1 > $O/write.log 2>&1 || { tail -5 $O/write.log; exit 1; }
-python tools/pmc_summary.py $O/fetch $O/write env_kernel 65536 $O/env_pmc.json procedural $O/ks/run_kernel_stats.csv $TAG
+python tools/pmc_summary.py $O/fetch $O/write env_kernel 4096 $O/env_pmc.json procedural $O/ks/run_kernel_stats.csv $TAG
 echo "pmc passes done"
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F16 SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex gemm --output-format csv -d $O/mfma -o run -- python3 bench.py $B1 > $O/mfma.log 2>&1 || { tail -5 $O/mfma.log; exit 1; }
 python tools/mfma_summary.py $O/mfma $O/ks/run_kernel_stats.csv $TAG > $O/gemm_mfma_pmc.txt

@@ -16,9 +16,15 @@ import sys
 
 
 def per_launch(path, kernel, min_grid):
-    rows = list(csv.DictReader(open(path)))
-    v = [float(r["Counter_Value"]) for r in rows if kernel in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid]
-    return len(v), sum(v) / max(len(v), 1)
+    """Mean counter value per launch over the kernel's launches of its most frequent grid size (>= min_grid):
+    the collection's step launches (one per arena group and env step), not the set-up launches."""
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid]
+    grids = {}
+    for r in rows:
+        grids[int(r["Grid_Size"])] = grids.get(int(r["Grid_Size"]), 0) + 1
+    grid = max(grids, key=grids.get) if grids else 0
+    v = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == grid]
+    return len(v), sum(v) / max(len(v), 1), grid
 
 
 def main():
@@ -26,9 +32,11 @@ def main():
     mesh = sys.argv[6] if len(sys.argv) > 6 else "synthetic"
     stats = sys.argv[7] if len(sys.argv) > 7 else None
     tag = sys.argv[8] if len(sys.argv) > 8 else None
-    nf, fetch_kb = per_launch(f"{fdir}/run_counter_collection.csv", kernel, min_grid)
-    nw, write_kb = per_launch(f"{wdir}/run_counter_collection.csv", kernel, min_grid)
-    res = {"kernel": kernel, "launches": [nf, nw], "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+    nf, fetch_kb, gf = per_launch(f"{fdir}/run_counter_collection.csv", kernel, min_grid)
+    nw, write_kb, gw = per_launch(f"{wdir}/run_counter_collection.csv", kernel, min_grid)
+    assert gf == gw, (gf, gw)
+    res = {"kernel": kernel, "launches": [nf, nw], "grid_threads": gf, "arenas_per_launch": gf // 64 * 4,
+           "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
            "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1; KB = 1024 B", "mesh": mesh,
            "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --output-format csv -- python3 bench.py --steps 1 "
