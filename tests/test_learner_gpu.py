@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 def _learner(gpu, **kw):
     from rlgpu.learner import Learner, LearnerConfig
-    cfg = LearnerConfig(num_arenas=24, rollout_len=24, mini_batch_size=512, seed=5, **kw)
+    cfg = LearnerConfig(**{**dict(num_arenas=24, rollout_len=24, mini_batch_size=512, seed=5), **kw})
     return Learner(cfg, device=gpu)
 
 
