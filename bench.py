@@ -306,7 +306,8 @@ def main():
                         train_gemm=train_gemm, mesh=mesh, arith=arith,
                         collect_groups=int(os.environ.get("RLGPU_BENCH_COLLECT_GROUPS", "0")))  # 0: automatic
     L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
-    L.set_env_timing(True)  # HIP events around every fused env step, on the learner's stream
+    # HIP events around every fused env step, on the stream it runs on (RLGPU_BENCH_ENV_TIMING=0: none)
+    L.set_env_timing(os.environ.get("RLGPU_BENCH_ENV_TIMING", "1") != "0")
 
     for _ in range(args.warmup):
         L.iterate()
@@ -336,7 +337,7 @@ def main():
     env_steps = world * args.arenas * cfg.rollout_len * args.steps
     agent_steps = 4 * env_steps
     value = env_steps / el
-    kern_ms = sum(kern) / len(kern)
+    kern_ms = sum(kern) / len(kern) or float("nan")
     b_env = env_bytes_per_step(arena_state_size())
     achieved = b_env * launch_arenas / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(kern_ms, launch_arenas, args.mesh, args.pmc_file)

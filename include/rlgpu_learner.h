@@ -105,8 +105,9 @@ typedef struct {
                                       (libtorch Adam: no weight decay) */
     int32_t collect_groups;        /* the rollout collection's arena groups, each stepped and inferred on its own
                                       stream so one group's launch tail overlaps the others' work (same results
-                                      bit for bit); 0 = automatic (4 when the policy runs on the fused inference
-                                      kernel, without host plugins or frame stacking, and 16 | num_arenas), 1 = one */
+                                      bit for bit; measured slower so far); 0 / 1 = one launch per step; G > 1
+                                      when the policy runs on the fused inference kernel, without host plugins or
+                                      frame stacking, and 4 G | num_arenas */
 } rlgpu_learner_config;
 
 enum { RLGPU_ACT_LEAKY_RELU = 0, RLGPU_ACT_RELU = 1 };

@@ -379,13 +379,15 @@ Learner::~Learner() {
 }
 
 // Arena groups for the rollout collection: a launch lasts as long as its slowest workgroup, so with the
-// arenas split into groups stepped (and inferred) on their own streams, one group's launch tail overlaps the
-// other groups' work (tools/env_streams.py: 0.84 -> 0.75 ms per env step of 4,096 arenas with 4 groups).
+// arenas split into groups stepped (and inferred) on their own streams, one group's launch tail could overlap
+// the other groups' work (tools/env_streams.py, env steps alone: 0.84 -> 0.75 ms per step of 4,096 arenas with 4
+// groups).  In the Learner, with the inference between the steps, it measured slower (collection 139 -> 152 ms
+// with 2 groups, 260 ms with 4: profiles/r05y_collect_groups.txt), so the default stays one launch per step.
 // Each arena's step and each player's draw are the same as in one launch (the arenas' Philox streams and the
 // sampler's rows are global), so the rollout is bit-identical.  Only for the fused inference kernel (no
 // per-handle row buffers), without a step hook or stacked frames, and for whole workgroups of arenas.
 int Learner::CollectGroups() const {
-    const int want = cfg_.collect_groups > 0 ? cfg_.collect_groups : 4;
+    const int want = cfg_.collect_groups > 0 ? cfg_.collect_groups : 1;  // automatic = one group (see below)
     if (want <= 1 || hook_ || K_ > 1 || trajMode() || !rlgpu_ppo_fused_infer(ppo_->handle(), 0)) return 1;
     if (cfg_.num_arenas % (4 * want) != 0) return 1;
     return want;
