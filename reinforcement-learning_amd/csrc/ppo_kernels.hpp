@@ -145,14 +145,28 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
                 }
             const float r = (float)(philox(sample_key(seed, step), (uint32_t)(row0 + rw), (uint32_t)step) >> 8) *
                             (1.f / 16777216.f);
+            // the sequential running sum, 8 probs' LDS loads issued ahead of their adds (the loads do not depend
+            // on the sum; one LDS round trip per 8 columns instead of per column)
             float running = 0.f;
             bool found = false;
-            for (int j = 0; j < A; j++) {
-                running += p[j];
-                if (!found && r <= running) {
-                    mine = j;
-                    found = true;
+            int j = 0;
+            for (; j + 8 <= A; j += 8) {
+                float q[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) q[k] = p[j + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    running += q[k];
+                    const bool hit = !found && r <= running;
+                    mine = hit ? j + k : mine;
+                    found = found || hit;
                 }
+            }
+            for (; j < A; j++) {
+                running += p[j];
+                const bool hit = !found && r <= running;
+                mine = hit ? j : mine;
+                found = found || hit;
             }
         }
 #pragma unroll

@@ -5,7 +5,7 @@ O=gpurun_out/${TAG:-rowab}
 mkdir -p $O
 for v in ${VARIANTS:-0 1 2}; do
   RLGPU_ROW_GEMM=$v timeout -k 10 200 python -u tools/learn_bench.py 24 >> $O/learn_$v.txt 2>&1 || { tail -20 $O/learn_$v.txt; exit 1; }
-  RLGPU_ROW_GEMM=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o run -- python -u tools/learn_bench.py 8 > $O/prof_$v.log 2>&1 || { tail -20 $O/prof_$v.log; exit 1; }
+  RLGPU_ROW_GEMM=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$v -o run -- python -u tools/learn_bench.py 8 > $O/prof_$v.log 2>&1 || { tail -20 $O/prof_$v.log; exit 1; }
   find $O/prof_$v -type f ! -name '*kernel_stats.csv' -delete
 done
 grep -H "learn_bench:" $O/learn_*.txt
