@@ -1035,6 +1035,127 @@ __global__ void __launch_bounds__(256, 2) gemm_h3w(GemmArgs g) {
     }
 }
 
+// ---- H3 GEMM with 256 x 256 tiles (gemm_h3q): the forward and input-gradient GEMMs (A_IK fp32 x the
+// pre-split fp16 B planes, J a multiple of 256).  The 128 x 128 tile reads 32 KB from L2 per 128 x 128 x 32
+// stage; at ~70 GB/s of L2 per CU (MI355X_MICROARCH.md, "Indexed rows") three such workgroups per CU need
+// more feed cycles than their MFMAs take, so the stage skeleton, not the matrix pipe, sets gemm_x6's time.
+// A 256 x 256 tile halves the L2 bytes per product.  8 waves (512 threads, one workgroup per CU, two waves
+// per SIMD), each 64 x 128 as in gemm_h3w; double-buffered LDS (2 x 64 KB) with one barrier per stage:
+// this stage's MFMAs run on one buffer while the next stage (in registers since the previous iteration)
+// is split into the other and the stage after is loaded.  Per 16-deep k step and block the products enter
+// the one accumulator as l.h, h.l, h.h -- gemm_x6's H3 order -- so the results are bit-identical to it.
+constexpr int BQ = 256;
+template <bool AV>
+__global__ void __launch_bounds__(512, 1) gemm_h3q(GemmArgs g) {
+    constexpr int XK = 32, KG = XK / 8;
+    __shared__ uint16_t As[2][2][BQ][XK];  // [buffer][plane][row][k], 16-byte chunks XOR-swizzled (xchunk)
+    __shared__ uint16_t Bs[2][2][BQ][XK];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const Tile tl = xcd_tile(g.gx, g.gy, 1);
+    const int i0 = tl.y * BQ, j0 = tl.x * BQ;
+    const int ke = g.K;
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
+    // this thread's share of a stage: A groups e = t + 512 q (row e / KG, k group e % KG), 8 floats each;
+    // B chunks of the same (row, k group) in both planes
+    const float* arow[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int gi = i0 + (t + 512 * q) / KG;
+        arow[q] = gi < g.I ? g.A + (int64_t)gi * g.lda : nullptr;
+    }
+    const int kg = t % KG;
+    f32x4_t va[2][2];
+    u32x4_t vp[2][2];
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+    const int pa = h3_pow(shard_max_bits(g.amax_a));
+    const float sa = pow2f(pa);
+    auto load_stage = [&](int k0) {
+        const int kk = k0 + kg * 8;
+        const bool ok = kk < ke;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            va[q][0] = load4v<AV>(arow[q], kk, ke);
+            va[q][1] = load4v<AV>(arow[q], kk + 4, ke);
+            const int64_t off = (int64_t)(j0 + (t + 512 * q) / KG) * g.ldb + kk;
+#pragma unroll
+            for (int p = 0; p < 2; p++)
+                vp[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? Bp + p * g.bplane + off
+                                                               : reinterpret_cast<const uint16_t*>(g_zero_row));
+        }
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int row = (t + 512 * q) / KG, c = xchunk<XK, XK>(row, kg) * 8;
+            u32x4_t h, l;
+            split2h(va[q], sa, h, l);
+            *reinterpret_cast<u32x4_t*>(&As[buf][0][row][c]) = h;
+            *reinterpret_cast<u32x4_t*>(&As[buf][1][row][c]) = l;
+#pragma unroll
+            for (int p = 0; p < 2; p++) *reinterpret_cast<u32x4_t*>(&Bs[buf][p][row][c]) = vp[p][q];
+        }
+    };
+    const int ra = wm * 64 + (lane & 31), rb = wn * 128 + (lane & 31);
+    auto mfma_stage = [&](int buf) {
+#pragma unroll
+        for (int ks = 0; ks < XK / 16; ks++) {
+            const int kc = 2 * ks + (lane >> 5);
+            h16x8 a[2][2], b[2][4];
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+#pragma unroll
+                for (int u = 0; u < 2; u++)
+                    a[p][u] = *(const h16x8*)&As[buf][p][ra + 32 * u][xchunk<XK, XK>(ra + 32 * u, kc) * 8];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    b[p][u] = *(const h16x8*)&Bs[buf][p][rb + 32 * u][xchunk<XK, XK>(rb + 32 * u, kc) * 8];
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 4; tj++) {
+                    f32x16 c = acc[ti][tj];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1][ti], b[0][tj], c, 0, 0, 0);  // l h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h l
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[0][tj], c, 0, 0, 0);  // h h
+                }
+        }
+    };
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    load_stage(XK);  // unconditional: past K it reads the zero row
+    int buf = 0;
+    for (int k0 = 0; k0 < ke; k0 += XK) {
+        mfma_stage(buf);
+        store_stage(buf ^ 1);
+        load_stage(k0 + 2 * XK);
+        __syncthreads();
+        buf ^= 1;
+    }
+    const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+    for (int tj = 0; tj < 4; tj++) {
+        const int j = j0 + wn * 128 + tj * 32 + l32;
+        const float bsc = g.bscale[j];
+        const float bj = g.bias ? g.bias[j] : 0.f;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (i < g.I) g.C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * bsc, -pa) + bj;
+            }
+    }
+}
+
 // ---- H3 GEMM on an LDS-DMA ring (gemm_h3r): C = A . B^T + bias with A_IK fp32 (k contiguous) and
 // B the pre-split fp16 planes -- the forward and input-gradient GEMMs of training.  128 x 128 tile,
 // 4 waves of 64 x 64, one workgroup per CU.  Both operands travel global -> LDS by

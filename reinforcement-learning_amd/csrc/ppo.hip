@@ -102,6 +102,19 @@ inline bool h3_wide(int J) {
     }();
     return mode == 1 ? J > mlp::BN : (mode == 0 ? false : J >= 1024);
 }
+// Forward / input-gradient H3 GEMMs with output widths that are multiples of 256 on the 256 x 256 tile kernel
+// mlp::gemm_h3q (same bits as gemm_x6): by default for 1024 or more output columns (the C5 leg's 2048-wide
+// layers: 32.1 -> 30.0 ms per 50k minibatch against gemm_h3w, profiles/r05ad_h3_quad_ab.txt); at 512 columns
+// (K = 512, 16 stages per tile) its one workgroup per CU cannot hide the tile's prologue and epilogue and the
+// C2 minibatch takes 1.59 -> 1.70 ms.  RLGPU_H3_QUAD=0: never, 1: for every width that is a multiple of 256.
+inline bool h3_quad(int J) {
+    static const int mode = [] {
+        const char* e = getenv("RLGPU_H3_QUAD");
+        return e ? atoi(e) : -1;
+    }();
+    if (J % mlp::BQ != 0) return false;
+    return mode == 1 ? true : (mode == 0 ? false : J >= 1024);
+}
 // Forward / input-gradient H3 GEMMs (A_IK x pre-split B) on the LDS-DMA ring kernel mlp::gemm_h3r when
 // RLGPU_H3_RING = 1 (32-deep stages, 4-stage ring), 2 (64-deep, 2 stages), 3 (32-deep, 3 stages) or 4
 // (32-deep, 2 stages, two workgroups per CU); 0 (default): the register-staged gemm_x6 path.  Same
@@ -407,6 +420,13 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
     g.gy = (int)ceil_div(I, mlp::BM);
     g.gz = 1;
     const bool av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && (K % 4 == 0 || a_tail_ok);
+    if (h3 && av && h3_quad(J)) {  // 256 x 256 tiles (bit-identical to gemm_x6's H3 path)
+        g.gx = J / mlp::BQ;
+        g.gy = (int)ceil_div(I, mlp::BQ);
+        hipLaunchKernelGGL((mlp::gemm_h3q<true>), dim3(g.gx * g.gy), dim3(512), 0, s, g);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        return;
+    }
     if (h3 && h3_wide(J)) {  // planes padded to a multiple of BNW rows (build_model)
         g.gx = (int)ceil_div(J, mlp::BNW);
         dim3 gridw(g.gx * g.gy);

@@ -459,3 +459,45 @@ def test_row_gemm_option_keeps_the_gradients(gpu, variant):
                        env=env, capture_output=True, text=True, timeout=360, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout
+
+
+_QUAD_CHILD = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[2], sys.argv[2] + "/reinforcement-learning_amd", sys.argv[2] + "/tests"]
+from rlgpu.ppo import PPO
+from test_ppo import make_batch
+dev = torch.device("cuda:0")
+out = []
+for n, layers in ((1000, (512, 512)), (3000, (256, 768, 512)), (700, (2048, 1024))):
+    p = PPO(policy_layers=layers, critic_layers=layers, max_rows=4096, seed=5)
+    obs, masks, acts, old, adv, tgt = make_batch(np.random.default_rng(n), n)
+    d = [torch.from_numpy(v).to(dev) for v in (obs, masks, acts, old, adv, tgt)]
+    p.adv_normalizer(d[4])
+    p.zero_grad()
+    p.minibatch(*d, None, 0, n, n)
+    out += [p.flat(grads=True).cpu().numpy(), p.forward(0, d[0]).cpu().numpy().ravel()]
+np.save(sys.argv[1], np.concatenate(out))
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_h3_quad_tiles_bit_identical(gpu, tmp_path):
+    """The 256 x 256 tile H3 GEMM (mlp::gemm_h3q: RLGPU_H3_QUAD=1 for every width that is a multiple of 256, by
+    default from 1024 columns) gives the same minibatch gradients and forward outputs, bit for bit, as the
+    128 x 128 gemm_x6 and 128 x 256 gemm_h3w paths (RLGPU_H3_QUAD=0): same products, same order into one
+    accumulator.  Row counts off the 256-row tile, widths 256 / 512 / 768 / 1024 / 2048.  The knob is read once
+    per process: child processes."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for v in ("0", "1"):
+        f = str(tmp_path / f"q{v}.npy")
+        r = subprocess.run([sys.executable, "-c", _QUAD_CHILD, f, root], env=dict(os.environ, RLGPU_H3_QUAD=v),
+                           capture_output=True, text=True, timeout=240, cwd=root)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        res[v] = np.load(f)
+    assert res["0"].shape == res["1"].shape
+    np.testing.assert_array_equal(res["0"].view(np.uint32), res["1"].view(np.uint32))
