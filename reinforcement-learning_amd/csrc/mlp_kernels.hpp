@@ -1156,6 +1156,119 @@ __global__ void __launch_bounds__(512, 1) gemm_h3q(GemmArgs g) {
     }
 }
 
+// ---- gemm_h3q's weight-gradient form (gemm_h3qt): A_KI (dZ^T) x B_KJ (activations), both row-index
+// contiguous, staged k-major as gemm_h3w stages its B (float4 loads along the output index, planes [k][256 + 32],
+// fragments read back with ds_read_b64_tr_b16); split-K over grid z like the other kernels.  Same products in
+// the same order per split as gemm_x6 / gemm_h3w: bit-identical partials.
+template <bool VEC>
+DEV void q_kload(f32x4_t (&v)[4], const float* base, int64_t ld, int o0, int on, int k0, int ke) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // element group e = t + 512 q: k row e / 64, float4 e % 64 of the 256 columns
+        const int e = (int)threadIdx.x + 512 * q;
+        const int k = k0 + e / 64, o = o0 + (e % 64) * 4;
+        const float* row = k < ke ? base + (int64_t)k * ld : nullptr;
+        v[q] = load4v<VEC>(row, o, on);
+    }
+}
+DEV void q_kstore(uint16_t* ph, uint16_t* pl, const f32x4_t (&v)[4], float sc) {
+    constexpr int P = BQ + 32;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = (int)threadIdx.x + 512 * q;
+        const int off = (e / 64) * P + (e % 64) * 4;
+        uint32_t h2[2], l2[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const float x0 = v[q][2 * c] * sc, x1 = v[q][2 * c + 1] * sc;
+            const uint16_t h0 = f2hf(x0), h1 = f2hf(x1);
+            h2[c] = pack_h2(h0, h1);
+            l2[c] = pack_h2(f2hf(x0 - hf2f(h0)), f2hf(x1 - hf2f(h1)));
+        }
+        *reinterpret_cast<uint2*>(ph + off) = make_uint2(h2[0], h2[1]);
+        *reinterpret_cast<uint2*>(pl + off) = make_uint2(l2[0], l2[1]);
+    }
+}
+template <bool AV, bool BV>
+__global__ void __launch_bounds__(512, 1) gemm_h3qt(GemmArgs g) {
+    constexpr int XK = 32, P = BQ + 32;
+    __shared__ uint16_t As[2][2][XK * P];  // [buffer][plane][k][o]
+    __shared__ uint16_t Bs[2][2][XK * P];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
+    const int i0 = tl.y * BQ, j0 = tl.x * BQ;
+    const int kb = tl.z * g.kchunk;
+    const int ke = min(g.K, kb + g.kchunk);
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
+    f32x4_t va[4], vb[4];
+    const int pa = h3_pow(shard_max_bits(g.amax_a)), pb = h3_pow(shard_max_bits(g.amax_b));
+    const float sa = pow2f(pa), sb = pow2f(pb);
+    auto load_stage = [&](int k0) {
+        q_kload<AV>(va, g.A, g.lda, i0, g.I, k0, ke);
+        q_kload<BV>(vb, g.B, g.ldb, j0, g.J, k0, ke);
+    };
+    auto store_stage = [&](int buf) {
+        q_kstore(&As[buf][0][0], &As[buf][1][0], va, sa);
+        q_kstore(&Bs[buf][0][0], &Bs[buf][1][0], vb, sb);
+    };
+    auto mfma_stage = [&](int buf) {
+#pragma unroll
+        for (int ks = 0; ks < XK / 16; ks++) {
+            h16x8 a[2][2], b[2][4];
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+#pragma unroll
+                for (int u = 0; u < 2; u++) a[p][u] = trp_frag<P>(&As[buf][p][0], wm * 64 + 32 * u, ks * 16, lane);
+#pragma unroll
+                for (int u = 0; u < 4; u++) b[p][u] = trp_frag<P>(&Bs[buf][p][0], wn * 128 + 32 * u, ks * 16, lane);
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 4; tj++) {
+                    f32x16 c = acc[ti][tj];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1][ti], b[0][tj], c, 0, 0, 0);  // l h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h l
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[0][tj], c, 0, 0, 0);  // h h
+                }
+        }
+    };
+    load_stage(kb);
+    store_stage(0);
+    __syncthreads();
+    load_stage(kb + XK);  // unconditional: past ke it reads the zero row
+    int buf = 0;
+    for (int k0 = kb; k0 < ke; k0 += XK) {
+        mfma_stage(buf);
+        store_stage(buf ^ 1);
+        load_stage(k0 + 2 * XK);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* C = g.C + (int64_t)tl.z * g.c_split;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int pab = pa + pb;
+#pragma unroll
+    for (int tj = 0; tj < 4; tj++) {
+        const int j = j0 + wn * 128 + tj * 32 + l32;
+        if (j >= g.J) continue;
+        const float bj = g.bias ? g.bias[j] : 0.f;
+#pragma unroll
+        for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (i < g.I) C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * 1.f, -pab) + bj;
+            }
+    }
+}
+
 // ---- H3 GEMM on an LDS-DMA ring (gemm_h3r): C = A . B^T + bias with A_IK fp32 (k contiguous) and
 // B the pre-split fp16 planes -- the forward and input-gradient GEMMs of training.  128 x 128 tile,
 // 4 waves of 64 x 64, one workgroup per CU.  Both operands travel global -> LDS by

@@ -103,8 +103,9 @@ inline bool h3_wide(int J) {
     return mode == 1 ? J > mlp::BN : (mode == 0 ? false : J >= 1024);
 }
 // Forward / input-gradient H3 GEMMs with output widths that are multiples of 256 on the 256 x 256 tile kernel
-// mlp::gemm_h3q (same bits as gemm_x6): by default for 1024 or more output columns (the C5 leg's 2048-wide
-// layers: 32.1 -> 30.0 ms per 50k minibatch against gemm_h3w, profiles/r05ad_h3_quad_ab.txt); at 512 columns
+// mlp::gemm_h3q, and weight gradients on mlp::gemm_h3qt (same bits as gemm_x6 / gemm_h3w): by default for 1024 or
+// more output columns (the C5 leg's 2048-wide layers: 31.6 -> 27.6 ms per 50k minibatch against gemm_h3w for both,
+// profiles/r05ad_h3_quad_ab.txt); at 512 columns
 // (K = 512, 16 stages per tile) its one workgroup per CU cannot hide the tile's prologue and epilogue and the
 // C2 minibatch takes 1.59 -> 1.70 ms.  RLGPU_H3_QUAD=0: never, 1: for every width that is a multiple of 256.
 inline bool h3_quad(int J) {
@@ -359,6 +360,18 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
     g.gx = (int)ceil_div(J, mlp::BN);
     g.gy = (int)ceil_div(I, mlp::BM);
     g.gz = z;
+    if (mode == RLGPU_GEMM_F16X3 && la == mlp::A_KI && lb == mlp::B_KJ && I % mlp::BQ == 0 && h3_quad(J)) {
+        // 256 x 256 tiles, the same split-K chunks (same bits as gemm_h3w / gemm_x6)
+        g.gx = J / mlp::BQ;
+        g.gy = I / mlp::BQ;
+        dim3 gridq(g.gx * g.gy * g.gz), blkq(512);
+        if (av && bv) hipLaunchKernelGGL((mlp::gemm_h3qt<true, true>), gridq, blkq, 0, s, g);
+        else if (av) hipLaunchKernelGGL((mlp::gemm_h3qt<true, false>), gridq, blkq, 0, s, g);
+        else if (bv) hipLaunchKernelGGL((mlp::gemm_h3qt<false, true>), gridq, blkq, 0, s, g);
+        else hipLaunchKernelGGL((mlp::gemm_h3qt<false, false>), gridq, blkq, 0, s, g);
+        RLGPU_CHECK_HIP(hipGetLastError());
+        return;
+    }
     if (mode == RLGPU_GEMM_F16X3 && la == mlp::A_KI && lb == mlp::B_KJ && h3_wide(J)) {
         g.gx = (int)ceil_div(J, mlp::BNW);
         dim3 gridw(g.gx * g.gy * g.gz), blkw(256);
