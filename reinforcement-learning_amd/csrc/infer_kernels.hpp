@@ -408,21 +408,16 @@ __global__ void __launch_bounds__(IT, 1) mlp_infer(InferArgs a) {
     __syncthreads();
     INFER_MARK(14);
     {
-        const uint16_t* lg[IRW];
-        const uint8_t* mk[IRW];
-        float* pr[IRW];
-        int row[IRW];
-        bool ok[IRW];
-#pragma unroll
-        for (int g = 0; g < IRW; g++) {
+        const auto rowfn = [&](int g, const uint16_t*& lg, const uint8_t*& mk, float*& pr, int& row, bool& ok) {
             const int r = w + IW * g;
-            lg[g] = Xs[r];
-            mk[g] = Ms + r * N;
-            pr[g] = reinterpret_cast<float*>(&Xs[r][kSampleProbs]);  // the row past its logits: the probs
-            row[g] = r0 + r;
-            ok[g] = Sel[r] != 0;
-        }
-        ppo::sample_rows<IRW, F16>(lg, mk, pr, N, a.det, a.seed, a.step, a.row0, row, ok, lane, a.act, a.logp);
+            lg = Xs[r];
+            mk = Ms + r * N;
+            pr = reinterpret_cast<float*>(&Xs[r][kSampleProbs]);  // the row past its logits: the probs
+            row = r0 + r;
+            ok = Sel[r] != 0;
+        };
+        const auto mark = [&](int k) { INFER_MARK(k == 0 ? 7 : 11); };  // trace slots 7 / 11 are free here
+        ppo::sample_rows_looped<IRW, F16>(rowfn, N, a.det, a.seed, a.step, a.row0, lane, a.act, a.logp, mark);
     }
     INFER_MARK(15);
 }

@@ -66,8 +66,9 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 // RG rows, one wave, interleaved (each cross-lane step issues for all RG rows before the next, so
 // one wave hides the shuffle latency of RG independent rows): lg[g] = row g's A logits (global or
 // LDS), mk[g] its masks, pr[g] A floats of LDS scratch for its probs; writes act[row[g]], logp[row[g]]
-// where ok[g].  sample_actions runs it with RG = 1, the fused inference kernel (infer_kernels.hpp) with
-// RG = 8 -- the per-row arithmetic is the same, so both draw the same actions from the same logits.
+// where ok[g].  sample_actions runs it with RG = 1; the fused inference kernel (infer_kernels.hpp) runs
+// sample_rows_looped (below) over 8 rows -- the per-row arithmetic is the same, so both draw the same actions
+// from the same logits.
 template <int RG, bool F16>
 __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], const uint8_t* const (&mk)[RG],
                                             float* const (&pr)[RG], int A, int deterministic, uint64_t seed,
@@ -182,6 +183,112 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
         }
     }
 }
+// sample_rows with the softmax and the writes in a loop over the RG rows instead of unrolled, for the fused
+// inference kernel: the unrolled form is ~1,900 instructions that each call executes once, so instruction
+// fetch, not arithmetic, set its time (its phase trace: 17 us from the staged logits to the probs).  Same
+// per-row operations in the same order (the probs go to LDS in both modes and the pick's prob is read back
+// from there: the same float), so the same actions and log probs; the running-sum walk keeps one lane per row,
+// all RG rows at once.  rowfn(g, lg, mk, pr, row, ok) gives row g's logits, masks, LDS probs, row and write flag;
+// mark(k) optional phase timestamps (the fused kernel's trace): 0 = probs in LDS, 1 = picks known.
+struct NoMark {
+    __device__ void operator()(int) const {}
+};
+template <int RG, bool F16, typename RowFn, typename Mark = NoMark>
+__device__ __forceinline__ void sample_rows_looped(RowFn rowfn, int A, int deterministic, uint64_t seed, uint64_t step,
+                                                   int64_t row0, int lane, int32_t* act, float* logp,
+                                                   Mark mark = Mark{}) {
+#pragma clang fp contract(off)
+    const int a0 = 2 * lane, a1 = 2 * lane + 1;
+    const bool in0 = a0 < A, in1 = a1 < A;
+    const int c0 = min(a0, A - 1), c1 = min(a1, A - 1);
+    int mine = A - 1;  // lane g < RG: row g's pick (deterministic: its argmax)
+#pragma unroll 1
+    for (int g = 0; g < RG; g++) {
+        const uint16_t* lg;
+        const uint8_t* mk;
+        float* pr;
+        int rw;
+        bool ok;
+        rowfn(g, lg, mk, pr, rw, ok);
+        const float l0 = mlp::h2f<F16>(lg[c0]), l1 = mlp::h2f<F16>(lg[c1]);
+        const uint8_t m0 = mk[c0], m1 = mk[c1];
+        float z0 = in0 ? l0 + (m0 ? 0.f : kDisabledLogit) : 0.f;
+        float z1 = in1 ? l1 + (m1 ? 0.f : kDisabledLogit) : 0.f;
+        const float m = mlp::wave_max_x(fmaxf(in0 ? z0 : -INFINITY, in1 ? z1 : -INFINITY));
+        z0 = in0 ? rs_expf(z0 - m) : 0.f;
+        z1 = in1 ? rs_expf(z1 - m) : 0.f;
+        const float s = mlp::wave_sum_x(z0 + z1);
+        const float p0 = in0 ? fminf(fmaxf(z0 / s, kMinProb), 1.f) : 0.f;
+        const float p1 = in1 ? fminf(fmaxf(z1 / s, kMinProb), 1.f) : 0.f;
+        if (deterministic) {
+            float best = fmaxf(p0, p1);
+            int bi = p0 >= p1 ? a0 : a1;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const float ob = __shfl_xor(best, o, 64);
+                const int oi = __shfl_xor(bi, o, 64);
+                const bool take = ob > best || (ob == best && oi < bi);
+                best = take ? ob : best;
+                bi = take ? oi : bi;
+            }
+            mine = lane == g ? bi : mine;
+        }
+        if (in0) pr[a0] = p0;
+        if (in1) pr[a1] = p1;
+    }
+    mark(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!deterministic && lane < RG) {
+        const uint16_t* lg;
+        const uint8_t* mk;
+        float* p;
+        int rw;
+        bool ok;
+        rowfn(lane, lg, mk, p, rw, ok);
+        const float r = (float)(philox(sample_key(seed, step), (uint32_t)(row0 + rw), (uint32_t)step) >> 8) *
+                        (1.f / 16777216.f);
+        float running = 0.f;
+        bool found = false;
+        int j = 0;
+        for (; j + 8 <= A; j += 8) {
+            float q[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) q[k] = p[j + k];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                running += q[k];
+                const bool hit = !found && r <= running;
+                mine = hit ? j + k : mine;
+                found = found || hit;
+            }
+        }
+        for (; j < A; j++) {
+            running += p[j];
+            const bool hit = !found && r <= running;
+            mine = hit ? j : mine;
+            found = found || hit;
+        }
+    }
+    mark(1);
+#pragma unroll 1
+    for (int g = 0; g < RG; g++) {
+        const int pk = __shfl(mine, g, 64);
+        const uint16_t* lg;
+        const uint8_t* mk;
+        float* pr;
+        int rw;
+        bool ok;
+        rowfn(g, lg, mk, pr, rw, ok);
+        if (lane == 0 && ok) {
+            act[rw] = pk;
+            const float pp = pr[pk];
+            if (logp) logp[rw] = rs_logf(1e-12f < pp ? pp : 1e-12f);  // log(std::max(1e-12f, p))
+        }
+    }
+}
+
 template <bool F16>
 __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
                                                      int deterministic, uint64_t seed, uint64_t step, int64_t row0,

@@ -17,8 +17,8 @@ from rlgpu.ppo import PPO  # noqa: E402
 
 NAMES = {0: "start", 1: "obs staged", 2: "L0 mfma", 8: "L0 epilogue", 3: "L0 ln", 4: "L1 mfma", 9: "L1 epilogue",
          5: "L1 ln", 6: "L2 mfma", 10: "L2 epilogue", 12: "out start", 13: "out mfma", 14: "logits staged",
-         15: "sampled"}
-ORDER = [0, 1, 2, 8, 3, 4, 9, 5, 6, 10, 12, 13, 14, 15]
+         15: "sampled", 7: "probs", 11: "picks"}
+ORDER = [0, 1, 2, 8, 3, 4, 9, 5, 6, 10, 12, 13, 14, 7, 11, 15]
 
 
 def report(tag, tr, nblk):
