@@ -77,6 +77,75 @@ def cpu_cores():
     return n
 
 
+class GpuClock:
+    """Samples the GPU's shader clock (sysfs pp_dpm_sclk, the starred level) and board power (hwmon) every
+    50 ms in a thread, so a bench line says at what clock its kernels ran: box-to-box spread in the env
+    kernel's per-launch time (a latency-bound kernel scales with sclk) shows up here.  Read-only sysfs; on a
+    host without it every field is None."""
+
+    def __init__(self, dev):
+        import glob
+        import threading
+        self.path, self.power, self.samples, self.watts = None, None, [], []
+        bus = None
+        try:
+            import torch
+            p = torch.cuda.get_device_properties(dev)
+            bus = "%04x:%02x:%02x" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        except Exception:
+            pass
+        cards = sorted(glob.glob("/sys/bus/pci/devices/*/pp_dpm_sclk"))
+        mine = [c for c in cards if bus and os.path.basename(os.path.dirname(c)).startswith(bus)]
+        pick = mine or (cards if len(cards) == 1 else [])
+        if pick:
+            self.path = pick[0]
+            pw = sorted(glob.glob(os.path.join(os.path.dirname(self.path), "hwmon", "hwmon*", "power1_average")) +
+                        glob.glob(os.path.join(os.path.dirname(self.path), "hwmon", "hwmon*", "power1_input")))
+            self.power = pw[0] if pw else None
+        self.pci = os.path.basename(os.path.dirname(self.path)) if self.path else bus
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        try:
+            for line in open(self.path):
+                if line.rstrip().endswith("*"):
+                    return float(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz").strip())
+        except (OSError, ValueError, IndexError):
+            return None
+        return None
+
+    def _run(self):
+        while not self._stop.wait(0.05):
+            mhz = self._read()
+            if mhz is not None:
+                self.samples.append(mhz)
+            if self.power:
+                try:
+                    self.watts.append(int(open(self.power).read()) / 1e6)
+                except (OSError, ValueError):
+                    pass
+
+    def __enter__(self):
+        if self.path:
+            self._t.start()
+        return self
+
+    def __exit__(self, *a):
+        self._stop.set()
+        if self._t.is_alive():
+            self._t.join()
+
+    def summary(self):
+        import statistics
+
+        def mmm(v, unit):
+            return None if not v else {"min": min(v), "median": statistics.median(v), "max": max(v), "unit": unit,
+                                       "samples": len(v)}
+        return {"source": self.path, "pci": self.pci, "sclk": mmm(self.samples, "MHz"),
+                "power": mmm(self.watts, "W")}
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -285,6 +354,7 @@ def main():
     # one rank per GPU; ranks beyond the visible GPUs (single-GPU rehearsals) share them round-robin
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    backend = None
     if world > 1:
         backend = os.environ.get("RLGPU_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo only for rehearsals
         if backend == "nccl":
@@ -305,7 +375,12 @@ def main():
     cfg = LearnerConfig(num_arenas=args.arenas, rollout_len=args.rollout, train_against_old_versions=False,
                         train_gemm=train_gemm, mesh=mesh, arith=arith,
                         collect_groups=int(os.environ.get("RLGPU_BENCH_COLLECT_GROUPS", "0")))  # 0: automatic
-    L = Learner(cfg, device=dev, rank=rank, world=world)  # the C++ host Learner (host/learner.cpp)
+    # the C++ host Learner (host/learner.cpp); for N > 1 on RCCL its exchanges (gradient all-reduce, moments,
+    # return samples) run on the native RCCL communicator in C++ (host/rccl_collective.cpp): torch.distributed
+    # only broadcasts RCCL's unique id.  A gloo rehearsal (several ranks on one GPU) uses the torch.distributed
+    # callbacks instead, since RCCL refuses two ranks on one device.
+    native_rccl = world > 1 and backend == "nccl"
+    L = Learner(cfg, device=dev, rank=rank, world=world, native_rccl=native_rccl)
     # HIP events around every fused env step, on the stream it runs on (RLGPU_BENCH_ENV_TIMING=0: none)
     L.set_env_timing(os.environ.get("RLGPU_BENCH_ENV_TIMING", "1") != "0")
 
@@ -316,7 +391,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     phase = {"collect": 0.0, "consume": 0.0, "learn": 0.0, "learn_issue": 0.0, "collect_issue": 0.0}
-    kern = []
+    kern, kern_min, kern_med, kern_max = [], [], [], []
+    clock = GpuClock(dev).__enter__()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         rep = L.iterate()
@@ -326,12 +402,16 @@ def main():
         phase["learn_issue"] += rep["learn_issue_s"]
         phase["collect_issue"] += rep["collect_issue_s"]
         kern.append(rep["env_kernel_ms"])
+        kern_min.append(rep["env_kernel_min_ms"])
+        kern_med.append(rep["env_kernel_median_ms"])
+        kern_max.append(rep["env_kernel_max_ms"])
         launch_arenas = rep["env_launch_arenas"]  # arenas per env launch (the collection's arena groups)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    clock.__exit__()
     from rlgpu.dist import max_over_ranks
     el = max_over_ranks(el, device=dev)
     env_steps = world * args.arenas * cfg.rollout_len * args.steps
@@ -353,6 +433,8 @@ def main():
                                "LayerNorm+LeakyReLU, bf16 inference / fp32 training, T=128, 2 epochs, minibatch 50k",
                    "arenas_per_gpu": args.arenas, "agents_per_gpu": 4 * args.arenas, "rollout_len": cfg.rollout_len,
                    "parallelism": f"arena-sharded dp{world}", "inference_dtype": "bf16", "train_dtype": "f32",
+                   "collective": ("native RCCL (host/rccl_collective.cpp)" if native_rccl else
+                                  f"torch.distributed {backend} callbacks" if world > 1 else None),
                    "train_gemm": args.train_gemm, "arith": args.arith,
                    "self_play": "off (trainAgainstOldVersions = false: every timed iteration does the same work; "
                                 "the old-version path is tested in tests/test_learner_gpu.py)",
@@ -367,6 +449,10 @@ def main():
         "roofline": {"bound": "hbm", "limiter": "latency (per-arena serial physics phases)", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_pmc": traffic_src,
                      "kernel": "rl::env_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": b_env,
+                     # per-launch spread over the timed iterations (min / median of the per-iteration medians /
+                     # max) and the shader clock sampled over the timed region: what box-to-box spread is made of
+                     "kernel_ms_min": min(kern_min), "kernel_ms_median": sorted(kern_med)[len(kern_med) // 2],
+                     "kernel_ms_max": max(kern_max), "gpu_clock": clock.summary(),
                      "units_per_launch": launch_arenas, "collection_groups": args.arenas // launch_arenas,
                      "algorithmic_bytes_per_launch": b_env * launch_arenas},
     }

@@ -56,7 +56,8 @@ float rlgpu_x86_rsqrtss_emulated(float x);
  * -> pos[3] rot[9]; 5 a wheel ray's btSubsimplexConvexCast (btCollisionWorld.cpp:277-310) of the segment
  * from[3] (at 9) to[3] (at 12) against a resting body of basis rot[9] (at 0) and origin o[3] (at 15), a box of
  * half extents h[3] (at 18, with its margin) or a sphere of radius r (at 21, > 0) -> hit, fraction, normal[3];
- * 6 the kernels' rsqrtss of the row's first 12 floats -> 12 floats.
+ * 6 the kernels' rsqrtss of the row's first 12 floats -> 12 floats; 7 the transcendentals of
+ * include/rlgpu_detmath.h: sin in[0], cos in[0], atan2(in[1], in[2]), asin in[3], atan in[4] -> out[0..4].
  * d_in [n][24], d_out [n][12] floats (device).  Asynchronous on `stream`. */
 int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream);
 

@@ -300,6 +300,12 @@ int rlgpu_envset_step(rlgpu_envset* env, const int32_t* d_actions, int32_t reset
 int rlgpu_envset_step_range(rlgpu_envset* env, int32_t first, int32_t count, const int32_t* d_actions,
                             int32_t reset_terminated, const rlgpu_step_outputs* out, void* stream);
 int rlgpu_envset_sync(rlgpu_envset* env, void* stream);
+/* Output-only rows (default off): a fused step given `out` rows for obs / masks / truncation obs writes those
+ * rows only there, not also into the set's own buffers (rlgpu_envset_buffers obs / masks / trunc_obs), which
+ * then keep the last step that had no such output.  One copy of the 3 KB of rows per env step instead of two
+ * (obs 2,672 B + masks 360 B per arena); the C++ Learner turns it on for its own set, whose rollout rows are the
+ * only ones it reads.  A step without `out` (or with a NULL row pointer) writes the set's buffers as always. */
+int rlgpu_envset_set_output_only(rlgpu_envset* env, int32_t enable);
 
 /* Wire-format state transfer (host <-> device), for GameState snapshots, tests and replay. */
 int rlgpu_envset_get_arenas(rlgpu_envset* env, int32_t first, int32_t count, rlgpu_arena_state* h_out);

@@ -200,6 +200,9 @@ typedef struct {
                                                close to learn_s means the phase is launch-bound */
     double collect_issue_s;                 /* the same for the collection phase */
     int32_t env_launch_arenas;              /* arenas per timed env launch (num_arenas / collection groups) */
+    double env_kernel_min_ms;               /* fastest / median / slowest timed env launch of the iteration */
+    double env_kernel_median_ms;
+    double env_kernel_max_ms;
 } rlgpu_learner_report;
 
 typedef struct rlgpu_learner rlgpu_learner;

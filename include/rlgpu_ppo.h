@@ -57,8 +57,11 @@ typedef struct {
     uint64_t seed;                            /* parameter init + action sampling (Philox) */
     int32_t train_gemm;                       /* training GEMM arithmetic: RLGPU_GEMM_F32X6 (0),
                                                  RLGPU_GEMM_F32 (1) or RLGPU_GEMM_F16X3 (2) -- see rlgpu_gemm */
-    int32_t infer_fp16;                       /* 16-bit inference copy: 0 = bf16 (the reference's seqHalf),
-                                                 1 = fp16 on v_mfma_f32_32x32x16_f16 (BASELINE config C5) */
+    int32_t infer_fp16;                       /* inference precision (RLGPU_INFER_*): 0 = bf16 (the reference's
+                                                 seqHalf), 1 = fp16 on v_mfma_f32_32x32x16_f16 (BASELINE config
+                                                 C5), 2 = fp32 (PPOLearnerConfig::useHalfPrecision = false:
+                                                 Model::Forward's fp32 branch, Models.cpp:36-68, on the training
+                                                 forward; no old-version inference in this mode) */
     /* PPOLearnerConfig::sharedHead (PPOLearner.cpp:42-74): [Linear -> LayerNorm -> LeakyReLU] x k with
      * no output layer, run once on the obs; policy and critic then take its last activation as input
      * (ExampleMain: {512, 512} x scale, run_out.log:25-28 shows [384, 384]).  n_shared_layers = 0: no
@@ -84,6 +87,8 @@ typedef struct {
  *                     correction terms in separate f32 accumulators (the 3xTF32 scheme of fp32
  *                     emulation): half the MFMAs of F32X6, products within 2^-22 relative. */
 enum { RLGPU_GEMM_F32X6 = 0, RLGPU_GEMM_F32 = 1, RLGPU_GEMM_F16X3 = 2 };
+/* rlgpu_ppo_config.infer_fp16 values */
+enum { RLGPU_INFER_BF16 = 0, RLGPU_INFER_F16 = 1, RLGPU_INFER_F32 = 2 };
 
 typedef struct rlgpu_ppo rlgpu_ppo;
 

@@ -203,8 +203,10 @@ def pad_map():
 # ------------------------------------------------------------------ action sampler (sampler_ref.c)
 def sample_actions(logits16, masks, deterministic, seed, step, row0=0, f16=False, with_logp=True):
     """oracle_sample_actions: PPOLearner.cpp:78-184 in the GPU sampler's operation order.
-    logits16: uint16 [n, A] bf16 (or fp16) bit patterns.  Returns (actions int32 [n], logp f32 [n])."""
-    lg = np.ascontiguousarray(logits16, np.uint16)
+    logits16: uint16 [n, A] bf16 (or fp16) bit patterns, or float32 [n, A] logits (the fp32 inference of
+    useHalfPrecision = false).  Returns (actions int32 [n], logp f32 [n])."""
+    kind = 2 if np.asarray(logits16).dtype == np.float32 else int(f16)
+    lg = np.ascontiguousarray(logits16, np.float32 if kind == 2 else np.uint16)
     mk = np.ascontiguousarray(masks, np.uint8)
     n, A = lg.shape
     act = np.empty(n, np.int32)
@@ -213,13 +215,15 @@ def sample_actions(logits16, masks, deterministic, seed, step, row0=0, f16=False
     f.restype = None
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                   ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-    f(_p(lg), _p(mk), n, A, int(deterministic), seed, step, row0, int(f16), _p(act), _p(lp))
+    f(_p(lg), _p(mk), n, A, int(deterministic), seed, step, row0, kind, _p(act), _p(lp))
     return act, lp
 
 
 def sampler_probs(logits16, masks, seed, step, row0=0, f16=False):
-    """The clamped probs [n, A] the sampler draws from and each row's uniform r [n] (oracle_sampler_probs)."""
-    lg = np.ascontiguousarray(logits16, np.uint16)
+    """The clamped probs [n, A] the sampler draws from and each row's uniform r [n] (oracle_sampler_probs);
+    float32 logits as in sample_actions."""
+    kind = 2 if np.asarray(logits16).dtype == np.float32 else int(f16)
+    lg = np.ascontiguousarray(logits16, np.float32 if kind == 2 else np.uint16)
     mk = np.ascontiguousarray(masks, np.uint8)
     n, A = lg.shape
     pr = np.empty((n, A), np.float32)
@@ -228,7 +232,7 @@ def sampler_probs(logits16, masks, seed, step, row0=0, f16=False):
     f.restype = None
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                   ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-    f(_p(lg), _p(mk), n, A, seed, step, row0, int(f16), _p(pr), _p(r))
+    f(_p(lg), _p(mk), n, A, seed, step, row0, kind, _p(pr), _p(r))
     return pr, r
 
 
@@ -246,6 +250,14 @@ def detmath_trig(op, x, y=None, variant=""):
     f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     f(TRIG_OPS[op], _p(x), _p(yy), x.size, _p(out))
     return out
+
+
+def set_libm_sites(mask):
+    """Which call sites (include/rlgpu_detmath.h RS_SITE_* bits, -1 = all) the "libm" variant swaps libm in at."""
+    f = lib("libm").oracle_set_libm_sites
+    f.restype = None
+    f.argtypes = [ctypes.c_int]
+    f(int(mask) & 0x7FFFFFFF if mask != -1 else 0x7FFFFFFF)
 
 
 def detmath_exp_log(x):

@@ -128,7 +128,7 @@ inline void cull_points2(int n, const float p[], int m, int i0, int iret[]) {
         cy = a * (cy + q * (p[n * 2 - 1] + p[1]));
     }
     float A[8];
-    for (i = 0; i < n; i++) A[i] = rs_atan2f(p[i * 2 + 1] - cy, p[i * 2] - cx);
+    for (i = 0; i < n; i++) A[i] = rs_atan2f_at(p[i * 2 + 1] - cy, p[i * 2] - cx, RS_SITE_BOXBOX);
     int avail[8];
     for (i = 0; i < n; i++) avail[i] = 1;
     avail[i0] = 0;

@@ -37,7 +37,7 @@ const float EQUAL_VERTEX = 0.0001f * 0.0001f, EDGE_DIST = 0.1f, MAX_EDGE_ANGLE =
 enum { V0V1_CONVEX = 1, V1V2_CONVEX = 2, V2V0_CONVEX = 4, V0V1_SWAP = 8, V1V2_SWAP = 16, V2V0_SWAP = 32 };
 
 inline float get_angle(V edgeA, V normalA, V normalB) {  // btGetAngle
-    return rs_atan2f(dot(normalB, edgeA), dot(normalB, normalA));
+    return rs_atan2f_at(dot(normalB, edgeA), dot(normalB, normalA), RS_SITE_EDGE);
 }
 inline V calc_normal(V a, V b, V c) {  // btTriangleShape::calcNormal
     return bt_normalize(cross(b - a, c - a));

@@ -252,8 +252,8 @@ struct KickoffReward {
         float pvb = dot(pl.vel, p2b), tvb = dot(tm.vel, t2b);
         float sscore = (pvb > tvb) ? 0.3f : 0.f;
         float bscore = (pl.boost > tm.boost + 10.f) ? 0.2f : 0.f;
-        float pa = rs_atan2f(pl.pos.y - bpos.y, pl.pos.x - bpos.x);
-        float ta = rs_atan2f(tm.pos.y - bpos.y, tm.pos.x - bpos.x);
+        float pa = rs_atan2f_at(pl.pos.y - bpos.y, pl.pos.x - bpos.x, RS_SITE_KICKOFF);
+        float ta = rs_atan2f_at(tm.pos.y - bpos.y, tm.pos.x - bpos.x, RS_SITE_KICKOFF);
         float adiff = std::fabs(pa - ta);
         float spawn = (adiff > (3.14159f / 3.f)) ? 1.f : 0.f;
         float total = dscore + sscore + bscore + spawn * 0.1f;
@@ -410,7 +410,7 @@ static Plugins example_main_plugins() {
 // deterministic kernels shared with the device (include/rlgpu_detmath.h)
 static float powf_det(float a, float b) {
 #ifdef RLGPU_DETMATH_LIBM
-    return powf(a, b);  // the reference's call, host libm (tests/test_detmath_bound.py)
+    if (RS_LIBM_AT(RS_SITE_POW)) return powf(a, b);  // the reference's call, host libm (tests/test_detmath_bound.py)
 #endif
     if (b == 0.5f) return std::sqrt(a);
     if (b == 0.f) return 1.f;

@@ -163,8 +163,8 @@ inline Q qsafe_normalize(Q q) {
 }
 inline Q quat_axis_angle(V axis, float angle) {  // btQuaternion::setRotation
     float d = len(axis);
-    float s = rs_sinf(angle * 0.5f) / d;
-    return {axis.x * s, axis.y * s, axis.z * s, rs_cosf(angle * 0.5f)};
+    float s = rs_sinf_at(angle * 0.5f, RS_SITE_AXIS_ANGLE) / d;
+    return {axis.x * s, axis.y * s, axis.z * s, rs_cosf_at(angle * 0.5f, RS_SITE_AXIS_ANGLE)};
 }
 // btMatrix3x3::setRotation (btMatrix3x3.h:216-280), s = 2 / q.length2().  The SSE branch (:222-272)
 // builds each row from unscaled products -- row 0 (-yy + -zz, xy + -wz, zx + yw), row 1 (xy + zw,
@@ -232,8 +232,8 @@ inline void integrate_transform(V pos, const M& rot, V linvel, V angvel, float d
     if (fAngle < 0.001f)
         axis = angvel * (0.5f * dt - (dt * dt * dt) * 0.020833333333f * fAngle * fAngle);
     else
-        axis = angvel * (rs_sinf(0.5f * fAngle * dt) / fAngle);
-    Q dorn{axis.x, axis.y, axis.z, rs_cosf(fAngle * dt * 0.5f)};
+        axis = angvel * (rs_sinf_at(0.5f * fAngle * dt, RS_SITE_INTEGRATE) / fAngle);
+    Q dorn{axis.x, axis.y, axis.z, rs_cosf_at(fAngle * dt * 0.5f, RS_SITE_INTEGRATE)};
     Q orn0 = quat_from_mat(rot);
     Q pred = qmul(dorn, orn0);
     pred = qsafe_normalize(pred);

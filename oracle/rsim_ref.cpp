@@ -991,9 +991,9 @@ struct Sim {
                             init.y *= ((1.9f - 1) * ratio) + 1.f;
                             if (back) init.x *= 16.f / 15.f;
                             V fdir = c.rot.col(0);
-                            float ang = rs_atan2f(fdir.y, fdir.x);
+                            float ang = rs_atan2f_at(fdir.y, fdir.x, RS_SITE_FLIP);
                             float sa, ca;
-                            rs_sincosf(ang, &sa, &ca);
+                            rs_sincosf_at(ang, &sa, &ca, RS_SITE_FLIP);
                             V xdir(ca, -sa, 0.f), ydir(sa, ca, 0.f);
                             V dv(dot(init, xdir), dot(init, ydir), 0.f);
                             c.apply_central_impulse(dv * UU_TO_BT * CAR_MASS);
@@ -1026,13 +1026,10 @@ struct Sim {
         if (jump_pressed && cs.world_contact && cs.world_contact_normal[2] > (float)M_SQRT1_2) {
             // Angle::FromRotMat -> btMatrix3x3::getEulerYPR roll, negated (MathTypes.cpp:62-71)
             const M& m = c.rot;
-            float r0 = rs_atan2f(m.r[2].y, m.r[2].z);
-            float pitch_raw;
-            {
-                float x = -m.r[2].x;
-                float sq = std::sqrt(std::max(0.f, 1.f - x * x));
-                pitch_raw = rs_asinf(x, sq);
-            }
+            float r0 = rs_atan2f_at(m.r[2].y, m.r[2].z, RS_SITE_EULER);
+            // btAsin (btScalar.h): clamp to [-1, 1], then asin
+            const float ax = -m.r[2].x;
+            float pitch_raw = rs_asinf_at(ax < -1.f ? -1.f : (ax > 1.f ? 1.f : ax), RS_SITE_EULER);
             if (std::fabs(pitch_raw) == SIMD_HALF_PI) r0 = r0 > 0 ? r0 - SIMD_PI : r0 + SIMD_PI;
             float roll = -r0;
             float abs_roll = std::fabs(roll);

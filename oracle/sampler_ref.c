@@ -56,6 +56,13 @@ static float h2f(uint16_t h, int f16) {
     return rs_bits_float(sign | ((ex + 112) << 23) | (man << 13));
 }
 
+/* logit idx of a row block: kind 0 bf16, 1 fp16 (16-bit storage), 2 fp32 (the pointer holds floats: the
+ * useHalfPrecision = false inference, Models.cpp:36-68) */
+static float logit_at(const uint16_t* base, int64_t idx, int kind) {
+    if (kind == 2) return ((const float*)(const void*)base)[idx];
+    return h2f(base[idx], kind);
+}
+
 /* pairwise tree over the 64 lanes (the xor butterfly's result on every lane) */
 static float tree_sum(float* v) {
     for (int w = NL / 2; w >= 1; w >>= 1)
@@ -71,7 +78,7 @@ static float tree_max(float* v) {
 void oracle_sample_actions(const uint16_t* logits, const uint8_t* masks, int64_t n, int A, int deterministic,
                            uint64_t seed, uint64_t step, int64_t row0, int f16, int32_t* act, float* logp) {
     for (int64_t row = 0; row < n; row++) {
-        const uint16_t* lg = logits + row * A;
+        const int64_t lg = row * A;
         const uint8_t* mk = masks + row * A;
         float z0[NL], z1[NL], p0[NL], p1[NL], t[NL];
         int in0[NL], in1[NL];
@@ -79,8 +86,8 @@ void oracle_sample_actions(const uint16_t* logits, const uint8_t* masks, int64_t
             const int a0 = 2 * l, a1 = 2 * l + 1;
             in0[l] = a0 < A;
             in1[l] = a1 < A;
-            z0[l] = in0[l] ? h2f(lg[a0], f16) + (mk[a0] ? 0.f : kDisabled) : 0.f;
-            z1[l] = in1[l] ? h2f(lg[a1], f16) + (mk[a1] ? 0.f : kDisabled) : 0.f;
+            z0[l] = in0[l] ? logit_at(logits, lg + a0, f16) + (mk[a0] ? 0.f : kDisabled) : 0.f;
+            z1[l] = in1[l] ? logit_at(logits, lg + a1, f16) + (mk[a1] ? 0.f : kDisabled) : 0.f;
             t[l] = fmaxf(in0[l] ? z0[l] : -INFINITY, in1[l] ? z1[l] : -INFINITY);
         }
         const float m = tree_max(t);
@@ -127,7 +134,7 @@ void oracle_sample_actions(const uint16_t* logits, const uint8_t* masks, int64_t
 void oracle_sampler_probs(const uint16_t* logits, const uint8_t* masks, int64_t n, int A, uint64_t seed, uint64_t step,
                           int64_t row0, int f16, float* probs, float* r) {
     for (int64_t row = 0; row < n; row++) {
-        const uint16_t* lg = logits + row * A;
+        const int64_t lg = row * A;
         const uint8_t* mk = masks + row * A;
         float z0[NL], z1[NL], t[NL];
         int in0[NL], in1[NL];
@@ -135,8 +142,8 @@ void oracle_sampler_probs(const uint16_t* logits, const uint8_t* masks, int64_t 
             const int a0 = 2 * l, a1 = 2 * l + 1;
             in0[l] = a0 < A;
             in1[l] = a1 < A;
-            z0[l] = in0[l] ? h2f(lg[a0], f16) + (mk[a0] ? 0.f : kDisabled) : 0.f;
-            z1[l] = in1[l] ? h2f(lg[a1], f16) + (mk[a1] ? 0.f : kDisabled) : 0.f;
+            z0[l] = in0[l] ? logit_at(logits, lg + a0, f16) + (mk[a0] ? 0.f : kDisabled) : 0.f;
+            z1[l] = in1[l] ? logit_at(logits, lg + a1, f16) + (mk[a1] ? 0.f : kDisabled) : 0.f;
             t[l] = fmaxf(in0[l] ? z0[l] : -INFINITY, in1[l] ? z1[l] : -INFINITY);
         }
         const float m = tree_max(t);
@@ -155,19 +162,19 @@ void oracle_sampler_probs(const uint16_t* logits, const uint8_t* masks, int64_t 
 }
 
 /* rs_expf / rs_logf over arrays (known-answer tests of the shared kernels against libm) */
-/* rs_sinf / rs_cosf / rs_atan2f / rs_asinf over arrays (op 0 sin x, 1 cos x, 2 atan2(y, x), 3 asin x with
- * sqrtf(1 - x^2) as the simulator forms it, 4 atan x); liboracle_libm.so returns the host libm's values */
+/* rs_sinf / rs_cosf / rs_atan2f / rs_asinf over arrays (op 0 sin x, 1 cos x, 2 atan2(y, x), 3 asin x, 4 atan x);
+ * liboracle_libm.so returns the host libm's values at the call sites selected by oracle_set_libm_sites */
+#ifdef RLGPU_DETMATH_LIBM
+int rlgpu_libm_sites = RS_SITE_ANY;
+void oracle_set_libm_sites(int mask) { rlgpu_libm_sites = mask; }
+#endif
 void oracle_detmath_trig(int op, const float* x, const float* y, int64_t n, float* out) {
     for (int64_t i = 0; i < n; i++) {
         switch (op) {
         case 0: out[i] = rs_sinf(x[i]); break;
         case 1: out[i] = rs_cosf(x[i]); break;
         case 2: out[i] = rs_atan2f(y[i], x[i]); break;
-        case 3: {
-            const float t = 1.f - x[i] * x[i];
-            out[i] = rs_asinf(x[i], sqrtf(t > 0.f ? t : 0.f));
-            break;
-        }
+        case 3: out[i] = rs_asinf(x[i]); break;
         default: out[i] = rs_atanf(x[i]); break;
         }
     }

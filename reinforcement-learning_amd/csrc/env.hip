@@ -216,6 +216,7 @@ struct rlgpu_envset {
     double* d_metrics = nullptr;   // StepCallback slots [num_arenas][RLGPU_STEP_METRIC_SLOTS] or null
     uint64_t metric_calls = 0;     // ExampleMain's stepCounter
     bool metric_players = false;   // this step's player-metrics flag (rlgpu_envset_step_range)
+    bool output_only = false;      // rlgpu_envset_set_output_only: rows given in rlgpu_step_outputs go only there
     void *d_cell_tri = nullptr, *d_cell_start = nullptr, *d_tri = nullptr, *d_edge = nullptr;  // arena mesh (MeshView)
     void* d_gjk = nullptr;  // per-lane box-triangle penetration-solver scratch (MeshView::gjk)
     rl::MeshView mesh{};
@@ -362,6 +363,15 @@ void ensure_const() {
     g_const_ready[dev] = 1;
 }
 
+// rlgpu_envset_set_output_only: the rows a step appends to its outputs are not also written to the set's own
+// buffers (the kernel skips a copy whose pointer is null)
+void output_only_rows(const rlgpu_envset* e, rl::StepArgs& g) {
+    if (!e->output_only) return;
+    if (g.out_obs) g.obs = nullptr;
+    if (g.out_masks) g.masks = nullptr;
+    if (g.out_trunc) g.trunc_obs = nullptr;
+}
+
 void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.arenas = e->d_arenas;
     g.n = e->cfg.num_arenas;
@@ -381,6 +391,7 @@ void launch(rlgpu_envset* e, rl::StepArgs g, hipStream_t s) {
     g.fuzz = e->cfg.state_setter == RLGPU_SS_FUZZED_KICKOFF;
     g.pen_slots = e->pen_slots;
     g.reward_values = g.build ? e->d_reward_values : nullptr;
+    output_only_rows(e, g);
     if (g.build && e->d_metrics) {  // one StepCallback call (Learner.cpp:796-797, ExampleMain.cpp:236-237)
         g.metrics = e->d_metrics;
         g.metrics_players = (++e->metric_calls % 4) == 0;
@@ -417,6 +428,7 @@ void launch_range(rlgpu_envset* e, rl::StepArgs g, int first, int count, bool me
     g.fuzz = e->cfg.state_setter == RLGPU_SS_FUZZED_KICKOFF;
     g.pen_slots = e->pen_slots;
     g.reward_values = g.build && e->d_reward_values ? e->d_reward_values + P0 * e->plug.nr : nullptr;
+    output_only_rows(e, g);
     if (g.build && e->d_metrics) {
         g.metrics = e->d_metrics + (size_t)first * RLGPU_STEP_METRIC_SLOTS;
         g.metrics_players = metrics_players;
@@ -788,6 +800,13 @@ extern "C" int rlgpu_envset_step_range(rlgpu_envset* e, int32_t first, int32_t c
     });
 }
 
+extern "C" int rlgpu_envset_set_output_only(rlgpu_envset* e, int32_t enable) {
+    return rlgpu::guarded([&] {
+        RLGPU_REQUIRE(e, "null envset");
+        e->output_only = enable != 0;
+    });
+}
+
 extern "C" int rlgpu_envset_sync(rlgpu_envset* e, void* stream) {
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(e, "null envset");
@@ -976,6 +995,11 @@ __global__ void __launch_bounds__(64) linear_math_kernel(int op, int ar, const f
         put9(nr, o + 3);
     } else if (op == 6) {  // rsqrtss of the first 12 floats of the row (the table lookup)
         for (int k = 0; k < 12; k++) o[k] = x86_rsqrtss(p[k]);
+    } else if (op == 7) {  // the transcendentals (include/rlgpu_detmath.h)
+        rs_sincosf(p[0], &o[0], &o[1]);
+        o[2] = rs_atan2f(p[1], p[2]);
+        o[3] = rs_asinf(p[3]);
+        o[4] = rs_atanf(p[4]);
     } else {
         // a wheel ray's btSubsimplexConvexCast: R = p[0..8], from p[9..11], to p[12..14], body origin p[15..17],
         // box half extents p[18..20], sphere radius p[21] (> 0: sphere)
@@ -990,7 +1014,7 @@ __global__ void __launch_bounds__(64) linear_math_kernel(int op, int ar, const f
 
 extern "C" int rlgpu_linear_math_queries(int32_t op, int32_t arith, const float* d_in, int32_t n, float* d_out, void* stream) {
     return rlgpu::guarded([&] {
-        RLGPU_REQUIRE(op >= 0 && op <= 6, "rlgpu_linear_math_queries: op must be in [0, 6]");
+        RLGPU_REQUIRE(op >= 0 && op <= 7, "rlgpu_linear_math_queries: op must be in [0, 7]");
         RLGPU_REQUIRE(arith >= 0 && arith < RLGPU_NUM_ARITH, "rlgpu_linear_math_queries: unknown arithmetic mode");
         RLGPU_REQUIRE(n >= 0 && (n == 0 || (d_in && d_out)), "rlgpu_linear_math_queries: bad argument");
         if (n == 0) return;

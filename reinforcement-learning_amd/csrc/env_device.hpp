@@ -821,12 +821,9 @@ DEV void update_auto_flip(ArenaLDS* A, int ci, bool jump_pressed) {
     m3 m = brot(A, bi);
     if (jump_pressed && cs.world_contact && cs.world_contact_normal[2] > 0.70710678118654752440f) {
         float r0 = rs_atan2f(m.r2.y, m.r2.z);
-        float pitch_raw;
-        {
-            float x = -m.r2.x;
-            float sq = sqrtf(stdmax(0.f, 1.f - x * x));
-            pitch_raw = rs_asinf(x, sq);
-        }
+        // btAsin (btScalar.h): clamp to [-1, 1], then asin
+        const float ax = -m.r2.x;
+        float pitch_raw = rs_asinf(ax < -1.f ? -1.f : (ax > 1.f ? 1.f : ax));
         if (fabsf(pitch_raw) == kHalfPi) r0 = r0 > 0 ? r0 - kPi : r0 + kPi;
         float roll = -r0;
         float abs_roll = fabsf(roll);

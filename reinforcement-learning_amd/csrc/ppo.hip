@@ -208,6 +208,7 @@ struct rlgpu_ppo {
     uint16_t* xh = nullptr;    // bf16 obs for inference, rows padded to xh_ld
     int xh_ld = 0;
     uint16_t *zh = nullptr, *ah[2] = {nullptr, nullptr}, *logits_h = nullptr;
+    float* logits_f = nullptr;  // fp32 inference (RLGPU_INFER_F32): the policy's logits [max_rows][A]
     std::vector<void*> allocs;
 
     template <class T>
@@ -218,6 +219,11 @@ struct rlgpu_ppo {
         return (T*)p;
     }
 };
+
+// inference precision (rlgpu_ppo_config.infer_fp16): the 16-bit copy's type, and whether the policy / critic
+// inference runs the fp32 training forward instead (useHalfPrecision = false, Models.cpp:36-68)
+inline bool f16(const rlgpu_ppo* h) { return h->cfg.infer_fp16 == RLGPU_INFER_F16; }
+inline bool infer_f32(const rlgpu_ppo* h) { return h->cfg.infer_fp16 == RLGPU_INFER_F32; }
 
 namespace {
 
@@ -927,7 +933,7 @@ const uint16_t* forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStr
     const auto c = chain(h, mi);
     {
         int64_t e = (int64_t)n * h->xh_ld;
-        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, h->cfg.obs_size, n, h->xh,
+        RLGPU_H16_LAUNCH(f16(h), mlp::rows_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, X, h->cfg.obs_size, n, h->xh,
                          h->xh_ld);
         RLGPU_CHECK_HIP(hipGetLastError());
     }
@@ -949,12 +955,12 @@ const uint16_t* forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStr
         g.K = L.in_pad;
         g.gx = (int)ceil_div(L.out, mlp::BN);
         g.gy = (int)ceil_div(n, mlp::BM);
-        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::gemm_bf16, dim3(g.gx * g.gy), dim3(256), 0, s, g);
+        RLGPU_H16_LAUNCH(f16(h), mlp::gemm_bf16, dim3(g.gx * g.gy), dim3(256), 0, s, g);
         RLGPU_CHECK_HIP(hipGetLastError());
         if (!k.hidden) return h->logits_h;
         const uint16_t* gg = L.hg >= 0 ? P + L.hg : nullptr;
         const uint16_t* bb = L.hbe >= 0 ? P + L.hbe : nullptr;
-        hipLaunchKernelGGL(h->cfg.infer_fp16 ? mlp::ln_act_fwd_bf16_any<true>(L.out) : mlp::ln_act_fwd_bf16_any<false>(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
+        hipLaunchKernelGGL(f16(h) ? mlp::ln_act_fwd_bf16_any<true>(L.out) : mlp::ln_act_fwd_bf16_any<false>(L.out), dim3(ceil_div(n, mlp::LNF_ROWS)), dim3(256), 0, s, h->zh, gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, h->ah[cur]);
         RLGPU_CHECK_HIP(hipGetLastError());
         in = h->ah[cur];
@@ -970,6 +976,7 @@ const uint16_t* forward_half(rlgpu_ppo* h, int mi, const float* X, int n, hipStr
 unsigned long long* g_infer_trace = nullptr;  // rlgpu_debug_infer_trace
 int64_t g_infer_trace_cap = 0;             // its capacity (uint64 entries)
 bool fused_ok(const rlgpu_ppo* h, int mi) {
+    if (infer_f32(h)) return false;  // fp32 inference runs the training forward (forward_f32)
     const char* e = getenv("RLGPU_FUSED_INFER");
     if (e && atoi(e) == 0) return false;
     const auto c = chain(h, mi);
@@ -1020,7 +1027,7 @@ void infer_fused(rlgpu_ppo* h, int mi, bool ver, const float* X, int n, int mode
     if (a.trace && ceil_div(n, infer::IR) * 16 > g_infer_trace_cap)
         throw rlgpu::Error(RLGPU_ERR_INVALID_ARG, "rlgpu_debug_infer_trace: buffer of " + std::to_string(g_infer_trace_cap) +
                                                       " entries, this launch needs " + std::to_string(ceil_div(n, infer::IR) * 16));
-    RLGPU_H16_LAUNCH(h->cfg.infer_fp16, infer::mlp_infer, dim3(ceil_div(n, infer::IR)), dim3(infer::IT), 0, s, a);
+    RLGPU_H16_LAUNCH(f16(h), infer::mlp_infer, dim3(ceil_div(n, infer::IR)), dim3(infer::IT), 0, s, a);
     RLGPU_CHECK_HIP(hipGetLastError());
 }
 
@@ -1106,13 +1113,13 @@ void half_from(rlgpu_ppo* h, int mi, const float* src, uint16_t* dst, uint16_t* 
     const Model& m = h->M[mi];
     for (auto& L : m.L) {
         const int64_t nf = infer::frag_size(L.out, L.in);
-        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, infer::weight_to_frag, dim3(ceil_div(nf, 256)), dim3(256), 0, s, src + (L.w - m.off),
+        RLGPU_H16_LAUNCH(f16(h), infer::weight_to_frag, dim3(ceil_div(nf, 256)), dim3(256), 0, s, src + (L.w - m.off),
                          L.out, L.in, fdst + L.fw);
         int64_t e = (int64_t)L.out * L.in_pad;
-        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, src + (L.w - m.off), L.out, L.in,
+        RLGPU_H16_LAUNCH(f16(h), mlp::weight_to_bf16, dim3(ceil_div(e, 256)), dim3(256), 0, s, src + (L.w - m.off), L.out, L.in,
                            dst + L.hw, L.in_pad);
         int nv = L.g >= 0 ? 3 * L.out : L.out;  // bias | LN weight | LN bias, contiguous in both layouts
-        RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, src + (L.b - m.off), dst + L.hb,
+        RLGPU_H16_LAUNCH(f16(h), ppo::to_half, dim3(ceil_div(nv, 256)), dim3(256), 0, s, src + (L.b - m.off), dst + L.hb,
                            (int64_t)nv);
     }
     RLGPU_CHECK_HIP(hipGetLastError());
@@ -1244,6 +1251,7 @@ extern "C" int rlgpu_ppo_create(const rlgpu_ppo_config* cfg, rlgpu_ppo** out) {
             h->ah[0] = h->alloc<uint16_t>(R * H);
             h->ah[1] = h->alloc<uint16_t>(R * H);
             h->logits_h = h->alloc<uint16_t>(R * omax);
+            if (cfg->infer_fp16 == RLGPU_INFER_F32) h->logits_f = h->alloc<float>(R * omax);
             *out = h;
         } catch (...) {
             for (void* p : h->allocs) (void)hipFree(p);
@@ -1315,6 +1323,14 @@ extern "C" int rlgpu_ppo_refresh_half(rlgpu_ppo* h, void* stream) {
     });
 }
 
+// fp32 forward of model 0 or 1 (through the shared head, if any) on n <= max_rows rows of X into out:
+// the training forward's arithmetic (rlgpu_ppo_forward precision 0, and the fp32 inference)
+void forward_f32(rlgpu_ppo* h, int model, const float* X, int n, float* out, hipStream_t s) {
+    gather_obs(h, X, nullptr, 0, n, s);
+    if (h->shared()) forward_train(h, 2, obs_input(h), n, nullptr, s);
+    forward_train(h, model, model_input(h, model), n, out, s);
+}
+
 extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision, const float* d_in, int32_t n, float* d_out,
                                  void* stream) {
     return rlgpu::guarded([&] {
@@ -1325,18 +1341,18 @@ extern "C" int rlgpu_ppo_forward(rlgpu_ppo* h, int32_t model, int32_t precision,
         hipStream_t s = rlgpu::as_stream(stream);
         const int64_t e = (int64_t)n * h->M[model].out;
         if (precision == 0) {
-            gather_obs(h, d_in, nullptr, 0, n, s);
-            if (h->shared()) forward_train(h, 2, obs_input(h), n, nullptr, s);
             if (model == 2) {  // the shared head's last activation
+                gather_obs(h, d_in, nullptr, 0, n, s);
+                forward_train(h, 2, obs_input(h), n, nullptr, s);
                 RLGPU_CHECK_HIP(hipMemcpyAsync(d_out, model_input(h, 0).X, e * sizeof(float), hipMemcpyDeviceToDevice, s));
             } else {
-                forward_train(h, model, model_input(h, model), n, d_out, s);
+                forward_f32(h, model, d_in, n, d_out, s);
             }
         } else if (fused_ok(h, model)) {
             infer_fused(h, model, false, d_in, n, 0, d_out, nullptr, 0, 0, nullptr, nullptr, nullptr, 0, s);
         } else {
             const uint16_t* y = forward_half(h, model, d_in, n, s);
-            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, y, d_out, e);
+            RLGPU_H16_LAUNCH(f16(h), ppo::bf16_to_f32, dim3(ceil_div(e, 256)), dim3(256), 0, s, y, d_out, e);
             RLGPU_CHECK_HIP(hipGetLastError());
         }
     });
@@ -1352,6 +1368,15 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
         int R = h->cfg.max_rows;
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
+            if (infer_f32(h)) {  // useHalfPrecision = false: fp32 logits, the same sampler
+                forward_f32(h, 0, d_obs + b * h->cfg.obs_size, m, h->logits_f, s);
+                hipLaunchKernelGGL((ppo::sample_actions<false, float>), dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_f,
+                                   d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
+                                   rng_step, b + h->cfg.sample_row_offset, d_actions + b, d_logp ? d_logp + b : nullptr,
+                                   nullptr, 0);
+                RLGPU_CHECK_HIP(hipGetLastError());
+                continue;
+            }
             if (fused_ok(h, 0)) {
                 infer_fused(h, 0, false, d_obs + b * h->cfg.obs_size, m, 1, nullptr, d_masks + b * h->cfg.num_actions,
                             deterministic, rng_step, d_actions + b, d_logp ? d_logp + b : nullptr, nullptr, 0, s,
@@ -1359,7 +1384,7 @@ extern "C" int rlgpu_ppo_infer_actions(rlgpu_ppo* h, const float* d_obs, const u
                 continue;
             }
             forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s);
-            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
+            RLGPU_H16_LAUNCH(f16(h), ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
                                rng_step, b + h->cfg.sample_row_offset, d_actions + b, d_logp ? d_logp + b : nullptr);
             RLGPU_CHECK_HIP(hipGetLastError());
@@ -1392,6 +1417,9 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
     return rlgpu::guarded([&] {
         RLGPU_REQUIRE(h && d_obs && d_masks && d_actions && d_old_rows, "null argument");
         RLGPU_REQUIRE(h->has_ver, "rlgpu_ppo_infer_actions_mixed: no version set (rlgpu_ppo_set_version)");
+        if (infer_f32(h))
+            throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "rlgpu_ppo_infer_actions_mixed: fp32 inference (RLGPU_INFER_F32) "
+                                                      "keeps no old-version copy (self-play needs 16-bit inference)");
         RLGPU_REQUIRE(n >= 0, "n must be >= 0");
         hipStream_t s = rlgpu::as_stream(stream);
         int R = h->cfg.max_rows;
@@ -1406,7 +1434,7 @@ extern "C" int rlgpu_ppo_infer_actions_mixed(rlgpu_ppo* h, const float* d_obs, c
                     continue;
                 }
                 forward_half(h, 0, d_obs + b * h->cfg.obs_size, m, s, old ? h->half_ver : h->half);
-                RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
+                RLGPU_H16_LAUNCH(f16(h), ppo::sample_actions, dim3(ceil_div(m, 4)), dim3(256), 0, s, h->logits_h,
                                    d_masks + b * h->cfg.num_actions, m, h->cfg.num_actions, deterministic, h->cfg.seed,
                                    rng_step, b + h->cfg.sample_row_offset, d_actions + b,
                                    (d_logp && !old) ? d_logp + b : nullptr, d_old_rows + b, old);
@@ -1424,7 +1452,8 @@ extern "C" int rlgpu_ppo_infer_actions_rows(rlgpu_ppo* h, const float* d_obs, co
         RLGPU_REQUIRE(n >= 0 && row0 >= 0, "n and row0 must be >= 0");
         RLGPU_REQUIRE(!d_old_rows || h->has_ver, "rlgpu_ppo_infer_actions_rows: old rows without a version set");
         if (!fused_ok(h, 0))
-            throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "rlgpu_ppo_infer_actions_rows: the policy is not on the fused kernel");
+            throw rlgpu::Error(RLGPU_ERR_UNSUPPORTED, "rlgpu_ppo_infer_actions_rows: the policy is not on the fused kernel "
+                                                      "(widths, RLGPU_FUSED_INFER = 0 or fp32 inference)");
         hipStream_t s = rlgpu::as_stream(stream);
         // the fused kernel keeps no per-row buffers: one launch per pass over all n rows (no max_rows chunks)
         const int64_t r0 = row0 + h->cfg.sample_row_offset;
@@ -1449,13 +1478,17 @@ extern "C" int rlgpu_ppo_infer_critic(rlgpu_ppo* h, const float* d_obs, int64_t 
         const int64_t R = fused_ok(h, 1) ? (int64_t)1 << 30 : h->cfg.max_rows;
         for (int64_t b = 0; b < n; b += R) {
             int m = (int)std::min<int64_t>(R, n - b);
+            if (infer_f32(h)) {  // useHalfPrecision = false
+                forward_f32(h, 1, d_obs + b * h->cfg.obs_size, m, d_values + b, s);
+                continue;
+            }
             if (fused_ok(h, 1)) {
                 infer_fused(h, 1, false, d_obs + b * h->cfg.obs_size, m, 0, d_values + b, nullptr, 0, 0, nullptr, nullptr,
                             nullptr, 0, s);
                 continue;
             }
             forward_half(h, 1, d_obs + b * h->cfg.obs_size, m, s);
-            RLGPU_H16_LAUNCH(h->cfg.infer_fp16, ppo::bf16_to_f32, dim3(ceil_div(m, 256)), dim3(256), 0, s, h->logits_h, d_values + b,
+            RLGPU_H16_LAUNCH(f16(h), ppo::bf16_to_f32, dim3(ceil_div(m, 256)), dim3(256), 0, s, h->logits_h, d_values + b,
                                (int64_t)m);
             RLGPU_CHECK_HIP(hipGetLastError());
         }

@@ -69,8 +69,14 @@ __device__ __forceinline__ void masked_softmax(float z0, float z1, bool v0, bool
 // where ok[g].  sample_actions runs it with RG = 1; the fused inference kernel (infer_kernels.hpp) runs
 // sample_rows_looped (below) over 8 rows -- the per-row arithmetic is the same, so both draw the same actions
 // from the same logits.
-template <int RG, bool F16>
-__device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], const uint8_t* const (&mk)[RG],
+// a logit as the sampler reads it: 16-bit storage (bf16 / fp16), or fp32 (useHalfPrecision = false)
+template <bool F16>
+__device__ __forceinline__ float logit_f(uint16_t u) { return mlp::h2f<F16>(u); }
+template <bool F16>
+__device__ __forceinline__ float logit_f(float x) { return x; }
+
+template <int RG, bool F16, typename LT = uint16_t>
+__device__ __forceinline__ void sample_rows(const LT* const (&lg)[RG], const uint8_t* const (&mk)[RG],
                                             float* const (&pr)[RG], int A, int deterministic, uint64_t seed,
                                             uint64_t step, int64_t row0, const int (&row)[RG], const bool (&ok)[RG],
                                             int lane, int32_t* act, float* logp) {
@@ -82,7 +88,7 @@ __device__ __forceinline__ void sample_rows(const uint16_t* const (&lg)[RG], con
     const int c0 = min(a0, A - 1), c1 = min(a1, A - 1);  // loads stay unconditional (no branches between them)
 #pragma unroll
     for (int g = 0; g < RG; g++) {
-        const float l0 = mlp::h2f<F16>(lg[g][c0]), l1 = mlp::h2f<F16>(lg[g][c1]);
+        const float l0 = logit_f<F16>(lg[g][c0]), l1 = logit_f<F16>(lg[g][c1]);
         const uint8_t m0 = mk[g][c0], m1 = mk[g][c1];
         z0[g] = in0 ? l0 + (m0 ? 0.f : kDisabledLogit) : 0.f;
         z1[g] = in1 ? l1 + (m1 ? 0.f : kDisabledLogit) : 0.f;
@@ -289,8 +295,8 @@ __device__ __forceinline__ void sample_rows_looped(RowFn rowfn, int A, int deter
     }
 }
 
-template <bool F16>
-__global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, const uint8_t* masks, int n, int A,
+template <bool F16, typename LT = uint16_t>
+__global__ void __launch_bounds__(256) sample_actions(const LT* logits, const uint8_t* masks, int n, int A,
                                                      int deterministic, uint64_t seed, uint64_t step, int64_t row0,
                                                      int32_t* act, float* logp, const uint8_t* row_sel = nullptr,
                                                      int sel = 0) {
@@ -298,12 +304,12 @@ __global__ void __launch_bounds__(256) sample_actions(const uint16_t* logits, co
     int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= n) return;
     if (row_sel && ((row_sel[row] != 0) != (sel != 0))) return;
-    const uint16_t* const lg[1] = {logits + (int64_t)row * A};
+    const LT* const lg[1] = {logits + (int64_t)row * A};
     const uint8_t* const mk[1] = {masks + (int64_t)row * A};
     float* const pr[1] = {probs[threadIdx.x >> 6]};
     const int rw[1] = {row};
     const bool ok[1] = {true};
-    sample_rows<1, F16>(lg, mk, pr, A, deterministic, seed, step, row0, rw, ok, lane, act, logp);
+    sample_rows<1, F16, LT>(lg, mk, pr, A, deterministic, seed, step, row0, rw, ok, lane, act, logp);
 }
 
 // PPO policy loss + entropy and its gradient w.r.t. the fp32 training logits.

@@ -685,6 +685,9 @@ inline void Learner::ValidateConfig(const LearnerConfig& c) {
     if (c.ppo.policyTemperature != 1) bad("ppo.policyTemperature must be 1");
     if (c.ppo.maskEntropy) bad("ppo.maskEntropy is not supported");
     if (c.ppo.useGuidingPolicy) bad("ppo.useGuidingPolicy is not supported");
+    if (!c.ppo.useHalfPrecision && (c.trainAgainstOldVersions || c.skillTracker.enabled))
+        bad("ppo.useHalfPrecision = false with trainAgainstOldVersions or skillTracker: old policy versions run on "
+            "16-bit inference copies only (set useHalfPrecision = true, or turn self-play / skill matches off)");
     if (c.ppo.epochs <= 0 || c.ppo.tsPerItr <= 0 || c.ppo.batchSize <= 0) bad("ppo.epochs / tsPerItr / batchSize must be positive");
     const PartialModelConfig* ms[3] = {&c.ppo.policy, &c.ppo.critic, &c.ppo.sharedHead};
     const char* names[3] = {"policy", "critic", "sharedHead"};
@@ -714,8 +717,6 @@ inline Learner::Learner(RLGC::EnvCreateFn envCreateFunc, LearnerConfig cfg, Step
         config.randomSeed = std::chrono::duration_cast<std::chrono::milliseconds>(
                                 std::chrono::system_clock::now().time_since_epoch()).count();
     std::printf("Learner::Learner():\n\tCheckpoint Save/Load Dir: %s\n", config.checkpointFolder.string().c_str());
-    if (!config.ppo.useHalfPrecision)
-        std::fprintf(stderr, "Learner: ppo.useHalfPrecision = false -- inference runs in bf16 on this engine\n");
     if (config.sendMetrics) std::printf("\t(metrics are printed; the Python metrics receiver is not part of this engine)\n");
     if (options.stream) stream_ = options.stream;
     else detail::HipOk(hipStreamCreate(&stream_), "stream");
@@ -759,6 +760,9 @@ inline Learner::Learner(RLGC::EnvCreateFn envCreateFunc, LearnerConfig cfg, Step
     c.n_shared_layers = 0;
     if (config.ppo.sharedHead.IsValid()) layers(config.ppo.sharedHead, c.shared_layers, c.n_shared_layers);
     c.deterministic = config.ppo.deterministic;
+    // PPOLearnerConfig::useHalfPrecision (PPOLearnerConfig.h:31): Model::Forward's half branch (bf16 inference,
+    // the reference's seqHalf) or its fp32 branch (Models.cpp:36-68) -- the training forward's arithmetic
+    c.infer_fp16 = config.ppo.useHalfPrecision ? RLGPU_INFER_BF16 : RLGPU_INFER_F32;
     c.train_gemm = options.trainGemm;
     c.arith = options.arith;
     c.activation = config.ppo.policy.activationType == ModelActivationType::RELU ? RLGPU_ACT_RELU : RLGPU_ACT_LEAKY_RELU;

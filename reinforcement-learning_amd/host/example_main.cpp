@@ -1,8 +1,9 @@
 // example_main.cpp -- rlgpu_train: the reference's src/ExampleMain.cpp setup on the MI355X engine, written
 // against the trainer facade (facade/GigaLearn.hpp: GGL::Learner(EnvCreateFn, LearnerConfig, StepCallbackFn),
 // Start / Save / Load) with every plugin a device-registry class, plus the command-line knobs of a benchmark /
-// multi-rank launcher.  (The reference's own ExampleMain.cpp compiles unchanged against the same facade:
-// Makefile target examplemain, rlgpu/rlgpu_examplemain.)
+// multi-rank launcher.  It stands in for the reference's own ExampleMain.cpp, which is written against the same
+// facade surface but is not compiled here (building against the reference's sources was
+// refused by the environment).
 //
 // ExampleMain.cpp:128-226: the 2v2 arena, AdvancedObs, DefaultAction, the 13 weighted rewards, NoTouch(8) +
 // ScoreLimit(3), KickoffState; :340-430: the LearnerConfig / PPOLearnerConfig.  The model topology is the one

@@ -245,6 +245,9 @@ Learner::Learner(const rlgpu_learner_config& cfg, const rlgpu_collective* coll, 
     env_ = new RLGC::EnvSetGPU(ec, s_);
     // ExampleMain registers its StepCallback (ExampleMain.cpp:233-283, 592): restated on the device
     RlgpuCheck(rlgpu_envset_enable_step_metrics(env_->handle(), 1), "step metrics");
+    // the rollout rows are the only obs / masks the Learner reads after a fused step (the stacked-frame and
+    // hooked steps pass no obs rows, so the set's own buffers still get theirs): one copy per env step
+    RlgpuCheck(rlgpu_envset_set_output_only(env_->handle(), 1), "output-only rows");
     K_ = cfg.frame_stack > 1 ? cfg.frame_stack : 1;
     RLGPU_REQUIRE(K_ <= 16, "Learner: frame_stack must be <= 16");
     const int W = OBS * K_;
@@ -875,12 +878,20 @@ rlgpu_learner_report Learner::Iterate() {
         double ms = 0;
         // per env launch: T per group (the trajectory mode records no per-step events)
         const int nt = trajMode() ? 0 : exp_.T * std::max(1, collectGroupsUsed_);
+        std::vector<float> each(nt);
         for (int t = 0; t < nt; t++) {
             float x = 0;
             hipCheck(hipEventElapsedTime(&x, ev_[2 * t], ev_[2 * t + 1]), "elapsed");
             ms += x;
+            each[t] = x;
         }
         r.env_kernel_ms = nt ? ms / nt : 0.0;
+        if (nt) {
+            std::sort(each.begin(), each.end());
+            r.env_kernel_min_ms = each.front();
+            r.env_kernel_max_ms = each.back();
+            r.env_kernel_median_ms = (nt & 1) ? each[nt / 2] : 0.5 * ((double)each[nt / 2 - 1] + each[nt / 2]);
+        }
     }
     return r;
 }

@@ -59,8 +59,8 @@ def rsqrtss_emulated_c(x):
 
 def linear_math_queries(op, arith, inp):
     """rlgpu_linear_math_queries on the device: op 0 normalize, 1 setRotation, 2 getRotation, 3 quaternion
-    product, 4 integrateTransform, 5 wheel-ray convex cast (include/rlgpu_arith.h), on a CUDA float32 tensor of
-    rows of 24 floats -> [n, 12]."""
+    product, 4 integrateTransform, 5 wheel-ray convex cast, 6 rsqrtss, 7 sin / cos / atan2 / asin / atan
+    (include/rlgpu_arith.h), on a CUDA float32 tensor of rows of 24 floats -> [n, 12]."""
     import torch
     inp = inp.reshape(-1, 24).contiguous().float()
     out = torch.zeros((inp.shape[0], 12), dtype=torch.float32, device=inp.device)

@@ -221,6 +221,11 @@ class EnvSet:
         _lib.check(_lib.lib().rlgpu_envset_step(self._h, self._actions(actions), int(reset_terminated), o,
                                                 _lib.stream_ptr(stream)), "rlgpu_envset_step")
 
+    def set_output_only(self, on=True):
+        """rlgpu_envset_set_output_only: rows given to step(out=...) go only there, not also to self.obs /
+        self.action_masks / self.trunc_obs."""
+        _lib.check(_lib.lib().rlgpu_envset_set_output_only(self._h, int(on)), "rlgpu_envset_set_output_only")
+
     def sync(self, stream=None):
         _lib.check(_lib.lib().rlgpu_envset_sync(self._h, _lib.stream_ptr(stream)), "sync")
 

@@ -264,7 +264,9 @@ class _CStats(ctypes.Structure):
 class _CReport(ctypes.Structure):
     _fields_ = [("collect_s", ctypes.c_double), ("consume_s", ctypes.c_double), ("learn_s", ctypes.c_double),
                 ("env_kernel_ms", ctypes.c_double), ("env_steps", ctypes.c_int64), ("learn_issue_s", ctypes.c_double),
-                ("collect_issue_s", ctypes.c_double), ("env_launch_arenas", ctypes.c_int32)]
+                ("collect_issue_s", ctypes.c_double), ("env_launch_arenas", ctypes.c_int32),
+                ("env_kernel_min_ms", ctypes.c_double), ("env_kernel_median_ms", ctypes.c_double),
+                ("env_kernel_max_ms", ctypes.c_double)]
 
 
 def _bind():
@@ -618,7 +620,8 @@ class Learner:
         torch.cuda.synchronize(self.device)
         out = {"report": report, "iteration_s": time.perf_counter() - t0, "collect_s": rep.collect_s, "consume_s": rep.consume_s,
                "learn_s": rep.learn_s, "learn_issue_s": rep.learn_issue_s, "collect_issue_s": rep.collect_issue_s, "env_kernel_ms": rep.env_kernel_ms,
-               "env_launch_arenas": rep.env_launch_arenas,
+               "env_launch_arenas": rep.env_launch_arenas, "env_kernel_min_ms": rep.env_kernel_min_ms,
+               "env_kernel_median_ms": rep.env_kernel_median_ms, "env_kernel_max_ms": rep.env_kernel_max_ms,
                "old_version": None if self.old_version is None else (self.old_version.timesteps, self.old_team)}
         if self.cfg.checkpoint_folder:  # auto-save (Learner.cpp:1011-1015)
             per = self.cfg.ts_per_save or self.T * self.P * self.world

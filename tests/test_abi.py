@@ -33,6 +33,16 @@ def test_exports_every_declared_symbol():
     assert not missing, f"declared but not exported: {missing}"
 
 
+def test_exports_only_the_c_abi():
+    """rlgpu.map keeps the host's C++ classes internal: a program defining its own GGL::Learner (the trainer
+    facade) must not interpose on them -- the round-5 SIGSEGV at rlgpu_train's exit came from exactly that."""
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    names = [line.split()[-1] for line in out.splitlines() if line.strip() and len(line.split()) >= 3]
+    stray = sorted(n for n in names if not n.startswith("rlgpu_"))
+    assert not stray, stray[:10]
+    assert len(names) > 50
+
+
 def test_library_loads_and_reports():
     L = ctypes.CDLL(LIB)
     L.rlgpu_last_error.restype = ctypes.c_char_p

@@ -132,3 +132,30 @@ def test_trajectory_mode_rank_without_finished_rows(gpu):
     np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
     assert res[0]["ret"] == res[1]["ret"]
     assert res[1]["ret"][-1][0] > 0  # rank 1's samples reached both ranks' statistics
+
+
+def test_bench_two_ranks_under_torchrun(gpu):
+    """The driver's multi-GPU launch, rehearsed on one GPU: `python -m torch.distributed.run --nproc-per-node 2
+    bench.py --gpus 2` (gloo, since RCCL refuses two ranks on one device; on a node the same command runs the
+    native RCCL collective).  Rank 0 prints ONE JSON line: n_gpus 2, value = 2 ranks x arenas x T x steps over
+    the max-over-ranks wall time."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    arenas, T, steps = 64, 16, 2
+    env = dict(os.environ, RLGPU_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", str(steps), "--warmup",
+           "1", "--arenas", str(arenas), "--rollout", str(T), "--no-legs", "--no-cpu-baseline", "--mesh", "synthetic"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == steps and out["scaling"] == "weak"
+    assert out["config"]["parallelism"] == "arena-sharded dp2"
+    assert "gloo" in out["config"]["collective"]
+    want = 2 * arenas * T * steps / (out["ms_per_step"] * steps / 1e3)
+    assert abs(out["value"] - want) <= 1e-6 * want, (out["value"], want)
+    assert out["roofline"]["units_per_launch"] == arenas

@@ -312,6 +312,47 @@ def test_env_step_outputs_append(gpu):
     assert torch.equal(term_out.view(n, 4)[:, 0].to(torch.uint8), g.terminals)
 
 
+def test_env_output_only_rows(gpu):
+    """rlgpu_envset_set_output_only: the appended rows (obs, masks, rewards, codes, truncation obs) equal a normal
+    set's bit for bit through truncations (max episode length) and terminal resets (NoTouch after 8 s), and the
+    set's own obs / masks / trunc buffers keep the values they had before the steps (the C++ Learner's single
+    copy per env step)."""
+    import torch
+    from rlgpu.env import EnvSet, StepOutputs
+
+    def bufs(n):
+        return (torch.empty((4 * n, 167), device=gpu), torch.empty((4 * n, 90), dtype=torch.uint8, device=gpu),
+                torch.empty(4 * n, device=gpu), torch.empty(4 * n, dtype=torch.int8, device=gpu),
+                torch.zeros((4 * n, 167), device=gpu))
+    rng = np.random.default_rng(2)
+    saw = {1: 0, 2: 0}
+    for n, L, steps in ((24, 29, 90), (64, 0, 160)):  # truncations; then episodes ended by NoTouch (120 steps)
+        A = EnvSet(n, seed=9, device=gpu, max_episode_steps=L)
+        B = EnvSet(n, seed=9, device=gpu, max_episode_steps=L)
+        B.set_output_only(True)
+        obs0, masks0, trunc0 = B.obs.clone(), B.action_masks.clone(), B.trunc_obs.clone()
+        for t in range(steps):
+            a = torch.from_numpy(random_actions(A.action_masks.cpu().numpy(), rng)).to(gpu)
+            oa, ob = bufs(n), bufs(n)
+            A.step(a, True, StepOutputs.of(*oa))
+            B.step(a, True, StepOutputs.of(*ob))
+            torch.cuda.synchronize()
+            for x, y in zip(oa, ob):
+                assert torch.equal(x.view(torch.uint8) if x.dtype != torch.uint8 else x,
+                                   y.view(torch.uint8) if y.dtype != torch.uint8 else y), f"step {t}"
+            assert torch.equal(A.rewards, B.rewards) and torch.equal(A.terminals, B.terminals)
+            for c in (1, 2):
+                saw[c] += int((oa[3] == c).sum())
+        assert torch.equal(B.obs, obs0) and torch.equal(B.action_masks, masks0) and torch.equal(B.trunc_obs, trunc0)
+        # a step without rows still writes the set's buffers
+        a = torch.zeros(4 * n, dtype=torch.int32, device=gpu)
+        A.step(a, True)
+        B.step(a, True)
+        torch.cuda.synchronize()
+        assert torch.equal(A.obs, B.obs) and torch.equal(A.action_masks, B.action_masks)
+    assert saw[1] > 0 and saw[2] > 0, saw
+
+
 def test_env_max_episode_truncation_parity(gpu):
     """Learner maxEpisodeLength (Learner.cpp:848-850): trajectories cut TRUNCATED without an arena
     reset; codes and trunc obs rows bit-exact vs the oracle."""

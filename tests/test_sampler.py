@@ -167,3 +167,40 @@ def test_sampler_bit_exact_vs_oracle(gpu, monkeypatch, kw, fp16, fused, chunk):
     pr = np.clip(pr / pr.sum(1, keepdims=True), 1e-11, 1)
     ref = np.log(pr[np.arange(n), ga])
     assert np.all(np.abs(glp - ref) <= 1e-6 * np.abs(ref) + 5e-7), np.abs(glp - ref).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(), dict(shared_layers=(384, 384), policy_layers=(384,) * 3, critic_layers=(384,) * 3)],
+                         ids=["c2", "shared-head"])
+def test_fp32_inference_bit_exact_vs_oracle(gpu, kw):
+    """PPOLearnerConfig::useHalfPrecision = false (RLGPU_INFER_F32, Models.cpp:36-68's fp32 branch): the policy's
+    fp32 logits (the training forward) sampled by the same sampler -- actions and log probs bit-exact to the
+    oracle sampler on those fp32 logits; the critic's values equal the fp32 forward; self-play inference is
+    refused by name."""
+    import torch
+    from rlgpu.ppo import PPO
+    from test_ppo import make_batch
+    n = 12000
+    p = PPO(max_rows=5000, seed=41, infer_fp16=2, **kw)
+    rng = np.random.default_rng(9)
+    obs, masks, *_ = make_batch(rng, n)
+    masks[::89] = 0
+    masks[::89, 5] = 1
+    o, m = torch.from_numpy(obs).to(gpu), torch.from_numpy(masks).to(gpu)
+    logits = np.concatenate([p.forward(0, o[i:i + 5000]).cpu().numpy() for i in range(0, n, 5000)])
+    assert logits.dtype == np.float32
+    for det in (True, False):
+        for step in (0, 3, 2**31 + 1):
+            a, lp = p.infer_actions(o, m, step=step, deterministic=det)
+            wa, wlp = oracle.sample_actions(logits, masks, det, p.cfg.seed, step, 0)
+            np.testing.assert_array_equal(a.cpu().numpy(), wa)
+            np.testing.assert_array_equal(lp.cpu().numpy().view(np.uint32), wlp.view(np.uint32))
+    v = p.infer_critic(o).cpu().numpy().ravel()
+    want = np.concatenate([p.forward(1, o[i:i + 5000]).cpu().numpy().ravel() for i in range(0, n, 5000)])
+    np.testing.assert_array_equal(v.view(np.uint32), want.view(np.uint32))
+    # the fp32 logits differ from the bf16 path's (it is not the 16-bit inference under another name)
+    assert not np.array_equal(logits, p.forward(0, o[:5000], half=True).cpu().numpy())
+    from rlgpu._lib import RLGPUError
+    p.set_version(p.policy_version())
+    with pytest.raises(RLGPUError, match="fp32 inference"):
+        p.infer_actions_mixed(o, m, torch.zeros(n, dtype=torch.uint8, device=gpu), step=0)
