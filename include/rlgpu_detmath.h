@@ -2,17 +2,16 @@
  * rlgpu_detmath.h -- deterministic float transcendentals shared by the HIP kernels and the
  * CPU oracle.
  *
- * The reference calls libm sinf/cosf/atan2f (btSin/btCos in btTransformUtil.h:71-73,
- * atan2f in Car.cpp:713, btAtan2/btAsin in btMatrix3x3.h:530-532).  libm and the device
+ * The reference calls libm sinf/cosf/atan2f/asinf (btSin/btCos in btTransformUtil.h:71-73,
+ * atan2f in Car.cpp:722, btAtan2/btAsin in btMatrix3x3.h:530-532).  libm and the device
  * math library differ in the last bits, and rigid-body simulation amplifies 1-ulp
- * differences over ticks.  Both sides of the parity test therefore use these Cephes-style
- * single-precision kernels, compiled with -ffp-contract=off on both sides, so the GPU and the oracle agree bit
- * for bit.  This is arithmetic infrastructure, not simulator logic.
- *
- * Measured against the float64 truth over the simulator's domains (tests/test_detmath_bound.py):
- * sin / cos <= 1 ulp, atan2 <= 3 ulp, asin <= 7 ulp (near |x| -> 1 only; glibc: <= 1 ulp each).
- * Swapping the host libm in moves one env step's obs / rewards by < 5e-5 relative, no mask or
- * terminal flips.
+ * differences over ticks.  Both sides of the parity test therefore use these kernels, compiled with
+ * -ffp-contract=off on both sides, so the GPU and the oracle agree bit for bit.  The trig kernels are
+ * correctly rounded (double evaluation, one rounding): against the float64 truth over the simulator's
+ * domains they are 0 ulp (glibc: <= 1 ulp, 1-13 % of its results misrounded), so against any CRT the
+ * only difference is that CRT's misroundings; swapping glibc in moves one env step's rewards and GAE
+ * advantages by <= 7.5e-6 relative (tests/test_detmath_bound.py).  This is
+ * arithmetic infrastructure, not simulator logic.
  */
 #ifndef RLGPU_DETMATH_H
 #define RLGPU_DETMATH_H

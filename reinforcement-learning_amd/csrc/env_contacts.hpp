@@ -539,31 +539,9 @@ DEV void narrow_deferred(ArenaLDS* base, int nvalid, const MeshView& M) {
     }
 }
 
-// ---- body-vs-mesh grid walks dealt over the workgroup by grid entry (narrow_mesh) ---------------------------
-// mesh_plan (the arena's lanes 0..4, one per body) lists each active body's query: its box and the (y, z) rows
-// of its cells, each row one contiguous range of grid entries, in the arena's small penetration-solver bytes
-// (the arena's LDS solver set is locked meanwhile: a full queue's in-place query takes its HBM set, which
-// gives the same bits).  narrow_mesh then deals the entries of all the workgroup's arenas round-robin over
-// every lane, so a body over a dense part of the mesh no longer holds its arena's 16 lanes while the other
-// arenas' lanes idle.  Each entry is tested exactly as grid_query tests it, and every candidate carries
-// (rank, triangle) -- the queue's order does not matter either -- so the results do not depend on the deal.
-// RLGPU_MESH_DEAL=1 builds this path; the default 0 keeps each arena's bodies' walks on its own 16 lanes
-// (kMeshChunks per body): the deal shortens the walk phase (mean 298k -> 260k cycles per workgroup and step,
-// slowest 478k -> 406k) but the kernel measured 1.040 -> 1.053 ms (profiles/r05l_env_mesh_deal_ab.txt)
-#ifndef RLGPU_MESH_DEAL
-#define RLGPU_MESH_DEAL 0
-#endif
-constexpr int kSegRows = 9;  // rows of one body's query: a box under 2 cells per axis spans 4, the ball 9
-constexpr int kMaxSegs = 5 * kSegRows;
-struct MeshSegs {
-    v3 mn[5], mx[5];  // the bodies' query boxes
-    int c0[5][3];     // and their low cells
-    int nseg, nent;   // rows listed, their entries
-    int sb[kMaxSegs], sn[kMaxSegs], sm[kMaxSegs];  // a row's first entry, entry count, body | cy << 8 | cz << 20
-};
-static_assert(sizeof(MeshSegs) <= gjk::kSmallBytes, "the mesh plan fits the arena's small solver set");
-DEV MeshSegs* mesh_segs(ArenaLDS* A) { return reinterpret_cast<MeshSegs*>(&A->u.cand[kMaxCand]); }
-
+// ---- body-vs-mesh grid walks: each body's walk split over kMeshChunks lanes of its arena (narrow_pair).
+// Dealing the entries of a workgroup's four arenas over all 64 lanes shortened the walk phase but not the
+// launch (1.040 -> 1.053 ms, profiles/r05l_env_mesh_deal_ab.txt) and was removed.
 // body bi's query box: the ball's sphere grown by 0.08 (SphereTriangleDetector's contact threshold margin),
 // a car's compound AABB
 DEV void mesh_box(ArenaLDS* A, int bi, v3& mn, v3& mx) {
@@ -592,121 +570,6 @@ DEV void mesh_hit(ArenaLDS* A, const MeshView& M, int bi, int t, v3 v0, v3 v1, v
             box_tri_query(A, M, bi, t, obj, v0, v1, v2, false);
     }
 }
-// every lane of a valid arena's team (l = its lane in the team); a query over more than kSegRows rows is
-// walked by its own lane here instead
-DEV void mesh_plan(ArenaLDS* A, const MeshView& M, int l) {
-    MeshSegs* S = mesh_segs(A);
-    const int team = (int)threadIdx.x & ~(kTeam - 1);
-    int rows = 0, c0[3] = {0, 0, 0}, c1[3] = {0, 0, 0};
-    v3 mn = zero3(), mx = zero3();
-    bool here = false;
-    if (l < 5 && (l == 0 ? A->a.ball_awake != 0 : A->a.active[l] != 0)) {
-        mesh_box(A, l, mn, mx);
-        c0[0] = grid_cell(mn.x, M.ox, M.inv_cell, M.nx), c1[0] = grid_cell(mx.x, M.ox, M.inv_cell, M.nx);
-        c0[1] = grid_cell(mn.y, M.oy, M.inv_cell, M.ny), c1[1] = grid_cell(mx.y, M.oy, M.inv_cell, M.ny);
-        c0[2] = grid_cell(mn.z, M.oz, M.inv_cell, M.nz), c1[2] = grid_cell(mx.z, M.oz, M.inv_cell, M.nz);
-        rows = (c1[1] - c0[1] + 1) * (c1[2] - c0[2] + 1);
-        if (rows > kSegRows) {
-            here = true;
-            rows = 0;
-        }
-    }
-    int off = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const int rk = __shfl(rows, team + k, 64);
-        off += k < l ? rk : 0;
-        tot += rk;
-    }
-    int ent = 0;
-    if (rows) {
-        S->mn[l] = mn;
-        S->mx[l] = mx;
-#pragma unroll
-        for (int a = 0; a < 3; a++) S->c0[l][a] = c0[a];
-        int s = off;
-        for (int cz = c0[2]; cz <= c1[2]; cz++)
-            for (int cy = c0[1]; cy <= c1[1]; cy++, s++) {
-                const int row = (cz * M.ny + cy) * M.nx;
-                const int b = M.cell_start[row + c0[0]], e = M.cell_start[row + c1[0] + 1];
-                S->sb[s] = b;
-                S->sn[s] = e - b;
-                S->sm[s] = l | (cy << 8) | (cz << 20);
-                ent += e - b;
-            }
-    }
-    int all = 0;
-#pragma unroll
-    for (int k = 0; k < 5; k++) all += __shfl(ent, team + k, 64);
-    if (l == 0) {
-        S->nseg = tot;
-        S->nent = all;
-        A->a.epa_lock = 1;  // the plan lives in the small solver set until narrow_mesh is done
-    }
-    if (here) grid_query(M, mn, mx, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int obj) { mesh_hit(A, M, l, t, v0, v1, v2, obj); });
-}
-// every lane of the workgroup: the planned entries of arenas 0 .. nvalid-1 (base = the first), dealt round-robin
-// in (arena, row, entry) order, kGridBatch entries' loads issued before the first is tested
-DEV void narrow_mesh(ArenaLDS* base, int nvalid, const MeshView& M) {
-    int total = 0;
-#pragma unroll
-    for (int a = 0; a < kArenas; a++) total += a < nvalid ? mesh_segs(base + a)->nent : 0;
-    int ca = 0, cs = 0, cbase = 0;  // this lane's cursor: arena, row, index of the row's first entry (only advances)
-    for (int p0 = 0; p0 < total; p0 += kWG * kGridBatch) {
-        int pa[kGridBatch], pm[kGridBatch];
-        float4 q[kGridBatch][3];
-#pragma unroll
-        for (int j = 0; j < kGridBatch; j++) {
-            const int p = p0 + (int)threadIdx.x + kWG * j;
-            pa[j] = -1;
-            pm[j] = 0;
-            int k = 0;
-            if (p < total) {
-                while (ca < nvalid) {
-                    const MeshSegs* S = mesh_segs(base + ca);
-                    if (cs < S->nseg) {
-                        const int n = S->sn[cs];
-                        if (p < cbase + n) break;
-                        cbase += n;
-                        cs++;
-                    } else {
-                        ca++;
-                        cs = 0;
-                    }
-                }
-                if (ca < nvalid) {
-                    const MeshSegs* S = mesh_segs(base + ca);
-                    pa[j] = ca;
-                    pm[j] = S->sm[cs];
-                    k = S->sb[cs] + (p - cbase);
-                }
-            }
-            const float4* e = M.cell_tri + 3 * (size_t)k;
-            q[j][0] = e[0];
-            q[j][1] = e[1];
-            q[j][2] = e[2];
-        }
-#pragma unroll
-        for (int j = 0; j < kGridBatch; j++) {
-            if (pa[j] < 0) continue;
-            ArenaLDS* A = base + pa[j];
-            const MeshSegs* S = mesh_segs(A);
-            const int bi = pm[j] & 255, cy = (pm[j] >> 8) & 4095, cz = pm[j] >> 20;
-            const v3 v0 = v3{q[j][0].x, q[j][0].y, q[j][0].z}, v1 = v3{q[j][1].x, q[j][1].y, q[j][1].z},
-                     v2 = v3{q[j][2].x, q[j][2].y, q[j][2].z};
-            const int obj = __float_as_int(q[j][0].w), t = __float_as_int(q[j][1].w), cx = __float_as_int(q[j][2].w);
-            const v3 tmn = v3{fminf(v0.x, fminf(v1.x, v2.x)), fminf(v0.y, fminf(v1.y, v2.y)), fminf(v0.z, fminf(v1.z, v2.z))};
-            const v3 tmx = v3{fmaxf(v0.x, fmaxf(v1.x, v2.x)), fmaxf(v0.y, fmaxf(v1.y, v2.y)), fmaxf(v0.z, fmaxf(v1.z, v2.z))};
-            if (!aabb_overlap(S->mn[bi], S->mx[bi], tmn, tmx)) continue;
-            if (cx != max(S->c0[bi][0], grid_cell(tmn.x, M.ox, M.inv_cell, M.nx)) ||
-                cy != max(S->c0[bi][1], grid_cell(tmn.y, M.oy, M.inv_cell, M.ny)) ||
-                cz != max(S->c0[bi][2], grid_cell(tmn.z, M.oz, M.inv_cell, M.nz)))
-                continue;
-            mesh_hit(A, M, bi, t, v0, v1, v2, obj);
-        }
-    }
-}
-
 // runs the narrowphase of one canonical pair rank and emits candidates; returns 1 when it ran.
 // Body-vs-mesh ranks are split over `parts` lanes (grid entries dealt round-robin); candidates
 // carry (rank, triangle), so the commit order does not depend on the split.
@@ -725,12 +588,10 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                 float dist = dot(n, vtx - C.plane_p[pl]);
                 v3 on_plane = vtx - n * dist;
                 if (dist < pair_cbt(0, 10)) emit(A, rank, 0, plane_key(0, pl), n, on_plane, dist);
-            } else {  // sphere vs mesh triangles (the per-arena walk; RLGPU_MESH_DEAL: narrow_mesh)
-#if !RLGPU_MESH_DEAL
+            } else {  // sphere vs mesh triangles
                 v3 mn, mx;
                 mesh_box(A, 0, mn, mx);
                 grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) { mesh_hit(A, M, 0, t, v0, v1, v2, obj); });
-#endif
             }
         } else {
             m3 R = brot(A, bi);
@@ -741,13 +602,11 @@ DEV int narrow_pair(ArenaLDS* A, const MeshView& M, int rank, int part = 0, int 
                 v3 on_plane = vtx - n * dist;
                 if (dist < pair_cbt(bi, 10)) emit(A, rank, 0, plane_key(bi, pl), n, on_plane, dist);
             } else {
-#if !RLGPU_MESH_DEAL
                 // triangles past the AABB test are queued for Bullet's GJK / EPA query (box_tri_query),
                 // which the workgroup's lanes then share (narrow_queue); a full queue runs them here
                 v3 mn, mx;
                 mesh_box(A, bi, mn, mx);
                 grid_query(M, mn, mx, part, parts, [&](int t, v3 v0, v3 v1, v3 v2, int obj) { mesh_hit(A, M, bi, t, v0, v1, v2, obj); });
-#endif
             }
         }
         return 1;

@@ -34,10 +34,7 @@
 namespace rl {
 
 constexpr int kTeam = 16;           // lanes per arena
-#ifndef RLGPU_ENV_ARENAS_PER_WG
-#define RLGPU_ENV_ARENAS_PER_WG 4
-#endif
-constexpr int kArenas = RLGPU_ENV_ARENAS_PER_WG;  // arenas per workgroup (one wavefront)
+constexpr int kArenas = 4;                         // arenas per workgroup (one wavefront)
 constexpr int kWG = kArenas * kTeam;               // threads per workgroup
 static_assert(kWG <= 64, "one wavefront per workgroup");
 constexpr int kMaxCand = 64;        // narrowphase candidates per tick per arena

@@ -101,15 +101,12 @@ DEV void load_pad_regs(PadRegs& R, int l) {
 }
 
 // ------------------------------------------------------------------ one tick (Arena::Step body)
-// Inlined into the tick loop (RLGPU_TICK_ATTR).  Inlined, the compiler hoists the launch-invariant
+// Inlined into the tick loop.  Inlined, the compiler hoists the launch-invariant
 // constant-buffer values of all phases out of the loop (408 VGPR + AGPR, one wave per SIMD);
 // called (__noinline__) the kernel needs 248 VGPRs and could run two waves per SIMD, but measured
 // slower: 870 -> 938 us per launch at 4 arenas per wave, and 2 arenas per wave (two waves per
 // SIMD) 1.7x slower per arena.
-#ifndef RLGPU_TICK_ATTR
-#define RLGPU_TICK_ATTR DEV
-#endif
-RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R,
+DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, int arena, Prof& P, const PadRegs& R,
                           int nvalid) {
     if (valid) {  // per body / car on lanes 0-4: independent fields, read before the respawns below write
         rlgpu_arena_state& s = A->s;
@@ -209,18 +206,6 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
     if (threadIdx.x == 0) g_pen_save.n = 0;
     sync();
     P.mark(4);
-#if RLGPU_MESH_DEAL
-    // the bodies' mesh queries planned by lanes 0..4 of each arena, the 30 light pairs (planes, dynamic
-    // pairs) on the arena's lanes; then the mesh entries of all four arenas dealt over the workgroup
-    if (valid) {
-        mesh_plan(A, M, l);
-        for (int j = l; j < 30; j += kTeam) narrow_pair(A, M, j < 20 ? (j / 4) * 5 + 1 + (j % 4) : 25 + (j - 20));
-    }
-    sync();
-    narrow_mesh(A - (threadIdx.x >> 4), nvalid, M);
-    sync();
-    if (valid && l == 0) A->a.epa_lock = 0;  // the plan's bytes are the small solver set again
-#else
     if (valid)
         // work items: the 5 body-vs-mesh pairs split into kMeshChunks parts each (the heavy items,
         // spread over distinct lanes first), then the 30 light pairs
@@ -232,7 +217,6 @@ RLGPU_TICK_ATTR void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uin
                 narrow_pair(A, M, j < 20 ? (j / 4) * 5 + 1 + (j % 4) : 25 + (j - 20));
             }
         }
-#endif
     sync();
     P.mark(22);
     narrow_queue(A - (threadIdx.x >> 4), nvalid, M);

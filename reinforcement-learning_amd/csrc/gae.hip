@@ -63,7 +63,11 @@ struct GaeParams {
 //
 // The summary cannot know its truncation values (their index is a forward count over the tiles to its
 // left), so it composes maps of the form x -> c x + d + b T, T = the value of the tile's first truncation:
-// the tile's first terminal zeroes every coefficient to its right, so only that T can survive.
+// the tile's first terminal zeroes every coefficient to its right, so only that T can survive.  The carry pass
+// resolves such a tile as d + b T, i.e. the truncation element's delta as (n - v) + gamma T, where the apply
+// pass writes that element as (n + gamma T) - v: the carry into the tile to the left is the reassociated form
+// (same inputs, fixed order -- deterministic, within the 1e-5 contract of tests/test_gae.py, but not the
+// bits of a single sequential walk at those elements).
 constexpr int kFT = 256, kFV = 4;
 constexpr int kFTile = 8192;
 constexpr int kFRound = kFT * kFV, kFRounds = kFTile / kFRound;  // the apply pass: rounds of 1024
@@ -248,12 +252,13 @@ __global__ void __launch_bounds__(kFT) k_flat_summary(GaeParams p, float4* sumA,
 }
 
 struct FlatScratch {
+    std::mutex mu;  // held for one call on this device (calls on other devices run concurrently)
     char* p = nullptr;
     size_t bytes = 0;
     void* host = nullptr;  // pinned, mapped: the carry pass writes the FlatResult straight to the host
 };
-std::mutex g_flat_mu;
-std::vector<FlatScratch> g_flat_scratch;  // rlgpu_gae_flat's tile summaries, per device
+constexpr int kMaxDevices = 64;
+FlatScratch g_flat_scratch[kMaxDevices];  // rlgpu_gae_flat's tile summaries, per device
 
 struct FlatResult {
     int64_t total;  // truncations found (GAE.cpp:196-197 checks it against the values given)
@@ -635,11 +640,11 @@ extern "C" int rlgpu_gae_flat(const float* d_rews, const int8_t* d_terms, const 
                      o_p = take(sizeof(float2) * n), o_b = take(sizeof(int64_t) * (n + 1)),
                      o_x = take(sizeof(float2) * n), o_res = take(sizeof(FlatResult));
         // one scratch buffer per device, grown on demand and held for the call (the call ends synchronised)
-        std::lock_guard<std::mutex> lock(g_flat_mu);
         int dev = 0;
         RLGPU_CHECK_HIP(hipGetDevice(&dev));
-        if ((int)g_flat_scratch.size() <= dev) g_flat_scratch.resize(dev + 1);
+        RLGPU_REQUIRE(dev >= 0 && dev < kMaxDevices, "rlgpu_gae_flat: device index beyond the scratch table");
         FlatScratch& sc = g_flat_scratch[dev];
+        std::lock_guard<std::mutex> lock(sc.mu);
         if (sc.bytes < bytes) {
             if (sc.p) RLGPU_CHECK_HIP(hipFree(sc.p));
             sc.p = nullptr;

@@ -533,36 +533,8 @@ __global__ void __launch_bounds__(256) amax_rows(const float* X, int64_t rows, i
     h3_amax_commit(shards, m);
 }
 
-// Stage variants (the x6 GEMM's pipeline shape):
-//   V = 0: 32-deep stages, one LDS buffer, two workgroups per CU
-//   V = 1: 64-deep stages, one LDS buffer, one workgroup per CU
-//   V = 2: 32-deep stages, two LDS buffers (one barrier per stage: the next stage is split and
-//          stored while this stage's MFMAs run), one workgroup per CU
-template <int V> struct X6Shape;
-template <> struct X6Shape<0> { static constexpr int XK = 32, NB = 1, OCC = 2; };
-template <> struct X6Shape<1> { static constexpr int XK = 64, NB = 1, OCC = 1; };
-template <> struct X6Shape<2> { static constexpr int XK = 32, NB = 2, OCC = 1; };
-//   V = 3: 64-deep stages, one LDS buffer, two workgroups per CU (H3: two planes fit 2 x 73.7 KB)
-template <> struct X6Shape<3> { static constexpr int XK = 64, NB = 1, OCC = 2; };
-//   V = 4: 32-deep stages, two LDS buffers (one barrier per stage), two workgroups per CU (H3:
-//          2 x 80 KB of LDS)
-template <> struct X6Shape<4> { static constexpr int XK = 32, NB = 2, OCC = 2; };
-//   V = 5: V = 4 with the next stage's split / LDS stores interleaved between this stage's MFMAs
-//          (sched_group_barrier pattern), so one wave keeps the matrix pipe fed while it stages
-template <> struct X6Shape<5> { static constexpr int XK = 32, NB = 2, OCC = 2; };
-//   V = 6: V = 4 with the next stage stored first, then the stage after it loaded, then this
-//          stage's MFMAs (the loads get a whole stage of MFMAs and a barrier to land)
-template <> struct X6Shape<6> { static constexpr int XK = 32, NB = 2, OCC = 2; };
-//   V = 7 / 8 / 9: ablations of V = 0 for timing only (results are garbage): 7 stores the loaded
-//          bits without the split VALU, 8 issues no global loads after the first stage, 9 runs no MFMA
-template <> struct X6Shape<7> { static constexpr int XK = 32, NB = 1, OCC = 2; };
-template <> struct X6Shape<8> { static constexpr int XK = 32, NB = 1, OCC = 2; };
-template <> struct X6Shape<9> { static constexpr int XK = 32, NB = 1, OCC = 2; };
-template <> struct X6Shape<10> { static constexpr int XK = 32, NB = 1, OCC = 2; };  // 8 + 9
-template <> struct X6Shape<11> { static constexpr int XK = 32, NB = 1, OCC = 2; };  // no epilogue stores
-//   V = 12: V = 0 compiled for four workgroups per CU (<= 128 VGPRs; 4 x 40 KB of LDS)
-template <> struct X6Shape<12> { static constexpr int XK = 32, NB = 1, OCC = 4; };
-
+// gemm_x6's pipeline: 32-deep stages, one LDS buffer, the next stage prefetched into registers while this
+// stage's MFMAs run; two (x6) or three (H3: 146 VGPRs, 40 KB LDS) workgroups per CU.
 template <int XK>
 DEV void x6_mfma_stage(const uint16_t (*As)[BM][XK + XPAD], const uint16_t (*Bs)[BN][XK + XPAD], int ra, int rb, int lane,
                        f32x16 (&acc)[2][2], f32x16 (&cor)[2][2]) {
@@ -681,14 +653,14 @@ DEV void h3_mfma_stage(const uint16_t (*As)[BM][P], const uint16_t (*Bs)[BN][P],
     }
 }
 
-template <int LA, int LB, bool AV, bool BV, bool BPRE, int V, bool H3 = false>
-__global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
-    constexpr int XK = X6Shape<V>::XK, NB = X6Shape<V>::NB, NQ = XK / 16, NP = H3 ? 2 : 3;
+template <int LA, int LB, bool AV, bool BV, bool BPRE, bool H3 = false>
+__global__ void __launch_bounds__(256, 2) gemm_x6(GemmArgs g) {
+    constexpr int XK = 32, NB = 1, NQ = XK / 16, NP = H3 ? 2 : 3;
     constexpr bool AK = LA == A_IK, BKM = LB == B_JK;
     // H3 with 32-deep stages: row-index-contiguous operands staged k-major (xt_load / tr_frag)
     constexpr bool TA = H3 && !AK && XK == 32, TB = H3 && !BPRE && !BKM && XK == 32;
     // H3 with both operands k-contiguous, default variant: unpadded XOR-swizzled planes (xchunk)
-    constexpr bool SWZ = H3 && !TA && !TB && XK == 32 && V == 0;
+    constexpr bool SWZ = H3 && !TA && !TB;
     constexpr int P = SWZ ? XK : XK + XPAD;
     __shared__ uint16_t As[NB][NP][BM][P];
     __shared__ uint16_t Bs[NB][NP][BN][P];
@@ -717,10 +689,7 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     const float sa = pow2f(pa), sb = pow2f(pb);
     const RowPtrs arow = xs_rows<AK, XK>(g.A, g.lda, i0, g.I);
     const RowPtrs brow = xs_rows<BKM, XK>(g.B, g.ldb, j0, g.J);
-    bool first_load = true;
     auto load_stage = [&](int k0) {
-        if ((V == 8 || V == 10) && !first_load) return;
-        first_load = false;
         if constexpr (TA)
             xt_load<AV>(va, g.A, g.lda, i0, g.I, k0, ke);
         else
@@ -734,16 +703,6 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
     };
     const int ra = wm * 64 + (lane & 31), rb = wn * 64 + (lane & 31);
     auto store_stage = [&](int buf) {
-        if (V == 7 && !TA && !TB) {  // ablation: the loaded bits straight into the planes
-#pragma unroll
-            for (int q = 0; q < NQ; q++) {
-                const int row = xs_row<AK, XK>(q), c = xs_kg<AK, XK>(q) * 8;
-                *reinterpret_cast<f32x4_t*>(&As[buf][0][row][c]) = va[q][0];
-                *reinterpret_cast<f32x4_t*>(&As[buf][1][row][c]) = va[q][1];
-            }
-            if (BPRE) xp_store<XK, NP, P>(Bs[buf], vp);
-            return;
-        }
         if constexpr (TA)
             xt_store(As[buf], va, sa);
         else
@@ -756,67 +715,24 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
             xs_store<BKM, XK, H3, P>(Bs[buf], vb, sb);
     };
     auto mfma_stage = [&](int buf) {
-        if (V == 9 || V == 10) return;
         if constexpr (H3)
             h3_mfma_stage<XK, TA, TB, P>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
         else
             x6_mfma_stage<XK>(As[buf], Bs[buf], ra, rb, lane, acc, cor);
     };
     load_stage(kb);
-    if (NB == 1) {
-        for (int k0 = kb; k0 < ke; k0 += XK) {
-            store_stage(0);
-            __syncthreads();
-            // prefetch the next stage into registers while the MFMAs run; unconditional (past ke it
-            // reads the zero row) so the loop-carried registers are the load destinations
-            load_stage(k0 + XK);
-            __builtin_amdgcn_sched_barrier(0);  // keep the split of the prefetched stage after the MFMAs
-            mfma_stage(0);
-            __syncthreads();
-        }
-    } else {
+    for (int k0 = kb; k0 < ke; k0 += XK) {
         store_stage(0);
         __syncthreads();
-        load_stage(kb + XK);
-        int buf = 0;
-        for (int k0 = kb; k0 < ke; k0 += XK) {
-            // this stage's MFMAs on buf; the next stage (already in registers) is split into the
-            // other buffer, free since the previous barrier; then the stage after is prefetched
-            if (V == 6) {
-                store_stage(buf ^ 1);
-                load_stage(k0 + 2 * XK);
-                mfma_stage(buf);
-            } else {
-                mfma_stage(buf);
-                store_stage(buf ^ 1);
-                load_stage(k0 + 2 * XK);
-            }
-            if (V == 5 && H3) {
-                // per stage and wave: 16 ds_read (8 per 16-deep k step), 24 MFMA, 8 ds_write and the
-                // split VALU of the next stage, 8 global loads.  Masks: 0x8 MFMA, 0x2 VALU, 0x100
-                // DS read, 0x200 DS write, 0x20 VMEM read.
-                __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-                for (int i = 0; i < 12; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                }
-#pragma unroll
-                for (int i = 0; i < 12; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    if (i < 8) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                }
-                __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);
-            }
-            __syncthreads();
-            buf ^= 1;
-        }
+        // prefetch the next stage into registers while the MFMAs run; unconditional (past ke it
+        // reads the zero row) so the loop-carried registers are the load destinations
+        load_stage(k0 + XK);
+        __builtin_amdgcn_sched_barrier(0);  // keep the split of the prefetched stage after the MFMAs
+        mfma_stage(0);
+        __syncthreads();
     }
     float* C = g.C + (int64_t)tl.z * g.c_split;
     const int h = lane >> 5, l32 = lane & 31;
-    if (V == 11 && g.ldc != -7) return;  // ablation: no epilogue (the condition keeps the MFMAs alive)
     // H3: undo the operand scales (powers of two: exact); the pre-split B's per-row inverse scale
     // is read for the tile's columns (rows past J carry 1)
     const int pab = pa + pb;
@@ -855,45 +771,8 @@ __global__ void __launch_bounds__(256, X6Shape<V>::OCC) gemm_x6(GemmArgs g) {
         }
 }
 
-// ---- H3 GEMM with 128 x 256 tiles (gemm_h3w): each of the 4 waves computes 64 x 128 (2 x 4 MFMA
-// blocks), so per 16-deep k step a wave issues 24 MFMAs for 12 LDS fragment reads (the 128 x 128
-// kernel: 12 for 8) and every A panel is read once per 256 output columns instead of per 128.
-// Operands: A_IK (k-contiguous, split in the loader) or A_KI (k-major staging, tr reads); B the
-// pre-split planes (rows padded to a multiple of 256) or B_KJ (k-major staging).  32-deep stages,
-// one LDS buffer (20 KB A + 40 KB B), two workgroups per CU.  Same arithmetic and epilogue as the
-// H3 path of gemm_x6.
+// weight planes are padded to whole 256-row blocks (the 256 x 256 tiles of gemm_h3q / gemm_h3qt)
 constexpr int BNW = 2 * BN;
-template <bool VEC, int COLS>
-DEV void xtn_load(f32x4_t* v, const float* base, int64_t ld, int o0, int on, int k0, int ke) {
-    constexpr int PER = COLS / 4;  // float4 per k row
-#pragma unroll
-    for (int q = 0; q < COLS / 32; q++) {
-        const int e = threadIdx.x + 256 * q;
-        const int k = k0 + e / PER, o = o0 + (e % PER) * 4;
-        const float* row = k < ke ? base + (int64_t)k * ld : nullptr;
-        v[q] = load4v<VEC>(row, o, on);
-    }
-}
-template <int COLS>
-DEV void xtn_store(uint16_t* ph, uint16_t* pl, const f32x4_t* v, float sc) {
-    constexpr int PER = COLS / 4, P = COLS + 32;
-#pragma unroll
-    for (int q = 0; q < COLS / 32; q++) {
-        const int e = threadIdx.x + 256 * q;
-        const int off = (e / PER) * P + (e % PER) * 4;
-        const f32x4_t x = v[q];
-        uint32_t h2[2], l2[2];
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const float x0 = x[2 * c] * sc, x1 = x[2 * c + 1] * sc;
-            const uint16_t h0 = f2hf(x0), h1 = f2hf(x1);
-            h2[c] = pack_h2(h0, h1);
-            l2[c] = pack_h2(f2hf(x0 - hf2f(h0)), f2hf(x1 - hf2f(h1)));
-        }
-        *reinterpret_cast<uint2*>(ph + off) = make_uint2(h2[0], h2[1]);
-        *reinterpret_cast<uint2*>(pl + off) = make_uint2(l2[0], l2[1]);
-    }
-}
 // tr_frag over a k-major plane of row pitch P halves (P = COLS + 32: conflict-free, see TPITCH)
 template <int P>
 DEV h16x8 trp_frag(const uint16_t* plane, int ob, int kof0, int lane) {
@@ -908,139 +787,12 @@ DEV h16x8 trp_frag(const uint16_t* plane, int ob, int kof0, int lane) {
     return __builtin_bit_cast(h16x8, r);
 }
 
-template <int LA, int LB, bool AV, bool BV, bool BPRE>
-__global__ void __launch_bounds__(256, 2) gemm_h3w(GemmArgs g) {
-    constexpr int XK = 32;
-    constexpr bool TA = LA == A_KI, TB = !BPRE;
-    static_assert(BPRE || LB == B_KJ, "gemm_h3w: B is either pre-split or B_KJ");
-    static_assert(32 * (BNW + 32) <= BNW * (XK + XPAD), "k-major B plane must fit");
-    __shared__ uint16_t As[2][BM][XK + XPAD];
-    __shared__ uint16_t Bs[2][BNW][XK + XPAD];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wm = w >> 1, wn = w & 1;
-    const Tile tl = xcd_tile(g.gx, g.gy, g.gz);
-    const int i0 = tl.y * BM, j0 = tl.x * BNW;
-    const int kb = tl.z * g.kchunk;
-    const int ke = min(g.K, kb + g.kchunk);
-    f32x16 acc[2][4];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
-    f32x4_t va[4];           // A stage: 128 x 32 floats
-    f32x4_t vb[8];           // B_KJ stage: 32 x 256 floats
-    u32x4_t vp[2][4];        // pre-split B stage: 2 planes x 256 rows x 32 halves
-    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
-    const int pa = h3_pow(shard_max_bits(g.amax_a));
-    const int pb = BPRE ? 0 : h3_pow(shard_max_bits(g.amax_b));
-    const float sa = pow2f(pa), sb = pow2f(pb);
-    const RowPtrs arow = xs_rows<!TA, XK>(g.A, g.lda, i0, g.I);
-    auto load_stage = [&](int k0) {
-        if constexpr (TA) {
-            xtn_load<AV, BM>(va, g.A, g.lda, i0, g.I, k0, ke);
-        } else {
-            f32x4_t (&v2)[2][2] = *reinterpret_cast<f32x4_t (*)[2][2]>(va);
-            xs_load<true, AV, XK>(v2, arow, g.A, g.lda, i0, g.I, k0, ke);
-        }
-        if constexpr (BPRE) {
-            constexpr int KG = XK / 8;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int e = threadIdx.x + 256 * q;
-                const int64_t off = (int64_t)(j0 + e / KG) * g.ldb + k0 + (e % KG) * 8;
-                const bool ok = k0 + (e % KG) * 8 < ke;
-#pragma unroll
-                for (int p = 0; p < 2; p++)
-                    vp[p][q] = *reinterpret_cast<const u32x4_t*>(ok ? Bp + p * g.bplane + off
-                                                                   : reinterpret_cast<const uint16_t*>(g_zero_row));
-            }
-        } else {
-            xtn_load<BV, BNW>(vb, g.B, g.ldb, j0, g.J, k0, ke);
-        }
-    };
-    auto store_stage = [&]() {
-        if constexpr (TA) {
-            xtn_store<BM>(&As[0][0][0], &As[1][0][0], va, sa);
-        } else {
-            const f32x4_t (&v2)[2][2] = *reinterpret_cast<const f32x4_t (*)[2][2]>(va);
-            xs_store<true, XK, true>(As, v2, sa);
-        }
-        if constexpr (BPRE) {
-            constexpr int KG = XK / 8;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int e = threadIdx.x + 256 * q;
-#pragma unroll
-                for (int p = 0; p < 2; p++) *reinterpret_cast<u32x4_t*>(&Bs[p][e / KG][(e % KG) * 8]) = vp[p][q];
-            }
-        } else {
-            xtn_store<BNW>(&Bs[0][0][0], &Bs[1][0][0], vb, sb);
-        }
-    };
-    const int ra = wm * 64 + (lane & 31), rb = wn * 128 + (lane & 31);
-    auto mfma_stage = [&]() {
-#pragma unroll
-        for (int ks = 0; ks < XK / 16; ks++) {
-            const int kof = ks * 16 + 8 * (lane >> 5);
-            h16x8 a[2][2], b[2][4];
-#pragma unroll
-            for (int p = 0; p < 2; p++) {
-#pragma unroll
-                for (int u = 0; u < 2; u++)
-                    a[p][u] = TA ? trp_frag<BM + 32>(&As[p][0][0], wm * 64 + 32 * u, ks * 16, lane)
-                                 : *(const h16x8*)&As[p][ra + 32 * u][kof];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    b[p][u] = TB ? trp_frag<BNW + 32>(&Bs[p][0][0], wn * 128 + 32 * u, ks * 16, lane)
-                                 : *(const h16x8*)&Bs[p][rb + 32 * u][kof];
-            }
-#pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 4; tj++) {
-                    f32x16 c = acc[ti][tj];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1][ti], b[0][tj], c, 0, 0, 0);  // l h
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[1][tj], c, 0, 0, 0);  // h l
-                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0][ti], b[0][tj], c, 0, 0, 0);  // h h
-                }
-        }
-    };
-    load_stage(kb);
-    for (int k0 = kb; k0 < ke; k0 += XK) {
-        store_stage();
-        __syncthreads();
-        load_stage(k0 + XK);  // unconditional: past ke it reads the zero row
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_stage();
-        __syncthreads();
-    }
-    float* C = g.C + (int64_t)tl.z * g.c_split;
-    const int h = lane >> 5, l32 = lane & 31;
-    const int pab = pa + pb;
-#pragma unroll
-    for (int tj = 0; tj < 4; tj++) {
-        const int j = j0 + wn * 128 + tj * 32 + l32;
-        if (j >= g.J) continue;
-        const float bsc = BPRE ? g.bscale[j] : 1.f;
-        const float bj = g.bias ? g.bias[j] : 0.f;
-#pragma unroll
-        for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (i < g.I) C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * bsc, -pab) + bj;
-            }
-    }
-}
-
 // ---- H3 GEMM with 256 x 256 tiles (gemm_h3q): the forward and input-gradient GEMMs (A_IK fp32 x the
 // pre-split fp16 B planes, J a multiple of 256).  The 128 x 128 tile reads 32 KB from L2 per 128 x 128 x 32
 // stage; at ~70 GB/s of L2 per CU (MI355X_MICROARCH.md, "Indexed rows") three such workgroups per CU need
 // more feed cycles than their MFMAs take, so the stage skeleton, not the matrix pipe, sets gemm_x6's time.
 // A 256 x 256 tile halves the L2 bytes per product.  8 waves (512 threads, one workgroup per CU, two waves
-// per SIMD), each 64 x 128 as in gemm_h3w; double-buffered LDS (2 x 64 KB) with one barrier per stage:
+// per SIMD), each 64 x 128 (2 x 4 MFMA blocks); double-buffered LDS (2 x 64 KB) with one barrier per stage:
 // this stage's MFMAs run on one buffer while the next stage (in registers since the previous iteration)
 // is split into the other and the stage after is loaded.  Per 16-deep k step and block the products enter
 // the one accumulator as l.h, h.l, h.h -- gemm_x6's H3 order -- so the results are bit-identical to it.
@@ -1157,9 +909,9 @@ __global__ void __launch_bounds__(512, 1) gemm_h3q(GemmArgs g) {
 }
 
 // ---- gemm_h3q's weight-gradient form (gemm_h3qt): A_KI (dZ^T) x B_KJ (activations), both row-index
-// contiguous, staged k-major as gemm_h3w stages its B (float4 loads along the output index, planes [k][256 + 32],
+// contiguous, staged k-major (float4 loads along the output index, planes [k][256 + 32],
 // fragments read back with ds_read_b64_tr_b16); split-K over grid z like the other kernels.  Same products in
-// the same order per split as gemm_x6 / gemm_h3w: bit-identical partials.
+// the same order per split as gemm_x6: bit-identical partials.
 template <bool VEC>
 DEV void q_kload(f32x4_t (&v)[4], const float* base, int64_t ld, int o0, int on, int k0, int ke) {
 #pragma unroll
@@ -1267,168 +1019,6 @@ __global__ void __launch_bounds__(512, 1) gemm_h3qt(GemmArgs g) {
                 if (i < g.I) C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * 1.f, -pab) + bj;
             }
     }
-}
-
-// ---- H3 GEMM on an LDS-DMA ring (gemm_h3r): C = A . B^T + bias with A_IK fp32 (k contiguous) and
-// B the pre-split fp16 planes -- the forward and input-gradient GEMMs of training.  128 x 128 tile,
-// 4 waves of 64 x 64, one workgroup per CU.  Both operands travel global -> LDS by
-// global_load_lds_dwordx4 (no VGPR round trip, no staging VALU) into a ring of NS stages of RK k;
-// the ring keeps NS - 1 stages in flight across the raw barriers (counted vmcnt, never 0 inside the
-// loop), so the loads of a stage have NS - 1 stages of MFMAs to land instead of one.  A stays fp32
-// in LDS and each wave splits its own fragments after ds_read (split2h, the same scaled fp16 pair
-// as the staged kernels), so the products, their order (per 16-deep k step: l.h, h.l, h.h into the
-// one accumulator) and the epilogue are gemm_x6's H3 path: the results are bit-identical.
-// LDS images are lane-linear per DMA instruction; bank conflicts are removed by an XOR swizzle of
-// the 16-byte slot within a row (rswz), applied on the DMA's global source address and on the read.
-template <int RK>
-struct RingGeom {
-    static constexpr int AROW = RK * 4, BROW = RK * 2;                      // bytes per LDS row
-    static constexpr int ABYTES = BM * AROW, BPLANE = BN * BROW;
-    static constexpr int STAGE = ABYTES + 2 * BPLANE;
-    static constexpr int AINS = ABYTES / 1024 / 4, BINS = 2 * BPLANE / 1024 / 4;  // DMAs per wave and stage
-    static constexpr int ARPI = 1024 / AROW, BRPI = 1024 / BROW;           // rows per DMA
-};
-// physical 16-byte slot of logical slot s in row r of an LDS image with ROWB-byte rows (<= 256):
-// the rows sharing one 256-byte bank row, and the 16 lanes of a ds_read_b128 group (rows {0-3,
-// 12-15, 20-27} + 32 u), land on 16 distinct slots
-template <int ROWB>
-DEV int rswz(int r, int s) {
-    constexpr int S = ROWB / 16, Q = 256 / ROWB;
-    return s ^ ((r / Q) & (S - 1));
-}
-DEV void glds16(const void* src, void* lds) {
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
-}
-template <int RK, int NS>
-__global__ void __launch_bounds__(256, NS * RingGeom<RK>::STAGE <= 80 * 1024 ? 2 : 1) gemm_h3r(GemmArgs g) {
-    using G = RingGeom<RK>;
-    static_assert(NS * G::STAGE <= 160 * 1024, "ring exceeds the CU's LDS");
-    constexpr int NV = (G::AINS + G::BINS) * (NS - 2);  // DMAs per wave allowed in flight at a stage's wait
-    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * G::STAGE];  // the kernel's only LDS object
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wm = w >> 1, wn = w & 1;
-    const Tile tl = xcd_tile(g.gx, g.gy, 1);
-    const int i0 = tl.y * BM, j0 = tl.x * BN;
-    const int K = g.K;
-    // operand scale first: its load retires before the first DMA is issued
-    const int pa = h3_pow(shard_max_bits(g.amax_a));
-    const float sa = pow2f(pa);
-    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
-    const float* zero = reinterpret_cast<const float*>(g_zero_row);
-    // per-lane DMA sources, fixed for the whole K loop: row base + swizzled chunk (stage k0 added)
-    const float* asrc[G::AINS];
-    int akc[G::AINS];  // first k of the lane's chunk within a stage
-#pragma unroll
-    for (int q = 0; q < G::AINS; q++) {
-        const int r = (w * G::AINS + q) * G::ARPI + lane / (G::AROW / 16);
-        const int c = rswz<G::AROW>(r, lane % (G::AROW / 16));
-        akc[q] = 4 * c;
-        asrc[q] = (i0 + r < g.I) ? g.A + (int64_t)(i0 + r) * g.lda + 4 * c : nullptr;
-    }
-    const uint16_t* bsrc[G::BINS];
-#pragma unroll
-    for (int q = 0; q < G::BINS; q++) {
-        constexpr int PER_PLANE = G::BPLANE / 1024;
-        const int e = w * G::BINS + q, p = e / PER_PLANE;
-        const int r = (e % PER_PLANE) * G::BRPI + lane / (G::BROW / 16);
-        const int c = rswz<G::BROW>(r, lane % (G::BROW / 16));
-        bsrc[q] = Bp + p * g.bplane + (int64_t)(j0 + r) * g.ldb + 8 * c;
-    }
-    const int nst = (K + RK - 1) / RK;
-    // stage s into ring slot s % NS (a stage past the last reads the zero row: the in-flight count
-    // stays NS - 1 to the end, so every wait is the same constant)
-    auto issue = [&](int s) {
-        uint8_t* dst = ring + (s % NS) * G::STAGE;
-        const int k0 = s * RK;
-        const bool live = s < nst;
-#pragma unroll
-        for (int q = 0; q < G::AINS; q++) {
-            const bool ok = live && asrc[q] && (k0 + akc[q] < K);
-            glds16(ok ? asrc[q] + k0 : zero, dst + (w * G::AINS + q) * 1024);
-        }
-#pragma unroll
-        for (int q = 0; q < G::BINS; q++)
-            glds16(live ? (const void*)(bsrc[q] + k0) : (const void*)zero, dst + G::ABYTES + (w * G::BINS + q) * 1024);
-    };
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[a][b][r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < NS - 1; s++) issue(s);
-    const int l32 = lane & 31, hk = lane >> 5;
-    for (int it = 0; it < nst; it++) {
-        // this wave's DMAs of stage it have landed (NS - 2 younger stages may still fly); the barrier
-        // extends that to every wave's, and retires every wave's reads of the slot refilled next
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NV) : "memory");
-        issue(it + NS - 1);
-        const uint8_t* As = ring + (it % NS) * G::STAGE;
-        const uint8_t* Bs = As + G::ABYTES;
-#pragma unroll
-        for (int ks = 0; ks < RK / 16; ks++) {
-            h16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int ra = wm * 64 + 32 * u + l32, sa0 = ks * 4 + 2 * hk;
-                f32x4_t v[2];
-                v[0] = *(const f32x4_t*)(As + ra * G::AROW + rswz<G::AROW>(ra, sa0) * 16);
-                v[1] = *(const f32x4_t*)(As + ra * G::AROW + rswz<G::AROW>(ra, sa0 + 1) * 16);
-                u32x4_t h, l;
-                split2h(v, sa, h, l);
-                ah[u] = __builtin_bit_cast(h16x8, h);
-                al[u] = __builtin_bit_cast(h16x8, l);
-                const int rb = wn * 64 + 32 * u + l32;
-                const int ob = rb * G::BROW + rswz<G::BROW>(rb, ks * 2 + hk) * 16;
-                bh[u] = *(const h16x8*)(Bs + ob);
-                bl[u] = *(const h16x8*)(Bs + G::BPLANE + ob);
-            }
-#pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++) {
-                    f32x16 c = acc[ti][tj];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ti], bh[tj], c, 0, 0, 0);  // l h
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ti], bl[tj], c, 0, 0, 0);  // h l
-                    acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ti], bh[tj], c, 0, 0, 0);  // h h
-                }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-row DMAs past the last stage
-    const int h = hk;
-    float csc[2];
-#pragma unroll
-    for (int tj = 0; tj < 2; tj++) csc[tj] = g.bscale[j0 + wn * 64 + tj * 32 + l32];
-    if (i0 + BM <= g.I && j0 + BN <= g.J) {
-        float* cb = g.C + (int64_t)(i0 + wm * 64 + 4 * h) * g.ldc + j0 + wn * 64 + l32;
-#pragma unroll
-        for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-            for (int tj = 0; tj < 2; tj++) {
-                const float bj = g.bias ? g.bias[j0 + wn * 64 + tj * 32 + l32] : 0.f;
-                float* ct = cb + (int64_t)(ti * 32) * g.ldc + tj * 32;
-#pragma unroll
-                for (int r = 0; r < 16; r++)
-                    ct[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = ldexpf(acc[ti][tj][r] * csc[tj], -pa) + bj;
-            }
-        return;
-    }
-#pragma unroll
-    for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-        for (int tj = 0; tj < 2; tj++) {
-            const int j = j0 + wn * 64 + tj * 32 + l32;
-            if (j >= g.J) continue;
-            const float bj = g.bias ? g.bias[j] : 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int i = i0 + wm * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (i < g.I) g.C[(int64_t)i * g.ldc + j] = ldexpf(acc[ti][tj][r] * csc[tj], -pa) + bj;
-            }
-        }
 }
 
 // ---- bf16 inference GEMM: C[i,j] = bf16( sum_k A[i,k] W[j,k] + bias[j] ) on
@@ -2047,15 +1637,6 @@ __global__ void __launch_bounds__(256) ln_act_bwd(const float* dA, const float* 
 // is one contiguous 1 KB), the row sums reduced over the 4 waves through LDS in a fixed order.  Same
 // arguments as the wave-per-row kernels (the rank-1 head options are not taken: those layers keep them).
 constexpr int LNW_ROWS = 32;
-// RLGPU_WIDE_LN=0: the wave-per-row kernels at every width; 2: the wide kernels with 2 rows per pass (A/B)
-inline int wide_ln_mode() {
-    static const int v = [] {
-        const char* e = std::getenv("RLGPU_WIDE_LN");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
-}
-inline bool wide_ln() { return wide_ln_mode() != 0; }
 DEV int wcol(int k) { return 4 * (int)threadIdx.x + 1024 * k; }
 DEV float4 ld4(const float* p, int c, int H) { return c < H ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f); }
 
@@ -2251,17 +1832,15 @@ __global__ void __launch_bounds__(256) ln_act_bwd_wide(const float* dA, const fl
 // the wide kernels for H in (512, 4096] with H % 4 == 0 (null: not applicable)
 inline decltype(&ln_act_fwd_wide<2>) ln_act_fwd_wide_any(int H) {
     if (H <= 512 || H % 4 != 0 || H > 4096) return nullptr;
-    const bool r2 = wide_ln_mode() == 2;
-    if (H <= 1024) return r2 ? &ln_act_fwd_wide<1, 2> : &ln_act_fwd_wide<1>;
-    if (H <= 2048) return r2 ? &ln_act_fwd_wide<2, 2> : &ln_act_fwd_wide<2>;
-    return r2 ? &ln_act_fwd_wide<4, 2> : &ln_act_fwd_wide<4>;
+    if (H <= 1024) return &ln_act_fwd_wide<1>;
+    if (H <= 2048) return &ln_act_fwd_wide<2>;
+    return &ln_act_fwd_wide<4>;
 }
 inline decltype(&ln_act_bwd_wide<2>) ln_act_bwd_wide_any(int H) {
     if (H <= 512 || H % 4 != 0 || H > 4096) return nullptr;
-    const bool r2 = wide_ln_mode() == 2;
-    if (H <= 1024) return r2 ? &ln_act_bwd_wide<1, 2> : &ln_act_bwd_wide<1>;
-    if (H <= 2048) return r2 ? &ln_act_bwd_wide<2, 2> : &ln_act_bwd_wide<2>;
-    return r2 ? &ln_act_bwd_wide<4, 2> : &ln_act_bwd_wide<4>;
+    if (H <= 1024) return &ln_act_bwd_wide<1>;
+    if (H <= 2048) return &ln_act_bwd_wide<2>;
+    return &ln_act_bwd_wide<4>;
 }
 
 // NPER (columns per lane) dispatch: H <= 64 * NPER
@@ -2295,36 +1874,23 @@ inline decltype(&ln_act_bwd<16, true>) ln_act_bwd_head_any(int H) {
     return &ln_act_bwd<32, true>;
 }
 
-// Row-shape variants of the H in (256, 512] kernels (host: RLGPU_LNF_VARIANT / RLGPU_LNB_VARIANT):
-// rows per block and rows in flight per wave.  Same bits for any forward variant; a backward
-// variant with other rows per block regroups the column partials (fp32 sums in another order).
-inline decltype(&ln_act_fwd_f32<8>) ln_act_fwd_f32_pick(int H, int v, int* rows, bool head = false) {
+// The LayerNorm kernels by width: the wide workgroup-per-row-group kernels above 512 columns (not for the
+// rank-1 head's fused backward), the wave-per-row kernels below.
+inline decltype(&ln_act_fwd_f32<8>) ln_act_fwd_f32_pick(int H, int* rows, bool head = false) {
     *rows = LNF_ROWS;
-    if (!head && wide_ln())
+    if (!head)
         if (auto f = ln_act_fwd_wide_any(H)) {
             *rows = LNW_ROWS;
             return f;
         }
-    if (H > 256 && H <= 512) switch (v) {
-            case 1: *rows = 32; return &ln_act_fwd_f32<8, 32, 4>;
-            case 2: *rows = 8; return &ln_act_fwd_f32<8, 8, 2>;
-            case 3: *rows = 64; return &ln_act_fwd_f32<8, 64, 4>;
-            default: break;
-        }
     return ln_act_fwd_f32_any(H);
 }
-inline decltype(&ln_act_bwd<8>) ln_act_bwd_pick(int H, bool head, int v, int* rows) {
+inline decltype(&ln_act_bwd<8>) ln_act_bwd_pick(int H, bool head, int* rows) {
     *rows = LNB_ROWS;
-    if (!head && wide_ln())
+    if (!head)
         if (auto f = ln_act_bwd_wide_any(H)) {
             *rows = LNW_ROWS;
             return f;
-        }
-    if (H > 256 && H <= 512) switch (v) {
-            case 1: *rows = 16; return head ? &ln_act_bwd<8, true, 16, 2> : &ln_act_bwd<8, false, 16, 2>;
-            case 2: return head ? &ln_act_bwd<8, true, 32, 4> : &ln_act_bwd<8, false, 32, 4>;
-            case 3: *rows = 64; return head ? &ln_act_bwd<8, true, 64, 4> : &ln_act_bwd<8, false, 64, 4>;
-            default: break;
         }
     return head ? ln_act_bwd_head_any(H) : ln_act_bwd_any(H);
 }

@@ -10,7 +10,6 @@
 #include "common.hpp"
 #include "mlp_kernels.hpp"
 #include "ppo_kernels.hpp"
-#include "row_gemm.hpp"
 #include "infer_kernels.hpp"
 
 namespace {
@@ -72,39 +71,9 @@ constexpr int kMaxSplits = 256;
 // concurrent gemm_f32 workgroups on the device (CUs x RLGPU_GEMM_OCC), set at create: the split-K
 // weight gradients are sized to fill whole rounds of workgroups
 int g_cus = 256;  // compute units of the device, set at create
-// x6 GEMM pipeline shape (mlp::X6Shape): RLGPU_X6_VARIANT=0/1/2 selects it (experiments), default 0
-inline int x6_variant() {
-    static const int v = [] {
-        const char* e = getenv("RLGPU_X6_VARIANT");
-        int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 2) ? x : 0;
-    }();
-    return v;
-}
-// H3 pipeline shape: RLGPU_H3_VARIANT=0..3 (experiments), default 0 (32-deep stages, 2 WGs / CU:
-// measured 144.6 ms learn per C2 iteration against 153.1 ms for the 64-deep variant 3)
-inline int h3_variant() {
-    static const int v = [] {
-        const char* e = getenv("RLGPU_H3_VARIANT");
-        int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 12) ? x : 0;
-    }();
-    return v;
-}
-// H3 GEMMs on the 128 x 256 tile kernel (mlp::gemm_h3w): by default for 1024 or more output columns (the C5
-// leg's 2048-wide layers: 32.8 -> 31.6 ms per 50k minibatch, profiles/r05u_h3_wide_ab.txt); at 512 columns the
-// 128 x 128 gemm_x6 at three workgroups per CU is faster (1.57 vs 1.81 ms per C2 minibatch).  RLGPU_H3_WIDE=0:
-// never, 1: for every width above 128.
-inline bool h3_wide(int J) {
-    static const int mode = [] {
-        const char* e = getenv("RLGPU_H3_WIDE");
-        return e ? atoi(e) : -1;
-    }();
-    return mode == 1 ? J > mlp::BN : (mode == 0 ? false : J >= 1024);
-}
 // Forward / input-gradient H3 GEMMs with output widths that are multiples of 256 on the 256 x 256 tile kernel
-// mlp::gemm_h3q, and weight gradients on mlp::gemm_h3qt (same bits as gemm_x6 / gemm_h3w): by default for 1024 or
-// more output columns (the C5 leg's 2048-wide layers: 31.6 -> 27.6 ms per 50k minibatch against gemm_h3w for both,
+// mlp::gemm_h3q, and weight gradients on mlp::gemm_h3qt (same bits as gemm_x6): by default for 1024 or
+// more output columns (the C5 leg's 2048-wide layers: 31.6 -> 27.6 ms per 50k minibatch against 128 x 256 tiles,
 // profiles/r05ad_h3_quad_ab.txt); at 512 columns
 // (K = 512, 16 stages per tile) its one workgroup per CU cannot hide the tile's prologue and epilogue and the
 // C2 minibatch takes 1.59 -> 1.70 ms.  RLGPU_H3_QUAD=0: never, 1: for every width that is a multiple of 256.
@@ -116,61 +85,12 @@ inline bool h3_quad(int J) {
     if (J % mlp::BQ != 0) return false;
     return mode == 1 ? true : (mode == 0 ? false : J >= 1024);
 }
-// Forward / input-gradient H3 GEMMs (A_IK x pre-split B) on the LDS-DMA ring kernel mlp::gemm_h3r when
-// RLGPU_H3_RING = 1 (32-deep stages, 4-stage ring), 2 (64-deep, 2 stages), 3 (32-deep, 3 stages) or 4
-// (32-deep, 2 stages, two workgroups per CU); 0 (default): the register-staged gemm_x6 path.  Same
-// bits either way.  Measured in the C2 learn phase (tools/learn_bench.py, 50k minibatch): 1.58 ms per
-// minibatch on gemm_x6, 1.81 (ring 1 / 2) and 1.63 (ring 4) -- one wave per SIMD cannot hide the
-// per-wave split of the fp32 A fragments, so the ring stays an experiment.
-inline int h3_ring() {
-    static const int v = [] {
-        const char* e = getenv("RLGPU_H3_RING");
-        const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 4) ? x : 0;
-    }();
-    return v;
-}
-inline int x6_occ() { return x6_variant() == 0 ? 2 : 1; }
-// LayerNorm row-shape variants (mlp::ln_act_fwd_f32_pick / ln_act_bwd_pick), for microbenchmarks
-inline int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-// Full-row H3 GEMMs (mlp::gemm_row, row_gemm.hpp): the training forward's Linear + LayerNorm + LeakyReLU of a
-// hidden layer with 256 or 512 outputs in one kernel, and the dA GEMM with the LayerNorm backward.
-// RLGPU_ROW_GEMM: 0 (default) off (the 128 x 128 GEMM + ln_act_fwd / ln_act_bwd), 1 on (ring of 2 stages x 32 k),
-// 2 on (4 stages x 16 k).
-inline int row_gemm() {
-    // off by default: measured slower than gemm_x6 + the LayerNorm passes (profiles/r05h_row_gemm_ab.txt)
-    static const int v = env_int("RLGPU_ROW_GEMM", 0);
-    return v;
-}
-// the full-row kernel's ring: RLGPU_ROW_GEMM=1 -> 2 stages of 32 k, 2 -> 4 stages of 16 k (3 in flight)
-template <int EPI>
-void launch_row(int N, int n, hipStream_t s, const mlp::RowArgs& a) {
-    const dim3 grid(ceil_div(n, mlp::RM)), blk(256);
-    if (row_gemm() == 2) {
-        if (N == 512) hipLaunchKernelGGL((mlp::gemm_row<16, 4, 4, EPI>), grid, blk, 0, s, a);
-        else hipLaunchKernelGGL((mlp::gemm_row<16, 4, 2, EPI>), grid, blk, 0, s, a);
-    } else {
-        if (N == 512) hipLaunchKernelGGL((mlp::gemm_row<32, 2, 4, EPI>), grid, blk, 0, s, a);
-        else hipLaunchKernelGGL((mlp::gemm_row<32, 2, 2, EPI>), grid, blk, 0, s, a);
-    }
-}
-inline int lnf_variant() {
-    static const int v = env_int("RLGPU_LNF_VARIANT", 0);
-    return v;
-}
-inline int lnb_variant() {
-    static const int v = env_int("RLGPU_LNB_VARIANT", 0);
-    return v;
-}
 inline bool split_mode_(int mode) { return mode == RLGPU_GEMM_F32X6 || mode == RLGPU_GEMM_F16X3; }
 inline int gemm_slots(int mode) {
-    // H3 variant 0: 146 / 156 VGPRs (forward / weight-gradient instances), 40 KB LDS -> three
-    // workgroups per CU (-Rpass-analysis=kernel-resource-usage: occupancy 3 waves / SIMD)
-    if (mode == RLGPU_GEMM_F16X3) return g_cus * (h3_variant() == 0 ? 3 : (h3_variant() >= 3 ? 2 : 1));
-    return g_cus * (split_mode_(mode) ? x6_occ() : RLGPU_GEMM_OCC);
+    // H3: 146 / 156 VGPRs (forward / weight-gradient instances), 40 KB LDS -> three workgroups per CU
+    // (-Rpass-analysis=kernel-resource-usage: occupancy 3 waves / SIMD); x6: two
+    if (mode == RLGPU_GEMM_F16X3) return g_cus * 3;
+    return g_cus * (split_mode_(mode) ? 2 : RLGPU_GEMM_OCC);
 }
 // K granularity of a split-K chunk: a whole number of stages of either kernel
 inline int kgran(int mode) { return split_mode_(mode) ? mlp::XKMAX : mlp::BK; }
@@ -282,51 +202,7 @@ struct Span {
 // zero-padded up to a multiple of 4 past the bound (so float4 loads may straddle it).
 template <int LA, int LB, bool AV, bool BV, bool PRE, bool H3>
 void x6_launch_v(dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
-    switch (H3 ? h3_variant() : x6_variant()) {
-        case 3: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 3, H3>), grid, blk, 0, s, g); break;
-        case 4:
-            if (H3) {  // two-plane LDS only: 2 x 80 KB per CU
-                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 4, true>), grid, blk, 0, s, g);
-                break;
-            }
-            [[fallthrough]];
-        case 5:
-            if (H3) {
-                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 5, true>), grid, blk, 0, s, g);
-                break;
-            }
-            [[fallthrough]];
-        case 6:
-            if (H3) {
-                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 6, true>), grid, blk, 0, s, g);
-                break;
-            }
-            [[fallthrough]];
-        case 12:
-            if (H3) {
-                hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 12, true>), grid, blk, 0, s, g);
-                break;
-            }
-            [[fallthrough]];
-        case 7:
-        case 8:
-        case 9:
-        case 10:
-        case 11:  // timing ablations (garbage results): RLGPU_H3_VARIANT=7/8/9 in microbenchmarks only
-            if (H3 && PRE) {
-                const int v = h3_variant();
-                if (v == 7) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 7, true>), grid, blk, 0, s, g);
-                if (v == 8) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 8, true>), grid, blk, 0, s, g);
-                if (v == 9) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 9, true>), grid, blk, 0, s, g);
-                if (v == 10) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 10, true>), grid, blk, 0, s, g);
-                if (v == 11) hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 11, true>), grid, blk, 0, s, g);
-                break;
-            }
-            [[fallthrough]];
-        case 1: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 1, H3>), grid, blk, 0, s, g); break;
-        case 2: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 2, H3>), grid, blk, 0, s, g); break;
-        default: hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, 0, H3>), grid, blk, 0, s, g); break;
-    }
+    hipLaunchKernelGGL((mlp::gemm_x6<LA, LB, AV, BV, PRE, H3>), grid, blk, 0, s, g);
 }
 template <int LA, int LB, bool H3>
 void x6_launch(bool av, bool bv, dim3 grid, dim3 blk, hipStream_t s, const mlp::GemmArgs& g) {
@@ -367,7 +243,7 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
     g.gy = (int)ceil_div(I, mlp::BM);
     g.gz = z;
     if (mode == RLGPU_GEMM_F16X3 && la == mlp::A_KI && lb == mlp::B_KJ && I % mlp::BQ == 0 && h3_quad(J)) {
-        // 256 x 256 tiles, the same split-K chunks (same bits as gemm_h3w / gemm_x6)
+        // 256 x 256 tiles, the same split-K chunks (same bits as gemm_x6)
         g.gx = J / mlp::BQ;
         g.gy = I / mlp::BQ;
         dim3 gridq(g.gx * g.gy * g.gz), blkq(512);
@@ -375,16 +251,6 @@ void gemm_f32(int mode, int la, int lb, const float* A, int64_t lda, const float
         else if (av) hipLaunchKernelGGL((mlp::gemm_h3qt<true, false>), gridq, blkq, 0, s, g);
         else if (bv) hipLaunchKernelGGL((mlp::gemm_h3qt<false, true>), gridq, blkq, 0, s, g);
         else hipLaunchKernelGGL((mlp::gemm_h3qt<false, false>), gridq, blkq, 0, s, g);
-        RLGPU_CHECK_HIP(hipGetLastError());
-        return;
-    }
-    if (mode == RLGPU_GEMM_F16X3 && la == mlp::A_KI && lb == mlp::B_KJ && h3_wide(J)) {
-        g.gx = (int)ceil_div(J, mlp::BNW);
-        dim3 gridw(g.gx * g.gy * g.gz), blkw(256);
-        if (av && bv) hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, true, true, false>), gridw, blkw, 0, s, g);
-        else if (av) hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, true, false, false>), gridw, blkw, 0, s, g);
-        else if (bv) hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, false, true, false>), gridw, blkw, 0, s, g);
-        else hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_KI, mlp::B_KJ, false, false, false>), gridw, blkw, 0, s, g);
         RLGPU_CHECK_HIP(hipGetLastError());
         return;
     }
@@ -446,25 +312,8 @@ void gemm_x6_pre(const float* A, int64_t lda, const uint16_t* Bp, int ldbp, int6
         RLGPU_CHECK_HIP(hipGetLastError());
         return;
     }
-    if (h3 && h3_wide(J)) {  // planes padded to a multiple of BNW rows (build_model)
-        g.gx = (int)ceil_div(J, mlp::BNW);
-        dim3 gridw(g.gx * g.gy);
-        if (av)
-            hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_IK, mlp::B_JK, true, true, true>), gridw, dim3(256), 0, s, g);
-        else
-            hipLaunchKernelGGL((mlp::gemm_h3w<mlp::A_IK, mlp::B_JK, false, true, true>), gridw, dim3(256), 0, s, g);
-        RLGPU_CHECK_HIP(hipGetLastError());
-        return;
-    }
     dim3 grid(g.gx * g.gy), blk(256);
-    if (h3 && av && h3_ring() != 0) {  // LDS-DMA ring kernel (bit-identical to gemm_x6's H3 path)
-        switch (h3_ring()) {
-            case 2: hipLaunchKernelGGL((mlp::gemm_h3r<64, 2>), grid, blk, 0, s, g); break;
-            case 3: hipLaunchKernelGGL((mlp::gemm_h3r<32, 3>), grid, blk, 0, s, g); break;
-            case 4: hipLaunchKernelGGL((mlp::gemm_h3r<32, 2>), grid, blk, 0, s, g); break;
-            default: hipLaunchKernelGGL((mlp::gemm_h3r<32, 4>), grid, blk, 0, s, g); break;
-        }
-    } else if (h3) {
+    if (h3) {
         if (av)
             x6_launch_v<mlp::A_IK, mlp::B_JK, true, true, true, true>(grid, blk, s, g);
         else
@@ -512,7 +361,9 @@ void split_weights(const float* P, Model& m, hipStream_t s) {
 // split-K count of a weight gradient [out, in] over `rows`: one full round of workgroups
 // (tiles x splits ~ gemm_slots), each split at least 4 K steps
 int splits_for(int mode, int rows, int out, int in) {
-    const int bn = (mode == RLGPU_GEMM_F16X3 && h3_wide(in)) ? mlp::BNW : mlp::BN;
+    // H3 weight gradients of 1024 or more columns: counted in 128 x 256 blocks (the chunking gemm_h3qt's
+    // 256 x 256 tiles were tuned with, profiles/r05ad_h3_quad_ab.txt)
+    const int bn = (mode == RLGPU_GEMM_F16X3 && in >= 1024) ? mlp::BNW : mlp::BN;
     const int tiles = (int)(ceil_div(out, mlp::BM) * ceil_div(in, bn));
     int s = gemm_slots(mode) / tiles;
     const int maxs = rows / (4 * mlp::BK);
@@ -675,41 +526,6 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
         const float* gg = L.g >= 0 ? P + L.g : nullptr;
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool fuse = head1 && l == nh - 1;
-        // the full-row kernel: Linear + LayerNorm + LeakyReLU in one pass (row_gemm.hpp)
-        if (row_gemm() && m.mode == RLGPU_GEMM_F16X3 && L.sf >= 0 && gg && !fuse && (L.out == 512 || L.out == 256) &&
-            ld % 4 == 0 && (L.in % 4 == 0 || tail_ok)) {
-            mlp::RowArgs a{};
-            a.A = in;
-            a.lda = ld;
-            a.B = m.wsplit + L.sf;
-            a.ldb = L.sf_ld;
-            a.bplane = (int64_t)L.sf_rows * L.sf_ld;
-            a.bscale = wscale_at(m, L.sfs);
-            a.amax_a = in_amax;
-            a.bias = P + L.b;
-            a.C = m.xhat[l];
-            a.ldc = L.out;
-            a.I = n;
-            a.N = L.out;
-            a.K = L.in;
-            a.gamma = gg;
-            a.beta = bb;
-            a.slope = h->cfg.leaky_slope;
-            a.act = m.act[l];
-            a.stats = reinterpret_cast<float2*>(m.rstd[l]);
-            a.amax_out = amax_slot(m, l);
-            {
-                // flops of the GEMM (the LayerNorm's bytes ride along in the same launch)
-                ktime::Span span(ktime::FWD_GEMM, 2.0 * n * (double)L.out * L.in, s);
-                launch_row<mlp::ROW_LN>(L.out, n, s, a);
-                RLGPU_CHECK_HIP(hipGetLastError());
-            }
-            in = m.act[l];
-            in_amax = amax_slot(m, l);
-            ld = L.out;
-            tail_ok = false;
-            continue;
-        }
         if (L.sf >= 0)
             gemm_x6_pre(in, ld, m.wsplit + L.sf, L.sf_ld, (int64_t)L.sf_rows * L.sf_ld, m.xhat[l], L.out, P + L.b, n, L.out,
                         L.in, s, tail_ok, in_amax, wscale_at(m, L.sfs));
@@ -719,7 +535,7 @@ void forward_train(rlgpu_ppo* h, int mi, const Input& x, int n, float* out, hipS
         // bytes: z read, act written, (mean, rstd) written
         ktime::Span span(ktime::LN_FWD, (double)n * (8.0 * L.out + 8.0), s);
         int lnf_rows = 0;
-        const auto lnf = mlp::ln_act_fwd_f32_pick(L.out, lnf_variant(), &lnf_rows, fuse);
+        const auto lnf = mlp::ln_act_fwd_f32_pick(L.out, &lnf_rows, fuse);
         hipLaunchKernelGGL(lnf, dim3(ceil_div(n, lnf_rows)), dim3(256), 0, s, m.xhat[l], gg, bb, n, L.out,
                            h->cfg.leaky_slope, h->cfg.layer_norm, m.act[l], reinterpret_cast<float2*>(m.rstd[l]),
                            amax_slot(m, l), fuse ? P + O->w : nullptr, fuse ? P + O->b : nullptr, fuse ? out : nullptr);
@@ -761,52 +577,10 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
     const float* dA_top = m.dA;  // gradient of the last hidden layer's activation
     bool rank1 = false;          // rank-1 output layer folded into the last LayerNorm backward
     // the pass's bias / LayerNorm / weight-gradient reductions, launched together at its end
-    // (RLGPU_BATCH_REDUCE=0: each right after its producer, as before)
-    static const bool batch = [] {
-        const char* e = getenv("RLGPU_BATCH_REDUCE");
-        return !(e && e[0] == '0');
-    }();
     Reducer red;
     red.m = &m;
-    Reducer* R = batch ? &red : nullptr;
+    Reducer* R = &red;
     const Layer* O = m.head_only ? nullptr : &m.L[nh];
-    // The full-row input-gradient GEMM with hidden layer l's LayerNorm backward in its epilogue (row_gemm.hpp
-    // ROW_LNB): dA of layer l = A . src^T (src: the layer above, its pre-split transposed planes), then dZ_l into
-    // dst and layer l's column partials.  fusedDZ[l]: where dZ_l went (the fused layers ping-pong between m.dZ
-    // and m.dA, which the fused path no longer needs).
-    std::vector<float*> fusedDZ((size_t)std::max(nh, 1), nullptr);
-    auto row_lnb_ok = [&](int l, const Layer& src, int64_t lda) {
-        const Layer& L = m.L[l];
-        return row_gemm() && m.mode == RLGPU_GEMM_F16X3 && src.sb >= 0 && L.g >= 0 && L.be >= 0 &&
-               (L.out == 512 || L.out == 256) && lda % 4 == 0;
-    };
-    auto launch_lnb = [&](int l, const float* A, int64_t lda, const float* a_amax, const Layer& src, float* dst) {
-        const Layer& L = m.L[l];
-        mlp::RowArgs a{};
-        a.A = A;
-        a.lda = lda;
-        a.B = m.wsplit + src.sb;
-        a.ldb = src.sb_ld;
-        a.bplane = (int64_t)src.sb_rows * src.sb_ld;
-        a.bscale = wscale_at(m, src.sbs);
-        a.amax_a = a_amax;
-        a.C = dst;
-        a.ldc = L.out;
-        a.I = n;
-        a.N = L.out;
-        a.K = src.out;
-        a.gamma = P + L.g;
-        a.beta = P + L.be;
-        a.slope = h->cfg.leaky_slope;
-        a.stats = reinterpret_cast<float2*>(m.rstd[l]);
-        a.amax_out = amax_slot(m, kAmaxDZ + l);
-        a.Z = m.xhat[l];
-        a.part = m.cpart_l[l];
-        ktime::Span span(ktime::FWD_GEMM, 2.0 * n * (double)L.out * src.out, s);
-        launch_row<mlp::ROW_LNB>(L.out, n, s, a);
-        RLGPU_CHECK_HIP(hipGetLastError());
-        fusedDZ[l] = dst;
-    };
     if (!O) {
         dA_top = dout;
     } else if (O->out == 1 && nh == 0) {  // rank-1 head on the input: dA = dv w^T, dw / db partials in one pass
@@ -830,19 +604,15 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         const Input a = nh > 0 ? Input{m.act[nh - 1], O->in, amax_slot(m, nh - 1), false} : x;
         weight_grad(m, dout, O->out, a.X, a.ld, O->in, n, G + O->w, s, a.tail_ok, amax_slot(m, kAmaxOut), a.amax, dld, R,
                     m.wpart_l[nh]);
-        if (dout_part && R)
+        if (dout_part)
             R->add(dout_part, dout_nblk, O->out, O->out, G + O->b, false, s);
-        else if (dout_part)
-            reduce_partials(m, dout_part, dout_nblk, O->out, O->out, G + O->b, s);
         else if (dld == O->out)
             colsum_into(m, dout, n, O->out, G + O->b, s);
         else
             throw rlgpu::Error(RLGPU_ERR_STATE, "backward: padded dout needs the loss kernel's bias partials");
         // dA = dout . W_out (into the input gradient when the output layer reads the model input)
         float* dA = nh > 0 ? m.dA : m.dX;
-        if (nh > 0 && row_lnb_ok(nh - 1, *O, dld)) {
-            launch_lnb(nh - 1, dout, dld, amax_slot(m, kAmaxOut), *O, m.dZ);
-        } else if (dA) {
+        if (dA) {
             if (O->sb >= 0)
                 gemm_x6_pre(dout, dld, m.wsplit + O->sb, O->sb_ld, (int64_t)O->sb_rows * O->sb_ld, dA, O->in, nullptr, n, O->in,
                             O->out, s, dld > O->out, amax_slot(m, kAmaxOut), wscale_at(m, O->sbs));
@@ -857,38 +627,29 @@ void backward(rlgpu_ppo* h, int mi, const Input& x, int n, const float* dout, hi
         const float* bb = L.be >= 0 ? P + L.be : nullptr;
         const bool r1 = rank1 && l == nh - 1;  // dA of the rank-1 head, recomputed in the kernel
         int lnb_rows = 0;
-        const auto lnb = mlp::ln_act_bwd_pick(L.out, r1, lnb_variant(), &lnb_rows);
+        const auto lnb = mlp::ln_act_bwd_pick(L.out, r1, &lnb_rows);
         const float* dA_in = l == nh - 1 ? dA_top : m.dA;
-        float* dz = fusedDZ[l] ? fusedDZ[l] : m.dZ;  // this layer's dZ
-        const int nb = fusedDZ[l] ? (int)ceil_div(n, mlp::RM) : (int)ceil_div(n, lnb_rows);
-        if (!fusedDZ[l]) {
-        // bytes: dA (recomputed for the rank-1 head: its dv instead), z, stats read; dZ written
-        ktime::Span span(ktime::LN_BWD, (double)n * ((r1 ? 4.0 : 4.0 * L.out) + 8.0 * L.out + 8.0), s);
-        hipLaunchKernelGGL(lnb, dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
-                           reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
-                           h->cfg.layer_norm, m.dZ, m.cpart_l[l], amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
-                           r1 ? P + O->w : nullptr, r1 ? m.hpart : nullptr);
-        RLGPU_CHECK_HIP(hipGetLastError());
+        float* dz = m.dZ;  // this layer's dZ
+        const int nb = (int)ceil_div(n, lnb_rows);
+        {
+            // bytes: dA (recomputed for the rank-1 head: its dv instead), z, stats read; dZ written
+            ktime::Span span(ktime::LN_BWD, (double)n * ((r1 ? 4.0 : 4.0 * L.out) + 8.0 * L.out + 8.0), s);
+            hipLaunchKernelGGL(lnb, dim3(nb), dim3(256), 0, s, r1 ? nullptr : dA_in, m.xhat[l],
+                               reinterpret_cast<const float2*>(m.rstd[l]), gg, bb, n, L.out, h->cfg.leaky_slope,
+                               h->cfg.layer_norm, m.dZ, m.cpart_l[l], amax_slot(m, kAmaxDZ + l), r1 ? dout : nullptr,
+                               r1 ? P + O->w : nullptr, r1 ? m.hpart : nullptr);
+            RLGPU_CHECK_HIP(hipGetLastError());
         }
         // partials [blk][dbias | dgamma | dbeta] -> flat grads [b][g][be] (contiguous after L.b); the rank-1
         // head's [w | b] are contiguous too
         int ncol = h->cfg.layer_norm ? 3 * L.out : L.out;
-        if (R) {
-            if (r1) R->add(m.hpart, nb, O->in + 1, O->in + 1, G + O->w, false, s);
-            R->add(m.cpart_l[l], nb, 3 * (int64_t)L.out, ncol, G + L.b, false, s);
-        } else {
-            if (r1) reduce_partials(m, m.hpart, nb, O->in + 1, O->in + 1, G + O->w, s);
-            reduce_partials(m, m.cpart_l[l], nb, 3 * (int64_t)L.out, ncol, G + L.b, s);
-        }
+        if (r1) R->add(m.hpart, nb, O->in + 1, O->in + 1, G + O->w, false, s);
+        R->add(m.cpart_l[l], nb, 3 * (int64_t)L.out, ncol, G + L.b, false, s);
         const Input a = l > 0 ? Input{m.act[l - 1], L.in, amax_slot(m, l - 1), false} : x;
         weight_grad(m, dz, L.out, a.X, a.ld, L.in, n, G + L.w, s, a.tail_ok, amax_slot(m, kAmaxDZ + l), a.amax, 0, R,
                     m.wpart_l[l]);
         float* dA = l > 0 ? m.dA : m.dX;  // the first layer's only when the input gradient is wanted
         if (!dA) continue;
-        if (l > 0 && row_lnb_ok(l - 1, L, L.out)) {  // layer l - 1's LayerNorm backward inside its dA GEMM
-            launch_lnb(l - 1, dz, L.out, amax_slot(m, kAmaxDZ + l), L, dz == m.dZ ? m.dA : m.dZ);
-            continue;
-        }
         if (L.sb >= 0)
             gemm_x6_pre(dz, L.out, m.wsplit + L.sb, L.sb_ld, (int64_t)L.sb_rows * L.sb_ld, dA, L.in, nullptr, n, L.in,
                         L.out, s, false, amax_slot(m, kAmaxDZ + l), wscale_at(m, L.sbs));
@@ -1527,12 +1288,9 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
         if (h->shared()) forward_train(h, 2, obs_in, n, nullptr, s);
         // the critic's pass runs on the auxiliary stream (disjoint parameters, gradients, workspace
         // and metric slots), overlapping the policy's; the caller's stream waits for both
-        static const bool serial = getenv("RLGPU_SERIAL_MINIBATCH") != nullptr;  // experiment switch
-        hipStream_t cs = serial ? s : h->aux;
-        if (!serial) {
-            RLGPU_CHECK_HIP(hipEventRecord(h->ev_fork, s));
-            RLGPU_CHECK_HIP(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-        }
+        hipStream_t cs = h->aux;
+        RLGPU_CHECK_HIP(hipEventRecord(h->ev_fork, s));
+        RLGPU_CHECK_HIP(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
         Model& pm = h->M[0];
         Model& cm = h->M[1];
         forward_train(h, 1, xin, n, cm.y, cs);
@@ -1540,7 +1298,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
                            bsr, cm.dy, d_metrics);
         RLGPU_CHECK_HIP(hipGetLastError());
         backward(h, 1, xin, n, cm.dy, cs);
-        if (!serial) RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
+        RLGPU_CHECK_HIP(hipEventRecord(h->ev_join, h->aux));
         // policy on the caller's stream
         forward_train(h, 0, xin, n, pm.y, s);
         const int pl_blocks = (int)ceil_div(n, ppo::PL_ROWS);
@@ -1549,7 +1307,7 @@ extern "C" int rlgpu_ppo_minibatch(rlgpu_ppo* h, const float* d_obs, const uint8
                            1.f / std::log((float)A), pm.dy, dout_ld(A), d_metrics, pm.lpart, amax_slot(pm, kAmaxOut));
         RLGPU_CHECK_HIP(hipGetLastError());
         backward(h, 0, xin, n, pm.dy, s, pm.lpart, pl_blocks);
-        if (!serial) RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
+        RLGPU_CHECK_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
         if (h->shared()) {  // (ppoLoss + criticLoss).backward() through the shared features (:498)
             const int64_t e = (int64_t)n * h->M[2].out;
             hipLaunchKernelGGL(ppo::add2, dim3(ceil_div(ceil_div(e, 4), 256)), dim3(256), 0, s, pm.dX, cm.dX, h->dshared, e);

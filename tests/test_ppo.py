@@ -441,26 +441,6 @@ def test_c5_minibatch_grads_match_torch(gpu):
     assert_grads_close(p.flat(grads=True).cpu(), pol, crit, rel_tol=1e-4, frac=1.0)
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(400)
-@pytest.mark.parametrize("variant", ["1", "2"])
-def test_row_gemm_option_keeps_the_gradients(gpu, variant):
-    """The full-row H3 GEMMs (RLGPU_ROW_GEMM=1 / 2, csrc/row_gemm.hpp; off by default, slower) still pass the
-    forward and minibatch-gradient tests against torch fp32: the knob is read once per process, so they run in a
-    child process with it set."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RLGPU_ROW_GEMM=variant)
-    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
-                        os.path.join(root, "tests", "test_ppo.py"), "-k",
-                        "(minibatch_grads_match_torch and h3) or forward_fp32_h3"],
-                       env=env, capture_output=True, text=True, timeout=360, cwd=root)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout
-
-
 _QUAD_CHILD = r"""
 import sys, numpy as np, torch
 sys.path[:0] = [sys.argv[2], sys.argv[2] + "/reinforcement-learning_amd", sys.argv[2] + "/tests"]
@@ -485,7 +465,7 @@ np.save(sys.argv[1], np.concatenate(out))
 def test_h3_quad_tiles_bit_identical(gpu, tmp_path):
     """The 256 x 256 tile H3 GEMM (mlp::gemm_h3q: RLGPU_H3_QUAD=1 for every width that is a multiple of 256, by
     default from 1024 columns) gives the same minibatch gradients and forward outputs, bit for bit, as the
-    128 x 128 gemm_x6 and 128 x 256 gemm_h3w paths (RLGPU_H3_QUAD=0): same products, same order into one
+    128 x 128 gemm_x6 path (RLGPU_H3_QUAD=0): same products, same order into one
     accumulator.  Row counts off the 256-row tile, widths 256 / 512 / 768 / 1024 / 2048.  The knob is read once
     per process: child processes."""
     import os
