@@ -166,53 +166,93 @@ DEV int grid_cell(float x, float o, float inv, int n) {
     return (int)f;
 }
 constexpr int kGridBatch = 4;  // grid entries whose loads are issued together
+constexpr int kGridRows = 4;   // (y, z) rows of a query walked as one sequence (more: row by row)
 // Calls f(t, v0, v1, v2, obj) once for every triangle whose AABB overlaps [qmn, qmx] (the exact
 // test of the linear scan it replaces), in no particular order.  A triangle is listed in every
 // cell its AABB touches; it is visited only from the cell max(query lo, triangle lo) per axis,
-// which lies in both cell ranges whenever the boxes overlap (grid_cell is monotone).  Entries
-// are dealt round-robin over `parts` callers.  Entries hold their triangle inline (no index
-// indirection), and kGridBatch entries' loads are issued before the first is tested: the walk is
-// latency-bound (one dependent L2 round trip per entry otherwise).
+// which lies in both cell ranges whenever the boxes overlap (grid_cell is monotone); every entry
+// carries its cell (x | y << 8 | z << 16) for that rule.  Entries hold their triangle inline (no index
+// indirection).  The walk is latency-bound (one dependent L2 round trip per batch): the cells x0..x1 of
+// one (y, z) row are one contiguous entry range, the ranges of a query's rows (up to kGridRows: a wheel
+// ray, a car or a ball at the usual cell size) are read with one round of loads and walked as one
+// sequence, kGridBatch entries' loads issued before the first is tested, batches running across row ends.
+// Entry i of the sequence goes to caller i % parts.
+template <class F>
+DEV void grid_entry(const MeshView& M, const float4 (&q)[3], v3 qmn, v3 qmx, int x0, int y0, int z0, F&& f) {
+    const v3 v0 = v3{q[0].x, q[0].y, q[0].z}, v1 = v3{q[1].x, q[1].y, q[1].z}, v2 = v3{q[2].x, q[2].y, q[2].z};
+    const int obj = __float_as_int(q[0].w), t = __float_as_int(q[1].w), cell = __float_as_int(q[2].w);
+    const v3 tmn = v3{fminf(v0.x, fminf(v1.x, v2.x)), fminf(v0.y, fminf(v1.y, v2.y)), fminf(v0.z, fminf(v1.z, v2.z))};
+    const v3 tmx = v3{fmaxf(v0.x, fmaxf(v1.x, v2.x)), fmaxf(v0.y, fmaxf(v1.y, v2.y)), fmaxf(v0.z, fmaxf(v1.z, v2.z))};
+    if (!aabb_overlap(qmn, qmx, tmn, tmx)) return;
+    const int vx = max(x0, grid_cell(tmn.x, M.ox, M.inv_cell, M.nx)), vy = max(y0, grid_cell(tmn.y, M.oy, M.inv_cell, M.ny)),
+              vz = max(z0, grid_cell(tmn.z, M.oz, M.inv_cell, M.nz));
+    if (cell != (vx | (vy << 8) | (vz << 16))) return;
+    f(t, v0, v1, v2, obj);
+}
 template <class F>
 DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& f) {
     const int x0 = grid_cell(qmn.x, M.ox, M.inv_cell, M.nx), x1 = grid_cell(qmx.x, M.ox, M.inv_cell, M.nx);
     const int y0 = grid_cell(qmn.y, M.oy, M.inv_cell, M.ny), y1 = grid_cell(qmx.y, M.oy, M.inv_cell, M.ny);
     const int z0 = grid_cell(qmn.z, M.oz, M.inv_cell, M.nz), z1 = grid_cell(qmx.z, M.oz, M.inv_cell, M.nz);
-    int seen = 0;
-    // the cells x0..x1 of one (y, z) row are consecutive, so their entries are one contiguous range
-    // (each entry carries its cell's x in v2.w for the visit-once rule)
-    for (int cz = z0; cz <= z1; cz++)
-        for (int cy = y0; cy <= y1; cy++) {
-            const int row = (cz * M.ny + cy) * M.nx;
-            const int b = M.cell_start[row + x0], e = M.cell_start[row + x1 + 1];
-            int k = b + ((part - seen % parts) + parts) % parts;
-            seen += e - b;
-            for (; k < e; k += kGridBatch * parts) {
-                float4 q[kGridBatch][3];
+    const int nyr = y1 - y0 + 1, nrows = nyr * (z1 - z0 + 1);
+    if (nrows > kGridRows) {  // a larger query: row by row, the sequence numbering continued across rows
+        int seen = 0;
+        for (int cz = z0; cz <= z1; cz++)
+            for (int cy = y0; cy <= y1; cy++) {
+                const int row = (cz * M.ny + cy) * M.nx;
+                const int b = M.cell_start[row + x0], e = M.cell_start[row + x1 + 1];
+                int k = b + ((part - seen % parts) + parts) % parts;
+                seen += e - b;
+                for (; k < e; k += kGridBatch * parts) {
+                    float4 q[kGridBatch][3];
 #pragma unroll
-                for (int j = 0; j < kGridBatch; j++) {  // past the range's end: the last entry again (not visited)
-                    const float4* p = M.cell_tri + 3 * (size_t)min(k + j * parts, e - 1);
-                    q[j][0] = p[0];
-                    q[j][1] = p[1];
-                    q[j][2] = p[2];
-                }
+                    for (int j = 0; j < kGridBatch; j++) {  // past the range's end: the last entry again (not visited)
+                        const float4* p = M.cell_tri + 3 * (size_t)min(k + j * parts, e - 1);
+                        q[j][0] = p[0];
+                        q[j][1] = p[1];
+                        q[j][2] = p[2];
+                    }
 #pragma unroll
-                for (int j = 0; j < kGridBatch; j++) {
-                    if (k + j * parts >= e) break;
-                    const v3 v0 = v3{q[j][0].x, q[j][0].y, q[j][0].z}, v1 = v3{q[j][1].x, q[j][1].y, q[j][1].z},
-                             v2 = v3{q[j][2].x, q[j][2].y, q[j][2].z};
-                    const int obj = __float_as_int(q[j][0].w), t = __float_as_int(q[j][1].w), cx = __float_as_int(q[j][2].w);
-                    const v3 tmn = v3{fminf(v0.x, fminf(v1.x, v2.x)), fminf(v0.y, fminf(v1.y, v2.y)), fminf(v0.z, fminf(v1.z, v2.z))};
-                    const v3 tmx = v3{fmaxf(v0.x, fmaxf(v1.x, v2.x)), fmaxf(v0.y, fmaxf(v1.y, v2.y)), fmaxf(v0.z, fmaxf(v1.z, v2.z))};
-                    if (!aabb_overlap(qmn, qmx, tmn, tmx)) continue;
-                    if (cx != max(x0, grid_cell(tmn.x, M.ox, M.inv_cell, M.nx)) ||
-                        cy != max(y0, grid_cell(tmn.y, M.oy, M.inv_cell, M.ny)) ||
-                        cz != max(z0, grid_cell(tmn.z, M.oz, M.inv_cell, M.nz)))
-                        continue;
-                    f(t, v0, v1, v2, obj);
+                    for (int j = 0; j < kGridBatch; j++) {
+                        if (k + j * parts >= e) break;
+                        grid_entry(M, q[j], qmn, qmx, x0, y0, z0, f);
+                    }
                 }
             }
+        return;
+    }
+    // the rows' entry ranges, all loads issued together; c[r] = entries before row r in the sequence
+    int b[kGridRows], c[kGridRows + 1];
+    c[0] = 0;
+#pragma unroll
+    for (int r = 0; r < kGridRows; r++) {
+        const bool live = r < nrows;
+        const int rr = live ? r : 0;
+        const int row = ((z0 + rr / nyr) * M.ny + (y0 + rr % nyr)) * M.nx;
+        const int bb = M.cell_start[row + x0], ee = M.cell_start[row + x1 + 1];
+        b[r] = bb;
+        c[r + 1] = c[r] + (live ? ee - bb : 0);
+    }
+    const int total = c[kGridRows];
+    for (int i = part; i < total; i += kGridBatch * parts) {
+        float4 q[kGridBatch][3];
+#pragma unroll
+        for (int j = 0; j < kGridBatch; j++) {  // past the sequence's end: its last entry again (not visited)
+            const int s = min(i + j * parts, total - 1);
+            int e = b[0] + s;
+#pragma unroll
+            for (int r = 1; r < kGridRows; r++) e = s >= c[r] ? b[r] + (s - c[r]) : e;
+            const float4* p = M.cell_tri + 3 * (size_t)e;
+            q[j][0] = p[0];
+            q[j][1] = p[1];
+            q[j][2] = p[2];
         }
+#pragma unroll
+        for (int j = 0; j < kGridBatch; j++) {
+            if (i + j * parts >= total) break;
+            grid_entry(M, q[j], qmn, qmx, x0, y0, z0, f);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ ray cast (btCollisionWorld::rayTest)

@@ -160,7 +160,8 @@ MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_
                         for (int a = 0; a < 3; a++) d[v * 4 + a] = p[v * 3 + a];
                     std::memcpy(&d[3], &obj[t], sizeof(int));
                     std::memcpy(&d[7], &t, sizeof(int));
-                    std::memcpy(&d[11], &x, sizeof(int));
+                    const int cell = x | (y << 8) | (z << 16);  // the entry's cell (dims <= 128 per axis)
+                    std::memcpy(&d[11], &cell, sizeof(int));
                 }
     }
     g.tri.assign((size_t)ntris * 12, 0.f);
