@@ -20,7 +20,7 @@
 // communicator (host/rccl_collective.cpp).
 //
 //   rlgpu_train [--iterations N] [--arenas A] [--rollout T] [--trajectories] [--f32-gemm] [--c2-model] [--seed S]
-//               [--checkpoint-folder DIR [--ts-per-save N] [--resave-to DIR2]] [--self-play]
+//               [--checkpoint-folder DIR [--ts-per-save N] [--resave-to DIR2]] [--self-play] [--fp32-inference]
 //               [--rank r --world N --rccl-id FILE [--rccl-nonce STR]]
 #include <execinfo.h>
 #include <signal.h>
@@ -167,6 +167,7 @@ int main(int argc, char** argv) {
             else if (!std::strcmp(argv[i], "--ts-per-save")) cfg.tsPerSave = std::atoll(next());
             else if (!std::strcmp(argv[i], "--resave-to")) resaveTo = next();
             else if (!std::strcmp(argv[i], "--self-play")) cfg.trainAgainstOldVersions = true;
+            else if (!std::strcmp(argv[i], "--fp32-inference")) cfg.ppo.useHalfPrecision = false;
             else if (!std::strcmp(argv[i], "--rank")) opt.rank = std::atoi(next());
             else if (!std::strcmp(argv[i], "--world")) opt.world = std::atoi(next());
             else if (!std::strcmp(argv[i], "--rccl-id")) idFile = next();
@@ -180,7 +181,7 @@ int main(int argc, char** argv) {
         } catch (const std::exception& e) {
             std::fprintf(stderr, "%s\nusage: %s [--iterations N] [--arenas A] [--rollout T] [--trajectories] [--f32-gemm] "
                                  "[--c2-model] [--seed S] [--checkpoint-folder DIR [--ts-per-save N] [--resave-to DIR2]] "
-                                 "[--self-play] [--rank r --world N --rccl-id FILE]\n", e.what(), argv[0]);
+                                 "[--self-play] [--fp32-inference] [--rank r --world N --rccl-id FILE]\n", e.what(), argv[0]);
             return 2;
         }
     }

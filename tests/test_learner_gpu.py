@@ -45,6 +45,23 @@ def test_rollout_buffer_matches_oracle_env(gpu):
     assert (terms == 2).any()
 
 
+def test_fp32_inference_rollout_actions(gpu):
+    """useHalfPrecision = false in the C++ Learner (LearnerConfig(infer_fp16=2)): every collected action and log
+    prob is the oracle sampler's draw on the policy's fp32 logits of that step's obs (the training forward,
+    rlgpu_ppo_forward precision 0), with the sampler's (seed, row, step) counter."""
+    import torch
+    L = _learner(gpu, infer_fp16=2, rollout_len=6, train_against_old_versions=False)
+    step0 = L._stats().rng_step
+    L.collect()
+    torch.cuda.synchronize()
+    acts, logp, masks = L.actions.cpu().numpy(), L.logp.cpu().numpy(), L.masks.cpu().numpy()
+    for t in range(L.T):
+        logits = L.ppo.forward(0, L.obs[t]).cpu().numpy()
+        wa, wlp = oracle.sample_actions(logits, masks[t], False, L.cfg.seed, step0 + t, 0)
+        np.testing.assert_array_equal(acts[t], wa, err_msg=f"t={t}")
+        np.testing.assert_array_equal(logp[t].view(np.uint32), wlp.view(np.uint32), err_msg=f"t={t}")
+
+
 def test_consume_gae_matches_oracle(gpu):
     import torch
     L = _learner(gpu)

@@ -80,3 +80,16 @@ def test_rlgpu_train_checkpoint_round_trip(gpu, tmp_path):
     o, c = L.ppo.model_range(0)
     assert torch.equal(L.ppo.params[o:o + c].cpu(), pol)
     L.close()
+
+
+@pytest.mark.gpu
+def test_rlgpu_train_fp32_inference(gpu):
+    """PPOLearnerConfig::useHalfPrecision = false through the trainer facade (rlgpu_train --fp32-inference): the
+    Learner runs its inference on the fp32 training forward (RLGPU_INFER_F32) and trains; with self-play the
+    config is refused by name (old versions are 16-bit copies only)."""
+    args = ["--arenas", "16", "--rollout", "8", "--seed", "3", "--c2-model", "--fp32-inference"]
+    r = subprocess.run([TRAIN, *args, "--iterations", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run([TRAIN, *args, "--iterations", "1", "--self-play"], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "useHalfPrecision" in r.stdout + r.stderr, r.stdout + r.stderr
