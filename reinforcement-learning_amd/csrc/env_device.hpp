@@ -592,14 +592,16 @@ DEV v3 upwards_dir_from_wheels(ArenaLDS* A, int ci) {
     return safe_normalized(sum);
 }
 
-// Car::_UpdateWheels (Car.cpp:330-475)
-DEV void update_wheels(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
+// Car::_UpdateWheels (Car.cpp:330-475), in three parts so that the per-wheel friction runs one wheel per lane:
+// update_wheels_pre (the car's lane: handbrake, throttle / brake, engine and brake forces, steer; the throttle
+// for the friction lanes into A->a.real_throttle), wheel_friction (lane 4 car + wheel: the wheel's lateral and
+// longitudinal friction, the loop body of Car.cpp's per-wheel loop, same operations) and update_wheels_post (the
+// car's lane: the world-contact sticky force).  Every wheel's values depend only on the car state the pre part
+// leaves and on its own wheel, so the split gives the sequential loop's bits.
+DEV void update_wheels_pre(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
     rlgpu_car& cs = A->s.cars[ci];
-    int bi = ci + 1;
     const float* ctl = cs.controls;
     float abs_fwd = fabsf(fwd_speed);
-    bool world_contact = false;
-    for (int i = 0; i < 4; i++) world_contact |= A->u.wt[ci * 4 + i].contact_world != 0;
     if (ctl[7] != 0.f)
         cs.handbrake_val += 5.f * kTick;
     else
@@ -640,39 +642,48 @@ DEV void update_wheels(ArenaLDS* A, int ci, int nwc, float fwd_speed) {
         cs.wheel_steer[0] = steer;
         cs.wheel_steer[1] = steer;
     }
+    A->a.real_throttle[ci] = real_throttle;
+}
+DEV void wheel_friction(ArenaLDS* A, int ci, int i) {
+    rlgpu_car& cs = A->s.cars[ci];
+    const int bi = ci + 1;
+    WheelT& W = A->u.wt[ci * 4 + i];
+    if (W.ground < 0) return;
+    const float real_throttle = A->a.real_throttle[ci];
     v3 P = bpos(A, bi), Vv = bvel(A, bi), Av = bang(A, bi);
-    for (int i = 0; i < 4; i++) {
-        WheelT& W = A->u.wt[ci * 4 + i];
-        if (W.ground >= 0) {
-            v3 lat_dir = W.wt_col1;
-            v3 long_dir = cross(lat_dir, W.contact_normal);
-            float fin = 0;
-            v3 delta = W.hard_point - P;
-            v3 cv = (cross(Av, delta) + Vv) * kBT2UU;
-            float base = fabsf(dot(cv, lat_dir));
-            if (base > 5) fin = base / (fabsf(dot(cv, long_dir)) + base);
-            float lat = curve_out<kLatFriction>(fin);
-            float lon = curve_out<kLongFriction>(fin);
-            if (cs.handbrake_val != 0.f) {
-                float hb = cs.handbrake_val;
-                lat *= (curve_out<kHbLat>(fin) - 1) * hb + 1;
-                lon *= (curve_out<kHbLong>(fin) - 1) * hb + 1;
-            } else {
-                lon = 1;
-            }
-            bool sticky = real_throttle != 0;
-            if (!sticky) {
-                float ns = curve_out<kNonSticky>(W.contact_normal.z);
-                lat *= ns;
-                lon *= ns;
-            }
-            cs.wheel_lat_friction[i] = lat;
-            cs.wheel_long_friction[i] = lon;
-        }
+    v3 lat_dir = W.wt_col1;
+    v3 long_dir = cross(lat_dir, W.contact_normal);
+    float fin = 0;
+    v3 delta = W.hard_point - P;
+    v3 cv = (cross(Av, delta) + Vv) * kBT2UU;
+    float base = fabsf(dot(cv, lat_dir));
+    if (base > 5) fin = base / (fabsf(dot(cv, long_dir)) + base);
+    float lat = curve_out<kLatFriction>(fin);
+    float lon = curve_out<kLongFriction>(fin);
+    if (cs.handbrake_val != 0.f) {
+        float hb = cs.handbrake_val;
+        lat *= (curve_out<kHbLat>(fin) - 1) * hb + 1;
+        lon *= (curve_out<kHbLong>(fin) - 1) * hb + 1;
+    } else {
+        lon = 1;
     }
+    bool sticky = real_throttle != 0;
+    if (!sticky) {
+        float ns = curve_out<kNonSticky>(W.contact_normal.z);
+        lat *= ns;
+        lon *= ns;
+    }
+    cs.wheel_lat_friction[i] = lat;
+    cs.wheel_long_friction[i] = lon;
+}
+DEV void update_wheels_post(ArenaLDS* A, int ci, float fwd_speed) {
+    int bi = ci + 1;
+    bool world_contact = false;
+    for (int i = 0; i < 4; i++) world_contact |= A->u.wt[ci * 4 + i].contact_world != 0;
     if (world_contact) {
+        const float real_throttle = A->a.real_throttle[ci];
         v3 up = upwards_dir_from_wheels(A, ci);
-        bool full = (real_throttle != 0) || (abs_fwd > 25.f);
+        bool full = (real_throttle != 0) || (fabsf(fwd_speed) > 25.f);
         float scale = 0.5f;
         if (full) scale += 1 - fabsf(up.z);
         add_force(A, bi, up * scale * (-650.f * kUU2BT) * kCarMass);
@@ -905,7 +916,22 @@ DEV void update_auto_roll(ArenaLDS* A, int ci, int nwc) {
     add_torque(A, bi, inverse(A->a.iiw[bi]) * (tf + tr) * 80.f);
 }
 
-// Car::_PreTickUpdate after the wheel phase (Car.cpp:86-131 + btVehicleRL::updateVehicleSecond)
+// Car::_PreTickUpdate after the wheel phase (Car.cpp:86-131 + btVehicleRL::updateVehicleSecond), in two parts
+// around the per-wheel friction lanes (wheel_friction): car_phase_a up to _UpdateWheels' per-wheel loop, car_phase_b
+// from its world-contact force on.  The body's velocity and rotation do not change in between (the wheel forces
+// go to the force accumulator), so car_phase_b's forward speed is car_phase_a's.
+DEV float car_fwd_speed(ArenaLDS* A, int bi) { return dot(bvel(A, bi), col(brot(A, bi), 0)) * kBT2UU; }
+DEV void car_phase_a(ArenaLDS* A, int ci) {
+    rlgpu_car& cs = A->s.cars[ci];
+    if (cs.is_demoed) return;
+    int nwc = 0;
+    for (int i = 0; i < 4; i++) {
+        cs.wheel_contact[i] = (uint8_t)A->u.wt[ci * 4 + i].in_contact;
+        nwc += A->u.wt[ci * 4 + i].in_contact;
+    }
+    cs.is_on_ground = nwc >= 3;
+    update_wheels_pre(A, ci, nwc, car_fwd_speed(A, ci + 1));
+}
 DEV void car_phase(ArenaLDS* A, int ci) {
     rlgpu_car& cs = A->s.cars[ci];
     if (cs.is_demoed) return;
@@ -913,13 +939,9 @@ DEV void car_phase(ArenaLDS* A, int ci) {
     float* ctl = cs.controls;
     bool jump_pressed = ctl[5] != 0.f && cs.last_controls[5] == 0.f;
     int nwc = 0;
-    for (int i = 0; i < 4; i++) {
-        cs.wheel_contact[i] = (uint8_t)A->u.wt[ci * 4 + i].in_contact;
-        nwc += A->u.wt[ci * 4 + i].in_contact;
-    }
-    cs.is_on_ground = nwc >= 3;
-    float fwd_speed = dot(bvel(A, bi), col(brot(A, bi), 0)) * kBT2UU;
-    update_wheels(A, ci, nwc, fwd_speed);
+    for (int i = 0; i < 4; i++) nwc += A->u.wt[ci * 4 + i].in_contact;
+    float fwd_speed = car_fwd_speed(A, bi);
+    update_wheels_post(A, ci, fwd_speed);
     if (nwc < 3)
         update_air_torque(A, ci, nwc == 0);
     else

@@ -177,6 +177,7 @@ struct Aux {
     int traj_term;
     float all_rewards[4];
     int arith;     // the set's arithmetic mode (rlgpu_envset_config.arith, include/rlgpu_arith.h)
+    float real_throttle[4];  // T2: each car's Car::_UpdateWheels throttle, for its four wheels' friction lanes
 };
 
 union Scratch {
