@@ -29,13 +29,17 @@ H3_TFS = MFMA_F16_TFS / 3  # fp32 GEMM ceiling of the H3 split: three fp16 MFMAs
 ARENAS_PER_GPU = 4096   # BASELINE configs[1] (C2)
 
 
-def env_bytes_per_step(arena_state_size, append=True):
+def env_bytes_per_step(arena_state_size, append=True, output_only=True):
     """B_env = 2*S_arena + 16 (actions) + 2672 (obs) + 360 (masks) + 16 (rewards) + 1
-    (terminal); the fused step's experience append writes the obs / mask / reward / terminal rows a
-    second time into the rollout buffer (+2672 + 360 + 16 + 4)."""
+    (terminal); the fused step's experience append writes the reward / terminal-code rows into the rollout
+    buffer (+16 + 4) and the obs / mask rows a second time (+2672 + 360) -- unless the env set is output-only
+    (rlgpu_envset_set_output_only, the C++ Learner's mode since round 6): then the rollout rows are the step's
+    only obs / mask output and they are counted once."""
     b = 2 * arena_state_size + 16 + 4 * 167 * 4 + 4 * 90 + 16 + 1
     if append:
-        b += 4 * 167 * 4 + 4 * 90 + 16 + 4
+        b += 16 + 4
+        if not output_only:
+            b += 4 * 167 * 4 + 4 * 90
     return b
 
 
