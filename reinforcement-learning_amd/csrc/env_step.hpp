@@ -148,11 +148,13 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
     P.mark(0);
     if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase(A, M, l >> 2, l & 3);
     sync();
+    P.mark(1);
     wheel_casts(A - (threadIdx.x >> 4), nvalid);
     sync();
+    P.mark(30);
     if (valid && !A->s.cars[l >> 2].is_demoed) wheel_phase_b(A, l >> 2, l & 3);
     sync();
-    P.mark(1);
+    P.mark(31);
     if (valid && l < 4) car_phase_a(A, l);
     sync();
     // Car::_UpdateWheels' per-wheel friction: lane 4 car + wheel

@@ -11,10 +11,12 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "reinforcement-learning_amd")]
 from rlgpu import _lib  # noqa: E402
 from rlgpu.env import EnvSet  # noqa: E402
 
-NAMES = ["T0 sleep/demo/snapshot", "T1 wheels (16 lanes)", "T2 car logic + pads pre", "T3 gravity/predict",
+NAMES = ["T0 sleep/demo/snapshot", "T1 wheels static rays (16 lanes)", "T2 car logic + pads pre", "T3 gravity/predict",
          "T4 ball awake", "T5 narrowphase (queue GJK)", "T6 commit + solve (lane 0)", "T7 integrate", "T8 car post/finish",
          "T9 pad collide", "T10 pad post + ball finish", "prelude / halves", "builders", "obs rows", "resets", "store", "T6 commit loop", "T6 commit sort",
-         "T5 deferred EPA (wave)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T5 narrow pairs (grid walks)"]
+         "T5 deferred EPA (wave)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T5 narrow pairs (grid walks)",
+         "T1 wheel casts (wave)", "T1 wheel finish"]
+PH = list(range(23)) + [30, 31]  # the phase slots (env_kernel.hpp kProfPhases; slot 23 = penetration-solver calls)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 8  # env steps before profiling (late-episode states)
@@ -33,7 +35,7 @@ for i in range(warm):
     env.step(acts, True)
 APW = int(os.environ.get("RLGPU_ENV_APW", "4"))  # arenas per workgroup of the built library (env_kernel.hpp)
 wg = (n + APW - 1) // APW
-KP, KW = 24, 64  # env_kernel.hpp kProfPhases, kProfWG
+KP, KW = 32, 64  # env_kernel.hpp kProfPhases, kProfWG
 prof = torch.zeros(KW + wg * KP + n, dtype=torch.int64, device=dev)  # + per-arena penetration-solver calls
 spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
 L = _lib.lib()
@@ -50,7 +52,7 @@ for i in range(steps):
     e1.record()
     torch.cuda.synchronize()
     tot_ms += e0.elapsed_time(e1)
-    per = prof[KW:KW + wg * KP].view(wg, KP)[:, :23].double()
+    per = prof[KW:KW + wg * KP].view(wg, KP)[:, PH].double()
     tots = per.sum(1)
     k = int(tots.argmax())
     spread.append((tots.max().item(), tots.mean().item(), per[k].cpu(), per.mean(0).cpu()))
@@ -62,13 +64,13 @@ for i in range(steps):
     slow_arenas.append(pa[k].cpu().tolist())
     prof[KW:].zero_()
 c = prof.cpu().tolist()
-total = sum(c[:23])
+total = sum(c[k] for k in PH)
 print(f"{n} arenas, {steps} steps, {mesh_name} mesh, {tot_ms / steps:.3f} ms/step (profiled build)")
 ticks = steps * 8
 print(f"  per tick (workgroup 0, arena 0): candidates {c[24] / ticks / wg:.2f}, mode-1 ranks {c[27] / ticks / wg:.2f}, "
       f"refresh-needing ranks {c[25] / ticks / wg:.2f}, live ranks {c[26] / ticks / wg:.2f}")
-for k in range(23):
-    print(f"  {NAMES[k]:28s} {c[k] / total * 100:6.2f} %   {c[k] / wg / steps:12.0f} cycles/WG/step")
+for i, k in enumerate(PH):
+    print(f"  {NAMES[i]:28s} {c[k] / total * 100:6.2f} %   {c[k] / wg / steps:12.0f} cycles/WG/step")
 
 # The kernel ends with its slowest workgroup: per step, slowest vs mean workgroup, and where the
 # slowest one spends the difference.
@@ -77,7 +79,7 @@ mn = sum(x[1] for x in spread) / len(spread)
 print(f"  slowest workgroup per step: {mx:.0f} cycles, mean workgroup {mn:.0f} (max / mean {mx / mn:.2f})")
 slow = sum(x[2] for x in spread) / len(spread)
 mean = sum(x[3] for x in spread) / len(spread)
-order = sorted(range(23), key=lambda k: -(slow[k] - mean[k]).item())
+order = sorted(range(len(PH)), key=lambda k: -(slow[k] - mean[k]).item())
 for k in order[:8]:
     print(f"    {NAMES[k]:28s} slowest {slow[k].item():10.0f}  mean {mean[k].item():10.0f}  excess {slow[k].item() - mean[k].item():10.0f}")
 pr = np.array(pen_rows)
