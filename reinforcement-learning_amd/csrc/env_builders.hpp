@@ -84,9 +84,13 @@ DEV void build_obs_row(ArenaLDS* A, int pi, int part) {
         for (int k = 0; k < 8; k++) o[9 + k] = A->s.env.prev_action[pi][k];
         add_player_obs(o + 51, view_player(A, pi), inv, bp, bv);
     } else if (part == 1) {
+#pragma unroll
         for (int k = 0; k < RLGPU_PADS; k++) {
-            int act_idx = inv ? C.pad_map[RLGPU_PADS - k - 1] : C.pad_map[k];
-            int tim_idx = inv ? C.pad_map[k] : C.pad_map[RLGPU_PADS - k - 1];  // GameState.h:60 quirk
+            // both map entries at uniform indices (scalar loads), the player's team picks: a lane-dependent
+            // index would be a vector load from the constant bank on every pad's chain
+            const int fwd = C.pad_map[k], rev = C.pad_map[RLGPU_PADS - k - 1];
+            int act_idx = inv ? rev : fwd;
+            int tim_idx = inv ? fwd : rev;  // GameState.h:60 quirk
             bool active = A->s.pads[act_idx].is_active;
             float timer = A->s.pads[tim_idx].cooldown;
             o[17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
