@@ -339,22 +339,34 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
     }
     sync();
     P.mark(9);
-    if (valid && l == 0) {
-        for (int p = 0; p < RLGPU_PADS; p++) {  // BoostPad::_PostTickUpdate (BoostPad.cpp:88-105)
+    // BoostPad::_PostTickUpdate (BoostPad.cpp:88-105): each pad's own state on the lane that tested it (pads
+    // l, l + 16, l + 32), then the pickups' boost in pad order on the arena's lane 0 (a car may pick two pads)
+    uint64_t picked[kPadsPerLane];
+#pragma unroll
+    for (int k = 0; k < kPadsPerLane; k++) {
+        const int p = l + k * kTeam;
+        bool pick = false;
+        if (valid && p < RLGPU_PADS) {
             rlgpu_pad& pd = A->s.pads[p];
-            uint32_t lid = 0;
-            int lk = A->a.locked[p];
-            if (lk >= 0) {
-                lid = (uint32_t)(lk + 1);
-                if (pd.is_active) {
-                    rlgpu_car& cs = A->s.cars[lk];
-                    cs.boost = stdmin(cs.boost + (C.pad_big[p] ? 100.f : 12.f), 100.f);
-                    pd.is_active = 0;
-                    pd.cooldown = C.pad_big[p] ? 10.f : 4.f;
-                }
+            const int lk = A->a.locked[p];
+            if (lk >= 0 && pd.is_active) {
+                pick = true;
+                pd.is_active = 0;
+                pd.cooldown = R.rad[k] > 144.f * kUU2BT ? 10.f : 4.f;  // a big pad (pad_big: radius 208)
             }
-            pd.prev_locked_car_id = lid;
+            pd.prev_locked_car_id = lk >= 0 ? (uint32_t)(lk + 1) : 0u;
         }
+        picked[k] = __ballot(pick);
+    }
+    if (valid && l == 0) {
+        const int team = (int)(threadIdx.x >> 4);
+#pragma unroll
+        for (int k = 0; k < kPadsPerLane; k++)
+            for (uint32_t bits = (uint32_t)(picked[k] >> (16 * team)) & 0xffffu; bits; bits &= bits - 1u) {
+                const int p = __ffs(bits) - 1 + k * kTeam;
+                rlgpu_car& cs = A->s.cars[A->a.locked[p]];
+                cs.boost = stdmin(cs.boost + (C.pad_big[p] ? 100.f : 12.f), 100.f);
+            }
         rlgpu_body* b = &A->s.ball;  // Ball::_FinishPhysicsTick (Ball.cpp:112-138)
         v3 v = ld3(b->vel), w = ld3(b->angvel);
         v3 cache = ld3(A->s.ball_vel_impulse_cache);
