@@ -531,19 +531,36 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
             A->a.traj_term = tj;
         }
         sync(); P.mark(12);
-        if (valid && l < 4) {
-            const PView me = view_player(A, l);  // the other players' views are read where used
+        if (valid) {
+            // the arena's 16 lanes: lane l evaluates player l & 3's rewards r = l >> 2, + 4, + 8, ... (each reward is a
+            // pure function of the snapshot); then the player's lane sums them in list order, allRewards[i] +=
+            // out[i] * weight (EnvSet.cpp:199-222), fetching each value from the lane that computed it
+            const int pi = l & 3, q = l >> 2;
+            const PView me = view_player(A, pi);  // the other players' views are read where used
             v3 bp = ld3(A->s.ball.pos) * kBT2UU, bv = ld3(A->s.ball.vel) * kBT2UU, pbv = ld3(A->s.env.prev_ball_vel);
-            float all = 0.f;  // allRewards[i] += out[i] * weight in list order (EnvSet.cpp:199-222)
             const int nr = g.plug->nr;
-            for (int r = 0; r < nr; r++) {
-                const rlgpu_reward_spec& rs = g.plug->rw[r];
-                float o = reward_value(A, rs, l, me, bp, bv, pbv, A->a.goal != 0);
-                all += o * rs.weight;
-                if (l == 0 && g.last_rewards) g.last_rewards[(size_t)arena * nr + r] = o;
-                if (g.reward_values) g.reward_values[((size_t)arena * 4 + l) * nr + r] = o;
+            constexpr int kPer = (RLGPU_MAX_REWARDS + 3) / 4;
+            float ov[kPer];
+#pragma unroll
+            for (int k = 0; k < kPer; k++) ov[k] = 0.f;
+#pragma unroll 1
+            for (int k = 0; q + 4 * k < nr; k++) {
+                const int r = q + 4 * k;
+                const float o = reward_value(A, g.plug->rw[r], pi, me, bp, bv, pbv, A->a.goal != 0);
+#pragma unroll
+                for (int j = 0; j < kPer; j++) ov[j] = j == k ? o : ov[j];  // no run-time register index
+                if (pi == 0 && g.last_rewards) g.last_rewards[(size_t)arena * nr + r] = o;
+                if (g.reward_values) g.reward_values[((size_t)arena * 4 + pi) * nr + r] = o;
             }
-            A->a.all_rewards[l] = all;
+            float all = 0.f;
+            const int base = (int)(threadIdx.x & ~15u) + pi;
+#pragma unroll
+            for (int r = 0; r < RLGPU_MAX_REWARDS; r++) {
+                if (r >= nr) break;
+                const float o = __shfl(ov[r >> 2], base + 4 * (r & 3));
+                all += o * g.plug->rw[r].weight;
+            }
+            if (l < 4) A->a.all_rewards[l] = all;
         }
         sync(); P.mark(12);
         if (valid && l < 4) {
