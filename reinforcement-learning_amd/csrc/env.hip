@@ -190,6 +190,7 @@ static EnvConst make_env_const() {
             k.mask_ground[i] = i < ng;
             k.mask_air[i] = (i > ng && x[5] == 0);
             if (i < ng && x[0] == x[6] && ((x[3] != 0) == (x[7] != 0))) k.mask_air[i] = 1;
+            k.mask_bits[i] = (uint8_t)(k.mask_ground[i] | k.mask_air[i] << 1 | k.mask_jump[i] << 2 | k.mask_boost[i] << 3);
         }
     }
     return k;

@@ -64,55 +64,62 @@ DEV void add_player_obs(float* o, const PView& pl, bool inv, v3 bp, v3 bv) {
     o[28] = pl.has_jumped ? 1.0f : 0.0f;
 }
 
-// AdvancedObs::BuildObs + DefaultAction::GetActionMask for player pi, into LDS rows
-// One quarter of player pi's AdvancedObs row and action mask (AdvancedObs.cpp, DefaultAction masks), so
-// that the arena's 16 lanes build its 4 rows together: part 0 the ball, previous action and self block,
-// part 1 the boost pads, part 2 the teammate and the first opponent, part 3 the second opponent and the
-// mask.  Every element is the same expression as in a whole-row build; only the lane that writes it differs.
-DEV void build_obs_row(ArenaLDS* A, int pi, int part) {
-    // player views are read from LDS where used: an array of them indexed by the lane's player
-    // would live in private (scratch) memory
-    const bool inv = pi & 1;  // the player's team (orange = index & 1)
-    float* o = A->u.out.obs[pi];
-    v3 bp = inv_if(ld3(A->s.ball.pos) * kBT2UU, inv), bv = inv_if(ld3(A->s.ball.vel) * kBT2UU, inv);
-    if (part == 0) {
-        const v3 ba = inv_if(ld3(A->s.ball.angvel), inv);
-        const float BPOS = 1 / 5000.f, BVEL = 1 / 2300.f, BANG = 1 / 3.f;  // AdvancedObs.h:10-13
-        o[0] = bp.x * BPOS; o[1] = bp.y * BPOS; o[2] = bp.z * BPOS;
-        o[3] = bv.x * BVEL; o[4] = bv.y * BVEL; o[5] = bv.z * BVEL;
-        o[6] = ba.x * BANG; o[7] = ba.y * BANG; o[8] = ba.z * BANG;
-        for (int k = 0; k < 8; k++) o[9 + k] = A->s.env.prev_action[pi][k];
-        add_player_obs(o + 51, view_player(A, pi), inv, bp, bv);
-    } else if (part == 1) {
+// AdvancedObs::BuildObs + DefaultAction::GetActionMask of the arena's 4 players into LDS rows, on its 16 lanes with
+// one code path (AdvancedObs.cpp, DefaultAction masks): the 29-float player blocks of every row on lanes 4 j + pi
+// (j: self, teammate, first opponent, second opponent), then the ball / previous-action, boost-pad and mask
+// elements dealt over the lanes.  Every element is the same expression as in a per-player build; only the lane
+// that writes it differs.
+DEV void build_obs_rows(ArenaLDS* A, int l) {
+    {
+        const int pi = l & 3, j = l >> 2;
+        const bool inv = pi & 1;  // the player's team (orange = index & 1)
+        const v3 bp = inv_if(ld3(A->s.ball.pos) * kBT2UU, inv), bv = inv_if(ld3(A->s.ball.vel) * kBT2UU, inv);
+        const int opp = (pi & 1) ^ 1;  // the first opponent: the other team's lower index
+        const int who = j == 0 ? pi : (j == 1 ? pi ^ 2 : (j == 2 ? opp : opp + 2));
+        add_player_obs(A->u.out.obs[pi] + 51 + 29 * j, view_player(A, who), inv, bp, bv);
+    }
+    // ball (AdvancedObs.h:10-13 scales) and previous action: 4 x 17 elements
+    for (int e = l; e < 4 * 17; e += kTeam) {
+        const int p = e / 17, k = e - 17 * (e / 17);
+        float* o = A->u.out.obs[p];
+        if (k < 9) {
+            const int w = k / 3, c = k - 3 * (k / 3);  // w: position, velocity, angular velocity
+            const float* src = w == 0 ? A->s.ball.pos : (w == 1 ? A->s.ball.vel : A->s.ball.angvel);
+            float x = w < 2 ? src[c] * kBT2UU : src[c];
+            if ((p & 1) && c < 2) x = -x;  // inv_if
+            const float sc = w == 0 ? 1 / 5000.f : (w == 1 ? 1 / 2300.f : 1 / 3.f);
+            o[k] = x * sc;
+        } else {
+            o[k] = A->s.env.prev_action[p][k - 9];
+        }
+    }
+    // boost pads: 4 x 34 elements
+    for (int e = l; e < 4 * RLGPU_PADS; e += kTeam) {
+        const int p = e / RLGPU_PADS, k = e - RLGPU_PADS * (e / RLGPU_PADS);
+        const bool inv = p & 1;
+        const int fwd = C.pad_map[k], rev = C.pad_map[RLGPU_PADS - k - 1];
+        const int act_idx = inv ? rev : fwd;
+        const int tim_idx = inv ? fwd : rev;  // GameState.h:60 quirk
+        const bool active = A->s.pads[act_idx].is_active;
+        const float timer = A->s.pads[tim_idx].cooldown;
+        A->u.out.obs[p][17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
+    }
+    // action masks: 4 x 90 bytes; the players' flags packed 3 bits each (no run-time register index)
+    uint32_t fl = 0;
 #pragma unroll
-        for (int k = 0; k < RLGPU_PADS; k++) {
-            // both map entries at uniform indices (scalar loads), the player's team picks: a lane-dependent
-            // index would be a vector load from the constant bank on every pad's chain
-            const int fwd = C.pad_map[k], rev = C.pad_map[RLGPU_PADS - k - 1];
-            int act_idx = inv ? rev : fwd;
-            int tim_idx = inv ? fwd : rev;  // GameState.h:60 quirk
-            bool active = A->s.pads[act_idx].is_active;
-            float timer = A->s.pads[tim_idx].cooldown;
-            o[17 + k] = active ? 1.0f : 1.0f / (1.0f + timer);
-        }
-    } else if (part == 2) {
-        // the teammate (the other player of this team), then the first opponent (player of the other
-        // team with the lower index)
-        add_player_obs(o + 51 + 29, view_player(A, pi ^ 2), inv, bp, bv);
-        add_player_obs(o + 51 + 58, view_player(A, (pi & 1) ^ 1), inv, bp, bv);
-    } else {
-        add_player_obs(o + 51 + 87, view_player(A, ((pi & 1) ^ 1) + 2), inv, bp, bv);
-        const rlgpu_car& c = A->s.cars[pi];
-        const bool on_ground = c.is_on_ground;
+    for (int p = 0; p < 4; p++) {
+        const rlgpu_car& c = A->s.cars[p];
         const bool hfj = c.is_on_ground || (!c.has_flipped && !c.has_double_jumped && c.air_time_since_jump < 1.25f);
-        uint8_t* m = A->u.out.masks[pi];
-        bool turtled = c.world_contact && c.world_contact_normal[2] > 0.9f;
-        for (int k = 0; k < RLGPU_ACTIONS; k++) {
-            uint8_t r = on_ground ? C.mask_ground[k] : C.mask_air[k];
-            if (c.boost == 0) r &= (uint8_t)~C.mask_boost[k];
-            if (hfj || turtled) r |= C.mask_jump[k];
-            m[k] = r & 1;
-        }
+        const bool turtled = c.world_contact && c.world_contact_normal[2] > 0.9f;
+        fl |= (uint32_t)((c.is_on_ground ? 1 : 0) | (c.boost == 0 ? 2 : 0) | ((hfj || turtled) ? 4 : 0)) << (3 * p);
+    }
+    for (int e = l; e < 4 * RLGPU_ACTIONS; e += kTeam) {
+        const int p = e / RLGPU_ACTIONS, k = e - RLGPU_ACTIONS * (e / RLGPU_ACTIONS);
+        const uint32_t f = fl >> (3 * p), bits = C.mask_bits[k];
+        uint32_t r = (f & 1) ? (bits & 1) : ((bits >> 1) & 1);  // ground / air table
+        if (f & 2) r &= ~(bits >> 3);                           // no boost: the boost actions off
+        if (f & 4) r |= (bits >> 2) & 1;                         // can jump (or turtled): the jump actions on
+        A->u.out.masks[p][k] = (uint8_t)(r & 1);
     }
 }
 

@@ -79,6 +79,7 @@ struct EnvConst {
     v3 boost_loc[RLGPU_PADS];          // CommonValues::BOOST_LOCATIONS (uu)
     float action[RLGPU_ACTIONS][8];    // DefaultAction table
     uint8_t mask_ground[RLGPU_ACTIONS], mask_air[RLGPU_ACTIONS], mask_jump[RLGPU_ACTIONS], mask_boost[RLGPU_ACTIONS];
+    uint8_t mask_bits[RLGPU_ACTIONS];  // the four tables as bits: ground 1, air 2, jump 4, boost 8 (one load per mask byte)
 };
 
 // The env set's reward / terminal registry (rlgpu_envset_config rewards / terminals), one device copy

@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
             A->s.env.last_tick_count = A->s.env.tick_count;
         }
         const bool fused_reset = g.reset_mode == 1 && valid && term != 0;
-        if (valid) build_obs_row(A, l & 3, l >> 2);
+        if (valid) build_obs_rows(A, l);
         sync(); P.mark(13);
         if (valid) {
             copy_rows(A, l, arena, g.obs, g.masks);
@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
         if (g.reset_mode == 1) {
             if (fused_reset && l == 0) kickoff_reset(A, g.seed, arena + g.arena_offset, g.fuzz != 0);
             sync(); P.mark(14);
-            if (fused_reset) build_obs_row(A, l & 3, l >> 2);
+            if (fused_reset) build_obs_rows(A, l);
             sync(); P.mark(14);
             if (fused_reset) {
                 copy_rows(A, l, arena, g.obs, g.masks);
@@ -620,7 +620,7 @@ __global__ void __launch_bounds__(kWG) RLGPU_ENV_KERNEL(StepArgs g) {
         }
         sync(); P.mark(14);
         bool rebuild = do_reset || (valid && g.reset_mode == 5);
-        if (rebuild) build_obs_row(A, l & 3, l >> 2);
+        if (rebuild) build_obs_rows(A, l);
         sync(); P.mark(14);
         if (rebuild) copy_rows(A, l, arena, g.obs, g.masks);
         sync(); P.mark(14);
