@@ -964,25 +964,40 @@ DEV void car_phase(ArenaLDS* A, int ci) {
             W.susp_rel_vel = 0;
         }
     }
-    for (int i = 0; i < 4; i++) {
-        WheelT& W = A->u.wt[ci * 4 + i];
-        if (W.susp_rel_vel != 0) {
-            v3 off = W.contact_point - bpos(A, bi);
-            float base = (W.susp_rel_vel * kTick) + cs.wheel_extra_pushback[i];
-            apply_impulse(A, bi, W.contact_normal * base, off);
-        }
-    }
-    {
-        v3 up = col(brot(A, bi), 2);
+    // the suspension, then the friction impulses (apply_impulse each, in this order), accumulated in registers
+    // and stored once: the same additions as eight read-modify-writes of the body's velocities in LDS
+    if (binv_mass(bi) != 0.f) {
+        rlgpu_body* b = body(A, bi);
+        const v3 P = bpos(A, bi);
+        const m3 iiw = A->a.iiw[bi];
+        const float im = binv_mass(bi);
+        v3 lin = ld3(b->vel), ang = ld3(b->angvel);
+#pragma unroll
         for (int i = 0; i < 4; i++) {
-            WheelT& W = A->u.wt[ci * 4 + i];
-            if (!is_zero(W.impulse)) {
-                v3 off = W.contact_point - bpos(A, bi);
-                float d = dot(up, off);
-                v3 rel = off - up * d;
-                apply_impulse(A, bi, W.impulse * kTick, rel);
+            const WheelT& W = A->u.wt[ci * 4 + i];
+            if (W.susp_rel_vel != 0) {
+                const v3 off = W.contact_point - P;
+                const float base = (W.susp_rel_vel * kTick) + cs.wheel_extra_pushback[i];
+                const v3 imp = W.contact_normal * base;
+                lin = lin + imp * im;
+                ang = ang + iiw * cross(off, imp);
             }
         }
+        const v3 up = col(brot(A, bi), 2);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const WheelT& W = A->u.wt[ci * 4 + i];
+            if (!is_zero(W.impulse)) {
+                const v3 off = W.contact_point - P;
+                const float d = dot(up, off);
+                const v3 rel = off - up * d;
+                const v3 imp = W.impulse * kTick;
+                lin = lin + imp * im;
+                ang = ang + iiw * cross(rel, imp);
+            }
+        }
+        st3(b->vel, lin);
+        st3(b->angvel, ang);
     }
     update_boost(A, ci);
 }

@@ -216,7 +216,7 @@ struct alignas(16) ArenaLDS {
 // the s_memtime delta since the previous mark to prof[phase] (all workgroups) and to
 // prof[kProfWG + blockIdx.x * kProfPhases + phase] (this workgroup: the kernel ends with its slowest
 // workgroup, so the spread matters as much as the mean).  Used by tools/env_phase_profile.py.
-constexpr int kProfPhases = 32, kProfWG = 64;  // per workgroup: phases 0-22 and 30-31, slot 23 = penetration-solver calls
+constexpr int kProfPhases = 35, kProfWG = 64;  // per workgroup: phases 0-22 and 30-31, slot 23 = penetration-solver calls
 // workgroup barrier (a workgroup is one wave of 4 arenas): LDS writes before it are visible after it
 __device__ __forceinline__ void sync() { __syncthreads(); }
 struct Prof {

@@ -157,9 +157,11 @@ DEV void tick(ArenaLDS* A, const MeshView& M, int l, bool valid, uint64_t seed, 
     P.mark(31);
     if (valid && l < 4) car_phase_a(A, l);
     sync();
+    P.mark(33);
     // Car::_UpdateWheels' per-wheel friction: lane 4 car + wheel
     if (valid && !A->s.cars[l >> 2].is_demoed) wheel_friction(A, l >> 2, l & 3);
     sync();
+    P.mark(34);
     if (valid) {
         if (l < 4) {
             car_phase(A, l);

@@ -218,7 +218,7 @@ def test_env_procedural_soccar_mesh_parity(gpu, pen_slots, monkeypatch):
     if pen_slots is not None:
         monkeypatch.setenv("RLGPU_DEBUG_PEN_SAVE_SLOTS", str(pen_slots))
     g, o = EnvSet(n, seed=21, device=gpu, mesh=mesh), oracle.EnvSet(n, seed=21, mesh=mesh, threads=8)
-    prof = torch.zeros(64 + 32 * (n // 4) + n, dtype=torch.int64, device=gpu)
+    prof = torch.zeros(64 + 35 * (n // 4) + n, dtype=torch.int64, device=gpu)
     L = _lib.lib()
     L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     _lib.check(L.rlgpu_envset_set_profile(g._h, ctypes.c_void_p(prof.data_ptr()), prof.numel()), "set_profile")
@@ -243,7 +243,7 @@ def test_env_procedural_soccar_mesh_parity(gpu, pen_slots, monkeypatch):
         _check_step(g, o, f"procedural soccar step {t}")
     torch.cuda.synchronize()
     pen = int(prof[28])
-    assert pen > 0 and int(prof[64 + 32 * (n // 4):].sum()) == pen, pen  # the penetration solver ran
+    assert pen > 0 and int(prof[64 + 35 * (n // 4):].sum()) == pen, pen  # the penetration solver ran
     _lib.check(L.rlgpu_envset_set_profile(g._h, None, 0), "set_profile")
 
 

@@ -15,8 +15,8 @@ NAMES = ["T0 sleep/demo/snapshot", "T1 wheels static rays (16 lanes)", "T2 car l
          "T4 ball awake", "T5 narrowphase (queue GJK)", "T6 commit + solve (lane 0)", "T7 integrate", "T8 car post/finish",
          "T9 pad collide", "T10 pad post + ball finish", "prelude / halves", "builders", "obs rows", "resets", "store", "T6 commit loop", "T6 commit sort",
          "T5 deferred EPA (wave)", "T6 solve body setup", "T6 solve rows build", "T6 solve iterations", "T5 narrow pairs (grid walks)",
-         "T1 wheel casts (wave)", "T1 wheel finish"]
-PH = list(range(23)) + [30, 31]  # the phase slots (env_kernel.hpp kProfPhases; slot 23 = penetration-solver calls)
+         "T1 wheel casts (wave)", "T1 wheel finish", "T2a car phase a", "T2b wheel friction"]
+PH = list(range(23)) + [30, 31, 33, 34]  # the phase slots (env_kernel.hpp kProfPhases; slot 23 = penetration-solver calls)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 8  # env steps before profiling (late-episode states)
@@ -35,7 +35,7 @@ for i in range(warm):
     env.step(acts, True)
 APW = int(os.environ.get("RLGPU_ENV_APW", "4"))  # arenas per workgroup of the built library (env_kernel.hpp)
 wg = (n + APW - 1) // APW
-KP, KW = 32, 64  # env_kernel.hpp kProfPhases, kProfWG
+KP, KW = 35, 64  # env_kernel.hpp kProfPhases, kProfWG
 prof = torch.zeros(KW + wg * KP + n, dtype=torch.int64, device=dev)  # + per-arena penetration-solver calls
 spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
 L = _lib.lib()
