@@ -384,7 +384,24 @@ def main():
     # only broadcasts RCCL's unique id.  A gloo rehearsal (several ranks on one GPU) uses the torch.distributed
     # callbacks instead, since RCCL refuses two ranks on one device.
     native_rccl = world > 1 and backend == "nccl"
-    L = Learner(cfg, device=dev, rank=rank, world=world, native_rccl=native_rccl)
+    L = None
+    if native_rccl:
+        # every rank must agree on the collective: a rank whose native communicator could not be created falls
+        # back, with all the others, to the torch.distributed (RCCL) callbacks, and the line says so
+        try:
+            L = Learner(cfg, device=dev, rank=rank, world=world, native_rccl=True)
+        except Exception as e:  # noqa: BLE001 - reported, then the consensus decides
+            print(f"bench.py rank {rank}: native RCCL collective unavailable ({e}); voting for torch.distributed",
+                  file=sys.stderr)
+        ok = torch.tensor([1 if L is not None else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if L is not None:
+                L.close()
+                L = None
+            native_rccl = False
+    if L is None:
+        L = Learner(cfg, device=dev, rank=rank, world=world, native_rccl=native_rccl)
     # HIP events around every fused env step, on the stream it runs on (RLGPU_BENCH_ENV_TIMING=0: none)
     L.set_env_timing(os.environ.get("RLGPU_BENCH_ENV_TIMING", "1") != "0")
 
