@@ -511,6 +511,7 @@ extern "C" int rlgpu_envset_create(const rlgpu_envset_config* cfg, rlgpu_envset*
         e->mesh.ny = grid.ny;
         e->mesh.nz = grid.nz;
         e->mesh.ntris = grid.ntris;
+        for (int k = 0; k < 6; k++) e->mesh.empty[k] = grid.empty[k];
         int n = cfg->num_arenas;
         {  // one GjkScratch per lane of the env kernel's grid (touched only by penetration-solver calls)
             const size_t lanes = (size_t)rlgpu::ceil_div(n, rl::kArenas) * rl::kWG;

@@ -194,6 +194,9 @@ DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& 
     const int x0 = grid_cell(qmn.x, M.ox, M.inv_cell, M.nx), x1 = grid_cell(qmx.x, M.ox, M.inv_cell, M.nx);
     const int y0 = grid_cell(qmn.y, M.oy, M.inv_cell, M.ny), y1 = grid_cell(qmx.y, M.oy, M.inv_cell, M.ny);
     const int z0 = grid_cell(qmn.z, M.oz, M.inv_cell, M.nz), z1 = grid_cell(qmx.z, M.oz, M.inv_cell, M.nz);
+    // every cell of the query inside the grid's empty box: no entries to walk (the same result, no loads)
+    if (x0 >= M.empty[0] && x1 <= M.empty[1] && y0 >= M.empty[2] && y1 <= M.empty[3] && z0 >= M.empty[4] && z1 <= M.empty[5])
+        return;
     const int nyr = y1 - y0 + 1, nrows = nyr * (z1 - z0 + 1);
     if (nrows > kGridRows) {  // a larger query: row by row, the sequence numbering continued across rows
         int seen = 0;

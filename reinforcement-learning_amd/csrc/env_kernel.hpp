@@ -127,6 +127,7 @@ struct MeshView {
     gjk::GjkScratch* gjk;    // [grid lanes]: box-triangle penetration-solver scratch (gjk.hpp)
     float ox, oy, oz, inv_cell;
     int nx, ny, nz, ntris;
+    int empty[6];  // cells x0..x1, y0..y1, z0..z1 that list no triangle (MeshGrid::empty; x0 > x1: none)
 };
 
 struct SB {  // btSolverBody subset

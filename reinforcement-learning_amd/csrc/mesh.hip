@@ -145,6 +145,35 @@ MeshGrid build_mesh_grid(const float* tris_in, int ntris, const int32_t* object_
     }
     g.cell_start.assign(ncell + 1, 0);
     for (size_t c = 0; c < ncell; c++) g.cell_start[c + 1] = g.cell_start[c] + count[c];
+    {  // the empty box: from the centre cell (if empty), grow one face at a time while the added slab is empty
+        auto slab_empty = [&](int x0, int x1, int y0, int y1, int z0, int z1) {
+            for (int z = z0; z <= z1; z++)
+                for (int y = y0; y <= y1; y++)
+                    for (int x = x0; x <= x1; x++)
+                        if (count[((size_t)z * g.ny + y) * g.nx + x]) return false;
+            return true;
+        };
+        int b[6] = {g.nx / 2, g.nx / 2, g.ny / 2, g.ny / 2, g.nz / 2, g.nz / 2};
+        if (slab_empty(b[0], b[1], b[2], b[3], b[4], b[5])) {
+            const int lim[6] = {0, g.nx - 1, 0, g.ny - 1, 0, g.nz - 1};
+            for (bool grew = true; grew;) {
+                grew = false;
+                for (int f = 0; f < 6; f++) {
+                    if (b[f] == lim[f]) continue;
+                    int c[6] = {b[0], b[1], b[2], b[3], b[4], b[5]};
+                    c[f] += (f & 1) ? 1 : -1;
+                    const int ax = f >> 1;  // the new slab: the face's new layer across the box
+                    int s[6] = {b[0], b[1], b[2], b[3], b[4], b[5]};
+                    s[2 * ax] = s[2 * ax + 1] = c[f];
+                    if (slab_empty(s[0], s[1], s[2], s[3], s[4], s[5])) {
+                        b[f] = c[f];
+                        grew = true;
+                    }
+                }
+            }
+            std::memcpy(g.empty, b, sizeof b);
+        }
+    }
     RLGPU_REQUIRE(g.cell_start[ncell] < (1 << 26), "mesh: grid index too large");
     g.cell_tri.assign((size_t)g.cell_start[ncell] * 12, 0.f);
     std::vector<int> fill(g.cell_start.begin(), g.cell_start.end() - 1);

@@ -21,6 +21,9 @@ struct MeshGrid {
     std::vector<int> visit_pos, visit_tri;
     float ox = 0, oy = 0, oz = 0, inv_cell = 1;
     int nx = 1, ny = 1, nz = 1, ntris = 0;
+    // a box of cells that lists no triangle, grown from the grid's centre (x0, x1, y0, y1, z0, z1; x0 > x1: none):
+    // a query whose cells all lie in it has nothing to walk
+    int empty[6] = {1, 0, 1, 0, 1, 0};
 };
 
 // tris_bt: ntris x 9 floats (bullet units); object k owns the next object_ntris[k] triangles
