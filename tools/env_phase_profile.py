@@ -37,6 +37,7 @@ APW = int(os.environ.get("RLGPU_ENV_APW", "4"))  # arenas per workgroup of the b
 wg = (n + APW - 1) // APW
 KP, KW = 35, 64  # env_kernel.hpp kProfPhases, kProfWG
 prof = torch.zeros(KW + wg * KP + n, dtype=torch.int64, device=dev)  # + per-arena penetration-solver calls
+top32 = []  # per step: the mean phase vector of the 32 slowest workgroups
 spread = []  # per step: (max WG cycles, mean WG cycles, phase vector of the slowest WG, mean phase vector)
 L = _lib.lib()
 L.rlgpu_envset_set_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
@@ -56,6 +57,8 @@ for i in range(steps):
     tots = per.sum(1)
     k = int(tots.argmax())
     spread.append((tots.max().item(), tots.mean().item(), per[k].cpu(), per.mean(0).cpu()))
+    top = tots.topk(min(32, wg)).indices  # the 32 slowest workgroups of this step (~3 % of them)
+    top32.append(per[top].mean(0).cpu())
     pens = prof[KW:KW + wg * KP].view(wg, KP)[:, 23]
     pen_rows.append((int(pens.sum()), int(pens.max()), int(pens[k])))
     pa = prof[KW + wg * KP:].view(-1)
@@ -87,3 +90,7 @@ print(f"  penetration-solver (EPA) calls per step: mean {pr[:, 0].mean():.1f} ov
       f"{pr[:, 1].mean():.1f} (max {pr[:, 1].max()}), slowest workgroup {pr[:, 2].mean():.1f}")
 print(f"  workgroups with two or more arenas calling the penetration solver, per step: {np.mean(arena_rows):.1f}; "
       f"the slowest workgroup's calls per arena, first steps: {slow_arenas[:6]}")
+t32 = sum(top32) / len(top32)
+print(f"  the 32 slowest workgroups per step (the launch's tail): mean {t32.sum().item():.0f} cycles; phases by excess over the mean")
+for k in sorted(range(len(PH)), key=lambda k: -(t32[k] - mean[k]).item())[:8]:
+    print(f"    {NAMES[k]:28s} top32 {t32[k].item():10.0f}  mean {mean[k].item():10.0f}  excess {t32[k].item() - mean[k].item():10.0f}")
