@@ -166,6 +166,7 @@ DEV int grid_cell(float x, float o, float inv, int n) {
     return (int)f;
 }
 constexpr int kGridBatch = 4;  // grid entries whose loads are issued together
+constexpr int kRayBatch = 8;   // the same for a wheel ray's walk (one query per lane, the phase's longest chain)
 constexpr int kGridRows = 4;   // (y, z) rows of a query walked as one sequence (more: row by row)
 // Calls f(t, v0, v1, v2, obj) once for every triangle whose AABB overlaps [qmn, qmx] (the exact
 // test of the linear scan it replaces), in no particular order.  A triangle is listed in every
@@ -189,7 +190,7 @@ DEV void grid_entry(const MeshView& M, const float4 (&q)[3], v3 qmn, v3 qmx, int
     if (cell != (vx | (vy << 8) | (vz << 16))) return;
     f(t, v0, v1, v2, obj);
 }
-template <class F>
+template <int kBatch = kGridBatch, class F>
 DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& f) {
     const int x0 = grid_cell(qmn.x, M.ox, M.inv_cell, M.nx), x1 = grid_cell(qmx.x, M.ox, M.inv_cell, M.nx);
     const int y0 = grid_cell(qmn.y, M.oy, M.inv_cell, M.ny), y1 = grid_cell(qmx.y, M.oy, M.inv_cell, M.ny);
@@ -237,10 +238,10 @@ DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& 
         c[r + 1] = c[r] + (live ? ee - bb : 0);
     }
     const int total = c[kGridRows];
-    for (int i = part; i < total; i += kGridBatch * parts) {
-        float4 q[kGridBatch][3];
+    for (int i = part; i < total; i += kBatch * parts) {
+        float4 q[kBatch][3];
 #pragma unroll
-        for (int j = 0; j < kGridBatch; j++) {  // past the sequence's end: its last entry again (not visited)
+        for (int j = 0; j < kBatch; j++) {  // past the sequence's end: its last entry again (not visited)
             const int s = min(i + j * parts, total - 1);
             int e = b[0] + s;
 #pragma unroll
@@ -251,7 +252,7 @@ DEV void grid_query(const MeshView& M, v3 qmn, v3 qmx, int part, int parts, F&& 
             q[j][2] = p[2];
         }
 #pragma unroll
-        for (int j = 0; j < kGridBatch; j++) {
+        for (int j = 0; j < kBatch; j++) {
             if (i + j * parts >= total) break;
             grid_entry(M, q[j], qmn, qmx, x0, y0, z0, f);
         }
@@ -315,7 +316,7 @@ DEV void ray_cast_static(ArenaLDS* A, const MeshView& M, v3 from, v3 to, int sel
     const v3 smax = v3{fmaxf(from.x, to.x) + kRayCull, fmaxf(from.y, to.y) + kRayCull, fmaxf(from.z, to.z) + kRayCull};
     int best_t = -1;
     const int ar = arith(A);
-    grid_query(M, smin, smax, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int) {
+    grid_query<kRayBatch>(M, smin, smax, 0, 1, [&](int t, v3 v0, v3 v1, v3 v2, int) {
         v3 n;
         const float f = ray_tri(v0, v1, v2, from, to, best, best_t >= 0 && t < best_t, n, ar);
         if (f < 0.f) return;
