@@ -46,7 +46,7 @@ def env_bytes_per_step(arena_state_size, append=True, output_only=True):
 # The env kernel's PMC summary of the committed HEAD (tools/pmc_summary.py over separate FETCH_SIZE /
 # WRITE_SIZE rocprofv3 passes of this bench, procedural mesh, ARENAS_PER_GPU arenas).  Named explicitly and
 # updated with every re-measurement -- never picked by file-name order.
-ENV_PMC_FILE = "profiles/r06zz_env_pmc.json"
+ENV_PMC_FILE = "profiles/r06zy_env_pmc.json"
 
 
 def pmc_traffic(kernel_ms, launch_arenas, mesh_name, pmc_file):
